@@ -1,0 +1,209 @@
+"""bench.py -- headline benchmark of the MI355X de Bruijn + Euler-tour core.
+
+Metric (BASELINE.json): k-mers/sec (encode+hash+deBruijn+Euler), 10Mx100bp k=31, 1/2/4/8 GPU.
+One step = one full fused assembly (encode -> canonical count -> solid filter -> links ->
+list ranking -> contig starts/order -> contig strings -> GFA links, i.e. the reference's
+build() + all_contigs()) of the whole synthetic read set, reads already resident in HBM.
+value = k-mer positions of the whole job / wall time of one step (max over ranks).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (read-sharded, RCCL exchange)
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "pycuda-euler_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "k-mers/sec (encode+hash+deBruijn+Euler), 10Mx100bp k=31, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+# SURVEY §8d synthetic inputs: seed = 20261015 + config#
+CONFIGS = {
+    # the metric's own workload (BASELINE configs[3] data: E. coli size, 10M x 100 bp, k = 31)
+    "ecoli10m": dict(genome=4_600_000, reads=10_000_000, read_len=100, k=31, seed=20261015 + 4,
+                     name="ecoli-4.6Mbp-10Mx100bp-k31"),
+    # BASELINE configs[1]: 1M x 100 bp
+    "ecoli1m": dict(genome=4_600_000, reads=1_000_000, read_len=100, k=31, seed=20261015 + 2,
+                    name="ecoli-4.6Mbp-1Mx100bp-k31"),
+    # BASELINE configs[2]: S. cerevisiae size, 5M x 100 bp
+    "yeast5m": dict(genome=12_000_000, reads=5_000_000, read_len=100, k=31, seed=20261015 + 3,
+                    name="yeast-12Mbp-5Mx100bp-k31"),
+    "tiny": dict(genome=50_000, reads=50_000, read_len=100, k=31, seed=7, name="tiny-50kbp-50kx100bp-k31"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def alg_bytes(P, R, L, U, K=8):
+    """SURVEY §8d official algorithmic bytes: R*L + P*(K+8) + U*(10K+33)."""
+    return R * L + P * (K + 8) + U * (10 * K + 33)
+
+
+def count_kernel_bytes(P, R, L, K=8):
+    """Algorithmic bytes of the dominant (count) kernel per launch: read the ASCII reads once
+    (R*L) + one canonical insert per position (key compare K + 4-B count RMW = K+8)."""
+    return R * L + P * (K + 8)
+
+
+def cpu_baseline(buf, off, k, sample_reads):
+    """The test-only C restatement (oracle/refasm.c) of the reference CPU assembler, 1 core,
+    on the first `sample_reads` reads of the same workload."""
+    import oracle
+
+    n = min(sample_reads, len(off) - 1)
+    sb = buf[: int(off[n])]
+    so = off[: n + 1]
+    t0 = time.perf_counter()
+    out = oracle.assemble_packed(sb, so, k, 1)
+    dt = time.perf_counter() - t0
+    P = int(out["n_positions"])
+    return {"value": P / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": "first %d of %d reads (%d k-mer positions), oracle/refasm.c single-threaded, %.1f s"
+                      % (n, len(off) - 1, P, dt),
+            "cpu": platform.processor() or platform.machine()}
+
+
+def load_traffic(workload):
+    """HBM bytes per count-kernel launch from rocprofv3 PMC passes (profiles/traffic_*.json,
+    written by profiles/collect_traffic.py; FETCH_SIZE doubled per the gfx950 note)."""
+    import glob
+
+    best = None
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json"))):
+        try:
+            d = json.load(open(fn))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("kernel_bytes_per_launch"):
+            best = d
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="ecoli10m", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import eulerhip
+
+    cfg = CONFIGS[args.config]
+    t0 = time.time()
+    from synth import make_reads
+
+    buf, off = make_reads(cfg["genome"], cfg["reads"], cfg["read_len"], cfg["seed"])
+    log("rank %d: generated %d reads in %.1f s" % (rank, cfg["reads"], time.time() - t0))
+    k = cfg["k"]
+
+    if world == 1:
+        d_buf = torch.from_numpy(buf).cuda()
+        d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+        torch.cuda.synchronize()
+        sess = eulerhip.Session(local, stream=torch.cuda.current_stream().cuda_stream)
+
+        def step(timing=False):
+            sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), cfg["reads"], k, 1,
+                            eulerhip.EC_FLAG_TIMING if timing else 0)
+    else:
+        import distributed
+
+        runner = distributed.ShardedAssembler(buf, off, k, 1, rank, world, local)
+
+        def step(timing=False):
+            runner.run(timing)
+
+    for _ in range(args.warmup):
+        step(True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    stage = np.zeros(eulerhip.EC_NSTAGES)
+    count_ms = []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+        st = sess.stats() if world == 1 else runner.stats()
+        stage += np.array(list(st.stage_ms))
+        count_ms.append(st.count_kernel_ms)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    st = sess.stats() if world == 1 else runner.stats()
+    P = int(st.n_positions) if world == 1 else runner.total_positions
+    U = int(st.n_solid)
+    R, L = cfg["reads"], cfg["read_len"]
+    value = P / (ms / 1e3)
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    avg_count_ms = float(np.mean(count_ms))
+    kb = count_kernel_bytes(P if world == 1 else P // world, R // world, L)
+    achieved = kb / (avg_count_ms / 1e3) / 1e9
+    tr = load_traffic(cfg["name"])
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": (tr["kernel_bytes_per_launch"] if tr else None),
+            "kernel": "k_count", "kernel_ms": round(avg_count_ms, 4), "alg_bytes_per_launch": int(kb),
+            "pipeline_alg_bytes": int(alg_bytes(P, R, L, U)),
+            "pipeline_frac": round(alg_bytes(P, R, L, U) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(buf, off, k, args.cpu_sample_reads)
+    names = eulerhip.stage_names()
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (iid ACGT genome, uniform error-free 100 bp reads, 50% reverse-complemented, numpy PCG64 seed %d)" % cfg["seed"],
+        "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
+                   "positions": P, "solid_kmers": U, "contigs": int(st.n_contigs),
+                   "parallelism": "dp%d" % world},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "stage_ms": {names[i]: round(stage[i] / args.steps, 3) for i in range(len(names))},
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

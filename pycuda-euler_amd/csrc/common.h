@@ -1,0 +1,83 @@
+// common.h -- shared device/host helpers for libeulerhip (gfx950 / CDNA4, wave64).
+#pragma once
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+#include "../../include/eulerhip.h"
+
+namespace ec {
+
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr uint64_t NONE64 = ~0ull;
+constexpr uint64_t EMPTY_KEY = ~0ull;  // canonical 2-bit keys (k <= 32) never equal all-ones
+
+// thread-local last error (ec_last_error)
+void set_error(const char *fmt, ...);
+
+#define EC_HIP(call)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            ::ec::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+            return EC_ERR_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+#define EC_CHECK(call)                 \
+    do {                               \
+        int rc_ = (call);              \
+        if (rc_ != EC_OK) return rc_;  \
+    } while (0)
+
+// ---- 2-bit k-mer algebra (A=0 C=1 G=2 T=3, first base most significant) ------------------
+// matches referenceAssembler.py kmers/twin/fw/bw (:7-22) and the reference GPU encoding
+// (src/pyencode.py:40 codeF, :62-69 MSB-first packing).
+__host__ __device__ inline uint64_t kmask64(int k) { return k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1); }
+
+__host__ __device__ inline uint64_t rev2_64(uint64_t x) {
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bswap64(x);
+#else
+    return __builtin_bswap64(x);
+#endif
+}
+
+// reverse complement of a k-mer code (twin, referenceAssembler.py:7-10)
+__host__ __device__ inline uint64_t twin64(uint64_t x, int k) { return rev2_64(x ^ kmask64(k)) >> (64 - 2 * k); }
+
+// 64-bit finaliser (murmur3 fmix64): table placement only, never part of a result
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// ASCII -> 2-bit code; 4 = 'N' (segment break, referenceAssembler.py:29), 5 = invalid byte
+__device__ inline uint32_t base_code(uint32_t c) {
+    // A=65 C=67 G=71 T=84 N=78
+    switch (c) {
+    case 'A': return 0;
+    case 'C': return 1;
+    case 'G': return 2;
+    case 'T': return 3;
+    case 'N': return 4;
+    default: return 5;
+    }
+}
+
+inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 1u << 20) {
+    uint64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+}  // namespace ec

@@ -1,0 +1,270 @@
+"""eulerhip -- ctypes binding of libeulerhip.so (include/eulerhip.h), the MI355X HIP core.
+
+The product path.  Every call goes to the gfx950 kernels in csrc/; there is no CPU
+fallback: if the shared library (or a GPU) is missing, the calls raise EulerHipError.
+
+Layer 1 (fused, device-resident) mirrors the reference CPU assembler
+src/referenceassembler/referenceAssembler.py build:25-42 + all_contigs:79-111:
+
+    with Session() as s:
+        res = s.assemble(reads, k=31, limit=1, want_dict=True)
+        res.contigs      # == all_contigs(d, k)[1]   (r, in order)
+        res.links        # == all_contigs(d, k)[0]   (G as [[fw], [bw]] per contig)
+        res.dict_items   # == list(build(reads, k, limit).items())
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libeulerhip.so")
+
+EC_OK = 0
+EC_ERR_ARG = -1
+EC_ERR_ALPHABET = -2
+EC_ERR_NOMEM = -3
+EC_ERR_HIP = -4
+EC_ERR_CAPACITY = -5
+EC_ERR_STATE = -6
+
+EC_FLAG_WANT_DICT = 1
+EC_FLAG_TIMING = 2
+EC_NSTAGES = 8
+EC_MAX_K = 32
+
+
+class EulerHipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("eulerhip error %d: %s" % (code, msg))
+        self.code = code
+
+
+class AlphabetError(EulerHipError, ValueError):
+    pass
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("n_reads", ctypes.c_uint64),
+        ("n_positions", ctypes.c_uint64),
+        ("n_distinct_est", ctypes.c_uint64),
+        ("n_distinct", ctypes.c_uint64),
+        ("n_solid", ctypes.c_uint64),
+        ("n_dict", ctypes.c_uint64),
+        ("n_contigs", ctypes.c_uint64),
+        ("n_contig_chars", ctypes.c_uint64),
+        ("n_links", ctypes.c_uint64),
+        ("table_capacity", ctypes.c_uint64),
+        ("table_retries", ctypes.c_uint32),
+        ("rank_rounds", ctypes.c_uint32),
+        ("stage_ms", ctypes.c_float * EC_NSTAGES),
+        ("count_kernel_ms", ctypes.c_float),
+    ]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "stage_ms"}
+        d["stage_ms"] = list(self.stage_ms)
+        return d
+
+
+_lib = None
+
+# exported symbols and their signatures (tests check that every one declared in
+# include/eulerhip.h is exported by the library)
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+_SIGS = {
+    "ec_last_error": (ctypes.c_char_p, []),
+    "ec_version": (ctypes.c_int, []),
+    "ec_session_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int]),
+    "ec_session_set_stream": (ctypes.c_int, [_P, _P]),
+    "ec_session_destroy": (ctypes.c_int, [_P]),
+    "ec_assemble_device": (ctypes.c_int, [_P, _P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
+    "ec_assemble_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
+    "ec_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
+    "ec_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "ec_copy_contigs": (ctypes.c_int, [_P, _P, _P]),
+    "ec_copy_links": (ctypes.c_int, [_P, _P, _P]),
+    "ec_copy_dict": (ctypes.c_int, [_P, _P, _P]),
+}
+
+
+def lib():
+    """Load libeulerhip.so (in-tree).  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EulerHipError(EC_ERR_STATE, "libeulerhip.so not built (run __graft_entry__.build() or make -C csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def register(name, restype, argtypes):
+    """Per-module wrappers declare their extra symbols here."""
+    _SIGS[name] = (restype, argtypes)
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+
+
+def check(rc):
+    if rc != EC_OK:
+        msg = lib().ec_last_error().decode(errors="replace")
+        if rc == EC_ERR_ALPHABET:
+            raise AlphabetError(rc, msg)
+        raise EulerHipError(rc, msg)
+    return rc
+
+
+def stage_names():
+    L = lib()
+    return [L.ec_stage_name(i).decode() for i in range(EC_NSTAGES)]
+
+
+def pack_reads(reads):
+    """list[str|bytes] -> (uint8 buffer, uint64 offsets[n+1]).  Host-side CSR packing."""
+    bs = [r.encode("ascii") if isinstance(r, str) else bytes(r) for r in reads]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(bs), dtype=np.uint8)
+    return buf, off
+
+
+class Result:
+    """Outputs of one fused assembly (host copies)."""
+
+    def __init__(self, k, stats, chars, coff, loff, links, dict_items=None):
+        self.k = k
+        self.stats = stats
+        self._chars = chars
+        self.contig_offsets = coff
+        self.link_offsets = loff
+        self.link_codes = links
+        self.dict_items = dict_items
+
+    @property
+    def contig_bytes(self):
+        return self._chars
+
+    @property
+    def contigs(self):
+        ch = self._chars.decode("ascii")
+        o = self.contig_offsets
+        return [ch[int(o[i]):int(o[i + 1])] for i in range(len(o) - 1)]
+
+    @property
+    def links(self):
+        """G of all_contigs as [[fw links], [bw links]] per contig, link = [j, '+'|'-']."""
+        out = []
+        lo, lk = self.link_offsets, self.link_codes
+        for i in range((len(lo) - 1) // 2):
+            sides = []
+            for s in range(2):
+                a, b = int(lo[2 * i + s]), int(lo[2 * i + s + 1])
+                sides.append([[int(v) >> 1, "-" if v & 1 else "+"] for v in lk[a:b]])
+            out.append(sides)
+        return out
+
+    def G(self):
+        """all_contigs' G exactly: {i: ([(j, o), ...], [(j, o), ...])}"""
+        return {i: ([tuple(x) for x in s[0]], [tuple(x) for x in s[1]]) for i, s in enumerate(self.links)}
+
+
+class Session:
+    """A device-resident assembly session on one GPU (ec_session)."""
+
+    def __init__(self, device=0, stream=None):
+        L = lib()
+        h = ctypes.c_void_p()
+        check(L.ec_session_create(ctypes.byref(h), int(device)))
+        self._h = h
+        self.device = device
+        if stream is not None:
+            check(L.ec_session_set_stream(self._h, ctypes.c_void_p(int(stream))))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().ec_session_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream):
+        check(lib().ec_session_set_stream(self._h, ctypes.c_void_p(int(stream) if stream else None)))
+
+    # -- run -------------------------------------------------------------------------------
+    def run_host(self, buf, offsets, k, limit=1, flags=0):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = len(offsets) - 1
+        pbuf = buf.ctypes.data if buf.size else None
+        check(lib().ec_assemble_host(self._h, pbuf, buf.size, offsets.ctypes.data, n, int(k), int(limit), flags))
+
+    def run_device(self, d_reads_ptr, d_offsets_ptr, nreads, k, limit=1, flags=0):
+        """Reads already in HBM (e.g. torch uint8 / int64 tensors' data_ptr())."""
+        check(lib().ec_assemble_device(self._h, ctypes.c_void_p(int(d_reads_ptr)), ctypes.c_void_p(int(d_offsets_ptr)),
+                                       int(nreads), int(k), int(limit), flags))
+
+    def stats(self):
+        st = Stats()
+        check(lib().ec_get_stats(self._h, ctypes.byref(st)))
+        return st
+
+    def fetch(self, k, want_dict=False):
+        st = self.stats()
+        L = lib()
+        nc, nch, nl = st.n_contigs, st.n_contig_chars, st.n_links
+        chars = ctypes.create_string_buffer(max(nch, 1))
+        coff = np.zeros(nc + 1, dtype=np.uint64)
+        check(L.ec_copy_contigs(self._h, chars, coff.ctypes.data))
+        loff = np.zeros(2 * nc + 1, dtype=np.uint64)
+        links = np.zeros(max(nl, 1), dtype=np.int64)
+        check(L.ec_copy_links(self._h, loff.ctypes.data, links.ctypes.data))
+        items = None
+        if want_dict:
+            nd = st.n_dict
+            km = ctypes.create_string_buffer(max(nd * k, 1))
+            cnt = np.zeros(max(nd, 1), dtype=np.uint32)
+            check(L.ec_copy_dict(self._h, km, cnt.ctypes.data))
+            s = km.raw[: nd * k].decode("ascii")
+            items = [(s[i * k:(i + 1) * k], int(cnt[i])) for i in range(nd)]
+        return Result(k, st, chars.raw[:nch], coff, loff, links[:nl], items)
+
+    def assemble(self, reads, k, limit=1, want_dict=False, timing=False):
+        buf, off = pack_reads(reads)
+        flags = (EC_FLAG_WANT_DICT if want_dict else 0) | (EC_FLAG_TIMING if timing else 0)
+        self.run_host(buf, off, k, limit, flags)
+        return self.fetch(k, want_dict)
+
+
+_default = {}
+
+
+def default_session(device=0):
+    s = _default.get(device)
+    if s is None:
+        s = _default[device] = Session(device)
+    return s
+
+
+def assemble(reads, k, limit=1, want_dict=False, device=0):
+    """One-shot fused assembly on `device`."""
+    return default_session(device).assemble(reads, k, limit, want_dict)

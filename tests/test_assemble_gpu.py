@@ -1,0 +1,114 @@
+"""Parity of the fused HIP path (libeulerhip.so, ec_assemble_*) with the reference.
+
+* every golden case generated from the real reference (tests/golden/): ordered dict,
+  contigs and GFA links must be identical;
+* larger seeded synthetic inputs against the C oracle (oracle/refasm.c, itself pinned to
+  the golden vectors in test_oracle.py): bit-exact contigs + links (+ dict on some);
+* error behaviour (alphabet, k range), determinism, device-pointer entry point.
+"""
+import numpy as np
+import pytest
+
+import eulerhip
+import oracle
+from conftest import golden_cases
+from synth import make_reads
+
+pytestmark = pytest.mark.gpu
+
+CASES = golden_cases("g200.json", "synthetic.json", "fuzz.json")
+CASES32 = [c for c in CASES if c["k"] <= eulerhip.EC_MAX_K]
+
+
+@pytest.mark.parametrize("case", CASES32, ids=[c["name"] for c in CASES32])
+def test_golden(gpu_session, case):
+    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True)
+    assert [[x, c] for x, c in res.dict_items] == case["d"]
+    assert res.contigs == case["contigs"]
+    assert res.links == case["links"]
+
+
+def test_extended_alphabet_rejected(gpu_session):
+    for case in golden_cases("synthetic.json", alphabet="extended"):
+        with pytest.raises(eulerhip.AlphabetError):
+            gpu_session.assemble(case["reads"], case["k"], case["limit"])
+
+
+def test_k_out_of_range(gpu_session):
+    with pytest.raises(eulerhip.EulerHipError):
+        gpu_session.assemble(["ACGT" * 20], 0)
+    with pytest.raises(eulerhip.EulerHipError):
+        gpu_session.assemble(["ACGT" * 20], 65)
+
+
+def _oracle_packed(buf, off, k, limit=1, want_dict=False):
+    out = oracle.assemble_packed(buf, off, k, limit, want_dict)
+    return out, oracle.unpack_contigs(out), oracle.unpack_links(out)
+
+
+SYN = [
+    # genome, reads, len, seed, err, n_rate, circular, k
+    (20_000, 4_000, 100, 1, 0.0, 0.0, False, 31),
+    (50_000, 20_000, 100, 2, 0.005, 0.0, False, 31),
+    (30_000, 10_000, 80, 3, 0.002, 0.002, True, 25),
+    (5_000, 5_000, 60, 4, 0.01, 0.0, False, 20),
+    (2_000, 3_000, 50, 5, 0.0, 0.0, True, 16),
+    (200_000, 60_000, 100, 6, 0.0, 0.0, False, 32),
+    (1_000, 2_000, 40, 7, 0.02, 0.01, False, 11),
+]
+
+
+@pytest.mark.parametrize("g,n,L,seed,err,nr,circ,k", SYN)
+def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k):
+    buf, off = make_reads(g, n, L, 1000 + seed, err=err, n_rate=nr, circular=circ)
+    want_dict = g <= 50_000
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT if want_dict else 0)
+    res = gpu_session.fetch(k, want_dict)
+    assert res.stats.n_positions == ref["n_positions"]
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert res.links == rl
+    if want_dict:
+        assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+def test_limits_vs_oracle(gpu_session):
+    buf, off = make_reads(3_000, 1_500, 50, 99, err=0.01)
+    for lim in (-1, 0, 2, 5):
+        _, rc, rl = _oracle_packed(buf, off, 15, lim)
+        gpu_session.run_host(buf, off, 15, lim)
+        res = gpu_session.fetch(15)
+        assert res.contigs == rc and res.links == rl, lim
+
+
+def test_deterministic(gpu_session):
+    buf, off = make_reads(100_000, 30_000, 100, 11, err=0.003)
+    outs = []
+    for _ in range(3):
+        gpu_session.run_host(buf, off, 31, 1)
+        r = gpu_session.fetch(31)
+        outs.append((r.contig_bytes, r.contig_offsets.tobytes(), r.link_codes.tobytes()))
+    assert outs[0] == outs[1] == outs[2]
+
+
+def test_device_pointer_entry_point(gpu_session):
+    torch = pytest.importorskip("torch")
+    buf, off = make_reads(40_000, 12_000, 100, 12, err=0.002)
+    gpu_session.run_host(buf, off, 31, 1)
+    want = gpu_session.fetch(31)
+    d_buf = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    torch.cuda.synchronize()
+    gpu_session.run_device(d_buf.data_ptr(), d_off.data_ptr(), len(off) - 1, 31, 1)
+    got = gpu_session.fetch(31)
+    assert got.contig_bytes == want.contig_bytes and got.links == want.links
+
+
+def test_empty_and_ragged(gpu_session):
+    for reads in ([], [""], ["ACG"], ["N" * 50], ["ACGTTGCA" * 3, "", "A", "ACGTTGCAACG" * 2, "NNACGTTGCAAC"]):
+        for k in (1, 3, 5):
+            res = gpu_session.assemble(reads, k, 1, want_dict=True)
+            d, r, g = oracle.assemble(reads, k, 1)
+            assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g

@@ -1,0 +1,38 @@
+"""The CPU oracle (oracle/refasm.c) and the parallel design model (tests/model_parallel.py)
+pinned against every golden vector generated from the real reference
+(tests/golden/make_golden.py -> referenceAssembler.build/all_contigs)."""
+import pytest
+
+import oracle
+from conftest import golden_cases
+from model_parallel import model_assemble
+
+CASES = golden_cases("g200.json", "synthetic.json", "fuzz.json")
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_matches_reference(case):
+    d, r, g = oracle.assemble(case["reads"], case["k"], case["limit"])
+    assert d == case["d"]
+    assert r == case["contigs"]
+    assert g == case["links"]
+
+
+@pytest.mark.parametrize("case", CASES[::3], ids=[c["name"] for c in CASES[::3]])
+def test_parallel_model_matches_reference(case):
+    d, r, g = model_assemble(case["reads"], case["k"], case["limit"])
+    assert d == case["d"]
+    assert r == case["contigs"]
+    assert g == case["links"]
+
+
+def test_oracle_rejects_extended_alphabet():
+    for case in golden_cases("synthetic.json", alphabet="extended"):
+        with pytest.raises(oracle.OracleError):
+            oracle.assemble(case["reads"], case["k"], case["limit"])
+
+
+def test_g200_config1_is_empty_at_k21():
+    (case,) = [c for c in golden_cases("g200.json") if c["k"] == 21]
+    d, r, g = oracle.assemble(case["reads"], 21)
+    assert d == [] and r == [] and g == []
