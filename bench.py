@@ -192,7 +192,7 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u64",
-        "data": "synthetic (iid ACGT genome, uniform error-free 100 bp reads, 50% reverse-complemented, numpy PCG64 seed %d)" % cfg["seed"],
+        "data": "synthetic (iid ACGT genome, uniform error-free 100 bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)" % cfg["seed"],
         "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
                    "positions": P, "solid_kmers": U, "contigs": int(st.n_contigs),
                    "parallelism": "dp%d" % world},

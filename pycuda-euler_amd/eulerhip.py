@@ -94,6 +94,15 @@ def lib():
     """Load libeulerhip.so (in-tree).  Raises if it has not been built."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: PyTorch-ROCm bundles libamdhip64.so.7 /
+        # libhsa-runtime64.so.1 with the same SONAMEs as /opt/rocm.  Loading torch first makes
+        # the dynamic loader bind libeulerhip.so to torch's copy, so torch tensors, streams and
+        # our kernels share one runtime (loading ours first would give torch a second HSA
+        # runtime that sees no GPUs).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise EulerHipError(EC_ERR_STATE, "libeulerhip.so not built (run __graft_entry__.build() or make -C csrc)")
         L = ctypes.CDLL(LIB_PATH)
