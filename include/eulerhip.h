@@ -72,7 +72,8 @@ typedef struct {
     uint64_t n_links;
     uint64_t table_capacity; /* hash slots (32 B each)                                         */
     uint32_t table_retries;
-    uint32_t rank_rounds;
+    uint32_t rank_rounds;    /* Wyllie rounds on the ruler list                            */
+    uint64_t n_rulers;       /* sparse ruling-set size used by the list ranking            */
     float stage_ms[EC_NSTAGES]; /* EC_FLAG_TIMING only */
     float count_kernel_ms;      /* EC_FLAG_TIMING: the count kernel alone (dominant kernel)    */
 } ec_stats;

@@ -39,18 +39,6 @@ struct alignas(32) Slot {
 };
 static_assert(sizeof(Slot) == 32, "slot layout");
 
-// pointer-jumping state of one oriented node, 32 B (read as two 16-B loads)
-struct alignas(32) Jump {
-    unsigned int a;   // ancestor 2^j steps back (NONE past the head)
-    unsigned int d;   // window size (nodes x .. P^{d-1}(x))
-    unsigned int h;   // last node of the window (the head once a == NONE)
-    unsigned int cm;  // min node id in the window
-    unsigned int cd;  // distance from x back to cm
-    unsigned int pad;
-    unsigned long long fm;  // min first-event over the window
-};
-static_assert(sizeof(Jump) == 32, "jump layout");
-
 constexpr int HLL_BITS = 12;
 constexpr int HLL_M = 1 << HLL_BITS;
 constexpr int MAX_PROBE = 1 << 14;
@@ -297,7 +285,7 @@ __device__ inline unsigned int twin_node(const uint8_t *upal, unsigned int x) {
 // links phase 1: out-degree (number of fw(x) in d, get_contig_forward:63) + the unique candidate
 __global__ void __launch_bounds__(256) k_neighbors(const Slot *table, uint64_t capmask, const unsigned long long *dkey,
                                                    unsigned int U, int k, uint8_t *upal, uint8_t *outdeg,
-                                                   unsigned int *cand) {
+                                                   unsigned int *cand, unsigned int *npal) {
     const uint64_t mask = kmask64(k);
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < 2ull * U; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
@@ -312,6 +300,7 @@ __global__ void __launch_bounds__(256) k_neighbors(const Slot *table, uint64_t c
             }
         } else {
             upal[x >> 1] = pal ? 1 : 0;
+            if (pal) atomicAdd(npal, 1u);
         }
         const uint64_t xs = (x & 1) ? tc : c;
         unsigned int n = 0, cd = NONE32;
@@ -352,50 +341,127 @@ __device__ inline unsigned long long first_event(const unsigned long long *dfc, 
     return (x & 1) ? dft[x >> 1] : dfc[x >> 1];
 }
 
-// pred(x) = twin(succ(twin(x))) (links are closed under twin-reversal); jump state init
-__global__ void __launch_bounds__(256) k_jump_init(const uint8_t *upal, const unsigned int *succ,
-                                                   const unsigned long long *dfc, const unsigned long long *dft,
-                                                   unsigned int N, unsigned int *pred, Jump *st) {
+// pred(x) = twin(succ(twin(x))): the links are closed under twin-reversal
+__global__ void __launch_bounds__(256) k_pred(const uint8_t *upal, const unsigned int *succ, unsigned int N,
+                                              unsigned int *pred) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
-        const bool valid = !((x & 1) && upal[x >> 1]);
         unsigned int p = NONE32;
-        if (valid) {
+        if (!((x & 1) && upal[x >> 1])) {
             const unsigned int sx = succ[twin_node(upal, x)];
             if (sx != NONE32) p = twin_node(upal, sx);
         }
         pred[x] = p;
-        Jump j;
-        j.a = p;
-        j.d = 1;
-        j.h = x;
-        j.cm = x;
-        j.cd = 0;
-        j.pad = 0;
-        j.fm = valid ? first_event(dfc, dft, x) : NONE64;
-        st[x] = j;
     }
 }
 
-// one Wyllie round: W(x) <- W(x) u W(a(x)).  A node settles once its chain has reached the
-// head (a == NONE) or its window has covered >= N nodes (it sits on a cycle of length <= N).
-__global__ void __launch_bounds__(256) k_jump(const Jump *src, Jump *dst, unsigned int N, const unsigned int *active_in,
-                                              unsigned int *active_out, unsigned int *final_sel, unsigned int sel) {
-    if (active_in && *active_in == 0) return;  // converged in an earlier round
-    unsigned int act = 0;
+// ---- list ranking by a sparse ruling set ------------------------------------------------
+// Rulers: every path head plus every node whose hash hits the sampling mask.  Each ruler
+// walks its segment (up to the next ruler) serially, stamping (ruler, offset) on every node;
+// the much shorter ruler list is then ranked by weighted Wyllie pointer jumping.  Cycles
+// that drew no ruler are caught by later iterations with a denser sampling mask (the last
+// one makes every still-unvisited node a ruler).
+__device__ inline bool ruler_hash(unsigned int x, unsigned int smask) {
+    return (mix64(0x9E3779B97F4A7C15ull ^ x) & smask) == 0;
+}
+
+__global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsigned int *pred, unsigned int N,
+                                                unsigned int smask, int first, unsigned int *rid, unsigned int *roff,
+                                                unsigned int *rlist, unsigned int *nr) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        Jump j = src[t];
-        if (j.a != NONE32 && j.d < N) {
-            const Jump y = src[j.a];
-            j.a = y.a;
+        const unsigned int x = (unsigned int)t;
+        if ((x & 1) && upal[x >> 1]) continue;
+        if (rid[x] != NONE32) continue;
+        if ((first && pred[x] == NONE32) || ruler_hash(x, smask)) {
+            const unsigned int i = atomicAdd(nr, 1u);
+            rlist[i] = x;
+            rid[x] = i;
+            roff[x] = 0;
+        }
+    }
+}
+
+// ruler jump state (32 B): window = rulers i, P(i), .., P^{c-1}(i)
+struct alignas(32) RJump {
+    unsigned int a;    // P^c(i) or NONE
+    unsigned int s;    // nodes in the segments of P(i)..P^{c-1}(i)  (= rank of i's node on a path)
+    unsigned int h;    // last ruler of the window (the head ruler once a == NONE)
+    unsigned int cm;   // min ruler node id in the window
+    unsigned int cd;   // nodes from cm forward to i's node
+    unsigned int len;  // nodes in i's own segment
+    unsigned long long fm;  // min first event over the window's segments (incl. i's)
+};
+static_assert(sizeof(RJump) == 32, "rjump layout");
+
+__global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const unsigned long long *dfc,
+                                              const unsigned long long *dft, const unsigned int *rlist,
+                                              unsigned int r0, const unsigned int *nr, unsigned int smask,
+                                              unsigned int *rid, unsigned int *roff, unsigned int *nextR, RJump *rs,
+                                              unsigned long long *nvisited) {
+    const unsigned int r1 = *nr;
+    unsigned long long seen = 0;
+    for (uint64_t t = r0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < r1; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int i = (unsigned int)t;
+        unsigned int v = rlist[i];
+        unsigned long long fm = first_event(dfc, dft, v);
+        unsigned int j = 0, nx = NONE32;
+        for (;;) {
+            const unsigned int w = succ[v];
+            if (w == NONE32) break;
+            if (ruler_hash(w, smask) && rid[w] != NONE32) {  // the next ruler
+                nx = rid[w];
+                break;
+            }
+            v = w;
+            j++;
+            rid[v] = i;
+            roff[v] = j;
+            const unsigned long long f = first_event(dfc, dft, v);
+            fm = f < fm ? f : fm;
+        }
+        nextR[i] = nx;
+        RJump r;
+        r.a = NONE32;  // set from prevR by k_rjump_init
+        r.s = 0;
+        r.h = i;
+        r.cm = rlist[i];
+        r.cd = 0;
+        r.len = j + 1;
+        r.fm = fm;
+        rs[i] = r;
+        seen += j + 1;
+    }
+    for (int o = 32; o > 0; o >>= 1) seen += __shfl_down(seen, o);
+    if ((threadIdx.x & 63) == 0 && seen) atomicAdd(nvisited, seen);
+}
+
+__global__ void __launch_bounds__(256) k_rjump_init(const unsigned int *nextR, unsigned int nr, RJump *rs) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int n = nextR[t];
+        if (n != NONE32) rs[n].a = (unsigned int)t;  // prevR[next] = me (unique predecessor)
+    }
+}
+
+// one weighted Wyllie round on the ruler list
+__global__ void __launch_bounds__(256) k_rjump(const RJump *src, RJump *dst, unsigned int nr, unsigned int N,
+                                               const unsigned int *active_in, unsigned int *active_out,
+                                               unsigned int *final_sel, unsigned int sel) {
+    if (active_in && *active_in == 0) return;
+    unsigned int act = 0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
+        RJump j = src[t];
+        if (j.a != NONE32 && j.s < N) {
+            const RJump y = src[j.a];
+            const unsigned int back = j.s + y.len;  // nodes from ruler a's node forward to i's node
             if (y.cm < j.cm) {
                 j.cm = y.cm;
-                j.cd = j.d + y.cd;
+                j.cd = back + y.cd;
             }
-            j.d += y.d;
+            j.s = back + y.s;
+            j.a = y.a;
             j.h = y.h;
             j.fm = y.fm < j.fm ? y.fm : j.fm;
-            act += (j.a != NONE32 && j.d < N);
+            act += (j.a != NONE32 && j.s < N);
         }
         dst[t] = j;
     }
@@ -404,39 +470,66 @@ __global__ void __launch_bounds__(256) k_jump(const Jump *src, Jump *dst, unsign
     if (blockIdx.x == 0 && threadIdx.x == 0) *final_sel = sel;
 }
 
-// per-node path descriptors after ranking
-//   cyc: on a cycle; pk = path key (head id for paths, min id for cycles); rk = rank
-__device__ inline void node_desc(const Jump &j, bool &cyc, unsigned int &pk, unsigned int &rk) {
-    cyc = j.a != NONE32;
-    pk = cyc ? j.cm : j.h;
-    rk = cyc ? j.cd : j.d - 1;
+// per-node path descriptor: PK = path key (head node for paths, min ruler node for cycles)
+// with bit 31 = on a cycle; RK = rank (from the head / from the cycle key).  Path records
+// at the key node: PL = path / cycle length, PM = min first event over it.
+constexpr unsigned int CYC = 0x80000000u;
+
+__global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const unsigned int *succ, const unsigned int *rid,
+                                                  const unsigned int *roff, const unsigned int *rlist, const RJump *rs,
+                                                  unsigned int N, unsigned int *PK, unsigned int *RK, unsigned int *PL,
+                                                  unsigned long long *PM) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        if ((x & 1) && upal[x >> 1]) continue;
+        const unsigned int i = rid[x], j = roff[x];
+        const RJump r = rs[i];
+        if (r.a == NONE32) {  // path
+            const unsigned int pk = rlist[r.h], rk = r.s + j;
+            PK[x] = pk;
+            RK[x] = rk;
+            if (succ[x] == NONE32) {  // tail: its ruler's window spans the whole path
+                PL[pk] = rk + 1;
+                PM[pk] = r.fm;
+            }
+        } else {  // cycle
+            PK[x] = r.cm | CYC;
+            RK[x] = r.cd + j;
+        }
+    }
 }
 
-// min first event over the whole path / cycle containing x
-__device__ inline unsigned long long path_min(const Jump *st, const uint8_t *upal, unsigned int x) {
-    const Jump j = st[x];
-    if (j.a != NONE32) return j.fm;
-    // tail(x) = twin(head(twin(x)))
-    const unsigned int tail = twin_node(upal, st[twin_node(upal, x)].h);
-    return st[tail].fm;
+// cycle length / min: the ruler whose successor ruler is the key ruler closes the ring
+__global__ void __launch_bounds__(256) k_cycle_len(const unsigned int *nextR, const unsigned int *rlist, const RJump *rs,
+                                                   unsigned int nr, unsigned int *PL, unsigned long long *PM) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
+        const RJump r = rs[t];
+        if (r.a == NONE32) continue;
+        const unsigned int n = nextR[t];
+        if (n != NONE32 && rlist[n] == r.cm) {
+            PL[r.cm] = r.cd + r.len;
+            PM[r.cm] = r.fm;
+        }
+    }
+}
+
+__device__ inline unsigned long long path_min(const unsigned int *PK, const unsigned long long *PM, unsigned int x) {
+    return PM[PK[x] & ~CYC];
 }
 
 // start of each component (all_contigs:82-84): the oriented k-mer with the smallest first
 // event over the path and its twin path (= the first dict entry not yet `done`).
-__global__ void __launch_bounds__(256) k_starts(const Jump *st, const uint8_t *upal, const unsigned long long *dfc,
-                                                const unsigned long long *dft, unsigned int N, unsigned int *startOf,
+__global__ void __launch_bounds__(256) k_starts(const uint8_t *upal, const unsigned long long *dfc,
+                                                const unsigned long long *dft, const unsigned int *PK,
+                                                const unsigned long long *PM, unsigned int N,
                                                 unsigned long long *skeys, unsigned int *svals, unsigned int *nstarts) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         if ((x & 1) && upal[x >> 1]) continue;
         const unsigned long long f = first_event(dfc, dft, x);
-        const unsigned long long a = path_min(st, upal, x);
-        const unsigned long long b = path_min(st, upal, twin_node(upal, x));
+        const unsigned long long a = path_min(PK, PM, x);
+        const unsigned long long b = path_min(PK, PM, twin_node(upal, x));
         if (f == (a < b ? a : b)) {
-            bool cyc;
-            unsigned int pk, rk;
-            node_desc(st[x], cyc, pk, rk);
-            startOf[pk] = x;
             const unsigned int i = atomicAdd(nstarts, 1u);
             skeys[i] = f;
             svals[i] = x;
@@ -454,22 +547,18 @@ struct Walk {
     unsigned int kind, n, j, m, lo, len;
 };
 
-__device__ inline Walk walk_of(const Jump *st, const uint8_t *upal, const unsigned int *pred, unsigned int s) {
+__device__ inline Walk walk_of(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+                               const unsigned int *PL, unsigned int s) {
     Walk w;
-    bool cyc;
-    unsigned int pk, rk;
-    node_desc(st[s], cyc, pk, rk);
+    const unsigned int pk = PK[s], rk = RK[s];
     const unsigned int ts = twin_node(upal, s);
-    bool cyc2;
-    unsigned int pk2, rk2;
-    node_desc(st[ts], cyc2, pk2, rk2);
+    const unsigned int pk2 = PK[ts], rk2 = RK[ts];
     const bool self = pk2 == pk;
+    const unsigned int plen = PL[pk & ~CYC];
     w.j = rk;
     w.m = 0;
     w.lo = 0;
-    if (!cyc) {
-        const unsigned int tail = twin_node(upal, st[ts].h);
-        const unsigned int plen = st[tail].d;  // rank(tail) + 1
+    if (!(pk & CYC)) {
         if (!self) {
             w.kind = 0;
             w.n = plen;
@@ -490,7 +579,7 @@ __device__ inline Walk walk_of(const Jump *st, const uint8_t *upal, const unsign
             }
         }
     } else {
-        const unsigned int n = st[pred[pk]].cd + 1;  // rank of the rep's predecessor + 1
+        const unsigned int n = plen;
         w.n = n;
         if (!self) {
             w.kind = 2;
@@ -504,37 +593,34 @@ __device__ inline Walk walk_of(const Jump *st, const uint8_t *upal, const unsign
     return w;
 }
 
-__global__ void __launch_bounds__(256) k_contig_len(const Jump *st, const uint8_t *upal, const unsigned int *pred,
-                                                    const unsigned int *sorted_nodes, unsigned int nc, int k,
-                                                    unsigned int *cidxOf, unsigned long long *clen) {
+__global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+                                                    const unsigned int *PL, const unsigned int *sorted_nodes,
+                                                    unsigned int nc, int k, unsigned int *cidxOf,
+                                                    unsigned long long *clen) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int s = sorted_nodes[i];
-        bool cyc;
-        unsigned int pk, rk;
-        node_desc(st[s], cyc, pk, rk);
-        cidxOf[pk] = (unsigned int)i;
-        const Walk w = walk_of(st, upal, pred, s);
+        cidxOf[PK[s] & ~CYC] = (unsigned int)i;
+        const Walk w = walk_of(upal, PK, RK, PL, s);
         clen[i] = (unsigned long long)(k - 1) + w.len;
     }
 }
 
 // emit: every node finds its contig through its path key, computes its walk position and
 // writes its chars (contig_to_string:44-45: first node k chars, later nodes their last base).
-__global__ void __launch_bounds__(256) k_emit(const Jump *st, const uint8_t *upal, const unsigned int *pred,
-                                              const unsigned long long *dkey, const unsigned int *cidxOf,
-                                              const unsigned int *sorted_nodes, const unsigned long long *coff,
-                                              unsigned int N, int k, char *chars, unsigned int *cfirst,
-                                              unsigned int *clast, unsigned int *headOf, unsigned int *tailOf) {
+__global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+                                              const unsigned int *PL, const unsigned long long *dkey,
+                                              const unsigned int *cidxOf, const unsigned int *sorted_nodes,
+                                              const unsigned long long *coff, unsigned int N, int k, char *chars,
+                                              unsigned int *cfirst, unsigned int *clast, unsigned int *headOf,
+                                              unsigned int *tailOf) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         if ((x & 1) && upal[x >> 1]) continue;
-        bool cyc;
-        unsigned int pk, rk;
-        node_desc(st[x], cyc, pk, rk);
-        const unsigned int ci = cidxOf[pk];
+        const unsigned int pk = PK[x], rk = RK[x];
+        const unsigned int ci = cidxOf[pk & ~CYC];
         if (ci == NONE32) continue;  // the twin path of a disjoint pair carries the contig
         const unsigned int s = sorted_nodes[ci];
-        const Walk w = walk_of(st, upal, pred, s);
+        const Walk w = walk_of(upal, PK, RK, PL, s);
         long long pos = -1;
         if (w.kind == 0) {
             pos = rk;
@@ -665,6 +751,7 @@ struct ec_session {
     // scratch
     DevBuf h_reads, h_offsets;  // H2D staging for ec_assemble_host
     DevBuf hll, scal, table, dkey, dcnt, dfc, dft, upal, outdeg, cand, succ, pred, st0, st1;
+    DevBuf rid, roff, rlist, nextR, PK, RK, PL, PM;
     DevBuf startOf, skeys, svals, skeys2, svals2, cidxOf, clen, coff, chars, cfirst, clast, headOf, tailOf;
     DevBuf lk, lcnt, tmp, dchars, dcounts;
     // results (host)
@@ -692,7 +779,10 @@ struct Scalars {  // device scalars block
     unsigned int nstarts;
     unsigned int final_sel;
     unsigned int ndict;
+    unsigned int nr;
+    unsigned int npal;
     unsigned int pad;
+    unsigned long long nvisited;
     unsigned int active[64];
 };
 
@@ -833,65 +923,100 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     EC_CHECK(s->cand.ensure(Nn * 4));
     EC_CHECK(s->succ.ensure(Nn * 4));
     EC_CHECK(s->pred.ensure(Nn * 4));
-    EC_CHECK(s->st0.ensure(Nn * sizeof(Jump)));
-    EC_CHECK(s->st1.ensure(Nn * sizeof(Jump)));
     if (U) {
-        // every k_neighbors thread with odd x reads upal of its even sibling: write upal first
         k_neighbors<<<grid_for(N, B), B, 0, st>>>(s->table.as<Slot>(), cap - 1, s->dkey.as<unsigned long long>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
-                                                 s->cand.as<unsigned int>());
+                                                 s->cand.as<unsigned int>(), &dsc->npal);
         k_succ<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(),
                                             N, s->succ.as<unsigned int>());
+        k_pred<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
+                                            s->pred.as<unsigned int>());
     }
     mark(s, 2 * EC_STAGE_LINKS + 1);
 
-    // ---- rank -----------------------------------------------------------------------------
+    // ---- rank (sparse ruling set + weighted Wyllie on the rulers) -------------------------
     mark(s, 2 * EC_STAGE_RANK);
-    int rounds = 1;
-    while ((1ull << (rounds - 1)) < (unsigned long long)Nn) rounds++;
-    rounds = std::min(rounds + 1, 63);
-    s->stats.rank_rounds = rounds;
+    EC_CHECK(s->rid.ensure(Nn * 4));
+    EC_CHECK(s->roff.ensure(Nn * 4));
+    EC_CHECK(s->rlist.ensure(Nn * 4));
+    EC_CHECK(s->nextR.ensure(Nn * 4));
+    EC_CHECK(s->st0.ensure(Nn * sizeof(RJump)));
+    EC_CHECK(s->st1.ensure(Nn * sizeof(RJump)));
+    EC_CHECK(s->PK.ensure(Nn * 4));
+    EC_CHECK(s->RK.ensure(Nn * 4));
+    EC_CHECK(s->PL.ensure(Nn * 4));
+    EC_CHECK(s->PM.ensure(Nn * 8));
+    unsigned int nr = 0;
+    RJump *fin = s->st0.as<RJump>();
+    s->stats.rank_rounds = 0;
     if (U) {
-        k_jump_init<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(),
-                                                 s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), N,
-                                                 s->pred.as<unsigned int>(), s->st0.as<Jump>());
-        Jump *bufs[2] = {s->st0.as<Jump>(), s->st1.as<Jump>()};
-        for (int r = 0; r < rounds; r++) {
-            k_jump<<<grid_for(N, B), B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], N, r ? &dsc->active[r - 1] : nullptr,
-                                                &dsc->active[r], &dsc->final_sel, (unsigned)((r + 1) & 1));
+        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 4, st));
+        const unsigned int masks[4] = {31u, 7u, 1u, 0u};
+        unsigned int r0 = 0;
+        for (int it = 0; it < 4; it++) {
+            k_rulers<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it],
+                                                  it == 0, s->rid.as<unsigned int>(), s->roff.as<unsigned int>(),
+                                                  s->rlist.as<unsigned int>(), &dsc->nr);
+            k_walk<<<2048, B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                      s->dft.as<unsigned long long>(), s->rlist.as<unsigned int>(), r0, &dsc->nr,
+                                      masks[it], s->rid.as<unsigned int>(), s->roff.as<unsigned int>(),
+                                      s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
+            EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+            EC_HIP(hipStreamSynchronize(st));
+            r0 = hsc.nr;
+            if (hsc.nvisited + hsc.npal >= N) break;
         }
-    }
-    mark(s, 2 * EC_STAGE_RANK + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
-    Jump *fin = (hsc.final_sel & 1) ? s->st1.as<Jump>() : s->st0.as<Jump>();
-    if (U) {
-        unsigned int used = 0;
-        for (int r = 0; r < rounds; r++)
-            if (hsc.active[r]) used = r + 2;
-        s->stats.rank_rounds = std::min<unsigned int>(used ? used : 1, rounds);
-        if (hsc.active[rounds - 1] != 0) {
-            set_error("list ranking did not converge in %d rounds", rounds);
+        nr = hsc.nr;
+        if (hsc.nvisited + hsc.npal != N) {
+            set_error("ruling set covered %llu of %u nodes", (unsigned long long)(hsc.nvisited + hsc.npal), N);
             s->events = saved_events;
             return EC_ERR_STATE;
         }
+        k_rjump_init<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), nr, s->st0.as<RJump>());
+        int rounds = 1;
+        while ((1ull << (rounds - 1)) < (unsigned long long)nr) rounds++;
+        rounds = std::min(rounds + 1, 63);
+        RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
+        for (int r = 0; r < rounds; r++)
+            k_rjump<<<grid_for(nr, B), B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], nr, N,
+                                                  r ? &dsc->active[r - 1] : nullptr, &dsc->active[r],
+                                                  &dsc->final_sel, (unsigned)((r + 1) & 1));
+        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        unsigned int used = 1;
+        for (int r = 0; r < rounds; r++)
+            if (hsc.active[r]) used = r + 2;
+        s->stats.rank_rounds = std::min<unsigned int>(used, rounds);
+        if (hsc.active[rounds - 1] != 0) {
+            set_error("ruler list ranking did not converge in %d rounds", rounds);
+            s->events = saved_events;
+            return EC_ERR_STATE;
+        }
+        fin = (hsc.final_sel & 1) ? s->st1.as<RJump>() : s->st0.as<RJump>();
+        k_finalize<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(),
+                                                s->rid.as<unsigned int>(), s->roff.as<unsigned int>(),
+                                                s->rlist.as<unsigned int>(), fin, N, s->PK.as<unsigned int>(),
+                                                s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
+                                                s->PM.as<unsigned long long>());
+        k_cycle_len<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), fin, nr,
+                                                  s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
     }
+    s->stats.n_rulers = nr;
+    mark(s, 2 * EC_STAGE_RANK + 1);
 
     // ---- starts + order -------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_STARTS);
-    EC_CHECK(s->startOf.ensure(Nn * 4));
     EC_CHECK(s->cidxOf.ensure(Nn * 4));
     EC_CHECK(s->skeys.ensure(Nn * 8));
     EC_CHECK(s->svals.ensure(Nn * 4));
     EC_CHECK(s->skeys2.ensure(Nn * 8));
     EC_CHECK(s->svals2.ensure(Nn * 4));
-    EC_HIP(hipMemsetAsync(s->startOf.p, 0xFF, Nn * 4, st));
     EC_HIP(hipMemsetAsync(s->cidxOf.p, 0xFF, Nn * 4, st));
     if (U)
-        k_starts<<<grid_for(N, B), B, 0, st>>>(fin, s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
-                                              s->dft.as<unsigned long long>(), N, s->startOf.as<unsigned int>(),
-                                              s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(),
-                                              &dsc->nstarts);
+        k_starts<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
+                                              s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                              s->PM.as<unsigned long long>(), N, s->skeys.as<unsigned long long>(),
+                                              s->svals.as<unsigned int>(), &dsc->nstarts);
     EC_HIP(hipMemcpyAsync(&hsc.nstarts, &dsc->nstarts, 4, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     const unsigned int nc = hsc.nstarts;
@@ -904,8 +1029,9 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     EC_CHECK(s->coff.ensure((size_t)(nc + 1) * 8));
     EC_HIP(hipMemsetAsync(s->clen.p, 0, (size_t)(nc + 1) * 8, st));
     if (nc) {
-        k_contig_len<<<grid_for(nc, B), B, 0, st>>>(fin, s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), sorted_nodes,
-                                                   nc, k, s->cidxOf.as<unsigned int>(), s->clen.as<unsigned long long>());
+        k_contig_len<<<grid_for(nc, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(),
+                                                   s->RK.as<unsigned int>(), s->PL.as<unsigned int>(), sorted_nodes, nc,
+                                                   k, s->cidxOf.as<unsigned int>(), s->clen.as<unsigned long long>());
     }
     EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
     s->h_coff.assign(nc + 1, 0);
@@ -925,11 +1051,12 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
     EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
     if (U)
-        k_emit<<<grid_for(N, B), B, 0, st>>>(fin, s->upal.as<uint8_t>(), s->pred.as<unsigned int>(),
-                                            s->dkey.as<unsigned long long>(), s->cidxOf.as<unsigned int>(), sorted_nodes,
-                                            s->coff.as<unsigned long long>(), N, k, s->chars.as<char>(),
-                                            s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(),
-                                            s->headOf.as<unsigned int>(), s->tailOf.as<unsigned int>());
+        k_emit<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
+                                            s->PL.as<unsigned int>(), s->dkey.as<unsigned long long>(),
+                                            s->cidxOf.as<unsigned int>(), sorted_nodes, s->coff.as<unsigned long long>(),
+                                            N, k, s->chars.as<char>(), s->cfirst.as<unsigned int>(),
+                                            s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
+                                            s->tailOf.as<unsigned int>());
     mark(s, 2 * EC_STAGE_EMIT + 1);
 
     // ---- GFA ------------------------------------------------------------------------------
@@ -962,14 +1089,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     }
     s->stats.n_links = s->h_links.size();
 
-    // dict count (len(build()))
-    uint64_t npal = 0;
-    if (U) {
-        std::vector<uint8_t> pal(U);
-        EC_HIP(hipMemcpy(pal.data(), s->upal.p, U, hipMemcpyDeviceToHost));
-        for (auto v : pal) npal += v;
-    }
-    s->stats.n_dict = 2ull * U - npal;
+    s->stats.n_dict = 2ull * U - hsc.npal;  // len(build()): palindromes have one entry
 
     if (timing) {
         for (int i = 0; i < EC_NSTAGES; i++) {
@@ -1033,7 +1153,8 @@ int ec_session_destroy(ec_session *s) {
     DevBuf *all[] = {&s->h_reads, &s->h_offsets, &s->hll, &s->scal, &s->table, &s->dkey, &s->dcnt, &s->dfc, &s->dft,
                      &s->upal, &s->outdeg, &s->cand, &s->succ, &s->pred, &s->st0, &s->st1, &s->startOf, &s->skeys,
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
-                     &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts};
+                     &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
+                     &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM};
     for (auto *b : all) b->release();
     if (s->events)
         for (auto &e : s->ev) hipEventDestroy(e);

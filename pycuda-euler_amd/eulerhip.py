@@ -58,6 +58,7 @@ class Stats(ctypes.Structure):
         ("table_capacity", ctypes.c_uint64),
         ("table_retries", ctypes.c_uint32),
         ("rank_rounds", ctypes.c_uint32),
+        ("n_rulers", ctypes.c_uint64),
         ("stage_ms", ctypes.c_float * EC_NSTAGES),
         ("count_kernel_ms", ctypes.c_float),
     ]
