@@ -50,10 +50,15 @@ def alg_bytes(P, R, L, U, K=8):
     return R * L + P * (K + 8) + U * (10 * K + 33)
 
 
-def count_kernel_bytes(P, R, L, K=8):
-    """Algorithmic bytes of the dominant (count) kernel per launch: read the ASCII reads once
-    (R*L) + one canonical insert per position (key compare K + 4-B count RMW = K+8)."""
-    return R * L + P * (K + 8)
+def kernel_alg_bytes(name, P, R, L, K=8):
+    """Algorithmic bytes per launch of the counting kernels (DESIGN.md "Roofline accounting"):
+    k_upsweep   reads the ASCII reads once                       R*L
+    k_downsweep reads them again + writes one 16-B record/pos    R*L + 16*P
+    k_bucket    one canonical insert per position   P*(K+8)
+    k_count     general path: read once + one insert/position    R*L + P*(K+8)
+    k_refine    reads + writes every 16-B record once            32*P"""
+    return {"k_upsweep": R * L, "k_downsweep": R * L + 16 * P, "k_bucket": P * (K + 8),
+            "k_count": R * L + P * (K + 8), "k_refine": 32 * P}[name]
 
 
 def cpu_baseline(buf, off, k, sample_reads):
@@ -74,7 +79,7 @@ def cpu_baseline(buf, off, k, sample_reads):
             "cpu": platform.processor() or platform.machine()}
 
 
-def load_traffic(workload):
+def load_traffic(workload, kernel):
     """HBM bytes per count-kernel launch from rocprofv3 PMC passes (profiles/traffic_*.json,
     written by profiles/collect_traffic.py; FETCH_SIZE doubled per the gfx950 note)."""
     import glob
@@ -85,7 +90,7 @@ def load_traffic(workload):
             d = json.load(open(fn))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("kernel_bytes_per_launch"):
+        if d.get("workload") == workload and d.get("kernel") == kernel and d.get("kernel_bytes_per_launch"):
             best = d
     return best
 
@@ -147,13 +152,13 @@ def main():
     if dist:
         dist.barrier()
     stage = np.zeros(eulerhip.EC_NSTAGES)
-    count_ms = []
+    kern = np.zeros(eulerhip.EC_NKERNELS)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step(True)
         st = sess.stats() if world == 1 else runner.stats()
         stage += np.array(list(st.stage_ms))
-        count_ms.append(st.count_kernel_ms)
+        kern += np.array(list(st.kernel_ms))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -174,14 +179,18 @@ def main():
             dist.destroy_process_group()
         return
 
-    avg_count_ms = float(np.mean(count_ms))
-    kb = count_kernel_bytes(P if world == 1 else P // world, R // world, L)
-    achieved = kb / (avg_count_ms / 1e3) / 1e9
-    tr = load_traffic(cfg["name"])
+    kern /= args.steps
+    kid = int(np.argmax(kern))
+    kname = eulerhip.KERNEL_NAMES[kid]
+    kms = float(kern[kid])
+    kb = kernel_alg_bytes(kname, P if world == 1 else P // world, R // world, L)
+    achieved = kb / (kms / 1e3) / 1e9
+    tr = load_traffic(cfg["name"], kname)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": (tr["kernel_bytes_per_launch"] if tr else None),
-            "kernel": "k_count", "kernel_ms": round(avg_count_ms, 4), "alg_bytes_per_launch": int(kb),
+            "kernel": kname, "kernel_ms": round(kms, 4), "alg_bytes_per_launch": int(kb),
+            "kernels_ms": {eulerhip.KERNEL_NAMES[i]: round(float(kern[i]), 4) for i in range(len(kern))},
             "pipeline_alg_bytes": int(alg_bytes(P, R, L, U)),
             "pipeline_frac": round(alg_bytes(P, R, L, U) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
     cpu = None
@@ -195,6 +204,7 @@ def main():
         "data": "synthetic (iid ACGT genome, uniform error-free 100 bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)" % cfg["seed"],
         "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
                    "positions": P, "solid_kmers": U, "contigs": int(st.n_contigs),
+                   "count_path": ["partitioned", "general"][int(st.count_path)], "buckets": int(st.n_buckets),
                    "parallelism": "dp%d" % world},
         "roofline": roof,
         "cpu_baseline": cpu,

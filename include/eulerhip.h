@@ -48,6 +48,7 @@ typedef struct ec_session ec_session;
 
 #define EC_FLAG_WANT_DICT 1u /* also keep build()'s ordered dict for ec_copy_dict */
 #define EC_FLAG_TIMING 2u    /* record per-stage HIP-event times (ec_stats.stage_ms) */
+#define EC_FLAG_GENERAL 4u   /* force the general (single HBM hash table) counting path */
 
 #define EC_NSTAGES 8
 /* stage ids for ec_stats.stage_ms / ec_stage_name */
@@ -60,6 +61,17 @@ typedef struct ec_session ec_session;
 #define EC_STAGE_EMIT 6    /* contig strings (contig_to_string:44-45)                     */
 #define EC_STAGE_GFA 7     /* GFA link table G (all_contigs:90-109)                       */
 
+#define EC_NKERNELS 5
+/* kernel ids for ec_stats.kernel_ms (EC_FLAG_TIMING) */
+#define EC_KERNEL_UPSWEEP 0   /* encode pass 1: alphabet, P, HyperLogLog, bucket histogram   */
+#define EC_KERNEL_DOWNSWEEP 1 /* encode pass 2: 16-B k-mer records scattered by bucket       */
+#define EC_KERNEL_BUCKET 2    /* per-bucket LDS counting + solid filter + compaction          */
+#define EC_KERNEL_COUNT 3     /* general path: HBM hash-table counting                        */
+#define EC_KERNEL_REFINE 4    /* split coarse bucket runs into final buckets (LDS sort)       */
+
+#define EC_PATH_PARTITIONED 0 /* radix-partitioned LDS counting (count_part.h)               */
+#define EC_PATH_GENERAL 1     /* single HBM hash table (count_global.h)                      */
+
 typedef struct {
     uint64_t n_reads;
     uint64_t n_positions;    /* P: forward k-mer windows over all N-split segments            */
@@ -70,12 +82,14 @@ typedef struct {
     uint64_t n_contigs;
     uint64_t n_contig_chars;
     uint64_t n_links;
-    uint64_t table_capacity; /* hash slots (32 B each)                                         */
+    uint64_t table_capacity; /* general path: HBM hash slots; partitioned: buckets * LDS slots */
+    uint64_t n_rulers;       /* sparse ruling-set size used by the list ranking               */
     uint32_t table_retries;
-    uint32_t rank_rounds;    /* Wyllie rounds on the ruler list                            */
-    uint64_t n_rulers;       /* sparse ruling-set size used by the list ranking            */
-    float stage_ms[EC_NSTAGES]; /* EC_FLAG_TIMING only */
-    float count_kernel_ms;      /* EC_FLAG_TIMING: the count kernel alone (dominant kernel)    */
+    uint32_t rank_rounds;    /* Wyllie rounds on the ruler list                               */
+    uint32_t count_path;     /* EC_PATH_*                                                     */
+    uint32_t n_buckets;      /* partitioned path: B                                           */
+    float stage_ms[EC_NSTAGES];   /* EC_FLAG_TIMING only */
+    float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING only */
 } ec_stats;
 
 int ec_session_create(ec_session **out, int device);

@@ -18,6 +18,8 @@
 //   emit     thread/node : closed-form position of every node in its contig walk
 //   gfa      thread/contig: heads/tails lookups -> G
 #include "common.h"
+#include "count_global.h"
+#include "graph.h"
 
 #include <rocprim/rocprim.hpp>
 
@@ -25,693 +27,9 @@
 #include <cmath>
 #include <vector>
 
+#include "count_part.h"
+
 namespace ec {
-
-// ---------------------------------------------------------------------------------------
-// hash slot: 32 B, one per distinct canonical k-mer.  key + count + dense id + the first
-// insertion event of the canonical string (fC) and of its twin (fT).
-struct alignas(32) Slot {
-    unsigned long long key;
-    unsigned int count;
-    unsigned int idx;
-    unsigned long long fC;
-    unsigned long long fT;
-};
-static_assert(sizeof(Slot) == 32, "slot layout");
-
-constexpr int HLL_BITS = 12;
-constexpr int HLL_M = 1 << HLL_BITS;
-constexpr int MAX_PROBE = 1 << 14;
-
-// sequential byte reader over aligned 32-bit words (an aligned word never crosses a page,
-// so reading the word that holds a valid byte is always in-bounds of the allocation)
-struct ByteReader {
-    uint64_t base;  // absolute address of byte 0
-    uint64_t wpos;
-    uint32_t word;
-    __device__ ByteReader(const uint8_t *b) : base((uint64_t)b), wpos(~0ull), word(0) {}
-    __device__ inline uint32_t operator()(uint64_t pos) {
-        const uint64_t addr = base + pos;
-        const uint64_t a = addr & ~3ull;
-        if (a != wpos) {
-            wpos = a;
-            word = *reinterpret_cast<const uint32_t *>(a);
-        }
-        return (word >> ((addr & 3) * 8)) & 0xFFu;
-    }
-};
-
-// Iterate the windows of read r in reference insertion order (build:27-35).  For every
-// valid window calls fn(fwd, rc, ef, er): fwd/rc = 2-bit codes of the window and of its
-// twin, ef/er = the dict insertion events of the forward string (build:31-32) and of the
-// twin string (build:33-35, window j of twin(seg) is the twin of forward window m-1-j).
-// Event = (read << 32) | local, local = 2*wb + i (forward) or 2*wb + 2m-1-i (twin).
-template <typename Fn>
-__device__ inline uint32_t for_each_window(ByteReader &rd, uint64_t s, uint64_t len, int k,
-                                           uint64_t r, Fn &&fn) {
-    const uint64_t mask = kmask64(k);
-    const int sh = 2 * (k - 1);
-    uint32_t wb = 0;
-    uint64_t p = 0;
-    while (p < len) {
-        uint64_t q = p;
-        while (q < len && base_code(rd(s + q)) < 4) q++;
-        if (q - p >= (uint64_t)k) {
-            const uint32_t m = (uint32_t)(q - p - k + 1);
-            uint64_t fwd = 0, rc = 0;
-            for (uint64_t t = p; t < q; t++) {
-                const uint64_t b = base_code(rd(s + t));
-                fwd = ((fwd << 2) | b) & mask;
-                rc = (rc >> 2) | ((3ull - b) << sh);
-                if (t - p + 1 >= (uint64_t)k) {
-                    const uint32_t i = (uint32_t)(t - p + 1 - k);
-                    const uint64_t ef = (r << 32) | (uint64_t)(2 * wb + i);
-                    const uint64_t er = (r << 32) | (uint64_t)(2 * wb + 2 * m - 1 - i);
-                    fn(fwd, rc, ef, er);
-                }
-            }
-            wb += m;
-        }
-        p = q + 1;
-    }
-    return wb;
-}
-
-// ---------------------------------------------------------------------------------------
-// prescan: alphabet, positions, HyperLogLog registers (one LDS copy per block)
-__global__ void __launch_bounds__(256) k_prescan(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
-                                                 int k, uint8_t *hll_blocks, unsigned long long *npos,
-                                                 unsigned long long *bad) {
-    __shared__ uint32_t reg[HLL_M];
-    for (int i = threadIdx.x; i < HLL_M; i += blockDim.x) reg[i] = 0;
-    __syncthreads();
-    unsigned long long mypos = 0;
-    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nreads;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t s = off[r], len = off[r + 1] - s;
-        ByteReader rd(buf);
-        for (uint64_t t = 0; t < len; t++) {
-            if (base_code(rd(s + t)) == 5) {
-                atomicMin(bad, (unsigned long long)(s + t));
-                break;
-            }
-        }
-        mypos += for_each_window(rd, s, len, k, r, [&](uint64_t fwd, uint64_t rc, uint64_t, uint64_t) {
-            const uint64_t c = fwd < rc ? fwd : rc;
-            const uint64_t h = mix64(c);
-            const uint32_t j = (uint32_t)(h >> (64 - HLL_BITS));
-            const uint64_t w = (h << HLL_BITS) | (1ull << (HLL_BITS - 1));
-            const uint32_t rho = (uint32_t)__clzll((long long)w) + 1;
-            atomicMax(&reg[j], rho);
-        });
-    }
-    // block reduce positions
-    for (int o = 32; o > 0; o >>= 1) mypos += __shfl_down(mypos, o);
-    if ((threadIdx.x & 63) == 0 && mypos) atomicAdd(npos, mypos);
-    __syncthreads();
-    for (int i = threadIdx.x; i < HLL_M; i += blockDim.x) hll_blocks[(uint64_t)blockIdx.x * HLL_M + i] = (uint8_t)reg[i];
-}
-
-__global__ void __launch_bounds__(1024) k_hll_final(const uint8_t *hll_blocks, int nblocks, double *est) {
-    __shared__ double red[1024];
-    __shared__ int zeros[1024];
-    double sum = 0;
-    int z = 0;
-    for (int j = threadIdx.x; j < HLL_M; j += blockDim.x) {
-        uint32_t m = 0;
-        for (int b = 0; b < nblocks; b++) m = max(m, (uint32_t)hll_blocks[(uint64_t)b * HLL_M + j]);
-        sum += ldexp(1.0, -(int)m);
-        z += (m == 0);
-    }
-    red[threadIdx.x] = sum;
-    zeros[threadIdx.x] = z;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            red[threadIdx.x] += red[threadIdx.x + o];
-            zeros[threadIdx.x] += zeros[threadIdx.x + o];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const double m = HLL_M;
-        const double alpha = 0.7213 / (1.0 + 1.079 / m);
-        double e = alpha * m * m / red[0];
-        if (e <= 2.5 * m && zeros[0] > 0) e = m * log(m / (double)zeros[0]);
-        *est = e;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_table_clear(Slot *t, uint64_t cap) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
-        Slot s;
-        s.key = EMPTY_KEY;
-        s.count = 0;
-        s.idx = NONE32;
-        s.fC = NONE64;
-        s.fT = NONE64;
-        t[i] = s;
-    }
-}
-
-// count: thread per read.  Reference semantics: d[km] += 1 for every forward window and for
-// every window of twin(seg) (build:31-35) == +1 per window on the canonical key, +2 when the
-// window is its own twin (even-k palindrome: both loops hit the same string).
-__global__ void __launch_bounds__(256) k_count(const uint8_t *buf, const uint64_t *off, uint64_t nreads, int k,
-                                               Slot *table, uint64_t capmask, unsigned int *overflow) {
-    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nreads;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t s = off[r], len = off[r + 1] - s;
-        ByteReader rd(buf);
-        for_each_window(rd, s, len, k, r, [&](uint64_t fwd, uint64_t rc, uint64_t ef, uint64_t er) {
-            const bool pal = fwd == rc;
-            const uint64_t c = fwd < rc ? fwd : rc;
-            // first events of the canonical string and of its twin
-            uint64_t eC = fwd <= rc ? ef : er;
-            uint64_t eT = fwd <= rc ? er : ef;
-            if (pal) eC = eT = ef;
-            uint64_t h = mix64(c) & capmask;
-            for (int probe = 0;; probe++) {
-                if (probe >= MAX_PROBE) {
-                    atomicOr(overflow, 1u);
-                    return;
-                }
-                Slot *sl = table + h;
-                unsigned long long cur = sl->key;
-                if (cur == EMPTY_KEY) {
-                    cur = atomicCAS(&sl->key, EMPTY_KEY, (unsigned long long)c);
-                    if (cur == EMPTY_KEY) cur = c;
-                }
-                if (cur == c) {
-                    atomicAdd(&sl->count, pal ? 2u : 1u);
-                    if (eC < sl->fC) atomicMin(&sl->fC, (unsigned long long)eC);
-                    if (eT < sl->fT) atomicMin(&sl->fT, (unsigned long long)eT);
-                    return;
-                }
-                h = (h + 1) & capmask;
-            }
-        });
-    }
-}
-
-// compact: solid (count > limit, build:37-39) slots -> dense arrays
-__global__ void __launch_bounds__(256) k_compact(Slot *table, uint64_t cap, long long limit,
-                                                 unsigned long long *dkey, unsigned int *dcnt,
-                                                 unsigned long long *dfc, unsigned long long *dft,
-                                                 unsigned int *nsolid, unsigned long long *ndistinct) {
-    __shared__ unsigned int wave_cnt[4];
-    __shared__ unsigned int base;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < cap; i0 += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t i = i0 + threadIdx.x;
-        Slot sl;
-        bool present = false, solid = false;
-        if (i < cap) {
-            sl = table[i];
-            present = sl.key != EMPTY_KEY;
-            solid = present && (long long)sl.count > limit;
-        }
-        const unsigned long long m = __ballot(solid);
-        const unsigned long long mp = __ballot(present);
-        const unsigned int before = __popcll(m & ((1ull << lane) - 1));
-        if (lane == 0) {
-            wave_cnt[wid] = __popcll(m);
-            if (mp) atomicAdd(ndistinct, (unsigned long long)__popcll(mp));
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned int tot = 0;
-            for (int w = 0; w < 4; w++) {
-                unsigned int c = wave_cnt[w];
-                wave_cnt[w] = tot;
-                tot += c;
-            }
-            base = tot ? atomicAdd(nsolid, tot) : 0;
-        }
-        __syncthreads();
-        if (solid) {
-            const unsigned int u = base + wave_cnt[wid] + before;
-            dkey[u] = sl.key;
-            dcnt[u] = sl.count;
-            dfc[u] = sl.fC;
-            dft[u] = sl.fT;
-            table[i].idx = u;
-        }
-        __syncthreads();
-    }
-}
-
-__device__ inline unsigned int lookup(const Slot *table, uint64_t capmask, uint64_t c) {
-    uint64_t h = mix64(c) & capmask;
-    for (int probe = 0; probe < MAX_PROBE; probe++) {
-        const unsigned long long kk = table[h].key;
-        if (kk == c) return table[h].idx;
-        if (kk == EMPTY_KEY) return NONE32;
-        h = (h + 1) & capmask;
-    }
-    return NONE32;
-}
-
-// oriented node id: 2u + o (o = 1: twin of the canonical string); palindromes use o = 0 only
-__device__ inline uint64_t node_code(const unsigned long long *dkey, unsigned int x, int k) {
-    const uint64_t c = dkey[x >> 1];
-    return (x & 1) ? twin64(c, k) : c;
-}
-__device__ inline unsigned int twin_node(const uint8_t *upal, unsigned int x) {
-    return upal[x >> 1] ? x : (x ^ 1u);
-}
-
-// links phase 1: out-degree (number of fw(x) in d, get_contig_forward:63) + the unique candidate
-__global__ void __launch_bounds__(256) k_neighbors(const Slot *table, uint64_t capmask, const unsigned long long *dkey,
-                                                   unsigned int U, int k, uint8_t *upal, uint8_t *outdeg,
-                                                   unsigned int *cand, unsigned int *npal) {
-    const uint64_t mask = kmask64(k);
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < 2ull * U; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        const uint64_t c = dkey[x >> 1];
-        const uint64_t tc = twin64(c, k);
-        const bool pal = tc == c;
-        if (x & 1) {
-            if (pal) {  // the palindrome has a single dict entry: node 2u+1 does not exist
-                outdeg[x] = 0;
-                cand[x] = NONE32;
-                continue;
-            }
-        } else {
-            upal[x >> 1] = pal ? 1 : 0;
-            if (pal) atomicAdd(npal, 1u);
-        }
-        const uint64_t xs = (x & 1) ? tc : c;
-        unsigned int n = 0, cd = NONE32;
-        for (int b = 0; b < 4; b++) {
-            const uint64_t y = ((xs << 2) | (uint64_t)b) & mask;
-            const uint64_t ty = twin64(y, k);
-            const uint64_t cy = y < ty ? y : ty;
-            const unsigned int u = lookup(table, capmask, cy);
-            if (u != NONE32) {
-                if (n == 0) cd = 2 * u + (y != cy ? 1u : 0u);
-                n++;
-            }
-        }
-        outdeg[x] = (uint8_t)n;
-        cand[x] = n == 1 ? cd : NONE32;
-    }
-}
-
-// links phase 2: x -> y iff |fw(x) in d| == 1, |bw(y) in d| == 1 and y != twin(x)
-// (get_contig_forward:63-73; the cand == km / twin(km) stop is applied by the walk emulation)
-// |bw(y) in d| == |fw(twin y) in d| == outdeg[twin y].
-__global__ void __launch_bounds__(256) k_succ(const uint8_t *upal, const uint8_t *outdeg, const unsigned int *cand,
-                                              unsigned int N, unsigned int *succ) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        unsigned int s = NONE32;
-        const unsigned int y = cand[x];
-        if (y != NONE32 && !((x & 1) && upal[x >> 1])) {
-            const unsigned int ty = twin_node(upal, y);
-            if (outdeg[ty] == 1 && y != twin_node(upal, x)) s = y;
-        }
-        succ[x] = s;
-    }
-}
-
-__device__ inline unsigned long long first_event(const unsigned long long *dfc, const unsigned long long *dft,
-                                                 unsigned int x) {
-    return (x & 1) ? dft[x >> 1] : dfc[x >> 1];
-}
-
-// pred(x) = twin(succ(twin(x))): the links are closed under twin-reversal
-__global__ void __launch_bounds__(256) k_pred(const uint8_t *upal, const unsigned int *succ, unsigned int N,
-                                              unsigned int *pred) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        unsigned int p = NONE32;
-        if (!((x & 1) && upal[x >> 1])) {
-            const unsigned int sx = succ[twin_node(upal, x)];
-            if (sx != NONE32) p = twin_node(upal, sx);
-        }
-        pred[x] = p;
-    }
-}
-
-// ---- list ranking by a sparse ruling set ------------------------------------------------
-// Rulers: every path head plus every node whose hash hits the sampling mask.  Each ruler
-// walks its segment (up to the next ruler) serially, stamping (ruler, offset) on every node;
-// the much shorter ruler list is then ranked by weighted Wyllie pointer jumping.  Cycles
-// that drew no ruler are caught by later iterations with a denser sampling mask (the last
-// one makes every still-unvisited node a ruler).
-__device__ inline bool ruler_hash(unsigned int x, unsigned int smask) {
-    return (mix64(0x9E3779B97F4A7C15ull ^ x) & smask) == 0;
-}
-
-__global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsigned int *pred, unsigned int N,
-                                                unsigned int smask, int first, unsigned int *rid, unsigned int *roff,
-                                                unsigned int *rlist, unsigned int *nr) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        if ((x & 1) && upal[x >> 1]) continue;
-        if (rid[x] != NONE32) continue;
-        if ((first && pred[x] == NONE32) || ruler_hash(x, smask)) {
-            const unsigned int i = atomicAdd(nr, 1u);
-            rlist[i] = x;
-            rid[x] = i;
-            roff[x] = 0;
-        }
-    }
-}
-
-// ruler jump state (32 B): window = rulers i, P(i), .., P^{c-1}(i)
-struct alignas(32) RJump {
-    unsigned int a;    // P^c(i) or NONE
-    unsigned int s;    // nodes in the segments of P(i)..P^{c-1}(i)  (= rank of i's node on a path)
-    unsigned int h;    // last ruler of the window (the head ruler once a == NONE)
-    unsigned int cm;   // min ruler node id in the window
-    unsigned int cd;   // nodes from cm forward to i's node
-    unsigned int len;  // nodes in i's own segment
-    unsigned long long fm;  // min first event over the window's segments (incl. i's)
-};
-static_assert(sizeof(RJump) == 32, "rjump layout");
-
-__global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const unsigned long long *dfc,
-                                              const unsigned long long *dft, const unsigned int *rlist,
-                                              unsigned int r0, const unsigned int *nr, unsigned int smask,
-                                              unsigned int *rid, unsigned int *roff, unsigned int *nextR, RJump *rs,
-                                              unsigned long long *nvisited) {
-    const unsigned int r1 = *nr;
-    unsigned long long seen = 0;
-    for (uint64_t t = r0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < r1; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int i = (unsigned int)t;
-        unsigned int v = rlist[i];
-        unsigned long long fm = first_event(dfc, dft, v);
-        unsigned int j = 0, nx = NONE32;
-        for (;;) {
-            const unsigned int w = succ[v];
-            if (w == NONE32) break;
-            if (ruler_hash(w, smask) && rid[w] != NONE32) {  // the next ruler
-                nx = rid[w];
-                break;
-            }
-            v = w;
-            j++;
-            rid[v] = i;
-            roff[v] = j;
-            const unsigned long long f = first_event(dfc, dft, v);
-            fm = f < fm ? f : fm;
-        }
-        nextR[i] = nx;
-        RJump r;
-        r.a = NONE32;  // set from prevR by k_rjump_init
-        r.s = 0;
-        r.h = i;
-        r.cm = rlist[i];
-        r.cd = 0;
-        r.len = j + 1;
-        r.fm = fm;
-        rs[i] = r;
-        seen += j + 1;
-    }
-    for (int o = 32; o > 0; o >>= 1) seen += __shfl_down(seen, o);
-    if ((threadIdx.x & 63) == 0 && seen) atomicAdd(nvisited, seen);
-}
-
-__global__ void __launch_bounds__(256) k_rjump_init(const unsigned int *nextR, unsigned int nr, RJump *rs) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int n = nextR[t];
-        if (n != NONE32) rs[n].a = (unsigned int)t;  // prevR[next] = me (unique predecessor)
-    }
-}
-
-// one weighted Wyllie round on the ruler list
-__global__ void __launch_bounds__(256) k_rjump(const RJump *src, RJump *dst, unsigned int nr, unsigned int N,
-                                               const unsigned int *active_in, unsigned int *active_out,
-                                               unsigned int *final_sel, unsigned int sel) {
-    if (active_in && *active_in == 0) return;
-    unsigned int act = 0;
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
-        RJump j = src[t];
-        if (j.a != NONE32 && j.s < N) {
-            const RJump y = src[j.a];
-            const unsigned int back = j.s + y.len;  // nodes from ruler a's node forward to i's node
-            if (y.cm < j.cm) {
-                j.cm = y.cm;
-                j.cd = back + y.cd;
-            }
-            j.s = back + y.s;
-            j.a = y.a;
-            j.h = y.h;
-            j.fm = y.fm < j.fm ? y.fm : j.fm;
-            act += (j.a != NONE32 && j.s < N);
-        }
-        dst[t] = j;
-    }
-    for (int o = 32; o > 0; o >>= 1) act += __shfl_down(act, o);
-    if ((threadIdx.x & 63) == 0 && act) atomicAdd(active_out, act);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *final_sel = sel;
-}
-
-// per-node path descriptor: PK = path key (head node for paths, min ruler node for cycles)
-// with bit 31 = on a cycle; RK = rank (from the head / from the cycle key).  Path records
-// at the key node: PL = path / cycle length, PM = min first event over it.
-constexpr unsigned int CYC = 0x80000000u;
-
-__global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const unsigned int *succ, const unsigned int *rid,
-                                                  const unsigned int *roff, const unsigned int *rlist, const RJump *rs,
-                                                  unsigned int N, unsigned int *PK, unsigned int *RK, unsigned int *PL,
-                                                  unsigned long long *PM) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        if ((x & 1) && upal[x >> 1]) continue;
-        const unsigned int i = rid[x], j = roff[x];
-        const RJump r = rs[i];
-        if (r.a == NONE32) {  // path
-            const unsigned int pk = rlist[r.h], rk = r.s + j;
-            PK[x] = pk;
-            RK[x] = rk;
-            if (succ[x] == NONE32) {  // tail: its ruler's window spans the whole path
-                PL[pk] = rk + 1;
-                PM[pk] = r.fm;
-            }
-        } else {  // cycle
-            PK[x] = r.cm | CYC;
-            RK[x] = r.cd + j;
-        }
-    }
-}
-
-// cycle length / min: the ruler whose successor ruler is the key ruler closes the ring
-__global__ void __launch_bounds__(256) k_cycle_len(const unsigned int *nextR, const unsigned int *rlist, const RJump *rs,
-                                                   unsigned int nr, unsigned int *PL, unsigned long long *PM) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
-        const RJump r = rs[t];
-        if (r.a == NONE32) continue;
-        const unsigned int n = nextR[t];
-        if (n != NONE32 && rlist[n] == r.cm) {
-            PL[r.cm] = r.cd + r.len;
-            PM[r.cm] = r.fm;
-        }
-    }
-}
-
-__device__ inline unsigned long long path_min(const unsigned int *PK, const unsigned long long *PM, unsigned int x) {
-    return PM[PK[x] & ~CYC];
-}
-
-// start of each component (all_contigs:82-84): the oriented k-mer with the smallest first
-// event over the path and its twin path (= the first dict entry not yet `done`).
-__global__ void __launch_bounds__(256) k_starts(const uint8_t *upal, const unsigned long long *dfc,
-                                                const unsigned long long *dft, const unsigned int *PK,
-                                                const unsigned long long *PM, unsigned int N,
-                                                unsigned long long *skeys, unsigned int *svals, unsigned int *nstarts) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        if ((x & 1) && upal[x >> 1]) continue;
-        const unsigned long long f = first_event(dfc, dft, x);
-        const unsigned long long a = path_min(PK, PM, x);
-        const unsigned long long b = path_min(PK, PM, twin_node(upal, x));
-        if (f == (a < b ? a : b)) {
-            const unsigned int i = atomicAdd(nstarts, 1u);
-            skeys[i] = f;
-            svals[i] = x;
-        }
-    }
-}
-
-// geometry of the walk from start s (get_contig:47-56 + get_contig_forward:59-77):
-//   kind 0 path, twin path disjoint   : contig = the path holding s, head..tail
-//   kind 1 path equal to its twin     : p_0..p_n, s = p_j : p_0..p_{n-j-1} | p_{n-j+1}..p_n | all
-//   kind 2 cycle, twin cycle disjoint : s, succ(s), ... (n nodes)
-//   kind 3 cycle equal to its twin    : m = dist(s -> twin s): m == 0 -> all n from s,
-//                                       else p_{m+1}..p_{n-1}, p_0..p_{m-1} (n-1 nodes)
-struct Walk {
-    unsigned int kind, n, j, m, lo, len;
-};
-
-__device__ inline Walk walk_of(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
-                               const unsigned int *PL, unsigned int s) {
-    Walk w;
-    const unsigned int pk = PK[s], rk = RK[s];
-    const unsigned int ts = twin_node(upal, s);
-    const unsigned int pk2 = PK[ts], rk2 = RK[ts];
-    const bool self = pk2 == pk;
-    const unsigned int plen = PL[pk & ~CYC];
-    w.j = rk;
-    w.m = 0;
-    w.lo = 0;
-    if (!(pk & CYC)) {
-        if (!self) {
-            w.kind = 0;
-            w.n = plen;
-            w.len = plen;
-        } else {
-            w.kind = 1;
-            const unsigned int n = plen - 1, j = rk;
-            w.n = n;
-            if (2 * j < n) {
-                w.lo = 0;
-                w.len = n - j;
-            } else if (2 * j > n) {
-                w.lo = n - j + 1;
-                w.len = j;
-            } else {
-                w.lo = 0;
-                w.len = n + 1;
-            }
-        }
-    } else {
-        const unsigned int n = plen;
-        w.n = n;
-        if (!self) {
-            w.kind = 2;
-            w.len = n;
-        } else {
-            w.kind = 3;
-            w.m = (rk2 + n - rk) % n;
-            w.len = w.m == 0 ? n : n - 1;
-        }
-    }
-    return w;
-}
-
-__global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
-                                                    const unsigned int *PL, const unsigned int *sorted_nodes,
-                                                    unsigned int nc, int k, unsigned int *cidxOf,
-                                                    unsigned long long *clen) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int s = sorted_nodes[i];
-        cidxOf[PK[s] & ~CYC] = (unsigned int)i;
-        const Walk w = walk_of(upal, PK, RK, PL, s);
-        clen[i] = (unsigned long long)(k - 1) + w.len;
-    }
-}
-
-// emit: every node finds its contig through its path key, computes its walk position and
-// writes its chars (contig_to_string:44-45: first node k chars, later nodes their last base).
-__global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
-                                              const unsigned int *PL, const unsigned long long *dkey,
-                                              const unsigned int *cidxOf, const unsigned int *sorted_nodes,
-                                              const unsigned long long *coff, unsigned int N, int k, char *chars,
-                                              unsigned int *cfirst, unsigned int *clast, unsigned int *headOf,
-                                              unsigned int *tailOf) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        if ((x & 1) && upal[x >> 1]) continue;
-        const unsigned int pk = PK[x], rk = RK[x];
-        const unsigned int ci = cidxOf[pk & ~CYC];
-        if (ci == NONE32) continue;  // the twin path of a disjoint pair carries the contig
-        const unsigned int s = sorted_nodes[ci];
-        const Walk w = walk_of(upal, PK, RK, PL, s);
-        long long pos = -1;
-        if (w.kind == 0) {
-            pos = rk;
-        } else if (w.kind == 1) {
-            if (rk >= w.lo && rk < w.lo + w.len) pos = rk - w.lo;
-        } else {
-            const unsigned int i = (rk + w.n - w.j) % w.n;  // steps from s
-            if (w.kind == 2 || w.m == 0) {
-                pos = i;
-            } else if (i > w.m) {
-                pos = i - w.m - 1;
-            } else if (i < w.m) {
-                pos = w.n - 1 - w.m + i;
-            }
-        }
-        if (pos < 0) continue;
-        const uint64_t code = node_code(dkey, x, k);
-        char *dst = chars + coff[ci];
-        if (pos == 0) {
-            uint64_t c = code;
-            for (int i = k - 1; i >= 0; i--) {
-                dst[i] = "ACGT"[c & 3];
-                c >>= 2;
-            }
-            cfirst[ci] = x;
-            headOf[x] = ci;
-        } else {
-            dst[k - 1 + pos] = "ACGT"[code & 3];
-        }
-        if ((unsigned long long)pos == (unsigned long long)w.len - 1) {
-            clast[ci] = x;
-            tailOf[twin_node(upal, x)] = ci;
-        }
-    }
-}
-
-// GFA links (all_contigs:90-109): for y in fw(last kmer): heads[y] then tails[y];
-// for z in fw(twin(first kmer)): heads[z] then tails[z].  Up to 8 per side.
-__global__ void __launch_bounds__(256) k_gfa(const Slot *table, uint64_t capmask, const unsigned long long *dkey,
-                                             const uint8_t *upal, const unsigned int *cfirst, const unsigned int *clast,
-                                             const unsigned int *headOf, const unsigned int *tailOf, unsigned int nc,
-                                             int k, long long *lk, unsigned int *lcnt) {
-    const uint64_t mask = kmask64(k);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
-        for (int side = 0; side < 2; side++) {
-            const unsigned int src = side == 0 ? clast[i] : twin_node(upal, cfirst[i]);
-            const uint64_t xs = node_code(dkey, src, k);
-            unsigned int n = 0;
-            long long *o = lk + (i * 2 + side) * 8;
-            for (int b = 0; b < 4; b++) {
-                const uint64_t y = ((xs << 2) | (uint64_t)b) & mask;
-                const uint64_t ty = twin64(y, k);
-                const uint64_t cy = y < ty ? y : ty;
-                const unsigned int u = lookup(table, capmask, cy);
-                if (u == NONE32) continue;
-                const unsigned int oy = (y != cy) ? 2 * u + 1 : 2 * u;
-                const unsigned int hh = headOf[oy], tt = tailOf[oy];
-                if (hh != NONE32) o[n++] = 2ll * hh;
-                if (tt != NONE32) o[n++] = 2ll * tt + 1;
-            }
-            lcnt[i * 2 + side] = n;
-        }
-    }
-}
-
-// ordered dict of build(): every valid oriented node with its first event (sort key)
-__global__ void __launch_bounds__(256) k_dict_items(const uint8_t *upal, const unsigned long long *dfc,
-                                                    const unsigned long long *dft, unsigned int N,
-                                                    unsigned long long *keys, unsigned int *vals, unsigned int *n) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        if ((x & 1) && upal[x >> 1]) continue;
-        const unsigned int i = atomicAdd(n, 1u);
-        keys[i] = first_event(dfc, dft, x);
-        vals[i] = x;
-    }
-}
-
-__global__ void __launch_bounds__(256) k_dict_render(const unsigned int *nodes, unsigned int n,
-                                                     const unsigned long long *dkey, const unsigned int *dcnt, int k,
-                                                     char *out, unsigned int *counts) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = nodes[i];
-        uint64_t c = node_code(dkey, x, k);
-        for (int p = k - 1; p >= 0; p--) {
-            out[i * k + p] = "ACGT"[c & 3];
-            c >>= 2;
-        }
-        counts[i] = dcnt[x >> 1];
-    }
-}
 
 // ---------------------------------------------------------------------------------------
 // host side
@@ -752,6 +70,7 @@ struct ec_session {
     DevBuf h_reads, h_offsets;  // H2D staging for ec_assemble_host
     DevBuf hll, scal, table, dkey, dcnt, dfc, dft, upal, outdeg, cand, succ, pred, st0, st1;
     DevBuf rid, roff, rlist, nextR, PK, RK, PL, PM;
+    DevBuf hist, cnt, offs, bstart, tot, recs, recs2, sub;
     DevBuf startOf, skeys, svals, skeys2, svals2, cidxOf, clen, coff, chars, cfirst, clast, headOf, tailOf;
     DevBuf lk, lcnt, tmp, dchars, dcounts;
     // results (host)
@@ -763,8 +82,11 @@ struct ec_session {
     std::vector<uint64_t> h_loff;
     std::vector<int64_t> h_links;
     bool want_dict = false;
-    hipEvent_t ev[2 * EC_NSTAGES + 2] = {};
+    hipEvent_t ev[2 * EC_NSTAGES] = {};
+    hipEvent_t kev[2 * EC_NKERNELS] = {};
+    bool kused[EC_NKERNELS] = {};
     bool events = false;
+    bool timing = false;
 };
 
 namespace {
@@ -783,6 +105,8 @@ struct Scalars {  // device scalars block
     unsigned int npal;
     unsigned int pad;
     unsigned long long nvisited;
+    unsigned int maxlocal;
+    unsigned int skew;
     unsigned int active[64];
 };
 
@@ -804,7 +128,14 @@ int sort_pairs(ec_session *s, unsigned long long *kin, unsigned long long *kout,
 }
 
 inline void mark(ec_session *s, int idx) {
-    if (s->events) hipEventRecord(s->ev[idx], s->stream);
+    if (s->timing) hipEventRecord(s->ev[idx], s->stream);
+}
+// kernel-level timing events: kernel id, 0 = before / 1 = after
+inline void kmark(ec_session *s, int kid, int end) {
+    if (s->timing) {
+        hipEventRecord(s->kev[2 * kid + end], s->stream);
+        if (end) s->kused[kid] = true;
+    }
 }
 
 int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, int k, int limit,
@@ -826,10 +157,11 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     const bool timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
         for (auto &e : s->ev) EC_HIP(hipEventCreate(&e));
+        for (auto &e : s->kev) EC_HIP(hipEventCreate(&e));
         s->events = true;
     }
-    bool saved_events = s->events;
-    if (!timing) s->events = false;
+    s->timing = timing;
+    for (auto &u : s->kused) u = false;
     hipStream_t st = s->stream;
     const unsigned B = 256;
 
@@ -839,13 +171,21 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
     Scalars hsc;
 
-    // ---- prescan ------------------------------------------------------------------------
+    // ---- prescan = partition upsweep ------------------------------------------------------
     mark(s, 2 * EC_STAGE_PRESCAN);
-    const unsigned pre_blocks = grid_for(nreads ? nreads : 1, B, 1024);
-    EC_CHECK(s->hll.ensure((size_t)pre_blocks * HLL_M));
+    const uint64_t ntiles = (nreads + TILE_READS - 1) / TILE_READS;
+    uint64_t ngroups = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 1024));
+    const uint64_t gsize = std::max<uint64_t>(1, (ntiles + ngroups - 1) / ngroups) * TILE_READS;
+    ngroups = std::max<uint64_t>(1, (nreads + gsize - 1) / gsize);
+    EC_CHECK(s->hist.ensure(ngroups * FINE * 4));
+    EC_CHECK(s->hll.ensure(ngroups * (1 << HLL_REG_BITS)));
     if (nreads) {
-        k_prescan<<<pre_blocks, B, 0, st>>>(d_reads, d_off, nreads, k, s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad);
-        k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<uint8_t>(), pre_blocks, &dsc->est);
+        kmark(s, 0, 0);
+        k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
+                                                           s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad,
+                                                           &dsc->maxlocal, &dsc->skew);
+        kmark(s, 0, 1);
+        k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<uint8_t>(), (int)ngroups, HLL_REG_BITS, &dsc->est);
     }
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -854,63 +194,140 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
         uint8_t byte = 0;
         hipMemcpy(&byte, d_reads + hsc.bad, 1, hipMemcpyDeviceToHost);
         set_error("byte %llu (0x%02x) outside {A,C,G,T,N}", (unsigned long long)hsc.bad, byte);
-        s->events = saved_events;
         return EC_ERR_ALPHABET;
     }
-    s->stats.n_positions = nreads ? hsc.npos : 0;
-    s->stats.n_distinct_est = nreads ? (uint64_t)llround(hsc.est) : 0;
+    const uint64_t P = nreads ? hsc.npos : 0;
+    s->stats.n_positions = P;
+    const double est = nreads ? hsc.est : 0.0;
+    s->stats.n_distinct_est = (uint64_t)llround(est);
 
-    // ---- count (with capacity retries) ----------------------------------------------------
-    uint64_t want = (uint64_t)(std::max<double>(nreads ? hsc.est : 0, 1.0) * 2.2) + 1024;
-    want = std::min<uint64_t>(want, 2 * s->stats.n_positions + 1024);
-    uint64_t cap = 1024;
-    while (cap < want) cap <<= 1;
-    for (int attempt = 0;; attempt++) {
-        EC_CHECK(s->table.ensure(cap * sizeof(Slot)));
+    // ---- count + compact ------------------------------------------------------------------
+    // partitioned path when every bucket fits an LDS table and local events fit 16 bits
+    bool part = !(flags & EC_FLAG_GENERAL) && nreads && P && hsc.maxlocal <= MAX_LOCAL_EVENT && !hsc.skew &&
+                est / FINE <= 2400.0;
+    int bbits = 0;
+    unsigned int slots = 2048;
+    SolidIndex sidx{};
+    uint64_t umax = 0;
+    if (part) {
+        while (bbits < FINE_BITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
+        slots = est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
+        int maxc = MAX_COARSE_BITS;
+        if (const char *e = getenv("EULERHIP_COARSE_BITS")) maxc = std::max(1, std::min(MAX_COARSE_BITS, atoi(e)));
+        const int cbits = std::min(bbits, std::max(maxc, bbits - 6));  // refine splits <= 64 ways
+        const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
         mark(s, 2 * EC_STAGE_COUNT);
-        k_table_clear<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap);
-        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
-        if (timing) hipEventRecord(s->ev[2 * EC_NSTAGES], st);
-        if (nreads)
-            k_count<<<grid_for(nreads, B), B, 0, st>>>(d_reads, d_off, nreads, k, s->table.as<Slot>(), cap - 1,
-                                                      &dsc->overflow);
-        if (timing) hipEventRecord(s->ev[2 * EC_NSTAGES + 1], st);
-        mark(s, 2 * EC_STAGE_COUNT + 1);
-        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
-        if (!hsc.overflow) break;
-        if (attempt >= 4) {
-            set_error("hash table overflow at capacity %llu", (unsigned long long)cap);
-            s->events = saved_events;
-            return EC_ERR_CAPACITY;
+        EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
+        EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
+        EC_CHECK(s->tot.ensure((Bk + 1) * 8));
+        EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
+        EC_CHECK(s->recs.ensure(P * sizeof(Rec)));
+        if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * sizeof(Rec)));
+        k_coarse<<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
+                                                               s->cnt.as<unsigned long long>());
+        EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ngroups));
+        k_bucket_totals<<<grid_for(Bk + 1, B), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, bbits,
+                                                          s->tot.as<unsigned long long>());
+        EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
+        kmark(s, 1, 0);
+        k_downsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups, cbits,
+                                                             s->offs.as<unsigned long long>(), s->recs.as<Rec>());
+        kmark(s, 1, 1);
+        Rec *final_recs = s->recs.as<Rec>();
+        if (bbits > cbits) {
+            kmark(s, 4, 0);
+            k_refine<<<(unsigned)Ck, BUCKET_THREADS, 0, st>>>(s->recs.as<Rec>(), s->recs2.as<Rec>(),
+                                                             s->bstart.as<unsigned long long>(), cbits, bbits);
+            kmark(s, 4, 1);
+            final_recs = s->recs2.as<Rec>();
         }
-        cap <<= 2;
-        s->stats.table_retries++;
+        mark(s, 2 * EC_STAGE_COUNT + 1);
+        mark(s, 2 * EC_STAGE_COMPACT);
+        umax = Bk * slots;
+        EC_CHECK(s->dkey.ensure(umax * 8));
+        EC_CHECK(s->dcnt.ensure(umax * 4));
+        EC_CHECK(s->dfc.ensure(umax * 8));
+        EC_CHECK(s->dft.ensure(umax * 8));
+        EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
+        kmark(s, 2, 0);
+        if (slots == 2048)
+            k_bucket<2048><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
+                final_recs, s->bstart.as<unsigned long long>(), (long long)limit,
+                s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+        else
+            k_bucket<4096><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
+                final_recs, s->bstart.as<unsigned long long>(), (long long)limit,
+                s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+        kmark(s, 2, 1);
+        mark(s, 2 * EC_STAGE_COMPACT + 1);
+        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (hsc.overflow) {  // a bucket outgrew its LDS table: redo on the general path
+            part = false;
+            s->stats.table_retries++;
+            EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
+            EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
+            EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        } else {
+            sidx.sub = s->sub.as<SubSlot>();
+            sidx.bbits = bbits;
+            sidx.slots = slots;
+            s->stats.count_path = EC_PATH_PARTITIONED;
+            s->stats.n_buckets = (uint32_t)Bk;
+            s->stats.table_capacity = umax;
+        }
     }
-    s->stats.table_capacity = cap;
-
-    // ---- compact --------------------------------------------------------------------------
-    mark(s, 2 * EC_STAGE_COMPACT);
-    // dense arrays sized by the distinct estimate bound: at most cap/1 entries
-    // (allocate lazily after knowing U is cheaper but needs a sync; size by cap)
-    const uint64_t umax = cap;
-    EC_CHECK(s->dkey.ensure(umax * 8));
-    EC_CHECK(s->dcnt.ensure(umax * 4));
-    EC_CHECK(s->dfc.ensure(umax * 8));
-    EC_CHECK(s->dft.ensure(umax * 8));
-    k_compact<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap, (long long)limit,
-                                                   s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
-                                                   s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-                                                   &dsc->nsolid, &dsc->ndistinct);
-    mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    if (!part) {
+        uint64_t want = (uint64_t)(std::max<double>(est, 1.0) * 2.2) + 1024;
+        want = std::min<uint64_t>(want, 2 * P + 1024);
+        uint64_t cap = 1024;
+        while (cap < want) cap <<= 1;
+        for (int attempt = 0;; attempt++) {
+            EC_CHECK(s->table.ensure(cap * sizeof(Slot)));
+            mark(s, 2 * EC_STAGE_COUNT);
+            k_table_clear<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap);
+            EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+            kmark(s, 3, 0);
+            if (nreads)
+                k_count<<<grid_for(nreads, B), B, 0, st>>>(d_reads, d_off, nreads, k, s->table.as<Slot>(), cap - 1,
+                                                          &dsc->overflow);
+            kmark(s, 3, 1);
+            mark(s, 2 * EC_STAGE_COUNT + 1);
+            EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
+            EC_HIP(hipStreamSynchronize(st));
+            if (!hsc.overflow) break;
+            if (attempt >= 4) {
+                set_error("hash table overflow at capacity %llu", (unsigned long long)cap);
+                return EC_ERR_CAPACITY;
+            }
+            cap <<= 2;
+            s->stats.table_retries++;
+        }
+        s->stats.table_capacity = cap;
+        mark(s, 2 * EC_STAGE_COMPACT);
+        umax = cap;
+        EC_CHECK(s->dkey.ensure(umax * 8));
+        EC_CHECK(s->dcnt.ensure(umax * 4));
+        EC_CHECK(s->dfc.ensure(umax * 8));
+        EC_CHECK(s->dft.ensure(umax * 8));
+        k_compact<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap, (long long)limit,
+                                                       s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+                                                       s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                       &dsc->nsolid, &dsc->ndistinct);
+        mark(s, 2 * EC_STAGE_COMPACT + 1);
+        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        sidx.table = s->table.as<Slot>();
+        sidx.capmask = cap - 1;
+        s->stats.count_path = EC_PATH_GENERAL;
+    }
     const unsigned int U = hsc.nsolid;
     s->stats.n_distinct = hsc.ndistinct;
     s->stats.n_solid = U;
-    if (2ull * U >= 0xFFFFFFF0ull) {
-        set_error("too many solid k-mers (%u) for 32-bit node ids", U);
-        s->events = saved_events;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
     }
     const unsigned int N = 2 * U;
@@ -924,7 +341,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     EC_CHECK(s->succ.ensure(Nn * 4));
     EC_CHECK(s->pred.ensure(Nn * 4));
     if (U) {
-        k_neighbors<<<grid_for(N, B), B, 0, st>>>(s->table.as<Slot>(), cap - 1, s->dkey.as<unsigned long long>(), U, k,
+        k_neighbors<<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<unsigned long long>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
                                                  s->cand.as<unsigned int>(), &dsc->npal);
         k_succ<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(),
@@ -969,8 +386,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
         nr = hsc.nr;
         if (hsc.nvisited + hsc.npal != N) {
             set_error("ruling set covered %llu of %u nodes", (unsigned long long)(hsc.nvisited + hsc.npal), N);
-            s->events = saved_events;
-            return EC_ERR_STATE;
+                return EC_ERR_STATE;
         }
         k_rjump_init<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), nr, s->st0.as<RJump>());
         int rounds = 1;
@@ -989,8 +405,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
         s->stats.rank_rounds = std::min<unsigned int>(used, rounds);
         if (hsc.active[rounds - 1] != 0) {
             set_error("ruler list ranking did not converge in %d rounds", rounds);
-            s->events = saved_events;
-            return EC_ERR_STATE;
+                return EC_ERR_STATE;
         }
         fin = (hsc.final_sel & 1) ? s->st1.as<RJump>() : s->st0.as<RJump>();
         k_finalize<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(),
@@ -1064,7 +479,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     EC_CHECK(s->lk.ensure((size_t)std::max(nc, 1u) * 16 * 8));
     EC_CHECK(s->lcnt.ensure((size_t)std::max(nc, 1u) * 2 * 4));
     if (nc)
-        k_gfa<<<grid_for(nc, B), B, 0, st>>>(s->table.as<Slot>(), cap - 1, s->dkey.as<unsigned long long>(),
+        k_gfa<<<grid_for(nc, B), B, 0, st>>>(sidx, s->dkey.as<unsigned long long>(),
                                             s->upal.as<uint8_t>(), s->cfirst.as<unsigned int>(),
                                             s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
                                             s->tailOf.as<unsigned int>(), nc, k, s->lk.as<long long>(),
@@ -1097,11 +512,12 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
             hipEventElapsedTime(&ms, s->ev[2 * i], s->ev[2 * i + 1]);
             s->stats.stage_ms[i] = ms;
         }
-        float ms = 0;
-        hipEventElapsedTime(&ms, s->ev[2 * EC_NSTAGES], s->ev[2 * EC_NSTAGES + 1]);
-        s->stats.count_kernel_ms = ms;
+        for (int i = 0; i < EC_NKERNELS; i++) {
+            float ms = 0;
+            if (s->kused[i]) hipEventElapsedTime(&ms, s->kev[2 * i], s->kev[2 * i + 1]);
+            s->stats.kernel_ms[i] = ms;
+        }
     }
-    s->events = saved_events || timing;
     s->have = true;
     return EC_OK;
 }
@@ -1154,10 +570,13 @@ int ec_session_destroy(ec_session *s) {
                      &s->upal, &s->outdeg, &s->cand, &s->succ, &s->pred, &s->st0, &s->st1, &s->startOf, &s->skeys,
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
-                     &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM};
+                     &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
+                     &s->hist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub};
     for (auto *b : all) b->release();
-    if (s->events)
+    if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);
+        for (auto &e : s->kev) hipEventDestroy(e);
+    }
     if (s->own_stream && s->stream) hipStreamDestroy(s->stream);
     delete s;
     return EC_OK;

@@ -1,0 +1,424 @@
+// count_part.h -- partitioned k-mer counting (the production path of build:25-42).
+//
+// Instead of one HBM hash table hit by a global atomic per k-mer position, the positions
+// are radix-partitioned by the top bits of mix64(canonical key) into B buckets and each
+// bucket is counted in a 2048-slot hash table in LDS by one workgroup:
+//
+//   k_upsweep    per read group : LDS-staged reads -> windows -> alphabet check, P,
+//                                 HyperLogLog registers, 4096-way fine histogram
+//   (host)                      : B = 2^bbits from the distinct estimate (<= ~1024 keys per bucket)
+//   k_coarse     per (bucket,group): coarse counts, bucket-major; exclusive scan -> offsets
+//   k_downsweep  per read group : windows again -> 16-B records {key, read, local events}
+//                                 scattered to their (bucket, group) run
+//   k_bucket     per bucket     : records -> LDS table (CAS insert, count += 1|2, 64-bit
+//                                 atomicMin of first events) -> solid filter (count > limit,
+//                                 build:37-39) -> dense arrays + the bucket's lookup sub-table
+//
+// Record = {u64 canonical key, u32 read, u32 lC | lT << 16}: the first events of the canonical
+// string and of its twin are (read << 32) | lC and (read << 32) | lT (window.h); a window is its
+// own twin (even-k palindrome, counted twice by build) iff lC == lT.  Local events < 2^16 limit
+// this path to reads of < 32768 windows; longer reads take the general path (count_global.h).
+#pragma once
+#include "window.h"
+
+namespace ec {
+
+constexpr int FINE_BITS = 13;
+constexpr int FINE = 1 << FINE_BITS;       // fine histogram bins = max buckets
+constexpr int HLL_REG_BITS = 11;           // HyperLogLog registers (top 11 hash bits, 2.3% error)
+constexpr int TILE_READS = 256;            // reads staged per tile (one per thread)
+constexpr int STAGE_BYTES = 28672;         // LDS staging per tile
+constexpr int BUCKET_THREADS = 1024;
+constexpr int MAX_COARSE_BITS = 9;         // downsweep writes <= 512 bucket runs per group
+constexpr int REFINE_TILE = 4096;          // records per refine tile (64 KiB of LDS)
+constexpr unsigned int MAX_LOCAL_EVENT = 65535;
+
+struct alignas(16) Rec {
+    unsigned long long key;
+    unsigned int read;
+    unsigned int ev;  // lC | lT << 16
+};
+static_assert(sizeof(Rec) == 16, "record layout");
+
+// solid lookup sub-table slot (bucket region of `slots` slots); id NONE = present, not solid
+struct alignas(16) SubSlot {
+    unsigned long long key;
+    unsigned int id;
+    unsigned int pad;
+};
+
+// LDS byte reader over a staged tile (slow path: reads with 'N')
+struct LdsReader {
+    const uint8_t *lds;
+    uint64_t base;  // buffer offset of lds[0]
+    __device__ inline uint32_t operator()(uint64_t pos) const { return lds[pos - base]; }
+};
+
+// Stage reads [r0, r1) of the tile into LDS (coalesced 16-B loads from the 16-B aligned
+// absolute address below the first byte).  Returns false when the tile does not fit.
+__device__ inline bool stage_tile(const uint8_t *buf, const uint64_t *off, uint64_t r0, uint64_t r1,
+                                  uint8_t *stage, uint64_t &base) {
+    const uint64_t b0 = off[r0], b1 = off[r1];
+    const uint64_t a0 = ((uint64_t)(buf + b0)) & ~15ull;
+    const uint64_t a1 = (((uint64_t)(buf + b1)) + 15) & ~15ull;
+    if (a1 - a0 > (uint64_t)STAGE_BYTES) return false;
+    base = a0 - (uint64_t)buf;
+    const uint4 *src = reinterpret_cast<const uint4 *>(a0);
+    uint4 *dst = reinterpret_cast<uint4 *>(stage);
+    const unsigned n16 = (unsigned)((a1 - a0) >> 4);
+    for (unsigned i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    return true;
+}
+
+// For every read of the group (one read per thread, TILE_READS-read tiles staged in LDS):
+// fn(staged, LdsRead, LdsReader, read, offset, len).  `staged` = false when a tile's bytes
+// exceed the stage (long reads): the callback then reads global memory.
+template <typename Fn>
+__device__ inline void for_group_reads(const uint8_t *buf, const uint64_t *off, uint64_t g0, uint64_t g1,
+                                       uint8_t *stage, Fn &&fn) {
+    for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
+        const uint64_t r1 = min(r0 + TILE_READS, g1);
+        uint64_t base = 0;
+        __syncthreads();  // previous tile fully consumed
+        const bool staged = stage_tile(buf, off, r0, r1, stage, base);
+        __syncthreads();
+        const uint64_t r = r0 + threadIdx.x;
+        if (r < r1) {
+            const uint64_t s = off[r], len = off[r + 1] - s;
+            const uint64_t rel = s - base;
+            LdsRead rv{reinterpret_cast<const uint32_t *>(stage), (uint32_t)(rel >> 2), (uint32_t)(rel & 3)};
+            LdsReader lr{stage, base};
+            fn(staged, rv, lr, r, s, len);
+        }
+    }
+}
+
+__device__ inline uint64_t group_begin(uint64_t g, uint64_t gsize, uint64_t nreads) {
+    return min(g * gsize, nreads);
+}
+
+// ---- upsweep: alphabet + P + HLL + fine histogram per read group -------------------------
+// fine bins are packed 2 x u16 per LDS word; a bin reaching 65535 sets *skew (the host then
+// takes the general path: one k-mer repeated > 65535 times inside one read group)
+__global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
+                                                       int k, uint64_t gsize, unsigned int *hist, uint8_t *hll_blocks,
+                                                       unsigned long long *npos, unsigned long long *bad,
+                                                       unsigned int *maxlocal, unsigned int *skew) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
+    __shared__ unsigned int h_cnt[FINE / 2];
+    __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
+    for (int i = threadIdx.x; i < FINE / 2; i += blockDim.x) h_cnt[i] = 0;
+    for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x) h_reg[i] = 0;
+    const uint64_t g = blockIdx.x;
+    const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
+    unsigned long long mypos = 0;
+    unsigned int mymax = 0, myskew = 0;
+    auto win = [&](uint64_t fwd, uint64_t rc) {
+        const uint64_t c = fwd < rc ? fwd : rc;
+        const uint64_t h = mix64(c);
+        const uint32_t j = (uint32_t)(h >> (64 - HLL_REG_BITS));
+        const uint64_t wv = (h << HLL_REG_BITS) | (1ull << (HLL_REG_BITS - 1));
+        const uint32_t rho = (uint32_t)__clzll((long long)wv) + 1;
+        const uint32_t f = (uint32_t)(h >> (64 - FINE_BITS));
+        const uint32_t sh16 = (f & 1) * 16;
+        const uint32_t old = atomicAdd(&h_cnt[f >> 1], 1u << sh16);
+        myskew |= ((old >> sh16) & 0xFFFFu) >= 0xFFFEu;
+        if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
+    };
+    for_group_reads(buf, off, g0, g1, stage,
+                    [&](bool staged, const LdsRead &rv, const LdsReader &lr, uint64_t r, uint64_t s, uint64_t len) {
+        uint32_t flags = 3;
+        if (staged) flags = read_flags(rv, (uint32_t)len);
+        if (flags == 0) {  // N-free read: one segment
+            if (len >= (uint64_t)k) {
+                const uint32_t m = (uint32_t)(len - k + 1);
+                windows_clean(rv, (uint32_t)len, k, [&](uint64_t fwd, uint64_t rc, uint32_t) { win(fwd, rc); });
+                mypos += m;
+                mymax = max(mymax, 2 * m - 1);
+            }
+            return;
+        }
+        auto slow = [&](auto &rd) {
+            for (uint64_t t = 0; t < len; t++) {
+                if (base_code(rd(s + t)) == 5) {
+                    atomicMin(bad, (unsigned long long)(s + t));
+                    break;
+                }
+            }
+            mypos += for_each_window(rd, s, len, k, r, [&](uint64_t fwd, uint64_t rc, uint64_t ef, uint64_t er) {
+                win(fwd, rc);
+                const uint32_t le = max((uint32_t)ef, (uint32_t)er);
+                mymax = max(mymax, le);
+            });
+        };
+        if (staged) {
+            LdsReader l2 = lr;
+            slow(l2);
+        } else {
+            ByteReader br(buf);
+            slow(br);
+        }
+    });
+    for (int o = 32; o > 0; o >>= 1) {
+        mypos += __shfl_down(mypos, o);
+        mymax = max(mymax, (unsigned int)__shfl_down(mymax, o));
+        myskew |= (unsigned int)__shfl_down(myskew, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (mypos) atomicAdd(npos, mypos);
+        if (mymax) atomicMax(maxlocal, mymax);
+        if (myskew) atomicOr(skew, 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < FINE; i += blockDim.x) hist[g * FINE + i] = (h_cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+    for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x)
+        hll_blocks[g * (1 << HLL_REG_BITS) + i] = (uint8_t)h_reg[i];
+}
+
+// coarse counts, bucket-major: cnt[c * ngroups + g] = the group's fine bins in coarse bucket c
+__global__ void __launch_bounds__(256) k_coarse(const unsigned int *hist, uint64_t ngroups, int cbits,
+                                                unsigned long long *cnt) {
+    const uint64_t C = 1ull << cbits;
+    const int per = 1 << (FINE_BITS - cbits);
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < C * ngroups;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = t / ngroups, g = t % ngroups;
+        const unsigned int *h = hist + g * FINE + c * per;
+        unsigned long long sum = 0;
+        for (int i = 0; i < per; i++) sum += h[i];
+        cnt[t] = sum;
+    }
+}
+
+// records per final bucket (bbits granularity); tot[B] = 0 so its exclusive scan ends at P
+__global__ void __launch_bounds__(256) k_bucket_totals(const unsigned int *hist, uint64_t ngroups, int bbits,
+                                                       unsigned long long *tot) {
+    const uint64_t B = 1ull << bbits;
+    const int per = 1 << (FINE_BITS - bbits);
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b <= B; b += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned long long sum = 0;
+        if (b < B)
+            for (uint64_t g = 0; g < ngroups; g++) {
+                const unsigned int *h = hist + g * FINE + b * per;
+                for (int i = 0; i < per; i++) sum += h[i];
+            }
+        tot[b] = sum;
+    }
+}
+
+// ---- downsweep: scatter records to their (coarse bucket, group) run -----------------------
+__global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
+                                                         int k, uint64_t gsize, uint64_t ngroups, int cbits,
+                                                         const unsigned long long *offs, Rec *recs) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
+    __shared__ unsigned long long cur[1 << MAX_COARSE_BITS];
+    const uint64_t g = blockIdx.x;
+    const int C = 1 << cbits;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) cur[c] = offs[(uint64_t)c * ngroups + g];
+    const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
+    auto emit = [&](uint64_t fwd, uint64_t rc, uint32_t lf, uint32_t lr, uint64_t r) {
+        const uint64_t c = fwd < rc ? fwd : rc;
+        const uint64_t h = mix64(c);
+        const unsigned int cb = cbits ? (unsigned int)(h >> (64 - cbits)) : 0u;
+        uint32_t lC = fwd <= rc ? lf : lr, lT = fwd <= rc ? lr : lf;
+        if (fwd == rc) lT = lC = lf;
+        const unsigned long long p = atomicAdd(&cur[cb], 1ull);
+        Rec rec;
+        rec.key = c;
+        rec.read = (unsigned int)r;
+        rec.ev = lC | (lT << 16);
+        recs[p] = rec;
+    };
+    for_group_reads(buf, off, g0, g1, stage,
+                    [&](bool staged, const LdsRead &rv, const LdsReader &lr, uint64_t r, uint64_t s, uint64_t len) {
+        if (staged && (read_flags(rv, (uint32_t)len) & 1) == 0) {
+            if (len >= (uint64_t)k) {
+                const uint32_t m2 = 2 * (uint32_t)(len - k + 1) - 1;
+                windows_clean(rv, (uint32_t)len, k,
+                              [&](uint64_t fwd, uint64_t rc, uint32_t i) { emit(fwd, rc, i, m2 - i, r); });
+            }
+            return;
+        }
+        auto slow = [&](auto &rd) {
+            for_each_window(rd, s, len, k, r, [&](uint64_t fwd, uint64_t rc, uint64_t ef, uint64_t er) {
+                emit(fwd, rc, (uint32_t)ef, (uint32_t)er, r);
+            });
+        };
+        if (staged) {
+            LdsReader l2 = lr;
+            slow(l2);
+        } else {
+            ByteReader br(buf);
+            slow(br);
+        }
+    });
+}
+
+// ---- refine: split each coarse bucket into its 2^(bbits-cbits) final buckets ----------------
+// one workgroup per coarse bucket; tiles of REFINE_TILE records are sorted by final bucket in
+// LDS and written out as contiguous runs (the final-bucket cursors live in LDS).
+__global__ void __launch_bounds__(BUCKET_THREADS) k_refine(const Rec *in, Rec *out, const unsigned long long *bstart,
+                                                          int cbits, int bbits) {
+    __shared__ Rec tile[REFINE_TILE];
+    __shared__ unsigned long long cur[64];
+    __shared__ unsigned int tcnt[64], tbeg[64];
+    const int F = 1 << (bbits - cbits);
+    const uint64_t c = blockIdx.x;
+    for (int j = threadIdx.x; j < F; j += blockDim.x) cur[j] = bstart[c * F + j];
+    const uint64_t r0 = bstart[c * F], r1 = bstart[(c + 1) * F];
+    constexpr int PER = REFINE_TILE / BUCKET_THREADS;
+    for (uint64_t t0 = r0; t0 < r1; t0 += REFINE_TILE) {
+        const unsigned int n = (unsigned int)min((uint64_t)REFINE_TILE, r1 - t0);
+        if (threadIdx.x < 64) tcnt[threadIdx.x] = 0;
+        __syncthreads();
+        Rec rr[PER];
+        unsigned int jj[PER], rk[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                rr[q] = in[t0 + i];
+                jj[q] = (unsigned int)(mix64(rr[q].key) >> (64 - bbits)) & (F - 1);
+                rk[q] = atomicAdd(&tcnt[jj[q]], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned int acc = 0;
+            for (int j = 0; j < F; j++) {
+                tbeg[j] = acc;
+                acc += tcnt[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) tile[tbeg[jj[q]] + rk[q]] = rr[q];
+        }
+        __syncthreads();
+        for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
+            const Rec rec = tile[i];
+            const unsigned int j = (unsigned int)(mix64(rec.key) >> (64 - bbits)) & (F - 1);
+            out[cur[j] + (i - tbeg[j])] = rec;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < F) cur[threadIdx.x] += tcnt[threadIdx.x];
+        __syncthreads();
+    }
+}
+
+// ---- bucket counting in LDS -------------------------------------------------------------
+struct alignas(8) LSlot {
+    unsigned long long key;
+    unsigned long long fC;
+    unsigned long long fT;
+    unsigned int count;
+    unsigned int pad;
+};
+
+template <int SLOTS>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(const Rec *recs, const unsigned long long *bstart,
+                                                          long long limit,
+                                                          unsigned long long *dkey, unsigned int *dcnt,
+                                                          unsigned long long *dfc, unsigned long long *dft,
+                                                          SubSlot *sub, unsigned int *nsolid,
+                                                          unsigned long long *ndistinct, unsigned int *overflow) {
+    __shared__ LSlot tab[SLOTS];
+    __shared__ unsigned int s_over;
+    __shared__ unsigned int s_wave[BUCKET_THREADS / 64];
+    __shared__ unsigned int s_base;
+    const unsigned int b = blockIdx.x;
+    for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
+        tab[i].key = EMPTY_KEY;
+        tab[i].fC = NONE64;
+        tab[i].fT = NONE64;
+        tab[i].count = 0;
+    }
+    if (threadIdx.x == 0) s_over = 0;
+    __syncthreads();
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+        const Rec rec = recs[i];
+        const uint64_t c = rec.key;
+        const unsigned int lC = rec.ev & 0xFFFFu, lT = rec.ev >> 16;
+        const unsigned long long eC = ((unsigned long long)rec.read << 32) | lC;
+        const unsigned long long eT = ((unsigned long long)rec.read << 32) | lT;
+        unsigned int slot = (unsigned int)mix64(c) & (SLOTS - 1);
+        int probe = 0;
+        for (; probe < SLOTS; probe++) {
+            unsigned long long cur = tab[slot].key;
+            if (cur == EMPTY_KEY) {
+                cur = atomicCAS(&tab[slot].key, EMPTY_KEY, (unsigned long long)c);
+                if (cur == EMPTY_KEY) cur = c;
+            }
+            if (cur == c) break;
+            slot = (slot + 1) & (SLOTS - 1);
+        }
+        if (probe == SLOTS) {
+            s_over = 1;
+            continue;
+        }
+        atomicAdd(&tab[slot].count, lC == lT ? 2u : 1u);
+        if (eC < tab[slot].fC) atomicMin(&tab[slot].fC, eC);
+        if (eT < tab[slot].fT) atomicMin(&tab[slot].fT, eT);
+    }
+    __syncthreads();
+    if (s_over) {
+        if (threadIdx.x == 0) atomicAdd(overflow, 1u);
+        return;
+    }
+    // solid filter + compaction (wave ballot, one global atomic per block)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int PER = SLOTS / BUCKET_THREADS;
+    bool solid[PER];
+    unsigned int mine = 0, present = 0;
+    for (int q = 0; q < PER; q++) {
+        const LSlot &sl = tab[threadIdx.x * PER + q];
+        present += sl.key != EMPTY_KEY;
+        solid[q] = sl.key != EMPTY_KEY && (long long)sl.count > limit;
+        mine += solid[q];
+    }
+    // wave exclusive scan of `mine`
+    unsigned int incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wave[wid] = incl;
+    unsigned int pres = present;
+    for (int o = 32; o > 0; o >>= 1) pres += __shfl_down(pres, o);
+    if (lane == 0 && pres) atomicAdd(ndistinct, (unsigned long long)pres);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int tot = 0;
+        for (int w = 0; w < BUCKET_THREADS / 64; w++) {
+            const unsigned int c = s_wave[w];
+            s_wave[w] = tot;
+            tot += c;
+        }
+        s_base = tot ? atomicAdd(nsolid, tot) : 0;
+    }
+    __syncthreads();
+    unsigned int u = s_base + s_wave[wid] + incl - mine;
+    SubSlot *region = sub + (uint64_t)b * SLOTS;
+    for (int q = 0; q < PER; q++) {
+        const int i = threadIdx.x * PER + q;
+        const LSlot &sl = tab[i];
+        SubSlot o;
+        o.key = sl.key;
+        o.id = NONE32;
+        o.pad = 0;
+        if (solid[q]) {
+            dkey[u] = sl.key;
+            dcnt[u] = sl.count;
+            dfc[u] = sl.fC;
+            dft[u] = sl.fT;
+            o.id = u;
+            u++;
+        }
+        region[i] = o;
+    }
+}
+
+}  // namespace ec

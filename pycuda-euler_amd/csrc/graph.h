@@ -1,0 +1,473 @@
+// graph.h -- de Bruijn links, list ranking, contig starts/order, emission, GFA links.
+#pragma once
+#include "count_global.h"
+#include "count_part.h"
+
+namespace ec {
+
+// canonical key -> dense solid id (NONE if absent or not solid).  Two layouts: the bucketed
+// sub-tables written by k_bucket (partitioned path) or the single HBM table (general path).
+struct SolidIndex {
+    const Slot *table;
+    uint64_t capmask;
+    const SubSlot *sub;
+    int bbits;
+    unsigned int slots;  // sub-table slots per bucket (power of 2)
+    __device__ inline unsigned int find(uint64_t c) const {
+        const uint64_t h = mix64(c);
+        if (sub) {
+            const uint64_t b = bbits ? (h >> (64 - bbits)) : 0;
+            const SubSlot *r = sub + b * slots;
+            unsigned int slot = (unsigned int)h & (slots - 1);
+            for (unsigned int probe = 0; probe < slots; probe++) {
+                const unsigned long long kk = r[slot].key;
+                if (kk == c) return r[slot].id;
+                if (kk == EMPTY_KEY) return NONE32;
+                slot = (slot + 1) & (slots - 1);
+            }
+            return NONE32;
+        }
+        return lookup(table, capmask, c);
+    }
+};
+// oriented node id: 2u + o (o = 1: twin of the canonical string); palindromes use o = 0 only
+__device__ inline uint64_t node_code(const unsigned long long *dkey, unsigned int x, int k) {
+    const uint64_t c = dkey[x >> 1];
+    return (x & 1) ? twin64(c, k) : c;
+}
+__device__ inline unsigned int twin_node(const uint8_t *upal, unsigned int x) {
+    return upal[x >> 1] ? x : (x ^ 1u);
+}
+
+// links phase 1: out-degree (number of fw(x) in d, get_contig_forward:63) + the unique candidate
+__global__ void __launch_bounds__(256) k_neighbors(SolidIndex idx, const unsigned long long *dkey,
+                                                   unsigned int U, int k, uint8_t *upal, uint8_t *outdeg,
+                                                   unsigned int *cand, unsigned int *npal) {
+    const uint64_t mask = kmask64(k);
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < 2ull * U; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        const uint64_t c = dkey[x >> 1];
+        const uint64_t tc = twin64(c, k);
+        const bool pal = tc == c;
+        if (x & 1) {
+            if (pal) {  // the palindrome has a single dict entry: node 2u+1 does not exist
+                outdeg[x] = 0;
+                cand[x] = NONE32;
+                continue;
+            }
+        } else {
+            upal[x >> 1] = pal ? 1 : 0;
+            if (pal) atomicAdd(npal, 1u);
+        }
+        const uint64_t xs = (x & 1) ? tc : c;
+        unsigned int n = 0, cd = NONE32;
+        for (int b = 0; b < 4; b++) {
+            const uint64_t y = ((xs << 2) | (uint64_t)b) & mask;
+            const uint64_t ty = twin64(y, k);
+            const uint64_t cy = y < ty ? y : ty;
+            const unsigned int u = idx.find(cy);
+            if (u != NONE32) {
+                if (n == 0) cd = 2 * u + (y != cy ? 1u : 0u);
+                n++;
+            }
+        }
+        outdeg[x] = (uint8_t)n;
+        cand[x] = n == 1 ? cd : NONE32;
+    }
+}
+
+// links phase 2: x -> y iff |fw(x) in d| == 1, |bw(y) in d| == 1 and y != twin(x)
+// (get_contig_forward:63-73; the cand == km / twin(km) stop is applied by the walk emulation)
+// |bw(y) in d| == |fw(twin y) in d| == outdeg[twin y].
+__global__ void __launch_bounds__(256) k_succ(const uint8_t *upal, const uint8_t *outdeg, const unsigned int *cand,
+                                              unsigned int N, unsigned int *succ) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        unsigned int s = NONE32;
+        const unsigned int y = cand[x];
+        if (y != NONE32 && !((x & 1) && upal[x >> 1])) {
+            const unsigned int ty = twin_node(upal, y);
+            if (outdeg[ty] == 1 && y != twin_node(upal, x)) s = y;
+        }
+        succ[x] = s;
+    }
+}
+
+__device__ inline unsigned long long first_event(const unsigned long long *dfc, const unsigned long long *dft,
+                                                 unsigned int x) {
+    return (x & 1) ? dft[x >> 1] : dfc[x >> 1];
+}
+
+// pred(x) = twin(succ(twin(x))): the links are closed under twin-reversal
+__global__ void __launch_bounds__(256) k_pred(const uint8_t *upal, const unsigned int *succ, unsigned int N,
+                                              unsigned int *pred) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        unsigned int p = NONE32;
+        if (!((x & 1) && upal[x >> 1])) {
+            const unsigned int sx = succ[twin_node(upal, x)];
+            if (sx != NONE32) p = twin_node(upal, sx);
+        }
+        pred[x] = p;
+    }
+}
+
+// ---- list ranking by a sparse ruling set ------------------------------------------------
+// Rulers: every path head plus every node whose hash hits the sampling mask.  Each ruler
+// walks its segment (up to the next ruler) serially, stamping (ruler, offset) on every node;
+// the much shorter ruler list is then ranked by weighted Wyllie pointer jumping.  Cycles
+// that drew no ruler are caught by later iterations with a denser sampling mask (the last
+// one makes every still-unvisited node a ruler).
+__device__ inline bool ruler_hash(unsigned int x, unsigned int smask) {
+    return (mix64(0x9E3779B97F4A7C15ull ^ x) & smask) == 0;
+}
+
+__global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsigned int *pred, unsigned int N,
+                                                unsigned int smask, int first, unsigned int *rid, unsigned int *roff,
+                                                unsigned int *rlist, unsigned int *nr) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        if ((x & 1) && upal[x >> 1]) continue;
+        if (rid[x] != NONE32) continue;
+        if ((first && pred[x] == NONE32) || ruler_hash(x, smask)) {
+            const unsigned int i = atomicAdd(nr, 1u);
+            rlist[i] = x;
+            rid[x] = i;
+            roff[x] = 0;
+        }
+    }
+}
+
+// ruler jump state (32 B): window = rulers i, P(i), .., P^{c-1}(i)
+struct alignas(32) RJump {
+    unsigned int a;    // P^c(i) or NONE
+    unsigned int s;    // nodes in the segments of P(i)..P^{c-1}(i)  (= rank of i's node on a path)
+    unsigned int h;    // last ruler of the window (the head ruler once a == NONE)
+    unsigned int cm;   // min ruler node id in the window
+    unsigned int cd;   // nodes from cm forward to i's node
+    unsigned int len;  // nodes in i's own segment
+    unsigned long long fm;  // min first event over the window's segments (incl. i's)
+};
+static_assert(sizeof(RJump) == 32, "rjump layout");
+
+__global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const unsigned long long *dfc,
+                                              const unsigned long long *dft, const unsigned int *rlist,
+                                              unsigned int r0, const unsigned int *nr, unsigned int smask,
+                                              unsigned int *rid, unsigned int *roff, unsigned int *nextR, RJump *rs,
+                                              unsigned long long *nvisited) {
+    const unsigned int r1 = *nr;
+    unsigned long long seen = 0;
+    for (uint64_t t = r0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < r1; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int i = (unsigned int)t;
+        unsigned int v = rlist[i];
+        unsigned long long fm = first_event(dfc, dft, v);
+        unsigned int j = 0, nx = NONE32;
+        for (;;) {
+            const unsigned int w = succ[v];
+            if (w == NONE32) break;
+            if (ruler_hash(w, smask) && rid[w] != NONE32) {  // the next ruler
+                nx = rid[w];
+                break;
+            }
+            v = w;
+            j++;
+            rid[v] = i;
+            roff[v] = j;
+            const unsigned long long f = first_event(dfc, dft, v);
+            fm = f < fm ? f : fm;
+        }
+        nextR[i] = nx;
+        RJump r;
+        r.a = NONE32;  // set from prevR by k_rjump_init
+        r.s = 0;
+        r.h = i;
+        r.cm = rlist[i];
+        r.cd = 0;
+        r.len = j + 1;
+        r.fm = fm;
+        rs[i] = r;
+        seen += j + 1;
+    }
+    for (int o = 32; o > 0; o >>= 1) seen += __shfl_down(seen, o);
+    if ((threadIdx.x & 63) == 0 && seen) atomicAdd(nvisited, seen);
+}
+
+__global__ void __launch_bounds__(256) k_rjump_init(const unsigned int *nextR, unsigned int nr, RJump *rs) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int n = nextR[t];
+        if (n != NONE32) rs[n].a = (unsigned int)t;  // prevR[next] = me (unique predecessor)
+    }
+}
+
+// one weighted Wyllie round on the ruler list
+__global__ void __launch_bounds__(256) k_rjump(const RJump *src, RJump *dst, unsigned int nr, unsigned int N,
+                                               const unsigned int *active_in, unsigned int *active_out,
+                                               unsigned int *final_sel, unsigned int sel) {
+    if (active_in && *active_in == 0) return;
+    unsigned int act = 0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
+        RJump j = src[t];
+        if (j.a != NONE32 && j.s < N) {
+            const RJump y = src[j.a];
+            const unsigned int back = j.s + y.len;  // nodes from ruler a's node forward to i's node
+            if (y.cm < j.cm) {
+                j.cm = y.cm;
+                j.cd = back + y.cd;
+            }
+            j.s = back + y.s;
+            j.a = y.a;
+            j.h = y.h;
+            j.fm = y.fm < j.fm ? y.fm : j.fm;
+            act += (j.a != NONE32 && j.s < N);
+        }
+        dst[t] = j;
+    }
+    for (int o = 32; o > 0; o >>= 1) act += __shfl_down(act, o);
+    if ((threadIdx.x & 63) == 0 && act) atomicAdd(active_out, act);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *final_sel = sel;
+}
+
+// per-node path descriptor: PK = path key (head node for paths, min ruler node for cycles)
+// with bit 31 = on a cycle; RK = rank (from the head / from the cycle key).  Path records
+// at the key node: PL = path / cycle length, PM = min first event over it.
+constexpr unsigned int CYC = 0x80000000u;
+
+__global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const unsigned int *succ, const unsigned int *rid,
+                                                  const unsigned int *roff, const unsigned int *rlist, const RJump *rs,
+                                                  unsigned int N, unsigned int *PK, unsigned int *RK, unsigned int *PL,
+                                                  unsigned long long *PM) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        if ((x & 1) && upal[x >> 1]) continue;
+        const unsigned int i = rid[x], j = roff[x];
+        const RJump r = rs[i];
+        if (r.a == NONE32) {  // path
+            const unsigned int pk = rlist[r.h], rk = r.s + j;
+            PK[x] = pk;
+            RK[x] = rk;
+            if (succ[x] == NONE32) {  // tail: its ruler's window spans the whole path
+                PL[pk] = rk + 1;
+                PM[pk] = r.fm;
+            }
+        } else {  // cycle
+            PK[x] = r.cm | CYC;
+            RK[x] = r.cd + j;
+        }
+    }
+}
+
+// cycle length / min: the ruler whose successor ruler is the key ruler closes the ring
+__global__ void __launch_bounds__(256) k_cycle_len(const unsigned int *nextR, const unsigned int *rlist, const RJump *rs,
+                                                   unsigned int nr, unsigned int *PL, unsigned long long *PM) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
+        const RJump r = rs[t];
+        if (r.a == NONE32) continue;
+        const unsigned int n = nextR[t];
+        if (n != NONE32 && rlist[n] == r.cm) {
+            PL[r.cm] = r.cd + r.len;
+            PM[r.cm] = r.fm;
+        }
+    }
+}
+
+__device__ inline unsigned long long path_min(const unsigned int *PK, const unsigned long long *PM, unsigned int x) {
+    return PM[PK[x] & ~CYC];
+}
+
+// start of each component (all_contigs:82-84): the oriented k-mer with the smallest first
+// event over the path and its twin path (= the first dict entry not yet `done`).
+__global__ void __launch_bounds__(256) k_starts(const uint8_t *upal, const unsigned long long *dfc,
+                                                const unsigned long long *dft, const unsigned int *PK,
+                                                const unsigned long long *PM, unsigned int N,
+                                                unsigned long long *skeys, unsigned int *svals, unsigned int *nstarts) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        if ((x & 1) && upal[x >> 1]) continue;
+        const unsigned long long f = first_event(dfc, dft, x);
+        const unsigned long long a = path_min(PK, PM, x);
+        const unsigned long long b = path_min(PK, PM, twin_node(upal, x));
+        if (f == (a < b ? a : b)) {
+            const unsigned int i = atomicAdd(nstarts, 1u);
+            skeys[i] = f;
+            svals[i] = x;
+        }
+    }
+}
+
+// geometry of the walk from start s (get_contig:47-56 + get_contig_forward:59-77):
+//   kind 0 path, twin path disjoint   : contig = the path holding s, head..tail
+//   kind 1 path equal to its twin     : p_0..p_n, s = p_j : p_0..p_{n-j-1} | p_{n-j+1}..p_n | all
+//   kind 2 cycle, twin cycle disjoint : s, succ(s), ... (n nodes)
+//   kind 3 cycle equal to its twin    : m = dist(s -> twin s): m == 0 -> all n from s,
+//                                       else p_{m+1}..p_{n-1}, p_0..p_{m-1} (n-1 nodes)
+struct Walk {
+    unsigned int kind, n, j, m, lo, len;
+};
+
+__device__ inline Walk walk_of(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+                               const unsigned int *PL, unsigned int s) {
+    Walk w;
+    const unsigned int pk = PK[s], rk = RK[s];
+    const unsigned int ts = twin_node(upal, s);
+    const unsigned int pk2 = PK[ts], rk2 = RK[ts];
+    const bool self = pk2 == pk;
+    const unsigned int plen = PL[pk & ~CYC];
+    w.j = rk;
+    w.m = 0;
+    w.lo = 0;
+    if (!(pk & CYC)) {
+        if (!self) {
+            w.kind = 0;
+            w.n = plen;
+            w.len = plen;
+        } else {
+            w.kind = 1;
+            const unsigned int n = plen - 1, j = rk;
+            w.n = n;
+            if (2 * j < n) {
+                w.lo = 0;
+                w.len = n - j;
+            } else if (2 * j > n) {
+                w.lo = n - j + 1;
+                w.len = j;
+            } else {
+                w.lo = 0;
+                w.len = n + 1;
+            }
+        }
+    } else {
+        const unsigned int n = plen;
+        w.n = n;
+        if (!self) {
+            w.kind = 2;
+            w.len = n;
+        } else {
+            w.kind = 3;
+            w.m = (rk2 + n - rk) % n;
+            w.len = w.m == 0 ? n : n - 1;
+        }
+    }
+    return w;
+}
+
+__global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+                                                    const unsigned int *PL, const unsigned int *sorted_nodes,
+                                                    unsigned int nc, int k, unsigned int *cidxOf,
+                                                    unsigned long long *clen) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int s = sorted_nodes[i];
+        cidxOf[PK[s] & ~CYC] = (unsigned int)i;
+        const Walk w = walk_of(upal, PK, RK, PL, s);
+        clen[i] = (unsigned long long)(k - 1) + w.len;
+    }
+}
+
+// emit: every node finds its contig through its path key, computes its walk position and
+// writes its chars (contig_to_string:44-45: first node k chars, later nodes their last base).
+__global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+                                              const unsigned int *PL, const unsigned long long *dkey,
+                                              const unsigned int *cidxOf, const unsigned int *sorted_nodes,
+                                              const unsigned long long *coff, unsigned int N, int k, char *chars,
+                                              unsigned int *cfirst, unsigned int *clast, unsigned int *headOf,
+                                              unsigned int *tailOf) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        if ((x & 1) && upal[x >> 1]) continue;
+        const unsigned int pk = PK[x], rk = RK[x];
+        const unsigned int ci = cidxOf[pk & ~CYC];
+        if (ci == NONE32) continue;  // the twin path of a disjoint pair carries the contig
+        const unsigned int s = sorted_nodes[ci];
+        const Walk w = walk_of(upal, PK, RK, PL, s);
+        long long pos = -1;
+        if (w.kind == 0) {
+            pos = rk;
+        } else if (w.kind == 1) {
+            if (rk >= w.lo && rk < w.lo + w.len) pos = rk - w.lo;
+        } else {
+            const unsigned int i = (rk + w.n - w.j) % w.n;  // steps from s
+            if (w.kind == 2 || w.m == 0) {
+                pos = i;
+            } else if (i > w.m) {
+                pos = i - w.m - 1;
+            } else if (i < w.m) {
+                pos = w.n - 1 - w.m + i;
+            }
+        }
+        if (pos < 0) continue;
+        const uint64_t code = node_code(dkey, x, k);
+        char *dst = chars + coff[ci];
+        if (pos == 0) {
+            uint64_t c = code;
+            for (int i = k - 1; i >= 0; i--) {
+                dst[i] = "ACGT"[c & 3];
+                c >>= 2;
+            }
+            cfirst[ci] = x;
+            headOf[x] = ci;
+        } else {
+            dst[k - 1 + pos] = "ACGT"[code & 3];
+        }
+        if ((unsigned long long)pos == (unsigned long long)w.len - 1) {
+            clast[ci] = x;
+            tailOf[twin_node(upal, x)] = ci;
+        }
+    }
+}
+
+// GFA links (all_contigs:90-109): for y in fw(last kmer): heads[y] then tails[y];
+// for z in fw(twin(first kmer)): heads[z] then tails[z].  Up to 8 per side.
+__global__ void __launch_bounds__(256) k_gfa(SolidIndex idx, const unsigned long long *dkey,
+                                             const uint8_t *upal, const unsigned int *cfirst, const unsigned int *clast,
+                                             const unsigned int *headOf, const unsigned int *tailOf, unsigned int nc,
+                                             int k, long long *lk, unsigned int *lcnt) {
+    const uint64_t mask = kmask64(k);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
+        for (int side = 0; side < 2; side++) {
+            const unsigned int src = side == 0 ? clast[i] : twin_node(upal, cfirst[i]);
+            const uint64_t xs = node_code(dkey, src, k);
+            unsigned int n = 0;
+            long long *o = lk + (i * 2 + side) * 8;
+            for (int b = 0; b < 4; b++) {
+                const uint64_t y = ((xs << 2) | (uint64_t)b) & mask;
+                const uint64_t ty = twin64(y, k);
+                const uint64_t cy = y < ty ? y : ty;
+                const unsigned int u = idx.find(cy);
+                if (u == NONE32) continue;
+                const unsigned int oy = (y != cy) ? 2 * u + 1 : 2 * u;
+                const unsigned int hh = headOf[oy], tt = tailOf[oy];
+                if (hh != NONE32) o[n++] = 2ll * hh;
+                if (tt != NONE32) o[n++] = 2ll * tt + 1;
+            }
+            lcnt[i * 2 + side] = n;
+        }
+    }
+}
+
+// ordered dict of build(): every valid oriented node with its first event (sort key)
+__global__ void __launch_bounds__(256) k_dict_items(const uint8_t *upal, const unsigned long long *dfc,
+                                                    const unsigned long long *dft, unsigned int N,
+                                                    unsigned long long *keys, unsigned int *vals, unsigned int *n) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        if ((x & 1) && upal[x >> 1]) continue;
+        const unsigned int i = atomicAdd(n, 1u);
+        keys[i] = first_event(dfc, dft, x);
+        vals[i] = x;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_dict_render(const unsigned int *nodes, unsigned int n,
+                                                     const unsigned long long *dkey, const unsigned int *dcnt, int k,
+                                                     char *out, unsigned int *counts) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = nodes[i];
+        uint64_t c = node_code(dkey, x, k);
+        for (int p = k - 1; p >= 0; p--) {
+            out[i * k + p] = "ACGT"[c & 3];
+            c >>= 2;
+        }
+        counts[i] = dcnt[x >> 1];
+    }
+}
+
+}  // namespace ec

@@ -30,7 +30,12 @@ EC_ERR_STATE = -6
 
 EC_FLAG_WANT_DICT = 1
 EC_FLAG_TIMING = 2
+EC_FLAG_GENERAL = 4
 EC_NSTAGES = 8
+EC_NKERNELS = 5
+KERNEL_NAMES = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
+EC_PATH_PARTITIONED = 0
+EC_PATH_GENERAL = 1
 EC_MAX_K = 32
 
 
@@ -56,16 +61,19 @@ class Stats(ctypes.Structure):
         ("n_contig_chars", ctypes.c_uint64),
         ("n_links", ctypes.c_uint64),
         ("table_capacity", ctypes.c_uint64),
+        ("n_rulers", ctypes.c_uint64),
         ("table_retries", ctypes.c_uint32),
         ("rank_rounds", ctypes.c_uint32),
-        ("n_rulers", ctypes.c_uint64),
+        ("count_path", ctypes.c_uint32),
+        ("n_buckets", ctypes.c_uint32),
         ("stage_ms", ctypes.c_float * EC_NSTAGES),
-        ("count_kernel_ms", ctypes.c_float),
+        ("kernel_ms", ctypes.c_float * EC_NKERNELS),
     ]
 
     def as_dict(self):
-        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "stage_ms"}
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("stage_ms", "kernel_ms")}
         d["stage_ms"] = list(self.stage_ms)
+        d["kernel_ms"] = list(self.kernel_ms)
         return d
 
 
@@ -258,9 +266,10 @@ class Session:
             items = [(s[i * k:(i + 1) * k], int(cnt[i])) for i in range(nd)]
         return Result(k, st, chars.raw[:nch], coff, loff, links[:nl], items)
 
-    def assemble(self, reads, k, limit=1, want_dict=False, timing=False):
+    def assemble(self, reads, k, limit=1, want_dict=False, timing=False, general=False):
         buf, off = pack_reads(reads)
         flags = (EC_FLAG_WANT_DICT if want_dict else 0) | (EC_FLAG_TIMING if timing else 0)
+        flags |= EC_FLAG_GENERAL if general else 0
         self.run_host(buf, off, k, limit, flags)
         return self.fetch(k, want_dict)
 

@@ -26,6 +26,16 @@ def test_golden(gpu_session, case):
     assert [[x, c] for x, c in res.dict_items] == case["d"]
     assert res.contigs == case["contigs"]
     assert res.links == case["links"]
+    if res.stats.n_positions > 0:
+        assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
+
+
+@pytest.mark.parametrize("case", CASES32[::2], ids=[c["name"] for c in CASES32[::2]])
+def test_golden_general_path(gpu_session, case):
+    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, general=True)
+    assert [[x, c] for x, c in res.dict_items] == case["d"]
+    assert res.contigs == case["contigs"]
+    assert res.links == case["links"]
 
 
 def test_extended_alphabet_rejected(gpu_session):
@@ -58,12 +68,14 @@ SYN = [
 ]
 
 
+@pytest.mark.parametrize("general", [False, True], ids=["partitioned", "general"])
 @pytest.mark.parametrize("g,n,L,seed,err,nr,circ,k", SYN)
-def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k):
+def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, general):
     buf, off = make_reads(g, n, L, 1000 + seed, err=err, n_rate=nr, circular=circ)
     want_dict = g <= 50_000
     ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
-    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT if want_dict else 0)
+    flags = (eulerhip.EC_FLAG_WANT_DICT if want_dict else 0) | (eulerhip.EC_FLAG_GENERAL if general else 0)
+    gpu_session.run_host(buf, off, k, 1, flags)
     res = gpu_session.fetch(k, want_dict)
     assert res.stats.n_positions == ref["n_positions"]
     assert res.stats.n_dict == ref["n_dict"]
@@ -112,3 +124,23 @@ def test_empty_and_ragged(gpu_session):
             res = gpu_session.assemble(reads, k, 1, want_dict=True)
             d, r, g = oracle.assemble(reads, k, 1)
             assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g
+
+
+def test_long_reads_take_general_path(gpu_session):
+    # > 32767 windows in one read: local events exceed 16 bits -> general counting path
+    buf, off = make_reads(60_000, 4, 40_000, 31, err=0.0, circular=True)
+    ref, rc, rl = _oracle_packed(buf, off, 21)
+    gpu_session.run_host(buf, off, 21, 1)
+    res = gpu_session.fetch(21)
+    assert res.stats.count_path == eulerhip.EC_PATH_GENERAL
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+def test_many_buckets_vs_oracle(gpu_session):
+    # enough distinct k-mers for B > 1 buckets with errors (singletons fill the LDS tables)
+    buf, off = make_reads(300_000, 200_000, 100, 32, err=0.004)
+    ref, rc, rl = _oracle_packed(buf, off, 31)
+    gpu_session.run_host(buf, off, 31, 1)
+    res = gpu_session.fetch(31)
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.n_buckets > 64
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
