@@ -70,7 +70,7 @@ struct ec_session {
     DevBuf h_reads, h_offsets;  // H2D staging for ec_assemble_host
     DevBuf hll, scal, table, dkey, dcnt, dfc, dft, upal, outdeg, cand, succ, pred, st0, st1;
     DevBuf rid, roff, rlist, nextR, PK, RK, PL, PM;
-    DevBuf hist, cnt, offs, bstart, tot, recs, recs2, sub;
+    DevBuf hist, thist, cnt, offs, bstart, tot, recs, recs2, sub;
     DevBuf startOf, skeys, svals, skeys2, svals2, cidxOf, clen, coff, chars, cfirst, clast, headOf, tailOf;
     DevBuf lk, lcnt, tmp, dchars, dcounts;
     // results (host)
@@ -179,11 +179,12 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     ngroups = std::max<uint64_t>(1, (nreads + gsize - 1) / gsize);
     EC_CHECK(s->hist.ensure(ngroups * FINE * 4));
     EC_CHECK(s->hll.ensure(ngroups * (1 << HLL_REG_BITS)));
+    EC_CHECK(s->thist.ensure(std::max<uint64_t>(ntiles, 1) * (1 << MAX_COARSE_BITS) * 4));
     if (nreads) {
         kmark(s, 0, 0);
         k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
                                                            s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad,
-                                                           &dsc->maxlocal, &dsc->skew);
+                                                           &dsc->maxlocal, &dsc->skew, s->thist.as<unsigned int>());
         kmark(s, 0, 1);
         k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<uint8_t>(), (int)ngroups, HLL_REG_BITS, &dsc->est);
     }
@@ -214,23 +215,24 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
         slots = est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
         int maxc = MAX_COARSE_BITS;
         if (const char *e = getenv("EULERHIP_COARSE_BITS")) maxc = std::max(1, std::min(MAX_COARSE_BITS, atoi(e)));
+        maxc = std::min(maxc, DS_MAX_CBITS);
         const int cbits = std::min(bbits, std::max(maxc, bbits - 6));  // refine splits <= 64 ways
         const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
         mark(s, 2 * EC_STAGE_COUNT);
-        EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
-        EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
+        EC_CHECK(s->cnt.ensure(Ck * ntiles * 8));
+        EC_CHECK(s->offs.ensure(Ck * ntiles * 8));
         EC_CHECK(s->tot.ensure((Bk + 1) * 8));
         EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
         EC_CHECK(s->recs.ensure(P * sizeof(Rec)));
         if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * sizeof(Rec)));
-        k_coarse<<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
-                                                               s->cnt.as<unsigned long long>());
-        EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ngroups));
+        k_coarse<<<grid_for(Ck * ntiles, B, 8192), B, 0, st>>>(s->thist.as<unsigned int>(), ntiles, cbits,
+                                                              s->cnt.as<unsigned long long>());
+        EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ntiles));
         k_bucket_totals<<<grid_for(Bk + 1, B), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, bbits,
                                                           s->tot.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
         kmark(s, 1, 0);
-        k_downsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups, cbits,
+        k_downsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ntiles, cbits,
                                                              s->offs.as<unsigned long long>(), s->recs.as<Rec>());
         kmark(s, 1, 1);
         Rec *final_recs = s->recs.as<Rec>();
@@ -571,7 +573,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
-                     &s->hist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub};
+                     &s->hist, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub};
     for (auto *b : all) b->release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);

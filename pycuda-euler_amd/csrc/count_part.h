@@ -73,13 +73,18 @@ __device__ inline bool stage_tile(const uint8_t *buf, const uint64_t *off, uint6
 // For every read of the group (one read per thread, TILE_READS-read tiles staged in LDS):
 // fn(staged, LdsRead, LdsReader, read, offset, len).  `staged` = false when a tile's bytes
 // exceed the stage (long reads): the callback then reads global memory.
-template <typename Fn>
+struct NoHook {
+    __device__ inline void operator()(uint64_t) const {}
+};
+
+template <typename Fn, typename Pre = NoHook, typename Post = NoHook>
 __device__ inline void for_group_reads(const uint8_t *buf, const uint64_t *off, uint64_t g0, uint64_t g1,
-                                       uint8_t *stage, Fn &&fn) {
+                                       uint8_t *stage, Fn &&fn, Pre pre = Pre(), Post post = Post()) {
     for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
         const uint64_t r1 = min(r0 + TILE_READS, g1);
         uint64_t base = 0;
         __syncthreads();  // previous tile fully consumed
+        pre(r0 / TILE_READS);
         const bool staged = stage_tile(buf, off, r0, r1, stage, base);
         __syncthreads();
         const uint64_t r = r0 + threadIdx.x;
@@ -90,6 +95,8 @@ __device__ inline void for_group_reads(const uint8_t *buf, const uint64_t *off, 
             LdsReader lr{stage, base};
             fn(staged, rv, lr, r, s, len);
         }
+        __syncthreads();
+        post(r0 / TILE_READS);
     }
 }
 
@@ -103,9 +110,11 @@ __device__ inline uint64_t group_begin(uint64_t g, uint64_t gsize, uint64_t nrea
 __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                        int k, uint64_t gsize, unsigned int *hist, uint8_t *hll_blocks,
                                                        unsigned long long *npos, unsigned long long *bad,
-                                                       unsigned int *maxlocal, unsigned int *skew) {
+                                                       unsigned int *maxlocal, unsigned int *skew,
+                                                       unsigned int *thist) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
     __shared__ unsigned int h_cnt[FINE / 2];
+    __shared__ unsigned int t_cnt[1 << MAX_COARSE_BITS];  // this tile's coarse histogram
     __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
     for (int i = threadIdx.x; i < FINE / 2; i += blockDim.x) h_cnt[i] = 0;
     for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x) h_reg[i] = 0;
@@ -122,6 +131,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
         const uint32_t f = (uint32_t)(h >> (64 - FINE_BITS));
         const uint32_t sh16 = (f & 1) * 16;
         const uint32_t old = atomicAdd(&h_cnt[f >> 1], 1u << sh16);
+        atomicAdd(&t_cnt[f >> (FINE_BITS - MAX_COARSE_BITS)], 1u);
         myskew |= ((old >> sh16) & 0xFFFFu) >= 0xFFFEu;
         if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
     };
@@ -158,6 +168,11 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
             ByteReader br(buf);
             slow(br);
         }
+    }, [&](uint64_t) {
+        for (int i = threadIdx.x; i < (1 << MAX_COARSE_BITS); i += blockDim.x) t_cnt[i] = 0;
+    }, [&](uint64_t tile) {
+        for (int i = threadIdx.x; i < (1 << MAX_COARSE_BITS); i += blockDim.x)
+            thist[tile * (1 << MAX_COARSE_BITS) + i] = t_cnt[i];
     });
     for (int o = 32; o > 0; o >>= 1) {
         mypos += __shfl_down(mypos, o);
@@ -175,18 +190,18 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
         hll_blocks[g * (1 << HLL_REG_BITS) + i] = (uint8_t)h_reg[i];
 }
 
-// coarse counts, bucket-major: cnt[c * ngroups + g] = the group's fine bins in coarse bucket c
-__global__ void __launch_bounds__(256) k_coarse(const unsigned int *hist, uint64_t ngroups, int cbits,
+// coarse counts, bucket-major: cnt[c * ntiles + t] = tile t's records in coarse bucket c
+__global__ void __launch_bounds__(256) k_coarse(const unsigned int *thist, uint64_t ntiles, int cbits,
                                                 unsigned long long *cnt) {
     const uint64_t C = 1ull << cbits;
-    const int per = 1 << (FINE_BITS - cbits);
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < C * ngroups;
-         t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t c = t / ngroups, g = t % ngroups;
-        const unsigned int *h = hist + g * FINE + c * per;
+    const int per = 1 << (MAX_COARSE_BITS - cbits);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C * ntiles;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c = i / ntiles, t = i % ntiles;
+        const unsigned int *h = thist + t * (1 << MAX_COARSE_BITS) + c * per;
         unsigned long long sum = 0;
-        for (int i = 0; i < per; i++) sum += h[i];
-        cnt[t] = sum;
+        for (int j = 0; j < per; j++) sum += h[j];
+        cnt[i] = sum;
     }
 }
 
@@ -206,52 +221,150 @@ __global__ void __launch_bounds__(256) k_bucket_totals(const unsigned int *hist,
     }
 }
 
-// ---- downsweep: scatter records to their (coarse bucket, group) run -----------------------
+// ---- downsweep: records to their (coarse bucket, tile) run --------------------------------
+// N-free reads (the bulk) are processed in lock-step batches of DS_R windows per thread; each
+// batch (2048 records) is counting-sorted by coarse bucket in LDS and stored as contiguous
+// runs, so a wave's stores cover a few full lines instead of 64 scattered 16-B pieces.
+// Reads with 'N' (and tiles too long to stage) follow after the batches, storing directly.
+constexpr int DS_R = 8;
+constexpr int DS_BATCH = TILE_READS * DS_R;
+constexpr int DS_MAX_CBITS = 8;
+
 __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
-                                                         int k, uint64_t gsize, uint64_t ngroups, int cbits,
+                                                         int k, uint64_t gsize, uint64_t ntiles, int cbits,
                                                          const unsigned long long *offs, Rec *recs) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
-    __shared__ unsigned long long cur[1 << MAX_COARSE_BITS];
+    __shared__ Rec sorted[DS_BATCH];
+    __shared__ uint8_t sbk[DS_BATCH];
+    __shared__ unsigned int bcnt[1 << DS_MAX_CBITS], bbeg[1 << DS_MAX_CBITS];
+    __shared__ unsigned long long cur[1 << DS_MAX_CBITS], gbase[1 << DS_MAX_CBITS];
+    __shared__ unsigned int s_rounds, s_total, s_wave[TILE_READS / 64];
     const uint64_t g = blockIdx.x;
     const int C = 1 << cbits;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) cur[c] = offs[(uint64_t)c * ngroups + g];
+    const unsigned int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t mask = kmask64(k);
+    const int sh = 2 * (k - 1);
     const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
-    auto emit = [&](uint64_t fwd, uint64_t rc, uint32_t lf, uint32_t lr, uint64_t r) {
+    auto make = [&](uint64_t fwd, uint64_t rc, uint32_t lf, uint32_t lr, uint64_t r, unsigned int &cb) {
         const uint64_t c = fwd < rc ? fwd : rc;
-        const uint64_t h = mix64(c);
-        const unsigned int cb = cbits ? (unsigned int)(h >> (64 - cbits)) : 0u;
+        cb = cbits ? (unsigned int)(mix64(c) >> (64 - cbits)) : 0u;
         uint32_t lC = fwd <= rc ? lf : lr, lT = fwd <= rc ? lr : lf;
         if (fwd == rc) lT = lC = lf;
-        const unsigned long long p = atomicAdd(&cur[cb], 1ull);
         Rec rec;
         rec.key = c;
         rec.read = (unsigned int)r;
         rec.ev = lC | (lT << 16);
-        recs[p] = rec;
+        return rec;
     };
-    for_group_reads(buf, off, g0, g1, stage,
-                    [&](bool staged, const LdsRead &rv, const LdsReader &lr, uint64_t r, uint64_t s, uint64_t len) {
-        if (staged && (read_flags(rv, (uint32_t)len) & 1) == 0) {
-            if (len >= (uint64_t)k) {
-                const uint32_t m2 = 2 * (uint32_t)(len - k + 1) - 1;
-                windows_clean(rv, (uint32_t)len, k,
-                              [&](uint64_t fwd, uint64_t rc, uint32_t i) { emit(fwd, rc, i, m2 - i, r); });
+    for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
+        const uint64_t r1 = min(r0 + TILE_READS, g1);
+        const uint64_t tile = r0 / TILE_READS;
+        __syncthreads();
+        for (int c = tid; c < C; c += TILE_READS) {
+            cur[c] = offs[(uint64_t)c * ntiles + tile];
+            bcnt[c] = 0;
+        }
+        if (tid == 0) s_rounds = 0;
+        uint64_t base = 0;
+        const bool staged = stage_tile(buf, off, r0, r1, stage, base);
+        __syncthreads();
+        const uint64_t r = r0 + tid;
+        const bool valid = r < r1;
+        uint64_t s = 0, len = 0;
+        bool clean = false;
+        uint32_t rel = 0;
+        if (valid) {
+            s = off[r];
+            len = off[r + 1] - s;
+            rel = (uint32_t)(s - base);
+            if (staged) {
+                const LdsRead rv{reinterpret_cast<const uint32_t *>(stage), rel >> 2, rel & 3};
+                clean = (read_flags(rv, (uint32_t)len) & 1) == 0;
             }
-            return;
         }
-        auto slow = [&](auto &rd) {
-            for_each_window(rd, s, len, k, r, [&](uint64_t fwd, uint64_t rc, uint64_t ef, uint64_t er) {
-                emit(fwd, rc, (uint32_t)ef, (uint32_t)er, r);
-            });
-        };
-        if (staged) {
-            LdsReader l2 = lr;
-            slow(l2);
-        } else {
-            ByteReader br(buf);
-            slow(br);
+        const uint32_t m = (clean && len >= (uint64_t)k) ? (uint32_t)(len - k + 1) : 0u;
+        if (m) atomicMax(&s_rounds, (m + DS_R - 1) / DS_R);
+        __syncthreads();
+        const unsigned int nrounds = s_rounds;
+        uint64_t fwd = 0, rc = 0;
+        uint32_t t = 0, w = 0;
+        if (m)
+            for (; t < (uint32_t)(k - 1); t++) {
+                const uint64_t b = code2(stage[rel + t]);
+                fwd = ((fwd << 2) | b) & mask;
+                rc = (rc >> 2) | ((3ull - b) << sh);
+            }
+        const uint32_t m2 = 2 * m - 1;
+        for (unsigned int round = 0; round < nrounds; round++) {
+            Rec rr[DS_R];
+            unsigned int cb[DS_R], rk[DS_R];
+#pragma unroll
+            for (int j = 0; j < DS_R; j++) {
+                cb[j] = 0xFFFFFFFFu;
+                if (w < m) {
+                    const uint64_t b = code2(stage[rel + t]);
+                    fwd = ((fwd << 2) | b) & mask;
+                    rc = (rc >> 2) | ((3ull - b) << sh);
+                    rr[j] = make(fwd, rc, w, m2 - w, r, cb[j]);
+                    rk[j] = atomicAdd(&bcnt[cb[j]], 1u);
+                    t++;
+                    w++;
+                }
+            }
+            __syncthreads();
+            // exclusive scan of the batch's bucket counts; reserve each bucket's run
+            const unsigned int v = (int)tid < C ? bcnt[tid] : 0u;
+            unsigned int incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int u = __shfl_up(incl, o);
+                if ((int)lane >= o) incl += u;
+            }
+            if (lane == 63) s_wave[wid] = incl;
+            __syncthreads();
+            unsigned int before = 0;
+            for (unsigned int q = 0; q < wid; q++) before += s_wave[q];
+            if ((int)tid < C) {
+                bbeg[tid] = before + incl - v;
+                gbase[tid] = cur[tid];
+                cur[tid] += v;
+            }
+            if (tid == TILE_READS - 1) s_total = before + incl;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < DS_R; j++) {
+                if (cb[j] != 0xFFFFFFFFu) {
+                    const unsigned int p = bbeg[cb[j]] + rk[j];
+                    sorted[p] = rr[j];
+                    sbk[p] = (uint8_t)cb[j];
+                }
+            }
+            __syncthreads();
+            const unsigned int total = s_total;
+            for (unsigned int i = tid; i < total; i += TILE_READS) {
+                const unsigned int c = sbk[i];
+                recs[gbase[c] + (i - bbeg[c])] = sorted[i];
+            }
+            if ((int)tid < C) bcnt[tid] = 0;
+            __syncthreads();
         }
-    });
+        // reads with 'N' or an unstaged tile: reference-order slow path, direct stores
+        if (valid && !clean) {
+            auto slow = [&](auto &rd) {
+                for_each_window(rd, s, len, k, r, [&](uint64_t f2, uint64_t r2, uint64_t ef, uint64_t er) {
+                    unsigned int c;
+                    const Rec rec = make(f2, r2, (uint32_t)ef, (uint32_t)er, r, c);
+                    recs[atomicAdd(&cur[c], 1ull)] = rec;
+                });
+            };
+            if (staged) {
+                LdsReader lr{stage, base};
+                slow(lr);
+            } else {
+                ByteReader br(buf);
+                slow(br);
+            }
+        }
+    }
 }
 
 // ---- refine: split each coarse bucket into its 2^(bbits-cbits) final buckets ----------------
