@@ -115,6 +115,34 @@ int ec_copy_links(ec_session *s, uint64_t *link_offsets, int64_t *links);
 /* ordered dict of build(): kmers[n_dict*k] chars, counts[n_dict]; needs EC_FLAG_WANT_DICT */
 int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts);
 
+/* ---- read-sharded multi-GPU building blocks (pycuda-euler_amd/distributed.py) ------------
+ * Replace the reference's distribution layer (Spark mapPartitions of assemble2,
+ * src/cli_spark_gpu.py:37, and the reduceByKey k-mer shuffle of src/ref_spark.py:83-84) with
+ * count-local -> all-to-all by owner -> merge + solid filter -> all-gather -> graph phase.
+ * All record buffers are device memory of ec_kmer_record (32 B). */
+typedef struct {
+    uint64_t key;   /* canonical 2-bit k-mer                                                */
+    uint32_t count; /* dict count contribution (palindromes count 2 per occurrence)          */
+    uint32_t pad;
+    uint64_t first_canon; /* first insertion event of the canonical string: read << 32 | local */
+    uint64_t first_twin;  /* first insertion event of its twin                                */
+} ec_kmer_record;
+
+/* count the shard (global read ids start at read_base); keeps every distinct k-mer */
+int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offsets, uint64_t nreads,
+                   uint64_t read_base, int k, unsigned flags);
+/* number of dense k-mer records the session holds (after ec_count_shard / ec_merge_owned) */
+uint64_t ec_dense_count(ec_session *s);
+/* pack the held records owner-major into d_out (ec_kmer_record[ec_dense_count]); owner_counts
+ * (host, nowners <= 256) receives the records per owner.  d_out = NULL: counts only. */
+int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts);
+/* owner side: aggregate received records, keep count > limit */
+int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags);
+/* copy the held records (ec_merge_owned's solid set) to d_out */
+int ec_export_dense(ec_session *s, void *d_out);
+/* graph phase (links .. GFA) on a complete solid set; results via ec_copy_* */
+int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags);
+
 #ifdef __cplusplus
 }
 #endif

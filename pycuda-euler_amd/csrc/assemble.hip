@@ -25,9 +25,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <climits>
 #include <vector>
 
 #include "count_part.h"
+#include "shard.h"
 
 namespace ec {
 
@@ -70,7 +72,7 @@ struct ec_session {
     DevBuf h_reads, h_offsets;  // H2D staging for ec_assemble_host
     DevBuf hll, scal, table, dkey, dcnt, dfc, dft, upal, outdeg, cand, succ, pred, st0, st1;
     DevBuf rid, roff, rlist, nextR, PK, RK, PL, PM;
-    DevBuf hist, thist, cnt, offs, bstart, tot, recs, recs2, sub;
+    DevBuf hist, ftot, thist, cnt, offs, bstart, tot, recs, recs2, sub;
     DevBuf startOf, skeys, svals, skeys2, svals2, cidxOf, clen, coff, chars, cfirst, clast, headOf, tailOf;
     DevBuf lk, lcnt, tmp, dchars, dcounts;
     // results (host)
@@ -87,6 +89,8 @@ struct ec_session {
     bool kused[EC_NKERNELS] = {};
     bool events = false;
     bool timing = false;
+    unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
+    DevBuf ocnt;
 };
 
 namespace {
@@ -138,20 +142,16 @@ inline void kmark(ec_session *s, int kid, int end) {
     }
 }
 
-int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, int k, int limit,
-             unsigned flags) {
+// per-call setup shared by every entry point: argument checks, stats reset, timing events,
+// zeroed device scalars
+int begin_call(ec_session *s, int k, unsigned flags) {
     s->have = false;
     if (k < 1 || k > EC_MAX_K) {
         set_error("k=%d outside [1,%d] (fused path uses 64-bit keys)", k, EC_MAX_K);
         return EC_ERR_ARG;
     }
-    if (nreads >= (1ull << 32)) {
-        set_error("nreads=%llu >= 2^32", (unsigned long long)nreads);
-        return EC_ERR_ARG;
-    }
     EC_HIP(hipSetDevice(s->device));
     memset(&s->stats, 0, sizeof(s->stats));
-    s->stats.n_reads = nreads;
     s->k = k;
     s->want_dict = (flags & EC_FLAG_WANT_DICT) != 0;
     const bool timing = (flags & EC_FLAG_TIMING) != 0;
@@ -162,13 +162,26 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     }
     s->timing = timing;
     for (auto &u : s->kused) u = false;
-    hipStream_t st = s->stream;
-    const unsigned B = 256;
-
     EC_CHECK(s->scal.ensure(sizeof(Scalars)));
     Scalars *dsc = s->scal.as<Scalars>();
-    EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
-    EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
+    EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), s->stream));
+    EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), s->stream));
+    return EC_OK;
+}
+
+// build:25-42 on the device: count canonical k-mers of reads [0, nreads) (global read ids
+// start at read_base), keep those with count > limit as dense arrays dkey/dcnt/dfc/dft (U of
+// them) and a SolidIndex over them.
+int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, uint64_t read_base,
+                int k, long long limit, unsigned flags, unsigned int &U, SolidIndex &sidx) {
+    if (nreads + read_base > (1ull << 32)) {
+        set_error("global read ids reach %llu >= 2^32", (unsigned long long)(nreads + read_base));
+        return EC_ERR_ARG;
+    }
+    s->stats.n_reads = nreads;
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc;
 
     // ---- prescan = partition upsweep ------------------------------------------------------
@@ -179,6 +192,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     ngroups = std::max<uint64_t>(1, (nreads + gsize - 1) / gsize);
     EC_CHECK(s->hist.ensure(ngroups * FINE * 4));
     EC_CHECK(s->hll.ensure(ngroups * (1 << HLL_REG_BITS)));
+    EC_CHECK(s->ftot.ensure((FINE + (1 << HLL_REG_BITS)) * 8));
     EC_CHECK(s->thist.ensure(std::max<uint64_t>(ntiles, 1) * (1 << MAX_COARSE_BITS) * 4));
     if (nreads) {
         kmark(s, 0, 0);
@@ -186,7 +200,12 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
                                                            s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad,
                                                            &dsc->maxlocal, &dsc->skew, s->thist.as<unsigned int>());
         kmark(s, 0, 1);
-        k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<uint8_t>(), (int)ngroups, HLL_REG_BITS, &dsc->est);
+        EC_HIP(hipMemsetAsync(s->ftot.p, 0, (FINE + (1 << HLL_REG_BITS)) * 8, st));
+        k_fine_totals<<<dim3(FINE / 256, TOT_SLICES), 256, 0, st>>>(
+            s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), ngroups, s->ftot.as<unsigned long long>(),
+            reinterpret_cast<unsigned int *>(s->ftot.as<unsigned long long>() + FINE));
+        k_hll_final<<<1, 1024, 0, st>>>(reinterpret_cast<unsigned int *>(s->ftot.as<unsigned long long>() + FINE),
+                                        HLL_REG_BITS, &dsc->est);
     }
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -208,7 +227,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
                 est / FINE <= 2400.0;
     int bbits = 0;
     unsigned int slots = 2048;
-    SolidIndex sidx{};
+    sidx = SolidIndex{};
     uint64_t umax = 0;
     if (part) {
         while (bbits < FINE_BITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
@@ -228,12 +247,13 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
         k_coarse<<<grid_for(Ck * ntiles, B, 8192), B, 0, st>>>(s->thist.as<unsigned int>(), ntiles, cbits,
                                                               s->cnt.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ntiles));
-        k_bucket_totals<<<grid_for(Bk + 1, B), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, bbits,
+        k_bucket_totals<<<grid_for(Bk + 1, B), B, 0, st>>>(s->ftot.as<unsigned long long>(), bbits,
                                                           s->tot.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
         kmark(s, 1, 0);
         k_downsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ntiles, cbits,
-                                                             s->offs.as<unsigned long long>(), s->recs.as<Rec>());
+                                                             s->offs.as<unsigned long long>(), s->recs.as<Rec>(),
+                                                             read_base);
         kmark(s, 1, 1);
         Rec *final_recs = s->recs.as<Rec>();
         if (bbits > cbits) {
@@ -294,7 +314,7 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
             kmark(s, 3, 0);
             if (nreads)
                 k_count<<<grid_for(nreads, B), B, 0, st>>>(d_reads, d_off, nreads, k, s->table.as<Slot>(), cap - 1,
-                                                          &dsc->overflow);
+                                                          &dsc->overflow, read_base);
             kmark(s, 3, 1);
             mark(s, 2 * EC_STAGE_COUNT + 1);
             EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
@@ -325,15 +345,82 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
         sidx.capmask = cap - 1;
         s->stats.count_path = EC_PATH_GENERAL;
     }
-    const unsigned int U = hsc.nsolid;
+    U = hsc.nsolid;
     s->stats.n_distinct = hsc.ndistinct;
     s->stats.n_solid = U;
     if (2ull * U >= (unsigned long long)CYC) {
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
     }
+    return EC_OK;
+}
+
+// Owner-side aggregation of exchanged k-mer records (count sum, first-event min) followed by
+// the solid filter: the merge step of the sharded path, and the way a gathered solid set is
+// loaded for phase_graph (limit = keep all).
+int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)(2.2 * (double)n) + 1024) cap <<= 1;
+    for (int attempt = 0;; attempt++) {
+        EC_CHECK(s->table.ensure(cap * sizeof(Slot)));
+        mark(s, 2 * EC_STAGE_COUNT);
+        k_table_clear<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap);
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        if (n) k_merge_agg<<<grid_for(n, B), B, 0, st>>>(d_agg, n, s->table.as<Slot>(), cap - 1, &dsc->overflow);
+        mark(s, 2 * EC_STAGE_COUNT + 1);
+        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (!hsc.overflow) break;
+        if (attempt >= 4) {
+            set_error("merge table overflow at capacity %llu", (unsigned long long)cap);
+            return EC_ERR_CAPACITY;
+        }
+        cap <<= 2;
+        s->stats.table_retries++;
+    }
+    s->stats.table_capacity = cap;
+    mark(s, 2 * EC_STAGE_COMPACT);
+    EC_CHECK(s->dkey.ensure(cap * 8));
+    EC_CHECK(s->dcnt.ensure(cap * 4));
+    EC_CHECK(s->dfc.ensure(cap * 8));
+    EC_CHECK(s->dft.ensure(cap * 8));
+    EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
+    k_compact<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap, limit, s->dkey.as<unsigned long long>(),
+                                                   s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                                   s->dft.as<unsigned long long>(), &dsc->nsolid, &dsc->ndistinct);
+    mark(s, 2 * EC_STAGE_COMPACT + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    U = hsc.nsolid;
+    s->stats.n_distinct = hsc.ndistinct;
+    s->stats.n_solid = U;
+    s->stats.count_path = EC_PATH_GENERAL;
+    sidx = SolidIndex{};
+    sidx.table = s->table.as<Slot>();
+    sidx.capmask = cap - 1;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
+    return EC_OK;
+}
+
+// all_contigs:79-111 on the device from the solid set of phase_count / phase_merge
+int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
     const unsigned int N = 2 * U;
     const size_t Nn = std::max<size_t>(N, 1);
+    const bool timing = s->timing;
 
     // ---- links ----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_LINKS);
@@ -524,6 +611,15 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     return EC_OK;
 }
 
+int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, int k, int limit,
+             unsigned flags) {
+    EC_CHECK(begin_call(s, k, flags));
+    unsigned int U = 0;
+    SolidIndex sidx{};
+    EC_CHECK(phase_count(s, d_reads, d_off, nreads, 0, k, (long long)limit, flags, U, sidx));
+    return phase_graph(s, k, U, sidx);
+}
+
 }  // namespace
 
 extern "C" {
@@ -573,7 +669,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
-                     &s->hist, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub};
+                     &s->ocnt, &s->hist, &s->ftot, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub};
     for (auto *b : all) b->release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);
@@ -684,6 +780,95 @@ int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts) {
     if (counts) EC_HIP(hipMemcpyAsync(counts, s->dcounts.p, (size_t)nd * 4, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     return EC_OK;
+}
+
+
+// ---- sharded (multi-GPU) building blocks ---------------------------------------------------
+int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offsets, uint64_t nreads,
+                   uint64_t read_base, int k, unsigned flags) {
+    if (!s || !d_offsets) {
+        set_error("null session/offsets");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(begin_call(s, k, flags));
+    unsigned int U = 0;
+    SolidIndex sidx{};
+    EC_CHECK(phase_count(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, flags, U, sidx));
+    s->n_dense = U;
+    return EC_OK;
+}
+
+int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts) {
+    if (!s || nowners < 1 || nowners > MAX_OWNERS || !owner_counts) {
+        set_error("bad ec_export_by_owner arguments (nowners=%d)", nowners);
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    const unsigned int n = s->n_dense;
+    EC_CHECK(s->ocnt.ensure(2 * MAX_OWNERS * 8));
+    unsigned long long *cnt = s->ocnt.as<unsigned long long>(), *cur = cnt + MAX_OWNERS;
+    EC_HIP(hipMemsetAsync(cnt, 0, MAX_OWNERS * 8, st));
+    if (n) k_owner_hist<<<grid_for(n, B, 2048), B, 0, st>>>(s->dkey.as<unsigned long long>(), n, nowners, cnt);
+    std::vector<unsigned long long> h(nowners), o(nowners);
+    EC_HIP(hipMemcpyAsync(h.data(), cnt, nowners * 8, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    unsigned long long acc = 0;
+    for (int i = 0; i < nowners; i++) {
+        o[i] = acc;
+        acc += h[i];
+        owner_counts[i] = h[i];
+    }
+    if (n && d_out) {
+        EC_HIP(hipMemcpyAsync(cur, o.data(), nowners * 8, hipMemcpyHostToDevice, st));
+        k_owner_scatter<<<grid_for(n, B, 4096), B, 0, st>>>(s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+                                                            s->dfc.as<unsigned long long>(),
+                                                            s->dft.as<unsigned long long>(), n, nowners, cur,
+                                                            reinterpret_cast<Agg *>(d_out));
+        EC_HIP(hipStreamSynchronize(st));
+    }
+    return EC_OK;
+}
+
+int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags) {
+    if (!s || (n && !d_records)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(begin_call(s, k, flags));
+    unsigned int U = 0;
+    SolidIndex sidx{};
+    EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx));
+    s->n_dense = U;
+    return EC_OK;
+}
+
+int ec_export_dense(ec_session *s, void *d_out) {
+    if (!s) return EC_ERR_ARG;
+    EC_HIP(hipSetDevice(s->device));
+    const unsigned int n = s->n_dense;
+    if (n && d_out) {
+        k_export_dense<<<grid_for(n, 256), 256, 0, s->stream>>>(
+            s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+            s->dft.as<unsigned long long>(), n, reinterpret_cast<Agg *>(d_out));
+        EC_HIP(hipStreamSynchronize(s->stream));
+    }
+    return EC_OK;
+}
+
+uint64_t ec_dense_count(ec_session *s) { return s ? s->n_dense : 0; }
+
+int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags) {
+    if (!s || (n && !d_records)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(begin_call(s, k, flags));
+    unsigned int U = 0;
+    SolidIndex sidx{};
+    EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, LLONG_MIN, U, sidx));
+    return phase_graph(s, k, U, sidx);
 }
 
 }  // extern "C"

@@ -73,6 +73,19 @@ __device__ inline uint32_t base_code(uint32_t c) {
     }
 }
 
+// Wave-aggregated append: every lane of the wave must call it (convergent).  Lanes with
+// pred get consecutive slots of *counter; one atomic per wave instead of one per lane.
+__device__ inline unsigned int wave_append(unsigned int *counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (!m) return 0;
+    const unsigned int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    unsigned int base = 0;
+    if ((int)lane == leader) base = atomicAdd(counter, (unsigned int)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (unsigned int)__popcll(m & ((1ull << lane) - 1));
+}
+
 inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 1u << 20) {
     uint64_t g = (n + block - 1) / block;
     if (g < 1) g = 1;

@@ -17,16 +17,15 @@ struct alignas(32) Slot {
 };
 static_assert(sizeof(Slot) == 32, "slot layout");
 
-// HyperLogLog estimate (harmonic mean + small-range correction) over per-group registers
-__global__ void __launch_bounds__(1024) k_hll_final(const uint8_t *hll_blocks, int nblocks, int mbits, double *est) {
+// HyperLogLog estimate (harmonic mean + small-range correction) from the merged registers
+__global__ void __launch_bounds__(1024) k_hll_final(const unsigned int *reg, int mbits, double *est) {
     const int M = 1 << mbits;
     __shared__ double red[1024];
     __shared__ int zeros[1024];
     double sum = 0;
     int z = 0;
     for (int j = threadIdx.x; j < M; j += blockDim.x) {
-        uint32_t m = 0;
-        for (int b = 0; b < nblocks; b++) m = max(m, (uint32_t)hll_blocks[(uint64_t)b * M + j]);
+        const uint32_t m = reg[j];
         sum += ldexp(1.0, -(int)m);
         z += (m == 0);
     }
@@ -66,12 +65,13 @@ __global__ void __launch_bounds__(256) k_table_clear(Slot *t, uint64_t cap) {
 // every window of twin(seg) (build:31-35) == +1 per window on the canonical key, +2 when the
 // window is its own twin (even-k palindrome: both loops hit the same string).
 __global__ void __launch_bounds__(256) k_count(const uint8_t *buf, const uint64_t *off, uint64_t nreads, int k,
-                                               Slot *table, uint64_t capmask, unsigned int *overflow) {
+                                               Slot *table, uint64_t capmask, unsigned int *overflow,
+                                               uint64_t read_base) {
     for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nreads;
          r += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t s = off[r], len = off[r + 1] - s;
         ByteReader rd(buf);
-        for_each_window(rd, s, len, k, r, [&](uint64_t fwd, uint64_t rc, uint64_t ef, uint64_t er) {
+        for_each_window(rd, s, len, k, r + read_base, [&](uint64_t fwd, uint64_t rc, uint64_t ef, uint64_t er) {
             const bool pal = fwd == rc;
             const uint64_t c = fwd < rc ? fwd : rc;
             // first events of the canonical string and of its twin

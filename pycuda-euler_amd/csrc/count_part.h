@@ -205,18 +205,32 @@ __global__ void __launch_bounds__(256) k_coarse(const unsigned int *thist, uint6
     }
 }
 
+// fine-bin totals over all groups (2-D: bins x group slices, one atomic per slice) and the
+// HyperLogLog register maxima over all groups
+constexpr int TOT_SLICES = 32;
+__global__ void __launch_bounds__(256) k_fine_totals(const unsigned int *hist, const uint8_t *hll, uint64_t ngroups,
+                                                     unsigned long long *ftot, unsigned int *hreg) {
+    const unsigned int f = blockIdx.x * blockDim.x + threadIdx.x;  // < FINE
+    const unsigned int sl = blockIdx.y;
+    unsigned long long sum = 0;
+    unsigned int mx = 0;
+    for (uint64_t g = sl; g < ngroups; g += TOT_SLICES) {
+        sum += hist[g * FINE + f];
+        if (f < (1u << HLL_REG_BITS)) mx = max(mx, (unsigned int)hll[g * (1 << HLL_REG_BITS) + f]);
+    }
+    if (sum) atomicAdd(&ftot[f], sum);
+    if (f < (1u << HLL_REG_BITS) && mx) atomicMax(&hreg[f], mx);
+}
+
 // records per final bucket (bbits granularity); tot[B] = 0 so its exclusive scan ends at P
-__global__ void __launch_bounds__(256) k_bucket_totals(const unsigned int *hist, uint64_t ngroups, int bbits,
+__global__ void __launch_bounds__(256) k_bucket_totals(const unsigned long long *ftot, int bbits,
                                                        unsigned long long *tot) {
     const uint64_t B = 1ull << bbits;
     const int per = 1 << (FINE_BITS - bbits);
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b <= B; b += (uint64_t)gridDim.x * blockDim.x) {
         unsigned long long sum = 0;
         if (b < B)
-            for (uint64_t g = 0; g < ngroups; g++) {
-                const unsigned int *h = hist + g * FINE + b * per;
-                for (int i = 0; i < per; i++) sum += h[i];
-            }
+            for (int i = 0; i < per; i++) sum += ftot[b * per + i];
         tot[b] = sum;
     }
 }
@@ -232,7 +246,8 @@ constexpr int DS_MAX_CBITS = 8;
 
 __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                          int k, uint64_t gsize, uint64_t ntiles, int cbits,
-                                                         const unsigned long long *offs, Rec *recs) {
+                                                         const unsigned long long *offs, Rec *recs,
+                                                         uint64_t read_base) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
     __shared__ Rec sorted[DS_BATCH];
     __shared__ uint8_t sbk[DS_BATCH];
@@ -252,7 +267,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
         if (fwd == rc) lT = lC = lf;
         Rec rec;
         rec.key = c;
-        rec.read = (unsigned int)r;
+        rec.read = (unsigned int)(r + read_base);
         rec.ev = lC | (lT << 16);
         return rec;
     };

@@ -125,12 +125,14 @@ __device__ inline bool ruler_hash(unsigned int x, unsigned int smask) {
 __global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsigned int *pred, unsigned int N,
                                                 unsigned int smask, int first, unsigned int *rid, unsigned int *roff,
                                                 unsigned int *rlist, unsigned int *nr) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+    for (uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x; t0 < N; t0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = t0 + threadIdx.x;
         const unsigned int x = (unsigned int)t;
-        if ((x & 1) && upal[x >> 1]) continue;
-        if (rid[x] != NONE32) continue;
-        if ((first && pred[x] == NONE32) || ruler_hash(x, smask)) {
-            const unsigned int i = atomicAdd(nr, 1u);
+        bool sel = false;
+        if (t < N && !((x & 1) && upal[x >> 1]) && rid[x] == NONE32)
+            sel = (first && pred[x] == NONE32) || ruler_hash(x, smask);
+        const unsigned int i = wave_append(nr, sel);
+        if (sel) {
             rlist[i] = x;
             rid[x] = i;
             roff[x] = 0;

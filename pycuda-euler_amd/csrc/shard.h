@@ -1,0 +1,115 @@
+// shard.h -- building blocks of the read-sharded multi-GPU path (distributed.py):
+//   every rank counts its read shard (phase_count, no solid filter), exports its distinct
+//   k-mers grouped by owner rank (owner = hash of the canonical key), the records are
+//   exchanged with one RCCL all-to-all, each owner merges what it received (sum of counts,
+//   min of first events) and applies the solid filter; the solid sets are all-gathered and
+//   every rank runs the graph phase on the full set.
+#pragma once
+#include "count_global.h"
+
+namespace ec {
+
+// one aggregated canonical k-mer: the payload of the exchange (ec_kmer_record in eulerhip.h)
+struct alignas(16) Agg {
+    unsigned long long key;
+    unsigned int count;
+    unsigned int pad;
+    unsigned long long fC;
+    unsigned long long fT;
+};
+static_assert(sizeof(Agg) == 32, "agg layout");
+
+__device__ inline unsigned int owner_of(uint64_t key, unsigned int nowners) {
+    return (unsigned int)(((mix64(key ^ 0xD6E8FEB86659FD93ull) >> 32) * (uint64_t)nowners) >> 32);
+}
+
+constexpr int MAX_OWNERS = 256;
+
+__global__ void __launch_bounds__(256) k_owner_hist(const unsigned long long *dkey, unsigned int n, unsigned int nowners,
+                                                    unsigned long long *cnt) {
+    __shared__ unsigned int h[MAX_OWNERS];
+    for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[owner_of(dkey[t], nowners)], 1u);
+    __syncthreads();
+    for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x)
+        if (h[i]) atomicAdd(&cnt[i], (unsigned long long)h[i]);
+}
+
+// scatter dense records into owner-major order; cursor[o] starts at the owner's offset
+__global__ void __launch_bounds__(256) k_owner_scatter(const unsigned long long *dkey, const unsigned int *dcnt,
+                                                       const unsigned long long *dfc, const unsigned long long *dft,
+                                                       unsigned int n, unsigned int nowners,
+                                                       unsigned long long *cursor, Agg *out) {
+    __shared__ unsigned int h[MAX_OWNERS];
+    __shared__ unsigned long long base[MAX_OWNERS];
+    for (uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x; t0 < n; t0 += (uint64_t)gridDim.x * blockDim.x) {
+        for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        const uint64_t t = t0 + threadIdx.x;
+        unsigned int o = 0, rk = 0;
+        if (t < n) {
+            o = owner_of(dkey[t], nowners);
+            rk = atomicAdd(&h[o], 1u);
+        }
+        __syncthreads();
+        for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x)
+            base[i] = h[i] ? atomicAdd(&cursor[i], (unsigned long long)h[i]) : 0ull;
+        __syncthreads();
+        if (t < n) {
+            Agg a;
+            a.key = dkey[t];
+            a.count = dcnt[t];
+            a.pad = 0;
+            a.fC = dfc[t];
+            a.fT = dft[t];
+            out[base[o] + rk] = a;
+        }
+        __syncthreads();
+    }
+}
+
+// owner side: aggregate received records into the HBM table (count sum, first-event min)
+__global__ void __launch_bounds__(256) k_merge_agg(const Agg *in, uint64_t n, Slot *table, uint64_t capmask,
+                                                   unsigned int *overflow) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const Agg a = in[t];
+        uint64_t h = mix64(a.key) & capmask;
+        for (int probe = 0;; probe++) {
+            if (probe >= MAX_PROBE) {
+                atomicOr(overflow, 1u);
+                break;
+            }
+            Slot *sl = table + h;
+            unsigned long long cur = sl->key;
+            if (cur == EMPTY_KEY) {
+                cur = atomicCAS(&sl->key, EMPTY_KEY, a.key);
+                if (cur == EMPTY_KEY) cur = a.key;
+            }
+            if (cur == a.key) {
+                atomicAdd(&sl->count, a.count);
+                if (a.fC < sl->fC) atomicMin(&sl->fC, a.fC);
+                if (a.fT < sl->fT) atomicMin(&sl->fT, a.fT);
+                break;
+            }
+            h = (h + 1) & capmask;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_export_dense(const unsigned long long *dkey, const unsigned int *dcnt,
+                                                      const unsigned long long *dfc, const unsigned long long *dft,
+                                                      unsigned int n, Agg *out) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        Agg a;
+        a.key = dkey[t];
+        a.count = dcnt[t];
+        a.pad = 0;
+        a.fC = dfc[t];
+        a.fT = dft[t];
+        out[t] = a;
+    }
+}
+
+}  // namespace ec

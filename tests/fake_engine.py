@@ -1,0 +1,103 @@
+"""CPU stand-in for distributed.HipEngine -- TEST INFRASTRUCTURE ONLY.
+
+Lets tests drive the real multi-rank orchestration (distributed.sharded_assemble, TorchComm)
+over the gloo backend on CPU.  Its compute comes from the design model (model_parallel.py),
+which is pinned to the reference's golden vectors; the record layout and the owner function
+are the device ones (ec_kmer_record, shard.h owner_of), so the exchange is byte-identical.
+"""
+import numpy as np
+import torch
+
+from distributed import REC_BYTES, REC_DTYPE
+from model_parallel import model_count, model_graph, twin
+
+M64 = (1 << 64) - 1
+CODE = {"A": 0, "C": 1, "G": 2, "T": 3}
+
+
+def mix64(x):
+    x &= M64
+    x ^= x >> 33
+    x = (x * 0xff51afd7ed558ccd) & M64
+    x ^= x >> 33
+    x = (x * 0xc4ceb9fe1a85ec53) & M64
+    x ^= x >> 33
+    return x
+
+
+def owner_of(key, n):
+    return ((mix64(key ^ 0xD6E8FEB86659FD93) >> 32) * n) >> 32
+
+
+def encode(s):
+    v = 0
+    for c in s:
+        v = (v << 2) | CODE[c]
+    return v
+
+
+def decode(v, k):
+    return "".join("ACGT"[(v >> (2 * (k - 1 - i))) & 3] for i in range(k))
+
+
+class _Stats:
+    def __init__(self, P):
+        self.n_positions = P
+
+
+class _Result:
+    def __init__(self, d, contigs, links):
+        self.dict_items, self.contigs, self.links = d, contigs, links
+
+
+class FakeEngine:
+    def __init__(self, k):
+        self.k = k
+        self.recs = np.zeros(0, REC_DTYPE)
+
+    def _bytes(self, recs):
+        return torch.from_numpy(np.frombuffer(recs.tobytes(), dtype=np.uint8).copy())
+
+    def _recs(self, t):
+        return np.frombuffer(t.numpy().tobytes(), dtype=REC_DTYPE)
+
+    def count_shard(self, d_reads, d_off, nreads, read_base, k, flags=0):
+        buf = d_reads.numpy().tobytes()
+        off = d_off.numpy()
+        reads = [buf[int(off[i]):int(off[i + 1])].decode() for i in range(nreads)]
+        cnt, first = model_count(reads, k, read_base)
+        P = sum(max(0, len(seg) - k + 1) for r in reads for seg in r.split("N"))
+        out = np.zeros(len(cnt), REC_DTYPE)
+        for i, (c, v) in enumerate(cnt.items()):
+            out[i] = (encode(c), v, 0, first[c], first[twin(c)])
+        self.recs = out
+        return _Stats(P)
+
+    def export_by_owner(self, nowners):
+        own = np.array([owner_of(int(x), nowners) for x in self.recs["key"]], dtype=np.int64)
+        order = np.argsort(own, kind="stable")
+        counts = [int((own == o).sum()) for o in range(nowners)]
+        return self._bytes(self.recs[order]), counts
+
+    def merge_owned(self, recs, k, limit, flags=0):
+        agg = {}
+        for r in self._recs(recs):
+            key = int(r["key"])
+            c, a, b = agg.get(key, (0, 1 << 63, 1 << 63))
+            agg[key] = (c + int(r["count"]), min(a, int(r["first_canon"])), min(b, int(r["first_twin"])))
+        keep = [(key, c, a, b) for key, (c, a, b) in agg.items() if c > limit]
+        out = np.zeros(len(keep), REC_DTYPE)
+        for i, (key, c, a, b) in enumerate(keep):
+            out[i] = (key, c, 0, a, b)
+        self.recs = out
+        return self._bytes(out)
+
+    def assemble_from_solid(self, recs, k, flags=0):
+        cnt, first = {}, {}
+        for r in self._recs(recs):
+            c = decode(int(r["key"]), k)
+            cnt[c] = int(r["count"])
+            first[c] = int(r["first_canon"])
+            first[twin(c)] = int(r["first_twin"]) if twin(c) != c else int(r["first_canon"])
+        d, contigs, links = model_graph(cnt, first, k)
+        return _Result(d, contigs, links)

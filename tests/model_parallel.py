@@ -16,10 +16,11 @@ def twin(s):
     return "".join(COMP[c] for c in reversed(s))
 
 
-def model_assemble(reads, k, limit=1):
-    # --- count: canonical key, window count, first event per strand string ---------------
+def model_count(reads, k, read_base=0):
+    """canonical key -> dict count contribution, string -> first insertion event"""
     cnt, first = {}, {}
-    for r, read in enumerate(reads):
+    for r0, read in enumerate(reads):
+        r = r0 + read_base
         wb = 0  # windows in earlier segments of this read
         for seg in read.split("N"):
             m = len(seg) - k + 1
@@ -35,7 +36,18 @@ def model_assemble(reads, k, limit=1):
                 first[x] = min(first.get(x, 1 << 62), ef)
                 first[t] = min(first.get(t, 1 << 62), er)
             wb += m
+    return cnt, first
+
+
+def model_assemble(reads, k, limit=1):
+    cnt, first = model_count(reads, k)
     solid = {c for c, v in cnt.items() if v > limit}
+    return model_graph({c: cnt[c] for c in solid}, first, k)
+
+
+def model_graph(cnt, first, k):
+    """all_contigs from a solid set: cnt = canonical -> count, first = string -> first event"""
+    solid = set(cnt)
     ind = lambda s: min(s, twin(s)) in solid  # noqa: E731
     fw = lambda s: [s[1:] + b for b in "ACGT"]  # noqa: E731
     bw = lambda s: [b + s[:-1] for b in "ACGT"]  # noqa: E731

@@ -1,0 +1,92 @@
+"""The N > 1 path (pycuda-euler_amd/distributed.py) on CPU: world_size 2 and 3 over gloo, the
+real orchestration and collectives (TorchComm: all-to-all-v, all-gather-v, all-reduce), the
+compute from tests/fake_engine.py.  Every rank must hold the reference's result for the
+whole read set (checked against the oracle, itself pinned to the golden vectors)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle
+from conftest import PKG, ROOT, golden_cases
+from synth import make_reads
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, reads, k, limit, q):
+    import torch
+    import torch.distributed as dist
+
+    for p in (PKG, os.path.join(ROOT, "oracle"), os.path.dirname(os.path.abspath(__file__))):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import distributed
+        from fake_engine import FakeEngine
+
+        lo, hi = distributed.shard_range(len(reads), rank, world)
+        mine = reads[lo:hi]
+        buf = "".join(mine).encode()
+        off = np.zeros(len(mine) + 1, np.int64)
+        off[1:] = np.cumsum([len(r) for r in mine])
+        res, P = distributed.sharded_assemble(FakeEngine(k), distributed.TorchComm(),
+                                              torch.frombuffer(bytearray(buf or b"\0"), dtype=torch.uint8),
+                                              torch.from_numpy(off), len(mine), lo, k, limit)
+        q.put((rank, P, res.contigs, res.links))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(reads, k, limit, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return sorted(out)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_matches_reference_g200(world):
+    (case,) = [c for c in golden_cases("g200.json") if c["k"] == 15]
+    for rank, P, contigs, links in _run(case["reads"], 15, 1, world):
+        assert contigs == case["contigs"] and links == case["links"]
+
+
+def test_sharded_matches_oracle_synthetic():
+    buf, off = make_reads(3_000, 600, 60, 5151, err=0.003, circular=True)
+    reads = [buf[int(off[i]):int(off[i + 1])].tobytes().decode() for i in range(len(off) - 1)]
+    _, rc, rl = oracle.assemble(reads, 17, 1, want_dict=False)
+    out = _run(reads, 17, 1, 2)
+    P_ref = sum(len(r) - 16 for r in reads)
+    for rank, P, contigs, links in out:
+        assert P == P_ref
+        assert contigs == rc and links == rl
+
+
+def test_shard_range_partitions_reads():
+    import distributed
+
+    for n in (0, 1, 7, 100):
+        for w in (1, 2, 3, 8):
+            spans = [distributed.shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
