@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--config", default="ecoli10m", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true", help="use the multi-GPU path even with one rank")
     args = ap.parse_args()
 
     import torch
@@ -114,9 +115,14 @@ def main():
         log("note: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world))
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.sharded
+    if use_dist:
         import torch.distributed as dist
 
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29541")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import eulerhip
@@ -129,7 +135,7 @@ def main():
     log("rank %d: generated %d reads in %.1f s" % (rank, cfg["reads"], time.time() - t0))
     k = cfg["k"]
 
-    if world == 1:
+    if not use_dist:
         d_buf = torch.from_numpy(buf).cuda()
         d_off = torch.from_numpy(off.astype(np.int64)).cuda()
         torch.cuda.synchronize()
@@ -156,7 +162,7 @@ def main():
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step(True)
-        st = sess.stats() if world == 1 else runner.stats()
+        st = sess.stats() if not use_dist else runner.stats()
         stage += np.array(list(st.stage_ms))
         kern += np.array(list(st.kernel_ms))
     torch.cuda.synchronize()
@@ -168,9 +174,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
-    st = sess.stats() if world == 1 else runner.stats()
-    P = int(st.n_positions) if world == 1 else runner.total_positions
-    U = int(st.n_solid)
+    st = sess.stats() if not use_dist else runner.stats()
+    P = int(st.n_positions) if not use_dist else runner.total_positions
+    U = int(st.n_solid) if not use_dist else int(runner.engine.stats().n_solid)
     R, L = cfg["reads"], cfg["read_len"]
     value = P / (ms / 1e3)
 
@@ -183,7 +189,7 @@ def main():
     kid = int(np.argmax(kern))
     kname = eulerhip.KERNEL_NAMES[kid]
     kms = float(kern[kid])
-    kb = kernel_alg_bytes(kname, P if world == 1 else P // world, R // world, L)
+    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L)  # this rank's launch
     achieved = kb / (kms / 1e3) / 1e9
     tr = load_traffic(cfg["name"], kname)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -203,9 +209,10 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic (iid ACGT genome, uniform error-free 100 bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)" % cfg["seed"],
         "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
-                   "positions": P, "solid_kmers": U, "contigs": int(st.n_contigs),
+                   "positions": P, "solid_kmers": U,
+                   "contigs": int(st.n_contigs if not use_dist else runner.engine.stats().n_contigs),
                    "count_path": ["partitioned", "general"][int(st.count_path)], "buckets": int(st.n_buckets),
-                   "parallelism": "dp%d" % world},
+                   "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
         "roofline": roof,
         "cpu_baseline": cpu,
         "stage_ms": {names[i]: round(stage[i] / args.steps, 3) for i in range(len(names))},

@@ -87,9 +87,11 @@ struct ec_session {
     hipEvent_t ev[2 * EC_NSTAGES] = {};
     hipEvent_t kev[2 * EC_NKERNELS] = {};
     bool kused[EC_NKERNELS] = {};
+    bool sused[EC_NSTAGES] = {};
     bool events = false;
     bool timing = false;
     unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
+    bool stats_ok = false;     // ec_get_stats valid (any successful call)
     DevBuf ocnt;
 };
 
@@ -132,7 +134,10 @@ int sort_pairs(ec_session *s, unsigned long long *kin, unsigned long long *kout,
 }
 
 inline void mark(ec_session *s, int idx) {
-    if (s->timing) hipEventRecord(s->ev[idx], s->stream);
+    if (s->timing) {
+        hipEventRecord(s->ev[idx], s->stream);
+        if (idx & 1) s->sused[idx >> 1] = true;
+    }
 }
 // kernel-level timing events: kernel id, 0 = before / 1 = after
 inline void kmark(ec_session *s, int kid, int end) {
@@ -142,10 +147,27 @@ inline void kmark(ec_session *s, int kid, int end) {
     }
 }
 
+// elapsed times of the stage / kernel events recorded during this call (EC_FLAG_TIMING)
+void collect_timing(ec_session *s) {
+    if (!s->timing) return;
+    hipStreamSynchronize(s->stream);
+    for (int i = 0; i < EC_NSTAGES; i++) {
+        float ms = 0;
+        if (s->sused[i]) hipEventElapsedTime(&ms, s->ev[2 * i], s->ev[2 * i + 1]);
+        s->stats.stage_ms[i] = ms;
+    }
+    for (int i = 0; i < EC_NKERNELS; i++) {
+        float ms = 0;
+        if (s->kused[i]) hipEventElapsedTime(&ms, s->kev[2 * i], s->kev[2 * i + 1]);
+        s->stats.kernel_ms[i] = ms;
+    }
+}
+
 // per-call setup shared by every entry point: argument checks, stats reset, timing events,
 // zeroed device scalars
 int begin_call(ec_session *s, int k, unsigned flags) {
     s->have = false;
+    s->stats_ok = false;
     if (k < 1 || k > EC_MAX_K) {
         set_error("k=%d outside [1,%d] (fused path uses 64-bit keys)", k, EC_MAX_K);
         return EC_ERR_ARG;
@@ -162,6 +184,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     }
     s->timing = timing;
     for (auto &u : s->kused) u = false;
+    for (auto &u : s->sused) u = false;
     EC_CHECK(s->scal.ensure(sizeof(Scalars)));
     Scalars *dsc = s->scal.as<Scalars>();
     EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), s->stream));
@@ -595,19 +618,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
 
     s->stats.n_dict = 2ull * U - hsc.npal;  // len(build()): palindromes have one entry
 
-    if (timing) {
-        for (int i = 0; i < EC_NSTAGES; i++) {
-            float ms = 0;
-            hipEventElapsedTime(&ms, s->ev[2 * i], s->ev[2 * i + 1]);
-            s->stats.stage_ms[i] = ms;
-        }
-        for (int i = 0; i < EC_NKERNELS; i++) {
-            float ms = 0;
-            if (s->kused[i]) hipEventElapsedTime(&ms, s->kev[2 * i], s->kev[2 * i + 1]);
-            s->stats.kernel_ms[i] = ms;
-        }
-    }
+    collect_timing(s);
     s->have = true;
+    s->stats_ok = true;
     return EC_OK;
 }
 
@@ -714,8 +727,8 @@ int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const
 
 int ec_get_stats(ec_session *s, ec_stats *out) {
     if (!s || !out) return EC_ERR_ARG;
-    if (!s->have) {
-        set_error("no successful assembly in this session");
+    if (!s->stats_ok) {
+        set_error("no successful call in this session");
         return EC_ERR_STATE;
     }
     *out = s->stats;
@@ -795,6 +808,8 @@ int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offs
     SolidIndex sidx{};
     EC_CHECK(phase_count(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, flags, U, sidx));
     s->n_dense = U;
+    collect_timing(s);
+    s->stats_ok = true;
     return EC_OK;
 }
 
@@ -841,6 +856,8 @@ int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int 
     SolidIndex sidx{};
     EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx));
     s->n_dense = U;
+    collect_timing(s);
+    s->stats_ok = true;
     return EC_OK;
 }
 

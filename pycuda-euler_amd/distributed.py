@@ -145,9 +145,12 @@ class TorchComm:
 
 
 # ---- the orchestration -----------------------------------------------------------------------
-def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0):
-    """Run steps 1-4 for this rank; returns (result, n_positions_total)."""
+def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None):
+    """Run steps 1-4 for this rank; returns (result, n_positions_total).  on_count(stats)
+    receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING)."""
     st = engine.count_shard(d_reads, d_off, nreads, read_base, k, flags)
+    if on_count:
+        on_count(st)
     P = comm.allreduce_sum(st.n_positions)
     recs, counts = engine.export_by_owner(comm.world)
     received = comm.alltoallv(recs, [c * REC_BYTES for c in counts])
@@ -180,11 +183,16 @@ class ShardedAssembler:
     def run(self, timing=False):
         flags = eulerhip.EC_FLAG_TIMING if timing else 0
         self.result, self.total_positions = sharded_assemble(self.engine, self.comm, self.d_reads, self.d_off,
-                                                             self.nreads, self.read_base, self.k, self.limit, flags)
+                                                             self.nreads, self.read_base, self.k, self.limit, flags,
+                                                             on_count=self._keep)
         return self.result
 
+    def _keep(self, st):
+        self.count_stats = st
+
     def stats(self):
-        return self.engine.stats()
+        """counting-phase statistics of this rank's shard (kernel_ms / stage_ms)"""
+        return self.count_stats
 
 
 def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0):
