@@ -115,6 +115,84 @@ int ec_copy_links(ec_session *s, uint64_t *link_offsets, int64_t *links);
 /* ordered dict of build(): kmers[n_dict*k] chars, counts[n_dict]; needs EC_FLAG_WANT_DICT */
 int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts);
 
+/* ---- layer 2: per-module drop-ins (host buffers, one H2D/D2H round trip per call) ---------
+ * Each restates the INTENDED semantics of the reference PyCUDA function named; the reference's
+ * out-of-bounds and race defects are fixed, flags reproduce them where a caller may
+ * depend on them.  Struct layouts match the reference numpy dtypes (packed):
+ *   EulerVertex {u64 vid; u32 ep, ecount, lp, lcount}   24 B  (src/pydebruijn.py:606)
+ *   EulerEdge   {u64 eid; u32 v1, v2, s, pad}           24 B  (src/pydebruijn.py:604)
+ *   Vertex      {u32 vid, n1, n2}                        12 B  (src/pyeulertour.py:734)
+ *   CircuitEdge {u32 ceid, e1, e2, c1, c2}               20 B  (src/pyeulertour.py:785) */
+#define EC_MOD_TAIL_DROP 1u  /* pygpuhash: floor(n/1024)-block grid drops the tail (src/pygpuhash.py:57-61) */
+#define EC_MOD_REF_BOUNDS 2u /* pydebruijn: setupEdges' `< lmerCount` bounds (src/pydebruijn.py:449)     */
+#define EC_MOD_SWIPE 4u      /* pyeulertour: run the commented-out swipe body (src/pyeulertour.py:539-552) */
+#define EC_HASH_BUCKET_ITEMS 520 /* MAX_BUCKET_ITEM (src/pygpuhash.py:14) */
+
+/* E1 encode_lmer_device (src/pyencode.py:14-98): out[p] = MSB-first 2-bit code of buf[p..p+L-1]
+ * with the reference table codeF[c & 7] (N and '\n' -> A); bytes past the end read as 0 */
+int ec_encode_lmers(const uint8_t *buf, uint64_t n, uint32_t L, uint64_t *out);
+/* E2 compute_kmer_device (src/pyencode.py:101-159): pk = (x & (mask<<2)) >> 2, sk = x & mask */
+int ec_split_kmers(const uint64_t *lmers, uint64_t n, uint64_t mask, uint64_t *pk, uint64_t *sk);
+/* E3 compute_lmer_complement_device, intended (src/pyencode.py:162-232): sum codeR(c[p+i]) << 2i */
+int ec_encode_lmers_rc(const uint8_t *buf, uint64_t n, uint32_t L, uint64_t *out);
+/* H1-H5 create_hash_table_device (src/pygpuhash.py:261-314): nb = 0 -> n/409+1 buckets;
+ * TK[nb*520], TV[nb*520] (bucket b, rank within the bucket), bucket_size[nb] */
+uint32_t ec_hash_bucket_count(uint64_t n);
+int ec_hash_build(const uint64_t *keys, const uint32_t *vals, uint64_t n, uint32_t nb, unsigned flags, uint64_t *TK,
+                  uint32_t *TV, uint32_t *bucket_size);
+/* H6 getHashValue (src/pydebruijn.py:56-87): out[i] = TV of keys[i] or 0xFFFFFFFF */
+int ec_hash_lookup(const uint64_t *TK, const uint32_t *TV, const uint32_t *bucket_size, uint32_t nb,
+                   const uint64_t *keys, uint64_t n, uint32_t *out);
+/* G1-G5 construct_debruijn_graph_device (src/pydebruijn.py:515-619): ev[nk] EulerVertex,
+ * ee/l/e[E] with E = sum(lmer_values) (*edge_count; ee_out = NULL -> sizing only) */
+int ec_debruijn_build(const uint64_t *lmer_keys, const uint32_t *lmer_values, uint64_t nl, const uint64_t *kmer_keys,
+                      uint64_t nk, uint32_t l, const uint64_t *TK, const uint32_t *TV, const uint32_t *bucket_size,
+                      uint32_t nb, unsigned flags, void *ev_out, void *ee_out, uint32_t *l_out, uint32_t *e_out,
+                      uint64_t *edge_count);
+/* C1 find_component_device (src/pycomponent.py:668-723): D[i] = smallest vertex of i's
+ * component over edges i-n1, i-n2 (fixpoint; the reference stops after one iteration) */
+int ec_components(const void *vertices, uint64_t n, uint32_t *D);
+/* T1-T3 findEulerDevice (src/pyeulertour.py:714-792): successors written into ee (in place),
+ * circuit-graph edges (CircuitEdge[E] capacity, unsorted) and their / the circuit counts */
+int ec_find_euler(const void *ev, uint64_t vcount, const uint32_t *l, const uint32_t *e, void *ee, uint64_t E,
+                  void *cg_edges, uint64_t *cg_edge_count, uint32_t *cg_vertex_count);
+/* T5 executeSwipeDevice (src/pyeulertour.py:656-664): mark (all ones, :659) + tree marks;
+ * the swipe itself only with EC_MOD_SWIPE (a no-op in the reference) */
+int ec_execute_swipe(const void *ev, uint64_t vcount, const uint32_t *e, void *ee, uint64_t E, const void *cg_edges,
+                     uint64_t cg_edge_count, const uint32_t *tree, uint64_t tree_count, unsigned flags,
+                     uint32_t *mark_out);
+/* T6 identify_contig_start (src/pyeulertour.py:667-706): contig_start[ee[i].s] = 0 for s < E */
+int ec_identify_contig_start(const void *ee, uint64_t E, uint32_t *contig_start);
+
+/* step-level drop-ins for the reference's intermediate module functions */
+/* phase1_device (src/pygpuhash.py:18-73): offset[i] = position of key i among the keys of its
+ * bucket in input order (the reference's atomicInc order is arbitrary), bucket_size[nb] */
+int ec_hash_phase1(const uint64_t *keys, uint64_t n, uint32_t nb, unsigned flags, uint32_t *offset,
+                   uint32_t *bucket_size);
+/* copy_to_bucket_device (src/pygpuhash.py:76-170): buf[start[bucket] + offset[i]] = key/value */
+int ec_hash_copy_to_bucket(const uint64_t *keys, const uint32_t *vals, const uint32_t *offset, uint64_t n,
+                           const uint32_t *start, uint32_t nb, uint64_t *buf_k, uint32_t *buf_v, uint64_t buf_len);
+/* bucket_sort_device (src/pygpuhash.py:173-258): per-bucket rank sort into TK/TV[nb*520] */
+int ec_hash_bucket_sort(const uint64_t *buf_k, const uint32_t *buf_v, uint64_t buf_len, const uint32_t *start,
+                        const uint32_t *bucket_size, uint32_t nb, uint64_t *TK, uint32_t *TV);
+/* debruijn_count_device (src/pydebruijn.py:15-178): lcount/ecount[size = 4V], updated in place */
+int ec_db_counts(const uint64_t *lmer_keys, const uint32_t *lmer_values, uint64_t nl, uint32_t l, const uint64_t *TK,
+                 const uint32_t *TV, const uint32_t *bucket_size, uint32_t nb, uint64_t size, uint32_t *lcount,
+                 uint32_t *ecount);
+/* setup_vertices_device (src/pydebruijn.py:181-324): ev[nk] updated in place */
+int ec_db_vertices(const uint64_t *kmer_keys, uint64_t nk, const uint64_t *TK, const uint32_t *TV,
+                   const uint32_t *bucket_size, uint32_t nb, const uint32_t *lcount, const uint32_t *lstart,
+                   const uint32_t *ecount, const uint32_t *estart, void *ev);
+/* setup_edges_device (src/pydebruijn.py:326-512): ee / l_out / e_out[E] updated in place */
+int ec_db_edges(const uint64_t *lmer_keys, const uint32_t *lmer_values, const uint32_t *lmer_offsets, uint64_t nl,
+                uint32_t l, const uint64_t *TK, const uint32_t *TV, const uint32_t *bucket_size, uint32_t nb,
+                uint64_t nk, const uint32_t *lstart, const uint32_t *estart, unsigned flags, void *ee, uint32_t *l_out,
+                uint32_t *e_out, uint64_t E);
+/* assign_successor_device (src/pyeulertour.py:17-107): ee[e[ep+i]].s = l[lp+i] (in place) */
+int ec_assign_successor(const void *ev, uint64_t vcount, const uint32_t *l, const uint32_t *e, void *ee, uint64_t E);
+/* construct_successor_graphP1/P2_device (src/pyeulertour.py:109-216): Vertex{eid, s, pred} */
+int ec_successor_graph(const void *ee, uint64_t E, void *vertices);
+
 /* ---- read-sharded multi-GPU building blocks (pycuda-euler_amd/distributed.py) ------------
  * Replace the reference's distribution layer (Spark mapPartitions of assemble2,
  * src/cli_spark_gpu.py:37, and the reduceByKey k-mer shuffle of src/ref_spark.py:83-84) with

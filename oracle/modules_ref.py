@@ -1,0 +1,270 @@
+"""oracle/modules_ref.py -- TEST INFRASTRUCTURE ONLY.
+
+numpy / pure-Python restatement of the INTENDED semantics of the reference's per-module PyCUDA
+kernels (the rows E1-E3, H1-H6, G1-G4, C1, T1-T3, T5, T6 of SURVEY §8a), written from the
+kernel sources' behaviour.  Each function cites the reference lines it restates.  Pinned by
+the known answers in tests/golden/kat.json (SURVEY §8a E1 values; hash_h values; the bucket
+layout of the reference's own dump src/hash_tk.txt) -- see tests/test_modules_oracle.py.
+The product (pycuda-euler_amd/) never imports this module.
+"""
+import numpy as np
+
+CODE_F = [0, 0, 0, 1, 3, 0, 0, 2]  # src/pyencode.py:40 codeF
+CODE_R = [0, 3, 0, 2, 0, 0, 0, 1]  # src/pyencode.py:41 codeR
+M64 = (1 << 64) - 1
+BUCKET_ITEMS = 520                 # src/pygpuhash.py:14
+
+
+def encode_lmers(buf, L):
+    """E1 encodeLmerDevice (src/pyencode.py:43-74): MSB-first codeF of buf[p..p+L-1]; 0 past end."""
+    b = bytes(buf)
+    n = len(b)
+    out = np.zeros(n, np.uint64)
+    for p in range(n):
+        v = 0
+        for i in range(L):
+            c = b[p + i] if p + i < n else 0
+            v = (v << 2) | CODE_F[c & 7]
+        out[p] = v
+    return out
+
+
+def encode_lmers_rc(buf, L):
+    """E3 encodeLmerComplementDevice, intended (src/pyencode.py:199-203): sum codeR(c[p+i]) << 2i."""
+    b = bytes(buf)
+    n = len(b)
+    out = np.zeros(n, np.uint64)
+    for p in range(n):
+        v = 0
+        for i in range(L):
+            c = b[p + i] if p + i < n else 0
+            v |= CODE_R[c & 7] << (2 * i)
+        out[p] = v
+    return out
+
+
+def split_kmers(lmers, mask):
+    """E2 computeKmerDevice (src/pyencode.py:107-130)."""
+    lm = np.asarray(lmers, np.uint64)
+    m = np.uint64(mask)
+    return (lm & (m << np.uint64(2))) >> np.uint64(2), lm & m
+
+
+def hash_h(key, nb):
+    """src/pygpuhash.py:32-35"""
+    return (((0x01010101 + 0x12345678 * int(key)) & M64) % 1900813) % nb
+
+
+def bucket_count(n):
+    return n // 409 + 1  # src/pygpuhash.py:273
+
+
+def hash_build(keys, vals, nb=0, tail_drop=False):
+    """H1-H5 phase1 / scan / copyToBucket / bucketSort (src/pygpuhash.py:36-231, 261-314)."""
+    keys = [int(k) for k in keys]
+    n = len(keys)
+    nb = nb or bucket_count(n)
+    used = (n // 1024) * 1024 if tail_drop and n >= 1024 else n
+    TK = np.zeros(nb * BUCKET_ITEMS, np.uint64)
+    TV = np.zeros(nb * BUCKET_ITEMS, np.uint32)
+    size = np.zeros(nb, np.uint32)
+    kk = np.array(keys[:used], dtype=np.uint64)
+    hb = np.array([hash_h(x, nb) for x in keys[:used]], dtype=np.int64)
+    for b in range(nb):
+        idx = np.nonzero(hb == b)[0]  # input order
+        size[b] = len(idx)
+        ks = np.sort(kk[idx])
+        rank = np.searchsorted(ks, kk[idx], side="left")  # #{bucket keys < key}
+        for i, r in zip(idx, rank):  # a later input index wins a tie
+            TK[b * BUCKET_ITEMS + r] = kk[i]
+            TV[b * BUCKET_ITEMS + r] = vals[i]
+    return TK, TV, size, nb
+
+
+def hash_lookup(TK, TV, size, nb, key):
+    """H6 getHashValue (src/pydebruijn.py:56-87)."""
+    b = hash_h(key, nb)
+    row = TK[b * BUCKET_ITEMS:b * BUCKET_ITEMS + int(size[b])]
+    i = int(np.searchsorted(row, np.uint64(key)))
+    if i < len(row) and int(row[i]) == int(key):
+        return int(TV[b * BUCKET_ITEMS + i])
+    return 0xFFFFFFFF
+
+
+EV = np.dtype([("vid", "<u8"), ("ep", "<u4"), ("ecount", "<u4"), ("lp", "<u4"), ("lcount", "<u4")])
+EE = np.dtype([("eid", "<u8"), ("v1", "<u4"), ("v2", "<u4"), ("s", "<u4"), ("pad", "<u4")])
+VTX = np.dtype([("vid", "<u4"), ("n1", "<u4"), ("n2", "<u4")])
+CE = np.dtype([("ceid", "<u4"), ("e1", "<u4"), ("e2", "<u4"), ("c1", "<u4"), ("c2", "<u4")])
+
+
+def debruijn(lmer_keys, lmer_values, kmer_keys, l, table, ref_bounds=False):
+    """G1-G4 debruijnCount / scans / setupVertices / setupEdges (src/pydebruijn.py:89-145,
+    259-295, 403-477, 515-619) with fixed bounds (4V) unless ref_bounds."""
+    TK, TV, size, nb = table
+    mask = (1 << (2 * (l - 1))) - 1
+    nl, nk = len(lmer_keys), len(kmer_keys)
+    V4 = 4 * nk
+    lc = np.zeros(V4, np.int64)
+    ec = np.zeros(V4, np.int64)
+    geo = []
+    for i in range(nl):
+        x = int(lmer_keys[i])
+        pre, suf = (x & (mask << 2)) >> 2, x & mask
+        pi, si = hash_lookup(TK, TV, size, nb, pre), hash_lookup(TK, TV, size, nb, suf)
+        to = ((pi << 2) & 0xFFFFFFFF) + (x & 3)
+        fr = ((si << 2) & 0xFFFFFFFF) + ((x >> (2 * (l - 1))) & 3)
+        geo.append((pi, si, to, fr))
+        if to < V4:
+            lc[to] = lmer_values[i]
+        if fr < V4:
+            ec[fr] = lmer_values[i]
+    ls = np.concatenate([[0], np.cumsum(lc)[:-1]]) if V4 else lc
+    es = np.concatenate([[0], np.cumsum(ec)[:-1]]) if V4 else ec
+    lv = np.asarray(lmer_values, np.int64)
+    lo = np.concatenate([[0], np.cumsum(lv)[:-1]]) if nl else lv
+    E = int(lv.sum()) if nl else 0
+    ev = np.zeros(nk, EV)
+    for key in kmer_keys:
+        i = hash_lookup(TK, TV, size, nb, int(key))
+        if i < nk:
+            q = 4 * i
+            ev[i] = (int(key), es[q], ec[q:q + 4].sum(), ls[q], lc[q:q + 4].sum())
+    ee = np.zeros(E, EE)
+    L = np.zeros(E, np.uint32)
+    Ee = np.zeros(E, np.uint32)
+    bound = min(nl, V4) if ref_bounds else V4
+    for i in range(nl):
+        pi, si, to, fr = geo[i]
+        if not (to < bound and fr < bound):
+            continue
+        lo_, eo, off = int(ls[to]), int(es[fr]), int(lo[i])
+        if ref_bounds and off >= nl:
+            continue
+        for _ in range(int(lmer_values[i])):
+            if off >= E:
+                break
+            ee[off] = (off, pi, si, E, 0)
+            if lo_ < E:
+                L[lo_] = off
+            if eo < E:
+                Ee[eo] = off
+            lo_ += 1
+            eo += 1
+            off += 1
+    return ev, ee, L, Ee, E
+
+
+def components(vtx):
+    """C1 intended fixpoint (src/pycomponent.py:668-723): smallest vertex of the component."""
+    n = len(vtx)
+    parent = list(range(n))
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    for i in range(n):
+        for nb in (int(vtx[i]["n1"]), int(vtx[i]["n2"])):
+            if nb < n:
+                a, b = find(i), find(nb)
+                if a != b:
+                    parent[max(a, b)] = min(a, b)
+    return np.array([find(i) for i in range(n)], np.uint32)
+
+
+def find_euler(ev, l, e, ee):
+    """T1-T3 findEulerDevice (src/pyeulertour.py:53-83, 133-199, 223-469, 714-792)."""
+    ee = ee.copy()
+    E = len(ee)
+    for v in ev:
+        for i in range(min(int(v["ecount"]), int(v["lcount"]))):
+            ei, li = int(v["ep"]) + i, int(v["lp"]) + i
+            if ei < E:
+                x = int(e[ei])
+                if li < E and x < E:
+                    ee[x]["s"] = l[li]
+    vtx = np.zeros(E, VTX)
+    vtx["vid"] = ee["eid"].astype(np.uint32)
+    vtx["n1"] = ee["s"]
+    vtx["n2"] = E
+    for i in range(E):
+        if vtx[i]["n1"] < E:
+            vtx[int(vtx[i]["n1"])]["n2"] = vtx[i]["vid"]
+    D = components(vtx) if E else np.zeros(0, np.uint32)
+    C = np.zeros(E, np.uint32)
+    C[D] = 1
+    mp = np.concatenate([[0], np.cumsum(C)[:-1]]).astype(np.uint32) if E else C
+    cgV = int(mp[-1] + C[-1]) if E else 0
+    edges = []
+    if cgV > 1:
+        for v in ev:
+            if int(v["ecount"]) == 0:
+                continue
+            mx = int(v["ep"]) + int(v["ecount"]) - 1
+            idx = int(v["ep"])
+            while idx < mx and idx + 1 < E:
+                if int(e[idx]) < E and int(e[idx + 1]) < E:
+                    c1, c2 = int(mp[D[e[idx]]]), int(mp[D[e[idx + 1]]])
+                    if c1 != c2:
+                        edges.append((0, int(e[idx]), int(e[idx + 1]), min(c1, c2), max(c1, c2)))
+                idx += 1
+    cg = np.array(edges, CE) if edges else np.zeros(0, CE)
+    cg.sort(order=["c1", "c2"])
+    return ee, cg, cgV
+
+
+def contig_start(ee):
+    """T6 identifyContigStart (src/pyeulertour.py:680-688)."""
+    E = len(ee)
+    cs = np.ones(E, np.uint32)
+    for s in ee["s"]:
+        if s < E:
+            cs[s] = 0
+    return cs
+
+
+def mark_spanning(cg, tree, E):
+    """T5 markSpanningEulerEdges (src/pyeulertour.py:613-632): mark starts all ones (:659);
+    tree holds circuit-graph EDGE indices."""
+    mark = np.ones(E, np.uint32)
+    for t in tree:
+        c = cg[int(t)]
+        m = min(int(c["e1"]), int(c["e2"]))
+        if m < E:
+            mark[m] = 1
+    return mark
+
+
+def swipe(ev, e, ee, mark):
+    """T5 executeSwipe, the body the reference comments out (src/pyeulertour.py:539-552)."""
+    ee = ee.copy()
+    E = len(ee)
+    for v in ev:
+        if int(v["ecount"]) == 0:
+            continue
+        index = int(v["ep"])
+        mx = index + int(v["ecount"]) - 1
+        if mx >= E:
+            continue
+        if mark[int(ee[int(e[index])]["eid"])] == 1:
+            t0, s = index, int(ee[int(e[index])]["s"])
+            while mark[int(ee[int(e[index])]["eid"])] == 1 and index < mx:
+                ee[int(e[index])]["s"] = ee[int(e[index + 1])]["s"]
+                index += 1
+            if t0 != index:
+                ee[int(e[index])]["s"] = s
+    return ee
+
+
+def lmer_table(buf, l):
+    """H0 host dedup of readLmersKmersCuda (src/eulercuda.py:73-179) as the modular pipeline
+    feeds it: distinct l-mer codes of the whole buffer with their counts (ascending), the
+    distinct (l-1)-mer prefix/suffix codes (ascending)."""
+    lm = encode_lmers(buf, l)
+    keys, counts = np.unique(lm, return_counts=True)
+    mask = (1 << (2 * (l - 1))) - 1
+    pre, suf = split_kmers(keys, mask)
+    kmers = np.unique(np.concatenate([pre, suf]))
+    return keys, counts.astype(np.uint32), kmers

@@ -1,0 +1,1079 @@
+// modules.hip -- per-module drop-ins for the reference's PyCUDA module functions (layer 2 of
+// include/eulerhip.h).  Host buffers in / out, like the reference's drv.In / .get() round
+// trips; every kernel restates the INTENDED semantics of the reference kernel it replaces
+// (file:line cited), with the reference's out-of-bounds / race defects fixed and,
+// where a caller may depend on it, a flag that reproduces the reference's behaviour.
+#include "common.h"
+
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <vector>
+
+namespace ec {
+
+// reference codeF / codeR tables (src/pyencode.py:40-41), indexed by (c & 7)
+__device__ inline uint32_t codeF(uint32_t c) { return (0x20031000u >> ((c & 7u) * 4)) & 0xFu; }
+__device__ inline uint32_t codeR(uint32_t c) { return (0x10002030u >> ((c & 7u) * 4)) & 0xFu; }
+
+// ---- E1 encodeLmerDevice (src/pyencode.py:43-74) --------------------------------------------
+// lmer[p] = sum_i codeF(buf[p+i]) << 2(L-1-i): the first L bases of buf[p..], MSB first.
+// Bytes past the end of the buffer read as 0 (the reference reads past the end).
+__global__ void __launch_bounds__(256) k_encode_lmer(const uint8_t *buf, uint64_t n, uint32_t L, int rc,
+                                                     unsigned long long *out) {
+    __shared__ uint8_t tile[256 + 32];
+    for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < n; b0 += (uint64_t)gridDim.x * 256) {
+        __syncthreads();
+        for (unsigned i = threadIdx.x; i < 256 + 32; i += blockDim.x) tile[i] = (b0 + i < n) ? buf[b0 + i] : 0;
+        __syncthreads();
+        const uint64_t p = b0 + threadIdx.x;
+        if (p < n) {
+            unsigned long long v = 0;
+            if (!rc) {
+                for (uint32_t i = 0; i < L; i++) v = (v << 2) | codeF(tile[threadIdx.x + i]);
+            } else {  // encodeLmerComplementDevice intended (:199-203): sum codeR(c[p+i]) << 2i
+                for (uint32_t i = 0; i < L; i++) v |= (unsigned long long)codeR(tile[threadIdx.x + i]) << (2 * i);
+            }
+            out[p] = v;
+        }
+    }
+}
+
+// ---- E2 computeKmerDevice (src/pyencode.py:107-133) ------------------------------------------
+__global__ void __launch_bounds__(256) k_split(const unsigned long long *lmers, uint64_t n, unsigned long long mask,
+                                               unsigned long long *pk, unsigned long long *sk) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long l = lmers[t];
+        pk[t] = (l & (mask << 2)) >> 2;  // LMER_PREFIX
+        sk[t] = l & mask;                // LMER_SUFFIX
+    }
+}
+
+// ---- H1-H6 bucketed static hash (src/pygpuhash.py, src/pydebruijn.py:56-87) ------------------
+constexpr uint32_t BUCKET_ITEMS = 520;  // MAX_BUCKET_ITEM (src/pygpuhash.py:14)
+
+__host__ __device__ inline uint32_t hash_h(unsigned long long key, uint32_t nb) {
+    return (uint32_t)(((0x01010101ull + 0x12345678ull * key) % 1900813ull) % nb);  // :32-35
+}
+
+// phase1 (:36-51): per-bucket counts
+__global__ void __launch_bounds__(256) k_hash_count(const unsigned long long *keys, uint64_t n, uint32_t nb,
+                                                    unsigned int *bsize) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        atomicAdd(&bsize[hash_h(keys[t], nb)], 1u);
+}
+
+// copyToBucket (:94-126): scatter (key, input index) to the bucket's staging range
+__global__ void __launch_bounds__(256) k_hash_scatter(const unsigned long long *keys, uint64_t n, uint32_t nb,
+                                                      const unsigned long long *start, unsigned int *cursor,
+                                                      unsigned long long *bk, unsigned int *bi) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = hash_h(keys[t], nb);
+        const unsigned long long p = start[b] + atomicAdd(&cursor[b], 1u);
+        bk[p] = keys[t];
+        bi[p] = (unsigned int)t;
+    }
+}
+
+// bucketSort (:186-231): TK[b*520 + rank] with rank = #{keys of the bucket < key}.  Equal
+// keys share a rank as in the reference; the highest input index then wins (deterministic).
+__global__ void __launch_bounds__(256) k_hash_bucket_sort(const unsigned long long *bk, const unsigned int *bi,
+                                                          const unsigned long long *start, const unsigned int *bsize,
+                                                          const unsigned int *vals, unsigned long long *TK,
+                                                          unsigned int *TV) {
+    __shared__ unsigned long long keys[BUCKET_ITEMS];
+    __shared__ unsigned int idx[BUCKET_ITEMS];
+    __shared__ unsigned int win[BUCKET_ITEMS];
+    const uint32_t b = blockIdx.x;
+    const unsigned int s = bsize[b];
+    const unsigned long long o = start[b];
+    for (unsigned i = threadIdx.x; i < s; i += blockDim.x) {
+        keys[i] = bk[o + i];
+        idx[i] = bi[o + i];
+        win[i] = 0;
+    }
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < s; i += blockDim.x) {
+        unsigned int rank = 0;
+        for (unsigned j = 0; j < s; j++) rank += keys[j] < keys[i];
+        atomicMax(&win[rank], idx[i] + 1);
+    }
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < s; i += blockDim.x) {
+        unsigned int rank = 0;
+        for (unsigned j = 0; j < s; j++) rank += keys[j] < keys[i];
+        if (win[rank] == idx[i] + 1) {
+            TK[(uint64_t)b * BUCKET_ITEMS + rank] = keys[i];
+            TV[(uint64_t)b * BUCKET_ITEMS + rank] = vals[idx[i]];
+        }
+    }
+}
+
+// phase1 offsets, deterministic: position of the key among the keys of its bucket in input
+// order (the reference's atomicInc order is arbitrary); bi = input indices sorted stably by bucket
+__global__ void __launch_bounds__(256) k_hash_offsets(const unsigned int *sorted_idx, const unsigned int *sorted_b,
+                                                      uint64_t n, const unsigned long long *start,
+                                                      unsigned int *offset) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        offset[sorted_idx[t]] = (unsigned int)(t - start[sorted_b[t]]);
+}
+
+__global__ void __launch_bounds__(256) k_hash_bucket_ids(const unsigned long long *keys, uint64_t n, uint32_t nb,
+                                                         unsigned int *b, unsigned int *idx) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        b[t] = hash_h(keys[t], nb);
+        idx[t] = (unsigned int)t;
+    }
+}
+
+// copyToBucket with given offsets (:94-126)
+__global__ void __launch_bounds__(256) k_hash_copy(const unsigned long long *keys, const unsigned int *vals,
+                                                   const unsigned int *offset, uint64_t n, uint32_t nb,
+                                                   const unsigned int *start, unsigned long long *bk, unsigned int *bv) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = (uint64_t)start[hash_h(keys[t], nb)] + offset[t];
+        bk[p] = keys[t];
+        bv[p] = vals[t];
+    }
+}
+
+// getHashValue (src/pydebruijn.py:56-87): binary search in the key's bucket; miss = 0xFFFFFFFF
+__device__ inline unsigned int hash_get(unsigned long long key, const unsigned long long *TK, const unsigned int *TV,
+                                        const unsigned int *bsize, uint32_t nb) {
+    const uint32_t b = hash_h(key, nb);
+    unsigned int lo = 0, hi = bsize[b];
+    const unsigned long long *row = TK + (uint64_t)b * BUCKET_ITEMS;
+    while (lo < hi) {
+        const unsigned int mid = lo + (hi - lo) / 2;
+        if (row[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < bsize[b] && row[lo] == key) ? TV[(uint64_t)b * BUCKET_ITEMS + lo] : NONE32;
+}
+
+__global__ void __launch_bounds__(256) k_hash_lookup(const unsigned long long *TK, const unsigned int *TV,
+                                                     const unsigned int *bsize, uint32_t nb,
+                                                     const unsigned long long *keys, uint64_t n, unsigned int *out) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        out[t] = hash_get(keys[t], TK, TV, bsize, nb);
+}
+
+// ---- G1-G4 de Bruijn graph (src/pydebruijn.py) -------------------------------------------
+struct EulerVertex {  // src/pydebruijn.py:196-202 (24 B, packed like the numpy dtype)
+    unsigned long long vid;
+    unsigned int ep, ecount, lp, lcount;
+};
+struct EulerEdge {  // src/pydebruijn.py:344-350 (24 B)
+    unsigned long long eid;
+    unsigned int v1, v2, s, pad;
+};
+static_assert(sizeof(EulerVertex) == 24 && sizeof(EulerEdge) == 24, "euler structs");
+
+struct HashView {
+    const unsigned long long *TK;
+    const unsigned int *TV, *bsize;
+    uint32_t nb;
+    __device__ inline unsigned int get(unsigned long long k) const { return hash_get(k, TK, TV, bsize, nb); }
+};
+
+// per l-mer: prefix / suffix vertex, first / last base (debruijnCount :89-145)
+__device__ inline void lmer_geometry(unsigned long long lmer, unsigned long long mask, const HashView &h,
+                                     unsigned int &pi, unsigned int &si, uint64_t &to, uint64_t &from) {
+    const unsigned long long prefix = (lmer & (mask << 2)) >> 2;
+    const unsigned long long suffix = lmer & mask;
+    pi = h.get(prefix);
+    si = h.get(suffix);
+    const unsigned long long tTo = lmer & 3ull;
+    const unsigned long long tFrom = (lmer >> __popcll(mask)) & 3ull;
+    // the reference forms (prefixIndex << 2) in 32 bits: a miss (0xFFFFFFFF) lands far out
+    to = (uint64_t)((pi << 2) & 0xFFFFFFFFu) + tTo;
+    from = (uint64_t)((si << 2) & 0xFFFFFFFFu) + tFrom;
+}
+
+__global__ void __launch_bounds__(256) k_db_count(const unsigned long long *lk, const unsigned int *lv, uint64_t nl,
+                                                  HashView h, unsigned long long mask, uint64_t size,
+                                                  unsigned int *lcount, unsigned int *ecount) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nl; t += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned int pi, si;
+        uint64_t to, from;
+        lmer_geometry(lk[t], mask, h, pi, si, to, from);
+        if (to < size) lcount[to] = lv[t];
+        if (from < size) ecount[from] = lv[t];
+    }
+}
+
+// setupVertices (:259-295)
+__global__ void __launch_bounds__(256) k_db_vertices(const unsigned long long *kk, uint64_t nk, HashView h,
+                                                     const unsigned int *lcount, const unsigned int *lstart,
+                                                     const unsigned int *ecount, const unsigned int *estart,
+                                                     EulerVertex *ev) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nk; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long key = kk[t];
+        const unsigned int i = h.get(key);
+        if (i < nk) {
+            const uint64_t q = 4ull * i;
+            EulerVertex v;
+            v.vid = key;
+            v.lp = lstart[q];
+            v.lcount = lcount[q] + lcount[q + 1] + lcount[q + 2] + lcount[q + 3];
+            v.ep = estart[q];
+            v.ecount = ecount[q] + ecount[q + 1] + ecount[q + 2] + ecount[q + 3];
+            ev[i] = v;
+        }
+    }
+}
+
+// setupEdges (:403-477).  Fixed bounds: the vertex slots are checked against 4V (the
+// reference compares with lmerCount, :449, dropping most edges; EC_MOD_REF_BOUNDS
+// reproduces that) and edges are written up to E = sum of multiplicities.
+__global__ void __launch_bounds__(256) k_db_edges(const unsigned long long *lk, const unsigned int *lv,
+                                                  const unsigned int *loffs, uint64_t nl, HashView h,
+                                                  unsigned long long mask, uint64_t size, uint64_t E, int refb,
+                                                  const unsigned int *lstart, const unsigned int *estart,
+                                                  unsigned int *l, unsigned int *e, EulerEdge *ee) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nl; t += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned int pi, si;
+        uint64_t to, from;
+        lmer_geometry(lk[t], mask, h, pi, si, to, from);
+        const uint64_t bound = refb ? (nl < size ? nl : size) : size;  // never past lstart/estart
+        if (!(to < bound && from < bound)) continue;
+        unsigned int lo = lstart[to], eo = estart[from], off = loffs[t];
+        if (refb && off >= nl) continue;
+        for (unsigned int j = 0; j < lv[t]; j++) {
+            if (off >= E) break;
+            EulerEdge x;
+            x.eid = off;
+            x.v1 = pi;
+            x.v2 = si;
+            x.s = (unsigned int)E;
+            x.pad = 0;
+            ee[off] = x;
+            if (lo < E) l[lo] = off;
+            if (eo < E) e[eo] = off;
+            lo++;
+            eo++;
+            off++;
+        }
+    }
+}
+
+// ---- C1 connected components (src/pycomponent.py:668-723) --------------------------------
+// Vertex{vid, n1, n2}; edges i-n1, i-n2 for neighbours < n.  Fixpoint of min-label hooking +
+// pointer jumping: D[i] = the smallest vertex index of i's component (the reference stops
+// after one Shiloach-Vishkin iteration, :716).
+struct Vtx {
+    unsigned int vid, n1, n2;
+};
+
+__global__ void __launch_bounds__(256) k_cc_init(unsigned int *D, uint64_t n) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        D[t] = (unsigned int)t;
+}
+
+__device__ inline unsigned int cc_find(const unsigned int *D, unsigned int x) {
+    unsigned int p = D[x];
+    while (true) {
+        const unsigned int q = D[p];
+        if (q == p) return p;
+        p = q;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cc_hook(const Vtx *v, uint64_t n, unsigned int *D, unsigned int *changed) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int nb[2] = {v[t].n1, v[t].n2};
+        for (int q = 0; q < 2; q++) {
+            if (nb[q] >= n) continue;
+            unsigned int a = cc_find(D, (unsigned int)t), b = cc_find(D, nb[q]);
+            while (a != b) {  // lock-free union: link the larger root under the smaller
+                const unsigned int hi = a > b ? a : b, lo = a < b ? a : b;
+                if (atomicCAS(&D[hi], hi, lo) == hi) {
+                    *changed = 1;
+                    break;
+                }
+                a = cc_find(D, hi);
+                b = cc_find(D, lo);
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cc_compress(unsigned int *D, uint64_t n) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        D[t] = cc_find(D, D[t]);
+}
+
+// ---- T1-T3 Euler tour machinery (src/pyeulertour.py) -----------------------------------------
+// assignSuccessor (:53-83)
+__global__ void __launch_bounds__(256) k_assign_successor(const EulerVertex *ev, uint64_t vcount, const unsigned int *l,
+                                                          const unsigned int *e, EulerEdge *ee, uint64_t E) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < vcount; t += (uint64_t)gridDim.x * blockDim.x) {
+        const EulerVertex v = ev[t];
+        for (unsigned int i = 0; i < v.ecount && i < v.lcount; i++) {
+            const uint64_t ei = (uint64_t)v.ep + i, li = (uint64_t)v.lp + i;
+            if (ei < E) {
+                const unsigned int x = e[ei];
+                if (li < E && x < E) ee[x].s = l[li];
+            }
+        }
+    }
+}
+
+// constructSuccessorGraphP1/P2 (:133-144, :187-199)
+__global__ void __launch_bounds__(256) k_succ_graph1(const EulerEdge *ee, uint64_t E, Vtx *v) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x) {
+        Vtx x;
+        x.vid = (unsigned int)ee[t].eid;
+        x.n1 = ee[t].s;
+        x.n2 = (unsigned int)E;
+        v[t] = x;
+    }
+}
+__global__ void __launch_bounds__(256) k_succ_graph2(Vtx *v, uint64_t E) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x)
+        if (v[t].n1 < E) v[v[t].n1].n2 = v[t].vid;
+}
+
+// calculateCircuitGraphVertexData (:223-231)
+__global__ void __launch_bounds__(256) k_circuit_mark(const unsigned int *D, uint64_t E, unsigned int *C) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x)
+        C[D[t]] = 1;
+}
+
+// calculateCircuitGraphEdgeData (:331-371) / assignCircuitGraphEdgeData (:428-469): adjacent
+// entering edges of a vertex that lie on different circuits form a circuit-graph edge
+struct CircuitEdge {  // :420-427
+    unsigned int ceid, e1, e2, c1, c2;
+};
+
+__global__ void __launch_bounds__(256) k_circuit_edges(const EulerVertex *ev, uint64_t vcount, const unsigned int *e,
+                                                       const unsigned int *D, const unsigned int *map, uint64_t E,
+                                                       unsigned int *slot, CircuitEdge *out) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < vcount; t += (uint64_t)gridDim.x * blockDim.x) {
+        const EulerVertex v = ev[t];
+        if (v.ecount == 0) continue;
+        const uint64_t maxIndex = (uint64_t)v.ep + v.ecount - 1;
+        for (uint64_t index = v.ep; index < maxIndex && index + 1 < E; index++) {
+            if (!(e[index] < E && e[index + 1] < E)) continue;
+            const unsigned int c1 = map[D[e[index]]], c2 = map[D[e[index + 1]]];
+            if (c1 == c2) continue;
+            CircuitEdge x;
+            x.ceid = 0;  // never assigned by the reference kernel
+            x.e1 = e[index];
+            x.e2 = e[index + 1];
+            x.c1 = min(c1, c2);
+            x.c2 = max(c1, c2);
+            // slot order is arbitrary (atomicDec in the reference); callers sort by (c1, c2) (:791)
+            out[atomicAdd(slot, 1u)] = x;
+        }
+    }
+}
+
+// markSpanningEulerEdges (:613-632) and executeSwipe (:518-557)
+__global__ void __launch_bounds__(256) k_mark_spanning(const CircuitEdge *cg, const unsigned int *tree, uint64_t nt,
+                                                       uint64_t E, unsigned int *mark) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nt; t += (uint64_t)gridDim.x * blockDim.x) {
+        const CircuitEdge c = cg[tree[t]];
+        const unsigned int m = min(c.e1, c.e2);
+        if (m < E) mark[m] = 1;
+    }
+}
+
+// the swipe body the reference comments out (:539-552): rotate the successors of a run of
+// marked entering edges of a vertex
+__global__ void __launch_bounds__(256) k_swipe(const EulerVertex *ev, uint64_t vcount, const unsigned int *e,
+                                               EulerEdge *ee, const unsigned int *mark, uint64_t E) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < vcount; t += (uint64_t)gridDim.x * blockDim.x) {
+        const EulerVertex v = ev[t];
+        if (v.ecount == 0) continue;
+        uint64_t index = v.ep;
+        const uint64_t maxIndex = index + v.ecount - 1;
+        if (maxIndex >= E) continue;
+        if (mark[ee[e[index]].eid] == 1) {
+            const uint64_t t0 = index;
+            const unsigned int s = ee[e[index]].s;
+            while (mark[ee[e[index]].eid] == 1 && index < maxIndex) {
+                ee[e[index]].s = ee[e[index + 1]].s;
+                index++;
+            }
+            if (t0 != index) ee[e[index]].s = s;
+        }
+    }
+}
+
+// identifyContigStart (:680-688); contigStart is u32 here (the reference passes u32 to an
+// unsigned char* kernel)
+__global__ void __launch_bounds__(256) k_contig_start(const EulerEdge *ee, uint64_t E, unsigned int *cs) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x)
+        if (ee[t].s < E) cs[ee[t].s] = 0;
+}
+
+// ---- host helpers ---------------------------------------------------------------------------
+struct Dev {
+    void *p = nullptr;
+    explicit Dev(size_t bytes) {
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) p = nullptr;
+    }
+    ~Dev() {
+        if (p) (void)hipFree(p);
+    }
+    template <typename T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+    Dev(const Dev &) = delete;
+};
+
+#define EC_DEV(name, bytes)                                   \
+    Dev name(bytes);                                          \
+    if (!name.p) {                                            \
+        set_error("hipMalloc(%zu) failed", (size_t)(bytes)); \
+        return EC_ERR_NOMEM;                                  \
+    }
+
+int exscan_u32(const unsigned int *in, unsigned int *out, size_t n) {
+    size_t bytes = 0;
+    EC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, n, rocprim::plus<unsigned int>(), (hipStream_t)0));
+    EC_DEV(tmp, bytes);
+    EC_HIP(rocprim::exclusive_scan(tmp.p, bytes, in, out, 0u, n, rocprim::plus<unsigned int>(), (hipStream_t)0));
+    return EC_OK;
+}
+
+int exscan_u64(const unsigned int *in, unsigned long long *out, size_t n) {
+    size_t bytes = 0;
+    EC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0ull, n, rocprim::plus<unsigned long long>(), (hipStream_t)0));
+    EC_DEV(tmp, bytes);
+    EC_HIP(rocprim::exclusive_scan(tmp.p, bytes, in, out, 0ull, n, rocprim::plus<unsigned long long>(), (hipStream_t)0));
+    return EC_OK;
+}
+
+int components_dev(const Vtx *v, uint64_t n, unsigned int *D) {
+    if (!n) return EC_OK;
+    EC_DEV(flag, 4);
+    k_cc_init<<<grid_for(n, 256), 256>>>(D, n);
+    for (int it = 0; it < 64; it++) {
+        EC_HIP(hipMemset(flag.p, 0, 4));
+        k_cc_hook<<<grid_for(n, 256), 256>>>(v, n, D, flag.as<unsigned int>());
+        k_cc_compress<<<grid_for(n, 256), 256>>>(D, n);
+        unsigned int h = 0;
+        EC_HIP(hipMemcpy(&h, flag.p, 4, hipMemcpyDeviceToHost));
+        if (!h) return EC_OK;
+    }
+    set_error("components did not converge");
+    return EC_ERR_STATE;
+}
+
+}  // namespace ec
+
+using namespace ec;
+
+// a user-supplied bucket table must keep every bucket inside its 520 slots (hash_get reads
+// TK[b*520 .. b*520 + size[b]))
+static int check_table(const uint32_t *bucket_size, uint32_t nb) {
+    for (uint32_t b = 0; b < nb; b++)
+        if (bucket_size[b] > BUCKET_ITEMS) {
+            set_error("bucketSize[%u] = %u > MAX_BUCKET_ITEM=520", b, bucket_size[b]);
+            return EC_ERR_ARG;
+        }
+    return EC_OK;
+}
+
+extern "C" {
+
+static int encode_common(const uint8_t *buf, uint64_t n, uint32_t L, uint64_t *out, int rc) {
+    if ((n && (!buf || !out)) || L < 1 || L > 32) {
+        set_error("bad arguments (L=%u must be in [1,32])", L);
+        return EC_ERR_ARG;
+    }
+    if (!n) return EC_OK;
+    EC_DEV(db, n);
+    EC_DEV(dout, n * 8);
+    EC_HIP(hipMemcpy(db.p, buf, n, hipMemcpyHostToDevice));
+    k_encode_lmer<<<grid_for(n, 256, 65535), 256>>>(db.as<uint8_t>(), n, L, rc, dout.as<unsigned long long>());
+    EC_HIP(hipMemcpy(out, dout.p, n * 8, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+int ec_encode_lmers(const uint8_t *buf, uint64_t n, uint32_t L, uint64_t *out) { return encode_common(buf, n, L, out, 0); }
+
+int ec_encode_lmers_rc(const uint8_t *buf, uint64_t n, uint32_t L, uint64_t *out) {
+    return encode_common(buf, n, L, out, 1);
+}
+
+int ec_split_kmers(const uint64_t *lmers, uint64_t n, uint64_t mask, uint64_t *pk, uint64_t *sk) {
+    if (n && (!lmers || !pk || !sk)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!n) return EC_OK;
+    EC_DEV(dl, n * 8);
+    EC_DEV(dp, n * 8);
+    EC_DEV(ds, n * 8);
+    EC_HIP(hipMemcpy(dl.p, lmers, n * 8, hipMemcpyHostToDevice));
+    k_split<<<grid_for(n, 256), 256>>>(dl.as<unsigned long long>(), n, mask, dp.as<unsigned long long>(),
+                                      ds.as<unsigned long long>());
+    EC_HIP(hipMemcpy(pk, dp.p, n * 8, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(sk, ds.p, n * 8, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+uint32_t ec_hash_bucket_count(uint64_t n) { return (uint32_t)(n / 409 + 1); }  // src/pygpuhash.py:273
+
+int ec_hash_build(const uint64_t *keys, const uint32_t *vals, uint64_t n, uint32_t nb, unsigned flags, uint64_t *TK,
+                  uint32_t *TV, uint32_t *bucket_size) {
+    if ((n && (!keys || !vals)) || !TK || !TV || !bucket_size) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!nb) nb = ec_hash_bucket_count(n);
+    // phase1 / copyToBucket launch floor(n/1024) blocks of 1024 threads (:57-61, :143-147)
+    uint64_t used = n;
+    if ((flags & EC_MOD_TAIL_DROP) && n >= 1024) used = (n / 1024) * 1024;
+    const uint64_t slots = (uint64_t)nb * BUCKET_ITEMS;
+    EC_DEV(dk, used * 8);
+    EC_DEV(dv, n * 4);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dcur, nb * 4ull);
+    EC_DEV(dstart, (nb + 1) * 8ull);
+    EC_DEV(dbk, used * 8);
+    EC_DEV(dbi, used * 4);
+    EC_DEV(dTK, slots * 8);
+    EC_DEV(dTV, slots * 4);
+    if (used) EC_HIP(hipMemcpy(dk.p, keys, used * 8, hipMemcpyHostToDevice));
+    if (n) EC_HIP(hipMemcpy(dv.p, vals, n * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemset(dsz.p, 0, nb * 4ull));
+    EC_HIP(hipMemset(dcur.p, 0, nb * 4ull));
+    EC_HIP(hipMemset(dTK.p, 0, slots * 8));
+    EC_HIP(hipMemset(dTV.p, 0, slots * 4));
+    if (used) k_hash_count<<<grid_for(used, 256), 256>>>(dk.as<unsigned long long>(), used, nb, dsz.as<unsigned int>());
+    std::vector<uint32_t> hsz(nb);
+    EC_HIP(hipMemcpy(hsz.data(), dsz.p, nb * 4ull, hipMemcpyDeviceToHost));
+    for (uint32_t b = 0; b < nb; b++)
+        if (hsz[b] > BUCKET_ITEMS) {
+            set_error("bucket %u holds %u keys > MAX_BUCKET_ITEM=520 (the reference would overrun)", b, hsz[b]);
+            return EC_ERR_CAPACITY;
+        }
+    EC_CHECK(exscan_u64(dsz.as<unsigned int>(), dstart.as<unsigned long long>(), nb));
+    if (used) {
+        k_hash_scatter<<<grid_for(used, 256), 256>>>(dk.as<unsigned long long>(), used, nb,
+                                                    dstart.as<unsigned long long>(), dcur.as<unsigned int>(),
+                                                    dbk.as<unsigned long long>(), dbi.as<unsigned int>());
+        k_hash_bucket_sort<<<nb, 256>>>(dbk.as<unsigned long long>(), dbi.as<unsigned int>(),
+                                        dstart.as<unsigned long long>(), dsz.as<unsigned int>(), dv.as<unsigned int>(),
+                                        dTK.as<unsigned long long>(), dTV.as<unsigned int>());
+    }
+    EC_HIP(hipMemcpy(TK, dTK.p, slots * 8, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(TV, dTV.p, slots * 4, hipMemcpyDeviceToHost));
+    memcpy(bucket_size, hsz.data(), nb * 4ull);
+    return EC_OK;
+}
+
+int ec_hash_lookup(const uint64_t *TK, const uint32_t *TV, const uint32_t *bucket_size, uint32_t nb,
+                   const uint64_t *keys, uint64_t n, uint32_t *out) {
+    if (!TK || !TV || !bucket_size || !nb || (n && (!keys || !out))) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(check_table(bucket_size, nb));
+    if (!n) return EC_OK;
+    const uint64_t slots = (uint64_t)nb * BUCKET_ITEMS;
+    EC_DEV(dTK, slots * 8);
+    EC_DEV(dTV, slots * 4);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dk, n * 8);
+    EC_DEV(dout, n * 4);
+    EC_HIP(hipMemcpy(dTK.p, TK, slots * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dTV.p, TV, slots * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dsz.p, bucket_size, nb * 4ull, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dk.p, keys, n * 8, hipMemcpyHostToDevice));
+    k_hash_lookup<<<grid_for(n, 256), 256>>>(dTK.as<unsigned long long>(), dTV.as<unsigned int>(),
+                                            dsz.as<unsigned int>(), nb, dk.as<unsigned long long>(), n,
+                                            dout.as<unsigned int>());
+    EC_HIP(hipMemcpy(out, dout.p, n * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+int ec_debruijn_build(const uint64_t *lmer_keys, const uint32_t *lmer_values, uint64_t nl, const uint64_t *kmer_keys,
+                      uint64_t nk, uint32_t l, const uint64_t *TK, const uint32_t *TV, const uint32_t *bucket_size,
+                      uint32_t nb, unsigned flags, void *ev_out, void *ee_out, uint32_t *l_out, uint32_t *e_out,
+                      uint64_t *edge_count) {
+    if (l < 2 || l > 32 || !TK || !TV || !bucket_size || !nb || !edge_count || (nl && (!lmer_keys || !lmer_values)) ||
+        (nk && (!kmer_keys || !ev_out))) {
+        set_error("bad arguments (l=%u must be in [2,32])", l);
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(check_table(bucket_size, nb));
+    uint64_t E = 0;
+    for (uint64_t i = 0; i < nl; i++) E += lmer_values[i];
+    *edge_count = E;
+    if (!ee_out && E) return EC_OK;  // sizing call
+    const unsigned long long mask = kmask64((int)l - 1);  // valid_bitmask: 2(l-1) ones (:526-529)
+    const uint64_t size = 4 * nk;
+    const uint64_t slots = (uint64_t)nb * BUCKET_ITEMS;
+    EC_DEV(dTK, slots * 8);
+    EC_DEV(dTV, slots * 4);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dlk, nl * 8);
+    EC_DEV(dlv, nl * 4);
+    EC_DEV(dlo, nl * 4);
+    EC_DEV(dkk, nk * 8);
+    EC_DEV(dlc, size * 4);
+    EC_DEV(dec, size * 4);
+    EC_DEV(dls, size * 4);
+    EC_DEV(des, size * 4);
+    EC_DEV(dev, nk * sizeof(EulerVertex));
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_DEV(dl, E * 4);
+    EC_DEV(de, E * 4);
+    EC_HIP(hipMemcpy(dTK.p, TK, slots * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dTV.p, TV, slots * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dsz.p, bucket_size, nb * 4ull, hipMemcpyHostToDevice));
+    if (nl) {
+        EC_HIP(hipMemcpy(dlk.p, lmer_keys, nl * 8, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dlv.p, lmer_values, nl * 4, hipMemcpyHostToDevice));
+    }
+    if (nk) EC_HIP(hipMemcpy(dkk.p, kmer_keys, nk * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemset(dlc.p, 0, std::max<uint64_t>(size, 1) * 4));
+    EC_HIP(hipMemset(dec.p, 0, std::max<uint64_t>(size, 1) * 4));
+    EC_HIP(hipMemset(dev.p, 0, std::max<uint64_t>(nk, 1) * sizeof(EulerVertex)));
+    EC_HIP(hipMemset(dee.p, 0, std::max<uint64_t>(E, 1) * sizeof(EulerEdge)));
+    EC_HIP(hipMemset(dl.p, 0, std::max<uint64_t>(E, 1) * 4));
+    EC_HIP(hipMemset(de.p, 0, std::max<uint64_t>(E, 1) * 4));
+    const HashView h{dTK.as<unsigned long long>(), dTV.as<unsigned int>(), dsz.as<unsigned int>(), nb};
+    if (nl)
+        k_db_count<<<grid_for(nl, 256), 256>>>(dlk.as<unsigned long long>(), dlv.as<unsigned int>(), nl, h, mask, size,
+                                              dlc.as<unsigned int>(), dec.as<unsigned int>());
+    if (size) {
+        EC_CHECK(exscan_u32(dlc.as<unsigned int>(), dls.as<unsigned int>(), size));
+        EC_CHECK(exscan_u32(dec.as<unsigned int>(), des.as<unsigned int>(), size));
+    }
+    if (nl) EC_CHECK(exscan_u32(dlv.as<unsigned int>(), dlo.as<unsigned int>(), nl));
+    if (nk)
+        k_db_vertices<<<grid_for(nk, 256), 256>>>(dkk.as<unsigned long long>(), nk, h, dlc.as<unsigned int>(),
+                                                 dls.as<unsigned int>(), dec.as<unsigned int>(), des.as<unsigned int>(),
+                                                 dev.as<EulerVertex>());
+    if (nl)
+        k_db_edges<<<grid_for(nl, 256), 256>>>(dlk.as<unsigned long long>(), dlv.as<unsigned int>(),
+                                              dlo.as<unsigned int>(), nl, h, mask, size, E,
+                                              (flags & EC_MOD_REF_BOUNDS) ? 1 : 0, dls.as<unsigned int>(),
+                                              des.as<unsigned int>(), dl.as<unsigned int>(), de.as<unsigned int>(),
+                                              dee.as<EulerEdge>());
+    if (nk) EC_HIP(hipMemcpy(ev_out, dev.p, nk * sizeof(EulerVertex), hipMemcpyDeviceToHost));
+    if (E) {
+        EC_HIP(hipMemcpy(ee_out, dee.p, E * sizeof(EulerEdge), hipMemcpyDeviceToHost));
+        if (l_out) EC_HIP(hipMemcpy(l_out, dl.p, E * 4, hipMemcpyDeviceToHost));
+        if (e_out) EC_HIP(hipMemcpy(e_out, de.p, E * 4, hipMemcpyDeviceToHost));
+    }
+    return EC_OK;
+}
+
+int ec_components(const void *vertices, uint64_t n, uint32_t *D) {
+    if (n && (!vertices || !D)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!n) return EC_OK;
+    EC_DEV(dv, n * sizeof(Vtx));
+    EC_DEV(dD, n * 4);
+    EC_HIP(hipMemcpy(dv.p, vertices, n * sizeof(Vtx), hipMemcpyHostToDevice));
+    EC_CHECK(components_dev(dv.as<Vtx>(), n, dD.as<unsigned int>()));
+    EC_HIP(hipMemcpy(D, dD.p, n * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+int ec_find_euler(const void *ev, uint64_t vcount, const uint32_t *l, const uint32_t *e, void *ee, uint64_t E,
+                  void *cg_edges, uint64_t *cg_edge_count, uint32_t *cg_vertex_count) {
+    if (!cg_edge_count || !cg_vertex_count || (vcount && !ev) || (E && (!l || !e || !ee || !cg_edges))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    *cg_edge_count = 0;
+    *cg_vertex_count = 0;
+    if (!E) return EC_OK;
+    EC_DEV(dev, vcount * sizeof(EulerVertex));
+    EC_DEV(dl, E * 4);
+    EC_DEV(de, E * 4);
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_DEV(dv, E * sizeof(Vtx));
+    EC_DEV(dD, E * 4);
+    EC_DEV(dC, E * 4);
+    EC_DEV(dmap, E * 4);
+    EC_DEV(dcnt, E * 4);
+    EC_DEV(dcg, E * sizeof(CircuitEdge));
+    if (vcount) EC_HIP(hipMemcpy(dev.p, ev, vcount * sizeof(EulerVertex), hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dl.p, l, E * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(de.p, e, E * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
+    if (vcount)
+        k_assign_successor<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), vcount, dl.as<unsigned int>(),
+                                                          de.as<unsigned int>(), dee.as<EulerEdge>(), E);
+    k_succ_graph1<<<grid_for(E, 256), 256>>>(dee.as<EulerEdge>(), E, dv.as<Vtx>());
+    k_succ_graph2<<<grid_for(E, 256), 256>>>(dv.as<Vtx>(), E);
+    EC_CHECK(components_dev(dv.as<Vtx>(), E, dD.as<unsigned int>()));
+    EC_HIP(hipMemset(dC.p, 0, E * 4));
+    k_circuit_mark<<<grid_for(E, 256), 256>>>(dD.as<unsigned int>(), E, dC.as<unsigned int>());
+    EC_CHECK(exscan_u32(dC.as<unsigned int>(), dmap.as<unsigned int>(), E));
+    uint32_t last[2];
+    EC_HIP(hipMemcpy(&last[0], dmap.as<unsigned int>() + (E - 1), 4, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(&last[1], dC.as<unsigned int>() + (E - 1), 4, hipMemcpyDeviceToHost));
+    const uint32_t cgV = last[0] + last[1];
+    *cg_vertex_count = cgV;
+    EC_HIP(hipMemcpy(ee, dee.p, E * sizeof(EulerEdge), hipMemcpyDeviceToHost));  // successors, in place
+    if (cgV <= 1 || !vcount) return EC_OK;
+    EC_HIP(hipMemset(dcnt.p, 0, 4));
+    k_circuit_edges<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), vcount, de.as<unsigned int>(),
+                                                   dD.as<unsigned int>(), dmap.as<unsigned int>(), E,
+                                                   dcnt.as<unsigned int>(), dcg.as<CircuitEdge>());
+    uint32_t total = 0;
+    EC_HIP(hipMemcpy(&total, dcnt.p, 4, hipMemcpyDeviceToHost));
+    *cg_edge_count = total;
+    if (total) EC_HIP(hipMemcpy(cg_edges, dcg.p, total * sizeof(CircuitEdge), hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+int ec_execute_swipe(const void *ev, uint64_t vcount, const uint32_t *e, void *ee, uint64_t E, const void *cg_edges,
+                     uint64_t cg_edge_count, const uint32_t *tree, uint64_t tree_count, unsigned flags, uint32_t *mark_out) {
+    if ((E && (!e || !ee)) || (vcount && !ev) || (tree_count && (!tree || !cg_edges))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!E) return EC_OK;
+    const EulerEdge *hee = static_cast<const EulerEdge *>(ee);
+    for (uint64_t i = 0; i < E; i++)
+        if (e[i] >= E || hee[i].eid >= E) {
+            set_error("e[%llu] = %u / ee[%llu].eid out of range (E = %llu)", (unsigned long long)i, e[i],
+                      (unsigned long long)i, (unsigned long long)E);
+            return EC_ERR_ARG;
+        }
+    for (uint64_t i = 0; i < tree_count; i++)
+        if (tree[i] >= cg_edge_count) {
+            set_error("tree[%llu] = %u is not a circuit-graph edge index", (unsigned long long)i, tree[i]);
+            return EC_ERR_ARG;
+        }
+    EC_DEV(dev, vcount * sizeof(EulerVertex));
+    EC_DEV(de, E * 4);
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_DEV(dcg, cg_edge_count * sizeof(CircuitEdge));
+    EC_DEV(dt, tree_count * 4);
+    EC_DEV(dm, E * 4);
+    if (vcount) EC_HIP(hipMemcpy(dev.p, ev, vcount * sizeof(EulerVertex), hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(de.p, e, E * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
+    if (cg_edge_count) EC_HIP(hipMemcpy(dcg.p, cg_edges, cg_edge_count * sizeof(CircuitEdge), hipMemcpyHostToDevice));
+    if (tree_count) EC_HIP(hipMemcpy(dt.p, tree, tree_count * 4, hipMemcpyHostToDevice));
+    // mark starts as all ones (src/pyeulertour.py:659)
+    std::vector<uint32_t> ones(E, 1u);
+    EC_HIP(hipMemcpy(dm.p, ones.data(), E * 4, hipMemcpyHostToDevice));
+    if (tree_count)
+        k_mark_spanning<<<grid_for(tree_count, 256), 256>>>(dcg.as<CircuitEdge>(), dt.as<unsigned int>(), tree_count, E,
+                                                           dm.as<unsigned int>());
+    if ((flags & EC_MOD_SWIPE) && vcount)
+        k_swipe<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), vcount, de.as<unsigned int>(),
+                                               dee.as<EulerEdge>(), dm.as<unsigned int>(), E);
+    EC_HIP(hipMemcpy(ee, dee.p, E * sizeof(EulerEdge), hipMemcpyDeviceToHost));
+    if (mark_out) EC_HIP(hipMemcpy(mark_out, dm.p, E * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+int ec_identify_contig_start(const void *ee, uint64_t E, uint32_t *contig_start) {
+    if (E && (!ee || !contig_start)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!E) return EC_OK;
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_DEV(dcs, E * 4);
+    EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dcs.p, contig_start, E * 4, hipMemcpyHostToDevice));
+    k_contig_start<<<grid_for(E, 256), 256>>>(dee.as<EulerEdge>(), E, dcs.as<unsigned int>());
+    EC_HIP(hipMemcpy(contig_start, dcs.p, E * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+
+// ---- step-level drop-ins (the reference's intermediate module functions) ---------------------
+// phase1_device (src/pygpuhash.py:18-73): per-key offset within its bucket + bucket sizes
+int ec_hash_phase1(const uint64_t *keys, uint64_t n, uint32_t nb, unsigned flags, uint32_t *offset,
+                   uint32_t *bucket_size) {
+    if (!nb || (n && (!keys || !offset)) || !bucket_size) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    uint64_t used = n;
+    if ((flags & EC_MOD_TAIL_DROP) && n >= 1024) used = (n / 1024) * 1024;
+    EC_DEV(dk, used * 8);
+    EC_DEV(db, used * 4);
+    EC_DEV(di, used * 4);
+    EC_DEV(db2, used * 4);
+    EC_DEV(di2, used * 4);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dst, (nb + 1) * 8ull);
+    EC_DEV(doff, used * 4);
+    EC_HIP(hipMemset(dsz.p, 0, nb * 4ull));
+    if (used) {
+        EC_HIP(hipMemcpy(dk.p, keys, used * 8, hipMemcpyHostToDevice));
+        k_hash_count<<<grid_for(used, 256), 256>>>(dk.as<unsigned long long>(), used, nb, dsz.as<unsigned int>());
+        k_hash_bucket_ids<<<grid_for(used, 256), 256>>>(dk.as<unsigned long long>(), used, nb, db.as<unsigned int>(),
+                                                       di.as<unsigned int>());
+        size_t bytes = 0;
+        EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, db.as<unsigned int>(), db2.as<unsigned int>(),
+                                         di.as<unsigned int>(), di2.as<unsigned int>(), used, 0, 32, (hipStream_t)0));
+        EC_DEV(tmp, bytes);
+        EC_HIP(rocprim::radix_sort_pairs(tmp.p, bytes, db.as<unsigned int>(), db2.as<unsigned int>(),
+                                         di.as<unsigned int>(), di2.as<unsigned int>(), used, 0, 32, (hipStream_t)0));
+        EC_CHECK(exscan_u64(dsz.as<unsigned int>(), dst.as<unsigned long long>(), nb));
+        k_hash_offsets<<<grid_for(used, 256), 256>>>(di2.as<unsigned int>(), db2.as<unsigned int>(), used,
+                                                    dst.as<unsigned long long>(), doff.as<unsigned int>());
+        EC_HIP(hipMemcpy(offset, doff.p, used * 4, hipMemcpyDeviceToHost));
+    }
+    for (uint64_t i = used; i < n; i++) offset[i] = 0;  // never processed by the dropped blocks
+    EC_HIP(hipMemcpy(bucket_size, dsz.p, nb * 4ull, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+// copy_to_bucket_device (src/pygpuhash.py:76-170): bufferK/V[start[b] + offset[i]] = key/value
+int ec_hash_copy_to_bucket(const uint64_t *keys, const uint32_t *vals, const uint32_t *offset, uint64_t n,
+                           const uint32_t *start, uint32_t nb, uint64_t *buf_k, uint32_t *buf_v, uint64_t buf_len) {
+    if (!nb || !start || (n && (!keys || !vals || !offset || !buf_k || !buf_v))) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    std::vector<uint32_t> sz(nb, 0);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t p = (uint64_t)start[hash_h(keys[i], nb)] + offset[i];
+        if (p >= buf_len) {
+            set_error("key %llu lands at %llu outside the %llu-entry bucket buffer", (unsigned long long)i,
+                      (unsigned long long)p, (unsigned long long)buf_len);
+            return EC_ERR_ARG;
+        }
+    }
+    if (!n) return EC_OK;
+    EC_DEV(dk, n * 8);
+    EC_DEV(dv, n * 4);
+    EC_DEV(doff, n * 4);
+    EC_DEV(dst, nb * 4ull);
+    EC_DEV(dbk, buf_len * 8);
+    EC_DEV(dbv, buf_len * 4);
+    EC_HIP(hipMemcpy(dk.p, keys, n * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dv.p, vals, n * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(doff.p, offset, n * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dst.p, start, nb * 4ull, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dbk.p, buf_k, buf_len * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dbv.p, buf_v, buf_len * 4, hipMemcpyHostToDevice));
+    k_hash_copy<<<grid_for(n, 256), 256>>>(dk.as<unsigned long long>(), dv.as<unsigned int>(), doff.as<unsigned int>(), n,
+                                          nb, dst.as<unsigned int>(), dbk.as<unsigned long long>(), dbv.as<unsigned int>());
+    EC_HIP(hipMemcpy(buf_k, dbk.p, buf_len * 8, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(buf_v, dbv.p, buf_len * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+// bucket_sort_device (src/pygpuhash.py:173-258): per-bucket rank sort into TK/TV[nb*520]
+int ec_hash_bucket_sort(const uint64_t *buf_k, const uint32_t *buf_v, uint64_t buf_len, const uint32_t *start,
+                        const uint32_t *bucket_size, uint32_t nb, uint64_t *TK, uint32_t *TV) {
+    if (!nb || !start || !bucket_size || !TK || !TV || (buf_len && (!buf_k || !buf_v))) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    for (uint32_t b = 0; b < nb; b++)
+        if (bucket_size[b] > BUCKET_ITEMS || (uint64_t)start[b] + bucket_size[b] > buf_len) {
+            set_error("bucket %u: size %u / start %u outside the buffer or > 520", b, bucket_size[b], start[b]);
+            return EC_ERR_CAPACITY;
+        }
+    const uint64_t slots = (uint64_t)nb * BUCKET_ITEMS;
+    std::vector<unsigned long long> st64(nb);
+    for (uint32_t b = 0; b < nb; b++) st64[b] = start[b];
+    EC_DEV(dbk, buf_len * 8);
+    EC_DEV(dbv, buf_len * 4);
+    EC_DEV(didx, buf_len * 4);
+    EC_DEV(dst, nb * 8ull);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dTK, slots * 8);
+    EC_DEV(dTV, slots * 4);
+    std::vector<uint32_t> iota(buf_len);
+    for (uint64_t i = 0; i < buf_len; i++) iota[i] = (uint32_t)i;
+    if (buf_len) {
+        EC_HIP(hipMemcpy(dbk.p, buf_k, buf_len * 8, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dbv.p, buf_v, buf_len * 4, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(didx.p, iota.data(), buf_len * 4, hipMemcpyHostToDevice));
+    }
+    EC_HIP(hipMemcpy(dst.p, st64.data(), nb * 8ull, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dsz.p, bucket_size, nb * 4ull, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dTK.p, TK, slots * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dTV.p, TV, slots * 4, hipMemcpyHostToDevice));
+    k_hash_bucket_sort<<<nb, 256>>>(dbk.as<unsigned long long>(), didx.as<unsigned int>(), dst.as<unsigned long long>(),
+                                    dsz.as<unsigned int>(), dbv.as<unsigned int>(), dTK.as<unsigned long long>(),
+                                    dTV.as<unsigned int>());
+    EC_HIP(hipMemcpy(TK, dTK.p, slots * 8, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(TV, dTV.p, slots * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+// assign_successor_device (src/pyeulertour.py:17-107): ee[e[ep+i]].s = l[lp+i]
+int ec_assign_successor(const void *ev, uint64_t vcount, const uint32_t *l, const uint32_t *e, void *ee, uint64_t E) {
+    if ((vcount && !ev) || (E && (!l || !e || !ee))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!E || !vcount) return EC_OK;
+    EC_DEV(dev, vcount * sizeof(EulerVertex));
+    EC_DEV(dl, E * 4);
+    EC_DEV(de, E * 4);
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_HIP(hipMemcpy(dev.p, ev, vcount * sizeof(EulerVertex), hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dl.p, l, E * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(de.p, e, E * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
+    k_assign_successor<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), vcount, dl.as<unsigned int>(),
+                                                      de.as<unsigned int>(), dee.as<EulerEdge>(), E);
+    EC_HIP(hipMemcpy(ee, dee.p, E * sizeof(EulerEdge), hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+// construct_successor_graphP1/P2_device (src/pyeulertour.py:109-216): Vertex{eid, s, pred}
+int ec_successor_graph(const void *ee, uint64_t E, void *vertices) {
+    if (E && (!ee || !vertices)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!E) return EC_OK;
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_DEV(dv, E * sizeof(Vtx));
+    EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
+    k_succ_graph1<<<grid_for(E, 256), 256>>>(dee.as<EulerEdge>(), E, dv.as<Vtx>());
+    k_succ_graph2<<<grid_for(E, 256), 256>>>(dv.as<Vtx>(), E);
+    EC_HIP(hipMemcpy(vertices, dv.p, E * sizeof(Vtx), hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+
+// debruijn_count_device (src/pydebruijn.py:15-178): lcount/ecount[4V]
+int ec_db_counts(const uint64_t *lmer_keys, const uint32_t *lmer_values, uint64_t nl, uint32_t l, const uint64_t *TK,
+                 const uint32_t *TV, const uint32_t *bucket_size, uint32_t nb, uint64_t size, uint32_t *lcount,
+                 uint32_t *ecount) {
+    if (l < 2 || l > 32 || !TK || !TV || !bucket_size || !nb || (nl && (!lmer_keys || !lmer_values)) ||
+        (size && (!lcount || !ecount))) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(check_table(bucket_size, nb));
+    const uint64_t slots = (uint64_t)nb * BUCKET_ITEMS;
+    EC_DEV(dTK, slots * 8);
+    EC_DEV(dTV, slots * 4);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dlk, nl * 8);
+    EC_DEV(dlv, nl * 4);
+    EC_DEV(dlc, size * 4);
+    EC_DEV(dec, size * 4);
+    EC_HIP(hipMemcpy(dTK.p, TK, slots * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dTV.p, TV, slots * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dsz.p, bucket_size, nb * 4ull, hipMemcpyHostToDevice));
+    if (nl) {
+        EC_HIP(hipMemcpy(dlk.p, lmer_keys, nl * 8, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dlv.p, lmer_values, nl * 4, hipMemcpyHostToDevice));
+    }
+    if (size) {
+        EC_HIP(hipMemcpy(dlc.p, lcount, size * 4, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dec.p, ecount, size * 4, hipMemcpyHostToDevice));
+    }
+    const HashView h{dTK.as<unsigned long long>(), dTV.as<unsigned int>(), dsz.as<unsigned int>(), nb};
+    if (nl)
+        k_db_count<<<grid_for(nl, 256), 256>>>(dlk.as<unsigned long long>(), dlv.as<unsigned int>(), nl, h,
+                                              kmask64((int)l - 1), size, dlc.as<unsigned int>(), dec.as<unsigned int>());
+    if (size) {
+        EC_HIP(hipMemcpy(lcount, dlc.p, size * 4, hipMemcpyDeviceToHost));
+        EC_HIP(hipMemcpy(ecount, dec.p, size * 4, hipMemcpyDeviceToHost));
+    }
+    return EC_OK;
+}
+
+// setup_vertices_device (src/pydebruijn.py:181-324)
+int ec_db_vertices(const uint64_t *kmer_keys, uint64_t nk, const uint64_t *TK, const uint32_t *TV,
+                   const uint32_t *bucket_size, uint32_t nb, const uint32_t *lcount, const uint32_t *lstart,
+                   const uint32_t *ecount, const uint32_t *estart, void *ev) {
+    if (!TK || !TV || !bucket_size || !nb || (nk && (!kmer_keys || !lcount || !lstart || !ecount || !estart || !ev))) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(check_table(bucket_size, nb));
+    if (!nk) return EC_OK;
+    const uint64_t slots = (uint64_t)nb * BUCKET_ITEMS, size = 4 * nk;
+    EC_DEV(dTK, slots * 8);
+    EC_DEV(dTV, slots * 4);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dkk, nk * 8);
+    EC_DEV(dlc, size * 4);
+    EC_DEV(dls, size * 4);
+    EC_DEV(dec, size * 4);
+    EC_DEV(des, size * 4);
+    EC_DEV(dev, nk * sizeof(EulerVertex));
+    EC_HIP(hipMemcpy(dTK.p, TK, slots * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dTV.p, TV, slots * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dsz.p, bucket_size, nb * 4ull, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dkk.p, kmer_keys, nk * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dlc.p, lcount, size * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dls.p, lstart, size * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dec.p, ecount, size * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(des.p, estart, size * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dev.p, ev, nk * sizeof(EulerVertex), hipMemcpyHostToDevice));
+    const HashView h{dTK.as<unsigned long long>(), dTV.as<unsigned int>(), dsz.as<unsigned int>(), nb};
+    k_db_vertices<<<grid_for(nk, 256), 256>>>(dkk.as<unsigned long long>(), nk, h, dlc.as<unsigned int>(),
+                                             dls.as<unsigned int>(), dec.as<unsigned int>(), des.as<unsigned int>(),
+                                             dev.as<EulerVertex>());
+    EC_HIP(hipMemcpy(ev, dev.p, nk * sizeof(EulerVertex), hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+// setup_edges_device (src/pydebruijn.py:326-512); E = length of ee / l / e
+int ec_db_edges(const uint64_t *lmer_keys, const uint32_t *lmer_values, const uint32_t *lmer_offsets, uint64_t nl,
+                uint32_t l, const uint64_t *TK, const uint32_t *TV, const uint32_t *bucket_size, uint32_t nb,
+                uint64_t nk, const uint32_t *lstart, const uint32_t *estart, unsigned flags, void *ee, uint32_t *l_out,
+                uint32_t *e_out, uint64_t E) {
+    if (l < 2 || l > 32 || !TK || !TV || !bucket_size || !nb || (nl && (!lmer_keys || !lmer_values || !lmer_offsets)) ||
+        (nk && (!lstart || !estart)) || (E && (!ee || !l_out || !e_out))) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(check_table(bucket_size, nb));
+    const uint64_t slots = (uint64_t)nb * BUCKET_ITEMS, size = 4 * nk;
+    EC_DEV(dTK, slots * 8);
+    EC_DEV(dTV, slots * 4);
+    EC_DEV(dsz, nb * 4ull);
+    EC_DEV(dlk, nl * 8);
+    EC_DEV(dlv, nl * 4);
+    EC_DEV(dlo, nl * 4);
+    EC_DEV(dls, size * 4);
+    EC_DEV(des, size * 4);
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_DEV(dl, E * 4);
+    EC_DEV(de, E * 4);
+    EC_HIP(hipMemcpy(dTK.p, TK, slots * 8, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dTV.p, TV, slots * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dsz.p, bucket_size, nb * 4ull, hipMemcpyHostToDevice));
+    if (nl) {
+        EC_HIP(hipMemcpy(dlk.p, lmer_keys, nl * 8, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dlv.p, lmer_values, nl * 4, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dlo.p, lmer_offsets, nl * 4, hipMemcpyHostToDevice));
+    }
+    if (size) {
+        EC_HIP(hipMemcpy(dls.p, lstart, size * 4, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(des.p, estart, size * 4, hipMemcpyHostToDevice));
+    }
+    if (E) {
+        EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dl.p, l_out, E * 4, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(de.p, e_out, E * 4, hipMemcpyHostToDevice));
+    }
+    const HashView h{dTK.as<unsigned long long>(), dTV.as<unsigned int>(), dsz.as<unsigned int>(), nb};
+    if (nl)
+        k_db_edges<<<grid_for(nl, 256), 256>>>(dlk.as<unsigned long long>(), dlv.as<unsigned int>(),
+                                              dlo.as<unsigned int>(), nl, h, kmask64((int)l - 1), size, E,
+                                              (flags & EC_MOD_REF_BOUNDS) ? 1 : 0, dls.as<unsigned int>(),
+                                              des.as<unsigned int>(), dl.as<unsigned int>(), de.as<unsigned int>(),
+                                              dee.as<EulerEdge>());
+    if (E) {
+        EC_HIP(hipMemcpy(ee, dee.p, E * sizeof(EulerEdge), hipMemcpyDeviceToHost));
+        EC_HIP(hipMemcpy(l_out, dl.p, E * 4, hipMemcpyDeviceToHost));
+        EC_HIP(hipMemcpy(e_out, de.p, E * 4, hipMemcpyDeviceToHost));
+    }
+    return EC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,203 @@
+"""GPU parity of the per-module drop-ins (pyencode, pygpuhash, pydebruijn, pycomponent,
+pyeulertour -> libeulerhip.so) against oracle/modules_ref.py on the same inputs (bit-exact)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import modules_ref as R  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def kat():
+    with open(os.path.join(HERE, "golden", "kat.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def mods():
+    import pycomponent
+    import pydebruijn
+    import pyencode
+    import pyeulertour
+    import pygpuhash
+
+    return pyencode, pygpuhash, pydebruijn, pycomponent, pyeulertour
+
+
+def _buffers(kat):
+    rng = np.random.default_rng(11)
+    g200 = "".join(kat["g200_reads"]).encode()
+    rnd = bytes(rng.choice(list(b"ACGTNacgt\n"), 3000).tolist())
+    return [g200, rnd, b"ACGT", b"A"]
+
+
+@pytest.mark.parametrize("L", [1, 3, 11, 21, 31, 32])
+def test_encode(kat, mods, L):
+    enc = mods[0]
+    for buf in _buffers(kat):
+        b = np.array(buf.decode()).astype("S")
+        d = np.zeros(len(buf), np.uint64)
+        out = enc.encode_lmer_device(b, len(buf), d, 0, L)
+        assert out is d
+        assert np.array_equal(out, R.encode_lmers(buf, L))
+        d2 = np.zeros(len(buf), np.uint64)
+        assert np.array_equal(enc.compute_lmer_complement_device(b, len(buf), d2, 0, L), R.encode_lmers_rc(buf, L))
+
+
+def test_encode_kat(kat, mods):
+    enc = mods[0]
+    for s, L, v in kat["encode"]:
+        d = np.zeros(len(s), np.uint64)
+        assert int(enc.encode_lmer_device(np.array(s).astype("S"), len(s), d, 0, L)[0]) == v
+
+
+def test_encode_reference_error_behaviour(mods):
+    enc = mods[0]
+    d = [0, 0]
+    assert enc.encode_lmer_device("AC", 2, d, 0, 2) is d  # non-ndarray input: returned unchanged
+
+
+def test_split(kat, mods):
+    enc = mods[0]
+    buf = "".join(kat["g200_reads"]).encode()
+    for l in (5, 12, 32):
+        lm = R.encode_lmers(buf, l)
+        mask = (1 << (2 * (l - 1))) - 1
+        pk, sk = np.zeros_like(lm), np.zeros_like(lm)
+        enc.compute_kmer_device(lm, pk, sk, mask, 0, len(lm))
+        p2, s2 = R.split_kmers(lm, mask)
+        assert np.array_equal(pk, p2) and np.array_equal(sk, s2)
+
+
+def test_hash_reproduces_reference_dump(kat, mods):
+    gh = mods[1]
+    nb = kat["hash_tk_bucket_count"]
+    buckets = [list(b) for b in kat["hash_tk_buckets"]]
+    if sum(len(b) for b in buckets) % 1024:
+        buckets[R.hash_h(0, nb)] = [0] + buckets[R.hash_h(0, nb)]
+    keys = np.array([x for row in buckets for x in row], np.uint64)
+    rng = np.random.default_rng(7)
+    rng.shuffle(keys)
+    tail = rng.integers(1, 1 << 62, 400, dtype=np.uint64)
+    allk = np.concatenate([keys, tail])
+    vals = np.arange(len(allk), dtype=np.uint32)
+    tl, size, nb2, TK, TV = gh.create_hash_table_device(allk, vals, len(allk), None, None, 0, None, 0, tail_drop=True)
+    assert nb2 == nb and tl == nb * 520
+    for b, row in enumerate(buckets):
+        assert int(size[b]) == len(row)
+        assert [int(x) for x in TK[b * 520:b * 520 + len(row)]] == row
+    rTK, rTV, rsize, _ = R.hash_build(allk, vals, tail_drop=True)
+    assert np.array_equal(TK, rTK) and np.array_equal(TV, rTV) and np.array_equal(size, rsize)
+    # lookups: hits give the input index, misses 0xFFFFFFFF
+    got = gh.hash_lookup(np.concatenate([keys[:500], tail[:50]]), TK, TV, size, nb)
+    assert got[:500].tolist() == list(range(500))
+    assert (got[500:] == 0xFFFFFFFF).all()
+    # fixed default: nothing dropped
+    tl, size, nb3, TK, TV = gh.create_hash_table_device(allk, vals, len(allk), None, None, 0, None, 0)
+    assert int(size.sum()) == len(allk)
+    assert (gh.hash_lookup(tail, TK, TV, size, nb3) == vals[len(keys):]).all()
+
+
+def test_hash_steps(mods):
+    gh = mods[1]
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 1 << 40, 5000, dtype=np.uint64)
+    keys[100:110] = keys[0]  # duplicates: the later index wins the shared rank
+    vals = np.arange(len(keys), dtype=np.uint32)
+    nb = R.bucket_count(len(keys))
+    off, cnt = gh.phase1_device(keys, None, len(keys), None, nb)
+    hb = np.array([R.hash_h(int(x), nb) for x in keys])
+    assert np.array_equal(cnt, np.bincount(hb, minlength=nb))
+    for b in range(nb):  # offsets: a permutation of 0..size-1 inside each bucket
+        assert sorted(off[hb == b].tolist()) == list(range(int(cnt[b])))
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint32)
+    bk, bv = gh.copy_to_bucket_device(keys, vals, off, len(keys), start, nb, np.zeros(len(keys), np.uint64),
+                                      np.zeros(len(keys), np.uint32))
+    assert np.array_equal(bk[start[hb] + off], keys)
+    TK, TV = gh.bucket_sort_device(bk, bv, start, cnt, nb, np.zeros(0), np.zeros(0))
+    rTK, rTV, rsize, _ = R.hash_build(keys, vals, nb)
+    assert np.array_equal(TK, rTK) and np.array_equal(TV, rTV)
+
+
+def _ref_pipeline(buf, l, ref_bounds=False):
+    keys, counts, kmers = R.lmer_table(buf, l)
+    table = R.hash_build(kmers, np.arange(len(kmers), dtype=np.uint32))
+    ev, ee, L, Ee, E = R.debruijn(keys, counts, kmers, l, table, ref_bounds)
+    return keys, counts, kmers, table, ev, ee, L, Ee, E
+
+
+@pytest.mark.parametrize("l,nreads,ref_bounds", [(10, 20, False), (12, 200, False), (8, 50, True), (21, 200, False)])
+def test_debruijn_and_euler(kat, mods, l, nreads, ref_bounds):
+    enc, gh, db, cc, et = mods
+    buf = "".join(kat["g200_reads"][:nreads]).encode()
+    keys, counts, kmers, (TK, TV, size, nb), ev, ee, L, Ee, E = _ref_pipeline(buf, l, ref_bounds)
+    mask = (1 << (2 * (l - 1))) - 1
+    tl, gsize, gnb, gTK, gTV = gh.create_hash_table_device(kmers, np.arange(len(kmers), dtype=np.uint32), len(kmers),
+                                                           None, None, 0, None, 0)
+    assert np.array_equal(gTK, TK) and np.array_equal(gTV, TV)
+    gee, gev, gl, ge, kc, gE = db.construct_debruijn_graph_device(keys, counts, len(keys), kmers, len(kmers), l, gTK,
+                                                                  gTV, gsize, gnb, None, None, None, None, 0,
+                                                                  ref_bounds=ref_bounds)
+    assert gE == E
+    assert np.array_equal(gev, ev) and np.array_equal(gee, ee)
+    assert np.array_equal(gl, L) and np.array_equal(ge, Ee)
+    # step-level G1 / G3 / G4
+    V4 = 4 * len(kmers)
+    lc, ec = np.zeros(V4, np.uint32), np.zeros(V4, np.uint32)
+    db.debruijn_count_device(keys, counts, len(keys), gTK, gTV, gsize, gnb, lc, ec, mask, 0)
+    ls = np.concatenate([[0], np.cumsum(lc)[:-1]]).astype(np.uint32)
+    es = np.concatenate([[0], np.cumsum(ec)[:-1]]).astype(np.uint32)
+    ev3 = db.setup_vertices_device(kmers, len(kmers), gTK, gTV, gsize, gnb, np.zeros(len(kmers), R.EV), lc, ls, ec, es)
+    assert np.array_equal(ev3, ev)
+    lo = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.uint32)
+    ee3, l3, e3 = db.setup_edges_device(keys, counts, lo, len(keys), gTK, gTV, gsize, gnb, np.zeros(E, np.uint32),
+                                        np.zeros(E, np.uint32), np.zeros(E, R.EE), ls, es, mask, ref_bounds=ref_bounds)
+    assert np.array_equal(ee3, ee) and np.array_equal(l3, L) and np.array_equal(e3, Ee)
+    # Euler tour: successors, circuits, circuit graph
+    ree, rcg, rcgV = R.find_euler(ev, L, Ee, ee)
+    work = ee.copy()
+    cg, ncg, cgV = et.findEulerDevice(ev, L, Ee, len(ev), work, E, None, 0, 0)
+    assert np.array_equal(work, ree)
+    assert cgV == rcgV and ncg == len(rcg)
+    key = lambda a: np.sort(a, order=["c1", "c2", "e1", "e2"])  # noqa: E731 -- ties in (c1, c2) are unordered
+    assert np.array_equal(key(cg), key(rcg))
+    assert np.array_equal(cg[["c1", "c2"]], rcg[["c1", "c2"]])
+    # step-level successor + successor graph + components
+    ev2, ee2 = et.assign_successor_device(ev, L, Ee, len(ev), ee.copy(), E)
+    assert np.array_equal(ee2, ree)
+    v = et.construct_successor_graph_device(ee2, None, E)
+    D = cc.find_component_device(v, np.zeros(E, np.uint32), E)
+    assert np.array_equal(D, R.components(v))
+    cs = et.identify_contig_start(ree, np.ones(E, np.uint32), E)
+    assert np.array_equal(cs, R.contig_start(ree))
+    # spanning marks + the swipe the reference leaves commented out
+    tree = np.arange(0, ncg, 2, dtype=np.uint32)
+    mk = et.mark_spanning_euler_edges(ree, None, E, cg, ncg, tree, len(tree))
+    assert np.array_equal(mk, R.mark_spanning(cg, tree, E))
+    sw = et.executeSwipeDevice(ev, Ee, len(ev), ree.copy(), E, cg, ncg, tree, len(tree), swipe=True)
+    assert np.array_equal(sw, R.swipe(ev, Ee, ree, R.mark_spanning(cg, tree, E)))
+    nosw = et.executeSwipeDevice(ev, Ee, len(ev), ree.copy(), E, cg, ncg, tree, len(tree))
+    assert np.array_equal(nosw, ree)  # reference: the swipe body is commented out
+
+
+def test_components_random(mods):
+    cc = mods[3]
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 17, 5000, 100000):
+        # random successor permutation -> cycles; break some links -> paths
+        s = rng.permutation(n).astype(np.uint32)
+        s[rng.random(n) < 0.01] = n
+        v = np.zeros(n, R.VTX)
+        v["vid"] = np.arange(n)
+        v["n1"] = s
+        v["n2"] = n
+        for i in range(n):
+            if s[i] < n:
+                v[s[i]]["n2"] = i
+        D = cc.find_component_device(v, np.zeros(n, np.uint32), n)
+        assert np.array_equal(D, R.components(v))
