@@ -157,7 +157,7 @@ int ec_components(const void *vertices, uint64_t n, uint32_t *D);
 int ec_find_euler(const void *ev, uint64_t vcount, const uint32_t *l, const uint32_t *e, void *ee, uint64_t E,
                   void *cg_edges, uint64_t *cg_edge_count, uint32_t *cg_vertex_count);
 /* T5 executeSwipeDevice (src/pyeulertour.py:656-664): mark (all ones, :659) + tree marks;
- * the swipe itself only with EC_MOD_SWIPE (a no-op in the reference) */
+ * the swipe itself only with EC_MOD_SWIPE (a no-op in the reference; needs e to be a permutation) */
 int ec_execute_swipe(const void *ev, uint64_t vcount, const uint32_t *e, void *ee, uint64_t E, const void *cg_edges,
                      uint64_t cg_edge_count, const uint32_t *tree, uint64_t tree_count, unsigned flags,
                      uint32_t *mark_out);

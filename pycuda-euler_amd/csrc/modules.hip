@@ -743,6 +743,16 @@ int ec_execute_swipe(const void *ev, uint64_t vcount, const uint32_t *e, void *e
                       (unsigned long long)i, (unsigned long long)E);
             return EC_ERR_ARG;
         }
+    if (flags & EC_MOD_SWIPE) {  // each vertex rewrites its own entering edges: e must be a permutation
+        std::vector<uint8_t> seen(E, 0);
+        for (uint64_t i = 0; i < E; i++) {
+            if (seen[e[i]]) {
+                set_error("swipe needs e to be a permutation of the edges (edge %u listed twice)", e[i]);
+                return EC_ERR_ARG;
+            }
+            seen[e[i]] = 1;
+        }
+    }
     for (uint64_t i = 0; i < tree_count; i++)
         if (tree[i] >= cg_edge_count) {
             set_error("tree[%llu] = %u is not a circuit-graph edge index", (unsigned long long)i, tree[i]);
