@@ -192,6 +192,20 @@ int ec_db_edges(const uint64_t *lmer_keys, const uint32_t *lmer_values, const ui
 int ec_assign_successor(const void *ev, uint64_t vcount, const uint32_t *l, const uint32_t *e, void *ee, uint64_t E);
 /* construct_successor_graphP1/P2_device (src/pyeulertour.py:109-216): Vertex{eid, s, pred} */
 int ec_successor_graph(const void *ee, uint64_t E, void *vertices);
+/* readLmersKmersCuda (src/eulercuda.py:73-179) host dedup, on the device: F / RC l-mer codes of
+ * the concatenated buffer (L = lmerLength), distinct nonzero l-mers in first-occurrence order of
+ * the stream F[0], R[0], F[1], ... with their counts, the number of zero ("empty") l-mers, and
+ * the distinct (L-1)-mers of pF, sF, pR, sR per position in first-occurrence order.
+ * Capacities: lmer_keys / lmer_values 2B, kmer_keys 4B; B < 2^30. */
+int ec_read_lmers_kmers(const uint8_t *buf, uint64_t B, uint32_t L, uint64_t *lmer_keys, uint32_t *lmer_values,
+                        uint64_t *n_lmers, uint64_t *lmer_empty, uint64_t *kmer_keys, uint64_t *n_kmers);
+/* generatePartialContig (src/eulercuda.py:328-402) walk, on the device: every successor path
+ * from its head (in head order), then every cycle from its smallest edge; contig c =
+ * chars[coff[c] .. coff[c+1]) = getString(l-1, vid) of each edge's v1, then of the last edge's
+ * v2.  Needs an injective successor map (EC_ERR_ARG otherwise).  Capacities: chars
+ * 2E(l-1), coff E+1. */
+int ec_partial_contigs(const void *ev, uint64_t vcount, const void *ee, uint64_t E, uint32_t l, char *chars,
+                       uint64_t *coff, uint64_t *n_contigs, uint64_t *n_chars);
 
 /* ---- read-sharded multi-GPU building blocks (pycuda-euler_amd/distributed.py) ------------
  * Replace the reference's distribution layer (Spark mapPartitions of assemble2,
@@ -218,6 +232,11 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
 int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags);
 /* copy the held records (ec_merge_owned's solid set) to d_out */
 int ec_export_dense(ec_session *s, void *d_out);
+/* all_contigs(d, k) (referenceAssembler.py:79-111) on a caller's dict: n entries of k
+ * characters (ACGT) in dict order with their counts; the dict must hold every k-mer together
+ * with its twin, as build() returns it.  Results via ec_copy_contigs / ec_copy_links. */
+int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *counts, uint64_t n, int k,
+                           unsigned flags);
 /* graph phase (links .. GFA) on a complete solid set; results via ec_copy_* */
 int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags);
 

@@ -268,3 +268,69 @@ def lmer_table(buf, l):
     pre, suf = split_kmers(keys, mask)
     kmers = np.unique(np.concatenate([pre, suf]))
     return keys, counts.astype(np.uint32), kmers
+
+
+def read_lmers_kmers(buf, L):
+    """H0 readLmersKmersCuda (src/eulercuda.py:73-179), dict-for-dict: returns
+    [lmerCount, kmerCount, lmerKeys, lmerValues, kmerKeys, kmerValues]."""
+    F = encode_lmers(buf, L)
+    R = encode_lmers_rc(buf, L)
+    mask = (1 << (2 * (L - 1))) - 1
+    pF, sF = split_kmers(F, mask)
+    pR, sR = split_kmers(R, mask)
+    kmerMap, lmerMap = {}, {}
+    lmerEmpty = 0
+    for i in range(len(F)):
+        for x in (pF[i], sF[i], pR[i], sR[i]):
+            kmerMap[int(x)] = 1
+        for x in (int(F[i]), int(R[i])):
+            if x == 0:
+                lmerEmpty += 1
+            else:
+                lmerMap[x] = lmerMap.get(x, 0) + 1
+    kmerKeys = list(kmerMap)
+    lmerKeys = list(lmerMap)
+    lmerValues = list(lmerMap.values())
+    if lmerEmpty > 0:  # :175-177 -- overwrites the last real l-mer
+        lmerKeys[len(lmerMap) - 1] = 0
+        lmerValues[len(lmerMap) - 1] = lmerEmpty
+    return [len(lmerMap) + lmerEmpty, len(kmerMap), lmerKeys, lmerValues, kmerKeys, list(range(len(kmerKeys)))]
+
+
+def get_string(length, value):
+    """T7 getString / dna_translate (src/eulercuda.py:307-320)."""
+    out = [""] * length
+    v = int(value)
+    for i in range(1, length + 1):
+        out[length - i] = "ACGT"[v % 4]
+        v //= 4
+    return "".join(out)
+
+
+def partial_contigs(ev, ee, l):
+    """T6 generatePartialContig (src/eulercuda.py:328-402), loop for loop; returns the list of
+    buffers (each a list of (l-1)-mer strings)."""
+    E = len(ee)
+    cs = contig_start(ee)
+    visited = np.zeros(E, np.uint32)
+    output = []
+
+    def walk(i):
+        buf = [get_string(l - 1, ev[int(ee[i]["v1"])]["vid"])]
+        nxt = i
+        while int(ee[nxt]["s"]) < E and visited[int(ee[nxt]["s"])] == 0:
+            visited[nxt] = 1
+            nxt = int(ee[nxt]["s"])
+            buf.append(get_string(l - 1, ev[int(ee[nxt]["v1"])]["vid"]))
+        if visited[nxt] == 0:
+            buf.append(get_string(l - 1, ev[int(ee[nxt]["v2"])]["vid"]))
+            visited[nxt] = 1
+        output.append(buf)
+
+    for i in range(E):
+        if cs[i] != 0 and visited[i] == 0:
+            walk(i)
+    for i in range(E):
+        if visited[i] == 0:
+            walk(i)
+    return output

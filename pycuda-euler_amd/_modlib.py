@@ -32,6 +32,9 @@ for name, res, args in [
     ("ec_db_vertices", INT, [P, U64, P, P, P, U32, P, P, P, P, P]),
     ("ec_db_edges", INT, [P, P, P, U64, U32, P, P, P, U32, U64, P, P, UINT, P, P, P, U64]),
     ("ec_successor_graph", INT, [P, U64, P]),
+    ("ec_read_lmers_kmers", INT, [P, U64, U32, P, P, ctypes.POINTER(U64), ctypes.POINTER(U64), P,
+                                  ctypes.POINTER(U64)]),
+    ("ec_partial_contigs", INT, [P, U64, P, U64, U32, P, P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
 ]:
     eulerhip.register(name, res, args)
 

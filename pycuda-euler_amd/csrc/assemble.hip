@@ -95,6 +95,36 @@ struct ec_session {
     DevBuf ocnt;
 };
 
+namespace ec {
+
+// all_contigs(d, k) from a caller's dict (referenceAssembler.py:79-111): entry i = (string,
+// count) in dict order becomes an exchange record of its canonical key whose first event of
+// the entry's orientation is i; a twin entry adds count 0 (build stores both strands with the
+// same count).  bad gets the smallest entry index holding a byte outside ACGT.
+__global__ void __launch_bounds__(256) k_kmers_to_agg(const char *chars, const unsigned int *counts, uint64_t n, int k,
+                                                      Agg *out, unsigned long long *bad) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const char *x = chars + t * (uint64_t)k;
+        unsigned long long code = 0;
+        bool ok = true;
+        for (int i = 0; i < k; i++) {
+            const uint32_t b = base_code((unsigned char)x[i]);
+            ok &= b < 4;
+            code = (code << 2) | (b & 3u);
+        }
+        if (!ok) atomicMin(bad, (unsigned long long)t);
+        const unsigned long long tw = twin64(code, k);
+        Agg a;
+        a.key = code < tw ? code : tw;
+        a.pad = 0;
+        a.count = code <= tw ? counts[t] : 0u;
+        a.fC = code <= tw ? (unsigned long long)t : ~0ull;
+        a.fT = code >= tw ? (unsigned long long)t : ~0ull;
+        out[t] = a;
+    }
+}
+}  // namespace ec
+
 namespace {
 
 struct Scalars {  // device scalars block
@@ -885,6 +915,36 @@ int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int
     unsigned int U = 0;
     SolidIndex sidx{};
     EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, LLONG_MIN, U, sidx));
+    return phase_graph(s, k, U, sidx);
+}
+
+int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *counts, uint64_t n, int k, unsigned flags) {
+    if (!s || (n && (!kmers || !counts))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    EC_CHECK(begin_call(s, k, flags));
+    hipStream_t st = s->stream;
+    EC_CHECK(s->dchars.ensure(std::max<size_t>(n * (size_t)k, 1)));
+    EC_CHECK(s->dcounts.ensure(std::max<size_t>(n * 4, 4)));
+    EC_CHECK(s->recs2.ensure(std::max<size_t>(n * sizeof(Agg), 16)));
+    Scalars *dsc = s->scal.as<Scalars>();
+    if (n) {
+        EC_HIP(hipMemcpyAsync(s->dchars.p, kmers, n * (size_t)k, hipMemcpyHostToDevice, st));
+        EC_HIP(hipMemcpyAsync(s->dcounts.p, counts, n * 4, hipMemcpyHostToDevice, st));
+        k_kmers_to_agg<<<grid_for(n, 256), 256, 0, st>>>(s->dchars.as<char>(), s->dcounts.as<unsigned int>(), n, k,
+                                                        s->recs2.as<Agg>(), &dsc->bad);
+        unsigned long long bad = 0;
+        EC_HIP(hipMemcpyAsync(&bad, &dsc->bad, 8, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (bad != ~0ull) {
+            set_error("dict entry %llu holds a byte outside ACGT", bad);
+            return EC_ERR_ALPHABET;
+        }
+    }
+    unsigned int U = 0;
+    SolidIndex sidx{};
+    EC_CHECK(phase_merge(s, s->recs2.as<Agg>(), n, LLONG_MIN, U, sidx));
     return phase_graph(s, k, U, sidx);
 }
 

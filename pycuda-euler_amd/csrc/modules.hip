@@ -408,6 +408,165 @@ __global__ void __launch_bounds__(256) k_contig_start(const EulerEdge *ee, uint6
         if (ee[t].s < E) cs[ee[t].s] = 0;
 }
 
+
+// ---- H0 readLmersKmersCuda host dedup, on the device (src/eulercuda.py:73-179) -------------
+// streams: l-mers S[2p] = F[p], S[2p+1] = R[p] (:147-160); k-mers K[4p..4p+3] = pF, sF, pR, sR
+// (:142-145).  unique_first() keeps each distinct key once, in order of first occurrence in
+// the stream (= Python dict insertion order), with its multiplicity.
+__global__ void __launch_bounds__(256) k_streams(const unsigned long long *F, const unsigned long long *R, uint64_t B,
+                                                 unsigned long long mask, unsigned long long *S,
+                                                 unsigned long long *K) {
+    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < B; p += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long f = F[p], r = R[p];
+        S[2 * p] = f;
+        S[2 * p + 1] = r;
+        K[4 * p + 0] = (f & (mask << 2)) >> 2;
+        K[4 * p + 1] = f & mask;
+        K[4 * p + 2] = (r & (mask << 2)) >> 2;
+        K[4 * p + 3] = r & mask;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_iota(unsigned int *x, uint64_t n) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        x[t] = (unsigned int)t;
+}
+
+// segment heads of the sorted keys (zero keys excluded when skip_zero)
+__global__ void __launch_bounds__(256) k_seg_heads(const unsigned long long *sk, uint64_t n, int skip_zero,
+                                                   unsigned int *flag) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        flag[t] = (t == 0 || sk[t] != sk[t - 1]) && !(skip_zero && sk[t] == 0ull);
+}
+
+__global__ void __launch_bounds__(256) k_seg_compact(const unsigned long long *sk, const unsigned int *si,
+                                                     const unsigned int *flag, const unsigned int *pos, uint64_t n,
+                                                     unsigned long long *uk, unsigned int *ufirst, unsigned int *ustart) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        if (flag[t]) {
+            const unsigned int j = pos[t];
+            uk[j] = sk[t];
+            ufirst[j] = si[t];  // the radix sort is stable: the head holds the first occurrence
+            ustart[j] = (unsigned int)t;
+        }
+}
+
+__global__ void __launch_bounds__(256) k_seg_emit(const unsigned int *order, const unsigned long long *uk,
+                                                  const unsigned int *ustart, uint64_t nu, uint64_t n,
+                                                  unsigned long long *out_k, unsigned int *out_c) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nu; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int j = order[t];
+        out_k[t] = uk[j];
+        if (out_c) out_c[t] = (unsigned int)((j + 1 < nu ? ustart[j + 1] : n) - ustart[j]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_count_zero(const unsigned long long *x, uint64_t n, unsigned long long *cnt) {
+    unsigned long long c = 0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        c += x[t] == 0ull;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+// ---- T6 generatePartialContig walk, on the device (src/eulercuda.py:328-402) ----------------
+// With an injective successor map the edges form disjoint paths and cycles.  The reference's
+// first loop emits every path from its head (edges that are no one's successor) in head order,
+// the second loop every cycle from its smallest edge, in that order.  Pointer jumping on the
+// predecessor links gives (head, rank); cycles are found (pointer never reaches a head after
+// ceil(log2 E) + 1 doublings), cut at their minimum edge and ranked again.
+__global__ void __launch_bounds__(256) k_pw_pred(const EulerEdge *ee, uint64_t E, unsigned int *pred,
+                                                 unsigned int *indeg) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int s = ee[t].s;
+        if (s < E) {
+            pred[s] = (unsigned int)t;
+            atomicAdd(&indeg[s], 1u);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pw_init(const unsigned int *pred, const unsigned int *mn_in, uint64_t E,
+                                                 unsigned int *nxt, unsigned int *d, unsigned int *hd,
+                                                 unsigned int *mn) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned int p = pred[t];
+        if (mn_in && mn_in[t] == (unsigned int)t) p = NONE32;  // cut a cycle at its minimum edge
+        nxt[t] = p;
+        d[t] = p == NONE32 ? 0u : 1u;
+        hd[t] = p == NONE32 ? (unsigned int)t : p;
+        mn[t] = (unsigned int)t;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pw_jump(const unsigned int *nxt, const unsigned int *d, const unsigned int *hd,
+                                                 const unsigned int *mn, uint64_t E, unsigned int *nxt2,
+                                                 unsigned int *d2, unsigned int *hd2, unsigned int *mn2) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int q = nxt[t];
+        if (q == NONE32) {
+            nxt2[t] = q;
+            d2[t] = d[t];
+            hd2[t] = hd[t];
+            mn2[t] = mn[t];
+        } else {
+            nxt2[t] = nxt[q];
+            d2[t] = d[t] + d[q];
+            hd2[t] = hd[q];
+            mn2[t] = min(mn[t], mn[q]);
+        }
+    }
+}
+
+// cycle members keep a live pointer; their window minimum is the cycle minimum
+__global__ void __launch_bounds__(256) k_pw_cycmin(const unsigned int *nxt, const unsigned int *mn, uint64_t E,
+                                                   unsigned int *cmin) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x)
+        cmin[t] = nxt[t] == NONE32 ? NONE32 : mn[t];
+}
+
+__global__ void __launch_bounds__(256) k_pw_keys(const unsigned int *cmin, const unsigned int *hd, const unsigned int *d,
+                                                 uint64_t E, unsigned long long *key, unsigned int *val) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < E; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long cyc = cmin[t] != NONE32;
+        key[t] = (cyc << 63) | ((unsigned long long)hd[t] << 32) | d[t];
+        val[t] = (unsigned int)t;
+    }
+}
+
+// chars contributed by the edge at sorted position j: its v1 (l-1)-mer, plus v2's when it ends the walk
+__global__ void __launch_bounds__(256) k_pw_len(const unsigned long long *skey, uint64_t E, unsigned int km1,
+                                                unsigned long long *len, unsigned int *start) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < E; j += (uint64_t)gridDim.x * blockDim.x) {
+        const bool first = (unsigned int)skey[j] == 0u;
+        const bool last = j + 1 == E || (unsigned int)skey[j + 1] == 0u;
+        len[j] = (unsigned long long)km1 * (last ? 2 : 1);
+        start[j] = first;
+    }
+}
+
+__device__ inline void put_kmer(char *out, unsigned long long vid, unsigned int km1) {
+    for (unsigned int t = 0; t < km1; t++) out[t] = "ACGT"[(vid >> (2 * (km1 - 1 - t))) & 3ull];  // getString :314-320
+}
+
+__global__ void __launch_bounds__(256) k_pw_emit(const unsigned long long *skey, const unsigned int *sval,
+                                                 const unsigned long long *pos, const unsigned int *cidx, uint64_t E,
+                                                 const EulerEdge *ee, const EulerVertex *ev, uint64_t vcount,
+                                                 unsigned int km1, char *chars, unsigned long long *coff,
+                                                 unsigned int *bad) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < E; j += (uint64_t)gridDim.x * blockDim.x) {
+        const EulerEdge x = ee[sval[j]];
+        if (x.v1 >= vcount || x.v2 >= vcount) {
+            atomicOr(bad, 1u);
+            continue;
+        }
+        put_kmer(chars + pos[j], ev[x.v1].vid, km1);
+        const bool last = j + 1 == E || (unsigned int)skey[j + 1] == 0u;
+        if (last) put_kmer(chars + pos[j] + km1, ev[x.v2].vid, km1);
+        if ((unsigned int)skey[j] == 0u) coff[cidx[j] - 1] = pos[j];
+    }
+}
+
 // ---- host helpers ---------------------------------------------------------------------------
 struct Dev {
     void *p = nullptr;
@@ -1087,3 +1246,234 @@ int ec_db_edges(const uint64_t *lmer_keys, const uint32_t *lmer_values, const ui
 }
 
 }  // extern "C"
+
+
+// readLmersKmersCuda (src/eulercuda.py:73-179) on the device: encode F / RC l-mers of the
+// concatenated buffer, split them, and dedup both streams in first-occurrence order.
+// Capacities: lmer_keys / lmer_values 2B, kmer_keys 4B.
+static int unique_first(const unsigned long long *keys, uint64_t n, int skip_zero, unsigned long long *out_k,
+                        unsigned int *out_c, uint64_t *nu_out) {
+    *nu_out = 0;
+    if (!n) return EC_OK;
+    EC_DEV(idx, n * 4);
+    EC_DEV(sk, n * 8);
+    EC_DEV(si, n * 4);
+    EC_DEV(flag, n * 4);
+    EC_DEV(pos, n * 4);
+    k_iota<<<grid_for(n, 256), 256>>>(idx.as<unsigned int>(), n);
+    size_t bytes = 0;
+    EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, keys, sk.as<unsigned long long>(), idx.as<unsigned int>(),
+                                     si.as<unsigned int>(), n, 0, 64, (hipStream_t)0));
+    {
+        EC_DEV(tmp, bytes);
+        EC_HIP(rocprim::radix_sort_pairs(tmp.p, bytes, keys, sk.as<unsigned long long>(), idx.as<unsigned int>(),
+                                         si.as<unsigned int>(), n, 0, 64, (hipStream_t)0));
+    }
+    k_seg_heads<<<grid_for(n, 256), 256>>>(sk.as<unsigned long long>(), n, skip_zero, flag.as<unsigned int>());
+    EC_CHECK(exscan_u32(flag.as<unsigned int>(), pos.as<unsigned int>(), n));
+    uint32_t last[2];
+    EC_HIP(hipMemcpy(&last[0], pos.as<unsigned int>() + (n - 1), 4, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(&last[1], flag.as<unsigned int>() + (n - 1), 4, hipMemcpyDeviceToHost));
+    const uint64_t nu = (uint64_t)last[0] + last[1];
+    *nu_out = nu;
+    if (!nu) return EC_OK;
+    EC_DEV(uk, nu * 8);
+    EC_DEV(ufirst, nu * 4);
+    EC_DEV(ustart, nu * 4);
+    EC_DEV(sfirst, nu * 4);
+    EC_DEV(ord0, nu * 4);
+    EC_DEV(ord, nu * 4);
+    k_seg_compact<<<grid_for(n, 256), 256>>>(sk.as<unsigned long long>(), si.as<unsigned int>(), flag.as<unsigned int>(),
+                                             pos.as<unsigned int>(), n, uk.as<unsigned long long>(),
+                                             ufirst.as<unsigned int>(), ustart.as<unsigned int>());
+    k_iota<<<grid_for(nu, 256), 256>>>(ord0.as<unsigned int>(), nu);
+    bytes = 0;
+    EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, ufirst.as<unsigned int>(), sfirst.as<unsigned int>(),
+                                     ord0.as<unsigned int>(), ord.as<unsigned int>(), nu, 0, 32, (hipStream_t)0));
+    {
+        EC_DEV(tmp, bytes);
+        EC_HIP(rocprim::radix_sort_pairs(tmp.p, bytes, ufirst.as<unsigned int>(), sfirst.as<unsigned int>(),
+                                         ord0.as<unsigned int>(), ord.as<unsigned int>(), nu, 0, 32, (hipStream_t)0));
+    }
+    k_seg_emit<<<grid_for(nu, 256), 256>>>(ord.as<unsigned int>(), uk.as<unsigned long long>(), ustart.as<unsigned int>(),
+                                           nu, n, out_k, out_c);
+    return EC_OK;
+}
+
+extern "C" int ec_read_lmers_kmers(const uint8_t *buf, uint64_t B, uint32_t L, uint64_t *lmer_keys,
+                                   uint32_t *lmer_values, uint64_t *n_lmers, uint64_t *lmer_empty, uint64_t *kmer_keys,
+                                   uint64_t *n_kmers) {
+    if (L < 2 || L > 32 || !n_lmers || !lmer_empty || !n_kmers || (B && (!buf || !lmer_keys || !lmer_values || !kmer_keys))) {
+        set_error("bad arguments (L=%u must be in [2,32])", L);
+        return EC_ERR_ARG;
+    }
+    *n_lmers = *lmer_empty = *n_kmers = 0;
+    if (!B) return EC_OK;
+    if (4 * B >= (1ull << 32)) {
+        set_error("buffer of %llu bases exceeds the 2^30 limit of the module path", (unsigned long long)B);
+        return EC_ERR_CAPACITY;
+    }
+    EC_DEV(db, B);
+    EC_DEV(F, B * 8);
+    EC_DEV(R, B * 8);
+    EC_DEV(S, 2 * B * 8);
+    EC_DEV(K, 4 * B * 8);
+    EC_DEV(zc, 8);
+    EC_DEV(ok, 2 * B * 8);
+    EC_DEV(oc, 2 * B * 4);
+    EC_DEV(okk, 4 * B * 8);
+    EC_HIP(hipMemcpy(db.p, buf, B, hipMemcpyHostToDevice));
+    k_encode_lmer<<<grid_for(B, 256, 65535), 256>>>(db.as<uint8_t>(), B, L, 0, F.as<unsigned long long>());
+    k_encode_lmer<<<grid_for(B, 256, 65535), 256>>>(db.as<uint8_t>(), B, L, 1, R.as<unsigned long long>());
+    k_streams<<<grid_for(B, 256), 256>>>(F.as<unsigned long long>(), R.as<unsigned long long>(), B, kmask64((int)L - 1),
+                                         S.as<unsigned long long>(), K.as<unsigned long long>());
+    EC_HIP(hipMemset(zc.p, 0, 8));
+    k_count_zero<<<grid_for(2 * B, 256, 4096), 256>>>(S.as<unsigned long long>(), 2 * B, zc.as<unsigned long long>());
+    uint64_t nl = 0, nk = 0, empty = 0;
+    EC_CHECK(unique_first(S.as<unsigned long long>(), 2 * B, 1, ok.as<unsigned long long>(), oc.as<unsigned int>(), &nl));
+    EC_CHECK(unique_first(K.as<unsigned long long>(), 4 * B, 0, okk.as<unsigned long long>(), nullptr, &nk));
+    EC_HIP(hipMemcpy(&empty, zc.p, 8, hipMemcpyDeviceToHost));
+    if (nl) {
+        EC_HIP(hipMemcpy(lmer_keys, ok.p, nl * 8, hipMemcpyDeviceToHost));
+        EC_HIP(hipMemcpy(lmer_values, oc.p, nl * 4, hipMemcpyDeviceToHost));
+    }
+    if (nk) EC_HIP(hipMemcpy(kmer_keys, okk.p, nk * 8, hipMemcpyDeviceToHost));
+    *n_lmers = nl;
+    *n_kmers = nk;
+    *lmer_empty = empty;
+    return EC_OK;
+}
+
+// generatePartialContig (src/eulercuda.py:328-402) on the device for an injective successor
+// map: contig c = chars[coff[c] .. coff[c+1]), the getString(l-1, vid) of every walked edge's
+// source vertex followed by the last edge's target vertex.  chars capacity: 2E(l-1);
+// coff capacity E+1.
+extern "C" int ec_partial_contigs(const void *ev, uint64_t vcount, const void *ee, uint64_t E, uint32_t l, char *chars,
+                                  uint64_t *coff, uint64_t *n_contigs, uint64_t *n_chars) {
+    if (l < 2 || l > 33 || !n_contigs || !n_chars || (E && (!ee || !chars || !coff || !ev))) {
+        set_error("bad arguments (l=%u must be in [2,33])", l);
+        return EC_ERR_ARG;
+    }
+    *n_contigs = *n_chars = 0;
+    if (!E) {
+        if (coff) coff[0] = 0;
+        return EC_OK;
+    }
+    if (E >= (1ull << 31)) {
+        set_error("%llu edges exceed the 2^31 limit", (unsigned long long)E);
+        return EC_ERR_CAPACITY;
+    }
+    const unsigned int km1 = l - 1;
+    EC_DEV(dev, vcount * sizeof(EulerVertex));
+    EC_DEV(dee, E * sizeof(EulerEdge));
+    EC_DEV(pred, E * 4);
+    EC_DEV(indeg, E * 4);
+    EC_DEV(nxt, E * 4);
+    EC_DEV(d, E * 4);
+    EC_DEV(hd, E * 4);
+    EC_DEV(mn, E * 4);
+    EC_DEV(nxt2, E * 4);
+    EC_DEV(d2, E * 4);
+    EC_DEV(hd2, E * 4);
+    EC_DEV(mn2, E * 4);
+    EC_DEV(cmin, E * 4);
+    EC_DEV(key, E * 8);
+    EC_DEV(val, E * 4);
+    EC_DEV(skey, E * 8);
+    EC_DEV(sval, E * 4);
+    EC_DEV(len, E * 8);
+    EC_DEV(pos, E * 8);
+    EC_DEV(start, E * 4);
+    EC_DEV(cidx, E * 4);
+    EC_DEV(bad, 4);
+    if (vcount) EC_HIP(hipMemcpy(dev.p, ev, vcount * sizeof(EulerVertex), hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
+    EC_HIP(hipMemset(pred.p, 0xFF, E * 4));
+    EC_HIP(hipMemset(indeg.p, 0, E * 4));
+    EC_HIP(hipMemset(bad.p, 0, 4));
+    k_pw_pred<<<grid_for(E, 256), 256>>>(dee.as<EulerEdge>(), E, pred.as<unsigned int>(), indeg.as<unsigned int>());
+    {
+        size_t bytes = 0;
+        EC_DEV(mx, 4);
+        EC_HIP(rocprim::reduce(nullptr, bytes, indeg.as<unsigned int>(), mx.as<unsigned int>(), 0u, E,
+                               rocprim::maximum<unsigned int>(), (hipStream_t)0));
+        EC_DEV(tmp, bytes);
+        EC_HIP(rocprim::reduce(tmp.p, bytes, indeg.as<unsigned int>(), mx.as<unsigned int>(), 0u, E,
+                               rocprim::maximum<unsigned int>(), (hipStream_t)0));
+        unsigned int h = 0;
+        EC_HIP(hipMemcpy(&h, mx.p, 4, hipMemcpyDeviceToHost));
+        if (h > 1) {
+            set_error("successor map is not injective (an edge is the successor of %u edges)", h);
+            return EC_ERR_ARG;
+        }
+    }
+    int rounds = 1;
+    while ((1ull << rounds) <= E) rounds++;
+    rounds++;
+    const unsigned int *cut = nullptr;
+    for (int pass = 0; pass < 2; pass++) {
+        k_pw_init<<<grid_for(E, 256), 256>>>(pred.as<unsigned int>(), cut, E, nxt.as<unsigned int>(), d.as<unsigned int>(),
+                                             hd.as<unsigned int>(), mn.as<unsigned int>());
+        unsigned int *a[4] = {nxt.as<unsigned int>(), d.as<unsigned int>(), hd.as<unsigned int>(), mn.as<unsigned int>()};
+        unsigned int *b[4] = {nxt2.as<unsigned int>(), d2.as<unsigned int>(), hd2.as<unsigned int>(), mn2.as<unsigned int>()};
+        for (int r = 0; r < rounds; r++) {
+            k_pw_jump<<<grid_for(E, 256), 256>>>(a[0], a[1], a[2], a[3], E, b[0], b[1], b[2], b[3]);
+            for (int q = 0; q < 4; q++) std::swap(a[q], b[q]);
+        }
+        if (pass == 0) {
+            k_pw_cycmin<<<grid_for(E, 256), 256>>>(a[0], a[3], E, cmin.as<unsigned int>());
+            cut = cmin.as<unsigned int>();
+        } else {
+            k_pw_keys<<<grid_for(E, 256), 256>>>(cmin.as<unsigned int>(), a[2], a[1], E, key.as<unsigned long long>(),
+                                                 val.as<unsigned int>());
+        }
+    }
+    {
+        size_t bytes = 0;
+        EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, key.as<unsigned long long>(), skey.as<unsigned long long>(),
+                                         val.as<unsigned int>(), sval.as<unsigned int>(), E, 0, 64, (hipStream_t)0));
+        EC_DEV(tmp, bytes);
+        EC_HIP(rocprim::radix_sort_pairs(tmp.p, bytes, key.as<unsigned long long>(), skey.as<unsigned long long>(),
+                                         val.as<unsigned int>(), sval.as<unsigned int>(), E, 0, 64, (hipStream_t)0));
+    }
+    k_pw_len<<<grid_for(E, 256), 256>>>(skey.as<unsigned long long>(), E, km1, len.as<unsigned long long>(),
+                                        start.as<unsigned int>());
+    {
+        size_t bytes = 0;
+        EC_HIP(rocprim::exclusive_scan(nullptr, bytes, len.as<unsigned long long>(), pos.as<unsigned long long>(), 0ull, E,
+                                       rocprim::plus<unsigned long long>(), (hipStream_t)0));
+        EC_DEV(tmp, bytes);
+        EC_HIP(rocprim::exclusive_scan(tmp.p, bytes, len.as<unsigned long long>(), pos.as<unsigned long long>(), 0ull, E,
+                                       rocprim::plus<unsigned long long>(), (hipStream_t)0));
+        bytes = 0;
+        EC_HIP(rocprim::inclusive_scan(nullptr, bytes, start.as<unsigned int>(), cidx.as<unsigned int>(), E,
+                                       rocprim::plus<unsigned int>(), (hipStream_t)0));
+        EC_DEV(tmp2, bytes);
+        EC_HIP(rocprim::inclusive_scan(tmp2.p, bytes, start.as<unsigned int>(), cidx.as<unsigned int>(), E,
+                                       rocprim::plus<unsigned int>(), (hipStream_t)0));
+    }
+    unsigned long long lastpos = 0, lastlen = 0;
+    unsigned int nc = 0;
+    EC_HIP(hipMemcpy(&lastpos, pos.as<unsigned long long>() + (E - 1), 8, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(&lastlen, len.as<unsigned long long>() + (E - 1), 8, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(&nc, cidx.as<unsigned int>() + (E - 1), 4, hipMemcpyDeviceToHost));
+    const uint64_t total = lastpos + lastlen;
+    EC_DEV(dchars, total);
+    EC_DEV(dcoff, (nc + 1ull) * 8);
+    k_pw_emit<<<grid_for(E, 256), 256>>>(skey.as<unsigned long long>(), sval.as<unsigned int>(),
+                                         pos.as<unsigned long long>(), cidx.as<unsigned int>(), E, dee.as<EulerEdge>(),
+                                         dev.as<EulerVertex>(), vcount, km1, dchars.as<char>(),
+                                         dcoff.as<unsigned long long>(), bad.as<unsigned int>());
+    unsigned int hb = 0;
+    EC_HIP(hipMemcpy(&hb, bad.p, 4, hipMemcpyDeviceToHost));
+    if (hb) {
+        set_error("an edge names a vertex outside ev[0..%llu)", (unsigned long long)vcount);
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipMemcpy(chars, dchars.p, total, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(coff, dcoff.p, nc * 8ull, hipMemcpyDeviceToHost));
+    coff[nc] = total;
+    *n_contigs = nc;
+    *n_chars = total;
+    return EC_OK;
+}

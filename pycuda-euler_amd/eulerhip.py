@@ -91,6 +91,7 @@ _SIGS = {
     "ec_session_destroy": (ctypes.c_int, [_P]),
     "ec_assemble_device": (ctypes.c_int, [_P, _P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_assemble_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
+    "ec_assemble_from_kmers": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _U64, ctypes.c_int, ctypes.c_uint]),
     "ec_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
     "ec_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
     "ec_copy_contigs": (ctypes.c_int, [_P, _P, _P]),
@@ -272,6 +273,19 @@ class Session:
         flags |= EC_FLAG_GENERAL if general else 0
         self.run_host(buf, off, k, limit, flags)
         return self.fetch(k, want_dict)
+
+    def assemble_dict(self, d, k):
+        """all_contigs on a caller's dict {k-mer: count} (dict order matters): the graph phase
+        of the fused path, on the device (ec_assemble_from_kmers)."""
+        items = list(d.items())
+        n = len(items)
+        for x, _ in items:
+            if len(x) != k:
+                raise EulerHipError(EC_ERR_ARG, "dict key %r is not a %d-mer" % (x, k))
+        km = "".join(x for x, _ in items).encode("ascii")
+        cnt = np.array([c for _, c in items], dtype=np.uint32) if n else np.zeros(1, np.uint32)
+        check(lib().ec_assemble_from_kmers(self._h, km, cnt.ctypes.data, n, int(k), 0))
+        return self.fetch(k)
 
 
 _default = {}
