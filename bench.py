@@ -80,7 +80,7 @@ def cpu_baseline(buf, off, k, sample_reads):
 
 
 def load_traffic(workload, kernel):
-    """HBM bytes per count-kernel launch from rocprofv3 PMC passes (profiles/traffic_*.json,
+    """HBM bytes per launch of `kernel` from rocprofv3 PMC passes (profiles/traffic_*.json,
     written by profiles/collect_traffic.py; FETCH_SIZE doubled per the gfx950 note)."""
     import glob
 
@@ -88,10 +88,11 @@ def load_traffic(workload, kernel):
     for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic_*.json"))):
         try:
             d = json.load(open(fn))
-        except Exception:
+        except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and d.get("kernel") == kernel and d.get("kernel_bytes_per_launch"):
-            best = d
+        kd = d.get("kernels", {}).get(kernel)
+        if d.get("workload") == workload and kd and kd.get("kernel_bytes_per_launch"):
+            best = dict(kd, file=os.path.basename(fn))
     return best
 
 
@@ -195,6 +196,7 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": (tr["kernel_bytes_per_launch"] if tr else None),
+            "traffic_source": (tr["file"] if tr else None),
             "kernel": kname, "kernel_ms": round(kms, 4), "alg_bytes_per_launch": int(kb),
             "kernels_ms": {eulerhip.KERNEL_NAMES[i]: round(float(kern[i]), 4) for i in range(len(kern))},
             "pipeline_alg_bytes": int(alg_bytes(P, R, L, U)),

@@ -92,7 +92,7 @@ struct ec_session {
     bool timing = false;
     unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
-    DevBuf ocnt;
+    DevBuf ocnt, rbc;
 };
 
 namespace ec {
@@ -151,6 +151,14 @@ int scan_u64(ec_session *s, const unsigned long long *in, unsigned long long *ou
     EC_HIP(rocprim::exclusive_scan(nullptr, bytes, in, out, 0ull, n, rocprim::plus<unsigned long long>(), s->stream));
     EC_CHECK(s->tmp.ensure(bytes));
     EC_HIP(rocprim::exclusive_scan(s->tmp.p, bytes, in, out, 0ull, n, rocprim::plus<unsigned long long>(), s->stream));
+    return EC_OK;
+}
+
+int scan_incl_u32(ec_session *s, const unsigned int *in, unsigned int *out, size_t n) {
+    size_t bytes = 0;
+    EC_HIP(rocprim::inclusive_scan(nullptr, bytes, in, out, n, rocprim::plus<unsigned int>(), s->stream));
+    EC_CHECK(s->tmp.ensure(bytes));
+    EC_HIP(rocprim::inclusive_scan(s->tmp.p, bytes, in, out, n, rocprim::plus<unsigned int>(), s->stream));
     return EC_OK;
 }
 
@@ -498,6 +506,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
     EC_CHECK(s->rid.ensure(Nn * 4));
     EC_CHECK(s->roff.ensure(Nn * 4));
     EC_CHECK(s->rlist.ensure(Nn * 4));
+    EC_CHECK(s->rbc.ensure(((Nn + RULER_CHUNK - 1) / RULER_CHUNK) * 8));
     EC_CHECK(s->nextR.ensure(Nn * 4));
     EC_CHECK(s->st0.ensure(Nn * sizeof(RJump)));
     EC_CHECK(s->st1.ensure(Nn * sizeof(RJump)));
@@ -513,9 +522,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
         const unsigned int masks[4] = {31u, 7u, 1u, 0u};
         unsigned int r0 = 0;
         for (int it = 0; it < 4; it++) {
-            k_rulers<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it],
-                                                  it == 0, s->rid.as<unsigned int>(), s->roff.as<unsigned int>(),
-                                                  s->rlist.as<unsigned int>(), &dsc->nr);
+            const unsigned int nblk = (unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK);
+            k_rulers_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it], it == 0,
+                                               s->rid.as<unsigned int>(), s->rbc.as<unsigned int>());
+            EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
+            k_rulers<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it], it == 0,
+                                         s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<unsigned int>(),
+                                         s->roff.as<unsigned int>(), s->rlist.as<unsigned int>());
+            k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
             k_walk<<<2048, B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
                                       s->dft.as<unsigned long long>(), s->rlist.as<unsigned int>(), r0, &dsc->nr,
                                       masks[it], s->rid.as<unsigned int>(), s->roff.as<unsigned int>(),
@@ -712,7 +726,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
-                     &s->ocnt, &s->hist, &s->ftot, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub};
+                     &s->ocnt, &s->hist, &s->ftot, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc};
     for (auto *b : all) b->release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);

@@ -122,23 +122,61 @@ __device__ inline bool ruler_hash(unsigned int x, unsigned int smask) {
     return (mix64(0x9E3779B97F4A7C15ull ^ x) & smask) == 0;
 }
 
+// Ruler selection in two passes with one scan in between (deterministic ruler order, no
+// contended counter): RULER_CHUNK nodes per block.
+constexpr unsigned int RULER_CHUNK = 4096;
+
+__device__ inline bool ruler_sel(const uint8_t *upal, const unsigned int *pred, const unsigned int *rid, unsigned int x,
+                                 unsigned int smask, int first) {
+    if (((x & 1) && upal[x >> 1]) || rid[x] != NONE32) return false;
+    return (first && pred[x] == NONE32) || ruler_hash(x, smask);
+}
+
+__global__ void __launch_bounds__(256) k_rulers_count(const uint8_t *upal, const unsigned int *pred, unsigned int N,
+                                                      unsigned int smask, int first, const unsigned int *rid,
+                                                      unsigned int *bc) {
+    const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
+    const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
+    unsigned int c = 0;
+    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) c += ruler_sel(upal, pred, rid, (unsigned int)t, smask, first);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    __shared__ unsigned int w[4];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bc[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+}
+
+// bs = inclusive scan of bc; new rulers get ids nr + bs[b-1] + (rank in chunk)
 __global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsigned int *pred, unsigned int N,
-                                                unsigned int smask, int first, unsigned int *rid, unsigned int *roff,
-                                                unsigned int *rlist, unsigned int *nr) {
-    for (uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x; t0 < N; t0 += (uint64_t)gridDim.x * blockDim.x) {
+                                                unsigned int smask, int first, const unsigned int *bs,
+                                                const unsigned int *nr, unsigned int *rid, unsigned int *roff,
+                                                unsigned int *rlist) {
+    __shared__ unsigned int wsum[4];
+    const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
+    const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
+    unsigned int base = *nr + (blockIdx.x ? bs[blockIdx.x - 1] : 0u);
+    const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
         const uint64_t t = t0 + threadIdx.x;
-        const unsigned int x = (unsigned int)t;
-        bool sel = false;
-        if (t < N && !((x & 1) && upal[x >> 1]) && rid[x] == NONE32)
-            sel = (first && pred[x] == NONE32) || ruler_hash(x, smask);
-        const unsigned int i = wave_append(nr, sel);
+        const bool sel = t < c1 && ruler_sel(upal, pred, rid, (unsigned int)t, smask, first);
+        const unsigned long long m = __ballot(sel);
+        if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
+        __syncthreads();
+        unsigned int off = base;
+        for (unsigned int q = 0; q < wid; q++) off += wsum[q];
+        const unsigned int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
         if (sel) {
-            rlist[i] = x;
-            rid[x] = i;
-            roff[x] = 0;
+            const unsigned int i = off + (unsigned int)__popcll(m & ((1ull << lane) - 1));
+            rlist[i] = (unsigned int)t;
+            rid[t] = i;
+            roff[t] = 0;
         }
+        base += tot;
+        __syncthreads();
     }
 }
+
+__global__ void k_rulers_total(const unsigned int *bs, unsigned int nblk, unsigned int *nr) { *nr += bs[nblk - 1]; }
 
 // ruler jump state (32 B): window = rulers i, P(i), .., P^{c-1}(i)
 struct alignas(32) RJump {
@@ -224,8 +262,9 @@ __global__ void __launch_bounds__(256) k_rjump(const RJump *src, RJump *dst, uns
         }
         dst[t] = j;
     }
-    for (int o = 32; o > 0; o >>= 1) act += __shfl_down(act, o);
-    if ((threadIdx.x & 63) == 0 && act) atomicAdd(active_out, act);
+    // one flag store per block that still has live pointers (a per-wave atomic on one word
+    // serialises at the memory side: ~4.5K waves cost ~50 us per round)
+    if (__syncthreads_or(act != 0) && threadIdx.x == 0) *active_out = 1u;
     if (blockIdx.x == 0 && threadIdx.x == 0) *final_sel = sel;
 }
 
