@@ -207,6 +207,26 @@ int ec_read_lmers_kmers(const uint8_t *buf, uint64_t B, uint32_t L, uint64_t *lm
 int ec_partial_contigs(const void *ev, uint64_t vcount, const void *ee, uint64_t E, uint32_t l, char *chars,
                        uint64_t *coff, uint64_t *n_contigs, uint64_t *n_chars);
 
+/* ---- native read ingest -----------------------------------------------
+ * FASTA / FASTQ file -> packed bases + uint64 offsets (the CSR layout ec_assemble_* takes).
+ * EC_FASTA_RECORDS: one read per '>' record, lines stripped and joined (SeqIO parse of
+ *   tests/referenceAssembler.py:28; src/fastareader/parse_fasta.py:32-45; src/readTest.c:9-50);
+ * EC_FASTA_LINES: one read per non-header line, stripped (read_fasta, src/eulercuda.py:437-445);
+ * EC_FASTQ: line 1 of every 4-line record (read_fastq, src/eulercuda.py:43-55; a trailing '\r'
+ *   is dropped).  threads <= 0: up to 16 host threads. */
+#define EC_FASTA_RECORDS 0
+#define EC_FASTA_LINES 1
+#define EC_FASTQ 2
+typedef struct ec_reads ec_reads;
+int ec_reads_load(const char *path, int format, int threads, ec_reads **out);
+uint64_t ec_reads_count(const ec_reads *r);
+uint64_t ec_reads_bases(const ec_reads *r);
+/* bases held by reads [first, first+count) (0 for a bad range) */
+uint64_t ec_reads_span(const ec_reads *r, uint64_t first, uint64_t count);
+/* copy reads [first, first+count): their bases and count+1 offsets rebased to 0 */
+int ec_reads_copy(const ec_reads *r, uint64_t first, uint64_t count, uint8_t *bases, uint64_t *offsets);
+void ec_reads_free(ec_reads *r);
+
 /* ---- read-sharded multi-GPU building blocks (pycuda-euler_amd/distributed.py) ------------
  * Replace the reference's distribution layer (Spark mapPartitions of assemble2,
  * src/cli_spark_gpu.py:37, and the reduceByKey k-mer shuffle of src/ref_spark.py:83-84) with

@@ -481,7 +481,6 @@ int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
     EC_HIP(hipStreamSynchronize(st));
     const unsigned int N = 2 * U;
     const size_t Nn = std::max<size_t>(N, 1);
-    const bool timing = s->timing;
 
     // ---- links ----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_LINKS);

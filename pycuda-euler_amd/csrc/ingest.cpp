@@ -1,0 +1,298 @@
+// ingest.cpp -- native read ingest: FASTA / FASTQ file -> one packed
+// base buffer + uint64 offsets (CSR), the input layout of ec_assemble_* and ec_count_shard.
+//
+// Semantics follow the reference's readers:
+//   EC_FASTA_RECORDS  one read per '>' record, sequence lines stripped and joined -- the
+//                     SeqIO parse of tests/referenceAssembler.py:28, src/fastareader/parse_fasta.py:32-45
+//                     and src/readTest.c:9-50 (text before the first header is ignored);
+//   EC_FASTA_LINES    one read per non-header line, stripped (empty lines give empty reads) --
+//                     read_fasta, src/eulercuda.py:437-445;
+//   EC_FASTQ          the sequence line of every 4-line record -- read_fastq, src/eulercuda.py:43-55.
+// "stripped" = leading / trailing ASCII whitespace removed (Python str.strip()).
+//
+// The file is memory-mapped and parsed by T threads over byte ranges in two passes (count,
+// then copy at prefix-summed offsets), so a multi-GB read set is ingested at memory speed.
+#include "common.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+using ec::set_error;
+
+struct ec_reads {
+    std::vector<uint8_t> bases;
+    std::vector<uint64_t> offsets;  // n_reads + 1
+};
+
+namespace {
+
+inline bool is_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
+
+// [b, e) of line content after strip()
+inline void strip(const uint8_t *p, uint64_t &b, uint64_t &e) {
+    while (b < e && is_ws(p[b])) b++;
+    while (e > b && is_ws(p[e - 1])) e--;
+}
+
+struct Chunk {
+    uint64_t lo = 0, hi = 0;       // byte range [lo, hi), starts at a line start
+    uint64_t lines_before = 0;     // FASTQ: global index of the first line of the chunk
+    uint64_t reads = 0, bases = 0; // pass-1 counts
+};
+
+// visit the lines of [lo, hi): fn(line_begin, line_end_excl_newline)
+template <typename Fn>
+void for_lines(const uint8_t *p, uint64_t lo, uint64_t hi, Fn fn) {
+    uint64_t s = lo;
+    while (s < hi) {
+        const void *nl = memchr(p + s, '\n', hi - s);
+        const uint64_t e = nl ? (uint64_t)((const uint8_t *)nl - p) : hi;
+        fn(s, e);
+        s = e + 1;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
+    if (!path || !out || format < EC_FASTA_RECORDS || format > EC_FASTQ) {
+        set_error("bad arguments");
+        return EC_ERR_ARG;
+    }
+    *out = nullptr;
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) {
+        set_error("cannot open %s", path);
+        return EC_ERR_ARG;
+    }
+    struct stat stt;
+    if (fstat(fd, &stt) != 0) {
+        close(fd);
+        set_error("cannot stat %s", path);
+        return EC_ERR_ARG;
+    }
+    const uint64_t n = (uint64_t)stt.st_size;
+    const uint8_t *p = nullptr;
+    if (n) {
+        void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) {
+            close(fd);
+            set_error("mmap of %s failed", path);
+            return EC_ERR_NOMEM;
+        }
+        madvise(m, n, MADV_SEQUENTIAL);
+        p = static_cast<const uint8_t *>(m);
+    }
+    close(fd);
+    ec_reads *r = new (std::nothrow) ec_reads();
+    if (!r) {
+        if (p) munmap((void *)p, n);
+        set_error("out of host memory");
+        return EC_ERR_NOMEM;
+    }
+    int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < (1u << 20)) T = 1;
+    // chunk boundaries at line starts
+    std::vector<Chunk> ch(T);
+    for (int t = 0; t < T; t++) {
+        uint64_t lo = n * (uint64_t)t / T;
+        if (t) {
+            while (lo < n && p[lo - 1] != '\n') lo++;
+        }
+        ch[t].lo = lo;
+    }
+    for (int t = 0; t < T; t++) ch[t].hi = t + 1 < T ? ch[t + 1].lo : n;
+
+    // pass 1: counts (and FASTQ line counts)
+    auto pass1 = [&](int t) {
+        Chunk &c = ch[t];
+        if (format == EC_FASTQ) {
+            uint64_t lines = 0;
+            for_lines(p, c.lo, c.hi, [&](uint64_t, uint64_t) { lines++; });
+            c.reads = lines;  // temporarily: line count
+        } else if (format == EC_FASTA_LINES) {
+            for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
+                if (b < e && p[b] == '>') return;
+                strip(p, b, e);
+                c.reads++;
+                c.bases += e - b;
+            });
+        } else {
+            for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
+                if (b < e && p[b] == '>') {
+                    c.reads++;
+                    return;
+                }
+                strip(p, b, e);
+                c.bases += e - b;  // bases before the chunk's first header are resolved below
+            });
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; t++) th.emplace_back(pass1, t);
+        pass1(0);
+        for (auto &x : th) x.join();
+    }
+    if (format == EC_FASTQ) {
+        uint64_t lines = 0;
+        for (auto &c : ch) {
+            c.lines_before = lines;
+            lines += c.reads;
+        }
+        // file ends without a trailing newline-only line: a partial last record still counts
+        // its sequence line (read_fastq yields every line with index % 4 == 1)
+        for (auto &c : ch) {
+            c.reads = 0;
+            c.bases = 0;
+        }
+        auto pass1b = [&](int t) {
+            Chunk &c = ch[t];
+            uint64_t li = c.lines_before;
+            for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
+                if (li % 4 == 1) {
+                    if (e > b && p[e - 1] == '\r') e--;  // rstrip('\n') of a CRLF line keeps '\r'; drop it
+                    c.reads++;
+                    c.bases += e - b;
+                }
+                li++;
+            });
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; t++) th.emplace_back(pass1b, t);
+        pass1b(0);
+        for (auto &x : th) x.join();
+    }
+    // FASTA records: sequence bytes before a chunk's first header belong to the previous
+    // chunk's last record (or to no record at the file start)
+    std::vector<uint64_t> lead(T, 0);
+    if (format == EC_FASTA_RECORDS) {
+        auto lead_of = [&](int t) {  // stripped bytes before the chunk's first header
+            uint64_t sum = 0, q = ch[t].lo;
+            while (q < ch[t].hi) {
+                const void *nl = memchr(p + q, '\n', ch[t].hi - q);
+                uint64_t e = nl ? (uint64_t)((const uint8_t *)nl - p) : ch[t].hi;
+                if (q < e && p[q] == '>') break;
+                uint64_t b = q;
+                const uint64_t next = e + 1;
+                strip(p, b, e);
+                sum += e - b;
+                q = next;
+            }
+            lead[t] = sum;
+        };
+        for (int t = 0; t < T; t++) lead_of(t);
+        // chunk t's leading bytes: counted by chunk t, belong to the last record before it
+        bool any_header_before = false;
+        for (int t = 0; t < T; t++) {
+            if (!any_header_before) ch[t].bases -= lead[t];  // no record yet: ignored text
+            any_header_before |= ch[t].reads > 0;
+        }
+    }
+    uint64_t R = 0, B = 0;
+    std::vector<uint64_t> r0(T), b0(T);
+    for (int t = 0; t < T; t++) {
+        r0[t] = R;
+        b0[t] = B;
+        R += ch[t].reads;
+        B += ch[t].bases;
+    }
+    try {
+        r->bases.resize(std::max<uint64_t>(B, 1));
+        r->offsets.resize(R + 1);
+    } catch (...) {
+        delete r;
+        if (p) munmap((void *)p, n);
+        set_error("out of host memory (%llu reads, %llu bases)", (unsigned long long)R, (unsigned long long)B);
+        return EC_ERR_NOMEM;
+    }
+    uint8_t *ob = r->bases.data();
+    uint64_t *oo = r->offsets.data();
+    // pass 2: copy.  Record reads get offsets[i] at their header; their bytes follow contiguously
+    // across chunk boundaries because b0 is a prefix sum in file order.
+    auto pass2 = [&](int t) {
+        const Chunk &c = ch[t];
+        uint64_t ri = r0[t], bi = b0[t];
+        if (format == EC_FASTQ) {
+            uint64_t li = c.lines_before;
+            for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
+                if (li % 4 == 1) {
+                    if (e > b && p[e - 1] == '\r') e--;
+                    oo[ri++] = bi;
+                    memcpy(ob + bi, p + b, e - b);
+                    bi += e - b;
+                }
+                li++;
+            });
+        } else if (format == EC_FASTA_LINES) {
+            for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
+                if (b < e && p[b] == '>') return;
+                strip(p, b, e);
+                oo[ri++] = bi;
+                memcpy(ob + bi, p + b, e - b);
+                bi += e - b;
+            });
+        } else {
+            const bool owned_lead = ri > 0;  // leading bytes continue the previous record
+            bool in_lead = true;
+            for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
+                if (b < e && p[b] == '>') {
+                    in_lead = false;
+                    oo[ri++] = bi;
+                    return;
+                }
+                if (in_lead && !owned_lead) return;
+                strip(p, b, e);
+                memcpy(ob + bi, p + b, e - b);
+                bi += e - b;
+            });
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; t++) th.emplace_back(pass2, t);
+        pass2(0);
+        for (auto &x : th) x.join();
+    }
+    oo[R] = B;
+    if (p) munmap((void *)p, n);
+    *out = r;
+    return EC_OK;
+}
+
+uint64_t ec_reads_count(const ec_reads *r) { return r ? r->offsets.size() - 1 : 0; }
+
+uint64_t ec_reads_bases(const ec_reads *r) { return r ? r->offsets.back() : 0; }
+
+uint64_t ec_reads_span(const ec_reads *r, uint64_t first, uint64_t count) {
+    if (!r || first + count > r->offsets.size() - 1) return 0;
+    return r->offsets[first + count] - r->offsets[first];
+}
+
+int ec_reads_copy(const ec_reads *r, uint64_t first, uint64_t count, uint8_t *bases, uint64_t *offsets) {
+    if (!r || first + count > r->offsets.size() - 1 || (count && !offsets)) {
+        set_error("bad shard [%llu, +%llu)", (unsigned long long)first, (unsigned long long)count);
+        return EC_ERR_ARG;
+    }
+    const uint64_t b0 = r->offsets[first], b1 = r->offsets[first + count];
+    if (b1 > b0 && !bases) {
+        set_error("null base buffer");
+        return EC_ERR_ARG;
+    }
+    if (b1 > b0) memcpy(bases, r->bases.data() + b0, b1 - b0);
+    for (uint64_t i = 0; i <= count; i++) offsets[i] = r->offsets[first + i] - b0;
+    return EC_OK;
+}
+
+void ec_reads_free(ec_reads *r) { delete r; }
+
+}  // extern "C"

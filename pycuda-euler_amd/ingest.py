@@ -1,0 +1,118 @@
+"""ingest -- native FASTA / FASTQ ingest and contig / GFA writers (row 2).
+
+ReadSet parses a read file with the multi-threaded C++ reader of libeulerhip.so
+(csrc/ingest.cpp: mmap + two-pass parallel parse) straight into the packed CSR layout the
+device path consumes (uint8 bases + uint64 offsets); packed(first, count) hands out one
+rank's shard.  The writers emit the reference's output formats from a Result.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+import eulerhip
+
+FASTA_RECORDS, FASTA_LINES, FASTQ = 0, 1, 2
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+eulerhip.register("ec_reads_load", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)])
+eulerhip.register("ec_reads_count", _U64, [_P])
+eulerhip.register("ec_reads_bases", _U64, [_P])
+eulerhip.register("ec_reads_span", _U64, [_P, _U64, _U64])
+eulerhip.register("ec_reads_copy", ctypes.c_int, [_P, _U64, _U64, _P, _P])
+eulerhip.register("ec_reads_free", None, [_P])
+
+
+def detect_format(path, fasta_mode="records"):
+    """FASTQ for .fq/.fastq (or a leading '@'), else FASTA as records or lines."""
+    fasta = FASTA_LINES if fasta_mode == "lines" else FASTA_RECORDS
+    ext = path.rsplit(".", 1)[-1].lower()
+    if ext in ("fq", "fastq"):
+        return FASTQ
+    if ext in ("fa", "fasta", "fsa", "fna"):
+        return fasta
+    with open(path, "rb") as f:
+        return FASTQ if f.read(1) == b"@" else fasta
+
+
+class ReadSet:
+    """A read file parsed by the native reader (host memory, freed on close)."""
+
+    def __init__(self, path, fmt=None, threads=0, fasta_mode="records"):
+        self.path = path
+        self.format = detect_format(path, fasta_mode) if fmt is None else fmt
+        h = _P()
+        eulerhip.check(eulerhip.lib().ec_reads_load(os.fsencode(path), int(self.format), int(threads), ctypes.byref(h)))
+        self._h = h
+
+    def __len__(self):
+        return int(eulerhip.lib().ec_reads_count(self._h))
+
+    @property
+    def n_bases(self):
+        return int(eulerhip.lib().ec_reads_bases(self._h))
+
+    def packed(self, first=0, count=None):
+        """(bases uint8[], offsets uint64[count + 1]) of reads [first, first + count)."""
+        n = len(self)
+        count = n - first if count is None else int(count)
+        nb = int(eulerhip.lib().ec_reads_span(self._h, int(first), count))
+        buf = np.zeros(max(nb, 1), np.uint8)
+        off = np.zeros(count + 1, np.uint64)
+        eulerhip.check(eulerhip.lib().ec_reads_copy(self._h, int(first), count, buf.ctypes.data, off.ctypes.data))
+        return buf[:nb], off
+
+    def reads(self):
+        """the reads as Python strings (small inputs / tests)"""
+        buf, off = self.packed()
+        s = buf.tobytes().decode("ascii", errors="replace")
+        return [s[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            eulerhip.lib().ec_reads_free(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        self.close()
+
+
+def load_reads(path, fmt=None, threads=0, fasta_mode="records", first=0, count=None):
+    """(bases, offsets) of a read file (or of reads [first, first + count))."""
+    with ReadSet(path, fmt, threads, fasta_mode) as rs:
+        return rs.packed(first, count)
+
+
+# ---- writers ---------------------------------------------------------------
+def write_contigs_fasta(path, result, header="contig%d", blank_line=False):
+    """Contigs of a Result as FASTA: header 'contig%d' with a blank line = print_dbg
+    (tests/referenceAssembler.py:131-134); header '%u' = generatePartialContig / assemble2
+    (src/eulercuda.py:352)."""
+    ch = result.contig_bytes
+    o = result.contig_offsets
+    with open(path, "wb") as f:
+        for i in range(len(o) - 1):
+            f.write(b">" + (header % i).encode() + b"\n")
+            f.write(ch[int(o[i]):int(o[i + 1])])
+            f.write(b"\n\n" if blank_line else b"\n")
+
+
+def write_gfa(path, result, k):
+    """GFA 1 of a Result: print_GFA (tests/referenceAssembler.py:119-129)."""
+    ch = result.contig_bytes
+    o = result.contig_offsets
+    lo, lk = result.link_offsets, result.link_codes
+    with open(path, "w") as f:
+        f.write("H  VN:Z:1.0\n")
+        for i in range(len(o) - 1):
+            f.write("S\t%d\t%s\t*\n" % (i, ch[int(o[i]):int(o[i + 1])].decode("ascii")))
+        for i in range(len(o) - 1):
+            for side, sgn in ((0, "+"), (1, "-")):
+                for v in lk[int(lo[2 * i + side]):int(lo[2 * i + side + 1])]:
+                    f.write("L\t%d\t%s\t%d\t%s\t%dM\n" % (i, sgn, int(v) >> 1, "-" if v & 1 else "+", k - 1))

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 def test_binding_signatures_cover_header():
     import importlib
     import eulerhip
-    for m in ("pyencode", "pygpuhash", "pydebruijn", "pycomponent", "pyeulertour", "distributed"):
+    for m in ("pyencode", "pygpuhash", "pydebruijn", "pycomponent", "pyeulertour", "distributed", "eulercuda", "ingest"):
         if os.path.exists(os.path.join(PKG, m + ".py")):
             importlib.import_module(m)  # registers the module's symbols
     assert set(declared_functions()) <= set(eulerhip._SIGS), set(declared_functions()) - set(eulerhip._SIGS)

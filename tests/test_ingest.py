@@ -1,0 +1,106 @@
+"""Native ingest (csrc/ingest.cpp, host code: runs without a GPU) against the reference's
+Python readers restated in eulercuda.py / assembler.py, incl. multi-threaded chunking."""
+import os
+
+import numpy as np
+import pytest
+
+import assembler
+import eulercuda
+import ingest
+from conftest import GOLDEN
+
+
+def _reads(path, fmt, threads=0):
+    with ingest.ReadSet(str(path), fmt, threads) as rs:
+        out = rs.reads()
+        assert rs.n_bases == sum(len(r) for r in out)
+        return out
+
+
+def test_g200():
+    p = os.path.join(GOLDEN, "g200reads.fa")
+    assert _reads(p, ingest.FASTA_RECORDS) == assembler.read_fasta_records(p)
+    assert _reads(p, ingest.FASTA_LINES) == eulercuda.read_fasta(p)
+
+
+EDGE = [
+    "",
+    "\n",
+    ">only\n",
+    ">a\nACGT\n>b\n\n>c\nAC\nGT\n  TT  \n",
+    "junk before\n>a\nAC\r\nGT\r\n>b\nNNNN",
+    ">a\n\n\nACG\n>b\n>c\nT\n",
+    "ACGT\nGGCC\n",
+]
+
+
+@pytest.mark.parametrize("text", EDGE)
+def test_fasta_edge_cases(tmp_path, text):
+    p = tmp_path / "x.fa"
+    p.write_text(text)
+    assert _reads(p, ingest.FASTA_RECORDS) == assembler.read_fasta_records(str(p))
+    assert _reads(p, ingest.FASTA_LINES) == eulercuda.read_fasta(str(p))
+
+
+def test_fastq(tmp_path):
+    p = tmp_path / "r.fastq"
+    p.write_text("@r1\nACGT\n+\n@@@@\n@r2\nGGCN\n+\nIIII\n@r3\nTT")
+    assert _reads(p, ingest.FASTQ) == eulercuda.read_fastq(str(p)) == ["ACGT", "GGCN", "TT"]
+
+
+@pytest.mark.parametrize("threads", [1, 3, 7, 16])
+def test_large_multithreaded(tmp_path, threads):
+    """~3 MB files split into many chunks: records spanning chunk boundaries, FASTQ line
+    numbering across chunks, quality lines starting with '@' or '>'."""
+    rng = np.random.default_rng(threads)
+    recs = []
+    for i in range(6000):
+        n = int(rng.integers(0, 700))
+        recs.append("".join(rng.choice(list("ACGTN"), n)))
+    fa = tmp_path / "big.fa"
+    with open(fa, "w") as f:
+        for i, r in enumerate(recs):
+            f.write(">r%d\n" % i)
+            for j in range(0, len(r), 61):
+                f.write(r[j:j + 61] + ("\n" if i % 5 else "\r\n"))
+    assert _reads(fa, ingest.FASTA_RECORDS, threads) == assembler.read_fasta_records(str(fa))
+    assert _reads(fa, ingest.FASTA_LINES, threads) == eulercuda.read_fasta(str(fa))
+    fq = tmp_path / "big.fastq"
+    with open(fq, "w") as f:
+        for i, r in enumerate(recs):
+            f.write("@r%d\n%s\n+\n%s\n" % (i, r, ("@>" * len(r))[:len(r)]))
+    assert _reads(fq, ingest.FASTQ, threads) == eulercuda.read_fastq(str(fq)) == recs
+
+
+def test_shards(tmp_path):
+    p = os.path.join(GOLDEN, "g200reads.fa")
+    with ingest.ReadSet(p) as rs:
+        allr = rs.reads()
+        buf, off = rs.packed()
+        assert off[0] == 0 and int(off[-1]) == len(buf) == rs.n_bases
+        got = []
+        for first, count in [(0, 30), (30, 0), (30, 41), (71, len(rs) - 71)]:
+            b, o = rs.packed(first, count)
+            s = b.tobytes().decode()
+            got += [s[int(o[i]):int(o[i + 1])] for i in range(count)]
+        assert got == allr
+        import eulerhip
+
+        with pytest.raises(eulerhip.EulerHipError):
+            rs.packed(50, len(rs))
+
+
+def test_missing_file(tmp_path):
+    import eulerhip
+
+    with pytest.raises(eulerhip.EulerHipError):
+        ingest.ReadSet(str(tmp_path / "nope.fa"))
+
+
+def test_detect_format(tmp_path):
+    a = tmp_path / "reads.txt"
+    a.write_text("@r\nAC\n+\nII\n")
+    assert ingest.detect_format(str(a)) == ingest.FASTQ
+    assert ingest.detect_format("x.fna") == ingest.FASTA_RECORDS
+    assert ingest.detect_format("x.fa", "lines") == ingest.FASTA_LINES
