@@ -38,7 +38,7 @@ extern "C" {
 #define EC_ERR_CAPACITY (-5) /* table overflow that survived the retries                       */
 #define EC_ERR_STATE (-6)    /* result requested before a successful ec_assemble_*            */
 
-#define EC_MAX_K 32 /* fused path: k <= 32 (64-bit keys) */
+#define EC_MAX_K 63 /* k <= 32: 64-bit keys; 32 < k <= 63: 128-bit keys (general table) */
 
 const char *ec_last_error(void);
 int ec_version(void); /* major*10000 + minor*100 + patch */
@@ -257,6 +257,9 @@ int ec_export_dense(ec_session *s, void *d_out);
  * with its twin, as build() returns it.  Results via ec_copy_contigs / ec_copy_links. */
 int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *counts, uint64_t n, int k,
                            unsigned flags);
+/* bytes per exchange record for node length k: 32 (ec_kmer_record, k <= 32) or 48
+ * (ec_kmer_record_wide: uint64 lo, hi; uint32 count, pad; uint64 first_canon, first_twin, pad) */
+int ec_record_bytes(int k);
 /* graph phase (links .. GFA) on a complete solid set; results via ec_copy_* */
 int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags);
 

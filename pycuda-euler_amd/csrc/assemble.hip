@@ -101,26 +101,24 @@ namespace ec {
 // count) in dict order becomes an exchange record of its canonical key whose first event of
 // the entry's orientation is i; a twin entry adds count 0 (build stores both strands with the
 // same count).  bad gets the smallest entry index holding a byte outside ACGT.
+template <typename Ops>
 __global__ void __launch_bounds__(256) k_kmers_to_agg(const char *chars, const unsigned int *counts, uint64_t n, int k,
-                                                      Agg *out, unsigned long long *bad) {
+                                                      typename RecOf<typename Ops::K>::T *out, unsigned long long *bad) {
+    using K = typename Ops::K;
+    const K mask = Ops::mask(k);
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
         const char *x = chars + t * (uint64_t)k;
-        unsigned long long code = 0;
+        K code{};
         bool ok = true;
         for (int i = 0; i < k; i++) {
             const uint32_t b = base_code((unsigned char)x[i]);
             ok &= b < 4;
-            code = (code << 2) | (b & 3u);
+            code = Ops::push(code, b & 3u, mask);
         }
         if (!ok) atomicMin(bad, (unsigned long long)t);
-        const unsigned long long tw = twin64(code, k);
-        Agg a;
-        a.key = code < tw ? code : tw;
-        a.pad = 0;
-        a.count = code <= tw ? counts[t] : 0u;
-        a.fC = code <= tw ? (unsigned long long)t : ~0ull;
-        a.fT = code >= tw ? (unsigned long long)t : ~0ull;
-        out[t] = a;
+        const K tw = Ops::twin(code, k);
+        out[t] = RecOf<K>::make(code < tw ? code : tw, code <= tw ? counts[t] : 0u,
+                                code <= tw ? (unsigned long long)t : ~0ull, tw <= code ? (unsigned long long)t : ~0ull);
     }
 }
 }  // namespace ec
@@ -207,7 +205,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     s->have = false;
     s->stats_ok = false;
     if (k < 1 || k > EC_MAX_K) {
-        set_error("k=%d outside [1,%d] (fused path uses 64-bit keys)", k, EC_MAX_K);
+        set_error("k=%d outside [1,%d]", k, EC_MAX_K);
         return EC_ERR_ARG;
     }
     EC_HIP(hipSetDevice(s->device));
@@ -471,8 +469,130 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
     return EC_OK;
 }
 
+
+// ---- 32 < k <= 63: 128-bit keys (wide.h), general-table counting ---------------------------
+int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, SolidIndexW &sidx) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    mark(s, 2 * EC_STAGE_COMPACT);
+    EC_CHECK(s->dkey.ensure(cap * sizeof(K128)));
+    EC_CHECK(s->dcnt.ensure(cap * 4));
+    EC_CHECK(s->dfc.ensure(cap * 8));
+    EC_CHECK(s->dft.ensure(cap * 8));
+    EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
+    k_compact_w<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<SlotW>(), cap, limit, s->dkey.as<K128>(),
+                                                     s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                                     s->dft.as<unsigned long long>(), &dsc->nsolid, &dsc->ndistinct);
+    mark(s, 2 * EC_STAGE_COMPACT + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    U = hsc.nsolid;
+    s->stats.n_distinct = hsc.ndistinct;
+    s->stats.n_solid = U;
+    s->stats.count_path = EC_PATH_GENERAL;
+    s->stats.table_capacity = cap;
+    sidx.table = s->table.as<SlotW>();
+    sidx.capmask = cap - 1;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
+    return EC_OK;
+}
+
+int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, uint64_t read_base,
+                  int k, long long limit, unsigned int &U, SolidIndexW &sidx) {
+    if (nreads + read_base > (1ull << 32)) {
+        set_error("global read ids reach %llu >= 2^32", (unsigned long long)(nreads + read_base));
+        return EC_ERR_ARG;
+    }
+    s->stats.n_reads = nreads;
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    mark(s, 2 * EC_STAGE_PRESCAN);
+    EC_CHECK(s->hll.ensure(HLL_M * 4));
+    EC_HIP(hipMemsetAsync(s->hll.p, 0, HLL_M * 4, st));
+    if (nreads) {
+        k_prescan_w<<<grid_for(nreads, B, 4096), B, 0, st>>>(d_reads, d_off, nreads, k, s->hll.as<unsigned int>(),
+                                                            &dsc->npos, &dsc->bad);
+        k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<unsigned int>(), HLL_BITS, &dsc->est);
+    }
+    mark(s, 2 * EC_STAGE_PRESCAN + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.bad != ~0ull) {
+        uint8_t byte = 0;
+        hipMemcpy(&byte, d_reads + hsc.bad, 1, hipMemcpyDeviceToHost);
+        set_error("byte %llu (0x%02x) outside {A,C,G,T,N}", (unsigned long long)hsc.bad, byte);
+        return EC_ERR_ALPHABET;
+    }
+    const uint64_t P = nreads ? hsc.npos : 0;
+    s->stats.n_positions = P;
+    const double est = nreads ? hsc.est : 0.0;
+    s->stats.n_distinct_est = (uint64_t)llround(est);
+    uint64_t cap = 1024;
+    const double want = std::min((double)P, 1.05 * est) * 1.6 + 1024;
+    while ((double)cap < want) cap <<= 1;
+    for (int attempt = 0;; attempt++) {
+        EC_CHECK(s->table.ensure(cap * sizeof(SlotW)));
+        mark(s, 2 * EC_STAGE_COUNT);
+        k_table_clear_w<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<SlotW>(), cap);
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        if (nreads) {
+            kmark(s, 3, 0);
+            k_count_w<<<grid_for(nreads, B), B, 0, st>>>(d_reads, d_off, nreads, k, s->table.as<SlotW>(), cap - 1,
+                                                        &dsc->overflow, read_base);
+            kmark(s, 3, 1);
+        }
+        mark(s, 2 * EC_STAGE_COUNT + 1);
+        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (!hsc.overflow) break;
+        if (attempt >= 4) {
+            set_error("hash table overflow at capacity %llu", (unsigned long long)cap);
+            return EC_ERR_CAPACITY;
+        }
+        cap <<= 2;
+        s->stats.table_retries++;
+    }
+    return finish_wide(s, cap, limit, U, sidx);
+}
+
+int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndexW &sidx) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)(2.2 * (double)n) + 1024) cap <<= 1;
+    for (int attempt = 0;; attempt++) {
+        EC_CHECK(s->table.ensure(cap * sizeof(SlotW)));
+        mark(s, 2 * EC_STAGE_COUNT);
+        k_table_clear_w<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<SlotW>(), cap);
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        if (n) k_merge_agg_w<<<grid_for(n, B), B, 0, st>>>(d_agg, n, s->table.as<SlotW>(), cap - 1, &dsc->overflow);
+        mark(s, 2 * EC_STAGE_COUNT + 1);
+        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (!hsc.overflow) break;
+        if (attempt >= 4) {
+            set_error("merge table overflow at capacity %llu", (unsigned long long)cap);
+            return EC_ERR_CAPACITY;
+        }
+        cap <<= 2;
+        s->stats.table_retries++;
+    }
+    return finish_wide(s, cap, limit, U, sidx);
+}
+
 // all_contigs:79-111 on the device from the solid set of phase_count / phase_merge
-int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
+template <typename Ops, typename Index>
+int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -490,7 +610,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
     EC_CHECK(s->succ.ensure(Nn * 4));
     EC_CHECK(s->pred.ensure(Nn * 4));
     if (U) {
-        k_neighbors<<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<unsigned long long>(), U, k,
+        k_neighbors<Ops, Index><<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
                                                  s->cand.as<unsigned int>(), &dsc->npal);
         k_succ<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(),
@@ -621,8 +741,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
     EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
     EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
     if (U)
-        k_emit<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
-                                            s->PL.as<unsigned int>(), s->dkey.as<unsigned long long>(),
+        k_emit<Ops><<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
+                                            s->PL.as<unsigned int>(), s->dkey.as<typename Ops::K>(),
                                             s->cidxOf.as<unsigned int>(), sorted_nodes, s->coff.as<unsigned long long>(),
                                             N, k, s->chars.as<char>(), s->cfirst.as<unsigned int>(),
                                             s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
@@ -634,7 +754,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const SolidIndex &sidx) {
     EC_CHECK(s->lk.ensure((size_t)std::max(nc, 1u) * 16 * 8));
     EC_CHECK(s->lcnt.ensure((size_t)std::max(nc, 1u) * 2 * 4));
     if (nc)
-        k_gfa<<<grid_for(nc, B), B, 0, st>>>(sidx, s->dkey.as<unsigned long long>(),
+        k_gfa<Ops, Index><<<grid_for(nc, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(),
                                             s->upal.as<uint8_t>(), s->cfirst.as<unsigned int>(),
                                             s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
                                             s->tailOf.as<unsigned int>(), nc, k, s->lk.as<long long>(),
@@ -671,9 +791,14 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
              unsigned flags) {
     EC_CHECK(begin_call(s, k, flags));
     unsigned int U = 0;
+    if (k > 32) {
+        SolidIndexW sidx{};
+        EC_CHECK(phase_count_w(s, d_reads, d_off, nreads, 0, k, (long long)limit, U, sidx));
+        return phase_graph<OpsW>(s, k, U, sidx);
+    }
     SolidIndex sidx{};
     EC_CHECK(phase_count(s, d_reads, d_off, nreads, 0, k, (long long)limit, flags, U, sidx));
-    return phase_graph(s, k, U, sidx);
+    return phase_graph<Ops64>(s, k, U, sidx);
 }
 
 }  // namespace
@@ -829,9 +954,14 @@ int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts) {
                         s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nd));
     EC_CHECK(s->dchars.ensure((size_t)nd * s->k));
     EC_CHECK(s->dcounts.ensure((size_t)nd * 4));
-    k_dict_render<<<grid_for(nd, B), B, 0, st>>>(s->svals2.as<unsigned int>(), nd, s->dkey.as<unsigned long long>(),
-                                                s->dcnt.as<unsigned int>(), s->k, s->dchars.as<char>(),
-                                                s->dcounts.as<unsigned int>());
+    if (s->k > 32)
+        k_dict_render<OpsW><<<grid_for(nd, B), B, 0, st>>>(s->svals2.as<unsigned int>(), nd, s->dkey.as<K128>(),
+                                                          s->dcnt.as<unsigned int>(), s->k, s->dchars.as<char>(),
+                                                          s->dcounts.as<unsigned int>());
+    else
+        k_dict_render<Ops64><<<grid_for(nd, B), B, 0, st>>>(s->svals2.as<unsigned int>(), nd,
+                                                           s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+                                                           s->k, s->dchars.as<char>(), s->dcounts.as<unsigned int>());
     if (kmers) EC_HIP(hipMemcpyAsync(kmers, s->dchars.p, (size_t)nd * s->k, hipMemcpyDeviceToHost, st));
     if (counts) EC_HIP(hipMemcpyAsync(counts, s->dcounts.p, (size_t)nd * 4, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
@@ -848,8 +978,13 @@ int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offs
     }
     EC_CHECK(begin_call(s, k, flags));
     unsigned int U = 0;
-    SolidIndex sidx{};
-    EC_CHECK(phase_count(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, flags, U, sidx));
+    if (k > 32) {
+        SolidIndexW sidx{};
+        EC_CHECK(phase_count_w(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, U, sidx));
+    } else {
+        SolidIndex sidx{};
+        EC_CHECK(phase_count(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, flags, U, sidx));
+    }
     s->n_dense = U;
     collect_timing(s);
     s->stats_ok = true;
@@ -868,7 +1003,11 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
     EC_CHECK(s->ocnt.ensure(2 * MAX_OWNERS * 8));
     unsigned long long *cnt = s->ocnt.as<unsigned long long>(), *cur = cnt + MAX_OWNERS;
     EC_HIP(hipMemsetAsync(cnt, 0, MAX_OWNERS * 8, st));
-    if (n) k_owner_hist<<<grid_for(n, B, 2048), B, 0, st>>>(s->dkey.as<unsigned long long>(), n, nowners, cnt);
+    const bool wide = s->k > 32;
+    if (n && wide) k_owner_hist<K128><<<grid_for(n, B, 2048), B, 0, st>>>(s->dkey.as<K128>(), n, nowners, cnt);
+    if (n && !wide)
+        k_owner_hist<unsigned long long><<<grid_for(n, B, 2048), B, 0, st>>>(s->dkey.as<unsigned long long>(), n,
+                                                                            nowners, cnt);
     std::vector<unsigned long long> h(nowners), o(nowners);
     EC_HIP(hipMemcpyAsync(h.data(), cnt, nowners * 8, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
@@ -880,10 +1019,14 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
     }
     if (n && d_out) {
         EC_HIP(hipMemcpyAsync(cur, o.data(), nowners * 8, hipMemcpyHostToDevice, st));
-        k_owner_scatter<<<grid_for(n, B, 4096), B, 0, st>>>(s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
-                                                            s->dfc.as<unsigned long long>(),
-                                                            s->dft.as<unsigned long long>(), n, nowners, cur,
-                                                            reinterpret_cast<Agg *>(d_out));
+        if (wide)
+            k_owner_scatter<K128><<<grid_for(n, B, 4096), B, 0, st>>>(
+                s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<AggW *>(d_out));
+        else
+            k_owner_scatter<unsigned long long><<<grid_for(n, B, 4096), B, 0, st>>>(
+                s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<Agg *>(d_out));
         EC_HIP(hipStreamSynchronize(st));
     }
     return EC_OK;
@@ -896,8 +1039,13 @@ int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int 
     }
     EC_CHECK(begin_call(s, k, flags));
     unsigned int U = 0;
-    SolidIndex sidx{};
-    EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx));
+    if (k > 32) {
+        SolidIndexW sidx{};
+        EC_CHECK(phase_merge_w(s, reinterpret_cast<const AggW *>(d_records), n, (long long)limit, U, sidx));
+    } else {
+        SolidIndex sidx{};
+        EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx));
+    }
     s->n_dense = U;
     collect_timing(s);
     s->stats_ok = true;
@@ -909,9 +1057,14 @@ int ec_export_dense(ec_session *s, void *d_out) {
     EC_HIP(hipSetDevice(s->device));
     const unsigned int n = s->n_dense;
     if (n && d_out) {
-        k_export_dense<<<grid_for(n, 256), 256, 0, s->stream>>>(
-            s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-            s->dft.as<unsigned long long>(), n, reinterpret_cast<Agg *>(d_out));
+        if (s->k > 32)
+            k_export_dense<K128><<<grid_for(n, 256), 256, 0, s->stream>>>(
+                s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                s->dft.as<unsigned long long>(), n, reinterpret_cast<AggW *>(d_out));
+        else
+            k_export_dense<unsigned long long><<<grid_for(n, 256), 256, 0, s->stream>>>(
+                s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                s->dft.as<unsigned long long>(), n, reinterpret_cast<Agg *>(d_out));
         EC_HIP(hipStreamSynchronize(s->stream));
     }
     return EC_OK;
@@ -926,10 +1079,17 @@ int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int
     }
     EC_CHECK(begin_call(s, k, flags));
     unsigned int U = 0;
+    if (k > 32) {
+        SolidIndexW sidx{};
+        EC_CHECK(phase_merge_w(s, reinterpret_cast<const AggW *>(d_records), n, LLONG_MIN, U, sidx));
+        return phase_graph<OpsW>(s, k, U, sidx);
+    }
     SolidIndex sidx{};
     EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, LLONG_MIN, U, sidx));
-    return phase_graph(s, k, U, sidx);
+    return phase_graph<Ops64>(s, k, U, sidx);
 }
+
+int ec_record_bytes(int k) { return k > 32 ? (int)sizeof(AggW) : (int)sizeof(Agg); }
 
 int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *counts, uint64_t n, int k, unsigned flags) {
     if (!s || (n && (!kmers || !counts))) {
@@ -940,13 +1100,18 @@ int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *cou
     hipStream_t st = s->stream;
     EC_CHECK(s->dchars.ensure(std::max<size_t>(n * (size_t)k, 1)));
     EC_CHECK(s->dcounts.ensure(std::max<size_t>(n * 4, 4)));
-    EC_CHECK(s->recs2.ensure(std::max<size_t>(n * sizeof(Agg), 16)));
+    const bool wide = k > 32;
+    EC_CHECK(s->recs2.ensure(std::max<size_t>(n * (wide ? sizeof(AggW) : sizeof(Agg)), 16)));
     Scalars *dsc = s->scal.as<Scalars>();
     if (n) {
         EC_HIP(hipMemcpyAsync(s->dchars.p, kmers, n * (size_t)k, hipMemcpyHostToDevice, st));
         EC_HIP(hipMemcpyAsync(s->dcounts.p, counts, n * 4, hipMemcpyHostToDevice, st));
-        k_kmers_to_agg<<<grid_for(n, 256), 256, 0, st>>>(s->dchars.as<char>(), s->dcounts.as<unsigned int>(), n, k,
-                                                        s->recs2.as<Agg>(), &dsc->bad);
+        if (wide)
+            k_kmers_to_agg<OpsW><<<grid_for(n, 256), 256, 0, st>>>(s->dchars.as<char>(), s->dcounts.as<unsigned int>(),
+                                                                  n, k, s->recs2.as<AggW>(), &dsc->bad);
+        else
+            k_kmers_to_agg<Ops64><<<grid_for(n, 256), 256, 0, st>>>(s->dchars.as<char>(), s->dcounts.as<unsigned int>(),
+                                                                   n, k, s->recs2.as<Agg>(), &dsc->bad);
         unsigned long long bad = 0;
         EC_HIP(hipMemcpyAsync(&bad, &dsc->bad, 8, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
@@ -956,9 +1121,14 @@ int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *cou
         }
     }
     unsigned int U = 0;
+    if (wide) {
+        SolidIndexW sidx{};
+        EC_CHECK(phase_merge_w(s, s->recs2.as<AggW>(), n, LLONG_MIN, U, sidx));
+        return phase_graph<OpsW>(s, k, U, sidx);
+    }
     SolidIndex sidx{};
     EC_CHECK(phase_merge(s, s->recs2.as<Agg>(), n, LLONG_MIN, U, sidx));
-    return phase_graph(s, k, U, sidx);
+    return phase_graph<Ops64>(s, k, U, sidx);
 }
 
 }  // extern "C"

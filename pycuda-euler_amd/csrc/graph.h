@@ -2,6 +2,7 @@
 #pragma once
 #include "count_global.h"
 #include "count_part.h"
+#include "wide.h"
 
 namespace ec {
 
@@ -30,24 +31,52 @@ struct SolidIndex {
         return lookup(table, capmask, c);
     }
 };
+// key algebra of the graph phase: 64-bit codes (k <= 32) or K128 (32 < k <= 63)
+struct Ops64 {
+    using K = unsigned long long;
+    __device__ static inline K mask(int k) { return kmask64(k); }
+    __device__ static inline K twin(const K &x, int k) { return twin64(x, k); }
+    __device__ static inline K push(const K &x, uint32_t b, const K &m) { return ((x << 2) | b) & m; }
+    __device__ static inline uint32_t base(const K &x, int k, int i) { return (uint32_t)(x >> (2 * (k - 1 - i))) & 3u; }
+    __device__ static inline uint32_t last(const K &x) { return (uint32_t)x & 3u; }
+};
+struct OpsW {
+    using K = K128;
+    __device__ static inline K mask(int k) { return kmask128(k); }
+    __device__ static inline K twin(const K &x, int k) { return twin128(x, k); }
+    __device__ static inline K push(const K &x, uint32_t b, const K &m) { return push128(x, b, m); }
+    __device__ static inline uint32_t base(const K &x, int k, int i) { return base_at128(x, k, i); }
+    __device__ static inline uint32_t last(const K &x) { return (uint32_t)x.lo & 3u; }
+};
+
+// canonical K128 key -> dense solid id in the wide table
+struct SolidIndexW {
+    const SlotW *table;
+    uint64_t capmask;
+    __device__ inline unsigned int find(const K128 &c) const { return lookup_w(table, capmask, c); }
+};
+
 // oriented node id: 2u + o (o = 1: twin of the canonical string); palindromes use o = 0 only
-__device__ inline uint64_t node_code(const unsigned long long *dkey, unsigned int x, int k) {
-    const uint64_t c = dkey[x >> 1];
-    return (x & 1) ? twin64(c, k) : c;
+template <typename Ops>
+__device__ inline typename Ops::K node_code(const typename Ops::K *dkey, unsigned int x, int k) {
+    const typename Ops::K c = dkey[x >> 1];
+    return (x & 1) ? Ops::twin(c, k) : c;
 }
 __device__ inline unsigned int twin_node(const uint8_t *upal, unsigned int x) {
     return upal[x >> 1] ? x : (x ^ 1u);
 }
 
 // links phase 1: out-degree (number of fw(x) in d, get_contig_forward:63) + the unique candidate
-__global__ void __launch_bounds__(256) k_neighbors(SolidIndex idx, const unsigned long long *dkey,
-                                                   unsigned int U, int k, uint8_t *upal, uint8_t *outdeg,
-                                                   unsigned int *cand, unsigned int *npal) {
-    const uint64_t mask = kmask64(k);
+template <typename Ops, typename Index>
+__global__ void __launch_bounds__(256) k_neighbors(Index idx, const typename Ops::K *dkey, unsigned int U, int k,
+                                                   uint8_t *upal, uint8_t *outdeg, unsigned int *cand,
+                                                   unsigned int *npal) {
+    using K = typename Ops::K;
+    const K mask = Ops::mask(k);
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < 2ull * U; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
-        const uint64_t c = dkey[x >> 1];
-        const uint64_t tc = twin64(c, k);
+        const K c = dkey[x >> 1];
+        const K tc = Ops::twin(c, k);
         const bool pal = tc == c;
         if (x & 1) {
             if (pal) {  // the palindrome has a single dict entry: node 2u+1 does not exist
@@ -59,12 +88,12 @@ __global__ void __launch_bounds__(256) k_neighbors(SolidIndex idx, const unsigne
             upal[x >> 1] = pal ? 1 : 0;
             if (pal) atomicAdd(npal, 1u);
         }
-        const uint64_t xs = (x & 1) ? tc : c;
+        const K xs = (x & 1) ? tc : c;
         unsigned int n = 0, cd = NONE32;
-        for (int b = 0; b < 4; b++) {
-            const uint64_t y = ((xs << 2) | (uint64_t)b) & mask;
-            const uint64_t ty = twin64(y, k);
-            const uint64_t cy = y < ty ? y : ty;
+        for (uint32_t b = 0; b < 4; b++) {
+            const K y = Ops::push(xs, b, mask);
+            const K ty = Ops::twin(y, k);
+            const K cy = y < ty ? y : ty;
             const unsigned int u = idx.find(cy);
             if (u != NONE32) {
                 if (n == 0) cd = 2 * u + (y != cy ? 1u : 0u);
@@ -405,8 +434,9 @@ __global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const u
 
 // emit: every node finds its contig through its path key, computes its walk position and
 // writes its chars (contig_to_string:44-45: first node k chars, later nodes their last base).
+template <typename Ops>
 __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
-                                              const unsigned int *PL, const unsigned long long *dkey,
+                                              const unsigned int *PL, const typename Ops::K *dkey,
                                               const unsigned int *cidxOf, const unsigned int *sorted_nodes,
                                               const unsigned long long *coff, unsigned int N, int k, char *chars,
                                               unsigned int *cfirst, unsigned int *clast, unsigned int *headOf,
@@ -435,18 +465,14 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
             }
         }
         if (pos < 0) continue;
-        const uint64_t code = node_code(dkey, x, k);
+        const typename Ops::K code = node_code<Ops>(dkey, x, k);
         char *dst = chars + coff[ci];
         if (pos == 0) {
-            uint64_t c = code;
-            for (int i = k - 1; i >= 0; i--) {
-                dst[i] = "ACGT"[c & 3];
-                c >>= 2;
-            }
+            for (int i = 0; i < k; i++) dst[i] = "ACGT"[Ops::base(code, k, i)];
             cfirst[ci] = x;
             headOf[x] = ci;
         } else {
-            dst[k - 1 + pos] = "ACGT"[code & 3];
+            dst[k - 1 + pos] = "ACGT"[Ops::last(code)];
         }
         if ((unsigned long long)pos == (unsigned long long)w.len - 1) {
             clast[ci] = x;
@@ -457,21 +483,23 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
 
 // GFA links (all_contigs:90-109): for y in fw(last kmer): heads[y] then tails[y];
 // for z in fw(twin(first kmer)): heads[z] then tails[z].  Up to 8 per side.
-__global__ void __launch_bounds__(256) k_gfa(SolidIndex idx, const unsigned long long *dkey,
-                                             const uint8_t *upal, const unsigned int *cfirst, const unsigned int *clast,
+template <typename Ops, typename Index>
+__global__ void __launch_bounds__(256) k_gfa(Index idx, const typename Ops::K *dkey, const uint8_t *upal,
+                                             const unsigned int *cfirst, const unsigned int *clast,
                                              const unsigned int *headOf, const unsigned int *tailOf, unsigned int nc,
                                              int k, long long *lk, unsigned int *lcnt) {
-    const uint64_t mask = kmask64(k);
+    using K = typename Ops::K;
+    const K mask = Ops::mask(k);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
         for (int side = 0; side < 2; side++) {
             const unsigned int src = side == 0 ? clast[i] : twin_node(upal, cfirst[i]);
-            const uint64_t xs = node_code(dkey, src, k);
+            const K xs = node_code<Ops>(dkey, src, k);
             unsigned int n = 0;
             long long *o = lk + (i * 2 + side) * 8;
-            for (int b = 0; b < 4; b++) {
-                const uint64_t y = ((xs << 2) | (uint64_t)b) & mask;
-                const uint64_t ty = twin64(y, k);
-                const uint64_t cy = y < ty ? y : ty;
+            for (uint32_t b = 0; b < 4; b++) {
+                const K y = Ops::push(xs, b, mask);
+                const K ty = Ops::twin(y, k);
+                const K cy = y < ty ? y : ty;
                 const unsigned int u = idx.find(cy);
                 if (u == NONE32) continue;
                 const unsigned int oy = (y != cy) ? 2 * u + 1 : 2 * u;
@@ -497,16 +525,14 @@ __global__ void __launch_bounds__(256) k_dict_items(const uint8_t *upal, const u
     }
 }
 
+template <typename Ops>
 __global__ void __launch_bounds__(256) k_dict_render(const unsigned int *nodes, unsigned int n,
-                                                     const unsigned long long *dkey, const unsigned int *dcnt, int k,
+                                                     const typename Ops::K *dkey, const unsigned int *dcnt, int k,
                                                      char *out, unsigned int *counts) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = nodes[i];
-        uint64_t c = node_code(dkey, x, k);
-        for (int p = k - 1; p >= 0; p--) {
-            out[i * k + p] = "ACGT"[c & 3];
-            c >>= 2;
-        }
+        const typename Ops::K c = node_code<Ops>(dkey, x, k);
+        for (int p = 0; p < k; p++) out[i * k + p] = "ACGT"[Ops::base(c, k, p)];
         counts[i] = dcnt[x >> 1];
     }
 }

@@ -6,6 +6,7 @@
 //   every rank runs the graph phase on the full set.
 #pragma once
 #include "count_global.h"
+#include "wide.h"
 
 namespace ec {
 
@@ -25,7 +26,39 @@ __device__ inline unsigned int owner_of(uint64_t key, unsigned int nowners) {
 
 constexpr int MAX_OWNERS = 256;
 
-__global__ void __launch_bounds__(256) k_owner_hist(const unsigned long long *dkey, unsigned int n, unsigned int nowners,
+__device__ inline unsigned int owner_of(const K128 &c, unsigned int nowners) { return owner_of_w(c, nowners); }
+
+// the exchange record of a key type: Agg (64-bit keys) or AggW (K128)
+template <typename K> struct RecOf;
+template <> struct RecOf<unsigned long long> {
+    using T = Agg;
+    __device__ static inline Agg make(unsigned long long k, unsigned int c, unsigned long long fc, unsigned long long ft) {
+        Agg a;
+        a.key = k;
+        a.count = c;
+        a.pad = 0;
+        a.fC = fc;
+        a.fT = ft;
+        return a;
+    }
+};
+template <> struct RecOf<K128> {
+    using T = AggW;
+    __device__ static inline AggW make(const K128 &k, unsigned int c, unsigned long long fc, unsigned long long ft) {
+        AggW a;
+        a.lo = k.lo;
+        a.hi = k.hi;
+        a.count = c;
+        a.pad = 0;
+        a.fC = fc;
+        a.fT = ft;
+        a.pad2 = 0;
+        return a;
+    }
+};
+
+template <typename K>
+__global__ void __launch_bounds__(256) k_owner_hist(const K *dkey, unsigned int n, unsigned int nowners,
                                                     unsigned long long *cnt) {
     __shared__ unsigned int h[MAX_OWNERS];
     for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) h[i] = 0;
@@ -38,10 +71,11 @@ __global__ void __launch_bounds__(256) k_owner_hist(const unsigned long long *dk
 }
 
 // scatter dense records into owner-major order; cursor[o] starts at the owner's offset
-__global__ void __launch_bounds__(256) k_owner_scatter(const unsigned long long *dkey, const unsigned int *dcnt,
+template <typename K>
+__global__ void __launch_bounds__(256) k_owner_scatter(const K *dkey, const unsigned int *dcnt,
                                                        const unsigned long long *dfc, const unsigned long long *dft,
                                                        unsigned int n, unsigned int nowners,
-                                                       unsigned long long *cursor, Agg *out) {
+                                                       unsigned long long *cursor, typename RecOf<K>::T *out) {
     __shared__ unsigned int h[MAX_OWNERS];
     __shared__ unsigned long long base[MAX_OWNERS];
     for (uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x; t0 < n; t0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -57,15 +91,7 @@ __global__ void __launch_bounds__(256) k_owner_scatter(const unsigned long long 
         for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x)
             base[i] = h[i] ? atomicAdd(&cursor[i], (unsigned long long)h[i]) : 0ull;
         __syncthreads();
-        if (t < n) {
-            Agg a;
-            a.key = dkey[t];
-            a.count = dcnt[t];
-            a.pad = 0;
-            a.fC = dfc[t];
-            a.fT = dft[t];
-            out[base[o] + rk] = a;
-        }
+        if (t < n) out[base[o] + rk] = RecOf<K>::make(dkey[t], dcnt[t], dfc[t], dft[t]);
         __syncthreads();
     }
 }
@@ -98,18 +124,12 @@ __global__ void __launch_bounds__(256) k_merge_agg(const Agg *in, uint64_t n, Sl
     }
 }
 
-__global__ void __launch_bounds__(256) k_export_dense(const unsigned long long *dkey, const unsigned int *dcnt,
+template <typename K>
+__global__ void __launch_bounds__(256) k_export_dense(const K *dkey, const unsigned int *dcnt,
                                                       const unsigned long long *dfc, const unsigned long long *dft,
-                                                      unsigned int n, Agg *out) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
-        Agg a;
-        a.key = dkey[t];
-        a.count = dcnt[t];
-        a.pad = 0;
-        a.fC = dfc[t];
-        a.fT = dft[t];
-        out[t] = a;
-    }
+                                                      unsigned int n, typename RecOf<K>::T *out) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+        out[t] = RecOf<K>::make(dkey[t], dcnt[t], dfc[t], dft[t]);
 }
 
 }  // namespace ec

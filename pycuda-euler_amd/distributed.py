@@ -26,7 +26,15 @@ import numpy as np
 
 import eulerhip
 
-REC_BYTES = 32  # ec_kmer_record
+REC_BYTES = 32  # ec_kmer_record (k <= 32)
+REC_BYTES_WIDE = 48  # ec_kmer_record_wide (32 < k <= 63)
+
+
+def rec_bytes(k):
+    """exchange record size for node length k (ec_record_bytes)"""
+    return REC_BYTES if k <= 32 else REC_BYTES_WIDE
+
+
 REC_DTYPE = np.dtype([("key", "<u8"), ("count", "<u4"), ("pad", "<u4"), ("first_canon", "<u8"),
                       ("first_twin", "<u8")])
 
@@ -38,6 +46,7 @@ eulerhip.register("ec_export_by_owner", ctypes.c_int, [_P, ctypes.c_int, _P, cty
 eulerhip.register("ec_merge_owned", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint])
 eulerhip.register("ec_export_dense", ctypes.c_int, [_P, _P])
 eulerhip.register("ec_assemble_from_solid", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_uint])
+eulerhip.register("ec_record_bytes", ctypes.c_int, [ctypes.c_int])
 
 
 def shard_range(nreads, rank, world):
@@ -66,28 +75,36 @@ class HipEngine:
         return self.torch.empty(max(int(nbytes), 1), dtype=self.torch.uint8, device=self.device)
 
     def count_shard(self, d_reads, d_off, nreads, read_base, k, flags=0):
+        self.k = int(k)
         eulerhip.check(self.L.ec_count_shard(self._h(), ctypes.c_void_p(d_reads.data_ptr()),
                                              ctypes.c_void_p(d_off.data_ptr()), int(nreads), int(read_base), int(k),
                                              flags))
         return self.sess.stats()
 
+    def rec_bytes(self):
+        return int(self.L.ec_record_bytes(self.k))
+
     def export_by_owner(self, nowners):
         n = int(self.L.ec_dense_count(self._h()))
+        rb = self.rec_bytes()
         counts = (ctypes.c_uint64 * nowners)()
-        out = self.empty(n * REC_BYTES)
+        out = self.empty(n * rb)
         eulerhip.check(self.L.ec_export_by_owner(self._h(), int(nowners), ctypes.c_void_p(out.data_ptr()), counts))
-        return out[: n * REC_BYTES], [int(c) for c in counts]
+        return out[: n * rb], [int(c) for c in counts]
 
     def merge_owned(self, recs, k, limit, flags=0):
-        n = recs.numel() // REC_BYTES
+        self.k = int(k)
+        rb = self.rec_bytes()
+        n = recs.numel() // rb
         eulerhip.check(self.L.ec_merge_owned(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), int(limit), flags))
         m = int(self.L.ec_dense_count(self._h()))
-        out = self.empty(m * REC_BYTES)
+        out = self.empty(m * rb)
         eulerhip.check(self.L.ec_export_dense(self._h(), ctypes.c_void_p(out.data_ptr())))
-        return out[: m * REC_BYTES]
+        return out[: m * rb]
 
     def assemble_from_solid(self, recs, k, flags=0):
-        n = recs.numel() // REC_BYTES
+        self.k = int(k)
+        n = recs.numel() // self.rec_bytes()
         eulerhip.check(self.L.ec_assemble_from_solid(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), flags))
         return self.sess.fetch(k)
 
@@ -153,7 +170,7 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
         on_count(st)
     P = comm.allreduce_sum(st.n_positions)
     recs, counts = engine.export_by_owner(comm.world)
-    received = comm.alltoallv(recs, [c * REC_BYTES for c in counts])
+    received = comm.alltoallv(recs, [c * rec_bytes(k) for c in counts])
     solid = engine.merge_owned(received, k, limit, flags)
     everything = comm.allgatherv(solid)
     res = engine.assemble_from_solid(everything, k, flags)
@@ -220,8 +237,9 @@ def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0):
         parts = []
         for src in range(world):
             recs, counts = sends[src]
-            o = sum(counts[:dst]) * REC_BYTES
-            parts.append(recs[o:o + counts[dst] * REC_BYTES].to(eng.device))
+            rb = rec_bytes(k)
+            o = sum(counts[:dst]) * rb
+            parts.append(recs[o:o + counts[dst] * rb].to(eng.device))
         solids.append(eng.merge_owned(torch.cat(parts), k, limit, flags))
     allsolid = torch.cat([s.to(engines[0].device) for s in solids])
     res = engines[0].assemble_from_solid(allsolid, k, flags)

@@ -36,7 +36,7 @@ EC_NKERNELS = 5
 KERNEL_NAMES = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
 EC_PATH_PARTITIONED = 0
 EC_PATH_GENERAL = 1
-EC_MAX_K = 32
+EC_MAX_K = 63
 
 
 class EulerHipError(RuntimeError):

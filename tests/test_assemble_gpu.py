@@ -26,8 +26,9 @@ def test_golden(gpu_session, case):
     assert [[x, c] for x, c in res.dict_items] == case["d"]
     assert res.contigs == case["contigs"]
     assert res.links == case["links"]
-    if res.stats.n_positions > 0:
-        assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
+    if res.stats.n_positions > 0:  # 128-bit keys (k > 32) count in the general table
+        want = eulerhip.EC_PATH_PARTITIONED if case["k"] <= 32 else eulerhip.EC_PATH_GENERAL
+        assert res.stats.count_path == want
 
 
 @pytest.mark.parametrize("case", CASES32[::2], ids=[c["name"] for c in CASES32[::2]])
@@ -48,6 +49,8 @@ def test_k_out_of_range(gpu_session):
     with pytest.raises(eulerhip.EulerHipError):
         gpu_session.assemble(["ACGT" * 20], 0)
     with pytest.raises(eulerhip.EulerHipError):
+        gpu_session.assemble(["ACGT" * 20], 64)
+    with pytest.raises(eulerhip.EulerHipError):
         gpu_session.assemble(["ACGT" * 20], 65)
 
 
@@ -65,6 +68,11 @@ SYN = [
     (2_000, 3_000, 50, 5, 0.0, 0.0, True, 16),
     (200_000, 60_000, 100, 6, 0.0, 0.0, False, 32),
     (1_000, 2_000, 40, 7, 0.02, 0.01, False, 11),
+    # 128-bit keys (32 < k <= 63; BASELINE config 5 uses k = 51)
+    (30_000, 12_000, 150, 8, 0.002, 0.0, False, 51),
+    (20_000, 8_000, 100, 9, 0.003, 0.002, True, 33),
+    (10_000, 6_000, 120, 10, 0.0, 0.0, False, 63),
+    (3_000, 4_000, 90, 11, 0.01, 0.0, False, 40),
 ]
 
 

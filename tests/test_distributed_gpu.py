@@ -27,7 +27,8 @@ def engines():
 
 @pytest.mark.parametrize("world", [1, 2, 3, 4])
 @pytest.mark.parametrize("seed,g,n,L,err,k", [(1, 20_000, 6_000, 100, 0.002, 31), (2, 3_000, 2_000, 50, 0.01, 15),
-                                              (3, 200_000, 60_000, 100, 0.0, 25)])
+                                              (3, 200_000, 60_000, 100, 0.0, 25),
+                                              (4, 30_000, 8_000, 150, 0.002, 51)])
 def test_local_sharded_equals_oracle(engines, world, seed, g, n, L, err, k):
     import distributed
 

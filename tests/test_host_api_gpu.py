@@ -14,7 +14,7 @@ from conftest import GOLDEN, golden_cases
 
 pytestmark = pytest.mark.gpu
 
-CASES = [c for c in golden_cases("g200.json", "synthetic.json") if c["k"] <= 32]  # 64-bit keys
+CASES = golden_cases("g200.json", "synthetic.json")
 
 
 @pytest.fixture(scope="module")
