@@ -37,6 +37,12 @@ CONFIGS = {
     # BASELINE configs[2]: S. cerevisiae size, 5M x 100 bp
     "yeast5m": dict(genome=12_000_000, reads=5_000_000, read_len=100, k=31, seed=20261015 + 3,
                     name="yeast-12Mbp-5Mx100bp-k31"),
+    # BASELINE configs[4]: synthetic 200 Mbp genome, 100M x 150 bp, k = 51 (128-bit keys)
+    "genome200m_k51": dict(genome=200_000_000, reads=100_000_000, read_len=150, k=51, seed=20261015 + 5,
+                           name="synthetic-200Mbp-100Mx150bp-k51"),
+    # the same read length / k at a tenth of the size (20 Mbp genome, same 75x coverage)
+    "genome20m_k51": dict(genome=20_000_000, reads=10_000_000, read_len=150, k=51, seed=20261015 + 5,
+                          name="synthetic-20Mbp-10Mx150bp-k51"),
     "tiny": dict(genome=50_000, reads=50_000, read_len=100, k=31, seed=7, name="tiny-50kbp-50kx100bp-k31"),
 }
 
@@ -106,6 +112,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the multi-GPU path even with one rank")
     args = ap.parse_args()
+    # stdout carries exactly one JSON line: libraries that print banners (RCCL prints its
+    # version block on communicator init) are sent to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     import torch
 
@@ -187,10 +198,14 @@ def main():
         return
 
     kern /= args.steps
+    sharded_ms = None
+    if use_dist:
+        sharded_ms = {kk: round(v / (args.steps + args.warmup), 3) for kk, v in runner.phase_ms.items()}
     kid = int(np.argmax(kern))
     kname = eulerhip.KERNEL_NAMES[kid]
     kms = float(kern[kid])
-    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L)  # this rank's launch
+    K = 8 if k <= 32 else 16  # key bytes
+    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L, K)  # this rank's launch
     achieved = kb / (kms / 1e3) / 1e9
     tr = load_traffic(cfg["name"], kname)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -199,8 +214,8 @@ def main():
             "traffic_source": (tr["file"] if tr else None),
             "kernel": kname, "kernel_ms": round(kms, 4), "alg_bytes_per_launch": int(kb),
             "kernels_ms": {eulerhip.KERNEL_NAMES[i]: round(float(kern[i]), 4) for i in range(len(kern))},
-            "pipeline_alg_bytes": int(alg_bytes(P, R, L, U)),
-            "pipeline_frac": round(alg_bytes(P, R, L, U) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
+            "pipeline_alg_bytes": int(alg_bytes(P, R, L, U, K)),
+            "pipeline_frac": round(alg_bytes(P, R, L, U, K) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(buf, off, k, args.cpu_sample_reads)
@@ -208,7 +223,7 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "scaling": "strong", "vs_baseline": None, "dtype": "u64" if k <= 32 else "u128",
         "data": "synthetic (iid ACGT genome, uniform error-free 100 bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)" % cfg["seed"],
         "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
                    "positions": P, "solid_kmers": U,
@@ -218,8 +233,9 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "stage_ms": {names[i]: round(stage[i] / args.steps, 3) for i in range(len(names))},
+        "sharded_phase_ms": sharded_ms,
     }
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 

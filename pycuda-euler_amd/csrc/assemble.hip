@@ -30,6 +30,7 @@
 
 #include "count_part.h"
 #include "shard.h"
+#include "compact.h"
 
 namespace ec {
 
@@ -228,6 +229,26 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     return EC_OK;
 }
 
+
+// solid slots of an HBM table -> dense arrays (ids in table order); sets dsc->nsolid / ndistinct
+template <typename SlotT, typename KeyT>
+int compact_table(ec_session *s, SlotT *table, uint64_t cap, long long limit, KeyT *dkey) {
+    hipStream_t st = s->stream;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int nblk = (unsigned int)((cap + COMPACT_CHUNK - 1) / COMPACT_CHUNK);
+    EC_CHECK(s->rbc.ensure((size_t)nblk * 8 + 8));
+    unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk;
+    EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
+    k_compact_count<SlotT><<<nblk, 256, 0, st>>>(table, cap, limit, bc, &dsc->ndistinct);
+    EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
+    k_compact_write<SlotT, KeyT><<<nblk, 256, 0, st>>>(table, cap, limit, bs, dkey, s->dcnt.as<unsigned int>(),
+                                                      s->dfc.as<unsigned long long>(),
+                                                      s->dft.as<unsigned long long>());
+    k_compact_total<<<1, 1, 0, st>>>(bs, nblk, &dsc->nsolid);
+    return EC_OK;
+}
+
 // build:25-42 on the device: count canonical k-mers of reads [0, nreads) (global read ids
 // start at read_base), keep those with count > limit as dense arrays dkey/dcnt/dfc/dft (U of
 // them) and a SolidIndex over them.
@@ -393,10 +414,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->dcnt.ensure(umax * 4));
         EC_CHECK(s->dfc.ensure(umax * 8));
         EC_CHECK(s->dft.ensure(umax * 8));
-        k_compact<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap, (long long)limit,
-                                                       s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
-                                                       s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-                                                       &dsc->nsolid, &dsc->ndistinct);
+        EC_CHECK(compact_table(s, s->table.as<Slot>(), cap, (long long)limit, s->dkey.as<unsigned long long>()));
         mark(s, 2 * EC_STAGE_COMPACT + 1);
         EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
@@ -449,9 +467,7 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
     EC_CHECK(s->dft.ensure(cap * 8));
     EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
     EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
-    k_compact<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<Slot>(), cap, limit, s->dkey.as<unsigned long long>(),
-                                                   s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                                   s->dft.as<unsigned long long>(), &dsc->nsolid, &dsc->ndistinct);
+    EC_CHECK(compact_table(s, s->table.as<Slot>(), cap, limit, s->dkey.as<unsigned long long>()));
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
@@ -473,7 +489,6 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
 // ---- 32 < k <= 63: 128-bit keys (wide.h), general-table counting ---------------------------
 int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, SolidIndexW &sidx) {
     hipStream_t st = s->stream;
-    const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc;
     mark(s, 2 * EC_STAGE_COMPACT);
@@ -483,9 +498,7 @@ int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, S
     EC_CHECK(s->dft.ensure(cap * 8));
     EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
     EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
-    k_compact_w<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<SlotW>(), cap, limit, s->dkey.as<K128>(),
-                                                     s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                                     s->dft.as<unsigned long long>(), &dsc->nsolid, &dsc->ndistinct);
+    EC_CHECK(compact_table(s, s->table.as<SlotW>(), cap, limit, s->dkey.as<K128>()));
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));

@@ -102,53 +102,6 @@ __global__ void __launch_bounds__(256) k_count(const uint8_t *buf, const uint64_
     }
 }
 
-// compact: solid (count > limit, build:37-39) slots -> dense arrays
-__global__ void __launch_bounds__(256) k_compact(Slot *table, uint64_t cap, long long limit,
-                                                 unsigned long long *dkey, unsigned int *dcnt,
-                                                 unsigned long long *dfc, unsigned long long *dft,
-                                                 unsigned int *nsolid, unsigned long long *ndistinct) {
-    __shared__ unsigned int wave_cnt[4];
-    __shared__ unsigned int base;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < cap; i0 += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t i = i0 + threadIdx.x;
-        Slot sl;
-        bool present = false, solid = false;
-        if (i < cap) {
-            sl = table[i];
-            present = sl.key != EMPTY_KEY;
-            solid = present && (long long)sl.count > limit;
-        }
-        const unsigned long long m = __ballot(solid);
-        const unsigned long long mp = __ballot(present);
-        const unsigned int before = __popcll(m & ((1ull << lane) - 1));
-        if (lane == 0) {
-            wave_cnt[wid] = __popcll(m);
-            if (mp) atomicAdd(ndistinct, (unsigned long long)__popcll(mp));
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned int tot = 0;
-            for (int w = 0; w < 4; w++) {
-                unsigned int c = wave_cnt[w];
-                wave_cnt[w] = tot;
-                tot += c;
-            }
-            base = tot ? atomicAdd(nsolid, tot) : 0;
-        }
-        __syncthreads();
-        if (solid) {
-            const unsigned int u = base + wave_cnt[wid] + before;
-            dkey[u] = sl.key;
-            dcnt[u] = sl.count;
-            dfc[u] = sl.fC;
-            dft[u] = sl.fT;
-            table[i].idx = u;
-        }
-        __syncthreads();
-    }
-}
-
 __device__ inline unsigned int lookup(const Slot *table, uint64_t capmask, uint64_t c) {
     uint64_t h = mix64(c) & capmask;
     for (int probe = 0; probe < MAX_PROBE; probe++) {

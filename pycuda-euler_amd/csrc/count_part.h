@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(const Rec *recs, cons
                                                           unsigned long long *ndistinct, unsigned int *overflow) {
     __shared__ LSlot tab[SLOTS];
     __shared__ unsigned int s_over;
-    __shared__ unsigned int s_wave[BUCKET_THREADS / 64];
+    __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
     __shared__ unsigned int s_base;
     const unsigned int b = blockIdx.x;
     for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
@@ -516,16 +516,18 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(const Rec *recs, cons
     if (lane == 63) s_wave[wid] = incl;
     unsigned int pres = present;
     for (int o = 32; o > 0; o >>= 1) pres += __shfl_down(pres, o);
-    if (lane == 0 && pres) atomicAdd(ndistinct, (unsigned long long)pres);
+    if (lane == 0) s_pres[wid] = pres;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned int tot = 0;
+    if (threadIdx.x == 0) {  // one global atomic each per block (a per-wave atomic on one word serialises)
+        unsigned int tot = 0, np = 0;
         for (int w = 0; w < BUCKET_THREADS / 64; w++) {
             const unsigned int c = s_wave[w];
             s_wave[w] = tot;
             tot += c;
+            np += s_pres[w];
         }
         s_base = tot ? atomicAdd(nsolid, tot) : 0;
+        if (np) atomicAdd(ndistinct, (unsigned long long)np);
     }
     __syncthreads();
     unsigned int u = s_base + s_wave[wid] + incl - mine;

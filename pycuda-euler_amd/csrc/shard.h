@@ -101,6 +101,7 @@ __global__ void __launch_bounds__(256) k_merge_agg(const Agg *in, uint64_t n, Sl
                                                    unsigned int *overflow) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
         const Agg a = in[t];
+        if (a.key == EMPTY_KEY) continue;  // all-gather filler record (never a canonical key)
         uint64_t h = mix64(a.key) & capmask;
         for (int probe = 0;; probe++) {
             if (probe >= MAX_PROBE) {

@@ -231,6 +231,7 @@ __global__ void __launch_bounds__(256) k_merge_agg_w(const AggW *in, uint64_t n,
                                                      unsigned int *overflow) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
         const AggW a = in[t];
+        if (a.lo == ~0ull && a.hi == ~0ull) continue;  // all-gather filler record
         const K128 c{a.lo, a.hi};
         SlotW *sl = wide_slot(table, capmask, c);
         if (!sl) {
@@ -240,53 +241,6 @@ __global__ void __launch_bounds__(256) k_merge_agg_w(const AggW *in, uint64_t n,
         if (a.count) atomicAdd(&sl->count, a.count);
         if (a.fC < sl->fC) atomicMin(&sl->fC, a.fC);
         if (a.fT < sl->fT) atomicMin(&sl->fT, a.fT);
-    }
-}
-
-// solid slots -> dense arrays (keys as K128)
-__global__ void __launch_bounds__(256) k_compact_w(SlotW *table, uint64_t cap, long long limit, K128 *dkey,
-                                                   unsigned int *dcnt, unsigned long long *dfc,
-                                                   unsigned long long *dft, unsigned int *nsolid,
-                                                   unsigned long long *ndistinct) {
-    __shared__ unsigned int wave_cnt[4];
-    __shared__ unsigned int base;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x; i0 < cap; i0 += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t i = i0 + threadIdx.x;
-        SlotW sl;
-        bool present = false, solid = false;
-        if (i < cap) {
-            sl = table[i];
-            present = sl.w1 != 0;
-            solid = present && (long long)sl.count > limit;
-        }
-        const unsigned long long m = __ballot(solid);
-        const unsigned long long mp = __ballot(present);
-        const unsigned int before = __popcll(m & ((1ull << lane) - 1));
-        if (lane == 0) {
-            wave_cnt[wid] = __popcll(m);
-            if (mp) atomicAdd(ndistinct, (unsigned long long)__popcll(mp));
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned int tot = 0;
-            for (int w = 0; w < 4; w++) {
-                const unsigned int c = wave_cnt[w];
-                wave_cnt[w] = tot;
-                tot += c;
-            }
-            base = tot ? atomicAdd(nsolid, tot) : 0;
-        }
-        __syncthreads();
-        if (solid) {
-            const unsigned int u = base + wave_cnt[wid] + before;
-            dkey[u] = wide_key(sl.w1, sl.w2);
-            dcnt[u] = sl.count;
-            dfc[u] = sl.fC;
-            dft[u] = sl.fT;
-            table[i].idx = u;
-        }
-        __syncthreads();
     }
 }
 

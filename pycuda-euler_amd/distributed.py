@@ -138,18 +138,22 @@ class TorchComm:
                                    input_split_sizes=list(counts_bytes), group=self.group)
         return recv[: sum(rcl)]
 
-    def allgatherv(self, t):
+    def allgatherv(self, t, fill=0):
+        """Concatenation of every rank's `t` in rank order, each part padded with `fill` bytes
+        to the largest part (no compaction copy: the record consumers skip all-0xFF filler
+        records, ec_assemble_from_solid)."""
         torch, dist = self.torch, self.dist
         n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
         sizes = [torch.empty_like(n) for _ in range(self.world)]
         dist.all_gather(sizes, n, group=self.group)
-        sizes = [int(x.item()) for x in sizes]
-        mx = max(max(sizes), 1)
-        pad = torch.zeros(mx, dtype=torch.uint8, device=t.device)
+        mx = max(max(int(x.item()) for x in sizes), 1)
+        if self.world == 1:
+            return t
+        pad = torch.full((mx,), fill, dtype=torch.uint8, device=t.device)
         pad[: t.numel()] = t
         out = torch.empty(self.world * mx, dtype=torch.uint8, device=t.device)
         dist.all_gather_into_tensor(out, pad, group=self.group)
-        return torch.cat([out[i * mx: i * mx + sizes[i]] for i in range(self.world)])
+        return out
 
     def allreduce_sum(self, v):
         dev = "cuda" if self.dist.get_backend(self.group) == "nccl" else "cpu"
@@ -162,18 +166,36 @@ class TorchComm:
 
 
 # ---- the orchestration -----------------------------------------------------------------------
-def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None):
+def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None,
+                     phase_ms=None):
     """Run steps 1-4 for this rank; returns (result, n_positions_total).  on_count(stats)
-    receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING)."""
+    receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING); phase_ms, a
+    dict, receives the wall time of every step (device-synchronised by the engine calls)."""
+    import time
+
+    t = [time.perf_counter()]
+
+    def tick():
+        t.append(time.perf_counter())
+
     st = engine.count_shard(d_reads, d_off, nreads, read_base, k, flags)
+    tick()
     if on_count:
         on_count(st)
     P = comm.allreduce_sum(st.n_positions)
     recs, counts = engine.export_by_owner(comm.world)
+    tick()
     received = comm.alltoallv(recs, [c * rec_bytes(k) for c in counts])
+    tick()
     solid = engine.merge_owned(received, k, limit, flags)
-    everything = comm.allgatherv(solid)
+    tick()
+    everything = comm.allgatherv(solid, fill=0xFF)  # filler records: all-ones keys, skipped
+    tick()
     res = engine.assemble_from_solid(everything, k, flags)
+    tick()
+    if phase_ms is not None:
+        for name, a, b in zip(("count", "export", "alltoall", "merge", "allgather", "graph"), t, t[1:]):
+            phase_ms[name] = phase_ms.get(name, 0.0) + (b - a) * 1e3
     return res, P
 
 
@@ -196,12 +218,13 @@ class ShardedAssembler:
         self.comm = comm or TorchComm()
         self.total_positions = 0
         self.result = None
+        self.phase_ms = {}
 
     def run(self, timing=False):
         flags = eulerhip.EC_FLAG_TIMING if timing else 0
         self.result, self.total_positions = sharded_assemble(self.engine, self.comm, self.d_reads, self.d_off,
                                                              self.nreads, self.read_base, self.k, self.limit, flags,
-                                                             on_count=self._keep)
+                                                             on_count=self._keep, phase_ms=self.phase_ms)
         return self.result
 
     def _keep(self, st):
@@ -241,6 +264,9 @@ def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0):
             o = sum(counts[:dst]) * rb
             parts.append(recs[o:o + counts[dst] * rb].to(eng.device))
         solids.append(eng.merge_owned(torch.cat(parts), k, limit, flags))
-    allsolid = torch.cat([s.to(engines[0].device) for s in solids])
+    mx = max(max(x.numel() for x in solids), 1)  # padded like TorchComm.allgatherv (0xFF filler records)
+    allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device=engines[0].device)
+    for i, x in enumerate(solids):
+        allsolid[i * mx: i * mx + x.numel()] = x.to(engines[0].device)
     res = engines[0].assemble_from_solid(allsolid, k, flags)
     return res, P

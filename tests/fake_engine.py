@@ -95,6 +95,8 @@ class FakeEngine:
     def assemble_from_solid(self, recs, k, flags=0):
         cnt, first = {}, {}
         for r in self._recs(recs):
+            if int(r["key"]) == M64:  # all-gather filler record (ec_assemble_from_solid skips it)
+                continue
             c = decode(int(r["key"]), k)
             cnt[c] = int(r["count"])
             first[c] = int(r["first_canon"])
