@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the multi-GPU path even with one rank")
+    ap.add_argument("--compact-records", action="store_true", help="12-B count records (EC_FLAG_COMPACT_RECORDS)")
     args = ap.parse_args()
     # stdout carries exactly one JSON line: libraries that print banners (RCCL prints its
     # version block on communicator init) are sent to stderr
@@ -155,7 +156,8 @@ def main():
 
         def step(timing=False):
             sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), cfg["reads"], k, 1,
-                            eulerhip.EC_FLAG_TIMING if timing else 0)
+                            (eulerhip.EC_FLAG_TIMING if timing else 0)
+                            | (eulerhip.EC_FLAG_COMPACT_RECORDS if args.compact_records else 0))
     else:
         import distributed
 

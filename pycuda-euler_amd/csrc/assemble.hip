@@ -93,7 +93,8 @@ struct ec_session {
     bool timing = false;
     unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
-    DevBuf ocnt, rbc;
+    unsigned flags = 0;        // flags of the current call
+    DevBuf ocnt, rbc, mbid, mbid2, midx, midx2;
 };
 
 namespace ec {
@@ -142,6 +143,7 @@ struct Scalars {  // device scalars block
     unsigned long long nvisited;
     unsigned int maxlocal;
     unsigned int skew;
+    unsigned int lens[4];  // k_upsweep: max read length, ~min read length (reads with windows), any slow-path read
     unsigned int active[64];
 };
 
@@ -213,6 +215,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     memset(&s->stats, 0, sizeof(s->stats));
     s->k = k;
     s->want_dict = (flags & EC_FLAG_WANT_DICT) != 0;
+    s->flags = flags;
     const bool timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
         for (auto &e : s->ev) EC_HIP(hipEventCreate(&e));
@@ -249,6 +252,24 @@ int compact_table(ec_session *s, SlotT *table, uint64_t cap, long long limit, Ke
     return EC_OK;
 }
 
+
+template <typename Src>
+int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long limit) {
+    Scalars *dsc = s->scal.as<Scalars>();
+    hipStream_t st = s->stream;
+    if (slots == 2048)
+        k_bucket<Src, 2048><<<nb, BUCKET_THREADS, 0, st>>>(
+            src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid,
+            &dsc->ndistinct, &dsc->overflow);
+    else
+        k_bucket<Src, 4096><<<nb, BUCKET_THREADS, 0, st>>>(
+            src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid,
+            &dsc->ndistinct, &dsc->overflow);
+    return EC_OK;
+}
+
 // build:25-42 on the device: count canonical k-mers of reads [0, nreads) (global read ids
 // start at read_base), keep those with count > limit as dense arrays dkey/dcnt/dfc/dft (U of
 // them) and a SolidIndex over them.
@@ -278,7 +299,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         kmark(s, 0, 0);
         k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
                                                            s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad,
-                                                           &dsc->maxlocal, &dsc->skew, s->thist.as<unsigned int>());
+                                                           &dsc->maxlocal, &dsc->skew, s->thist.as<unsigned int>(),
+                                                           dsc->lens);
         kmark(s, 0, 1);
         EC_HIP(hipMemsetAsync(s->ftot.p, 0, (FINE + (1 << HLL_REG_BITS)) * 8, st));
         k_fine_totals<<<dim3(FINE / 256, TOT_SLICES), 256, 0, st>>>(
@@ -322,26 +344,51 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->offs.ensure(Ck * ntiles * 8));
         EC_CHECK(s->tot.ensure((Bk + 1) * 8));
         EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
-        EC_CHECK(s->recs.ensure(P * sizeof(Rec)));
-        if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * sizeof(Rec)));
+        // compact 12-B records (opt-in): every read staged and N-free, one read length, events fit
+        const unsigned int lmax = hsc.lens[0], lmin = ~hsc.lens[1];
+        bool compact = (flags & EC_FLAG_COMPACT_RECORDS) && hsc.lens[2] == 0 && hsc.lens[1] != 0 && lmax == lmin;
+        int ibits = 1;
+        if (compact) {
+            const uint64_t m = (uint64_t)lmax - (uint64_t)k + 1;
+            while ((1ull << ibits) < m) ibits++;
+            compact = ibits <= 15 && nreads + read_base <= (1ull << (31 - ibits));
+        }
+        const size_t rsz = compact ? sizeof(Rec12) : sizeof(Rec);
+        s->stats.record_bytes = (uint32_t)rsz;
+        EC_CHECK(s->recs.ensure(P * rsz));
+        if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * rsz));
         k_coarse<<<grid_for(Ck * ntiles, B, 8192), B, 0, st>>>(s->thist.as<unsigned int>(), ntiles, cbits,
                                                               s->cnt.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ntiles));
         k_bucket_totals<<<grid_for(Bk + 1, B), B, 0, st>>>(s->ftot.as<unsigned long long>(), bbits,
                                                           s->tot.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
+        // compact records: keys [0, 8P) and meta [8P, 12P) of the record buffer
+        const Store12 c1{s->recs.as<unsigned long long>(), reinterpret_cast<unsigned int *>(s->recs.as<uint8_t>() + P * 8)};
+        const Store12 c2{s->recs2.as<unsigned long long>(),
+                         reinterpret_cast<unsigned int *>(s->recs2.as<uint8_t>() + P * 8)};
         kmark(s, 1, 0);
-        k_downsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ntiles, cbits,
-                                                             s->offs.as<unsigned long long>(), s->recs.as<Rec>(),
-                                                             read_base);
+        if (compact)
+            k_downsweep<Rec12, MakeRec12, Store12><<<(unsigned)ngroups, TILE_READS, 0, st>>>(
+                d_reads, d_off, nreads, k, gsize, ntiles, cbits, s->offs.as<unsigned long long>(), c1,
+                MakeRec12{read_base, ibits});
+        else
+            k_downsweep<Rec, MakeRec, Store16><<<(unsigned)ngroups, TILE_READS, 0, st>>>(
+                d_reads, d_off, nreads, k, gsize, ntiles, cbits, s->offs.as<unsigned long long>(),
+                Store16{s->recs.as<Rec>()}, MakeRec{read_base});
         kmark(s, 1, 1);
-        Rec *final_recs = s->recs.as<Rec>();
+        bool second = false;
         if (bbits > cbits) {
             kmark(s, 4, 0);
-            k_refine<<<(unsigned)Ck, BUCKET_THREADS, 0, st>>>(s->recs.as<Rec>(), s->recs2.as<Rec>(),
-                                                             s->bstart.as<unsigned long long>(), cbits, bbits);
+            if (compact)
+                k_refine<Rec12, Store12><<<(unsigned)Ck, BUCKET_THREADS, 0, st>>>(c1, c2, s->bstart.as<unsigned long long>(),
+                                                                                 cbits, bbits);
+            else
+                k_refine<Rec, Store16><<<(unsigned)Ck, BUCKET_THREADS, 0, st>>>(
+                    Store16{s->recs.as<Rec>()}, Store16{s->recs2.as<Rec>()}, s->bstart.as<unsigned long long>(), cbits,
+                    bbits);
             kmark(s, 4, 1);
-            final_recs = s->recs2.as<Rec>();
+            second = true;
         }
         mark(s, 2 * EC_STAGE_COUNT + 1);
         mark(s, 2 * EC_STAGE_COMPACT);
@@ -352,16 +399,14 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->dft.ensure(umax * 8));
         EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
         kmark(s, 2, 0);
-        if (slots == 2048)
-            k_bucket<2048><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
-                final_recs, s->bstart.as<unsigned long long>(), (long long)limit,
-                s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
-        else
-            k_bucket<4096><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
-                final_recs, s->bstart.as<unsigned long long>(), (long long)limit,
-                s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+        if (compact) {
+            const Store12 &f = second ? c2 : c1;
+            EC_CHECK(launch_bucket(s, Rec12Source{f.key, f.meta, ibits, k, (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1)},
+                                   (unsigned)Bk, slots, (long long)limit));
+        } else {
+            EC_CHECK(launch_bucket(s, RecSource{second ? s->recs2.as<Rec>() : s->recs.as<Rec>()}, (unsigned)Bk, slots,
+                                   (long long)limit));
+        }
         kmark(s, 2, 1);
         mark(s, 2 * EC_STAGE_COMPACT + 1);
         EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -435,7 +480,86 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
 // Owner-side aggregation of exchanged k-mer records (count sum, first-event min) followed by
 // the solid filter: the merge step of the sharded path, and the way a gathered solid set is
 // loaded for phase_graph (limit = keep all).
+// The same on the LDS bucket tables of the fused path (k_bucket over the records sorted by
+// bucket): no HBM atomics.  Returns EC_OK with ok = false when a bucket overflows its table.
+int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx,
+                     bool &ok) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    ok = false;
+    int bbits = 0;
+    while (bbits < FINE_BITS && (double)n / (double)(1ull << bbits) > 1100.0) bbits++;
+    if ((double)n / (double)(1ull << bbits) > 2200.0) return EC_OK;  // too large for the LDS tables
+    const unsigned int nb = 1u << bbits;
+    const unsigned int slots = (double)n / (double)nb > 1100.0 ? 4096u : 2048u;
+    mark(s, 2 * EC_STAGE_COUNT);
+    EC_CHECK(s->mbid.ensure(std::max<uint64_t>(n, 1) * 4));
+    EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 1) * 4));
+    EC_CHECK(s->midx.ensure(std::max<uint64_t>(n, 1) * 4));
+    EC_CHECK(s->midx2.ensure(std::max<uint64_t>(n, 1) * 4));
+    EC_CHECK(s->bstart.ensure((nb + 1ull) * 8));
+    EC_HIP(hipMemsetAsync(s->bstart.p, 0, (nb + 1ull) * 8, st));
+    if (n) {
+        k_agg_bucket_ids<<<grid_for(n, B), B, 0, st>>>(d_agg, n, bbits, s->mbid.as<unsigned int>(),
+                                                      s->midx.as<unsigned int>());
+        size_t bytes = 0;
+        EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, s->mbid.as<unsigned int>(), s->mbid2.as<unsigned int>(),
+                                         s->midx.as<unsigned int>(), s->midx2.as<unsigned int>(), n, 0, bbits + 1, st));
+        EC_CHECK(s->tmp.ensure(bytes));
+        EC_HIP(rocprim::radix_sort_pairs(s->tmp.p, bytes, s->mbid.as<unsigned int>(), s->mbid2.as<unsigned int>(),
+                                         s->midx.as<unsigned int>(), s->midx2.as<unsigned int>(), n, 0, bbits + 1, st));
+        k_bucket_bounds<<<grid_for(n, B), B, 0, st>>>(s->mbid2.as<unsigned int>(), n, nb,
+                                                     s->bstart.as<unsigned long long>());
+    }
+    mark(s, 2 * EC_STAGE_COUNT + 1);
+    mark(s, 2 * EC_STAGE_COMPACT);
+    const uint64_t umax = (uint64_t)nb * slots;
+    EC_CHECK(s->dkey.ensure(umax * 8));
+    EC_CHECK(s->dcnt.ensure(umax * 4));
+    EC_CHECK(s->dfc.ensure(umax * 8));
+    EC_CHECK(s->dft.ensure(umax * 8));
+    EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
+    EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
+    EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+    const AggSource src{d_agg, s->midx2.as<unsigned int>()};
+    kmark(s, 2, 0);
+    EC_CHECK(launch_bucket(s, src, nb, slots, limit));
+    kmark(s, 2, 1);
+    mark(s, 2 * EC_STAGE_COMPACT + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.overflow) {
+        s->stats.table_retries++;
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        return EC_OK;
+    }
+    U = hsc.nsolid;
+    s->stats.n_distinct = hsc.ndistinct;
+    s->stats.n_solid = U;
+    s->stats.count_path = EC_PATH_PARTITIONED;
+    s->stats.n_buckets = nb;
+    s->stats.table_capacity = umax;
+    sidx = SolidIndex{};
+    sidx.sub = s->sub.as<SubSlot>();
+    sidx.bbits = bbits;
+    sidx.slots = slots;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
+    ok = true;
+    return EC_OK;
+}
+
 int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx) {
+    if (!(s->flags & EC_FLAG_GENERAL)) {
+        bool ok = false;
+        EC_CHECK(phase_merge_part(s, d_agg, n, limit, U, sidx, ok));
+        if (ok) return EC_OK;
+    }
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -863,7 +987,8 @@ int ec_session_destroy(ec_session *s) {
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
-                     &s->ocnt, &s->hist, &s->ftot, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc};
+                     &s->ocnt, &s->hist, &s->ftot, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
+                     &s->mbid, &s->mbid2, &s->midx, &s->midx2};
     for (auto *b : all) b->release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);

@@ -40,11 +40,76 @@ struct alignas(16) Rec {
 };
 static_assert(sizeof(Rec) == 16, "record layout");
 
+// Compact 12-B record for N-free reads of one length L (the common short-read case):
+// meta = read << (ibits + 1) | o << ibits | i, with i the window index (< m = L - k + 1 <=
+// 2^ibits) and o = 1 when the canonical string is the window's twin.  The local events are
+// then lC = o ? 2m-1-i : i and lT = o ? i : 2m-1-i (a palindrome: both i), as in window.h.
+struct Rec12 {
+    unsigned int klo, khi, meta;
+};
+static_assert(sizeof(Rec12) == 12, "compact record layout");
+
+__device__ inline unsigned long long rkey(const Rec &r) { return r.key; }
+__device__ inline unsigned long long rkey(const Rec12 &r) { return ((unsigned long long)r.khi << 32) | r.klo; }
+
+// record construction in the downsweep: window (fwd, rc) of read r with local events lf / lr
+struct MakeRec {
+    uint64_t read_base;
+    __device__ inline Rec operator()(uint64_t fwd, uint64_t rc, uint32_t lf, uint32_t lr, uint64_t r) const {
+        uint32_t lC = fwd <= rc ? lf : lr, lT = fwd <= rc ? lr : lf;
+        if (fwd == rc) lT = lC = lf;
+        Rec rec;
+        rec.key = fwd < rc ? fwd : rc;
+        rec.read = (unsigned int)(r + read_base);
+        rec.ev = lC | (lT << 16);
+        return rec;
+    }
+};
+struct MakeRec12 {
+    uint64_t read_base;
+    int ibits;
+    __device__ inline Rec12 operator()(uint64_t fwd, uint64_t rc, uint32_t lf, uint32_t, uint64_t r) const {
+        const uint64_t c = fwd < rc ? fwd : rc;
+        Rec12 rec;
+        rec.klo = (unsigned int)c;
+        rec.khi = (unsigned int)(c >> 32);
+        rec.meta = ((unsigned int)(r + read_base) << (ibits + 1)) | ((fwd <= rc ? 0u : 1u) << ibits) | lf;
+        return rec;
+    }
+};
+
 // solid lookup sub-table slot (bucket region of `slots` slots); id NONE = present, not solid
 struct alignas(16) SubSlot {
     unsigned long long key;
     unsigned int id;
     unsigned int pad;
+};
+
+// record stores: 16-B records in one array; compact records as split arrays (8-B keys,
+// 4-B meta) so every access is an aligned, coalesced dwordx2 / dword.  Measured (10M x 100 bp):
+// compact records cut the downsweep / refine / bucket traffic by 25 % but k_bucket runs 1.6x
+// longer over them (same instruction and LDS counts, half the resident waves -- not yet
+// understood), so they are opt-in (EC_FLAG_COMPACT_RECORDS) and 16-B records are the default.
+struct Store16 {
+    Rec *p;
+    __device__ inline Rec load(uint64_t i) const { return p[i]; }
+    __device__ inline void store(uint64_t i, const Rec &r) const { p[i] = r; }
+};
+struct Store12 {
+    unsigned long long *key;
+    unsigned int *meta;
+    __device__ inline Rec12 load(uint64_t i) const {
+        const unsigned long long k = key[i];
+        Rec12 r;
+        r.klo = (unsigned int)k;
+        r.khi = (unsigned int)(k >> 32);
+        r.meta = meta[i];
+        return r;
+    }
+    __device__ inline void store(uint64_t i, const Rec12 &r) const {
+        key[i] = rkey(r);
+        meta[i] = r.meta;
+    }
 };
 
 // LDS byte reader over a staged tile (slow path: reads with 'N')
@@ -111,7 +176,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
                                                        int k, uint64_t gsize, unsigned int *hist, uint8_t *hll_blocks,
                                                        unsigned long long *npos, unsigned long long *bad,
                                                        unsigned int *maxlocal, unsigned int *skew,
-                                                       unsigned int *thist) {
+                                                       unsigned int *thist, unsigned int *lens) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
     __shared__ unsigned int h_cnt[FINE / 2];
     __shared__ unsigned int t_cnt[1 << MAX_COARSE_BITS];  // this tile's coarse histogram
@@ -121,7 +186,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
     const uint64_t g = blockIdx.x;
     const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
     unsigned long long mypos = 0;
-    unsigned int mymax = 0, myskew = 0;
+    unsigned int mymax = 0, myskew = 0, mylmax = 0, mylmin = 0xFFFFFFFFu, mynonclean = 0;
     auto win = [&](uint64_t fwd, uint64_t rc) {
         const uint64_t c = fwd < rc ? fwd : rc;
         const uint64_t h = mix64(c);
@@ -142,12 +207,15 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
         if (flags == 0) {  // N-free read: one segment
             if (len >= (uint64_t)k) {
                 const uint32_t m = (uint32_t)(len - k + 1);
+                mylmax = max(mylmax, (uint32_t)len);
+                mylmin = min(mylmin, (uint32_t)len);
                 windows_clean(rv, (uint32_t)len, k, [&](uint64_t fwd, uint64_t rc, uint32_t) { win(fwd, rc); });
                 mypos += m;
                 mymax = max(mymax, 2 * m - 1);
             }
             return;
         }
+        mynonclean = 1;
         auto slow = [&](auto &rd) {
             for (uint64_t t = 0; t < len; t++) {
                 if (base_code(rd(s + t)) == 5) {
@@ -178,11 +246,17 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
         mypos += __shfl_down(mypos, o);
         mymax = max(mymax, (unsigned int)__shfl_down(mymax, o));
         myskew |= (unsigned int)__shfl_down(myskew, o);
+        mylmax = max(mylmax, (unsigned int)__shfl_down(mylmax, o));
+        mylmin = min(mylmin, (unsigned int)__shfl_down(mylmin, o));
+        mynonclean |= (unsigned int)__shfl_down(mynonclean, o);
     }
     if ((threadIdx.x & 63) == 0) {
         if (mypos) atomicAdd(npos, mypos);
         if (mymax) atomicMax(maxlocal, mymax);
         if (myskew) atomicOr(skew, 1u);
+        if (mylmax) atomicMax(&lens[0], mylmax);
+        if (mylmin != 0xFFFFFFFFu) atomicMax(&lens[1], ~mylmin);  // lens[1] = ~(min length)
+        if (mynonclean) atomicOr(&lens[2], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < FINE; i += blockDim.x) hist[g * FINE + i] = (h_cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
@@ -244,12 +318,12 @@ constexpr int DS_R = 8;
 constexpr int DS_BATCH = TILE_READS * DS_R;
 constexpr int DS_MAX_CBITS = 8;
 
+template <typename RecT, typename Make, typename Store>
 __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                          int k, uint64_t gsize, uint64_t ntiles, int cbits,
-                                                         const unsigned long long *offs, Rec *recs,
-                                                         uint64_t read_base) {
+                                                         const unsigned long long *offs, Store recs, Make mk) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
-    __shared__ Rec sorted[DS_BATCH];
+    __shared__ RecT sorted[DS_BATCH];
     __shared__ uint8_t sbk[DS_BATCH];
     __shared__ unsigned int bcnt[1 << DS_MAX_CBITS], bbeg[1 << DS_MAX_CBITS];
     __shared__ unsigned long long cur[1 << DS_MAX_CBITS], gbase[1 << DS_MAX_CBITS];
@@ -263,13 +337,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
     auto make = [&](uint64_t fwd, uint64_t rc, uint32_t lf, uint32_t lr, uint64_t r, unsigned int &cb) {
         const uint64_t c = fwd < rc ? fwd : rc;
         cb = cbits ? (unsigned int)(mix64(c) >> (64 - cbits)) : 0u;
-        uint32_t lC = fwd <= rc ? lf : lr, lT = fwd <= rc ? lr : lf;
-        if (fwd == rc) lT = lC = lf;
-        Rec rec;
-        rec.key = c;
-        rec.read = (unsigned int)(r + read_base);
-        rec.ev = lC | (lT << 16);
-        return rec;
+        return mk(fwd, rc, lf, lr, r);
     };
     for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
         const uint64_t r1 = min(r0 + TILE_READS, g1);
@@ -311,7 +379,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
             }
         const uint32_t m2 = 2 * m - 1;
         for (unsigned int round = 0; round < nrounds; round++) {
-            Rec rr[DS_R];
+            RecT rr[DS_R];
             unsigned int cb[DS_R], rk[DS_R];
 #pragma unroll
             for (int j = 0; j < DS_R; j++) {
@@ -357,7 +425,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
             const unsigned int total = s_total;
             for (unsigned int i = tid; i < total; i += TILE_READS) {
                 const unsigned int c = sbk[i];
-                recs[gbase[c] + (i - bbeg[c])] = sorted[i];
+                recs.store(gbase[c] + (i - bbeg[c]), sorted[i]);
             }
             if ((int)tid < C) bcnt[tid] = 0;
             __syncthreads();
@@ -367,8 +435,8 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
             auto slow = [&](auto &rd) {
                 for_each_window(rd, s, len, k, r, [&](uint64_t f2, uint64_t r2, uint64_t ef, uint64_t er) {
                     unsigned int c;
-                    const Rec rec = make(f2, r2, (uint32_t)ef, (uint32_t)er, r, c);
-                    recs[atomicAdd(&cur[c], 1ull)] = rec;
+                    const RecT rec = make(f2, r2, (uint32_t)ef, (uint32_t)er, r, c);
+                    recs.store(atomicAdd(&cur[c], 1ull), rec);
                 });
             };
             if (staged) {
@@ -385,9 +453,10 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
 // ---- refine: split each coarse bucket into its 2^(bbits-cbits) final buckets ----------------
 // one workgroup per coarse bucket; tiles of REFINE_TILE records are sorted by final bucket in
 // LDS and written out as contiguous runs (the final-bucket cursors live in LDS).
-__global__ void __launch_bounds__(BUCKET_THREADS) k_refine(const Rec *in, Rec *out, const unsigned long long *bstart,
+template <typename RecT, typename Store>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, const unsigned long long *bstart,
                                                           int cbits, int bbits) {
-    __shared__ Rec tile[REFINE_TILE];
+    __shared__ RecT tile[REFINE_TILE];
     __shared__ unsigned long long cur[64];
     __shared__ unsigned int tcnt[64], tbeg[64];
     const int F = 1 << (bbits - cbits);
@@ -399,14 +468,14 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(const Rec *in, Rec *o
         const unsigned int n = (unsigned int)min((uint64_t)REFINE_TILE, r1 - t0);
         if (threadIdx.x < 64) tcnt[threadIdx.x] = 0;
         __syncthreads();
-        Rec rr[PER];
+        RecT rr[PER];
         unsigned int jj[PER], rk[PER];
 #pragma unroll
         for (int q = 0; q < PER; q++) {
             const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
             if (i < n) {
-                rr[q] = in[t0 + i];
-                jj[q] = (unsigned int)(mix64(rr[q].key) >> (64 - bbits)) & (F - 1);
+                rr[q] = in.load(t0 + i);
+                jj[q] = (unsigned int)(mix64(rkey(rr[q])) >> (64 - bbits)) & (F - 1);
                 rk[q] = atomicAdd(&tcnt[jj[q]], 1u);
             }
         }
@@ -426,9 +495,9 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(const Rec *in, Rec *o
         }
         __syncthreads();
         for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
-            const Rec rec = tile[i];
-            const unsigned int j = (unsigned int)(mix64(rec.key) >> (64 - bbits)) & (F - 1);
-            out[cur[j] + (i - tbeg[j])] = rec;
+            const RecT rec = tile[i];
+            const unsigned int j = (unsigned int)(mix64(rkey(rec)) >> (64 - bbits)) & (F - 1);
+            out.store(cur[j] + (i - tbeg[j]), rec);
         }
         __syncthreads();
         if ((int)threadIdx.x < F) cur[threadIdx.x] += tcnt[threadIdx.x];
@@ -445,8 +514,46 @@ struct alignas(8) LSlot {
     unsigned int pad;
 };
 
-template <int SLOTS>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(const Rec *recs, const unsigned long long *bstart,
+// record sources of k_bucket: window records of the counting pass, or exchange records
+// (count sum, first-event min) of the multi-GPU merge, visited through a bucket-major permutation
+struct RecSource {
+    const Rec *recs;
+    __device__ inline void get(uint64_t i, unsigned long long &key, unsigned int &add, unsigned long long &eC,
+                               unsigned long long &eT) const {
+        const Rec rec = recs[i];
+        const unsigned int lC = rec.ev & 0xFFFFu, lT = rec.ev >> 16;
+        key = rec.key;
+        add = lC == lT ? 2u : 1u;  // even-k palindrome: build inserts it twice
+        eC = ((unsigned long long)rec.read << 32) | lC;
+        eT = ((unsigned long long)rec.read << 32) | lT;
+    }
+};
+
+struct Rec12Source {
+    const unsigned long long *key;
+    const unsigned int *meta;
+    int ibits;
+    int k;
+    unsigned int m2;  // 2m - 1
+    __device__ inline void get(uint64_t i, unsigned long long &kk, unsigned int &add, unsigned long long &eC,
+                               unsigned long long &eT) const {
+        kk = key[i];
+        const unsigned int mt = meta[i];
+        const unsigned long long rd = (unsigned long long)(mt >> (ibits + 1)) << 32;
+        const unsigned int w = mt & ((1u << ibits) - 1), o = (mt >> ibits) & 1u;
+        if (!(k & 1) && twin64(kk, k) == kk) {  // even-k palindrome: inserted twice at the forward event
+            add = 2;
+            eC = eT = rd | w;
+            return;
+        }
+        add = 1;
+        eC = rd | (o ? m2 - w : w);
+        eT = rd | (o ? w : m2 - w);
+    }
+};
+
+template <typename Src, int SLOTS>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsigned long long *bstart,
                                                           long long limit,
                                                           unsigned long long *dkey, unsigned int *dcnt,
                                                           unsigned long long *dfc, unsigned long long *dft,
@@ -466,12 +573,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(const Rec *recs, cons
     if (threadIdx.x == 0) s_over = 0;
     __syncthreads();
     const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
-    for (uint64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
-        const Rec rec = recs[i];
-        const uint64_t c = rec.key;
-        const unsigned int lC = rec.ev & 0xFFFFu, lT = rec.ev >> 16;
-        const unsigned long long eC = ((unsigned long long)rec.read << 32) | lC;
-        const unsigned long long eT = ((unsigned long long)rec.read << 32) | lT;
+    auto insert = [&](unsigned long long c, unsigned int add, unsigned long long eC, unsigned long long eT) {
         unsigned int slot = (unsigned int)mix64(c) & (SLOTS - 1);
         int probe = 0;
         for (; probe < SLOTS; probe++) {
@@ -485,11 +587,29 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(const Rec *recs, cons
         }
         if (probe == SLOTS) {
             s_over = 1;
-            continue;
+            return;
         }
-        atomicAdd(&tab[slot].count, lC == lT ? 2u : 1u);
+        if (add) atomicAdd(&tab[slot].count, add);
         if (eC < tab[slot].fC) atomicMin(&tab[slot].fC, eC);
         if (eT < tab[slot].fT) atomicMin(&tab[slot].fT, eT);
+    };
+    // BK_UNROLL records per thread per step, all loads issued before the inserts: the loop
+    // is bound by HBM latency, not bandwidth, without this memory-level parallelism
+    constexpr int BK_UNROLL = 4;
+    uint64_t i = r0 + threadIdx.x;
+    for (; i + (BK_UNROLL - 1) * (uint64_t)blockDim.x < r1; i += BK_UNROLL * (uint64_t)blockDim.x) {
+        unsigned long long c[BK_UNROLL], eC[BK_UNROLL], eT[BK_UNROLL];
+        unsigned int add[BK_UNROLL];
+#pragma unroll
+        for (int u = 0; u < BK_UNROLL; u++) src.get(i + u * (uint64_t)blockDim.x, c[u], add[u], eC[u], eT[u]);
+#pragma unroll
+        for (int u = 0; u < BK_UNROLL; u++) insert(c[u], add[u], eC[u], eT[u]);
+    }
+    for (; i < r1; i += blockDim.x) {
+        unsigned long long c, eC, eT;
+        unsigned int add;
+        src.get(i, c, add, eC, eT);
+        insert(c, add, eC, eT);
     }
     __syncthreads();
     if (s_over) {

@@ -133,4 +133,41 @@ __global__ void __launch_bounds__(256) k_export_dense(const K *dkey, const unsig
         out[t] = RecOf<K>::make(dkey[t], dcnt[t], dfc[t], dft[t]);
 }
 
+
+// ---- bucketed merge: exchange records -> LDS bucket tables (k_bucket over AggSource) -------
+// bucket id = top bbits of mix64(key) (the fused path's bucket hash, so the SolidIndex
+// sub-table layout is shared); filler records (all-ones key) go to bucket 2^bbits, past the end.
+__global__ void __launch_bounds__(256) k_agg_bucket_ids(const Agg *in, uint64_t n, int bbits, unsigned int *bid,
+                                                        unsigned int *idx) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long key = in[t].key;
+        bid[t] = key == EMPTY_KEY ? (1u << bbits) : (bbits ? (unsigned int)(mix64(key) >> (64 - bbits)) : 0u);
+        idx[t] = (unsigned int)t;
+    }
+}
+
+// bstart[b] = first position of bucket b in the sorted ids (b = 0..nb; bstart[nb] = real records)
+__global__ void __launch_bounds__(256) k_bucket_bounds(const unsigned int *sbid, uint64_t n, unsigned int nb,
+                                                       unsigned long long *bstart) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const long long b = sbid[i], pb = i ? (long long)sbid[i - 1] : -1;
+        for (long long q = pb + 1; q <= b && q <= (long long)nb; q++) bstart[q] = i;
+        if (i + 1 == n)
+            for (long long q = b + 1; q <= (long long)nb; q++) bstart[q] = n;
+    }
+}
+
+struct AggSource {
+    const Agg *in;
+    const unsigned int *perm;
+    __device__ inline void get(uint64_t i, unsigned long long &key, unsigned int &add, unsigned long long &eC,
+                               unsigned long long &eT) const {
+        const Agg a = in[perm[i]];
+        key = a.key;
+        add = a.count;
+        eC = a.fC;
+        eT = a.fT;
+    }
+};
+
 }  // namespace ec

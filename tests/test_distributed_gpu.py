@@ -40,6 +40,20 @@ def test_local_sharded_equals_oracle(engines, world, seed, g, n, L, err, k):
     assert res.links == oracle.unpack_links(ref)
 
 
+@pytest.mark.parametrize("world", [1, 3])
+def test_local_sharded_general_tables(engines, world):
+    """EC_FLAG_GENERAL: HBM-table counting and HBM-table merges instead of the LDS buckets"""
+    import distributed
+
+    buf, off = make_reads(20_000, 6_000, 100, 7100, err=0.002, n_rate=0.001)
+    ref = oracle.assemble_packed(buf, off, 27, 1)
+    res, P = distributed.local_sharded_assemble(engines[:world], buf, off, 27, 1, eulerhip.EC_FLAG_GENERAL)
+    assert P == ref["n_positions"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert res.links == oracle.unpack_links(ref)
+    assert res.stats.count_path == eulerhip.EC_PATH_GENERAL
+
+
 def test_rccl_world1_sharded(engines):
     import torch
     import torch.distributed as dist
