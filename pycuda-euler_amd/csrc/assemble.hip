@@ -94,7 +94,7 @@ struct ec_session {
     unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
     unsigned flags = 0;        // flags of the current call
-    DevBuf ocnt, rbc, mbid, mbid2, midx, midx2;
+    DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur;
 };
 
 namespace ec {
@@ -337,7 +337,12 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         int maxc = MAX_COARSE_BITS;
         if (const char *e = getenv("EULERHIP_COARSE_BITS")) maxc = std::max(1, std::min(MAX_COARSE_BITS, atoi(e)));
         maxc = std::min(maxc, DS_MAX_CBITS);
-        const int cbits = std::min(bbits, std::max(maxc, bbits - 6));  // refine splits <= 64 ways
+        // fewest coarse buckets the refine fan-out allows: longer downsweep runs (measured:
+        // 128 vs 256 coarse buckets, k_downsweep 5.56 -> 4.98 ms at 10M x 100 bp)
+        int fan = 0;
+        while ((1 << (fan + 1)) <= REFINE_FANOUT) fan++;
+        int cbits = std::min(bbits, std::max(1, bbits - fan));
+        if (getenv("EULERHIP_COARSE_BITS")) cbits = std::min(bbits, std::max(maxc, bbits - fan));
         const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
         mark(s, 2 * EC_STAGE_COUNT);
         EC_CHECK(s->cnt.ensure(Ck * ntiles * 8));
@@ -379,14 +384,18 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         kmark(s, 1, 1);
         bool second = false;
         if (bbits > cbits) {
+            // split every coarse bucket over RS workgroups (>= 4 per CU in flight)
+            const unsigned RS = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8, 1024 / Ck));
+            EC_CHECK(s->gcur.ensure(Bk * 8));
+            EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
             kmark(s, 4, 0);
             if (compact)
-                k_refine<Rec12, Store12><<<(unsigned)Ck, BUCKET_THREADS, 0, st>>>(c1, c2, s->bstart.as<unsigned long long>(),
-                                                                                 cbits, bbits);
+                k_refine<Rec12, Store12><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                    c1, c2, s->bstart.as<unsigned long long>(), s->gcur.as<unsigned long long>(), cbits, bbits);
             else
-                k_refine<Rec, Store16><<<(unsigned)Ck, BUCKET_THREADS, 0, st>>>(
-                    Store16{s->recs.as<Rec>()}, Store16{s->recs2.as<Rec>()}, s->bstart.as<unsigned long long>(), cbits,
-                    bbits);
+                k_refine<Rec, Store16><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                    Store16{s->recs.as<Rec>()}, Store16{s->recs2.as<Rec>()}, s->bstart.as<unsigned long long>(),
+                    s->gcur.as<unsigned long long>(), cbits, bbits);
             kmark(s, 4, 1);
             second = true;
         }
@@ -988,7 +997,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
                      &s->ocnt, &s->hist, &s->ftot, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
-                     &s->mbid, &s->mbid2, &s->midx, &s->midx2};
+                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur};
     for (auto *b : all) b->release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);

@@ -31,6 +31,7 @@ constexpr int STAGE_BYTES = 28672;         // LDS staging per tile
 constexpr int BUCKET_THREADS = 1024;
 constexpr int MAX_COARSE_BITS = 9;         // downsweep writes <= 512 bucket runs per group
 constexpr int REFINE_TILE = 4096;          // records per refine tile (64 KiB of LDS)
+constexpr int REFINE_FANOUT = 256;         // final buckets per coarse bucket
 constexpr unsigned int MAX_LOCAL_EVENT = 65535;
 
 struct alignas(16) Rec {
@@ -453,20 +454,24 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
 // ---- refine: split each coarse bucket into its 2^(bbits-cbits) final buckets ----------------
 // one workgroup per coarse bucket; tiles of REFINE_TILE records are sorted by final bucket in
 // LDS and written out as contiguous runs (the final-bucket cursors live in LDS).
+// gridDim.y workgroups share a coarse bucket (contiguous tile ranges); each tile reserves its
+// runs in the final buckets with one global atomic per final bucket (cursor gcur, initialised
+// to bstart).  Run order inside a final bucket is then arbitrary -- k_bucket is order-free.
 template <typename RecT, typename Store>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, const unsigned long long *bstart,
-                                                          int cbits, int bbits) {
+                                                          unsigned long long *gcur, int cbits, int bbits) {
     __shared__ RecT tile[REFINE_TILE];
-    __shared__ unsigned long long cur[64];
-    __shared__ unsigned int tcnt[64], tbeg[64];
+    __shared__ unsigned long long base[REFINE_FANOUT];
+    __shared__ unsigned int tcnt[REFINE_FANOUT], tbeg[REFINE_FANOUT], wsum[REFINE_FANOUT / 64];
     const int F = 1 << (bbits - cbits);
     const uint64_t c = blockIdx.x;
-    for (int j = threadIdx.x; j < F; j += blockDim.x) cur[j] = bstart[c * F + j];
     const uint64_t r0 = bstart[c * F], r1 = bstart[(c + 1) * F];
+    const uint64_t nt = (r1 - r0 + REFINE_TILE - 1) / REFINE_TILE;
+    const uint64_t tb = nt * blockIdx.y / gridDim.y, te = nt * (blockIdx.y + 1) / gridDim.y;
     constexpr int PER = REFINE_TILE / BUCKET_THREADS;
-    for (uint64_t t0 = r0; t0 < r1; t0 += REFINE_TILE) {
+    for (uint64_t t0 = r0 + tb * REFINE_TILE; t0 < r1 && t0 < r0 + te * REFINE_TILE; t0 += REFINE_TILE) {
         const unsigned int n = (unsigned int)min((uint64_t)REFINE_TILE, r1 - t0);
-        if (threadIdx.x < 64) tcnt[threadIdx.x] = 0;
+        if (threadIdx.x < REFINE_FANOUT) tcnt[threadIdx.x] = 0;
         __syncthreads();
         RecT rr[PER];
         unsigned int jj[PER], rk[PER];
@@ -480,12 +485,22 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, 
             }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned int acc = 0;
-            for (int j = 0; j < F; j++) {
-                tbeg[j] = acc;
-                acc += tcnt[j];
+        if (threadIdx.x < REFINE_FANOUT) {  // exclusive scan of the tile counts + run reservation
+            const unsigned int v = (int)threadIdx.x < F ? tcnt[threadIdx.x] : 0u;
+            unsigned int incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int u = __shfl_up(incl, o);
+                if ((int)(threadIdx.x & 63) >= o) incl += u;
             }
+            tbeg[threadIdx.x] = incl - v;
+            if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+            if (v) base[threadIdx.x] = atomicAdd(&gcur[c * F + threadIdx.x], (unsigned long long)v);
+        }
+        __syncthreads();
+        if (threadIdx.x >= 64 && threadIdx.x < REFINE_FANOUT) {
+            unsigned int add = 0;
+            for (unsigned int w = 0; w < (threadIdx.x >> 6); w++) add += wsum[w];
+            tbeg[threadIdx.x] += add;
         }
         __syncthreads();
 #pragma unroll
@@ -497,10 +512,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, 
         for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
             const RecT rec = tile[i];
             const unsigned int j = (unsigned int)(mix64(rkey(rec)) >> (64 - bbits)) & (F - 1);
-            out.store(cur[j] + (i - tbeg[j]), rec);
+            out.store(base[j] + (i - tbeg[j]), rec);
         }
-        __syncthreads();
-        if ((int)threadIdx.x < F) cur[threadIdx.x] += tcnt[threadIdx.x];
         __syncthreads();
     }
 }
