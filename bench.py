@@ -56,15 +56,16 @@ def alg_bytes(P, R, L, U, K=8):
     return R * L + P * (K + 8) + U * (10 * K + 33)
 
 
-def kernel_alg_bytes(name, P, R, L, K=8):
-    """Algorithmic bytes per launch of the counting kernels (DESIGN.md "Roofline accounting"):
-    k_upsweep   reads the ASCII reads once                       R*L
-    k_downsweep reads them again + writes one 16-B record/pos    R*L + 16*P
-    k_bucket    one canonical insert per position   P*(K+8)
-    k_count     general path: read once + one insert/position    R*L + P*(K+8)
-    k_refine    reads + writes every 16-B record once            32*P"""
-    return {"k_upsweep": R * L, "k_downsweep": R * L + 16 * P, "k_bucket": P * (K + 8),
-            "k_count": R * L + P * (K + 8), "k_refine": 32 * P}[name]
+def kernel_alg_bytes(name, P, R, L, K=8, rec=16):
+    """Algorithmic bytes per launch of the counting kernels (DESIGN.md "Roofline accounting"),
+    rec = window record bytes (16, or 12 for compact records):
+    k_upsweep   reads the ASCII reads once                          R*L
+    k_downsweep reads them again + writes one record/position       R*L + rec*P
+    k_refine    reads every record, writes it as a 16-B record      (rec + 16)*P
+    k_bucket    one canonical insert per position      P*(K+8)
+    k_count     general path: read once + one insert/position       R*L + P*(K+8)"""
+    return {"k_upsweep": R * L, "k_downsweep": R * L + rec * P, "k_bucket": P * (K + 8),
+            "k_count": R * L + P * (K + 8), "k_refine": (rec + 16) * P}[name]
 
 
 def cpu_baseline(buf, off, k, sample_reads):
@@ -111,7 +112,7 @@ def main():
     ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the multi-GPU path even with one rank")
-    ap.add_argument("--compact-records", action="store_true", help="12-B count records (EC_FLAG_COMPACT_RECORDS)")
+    ap.add_argument("--wide-records", action="store_true", help="16-B count records only (EC_FLAG_WIDE_RECORDS)")
     args = ap.parse_args()
     # stdout carries exactly one JSON line: libraries that print banners (RCCL prints its
     # version block on communicator init) are sent to stderr
@@ -157,7 +158,7 @@ def main():
         def step(timing=False):
             sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), cfg["reads"], k, 1,
                             (eulerhip.EC_FLAG_TIMING if timing else 0)
-                            | (eulerhip.EC_FLAG_COMPACT_RECORDS if args.compact_records else 0))
+                            | (eulerhip.EC_FLAG_WIDE_RECORDS if args.wide_records else 0))
     else:
         import distributed
 
@@ -207,7 +208,8 @@ def main():
     kname = eulerhip.KERNEL_NAMES[kid]
     kms = float(kern[kid])
     K = 8 if k <= 32 else 16  # key bytes
-    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L, K)  # this rank's launch
+    rec = int(st.record_bytes) or 16
+    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L, K, rec)  # this rank's launch
     achieved = kb / (kms / 1e3) / 1e9
     tr = load_traffic(cfg["name"], kname)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -231,6 +233,7 @@ def main():
                    "positions": P, "solid_kmers": U,
                    "contigs": int(st.n_contigs if not use_dist else runner.engine.stats().n_contigs),
                    "count_path": ["partitioned", "general"][int(st.count_path)], "buckets": int(st.n_buckets),
+                   "record_bytes": int(st.record_bytes),
                    "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
         "roofline": roof,
         "cpu_baseline": cpu,

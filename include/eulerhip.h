@@ -49,7 +49,8 @@ typedef struct ec_session ec_session;
 #define EC_FLAG_WANT_DICT 1u /* also keep build()'s ordered dict for ec_copy_dict */
 #define EC_FLAG_TIMING 2u    /* record per-stage HIP-event times (ec_stats.stage_ms) */
 #define EC_FLAG_GENERAL 4u   /* force the general (single HBM hash table) counting path */
-#define EC_FLAG_COMPACT_RECORDS 8u /* partitioned path: 12-B records when all reads are N-free and of one length */
+#define EC_FLAG_WIDE_RECORDS 8u /* partitioned path: 16-B records only (default: 12-B records when every
+                                  * read is N-free and of one length) */
 
 #define EC_NSTAGES 8
 /* stage ids for ec_stats.stage_ms / ec_stage_name */
@@ -89,7 +90,7 @@ typedef struct {
     uint32_t rank_rounds;    /* Wyllie rounds on the ruler list                               */
     uint32_t count_path;     /* EC_PATH_*                                                     */
     uint32_t n_buckets;      /* partitioned path: B                                           */
-    uint32_t record_bytes;   /* partitioned path: 16, or 12 with EC_FLAG_COMPACT_RECORDS        */
+    uint32_t record_bytes;   /* partitioned path: 12 (compact) or 16 bytes per window record    */
     uint32_t reserved;
     float stage_ms[EC_NSTAGES];   /* EC_FLAG_TIMING only */
     float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING only */

@@ -349,9 +349,9 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->offs.ensure(Ck * ntiles * 8));
         EC_CHECK(s->tot.ensure((Bk + 1) * 8));
         EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
-        // compact 12-B records (opt-in): every read staged and N-free, one read length, events fit
+        // compact 12-B records: every read staged and N-free, one read length, events fit
         const unsigned int lmax = hsc.lens[0], lmin = ~hsc.lens[1];
-        bool compact = (flags & EC_FLAG_COMPACT_RECORDS) && hsc.lens[2] == 0 && hsc.lens[1] != 0 && lmax == lmin;
+        bool compact = !(flags & EC_FLAG_WIDE_RECORDS) && hsc.lens[2] == 0 && hsc.lens[1] != 0 && lmax == lmin;
         int ibits = 1;
         if (compact) {
             const uint64_t m = (uint64_t)lmax - (uint64_t)k + 1;
@@ -361,17 +361,15 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         const size_t rsz = compact ? sizeof(Rec12) : sizeof(Rec);
         s->stats.record_bytes = (uint32_t)rsz;
         EC_CHECK(s->recs.ensure(P * rsz));
-        if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * rsz));
+        if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * sizeof(Rec)));  // refine writes 16-B records
         k_coarse<<<grid_for(Ck * ntiles, B, 8192), B, 0, st>>>(s->thist.as<unsigned int>(), ntiles, cbits,
                                                               s->cnt.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ntiles));
         k_bucket_totals<<<grid_for(Bk + 1, B), B, 0, st>>>(s->ftot.as<unsigned long long>(), bbits,
                                                           s->tot.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
-        // compact records: keys [0, 8P) and meta [8P, 12P) of the record buffer
+        // compact records: keys [0, 8P) and meta [8P, 12P) of the first record buffer
         const Store12 c1{s->recs.as<unsigned long long>(), reinterpret_cast<unsigned int *>(s->recs.as<uint8_t>() + P * 8)};
-        const Store12 c2{s->recs2.as<unsigned long long>(),
-                         reinterpret_cast<unsigned int *>(s->recs2.as<uint8_t>() + P * 8)};
         kmark(s, 1, 0);
         if (compact)
             k_downsweep<Rec12, MakeRec12, Store12><<<(unsigned)ngroups, TILE_READS, 0, st>>>(
@@ -389,11 +387,12 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             EC_CHECK(s->gcur.ensure(Bk * 8));
             EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
             kmark(s, 4, 0);
-            if (compact)
-                k_refine<Rec12, Store12><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
-                    c1, c2, s->bstart.as<unsigned long long>(), s->gcur.as<unsigned long long>(), cbits, bbits);
+            if (compact)  // 12-B in, 16-B out: k_bucket reads 16-B records
+                k_refine<Rec12, Store12, Store12to16><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                    c1, Store12to16{s->recs2.as<Rec>(), ibits, k, (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1)},
+                    s->bstart.as<unsigned long long>(), s->gcur.as<unsigned long long>(), cbits, bbits);
             else
-                k_refine<Rec, Store16><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                k_refine<Rec, Store16, Store16><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
                     Store16{s->recs.as<Rec>()}, Store16{s->recs2.as<Rec>()}, s->bstart.as<unsigned long long>(),
                     s->gcur.as<unsigned long long>(), cbits, bbits);
             kmark(s, 4, 1);
@@ -408,9 +407,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->dft.ensure(umax * 8));
         EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
         kmark(s, 2, 0);
-        if (compact) {
-            const Store12 &f = second ? c2 : c1;
-            EC_CHECK(launch_bucket(s, Rec12Source{f.key, f.meta, ibits, k, (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1)},
+        if (compact && !second) {
+            EC_CHECK(launch_bucket(s, Rec12Source{c1.key, c1.meta, ibits, k, (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1)},
                                    (unsigned)Bk, slots, (long long)limit));
         } else {
             EC_CHECK(launch_bucket(s, RecSource{second ? s->recs2.as<Rec>() : s->recs.as<Rec>()}, (unsigned)Bk, slots,

@@ -88,14 +88,34 @@ struct alignas(16) SubSlot {
 
 // record stores: 16-B records in one array; compact records as split arrays (8-B keys,
 // 4-B meta) so every access is an aligned, coalesced dwordx2 / dword.  Measured (10M x 100 bp):
-// compact records cut the downsweep / refine / bucket traffic by 25 % but k_bucket runs 1.6x
-// longer over them (same instruction and LDS counts, half the resident waves -- not yet
-// understood), so they are opt-in (EC_FLAG_COMPACT_RECORDS) and 16-B records are the default.
+// k_bucket runs 1.6x longer over compact records (same instruction and LDS counts, half the
+// resident waves -- not understood), so the refine widens them back to 16 B (Store12to16):
+// compact records then save 25 % of the downsweep write and the refine read.
 struct Store16 {
     Rec *p;
     __device__ inline Rec load(uint64_t i) const { return p[i]; }
     __device__ inline void store(uint64_t i, const Rec &r) const { p[i] = r; }
 };
+// refine output of compact records widened back to 16-B records (lC | lT events), so that
+// k_bucket reads the 16-B layout it runs fastest on
+struct Store12to16 {
+    Rec *p;
+    int ibits;
+    int k;
+    unsigned int m2;  // 2m - 1
+    __device__ inline void store(uint64_t i, const Rec12 &r) const {
+        const unsigned long long key = rkey(r);
+        const unsigned int w = r.meta & ((1u << ibits) - 1), o = (r.meta >> ibits) & 1u;
+        unsigned int lC = o ? m2 - w : w, lT = o ? w : m2 - w;
+        if (!(k & 1) && twin64(key, k) == key) lC = lT = w;  // even-k palindrome
+        Rec out;
+        out.key = key;
+        out.read = r.meta >> (ibits + 1);
+        out.ev = lC | (lT << 16);
+        p[i] = out;
+    }
+};
+
 struct Store12 {
     unsigned long long *key;
     unsigned int *meta;
@@ -457,8 +477,8 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
 // gridDim.y workgroups share a coarse bucket (contiguous tile ranges); each tile reserves its
 // runs in the final buckets with one global atomic per final bucket (cursor gcur, initialised
 // to bstart).  Run order inside a final bucket is then arbitrary -- k_bucket is order-free.
-template <typename RecT, typename Store>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, const unsigned long long *bstart,
+template <typename RecT, typename StoreIn, typename StoreOut>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut out, const unsigned long long *bstart,
                                                           unsigned long long *gcur, int cbits, int bbits) {
     __shared__ RecT tile[REFINE_TILE];
     __shared__ unsigned long long base[REFINE_FANOUT];
@@ -469,7 +489,23 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, 
     const uint64_t nt = (r1 - r0 + REFINE_TILE - 1) / REFINE_TILE;
     const uint64_t tb = nt * blockIdx.y / gridDim.y, te = nt * (blockIdx.y + 1) / gridDim.y;
     constexpr int PER = REFINE_TILE / BUCKET_THREADS;
-    for (uint64_t t0 = r0 + tb * REFINE_TILE; t0 < r1 && t0 < r0 + te * REFINE_TILE; t0 += REFINE_TILE) {
+    const uint64_t tend = min(r1, r0 + te * REFINE_TILE);
+    // software pipeline: tile t+1 is loaded into registers while tile t's runs are stored
+    RecT nx[PER];
+    auto load_tile = [&](uint64_t t0) {
+        const unsigned int n = (unsigned int)min((uint64_t)REFINE_TILE, r1 - t0);
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) nx[q] = in.load(t0 + i);
+        }
+    };
+    // (measured: pipelining pays for 12-B input, 4.86 -> 4.35 ms; 16-B input runs slower with it)
+    constexpr bool PIPE = sizeof(RecT) < 16;
+    uint64_t t0 = r0 + tb * REFINE_TILE;
+    if (t0 < tend) load_tile(t0);
+    for (; t0 < tend; t0 += REFINE_TILE) {
+        if (!PIPE && t0 != r0 + tb * REFINE_TILE) load_tile(t0);
         const unsigned int n = (unsigned int)min((uint64_t)REFINE_TILE, r1 - t0);
         if (threadIdx.x < REFINE_FANOUT) tcnt[threadIdx.x] = 0;
         __syncthreads();
@@ -478,8 +514,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, 
 #pragma unroll
         for (int q = 0; q < PER; q++) {
             const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            rr[q] = nx[q];
             if (i < n) {
-                rr[q] = in.load(t0 + i);
                 jj[q] = (unsigned int)(mix64(rkey(rr[q])) >> (64 - bbits)) & (F - 1);
                 rk[q] = atomicAdd(&tcnt[jj[q]], 1u);
             }
@@ -509,6 +545,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(Store in, Store out, 
             if (i < n) tile[tbeg[jj[q]] + rk[q]] = rr[q];
         }
         __syncthreads();
+        if (PIPE && t0 + REFINE_TILE < tend) load_tile(t0 + REFINE_TILE);
         for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
             const RecT rec = tile[i];
             const unsigned int j = (unsigned int)(mix64(rkey(rec)) >> (64 - bbits)) & (F - 1);

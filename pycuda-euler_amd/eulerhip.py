@@ -31,7 +31,7 @@ EC_ERR_STATE = -6
 EC_FLAG_WANT_DICT = 1
 EC_FLAG_TIMING = 2
 EC_FLAG_GENERAL = 4
-EC_FLAG_COMPACT_RECORDS = 8
+EC_FLAG_WIDE_RECORDS = 8
 EC_NSTAGES = 8
 EC_NKERNELS = 5
 KERNEL_NAMES = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
@@ -270,10 +270,10 @@ class Session:
             items = [(s[i * k:(i + 1) * k], int(cnt[i])) for i in range(nd)]
         return Result(k, st, chars.raw[:nch], coff, loff, links[:nl], items)
 
-    def assemble(self, reads, k, limit=1, want_dict=False, timing=False, general=False, compact_records=False):
+    def assemble(self, reads, k, limit=1, want_dict=False, timing=False, general=False, wide_records=False):
         buf, off = pack_reads(reads)
         flags = (EC_FLAG_WANT_DICT if want_dict else 0) | (EC_FLAG_TIMING if timing else 0)
-        flags |= (EC_FLAG_GENERAL if general else 0) | (EC_FLAG_COMPACT_RECORDS if compact_records else 0)
+        flags |= (EC_FLAG_GENERAL if general else 0) | (EC_FLAG_WIDE_RECORDS if wide_records else 0)
         self.run_host(buf, off, k, limit, flags)
         return self.fetch(k, want_dict)
 

@@ -32,9 +32,9 @@ def test_golden(gpu_session, case):
 
 
 @pytest.mark.parametrize("case", CASES32[1::2], ids=[c["name"] for c in CASES32[1::2]])
-def test_golden_compact_records(gpu_session, case):
-    """12-B records (EC_FLAG_COMPACT_RECORDS; taken when every read is N-free and of one length)"""
-    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, compact_records=True)
+def test_golden_wide_records(gpu_session, case):
+    """16-B records forced (EC_FLAG_WIDE_RECORDS; one-length N-free inputs default to 12-B records)"""
+    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, wide_records=True)
     assert [[x, c] for x, c in res.dict_items] == case["d"]
     assert res.contigs == case["contigs"]
     assert res.links == case["links"]
@@ -85,14 +85,14 @@ SYN = [
 ]
 
 
-@pytest.mark.parametrize("mode", ["partitioned", "compact_records", "general"])
+@pytest.mark.parametrize("mode", ["partitioned", "wide_records", "general"])
 @pytest.mark.parametrize("g,n,L,seed,err,nr,circ,k", SYN)
 def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode):
     buf, off = make_reads(g, n, L, 1000 + seed, err=err, n_rate=nr, circular=circ)
     want_dict = g <= 50_000
     ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
     flags = (eulerhip.EC_FLAG_WANT_DICT if want_dict else 0) | {"partitioned": 0, "general": eulerhip.EC_FLAG_GENERAL,
-                                                                "compact_records": eulerhip.EC_FLAG_COMPACT_RECORDS}[mode]
+                                                                "wide_records": eulerhip.EC_FLAG_WIDE_RECORDS}[mode]
     gpu_session.run_host(buf, off, k, 1, flags)
     res = gpu_session.fetch(k, want_dict)
     assert res.stats.n_positions == ref["n_positions"]
@@ -102,9 +102,9 @@ def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode)
     assert res.links == rl
     if want_dict:
         assert [[x, c] for x, c in res.dict_items] == ref["d"]
-    if mode == "compact_records" and k <= 32 and nr == 0:  # one read length, no N: 12-B records
+    if mode == "partitioned" and k <= 32 and nr == 0:  # one read length, no N: 12-B records
         assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.record_bytes == 12
-    if mode == "partitioned" and k <= 32:
+    if mode == "wide_records" and k <= 32:
         assert res.stats.record_bytes == 16
 
 
