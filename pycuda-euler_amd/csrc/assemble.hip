@@ -73,7 +73,7 @@ struct ec_session {
     DevBuf h_reads, h_offsets;  // H2D staging for ec_assemble_host
     DevBuf hll, scal, table, dkey, dcnt, dfc, dft, upal, outdeg, cand, succ, pred, st0, st1;
     DevBuf rid, roff, rlist, nextR, PK, RK, PL, PM;
-    DevBuf hist, ftot, thist, cnt, offs, bstart, tot, recs, recs2, sub;
+    DevBuf hist, ftot, cnt, offs, bstart, tot, recs, recs2, sub;
     DevBuf startOf, skeys, svals, skeys2, svals2, cidxOf, clen, coff, chars, cfirst, clast, headOf, tailOf;
     DevBuf lk, lcnt, tmp, dchars, dcounts;
     // results (host)
@@ -294,13 +294,11 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     EC_CHECK(s->hist.ensure(ngroups * FINE * 4));
     EC_CHECK(s->hll.ensure(ngroups * (1 << HLL_REG_BITS)));
     EC_CHECK(s->ftot.ensure((FINE + (1 << HLL_REG_BITS)) * 8));
-    EC_CHECK(s->thist.ensure(std::max<uint64_t>(ntiles, 1) * (1 << MAX_COARSE_BITS) * 4));
     if (nreads) {
         kmark(s, 0, 0);
         k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
                                                            s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad,
-                                                           &dsc->maxlocal, &dsc->skew, s->thist.as<unsigned int>(),
-                                                           dsc->lens);
+                                                           &dsc->maxlocal, &dsc->skew, dsc->lens);
         kmark(s, 0, 1);
         EC_HIP(hipMemsetAsync(s->ftot.p, 0, (FINE + (1 << HLL_REG_BITS)) * 8, st));
         k_fine_totals<<<dim3(FINE / 256, TOT_SLICES), 256, 0, st>>>(
@@ -345,8 +343,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         if (getenv("EULERHIP_COARSE_BITS")) cbits = std::min(bbits, std::max(maxc, bbits - fan));
         const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
         mark(s, 2 * EC_STAGE_COUNT);
-        EC_CHECK(s->cnt.ensure(Ck * ntiles * 8));
-        EC_CHECK(s->offs.ensure(Ck * ntiles * 8));
+        EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
+        EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
         EC_CHECK(s->tot.ensure((Bk + 1) * 8));
         EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
         // compact 12-B records: every read staged and N-free, one read length, events fit
@@ -362,9 +360,9 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         s->stats.record_bytes = (uint32_t)rsz;
         EC_CHECK(s->recs.ensure(P * rsz));
         if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * sizeof(Rec)));  // refine writes 16-B records
-        k_coarse<<<grid_for(Ck * ntiles, B, 8192), B, 0, st>>>(s->thist.as<unsigned int>(), ntiles, cbits,
-                                                              s->cnt.as<unsigned long long>());
-        EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ntiles));
+        k_coarse<<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
+                                                               s->cnt.as<unsigned long long>());
+        EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ngroups));
         k_bucket_totals<<<grid_for(Bk + 1, B), B, 0, st>>>(s->ftot.as<unsigned long long>(), bbits,
                                                           s->tot.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
@@ -373,11 +371,11 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         kmark(s, 1, 0);
         if (compact)
             k_downsweep<Rec12, MakeRec12, Store12><<<(unsigned)ngroups, TILE_READS, 0, st>>>(
-                d_reads, d_off, nreads, k, gsize, ntiles, cbits, s->offs.as<unsigned long long>(), c1,
+                d_reads, d_off, nreads, k, gsize, ngroups, cbits, s->offs.as<unsigned long long>(), c1,
                 MakeRec12{read_base, ibits});
         else
             k_downsweep<Rec, MakeRec, Store16><<<(unsigned)ngroups, TILE_READS, 0, st>>>(
-                d_reads, d_off, nreads, k, gsize, ntiles, cbits, s->offs.as<unsigned long long>(),
+                d_reads, d_off, nreads, k, gsize, ngroups, cbits, s->offs.as<unsigned long long>(),
                 Store16{s->recs.as<Rec>()}, MakeRec{read_base});
         kmark(s, 1, 1);
         bool second = false;
@@ -782,7 +780,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
     s->stats.rank_rounds = 0;
     if (U) {
         EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 4, st));
-        const unsigned int masks[4] = {31u, 7u, 1u, 0u};
+        unsigned int masks[4] = {31u, 7u, 1u, 0u};
+        if (const char *e = getenv("EULERHIP_RULER_MASK")) masks[0] = (unsigned int)atoi(e);
         unsigned int r0 = 0;
         for (int it = 0; it < 4; it++) {
             const unsigned int nblk = (unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK);
@@ -994,7 +993,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
-                     &s->ocnt, &s->hist, &s->ftot, &s->thist, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
+                     &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur};
     for (auto *b : all) b->release();
     if (s->events) {

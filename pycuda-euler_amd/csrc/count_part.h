@@ -197,10 +197,9 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
                                                        int k, uint64_t gsize, unsigned int *hist, uint8_t *hll_blocks,
                                                        unsigned long long *npos, unsigned long long *bad,
                                                        unsigned int *maxlocal, unsigned int *skew,
-                                                       unsigned int *thist, unsigned int *lens) {
+                                                       unsigned int *lens) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
     __shared__ unsigned int h_cnt[FINE / 2];
-    __shared__ unsigned int t_cnt[1 << MAX_COARSE_BITS];  // this tile's coarse histogram
     __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
     for (int i = threadIdx.x; i < FINE / 2; i += blockDim.x) h_cnt[i] = 0;
     for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x) h_reg[i] = 0;
@@ -217,7 +216,6 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
         const uint32_t f = (uint32_t)(h >> (64 - FINE_BITS));
         const uint32_t sh16 = (f & 1) * 16;
         const uint32_t old = atomicAdd(&h_cnt[f >> 1], 1u << sh16);
-        atomicAdd(&t_cnt[f >> (FINE_BITS - MAX_COARSE_BITS)], 1u);
         myskew |= ((old >> sh16) & 0xFFFFu) >= 0xFFFEu;
         if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
     };
@@ -257,11 +255,6 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
             ByteReader br(buf);
             slow(br);
         }
-    }, [&](uint64_t) {
-        for (int i = threadIdx.x; i < (1 << MAX_COARSE_BITS); i += blockDim.x) t_cnt[i] = 0;
-    }, [&](uint64_t tile) {
-        for (int i = threadIdx.x; i < (1 << MAX_COARSE_BITS); i += blockDim.x)
-            thist[tile * (1 << MAX_COARSE_BITS) + i] = t_cnt[i];
     });
     for (int o = 32; o > 0; o >>= 1) {
         mypos += __shfl_down(mypos, o);
@@ -285,15 +278,16 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
         hll_blocks[g * (1 << HLL_REG_BITS) + i] = (uint8_t)h_reg[i];
 }
 
-// coarse counts, bucket-major: cnt[c * ntiles + t] = tile t's records in coarse bucket c
-__global__ void __launch_bounds__(256) k_coarse(const unsigned int *thist, uint64_t ntiles, int cbits,
+// coarse counts, bucket-major: cnt[c * ngroups + g] = group g's records in coarse bucket c
+// (sum of its fine bins; a read group is one downsweep workgroup, which fills its runs in order)
+__global__ void __launch_bounds__(256) k_coarse(const unsigned int *hist, uint64_t ngroups, int cbits,
                                                 unsigned long long *cnt) {
     const uint64_t C = 1ull << cbits;
-    const int per = 1 << (MAX_COARSE_BITS - cbits);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C * ntiles;
+    const int per = 1 << (FINE_BITS - cbits);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C * ngroups;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t c = i / ntiles, t = i % ntiles;
-        const unsigned int *h = thist + t * (1 << MAX_COARSE_BITS) + c * per;
+        const uint64_t c = i / ngroups, g = i % ngroups;
+        const unsigned int *h = hist + g * FINE + c * per;
         unsigned long long sum = 0;
         for (int j = 0; j < per; j++) sum += h[j];
         cnt[i] = sum;
@@ -341,7 +335,7 @@ constexpr int DS_MAX_CBITS = 8;
 
 template <typename RecT, typename Make, typename Store>
 __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
-                                                         int k, uint64_t gsize, uint64_t ntiles, int cbits,
+                                                         int k, uint64_t gsize, uint64_t ngroups, int cbits,
                                                          const unsigned long long *offs, Store recs, Make mk) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_BYTES + 16];
     __shared__ RecT sorted[DS_BATCH];
@@ -362,10 +356,9 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
     };
     for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
         const uint64_t r1 = min(r0 + TILE_READS, g1);
-        const uint64_t tile = r0 / TILE_READS;
         __syncthreads();
         for (int c = tid; c < C; c += TILE_READS) {
-            cur[c] = offs[(uint64_t)c * ntiles + tile];
+            if (r0 == g0) cur[c] = offs[(uint64_t)c * ngroups + g];  // the group's run of coarse bucket c
             bcnt[c] = 0;
         }
         if (tid == 0) s_rounds = 0;
