@@ -97,7 +97,11 @@ typedef struct {
 } ec_stats;
 
 int ec_session_create(ec_session **out, int device);
-/* run on this hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream */
+/* run on this hipStream_t, e.g. torch.cuda.current_stream().cuda_stream (NULL = the null stream,
+ * torch's default); EC_OWN_STREAM = back to a non-blocking stream owned by the session (the
+ * state after ec_session_create).  Inputs produced asynchronously on another stream must be
+ * complete (or that stream must be this one) when an ec_* call starts. */
+#define EC_OWN_STREAM ((void *)-1)
 int ec_session_set_stream(ec_session *s, void *hip_stream);
 int ec_session_destroy(ec_session *s);
 

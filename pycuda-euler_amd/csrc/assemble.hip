@@ -974,13 +974,20 @@ int ec_session_create(ec_session **out, int device) {
 
 int ec_session_set_stream(ec_session *s, void *hip_stream) {
     if (!s) return EC_ERR_ARG;
-    if (s->own_stream && s->stream) hipStreamDestroy(s->stream);
-    s->own_stream = false;
-    s->stream = (hipStream_t)hip_stream;
-    if (!hip_stream) {
-        EC_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-        s->own_stream = true;
+    EC_HIP(hipSetDevice(s->device));
+    if (hip_stream == EC_OWN_STREAM) {
+        if (!s->own_stream) {
+            EC_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+            s->own_stream = true;
+        }
+        return EC_OK;
     }
+    if (s->own_stream && s->stream) {
+        hipStreamSynchronize(s->stream);
+        hipStreamDestroy(s->stream);
+    }
+    s->own_stream = false;
+    s->stream = (hipStream_t)hip_stream;  // NULL: the null stream
     return EC_OK;
 }
 

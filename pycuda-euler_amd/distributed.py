@@ -65,6 +65,10 @@ class HipEngine:
 
         self.torch = torch
         self.device = torch.device("cuda", device)
+        # default: torch's current stream, so the engine's kernels are ordered after the torch
+        # ops that produce its inputs (slices, concatenations, RCCL outputs)
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
         self.sess = eulerhip.Session(device, stream=stream)
         self.L = eulerhip.lib()
 

@@ -230,7 +230,10 @@ class Session:
             pass
 
     def set_stream(self, stream):
-        check(lib().ec_session_set_stream(self._h, ctypes.c_void_p(int(stream) if stream else None)))
+        """stream: a hipStream_t handle (0 = the null stream, torch's default) or None for the
+        session's own non-blocking stream"""
+        h = ctypes.c_void_p(-1 & 0xFFFFFFFFFFFFFFFF) if stream is None else ctypes.c_void_p(int(stream))
+        check(lib().ec_session_set_stream(self._h, h))
 
     # -- run -------------------------------------------------------------------------------
     def run_host(self, buf, offsets, k, limit=1, flags=0):

@@ -40,6 +40,40 @@ def test_local_sharded_equals_oracle(engines, world, seed, g, n, L, err, k):
     assert res.links == oracle.unpack_links(ref)
 
 
+def test_owner_partition_is_disjoint(engines):
+    """Every canonical k-mer is merged by exactly one owner: the owners' solid sets add up to the
+    single-GPU solid set (engines run on torch's stream, ordered after the torch ops that build
+    their inputs -- a session on a private stream raced with them)"""
+    import torch
+
+    import distributed
+
+    buf, off = make_reads(300_000, 400_000, 100, 4545)
+    s = eulerhip.Session(0)
+    s.run_host(buf, off, 31, 1, 0)
+    U = s.stats().n_solid
+    s.close()
+    world = len(engines)
+    sends = []
+    for r, eng in enumerate(engines):
+        lo, hi = distributed.shard_range(len(off) - 1, r, world)
+        d_reads = torch.from_numpy(np.ascontiguousarray(buf[int(off[lo]):int(off[hi])])).cuda()
+        d_off = torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).cuda()
+        eng.count_shard(d_reads, d_off, hi - lo, lo, 31, 0)
+        sends.append(eng.export_by_owner(world))
+    total = 0
+    rb = distributed.rec_bytes(31)
+    for dst, eng in enumerate(engines):
+        parts = []
+        for src in range(world):
+            recs, counts = sends[src]
+            o = sum(counts[:dst]) * rb
+            parts.append(recs[o:o + counts[dst] * rb])
+        solid = eng.merge_owned(torch.cat(parts), 31, 1, 0)
+        total += solid.numel() // rb
+    assert total == U
+
+
 @pytest.mark.parametrize("world", [1, 3])
 def test_local_sharded_general_tables(engines, world):
     """EC_FLAG_GENERAL: HBM-table counting and HBM-table merges instead of the LDS buckets"""

@@ -1,0 +1,78 @@
+"""Estimate per-rank step times of the read-sharded path at N ranks on ONE GPU: runs every
+rank's engine calls back to back (collectives by concatenation) and reports each phase's
+device time for rank 0 (counting its 1/N shard, exporting, merging its owned records,
+loading the gathered solid set + graph phase).  Communication time is not included."""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "pycuda-euler_amd"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+
+    import distributed
+    from synth import make_reads
+
+    buf, off = make_reads(4_600_000, a.reads, 100, 20261019)
+    world = a.ranks
+    engines = [distributed.HipEngine(0) for _ in range(world)]
+    shards = []
+    for r in range(world):
+        lo, hi = distributed.shard_range(a.reads, r, world)
+        shards.append((torch.from_numpy(np.ascontiguousarray(buf[int(off[lo]):int(off[hi])])).cuda(),
+                       torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).cuda(), hi - lo, lo))
+    torch.cuda.synchronize()
+    for rep in range(a.reps):
+        t = {}
+
+        def tick(name, t0):
+            torch.cuda.synchronize()
+            t[name] = t.get(name, []) + [(time.perf_counter() - t0) * 1e3]
+
+        sends = []
+        for eng, (d_reads, d_off, n, lo) in zip(engines, shards):
+            t0 = time.perf_counter()
+            eng.count_shard(d_reads, d_off, n, lo, 31, 0)
+            tick("count", t0)
+            t0 = time.perf_counter()
+            sends.append(eng.export_by_owner(world))
+            tick("export", t0)
+        solids = []
+        rb = distributed.rec_bytes(31)
+        for dst, eng in enumerate(engines):
+            parts = []
+            for src in range(world):
+                recs, counts = sends[src]
+                o = sum(counts[:dst]) * rb
+                parts.append(recs[o:o + counts[dst] * rb])
+            recv = torch.cat(parts)
+            t0 = time.perf_counter()
+            solids.append(eng.merge_owned(recv, 31, 1, 0))
+            tick("merge", t0)
+        mx = max(x.numel() for x in solids)
+        allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device="cuda")
+        for i, x in enumerate(solids):
+            allsolid[i * mx: i * mx + x.numel()] = x
+        t0 = time.perf_counter()
+        res = engines[0].assemble_from_solid(allsolid, 31, 0)
+        tick("graph", t0)
+        print("rep %d  ranks %d  per-rank max ms: %s  exchanged bytes/rank ~%.0f MB, gathered %.0f MB" % (
+            rep, world, {k: round(max(v), 2) for k, v in t.items()},
+            sum(c for c in sends[0][1]) * rb / 1e6, allsolid.numel() / 1e6))
+    print("contigs", len(res.contig_offsets) - 1)
+
+
+if __name__ == "__main__":
+    main()
