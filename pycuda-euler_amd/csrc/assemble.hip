@@ -72,7 +72,7 @@ struct ec_session {
     // scratch
     DevBuf h_reads, h_offsets;  // H2D staging for ec_assemble_host
     DevBuf hll, scal, table, dkey, dcnt, dfc, dft, upal, outdeg, cand, succ, pred, st0, st1;
-    DevBuf rid, roff, rlist, nextR, PK, RK, PL, PM;
+    DevBuf rid, rlist, nextR, PK, RK, PL, PM;
     DevBuf hist, ftot, cnt, offs, bstart, tot, recs, recs2, sub;
     DevBuf startOf, skeys, svals, skeys2, svals2, cidxOf, clen, coff, chars, cfirst, clast, headOf, tailOf;
     DevBuf lk, lcnt, tmp, dchars, dcounts;
@@ -764,8 +764,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
 
     // ---- rank (sparse ruling set + weighted Wyllie on the rulers) -------------------------
     mark(s, 2 * EC_STAGE_RANK);
-    EC_CHECK(s->rid.ensure(Nn * 4));
-    EC_CHECK(s->roff.ensure(Nn * 4));
+    EC_CHECK(s->rid.ensure(Nn * 8));  // (ruler, offset) per node
     EC_CHECK(s->rlist.ensure(Nn * 4));
     EC_CHECK(s->rbc.ensure(((Nn + RULER_CHUNK - 1) / RULER_CHUNK) * 8));
     EC_CHECK(s->nextR.ensure(Nn * 4));
@@ -779,22 +778,22 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
     RJump *fin = s->st0.as<RJump>();
     s->stats.rank_rounds = 0;
     if (U) {
-        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 4, st));
+        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 8, st));
         unsigned int masks[4] = {31u, 7u, 1u, 0u};
         if (const char *e = getenv("EULERHIP_RULER_MASK")) masks[0] = (unsigned int)atoi(e);
         unsigned int r0 = 0;
         for (int it = 0; it < 4; it++) {
             const unsigned int nblk = (unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK);
             k_rulers_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it], it == 0,
-                                               s->rid.as<unsigned int>(), s->rbc.as<unsigned int>());
+                                               s->rid.as<uint2>(), s->rbc.as<unsigned int>());
             EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
             k_rulers<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it], it == 0,
-                                         s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<unsigned int>(),
-                                         s->roff.as<unsigned int>(), s->rlist.as<unsigned int>());
+                                         s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<uint2>(),
+                                         s->rlist.as<unsigned int>());
             k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
             k_walk<<<2048, B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
                                       s->dft.as<unsigned long long>(), s->rlist.as<unsigned int>(), r0, &dsc->nr,
-                                      masks[it], s->rid.as<unsigned int>(), s->roff.as<unsigned int>(),
+                                      masks[it], s->rid.as<uint2>(),
                                       s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
             EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
             EC_HIP(hipStreamSynchronize(st));
@@ -827,7 +826,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
         }
         fin = (hsc.final_sel & 1) ? s->st1.as<RJump>() : s->st0.as<RJump>();
         k_finalize<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(),
-                                                s->rid.as<unsigned int>(), s->roff.as<unsigned int>(),
+                                                s->rid.as<uint2>(),
                                                 s->rlist.as<unsigned int>(), fin, N, s->PK.as<unsigned int>(),
                                                 s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
                                                 s->PM.as<unsigned long long>());
@@ -999,7 +998,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->upal, &s->outdeg, &s->cand, &s->succ, &s->pred, &s->st0, &s->st1, &s->startOf, &s->skeys,
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
-                     &s->rid, &s->roff, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
+                     &s->rid, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
                      &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur};
     for (auto *b : all) b->release();

@@ -155,14 +155,14 @@ __device__ inline bool ruler_hash(unsigned int x, unsigned int smask) {
 // contended counter): RULER_CHUNK nodes per block.
 constexpr unsigned int RULER_CHUNK = 4096;
 
-__device__ inline bool ruler_sel(const uint8_t *upal, const unsigned int *pred, const unsigned int *rid, unsigned int x,
+__device__ inline bool ruler_sel(const uint8_t *upal, const unsigned int *pred, const uint2 *rid, unsigned int x,
                                  unsigned int smask, int first) {
-    if (((x & 1) && upal[x >> 1]) || rid[x] != NONE32) return false;
+    if (((x & 1) && upal[x >> 1]) || rid[x].x != NONE32) return false;
     return (first && pred[x] == NONE32) || ruler_hash(x, smask);
 }
 
 __global__ void __launch_bounds__(256) k_rulers_count(const uint8_t *upal, const unsigned int *pred, unsigned int N,
-                                                      unsigned int smask, int first, const unsigned int *rid,
+                                                      unsigned int smask, int first, const uint2 *rid,
                                                       unsigned int *bc) {
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) k_rulers_count(const uint8_t *upal, const
 // bs = inclusive scan of bc; new rulers get ids nr + bs[b-1] + (rank in chunk)
 __global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsigned int *pred, unsigned int N,
                                                 unsigned int smask, int first, const unsigned int *bs,
-                                                const unsigned int *nr, unsigned int *rid, unsigned int *roff,
+                                                const unsigned int *nr, uint2 *rid,
                                                 unsigned int *rlist) {
     __shared__ unsigned int wsum[4];
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
@@ -197,8 +197,7 @@ __global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsig
         if (sel) {
             const unsigned int i = off + (unsigned int)__popcll(m & ((1ull << lane) - 1));
             rlist[i] = (unsigned int)t;
-            rid[t] = i;
-            roff[t] = 0;
+            rid[t] = make_uint2(i, 0u);
         }
         base += tot;
         __syncthreads();
@@ -222,7 +221,7 @@ static_assert(sizeof(RJump) == 32, "rjump layout");
 __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const unsigned long long *dfc,
                                               const unsigned long long *dft, const unsigned int *rlist,
                                               unsigned int r0, const unsigned int *nr, unsigned int smask,
-                                              unsigned int *rid, unsigned int *roff, unsigned int *nextR, RJump *rs,
+                                              uint2 *rid, unsigned int *nextR, RJump *rs,
                                               unsigned long long *nvisited) {
     const unsigned int r1 = *nr;
     unsigned long long seen = 0;
@@ -234,14 +233,16 @@ __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const un
         for (;;) {
             const unsigned int w = succ[v];
             if (w == NONE32) break;
-            if (ruler_hash(w, smask) && rid[w] != NONE32) {  // the next ruler
-                nx = rid[w];
-                break;
+            if (ruler_hash(w, smask)) {  // maybe the next ruler
+                const unsigned int q = rid[w].x;
+                if (q != NONE32) {
+                    nx = q;
+                    break;
+                }
             }
             v = w;
             j++;
-            rid[v] = i;
-            roff[v] = j;
+            rid[v] = make_uint2(i, j);  // (ruler, offset) in one 8-B store
             const unsigned long long f = first_event(dfc, dft, v);
             fm = f < fm ? f : fm;
         }
@@ -302,14 +303,15 @@ __global__ void __launch_bounds__(256) k_rjump(const RJump *src, RJump *dst, uns
 // at the key node: PL = path / cycle length, PM = min first event over it.
 constexpr unsigned int CYC = 0x80000000u;
 
-__global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const unsigned int *succ, const unsigned int *rid,
-                                                  const unsigned int *roff, const unsigned int *rlist, const RJump *rs,
+__global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const unsigned int *succ, const uint2 *rid,
+                                                  const unsigned int *rlist, const RJump *rs,
                                                   unsigned int N, unsigned int *PK, unsigned int *RK, unsigned int *PL,
                                                   unsigned long long *PM) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         if ((x & 1) && upal[x >> 1]) continue;
-        const unsigned int i = rid[x], j = roff[x];
+        const uint2 ro = rid[x];
+        const unsigned int i = ro.x, j = ro.y;
         const RJump r = rs[i];
         if (r.a == NONE32) {  // path
             const unsigned int pk = rlist[r.h], rk = r.s + j;
