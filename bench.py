@@ -56,14 +56,19 @@ def alg_bytes(P, R, L, U, K=8):
     return R * L + P * (K + 8) + U * (10 * K + 33)
 
 
-def kernel_alg_bytes(name, P, R, L, K=8, rec=16):
-    """Algorithmic bytes per launch of the counting kernels (DESIGN.md "Roofline accounting"),
-    rec = window record bytes (16, or 12 for compact records):
+def kernel_alg_bytes(name, P, R, L, K=8, rec=16, NR=None, nsub=0):
+    """Algorithmic bytes per launch of the counting kernels (DESIGN.md "Roofline accounting").
+    Window records (rec = 16, or 12 for compact records; NR = P records):
     k_upsweep   reads the ASCII reads once                          R*L
     k_downsweep reads them again + writes one record/position       R*L + rec*P
     k_refine    reads every record, writes it as a 16-B record      (rec + 16)*P
     k_bucket    one canonical insert per position      P*(K+8)
-    k_count     general path: read once + one insert/position       R*L + P*(K+8)"""
+    k_count     general path: read once + one insert/position       R*L + P*(K+8)
+    Super-k-mer records (rec = 32, NR records, nsub = bucket sub-table bytes written):
+    k_downsweep R*L + 32*NR;  k_refine 64*NR;  k_bucket 32*NR + nsub"""
+    if rec == 32:
+        return {"k_upsweep": R * L, "k_downsweep": R * L + 32 * NR, "k_bucket": 32 * NR + nsub,
+                "k_count": R * L + P * (K + 8), "k_refine": 64 * NR}[name]
     return {"k_upsweep": R * L, "k_downsweep": R * L + rec * P, "k_bucket": P * (K + 8),
             "k_count": R * L + P * (K + 8), "k_refine": (rec + 16) * P}[name]
 
@@ -113,6 +118,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the multi-GPU path even with one rank")
     ap.add_argument("--wide-records", action="store_true", help="16-B count records only (EC_FLAG_WIDE_RECORDS)")
+    ap.add_argument("--window-records", action="store_true",
+                    help="one record per k-mer window, no super-k-mers (EC_FLAG_WINDOW_RECORDS)")
+    ap.add_argument("--superkmer", action="store_true", help="super-k-mer records (EC_FLAG_SUPERKMER)")
     args = ap.parse_args()
     # stdout carries exactly one JSON line: libraries that print banners (RCCL prints its
     # version block on communicator init) are sent to stderr
@@ -158,7 +166,9 @@ def main():
         def step(timing=False):
             sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), cfg["reads"], k, 1,
                             (eulerhip.EC_FLAG_TIMING if timing else 0)
-                            | (eulerhip.EC_FLAG_WIDE_RECORDS if args.wide_records else 0))
+                            | (eulerhip.EC_FLAG_WIDE_RECORDS if args.wide_records else 0)
+                            | (eulerhip.EC_FLAG_WINDOW_RECORDS if args.window_records else 0)
+                            | (eulerhip.EC_FLAG_SUPERKMER if args.superkmer else 0))
     else:
         import distributed
 
@@ -209,7 +219,8 @@ def main():
     kms = float(kern[kid])
     K = 8 if k <= 32 else 16  # key bytes
     rec = int(st.record_bytes) or 16
-    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L, K, rec)  # this rank's launch
+    nsub = int(st.table_capacity) * 16 if int(st.count_path) == eulerhip.EC_PATH_SUPERKMER else 0
+    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L, K, rec, int(st.n_records), nsub)
     achieved = kb / (kms / 1e3) / 1e9
     tr = load_traffic(cfg["name"], kname)
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -232,8 +243,8 @@ def main():
         "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
                    "positions": P, "solid_kmers": U,
                    "contigs": int(st.n_contigs if not use_dist else runner.engine.stats().n_contigs),
-                   "count_path": ["partitioned", "general"][int(st.count_path)], "buckets": int(st.n_buckets),
-                   "record_bytes": int(st.record_bytes),
+                   "count_path": ["partitioned", "general", "superkmer"][int(st.count_path)],
+                   "buckets": int(st.n_buckets), "record_bytes": int(st.record_bytes), "records": int(st.n_records),
                    "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -49,8 +49,11 @@ typedef struct ec_session ec_session;
 #define EC_FLAG_WANT_DICT 1u /* also keep build()'s ordered dict for ec_copy_dict */
 #define EC_FLAG_TIMING 2u    /* record per-stage HIP-event times (ec_stats.stage_ms) */
 #define EC_FLAG_GENERAL 4u   /* force the general (single HBM hash table) counting path */
-#define EC_FLAG_WIDE_RECORDS 8u /* partitioned path: 16-B records only (default: 12-B records when every
-                                  * read is N-free and of one length) */
+#define EC_FLAG_WIDE_RECORDS 8u /* partitioned path: 16-B window records only (default for k < 21 or
+                                  * reads with N: 12-B records when every read is N-free and of one length) */
+#define EC_FLAG_WINDOW_RECORDS 16u /* partitioned path: one record per k-mer window, never super-k-mers */
+#define EC_FLAG_SUPERKMER 32u /* partitioned path: super-k-mer records (minimizer buckets) where they apply:
+                                * 21 <= k <= 32, N-free reads (else window records) */
 
 #define EC_NSTAGES 8
 /* stage ids for ec_stats.stage_ms / ec_stage_name */
@@ -73,6 +76,7 @@ typedef struct ec_session ec_session;
 
 #define EC_PATH_PARTITIONED 0 /* radix-partitioned LDS counting (count_part.h)               */
 #define EC_PATH_GENERAL 1     /* single HBM hash table (count_global.h)                      */
+#define EC_PATH_SUPERKMER 2   /* minimizer-partitioned super-k-mer records (superkmer.h)       */
 
 typedef struct {
     uint64_t n_reads;
@@ -86,11 +90,12 @@ typedef struct {
     uint64_t n_links;
     uint64_t table_capacity; /* general path: HBM hash slots; partitioned: buckets * LDS slots */
     uint64_t n_rulers;       /* sparse ruling-set size used by the list ranking               */
+    uint64_t n_records;      /* partitioned paths: records moved (P windows, or super-k-mers)  */
     uint32_t table_retries;
     uint32_t rank_rounds;    /* Wyllie rounds on the ruler list                               */
     uint32_t count_path;     /* EC_PATH_*                                                     */
     uint32_t n_buckets;      /* partitioned path: B                                           */
-    uint32_t record_bytes;   /* partitioned path: 12 (compact) or 16 bytes per window record    */
+    uint32_t record_bytes;   /* partitioned paths: 12 / 16 per window record, 32 per super-k-mer */
     uint32_t reserved;
     float stage_ms[EC_NSTAGES];   /* EC_FLAG_TIMING only */
     float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING only */

@@ -19,7 +19,7 @@ KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
 
 def short(name):
     for k in KERNELS:
-        if re.search(r"\b%s\b" % k, name):
+        if re.search(r"\b%s(_sk)?\b" % k, name):
             return k
     return None
 

@@ -144,6 +144,7 @@ struct Scalars {  // device scalars block
     unsigned int maxlocal;
     unsigned int skew;
     unsigned int lens[4];  // k_upsweep: max read length, ~min read length (reads with windows), any slow-path read
+    unsigned long long nrec;  // k_upsweep_sk: super-k-mer records
     unsigned int active[64];
 };
 
@@ -294,12 +295,38 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     EC_CHECK(s->hist.ensure(ngroups * FINE * 4));
     EC_CHECK(s->hll.ensure(ngroups * (1 << HLL_REG_BITS)));
     EC_CHECK(s->ftot.ensure((FINE + (1 << HLL_REG_BITS)) * 8));
+    // super-k-mer counting (superkmer.h) for 21 <= k <= 32 unless window records are asked for;
+    // it needs every read N-free and staged, else the window-record upsweep reruns
+    bool sk = !(flags & (EC_FLAG_GENERAL | EC_FLAG_WIDE_RECORDS | EC_FLAG_WINDOW_RECORDS)) &&
+              ((flags & EC_FLAG_SUPERKMER) || SK_DEFAULT) && k >= SK_MIN_K && k <= 32 && nreads;
+    const MinCfg mc = sk_cfg(k);
     if (nreads) {
         kmark(s, 0, 0);
-        k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
-                                                           s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad,
-                                                           &dsc->maxlocal, &dsc->skew, dsc->lens);
+        if (sk)
+            k_upsweep_sk<<<(unsigned)ngroups, TILE_READS, 0, st>>>(
+                d_reads, d_off, nreads, mc, gsize, s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), &dsc->npos,
+                &dsc->bad, &dsc->maxlocal, &dsc->skew, dsc->lens, &dsc->nrec);
+        else
+            k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
+                                                               s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
+                                                               &dsc->npos, &dsc->bad, &dsc->maxlocal, &dsc->skew,
+                                                               dsc->lens);
         kmark(s, 0, 1);
+        if (sk) {
+            EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+            EC_HIP(hipStreamSynchronize(st));
+            if (hsc.bad == ~0ull && (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT)) {
+                sk = false;
+                EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
+                EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
+                kmark(s, 0, 0);
+                k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
+                                                                   s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
+                                                                   &dsc->npos, &dsc->bad, &dsc->maxlocal,
+                                                                   &dsc->skew, dsc->lens);
+                kmark(s, 0, 1);
+            }
+        }
         EC_HIP(hipMemsetAsync(s->ftot.p, 0, (FINE + (1 << HLL_REG_BITS)) * 8, st));
         k_fine_totals<<<dim3(FINE / 256, TOT_SLICES), 256, 0, st>>>(
             s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), ngroups, s->ftot.as<unsigned long long>(),
@@ -349,17 +376,19 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
         // compact 12-B records: every read staged and N-free, one read length, events fit
         const unsigned int lmax = hsc.lens[0], lmin = ~hsc.lens[1];
-        bool compact = !(flags & EC_FLAG_WIDE_RECORDS) && hsc.lens[2] == 0 && hsc.lens[1] != 0 && lmax == lmin;
+        bool compact = !sk && !(flags & EC_FLAG_WIDE_RECORDS) && hsc.lens[2] == 0 && hsc.lens[1] != 0 && lmax == lmin;
         int ibits = 1;
         if (compact) {
             const uint64_t m = (uint64_t)lmax - (uint64_t)k + 1;
             while ((1ull << ibits) < m) ibits++;
             compact = ibits <= 15 && nreads + read_base <= (1ull << (31 - ibits));
         }
-        const size_t rsz = compact ? sizeof(Rec12) : sizeof(Rec);
+        const uint64_t NR = sk ? hsc.nrec : P;  // records
+        const size_t rsz = sk ? sizeof(SkRec) : compact ? sizeof(Rec12) : sizeof(Rec);
         s->stats.record_bytes = (uint32_t)rsz;
-        EC_CHECK(s->recs.ensure(P * rsz));
-        if (bbits > cbits) EC_CHECK(s->recs2.ensure(P * sizeof(Rec)));  // refine writes 16-B records
+        s->stats.n_records = NR;
+        EC_CHECK(s->recs.ensure(NR * rsz));
+        if (bbits > cbits) EC_CHECK(s->recs2.ensure(NR * (sk ? sizeof(SkRec) : sizeof(Rec))));  // refine output
         k_coarse<<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
                                                                s->cnt.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ngroups));
@@ -369,7 +398,11 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         // compact records: keys [0, 8P) and meta [8P, 12P) of the first record buffer
         const Store12 c1{s->recs.as<unsigned long long>(), reinterpret_cast<unsigned int *>(s->recs.as<uint8_t>() + P * 8)};
         kmark(s, 1, 0);
-        if (compact)
+        if (sk)
+            k_downsweep_sk<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, mc, gsize, ngroups, cbits,
+                                                                    s->offs.as<unsigned long long>(),
+                                                                    s->recs.as<SkRec>(), read_base);
+        else if (compact)
             k_downsweep<Rec12, MakeRec12, Store12><<<(unsigned)ngroups, TILE_READS, 0, st>>>(
                 d_reads, d_off, nreads, k, gsize, ngroups, cbits, s->offs.as<unsigned long long>(), c1,
                 MakeRec12{read_base, ibits});
@@ -385,7 +418,11 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             EC_CHECK(s->gcur.ensure(Bk * 8));
             EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
             kmark(s, 4, 0);
-            if (compact)  // 12-B in, 16-B out: k_bucket reads 16-B records
+            if (sk)
+                k_refine<SkRec, StoreSk, StoreSk><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                    StoreSk{s->recs.as<SkRec>()}, StoreSk{s->recs2.as<SkRec>()}, s->bstart.as<unsigned long long>(),
+                    s->gcur.as<unsigned long long>(), cbits, bbits);
+            else if (compact)  // 12-B in, 16-B out: k_bucket reads 16-B records
                 k_refine<Rec12, Store12, Store12to16><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
                     c1, Store12to16{s->recs2.as<Rec>(), ibits, k, (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1)},
                     s->bstart.as<unsigned long long>(), s->gcur.as<unsigned long long>(), cbits, bbits);
@@ -405,7 +442,19 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->dft.ensure(umax * 8));
         EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
         kmark(s, 2, 0);
-        if (compact && !second) {
+        if (sk) {
+            const SkRec *sr = second ? s->recs2.as<SkRec>() : s->recs.as<SkRec>();
+            if (slots == 2048)
+                k_bucket_sk<2048><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
+                    sr, s->bstart.as<unsigned long long>(), k, (long long)limit, s->dkey.as<unsigned long long>(),
+                    s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                    s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+            else
+                k_bucket_sk<4096><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
+                    sr, s->bstart.as<unsigned long long>(), k, (long long)limit, s->dkey.as<unsigned long long>(),
+                    s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                    s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+        } else if (compact && !second) {
             EC_CHECK(launch_bucket(s, Rec12Source{c1.key, c1.meta, ibits, k, (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1)},
                                    (unsigned)Bk, slots, (long long)limit));
         } else {
@@ -426,7 +475,9 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             sidx.sub = s->sub.as<SubSlot>();
             sidx.bbits = bbits;
             sidx.slots = slots;
-            s->stats.count_path = EC_PATH_PARTITIONED;
+            sidx.sk = sk ? 1 : 0;
+            sidx.mc = mc;
+            s->stats.count_path = sk ? EC_PATH_SUPERKMER : EC_PATH_PARTITIONED;
             s->stats.n_buckets = (uint32_t)Bk;
             s->stats.table_capacity = umax;
         }

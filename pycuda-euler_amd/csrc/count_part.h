@@ -52,6 +52,11 @@ static_assert(sizeof(Rec12) == 12, "compact record layout");
 
 __device__ inline unsigned long long rkey(const Rec &r) { return r.key; }
 __device__ inline unsigned long long rkey(const Rec12 &r) { return ((unsigned long long)r.khi << 32) | r.klo; }
+// final bucket of a window record: top bbits of mix64(key) (bbits >= 1)
+__device__ inline unsigned int rec_bucket(const Rec &r, int bbits) { return (unsigned int)(mix64(r.key) >> (64 - bbits)); }
+__device__ inline unsigned int rec_bucket(const Rec12 &r, int bbits) {
+    return (unsigned int)(mix64(rkey(r)) >> (64 - bbits));
+}
 
 // record construction in the downsweep: window (fwd, rc) of read r with local events lf / lr
 struct MakeRec {
@@ -473,20 +478,21 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
 template <typename RecT, typename StoreIn, typename StoreOut>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut out, const unsigned long long *bstart,
                                                           unsigned long long *gcur, int cbits, int bbits) {
-    __shared__ RecT tile[REFINE_TILE];
+    constexpr int TILE = sizeof(RecT) > 16 ? REFINE_TILE / 2 : REFINE_TILE;  // <= 64 KiB of LDS
+    __shared__ RecT tile[TILE];
     __shared__ unsigned long long base[REFINE_FANOUT];
     __shared__ unsigned int tcnt[REFINE_FANOUT], tbeg[REFINE_FANOUT], wsum[REFINE_FANOUT / 64];
     const int F = 1 << (bbits - cbits);
     const uint64_t c = blockIdx.x;
     const uint64_t r0 = bstart[c * F], r1 = bstart[(c + 1) * F];
-    const uint64_t nt = (r1 - r0 + REFINE_TILE - 1) / REFINE_TILE;
+    const uint64_t nt = (r1 - r0 + TILE - 1) / TILE;
     const uint64_t tb = nt * blockIdx.y / gridDim.y, te = nt * (blockIdx.y + 1) / gridDim.y;
-    constexpr int PER = REFINE_TILE / BUCKET_THREADS;
-    const uint64_t tend = min(r1, r0 + te * REFINE_TILE);
+    constexpr int PER = TILE / BUCKET_THREADS;
+    const uint64_t tend = min(r1, r0 + te * TILE);
     // software pipeline: tile t+1 is loaded into registers while tile t's runs are stored
     RecT nx[PER];
     auto load_tile = [&](uint64_t t0) {
-        const unsigned int n = (unsigned int)min((uint64_t)REFINE_TILE, r1 - t0);
+        const unsigned int n = (unsigned int)min((uint64_t)TILE, r1 - t0);
 #pragma unroll
         for (int q = 0; q < PER; q++) {
             const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
@@ -495,11 +501,11 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
     };
     // (measured: pipelining pays for 12-B input, 4.86 -> 4.35 ms; 16-B input runs slower with it)
     constexpr bool PIPE = sizeof(RecT) < 16;
-    uint64_t t0 = r0 + tb * REFINE_TILE;
+    uint64_t t0 = r0 + tb * TILE;
     if (t0 < tend) load_tile(t0);
-    for (; t0 < tend; t0 += REFINE_TILE) {
-        if (!PIPE && t0 != r0 + tb * REFINE_TILE) load_tile(t0);
-        const unsigned int n = (unsigned int)min((uint64_t)REFINE_TILE, r1 - t0);
+    for (; t0 < tend; t0 += TILE) {
+        if (!PIPE && t0 != r0 + tb * TILE) load_tile(t0);
+        const unsigned int n = (unsigned int)min((uint64_t)TILE, r1 - t0);
         if (threadIdx.x < REFINE_FANOUT) tcnt[threadIdx.x] = 0;
         __syncthreads();
         RecT rr[PER];
@@ -509,7 +515,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
             const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
             rr[q] = nx[q];
             if (i < n) {
-                jj[q] = (unsigned int)(mix64(rkey(rr[q])) >> (64 - bbits)) & (F - 1);
+                jj[q] = rec_bucket(rr[q], bbits) & (F - 1);
                 rk[q] = atomicAdd(&tcnt[jj[q]], 1u);
             }
         }
@@ -538,10 +544,10 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
             if (i < n) tile[tbeg[jj[q]] + rk[q]] = rr[q];
         }
         __syncthreads();
-        if (PIPE && t0 + REFINE_TILE < tend) load_tile(t0 + REFINE_TILE);
+        if (PIPE && t0 + TILE < tend) load_tile(t0 + TILE);
         for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
             const RecT rec = tile[i];
-            const unsigned int j = (unsigned int)(mix64(rkey(rec)) >> (64 - bbits)) & (F - 1);
+            const unsigned int j = rec_bucket(rec, bbits) & (F - 1);
             out.store(base[j] + (i - tbeg[j]), rec);
         }
         __syncthreads();
@@ -595,71 +601,59 @@ struct Rec12Source {
     }
 };
 
-template <typename Src, int SLOTS>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsigned long long *bstart,
-                                                          long long limit,
-                                                          unsigned long long *dkey, unsigned int *dcnt,
-                                                          unsigned long long *dfc, unsigned long long *dft,
-                                                          SubSlot *sub, unsigned int *nsolid,
-                                                          unsigned long long *ndistinct, unsigned int *overflow) {
-    __shared__ LSlot tab[SLOTS];
-    __shared__ unsigned int s_over;
-    __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
-    __shared__ unsigned int s_base;
-    const unsigned int b = blockIdx.x;
+// ---- LDS bucket table, shared by every bucket pass (window records, exchange records,
+// super-k-mers): SLOTS open-addressing slots, CAS claim, count += add, atomicMin of events
+template <int SLOTS>
+__device__ inline void lds_table_init(LSlot *tab, unsigned int *s_over) {
     for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
         tab[i].key = EMPTY_KEY;
         tab[i].fC = NONE64;
         tab[i].fT = NONE64;
         tab[i].count = 0;
     }
-    if (threadIdx.x == 0) s_over = 0;
+    if (threadIdx.x == 0) *s_over = 0;
     __syncthreads();
-    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
-    auto insert = [&](unsigned long long c, unsigned int add, unsigned long long eC, unsigned long long eT) {
-        unsigned int slot = (unsigned int)mix64(c) & (SLOTS - 1);
-        int probe = 0;
-        for (; probe < SLOTS; probe++) {
-            unsigned long long cur = tab[slot].key;
-            if (cur == EMPTY_KEY) {
-                cur = atomicCAS(&tab[slot].key, EMPTY_KEY, (unsigned long long)c);
-                if (cur == EMPTY_KEY) cur = c;
-            }
-            if (cur == c) break;
-            slot = (slot + 1) & (SLOTS - 1);
+}
+
+// slot0 = first probe slot (the bucket sub-table's lookups start at the same slot)
+template <int SLOTS>
+__device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
+                                  unsigned int add, unsigned long long eC, unsigned long long eT) {
+    if (*s_over) return;  // the bucket is redone on the general path anyway
+    unsigned int slot = slot0 & (SLOTS - 1);
+    int probe = 0;
+    for (; probe < SLOTS; probe++) {
+        unsigned long long cur = tab[slot].key;
+        if (cur == EMPTY_KEY) {
+            cur = atomicCAS(&tab[slot].key, EMPTY_KEY, (unsigned long long)c);
+            if (cur == EMPTY_KEY) cur = c;
         }
-        if (probe == SLOTS) {
-            s_over = 1;
-            return;
-        }
-        if (add) atomicAdd(&tab[slot].count, add);
-        if (eC < tab[slot].fC) atomicMin(&tab[slot].fC, eC);
-        if (eT < tab[slot].fT) atomicMin(&tab[slot].fT, eT);
-    };
-    // BK_UNROLL records per thread per step, all loads issued before the inserts: the loop
-    // is bound by HBM latency, not bandwidth, without this memory-level parallelism
-    constexpr int BK_UNROLL = 4;
-    uint64_t i = r0 + threadIdx.x;
-    for (; i + (BK_UNROLL - 1) * (uint64_t)blockDim.x < r1; i += BK_UNROLL * (uint64_t)blockDim.x) {
-        unsigned long long c[BK_UNROLL], eC[BK_UNROLL], eT[BK_UNROLL];
-        unsigned int add[BK_UNROLL];
-#pragma unroll
-        for (int u = 0; u < BK_UNROLL; u++) src.get(i + u * (uint64_t)blockDim.x, c[u], add[u], eC[u], eT[u]);
-#pragma unroll
-        for (int u = 0; u < BK_UNROLL; u++) insert(c[u], add[u], eC[u], eT[u]);
+        if (cur == c) break;
+        slot = (slot + 1) & (SLOTS - 1);
     }
-    for (; i < r1; i += blockDim.x) {
-        unsigned long long c, eC, eT;
-        unsigned int add;
-        src.get(i, c, add, eC, eT);
-        insert(c, add, eC, eT);
+    if (probe == SLOTS) {
+        *s_over = 1;
+        return;
     }
+    if (add) atomicAdd(&tab[slot].count, add);
+    if (eC < tab[slot].fC) atomicMin(&tab[slot].fC, eC);
+    if (eT < tab[slot].fT) atomicMin(&tab[slot].fT, eT);
+}
+
+// solid filter (count > limit, build:37-39) + compaction of bucket b's table into the dense
+// arrays (wave ballot, one global atomic per block) + the bucket's lookup sub-table
+template <int SLOTS>
+__device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_over, unsigned int b, long long limit,
+                                        unsigned long long *dkey, unsigned int *dcnt, unsigned long long *dfc,
+                                        unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
+                                        unsigned long long *ndistinct, unsigned int *overflow) {
+    __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
+    __shared__ unsigned int s_base;
     __syncthreads();
-    if (s_over) {
+    if (*s_over) {
         if (threadIdx.x == 0) atomicAdd(overflow, 1u);
         return;
     }
-    // solid filter + compaction (wave ballot, one global atomic per block)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int PER = SLOTS / BUCKET_THREADS;
     bool solid[PER];
@@ -712,6 +706,40 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
         }
         region[i] = o;
     }
+}
+
+template <typename Src, int SLOTS>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsigned long long *bstart,
+                                                          long long limit,
+                                                          unsigned long long *dkey, unsigned int *dcnt,
+                                                          unsigned long long *dfc, unsigned long long *dft,
+                                                          SubSlot *sub, unsigned int *nsolid,
+                                                          unsigned long long *ndistinct, unsigned int *overflow) {
+    __shared__ LSlot tab[SLOTS];
+    __shared__ unsigned int s_over;
+    const unsigned int b = blockIdx.x;
+    lds_table_init<SLOTS>(tab, &s_over);
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    // BK_UNROLL records per thread per step, all loads issued before the inserts: the loop
+    // is bound by HBM latency, not bandwidth, without this memory-level parallelism
+    constexpr int BK_UNROLL = 4;
+    uint64_t i = r0 + threadIdx.x;
+    for (; i + (BK_UNROLL - 1) * (uint64_t)blockDim.x < r1; i += BK_UNROLL * (uint64_t)blockDim.x) {
+        unsigned long long c[BK_UNROLL], eC[BK_UNROLL], eT[BK_UNROLL];
+        unsigned int add[BK_UNROLL];
+#pragma unroll
+        for (int u = 0; u < BK_UNROLL; u++) src.get(i + u * (uint64_t)blockDim.x, c[u], add[u], eC[u], eT[u]);
+#pragma unroll
+        for (int u = 0; u < BK_UNROLL; u++)
+            lds_insert<SLOTS>(tab, &s_over, c[u], (unsigned int)mix64(c[u]), add[u], eC[u], eT[u]);
+    }
+    for (; i < r1; i += blockDim.x) {
+        unsigned long long c, eC, eT;
+        unsigned int add;
+        src.get(i, c, add, eC, eT);
+        lds_insert<SLOTS>(tab, &s_over, c, (unsigned int)mix64(c), add, eC, eT);
+    }
+    lds_table_finish<SLOTS>(tab, &s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
 }
 
 }  // namespace ec

@@ -2,33 +2,66 @@
 #pragma once
 #include "count_global.h"
 #include "count_part.h"
+#include "superkmer.h"
 #include "wide.h"
 
 namespace ec {
 
 // canonical key -> dense solid id (NONE if absent or not solid).  Two layouts: the bucketed
-// sub-tables written by k_bucket (partitioned path) or the single HBM table (general path).
+// sub-tables written by k_bucket / k_bucket_sk (partitioned paths; the bucket of a key is the
+// top bits of mix64(key), or of its minimizer on the super-k-mer path) or the single HBM table
+// (general path).  Within a bucket the first probe slot is slot0(key), as in lds_insert.
 struct SolidIndex {
     const Slot *table;
     uint64_t capmask;
     const SubSlot *sub;
     int bbits;
     unsigned int slots;  // sub-table slots per bucket (power of 2)
+    int sk;              // buckets by minimizer (superkmer.h)
+    MinCfg mc;
+    __device__ inline unsigned int find_in(uint64_t c, unsigned int h, uint64_t b) const {
+        const SubSlot *r = sub + b * slots;
+        unsigned int slot = h & (slots - 1);
+        for (unsigned int probe = 0; probe < slots; probe++) {
+            const unsigned long long kk = r[slot].key;
+            if (kk == c) return r[slot].id;
+            if (kk == EMPTY_KEY) return NONE32;
+            slot = (slot + 1) & (slots - 1);
+        }
+        return NONE32;
+    }
+    // first probe slot in a bucket sub-table (k_bucket: mix64, k_bucket_sk: sk_slot top bits)
+    __device__ inline unsigned int slot0(uint64_t c) const {
+        return sk ? sk_slot(c) >> (32 - __builtin_ctz(slots)) : (unsigned int)mix64(c);
+    }
     __device__ inline unsigned int find(uint64_t c) const {
-        const uint64_t h = mix64(c);
         if (sub) {
-            const uint64_t b = bbits ? (h >> (64 - bbits)) : 0;
-            const SubSlot *r = sub + b * slots;
-            unsigned int slot = (unsigned int)h & (slots - 1);
-            for (unsigned int probe = 0; probe < slots; probe++) {
-                const unsigned long long kk = r[slot].key;
-                if (kk == c) return r[slot].id;
-                if (kk == EMPTY_KEY) return NONE32;
-                slot = (slot + 1) & (slots - 1);
-            }
-            return NONE32;
+            const uint64_t h = mix64(c);
+            const uint64_t b = sk ? sk_bucket_of(minimizer_of(c, mc), bbits) : (bbits ? (h >> (64 - bbits)) : 0);
+            return find_in(c, slot0(c), b);
         }
         return lookup(table, capmask, c);
+    }
+    // successors of oriented k-mer xs (k-mers xs << 2 | b): on the super-k-mer path their
+    // minimizers share the w - 1 m-mers of xs's last k - 1 bases
+    struct Nb {
+        uint32_t part;
+    };
+    __device__ inline Nb nb_begin(uint64_t xs) const {
+        Nb nb{0xFFFFFFFFu};
+        if (sub && sk)
+            for (int p = 1; p < mc.w; p++) {
+                const uint32_t h = mmer_canon_hash((uint32_t)(xs >> (2 * (mc.k - mc.m - p))) & mc.mmask, mc);
+                nb.part = h < nb.part ? h : nb.part;
+            }
+        return nb;
+    }
+    __device__ inline unsigned int find_nb(const Nb &nb, uint64_t y, uint64_t cy) const {
+        if (sub && sk) {
+            const uint32_t h = mmer_canon_hash((uint32_t)y & mc.mmask, mc);
+            return find_in(cy, slot0(cy), sk_bucket_of(min_remix(h < nb.part ? h : nb.part), bbits));
+        }
+        return find(cy);
     }
 };
 // key algebra of the graph phase: 64-bit codes (k <= 32) or K128 (32 < k <= 63)
@@ -54,6 +87,9 @@ struct SolidIndexW {
     const SlotW *table;
     uint64_t capmask;
     __device__ inline unsigned int find(const K128 &c) const { return lookup_w(table, capmask, c); }
+    struct Nb {};
+    __device__ inline Nb nb_begin(const K128 &) const { return Nb{}; }
+    __device__ inline unsigned int find_nb(const Nb &, const K128 &, const K128 &cy) const { return find(cy); }
 };
 
 // oriented node id: 2u + o (o = 1: twin of the canonical string); palindromes use o = 0 only
@@ -90,11 +126,12 @@ __global__ void __launch_bounds__(256) k_neighbors(Index idx, const typename Ops
         }
         const K xs = (x & 1) ? tc : c;
         unsigned int n = 0, cd = NONE32;
+        const typename Index::Nb nb = idx.nb_begin(xs);
         for (uint32_t b = 0; b < 4; b++) {
             const K y = Ops::push(xs, b, mask);
             const K ty = Ops::twin(y, k);
             const K cy = y < ty ? y : ty;
-            const unsigned int u = idx.find(cy);
+            const unsigned int u = idx.find_nb(nb, y, cy);
             if (u != NONE32) {
                 if (n == 0) cd = 2 * u + (y != cy ? 1u : 0u);
                 n++;

@@ -32,11 +32,14 @@ EC_FLAG_WANT_DICT = 1
 EC_FLAG_TIMING = 2
 EC_FLAG_GENERAL = 4
 EC_FLAG_WIDE_RECORDS = 8
+EC_FLAG_WINDOW_RECORDS = 16
+EC_FLAG_SUPERKMER = 32
 EC_NSTAGES = 8
 EC_NKERNELS = 5
 KERNEL_NAMES = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
 EC_PATH_PARTITIONED = 0
 EC_PATH_GENERAL = 1
+EC_PATH_SUPERKMER = 2
 EC_MAX_K = 63
 
 
@@ -63,6 +66,7 @@ class Stats(ctypes.Structure):
         ("n_links", ctypes.c_uint64),
         ("table_capacity", ctypes.c_uint64),
         ("n_rulers", ctypes.c_uint64),
+        ("n_records", ctypes.c_uint64),
         ("table_retries", ctypes.c_uint32),
         ("rank_rounds", ctypes.c_uint32),
         ("count_path", ctypes.c_uint32),
@@ -273,10 +277,12 @@ class Session:
             items = [(s[i * k:(i + 1) * k], int(cnt[i])) for i in range(nd)]
         return Result(k, st, chars.raw[:nch], coff, loff, links[:nl], items)
 
-    def assemble(self, reads, k, limit=1, want_dict=False, timing=False, general=False, wide_records=False):
+    def assemble(self, reads, k, limit=1, want_dict=False, timing=False, general=False, wide_records=False,
+                 window_records=False, superkmer=False):
         buf, off = pack_reads(reads)
         flags = (EC_FLAG_WANT_DICT if want_dict else 0) | (EC_FLAG_TIMING if timing else 0)
         flags |= (EC_FLAG_GENERAL if general else 0) | (EC_FLAG_WIDE_RECORDS if wide_records else 0)
+        flags |= (EC_FLAG_WINDOW_RECORDS if window_records else 0) | (EC_FLAG_SUPERKMER if superkmer else 0)
         self.run_host(buf, off, k, limit, flags)
         return self.fetch(k, want_dict)
 

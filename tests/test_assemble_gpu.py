@@ -27,8 +27,45 @@ def test_golden(gpu_session, case):
     assert res.contigs == case["contigs"]
     assert res.links == case["links"]
     if res.stats.n_positions > 0:  # 128-bit keys (k > 32) count in the general table
-        want = eulerhip.EC_PATH_PARTITIONED if case["k"] <= 32 else eulerhip.EC_PATH_GENERAL
-        assert res.stats.count_path == want
+        assert res.stats.count_path in _want_paths(case["reads"], case["k"], False)
+
+
+def _sk_applies(reads, k):
+    return 21 <= k <= 32 and not any("N" in r for r in reads)
+
+
+def _want_paths(reads, k, superkmer):
+    """super-k-mer records (default or EC_FLAG_SUPERKMER) for 21 <= k <= 32 and N-free reads,
+    else window records (k <= 32); k > 32 counts in the general table"""
+    if k > 32:
+        return (eulerhip.EC_PATH_GENERAL,)
+    if not _sk_applies(reads, k):
+        return (eulerhip.EC_PATH_PARTITIONED,)
+    if superkmer:
+        return (eulerhip.EC_PATH_SUPERKMER,)
+    return (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_SUPERKMER)
+
+
+@pytest.mark.parametrize("case", CASES32[1::3], ids=[c["name"] for c in CASES32[1::3]])
+def test_golden_superkmer(gpu_session, case):
+    """super-k-mer records asked for (EC_FLAG_SUPERKMER)"""
+    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, superkmer=True)
+    assert [[x, c] for x, c in res.dict_items] == case["d"]
+    assert res.contigs == case["contigs"]
+    assert res.links == case["links"]
+    if res.stats.n_positions > 0:
+        assert res.stats.count_path in _want_paths(case["reads"], case["k"], True)
+
+
+@pytest.mark.parametrize("case", CASES32[::3], ids=[c["name"] for c in CASES32[::3]])
+def test_golden_window_records(gpu_session, case):
+    """one record per window forced (EC_FLAG_WINDOW_RECORDS) where super-k-mers would apply"""
+    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, window_records=True)
+    assert [[x, c] for x, c in res.dict_items] == case["d"]
+    assert res.contigs == case["contigs"]
+    assert res.links == case["links"]
+    if res.stats.n_positions > 0 and case["k"] <= 32:
+        assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
 
 
 @pytest.mark.parametrize("case", CASES32[1::2], ids=[c["name"] for c in CASES32[1::2]])
@@ -85,14 +122,15 @@ SYN = [
 ]
 
 
-@pytest.mark.parametrize("mode", ["partitioned", "wide_records", "general"])
+@pytest.mark.parametrize("mode", ["partitioned", "superkmer", "window_records", "wide_records", "general"])
 @pytest.mark.parametrize("g,n,L,seed,err,nr,circ,k", SYN)
 def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode):
     buf, off = make_reads(g, n, L, 1000 + seed, err=err, n_rate=nr, circular=circ)
     want_dict = g <= 50_000
     ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
-    flags = (eulerhip.EC_FLAG_WANT_DICT if want_dict else 0) | {"partitioned": 0, "general": eulerhip.EC_FLAG_GENERAL,
-                                                                "wide_records": eulerhip.EC_FLAG_WIDE_RECORDS}[mode]
+    flags = (eulerhip.EC_FLAG_WANT_DICT if want_dict else 0) | {
+        "partitioned": 0, "general": eulerhip.EC_FLAG_GENERAL, "wide_records": eulerhip.EC_FLAG_WIDE_RECORDS,
+        "window_records": eulerhip.EC_FLAG_WINDOW_RECORDS, "superkmer": eulerhip.EC_FLAG_SUPERKMER}[mode]
     gpu_session.run_host(buf, off, k, 1, flags)
     res = gpu_session.fetch(k, want_dict)
     assert res.stats.n_positions == ref["n_positions"]
@@ -102,8 +140,15 @@ def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode)
     assert res.links == rl
     if want_dict:
         assert [[x, c] for x, c in res.dict_items] == ref["d"]
-    if mode == "partitioned" and k <= 32 and nr == 0:  # one read length, no N: 12-B records
-        assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.record_bytes == 12
+    if res.stats.count_path == eulerhip.EC_PATH_SUPERKMER:  # 32-B super-k-mer records
+        assert res.stats.record_bytes == 32 and 0 < res.stats.n_records < res.stats.n_positions
+    if mode == "superkmer" and 21 <= k <= 32 and nr == 0:
+        assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
+    if mode in ("partitioned", "window_records") and k <= 32 and nr == 0 \
+            and res.stats.count_path == eulerhip.EC_PATH_PARTITIONED:  # one read length, no N: 12-B records
+        assert res.stats.record_bytes == 12
+    if mode == "window_records" and k <= 32:
+        assert res.stats.count_path in (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_GENERAL)
     if mode == "wide_records" and k <= 32:
         assert res.stats.record_bytes == 16
 
@@ -164,5 +209,65 @@ def test_many_buckets_vs_oracle(gpu_session):
     ref, rc, rl = _oracle_packed(buf, off, 31)
     gpu_session.run_host(buf, off, 31, 1)
     res = gpu_session.fetch(31)
+    assert res.stats.count_path in (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_SUPERKMER)
+    assert res.stats.n_buckets > 64
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_SUPERKMER)
+    res = gpu_session.fetch(31)
+    assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER and res.stats.n_buckets > 64
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_WINDOW_RECORDS)
+    res = gpu_session.fetch(31)
     assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.n_buckets > 64
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+def _low_complexity_reads(n, L, seed):
+    """reads over short tandem repeats and homopolymers: minimizer runs reach the record cap,
+    heavy minimizers, palindromic k-mers for even k"""
+    rng = np.random.default_rng(seed)
+    units = ["A", "AC", "ACGT", "AT", "CG", "AAC", "GATC", "ACGTTGCA", "TTAGGG"]
+    out = []
+    for i in range(n):
+        u = units[rng.integers(len(units))]
+        body = (u * (L // len(u) + 2))[: L]
+        b = list(body)
+        for _ in range(rng.integers(0, 3)):  # a few substitutions
+            b[rng.integers(L)] = "ACGT"[rng.integers(4)]
+        out.append("".join(b))
+    rnd = "".join("ACGT"[x] for x in rng.integers(0, 4, 5000))
+    for i in range(n):
+        p = int(rng.integers(0, len(rnd) - L))
+        out.append(rnd[p:p + L])
+    return out
+
+
+@pytest.mark.parametrize("k", [21, 22, 27, 31, 32])
+def test_superkmer_low_complexity_vs_oracle(gpu_session, k):
+    reads = _low_complexity_reads(400, 120, 40 + k)
+    d, r, g = oracle.assemble(reads, k, 1)
+    res = gpu_session.assemble(reads, k, 1, want_dict=True, superkmer=True)
+    assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
+    assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g
+
+
+@pytest.mark.parametrize("k", [21, 26, 31])
+def test_superkmer_ragged_lengths_vs_oracle(gpu_session, k):
+    # mixed read lengths (some shorter than k, some long): per-read window counts in the records
+    rng = np.random.default_rng(k)
+    g = "".join("ACGT"[x] for x in rng.integers(0, 4, 30_000))
+    reads = []
+    for i in range(6000):
+        L = int(rng.choice([5, k - 1, k, k + 1, 60, 151, 300, 1000]))
+        p = int(rng.integers(0, len(g) - L))
+        x = g[p:p + L]
+        reads.append(x if rng.random() < 0.5 else x[::-1].translate(str.maketrans("ACGT", "TGCA")))
+    buf = np.frombuffer("".join(reads).encode(), np.uint8).copy()
+    off = np.zeros(len(reads) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in reads])
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT | eulerhip.EC_FLAG_SUPERKMER)
+    res = gpu_session.fetch(k, True)
+    assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
     assert res.contig_bytes == ref["contig_chars"] and res.links == rl
