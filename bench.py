@@ -179,6 +179,8 @@ def main():
 
     for _ in range(args.warmup):
         step(True)
+    if use_dist:
+        runner.phase_ms = {}  # per-phase times of the timed steps only
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -213,7 +215,7 @@ def main():
     kern /= args.steps
     sharded_ms = None
     if use_dist:
-        sharded_ms = {kk: round(v / (args.steps + args.warmup), 3) for kk, v in runner.phase_ms.items()}
+        sharded_ms = {kk: round(v / args.steps, 3) for kk, v in runner.phase_ms.items()}
     kid = int(np.argmax(kern))
     kname = eulerhip.KERNEL_NAMES[kid]
     kms = float(kern[kid])

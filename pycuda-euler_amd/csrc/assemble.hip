@@ -61,6 +61,35 @@ struct DevBuf {
     }
 };
 
+// pinned host buffer (page-locked: D2H copies of the results run at full PCIe rate)
+struct HostBuf {
+    char *p = nullptr;
+    size_t cap = 0, size = 0;
+    int resize(size_t bytes) {
+        size = bytes;
+        if (bytes <= cap) return EC_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        if (hipHostMalloc(reinterpret_cast<void **>(&p), want, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            size = 0;
+            set_error("hipHostMalloc(%zu) failed", want);
+            return EC_ERR_NOMEM;
+        }
+        cap = want;
+        return EC_OK;
+    }
+    char *data() const { return p; }
+    bool empty() const { return size == 0; }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = size = 0;
+    }
+};
+
 }  // namespace ec
 
 using namespace ec;
@@ -80,7 +109,7 @@ struct ec_session {
     bool have = false;
     int k = 0;
     ec_stats stats{};
-    std::vector<char> h_chars;
+    HostBuf h_chars;
     std::vector<uint64_t> h_coff;
     std::vector<uint64_t> h_loff;
     std::vector<int64_t> h_links;
@@ -666,6 +695,68 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
 }
 
 
+// The all-gathered solid set of the sharded path (distinct keys, filler records) straight into
+// the dense arrays and a bucketed SolidIndex: one compaction + CAS-insert pass instead of the
+// sort + LDS-table merge of phase_merge.  ok = false (nothing committed) when the set is too
+// large for the bucket layout or a bucket region overflowed: the caller merges instead.
+int phase_load_solid(ec_session *s, const Agg *d_agg, uint64_t n, unsigned int &U, SolidIndex &sidx, bool &ok) {
+    hipStream_t st = s->stream;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    ok = false;
+    int bbits = 0;
+    while (bbits < FINE_BITS && (double)n / (double)(1ull << bbits) > 1100.0) bbits++;
+    if ((double)n / (double)(1ull << bbits) > 2200.0) return EC_OK;
+    const unsigned int nb = 1u << bbits;
+    const unsigned int slots = (double)n / (double)nb > 1100.0 ? 4096u : 2048u;
+    const uint64_t umax = (uint64_t)nb * slots;
+    const unsigned int nblk = (unsigned int)std::max<uint64_t>((n + LOAD_CHUNK - 1) / LOAD_CHUNK, 1);
+    mark(s, 2 * EC_STAGE_COMPACT);
+    EC_CHECK(s->rbc.ensure((size_t)nblk * 8));
+    EC_CHECK(s->dkey.ensure(std::max<uint64_t>(n, 1) * 8));
+    EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(n, 1) * 4));
+    EC_CHECK(s->dfc.ensure(std::max<uint64_t>(n, 1) * 8));
+    EC_CHECK(s->dft.ensure(std::max<uint64_t>(n, 1) * 8));
+    EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
+    EC_HIP(hipMemsetAsync(s->sub.p, 0xFF, umax * sizeof(SubSlot), st));
+    EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
+    unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk;
+    if (n) {
+        k_load_count<<<nblk, 256, 0, st>>>(d_agg, n, bc);
+        EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
+        k_load_write<<<nblk, 256, 0, st>>>(d_agg, n, bs, bbits, slots, s->dkey.as<unsigned long long>(),
+                                           s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                           s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->overflow);
+        k_compact_total<<<1, 1, 0, st>>>(bs, nblk, &dsc->nsolid);
+    }
+    mark(s, 2 * EC_STAGE_COMPACT + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.overflow) {
+        s->stats.table_retries++;
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        return EC_OK;
+    }
+    U = hsc.nsolid;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
+    s->stats.n_distinct = U;
+    s->stats.n_solid = U;
+    s->stats.count_path = EC_PATH_PARTITIONED;
+    s->stats.n_buckets = nb;
+    s->stats.table_capacity = umax;
+    sidx = SolidIndex{};
+    sidx.sub = s->sub.as<SubSlot>();
+    sidx.bbits = bbits;
+    sidx.slots = slots;
+    ok = true;
+    return EC_OK;
+}
+
+
 // ---- 32 < k <= 63: 128-bit keys (wide.h), general-table counting ---------------------------
 int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, SolidIndexW &sidx) {
     hipStream_t st = s->stream;
@@ -955,7 +1046,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
     mark(s, 2 * EC_STAGE_GFA + 1);
 
     // ---- results to host --------------------------------------------------------------------
-    s->h_chars.resize(nchars);
+    EC_CHECK(s->h_chars.resize(nchars));
     std::vector<unsigned int> lcnt(2 * (size_t)nc);
     std::vector<long long> lk(16 * (size_t)nc);
     if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), s->chars.p, nchars, hipMemcpyDeviceToHost, st));
@@ -1053,6 +1144,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur};
     for (auto *b : all) b->release();
+    s->h_chars.release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);
         for (auto &e : s->kev) hipEventDestroy(e);
@@ -1115,7 +1207,7 @@ int ec_copy_contigs(ec_session *s, char *chars, uint64_t *offsets) {
         set_error("no successful assembly in this session");
         return EC_ERR_STATE;
     }
-    if (chars && !s->h_chars.empty()) memcpy(chars, s->h_chars.data(), s->h_chars.size());
+    if (chars && !s->h_chars.empty()) memcpy(chars, s->h_chars.data(), s->h_chars.size);
     if (offsets) memcpy(offsets, s->h_coff.data(), s->h_coff.size() * 8);
     return EC_OK;
 }
@@ -1286,7 +1378,10 @@ int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int
         return phase_graph<OpsW>(s, k, U, sidx);
     }
     SolidIndex sidx{};
-    EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, LLONG_MIN, U, sidx));
+    bool ok = false;
+    if (!(flags & EC_FLAG_GENERAL))
+        EC_CHECK(phase_load_solid(s, reinterpret_cast<const Agg *>(d_records), n, U, sidx, ok));
+    if (!ok) EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, LLONG_MIN, U, sidx));
     return phase_graph<Ops64>(s, k, U, sidx);
 }
 

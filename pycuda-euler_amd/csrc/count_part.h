@@ -555,13 +555,14 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
 }
 
 // ---- bucket counting in LDS -------------------------------------------------------------
-struct alignas(8) LSlot {
+struct alignas(16) LSlot {
     unsigned long long key;
-    unsigned long long fC;
-    unsigned long long fT;
     unsigned int count;
     unsigned int pad;
+    unsigned long long fC;  // fC, fT 16-B aligned: one ds_read_b128 reads both
+    unsigned long long fT;
 };
+static_assert(sizeof(LSlot) == 32, "LDS slot layout");
 
 // record sources of k_bucket: window records of the counting pass, or exchange records
 // (count sum, first-event min) of the multi-GPU merge, visited through a bucket-major permutation
@@ -603,15 +604,22 @@ struct Rec12Source {
 
 // ---- LDS bucket table, shared by every bucket pass (window records, exchange records,
 // super-k-mers): SLOTS open-addressing slots, CAS claim, count += add, atomicMin of events
+// s_over[0] = overflow flag, s_over[1] = claimed slots.  A lane reserves a slot in the fill count
+// before claiming one, and no claim takes the last free slot, so at least one slot stays empty
+// and every probe sequence ends without a probe bound (a bounded loop costs the wave a
+// counter, a compare and an exec-mask juggle per probe).
 template <int SLOTS>
 __device__ inline void lds_table_init(LSlot *tab, unsigned int *s_over) {
     for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
         tab[i].key = EMPTY_KEY;
+        tab[i].count = 0;
         tab[i].fC = NONE64;
         tab[i].fT = NONE64;
-        tab[i].count = 0;
     }
-    if (threadIdx.x == 0) *s_over = 0;
+    if (threadIdx.x == 0) {
+        s_over[0] = 0;
+        s_over[1] = 0;
+    }
     __syncthreads();
 }
 
@@ -619,25 +627,28 @@ __device__ inline void lds_table_init(LSlot *tab, unsigned int *s_over) {
 template <int SLOTS>
 __device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
                                   unsigned int add, unsigned long long eC, unsigned long long eT) {
-    if (*s_over) return;  // the bucket is redone on the general path anyway
     unsigned int slot = slot0 & (SLOTS - 1);
-    int probe = 0;
-    for (; probe < SLOTS; probe++) {
-        unsigned long long cur = tab[slot].key;
+    unsigned long long cur = tab[slot].key;
+#pragma unroll 1
+    while (cur != c) {
         if (cur == EMPTY_KEY) {
-            cur = atomicCAS(&tab[slot].key, EMPTY_KEY, (unsigned long long)c);
-            if (cur == EMPTY_KEY) cur = c;
+            if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {  // table full: the bucket is redone elsewhere
+                s_over[0] = 1;
+                return;
+            }
+            cur = atomicCAS(&tab[slot].key, EMPTY_KEY, c);
+            if (cur == EMPTY_KEY) break;  // claimed
+            atomicSub(&s_over[1], 1u);    // lost the race: re-check the winner's key
+            continue;
         }
-        if (cur == c) break;
         slot = (slot + 1) & (SLOTS - 1);
+        cur = tab[slot].key;
     }
-    if (probe == SLOTS) {
-        *s_over = 1;
-        return;
-    }
-    if (add) atomicAdd(&tab[slot].count, add);
-    if (eC < tab[slot].fC) atomicMin(&tab[slot].fC, eC);
-    if (eT < tab[slot].fT) atomicMin(&tab[slot].fT, eT);
+    LSlot &sl = tab[slot];
+    if (add) atomicAdd(&sl.count, add);
+    const ulonglong2 ev = *reinterpret_cast<const ulonglong2 *>(&sl.fC);
+    if (eC < ev.x) atomicMin(&sl.fC, eC);
+    if (eT < ev.y) atomicMin(&sl.fT, eT);
 }
 
 // solid filter (count > limit, build:37-39) + compaction of bucket b's table into the dense
@@ -716,9 +727,9 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
                                                           SubSlot *sub, unsigned int *nsolid,
                                                           unsigned long long *ndistinct, unsigned int *overflow) {
     __shared__ LSlot tab[SLOTS];
-    __shared__ unsigned int s_over;
+    __shared__ unsigned int s_over[2];
     const unsigned int b = blockIdx.x;
-    lds_table_init<SLOTS>(tab, &s_over);
+    lds_table_init<SLOTS>(tab, s_over);
     const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
     // BK_UNROLL records per thread per step, all loads issued before the inserts: the loop
     // is bound by HBM latency, not bandwidth, without this memory-level parallelism
@@ -731,15 +742,15 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
         for (int u = 0; u < BK_UNROLL; u++) src.get(i + u * (uint64_t)blockDim.x, c[u], add[u], eC[u], eT[u]);
 #pragma unroll
         for (int u = 0; u < BK_UNROLL; u++)
-            lds_insert<SLOTS>(tab, &s_over, c[u], (unsigned int)mix64(c[u]), add[u], eC[u], eT[u]);
+            lds_insert<SLOTS>(tab, s_over, c[u], (unsigned int)mix64(c[u]), add[u], eC[u], eT[u]);
     }
     for (; i < r1; i += blockDim.x) {
         unsigned long long c, eC, eT;
         unsigned int add;
         src.get(i, c, add, eC, eT);
-        lds_insert<SLOTS>(tab, &s_over, c, (unsigned int)mix64(c), add, eC, eT);
+        lds_insert<SLOTS>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT);
     }
-    lds_table_finish<SLOTS>(tab, &s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
+    lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
 }
 
 }  // namespace ec

@@ -255,6 +255,8 @@ struct alignas(32) RJump {
 };
 static_assert(sizeof(RJump) == 32, "rjump layout");
 
+// Each ruler walks its segment up to the next ruler (a chain of dependent loads).  The next
+// successor is requested before the node's first-event load, so the two latencies overlap.
 __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const unsigned long long *dfc,
                                               const unsigned long long *dft, const unsigned int *rlist,
                                               unsigned int r0, const unsigned int *nr, unsigned int smask,
@@ -267,8 +269,8 @@ __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const un
         unsigned int v = rlist[i];
         unsigned long long fm = first_event(dfc, dft, v);
         unsigned int j = 0, nx = NONE32;
+        unsigned int w = succ[v];
         for (;;) {
-            const unsigned int w = succ[v];
             if (w == NONE32) break;
             if (ruler_hash(w, smask)) {  // maybe the next ruler
                 const unsigned int q = rid[w].x;
@@ -279,8 +281,9 @@ __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const un
             }
             v = w;
             j++;
-            rid[v] = make_uint2(i, j);  // (ruler, offset) in one 8-B store
+            w = succ[v];  // chain load first
             const unsigned long long f = first_event(dfc, dft, v);
+            rid[v] = make_uint2(i, j);  // (ruler, offset) in one 8-B store
             fm = f < fm ? f : fm;
         }
         nextR[i] = nx;

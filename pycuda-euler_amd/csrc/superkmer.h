@@ -487,14 +487,14 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_sk(const SkRec *recs,
     constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
     constexpr unsigned int NW = BUCKET_THREADS / 64;
     __shared__ LSlot tab[SLOTS];
-    __shared__ unsigned int s_over;
+    __shared__ unsigned int s_over[2];
     __shared__ SkRec wrec[CH];
     __shared__ unsigned int wpre[CH + 1];
     __shared__ unsigned short chunk_first[NCH];
     __shared__ unsigned long long wmask[NW];
     __shared__ unsigned int s_next, s_wsum[NW];
     const unsigned int b = blockIdx.x;
-    lds_table_init<SLOTS>(tab, &s_over);
+    lds_table_init<SLOTS>(tab, s_over);
     const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
     const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint64_t c0 = r0; c0 < r1; c0 += CH) {
@@ -557,12 +557,12 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_sk(const SkRec *recs,
                 const unsigned long long c = f ? fwd : rc;
                 const unsigned int add = fwd == rc ? 2u : 1u;  // even-k palindrome: inserted twice,
                 const unsigned int lC = f || fwd == rc ? lf : lr, lT = f && fwd != rc ? lr : lf;  // at lf
-                lds_insert<SLOTS>(tab, &s_over, c, sk_slot(c) >> (32 - SBITS), add, rd | lC, rd | lT);
+                lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, rd | lC, rd | lT);
             }
         }
         __syncthreads();
     }
-    lds_table_finish<SLOTS>(tab, &s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
+    lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
 }
 
 }  // namespace ec

@@ -66,8 +66,17 @@ def main():
         for i, x in enumerate(solids):
             allsolid[i * mx: i * mx + x.numel()] = x
         t0 = time.perf_counter()
-        res = engines[0].assemble_from_solid(allsolid, 31, 0)
-        tick("graph", t0)
+        eng = engines[0]
+        import ctypes
+        import eulerhip
+        eulerhip.check(eng.L.ec_assemble_from_solid(eng._h(), ctypes.c_void_p(allsolid.data_ptr()),
+                                                    allsolid.numel() // rb, 31, eulerhip.EC_FLAG_TIMING))
+        tick("graph_core", t0)
+        t0 = time.perf_counter()
+        res = eng.sess.fetch(31)
+        tick("fetch", t0)
+        st = eng.stats()
+        print("graph stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
         print("rep %d  ranks %d  per-rank max ms: %s  exchanged bytes/rank ~%.0f MB, gathered %.0f MB" % (
             rep, world, {k: round(max(v), 2) for k, v in t.items()},
             sum(c for c in sends[0][1]) * rb / 1e6, allsolid.numel() / 1e6))
