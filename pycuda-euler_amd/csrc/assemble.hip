@@ -318,7 +318,9 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     // ---- prescan = partition upsweep ------------------------------------------------------
     mark(s, 2 * EC_STAGE_PRESCAN);
     const uint64_t ntiles = (nreads + TILE_READS - 1) / TILE_READS;
-    uint64_t ngroups = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, 1024));
+    uint64_t maxg = 2048;
+    if (const char *e = getenv("EULERHIP_MAX_GROUPS")) maxg = std::max(1, atoi(e));
+    uint64_t ngroups = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, maxg));
     const uint64_t gsize = std::max<uint64_t>(1, (ntiles + ngroups - 1) / ngroups) * TILE_READS;
     ngroups = std::max<uint64_t>(1, (nreads + gsize - 1) / gsize);
     EC_CHECK(s->hist.ensure(ngroups * FINE * 4));
@@ -426,6 +428,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
         // compact records: keys [0, 8P) and meta [8P, 12P) of the first record buffer
         const Store12 c1{s->recs.as<unsigned long long>(), reinterpret_cast<unsigned int *>(s->recs.as<uint8_t>() + P * 8)};
+        // refine output of compact records: packed 12-B records (EULERHIP_PACK12=0: widened to 16 B)
+        const bool pack12 = !(getenv("EULERHIP_PACK12") && atoi(getenv("EULERHIP_PACK12")) == 0);
         kmark(s, 1, 0);
         if (sk)
             k_downsweep_sk<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, mc, gsize, ngroups, cbits,
@@ -450,6 +454,10 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             if (sk)
                 k_refine<SkRec, StoreSk, StoreSk><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
                     StoreSk{s->recs.as<SkRec>()}, StoreSk{s->recs2.as<SkRec>()}, s->bstart.as<unsigned long long>(),
+                    s->gcur.as<unsigned long long>(), cbits, bbits);
+            else if (compact && pack12)  // 12-B in, packed 12-B out
+                k_refine<Rec12, Store12, Store12P><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                    c1, Store12P{s->recs2.as<unsigned int>()}, s->bstart.as<unsigned long long>(),
                     s->gcur.as<unsigned long long>(), cbits, bbits);
             else if (compact)  // 12-B in, 16-B out: k_bucket reads 16-B records
                 k_refine<Rec12, Store12, Store12to16><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
@@ -483,9 +491,28 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
                     sr, s->bstart.as<unsigned long long>(), k, (long long)limit, s->dkey.as<unsigned long long>(),
                     s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
                     s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+        } else if (compact && second && pack12) {
+            const unsigned int m2 = (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1);
+            if (k & 1) {
+                Rec12PSource<false> src;
+                src.ibits = ibits, src.k = k, src.m2 = m2, src.p = s->recs2.as<unsigned int>();
+                EC_CHECK(launch_bucket(s, src, (unsigned)Bk, slots, (long long)limit));
+            } else {
+                Rec12PSource<true> src;
+                src.ibits = ibits, src.k = k, src.m2 = m2, src.p = s->recs2.as<unsigned int>();
+                EC_CHECK(launch_bucket(s, src, (unsigned)Bk, slots, (long long)limit));
+            }
         } else if (compact && !second) {
-            EC_CHECK(launch_bucket(s, Rec12Source{c1.key, c1.meta, ibits, k, (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1)},
-                                   (unsigned)Bk, slots, (long long)limit));
+            const unsigned int m2 = (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1);
+            if (k & 1) {
+                Rec12Source<false> src;
+                src.ibits = ibits, src.k = k, src.m2 = m2, src.key = c1.key, src.meta = c1.meta;
+                EC_CHECK(launch_bucket(s, src, (unsigned)Bk, slots, (long long)limit));
+            } else {
+                Rec12Source<true> src;
+                src.ibits = ibits, src.k = k, src.m2 = m2, src.key = c1.key, src.meta = c1.meta;
+                EC_CHECK(launch_bucket(s, src, (unsigned)Bk, slots, (long long)limit));
+            }
         } else {
             EC_CHECK(launch_bucket(s, RecSource{second ? s->recs2.as<Rec>() : s->recs.as<Rec>()}, (unsigned)Bk, slots,
                                    (long long)limit));

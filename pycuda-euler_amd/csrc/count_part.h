@@ -121,6 +121,16 @@ struct Store12to16 {
     }
 };
 
+// compact records as one packed 12-B array (the refine output read by k_bucket)
+struct Store12P {
+    unsigned int *p;
+    __device__ inline void store(uint64_t i, const Rec12 &r) const {
+        p[3 * i] = r.klo;
+        p[3 * i + 1] = r.khi;
+        p[3 * i + 2] = r.meta;
+    }
+};
+
 struct Store12 {
     unsigned long long *key;
     unsigned int *meta;
@@ -566,11 +576,15 @@ static_assert(sizeof(LSlot) == 32, "LDS slot layout");
 
 // record sources of k_bucket: window records of the counting pass, or exchange records
 // (count sum, first-event min) of the multi-GPU merge, visited through a bucket-major permutation
+// Every source splits a record access into fetch (the loads) and decode (arithmetic), so
+// k_bucket issues the loads of all its unrolled records before decoding any: a branch inside
+// a decode (the even-k palindrome test) would otherwise serialise the loads behind it.
 struct RecSource {
     const Rec *recs;
-    __device__ inline void get(uint64_t i, unsigned long long &key, unsigned int &add, unsigned long long &eC,
-                               unsigned long long &eT) const {
-        const Rec rec = recs[i];
+    using Raw = Rec;
+    __device__ inline Raw fetch(uint64_t i) const { return recs[i]; }
+    __device__ inline void decode(const Raw &rec, unsigned long long &key, unsigned int &add, unsigned long long &eC,
+                                  unsigned long long &eT) const {
         const unsigned int lC = rec.ev & 0xFFFFu, lT = rec.ev >> 16;
         key = rec.key;
         add = lC == lT ? 2u : 1u;  // even-k palindrome: build inserts it twice
@@ -579,26 +593,57 @@ struct RecSource {
     }
 };
 
-struct Rec12Source {
-    const unsigned long long *key;
-    const unsigned int *meta;
+// compact record decode: meta = read << (ibits + 1) | orientation << ibits | window.  The
+// even-k palindrome test is a template branch: left to a runtime k test the compiler evaluates
+// twin64 for every record (k_bucket measured 45 % slower).
+template <bool EVEN_K>
+struct Rec12Decode {
     int ibits;
     int k;
     unsigned int m2;  // 2m - 1
-    __device__ inline void get(uint64_t i, unsigned long long &kk, unsigned int &add, unsigned long long &eC,
-                               unsigned long long &eT) const {
-        kk = key[i];
-        const unsigned int mt = meta[i];
+    __device__ inline void decode(const Rec12 &r, unsigned long long &kk, unsigned int &add, unsigned long long &eC,
+                                  unsigned long long &eT) const {
+        kk = rkey(r);
+        const unsigned int mt = r.meta;
         const unsigned long long rd = (unsigned long long)(mt >> (ibits + 1)) << 32;
         const unsigned int w = mt & ((1u << ibits) - 1), o = (mt >> ibits) & 1u;
-        if (!(k & 1) && twin64(kk, k) == kk) {  // even-k palindrome: inserted twice at the forward event
-            add = 2;
-            eC = eT = rd | w;
-            return;
-        }
+        unsigned int lC = o ? m2 - w : w, lT = o ? w : m2 - w;
         add = 1;
-        eC = rd | (o ? m2 - w : w);
-        eT = rd | (o ? w : m2 - w);
+        if (EVEN_K && twin64(kk, k) == kk) {  // even-k palindrome: inserted twice at the forward event
+            add = 2;
+            lC = lT = w;
+        }
+        eC = rd | lC;
+        eT = rd | lT;
+    }
+};
+
+template <bool EVEN_K>
+struct Rec12Source : Rec12Decode<EVEN_K> {
+    const unsigned long long *key;
+    const unsigned int *meta;
+    using Raw = Rec12;
+    __device__ inline Raw fetch(uint64_t i) const {
+        const unsigned long long kk = key[i];
+        Rec12 r;
+        r.klo = (unsigned int)kk;
+        r.khi = (unsigned int)(kk >> 32);
+        r.meta = meta[i];
+        return r;
+    }
+};
+
+// packed 12-B records (Store12P: one array, dwordx3 accesses)
+template <bool EVEN_K>
+struct Rec12PSource : Rec12Decode<EVEN_K> {
+    const unsigned int *p;
+    using Raw = Rec12;
+    __device__ inline Raw fetch(uint64_t i) const {
+        Rec12 r;
+        r.klo = p[3 * i];
+        r.khi = p[3 * i + 1];
+        r.meta = p[3 * i + 2];
+        return r;
     }
 };
 
@@ -623,29 +668,38 @@ __device__ inline void lds_table_init(LSlot *tab, unsigned int *s_over) {
     __syncthreads();
 }
 
-// slot0 = first probe slot (the bucket sub-table's lookups start at the same slot)
+// slot0 = first probe slot (the bucket sub-table's lookups start at the same slot).
+// The probe loop is wave-uniform (runs while any lane still misses; lanes that found their
+// slot idle under one exec mask): almost every wave has some lane past its first probe, and a
+// per-lane loop with several exits costs ~40 scalar mask instructions per iteration.
 template <int SLOTS>
 __device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
                                   unsigned int add, unsigned long long eC, unsigned long long eT) {
     unsigned int slot = slot0 & (SLOTS - 1);
     unsigned long long cur = tab[slot].key;
+    bool miss = cur != c;
 #pragma unroll 1
-    while (cur != c) {
-        if (cur == EMPTY_KEY) {
-            if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {  // table full: the bucket is redone elsewhere
-                s_over[0] = 1;
-                return;
+    while (__any(miss)) {
+        if (miss) {
+            if (cur == EMPTY_KEY) {
+                if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {  // table full: the bucket is redone elsewhere
+                    s_over[0] = 1;
+                    cur = c;  // give up (updates below land in a discarded table)
+                } else {
+                    cur = atomicCAS(&tab[slot].key, EMPTY_KEY, c);
+                    if (cur == EMPTY_KEY) cur = c;  // claimed
+                    else atomicSub(&s_over[1], 1u);  // lost the race: cur = the winner's key
+                }
             }
-            cur = atomicCAS(&tab[slot].key, EMPTY_KEY, c);
-            if (cur == EMPTY_KEY) break;  // claimed
-            atomicSub(&s_over[1], 1u);    // lost the race: re-check the winner's key
-            continue;
+            if (cur != c) {
+                slot = (slot + 1) & (SLOTS - 1);
+                cur = tab[slot].key;
+            }
+            miss = cur != c;
         }
-        slot = (slot + 1) & (SLOTS - 1);
-        cur = tab[slot].key;
     }
     LSlot &sl = tab[slot];
-    if (add) atomicAdd(&sl.count, add);
+    atomicAdd(&sl.count, add);
     const ulonglong2 ev = *reinterpret_cast<const ulonglong2 *>(&sl.fC);
     if (eC < ev.x) atomicMin(&sl.fC, eC);
     if (eT < ev.y) atomicMin(&sl.fT, eT);
@@ -736,18 +790,21 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
     constexpr int BK_UNROLL = 4;
     uint64_t i = r0 + threadIdx.x;
     for (; i + (BK_UNROLL - 1) * (uint64_t)blockDim.x < r1; i += BK_UNROLL * (uint64_t)blockDim.x) {
-        unsigned long long c[BK_UNROLL], eC[BK_UNROLL], eT[BK_UNROLL];
-        unsigned int add[BK_UNROLL];
+        typename Src::Raw raw[BK_UNROLL];
 #pragma unroll
-        for (int u = 0; u < BK_UNROLL; u++) src.get(i + u * (uint64_t)blockDim.x, c[u], add[u], eC[u], eT[u]);
+        for (int u = 0; u < BK_UNROLL; u++) raw[u] = src.fetch(i + u * (uint64_t)blockDim.x);
 #pragma unroll
-        for (int u = 0; u < BK_UNROLL; u++)
-            lds_insert<SLOTS>(tab, s_over, c[u], (unsigned int)mix64(c[u]), add[u], eC[u], eT[u]);
+        for (int u = 0; u < BK_UNROLL; u++) {
+            unsigned long long c, eC, eT;
+            unsigned int add;
+            src.decode(raw[u], c, add, eC, eT);
+            lds_insert<SLOTS>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT);
+        }
     }
     for (; i < r1; i += blockDim.x) {
         unsigned long long c, eC, eT;
         unsigned int add;
-        src.get(i, c, add, eC, eT);
+        src.decode(src.fetch(i), c, add, eC, eT);
         lds_insert<SLOTS>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT);
     }
     lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);

@@ -161,9 +161,10 @@ __global__ void __launch_bounds__(256) k_bucket_bounds(const unsigned int *sbid,
 struct AggSource {
     const Agg *in;
     const unsigned int *perm;
-    __device__ inline void get(uint64_t i, unsigned long long &key, unsigned int &add, unsigned long long &eC,
-                               unsigned long long &eT) const {
-        const Agg a = in[perm[i]];
+    using Raw = Agg;
+    __device__ inline Raw fetch(uint64_t i) const { return in[perm[i]]; }
+    __device__ inline void decode(const Agg &a, unsigned long long &key, unsigned int &add, unsigned long long &eC,
+                                  unsigned long long &eT) const {
         key = a.key;
         add = a.count;
         eC = a.fC;
