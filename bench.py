@@ -61,7 +61,7 @@ def kernel_alg_bytes(name, P, R, L, K=8, rec=16, NR=None, nsub=0):
     Window records (rec = 16, or 12 for compact records; NR = P records):
     k_upsweep   reads the ASCII reads once                          R*L
     k_downsweep reads them again + writes one record/position       R*L + rec*P
-    k_refine    reads every record, writes it as a 16-B record      (rec + 16)*P
+    k_refine    reads every record, writes it again (same size)     2*rec*P
     k_bucket    one canonical insert per position      P*(K+8)
     k_count     general path: read once + one insert/position       R*L + P*(K+8)
     Super-k-mer records (rec = 32, NR records, nsub = bucket sub-table bytes written):
@@ -70,7 +70,7 @@ def kernel_alg_bytes(name, P, R, L, K=8, rec=16, NR=None, nsub=0):
         return {"k_upsweep": R * L, "k_downsweep": R * L + 32 * NR, "k_bucket": 32 * NR + nsub,
                 "k_count": R * L + P * (K + 8), "k_refine": 64 * NR}[name]
     return {"k_upsweep": R * L, "k_downsweep": R * L + rec * P, "k_bucket": P * (K + 8),
-            "k_count": R * L + P * (K + 8), "k_refine": (rec + 16) * P}[name]
+            "k_count": R * L + P * (K + 8), "k_refine": 2 * rec * P}[name]
 
 
 def cpu_baseline(buf, off, k, sample_reads):

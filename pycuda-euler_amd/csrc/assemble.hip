@@ -447,7 +447,9 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         bool second = false;
         if (bbits > cbits) {
             // split every coarse bucket over RS workgroups (>= 4 per CU in flight)
-            const unsigned RS = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8, 1024 / Ck));
+            unsigned rsmax = 8;
+            if (const char *e = getenv("EULERHIP_REFINE_RS")) rsmax = (unsigned)std::max(1, atoi(e));
+            const unsigned RS = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(rsmax, 1024 * rsmax / 8 / Ck));
             EC_CHECK(s->gcur.ensure(Bk * 8));
             EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
             kmark(s, 4, 0);

@@ -490,6 +490,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
                                                           unsigned long long *gcur, int cbits, int bbits) {
     constexpr int TILE = sizeof(RecT) > 16 ? REFINE_TILE / 2 : REFINE_TILE;  // <= 64 KiB of LDS
     __shared__ RecT tile[TILE];
+    __shared__ uint8_t tj[TILE];  // final bucket of each sorted record (the store loop needs no rehash)
     __shared__ unsigned long long base[REFINE_FANOUT];
     __shared__ unsigned int tcnt[REFINE_FANOUT], tbeg[REFINE_FANOUT], wsum[REFINE_FANOUT / 64];
     const int F = 1 << (bbits - cbits);
@@ -530,7 +531,11 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
             }
         }
         __syncthreads();
-        if (threadIdx.x < REFINE_FANOUT) {  // exclusive scan of the tile counts + run reservation
+        // exclusive scan of the tile counts + run reservation.  The reservation's returning
+        // atomic is consumed only after the LDS scatter, so its latency overlaps the scatter
+        // instead of stalling the whole workgroup at the next barrier.
+        unsigned long long mybase = 0;
+        if (threadIdx.x < REFINE_FANOUT) {
             const unsigned int v = (int)threadIdx.x < F ? tcnt[threadIdx.x] : 0u;
             unsigned int incl = v;
             for (int o = 1; o < 64; o <<= 1) {
@@ -539,7 +544,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
             }
             tbeg[threadIdx.x] = incl - v;
             if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
-            if (v) base[threadIdx.x] = atomicAdd(&gcur[c * F + threadIdx.x], (unsigned long long)v);
+            if (v) mybase = atomicAdd(&gcur[c * F + threadIdx.x], (unsigned long long)v);
         }
         __syncthreads();
         if (threadIdx.x >= 64 && threadIdx.x < REFINE_FANOUT) {
@@ -551,14 +556,18 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
 #pragma unroll
         for (int q = 0; q < PER; q++) {
             const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
-            if (i < n) tile[tbeg[jj[q]] + rk[q]] = rr[q];
+            if (i < n) {
+                const unsigned int p = tbeg[jj[q]] + rk[q];
+                tile[p] = rr[q];
+                tj[p] = (uint8_t)jj[q];
+            }
         }
+        if (threadIdx.x < REFINE_FANOUT) base[threadIdx.x] = mybase;
         __syncthreads();
         if (PIPE && t0 + TILE < tend) load_tile(t0 + TILE);
         for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
-            const RecT rec = tile[i];
-            const unsigned int j = rec_bucket(rec, bbits) & (F - 1);
-            out.store(base[j] + (i - tbeg[j]), rec);
+            const unsigned int j = tj[i];
+            out.store(base[j] + (i - tbeg[j]), tile[i]);
         }
         __syncthreads();
     }
