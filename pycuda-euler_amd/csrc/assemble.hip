@@ -724,68 +724,6 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
 }
 
 
-// The all-gathered solid set of the sharded path (distinct keys, filler records) straight into
-// the dense arrays and a bucketed SolidIndex: one compaction + CAS-insert pass instead of the
-// sort + LDS-table merge of phase_merge.  ok = false (nothing committed) when the set is too
-// large for the bucket layout or a bucket region overflowed: the caller merges instead.
-int phase_load_solid(ec_session *s, const Agg *d_agg, uint64_t n, unsigned int &U, SolidIndex &sidx, bool &ok) {
-    hipStream_t st = s->stream;
-    Scalars *dsc = s->scal.as<Scalars>();
-    Scalars hsc;
-    ok = false;
-    int bbits = 0;
-    while (bbits < FINE_BITS && (double)n / (double)(1ull << bbits) > 1100.0) bbits++;
-    if ((double)n / (double)(1ull << bbits) > 2200.0) return EC_OK;
-    const unsigned int nb = 1u << bbits;
-    const unsigned int slots = (double)n / (double)nb > 1100.0 ? 4096u : 2048u;
-    const uint64_t umax = (uint64_t)nb * slots;
-    const unsigned int nblk = (unsigned int)std::max<uint64_t>((n + LOAD_CHUNK - 1) / LOAD_CHUNK, 1);
-    mark(s, 2 * EC_STAGE_COMPACT);
-    EC_CHECK(s->rbc.ensure((size_t)nblk * 8));
-    EC_CHECK(s->dkey.ensure(std::max<uint64_t>(n, 1) * 8));
-    EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(n, 1) * 4));
-    EC_CHECK(s->dfc.ensure(std::max<uint64_t>(n, 1) * 8));
-    EC_CHECK(s->dft.ensure(std::max<uint64_t>(n, 1) * 8));
-    EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
-    EC_HIP(hipMemsetAsync(s->sub.p, 0xFF, umax * sizeof(SubSlot), st));
-    EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
-    EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
-    unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk;
-    if (n) {
-        k_load_count<<<nblk, 256, 0, st>>>(d_agg, n, bc);
-        EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
-        k_load_write<<<nblk, 256, 0, st>>>(d_agg, n, bs, bbits, slots, s->dkey.as<unsigned long long>(),
-                                           s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                           s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->overflow);
-        k_compact_total<<<1, 1, 0, st>>>(bs, nblk, &dsc->nsolid);
-    }
-    mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
-    if (hsc.overflow) {
-        s->stats.table_retries++;
-        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
-        return EC_OK;
-    }
-    U = hsc.nsolid;
-    if (2ull * U >= (unsigned long long)CYC) {
-        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
-        return EC_ERR_CAPACITY;
-    }
-    s->stats.n_distinct = U;
-    s->stats.n_solid = U;
-    s->stats.count_path = EC_PATH_PARTITIONED;
-    s->stats.n_buckets = nb;
-    s->stats.table_capacity = umax;
-    sidx = SolidIndex{};
-    sidx.sub = s->sub.as<SubSlot>();
-    sidx.bbits = bbits;
-    sidx.slots = slots;
-    ok = true;
-    return EC_OK;
-}
-
-
 // ---- 32 < k <= 63: 128-bit keys (wide.h), general-table counting ---------------------------
 int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, SolidIndexW &sidx) {
     hipStream_t st = s->stream;
@@ -1406,11 +1344,11 @@ int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int
         EC_CHECK(phase_merge_w(s, reinterpret_cast<const AggW *>(d_records), n, LLONG_MIN, U, sidx));
         return phase_graph<OpsW>(s, k, U, sidx);
     }
+    // the gathered keys are distinct; the bucketed merge (sort by bucket + LDS tables) is also
+    // the fastest loader: measured 0.42 ms at 4.6 M keys against 0.60 ms for per-key CAS
+    // inserts into the HBM sub-table (random-address atomics)
     SolidIndex sidx{};
-    bool ok = false;
-    if (!(flags & EC_FLAG_GENERAL))
-        EC_CHECK(phase_load_solid(s, reinterpret_cast<const Agg *>(d_records), n, U, sidx, ok));
-    if (!ok) EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, LLONG_MIN, U, sidx));
+    EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, LLONG_MIN, U, sidx));
     return phase_graph<Ops64>(s, k, U, sidx);
 }
 

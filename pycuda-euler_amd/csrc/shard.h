@@ -173,70 +173,4 @@ struct AggSource {
 };
 
 
-// ---- gathered solid set -> dense arrays + bucketed lookup sub-table (no re-merge) -------------
-// The all-gathered records hold distinct keys (every key was merged by exactly one owner), so
-// loading them needs no counting: a chunked ballot compaction gives dense ids in record order
-// (filler records skipped) and each key is CAS-inserted into the sub-table region of its
-// bucket (top bbits of mix64, linear probing from the low bits -- SolidIndex::find's layout).
-constexpr unsigned int LOAD_CHUNK = 8192;
-
-__global__ void __launch_bounds__(256) k_load_count(const Agg *in, uint64_t n, unsigned int *bc) {
-    const uint64_t c0 = (uint64_t)blockIdx.x * LOAD_CHUNK;
-    const uint64_t c1 = c0 + LOAD_CHUNK < n ? c0 + LOAD_CHUNK : n;
-    unsigned int v = 0;
-    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) v += in[i].key != EMPTY_KEY;
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    __shared__ unsigned int ws[4];
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) bc[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-// bs = inclusive scan of the chunk counts
-__global__ void __launch_bounds__(256) k_load_write(const Agg *in, uint64_t n, const unsigned int *bs, int bbits,
-                                                    unsigned int slots, unsigned long long *dkey, unsigned int *dcnt,
-                                                    unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
-                                                    unsigned int *overflow) {
-    __shared__ unsigned int wsum[4];
-    const uint64_t c0 = (uint64_t)blockIdx.x * LOAD_CHUNK;
-    const uint64_t c1 = c0 + LOAD_CHUNK < n ? c0 + LOAD_CHUNK : n;
-    unsigned int base = blockIdx.x ? bs[blockIdx.x - 1] : 0u;
-    const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint64_t i0 = c0; i0 < c1; i0 += blockDim.x) {
-        const uint64_t i = i0 + threadIdx.x;
-        Agg a;
-        a.key = EMPTY_KEY;
-        if (i < c1) a = in[i];
-        const bool valid = a.key != EMPTY_KEY;
-        const unsigned long long m = __ballot(valid);
-        if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
-        __syncthreads();
-        unsigned int off = base;
-        for (unsigned int q = 0; q < wid; q++) off += wsum[q];
-        const unsigned int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        if (valid) {
-            const unsigned int u = off + (unsigned int)__popcll(m & ((1ull << lane) - 1));
-            dkey[u] = a.key;
-            dcnt[u] = a.count;
-            dfc[u] = a.fC;
-            dft[u] = a.fT;
-            const uint64_t h = mix64(a.key);
-            SubSlot *region = sub + (bbits ? (h >> (64 - bbits)) : 0ull) * slots;
-            unsigned int slot = (unsigned int)h & (slots - 1);
-            unsigned int probe = 0;
-            for (; probe < slots; probe++) {
-                const unsigned long long prev = atomicCAS(&region[slot].key, EMPTY_KEY, a.key);
-                if (prev == EMPTY_KEY || prev == a.key) {
-                    region[slot].id = u;
-                    break;
-                }
-                slot = (slot + 1) & (slots - 1);
-            }
-            if (probe == slots) atomicOr(overflow, 1u);
-        }
-        base += tot;
-        __syncthreads();
-    }
-}
-
 }  // namespace ec

@@ -128,31 +128,35 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
 
-    def alltoallv(self, send, counts_bytes):
-        """send: uint8 tensor laid out destination-major with counts_bytes[d] bytes for rank d."""
+    def alltoallv(self, send, counts_bytes, tag=0):
+        """send: uint8 tensor laid out destination-major with counts_bytes[d] bytes for rank d.
+        Returns (received bytes, sum over ranks of `tag`): the per-rank integer rides along with
+        the byte-count exchange, so no separate all-reduce (and host sync) is needed for it."""
         torch, dist = self.torch, self.dist
         dev = send.device
-        sc = torch.tensor(counts_bytes, dtype=torch.int64, device=dev)
+        sc = torch.tensor([[int(c), int(tag)] for c in counts_bytes], dtype=torch.int64, device=dev)
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=self.group)
-        rcl = [int(x) for x in rc.tolist()]
+        rcv = rc.tolist()
+        rcl = [int(x[0]) for x in rcv]
+        total_tag = sum(int(x[1]) for x in rcv)
         recv = torch.empty(max(sum(rcl), 1), dtype=torch.uint8, device=dev)
         if sum(rcl) or sum(counts_bytes):
             dist.all_to_all_single(recv[: sum(rcl)], send[: sum(counts_bytes)], output_split_sizes=rcl,
                                    input_split_sizes=list(counts_bytes), group=self.group)
-        return recv[: sum(rcl)]
+        return recv[: sum(rcl)], total_tag
 
     def allgatherv(self, t, fill=0):
         """Concatenation of every rank's `t` in rank order, each part padded with `fill` bytes
         to the largest part (no compaction copy: the record consumers skip all-0xFF filler
         records, ec_assemble_from_solid)."""
         torch, dist = self.torch, self.dist
-        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
-        sizes = [torch.empty_like(n) for _ in range(self.world)]
-        dist.all_gather(sizes, n, group=self.group)
-        mx = max(max(int(x.item()) for x in sizes), 1)
         if self.world == 1:
             return t
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+        sizes = torch.empty(self.world, dtype=torch.int64, device=t.device)
+        dist.all_gather_into_tensor(sizes, n, group=self.group)
+        mx = max(int(sizes.max().item()), 1)
         pad = torch.full((mx,), fill, dtype=torch.uint8, device=t.device)
         pad[: t.numel()] = t
         out = torch.empty(self.world * mx, dtype=torch.uint8, device=t.device)
@@ -186,10 +190,10 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     tick()
     if on_count:
         on_count(st)
-    P = comm.allreduce_sum(st.n_positions)
     recs, counts = engine.export_by_owner(comm.world)
     tick()
-    received = comm.alltoallv(recs, [c * rec_bytes(k) for c in counts])
+    # the job's k-mer positions ride along with the exchange's byte counts
+    received, P = comm.alltoallv(recs, [c * rec_bytes(k) for c in counts], tag=st.n_positions)
     tick()
     solid = engine.merge_owned(received, k, limit, flags)
     tick()

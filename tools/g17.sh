@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/g17; mkdir -p $O
+timeout -k 10 200 python tools/sim_sharded.py --ranks 8 > $O/sim8.log 2>&1 && tail -6 $O/sim8.log
+timeout -k 10 300 python bench.py --sharded --no-cpu-baseline > $O/bench_sh.json 2> $O/bench_sh.err && python -c "import json;d=json.load(open('$O/bench_sh.json'));print(d['ms_per_step'], d['sharded_phase_ms'])"

@@ -77,6 +77,7 @@ def main():
         tick("fetch", t0)
         st = eng.stats()
         print("graph stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
+        print("export per rank:", [round(x, 2) for x in t["export"]], "count per rank:", [round(x, 2) for x in t["count"]])
         print("rep %d  ranks %d  per-rank max ms: %s  exchanged bytes/rank ~%.0f MB, gathered %.0f MB" % (
             rep, world, {k: round(max(v), 2) for k, v in t.items()},
             sum(c for c in sends[0][1]) * rb / 1e6, allsolid.numel() / 1e6))
