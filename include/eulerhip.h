@@ -276,6 +276,17 @@ int ec_record_bytes(int k);
 /* graph phase (links .. GFA) on a complete solid set; results via ec_copy_* */
 int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags);
 
+/* partitioned graph phase (k <= 32), the multi-GPU form of ec_assemble_from_solid: every rank
+ * loads the same all-gathered solid set (dense ids = position among the non-filler records,
+ * so identical on every rank; ec_dense_count = U), computes the successor links of its own
+ * canonical ids [lo, hi) (d_succ receives 2(hi-lo) uint32 oriented-node successors, node
+ * 2u+o, NONE = 0xFFFFFFFF), and after the caller's all-gather of those parts finishes the
+ * graph phase on the complete successor array (uint32[2U], device) -- get_contig_forward:59-77
+ * links, then ranking .. GFA as ec_assemble_from_solid; results via ec_copy_*. */
+int ec_graph_load(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags);
+int ec_graph_links_part(ec_session *s, uint64_t lo, uint64_t hi, uint32_t *d_succ);
+int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags);
+
 #ifdef __cplusplus
 }
 #endif

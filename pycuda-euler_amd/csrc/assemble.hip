@@ -124,6 +124,8 @@ struct ec_session {
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
     unsigned flags = 0;        // flags of the current call
     DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur;
+    SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load)
+    bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
 };
 
 namespace ec {
@@ -597,7 +599,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
 // The same on the LDS bucket tables of the fused path (k_bucket over the records sorted by
 // bucket): no HBM atomics.  Returns EC_OK with ok = false when a bucket overflows its table.
 int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx,
-                     bool &ok) {
+                     bool &ok, const unsigned int *ids = nullptr, unsigned int nids = 0) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -638,9 +640,14 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
     EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
     EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
-    const AggSource src{d_agg, s->midx2.as<unsigned int>()};
     kmark(s, 2, 0);
-    EC_CHECK(launch_bucket(s, src, nb, slots, limit));
+    if (ids) {  // gathered solid set: dense ids given (partitioned graph phase)
+        const AggDetSource src{d_agg, s->midx2.as<unsigned int>(), ids};
+        EC_CHECK(launch_bucket(s, src, nb, slots, limit));
+    } else {
+        const AggSource src{d_agg, s->midx2.as<unsigned int>()};
+        EC_CHECK(launch_bucket(s, src, nb, slots, limit));
+    }
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -650,8 +657,8 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
         EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
         return EC_OK;
     }
-    U = hsc.nsolid;
-    s->stats.n_distinct = hsc.ndistinct;
+    U = ids ? nids : hsc.nsolid;
+    s->stats.n_distinct = ids ? nids : hsc.ndistinct;
     s->stats.n_solid = U;
     s->stats.count_path = EC_PATH_PARTITIONED;
     s->stats.n_buckets = nb;
@@ -723,6 +730,37 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
     return EC_OK;
 }
 
+
+// partitioned graph phase: the all-gathered solid set with dense ids = position among the
+// non-filler records (owner-major), identical on every rank, plus the bucketed lookup index
+int phase_load_det(ec_session *s, const Agg *d_agg, uint64_t n, unsigned int &U, SolidIndex &sidx) {
+    hipStream_t st = s->stream;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int nblk = (unsigned int)std::max<uint64_t>((n + DET_CHUNK - 1) / DET_CHUNK, 1);
+    EC_CHECK(s->rbc.ensure((size_t)nblk * 8));
+    EC_CHECK(s->nextR.ensure(std::max<uint64_t>(n, 1) * 4));  // ids (nextR is free until the rank stage)
+    unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk, *ids = s->nextR.as<unsigned int>();
+    unsigned int tot = 0;
+    if (n) {
+        k_det_count<<<nblk, 256, 0, st>>>(d_agg, n, bc);
+        EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
+        k_det_ids<<<nblk, 256, 0, st>>>(d_agg, n, bs, ids);
+        EC_HIP(hipMemcpyAsync(&tot, bs + nblk - 1, 4, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+    }
+    EC_CHECK(s->dkey.ensure(std::max<uint64_t>(tot, 1) * 8));
+    EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(tot, 1) * 4));
+    EC_CHECK(s->dfc.ensure(std::max<uint64_t>(tot, 1) * 8));
+    EC_CHECK(s->dft.ensure(std::max<uint64_t>(tot, 1) * 8));
+    bool ok = false;
+    EC_CHECK(phase_merge_part(s, d_agg, n, LLONG_MIN, U, sidx, ok, ids, tot));
+    if (!ok) {
+        set_error("gathered solid set of %llu records does not fit the bucketed index", (unsigned long long)n);
+        return EC_ERR_CAPACITY;
+    }
+    (void)dsc;
+    return EC_OK;
+}
 
 // ---- 32 < k <= 63: 128-bit keys (wide.h), general-table counting ---------------------------
 int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, SolidIndexW &sidx) {
@@ -843,7 +881,7 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
 
 // all_contigs:79-111 on the device from the solid set of phase_count / phase_merge
 template <typename Ops, typename Index>
-int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
+int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const unsigned int *ext_succ = nullptr) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -860,12 +898,18 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx) {
     EC_CHECK(s->cand.ensure(Nn * 4));
     EC_CHECK(s->succ.ensure(Nn * 4));
     EC_CHECK(s->pred.ensure(Nn * 4));
-    if (U) {
+    if (U && ext_succ) {  // partitioned links (ec_graph_finish): successors computed by the ranks
+        k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<typename Ops::K>(), U, k, s->upal.as<uint8_t>(),
+                                                 &dsc->npal);
+        EC_HIP(hipMemcpyAsync(s->succ.p, ext_succ, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
+    } else if (U) {
         k_neighbors<Ops, Index><<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
                                                  s->cand.as<unsigned int>(), &dsc->npal);
         k_succ<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(),
                                             N, s->succ.as<unsigned int>());
+    }
+    if (U) {
         k_pred<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
                                             s->pred.as<unsigned int>());
     }
@@ -1353,6 +1397,62 @@ int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int
 }
 
 int ec_record_bytes(int k) { return k > 32 ? (int)sizeof(AggW) : (int)sizeof(Agg); }
+
+int ec_graph_load(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags) {
+    if (!s || (n && !d_records)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    s->graph_loaded = false;
+    EC_CHECK(begin_call(s, k, flags));
+    if (k > 32) {
+        set_error("partitioned graph phase needs k <= 32 (k=%d): use ec_assemble_from_solid", k);
+        return EC_ERR_ARG;
+    }
+    unsigned int U = 0;
+    EC_CHECK(phase_load_det(s, reinterpret_cast<const Agg *>(d_records), n, U, s->gidx));
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
+    s->n_dense = U;
+    s->graph_loaded = true;
+    collect_timing(s);
+    s->stats_ok = true;
+    return EC_OK;
+}
+
+int ec_graph_links_part(ec_session *s, uint64_t lo, uint64_t hi, uint32_t *d_succ) {
+    if (!s || !s->graph_loaded || lo > hi || hi > s->n_dense || (hi > lo && !d_succ)) {
+        set_error("ec_graph_links_part: no loaded solid set or bad range [%llu, %llu)", (unsigned long long)lo,
+                  (unsigned long long)hi);
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    if (hi > lo) {
+        const uint64_t n = 2 * (hi - lo);
+        k_links_part<Ops64, SolidIndex><<<grid_for(n, 256), 256, 0, s->stream>>>(
+            s->gidx, s->dkey.as<unsigned long long>(), (unsigned int)lo, (unsigned int)hi, s->k, d_succ);
+        EC_HIP(hipGetLastError());
+    }
+    EC_HIP(hipStreamSynchronize(s->stream));
+    return EC_OK;
+}
+
+int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags) {
+    if (!s || !s->graph_loaded || (s->n_dense && !d_succ)) {
+        set_error("ec_graph_finish: no loaded solid set");
+        return EC_ERR_ARG;
+    }
+    const unsigned int U = (unsigned int)s->n_dense;
+    const ec_stats keep = s->stats;
+    EC_CHECK(begin_call(s, s->k, flags));
+    s->stats = keep;
+    for (float &v : s->stats.stage_ms) v = 0.0f;
+    for (float &v : s->stats.kernel_ms) v = 0.0f;
+    s->graph_loaded = false;
+    return phase_graph<Ops64>(s, s->k, U, s->gidx, d_succ);
+}
 
 int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *counts, uint64_t n, int k, unsigned flags) {
     if (!s || (n && (!kmers || !counts))) {

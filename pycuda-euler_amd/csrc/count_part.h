@@ -591,7 +591,9 @@ static_assert(sizeof(LSlot) == 32, "LDS slot layout");
 struct RecSource {
     const Rec *recs;
     using Raw = Rec;
+    static constexpr bool kDet = false;  // true: records carry their dense id (gathered solid set)
     __device__ inline Raw fetch(uint64_t i) const { return recs[i]; }
+    __device__ inline unsigned int id(const Raw &) const { return 0; }
     __device__ inline void decode(const Raw &rec, unsigned long long &key, unsigned int &add, unsigned long long &eC,
                                   unsigned long long &eT) const {
         const unsigned int lC = rec.ev & 0xFFFFu, lT = rec.ev >> 16;
@@ -632,6 +634,8 @@ struct Rec12Source : Rec12Decode<EVEN_K> {
     const unsigned long long *key;
     const unsigned int *meta;
     using Raw = Rec12;
+    static constexpr bool kDet = false;
+    __device__ inline unsigned int id(const Raw &) const { return 0; }
     __device__ inline Raw fetch(uint64_t i) const {
         const unsigned long long kk = key[i];
         Rec12 r;
@@ -647,6 +651,8 @@ template <bool EVEN_K>
 struct Rec12PSource : Rec12Decode<EVEN_K> {
     const unsigned int *p;
     using Raw = Rec12;
+    static constexpr bool kDet = false;
+    __device__ inline unsigned int id(const Raw &) const { return 0; }
     __device__ inline Raw fetch(uint64_t i) const {
         Rec12 r;
         r.klo = p[3 * i];
@@ -681,9 +687,10 @@ __device__ inline void lds_table_init(LSlot *tab, unsigned int *s_over) {
 // The probe loop is wave-uniform (runs while any lane still misses; lanes that found their
 // slot idle under one exec mask): almost every wave has some lane past its first probe, and a
 // per-lane loop with several exits costs ~40 scalar mask instructions per iteration.
-template <int SLOTS>
+template <int SLOTS, bool DET = false>
 __device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
-                                  unsigned int add, unsigned long long eC, unsigned long long eT) {
+                                  unsigned int add, unsigned long long eC, unsigned long long eT,
+                                  unsigned int id = 0) {
     unsigned int slot = slot0 & (SLOTS - 1);
     unsigned long long cur = tab[slot].key;
     bool miss = cur != c;
@@ -708,6 +715,7 @@ __device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned lon
         }
     }
     LSlot &sl = tab[slot];
+    if (DET) sl.pad = id;  // distinct keys: one writer per slot
     atomicAdd(&sl.count, add);
     const ulonglong2 ev = *reinterpret_cast<const ulonglong2 *>(&sl.fC);
     if (eC < ev.x) atomicMin(&sl.fC, eC);
@@ -716,7 +724,7 @@ __device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned lon
 
 // solid filter (count > limit, build:37-39) + compaction of bucket b's table into the dense
 // arrays (wave ballot, one global atomic per block) + the bucket's lookup sub-table
-template <int SLOTS>
+template <int SLOTS, bool DET = false>
 __device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_over, unsigned int b, long long limit,
                                         unsigned long long *dkey, unsigned int *dcnt, unsigned long long *dfc,
                                         unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
@@ -730,6 +738,27 @@ __device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int PER = SLOTS / BUCKET_THREADS;
+    if (DET) {  // dense ids given by the records (LSlot.pad): every present key is solid
+        SubSlot *region = sub + (uint64_t)b * SLOTS;
+        for (int q = 0; q < PER; q++) {
+            const int i = threadIdx.x * PER + q;
+            const LSlot &sl = tab[i];
+            SubSlot o;
+            o.key = sl.key;
+            o.id = NONE32;
+            o.pad = 0;
+            if (sl.key != EMPTY_KEY) {
+                const unsigned int u = sl.pad;
+                dkey[u] = sl.key;
+                dcnt[u] = sl.count;
+                dfc[u] = sl.fC;
+                dft[u] = sl.fT;
+                o.id = u;
+            }
+            region[i] = o;
+        }
+        return;
+    }
     bool solid[PER];
     unsigned int mine = 0, present = 0;
     for (int q = 0; q < PER; q++) {
@@ -807,16 +836,18 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
             unsigned long long c, eC, eT;
             unsigned int add;
             src.decode(raw[u], c, add, eC, eT);
-            lds_insert<SLOTS>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT);
+            lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, src.id(raw[u]));
         }
     }
     for (; i < r1; i += blockDim.x) {
         unsigned long long c, eC, eT;
         unsigned int add;
-        src.decode(src.fetch(i), c, add, eC, eT);
-        lds_insert<SLOTS>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT);
+        const typename Src::Raw r = src.fetch(i);
+        src.decode(r, c, add, eC, eT);
+        lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, src.id(r));
     }
-    lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
+    lds_table_finish<SLOTS, Src::kDet>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
+                                       overflow);
 }
 
 }  // namespace ec

@@ -159,6 +159,72 @@ __global__ void __launch_bounds__(256) k_succ(const uint8_t *upal, const uint8_t
     }
 }
 
+// partitioned links (multi-GPU): the successors of the oriented nodes of canonical ids
+// [lo, hi) without the other ranks' out-degrees: the candidate's in-degree |bw(y) in d| =
+// |fw(twin y) in d| is probed here (4 more probes) instead of read from a global outdeg
+// array (same rule as k_neighbors + k_succ, get_contig_forward:63-73).
+template <typename Ops, typename Index>
+__global__ void __launch_bounds__(256) k_links_part(Index idx, const typename Ops::K *dkey, unsigned int lo,
+                                                    unsigned int hi, int k, unsigned int *succ_out) {
+    using K = typename Ops::K;
+    const K mask = Ops::mask(k);
+    const uint64_t n = 2ull * (hi - lo);
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = 2 * lo + (unsigned int)t;
+        const K c = dkey[x >> 1];
+        const K tc = Ops::twin(c, k);
+        const bool pal = tc == c;
+        unsigned int s = NONE32;
+        if (!((x & 1) && pal)) {
+            const K xs = (x & 1) ? tc : c;
+            unsigned int nfw = 0, cd = NONE32;
+            const typename Index::Nb nb = idx.nb_begin(xs);
+            for (uint32_t b = 0; b < 4; b++) {
+                const K y = Ops::push(xs, b, mask);
+                const K ty = Ops::twin(y, k);
+                const K cy = y < ty ? y : ty;
+                const unsigned int u = idx.find_nb(nb, y, cy);
+                if (u != NONE32) {
+                    if (nfw == 0) cd = 2 * u + (y != cy ? 1u : 0u);
+                    nfw++;
+                }
+            }
+            const unsigned int tx = pal ? x : (x ^ 1u);
+            if (nfw == 1 && cd != tx) {
+                const K yc = dkey[cd >> 1];
+                const K yt = Ops::twin(yc, k);
+                const unsigned int tyn = yt == yc ? cd : (cd ^ 1u);  // twin node of the candidate
+                const K tys = (tyn & 1) ? yt : yc;
+                unsigned int nin = 0;
+                const typename Index::Nb nb2 = idx.nb_begin(tys);
+                for (uint32_t b = 0; b < 4; b++) {
+                    const K z = Ops::push(tys, b, mask);
+                    const K tz = Ops::twin(z, k);
+                    const K cz = z < tz ? z : tz;
+                    nin += idx.find_nb(nb2, z, cz) != NONE32;
+                }
+                if (nin == 1) s = cd;
+            }
+        }
+        succ_out[t] = s;
+    }
+}
+
+// palindrome flags (and count) of every canonical node, when the links come from outside
+template <typename Ops>
+__global__ void __launch_bounds__(256) k_upal(const typename Ops::K *dkey, unsigned int U, int k, uint8_t *upal,
+                                              unsigned int *npal) {
+    unsigned int np = 0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < U; t += (uint64_t)gridDim.x * blockDim.x) {
+        const typename Ops::K c = dkey[t];
+        const bool pal = Ops::twin(c, k) == c;
+        upal[t] = pal ? 1 : 0;
+        np += pal;
+    }
+    for (int o = 32; o > 0; o >>= 1) np += __shfl_down(np, o);
+    if ((threadIdx.x & 63) == 0 && np) atomicAdd(npal, np);
+}
+
 __device__ inline unsigned long long first_event(const unsigned long long *dfc, const unsigned long long *dft,
                                                  unsigned int x) {
     return (x & 1) ? dft[x >> 1] : dfc[x >> 1];

@@ -162,7 +162,9 @@ struct AggSource {
     const Agg *in;
     const unsigned int *perm;
     using Raw = Agg;
+    static constexpr bool kDet = false;
     __device__ inline Raw fetch(uint64_t i) const { return in[perm[i]]; }
+    __device__ inline unsigned int id(const Raw &) const { return 0; }
     __device__ inline void decode(const Agg &a, unsigned long long &key, unsigned int &add, unsigned long long &eC,
                                   unsigned long long &eT) const {
         key = a.key;
@@ -172,5 +174,69 @@ struct AggSource {
     }
 };
 
+
+
+// ---- partitioned graph phase (k <= 32): every rank loads the all-gathered solid set with the
+// SAME dense ids (position among the non-filler records, i.e. owner-major), computes the links
+// of its own owner segment only, and the successor arrays are all-gathered.
+struct AggDet {
+    Agg a;
+    unsigned int id;
+};
+struct AggDetSource {
+    const Agg *in;
+    const unsigned int *perm;
+    const unsigned int *ids;  // dense id of each record (NONE for fillers, which sort past the end)
+    using Raw = AggDet;
+    static constexpr bool kDet = true;
+    __device__ inline Raw fetch(uint64_t i) const {
+        const unsigned int j = perm[i];
+        AggDet r;
+        r.a = in[j];
+        r.id = ids[j];
+        return r;
+    }
+    __device__ inline unsigned int id(const Raw &r) const { return r.id; }
+    __device__ inline void decode(const AggDet &r, unsigned long long &key, unsigned int &add, unsigned long long &eC,
+                                  unsigned long long &eT) const {
+        key = r.a.key;
+        add = r.a.count;
+        eC = r.a.fC;
+        eT = r.a.fT;
+    }
+};
+
+constexpr unsigned int DET_CHUNK = 8192;
+__global__ void __launch_bounds__(256) k_det_count(const Agg *in, uint64_t n, unsigned int *bc) {
+    const uint64_t c0 = (uint64_t)blockIdx.x * DET_CHUNK;
+    const uint64_t c1 = c0 + DET_CHUNK < n ? c0 + DET_CHUNK : n;
+    unsigned int v = 0;
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) v += in[i].key != EMPTY_KEY;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    __shared__ unsigned int ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) bc[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+// bs = inclusive scan of the chunk counts; ids[i] = rank of record i among the non-fillers
+__global__ void __launch_bounds__(256) k_det_ids(const Agg *in, uint64_t n, const unsigned int *bs, unsigned int *ids) {
+    __shared__ unsigned int wsum[4];
+    const uint64_t c0 = (uint64_t)blockIdx.x * DET_CHUNK;
+    const uint64_t c1 = c0 + DET_CHUNK < n ? c0 + DET_CHUNK : n;
+    unsigned int base = blockIdx.x ? bs[blockIdx.x - 1] : 0u;
+    const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint64_t i0 = c0; i0 < c1; i0 += blockDim.x) {
+        const uint64_t i = i0 + threadIdx.x;
+        const bool valid = i < c1 && in[i].key != EMPTY_KEY;
+        const unsigned long long m = __ballot(valid);
+        if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
+        __syncthreads();
+        unsigned int off = base;
+        for (unsigned int q = 0; q < wid; q++) off += wsum[q];
+        if (i < c1) ids[i] = valid ? off + (unsigned int)__popcll(m & ((1ull << lane) - 1)) : NONE32;
+        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+}
 
 }  // namespace ec

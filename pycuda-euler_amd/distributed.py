@@ -47,6 +47,9 @@ eulerhip.register("ec_merge_owned", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, c
 eulerhip.register("ec_export_dense", ctypes.c_int, [_P, _P])
 eulerhip.register("ec_assemble_from_solid", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_uint])
 eulerhip.register("ec_record_bytes", ctypes.c_int, [ctypes.c_int])
+eulerhip.register("ec_graph_load", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_uint])
+eulerhip.register("ec_graph_links_part", ctypes.c_int, [_P, _U64, _U64, _P])
+eulerhip.register("ec_graph_finish", ctypes.c_int, [_P, _P, ctypes.c_uint])
 
 
 def shard_range(nreads, rank, world):
@@ -112,6 +115,21 @@ class HipEngine:
         eulerhip.check(self.L.ec_assemble_from_solid(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), flags))
         return self.sess.fetch(k)
 
+    # partitioned graph phase (k <= 32): ec_graph_load / ec_graph_links_part / ec_graph_finish
+    def graph_load(self, recs, k, flags=0):
+        self.k = int(k)
+        n = recs.numel() // self.rec_bytes()
+        eulerhip.check(self.L.ec_graph_load(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), flags))
+        return int(self.L.ec_dense_count(self._h()))
+
+    def graph_links_part(self, lo, hi, out):
+        """successors (uint32) of the oriented nodes of canonical ids [lo, hi) into `out`"""
+        eulerhip.check(self.L.ec_graph_links_part(self._h(), int(lo), int(hi), ctypes.c_void_p(out.data_ptr())))
+
+    def graph_finish(self, succ, k, flags=0):
+        eulerhip.check(self.L.ec_graph_finish(self._h(), ctypes.c_void_p(succ.data_ptr()), flags))
+        return self.sess.fetch(k)
+
     def stats(self):
         return self.sess.stats()
 
@@ -146,22 +164,23 @@ class TorchComm:
                                    input_split_sizes=list(counts_bytes), group=self.group)
         return recv[: sum(rcl)], total_tag
 
-    def allgatherv(self, t, fill=0):
+    def allgatherv(self, t, fill=0, with_sizes=False):
         """Concatenation of every rank's `t` in rank order, each part padded with `fill` bytes
         to the largest part (no compaction copy: the record consumers skip all-0xFF filler
-        records, ec_assemble_from_solid)."""
+        records, ec_assemble_from_solid).  with_sizes: also return every rank's byte count."""
         torch, dist = self.torch, self.dist
         if self.world == 1:
-            return t
+            return (t, [t.numel()]) if with_sizes else t
         n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
         sizes = torch.empty(self.world, dtype=torch.int64, device=t.device)
         dist.all_gather_into_tensor(sizes, n, group=self.group)
-        mx = max(int(sizes.max().item()), 1)
+        szl = [int(x) for x in sizes.tolist()]
+        mx = max(max(szl), 1)
         pad = torch.full((mx,), fill, dtype=torch.uint8, device=t.device)
         pad[: t.numel()] = t
         out = torch.empty(self.world * mx, dtype=torch.uint8, device=t.device)
         dist.all_gather_into_tensor(out, pad, group=self.group)
-        return out
+        return (out, szl) if with_sizes else out
 
     def allreduce_sum(self, v):
         dev = "cuda" if self.dist.get_backend(self.group) == "nccl" else "cpu"
@@ -175,34 +194,60 @@ class TorchComm:
 
 # ---- the orchestration -----------------------------------------------------------------------
 def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None,
-                     phase_ms=None):
+                     phase_ms=None, partitioned=None):
     """Run steps 1-4 for this rank; returns (result, n_positions_total).  on_count(stats)
     receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING); phase_ms, a
-    dict, receives the wall time of every step (device-synchronised by the engine calls)."""
+    dict, receives the wall time of every step (device-synchronised by the engine calls).
+    partitioned (default: k <= 32): each rank computes the successor links of its own owner
+    segment of the gathered solid set only ("each GPU builds its local graph partition");
+    the parts are all-gathered and every rank ranks the paths and emits the contigs."""
     import time
 
-    t = [time.perf_counter()]
+    if partitioned is None:
+        partitioned = k <= 32 and hasattr(engine, "graph_load") and not (flags & eulerhip.EC_FLAG_GENERAL)
+    marks = [("start", time.perf_counter())]
 
-    def tick():
-        t.append(time.perf_counter())
+    def tick(name):
+        marks.append((name, time.perf_counter()))
 
     st = engine.count_shard(d_reads, d_off, nreads, read_base, k, flags)
-    tick()
+    tick("count")
     if on_count:
         on_count(st)
     recs, counts = engine.export_by_owner(comm.world)
-    tick()
+    tick("export")
     # the job's k-mer positions ride along with the exchange's byte counts
     received, P = comm.alltoallv(recs, [c * rec_bytes(k) for c in counts], tag=st.n_positions)
-    tick()
+    tick("alltoall")
     solid = engine.merge_owned(received, k, limit, flags)
-    tick()
-    everything = comm.allgatherv(solid, fill=0xFF)  # filler records: all-ones keys, skipped
-    tick()
-    res = engine.assemble_from_solid(everything, k, flags)
-    tick()
+    tick("merge")
+    if not partitioned:
+        everything = comm.allgatherv(solid, fill=0xFF)  # filler records: all-ones keys, skipped
+        tick("allgather")
+        res = engine.assemble_from_solid(everything, k, flags)
+        tick("graph")
+    else:
+        everything, sizes = comm.allgatherv(solid, fill=0xFF, with_sizes=True)
+        tick("allgather")
+        nrec = [sz // rec_bytes(k) for sz in sizes]
+        lo = sum(nrec[: comm.rank])
+        hi = lo + nrec[comm.rank]
+        engine.graph_load(everything, k, flags)
+        tick("load")
+        part = engine.empty(8 * (hi - lo))
+        engine.graph_links_part(lo, hi, part)
+        tick("links")
+        gathered, psz = comm.allgatherv(part[: 8 * (hi - lo)], fill=0xFF, with_sizes=True)
+        if comm.world > 1:  # drop the padding: node order = rank order
+            mx = max(max(psz), 1)
+            succ = comm.torch.cat([gathered[r * mx: r * mx + psz[r]] for r in range(comm.world)])
+        else:
+            succ = gathered
+        tick("gather_links")
+        res = engine.graph_finish(succ, k, flags)
+        tick("graph")
     if phase_ms is not None:
-        for name, a, b in zip(("count", "export", "alltoall", "merge", "allgather", "graph"), t, t[1:]):
+        for (_, a), (name, b) in zip(marks, marks[1:]):
             phase_ms[name] = phase_ms.get(name, 0.0) + (b - a) * 1e3
     return res, P
 
@@ -243,7 +288,7 @@ class ShardedAssembler:
         return self.count_stats
 
 
-def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0):
+def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None):
     """Simulate the distributed algorithm with len(engines) ranks on the local device(s):
     same engine calls, the collectives done by concatenation.  Returns rank 0's result."""
     import torch
@@ -276,5 +321,22 @@ def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0):
     allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device=engines[0].device)
     for i, x in enumerate(solids):
         allsolid[i * mx: i * mx + x.numel()] = x.to(engines[0].device)
-    res = engines[0].assemble_from_solid(allsolid, k, flags)
+    if partitioned is None:
+        partitioned = k <= 32 and not (flags & eulerhip.EC_FLAG_GENERAL)
+    if not partitioned:
+        res = engines[0].assemble_from_solid(allsolid, k, flags)
+        return res, P
+    # partitioned graph phase: every simulated rank loads the gathered set and computes the
+    # links of its own segment; the parts are concatenated in rank order
+    rb = rec_bytes(k)
+    nrec = [x.numel() // rb for x in solids]
+    parts = []
+    for r, eng in enumerate(engines):
+        lo = sum(nrec[:r])
+        eng.graph_load(allsolid.to(eng.device), k, flags)
+        part = eng.empty(8 * nrec[r])
+        eng.graph_links_part(lo, lo + nrec[r], part)
+        parts.append(part[: 8 * nrec[r]].to(engines[0].device))
+    succ = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=engines[0].device)
+    res = engines[0].graph_finish(succ if succ.numel() else engines[0].empty(4), k, flags)
     return res, P

@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libeulerhip.so")
+LIB_PATH = os.environ.get("EULERHIP_LIB") or os.path.join(HERE, "libeulerhip.so")  # override: experiments
 
 EC_OK = 0
 EC_ERR_ARG = -1
@@ -178,11 +178,14 @@ class Result:
 
     @property
     def contig_bytes(self):
+        """all contig characters concatenated (bytes; converted once, on first use)"""
+        if not isinstance(self._chars, bytes):
+            self._chars = self._chars.tobytes()
         return self._chars
 
     @property
     def contigs(self):
-        ch = self._chars.decode("ascii")
+        ch = self.contig_bytes.decode("ascii")
         o = self.contig_offsets
         return [ch[int(o[i]):int(o[i + 1])] for i in range(len(o) - 1)]
 
@@ -261,9 +264,9 @@ class Session:
         st = self.stats()
         L = lib()
         nc, nch, nl = st.n_contigs, st.n_contig_chars, st.n_links
-        chars = ctypes.create_string_buffer(max(nch, 1))
-        coff = np.zeros(nc + 1, dtype=np.uint64)
-        check(L.ec_copy_contigs(self._h, chars, coff.ctypes.data))
+        chars = np.empty(max(nch, 1), dtype=np.uint8)  # one copy out of the pinned result buffer
+        coff = np.empty(nc + 1, dtype=np.uint64)
+        check(L.ec_copy_contigs(self._h, chars.ctypes.data, coff.ctypes.data))
         loff = np.zeros(2 * nc + 1, dtype=np.uint64)
         links = np.zeros(max(nl, 1), dtype=np.int64)
         check(L.ec_copy_links(self._h, loff.ctypes.data, links.ctypes.data))
@@ -275,7 +278,7 @@ class Session:
             check(L.ec_copy_dict(self._h, km, cnt.ctypes.data))
             s = km.raw[: nd * k].decode("ascii")
             items = [(s[i * k:(i + 1) * k], int(cnt[i])) for i in range(nd)]
-        return Result(k, st, chars.raw[:nch], coff, loff, links[:nl], items)
+        return Result(k, st, chars[:nch], coff, loff, links[:nl], items)
 
     def assemble(self, reads, k, limit=1, want_dict=False, timing=False, general=False, wide_records=False,
                  window_records=False, superkmer=False):

@@ -103,3 +103,58 @@ class FakeEngine:
             first[twin(c)] = int(r["first_twin"]) if twin(c) != c else int(r["first_canon"])
         d, contigs, links = model_graph(cnt, first, k)
         return _Result(d, contigs, links)
+
+    # ---- partitioned graph phase (distributed.sharded_assemble, k <= 32) ----------------------
+    # restates k_links_part on the oriented nodes 2u+o of the gathered order (ec_graph_load ids)
+    def empty(self, nbytes):
+        return torch.zeros(max(int(nbytes), 1), dtype=torch.uint8)
+
+    def graph_load(self, recs, k, flags=0):
+        self.grecs = np.array([r for r in self._recs(recs) if int(r["key"]) != M64], dtype=REC_DTYPE)
+        self.gid = {int(x): i for i, x in enumerate(self.grecs["key"])}
+        self.gk = k
+        return len(self.grecs)
+
+    def _tw(self, x):
+        return encode(twin(decode(x, self.gk)))
+
+    def _node_code(self, x):
+        c = int(self.grecs["key"][x >> 1])
+        return self._tw(c) if x & 1 else c
+
+    def _fw_present(self, xs):
+        mask = (1 << (2 * self.gk)) - 1
+        out = []
+        for b in range(4):
+            y = ((xs << 2) | b) & mask
+            ty = self._tw(y)
+            cy = min(y, ty)
+            if cy in self.gid:
+                out.append(2 * self.gid[cy] + (1 if y != cy else 0))
+        return out
+
+    def _succ_of(self, x):
+        c = int(self.grecs["key"][x >> 1])
+        pal = self._tw(c) == c
+        if (x & 1) and pal:
+            return 0xFFFFFFFF
+        fw = self._fw_present(self._node_code(x))
+        tx = x if pal else x ^ 1
+        if len(fw) != 1 or fw[0] == tx:
+            return 0xFFFFFFFF
+        y = fw[0]
+        yc = int(self.grecs["key"][y >> 1])
+        tyn = y if self._tw(yc) == yc else y ^ 1
+        return y if len(self._fw_present(self._node_code(tyn))) == 1 else 0xFFFFFFFF
+
+    def graph_links_part(self, lo, hi, out):
+        part = np.array([self._succ_of(x) for x in range(2 * lo, 2 * hi)], dtype=np.uint32)
+        if part.size:
+            out[: part.nbytes] = torch.from_numpy(part.view(np.uint8).copy())
+
+    def graph_finish(self, succ, k, flags=0):
+        got = np.frombuffer(succ.numpy().tobytes(), dtype=np.uint32)[: 2 * len(self.grecs)]
+        want = np.array([self._succ_of(x) for x in range(2 * len(self.grecs))], dtype=np.uint32)
+        assert np.array_equal(got, want), "gathered successor parts differ from the whole-set links"
+        return self.assemble_from_solid(self._bytes(self.grecs), k, flags)
+

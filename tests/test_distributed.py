@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, reads, k, limit, q):
+def _worker(rank, world, port, reads, k, limit, q, partitioned=None):
     import torch
     import torch.distributed as dist
 
@@ -44,17 +44,19 @@ def _worker(rank, world, port, reads, k, limit, q):
         off[1:] = np.cumsum([len(r) for r in mine])
         res, P = distributed.sharded_assemble(FakeEngine(k), distributed.TorchComm(),
                                               torch.frombuffer(bytearray(buf or b"\0"), dtype=torch.uint8),
-                                              torch.from_numpy(off), len(mine), lo, k, limit)
+                                              torch.from_numpy(off), len(mine), lo, k, limit,
+                                              partitioned=partitioned)
         q.put((rank, P, res.contigs, res.links))
     finally:
         dist.destroy_process_group()
 
 
-def _run(reads, k, limit, world):
+def _run(reads, k, limit, world, partitioned=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q, partitioned))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in range(world)]
@@ -64,10 +66,13 @@ def _run(reads, k, limit, world):
     return sorted(out)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_matches_reference_g200(world):
+# partitioned: each rank computes the links of its own owner segment (ec_graph_links_part's
+# rule restated in fake_engine) and the parts are all-gathered; replicated: one rank-local
+# graph phase on the gathered set (ec_assemble_from_solid)
+@pytest.mark.parametrize("world,partitioned", [(2, True), (3, True), (2, False)])
+def test_sharded_matches_reference_g200(world, partitioned):
     (case,) = [c for c in golden_cases("g200.json") if c["k"] == 15]
-    for rank, P, contigs, links in _run(case["reads"], 15, 1, world):
+    for rank, P, contigs, links in _run(case["reads"], 15, 1, world, partitioned):
         assert contigs == case["contigs"] and links == case["links"]
 
 

@@ -110,3 +110,49 @@ def test_rccl_world1_sharded(engines):
         assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("seed,g,n,L,err,k", [(5, 50_000, 20_000, 100, 0.003, 31), (6, 4_000, 3_000, 60, 0.01, 20),
+                                              (7, 2_000, 800, 40, 0.0, 32)])
+def test_partitioned_links_equal_replicated(engines, world, seed, g, n, L, err, k):
+    """ec_graph_load / ec_graph_links_part / ec_graph_finish (each simulated rank computes the
+    links of its own owner segment, parts concatenated) == ec_assemble_from_solid == oracle"""
+    import distributed
+
+    buf, off = make_reads(g, n, L, 7300 + seed, err=err, n_rate=0.001, circular=(seed == 7))
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    for partitioned in (True, False):
+        res, P = distributed.local_sharded_assemble(engines[:world], buf, off, k, 1, partitioned=partitioned)
+        assert P == ref["n_positions"]
+        assert res.contig_bytes == ref["contig_chars"], partitioned
+        assert res.links == oracle.unpack_links(ref), partitioned
+        assert res.stats.n_dict == ref["n_dict"], partitioned
+
+
+def test_partitioned_links_part_ranges(engines):
+    """the per-rank successor parts are independent of how the canonical ids are split"""
+    import torch
+
+    import distributed
+
+    buf, off = make_reads(30_000, 10_000, 100, 7401, err=0.002)
+    eng = engines[0]
+    d_reads = torch.from_numpy(buf).cuda()
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    eng.count_shard(d_reads, d_off, len(off) - 1, 0, 31, 0)
+    recs, counts = eng.export_by_owner(1)
+    solid = eng.merge_owned(recs, 31, 1, 0)
+    U = eng.graph_load(solid, 31)
+    whole = eng.empty(8 * U)
+    eng.graph_links_part(0, U, whole)
+    cuts = [0, 1, U // 3, U // 2 + 7, U - 1, U]
+    parts = []
+    for a, b in zip(cuts, cuts[1:]):
+        p = eng.empty(8 * (b - a))
+        eng.graph_links_part(a, b, p)
+        parts.append(p[: 8 * (b - a)])
+    assert torch.equal(torch.cat(parts), whole[: 8 * U])
+    ref = oracle.assemble_packed(buf, off, 31, 1)
+    res = eng.graph_finish(whole[: 8 * U], 31)
+    assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)

@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/g21; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_distributed_gpu.py tests/test_cli_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 300 python bench.py --sharded --no-cpu-baseline > $O/bench_sh.json 2> $O/bench_sh.err && python -c "import json;d=json.load(open('$O/bench_sh.json'));print(d['ms_per_step'], d['sharded_phase_ms'])"

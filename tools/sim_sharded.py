@@ -65,18 +65,30 @@ def main():
         allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device="cuda")
         for i, x in enumerate(solids):
             allsolid[i * mx: i * mx + x.numel()] = x
-        t0 = time.perf_counter()
+        nrec = [x.numel() // rb for x in solids]
+        parts = []
+        for r, eng in enumerate(engines):
+            lo = sum(nrec[:r])
+            t0 = time.perf_counter()
+            eng.graph_load(allsolid, 31)
+            tick("load", t0)
+            t0 = time.perf_counter()
+            part = eng.empty(8 * nrec[r])
+            eng.graph_links_part(lo, lo + nrec[r], part)
+            tick("links", t0)
+            parts.append(part[: 8 * nrec[r]])
+        succ = torch.cat(parts)
         eng = engines[0]
+        t0 = time.perf_counter()
         import ctypes
         import eulerhip
-        eulerhip.check(eng.L.ec_assemble_from_solid(eng._h(), ctypes.c_void_p(allsolid.data_ptr()),
-                                                    allsolid.numel() // rb, 31, eulerhip.EC_FLAG_TIMING))
-        tick("graph_core", t0)
+        eulerhip.check(eng.L.ec_graph_finish(eng._h(), ctypes.c_void_p(succ.data_ptr()), eulerhip.EC_FLAG_TIMING))
+        tick("finish", t0)
         t0 = time.perf_counter()
         res = eng.sess.fetch(31)
         tick("fetch", t0)
         st = eng.stats()
-        print("graph stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
+        print("finish stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
         print("export per rank:", [round(x, 2) for x in t["export"]], "count per rank:", [round(x, 2) for x in t["count"]])
         print("rep %d  ranks %d  per-rank max ms: %s  exchanged bytes/rank ~%.0f MB, gathered %.0f MB" % (
             rep, world, {k: round(max(v), 2) for k, v in t.items()},
