@@ -124,6 +124,7 @@ struct ec_session {
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
     unsigned flags = 0;        // flags of the current call
     DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur;
+    bool no_index = false;      // the call needs dense records only (shard count, owner merge)
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load)
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
 };
@@ -292,12 +293,12 @@ int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long
     if (slots == 2048)
         k_bucket<Src, 2048><<<nb, BUCKET_THREADS, 0, st>>>(
             src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
-            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid,
+            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
             &dsc->ndistinct, &dsc->overflow);
     else
         k_bucket<Src, 4096><<<nb, BUCKET_THREADS, 0, st>>>(
             src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
-            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->sub.as<SubSlot>(), &dsc->nsolid,
+            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
             &dsc->ndistinct, &dsc->overflow);
     return EC_OK;
 }
@@ -1282,13 +1283,17 @@ int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offs
     }
     EC_CHECK(begin_call(s, k, flags));
     unsigned int U = 0;
+    s->no_index = true;
+    int rc = EC_OK;
     if (k > 32) {
         SolidIndexW sidx{};
-        EC_CHECK(phase_count_w(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, U, sidx));
+        rc = phase_count_w(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, U, sidx);
     } else {
         SolidIndex sidx{};
-        EC_CHECK(phase_count(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, flags, U, sidx));
+        rc = phase_count(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, flags, U, sidx);
     }
+    s->no_index = false;
+    EC_CHECK(rc);
     s->n_dense = U;
     collect_timing(s);
     s->stats_ok = true;
@@ -1343,13 +1348,17 @@ int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int 
     }
     EC_CHECK(begin_call(s, k, flags));
     unsigned int U = 0;
+    s->no_index = true;
+    int rc = EC_OK;
     if (k > 32) {
         SolidIndexW sidx{};
-        EC_CHECK(phase_merge_w(s, reinterpret_cast<const AggW *>(d_records), n, (long long)limit, U, sidx));
+        rc = phase_merge_w(s, reinterpret_cast<const AggW *>(d_records), n, (long long)limit, U, sidx);
     } else {
         SolidIndex sidx{};
-        EC_CHECK(phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx));
+        rc = phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx);
     }
+    s->no_index = false;
+    EC_CHECK(rc);
     s->n_dense = U;
     collect_timing(s);
     s->stats_ok = true;

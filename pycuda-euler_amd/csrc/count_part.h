@@ -807,7 +807,7 @@ __device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_
             o.id = u;
             u++;
         }
-        region[i] = o;
+        if (sub) region[i] = o;  // no lookup index wanted (shard counts, owner merges): skip the dump
     }
 }
 
