@@ -43,6 +43,10 @@ CONFIGS = {
     # the same read length / k at a tenth of the size (20 Mbp genome, same 75x coverage)
     "genome20m_k51": dict(genome=20_000_000, reads=10_000_000, read_len=150, k=51, seed=20261015 + 5,
                           name="synthetic-20Mbp-10Mx150bp-k51"),
+    # the metric's workload with 0.5 % substitution errors (SURVEY §8d optional variant: most
+    # erroneous k-mers occur once and fail the count > 1 solid filter)
+    "ecoli10m_err": dict(genome=4_600_000, reads=10_000_000, read_len=100, k=31, seed=20261015 + 4, err=0.005,
+                         name="ecoli-4.6Mbp-10Mx100bp-k31-err0.5pct"),
     "tiny": dict(genome=50_000, reads=50_000, read_len=100, k=31, seed=7, name="tiny-50kbp-50kx100bp-k31"),
 }
 
@@ -153,7 +157,7 @@ def main():
     t0 = time.time()
     from synth import make_reads
 
-    buf, off = make_reads(cfg["genome"], cfg["reads"], cfg["read_len"], cfg["seed"])
+    buf, off = make_reads(cfg["genome"], cfg["reads"], cfg["read_len"], cfg["seed"], err=cfg.get("err", 0.0))
     log("rank %d: generated %d reads in %.1f s" % (rank, cfg["reads"], time.time() - t0))
     k = cfg["k"]
 
@@ -241,7 +245,8 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u64" if k <= 32 else "u128",
-        "data": "synthetic (iid ACGT genome, uniform error-free 100 bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)" % cfg["seed"],
+        "data": "synthetic (iid ACGT genome, uniform %s %d bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)"
+                % ("error-free" if not cfg.get("err") else "%.1f%%-substitution" % (100 * cfg["err"]), L, cfg["seed"]),
         "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
                    "positions": P, "solid_kmers": U,
                    "contigs": int(st.n_contigs if not use_dist else runner.engine.stats().n_contigs),

@@ -125,6 +125,7 @@ struct ec_session {
     unsigned flags = 0;        // flags of the current call
     DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur;
     bool no_index = false;      // the call needs dense records only (shard count, owner merge)
+    bool filt = false;          // phase_count: k_bucket_filt (more distinct keys than LDS tables hold)
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load)
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
 };
@@ -290,6 +291,13 @@ template <typename Src>
 int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long limit) {
     Scalars *dsc = s->scal.as<Scalars>();
     hipStream_t st = s->stream;
+    if (s->filt) {  // error-rich input: seen-twice filter + two half tables per bucket
+        k_bucket_filt<Src><<<nb, BUCKET_THREADS, 0, st>>>(
+            src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(),
+            &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+        return EC_OK;
+    }
     if (slots == 2048)
         k_bucket<Src, 2048><<<nb, BUCKET_THREADS, 0, st>>>(
             src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
@@ -384,15 +392,19 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
 
     // ---- count + compact ------------------------------------------------------------------
     // partitioned path when every bucket fits an LDS table and local events fit 16 bits
+    // error-rich inputs (distinct keys >> solid keys) use the seen-twice filter buckets when a
+    // key seen once cannot be solid by count alone (limit >= 1), up to ~32 K distinct per bucket
+    const bool filt_ok = !sk && limit >= 1 && !getenv("EULERHIP_NO_FILTER");
     bool part = !(flags & EC_FLAG_GENERAL) && nreads && P && hsc.maxlocal <= MAX_LOCAL_EVENT && !hsc.skew &&
-                est / FINE <= 2400.0;
+                (est / FINE <= 2400.0 || (filt_ok && est / FINE <= 32768.0));
+    const bool filt = part && filt_ok && (est / FINE > 2400.0 || getenv("EULERHIP_FORCE_FILTER"));
     int bbits = 0;
     unsigned int slots = 2048;
     sidx = SolidIndex{};
     uint64_t umax = 0;
     if (part) {
         while (bbits < FINE_BITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
-        slots = est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
+        slots = (filt || est / (double)(1ull << bbits) > 1100.0) ? 4096u : 2048u;  // filter mode: 2 x 2048
         int maxc = MAX_COARSE_BITS;
         if (const char *e = getenv("EULERHIP_COARSE_BITS")) maxc = std::max(1, std::min(MAX_COARSE_BITS, atoi(e)));
         maxc = std::min(maxc, DS_MAX_CBITS);
@@ -484,6 +496,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->dft.ensure(umax * 8));
         EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
         kmark(s, 2, 0);
+        s->filt = filt;
         if (sk) {
             const SkRec *sr = second ? s->recs2.as<SkRec>() : s->recs.as<SkRec>();
             if (slots == 2048)
@@ -522,6 +535,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             EC_CHECK(launch_bucket(s, RecSource{second ? s->recs2.as<Rec>() : s->recs.as<Rec>()}, (unsigned)Bk, slots,
                                    (long long)limit));
         }
+        s->filt = false;
         kmark(s, 2, 1);
         mark(s, 2 * EC_STAGE_COMPACT + 1);
         EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -537,6 +551,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             sidx.bbits = bbits;
             sidx.slots = slots;
             sidx.sk = sk ? 1 : 0;
+            sidx.split = filt ? 1 : 0;
             sidx.mc = mc;
             s->stats.count_path = sk ? EC_PATH_SUPERKMER : EC_PATH_PARTITIONED;
             s->stats.n_buckets = (uint32_t)Bk;
@@ -1057,23 +1072,30 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                             s->lcnt.as<unsigned int>());
     mark(s, 2 * EC_STAGE_GFA + 1);
 
-    // ---- results to host --------------------------------------------------------------------
+    // ---- results to host (links compacted on the device: only the used entries travel) -----
     EC_CHECK(s->h_chars.resize(nchars));
-    std::vector<unsigned int> lcnt(2 * (size_t)nc);
-    std::vector<long long> lk(16 * (size_t)nc);
+    const unsigned int n2 = 2 * nc;
+    s->h_loff.assign((size_t)n2 + 1, 0);
     if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), s->chars.p, nchars, hipMemcpyDeviceToHost, st));
     if (nc) {
-        EC_HIP(hipMemcpyAsync(lcnt.data(), s->lcnt.p, lcnt.size() * 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipMemcpyAsync(lk.data(), s->lk.p, lk.size() * 8, hipMemcpyDeviceToHost, st));
+        EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));   // per-side counts as u64 (starts sorted)
+        EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));  // their exclusive scan = link offsets
+        k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>());
+        EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
+        EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+    }
+    const uint64_t nlinks = s->h_loff[n2];
+    s->h_links.resize(nlinks);
+    if (nlinks) {
+        EC_CHECK(s->dcounts.ensure(nlinks * 8));
+        k_links_compact<<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
+                                                      s->skeys2.as<unsigned long long>(), n2,
+                                                      s->dcounts.as<long long>());
+        EC_HIP(hipMemcpyAsync(s->h_links.data(), s->dcounts.p, nlinks * 8, hipMemcpyDeviceToHost, st));
     }
     EC_HIP(hipStreamSynchronize(st));
-    s->h_loff.assign(2 * (size_t)nc + 1, 0);
-    s->h_links.clear();
-    for (size_t i = 0; i < 2 * (size_t)nc; i++) {
-        for (unsigned j = 0; j < lcnt[i]; j++) s->h_links.push_back(lk[i * 8 + j]);
-        s->h_loff[i + 1] = s->h_links.size();
-    }
-    s->stats.n_links = s->h_links.size();
+    s->stats.n_links = nlinks;
 
     s->stats.n_dict = 2ull * U - hsc.npal;  // len(build()): palindromes have one entry
 

@@ -850,4 +850,77 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
                                        overflow);
 }
 
+// ---- error-rich inputs: more distinct k-mers per bucket than an LDS table holds ------------
+// With sequencing errors most distinct k-mers occur once (150 M distinct for 4.6 M solid at
+// 0.5 % substitutions, 10 M x 100 bp): a bucket's distinct keys outgrow the 2048-slot table
+// although its solid keys fit.  A key occurring once is solid only if its single insert adds
+// more than `limit` (an even-k palindrome adds 2), so the workgroup first builds a
+// "seen twice" filter over the bucket's records (two 2^18-cell bitmaps: cell bit set on the
+// second sighting, two cells per key -- no false negatives, ~2 % of the singletons leak),
+// then inserts the keys that passed, in two halves of the key space (hash bit 11) with one
+// table each; half h's table becomes sub-table region 2b + h (SolidIndex::split).
+constexpr int FILT_BITS = 18;
+template <typename Src>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const unsigned long long *bstart,
+                                                               long long limit, unsigned long long *dkey,
+                                                               unsigned int *dcnt, unsigned long long *dfc,
+                                                               unsigned long long *dft, SubSlot *sub,
+                                                               unsigned int *nsolid, unsigned long long *ndistinct,
+                                                               unsigned int *overflow) {
+    constexpr int SLOTS = 2048;
+    constexpr unsigned int NW = 1u << (FILT_BITS - 5);
+    constexpr unsigned int CM = (1u << FILT_BITS) - 1;
+    __shared__ LSlot tab[SLOTS];
+    __shared__ unsigned int s_over[2];
+    __shared__ unsigned int seen1[NW], seen2[NW];
+    const unsigned int b = blockIdx.x;
+    for (unsigned int i = threadIdx.x; i < NW; i += blockDim.x) {
+        seen1[i] = 0;
+        seen2[i] = 0;
+    }
+    __syncthreads();
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    constexpr int U = 4;  // records per thread per step, loads issued before any decode
+    auto for_records = [&](auto &&fn) {
+        uint64_t i = r0 + threadIdx.x;
+        for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
+            typename Src::Raw raw[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) raw[u] = src.fetch(i + u * (uint64_t)blockDim.x);
+#pragma unroll
+            for (int u = 0; u < U; u++) fn(raw[u]);
+        }
+        for (; i < r1; i += blockDim.x) fn(src.fetch(i));
+    };
+    // pass 0: seen-twice filter
+    for_records([&](const typename Src::Raw &r) {
+        unsigned long long c, eC, eT;
+        unsigned int add;
+        src.decode(r, c, add, eC, eT);
+        const uint64_t h = mix64(c);
+        const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
+        const unsigned int m1 = 1u << (c1 & 31), m2 = 1u << (c2 & 31);
+        if (atomicOr(&seen1[c1 >> 5], m1) & m1) atomicOr(&seen2[c1 >> 5], m1);
+        if (atomicOr(&seen1[c2 >> 5], m2) & m2) atomicOr(&seen2[c2 >> 5], m2);
+    });
+    __syncthreads();
+    for (unsigned int half = 0; half < 2; half++) {
+        lds_table_init<SLOTS>(tab, s_over);
+        for_records([&](const typename Src::Raw &r) {
+            unsigned long long c, eC, eT;
+            unsigned int add;
+            src.decode(r, c, add, eC, eT);
+            const uint64_t h = mix64(c);
+            if (((unsigned int)(h >> 11) & 1u) != half) return;
+            const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
+            const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
+            if (!twice && (long long)add <= limit) return;
+            lds_insert<SLOTS>(tab, s_over, c, (unsigned int)h, add, eC, eT);
+        });
+        lds_table_finish<SLOTS>(tab, s_over, 2 * b + half, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
+                                overflow);
+        __syncthreads();
+    }
+}
+
 }  // namespace ec

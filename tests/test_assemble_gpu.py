@@ -271,3 +271,36 @@ def test_superkmer_ragged_lengths_vs_oracle(gpu_session, k):
     assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
     assert [[x, c] for x, c in res.dict_items] == ref["d"]
     assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+# ---- seen-twice filter buckets (k_bucket_filt) -----------------------------------------------
+# Taken automatically when the distinct k-mers (mostly error singletons) outgrow the LDS tables
+# (> ~2·10^7 distinct); EULERHIP_FORCE_FILTER takes it at any size so the oracle can check it.
+@pytest.mark.parametrize("fmt", ["compact", "wide_records"])
+@pytest.mark.parametrize("g,n,L,seed,err,nr,circ,k", [c for c in SYN if c[-1] <= 32])
+def test_filter_buckets_vs_oracle(gpu_session, monkeypatch, g, n, L, seed, err, nr, circ, k, fmt):
+    monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
+    buf, off = make_reads(g, n, L, 1000 + seed, err=err, n_rate=nr, circular=circ)
+    want_dict = g <= 50_000
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
+    flags = (eulerhip.EC_FLAG_WANT_DICT if want_dict else 0) | \
+        (eulerhip.EC_FLAG_WIDE_RECORDS if fmt == "wide_records" else 0)
+    gpu_session.run_host(buf, off, k, 1, flags)
+    res = gpu_session.fetch(k, want_dict)
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    if want_dict:
+        assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+def test_filter_buckets_limits_vs_oracle(gpu_session, monkeypatch):
+    """limit >= 1 only (a key seen once can be solid by count alone otherwise); even k keeps
+    palindromes, whose single insert adds 2"""
+    monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
+    for k, lim in ((15, 1), (15, 2), (16, 1), (20, 3), (31, 5)):
+        buf, off = make_reads(4_000, 3_000, 60, 500 + k + lim, err=0.01)
+        ref, rc, rl = _oracle_packed(buf, off, k, lim)
+        gpu_session.run_host(buf, off, k, lim)
+        res = gpu_session.fetch(k)
+        assert res.contig_bytes == ref["contig_chars"] and res.links == rl, (k, lim)
