@@ -90,6 +90,24 @@ struct HostBuf {
     }
 };
 
+template <typename T>
+struct PinnedVec {  // std::vector-like view of a pinned HostBuf
+    HostBuf b;
+    size_t n = 0;
+    int resize(size_t count) {
+        n = count;
+        return b.resize(count * sizeof(T));
+    }
+    T *data() const { return reinterpret_cast<T *>(b.p); }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    T &operator[](size_t i) const { return data()[i]; }
+    void release() {
+        b.release();
+        n = 0;
+    }
+};
+
 }  // namespace ec
 
 using namespace ec;
@@ -110,9 +128,9 @@ struct ec_session {
     int k = 0;
     ec_stats stats{};
     HostBuf h_chars;
-    std::vector<uint64_t> h_coff;
-    std::vector<uint64_t> h_loff;
-    std::vector<int64_t> h_links;
+    PinnedVec<uint64_t> h_coff;  // result readbacks land in pinned host memory
+    PinnedVec<uint64_t> h_loff;
+    PinnedVec<int64_t> h_links;
     bool want_dict = false;
     hipEvent_t ev[2 * EC_NSTAGES] = {};
     hipEvent_t kev[2 * EC_NKERNELS] = {};
@@ -1014,10 +1032,19 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->svals2.ensure(Nn * 4));
     EC_HIP(hipMemsetAsync(s->cidxOf.p, 0xFF, Nn * 4, st));
     if (U)
-        k_starts<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
-                                              s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
-                                              s->PM.as<unsigned long long>(), N, s->skeys.as<unsigned long long>(),
-                                              s->svals.as<unsigned int>(), &dsc->nstarts);
+    {
+        const unsigned int nblk = (unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK);
+        unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk;
+        k_starts_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
+                                           s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                           s->PM.as<unsigned long long>(), N, bc);
+        EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
+        k_starts_write<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
+                                           s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                           s->PM.as<unsigned long long>(), N, bs, s->skeys.as<unsigned long long>(),
+                                           s->svals.as<unsigned int>());
+        EC_HIP(hipMemcpyAsync(&dsc->nstarts, bs + nblk - 1, 4, hipMemcpyDeviceToDevice, st));
+    }
     EC_HIP(hipMemcpyAsync(&hsc.nstarts, &dsc->nstarts, 4, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     const unsigned int nc = hsc.nstarts;
@@ -1035,8 +1062,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                    k, s->cidxOf.as<unsigned int>(), s->clen.as<unsigned long long>());
     }
     EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
-    s->h_coff.assign(nc + 1, 0);
-    EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, (size_t)(nc + 1) * 8, hipMemcpyDeviceToHost, st));
+    // only the total is needed now; the offsets travel with the other results
+    EC_CHECK(s->h_coff.resize(nc + 1));
+    EC_HIP(hipMemcpyAsync(&s->h_coff[nc], s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     mark(s, 2 * EC_STAGE_STARTS + 1);
     const uint64_t nchars = s->h_coff[nc];
@@ -1075,8 +1103,11 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     // ---- results to host (links compacted on the device: only the used entries travel) -----
     EC_CHECK(s->h_chars.resize(nchars));
     const unsigned int n2 = 2 * nc;
-    s->h_loff.assign((size_t)n2 + 1, 0);
+    EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
+    s->h_loff[n2] = 0;
     if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), s->chars.p, nchars, hipMemcpyDeviceToHost, st));
+    if (nc) EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, (size_t)nc * 8, hipMemcpyDeviceToHost, st));
+    else s->h_coff[0] = 0;
     if (nc) {
         EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));   // per-side counts as u64 (starts sorted)
         EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));  // their exclusive scan = link offsets
@@ -1086,7 +1117,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_HIP(hipStreamSynchronize(st));
     }
     const uint64_t nlinks = s->h_loff[n2];
-    s->h_links.resize(nlinks);
+    EC_CHECK(s->h_links.resize(nlinks));
     if (nlinks) {
         EC_CHECK(s->dcounts.ensure(nlinks * 8));
         k_links_compact<<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
@@ -1179,6 +1210,9 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur};
     for (auto *b : all) b->release();
     s->h_chars.release();
+    s->h_coff.release();
+    s->h_loff.release();
+    s->h_links.release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);
         for (auto &e : s->kev) hipEventDestroy(e);
