@@ -141,7 +141,7 @@ struct ec_session {
     unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
     unsigned flags = 0;        // flags of the current call
-    DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur;
+    DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur, cwalk;
     bool no_index = false;      // the call needs dense records only (shard count, owner merge)
     bool filt = false;          // phase_count: k_bucket_filt (more distinct keys than LDS tables hold)
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load)
@@ -1054,12 +1054,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                             s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nc));
     const unsigned int *sorted_nodes = s->svals2.as<unsigned int>();
     EC_CHECK(s->clen.ensure((size_t)(nc + 1) * 8));
+    EC_CHECK(s->cwalk.ensure((size_t)std::max(nc, 1u) * sizeof(Walk)));
     EC_CHECK(s->coff.ensure((size_t)(nc + 1) * 8));
     EC_HIP(hipMemsetAsync(s->clen.p, 0, (size_t)(nc + 1) * 8, st));
     if (nc) {
         k_contig_len<<<grid_for(nc, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(),
                                                    s->RK.as<unsigned int>(), s->PL.as<unsigned int>(), sorted_nodes, nc,
-                                                   k, s->cidxOf.as<unsigned int>(), s->clen.as<unsigned long long>());
+                                                   k, s->cidxOf.as<unsigned int>(), s->clen.as<unsigned long long>(),
+                                                   s->cwalk.as<Walk>());
     }
     EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
     // only the total is needed now; the offsets travel with the other results
@@ -1082,7 +1084,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (U)
         k_emit<Ops><<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
                                             s->PL.as<unsigned int>(), s->dkey.as<typename Ops::K>(),
-                                            s->cidxOf.as<unsigned int>(), sorted_nodes, s->coff.as<unsigned long long>(),
+                                            s->cidxOf.as<unsigned int>(), s->cwalk.as<Walk>(), s->coff.as<unsigned long long>(),
                                             N, k, s->chars.as<char>(), s->cfirst.as<unsigned int>(),
                                             s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
                                             s->tailOf.as<unsigned int>());
@@ -1207,7 +1209,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
                      &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
-                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur};
+                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->h_coff.release();

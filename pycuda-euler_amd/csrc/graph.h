@@ -373,7 +373,13 @@ __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const un
         seen += j + 1;
     }
     for (int o = 32; o > 0; o >>= 1) seen += __shfl_down(seen, o);
-    if ((threadIdx.x & 63) == 0 && seen) atomicAdd(nvisited, seen);
+    __shared__ unsigned long long bseen[4];  // one atomic per block, not per wave
+    if ((threadIdx.x & 63) == 0) bseen[threadIdx.x >> 6] = seen;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long v = bseen[0] + bseen[1] + bseen[2] + bseen[3];
+        if (v) atomicAdd(nvisited, v);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_rjump_init(const unsigned int *nextR, unsigned int nr, RJump *rs) {
@@ -582,12 +588,13 @@ __device__ inline Walk walk_of(const uint8_t *upal, const unsigned int *PK, cons
 __global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
                                                     const unsigned int *PL, const unsigned int *sorted_nodes,
                                                     unsigned int nc, int k, unsigned int *cidxOf,
-                                                    unsigned long long *clen) {
+                                                    unsigned long long *clen, Walk *cwalk) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int s = sorted_nodes[i];
         cidxOf[PK[s] & ~CYC] = (unsigned int)i;
         const Walk w = walk_of(upal, PK, RK, PL, s);
         clen[i] = (unsigned long long)(k - 1) + w.len;
+        cwalk[i] = w;  // k_emit reads the contig's geometry once instead of re-deriving it per node
     }
 }
 
@@ -596,7 +603,7 @@ __global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const u
 template <typename Ops>
 __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
                                               const unsigned int *PL, const typename Ops::K *dkey,
-                                              const unsigned int *cidxOf, const unsigned int *sorted_nodes,
+                                              const unsigned int *cidxOf, const Walk *cwalk,
                                               const unsigned long long *coff, unsigned int N, int k, char *chars,
                                               unsigned int *cfirst, unsigned int *clast, unsigned int *headOf,
                                               unsigned int *tailOf) {
@@ -606,8 +613,7 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
         const unsigned int pk = PK[x], rk = RK[x];
         const unsigned int ci = cidxOf[pk & ~CYC];
         if (ci == NONE32) continue;  // the twin path of a disjoint pair carries the contig
-        const unsigned int s = sorted_nodes[ci];
-        const Walk w = walk_of(upal, PK, RK, PL, s);
+        const Walk w = cwalk[ci];
         long long pos = -1;
         if (w.kind == 0) {
             pos = rk;
