@@ -31,6 +31,7 @@
 #include "count_part.h"
 #include "shard.h"
 #include "compact.h"
+#include "count_wide.h"
 
 namespace ec {
 
@@ -819,10 +820,138 @@ int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, S
     s->stats.table_capacity = cap;
     sidx.table = s->table.as<SlotW>();
     sidx.capmask = cap - 1;
+    sidx.sub = nullptr;
     if (2ull * U >= (unsigned long long)CYC) {
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
     }
+    return EC_OK;
+}
+
+// Partitioned wide count (count_wide.h): upsweep, downsweep, refine and one LDS table per
+// bucket, as phase_count for k <= 32.  ok = false (scalars reset) when the input needs the
+// HBM table: reads with 'N' or other bytes, tiles over the 40 KB stage, a bucket past its table.
+int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads,
+                      uint64_t read_base, int k, long long limit, unsigned int &U, SolidIndexW &sidx, bool &ok) {
+    ok = false;
+    if ((s->flags & EC_FLAG_GENERAL) || !nreads || getenv("EULERHIP_WIDE_GENERAL")) return EC_OK;
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    auto reset = [&]() -> int {
+        EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
+        EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
+        return EC_OK;
+    };
+    mark(s, 2 * EC_STAGE_PRESCAN);
+    const uint64_t ntiles = (nreads + TILE_READS - 1) / TILE_READS;
+    uint64_t maxg = 2048;
+    if (const char *e = getenv("EULERHIP_MAX_GROUPS")) maxg = std::max(1, atoi(e));
+    uint64_t ngroups = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, maxg));
+    const uint64_t gsize = std::max<uint64_t>(1, (ntiles + ngroups - 1) / ngroups) * TILE_READS;
+    ngroups = std::max<uint64_t>(1, (nreads + gsize - 1) / gsize);
+    constexpr int HR = 1 << HLL_REG_BITS;
+    EC_CHECK(s->hist.ensure(ngroups * FINE_W * 4));
+    EC_CHECK(s->hll.ensure(ngroups * HR));
+    EC_CHECK(s->ftot.ensure((FINE_W + HR) * 8));
+    kmark(s, 0, 0);
+    k_upsweep_w<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
+                                                         s->hll.as<uint8_t>(), &dsc->npos, &dsc->maxlocal, &dsc->skew,
+                                                         dsc->lens);
+    kmark(s, 0, 1);
+    unsigned long long *ftot = s->ftot.as<unsigned long long>();
+    EC_HIP(hipMemsetAsync(ftot, 0, (FINE_W + HR) * 8, st));
+    k_fine_totals<FINE_W_BITS><<<dim3(FINE_W / 256, TOT_SLICES), 256, 0, st>>>(
+        s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), ngroups, ftot, reinterpret_cast<unsigned int *>(ftot + FINE_W));
+    k_hll_final<<<1, 1024, 0, st>>>(reinterpret_cast<unsigned int *>(ftot + FINE_W), HLL_REG_BITS, &dsc->est);
+    mark(s, 2 * EC_STAGE_PRESCAN + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    const uint64_t P = hsc.npos;
+    const double est = hsc.est;
+    double per_max = 1500.0;  // keys per 2048-slot bucket table
+    if (const char *e = getenv("EULERHIP_WIDE_BUCKET_MAX")) per_max = atof(e);
+    if (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT || !P || est / FINE_W > per_max) return reset();
+    s->stats.n_reads = nreads;
+    s->stats.n_positions = P;
+    s->stats.n_distinct_est = (uint64_t)llround(est);
+
+    int bbits = 0;
+    int maxb = FINE_W_BITS;  // (EULERHIP_WIDE_MAX_BBITS: tests force bucket overflow)
+    if (const char *e = getenv("EULERHIP_WIDE_MAX_BBITS")) maxb = std::max(0, std::min(FINE_W_BITS, atoi(e)));
+    while (bbits < maxb && est / (double)(1ull << bbits) > 1100.0) bbits++;
+    int fan = 0;
+    while ((1 << (fan + 1)) <= REFINE_FANOUT) fan++;
+    const int cbits = std::min(bbits, std::min(DS_MAX_CBITS, std::max(1, bbits - fan)));
+    const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
+    constexpr unsigned int SLOTS = 2048;
+    mark(s, 2 * EC_STAGE_COUNT);
+    EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
+    EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
+    EC_CHECK(s->tot.ensure((Bk + 1) * 8));
+    EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
+    EC_CHECK(s->recs.ensure(P * sizeof(RecW)));
+    const bool second = bbits > cbits;
+    if (second) EC_CHECK(s->recs2.ensure(P * sizeof(RecW)));
+    s->stats.record_bytes = (uint32_t)sizeof(RecW);
+    s->stats.n_records = P;
+    k_coarse<FINE_W_BITS><<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
+                                                                        s->cnt.as<unsigned long long>());
+    EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ngroups));
+    k_bucket_totals<FINE_W_BITS><<<grid_for(Bk + 1, B), B, 0, st>>>(ftot, bbits, s->tot.as<unsigned long long>());
+    EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
+    kmark(s, 1, 0);
+    k_downsweep_w<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups, cbits,
+                                                           s->offs.as<unsigned long long>(), s->recs.as<RecW>(), read_base);
+    kmark(s, 1, 1);
+    if (second) {
+        const unsigned RS = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8, 1024 / Ck));
+        EC_CHECK(s->gcur.ensure(Bk * 8));
+        EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
+        kmark(s, 4, 0);
+        k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+            StoreW{s->recs.as<RecW>()}, StoreW{s->recs2.as<RecW>()}, s->bstart.as<unsigned long long>(),
+            s->gcur.as<unsigned long long>(), cbits, bbits);
+        kmark(s, 4, 1);
+    }
+    mark(s, 2 * EC_STAGE_COUNT + 1);
+    mark(s, 2 * EC_STAGE_COMPACT);
+    const uint64_t umax = Bk * SLOTS;
+    EC_CHECK(s->dkey.ensure(umax * sizeof(K128)));
+    EC_CHECK(s->dcnt.ensure(umax * 4));
+    EC_CHECK(s->dfc.ensure(umax * 8));
+    EC_CHECK(s->dft.ensure(umax * 8));
+    if (!s->no_index) EC_CHECK(s->sub.ensure(umax * sizeof(SubSlotW)));
+    kmark(s, 2, 0);
+    k_bucket_w<SLOTS><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
+        second ? s->recs2.as<RecW>() : s->recs.as<RecW>(), s->bstart.as<unsigned long long>(), limit, s->dkey.as<K128>(),
+        s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+        s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+    kmark(s, 2, 1);
+    mark(s, 2 * EC_STAGE_COMPACT + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.overflow) {  // a bucket outgrew its LDS table: the caller counts on the HBM table
+        s->stats.table_retries++;
+        return reset();
+    }
+    U = hsc.nsolid;
+    s->stats.n_distinct = hsc.ndistinct;
+    s->stats.n_solid = U;
+    s->stats.count_path = EC_PATH_PARTITIONED;
+    s->stats.n_buckets = (uint32_t)Bk;
+    s->stats.table_capacity = umax;
+    sidx.table = nullptr;
+    sidx.capmask = 0;
+    sidx.sub = s->sub.as<SubSlotW>();
+    sidx.bbits = bbits;
+    sidx.slots = SLOTS;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
+    ok = true;
     return EC_OK;
 }
 
@@ -832,6 +961,9 @@ int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, 
         set_error("global read ids reach %llu >= 2^32", (unsigned long long)(nreads + read_base));
         return EC_ERR_ARG;
     }
+    bool ok = false;
+    EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok));
+    if (ok) return EC_OK;
     s->stats.n_reads = nreads;
     hipStream_t st = s->stream;
     const unsigned B = 256;

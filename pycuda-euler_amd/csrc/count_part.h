@@ -295,10 +295,13 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
 
 // coarse counts, bucket-major: cnt[c * ngroups + g] = group g's records in coarse bucket c
 // (sum of its fine bins; a read group is one downsweep workgroup, which fills its runs in order)
+// FB = fine histogram bits (FINE_BITS; count_wide.h uses FINE_W_BITS)
+template <int FB = FINE_BITS>
 __global__ void __launch_bounds__(256) k_coarse(const unsigned int *hist, uint64_t ngroups, int cbits,
                                                 unsigned long long *cnt) {
+    constexpr int FINE = 1 << FB;
     const uint64_t C = 1ull << cbits;
-    const int per = 1 << (FINE_BITS - cbits);
+    const int per = 1 << (FB - cbits);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < C * ngroups;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t c = i / ngroups, g = i % ngroups;
@@ -312,8 +315,10 @@ __global__ void __launch_bounds__(256) k_coarse(const unsigned int *hist, uint64
 // fine-bin totals over all groups (2-D: bins x group slices, one atomic per slice) and the
 // HyperLogLog register maxima over all groups
 constexpr int TOT_SLICES = 32;
+template <int FB = FINE_BITS>
 __global__ void __launch_bounds__(256) k_fine_totals(const unsigned int *hist, const uint8_t *hll, uint64_t ngroups,
                                                      unsigned long long *ftot, unsigned int *hreg) {
+    constexpr int FINE = 1 << FB;
     const unsigned int f = blockIdx.x * blockDim.x + threadIdx.x;  // < FINE
     const unsigned int sl = blockIdx.y;
     unsigned long long sum = 0;
@@ -327,10 +332,11 @@ __global__ void __launch_bounds__(256) k_fine_totals(const unsigned int *hist, c
 }
 
 // records per final bucket (bbits granularity); tot[B] = 0 so its exclusive scan ends at P
+template <int FB = FINE_BITS>
 __global__ void __launch_bounds__(256) k_bucket_totals(const unsigned long long *ftot, int bbits,
                                                        unsigned long long *tot) {
     const uint64_t B = 1ull << bbits;
-    const int per = 1 << (FINE_BITS - bbits);
+    const int per = 1 << (FB - bbits);
     for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b <= B; b += (uint64_t)gridDim.x * blockDim.x) {
         unsigned long long sum = 0;
         if (b < B)

@@ -1,0 +1,395 @@
+// count_wide.h -- partitioned (LDS-table) counting for 128-bit keys, 32 < k <= 63 (BASELINE
+// config 5: k = 51, 150 bp reads).  The same four passes as count_part.h -- upsweep (fine
+// histogram by hash + HyperLogLog), downsweep (records to their (coarse bucket, group) runs,
+// LDS counting sort per batch), refine (coarse -> final buckets, k_refine<RecW>), bucket
+// (one LDS table per final bucket) -- on 24-B records {key lo, key hi, read, lC | lT << 16}.
+// The bucket hash is mix128 of the canonical key throughout.  Taken for N-free reads whose
+// 256-read tiles fit the 40 KB stage (reads up to ~160 bp); other inputs keep the HBM-table
+// path of wide.h.
+#pragma once
+#include "count_part.h"
+#include "wide.h"
+
+namespace ec {
+
+constexpr int STAGE_W = 40896;  // LDS stage of the wide kernels (256 reads of <= 159 bases; upsweep in 80 KB)
+constexpr int FINE_W_BITS = 14;  // fine histogram bins (16384: up to ~25 M distinct keys in 2048-slot tables)
+constexpr int FINE_W = 1 << FINE_W_BITS;
+constexpr int DS_RW = 4;        // downsweep windows per lane per round (24-B records: 24 KB batch)
+constexpr int DS_BATCH_W = TILE_READS * DS_RW;
+
+struct alignas(8) RecW {
+    unsigned long long lo, hi;
+    unsigned int read;
+    unsigned int ev;  // lC | lT << 16
+};
+static_assert(sizeof(RecW) == 24, "wide record layout");
+__device__ inline K128 rkey(const RecW &r) { return K128{r.lo, r.hi}; }
+__device__ inline unsigned int rec_bucket(const RecW &r, int bbits) {
+    return (unsigned int)(mix128(rkey(r)) >> (64 - bbits));
+}
+struct StoreW {
+    RecW *p;
+    __device__ inline RecW load(uint64_t i) const { return p[i]; }
+    __device__ inline void store(uint64_t i, const RecW &r) const { p[i] = r; }
+};
+
+__device__ inline bool stage_tile_w(const uint8_t *buf, const uint64_t *off, uint64_t r0, uint64_t r1, uint8_t *stage,
+                                    uint64_t &base) {
+    const uint64_t b0 = off[r0], b1 = off[r1];
+    const uint64_t a0 = ((uint64_t)(buf + b0)) & ~15ull;
+    const uint64_t a1 = (((uint64_t)(buf + b1)) + 15) & ~15ull;
+    if (a1 - a0 > (uint64_t)STAGE_W) return false;
+    base = a0 - (uint64_t)buf;
+    const uint4 *src = reinterpret_cast<const uint4 *>(a0);
+    uint4 *dst = reinterpret_cast<uint4 *>(stage);
+    const unsigned n16 = (unsigned)((a1 - a0) >> 4);
+    for (unsigned i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    return true;
+}
+
+// one 2-bit base into the forward / reverse-complement 128-bit codes (sh = 2(k-1) >= 64)
+__device__ inline void roll_w(K128 &fwd, K128 &rc, uint32_t b, const K128 &mask, int sh) {
+    fwd = push128(fwd, b, mask);
+    rc.lo = (rc.lo >> 2) | (rc.hi << 62);
+    rc.hi = (rc.hi >> 2) | ((unsigned long long)(3u - b) << (sh - 64));
+}
+
+// ---- upsweep: fine histogram (16384 bins by mix128) + HyperLogLog, per read group ----------
+// lens[2] is set when a read has an 'N' / another byte, or a tile does not fit the stage:
+// the host then counts on the HBM table instead.
+__global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
+                                                          int k, uint64_t gsize, unsigned int *hist,
+                                                          uint8_t *hll_blocks, unsigned long long *npos,
+                                                          unsigned int *maxlocal, unsigned int *skew,
+                                                          unsigned int *lens) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
+    __shared__ unsigned int h_cnt[FINE_W / 2];
+    __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
+    for (int i = threadIdx.x; i < FINE_W / 2; i += blockDim.x) h_cnt[i] = 0;
+    for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x) h_reg[i] = 0;
+    const uint64_t g = blockIdx.x;
+    const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
+    const K128 mask = kmask128(k);
+    const int sh = 2 * (k - 1);
+    unsigned long long mypos = 0;
+    unsigned int mymax = 0, myskew = 0, mynonclean = 0;
+    for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
+        const uint64_t r1 = min(r0 + TILE_READS, g1);
+        uint64_t base = 0;
+        __syncthreads();
+        const bool staged = stage_tile_w(buf, off, r0, r1, stage, base);
+        __syncthreads();
+        const uint64_t r = r0 + threadIdx.x;
+        if (!staged) {
+            mynonclean = 1;
+            continue;
+        }
+        if (r >= r1) continue;
+        const uint64_t s = off[r], len = off[r + 1] - s;
+        const uint32_t rel = (uint32_t)(s - base);
+        const LdsRead rv{reinterpret_cast<const uint32_t *>(stage), rel >> 2, rel & 3};
+        if (read_flags(rv, (uint32_t)len) != 0) {
+            mynonclean = 1;
+            continue;
+        }
+        if (len < (uint64_t)k) continue;
+        const uint32_t m = (uint32_t)(len - k + 1);
+        mypos += m;
+        mymax = max(mymax, 2 * m - 1);
+        K128 fwd{0, 0}, rc{0, 0};
+        uint32_t c4 = 0;
+        for (uint32_t t = 0; t < (uint32_t)len; t++) {
+            if ((t & 3) == 0) c4 = rv.chunk(t >> 2);
+            roll_w(fwd, rc, code2(c4 >> (8 * (t & 3))), mask, sh);
+            if (t + 1 < (uint32_t)k) continue;
+            const K128 c = fwd < rc ? fwd : rc;
+            const uint64_t h = mix128(c);
+            const uint32_t j = (uint32_t)(h >> (64 - HLL_REG_BITS));
+            const uint32_t rho = (uint32_t)__clzll((long long)((h << HLL_REG_BITS) | (1ull << (HLL_REG_BITS - 1)))) + 1;
+            const uint32_t f = (uint32_t)(h >> (64 - FINE_W_BITS));
+            const uint32_t sh16 = (f & 1) * 16;
+            const uint32_t old = atomicAdd(&h_cnt[f >> 1], 1u << sh16);
+            myskew |= ((old >> sh16) & 0xFFFFu) >= 0xFFFEu;
+            if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        mypos += __shfl_down(mypos, o);
+        mymax = max(mymax, (unsigned int)__shfl_down(mymax, o));
+        myskew |= (unsigned int)__shfl_down(myskew, o);
+        mynonclean |= (unsigned int)__shfl_down(mynonclean, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (mypos) atomicAdd(npos, mypos);
+        if (mymax) atomicMax(maxlocal, mymax);
+        if (myskew) atomicOr(skew, 1u);
+        if (mynonclean) atomicOr(&lens[2], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < FINE_W; i += blockDim.x) hist[g * FINE_W + i] = (h_cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+    for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x)
+        hll_blocks[g * (1 << HLL_REG_BITS) + i] = (uint8_t)h_reg[i];
+}
+
+// ---- downsweep: records to their (coarse bucket, group) runs (count_part.h k_downsweep for
+// clean reads, 24-B records, DS_RW windows per lane per round) -------------------------------
+__global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
+                                                            int k, uint64_t gsize, uint64_t ngroups, int cbits,
+                                                            const unsigned long long *offs, RecW *recs,
+                                                            uint64_t read_base) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
+    __shared__ RecW sorted[DS_BATCH_W];
+    __shared__ uint8_t sbk[DS_BATCH_W];
+    __shared__ unsigned int bcnt[1 << DS_MAX_CBITS], bbeg[1 << DS_MAX_CBITS];
+    __shared__ unsigned long long cur[1 << DS_MAX_CBITS], gbase[1 << DS_MAX_CBITS];
+    __shared__ unsigned int s_rounds, s_total, s_wave[TILE_READS / 64];
+    const uint64_t g = blockIdx.x;
+    const int C = 1 << cbits;
+    const unsigned int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const K128 mask = kmask128(k);
+    const int sh = 2 * (k - 1);
+    const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
+    for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
+        const uint64_t r1 = min(r0 + TILE_READS, g1);
+        __syncthreads();
+        for (int c = tid; c < C; c += TILE_READS) {
+            if (r0 == g0) cur[c] = offs[(uint64_t)c * ngroups + g];
+            bcnt[c] = 0;
+        }
+        if (tid == 0) s_rounds = 0;
+        uint64_t base = 0;
+        stage_tile_w(buf, off, r0, r1, stage, base);  // fits: checked by the upsweep
+        __syncthreads();
+        const uint64_t r = r0 + tid;
+        uint64_t s = 0, len = 0;
+        if (r < r1) {
+            s = off[r];
+            len = off[r + 1] - s;
+        }
+        const uint32_t rel = (uint32_t)(s - base);
+        const uint32_t m = len >= (uint64_t)k ? (uint32_t)(len - k + 1) : 0u;
+        if (m) atomicMax(&s_rounds, (m + DS_RW - 1) / DS_RW);
+        __syncthreads();
+        const unsigned int nrounds = s_rounds;
+        K128 fwd{0, 0}, rc{0, 0};
+        uint32_t t = 0, w = 0;
+        if (m)
+            for (; t < (uint32_t)(k - 1); t++) roll_w(fwd, rc, code2(stage[rel + t]), mask, sh);
+        const uint32_t m2 = 2 * m - 1;
+        for (unsigned int round = 0; round < nrounds; round++) {
+            RecW rr[DS_RW];
+            unsigned int cb[DS_RW], rk[DS_RW];
+#pragma unroll
+            for (int j = 0; j < DS_RW; j++) {
+                cb[j] = 0xFFFFFFFFu;
+                if (w < m) {
+                    roll_w(fwd, rc, code2(stage[rel + t]), mask, sh);
+                    const bool f = fwd < rc, pal = fwd == rc;
+                    const K128 c = f ? fwd : rc;
+                    uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
+                    rr[j].lo = c.lo;
+                    rr[j].hi = c.hi;
+                    rr[j].read = (unsigned int)(r + read_base);
+                    rr[j].ev = lC | (lT << 16);
+                    cb[j] = cbits ? (unsigned int)(mix128(c) >> (64 - cbits)) : 0u;
+                    rk[j] = atomicAdd(&bcnt[cb[j]], 1u);
+                    t++;
+                    w++;
+                }
+            }
+            __syncthreads();
+            const unsigned int v = (int)tid < C ? bcnt[tid] : 0u;
+            unsigned int incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int u = __shfl_up(incl, o);
+                if ((int)lane >= o) incl += u;
+            }
+            if (lane == 63) s_wave[wid] = incl;
+            __syncthreads();
+            unsigned int before = 0;
+            for (unsigned int q = 0; q < wid; q++) before += s_wave[q];
+            if ((int)tid < C) {
+                bbeg[tid] = before + incl - v;
+                gbase[tid] = cur[tid];
+                cur[tid] += v;
+            }
+            if (tid == TILE_READS - 1) s_total = before + incl;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < DS_RW; j++) {
+                if (cb[j] != 0xFFFFFFFFu) {
+                    const unsigned int p = bbeg[cb[j]] + rk[j];
+                    sorted[p] = rr[j];
+                    sbk[p] = (uint8_t)cb[j];
+                }
+            }
+            __syncthreads();
+            const unsigned int total = s_total;
+            for (unsigned int i = tid; i < total; i += TILE_READS) {
+                const unsigned int c = sbk[i];
+                recs[gbase[c] + (i - bbeg[c])] = sorted[i];
+            }
+            if ((int)tid < C) bcnt[tid] = 0;
+            __syncthreads();
+        }
+    }
+}
+
+// ---- bucket pass: one LDS table of 128-bit keys per final bucket ----------------------------
+// Slots claim a key with two 64-bit CASes on its claim words (wide_w1 / wide_w2, never 0),
+// as wide_slot does in HBM; a slot whose first word matches but whose second word went to
+// another key is passed over.  Wave-uniform probe loop and fill reservation as lds_insert.
+struct alignas(16) LSlotW {
+    unsigned long long w1, w2;
+    unsigned int count, pad;
+    unsigned long long fC, fT;  // fC, fT 16-B aligned
+    unsigned long long pad2;
+};
+static_assert(sizeof(LSlotW) == 48, "wide LDS slot layout");
+
+template <int SLOTS>
+__device__ inline void lds_insert_w(LSlotW *tab, unsigned int *s_over, const K128 &c, unsigned int slot0,
+                                    unsigned int add, unsigned long long eC, unsigned long long eT) {
+    const unsigned long long w1 = wide_w1(c), w2 = wide_w2(c);
+    unsigned int slot = slot0 & (SLOTS - 1);
+    unsigned long long a = tab[slot].w1, bw = tab[slot].w2;
+    bool miss = !(a == w1 && bw == w2);
+#pragma unroll 1
+    while (__any(miss)) {
+        if (miss) {
+            if (a == 0) {  // free slot: reserve, then claim the first word
+                if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {
+                    s_over[0] = 1;
+                    a = w1;
+                    bw = w2;  // give up (the bucket is redone elsewhere)
+                } else {
+                    a = atomicCAS(&tab[slot].w1, 0ull, w1);
+                    if (a == 0) a = w1;
+                    else atomicSub(&s_over[1], 1u);
+                }
+            }
+            if (a == w1 && bw != w2) {  // first word ours: the second decides
+                bw = tab[slot].w2;
+                if (bw == 0) {
+                    bw = atomicCAS(&tab[slot].w2, 0ull, w2);
+                    if (bw == 0) bw = w2;
+                }
+            }
+            if (!(a == w1 && bw == w2)) {
+                slot = (slot + 1) & (SLOTS - 1);
+                a = tab[slot].w1;
+                bw = tab[slot].w2;
+            }
+            miss = !(a == w1 && bw == w2);
+        }
+    }
+    LSlotW &sl = tab[slot];
+    atomicAdd(&sl.count, add);
+    const ulonglong2 ev = *reinterpret_cast<const ulonglong2 *>(&sl.fC);
+    if (eC < ev.x) atomicMin(&sl.fC, eC);
+    if (eT < ev.y) atomicMin(&sl.fT, eT);
+}
+
+template <int SLOTS>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, const unsigned long long *bstart,
+                                                            long long limit, K128 *dkey, unsigned int *dcnt,
+                                                            unsigned long long *dfc, unsigned long long *dft,
+                                                            SubSlotW *sub, unsigned int *nsolid,
+                                                            unsigned long long *ndistinct, unsigned int *overflow) {
+    __shared__ LSlotW tab[SLOTS];
+    __shared__ unsigned int s_over[2];
+    __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
+    __shared__ unsigned int s_base;
+    const unsigned int b = blockIdx.x;
+    for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
+        tab[i].w1 = 0;
+        tab[i].w2 = 0;
+        tab[i].count = 0;
+        tab[i].fC = NONE64;
+        tab[i].fT = NONE64;
+    }
+    if (threadIdx.x == 0) {
+        s_over[0] = 0;
+        s_over[1] = 0;
+    }
+    __syncthreads();
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    constexpr int U = 4;  // loads of U records issued before any insert
+    auto ins = [&](const RecW &x) {
+        const unsigned int lC = x.ev & 0xFFFFu, lT = x.ev >> 16;
+        const K128 c = rkey(x);
+        const unsigned long long rd = (unsigned long long)x.read << 32;
+        lds_insert_w<SLOTS>(tab, s_over, c, (unsigned int)mix128(c), lC == lT ? 2u : 1u, rd | lC, rd | lT);
+    };
+    uint64_t i = r0 + threadIdx.x;
+    for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
+        RecW raw[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) raw[u] = recs[i + u * (uint64_t)blockDim.x];
+#pragma unroll
+        for (int u = 0; u < U; u++) ins(raw[u]);
+    }
+    for (; i < r1; i += blockDim.x) ins(recs[i]);
+    __syncthreads();
+    if (s_over[0]) {
+        if (threadIdx.x == 0) atomicAdd(overflow, 1u);
+        return;
+    }
+    // solid filter + compaction (as lds_table_finish)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int PER = SLOTS / BUCKET_THREADS;
+    bool solid[PER];
+    unsigned int mine = 0, present = 0;
+    for (int q = 0; q < PER; q++) {
+        const LSlotW &sl = tab[threadIdx.x * PER + q];
+        present += sl.w1 != 0;
+        solid[q] = sl.w1 != 0 && (long long)sl.count > limit;
+        mine += solid[q];
+    }
+    unsigned int incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wave[wid] = incl;
+    unsigned int pres = present;
+    for (int o = 32; o > 0; o >>= 1) pres += __shfl_down(pres, o);
+    if (lane == 0) s_pres[wid] = pres;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int tot = 0, np = 0;
+        for (int w = 0; w < BUCKET_THREADS / 64; w++) {
+            const unsigned int c = s_wave[w];
+            s_wave[w] = tot;
+            tot += c;
+            np += s_pres[w];
+        }
+        s_base = tot ? atomicAdd(nsolid, tot) : 0;
+        if (np) atomicAdd(ndistinct, (unsigned long long)np);
+    }
+    __syncthreads();
+    unsigned int u = s_base + s_wave[wid] + incl - mine;
+    SubSlotW *region = sub ? sub + (uint64_t)b * SLOTS : nullptr;
+    for (int q = 0; q < PER; q++) {
+        const int idx = threadIdx.x * PER + q;
+        const LSlotW &sl = tab[idx];
+        SubSlotW o;
+        o.w1 = sl.w1;
+        o.w2 = sl.w2;
+        o.id = NONE32;
+        o.pad = 0;
+        o.pad2 = 0;
+        if (solid[q]) {
+            dkey[u] = wide_key(sl.w1, sl.w2);
+            dcnt[u] = sl.count;
+            dfc[u] = sl.fC;
+            dft[u] = sl.fT;
+            o.id = u;
+            u++;
+        }
+        if (region) region[idx] = o;
+    }
+}
+
+}  // namespace ec

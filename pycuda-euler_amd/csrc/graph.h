@@ -92,9 +92,25 @@ struct OpsW {
 
 // canonical K128 key -> dense solid id in the wide table
 struct SolidIndexW {
-    const SlotW *table;
+    const SlotW *table;  // general count: the HBM table
     uint64_t capmask;
-    __device__ inline unsigned int find(const K128 &c) const { return lookup_w(table, capmask, c); }
+    const SubSlotW *sub;  // partitioned count (count_wide.h): bucket sub-tables of `slots` slots
+    int bbits;
+    unsigned int slots;
+    __device__ inline unsigned int find(const K128 &c) const {
+        if (!sub) return lookup_w(table, capmask, c);
+        const unsigned long long w1 = wide_w1(c), w2 = wide_w2(c);
+        const uint64_t h = mix128(c);
+        const SubSlotW *r = sub + (bbits ? (h >> (64 - bbits)) : 0ull) * slots;
+        unsigned int slot = (unsigned int)h & (slots - 1);
+        for (unsigned int probe = 0; probe < slots; probe++) {
+            const ulonglong2 ww = *reinterpret_cast<const ulonglong2 *>(&r[slot].w1);
+            if (ww.x == 0) return NONE32;
+            if (ww.x == w1 && ww.y == w2) return r[slot].id;
+            slot = (slot + 1) & (slots - 1);
+        }
+        return NONE32;
+    }
     struct Nb {};
     __device__ inline Nb nb_begin(const K128 &) const { return Nb{}; }
     __device__ inline unsigned int find_nb(const Nb &, const K128 &, const K128 &cy) const { return find(cy); }

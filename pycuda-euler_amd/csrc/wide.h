@@ -80,6 +80,15 @@ struct alignas(16) SlotW {
 };
 static_assert(sizeof(SlotW) == 48, "wide slot layout");
 
+// lookup sub-table slot of the partitioned wide count (count_wide.h k_bucket_w); id NONE =
+// present, not solid
+struct alignas(16) SubSlotW {
+    unsigned long long w1, w2;
+    unsigned int id, pad;
+    unsigned long long pad2;
+};
+static_assert(sizeof(SubSlotW) == 32, "wide sub-table slot layout");
+
 // exchange record of the multi-GPU path for k > 32 (ec_kmer_record_wide, 48 B)
 struct alignas(16) AggW {
     unsigned long long lo, hi;

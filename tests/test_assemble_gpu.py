@@ -26,7 +26,7 @@ def test_golden(gpu_session, case):
     assert [[x, c] for x, c in res.dict_items] == case["d"]
     assert res.contigs == case["contigs"]
     assert res.links == case["links"]
-    if res.stats.n_positions > 0:  # 128-bit keys (k > 32) count in the general table
+    if res.stats.n_positions > 0:
         assert res.stats.count_path in _want_paths(case["reads"], case["k"], False)
 
 
@@ -36,9 +36,9 @@ def _sk_applies(reads, k):
 
 def _want_paths(reads, k, superkmer):
     """super-k-mer records (default or EC_FLAG_SUPERKMER) for 21 <= k <= 32 and N-free reads,
-    else window records (k <= 32); k > 32 counts in the general table"""
-    if k > 32:
-        return (eulerhip.EC_PATH_GENERAL,)
+    else window records (k <= 32); k > 32: 24-B records without N, else the general table"""
+    if k > 32:  # partitioned 24-B records for N-free reads (count_wide.h)
+        return (eulerhip.EC_PATH_GENERAL,) if any("N" in r for r in reads) else (eulerhip.EC_PATH_PARTITIONED,)
     if not _sk_applies(reads, k):
         return (eulerhip.EC_PATH_PARTITIONED,)
     if superkmer:
@@ -304,3 +304,75 @@ def test_filter_buckets_limits_vs_oracle(gpu_session, monkeypatch):
         gpu_session.run_host(buf, off, k, lim)
         res = gpu_session.fetch(k)
         assert res.contig_bytes == ref["contig_chars"] and res.links == rl, (k, lim)
+
+
+# ---- partitioned 128-bit counting (count_wide.h, 32 < k <= 63) -------------------------------
+WIDE = [  # genome, reads, len, seed, err, circular, k
+    (30_000, 12_000, 150, 21, 0.002, False, 51),
+    (20_000, 8_000, 100, 22, 0.003, True, 33),
+    (10_000, 6_000, 120, 23, 0.0, False, 63),
+    (3_000, 4_000, 90, 24, 0.01, False, 40),
+    (300_000, 60_000, 150, 25, 0.002, False, 51),  # 2^9 buckets: refine pass
+    (200_000, 50_000, 150, 26, 0.0, True, 62),
+]
+
+
+@pytest.mark.parametrize("g,n,L,seed,err,circ,k", WIDE)
+def test_wide_partitioned_vs_oracle(gpu_session, g, n, L, seed, err, circ, k):
+    buf, off = make_reads(g, n, L, 2000 + seed, err=err, circular=circ)
+    want_dict = g <= 50_000
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT if want_dict else 0)
+    res = gpu_session.fetch(k, want_dict)
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.record_bytes == 24
+    if g >= 200_000:
+        assert res.stats.n_buckets >= 128
+    assert res.stats.n_positions == ref["n_positions"] and res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    if want_dict:
+        assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+@pytest.mark.parametrize("k", [34, 40, 51, 62])
+def test_wide_low_complexity_vs_oracle(gpu_session, k):
+    """tandem repeats: heavy keys, long probe chains; even k: palindromic 128-bit keys"""
+    reads = _low_complexity_reads(300, 140, 60 + k)
+    d, r, g = oracle.assemble(reads, k, 1)
+    res = gpu_session.assemble(reads, k, 1, want_dict=True)
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
+    assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g
+
+
+def test_wide_ragged_and_limits_vs_oracle(gpu_session):
+    rng = np.random.default_rng(77)
+    g = "".join("ACGT"[x] for x in rng.integers(0, 4, 20_000))
+    reads = []
+    for i in range(5000):
+        L = int(rng.choice([10, 50, 51, 52, 90, 150, 155]))
+        p = int(rng.integers(0, len(g) - L))
+        reads.append(g[p:p + L])
+    for lim in (-1, 0, 1, 3):
+        d, r, gl = oracle.assemble(reads, 51, lim)
+        res = gpu_session.assemble(reads, 51, lim, want_dict=True)
+        assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
+        assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == gl, lim
+
+
+def test_wide_fallbacks_vs_oracle(gpu_session, monkeypatch):
+    """N in a read, tiles over the 40 KB stage, buckets past their table: the HBM table"""
+    cases = [
+        (make_reads(20_000, 6_000, 100, 31, err=0.002, n_rate=0.002), None),
+        (make_reads(20_000, 3_000, 200, 32, err=0.002), None),   # 256 x 200 B > 40 KB
+        (make_reads(100_000, 30_000, 120, 33, err=0.003), "2"),  # 4 buckets of ~5e4 keys
+    ]
+    for (buf, off), maxb in cases:
+        if maxb:
+            monkeypatch.setenv("EULERHIP_WIDE_MAX_BBITS", maxb)
+        ref, rc, rl = _oracle_packed(buf, off, 45, 1)
+        gpu_session.run_host(buf, off, 45, 1)
+        res = gpu_session.fetch(45)
+        assert res.stats.count_path == eulerhip.EC_PATH_GENERAL
+        if maxb:
+            assert res.stats.table_retries >= 1
+        assert res.stats.n_positions == ref["n_positions"]
+        assert res.contig_bytes == ref["contig_chars"] and res.links == rl
