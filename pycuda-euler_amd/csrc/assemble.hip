@@ -870,7 +870,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_HIP(hipStreamSynchronize(st));
     const uint64_t P = hsc.npos;
     const double est = hsc.est;
-    double per_max = 1500.0;  // keys per 2048-slot bucket table
+    double per_max = 1800.0;  // keys per bucket table (SLOTS_W slots)
     if (const char *e = getenv("EULERHIP_WIDE_BUCKET_MAX")) per_max = atof(e);
     if (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT || !P || est / FINE_W > per_max) return reset();
     s->stats.n_reads = nreads;
@@ -885,7 +885,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     while ((1 << (fan + 1)) <= REFINE_FANOUT) fan++;
     const int cbits = std::min(bbits, std::min(DS_MAX_CBITS, std::max(1, bbits - fan)));
     const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
-    constexpr unsigned int SLOTS = 2048;
+    constexpr unsigned int SLOTS = SLOTS_W;
     mark(s, 2 * EC_STAGE_COUNT);
     EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
     EC_CHECK(s->offs.ensure(Ck * ngroups * 8));

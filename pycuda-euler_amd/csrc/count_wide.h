@@ -13,7 +13,8 @@
 namespace ec {
 
 constexpr int STAGE_W = 40896;  // LDS stage of the wide kernels (256 reads of <= 159 bases; upsweep in 80 KB)
-constexpr int FINE_W_BITS = 14;  // fine histogram bins (16384: up to ~25 M distinct keys in 2048-slot tables)
+constexpr int FINE_W_BITS = 14;  // fine histogram bins (16384 buckets: up to ~30 M distinct keys)
+constexpr int SLOTS_W = 3328;    // LDS table slots per bucket (156 KB of 48-B slots: load <= ~0.4)
 constexpr int FINE_W = 1 << FINE_W_BITS;
 constexpr int DS_RW = 4;        // downsweep windows per lane per round (24-B records: 24 KB batch)
 constexpr int DS_BATCH_W = TILE_READS * DS_RW;
@@ -248,11 +249,16 @@ struct alignas(16) LSlotW {
 };
 static_assert(sizeof(LSlotW) == 48, "wide LDS slot layout");
 
+// table sizes need not be powers of two: slot0 = (low 32 hash bits * SLOTS) >> 32
+__host__ __device__ inline unsigned int wide_slot0(uint64_t h, unsigned int slots) {
+    return (unsigned int)(((uint64_t)(uint32_t)h * slots) >> 32);
+}
+
 template <int SLOTS>
 __device__ inline void lds_insert_w(LSlotW *tab, unsigned int *s_over, const K128 &c, unsigned int slot0,
                                     unsigned int add, unsigned long long eC, unsigned long long eT) {
     const unsigned long long w1 = wide_w1(c), w2 = wide_w2(c);
-    unsigned int slot = slot0 & (SLOTS - 1);
+    unsigned int slot = slot0;
     unsigned long long a = tab[slot].w1, bw = tab[slot].w2;
     bool miss = !(a == w1 && bw == w2);
 #pragma unroll 1
@@ -277,7 +283,7 @@ __device__ inline void lds_insert_w(LSlotW *tab, unsigned int *s_over, const K12
                 }
             }
             if (!(a == w1 && bw == w2)) {
-                slot = (slot + 1) & (SLOTS - 1);
+                slot = slot + 1 == SLOTS ? 0u : slot + 1;
                 a = tab[slot].w1;
                 bw = tab[slot].w2;
             }
@@ -320,7 +326,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, c
         const unsigned int lC = x.ev & 0xFFFFu, lT = x.ev >> 16;
         const K128 c = rkey(x);
         const unsigned long long rd = (unsigned long long)x.read << 32;
-        lds_insert_w<SLOTS>(tab, s_over, c, (unsigned int)mix128(c), lC == lT ? 2u : 1u, rd | lC, rd | lT);
+        lds_insert_w<SLOTS>(tab, s_over, c, wide_slot0(mix128(c), SLOTS), lC == lT ? 2u : 1u, rd | lC, rd | lT);
     };
     uint64_t i = r0 + threadIdx.x;
     for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
@@ -338,11 +344,16 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, c
     }
     // solid filter + compaction (as lds_table_finish)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int PER = SLOTS / BUCKET_THREADS;
+    constexpr int PER = (SLOTS + BUCKET_THREADS - 1) / BUCKET_THREADS;
     bool solid[PER];
     unsigned int mine = 0, present = 0;
     for (int q = 0; q < PER; q++) {
-        const LSlotW &sl = tab[threadIdx.x * PER + q];
+        const int idx = threadIdx.x * PER + q;
+        if (idx >= SLOTS) {
+            solid[q] = false;
+            continue;
+        }
+        const LSlotW &sl = tab[idx];
         present += sl.w1 != 0;
         solid[q] = sl.w1 != 0 && (long long)sl.count > limit;
         mine += solid[q];
@@ -373,6 +384,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, c
     SubSlotW *region = sub ? sub + (uint64_t)b * SLOTS : nullptr;
     for (int q = 0; q < PER; q++) {
         const int idx = threadIdx.x * PER + q;
+        if (idx >= SLOTS) break;
         const LSlotW &sl = tab[idx];
         SubSlotW o;
         o.w1 = sl.w1;

@@ -78,6 +78,10 @@ struct Ops64 {
     __device__ static inline K mask(int k) { return kmask64(k); }
     __device__ static inline K twin(const K &x, int k) { return twin64(x, k); }
     __device__ static inline K push(const K &x, uint32_t b, const K &m) { return ((x << 2) | b) & m; }
+    // twin(push(x, b)) from tx = twin(x): the complement of b enters at the front
+    __device__ static inline K twin_push(const K &tx, uint32_t b, int k) {
+        return (tx >> 2) | ((K)(3u - b) << (2 * (k - 1)));
+    }
     __device__ static inline uint32_t base(const K &x, int k, int i) { return (uint32_t)(x >> (2 * (k - 1 - i))) & 3u; }
     __device__ static inline uint32_t last(const K &x) { return (uint32_t)x & 3u; }
 };
@@ -86,6 +90,12 @@ struct OpsW {
     __device__ static inline K mask(int k) { return kmask128(k); }
     __device__ static inline K twin(const K &x, int k) { return twin128(x, k); }
     __device__ static inline K push(const K &x, uint32_t b, const K &m) { return push128(x, b, m); }
+    __device__ static inline K twin_push(const K &tx, uint32_t b, int k) {  // 2(k-1) >= 64
+        K r;
+        r.lo = (tx.lo >> 2) | (tx.hi << 62);
+        r.hi = (tx.hi >> 2) | ((unsigned long long)(3u - b) << (2 * (k - 1) - 64));
+        return r;
+    }
     __device__ static inline uint32_t base(const K &x, int k, int i) { return base_at128(x, k, i); }
     __device__ static inline uint32_t last(const K &x) { return (uint32_t)x.lo & 3u; }
 };
@@ -102,12 +112,12 @@ struct SolidIndexW {
         const unsigned long long w1 = wide_w1(c), w2 = wide_w2(c);
         const uint64_t h = mix128(c);
         const SubSlotW *r = sub + (bbits ? (h >> (64 - bbits)) : 0ull) * slots;
-        unsigned int slot = (unsigned int)h & (slots - 1);
+        unsigned int slot = (unsigned int)(((uint64_t)(uint32_t)h * slots) >> 32);  // wide_slot0
         for (unsigned int probe = 0; probe < slots; probe++) {
             const ulonglong2 ww = *reinterpret_cast<const ulonglong2 *>(&r[slot].w1);
             if (ww.x == 0) return NONE32;
             if (ww.x == w1 && ww.y == w2) return r[slot].id;
-            slot = (slot + 1) & (slots - 1);
+            slot = slot + 1 == slots ? 0u : slot + 1;
         }
         return NONE32;
     }
@@ -148,12 +158,12 @@ __global__ void __launch_bounds__(256) k_neighbors(Index idx, const typename Ops
             upal[x >> 1] = pal ? 1 : 0;
             if (pal) atomicAdd(npal, 1u);
         }
-        const K xs = (x & 1) ? tc : c;
+        const K xs = (x & 1) ? tc : c, txs = (x & 1) ? c : tc;
         unsigned int n = 0, cd = NONE32;
         const typename Index::Nb nb = idx.nb_begin(xs);
         for (uint32_t b = 0; b < 4; b++) {
             const K y = Ops::push(xs, b, mask);
-            const K ty = Ops::twin(y, k);
+            const K ty = Ops::twin_push(txs, b, k);
             const K cy = y < ty ? y : ty;
             const unsigned int u = idx.find_nb(nb, y, cy);
             if (u != NONE32) {
@@ -200,12 +210,12 @@ __global__ void __launch_bounds__(256) k_links_part(Index idx, const typename Op
         const bool pal = tc == c;
         unsigned int s = NONE32;
         if (!((x & 1) && pal)) {
-            const K xs = (x & 1) ? tc : c;
+            const K xs = (x & 1) ? tc : c, txs = (x & 1) ? c : tc;
             unsigned int nfw = 0, cd = NONE32;
             const typename Index::Nb nb = idx.nb_begin(xs);
             for (uint32_t b = 0; b < 4; b++) {
                 const K y = Ops::push(xs, b, mask);
-                const K ty = Ops::twin(y, k);
+                const K ty = Ops::twin_push(txs, b, k);
                 const K cy = y < ty ? y : ty;
                 const unsigned int u = idx.find_nb(nb, y, cy);
                 if (u != NONE32) {
@@ -218,12 +228,12 @@ __global__ void __launch_bounds__(256) k_links_part(Index idx, const typename Op
                 const K yc = dkey[cd >> 1];
                 const K yt = Ops::twin(yc, k);
                 const unsigned int tyn = yt == yc ? cd : (cd ^ 1u);  // twin node of the candidate
-                const K tys = (tyn & 1) ? yt : yc;
+                const K tys = (tyn & 1) ? yt : yc, ttys = (tyn & 1) ? yc : yt;
                 unsigned int nin = 0;
                 const typename Index::Nb nb2 = idx.nb_begin(tys);
                 for (uint32_t b = 0; b < 4; b++) {
                     const K z = Ops::push(tys, b, mask);
-                    const K tz = Ops::twin(z, k);
+                    const K tz = Ops::twin_push(ttys, b, k);
                     const K cz = z < tz ? z : tz;
                     nin += idx.find_nb(nb2, z, cz) != NONE32;
                 }
