@@ -221,17 +221,16 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
     const uint64_t g = blockIdx.x;
     const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
     unsigned long long mypos = 0;
-    unsigned int mymax = 0, myskew = 0, mylmax = 0, mylmin = 0xFFFFFFFFu, mynonclean = 0;
+    unsigned int mymax = 0, mylmax = 0, mylmin = 0xFFFFFFFFu, mynonclean = 0;
+    // (rho from the 21 hash bits under the register index: registers saturate at 22, far
+    // above log2(distinct / 2048) for any input that fits one GPU)
     auto win = [&](uint64_t fwd, uint64_t rc) {
         const uint64_t c = fwd < rc ? fwd : rc;
-        const uint64_t h = mix64(c);
-        const uint32_t j = (uint32_t)(h >> (64 - HLL_REG_BITS));
-        const uint64_t wv = (h << HLL_REG_BITS) | (1ull << (HLL_REG_BITS - 1));
-        const uint32_t rho = (uint32_t)__clzll((long long)wv) + 1;
-        const uint32_t f = (uint32_t)(h >> (64 - FINE_BITS));
-        const uint32_t sh16 = (f & 1) * 16;
-        const uint32_t old = atomicAdd(&h_cnt[f >> 1], 1u << sh16);
-        myskew |= ((old >> sh16) & 0xFFFFu) >= 0xFFFEu;
+        const uint32_t hh = (uint32_t)(mix64(c) >> 32);
+        const uint32_t j = hh >> (32 - HLL_REG_BITS);
+        const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+        const uint32_t f = hh >> (32 - FINE_BITS);
+        atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
         if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
     };
     for_group_reads(buf, off, g0, g1, stage,
@@ -271,23 +270,32 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep(const uint8_t *buf, cons
             slow(br);
         }
     });
+    // a u16 bin that wrapped (one k-mer > 65535 times in the group) lowers the sum of the bins
+    // below the group's window count (65535 per carry into the neighbour, 65536 per wrap out)
+    unsigned long long binsum = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < FINE / 2; i += blockDim.x) binsum += (h_cnt[i] & 0xFFFFu) + (h_cnt[i] >> 16);
     for (int o = 32; o > 0; o >>= 1) {
         mypos += __shfl_down(mypos, o);
+        binsum += __shfl_down(binsum, o);
         mymax = max(mymax, (unsigned int)__shfl_down(mymax, o));
-        myskew |= (unsigned int)__shfl_down(myskew, o);
         mylmax = max(mylmax, (unsigned int)__shfl_down(mylmax, o));
         mylmin = min(mylmin, (unsigned int)__shfl_down(mylmin, o));
         mynonclean |= (unsigned int)__shfl_down(mynonclean, o);
     }
+    __shared__ unsigned long long s_diff;
+    if (threadIdx.x == 0) s_diff = 0;
+    __syncthreads();
     if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&s_diff, mypos - binsum);  // mod 2^64: 0 iff no bin overflowed
         if (mypos) atomicAdd(npos, mypos);
         if (mymax) atomicMax(maxlocal, mymax);
-        if (myskew) atomicOr(skew, 1u);
         if (mylmax) atomicMax(&lens[0], mylmax);
         if (mylmin != 0xFFFFFFFFu) atomicMax(&lens[1], ~mylmin);  // lens[1] = ~(min length)
         if (mynonclean) atomicOr(&lens[2], 1u);
     }
     __syncthreads();
+    if (threadIdx.x == 0 && s_diff != 0) atomicOr(skew, 1u);
     for (int i = threadIdx.x; i < FINE; i += blockDim.x) hist[g * FINE + i] = (h_cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
     for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x)
         hll_blocks[g * (1 << HLL_REG_BITS) + i] = (uint8_t)h_reg[i];

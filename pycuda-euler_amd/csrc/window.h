@@ -108,20 +108,30 @@ __device__ inline uint32_t read_flags(const LdsRead &rv, uint32_t len) {
 
 // Windows of an N-free read (one segment, wb = 0, m = len-k+1): fn(fwd, rc, i) for i < m;
 // the insertion events are i (forward string) and 2m-1-i (twin string), as in for_each_window.
-template <typename Fn>
-__device__ inline void windows_clean(const LdsRead &rv, uint32_t len, int k, Fn &&fn) {
+// HI (k >= 17): both rolls touch only the high word for the mask / the entering twin base.
+template <bool HI, typename Fn>
+__device__ inline void windows_clean_t(const LdsRead &rv, uint32_t len, int k, Fn &&fn) {
     const uint64_t mask = kmask64(k);
+    const uint32_t mhi = (uint32_t)(mask >> 32);
     const int sh = 2 * (k - 1);
     uint64_t fwd = 0, rc = 0;
-    const uint32_t full = len >> 2;
     const uint32_t km1 = (uint32_t)(k - 1);
+    auto roll = [&](uint32_t b) {
+        if (HI) {
+            fwd = (fwd << 2) | b;
+            fwd &= ((uint64_t)mhi << 32) | 0xFFFFFFFFull;
+            rc = (rc >> 2) | ((uint64_t)((3u - b) << (sh - 32)) << 32);
+        } else {
+            fwd = ((fwd << 2) | b) & mask;
+            rc = (rc >> 2) | ((uint64_t)(3u - b) << sh);
+        }
+    };
+    const uint32_t full = len >> 2;
     for (uint32_t i = 0; i < full; i++) {
         const uint32_t c4 = rv.chunk(i);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const uint64_t b = code2(c4 >> (8 * q));
-            fwd = ((fwd << 2) | b) & mask;
-            rc = (rc >> 2) | ((3ull - b) << sh);
+            roll(code2(c4 >> (8 * q)));
             const uint32_t t = 4 * i + q;
             if (t >= km1) fn(fwd, rc, t - km1);
         }
@@ -129,13 +139,18 @@ __device__ inline void windows_clean(const LdsRead &rv, uint32_t len, int k, Fn 
     if (len & 3) {
         const uint32_t c4 = rv.chunk(full);
         for (uint32_t q = 0; q < (len & 3); q++) {
-            const uint64_t b = code2(c4 >> (8 * q));
-            fwd = ((fwd << 2) | b) & mask;
-            rc = (rc >> 2) | ((3ull - b) << sh);
+            roll(code2(c4 >> (8 * q)));
             const uint32_t t = 4 * full + q;
             if (t >= km1) fn(fwd, rc, t - km1);
         }
     }
+}
+template <typename Fn>
+__device__ inline void windows_clean(const LdsRead &rv, uint32_t len, int k, Fn &&fn) {
+    if (k >= 17)
+        windows_clean_t<true>(rv, len, k, fn);
+    else
+        windows_clean_t<false>(rv, len, k, fn);
 }
 
 }  // namespace ec
