@@ -53,9 +53,12 @@ static_assert(sizeof(Rec12) == 12, "compact record layout");
 __device__ inline unsigned long long rkey(const Rec &r) { return r.key; }
 __device__ inline unsigned long long rkey(const Rec12 &r) { return ((unsigned long long)r.khi << 32) | r.klo; }
 // final bucket of a window record: top bbits of mix64(key) (bbits >= 1)
-__device__ inline unsigned int rec_bucket(const Rec &r, int bbits) { return (unsigned int)(mix64(r.key) >> (64 - bbits)); }
+// (the high word alone: the compiler then skips the low half of the 64-bit product)
+__device__ inline unsigned int rec_bucket(const Rec &r, int bbits) {
+    return (unsigned int)(mix64(r.key) >> 32) >> (32 - bbits);
+}
 __device__ inline unsigned int rec_bucket(const Rec12 &r, int bbits) {
-    return (unsigned int)(mix64(rkey(r)) >> (64 - bbits));
+    return (unsigned int)(mix64(rkey(r)) >> 32) >> (32 - bbits);
 }
 
 // record construction in the downsweep: window (fwd, rc) of read r with local events lf / lr
@@ -380,7 +383,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
     const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
     auto make = [&](uint64_t fwd, uint64_t rc, uint32_t lf, uint32_t lr, uint64_t r, unsigned int &cb) {
         const uint64_t c = fwd < rc ? fwd : rc;
-        cb = cbits ? (unsigned int)(mix64(c) >> (64 - cbits)) : 0u;
+        cb = cbits ? ((unsigned int)(mix64(c) >> 32) >> (32 - cbits)) : 0u;  // high word only
         return mk(fwd, rc, lf, lr, r);
     };
     for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {

@@ -27,7 +27,7 @@ struct alignas(8) RecW {
 static_assert(sizeof(RecW) == 24, "wide record layout");
 __device__ inline K128 rkey(const RecW &r) { return K128{r.lo, r.hi}; }
 __device__ inline unsigned int rec_bucket(const RecW &r, int bbits) {
-    return (unsigned int)(mix128(rkey(r)) >> (64 - bbits));
+    return (unsigned int)(mix128(rkey(r)) >> 32) >> (32 - bbits);
 }
 struct StoreW {
     RecW *p;
@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
     const K128 mask = kmask128(k);
     const int sh = 2 * (k - 1);
     unsigned long long mypos = 0;
-    unsigned int mymax = 0, myskew = 0, mynonclean = 0;
+    unsigned int mymax = 0, mynonclean = 0;
     for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
         const uint64_t r1 = min(r0 + TILE_READS, g1);
         uint64_t base = 0;
@@ -105,29 +105,34 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
             roll_w(fwd, rc, code2(c4 >> (8 * (t & 3))), mask, sh);
             if (t + 1 < (uint32_t)k) continue;
             const K128 c = fwd < rc ? fwd : rc;
-            const uint64_t h = mix128(c);
-            const uint32_t j = (uint32_t)(h >> (64 - HLL_REG_BITS));
-            const uint32_t rho = (uint32_t)__clzll((long long)((h << HLL_REG_BITS) | (1ull << (HLL_REG_BITS - 1)))) + 1;
-            const uint32_t f = (uint32_t)(h >> (64 - FINE_W_BITS));
-            const uint32_t sh16 = (f & 1) * 16;
-            const uint32_t old = atomicAdd(&h_cnt[f >> 1], 1u << sh16);
-            myskew |= ((old >> sh16) & 0xFFFFu) >= 0xFFFEu;
+            const uint32_t hh = (uint32_t)(mix128(c) >> 32);  // as k_upsweep
+            const uint32_t j = hh >> (32 - HLL_REG_BITS);
+            const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+            const uint32_t f = hh >> (32 - FINE_W_BITS);
+            atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
             if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
         }
     }
+    unsigned long long binsum = 0;  // bin-sum overflow check of k_upsweep
+    __syncthreads();
+    for (int i = threadIdx.x; i < FINE_W / 2; i += blockDim.x) binsum += (h_cnt[i] & 0xFFFFu) + (h_cnt[i] >> 16);
     for (int o = 32; o > 0; o >>= 1) {
         mypos += __shfl_down(mypos, o);
+        binsum += __shfl_down(binsum, o);
         mymax = max(mymax, (unsigned int)__shfl_down(mymax, o));
-        myskew |= (unsigned int)__shfl_down(myskew, o);
         mynonclean |= (unsigned int)__shfl_down(mynonclean, o);
     }
+    __shared__ unsigned long long s_diff;
+    if (threadIdx.x == 0) s_diff = 0;
+    __syncthreads();
     if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&s_diff, mypos - binsum);
         if (mypos) atomicAdd(npos, mypos);
         if (mymax) atomicMax(maxlocal, mymax);
-        if (myskew) atomicOr(skew, 1u);
         if (mynonclean) atomicOr(&lens[2], 1u);
     }
     __syncthreads();
+    if (threadIdx.x == 0 && s_diff != 0) atomicOr(skew, 1u);
     for (int i = threadIdx.x; i < FINE_W; i += blockDim.x) hist[g * FINE_W + i] = (h_cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
     for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x)
         hll_blocks[g * (1 << HLL_REG_BITS) + i] = (uint8_t)h_reg[i];
@@ -193,7 +198,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, 
                     rr[j].hi = c.hi;
                     rr[j].read = (unsigned int)(r + read_base);
                     rr[j].ev = lC | (lT << 16);
-                    cb[j] = cbits ? (unsigned int)(mix128(c) >> (64 - cbits)) : 0u;
+                    cb[j] = cbits ? ((unsigned int)(mix128(c) >> 32) >> (32 - cbits)) : 0u;
                     rk[j] = atomicAdd(&bcnt[cb[j]], 1u);
                     t++;
                     w++;
