@@ -38,7 +38,7 @@ extern "C" {
 #define EC_ERR_CAPACITY (-5) /* table overflow that survived the retries                       */
 #define EC_ERR_STATE (-6)    /* result requested before a successful ec_assemble_*            */
 
-#define EC_MAX_K 63 /* k <= 32: 64-bit keys; 32 < k <= 63: 128-bit keys (general table) */
+#define EC_MAX_K 63 /* k <= 32: 64-bit keys; 32 < k <= 63: 128-bit keys */
 
 const char *ec_last_error(void);
 int ec_version(void); /* major*10000 + minor*100 + patch */
@@ -276,7 +276,7 @@ int ec_record_bytes(int k);
 /* graph phase (links .. GFA) on a complete solid set; results via ec_copy_* */
 int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags);
 
-/* partitioned graph phase (k <= 32), the multi-GPU form of ec_assemble_from_solid: every rank
+/* partitioned graph phase (any k; records of ec_record_bytes(k)), the multi-GPU form of ec_assemble_from_solid: every rank
  * loads the same all-gathered solid set (dense ids = position among the non-filler records,
  * so identical on every rank; ec_dense_count = U), computes the successor links of its own
  * canonical ids [lo, hi) (d_succ receives 2(hi-lo) uint32 oriented-node successors, node

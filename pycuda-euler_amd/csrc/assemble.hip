@@ -145,7 +145,8 @@ struct ec_session {
     DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur, cwalk;
     bool no_index = false;      // the call needs dense records only (shard count, owner merge)
     bool filt = false;          // phase_count: k_bucket_filt (more distinct keys than LDS tables hold)
-    SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load)
+    SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
+    SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
 };
 
@@ -777,9 +778,9 @@ int phase_load_det(ec_session *s, const Agg *d_agg, uint64_t n, unsigned int &U,
     unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk, *ids = s->nextR.as<unsigned int>();
     unsigned int tot = 0;
     if (n) {
-        k_det_count<<<nblk, 256, 0, st>>>(d_agg, n, bc);
+        k_det_count<Agg><<<nblk, 256, 0, st>>>(d_agg, n, bc);
         EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
-        k_det_ids<<<nblk, 256, 0, st>>>(d_agg, n, bs, ids);
+        k_det_ids<Agg><<<nblk, 256, 0, st>>>(d_agg, n, bs, ids);
         EC_HIP(hipMemcpyAsync(&tot, bs + nblk - 1, 4, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
     }
@@ -794,6 +795,60 @@ int phase_load_det(ec_session *s, const Agg *d_agg, uint64_t n, unsigned int &U,
         return EC_ERR_CAPACITY;
     }
     (void)dsc;
+    return EC_OK;
+}
+
+// the same for k > 32: dense arrays in gathered order, HBM lookup table (SolidIndexW)
+int phase_load_det_w(ec_session *s, const AggW *d_agg, uint64_t n, unsigned int &U, SolidIndexW &sidx) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int nblk = (unsigned int)std::max<uint64_t>((n + DET_CHUNK - 1) / DET_CHUNK, 1);
+    EC_CHECK(s->rbc.ensure((size_t)nblk * 8));
+    EC_CHECK(s->nextR.ensure(std::max<uint64_t>(n, 1) * 4));
+    unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk, *ids = s->nextR.as<unsigned int>();
+    unsigned int tot = 0;
+    if (n) {
+        k_det_count<AggW><<<nblk, 256, 0, st>>>(d_agg, n, bc);
+        EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
+        k_det_ids<AggW><<<nblk, 256, 0, st>>>(d_agg, n, bs, ids);
+        EC_HIP(hipMemcpyAsync(&tot, bs + nblk - 1, 4, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+    }
+    EC_CHECK(s->dkey.ensure(std::max<uint64_t>(tot, 1) * sizeof(K128)));
+    EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(tot, 1) * 4));
+    EC_CHECK(s->dfc.ensure(std::max<uint64_t>(tot, 1) * 8));
+    EC_CHECK(s->dft.ensure(std::max<uint64_t>(tot, 1) * 8));
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)(2.2 * (double)tot) + 1024) cap <<= 1;
+    for (int attempt = 0;; attempt++) {
+        EC_CHECK(s->table.ensure(cap * sizeof(SlotW)));
+        mark(s, 2 * EC_STAGE_COUNT);
+        k_table_clear_w<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<SlotW>(), cap);
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        if (n)
+            k_load_det_w<<<grid_for(n, B), B, 0, st>>>(d_agg, n, ids, s->table.as<SlotW>(), cap - 1, s->dkey.as<K128>(),
+                                                      s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                                      s->dft.as<unsigned long long>(), &dsc->overflow);
+        mark(s, 2 * EC_STAGE_COUNT + 1);
+        unsigned int of = 0;
+        EC_HIP(hipMemcpyAsync(&of, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (!of) break;
+        if (attempt >= 4) {
+            set_error("load table overflow at capacity %llu", (unsigned long long)cap);
+            return EC_ERR_CAPACITY;
+        }
+        cap <<= 2;
+        s->stats.table_retries++;
+    }
+    U = tot;
+    s->stats.n_distinct = tot;
+    s->stats.n_solid = tot;
+    s->stats.table_capacity = cap;
+    sidx.table = s->table.as<SlotW>();
+    sidx.capmask = cap - 1;
+    sidx.sub = nullptr;
     return EC_OK;
 }
 
@@ -1604,12 +1659,11 @@ int ec_graph_load(ec_session *s, const void *d_records, uint64_t n, int k, unsig
     }
     s->graph_loaded = false;
     EC_CHECK(begin_call(s, k, flags));
-    if (k > 32) {
-        set_error("partitioned graph phase needs k <= 32 (k=%d): use ec_assemble_from_solid", k);
-        return EC_ERR_ARG;
-    }
     unsigned int U = 0;
-    EC_CHECK(phase_load_det(s, reinterpret_cast<const Agg *>(d_records), n, U, s->gidx));
+    if (k > 32)
+        EC_CHECK(phase_load_det_w(s, reinterpret_cast<const AggW *>(d_records), n, U, s->gidxw));
+    else
+        EC_CHECK(phase_load_det(s, reinterpret_cast<const Agg *>(d_records), n, U, s->gidx));
     if (2ull * U >= (unsigned long long)CYC) {
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
@@ -1630,8 +1684,12 @@ int ec_graph_links_part(ec_session *s, uint64_t lo, uint64_t hi, uint32_t *d_suc
     EC_HIP(hipSetDevice(s->device));
     if (hi > lo) {
         const uint64_t n = 2 * (hi - lo);
-        k_links_part<Ops64, SolidIndex><<<grid_for(n, 256), 256, 0, s->stream>>>(
-            s->gidx, s->dkey.as<unsigned long long>(), (unsigned int)lo, (unsigned int)hi, s->k, d_succ);
+        if (s->k > 32)
+            k_links_part<OpsW, SolidIndexW><<<grid_for(n, 256), 256, 0, s->stream>>>(
+                s->gidxw, s->dkey.as<K128>(), (unsigned int)lo, (unsigned int)hi, s->k, d_succ);
+        else
+            k_links_part<Ops64, SolidIndex><<<grid_for(n, 256), 256, 0, s->stream>>>(
+                s->gidx, s->dkey.as<unsigned long long>(), (unsigned int)lo, (unsigned int)hi, s->k, d_succ);
         EC_HIP(hipGetLastError());
     }
     EC_HIP(hipStreamSynchronize(s->stream));
@@ -1650,6 +1708,7 @@ int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags) {
     for (float &v : s->stats.stage_ms) v = 0.0f;
     for (float &v : s->stats.kernel_ms) v = 0.0f;
     s->graph_loaded = false;
+    if (s->k > 32) return phase_graph<OpsW>(s, s->k, U, s->gidxw, d_succ);
     return phase_graph<Ops64>(s, s->k, U, s->gidx, d_succ);
 }
 

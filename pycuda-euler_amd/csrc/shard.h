@@ -207,11 +207,16 @@ struct AggDetSource {
 };
 
 constexpr unsigned int DET_CHUNK = 8192;
-__global__ void __launch_bounds__(256) k_det_count(const Agg *in, uint64_t n, unsigned int *bc) {
+// non-filler records (all-gather filler: all-ones bytes)
+__device__ inline bool det_valid(const Agg &r) { return r.key != EMPTY_KEY; }
+__device__ inline bool det_valid(const AggW &r) { return !(r.lo == ~0ull && r.hi == ~0ull); }
+
+template <typename R>
+__global__ void __launch_bounds__(256) k_det_count(const R *in, uint64_t n, unsigned int *bc) {
     const uint64_t c0 = (uint64_t)blockIdx.x * DET_CHUNK;
     const uint64_t c1 = c0 + DET_CHUNK < n ? c0 + DET_CHUNK : n;
     unsigned int v = 0;
-    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) v += in[i].key != EMPTY_KEY;
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) v += det_valid(in[i]);
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     __shared__ unsigned int ws[4];
     if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
@@ -219,7 +224,8 @@ __global__ void __launch_bounds__(256) k_det_count(const Agg *in, uint64_t n, un
     if (threadIdx.x == 0) bc[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 // bs = inclusive scan of the chunk counts; ids[i] = rank of record i among the non-fillers
-__global__ void __launch_bounds__(256) k_det_ids(const Agg *in, uint64_t n, const unsigned int *bs, unsigned int *ids) {
+template <typename R>
+__global__ void __launch_bounds__(256) k_det_ids(const R *in, uint64_t n, const unsigned int *bs, unsigned int *ids) {
     __shared__ unsigned int wsum[4];
     const uint64_t c0 = (uint64_t)blockIdx.x * DET_CHUNK;
     const uint64_t c1 = c0 + DET_CHUNK < n ? c0 + DET_CHUNK : n;
@@ -227,7 +233,7 @@ __global__ void __launch_bounds__(256) k_det_ids(const Agg *in, uint64_t n, cons
     const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint64_t i0 = c0; i0 < c1; i0 += blockDim.x) {
         const uint64_t i = i0 + threadIdx.x;
-        const bool valid = i < c1 && in[i].key != EMPTY_KEY;
+        const bool valid = i < c1 && det_valid(in[i]);
         const unsigned long long m = __ballot(valid);
         if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
         __syncthreads();
@@ -236,6 +242,31 @@ __global__ void __launch_bounds__(256) k_det_ids(const Agg *in, uint64_t n, cons
         if (i < c1) ids[i] = valid ? off + (unsigned int)__popcll(m & ((1ull << lane) - 1)) : NONE32;
         base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
         __syncthreads();
+    }
+}
+
+// partitioned graph phase for k > 32: record i of the gathered set -> dense id ids[i] (dense
+// arrays in gathered order) + the key's slot in the HBM lookup table (gathered keys are
+// distinct: one writer per slot)
+__global__ void __launch_bounds__(256) k_load_det_w(const AggW *in, uint64_t n, const unsigned int *ids, SlotW *table,
+                                                   uint64_t capmask, K128 *dkey, unsigned int *dcnt,
+                                                   unsigned long long *dfc, unsigned long long *dft,
+                                                   unsigned int *overflow) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int id = ids[t];
+        if (id == NONE32) continue;
+        const AggW a = in[t];
+        const K128 c{a.lo, a.hi};
+        dkey[id] = c;
+        dcnt[id] = a.count;
+        dfc[id] = a.fC;
+        dft[id] = a.fT;
+        SlotW *sl = wide_slot(table, capmask, c);
+        if (!sl) {
+            atomicOr(overflow, 1u);
+            continue;
+        }
+        sl->idx = id;
     }
 }
 

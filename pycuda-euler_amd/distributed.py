@@ -115,7 +115,7 @@ class HipEngine:
         eulerhip.check(self.L.ec_assemble_from_solid(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), flags))
         return self.sess.fetch(k)
 
-    # partitioned graph phase (k <= 32): ec_graph_load / ec_graph_links_part / ec_graph_finish
+    # partitioned graph phase: ec_graph_load / ec_graph_links_part / ec_graph_finish
     def graph_load(self, recs, k, flags=0):
         self.k = int(k)
         n = recs.numel() // self.rec_bytes()
@@ -198,13 +198,13 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     """Run steps 1-4 for this rank; returns (result, n_positions_total).  on_count(stats)
     receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING); phase_ms, a
     dict, receives the wall time of every step (device-synchronised by the engine calls).
-    partitioned (default: k <= 32): each rank computes the successor links of its own owner
+    partitioned (default, unless EC_FLAG_GENERAL): each rank computes the successor links of its own owner
     segment of the gathered solid set only ("each GPU builds its local graph partition");
     the parts are all-gathered and every rank ranks the paths and emits the contigs."""
     import time
 
     if partitioned is None:
-        partitioned = k <= 32 and hasattr(engine, "graph_load") and not (flags & eulerhip.EC_FLAG_GENERAL)
+        partitioned = hasattr(engine, "graph_load") and not (flags & eulerhip.EC_FLAG_GENERAL)
     marks = [("start", time.perf_counter())]
 
     def tick(name):
@@ -322,7 +322,7 @@ def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=N
     for i, x in enumerate(solids):
         allsolid[i * mx: i * mx + x.numel()] = x.to(engines[0].device)
     if partitioned is None:
-        partitioned = k <= 32 and not (flags & eulerhip.EC_FLAG_GENERAL)
+        partitioned = not (flags & eulerhip.EC_FLAG_GENERAL)
     if not partitioned:
         res = engines[0].assemble_from_solid(allsolid, k, flags)
         return res, P

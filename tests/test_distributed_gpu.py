@@ -114,7 +114,9 @@ def test_rccl_world1_sharded(engines):
 
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("seed,g,n,L,err,k", [(5, 50_000, 20_000, 100, 0.003, 31), (6, 4_000, 3_000, 60, 0.01, 20),
-                                              (7, 2_000, 800, 40, 0.0, 32)])
+                                              (7, 2_000, 800, 40, 0.0, 32),
+                                              # 128-bit keys: HBM lookup table with gathered-order ids
+                                              (8, 40_000, 12_000, 150, 0.002, 51), (9, 3_000, 2_000, 90, 0.0, 36)])
 def test_partitioned_links_equal_replicated(engines, world, seed, g, n, L, err, k):
     """ec_graph_load / ec_graph_links_part / ec_graph_finish (each simulated rank computes the
     links of its own owner segment, parts concatenated) == ec_assemble_from_solid == oracle"""
@@ -130,7 +132,8 @@ def test_partitioned_links_equal_replicated(engines, world, seed, g, n, L, err, 
         assert res.stats.n_dict == ref["n_dict"], partitioned
 
 
-def test_partitioned_links_part_ranges(engines):
+@pytest.mark.parametrize("k", [31, 47])
+def test_partitioned_links_part_ranges(engines, k):
     """the per-rank successor parts are independent of how the canonical ids are split"""
     import torch
 
@@ -140,10 +143,10 @@ def test_partitioned_links_part_ranges(engines):
     eng = engines[0]
     d_reads = torch.from_numpy(buf).cuda()
     d_off = torch.from_numpy(off.astype(np.int64)).cuda()
-    eng.count_shard(d_reads, d_off, len(off) - 1, 0, 31, 0)
+    eng.count_shard(d_reads, d_off, len(off) - 1, 0, k, 0)
     recs, counts = eng.export_by_owner(1)
-    solid = eng.merge_owned(recs, 31, 1, 0)
-    U = eng.graph_load(solid, 31)
+    solid = eng.merge_owned(recs, k, 1, 0)
+    U = eng.graph_load(solid, k)
     whole = eng.empty(8 * U)
     eng.graph_links_part(0, U, whole)
     cuts = [0, 1, U // 3, U // 2 + 7, U - 1, U]
@@ -153,6 +156,6 @@ def test_partitioned_links_part_ranges(engines):
         eng.graph_links_part(a, b, p)
         parts.append(p[: 8 * (b - a)])
     assert torch.equal(torch.cat(parts), whole[: 8 * U])
-    ref = oracle.assemble_packed(buf, off, 31, 1)
-    res = eng.graph_finish(whole[: 8 * U], 31)
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    res = eng.graph_finish(whole[: 8 * U], k)
     assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
