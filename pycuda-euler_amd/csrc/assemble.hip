@@ -414,9 +414,12 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     // partitioned path when every bucket fits an LDS table and local events fit 16 bits
     // error-rich inputs (distinct keys >> solid keys) use the seen-twice filter buckets when a
     // key seen once cannot be solid by count alone (limit >= 1), up to ~32 K distinct per bucket
-    const bool filt_ok = !sk && limit >= 1 && !getenv("EULERHIP_NO_FILTER");
+    // with limit < 1 (shard counts: no filter possible) the same kernel keeps every key and its
+    // two half tables alone double a bucket's capacity (to ~3600 keys)
+    const bool filt_ok = !sk && !getenv("EULERHIP_NO_FILTER");
+    const double filt_max = limit >= 1 ? 32768.0 : 3600.0;
     bool part = !(flags & EC_FLAG_GENERAL) && nreads && P && hsc.maxlocal <= MAX_LOCAL_EVENT && !hsc.skew &&
-                (est / FINE <= 2400.0 || (filt_ok && est / FINE <= 32768.0));
+                (est / FINE <= 2400.0 || (filt_ok && est / FINE <= filt_max));
     const bool filt = part && filt_ok && (est / FINE > 2400.0 || getenv("EULERHIP_FORCE_FILTER"));
     int bbits = 0;
     unsigned int slots = 2048;

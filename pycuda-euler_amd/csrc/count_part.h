@@ -909,8 +909,10 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
         }
         for (; i < r1; i += blockDim.x) fn(src.fetch(i));
     };
-    // pass 0: seen-twice filter
-    for_records([&](const typename Src::Raw &r) {
+    // pass 0: seen-twice filter (limit < 1: every key is kept, the half tables alone split the
+    // bucket -- the multi-GPU shard count, whose singletons may meet their twins on other ranks)
+    const bool filter = limit >= 1;
+    if (filter) for_records([&](const typename Src::Raw &r) {
         unsigned long long c, eC, eT;
         unsigned int add;
         src.decode(r, c, add, eC, eT);
@@ -929,9 +931,11 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
             src.decode(r, c, add, eC, eT);
             const uint64_t h = mix64(c);
             if (((unsigned int)(h >> 11) & 1u) != half) return;
-            const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
-            const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
-            if (!twice && (long long)add <= limit) return;
+            if (filter) {
+                const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
+                const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
+                if (!twice && (long long)add <= limit) return;
+            }
             lds_insert<SLOTS>(tab, s_over, c, (unsigned int)h, add, eC, eT);
         });
         lds_table_finish<SLOTS>(tab, s_over, 2 * b + half, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,

@@ -295,10 +295,10 @@ def test_filter_buckets_vs_oracle(gpu_session, monkeypatch, g, n, L, seed, err, 
 
 
 def test_filter_buckets_limits_vs_oracle(gpu_session, monkeypatch):
-    """limit >= 1 only (a key seen once can be solid by count alone otherwise); even k keeps
-    palindromes, whose single insert adds 2"""
+    """limit >= 1: seen-twice filter; limit < 1: no filter, the two half tables only; even k
+    keeps palindromes, whose single insert adds 2"""
     monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
-    for k, lim in ((15, 1), (15, 2), (16, 1), (20, 3), (31, 5)):
+    for k, lim in ((15, 1), (15, 2), (16, 1), (20, 3), (31, 5), (15, 0), (16, -1), (31, 0)):
         buf, off = make_reads(4_000, 3_000, 60, 500 + k + lim, err=0.01)
         ref, rc, rl = _oracle_packed(buf, off, k, lim)
         gpu_session.run_host(buf, off, k, lim)

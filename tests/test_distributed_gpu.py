@@ -159,3 +159,17 @@ def test_partitioned_links_part_ranges(engines, k):
     ref = oracle.assemble_packed(buf, off, k, 1)
     res = eng.graph_finish(whole[: 8 * U], k)
     assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_local_sharded_split_tables(engines, monkeypatch, world):
+    """shard counts (no solid filter) on the half-table buckets of k_bucket_filt, as taken when
+    a rank's distinct keys outgrow one LDS table per bucket (error-rich input)"""
+    import distributed
+
+    monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
+    buf, off = make_reads(40_000, 15_000, 100, 7600 + world, err=0.01, n_rate=0.001)
+    ref = oracle.assemble_packed(buf, off, 31, 1)
+    res, P = distributed.local_sharded_assemble(engines[:world], buf, off, 31, 1)
+    assert P == ref["n_positions"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)

@@ -19,13 +19,14 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--err", type=float, default=0.0, help="substitution rate (bench ecoli10m_err: 0.005)")
     a = ap.parse_args()
     import torch
 
     import distributed
     from synth import make_reads
 
-    buf, off = make_reads(4_600_000, a.reads, 100, 20261019)
+    buf, off = make_reads(4_600_000, a.reads, 100, 20261019, err=a.err)
     world = a.ranks
     engines = [distributed.HipEngine(0) for _ in range(world)]
     shards = []
