@@ -47,6 +47,9 @@ CONFIGS = {
     # erroneous k-mers occur once and fail the count > 1 solid filter)
     "ecoli10m_err": dict(genome=4_600_000, reads=10_000_000, read_len=100, k=31, seed=20261015 + 4, err=0.005,
                          name="ecoli-4.6Mbp-10Mx100bp-k31-err0.5pct"),
+    # a genome past one LDS table per bucket (5·10^7 solid 31-mers: buckets split into part tables)
+    "genome50m": dict(genome=50_000_000, reads=10_000_000, read_len=100, k=31, seed=20261015 + 6,
+                      name="synthetic-50Mbp-10Mx100bp-k31"),
     "tiny": dict(genome=50_000, reads=50_000, read_len=100, k=31, seed=7, name="tiny-50kbp-50kx100bp-k31"),
 }
 

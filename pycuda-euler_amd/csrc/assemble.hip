@@ -145,6 +145,9 @@ struct ec_session {
     DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur, cwalk;
     bool no_index = false;      // the call needs dense records only (shard count, owner merge)
     bool filt = false;          // phase_count: k_bucket_filt (more distinct keys than LDS tables hold)
+    int pmax = 1, pmin = 0;     // k_bucket_filt: 2^pmax part tables per bucket region
+    float part_keys = 1400.0f;  // k_bucket_filt: target keys per part table
+    DevBuf bnp;                 // k_bucket_filt: per-bucket part bits
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
@@ -312,10 +315,13 @@ int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long
     Scalars *dsc = s->scal.as<Scalars>();
     hipStream_t st = s->stream;
     if (s->filt) {  // error-rich input: seen-twice filter + two half tables per bucket
+        EC_CHECK(s->bnp.ensure(nb));
         k_bucket_filt<Src><<<nb, BUCKET_THREADS, 0, st>>>(
-            src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
-            s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(),
-            &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+            src, s->bstart.as<unsigned long long>(), limit, s->pmin, s->pmax, s->part_keys,
+            s->dkey.as<unsigned long long>(),
+            s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+            s->no_index ? nullptr : s->sub.as<SubSlot>(), s->bnp.as<uint8_t>(), &dsc->nsolid, &dsc->ndistinct,
+            &dsc->overflow);
         return EC_OK;
     }
     if (slots == 2048)
@@ -414,20 +420,27 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     // partitioned path when every bucket fits an LDS table and local events fit 16 bits
     // error-rich inputs (distinct keys >> solid keys) use the seen-twice filter buckets when a
     // key seen once cannot be solid by count alone (limit >= 1), up to ~32 K distinct per bucket
-    // with limit < 1 (shard counts: no filter possible) the same kernel keeps every key and its
-    // two half tables alone double a bucket's capacity (to ~3600 keys)
+    // k_bucket_filt also splits a bucket into up to 2^PMAX part tables (large genomes; with
+    // limit < 1 -- shard counts, no filter possible -- every key is kept)
+    constexpr int PMAX = 3;
     const bool filt_ok = !sk && !getenv("EULERHIP_NO_FILTER");
-    const double filt_max = limit >= 1 ? 32768.0 : 3600.0;
+    const double filt_max = limit >= 1 ? 32768.0 : PART_KEYS * (1 << PMAX);
     bool part = !(flags & EC_FLAG_GENERAL) && nreads && P && hsc.maxlocal <= MAX_LOCAL_EVENT && !hsc.skew &&
                 (est / FINE <= 2400.0 || (filt_ok && est / FINE <= filt_max));
     const bool filt = part && filt_ok && (est / FINE > 2400.0 || getenv("EULERHIP_FORCE_FILTER"));
+    int pmax = 1;  // part tables per bucket region: 2^pmax (filter mode)
+    while (pmax < PMAX && est / FINE / (double)(1 << pmax) > PART_KEYS) pmax++;
+    if (const char *e = getenv("EULERHIP_FILTER_PMAX")) pmax = std::max(1, std::min(PMAX, atoi(e)));
+    s->pmax = pmax;
+    s->part_keys = getenv("EULERHIP_PART_KEYS") ? (float)atof(getenv("EULERHIP_PART_KEYS")) : (float)PART_KEYS;
+    s->pmin = getenv("EULERHIP_FILTER_PMIN") ? std::max(0, std::min(pmax, atoi(getenv("EULERHIP_FILTER_PMIN")))) : 0;
     int bbits = 0;
     unsigned int slots = 2048;
     sidx = SolidIndex{};
     uint64_t umax = 0;
     if (part) {
         while (bbits < FINE_BITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
-        slots = (filt || est / (double)(1ull << bbits) > 1100.0) ? 4096u : 2048u;  // filter mode: 2 x 2048
+        slots = filt ? (2048u << pmax) : est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
         int maxc = MAX_COARSE_BITS;
         if (const char *e = getenv("EULERHIP_COARSE_BITS")) maxc = std::max(1, std::min(MAX_COARSE_BITS, atoi(e)));
         maxc = std::min(maxc, DS_MAX_CBITS);
@@ -574,7 +587,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             sidx.bbits = bbits;
             sidx.slots = slots;
             sidx.sk = sk ? 1 : 0;
-            sidx.split = filt ? 1 : 0;
+            sidx.npb = filt ? s->bnp.as<uint8_t>() : nullptr;
+            sidx.pmax = pmax;
             sidx.mc = mc;
             s->stats.count_path = sk ? EC_PATH_SUPERKMER : EC_PATH_PARTITIONED;
             s->stats.n_buckets = (uint32_t)Bk;
@@ -1398,7 +1412,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
-                     &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->rbc,
+                     &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->bnp, &s->rbc,
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk};
     for (auto *b : all) b->release();
     s->h_chars.release();

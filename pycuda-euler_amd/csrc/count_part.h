@@ -867,21 +867,26 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
                                        overflow);
 }
 
-// ---- error-rich inputs: more distinct k-mers per bucket than an LDS table holds ------------
-// With sequencing errors most distinct k-mers occur once (150 M distinct for 4.6 M solid at
-// 0.5 % substitutions, 10 M x 100 bp): a bucket's distinct keys outgrow the 2048-slot table
-// although its solid keys fit.  A key occurring once is solid only if its single insert adds
-// more than `limit` (an even-k palindrome adds 2), so the workgroup first builds a
-// "seen twice" filter over the bucket's records (two 2^18-cell bitmaps: cell bit set on the
-// second sighting, two cells per key -- no false negatives, ~2 % of the singletons leak),
-// then inserts the keys that passed, in two halves of the key space (hash bit 11) with one
-// table each; half h's table becomes sub-table region 2b + h (SolidIndex::split).
+// ---- buckets with more distinct k-mers than an LDS table holds -----------------------------
+// Two cases: error-rich inputs (most distinct k-mers occur once: 150 M distinct for 4.6 M solid
+// at 0.5 % substitutions, 10 M x 100 bp) and large genomes (> ~2·10^7 solid k-mers).  A key
+// occurring once is solid only if its single insert adds more than `limit` (an even-k
+// palindrome adds 2), so with limit >= 1 the workgroup first builds a "seen twice" filter over
+// the bucket's records (two 2^18-cell bitmaps: cell bit set on the second sighting, two cells
+// per key -- no false negatives, ~2 % of the singletons leak).  From the bitmap it estimates
+// the keys it will insert (linear counting over the set cells) and splits the bucket into
+// 2^pb parts by hash bits 11.. (pb <= pmax), one table pass each; part q's table becomes
+// sub-table region (b << pmax) + q, and bnp[b] = pb tells the lookup how the bucket was split
+// (SolidIndex::npb).  With limit < 1 (the multi-GPU shard count: singletons may meet their
+// twins on other ranks) every key is kept; the bitmap then only counts the distinct keys.
 constexpr int FILT_BITS = 18;
+constexpr double PART_KEYS = 1400.0;  // target keys per 2048-slot part table
 template <typename Src>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const unsigned long long *bstart,
-                                                               long long limit, unsigned long long *dkey,
+                                                               long long limit, int pmin, int pmax, float part_keys,
+                                                               unsigned long long *dkey,
                                                                unsigned int *dcnt, unsigned long long *dfc,
-                                                               unsigned long long *dft, SubSlot *sub,
+                                                               unsigned long long *dft, SubSlot *sub, uint8_t *bnp,
                                                                unsigned int *nsolid, unsigned long long *ndistinct,
                                                                unsigned int *overflow) {
     constexpr int SLOTS = 2048;
@@ -890,11 +895,13 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
     __shared__ LSlot tab[SLOTS];
     __shared__ unsigned int s_over[2];
     __shared__ unsigned int seen1[NW], seen2[NW];
+    __shared__ unsigned int s_cells, s_pb;
     const unsigned int b = blockIdx.x;
     for (unsigned int i = threadIdx.x; i < NW; i += blockDim.x) {
         seen1[i] = 0;
         seen2[i] = 0;
     }
+    if (threadIdx.x == 0) s_cells = 0;
     __syncthreads();
     const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
     constexpr int U = 4;  // records per thread per step, loads issued before any decode
@@ -909,28 +916,50 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
         }
         for (; i < r1; i += blockDim.x) fn(src.fetch(i));
     };
-    // pass 0: seen-twice filter (limit < 1: every key is kept, the half tables alone split the
-    // bucket -- the multi-GPU shard count, whose singletons may meet their twins on other ranks)
+    // pass 0: seen-twice filter (limit >= 1) or distinct-key bitmap (limit < 1)
     const bool filter = limit >= 1;
-    if (filter) for_records([&](const typename Src::Raw &r) {
+    for_records([&](const typename Src::Raw &r) {
         unsigned long long c, eC, eT;
         unsigned int add;
         src.decode(r, c, add, eC, eT);
         const uint64_t h = mix64(c);
         const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
         const unsigned int m1 = 1u << (c1 & 31), m2 = 1u << (c2 & 31);
-        if (atomicOr(&seen1[c1 >> 5], m1) & m1) atomicOr(&seen2[c1 >> 5], m1);
-        if (atomicOr(&seen1[c2 >> 5], m2) & m2) atomicOr(&seen2[c2 >> 5], m2);
+        if (filter) {
+            if (atomicOr(&seen1[c1 >> 5], m1) & m1) atomicOr(&seen2[c1 >> 5], m1);
+            if (atomicOr(&seen1[c2 >> 5], m2) & m2) atomicOr(&seen2[c2 >> 5], m2);
+        } else if (!(seen1[c1 >> 5] & m1)) {
+            atomicOr(&seen1[c1 >> 5], m1);
+        }
     });
     __syncthreads();
-    for (unsigned int half = 0; half < 2; half++) {
+    // keys to insert, by linear counting over the cells (filter: two cells per key)
+    {
+        unsigned int cells = 0;
+        const unsigned int *w = filter ? seen2 : seen1;
+        for (unsigned int i = threadIdx.x; i < NW; i += blockDim.x) cells += __popc(w[i]);
+        for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&s_cells, cells);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const double m = (double)(1u << FILT_BITS), set = (double)min(s_cells, (1u << FILT_BITS) - 1);
+            const double keys = -m * log(1.0 - set / m) / (filter ? 2.0 : 1.0);
+            unsigned int pb = (unsigned int)pmin;  // (pmin > 0: tests force the split)
+            while ((int)pb < pmax && keys / (double)(1u << pb) > (double)part_keys) pb++;
+            s_pb = pb;
+            if (bnp) bnp[b] = (uint8_t)pb;
+        }
+        __syncthreads();
+    }
+    const unsigned int pb = s_pb, pmask = (1u << pb) - 1;
+    for (unsigned int part = 0; part <= pmask; part++) {
         lds_table_init<SLOTS>(tab, s_over);
         for_records([&](const typename Src::Raw &r) {
             unsigned long long c, eC, eT;
             unsigned int add;
             src.decode(r, c, add, eC, eT);
             const uint64_t h = mix64(c);
-            if (((unsigned int)(h >> 11) & 1u) != half) return;
+            if (((unsigned int)(h >> 11) & pmask) != part) return;
             if (filter) {
                 const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
                 const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
@@ -938,9 +967,10 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
             }
             lds_insert<SLOTS>(tab, s_over, c, (unsigned int)h, add, eC, eT);
         });
-        lds_table_finish<SLOTS>(tab, s_over, 2 * b + half, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
-                                overflow);
+        lds_table_finish<SLOTS>(tab, s_over, (b << pmax) + part, limit, dkey, dcnt, dfc, dft, sub, nsolid,
+                                ndistinct, overflow);
         __syncthreads();
+        if (s_over[0]) break;  // overflow already reported: the call is redone on the HBM table
     }
 }
 

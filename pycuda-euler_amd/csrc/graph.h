@@ -18,16 +18,17 @@ struct SolidIndex {
     int bbits;
     unsigned int slots;  // sub-table slots per bucket (power of 2)
     int sk;              // buckets by minimizer (superkmer.h)
-    int split;           // k_bucket_filt layout: two half regions (hash bit 11), probing within one
+    const uint8_t *npb;  // k_bucket_filt layout: bucket b split into 2^npb[b] parts (hash bits 11..)
+    int pmax;            // of a region of 2^pmax part tables
     MinCfg mc;
     // (measured: a wave-uniform probe loop with 16-B key+id loads made k_neighbors 0.70 ->
     // 1.3 ms; the per-lane loop below lets the four neighbour lookups overlap)
     __device__ inline unsigned int find_in(uint64_t c, unsigned int h, uint64_t b) const {
         const SubSlot *r = sub + b * slots;
         unsigned int n = slots;
-        if (split) {
-            n = slots >> 1;
-            r += ((h >> 11) & 1u) * n;
+        if (npb) {
+            n = slots >> pmax;
+            r += ((h >> 11) & ((1u << npb[b]) - 1)) * n;
         }
         unsigned int slot = h & (n - 1);
         for (unsigned int probe = 0; probe < n; probe++) {

@@ -376,3 +376,20 @@ def test_wide_fallbacks_vs_oracle(gpu_session, monkeypatch):
             assert res.stats.table_retries >= 1
         assert res.stats.n_positions == ref["n_positions"]
         assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+@pytest.mark.parametrize("pmax,lim", [(2, 1), (3, 1), (3, 0), (2, -1)])
+def test_filter_bucket_parts_vs_oracle(gpu_session, monkeypatch, pmax, lim):
+    """buckets split into 2^pmax part tables (hash bits 11..; SolidIndex::npb), as for genomes
+    past ~2·10^7 solid k-mers, forced here on small inputs"""
+    monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
+    monkeypatch.setenv("EULERHIP_FILTER_PMAX", str(pmax))
+    monkeypatch.setenv("EULERHIP_FILTER_PMIN", str(pmax))
+    for k in (31, 22):
+        buf, off = make_reads(60_000, 20_000, 100, 900 + pmax + k, err=0.004, n_rate=0.001)
+        ref, rc, rl = _oracle_packed(buf, off, k, lim, True)
+        gpu_session.run_host(buf, off, k, lim, eulerhip.EC_FLAG_WANT_DICT)
+        res = gpu_session.fetch(k, True)
+        assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
+        assert res.contig_bytes == ref["contig_chars"] and res.links == rl, (k, pmax, lim)
+        assert [[x, c] for x, c in res.dict_items] == ref["d"]
