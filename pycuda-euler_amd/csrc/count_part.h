@@ -591,14 +591,17 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
 }
 
 // ---- bucket counting in LDS -------------------------------------------------------------
-struct alignas(16) LSlot {
-    unsigned long long key;
-    unsigned int count;
-    unsigned int pad;
-    unsigned long long fC;  // fC, fT 16-B aligned: one ds_read_b128 reads both
-    unsigned long long fT;
+// Structure of arrays, 32 B per slot.  (An array of 32-B slot structs put every key in one of
+// four bank positions: a wave's 64 random probes then queued on a few banks -- PMC: 5.3·10^8
+// LDS bank-conflict cycles in k_bucket.  Here consecutive slots' keys, counts and event pairs
+// sit in consecutive banks.)
+template <int SLOTS>
+struct LTab {
+    unsigned long long key[SLOTS];
+    ulonglong2 ev[SLOTS];  // first events fC, fT: one ds_read_b128 reads both
+    unsigned int count[SLOTS];
+    unsigned int id[SLOTS];  // dense id carried by the records (DET sources)
 };
-static_assert(sizeof(LSlot) == 32, "LDS slot layout");
 
 // record sources of k_bucket: window records of the counting pass, or exchange records
 // (count sum, first-event min) of the multi-GPU merge, visited through a bucket-major permutation
@@ -686,12 +689,11 @@ struct Rec12PSource : Rec12Decode<EVEN_K> {
 // and every probe sequence ends without a probe bound (a bounded loop costs the wave a
 // counter, a compare and an exec-mask juggle per probe).
 template <int SLOTS>
-__device__ inline void lds_table_init(LSlot *tab, unsigned int *s_over) {
+__device__ inline void lds_table_init(LTab<SLOTS> &tab, unsigned int *s_over) {
     for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
-        tab[i].key = EMPTY_KEY;
-        tab[i].count = 0;
-        tab[i].fC = NONE64;
-        tab[i].fT = NONE64;
+        tab.key[i] = EMPTY_KEY;
+        tab.count[i] = 0;
+        tab.ev[i] = make_ulonglong2(NONE64, NONE64);
     }
     if (threadIdx.x == 0) {
         s_over[0] = 0;
@@ -705,11 +707,11 @@ __device__ inline void lds_table_init(LSlot *tab, unsigned int *s_over) {
 // slot idle under one exec mask): almost every wave has some lane past its first probe, and a
 // per-lane loop with several exits costs ~40 scalar mask instructions per iteration.
 template <int SLOTS, bool DET = false>
-__device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
+__device__ inline void lds_insert(LTab<SLOTS> &tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
                                   unsigned int add, unsigned long long eC, unsigned long long eT,
                                   unsigned int id = 0) {
     unsigned int slot = slot0 & (SLOTS - 1);
-    unsigned long long cur = tab[slot].key;
+    unsigned long long cur = tab.key[slot];
     bool miss = cur != c;
 #pragma unroll 1
     while (__any(miss)) {
@@ -719,30 +721,30 @@ __device__ inline void lds_insert(LSlot *tab, unsigned int *s_over, unsigned lon
                     s_over[0] = 1;
                     cur = c;  // give up (updates below land in a discarded table)
                 } else {
-                    cur = atomicCAS(&tab[slot].key, EMPTY_KEY, c);
+                    cur = atomicCAS(&tab.key[slot], EMPTY_KEY, c);
                     if (cur == EMPTY_KEY) cur = c;  // claimed
                     else atomicSub(&s_over[1], 1u);  // lost the race: cur = the winner's key
                 }
             }
             if (cur != c) {
                 slot = (slot + 1) & (SLOTS - 1);
-                cur = tab[slot].key;
+                cur = tab.key[slot];
             }
             miss = cur != c;
         }
     }
-    LSlot &sl = tab[slot];
-    if (DET) sl.pad = id;  // distinct keys: one writer per slot
-    atomicAdd(&sl.count, add);
-    const ulonglong2 ev = *reinterpret_cast<const ulonglong2 *>(&sl.fC);
-    if (eC < ev.x) atomicMin(&sl.fC, eC);
-    if (eT < ev.y) atomicMin(&sl.fT, eT);
+    if (DET) tab.id[slot] = id;  // distinct keys: one writer per slot
+    atomicAdd(&tab.count[slot], add);
+    const ulonglong2 ev = tab.ev[slot];
+    if (eC < ev.x) atomicMin(&tab.ev[slot].x, eC);
+    if (eT < ev.y) atomicMin(&tab.ev[slot].y, eT);
 }
 
 // solid filter (count > limit, build:37-39) + compaction of bucket b's table into the dense
 // arrays (wave ballot, one global atomic per block) + the bucket's lookup sub-table
 template <int SLOTS, bool DET = false>
-__device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_over, unsigned int b, long long limit,
+__device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned int *s_over, unsigned int b,
+                                        long long limit,
                                         unsigned long long *dkey, unsigned int *dcnt, unsigned long long *dfc,
                                         unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
                                         unsigned long long *ndistinct, unsigned int *overflow) {
@@ -755,21 +757,21 @@ __device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int PER = SLOTS / BUCKET_THREADS;
-    if (DET) {  // dense ids given by the records (LSlot.pad): every present key is solid
+    if (DET) {  // dense ids given by the records (LTab::id): every present key is solid
         SubSlot *region = sub + (uint64_t)b * SLOTS;
         for (int q = 0; q < PER; q++) {
             const int i = threadIdx.x * PER + q;
-            const LSlot &sl = tab[i];
+            const unsigned long long key = tab.key[i];
             SubSlot o;
-            o.key = sl.key;
+            o.key = key;
             o.id = NONE32;
             o.pad = 0;
-            if (sl.key != EMPTY_KEY) {
-                const unsigned int u = sl.pad;
-                dkey[u] = sl.key;
-                dcnt[u] = sl.count;
-                dfc[u] = sl.fC;
-                dft[u] = sl.fT;
+            if (key != EMPTY_KEY) {
+                const unsigned int u = tab.id[i];
+                dkey[u] = key;
+                dcnt[u] = tab.count[i];
+                dfc[u] = tab.ev[i].x;
+                dft[u] = tab.ev[i].y;
                 o.id = u;
             }
             region[i] = o;
@@ -779,9 +781,10 @@ __device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_
     bool solid[PER];
     unsigned int mine = 0, present = 0;
     for (int q = 0; q < PER; q++) {
-        const LSlot &sl = tab[threadIdx.x * PER + q];
-        present += sl.key != EMPTY_KEY;
-        solid[q] = sl.key != EMPTY_KEY && (long long)sl.count > limit;
+        const int i = threadIdx.x * PER + q;
+        const bool here = tab.key[i] != EMPTY_KEY;
+        present += here;
+        solid[q] = here && (long long)tab.count[i] > limit;
         mine += solid[q];
     }
     // wave exclusive scan of `mine`
@@ -811,16 +814,15 @@ __device__ inline void lds_table_finish(const LSlot *tab, const unsigned int *s_
     SubSlot *region = sub + (uint64_t)b * SLOTS;
     for (int q = 0; q < PER; q++) {
         const int i = threadIdx.x * PER + q;
-        const LSlot &sl = tab[i];
         SubSlot o;
-        o.key = sl.key;
+        o.key = tab.key[i];
         o.id = NONE32;
         o.pad = 0;
         if (solid[q]) {
-            dkey[u] = sl.key;
-            dcnt[u] = sl.count;
-            dfc[u] = sl.fC;
-            dft[u] = sl.fT;
+            dkey[u] = o.key;
+            dcnt[u] = tab.count[i];
+            dfc[u] = tab.ev[i].x;
+            dft[u] = tab.ev[i].y;
             o.id = u;
             u++;
         }
@@ -835,7 +837,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
                                                           unsigned long long *dfc, unsigned long long *dft,
                                                           SubSlot *sub, unsigned int *nsolid,
                                                           unsigned long long *ndistinct, unsigned int *overflow) {
-    __shared__ LSlot tab[SLOTS];
+    __shared__ LTab<SLOTS> tab;
     __shared__ unsigned int s_over[2];
     const unsigned int b = blockIdx.x;
     lds_table_init<SLOTS>(tab, s_over);
@@ -892,7 +894,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
     constexpr int SLOTS = 2048;
     constexpr unsigned int NW = 1u << (FILT_BITS - 5);
     constexpr unsigned int CM = (1u << FILT_BITS) - 1;
-    __shared__ LSlot tab[SLOTS];
+    __shared__ LTab<SLOTS> tab;
     __shared__ unsigned int s_over[2];
     __shared__ unsigned int seen1[NW], seen2[NW];
     __shared__ unsigned int s_cells, s_pb;

@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_sk(const SkRec *recs,
     constexpr unsigned int NCH = (CH * 127 + 63) / 64 + 1;   // 64-window chunks of CH records
     constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
     constexpr unsigned int NW = BUCKET_THREADS / 64;
-    __shared__ LSlot tab[SLOTS];
+    __shared__ LTab<SLOTS> tab;
     __shared__ unsigned int s_over[2];
     __shared__ SkRec wrec[CH];
     __shared__ unsigned int wpre[CH + 1];
