@@ -238,6 +238,12 @@ def main():
             "traffic_source": (tr["file"] if tr else None),
             "kernel": kname, "kernel_ms": round(kms, 4), "alg_bytes_per_launch": int(kb),
             "kernels_ms": {eulerhip.KERNEL_NAMES[i]: round(float(kern[i]), 4) for i in range(len(kern))},
+            # every counting kernel against the same roofline (k_downsweep and k_refine run within
+            # a few % of each other on the headline, so the dominant one can change between runs)
+            "kernels_frac": {eulerhip.KERNEL_NAMES[i]: round(
+                kernel_alg_bytes(eulerhip.KERNEL_NAMES[i], int(st.n_positions), int(st.n_reads), L, K, rec,
+                                 int(st.n_records), nsub) / (float(kern[i]) / 1e3) / (HBM_PEAK_GBS * 1e9), 5)
+                for i in range(len(kern)) if kern[i] > 0},
             "pipeline_alg_bytes": int(alg_bytes(P, R, L, U, K)),
             "pipeline_frac": round(alg_bytes(P, R, L, U, K) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
     cpu = None
