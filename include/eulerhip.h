@@ -52,6 +52,8 @@ typedef struct ec_session ec_session;
 #define EC_FLAG_WIDE_RECORDS 8u /* partitioned path: 16-B window records only (default for k < 21 or
                                   * reads with N: 12-B records when every read is N-free and of one length) */
 #define EC_FLAG_WINDOW_RECORDS 16u /* partitioned path: one record per k-mer window, never super-k-mers */
+#define EC_FLAG_EXACT_COUNT 64u /* partitioned path: histogram-sized runs only (count_part.h), never the
+                                  * fixed-capacity runs of count_v2.h */
 #define EC_FLAG_SUPERKMER 32u /* partitioned path: super-k-mer records (minimizer buckets) where they apply:
                                 * 21 <= k <= 32, N-free reads (else window records) */
 
@@ -96,7 +98,8 @@ typedef struct {
     uint32_t count_path;     /* EC_PATH_*                                                     */
     uint32_t n_buckets;      /* partitioned path: B                                           */
     uint32_t record_bytes;   /* partitioned paths: 12 / 16 per window record, 32 per super-k-mer */
-    uint32_t reserved;
+    uint32_t count_variant;  /* partitioned path: 0 = histogram-sized runs (count_part.h),
+                              * 1 = fixed-capacity runs without the upsweep (count_v2.h)       */
     float stage_ms[EC_NSTAGES];   /* EC_FLAG_TIMING only */
     float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING only */
 } ec_stats;

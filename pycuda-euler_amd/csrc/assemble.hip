@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "count_part.h"
+#include "count_v2.h"
 #include "shard.h"
 #include "compact.h"
 #include "count_wide.h"
@@ -148,6 +149,8 @@ struct ec_session {
     int pmax = 1, pmin = 0;     // k_bucket_filt: 2^pmax part tables per bucket region
     float part_keys = 1400.0f;  // k_bucket_filt: target keys per part table
     DevBuf bnp;                 // k_bucket_filt: per-bucket part bits
+    const unsigned long long *bbeg = nullptr, *bend = nullptr;  // launch_bucket: explicit bucket bounds
+    DevBuf fcur, bb2;           // count_v2.h: final-bucket cursors, bucket bounds
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
@@ -314,10 +317,14 @@ template <typename Src>
 int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long limit) {
     Scalars *dsc = s->scal.as<Scalars>();
     hipStream_t st = s->stream;
+    // bucket b = records [bb[b], be[b]): the exact path's scanned starts, or the fixed-capacity
+    // buckets of count_v2.h (s->bbeg / s->bend set)
+    const unsigned long long *bb = s->bbeg ? s->bbeg : s->bstart.as<unsigned long long>();
+    const unsigned long long *be = s->bbeg ? s->bend : s->bstart.as<unsigned long long>() + 1;
     if (s->filt) {  // error-rich input: seen-twice filter + two half tables per bucket
         EC_CHECK(s->bnp.ensure(nb));
         k_bucket_filt<Src><<<nb, BUCKET_THREADS, 0, st>>>(
-            src, s->bstart.as<unsigned long long>(), limit, s->pmin, s->pmax, s->part_keys,
+            src, bb, be, limit, s->pmin, s->pmax, s->part_keys,
             s->dkey.as<unsigned long long>(),
             s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
             s->no_index ? nullptr : s->sub.as<SubSlot>(), s->bnp.as<uint8_t>(), &dsc->nsolid, &dsc->ndistinct,
@@ -326,14 +333,198 @@ int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long
     }
     if (slots == 2048)
         k_bucket<Src, 2048><<<nb, BUCKET_THREADS, 0, st>>>(
-            src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+            src, bb, be, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
             s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
             &dsc->ndistinct, &dsc->overflow);
     else
         k_bucket<Src, 4096><<<nb, BUCKET_THREADS, 0, st>>>(
-            src, s->bstart.as<unsigned long long>(), limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+            src, bb, be, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
             s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
             &dsc->ndistinct, &dsc->overflow);
+    return EC_OK;
+}
+
+// Bucket geometry of the partitioned path from the distinct estimate (shared by count_part.h's
+// exact path and count_v2.h): 2^bbits final buckets of <= ~1100 keys, 2048- or 4096-slot LDS
+// tables, or k_bucket_filt's seen-twice filter / part tables past ~2400 keys per bucket.
+struct BucketPlan {
+    bool part = false;  // partitioned counting applies at all (else the HBM table)
+    bool filt = false;
+    int pmax = 1;
+    int bbits = 0;
+    unsigned int slots = 2048;
+};
+BucketPlan plan_buckets(double est, long long limit, bool filt_ok) {
+    constexpr int PMAX = 3;
+    BucketPlan p;
+    const double filt_max = limit >= 1 ? 32768.0 : PART_KEYS * (1 << PMAX);
+    p.part = est / FINE <= 2400.0 || (filt_ok && est / FINE <= filt_max);
+    p.filt = p.part && filt_ok && (est / FINE > 2400.0 || getenv("EULERHIP_FORCE_FILTER"));
+    while (p.pmax < PMAX && est / FINE / (double)(1 << p.pmax) > PART_KEYS) p.pmax++;
+    if (const char *e = getenv("EULERHIP_FILTER_PMAX")) p.pmax = std::max(1, std::min(PMAX, atoi(e)));
+    while (p.bbits < FINE_BITS && est / (double)(1ull << p.bbits) > 1100.0) p.bbits++;
+    p.slots = p.filt ? (2048u << p.pmax) : est / (double)(1ull << p.bbits) > 1100.0 ? 4096u : 2048u;
+    return p;
+}
+
+// count_v2.h: the partitioned count of N-free reads of one length without the histogram
+// upsweep.  ok = false (and nothing decided) when the input does not qualify or a run / final
+// bucket outgrew its fixed capacity: phase_count then takes count_part.h's exact path.
+int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, uint64_t read_base,
+                   int k, long long limit, unsigned int &U, SolidIndex &sidx, bool &ok) {
+    ok = false;
+    hipStream_t st = s->stream;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    // read groups of whole 64-read wave tiles, at most 2048 (k_refine2 run tables)
+    const uint64_t ntiles = (nreads + 63) / 64;
+    uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, RF_MAX_RUNS));
+    const uint64_t gsize = ((ntiles + G - 1) / G) * 64;
+    G = (nreads + gsize - 1) / gsize;
+    mark(s, 2 * EC_STAGE_PRESCAN);
+    kmark(s, 0, 0);
+    k_prescan<<<(unsigned)G, 256, 0, st>>>(d_reads, d_off, nreads, k, gsize, &dsc->npos, &dsc->bad, dsc->lens);
+    kmark(s, 0, 1);
+    mark(s, 2 * EC_STAGE_PRESCAN + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.bad != ~0ull) {
+        uint8_t byte = 0;
+        hipMemcpy(&byte, d_reads + hsc.bad, 1, hipMemcpyDeviceToHost);
+        set_error("byte %llu (0x%02x) outside {A,C,G,T,N}", (unsigned long long)hsc.bad, byte);
+        return EC_ERR_ALPHABET;
+    }
+    const unsigned int lmax = hsc.lens[0], lmin = ~hsc.lens[1], lall = hsc.lens[3];
+    const uint64_t P = hsc.npos;
+    if (hsc.lens[2] || P == 0 || lmax != lmin) return EC_OK;  // N, no windows, several lengths
+    const uint32_t M = lmax - (uint32_t)k + 1;
+    int ibits = 1;
+    while ((1ull << ibits) < M) ibits++;
+    if (ibits > 15 || nreads + read_base > (1ull << (31 - ibits)) || 2ull * M - 1 > MAX_LOCAL_EVENT) return EC_OK;
+    const uint64_t need16 = (64ull * lall + 30 + 15) / 16;  // 16-B chunks of a 64-read wave tile
+    const int npf = need16 <= 4 * 64 ? 4 : need16 <= 7 * 64 ? 7 : need16 <= 10 * 64 ? 10 : 0;
+    if (!npf) return EC_OK;
+
+    // ---- partition into fixed-capacity (coarse bucket, group) runs -------------------------
+    constexpr uint64_t C = 1ull << PT_CBITS;
+    const uint64_t cap = (gsize * M * 5 / 4 + C - 1) / C + 128;
+    EC_CHECK(s->recs.ensure(C * G * cap * 12));
+    EC_CHECK(s->cnt.ensure(C * G * 4));
+    EC_CHECK(s->hll.ensure(G * (1 << HLL_REG_BITS)));
+    EC_CHECK(s->ftot.ensure((1 << HLL_REG_BITS) * 4));
+    unsigned long long *rkeys = s->recs.as<unsigned long long>();
+    unsigned int *rmeta = reinterpret_cast<unsigned int *>(rkeys + C * G * cap);
+    unsigned int *hreg = s->ftot.as<unsigned int>();
+    mark(s, 2 * EC_STAGE_COUNT);
+    kmark(s, 1, 0);
+#define EC_PARTITION(NPF, HI)                                                                                         \
+    k_partition<NPF, HI><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, k, M, gsize, (uint32_t)G, cap, \
+                                                              ibits, read_base, rkeys, rmeta, s->cnt.as<unsigned int>(), \
+                                                              s->hll.as<uint8_t>(), &dsc->overflow)
+    if (k >= 17) {
+        if (npf == 4) EC_PARTITION(4, true);
+        else if (npf == 7) EC_PARTITION(7, true);
+        else EC_PARTITION(10, true);
+    } else {
+        if (npf == 4) EC_PARTITION(4, false);
+        else if (npf == 7) EC_PARTITION(7, false);
+        else EC_PARTITION(10, false);
+    }
+#undef EC_PARTITION
+    kmark(s, 1, 1);
+    EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));
+    k_hll_merge<<<dim3((1 << HLL_REG_BITS) / 256, TOT_SLICES), 256, 0, st>>>(s->hll.as<uint8_t>(), G, hreg);
+    k_hll_final<<<1, 1024, 0, st>>>(hreg, HLL_REG_BITS, &dsc->est);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.overflow) return EC_OK;  // a run outgrew its capacity (extreme skew)
+    const double est = hsc.est;
+    BucketPlan plan = plan_buckets(est, limit, !getenv("EULERHIP_NO_FILTER"));
+    if (!plan.part) return EC_OK;
+    plan.bbits = std::max(plan.bbits, PT_CBITS);
+    const int bbits = plan.bbits;
+    const uint64_t Bk = 1ull << bbits;
+
+    // ---- refine into fixed-capacity final buckets -------------------------------------------
+    const uint64_t fcap = P * 5 / 4 / Bk + 1024;
+    EC_CHECK(s->recs2.ensure(Bk * fcap * 12));
+    EC_CHECK(s->fcur.ensure(Bk * 8));
+    EC_CHECK(s->bb2.ensure(Bk * 16));
+    EC_HIP(hipMemsetAsync(s->fcur.p, 0, Bk * 8, st));
+    unsigned rs = 8;
+    if (const char *e = getenv("EULERHIP_REFINE_RS")) rs = (unsigned)std::max(1, atoi(e));
+    rs = (unsigned)std::min<uint64_t>(rs, G);
+    kmark(s, 4, 0);
+    k_refine2<<<dim3((unsigned)C, rs), BUCKET_THREADS, 0, st>>>(rkeys, rmeta, s->cnt.as<unsigned int>(), (uint32_t)G,
+                                                               cap, bbits, s->recs2.as<unsigned int>(), fcap,
+                                                               s->fcur.as<unsigned long long>(), &dsc->skew);
+    kmark(s, 4, 1);
+    unsigned long long *bbeg = s->bb2.as<unsigned long long>(), *bend = bbeg + Bk;
+    k_fixed_bounds<<<grid_for(Bk, 256), 256, 0, st>>>(s->fcur.as<unsigned long long>(), Bk, fcap, bbeg, bend);
+    mark(s, 2 * EC_STAGE_COUNT + 1);
+
+    // ---- count buckets in LDS tables ----------------------------------------------------------
+    mark(s, 2 * EC_STAGE_COMPACT);
+    const uint64_t umax = Bk * plan.slots;
+    EC_CHECK(s->dkey.ensure(umax * 8));
+    EC_CHECK(s->dcnt.ensure(umax * 4));
+    EC_CHECK(s->dfc.ensure(umax * 8));
+    EC_CHECK(s->dft.ensure(umax * 8));
+    EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
+    s->pmax = plan.pmax;
+    s->part_keys = getenv("EULERHIP_PART_KEYS") ? (float)atof(getenv("EULERHIP_PART_KEYS")) : (float)PART_KEYS;
+    s->pmin = getenv("EULERHIP_FILTER_PMIN") ? std::max(0, std::min(plan.pmax, atoi(getenv("EULERHIP_FILTER_PMIN")))) : 0;
+    s->filt = plan.filt;
+    s->bbeg = bbeg;
+    s->bend = bend;
+    kmark(s, 2, 0);
+    const unsigned int m2 = 2 * M - 1;
+    int rc;
+    if (k & 1) {
+        Rec12PSource<false> src;
+        src.ibits = ibits, src.k = k, src.m2 = m2, src.p = s->recs2.as<unsigned int>();
+        rc = launch_bucket(s, src, (unsigned)Bk, plan.slots, limit);
+    } else {
+        Rec12PSource<true> src;
+        src.ibits = ibits, src.k = k, src.m2 = m2, src.p = s->recs2.as<unsigned int>();
+        rc = launch_bucket(s, src, (unsigned)Bk, plan.slots, limit);
+    }
+    s->filt = false;
+    s->bbeg = s->bend = nullptr;
+    EC_CHECK(rc);
+    kmark(s, 2, 1);
+    mark(s, 2 * EC_STAGE_COMPACT + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.overflow || hsc.skew) {  // a final bucket or an LDS table overflowed: redo on the exact path
+        EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
+        EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
+        s->stats.table_retries++;
+        return EC_OK;
+    }
+    ok = true;
+    s->stats.n_positions = P;
+    s->stats.n_distinct_est = (uint64_t)llround(est);
+    s->stats.record_bytes = sizeof(Rec12);
+    s->stats.n_records = P;
+    s->stats.count_path = EC_PATH_PARTITIONED;
+    s->stats.count_variant = 1;
+    s->stats.n_buckets = (uint32_t)Bk;
+    s->stats.table_capacity = umax;
+    sidx = SolidIndex{};
+    sidx.sub = s->sub.as<SubSlot>();
+    sidx.bbits = bbits;
+    sidx.slots = plan.slots;
+    sidx.sk = 0;
+    sidx.npb = plan.filt ? s->bnp.as<uint8_t>() : nullptr;
+    sidx.pmax = plan.pmax;
+    U = hsc.nsolid;
+    s->stats.n_distinct = hsc.ndistinct;
+    s->stats.n_solid = U;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
     return EC_OK;
 }
 
@@ -351,6 +542,14 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc;
+    if (!(flags & (EC_FLAG_GENERAL | EC_FLAG_WIDE_RECORDS | EC_FLAG_SUPERKMER | EC_FLAG_EXACT_COUNT)) && nreads &&
+        k <= 32 && !getenv("EULERHIP_NO_V2")) {
+        bool ok = false;
+        EC_CHECK(phase_count_v2(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok));
+        if (ok) return EC_OK;
+        EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
+        EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
+    }
 
     // ---- prescan = partition upsweep ------------------------------------------------------
     mark(s, 2 * EC_STAGE_PRESCAN);

@@ -831,8 +831,8 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
 }
 
 template <typename Src, int SLOTS>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsigned long long *bstart,
-                                                          long long limit,
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsigned long long *bbeg,
+                                                          const unsigned long long *bend, long long limit,
                                                           unsigned long long *dkey, unsigned int *dcnt,
                                                           unsigned long long *dfc, unsigned long long *dft,
                                                           SubSlot *sub, unsigned int *nsolid,
@@ -841,7 +841,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
     __shared__ unsigned int s_over[2];
     const unsigned int b = blockIdx.x;
     lds_table_init<SLOTS>(tab, s_over);
-    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
     // BK_UNROLL records per thread per step, all loads issued before the inserts: the loop
     // is bound by HBM latency, not bandwidth, without this memory-level parallelism
     constexpr int BK_UNROLL = 4;
@@ -884,8 +884,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
 constexpr int FILT_BITS = 18;
 constexpr double PART_KEYS = 1400.0;  // target keys per 2048-slot part table
 template <typename Src>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const unsigned long long *bstart,
-                                                               long long limit, int pmin, int pmax, float part_keys,
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const unsigned long long *bbeg,
+                                                               const unsigned long long *bend, long long limit, int pmin, int pmax, float part_keys,
                                                                unsigned long long *dkey,
                                                                unsigned int *dcnt, unsigned long long *dfc,
                                                                unsigned long long *dft, SubSlot *sub, uint8_t *bnp,
@@ -905,7 +905,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
     }
     if (threadIdx.x == 0) s_cells = 0;
     __syncthreads();
-    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
     constexpr int U = 4;  // records per thread per step, loads issued before any decode
     auto for_records = [&](auto &&fn) {
         uint64_t i = r0 + threadIdx.x;

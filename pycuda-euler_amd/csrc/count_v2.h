@@ -1,0 +1,471 @@
+// count_v2.h -- partitioned k-mer counting without the histogram upsweep (the default path of
+// build:25-42 for N-free reads of one length, k <= 32).
+//
+// count_part.h sizes every (coarse bucket, read group) run exactly from a per-window fine
+// histogram (k_upsweep: every window hashed and counted once more before the downsweep).  Here
+// the runs get a fixed capacity instead -- the placement hash is uniform, so a group's records
+// per coarse bucket stay within a few standard deviations of (its windows) / C -- and the pass
+// before the downsweep only has to read bytes:
+//
+//   k_prescan    per read group : SWAR alphabet / N check of the group's bytes, read lengths,
+//                                 windows (no hashing)
+//   k_partition  per read group : each WAVE independently stages 64 reads in its own LDS
+//                                 slice (the next tile's loads in flight in registers while it
+//                                 works), rolls 8 windows per lane per round, ranks them by
+//                                 coarse bucket with LDS atomics on its own counters, and
+//                                 stores bucket runs; a run of the (bucket, group) region is
+//                                 reserved by one LDS atomic on the workgroup cursor.  No
+//                                 workgroup barrier inside the loop.  Also the HyperLogLog
+//                                 registers (the distinct estimate sets the bucket count).
+//   k_refine2    per coarse bucket slice : the region runs -> final buckets of fixed capacity
+//                                 (packed 12-B records, one returning atomic per final bucket
+//                                 per tile)
+//   k_bucket     (count_part.h) per final bucket, unchanged
+//
+// Any run or final bucket past its capacity (extreme k-mer skew) is reported, and the call
+// is redone on count_part.h's exact path.
+#pragma once
+#include "count_part.h"
+
+namespace ec {
+
+constexpr int PT_WAVES = 4;                // waves per k_partition workgroup
+constexpr int PT_THREADS = 64 * PT_WAVES;
+constexpr int PT_W = 8;                    // windows per lane per round
+constexpr int PT_REC = 64 * PT_W;          // records per wave round
+constexpr int PT_CBITS = 5;                // coarse buckets (one lane each)
+constexpr int PT_MAX_NPF = 8;              // staged bytes per wave tile <= PT_MAX_NPF KiB
+
+// wave-scope ordering of LDS accesses between the lanes of one wave (LDS operations of a wave
+// execute in issue order; this only keeps the compiler from moving them across)
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// inclusive prefix sum over the 64 lanes of a wave (DPP row shifts + row broadcasts)
+__device__ inline unsigned int wave_incl_scan(unsigned int v) {
+    v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (unsigned int)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+// 0x80 in every zero byte of v, 0 elsewhere (exact per byte: no borrow between bytes)
+__device__ inline uint32_t zero_bytes(uint32_t v) {
+    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
+}
+// 0x80 in every byte of w that is A, C, G or T
+__device__ inline uint32_t acgt_bytes(uint32_t w) {
+    return zero_bytes(w ^ 0x41414141u) | zero_bytes(w ^ 0x43434343u) | zero_bytes(w ^ 0x47474747u) |
+           zero_bytes(w ^ 0x54545454u);
+}
+
+// ---- prescan: alphabet, N, lengths, windows per read group ---------------------------------
+// lens[0] = max length of reads with windows, lens[1] = ~min of those, lens[2] = some read
+// holds an 'N', lens[3] = max length of any read; *bad = first byte outside {A,C,G,T,N}
+__global__ void __launch_bounds__(256) k_prescan(const uint8_t *buf, const uint64_t *off, uint64_t nreads, int k,
+                                                 uint64_t gsize, unsigned long long *npos, unsigned long long *bad,
+                                                 unsigned int *lens) {
+    const uint64_t g = blockIdx.x;
+    const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
+    unsigned long long pos = 0;
+    unsigned int lmax = 0, lmin = 0xFFFFFFFFu, lall = 0, anyn = 0;
+    for (uint64_t r = g0 + threadIdx.x; r < g1; r += blockDim.x) {
+        const uint64_t len = off[r + 1] - off[r];
+        lall = max(lall, (unsigned int)min(len, (uint64_t)0xFFFFFFFFu));
+        if (len >= (uint64_t)k) {
+            lmax = max(lmax, (unsigned int)min(len, (uint64_t)0xFFFFFFFFu));
+            lmin = min(lmin, (unsigned int)min(len, (uint64_t)0xFFFFFFFFu));
+            pos += len - k + 1;
+        }
+    }
+    if (g1 > g0) {
+        const uint64_t b0 = off[g0], b1 = off[g1];
+        const uint64_t a0 = ((uint64_t)(buf + b0)) & ~15ull, a1 = (((uint64_t)(buf + b1)) + 15) & ~15ull;
+        const uint64_t n16 = (a1 - a0) >> 4, lo = (uint64_t)buf + b0, hi = (uint64_t)buf + b1;
+        const uint4 *src = reinterpret_cast<const uint4 *>(a0);
+        for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x) {
+            const uint4 v = src[i];
+            const uint64_t a = a0 + 16 * i;
+            uint32_t all = acgt_bytes(v.x) & acgt_bytes(v.y) & acgt_bytes(v.z) & acgt_bytes(v.w);
+            if (a < lo || a + 16 > hi) all = 0;  // partial chunk: byte by byte
+            if (all != 0x80808080u) {
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                for (int q = 0; q < 16; q++) {
+                    const uint64_t p = a + q;
+                    if (p < lo || p >= hi) continue;
+                    const uint32_t c = base_code((w[q >> 2] >> ((q & 3) * 8)) & 0xFFu);
+                    if (c == 4) anyn = 1;
+                    if (c == 5) atomicMin(bad, (unsigned long long)(p - (uint64_t)buf));
+                }
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        pos += __shfl_down(pos, o);
+        lmax = max(lmax, (unsigned int)__shfl_down(lmax, o));
+        lmin = min(lmin, (unsigned int)__shfl_down(lmin, o));
+        lall = max(lall, (unsigned int)__shfl_down(lall, o));
+        anyn |= (unsigned int)__shfl_down(anyn, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (pos) atomicAdd(npos, pos);
+        if (lmax) atomicMax(&lens[0], lmax);
+        if (lmin != 0xFFFFFFFFu) atomicMax(&lens[1], ~lmin);
+        if (anyn) atomicOr(&lens[2], 1u);
+        if (lall) atomicMax(&lens[3], lall);
+    }
+}
+
+// ---- partition: window records into fixed-capacity (coarse bucket, group) runs ------------
+// Every read with windows has exactly M windows and no N (k_prescan checked).  Record of
+// window w of read r: key = canonical code, meta = (read_base + r) << (ibits + 1) | o << ibits | w
+// (Rec12, count_part.h).  Region of (c, g): records [(c * G + g) * cap, + cap) of keys / meta.
+// cnt[c * G + g] = records stored there; a run past cap sets *overflow (nothing past cap is
+// written).  hll[g * 2^HLL_REG_BITS + j] = the group's HyperLogLog register j.
+template <int NPF, bool HI>
+__global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
+                                                          int k, uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
+                                                          int ibits, uint64_t read_base, unsigned long long *keys,
+                                                          unsigned int *meta, unsigned int *cnt, uint8_t *hll,
+                                                          unsigned int *overflow) {
+    constexpr int SB = NPF * 1024;
+    constexpr int C = 1 << PT_CBITS;
+    constexpr int NREG = 1 << HLL_REG_BITS;
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[PT_WAVES][SB + 32];
+    __shared__ unsigned long long s_key[PT_WAVES][PT_REC + 1];  // + a dummy slot for invalid windows
+    __shared__ unsigned int s_meta[PT_WAVES][PT_REC + 1];
+    __shared__ uint8_t s_tag[PT_WAVES][PT_REC + 1];
+    __shared__ unsigned int s_wcnt[PT_WAVES][C + 1];  // + a dummy counter
+    __shared__ unsigned int s_cur[C];
+    __shared__ unsigned int s_hll[NREG / 4];  // u8 registers, four per word
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) s_hll[i] = 0;
+    if (threadIdx.x < C) s_cur[threadIdx.x] = 0;
+    if (lane <= C) s_wcnt[wid][lane] = 0;
+    __syncthreads();
+    const uint64_t g = blockIdx.x;
+    const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
+    const uint32_t ntile = (uint32_t)((g1 - g0 + 63) / 64);
+    const uint64_t mask = kmask64(k);
+    const uint32_t mhi = (uint32_t)(mask >> 32);
+    const int sh = 2 * (k - 1);
+    uint64_t fwd = 0, rc = 0;
+    auto roll = [&](uint32_t b) {
+        if (HI) {
+            fwd = (fwd << 2) | b;
+            fwd &= ((uint64_t)mhi << 32) | 0xFFFFFFFFull;
+            rc = (rc >> 2) | ((uint64_t)((3u - b) << (sh - 32)) << 32);
+        } else {
+            fwd = ((fwd << 2) | b) & mask;
+            rc = (rc >> 2) | ((uint64_t)(3u - b) << sh);
+        }
+    };
+    // the next tile's bytes (in flight while the current tile is processed) and its reads
+    uint4 pf[NPF];
+    uint64_t nx_base = 0, nx_s = 0;
+    uint32_t nx_len = 0, nx_n16 = 0;
+    // (a macro, not a lambda: a lambda capturing pf keeps the array in scratch memory)
+#define EC_PT_ISSUE(T)                                                                                   \
+    do {                                                                                                 \
+        const uint64_t r0_ = g0 + 64ull * (T), r1_ = min(r0_ + 64, g1);                                  \
+        const uint64_t b0_ = off[r0_], b1_ = off[r1_];                                                    \
+        const uint64_t a0_ = ((uint64_t)(buf + b0_)) & ~15ull, a1_ = (((uint64_t)(buf + b1_)) + 15) & ~15ull; \
+        nx_n16 = (uint32_t)((a1_ - a0_) >> 4); /* <= NPF * 64: host checks 64 * max length + 45 */       \
+        const uint4 *src_ = reinterpret_cast<const uint4 *>(a0_);                                         \
+        _Pragma("unroll") for (int q = 0; q < NPF; q++) {                                                 \
+            const uint32_t i_ = q * 64 + lane;                                                            \
+            pf[q] = i_ < nx_n16 ? src_[i_] : make_uint4(0, 0, 0, 0);                                      \
+        }                                                                                                \
+        nx_base = a0_ - (uint64_t)buf;                                                                   \
+        const uint64_t r_ = r0_ + lane;                                                                  \
+        nx_s = r_ < r1_ ? off[r_] : 0;                                                                   \
+        nx_len = r_ < r1_ ? (uint32_t)(off[r_ + 1] - nx_s) : 0u;                                         \
+    } while (0)
+    if (wid < ntile) EC_PT_ISSUE(wid);
+    const unsigned long long gcap = g * cap, gstride = (unsigned long long)G * cap;
+    const uint32_t mbits = ibits + 1;
+    for (uint32_t t = wid; t < ntile; t += PT_WAVES) {
+        // stage this tile, then put the next one in flight
+        uint4 *dst = reinterpret_cast<uint4 *>(s_stage[wid]);
+#pragma unroll
+        for (int q = 0; q < NPF; q++) {
+            const uint32_t i = q * 64 + lane;
+            if (i < nx_n16) dst[i] = pf[q];
+        }
+        const uint64_t tbase = nx_base, s = nx_s;
+        const uint32_t len = nx_len;
+        const uint64_t r = g0 + 64ull * t + lane;
+        if (t + PT_WAVES < ntile) EC_PT_ISSUE(t + PT_WAVES);
+        wave_sync();
+        const bool has = len >= (uint32_t)k;  // then len - k + 1 == M
+        const uint32_t rel = has ? (uint32_t)(s - tbase) : 0u;
+        const uint32_t *sw = reinterpret_cast<const uint32_t *>(s_stage[wid]);
+        const uint32_t d0 = rel >> 2, bsh = rel & 3;
+        const uint32_t mhead = (uint32_t)((r + read_base) << mbits);
+        fwd = 0;
+        rc = 0;
+        // the first k - 1 bases, four per chunk (chunk q = read bytes 4q..4q+3)
+        for (uint32_t q = 0; 4 * q < (uint32_t)(k - 1); q++) {
+            const uint32_t c4 = __builtin_amdgcn_alignbyte(sw[d0 + q + 1], sw[d0 + q], bsh);
+            const uint32_t nb = min(4u, (uint32_t)(k - 1) - 4 * q);
+            for (uint32_t e = 0; e < nb; e++) roll(code2(c4 >> (8 * e)));
+        }
+        const uint32_t nrounds = __any(has) ? (M + PT_W - 1) / PT_W : 0u;
+        uint32_t w = 0, tb = (uint32_t)(k - 1);
+        for (uint32_t round = 0; round < nrounds; round++, tb += PT_W) {
+            // bases tb .. tb + 7 of every lane's read: four stage words, two alignbytes
+            const uint32_t q = tb >> 2, ts = tb & 3;
+            const uint32_t x0 = sw[d0 + q], x1 = sw[d0 + q + 1], x2 = sw[d0 + q + 2], x3 = sw[d0 + q + 3];
+            const uint32_t k0 = __builtin_amdgcn_alignbyte(x1, x0, bsh), k1 = __builtin_amdgcn_alignbyte(x2, x1, bsh),
+                           k2 = __builtin_amdgcn_alignbyte(x3, x2, bsh);
+            const uint32_t by[2] = {__builtin_amdgcn_alignbyte(k1, k0, ts), __builtin_amdgcn_alignbyte(k2, k1, ts)};
+            unsigned long long rkey[PT_W];
+            unsigned int rmeta[PT_W], rcb[PT_W], rhh[PT_W], rhw[PT_W];
+#pragma unroll
+            for (int j = 0; j < PT_W; j++) {
+                roll(code2(by[j >> 2] >> (8 * (j & 3))));
+                const bool tw = fwd > rc;
+                const uint64_t c = tw ? rc : fwd;
+                const uint32_t hh = (uint32_t)(mix64(c) >> 32);
+                const bool ok = has && w + j < M;
+                rkey[j] = c;
+                rmeta[j] = mhead | ((tw ? 1u : 0u) << ibits) | (w + j);
+                rcb[j] = ok ? hh >> (32 - PT_CBITS) : (uint32_t)C;  // C: a dummy counter
+                rhh[j] = hh;
+                atomicAdd(&s_wcnt[wid][rcb[j]], 1u);  // bucket sizes (no return value)
+                rhw[j] = s_hll[hh >> (32 - HLL_REG_BITS + 2)];
+            }
+            w += PT_W;
+            // HyperLogLog (count_part.h k_upsweep's registers, u8 max by CAS): rarely any update
+            bool upd = false;
+#pragma unroll
+            for (int j = 0; j < PT_W; j++) {
+                const uint32_t hj = rhh[j] >> (32 - HLL_REG_BITS);
+                const uint32_t rho = (uint32_t)__clz((int)((rhh[j] << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+                upd |= rcb[j] != (uint32_t)C && rho > ((rhw[j] >> ((hj & 3) * 8)) & 0xFFu);
+            }
+            if (__any(upd)) {
+#pragma unroll
+                for (int j = 0; j < PT_W; j++) {
+                    if (rcb[j] == (uint32_t)C) continue;
+                    const uint32_t hj = rhh[j] >> (32 - HLL_REG_BITS);
+                    const uint32_t rho =
+                        (uint32_t)__clz((int)((rhh[j] << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+                    const uint32_t hs = (hj & 3) * 8;
+                    uint32_t old = s_hll[hj >> 2];
+                    while (rho > ((old >> hs) & 0xFFu)) {
+                        const uint32_t nw = (old & ~(0xFFu << hs)) | (rho << hs);
+                        const uint32_t prev = atomicCAS(&s_hll[hj >> 2], old, nw);
+                        if (prev == old) break;
+                        old = prev;
+                    }
+                }
+            }
+            wave_sync();
+            // lane c < C: bucket c's count -> wave-local start, run reserved in the region of (c, g)
+            const unsigned int v = lane < (uint32_t)C ? s_wcnt[wid][lane] : 0u;
+            const unsigned int incl = wave_incl_scan(v);
+            const unsigned int total = __builtin_amdgcn_readlane(incl, C - 1);
+            const unsigned int beg = incl - v;
+            // counters restart at the bucket starts: the second round of adds returns positions
+            // (the dummy counter at PT_REC: invalid windows land in the dummy slot)
+            if (lane <= (uint32_t)C) s_wcnt[wid][lane] = lane < (uint32_t)C ? beg : (unsigned int)PT_REC;
+            unsigned int at = 0;
+            if (lane < (uint32_t)C && v) {
+                at = atomicAdd(&s_cur[lane], v);
+                if (at + v > cap) atomicOr(overflow, 1u);  // the records past cap are dropped
+            }
+            const int dl = (int)at - (int)beg;  // sorted index i of bucket c -> run position i + dl
+            wave_sync();
+            unsigned int pos[PT_W];
+#pragma unroll
+            for (int j = 0; j < PT_W; j++) pos[j] = min(atomicAdd(&s_wcnt[wid][rcb[j]], 1u), (unsigned int)PT_REC);
+#pragma unroll
+            for (int j = 0; j < PT_W; j++) {
+                s_key[wid][pos[j]] = rkey[j];
+                s_meta[wid][pos[j]] = rmeta[j];
+                s_tag[wid][pos[j]] = (uint8_t)rcb[j];
+            }
+            wave_sync();
+            if (lane <= (uint32_t)C) s_wcnt[wid][lane] = 0;
+            unsigned long long ok_[PT_W];
+            unsigned int om[PT_W], ot[PT_W];
+#pragma unroll
+            for (int qq = 0; qq < PT_W; qq++) {
+                const unsigned int i = qq * 64 + lane;
+                ot[qq] = s_tag[wid][i] & (C - 1);
+                ok_[qq] = s_key[wid][i];
+                om[qq] = s_meta[wid][i];
+            }
+#pragma unroll
+            for (int qq = 0; qq < PT_W; qq++) ot[qq] |= (unsigned int)((int)(qq * 64 + lane) + __shfl(dl, ot[qq])) << 8;
+#pragma unroll
+            for (int qq = 0; qq < PT_W; qq++) {
+                const unsigned int i = qq * 64 + lane;
+                const unsigned int tag = ot[qq] & 0xFFu, rp = ot[qq] >> 8;
+                if (i < total && rp < cap) {
+                    const unsigned long long idx = tag * gstride + gcap + rp;
+                    keys[idx] = ok_[qq];
+                    meta[idx] = om[qq];
+                }
+            }
+            wave_sync();
+        }
+    }
+#undef EC_PT_ISSUE
+    __syncthreads();
+    if (threadIdx.x < C) cnt[(uint64_t)threadIdx.x * G + g] = (unsigned int)min((uint64_t)s_cur[threadIdx.x], cap);
+    unsigned int *hw = reinterpret_cast<unsigned int *>(hll + g * NREG);
+    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) hw[i] = s_hll[i];
+}
+
+// HyperLogLog register maxima over the groups' u8 registers (grid: NREG / 256 x TOT_SLICES)
+__global__ void __launch_bounds__(256) k_hll_merge(const uint8_t *hll, uint64_t ngroups, unsigned int *hreg) {
+    const unsigned int f = blockIdx.x * blockDim.x + threadIdx.x;  // < 2^HLL_REG_BITS
+    unsigned int mx = 0;
+    for (uint64_t g = blockIdx.y; g < ngroups; g += gridDim.y) mx = max(mx, (unsigned int)hll[g * (1 << HLL_REG_BITS) + f]);
+    if (mx) atomicMax(&hreg[f], mx);
+}
+
+// ---- refine: region runs of one coarse bucket -> fixed-capacity final buckets ----------------
+// Workgroup (c, y) reads the runs of groups [G y / RS, G (y+1) / RS) of coarse bucket c as one
+// sequence (run table in LDS), sorts 4096-record tiles by final bucket in LDS and appends each
+// final bucket's run at a cursor reserved by one global atomic (fcur[b] counts records stored
+// in final bucket b, whose records are [b * fcap, b * fcap + fcur[b]) of `out`, packed 12 B).
+constexpr int RF_MAX_RUNS = 2048;
+__global__ void __launch_bounds__(BUCKET_THREADS) k_refine2(const unsigned long long *keys, const unsigned int *meta,
+                                                           const unsigned int *cnt, uint32_t G, uint64_t cap, int bbits,
+                                                           unsigned int *out, uint64_t fcap, unsigned long long *fcur,
+                                                           unsigned int *overflow) {
+    constexpr int TILE = REFINE_TILE;
+    constexpr int PER = TILE / BUCKET_THREADS;
+    __shared__ Rec12 tile[TILE];
+    __shared__ uint8_t tj[TILE];
+    __shared__ unsigned long long base[REFINE_FANOUT];
+    __shared__ unsigned int tcnt[REFINE_FANOUT], tbeg[REFINE_FANOUT], wsum[BUCKET_THREADS / 64];
+    __shared__ unsigned int lst[RF_MAX_RUNS + 1];  // run j of the slice = logical [lst[j], lst[j+1])
+    const int F = 1 << (bbits - PT_CBITS);
+    const uint64_t c = blockIdx.x;
+    const uint32_t ga = (uint32_t)((uint64_t)G * blockIdx.y / gridDim.y),
+                   gb = (uint32_t)((uint64_t)G * (blockIdx.y + 1) / gridDim.y);
+    const uint32_t nr = gb - ga;  // <= RF_MAX_RUNS (host)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // exclusive scan of the run lengths (two per thread)
+    {
+        const uint32_t i0 = 2 * threadIdx.x;
+        const unsigned int a = i0 < nr ? cnt[c * G + ga + i0] : 0u, b = i0 + 1 < nr ? cnt[c * G + ga + i0 + 1] : 0u;
+        unsigned int incl = a + b;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        unsigned int before = 0;
+        for (int q = 0; q < wid; q++) before += wsum[q];
+        const unsigned int ex = before + incl - (a + b);
+        if (i0 <= nr) lst[i0] = ex;
+        if (i0 + 1 <= nr) lst[i0 + 1] = ex + a;
+        __syncthreads();
+    }
+    const uint64_t N = lst[nr];
+    const unsigned long long cbase = c * (unsigned long long)G * cap;
+    auto phys = [&](uint32_t jrun, uint64_t l) { return cbase + (uint64_t)(ga + jrun) * cap + (l - lst[jrun]); };
+    uint32_t j0 = 0;  // run holding the tile's first record (wave-uniform: every thread tracks it)
+    for (uint64_t t0 = 0; t0 < N; t0 += TILE) {
+        while (j0 + 1 < nr && lst[j0 + 1] <= t0) j0++;
+        const unsigned int n = (unsigned int)min((uint64_t)TILE, N - t0);
+        if (threadIdx.x < REFINE_FANOUT) tcnt[threadIdx.x] = 0;
+        __syncthreads();
+        Rec12 rr[PER];
+        unsigned int jj[PER], rk[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                const uint64_t l = t0 + i;
+                uint32_t jr = j0;
+                while (lst[jr + 1] <= l) jr++;
+                const uint64_t p = phys(jr, l);
+                const unsigned long long kk = keys[p];
+                rr[q].klo = (unsigned int)kk;
+                rr[q].khi = (unsigned int)(kk >> 32);
+                rr[q].meta = meta[p];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                jj[q] = rec_bucket(rr[q], bbits) & (F - 1);
+                rk[q] = atomicAdd(&tcnt[jj[q]], 1u);
+            }
+        }
+        __syncthreads();
+        unsigned long long mybase = 0;
+        unsigned int myv = 0;
+        if (threadIdx.x < REFINE_FANOUT) {
+            const unsigned int v = (int)threadIdx.x < F ? tcnt[threadIdx.x] : 0u;
+            unsigned int incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int u = __shfl_up(incl, o);
+                if (lane >= o) incl += u;
+            }
+            tbeg[threadIdx.x] = incl - v;
+            if (lane == 63) wsum[wid] = incl;
+            myv = v;
+            if (v) mybase = atomicAdd(&fcur[c * F + threadIdx.x], (unsigned long long)v);
+        }
+        __syncthreads();
+        if (threadIdx.x >= 64 && threadIdx.x < REFINE_FANOUT) {
+            unsigned int add = 0;
+            for (int w = 0; w < (int)(threadIdx.x >> 6); w++) add += wsum[w];
+            tbeg[threadIdx.x] += add;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                const unsigned int p = tbeg[jj[q]] + rk[q];
+                tile[p] = rr[q];
+                tj[p] = (uint8_t)jj[q];
+            }
+        }
+        if (threadIdx.x < REFINE_FANOUT) {
+            if (mybase + myv > fcap) atomicOr(overflow, 1u);  // the records past fcap are dropped
+            base[threadIdx.x] = (c * F + threadIdx.x) * fcap + mybase;
+            tcnt[threadIdx.x] = mybase < fcap ? (unsigned int)min<unsigned long long>(fcap - mybase, 0xFFFFFFFFull) : 0u;
+        }
+        __syncthreads();
+        for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
+            const unsigned int j = tj[i];
+            const unsigned int q = i - tbeg[j];
+            if (q < tcnt[j]) {
+                const uint64_t o = base[j] + q;
+                const Rec12 r = tile[i];
+                out[3 * o] = r.klo;
+                out[3 * o + 1] = r.khi;
+                out[3 * o + 2] = r.meta;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// k_bucket bounds of the fixed-capacity final buckets: records [b * fcap, b * fcap + fcur[b])
+__global__ void __launch_bounds__(256) k_fixed_bounds(const unsigned long long *fcur, uint64_t nb, uint64_t fcap,
+                                                      unsigned long long *bbeg, unsigned long long *bend) {
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+        bbeg[b] = b * fcap;
+        bend[b] = b * fcap + min((uint64_t)fcur[b], fcap);
+    }
+}
+
+}  // namespace ec

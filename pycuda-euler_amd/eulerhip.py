@@ -34,6 +34,7 @@ EC_FLAG_GENERAL = 4
 EC_FLAG_WIDE_RECORDS = 8
 EC_FLAG_WINDOW_RECORDS = 16
 EC_FLAG_SUPERKMER = 32
+EC_FLAG_EXACT_COUNT = 64
 EC_NSTAGES = 8
 EC_NKERNELS = 5
 KERNEL_NAMES = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
@@ -72,7 +73,7 @@ class Stats(ctypes.Structure):
         ("count_path", ctypes.c_uint32),
         ("n_buckets", ctypes.c_uint32),
         ("record_bytes", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("count_variant", ctypes.c_uint32),
         ("stage_ms", ctypes.c_float * EC_NSTAGES),
         ("kernel_ms", ctypes.c_float * EC_NKERNELS),
     ]
@@ -281,11 +282,12 @@ class Session:
         return Result(k, st, chars[:nch], coff, loff, links[:nl], items)
 
     def assemble(self, reads, k, limit=1, want_dict=False, timing=False, general=False, wide_records=False,
-                 window_records=False, superkmer=False):
+                 window_records=False, superkmer=False, exact_count=False):
         buf, off = pack_reads(reads)
         flags = (EC_FLAG_WANT_DICT if want_dict else 0) | (EC_FLAG_TIMING if timing else 0)
         flags |= (EC_FLAG_GENERAL if general else 0) | (EC_FLAG_WIDE_RECORDS if wide_records else 0)
         flags |= (EC_FLAG_WINDOW_RECORDS if window_records else 0) | (EC_FLAG_SUPERKMER if superkmer else 0)
+        flags |= EC_FLAG_EXACT_COUNT if exact_count else 0
         self.run_host(buf, off, k, limit, flags)
         return self.fetch(k, want_dict)
 

@@ -78,6 +78,16 @@ def test_golden_wide_records(gpu_session, case):
 
 
 @pytest.mark.parametrize("case", CASES32[::2], ids=[c["name"] for c in CASES32[::2]])
+def test_golden_exact_count(gpu_session, case):
+    """count_part.h's histogram-sized runs forced (EC_FLAG_EXACT_COUNT)"""
+    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, exact_count=True)
+    assert [[x, c] for x, c in res.dict_items] == case["d"]
+    assert res.contigs == case["contigs"]
+    assert res.links == case["links"]
+    assert res.stats.count_variant == 0
+
+
+@pytest.mark.parametrize("case", CASES32[::2], ids=[c["name"] for c in CASES32[::2]])
 def test_golden_general_path(gpu_session, case):
     res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, general=True)
     assert [[x, c] for x, c in res.dict_items] == case["d"]
@@ -122,14 +132,15 @@ SYN = [
 ]
 
 
-@pytest.mark.parametrize("mode", ["partitioned", "superkmer", "window_records", "wide_records", "general"])
+@pytest.mark.parametrize("mode", ["partitioned", "exact", "superkmer", "window_records", "wide_records", "general"])
 @pytest.mark.parametrize("g,n,L,seed,err,nr,circ,k", SYN)
 def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode):
     buf, off = make_reads(g, n, L, 1000 + seed, err=err, n_rate=nr, circular=circ)
     want_dict = g <= 50_000
     ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
     flags = (eulerhip.EC_FLAG_WANT_DICT if want_dict else 0) | {
-        "partitioned": 0, "general": eulerhip.EC_FLAG_GENERAL, "wide_records": eulerhip.EC_FLAG_WIDE_RECORDS,
+        "partitioned": 0, "exact": eulerhip.EC_FLAG_EXACT_COUNT,
+        "general": eulerhip.EC_FLAG_GENERAL, "wide_records": eulerhip.EC_FLAG_WIDE_RECORDS,
         "window_records": eulerhip.EC_FLAG_WINDOW_RECORDS, "superkmer": eulerhip.EC_FLAG_SUPERKMER}[mode]
     gpu_session.run_host(buf, off, k, 1, flags)
     res = gpu_session.fetch(k, want_dict)
@@ -151,6 +162,11 @@ def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode)
         assert res.stats.count_path in (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_GENERAL)
     if mode == "wide_records" and k <= 32:
         assert res.stats.record_bytes == 16
+    # one read length, no N, k <= 32: the fixed-capacity runs of count_v2.h unless asked otherwise
+    if mode in ("partitioned", "window_records") and k <= 32 and nr == 0:
+        assert res.stats.count_variant == 1 and res.stats.record_bytes == 12
+    if mode == "exact":
+        assert res.stats.count_variant == 0
 
 
 def test_limits_vs_oracle(gpu_session):
@@ -393,3 +409,58 @@ def test_filter_bucket_parts_vs_oracle(gpu_session, monkeypatch, pmax, lim):
         assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
         assert res.contig_bytes == ref["contig_chars"] and res.links == rl, (k, pmax, lim)
         assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+# ---- fixed-capacity runs (count_v2.h) ----------------------------------------------------------
+@pytest.mark.parametrize("k", [11, 16, 21, 31, 32])
+def test_v2_skew_falls_back_vs_oracle(gpu_session, k):
+    """tandem repeats and homopolymers of one length: heavy keys overfill a (bucket, group) run or
+    a final bucket; the call is redone on the exact path with the same results"""
+    reads = _low_complexity_reads(3000, 100, 70 + k)
+    d, r, g = oracle.assemble(reads, k, 1)
+    res = gpu_session.assemble(reads, k, 1, want_dict=True)
+    assert res.stats.count_path in (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_GENERAL)
+    assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g
+
+
+@pytest.mark.parametrize("L,k", [(40, 11), (63, 31), (100, 17), (111, 27), (150, 31), (159, 32), (200, 31)])
+def test_v2_read_lengths_vs_oracle(gpu_session, L, k):
+    """wave tiles of 64 reads staged in 4, 7 or 10 KiB per wave; longer reads take the exact path"""
+    buf, off = make_reads(40_000, 9_000 - 30 * L, L, 3000 + L + k, err=0.003)
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(k, True)
+    assert res.stats.count_variant == (1 if L <= 159 else 0)
+    assert res.stats.n_positions == ref["n_positions"]
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+@pytest.mark.parametrize("pmax,lim", [(2, 1), (3, 0)])
+def test_v2_filter_parts_vs_oracle(gpu_session, monkeypatch, pmax, lim):
+    """seen-twice filter + part tables over the fixed-capacity final buckets"""
+    monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
+    monkeypatch.setenv("EULERHIP_FILTER_PMAX", str(pmax))
+    monkeypatch.setenv("EULERHIP_FILTER_PMIN", str(pmax))
+    buf, off = make_reads(60_000, 20_000, 100, 950 + pmax, err=0.004)
+    ref, rc, rl = _oracle_packed(buf, off, 31, lim, True)
+    gpu_session.run_host(buf, off, 31, lim, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(31, True)
+    assert res.stats.count_variant == 1
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+def test_v2_read_base_and_short_reads_vs_oracle(gpu_session):
+    """reads shorter than k (any length) beside one windowed length; a non-multiple-of-64 count"""
+    rng = np.random.default_rng(5)
+    g = "".join("ACGT"[x] for x in rng.integers(0, 4, 20_000))
+    reads = []
+    for i in range(7_777):
+        L = 90 if rng.random() < 0.8 else int(rng.integers(0, 31))
+        p = int(rng.integers(0, len(g) - L))
+        reads.append(g[p:p + L])
+    d, r, gl = oracle.assemble(reads, 31, 1)
+    res = gpu_session.assemble(reads, 31, 1, want_dict=True)
+    assert res.stats.count_variant == 1
+    assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == gl
