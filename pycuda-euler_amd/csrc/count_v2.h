@@ -123,25 +123,39 @@ __global__ void __launch_bounds__(256) k_prescan(const uint8_t *buf, const uint6
 }
 
 // ---- partition: window records into fixed-capacity (coarse bucket, group) runs ------------
+// 4 ASCII bases (A C G T) -> 8 bits, base i at bits 2i (code2 of window.h, no table)
+__device__ inline uint32_t pack4(uint32_t w) {
+    const uint32_t x = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
+    const uint32_t y = x | (x >> 6);
+    return (y | (y >> 12)) & 0xFFu;
+}
+__device__ inline uint32_t pack16(const uint4 &v) {
+    return pack4(v.x) | (pack4(v.y) << 8) | (pack4(v.z) << 16) | (pack4(v.w) << 24);
+}
+
 // Every read with windows has exactly M windows and no N (k_prescan checked).  Record of
 // window w of read r: key = canonical code, meta = (read_base + r) << (ibits + 1) | o << ibits | w
-// (Rec12, count_part.h).  Region of (c, g): records [(c * G + g) * cap, + cap) of keys / meta.
-// cnt[c * G + g] = records stored there; a run past cap sets *overflow (nothing past cap is
-// written).  hll[g * 2^HLL_REG_BITS + j] = the group's HyperLogLog register j.
+// (Rec12, count_part.h).  Region of (c, g): records [(c * G + g) * cap, + cap) of keys / meta;
+// records [C * G * cap, + PT_REC) take the stores of a run past its capacity (*overflow is set
+// and the call is redone on the exact path).  cnt[c * G + g] = records stored in the region.
+// HyperLogLog over the keys whose low hash bits & smask are 0 (a 1 / (smask + 1) sample of the
+// key space): hll[g * 2^HLL_REG_BITS + j] = the group's register j.
+// The wave tile's bytes are staged 2 bits per base (word i = bases 16i .. 16i+15 of the tile).
 template <int NPF, bool HI>
 __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                           int k, uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
-                                                          int ibits, uint64_t read_base, unsigned long long *keys,
-                                                          unsigned int *meta, unsigned int *cnt, uint8_t *hll,
-                                                          unsigned int *overflow) {
-    constexpr int SB = NPF * 1024;
+                                                          int ibits, uint64_t read_base, uint32_t smask,
+                                                          unsigned long long *keys, unsigned int *meta,
+                                                          unsigned int *cnt, uint8_t *hll, unsigned int *overflow) {
     constexpr int C = 1 << PT_CBITS;
     constexpr int NREG = 1 << HLL_REG_BITS;
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[PT_WAVES][SB + 32];
+    constexpr int SW = NPF * 64 + 4;  // staged words per wave (+ reads past the last base)
+    __shared__ uint32_t s_stage[PT_WAVES][SW];
     __shared__ unsigned long long s_key[PT_WAVES][PT_REC + 1];  // + a dummy slot for invalid windows
     __shared__ unsigned int s_meta[PT_WAVES][PT_REC + 1];
     __shared__ uint8_t s_tag[PT_WAVES][PT_REC + 1];
-    __shared__ unsigned int s_wcnt[PT_WAVES][C + 1];  // + a dummy counter
+    __shared__ unsigned long long s_base[PT_WAVES][C];  // store index of sorted record 0 of bucket c
+    __shared__ unsigned int s_wcnt[PT_WAVES][C + 1];    // + a dummy counter
     __shared__ unsigned int s_cur[C];
     __shared__ unsigned int s_hll[NREG / 4];  // u8 registers, four per word
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -169,18 +183,18 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
     // the next tile's bytes (in flight while the current tile is processed) and its reads
     uint4 pf[NPF];
     uint64_t nx_base = 0, nx_s = 0;
-    uint32_t nx_len = 0, nx_n16 = 0;
+    uint32_t nx_len = 0;
     // (a macro, not a lambda: a lambda capturing pf keeps the array in scratch memory)
 #define EC_PT_ISSUE(T)                                                                                   \
     do {                                                                                                 \
         const uint64_t r0_ = g0 + 64ull * (T), r1_ = min(r0_ + 64, g1);                                  \
         const uint64_t b0_ = off[r0_], b1_ = off[r1_];                                                    \
         const uint64_t a0_ = ((uint64_t)(buf + b0_)) & ~15ull, a1_ = (((uint64_t)(buf + b1_)) + 15) & ~15ull; \
-        nx_n16 = (uint32_t)((a1_ - a0_) >> 4); /* <= NPF * 64: host checks 64 * max length + 45 */       \
+        const uint32_t n16_ = (uint32_t)((a1_ - a0_) >> 4); /* <= NPF * 64: host checks */              \
         const uint4 *src_ = reinterpret_cast<const uint4 *>(a0_);                                         \
         _Pragma("unroll") for (int q = 0; q < NPF; q++) {                                                 \
             const uint32_t i_ = q * 64 + lane;                                                            \
-            pf[q] = i_ < nx_n16 ? src_[i_] : make_uint4(0, 0, 0, 0);                                      \
+            pf[q] = i_ < n16_ ? src_[i_] : make_uint4(0, 0, 0, 0);                                        \
         }                                                                                                \
         nx_base = a0_ - (uint64_t)buf;                                                                   \
         const uint64_t r_ = r0_ + lane;                                                                  \
@@ -189,71 +203,58 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
     } while (0)
     if (wid < ntile) EC_PT_ISSUE(wid);
     const unsigned long long gcap = g * cap, gstride = (unsigned long long)G * cap;
+    const unsigned long long spill = (unsigned long long)C * gstride;
     const uint32_t mbits = ibits + 1;
+    uint32_t *st = s_stage[wid];
     for (uint32_t t = wid; t < ntile; t += PT_WAVES) {
-        // stage this tile, then put the next one in flight
-        uint4 *dst = reinterpret_cast<uint4 *>(s_stage[wid]);
+        // stage this tile 2 bits per base, then put the next one in flight
 #pragma unroll
-        for (int q = 0; q < NPF; q++) {
-            const uint32_t i = q * 64 + lane;
-            if (i < nx_n16) dst[i] = pf[q];
-        }
+        for (int q = 0; q < NPF; q++) st[q * 64 + lane] = pack16(pf[q]);
         const uint64_t tbase = nx_base, s = nx_s;
         const uint32_t len = nx_len;
         const uint64_t r = g0 + 64ull * t + lane;
         if (t + PT_WAVES < ntile) EC_PT_ISSUE(t + PT_WAVES);
         wave_sync();
         const bool has = len >= (uint32_t)k;  // then len - k + 1 == M
-        const uint32_t rel = has ? (uint32_t)(s - tbase) : 0u;
-        const uint32_t *sw = reinterpret_cast<const uint32_t *>(s_stage[wid]);
-        const uint32_t d0 = rel >> 2, bsh = rel & 3;
+        const uint32_t rel = has ? (uint32_t)(s - tbase) : 0u;  // the read's first base in the tile
         const uint32_t mhead = (uint32_t)((r + read_base) << mbits);
+        // bases p .. p + 15 of the tile, base p + i at bits 2i
+        auto bases16 = [&](uint32_t p) { return __builtin_amdgcn_alignbit(st[(p >> 4) + 1], st[p >> 4], 2 * (p & 15)); };
         fwd = 0;
         rc = 0;
-        // the first k - 1 bases, four per chunk (chunk q = read bytes 4q..4q+3)
-        for (uint32_t q = 0; 4 * q < (uint32_t)(k - 1); q++) {
-            const uint32_t c4 = __builtin_amdgcn_alignbyte(sw[d0 + q + 1], sw[d0 + q], bsh);
-            const uint32_t nb = min(4u, (uint32_t)(k - 1) - 4 * q);
-            for (uint32_t e = 0; e < nb; e++) roll(code2(c4 >> (8 * e)));
+        {
+            const uint32_t x0 = bases16(rel), x1 = bases16(rel + 16);
+            for (uint32_t tb = 0; tb < (uint32_t)(k - 1); tb++)
+                roll(tb < 16 ? (x0 >> (2 * tb)) & 3u : (x1 >> (2 * (tb - 16))) & 3u);
         }
         const uint32_t nrounds = __any(has) ? (M + PT_W - 1) / PT_W : 0u;
         uint32_t w = 0, tb = (uint32_t)(k - 1);
         for (uint32_t round = 0; round < nrounds; round++, tb += PT_W) {
-            // bases tb .. tb + 7 of every lane's read: four stage words, two alignbytes
-            const uint32_t q = tb >> 2, ts = tb & 3;
-            const uint32_t x0 = sw[d0 + q], x1 = sw[d0 + q + 1], x2 = sw[d0 + q + 2], x3 = sw[d0 + q + 3];
-            const uint32_t k0 = __builtin_amdgcn_alignbyte(x1, x0, bsh), k1 = __builtin_amdgcn_alignbyte(x2, x1, bsh),
-                           k2 = __builtin_amdgcn_alignbyte(x3, x2, bsh);
-            const uint32_t by[2] = {__builtin_amdgcn_alignbyte(k1, k0, ts), __builtin_amdgcn_alignbyte(k2, k1, ts)};
+            const uint32_t xb = bases16(rel + tb);
             unsigned long long rkey[PT_W];
-            unsigned int rmeta[PT_W], rcb[PT_W], rhh[PT_W], rhw[PT_W];
+            unsigned int rmeta[PT_W], rcb[PT_W], rhh[PT_W];
+            unsigned int smp = 0;  // windows whose key is in the HyperLogLog sample
 #pragma unroll
             for (int j = 0; j < PT_W; j++) {
-                roll(code2(by[j >> 2] >> (8 * (j & 3))));
+                roll((xb >> (2 * j)) & 3u);
                 const bool tw = fwd > rc;
                 const uint64_t c = tw ? rc : fwd;
-                const uint32_t hh = (uint32_t)(mix64(c) >> 32);
+                const uint64_t h = mix64(c);
+                const uint32_t hh = (uint32_t)(h >> 32);
                 const bool ok = has && w + j < M;
                 rkey[j] = c;
                 rmeta[j] = mhead | ((tw ? 1u : 0u) << ibits) | (w + j);
                 rcb[j] = ok ? hh >> (32 - PT_CBITS) : (uint32_t)C;  // C: a dummy counter
                 rhh[j] = hh;
+                smp |= (ok && ((uint32_t)h & smask) == 0) ? 1u << j : 0u;
                 atomicAdd(&s_wcnt[wid][rcb[j]], 1u);  // bucket sizes (no return value)
-                rhw[j] = s_hll[hh >> (32 - HLL_REG_BITS + 2)];
             }
             w += PT_W;
-            // HyperLogLog (count_part.h k_upsweep's registers, u8 max by CAS): rarely any update
-            bool upd = false;
-#pragma unroll
-            for (int j = 0; j < PT_W; j++) {
-                const uint32_t hj = rhh[j] >> (32 - HLL_REG_BITS);
-                const uint32_t rho = (uint32_t)__clz((int)((rhh[j] << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
-                upd |= rcb[j] != (uint32_t)C && rho > ((rhw[j] >> ((hj & 3) * 8)) & 0xFFu);
-            }
-            if (__any(upd)) {
+            // HyperLogLog registers (count_part.h k_upsweep's rho), u8 max by CAS
+            if (__any(smp)) {
 #pragma unroll
                 for (int j = 0; j < PT_W; j++) {
-                    if (rcb[j] == (uint32_t)C) continue;
+                    if (!((smp >> j) & 1u)) continue;
                     const uint32_t hj = rhh[j] >> (32 - HLL_REG_BITS);
                     const uint32_t rho =
                         (uint32_t)__clz((int)((rhh[j] << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
@@ -276,12 +277,16 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
             // counters restart at the bucket starts: the second round of adds returns positions
             // (the dummy counter at PT_REC: invalid windows land in the dummy slot)
             if (lane <= (uint32_t)C) s_wcnt[wid][lane] = lane < (uint32_t)C ? beg : (unsigned int)PT_REC;
-            unsigned int at = 0;
-            if (lane < (uint32_t)C && v) {
-                at = atomicAdd(&s_cur[lane], v);
-                if (at + v > cap) atomicOr(overflow, 1u);  // the records past cap are dropped
+            if (lane < (uint32_t)C) {
+                unsigned int at = 0;
+                if (v) at = atomicAdd(&s_cur[lane], v);
+                unsigned long long b0 = lane * gstride + gcap + at - beg;
+                if (at + v > cap) {  // past the capacity: stores go to the spill records, call redone
+                    atomicOr(overflow, 1u);
+                    b0 = spill - beg;
+                }
+                s_base[wid][lane] = b0;
             }
-            const int dl = (int)at - (int)beg;  // sorted index i of bucket c -> run position i + dl
             wave_sync();
             unsigned int pos[PT_W];
 #pragma unroll
@@ -294,23 +299,20 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
             }
             wave_sync();
             if (lane <= (uint32_t)C) s_wcnt[wid][lane] = 0;
-            unsigned long long ok_[PT_W];
-            unsigned int om[PT_W], ot[PT_W];
+            unsigned long long ok_[PT_W], ob[PT_W];
+            unsigned int om[PT_W];
 #pragma unroll
             for (int qq = 0; qq < PT_W; qq++) {
                 const unsigned int i = qq * 64 + lane;
-                ot[qq] = s_tag[wid][i] & (C - 1);
+                ob[qq] = s_base[wid][s_tag[wid][i] & (C - 1)];
                 ok_[qq] = s_key[wid][i];
                 om[qq] = s_meta[wid][i];
             }
 #pragma unroll
-            for (int qq = 0; qq < PT_W; qq++) ot[qq] |= (unsigned int)((int)(qq * 64 + lane) + __shfl(dl, ot[qq])) << 8;
-#pragma unroll
             for (int qq = 0; qq < PT_W; qq++) {
                 const unsigned int i = qq * 64 + lane;
-                const unsigned int tag = ot[qq] & 0xFFu, rp = ot[qq] >> 8;
-                if (i < total && rp < cap) {
-                    const unsigned long long idx = tag * gstride + gcap + rp;
+                if (i < total) {
+                    const unsigned long long idx = ob[qq] + i;
                     keys[idx] = ok_[qq];
                     meta[idx] = om[qq];
                 }
