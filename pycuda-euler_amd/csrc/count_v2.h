@@ -88,9 +88,8 @@ __global__ void __launch_bounds__(256) k_prescan(const uint8_t *buf, const uint6
         const uint64_t b0 = off[g0], b1 = off[g1];
         const uint64_t a0 = ((uint64_t)(buf + b0)) & ~15ull, a1 = (((uint64_t)(buf + b1)) + 15) & ~15ull;
         const uint64_t n16 = (a1 - a0) >> 4, lo = (uint64_t)buf + b0, hi = (uint64_t)buf + b1;
-        const uint4 *src = reinterpret_cast<const uint4 *>(a0);
-        for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x) {
-            const uint4 v = src[i];
+        const uint4 *src = reinterpret_cast<const uint4 *>(buf + b0 - (((uint64_t)(buf + b0)) & 15));
+        auto check = [&](const uint4 &v, uint64_t i) {
             const uint64_t a = a0 + 16 * i;
             uint32_t all = acgt_bytes(v.x) & acgt_bytes(v.y) & acgt_bytes(v.z) & acgt_bytes(v.w);
             if (a < lo || a + 16 > hi) all = 0;  // partial chunk: byte by byte
@@ -104,7 +103,18 @@ __global__ void __launch_bounds__(256) k_prescan(const uint8_t *buf, const uint6
                     if (c == 5) atomicMin(bad, (unsigned long long)(p - (uint64_t)buf));
                 }
             }
+        };
+        // eight 16-B loads per thread in flight before any check
+        constexpr int U = 8;
+        uint64_t i = threadIdx.x;
+        for (; i + (U - 1) * blockDim.x < n16; i += U * blockDim.x) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = src[i + u * blockDim.x];
+#pragma unroll
+            for (int u = 0; u < U; u++) check(v[u], i + u * blockDim.x);
         }
+        for (; i < n16; i += blockDim.x) check(src[i], i);
     }
     for (int o = 32; o > 0; o >>= 1) {
         pos += __shfl_down(pos, o);
@@ -142,7 +152,8 @@ __device__ inline uint32_t pack16(const uint4 &v) {
 // key space): hll[g * 2^HLL_REG_BITS + j] = the group's register j.
 // The wave tile's bytes are staged 2 bits per base (word i = bases 16i .. 16i+15 of the tile).
 template <int NPF, bool HI>
-__global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
+__global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restrict__ buf,
+                                                          const uint64_t *__restrict__ off, uint64_t nreads,
                                                           int k, uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
                                                           int ibits, uint64_t read_base, uint32_t smask,
                                                           unsigned long long *keys, unsigned int *meta,
@@ -158,7 +169,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
     __shared__ unsigned int s_wcnt[PT_WAVES][C + 1];    // + a dummy counter
     __shared__ unsigned int s_cur[C];
     __shared__ unsigned int s_hll[NREG / 4];  // u8 registers, four per word
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar tile loads
     for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) s_hll[i] = 0;
     if (threadIdx.x < C) s_cur[threadIdx.x] = 0;
     if (lane <= C) s_wcnt[wid][lane] = 0;
@@ -182,24 +194,25 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
     };
     // the next tile's bytes (in flight while the current tile is processed) and its reads
     uint4 pf[NPF];
-    uint64_t nx_base = 0, nx_s = 0;
-    uint32_t nx_len = 0;
+    uint64_t nx_base = 0;
+    uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
     // (a macro, not a lambda: a lambda capturing pf keeps the array in scratch memory)
 #define EC_PT_ISSUE(T)                                                                                   \
     do {                                                                                                 \
         const uint64_t r0_ = g0 + 64ull * (T), r1_ = min(r0_ + 64, g1);                                  \
-        const uint64_t b0_ = off[r0_], b1_ = off[r1_];                                                    \
-        const uint64_t a0_ = ((uint64_t)(buf + b0_)) & ~15ull, a1_ = (((uint64_t)(buf + b1_)) + 15) & ~15ull; \
-        const uint32_t n16_ = (uint32_t)((a1_ - a0_) >> 4); /* <= NPF * 64: host checks */              \
-        const uint4 *src_ = reinterpret_cast<const uint4 *>(a0_);                                         \
-        _Pragma("unroll") for (int q = 0; q < NPF; q++) {                                                 \
-            const uint32_t i_ = q * 64 + lane;                                                            \
-            pf[q] = i_ < n16_ ? src_[i_] : make_uint4(0, 0, 0, 0);                                        \
-        }                                                                                                \
-        nx_base = a0_ - (uint64_t)buf;                                                                   \
-        const uint64_t r_ = r0_ + lane;                                                                  \
-        nx_s = r_ < r1_ ? off[r_] : 0;                                                                   \
-        nx_len = r_ < r1_ ? (uint32_t)(off[r_ + 1] - nx_s) : 0u;                                         \
+        const uint64_t b0_ = off[r0_], b1_ = off[r1_]; /* wave-uniform: scalar loads */                  \
+        const uint8_t *p0_ = buf + b0_ - (((uint64_t)(buf + b0_)) & 15); /* derived from buf: global */  \
+        const uint64_t a1_ = (((uint64_t)(buf + b1_)) + 15) & ~15ull;                                      \
+        const uint32_t n16_ = (uint32_t)((a1_ - (uint64_t)p0_) >> 4); /* <= NPF * 64: host checks */    \
+        const uint4 *src_ = reinterpret_cast<const uint4 *>(p0_);                                         \
+        _Pragma("unroll") for (int q = 0; q < NPF; q++)                                                   \
+            pf[q] = src_[min(q * 64 + lane, n16_ - 1)]; /* in bounds: no branch around the load */       \
+        nx_base = (uint64_t)p0_ - (uint64_t)buf;                                                         \
+        /* low words of the read's offsets (differences mod 2^32; no wait until they are used) */       \
+        const uint64_t ri_ = min(r0_ + lane, r1_ - 1);                                                   \
+        nx_s = reinterpret_cast<const uint32_t *>(off)[2 * ri_];                                         \
+        nx_e = reinterpret_cast<const uint32_t *>(off)[2 * ri_ + 2];                                     \
+        nx_n = (uint32_t)(r1_ - r0_);                                                                    \
     } while (0)
     if (wid < ntile) EC_PT_ISSUE(wid);
     const unsigned long long gcap = g * cap, gstride = (unsigned long long)G * cap;
@@ -210,13 +223,13 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
         // stage this tile 2 bits per base, then put the next one in flight
 #pragma unroll
         for (int q = 0; q < NPF; q++) st[q * 64 + lane] = pack16(pf[q]);
-        const uint64_t tbase = nx_base, s = nx_s;
-        const uint32_t len = nx_len;
+        const uint32_t tbase = (uint32_t)nx_base, s = nx_s;
+        const uint32_t len = lane < nx_n ? nx_e - nx_s : 0u;
         const uint64_t r = g0 + 64ull * t + lane;
-        if (t + PT_WAVES < ntile) EC_PT_ISSUE(t + PT_WAVES);
+        const bool more = t + PT_WAVES < ntile;
         wave_sync();
         const bool has = len >= (uint32_t)k;  // then len - k + 1 == M
-        const uint32_t rel = has ? (uint32_t)(s - tbase) : 0u;  // the read's first base in the tile
+        const uint32_t rel = has ? s - tbase : 0u;  // the read's first base in the tile
         const uint32_t mhead = (uint32_t)((r + read_base) << mbits);
         // bases p .. p + 15 of the tile, base p + i at bits 2i
         auto bases16 = [&](uint32_t p) { return __builtin_amdgcn_alignbit(st[(p >> 4) + 1], st[p >> 4], 2 * (p & 15)); };
@@ -228,6 +241,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
                 roll(tb < 16 ? (x0 >> (2 * tb)) & 3u : (x1 >> (2 * (tb - 16))) & 3u);
         }
         const uint32_t nrounds = __any(has) ? (M + PT_W - 1) / PT_W : 0u;
+        if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
         uint32_t w = 0, tb = (uint32_t)(k - 1);
         for (uint32_t round = 0; round < nrounds; round++, tb += PT_W) {
             const uint32_t xb = bases16(rel + tb);
@@ -250,6 +264,9 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *buf, co
                 atomicAdd(&s_wcnt[wid][rcb[j]], 1u);  // bucket sizes (no return value)
             }
             w += PT_W;
+            // the next tile's loads go out in the last round (their wait at the next tile then
+            // does not also wait for a whole tile of stores)
+            if (round + 1 == nrounds && more) EC_PT_ISSUE(t + PT_WAVES);
             // HyperLogLog registers (count_part.h k_upsweep's rho), u8 max by CAS
             if (__any(smp)) {
 #pragma unroll
