@@ -63,21 +63,32 @@ def alg_bytes(P, R, L, U, K=8):
     return R * L + P * (K + 8) + U * (10 * K + 33)
 
 
-def kernel_alg_bytes(name, P, R, L, K=8, rec=16, NR=None, nsub=0):
-    """Algorithmic bytes per launch of the counting kernels (DESIGN.md "Roofline accounting").
-    Window records (rec = 16, or 12 for compact records; NR = P records):
-    k_upsweep   reads the ASCII reads once                          R*L
-    k_downsweep reads them again + writes one record/position       R*L + rec*P
-    k_refine    reads every record, writes it again (same size)     2*rec*P
-    k_bucket    one canonical insert per position      P*(K+8)
-    k_count     general path: read once + one insert/position       R*L + P*(K+8)
-    Super-k-mer records (rec = 32, NR records, nsub = bucket sub-table bytes written):
+def kernel_alg_bytes(name, P, R, L, K=8, rec=16, NR=None, nsub=0, rec2=None):
+    """HBM bytes per launch of the counting kernels, from the algorithm's data movement
+    (DESIGN.md "Roofline accounting"; kernel names by slot, see kernel_names()).
+    Window records (rec = 16, 12 or 10 bytes written by the partition pass, rec2 = bytes of the
+    refine's output records, NR = P records, nsub = bucket sub-table bytes written):
+    k_upsweep / k_prescan     reads the ASCII reads once                      R*L
+    k_downsweep / k_partition reads them again + writes one record/position   R*L + rec*P
+    k_refine / k_refine2      reads every record, writes it to its bucket     (rec + rec2)*P
+    k_bucket                  reads every record, writes the sub-tables       rec2*P + nsub
+    k_count     general path: read once + one insert per position R*L + P*(K+8)
+    Super-k-mer records (rec = 32, NR records):
     k_downsweep R*L + 32*NR;  k_refine 64*NR;  k_bucket 32*NR + nsub"""
     if rec == 32:
         return {"k_upsweep": R * L, "k_downsweep": R * L + 32 * NR, "k_bucket": 32 * NR + nsub,
                 "k_count": R * L + P * (K + 8), "k_refine": 64 * NR}[name]
-    return {"k_upsweep": R * L, "k_downsweep": R * L + rec * P, "k_bucket": P * (K + 8),
-            "k_count": R * L + P * (K + 8), "k_refine": 2 * rec * P}[name]
+    rec2 = rec2 or rec
+    return {"k_upsweep": R * L, "k_downsweep": R * L + rec * P, "k_bucket": rec2 * P + nsub,
+            "k_count": R * L + P * (K + 8), "k_refine": (rec + rec2) * P}[name]
+
+
+def kernel_names(variant):
+    """kernel names of the ec_stats.kernel_ms slots: count_part.h's exact path (variant 0) or
+    count_v2.h's fixed-capacity runs (variants 1, 2)"""
+    if variant:
+        return ("k_prescan", "k_partition", "k_bucket", "k_count", "k_refine2")
+    return ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
 
 
 def cpu_baseline(buf, off, k, sample_reads):
@@ -224,25 +235,28 @@ def main():
     if use_dist:
         sharded_ms = {kk: round(v / args.steps, 3) for kk, v in runner.phase_ms.items()}
     kid = int(np.argmax(kern))
-    kname = eulerhip.KERNEL_NAMES[kid]
+    kname = eulerhip.KERNEL_NAMES[kid]  # slot name (kernel_alg_bytes); reported by its variant name
+    variant = int(getattr(st, "count_variant", 0))
+    names_v = kernel_names(variant)
     kms = float(kern[kid])
     K = 8 if k <= 32 else 16  # key bytes
     rec = int(st.record_bytes) or 16
-    nsub = int(st.table_capacity) * 16 if int(st.count_path) == eulerhip.EC_PATH_SUPERKMER else 0
-    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L, K, rec, int(st.n_records), nsub)
+    rec2 = 12 if variant == 2 else rec  # the 10-B partition records are refined to 12 B
+    nsub = int(st.table_capacity) * 16  # bucket sub-tables written by k_bucket
+    kb = kernel_alg_bytes(kname, int(st.n_positions), int(st.n_reads), L, K, rec, int(st.n_records), nsub, rec2)
     achieved = kb / (kms / 1e3) / 1e9
-    tr = load_traffic(cfg["name"], kname)
+    tr = load_traffic(cfg["name"], names_v[kid])
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": (tr["kernel_bytes_per_launch"] if tr else None),
             "traffic_source": (tr["file"] if tr else None),
-            "kernel": kname, "kernel_ms": round(kms, 4), "alg_bytes_per_launch": int(kb),
-            "kernels_ms": {eulerhip.KERNEL_NAMES[i]: round(float(kern[i]), 4) for i in range(len(kern))},
+            "kernel": names_v[kid], "kernel_ms": round(kms, 4), "alg_bytes_per_launch": int(kb),
+            "kernels_ms": {names_v[i]: round(float(kern[i]), 4) for i in range(len(kern)) if kern[i] > 0},
             # every counting kernel against the same roofline (k_downsweep and k_refine run within
             # a few % of each other on the headline, so the dominant one can change between runs)
-            "kernels_frac": {eulerhip.KERNEL_NAMES[i]: round(
+            "kernels_frac": {names_v[i]: round(
                 kernel_alg_bytes(eulerhip.KERNEL_NAMES[i], int(st.n_positions), int(st.n_reads), L, K, rec,
-                                 int(st.n_records), nsub) / (float(kern[i]) / 1e3) / (HBM_PEAK_GBS * 1e9), 5)
+                                 int(st.n_records), nsub, rec2) / (float(kern[i]) / 1e3) / (HBM_PEAK_GBS * 1e9), 5)
                 for i in range(len(kern)) if kern[i] > 0},
             "pipeline_alg_bytes": int(alg_bytes(P, R, L, U, K)),
             "pipeline_frac": round(alg_bytes(P, R, L, U, K) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
@@ -260,6 +274,7 @@ def main():
                    "positions": P, "solid_kmers": U,
                    "contigs": int(st.n_contigs if not use_dist else runner.engine.stats().n_contigs),
                    "count_path": ["partitioned", "general", "superkmer"][int(st.count_path)],
+                   "count_variant": ["histogram runs", "fixed-capacity runs", "fixed-capacity runs, 10-B records"][variant],
                    "buckets": int(st.n_buckets), "record_bytes": int(st.record_bytes), "records": int(st.n_records),
                    "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
         "roofline": roof,

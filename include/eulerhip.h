@@ -84,7 +84,8 @@ typedef struct {
     uint64_t n_reads;
     uint64_t n_positions;    /* P: forward k-mer windows over all N-split segments            */
     uint64_t n_distinct_est; /* HyperLogLog estimate of distinct canonical k-mers             */
-    uint64_t n_distinct;     /* distinct canonical k-mers counted                              */
+    uint64_t n_distinct;     /* distinct canonical k-mers counted (an estimate, +-2 %, when the
+                              * seen-twice filter buckets of error-rich inputs drop singletons) */
     uint64_t n_solid;        /* U: canonical k-mers with dict count > limit                    */
     uint64_t n_dict;         /* len(build()) = strand-specific entries (2U minus palindromes)  */
     uint64_t n_contigs;
@@ -99,7 +100,8 @@ typedef struct {
     uint32_t n_buckets;      /* partitioned path: B                                           */
     uint32_t record_bytes;   /* partitioned paths: 12 / 16 per window record, 32 per super-k-mer */
     uint32_t count_variant;  /* partitioned path: 0 = histogram-sized runs (count_part.h),
-                              * 1 = fixed-capacity runs without the upsweep (count_v2.h)       */
+                              * 1 = fixed-capacity runs without the upsweep (count_v2.h), 12-B
+                              * records; 2 = the same with 10-B records (hashed-key remnants) */
     float stage_ms[EC_NSTAGES];   /* EC_FLAG_TIMING only */
     float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING only */
 } ec_stats;

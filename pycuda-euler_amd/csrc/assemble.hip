@@ -150,6 +150,7 @@ struct ec_session {
     float part_keys = 1400.0f;  // k_bucket_filt: target keys per part table
     DevBuf bnp;                 // k_bucket_filt: per-bucket part bits
     const unsigned long long *bbeg = nullptr, *bend = nullptr;  // launch_bucket: explicit bucket bounds
+    uint32_t nseg = 1;          // ... as nseg record ranges per bucket
     DevBuf fcur, bb2;           // count_v2.h: final-bucket cursors, bucket bounds
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
@@ -321,10 +322,11 @@ int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long
     // buckets of count_v2.h (s->bbeg / s->bend set)
     const unsigned long long *bb = s->bbeg ? s->bbeg : s->bstart.as<unsigned long long>();
     const unsigned long long *be = s->bbeg ? s->bend : s->bstart.as<unsigned long long>() + 1;
+    const uint32_t ns = s->bbeg ? s->nseg : 1u;  // record ranges per bucket
     if (s->filt) {  // error-rich input: seen-twice filter + two half tables per bucket
         EC_CHECK(s->bnp.ensure(nb));
         k_bucket_filt<Src><<<nb, BUCKET_THREADS, 0, st>>>(
-            src, bb, be, limit, s->pmin, s->pmax, s->part_keys,
+            src, bb, be, ns, limit, s->pmin, s->pmax, s->part_keys,
             s->dkey.as<unsigned long long>(),
             s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
             s->no_index ? nullptr : s->sub.as<SubSlot>(), s->bnp.as<uint8_t>(), &dsc->nsolid, &dsc->ndistinct,
@@ -333,12 +335,12 @@ int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long
     }
     if (slots == 2048)
         k_bucket<Src, 2048><<<nb, BUCKET_THREADS, 0, st>>>(
-            src, bb, be, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+            src, bb, be, ns, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
             s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
             &dsc->ndistinct, &dsc->overflow);
     else
         k_bucket<Src, 4096><<<nb, BUCKET_THREADS, 0, st>>>(
-            src, bb, be, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
+            src, bb, be, ns, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
             s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
             &dsc->ndistinct, &dsc->overflow);
     return EC_OK;
@@ -405,6 +407,17 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     const int npf = need16 <= 4 * 64 ? 4 : need16 <= 7 * 64 ? 7 : need16 <= 10 * 64 ? 10 : 0;
     if (!npf) return EC_OK;
 
+    // 10-byte partition records (count_v2.h R10) where the hashed-key remnant and the
+    // group-relative meta fit 80 bits (large inputs; EULERHIP_V2_R10 = 1 / 0 forces / disables)
+    auto nbits = [](uint64_t x) {  // bits of the values 0 .. x - 1
+        int b = 0;
+        while ((1ull << b) < x) b++;
+        return b;
+    };
+    const int r10env = getenv("EULERHIP_V2_R10") ? atoi(getenv("EULERHIP_V2_R10")) : -1;
+    const bool r10 = r10env != 0 && (r10env == 1 || P >= (1ull << 26)) && k >= 16 &&
+                     (2 * k - PT_CBITS) + std::max(0, nbits(gsize) + 1 + ibits - 16) <= 64;
+
     // ---- partition into fixed-capacity (coarse bucket, group) runs -------------------------
     constexpr uint64_t C = 1ull << PT_CBITS;
     const uint64_t cap = (gsize * M * 5 / 4 + C - 1) / C + 128;
@@ -420,20 +433,26 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     unsigned int *hreg = s->ftot.as<unsigned int>();
     mark(s, 2 * EC_STAGE_COUNT);
     kmark(s, 1, 0);
-#define EC_PARTITION(NPF, HI)                                                                                         \
-    k_partition<NPF, HI><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, k, M, gsize, (uint32_t)G, cap, \
-                                                              ibits, read_base, smask, rkeys, rmeta,                  \
-                                                              s->cnt.as<unsigned int>(),                              \
-                                                              s->hll.as<uint8_t>(), &dsc->overflow)
+#define EC_PARTITION(NPF, HI, R10)                                                                            \
+    k_partition<NPF, HI, R10><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, k, M, gsize, (uint32_t)G, \
+                                                                   cap, ibits, read_base, smask, rkeys, rmeta,        \
+                                                                   s->cnt.as<unsigned int>(),                         \
+                                                                   s->hll.as<uint8_t>(), &dsc->overflow)
+#define EC_PARTITION_R(NPF, HI)        \
+    if (r10)                           \
+        EC_PARTITION(NPF, HI, true);   \
+    else                               \
+        EC_PARTITION(NPF, HI, false)
     if (k >= 17) {
-        if (npf == 4) EC_PARTITION(4, true);
-        else if (npf == 7) EC_PARTITION(7, true);
-        else EC_PARTITION(10, true);
+        if (npf == 4) EC_PARTITION_R(4, true);
+        else if (npf == 7) EC_PARTITION_R(7, true);
+        else EC_PARTITION_R(10, true);
     } else {
-        if (npf == 4) EC_PARTITION(4, false);
-        else if (npf == 7) EC_PARTITION(7, false);
-        else EC_PARTITION(10, false);
+        if (npf == 4) EC_PARTITION_R(4, false);
+        else if (npf == 7) EC_PARTITION_R(7, false);
+        else EC_PARTITION_R(10, false);
     }
+#undef EC_PARTITION_R
 #undef EC_PARTITION
     kmark(s, 1, 1);
     EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));
@@ -459,9 +478,15 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     if (const char *e = getenv("EULERHIP_REFINE_RS")) rs = (unsigned)std::max(1, atoi(e));
     rs = (unsigned)std::min<uint64_t>(rs, G);
     kmark(s, 4, 0);
-    k_refine2<<<dim3((unsigned)C, rs), BUCKET_THREADS, 0, st>>>(rkeys, rmeta, s->cnt.as<unsigned int>(), (uint32_t)G,
-                                                               cap, bbits, s->recs2.as<unsigned int>(), fcap,
-                                                               s->fcur.as<unsigned long long>(), &dsc->skew);
+#define EC_REFINE(IN10)                                                                                           \
+    k_refine2<IN10><<<dim3((unsigned)C, rs), BUCKET_THREADS, 0, st>>>(                                          \
+        rkeys, rmeta, s->cnt.as<unsigned int>(), (uint32_t)G, cap, bbits, s->recs2.as<unsigned int>(), fcap,     \
+        s->fcur.as<unsigned long long>(), &dsc->skew, k, ibits, gsize, read_base)
+    if (r10)
+        EC_REFINE(true);
+    else
+        EC_REFINE(false);
+#undef EC_REFINE
     kmark(s, 4, 1);
     unsigned long long *bbeg = s->bb2.as<unsigned long long>(), *bend = bbeg + Bk;
     k_fixed_bounds<<<grid_for(Bk, 256), 256, 0, st>>>(s->fcur.as<unsigned long long>(), Bk, fcap, bbeg, bend);
@@ -484,7 +509,16 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     kmark(s, 2, 0);
     const unsigned int m2 = 2 * M - 1;
     int rc;
-    if (k & 1) {
+    auto p12 = [&](auto &src) { src.ibits = ibits, src.k = k, src.m2 = m2, src.p = s->recs2.as<unsigned int>(); };
+    if (r10 && (k & 1)) {  // the refine's key words hold h = bij_fwd(key)
+        Rec12PSource<false, true> src;
+        p12(src);
+        rc = launch_bucket(s, src, (unsigned)Bk, plan.slots, limit);
+    } else if (r10) {
+        Rec12PSource<true, true> src;
+        p12(src);
+        rc = launch_bucket(s, src, (unsigned)Bk, plan.slots, limit);
+    } else if (k & 1) {
         Rec12PSource<false> src;
         src.ibits = ibits, src.k = k, src.m2 = m2, src.p = s->recs2.as<unsigned int>();
         rc = launch_bucket(s, src, (unsigned)Bk, plan.slots, limit);
@@ -509,10 +543,10 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     ok = true;
     s->stats.n_positions = P;
     s->stats.n_distinct_est = (uint64_t)llround(est);
-    s->stats.record_bytes = sizeof(Rec12);
+    s->stats.record_bytes = r10 ? 10 : sizeof(Rec12);  // the partition's records (the refine writes 12 B)
     s->stats.n_records = P;
     s->stats.count_path = EC_PATH_PARTITIONED;
-    s->stats.count_variant = 1;
+    s->stats.count_variant = r10 ? 2 : 1;
     s->stats.n_buckets = (uint32_t)Bk;
     s->stats.table_capacity = umax;
     sidx = SolidIndex{};
@@ -522,6 +556,7 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     sidx.sk = 0;
     sidx.npb = plan.filt ? s->bnp.as<uint8_t>() : nullptr;
     sidx.pmax = plan.pmax;
+    sidx.bijk = r10 ? k : 0;  // R10 sub-tables hold bij_fwd(key)
     U = hsc.nsolid;
     s->stats.n_distinct = hsc.ndistinct;
     s->stats.n_solid = U;

@@ -62,6 +62,23 @@ __host__ __device__ inline uint64_t mix64(uint64_t x) {
     return x;
 }
 
+// Bijective placement hash of an n-bit key (n = 2k <= 64): xorshift, multiply mod 2^n, xorshift
+// (s = ceil(n/2), so one xorshift step inverts itself).  Its top bits pick the bucket of a key
+// and the remaining bits identify the key inside the bucket (count_v2.h 10-byte records), so
+// bij_inv recovers the key from (bucket, remnant).
+constexpr uint64_t BIJ_C = 0xbf58476d1ce4e5b9ull;
+constexpr uint64_t BIJ_CINV = 0x96de1b173f119089ull;  // BIJ_C^-1 mod 2^64
+__host__ __device__ inline uint64_t bij_fwd(uint64_t x, int s, uint64_t m) {
+    x ^= x >> s;
+    x = (x * BIJ_C) & m;
+    return x ^ (x >> s);
+}
+__host__ __device__ inline uint64_t bij_inv(uint64_t x, int s, uint64_t m) {
+    x ^= x >> s;
+    x = (x * BIJ_CINV) & m;
+    return x ^ (x >> s);
+}
+
 // ASCII -> 2-bit code; 4 = 'N' (segment break, referenceAssembler.py:29), 5 = invalid byte
 __device__ inline uint32_t base_code(uint32_t c) {
     // A=65 C=67 G=71 T=84 N=78

@@ -608,7 +608,15 @@ struct LTab {
 // Every source splits a record access into fetch (the loads) and decode (arithmetic), so
 // k_bucket issues the loads of all its unrolled records before decoding any: a branch inside
 // a decode (the even-k palindrome test) would otherwise serialise the loads behind it.
+// Every source also has seg(b, y) (called before segment y of bucket b is read; k_bucket's
+// buckets may be several record ranges) and key_out(c) (the k-mer of table key c: sources
+// whose table keys are not the k-mers themselves -- count_v2.h's hashed keys -- invert here).
+#define EC_PLAIN_SOURCE                                                              \
+    __device__ inline void seg(uint32_t, uint32_t) {}                                \
+    __device__ inline unsigned long long key_out(unsigned long long c) const { return c; }
+
 struct RecSource {
+    EC_PLAIN_SOURCE
     const Rec *recs;
     using Raw = Rec;
     static constexpr bool kDet = false;  // true: records carry their dense id (gathered solid set)
@@ -629,6 +637,7 @@ struct RecSource {
 // twin64 for every record (k_bucket measured 45 % slower).
 template <bool EVEN_K>
 struct Rec12Decode {
+    EC_PLAIN_SOURCE
     int ibits;
     int k;
     unsigned int m2;  // 2m - 1
@@ -666,12 +675,20 @@ struct Rec12Source : Rec12Decode<EVEN_K> {
     }
 };
 
-// packed 12-B records (Store12P: one array, dwordx3 accesses)
-template <bool EVEN_K>
-struct Rec12PSource : Rec12Decode<EVEN_K> {
+// packed 12-B records (Store12P: one array, dwordx3 accesses).  BIJ: the key words hold
+// h = bij_fwd(key) (count_v2.h R10 path); the table counts h and key_out inverts it.
+template <bool EVEN_K, bool BIJ = false>
+struct Rec12PSource {
+    int ibits;
+    int k;
+    unsigned int m2;  // 2m - 1
     const unsigned int *p;
     using Raw = Rec12;
     static constexpr bool kDet = false;
+    __device__ inline void seg(uint32_t, uint32_t) {}
+    __device__ inline unsigned long long key_out(unsigned long long c) const {
+        return BIJ ? bij_inv(c, k, kmask64(k)) : c;
+    }
     __device__ inline unsigned int id(const Raw &) const { return 0; }
     __device__ inline Raw fetch(uint64_t i) const {
         Rec12 r;
@@ -679,6 +696,24 @@ struct Rec12PSource : Rec12Decode<EVEN_K> {
         r.khi = p[3 * i + 1];
         r.meta = p[3 * i + 2];
         return r;
+    }
+    __device__ inline void decode(const Rec12 &r, unsigned long long &kk, unsigned int &add, unsigned long long &eC,
+                                  unsigned long long &eT) const {
+        kk = rkey(r);
+        const unsigned int mt = r.meta;
+        const unsigned long long rd = (unsigned long long)(mt >> (ibits + 1)) << 32;
+        const unsigned int w = mt & ((1u << ibits) - 1), o = (mt >> ibits) & 1u;
+        unsigned int lC = o ? m2 - w : w, lT = o ? w : m2 - w;
+        add = 1;
+        if (EVEN_K) {
+            const unsigned long long x = key_out(kk);
+            if (twin64(x, k) == x) {  // even-k palindrome: inserted twice at the forward event
+                add = 2;
+                lC = lT = w;
+            }
+        }
+        eC = rd | lC;
+        eT = rd | lT;
     }
 };
 
@@ -742,12 +777,15 @@ __device__ inline void lds_insert(LTab<SLOTS> &tab, unsigned int *s_over, unsign
 
 // solid filter (count > limit, build:37-39) + compaction of bucket b's table into the dense
 // arrays (wave ballot, one global atomic per block) + the bucket's lookup sub-table
-template <int SLOTS, bool DET = false>
+struct KeyId {
+    __device__ inline unsigned long long operator()(unsigned long long c) const { return c; }
+};
+template <int SLOTS, bool DET = false, typename KO = KeyId>
 __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned int *s_over, unsigned int b,
                                         long long limit,
                                         unsigned long long *dkey, unsigned int *dcnt, unsigned long long *dfc,
                                         unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
-                                        unsigned long long *ndistinct, unsigned int *overflow) {
+                                        unsigned long long *ndistinct, unsigned int *overflow, KO ko = KO()) {
     __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
     __shared__ unsigned int s_base;
     __syncthreads();
@@ -768,7 +806,7 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
             o.pad = 0;
             if (key != EMPTY_KEY) {
                 const unsigned int u = tab.id[i];
-                dkey[u] = key;
+                dkey[u] = ko(key);
                 dcnt[u] = tab.count[i];
                 dfc[u] = tab.ev[i].x;
                 dft[u] = tab.ev[i].y;
@@ -807,7 +845,7 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
             np += s_pres[w];
         }
         s_base = tot ? atomicAdd(nsolid, tot) : 0;
-        if (np) atomicAdd(ndistinct, (unsigned long long)np);
+        if (np && ndistinct) atomicAdd(ndistinct, (unsigned long long)np);
     }
     __syncthreads();
     unsigned int u = s_base + s_wave[wid] + incl - mine;
@@ -819,7 +857,7 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
         o.id = NONE32;
         o.pad = 0;
         if (solid[q]) {
-            dkey[u] = o.key;
+            dkey[u] = ko(o.key);
             dcnt[u] = tab.count[i];
             dfc[u] = tab.ev[i].x;
             dft[u] = tab.ev[i].y;
@@ -830,9 +868,18 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
     }
 }
 
+// the k-mer of a table key for the dense arrays (count_v2.h hashed keys are inverted)
+template <typename Src>
+struct KeyOutOf {
+    Src src;
+    __device__ inline unsigned long long operator()(unsigned long long c) const { return src.key_out(c); }
+};
+
+// bucket b = record ranges [bbeg[b * nseg + y], bend[b * nseg + y]) for y < nseg
 template <typename Src, int SLOTS>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsigned long long *bbeg,
-                                                          const unsigned long long *bend, long long limit,
+                                                          const unsigned long long *bend, uint32_t nseg,
+                                                          long long limit,
                                                           unsigned long long *dkey, unsigned int *dcnt,
                                                           unsigned long long *dfc, unsigned long long *dft,
                                                           SubSlot *sub, unsigned int *nsolid,
@@ -841,32 +888,36 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
     __shared__ unsigned int s_over[2];
     const unsigned int b = blockIdx.x;
     lds_table_init<SLOTS>(tab, s_over);
-    const uint64_t r0 = bbeg[b], r1 = bend[b];
     // BK_UNROLL records per thread per step, all loads issued before the inserts: the loop
     // is bound by HBM latency, not bandwidth, without this memory-level parallelism
     constexpr int BK_UNROLL = 4;
-    uint64_t i = r0 + threadIdx.x;
-    for (; i + (BK_UNROLL - 1) * (uint64_t)blockDim.x < r1; i += BK_UNROLL * (uint64_t)blockDim.x) {
-        typename Src::Raw raw[BK_UNROLL];
+    for (uint32_t y = 0; y < nseg; y++) {
+        Src s = src;
+        s.seg(b, y);
+        const uint64_t r0 = bbeg[(uint64_t)b * nseg + y], r1 = bend[(uint64_t)b * nseg + y];
+        uint64_t i = r0 + threadIdx.x;
+        for (; i + (BK_UNROLL - 1) * (uint64_t)blockDim.x < r1; i += BK_UNROLL * (uint64_t)blockDim.x) {
+            typename Src::Raw raw[BK_UNROLL];
 #pragma unroll
-        for (int u = 0; u < BK_UNROLL; u++) raw[u] = src.fetch(i + u * (uint64_t)blockDim.x);
+            for (int u = 0; u < BK_UNROLL; u++) raw[u] = s.fetch(i + u * (uint64_t)blockDim.x);
 #pragma unroll
-        for (int u = 0; u < BK_UNROLL; u++) {
+            for (int u = 0; u < BK_UNROLL; u++) {
+                unsigned long long c, eC, eT;
+                unsigned int add;
+                s.decode(raw[u], c, add, eC, eT);
+                lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, s.id(raw[u]));
+            }
+        }
+        for (; i < r1; i += blockDim.x) {
             unsigned long long c, eC, eT;
             unsigned int add;
-            src.decode(raw[u], c, add, eC, eT);
-            lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, src.id(raw[u]));
+            const typename Src::Raw r = s.fetch(i);
+            s.decode(r, c, add, eC, eT);
+            lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, s.id(r));
         }
     }
-    for (; i < r1; i += blockDim.x) {
-        unsigned long long c, eC, eT;
-        unsigned int add;
-        const typename Src::Raw r = src.fetch(i);
-        src.decode(r, c, add, eC, eT);
-        lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, src.id(r));
-    }
     lds_table_finish<SLOTS, Src::kDet>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
-                                       overflow);
+                                       overflow, KeyOutOf<Src>{src});
 }
 
 // ---- buckets with more distinct k-mers than an LDS table holds -----------------------------
@@ -885,7 +936,8 @@ constexpr int FILT_BITS = 18;
 constexpr double PART_KEYS = 1400.0;  // target keys per 2048-slot part table
 template <typename Src>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const unsigned long long *bbeg,
-                                                               const unsigned long long *bend, long long limit, int pmin, int pmax, float part_keys,
+                                                               const unsigned long long *bend, uint32_t nseg,
+                                                               long long limit, int pmin, int pmax, float part_keys,
                                                                unsigned long long *dkey,
                                                                unsigned int *dcnt, unsigned long long *dfc,
                                                                unsigned long long *dft, SubSlot *sub, uint8_t *bnp,
@@ -905,25 +957,29 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
     }
     if (threadIdx.x == 0) s_cells = 0;
     __syncthreads();
-    const uint64_t r0 = bbeg[b], r1 = bend[b];
     constexpr int U = 4;  // records per thread per step, loads issued before any decode
     auto for_records = [&](auto &&fn) {
-        uint64_t i = r0 + threadIdx.x;
-        for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
-            typename Src::Raw raw[U];
+        for (uint32_t y = 0; y < nseg; y++) {
+            Src s = src;
+            s.seg(b, y);
+            const uint64_t r0 = bbeg[(uint64_t)b * nseg + y], r1 = bend[(uint64_t)b * nseg + y];
+            uint64_t i = r0 + threadIdx.x;
+            for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
+                typename Src::Raw raw[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) raw[u] = src.fetch(i + u * (uint64_t)blockDim.x);
+                for (int u = 0; u < U; u++) raw[u] = s.fetch(i + u * (uint64_t)blockDim.x);
 #pragma unroll
-            for (int u = 0; u < U; u++) fn(raw[u]);
+                for (int u = 0; u < U; u++) fn(s, raw[u]);
+            }
+            for (; i < r1; i += blockDim.x) fn(s, s.fetch(i));
         }
-        for (; i < r1; i += blockDim.x) fn(src.fetch(i));
     };
     // pass 0: seen-twice filter (limit >= 1) or distinct-key bitmap (limit < 1)
     const bool filter = limit >= 1;
-    for_records([&](const typename Src::Raw &r) {
+    for_records([&](const Src &s, const typename Src::Raw &r) {
         unsigned long long c, eC, eT;
         unsigned int add;
-        src.decode(r, c, add, eC, eT);
+        s.decode(r, c, add, eC, eT);
         const uint64_t h = mix64(c);
         const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
         const unsigned int m1 = 1u << (c1 & 31), m2 = 1u << (c2 & 31);
@@ -935,31 +991,56 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
         }
     });
     __syncthreads();
-    // keys to insert, by linear counting over the cells (filter: two cells per key)
+    // keys to insert, by linear counting over the cells (filter: two cells per key); with the
+    // filter, the bucket's distinct keys (filtered singletons included) by the same estimate over
+    // the seen-once cells -- ndistinct is then an estimate (+-2 %), exact otherwise
+    __shared__ unsigned int s_cells1;
     {
-        unsigned int cells = 0;
+        if (threadIdx.x == 0) s_cells1 = 0;
+        unsigned int cells = 0, cells1 = 0;
         const unsigned int *w = filter ? seen2 : seen1;
-        for (unsigned int i = threadIdx.x; i < NW; i += blockDim.x) cells += __popc(w[i]);
-        for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o);
-        if ((threadIdx.x & 63) == 0) atomicAdd(&s_cells, cells);
+        for (unsigned int i = threadIdx.x; i < NW; i += blockDim.x) {
+            cells += __popc(w[i]);
+            cells1 += __popc(seen1[i]);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            cells += __shfl_down(cells, o);
+            cells1 += __shfl_down(cells1, o);
+        }
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&s_cells, cells);
+            atomicAdd(&s_cells1, cells1);
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             const double m = (double)(1u << FILT_BITS), set = (double)min(s_cells, (1u << FILT_BITS) - 1);
             const double keys = -m * log(1.0 - set / m) / (filter ? 2.0 : 1.0);
             unsigned int pb = (unsigned int)pmin;  // (pmin > 0: tests force the split)
             while ((int)pb < pmax && keys / (double)(1u << pb) > (double)part_keys) pb++;
+            // more keys than even the 2^pmax part tables hold (2047 each; 10 % above the linear-
+            // counting error): report the overflow now instead of after all the table passes
+            if (keys / (double)(1u << pb) > 2047.0 * 1.1) pb = 0xFFu;
             s_pb = pb;
-            if (bnp) bnp[b] = (uint8_t)pb;
+            if (bnp && pb != 0xFFu) bnp[b] = (uint8_t)pb;
+            if (filter && pb != 0xFFu) {
+                const double set1 = (double)min(s_cells1, (1u << FILT_BITS) - 1);
+                atomicAdd(ndistinct, (unsigned long long)llround(-m * log(1.0 - set1 / m) / 2.0));
+            }
         }
         __syncthreads();
+    }
+    if (s_pb == 0xFFu) {
+        if (threadIdx.x == 0) atomicAdd(overflow, 1u);
+        return;
     }
     const unsigned int pb = s_pb, pmask = (1u << pb) - 1;
     for (unsigned int part = 0; part <= pmask; part++) {
         lds_table_init<SLOTS>(tab, s_over);
-        for_records([&](const typename Src::Raw &r) {
+        for_records([&](const Src &s, const typename Src::Raw &r) {
             unsigned long long c, eC, eT;
             unsigned int add;
-            src.decode(r, c, add, eC, eT);
+            s.decode(r, c, add, eC, eT);
             const uint64_t h = mix64(c);
             if (((unsigned int)(h >> 11) & pmask) != part) return;
             if (filter) {
@@ -970,7 +1051,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
             lds_insert<SLOTS>(tab, s_over, c, (unsigned int)h, add, eC, eT);
         });
         lds_table_finish<SLOTS>(tab, s_over, (b << pmax) + part, limit, dkey, dcnt, dfc, dft, sub, nsolid,
-                                ndistinct, overflow);
+                                filter ? nullptr : ndistinct, overflow, KeyOutOf<Src>{src});
         __syncthreads();
         if (s_over[0]) break;  // overflow already reported: the call is redone on the HBM table
     }

@@ -151,12 +151,16 @@ __device__ inline uint32_t pack16(const uint4 &v) {
 // HyperLogLog over the keys whose low hash bits & smask are 0 (a 1 / (smask + 1) sample of the
 // key space): hll[g * 2^HLL_REG_BITS + j] = the group's register j.
 // The wave tile's bytes are staged 2 bits per base (word i = bases 16i .. 16i+15 of the tile).
-template <int NPF, bool HI>
+//
+// R10 (10-byte records, Pack10): the key is placed by h = bij_fwd(key) (coarse bucket = its top
+// PT_CBITS bits) and the record keeps the remnant h mod 2^(2k - PT_CBITS) and a group-relative
+// meta (read - g0 << (ibits + 1) | o << ibits | w); `meta` is then a uint16_t array.
+template <int NPF, bool HI, bool R10>
 __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restrict__ buf,
                                                           const uint64_t *__restrict__ off, uint64_t nreads,
                                                           int k, uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
                                                           int ibits, uint64_t read_base, uint32_t smask,
-                                                          unsigned long long *keys, unsigned int *meta,
+                                                          unsigned long long *keys, void *metap,
                                                           unsigned int *cnt, uint8_t *hll, unsigned int *overflow) {
     constexpr int C = 1 << PT_CBITS;
     constexpr int NREG = 1 << HLL_REG_BITS;
@@ -218,6 +222,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
     const unsigned long long gcap = g * cap, gstride = (unsigned long long)G * cap;
     const unsigned long long spill = (unsigned long long)C * gstride;
     const uint32_t mbits = ibits + 1;
+    const int rb = 2 * k - PT_CBITS;  // R10: remnant bits
+    const uint64_t rmask = rb >= 64 ? ~0ull : (1ull << rb) - 1;
     uint32_t *st = s_stage[wid];
     for (uint32_t t = wid; t < ntile; t += PT_WAVES) {
         // stage this tile 2 bits per base, then put the next one in flight
@@ -230,7 +236,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
         wave_sync();
         const bool has = len >= (uint32_t)k;  // then len - k + 1 == M
         const uint32_t rel = has ? s - tbase : 0u;  // the read's first base in the tile
-        const uint32_t mhead = (uint32_t)((r + read_base) << mbits);
+        const uint32_t mhead = R10 ? (uint32_t)((r - g0) << mbits) : (uint32_t)((r + read_base) << mbits);
         // bases p .. p + 15 of the tile, base p + i at bits 2i
         auto bases16 = [&](uint32_t p) { return __builtin_amdgcn_alignbit(st[(p >> 4) + 1], st[p >> 4], 2 * (p & 15)); };
         fwd = 0;
@@ -253,11 +259,21 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
                 roll((xb >> (2 * j)) & 3u);
                 const bool tw = fwd > rc;
                 const uint64_t c = tw ? rc : fwd;
-                const uint64_t h = mix64(c);
-                const uint32_t hh = (uint32_t)(h >> 32);
                 const bool ok = has && w + j < M;
-                rkey[j] = c;
-                rmeta[j] = mhead | ((tw ? 1u : 0u) << ibits) | (w + j);
+                const uint32_t mt = mhead | ((tw ? 1u : 0u) << ibits) | (w + j);
+                uint64_t h;
+                uint32_t hh;  // 32 well-mixed hash bits: the bucket in the top PT_CBITS
+                if (R10) {
+                    h = bij_fwd(c, k, mask);
+                    hh = (uint32_t)((h << (64 - 2 * k)) >> 32);
+                    rkey[j] = (h & rmask) | ((uint64_t)(mt >> 16) << rb);
+                    rmeta[j] = mt & 0xFFFFu;
+                } else {
+                    h = mix64(c);
+                    hh = (uint32_t)(h >> 32);
+                    rkey[j] = c;
+                    rmeta[j] = mt;
+                }
                 rcb[j] = ok ? hh >> (32 - PT_CBITS) : (uint32_t)C;  // C: a dummy counter
                 rhh[j] = hh;
                 smp |= (ok && ((uint32_t)h & smask) == 0) ? 1u << j : 0u;
@@ -331,7 +347,10 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
                 if (i < total) {
                     const unsigned long long idx = ob[qq] + i;
                     keys[idx] = ok_[qq];
-                    meta[idx] = om[qq];
+                    if (R10)
+                        reinterpret_cast<unsigned short *>(metap)[idx] = (unsigned short)om[qq];
+                    else
+                        reinterpret_cast<unsigned int *>(metap)[idx] = om[qq];
                 }
             }
             wave_sync();
@@ -358,10 +377,15 @@ __global__ void __launch_bounds__(256) k_hll_merge(const uint8_t *hll, uint64_t 
 // final bucket's run at a cursor reserved by one global atomic (fcur[b] counts records stored
 // in final bucket b, whose records are [b * fcap, b * fcap + fcur[b]) of `out`, packed 12 B).
 constexpr int RF_MAX_RUNS = 2048;
-__global__ void __launch_bounds__(BUCKET_THREADS) k_refine2(const unsigned long long *keys, const unsigned int *meta,
+// IN10: the input is the partition's R10 records (u64 + u16); the output record then carries
+// h = bij_fwd(key) in its key words (k_bucket counts h: Rec12PSource<., true>) and the absolute
+// read id (group gsize reads apart) in its meta.
+template <bool IN10>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_refine2(const unsigned long long *keys, const void *metap,
                                                            const unsigned int *cnt, uint32_t G, uint64_t cap, int bbits,
                                                            unsigned int *out, uint64_t fcap, unsigned long long *fcur,
-                                                           unsigned int *overflow) {
+                                                           unsigned int *overflow, int k, int ibits, uint64_t gsize,
+                                                           uint64_t read_base) {
     constexpr int TILE = REFINE_TILE;
     constexpr int PER = TILE / BUCKET_THREADS;
     __shared__ Rec12 tile[TILE];
@@ -404,6 +428,9 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine2(const unsigned long 
         __syncthreads();
         Rec12 rr[PER];
         unsigned int jj[PER], rk[PER];
+        // all loads of the tile first (their waits then overlap), decode after
+        unsigned long long lk[PER];
+        unsigned int lm[PER], lr[PER];
 #pragma unroll
         for (int q = 0; q < PER; q++) {
             const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
@@ -412,17 +439,38 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine2(const unsigned long 
                 uint32_t jr = j0;
                 while (lst[jr + 1] <= l) jr++;
                 const uint64_t p = phys(jr, l);
-                const unsigned long long kk = keys[p];
-                rr[q].klo = (unsigned int)kk;
-                rr[q].khi = (unsigned int)(kk >> 32);
-                rr[q].meta = meta[p];
+                lk[q] = keys[p];
+                lm[q] = IN10 ? (unsigned int)reinterpret_cast<const unsigned short *>(metap)[p]
+                             : reinterpret_cast<const unsigned int *>(metap)[p];
+                lr[q] = jr;
             }
         }
 #pragma unroll
         for (int q = 0; q < PER; q++) {
             const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
             if (i < n) {
-                jj[q] = rec_bucket(rr[q], bbits) & (F - 1);
+                const unsigned long long kk = lk[q];
+                if (IN10) {
+                    const int rb1 = 2 * k - PT_CBITS;
+                    const uint32_t mbits = ibits + 1;
+                    const uint32_t m1 = ((uint32_t)(kk >> rb1) << 16) | lm[q];
+                    const uint64_t h = (c << rb1) | (kk & ((1ull << rb1) - 1));
+                    rr[q].klo = (unsigned int)h;
+                    rr[q].khi = (unsigned int)(h >> 32);
+                    rr[q].meta = (uint32_t)((read_base + (uint64_t)(ga + lr[q]) * gsize + (m1 >> mbits)) << mbits) |
+                                 (m1 & ((1u << mbits) - 1));
+                } else {
+                    rr[q].klo = (unsigned int)kk;
+                    rr[q].khi = (unsigned int)(kk >> 32);
+                    rr[q].meta = lm[q];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                jj[q] = (IN10 ? (uint32_t)(rkey(rr[q]) >> (2 * k - bbits)) : rec_bucket(rr[q], bbits)) & (F - 1);
                 rk[q] = atomicAdd(&tcnt[jj[q]], 1u);
             }
         }

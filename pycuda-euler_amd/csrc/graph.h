@@ -21,6 +21,7 @@ struct SolidIndex {
     const uint8_t *npb;  // k_bucket_filt layout: bucket b split into 2^npb[b] parts (hash bits 11..)
     int pmax;            // of a region of 2^pmax part tables
     MinCfg mc;
+    int bijk = 0;        // count_v2.h 10-byte records (k): sub-tables keyed by bij_fwd(key), bucket = its top bits
     // (measured: a wave-uniform probe loop with 16-B key+id loads made k_neighbors 0.70 ->
     // 1.3 ms; the per-lane loop below lets the four neighbour lookups overlap)
     __device__ inline unsigned int find_in(uint64_t c, unsigned int h, uint64_t b) const {
@@ -44,6 +45,10 @@ struct SolidIndex {
         return sk ? sk_slot(c) >> (32 - __builtin_ctz(slots)) : (unsigned int)mix64(c);
     }
     __device__ inline unsigned int find(uint64_t c) const {
+        if (sub && bijk) {
+            const uint64_t hc = bij_fwd(c, bijk, kmask64(bijk));
+            return find_in(hc, slot0(hc), bbits ? (hc >> (2 * bijk - bbits)) : 0);
+        }
         if (sub) {
             const uint64_t h = mix64(c);
             const uint64_t b = sk ? sk_bucket_of(minimizer_of(c, mc), bbits) : (bbits ? (h >> (64 - bbits)) : 0);

@@ -159,6 +159,7 @@ __global__ void __launch_bounds__(256) k_bucket_bounds(const unsigned int *sbid,
 }
 
 struct AggSource {
+    EC_PLAIN_SOURCE
     const Agg *in;
     const unsigned int *perm;
     using Raw = Agg;
@@ -184,6 +185,7 @@ struct AggDet {
     unsigned int id;
 };
 struct AggDetSource {
+    EC_PLAIN_SOURCE
     const Agg *in;
     const unsigned int *perm;
     const unsigned int *ids;  // dense id of each record (NONE for fillers, which sort past the end)

@@ -164,7 +164,7 @@ def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode)
         assert res.stats.record_bytes == 16
     # one read length, no N, k <= 32: the fixed-capacity runs of count_v2.h unless asked otherwise
     if mode in ("partitioned", "window_records") and k <= 32 and nr == 0:
-        assert res.stats.count_variant == 1 and res.stats.record_bytes == 12
+        assert res.stats.count_variant == 1 and res.stats.record_bytes == 12  # small inputs: 12-B records
     if mode == "exact":
         assert res.stats.count_variant == 0
 
@@ -464,3 +464,64 @@ def test_v2_read_base_and_short_reads_vs_oracle(gpu_session):
     res = gpu_session.assemble(reads, 31, 1, want_dict=True)
     assert res.stats.count_variant == 1
     assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == gl
+
+
+# ---- 10-byte records (count_v2.h R10: hashed-key remnants, relative read ids) -------------------
+@pytest.mark.parametrize("g,n,L,seed,err,k", [
+    (20_000, 4_000, 100, 1, 0.0, 31), (50_000, 20_000, 100, 2, 0.005, 31), (30_000, 10_000, 80, 3, 0.002, 25),
+    (5_000, 5_000, 60, 4, 0.01, 20), (200_000, 60_000, 100, 6, 0.0, 32), (40_000, 30_000, 150, 7, 0.003, 16),
+    (30_000, 9_000, 120, 8, 0.002, 22), (10_000, 3_333, 64, 9, 0.0, 17)])
+def test_r10_vs_oracle(gpu_session, monkeypatch, g, n, L, seed, err, k):
+    monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    buf, off = make_reads(g, n, L, 4000 + seed, err=err)
+    want_dict = g <= 50_000
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT if want_dict else 0)
+    res = gpu_session.fetch(k, want_dict)
+    assert res.stats.count_variant == 2 and res.stats.record_bytes == 10
+    assert res.stats.n_positions == ref["n_positions"] and res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    if want_dict:
+        assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+@pytest.mark.parametrize("rs", ["8", "16", "32"])
+def test_r10_slices_vs_oracle(gpu_session, monkeypatch, rs):
+    """the refine over 8..32 group slices per coarse bucket"""
+    monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    monkeypatch.setenv("EULERHIP_REFINE_RS", rs)
+    buf, off = make_reads(60_000, 40_000, 100, 4100 + int(rs), err=0.003)
+    ref, rc, rl = _oracle_packed(buf, off, 27, 1, True)
+    gpu_session.run_host(buf, off, 27, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(27, True)
+    assert res.stats.count_variant == 2
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+@pytest.mark.parametrize("lim,pmax", [(1, 0), (0, 0), (2, 0), (1, 2), (0, 3)])
+def test_r10_filter_and_limits_vs_oracle(gpu_session, monkeypatch, lim, pmax):
+    """seen-twice filter / part tables and other limits over 10-byte records"""
+    monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    if pmax:
+        monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
+        monkeypatch.setenv("EULERHIP_FILTER_PMAX", str(pmax))
+        monkeypatch.setenv("EULERHIP_FILTER_PMIN", str(pmax))
+    buf, off = make_reads(40_000, 15_000, 100, 4200 + lim + pmax, err=0.004)
+    for k in (31, 24):
+        ref, rc, rl = _oracle_packed(buf, off, k, lim, True)
+        gpu_session.run_host(buf, off, k, lim, eulerhip.EC_FLAG_WANT_DICT)
+        res = gpu_session.fetch(k, True)
+        assert res.stats.count_variant == 2
+        assert [[x, c] for x, c in res.dict_items] == ref["d"], (k, lim, pmax)
+        assert res.contig_bytes == ref["contig_chars"] and res.links == rl, (k, lim, pmax)
+
+
+def test_r10_palindromes_vs_oracle(gpu_session, monkeypatch):
+    """even k: palindromic k-mers (inserted twice by build) recovered from the hashed keys"""
+    monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    reads = _low_complexity_reads(1500, 100, 77)
+    for k in (16, 20, 24, 32):
+        d, r, g = oracle.assemble(reads, k, 1)
+        res = gpu_session.assemble(reads, k, 1, want_dict=True)
+        assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g, k
