@@ -609,11 +609,13 @@ struct LTab {
 // k_bucket issues the loads of all its unrolled records before decoding any: a branch inside
 // a decode (the even-k palindrome test) would otherwise serialise the loads behind it.
 // Every source also has seg(b, y) (called before segment y of bucket b is read; k_bucket's
-// buckets may be several record ranges) and key_out(c) (the k-mer of table key c: sources
-// whose table keys are not the k-mers themselves -- count_v2.h's hashed keys -- invert here).
+// buckets may be several record ranges), key_out(c) (the k-mer of table key c: sources whose
+// table keys are not the k-mers themselves -- count_v2.h's hashed keys -- invert here) and
+// slot_hash(c) (table placement: mix64, or the hashed key itself).
 #define EC_PLAIN_SOURCE                                                              \
     __device__ inline void seg(uint32_t, uint32_t) {}                                \
-    __device__ inline unsigned long long key_out(unsigned long long c) const { return c; }
+    __device__ inline unsigned long long key_out(unsigned long long c) const { return c; } \
+    __device__ inline uint64_t slot_hash(unsigned long long c) const { return mix64(c); }
 
 struct RecSource {
     EC_PLAIN_SOURCE
@@ -689,6 +691,7 @@ struct Rec12PSource {
     __device__ inline unsigned long long key_out(unsigned long long c) const {
         return BIJ ? bij_inv(c, k, kmask64(k)) : c;
     }
+    __device__ inline uint64_t slot_hash(unsigned long long c) const { return BIJ ? c : mix64(c); }
     __device__ inline unsigned int id(const Raw &) const { return 0; }
     __device__ inline Raw fetch(uint64_t i) const {
         Rec12 r;
@@ -905,7 +908,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
                 unsigned long long c, eC, eT;
                 unsigned int add;
                 s.decode(raw[u], c, add, eC, eT);
-                lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, s.id(raw[u]));
+                lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)s.slot_hash(c), add, eC, eT, s.id(raw[u]));
             }
         }
         for (; i < r1; i += blockDim.x) {
@@ -913,7 +916,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
             unsigned int add;
             const typename Src::Raw r = s.fetch(i);
             s.decode(r, c, add, eC, eT);
-            lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)mix64(c), add, eC, eT, s.id(r));
+            lds_insert<SLOTS, Src::kDet>(tab, s_over, c, (unsigned int)s.slot_hash(c), add, eC, eT, s.id(r));
         }
     }
     lds_table_finish<SLOTS, Src::kDet>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
@@ -980,7 +983,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
         unsigned long long c, eC, eT;
         unsigned int add;
         s.decode(r, c, add, eC, eT);
-        const uint64_t h = mix64(c);
+        const uint64_t h = mix64(c);  // filter cells (the part tables follow slot_hash)
         const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
         const unsigned int m1 = 1u << (c1 & 31), m2 = 1u << (c2 & 31);
         if (filter) {
@@ -1041,14 +1044,14 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_filt(Src src, const u
             unsigned long long c, eC, eT;
             unsigned int add;
             s.decode(r, c, add, eC, eT);
-            const uint64_t h = mix64(c);
-            if (((unsigned int)(h >> 11) & pmask) != part) return;
+            const uint64_t hs = s.slot_hash(c), h = mix64(c);
+            if (((unsigned int)(hs >> 11) & pmask) != part) return;
             if (filter) {
                 const unsigned int c1 = (unsigned int)(h >> 12) & CM, c2 = (unsigned int)(h >> 30) & CM;
                 const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
                 if (!twice && (long long)add <= limit) return;
             }
-            lds_insert<SLOTS>(tab, s_over, c, (unsigned int)h, add, eC, eT);
+            lds_insert<SLOTS>(tab, s_over, c, (unsigned int)hs, add, eC, eT);
         });
         lds_table_finish<SLOTS>(tab, s_over, (b << pmax) + part, limit, dkey, dcnt, dfc, dft, sub, nsolid,
                                 filter ? nullptr : ndistinct, overflow, KeyOutOf<Src>{src});

@@ -46,8 +46,8 @@ struct SolidIndex {
     }
     __device__ inline unsigned int find(uint64_t c) const {
         if (sub && bijk) {
-            const uint64_t hc = bij_fwd(c, bijk, kmask64(bijk));
-            return find_in(hc, slot0(hc), bbits ? (hc >> (2 * bijk - bbits)) : 0);
+            const uint64_t hc = bij_fwd(c, bijk, kmask64(bijk));  // slot: hc itself (Rec12PSource<., true>)
+            return find_in(hc, (unsigned int)hc, bbits ? (hc >> (2 * bijk - bbits)) : 0);
         }
         if (sub) {
             const uint64_t h = mix64(c);
