@@ -14,7 +14,7 @@ import os
 import re
 import sys
 
-KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
+KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine", "k_prescan", "k_partition", "k_refine2")
 
 
 def short(name):
