@@ -31,7 +31,10 @@ namespace ec {
 
 constexpr int PT_WAVES = 4;                // waves per k_partition workgroup
 constexpr int PT_THREADS = 64 * PT_WAVES;
-constexpr int PT_W = 8;                    // windows per lane per round
+#ifndef PT_W_DEF
+#define PT_W_DEF 8
+#endif
+constexpr int PT_W = PT_W_DEF;             // windows per lane per round
 constexpr int PT_REC = 64 * PT_W;          // records per wave round
 constexpr int PT_CBITS = 5;                // coarse buckets (one lane each)
 constexpr int PT_MAX_NPF = 8;              // staged bytes per wave tile <= PT_MAX_NPF KiB
@@ -145,7 +148,9 @@ __device__ inline uint32_t pack16(const uint4 &v) {
 
 // Every read with windows has exactly M windows and no N (k_prescan checked).  Record of
 // window w of read r: key = canonical code, meta = (read_base + r) << (ibits + 1) | o << ibits | w
-// (Rec12, count_part.h).  Region of (c, g): records [(c * G + g) * cap, + cap) of keys / meta;
+// (Rec12, count_part.h).  Region of (c, g): records [(g * C + c) * cap, + cap) of keys / meta
+// (group-major: the C regions a workgroup appends to are adjacent, so its stores stay within a
+// few pages of address translation; coarse-bucket-major spread them 2 GiB and missed UTCL1);
 // records [C * G * cap, + PT_REC) take the stores of a run past its capacity (*overflow is set
 // and the call is redone on the exact path).  cnt[c * G + g] = records stored in the region.
 // HyperLogLog over the keys whose low hash bits & smask are 0 (a 1 / (smask + 1) sample of the
@@ -219,8 +224,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
         nx_n = (uint32_t)(r1_ - r0_);                                                                    \
     } while (0)
     if (wid < ntile) EC_PT_ISSUE(wid);
-    const unsigned long long gcap = g * cap, gstride = (unsigned long long)G * cap;
-    const unsigned long long spill = (unsigned long long)C * gstride;
+    const unsigned long long gcap = g * C * cap, gstride = cap;
+    const unsigned long long spill = (unsigned long long)C * G * cap;
     const uint32_t mbits = ibits + 1;
     const int rb = 2 * k - PT_CBITS;  // R10: remnant bits
     const uint64_t rmask = rb >= 64 ? ~0ull : (1ull << rb) - 1;
@@ -373,7 +378,7 @@ __global__ void __launch_bounds__(256) k_hll_merge(const uint8_t *hll, uint64_t 
 
 // ---- refine: region runs of one coarse bucket -> fixed-capacity final buckets ----------------
 // Workgroup (c, y) reads the runs of groups [G y / RS, G (y+1) / RS) of coarse bucket c as one
-// sequence (run table in LDS), sorts 4096-record tiles by final bucket in LDS and appends each
+// sequence (run table in LDS), sorts RF_TILE-record tiles by final bucket in LDS and appends each
 // final bucket's run at a cursor reserved by one global atomic (fcur[b] counts records stored
 // in final bucket b, whose records are [b * fcap, b * fcap + fcur[b]) of `out`, packed 12 B).
 constexpr int RF_MAX_RUNS = 2048;
@@ -421,8 +426,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine2(const unsigned long 
         __syncthreads();
     }
     const uint64_t N = lst[nr];
-    const unsigned long long cbase = c * (unsigned long long)G * cap;
-    auto phys = [&](uint32_t jrun, uint64_t l) { return cbase + (uint64_t)(ga + jrun) * cap + (l - lst[jrun]); };
+    constexpr uint64_t C = 1 << PT_CBITS;
+    auto phys = [&](uint32_t jrun, uint64_t l) { return ((ga + jrun) * C + c) * cap + (l - lst[jrun]); };
     uint32_t j0 = 0;  // run holding the tile's first record (wave-uniform: every thread tracks it)
     for (uint64_t t0 = 0; t0 < N; t0 += TILE) {
         while (j0 + 1 < nr && lst[j0 + 1] <= t0) j0++;
