@@ -78,14 +78,24 @@ __global__ void __launch_bounds__(256) k_prescan(const uint8_t *buf, const uint6
     const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
     unsigned long long pos = 0;
     unsigned int lmax = 0, lmin = 0xFFFFFFFFu, lall = 0, anyn = 0;
-    for (uint64_t r = g0 + threadIdx.x; r < g1; r += blockDim.x) {
-        const uint64_t len = off[r + 1] - off[r];
+    auto length = [&](uint64_t len) {
         lall = max(lall, (unsigned int)min(len, (uint64_t)0xFFFFFFFFu));
         if (len >= (uint64_t)k) {
             lmax = max(lmax, (unsigned int)min(len, (uint64_t)0xFFFFFFFFu));
             lmin = min(lmin, (unsigned int)min(len, (uint64_t)0xFFFFFFFFu));
             pos += len - k + 1;
         }
+    };
+    {  // read lengths, four offset pairs per thread in flight
+        uint64_t r = g0 + threadIdx.x;
+        for (; r + 3 * blockDim.x < g1; r += 4 * blockDim.x) {
+            uint64_t a[4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) a[u] = off[r + u * blockDim.x], b[u] = off[r + u * blockDim.x + 1];
+#pragma unroll
+            for (int u = 0; u < 4; u++) length(b[u] - a[u]);
+        }
+        for (; r < g1; r += blockDim.x) length(off[r + 1] - off[r]);
     }
     if (g1 > g0) {
         const uint64_t b0 = off[g0], b1 = off[g1];
@@ -126,7 +136,20 @@ __global__ void __launch_bounds__(256) k_prescan(const uint8_t *buf, const uint6
         lall = max(lall, (unsigned int)__shfl_down(lall, o));
         anyn |= (unsigned int)__shfl_down(anyn, o);
     }
+    // one set of global atomics per workgroup (per wave they queued on the same five words)
+    __shared__ unsigned long long s_pos[4];
+    __shared__ unsigned int s_l[4][4];
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
+        s_pos[w] = pos;
+        s_l[w][0] = lmax, s_l[w][1] = lmin, s_l[w][2] = anyn, s_l[w][3] = lall;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < (int)(blockDim.x >> 6); q++) {
+            pos += s_pos[q];
+            lmax = max(lmax, s_l[q][0]), lmin = min(lmin, s_l[q][1]), anyn |= s_l[q][2], lall = max(lall, s_l[q][3]);
+        }
         if (pos) atomicAdd(npos, pos);
         if (lmax) atomicMax(&lens[0], lmax);
         if (lmin != 0xFFFFFFFFu) atomicMax(&lens[1], ~lmin);
