@@ -73,19 +73,21 @@ def kernel_alg_bytes(name, P, R, L, K=8, rec=16, NR=None, nsub=0, rec2=None):
     k_refine / k_refine2      reads every record, writes it to its bucket     (rec + rec2)*P
     k_bucket                  reads every record, writes the sub-tables       rec2*P + nsub
     k_count     general path: read once + one insert per position R*L + P*(K+8)
-    Super-k-mer records (rec = 32, NR records):
-    k_downsweep R*L + 32*NR;  k_refine 64*NR;  k_bucket 32*NR + nsub"""
-    if rec == 32:
-        return {"k_upsweep": R * L, "k_downsweep": R * L + 32 * NR, "k_bucket": 32 * NR + nsub,
-                "k_count": R * L + P * (K + 8), "k_refine": 64 * NR}[name]
+    Super-k-mer records (rec = 32 or 16 bytes, NR records):
+    k_downsweep / k_skpart R*L + rec*NR;  k_refine / k_skrefine 2*rec*NR;  k_bucket / k_skbucket rec*NR + nsub"""
+    if NR is not None and NR < P and rec in (16, 32):
+        return {"k_upsweep": R * L, "k_downsweep": R * L + rec * NR, "k_bucket": rec * NR + nsub,
+                "k_count": R * L + P * (K + 8), "k_refine": 2 * rec * NR}[name]
     rec2 = rec2 or rec
     return {"k_upsweep": R * L, "k_downsweep": R * L + rec * P, "k_bucket": rec2 * P + nsub,
             "k_count": R * L + P * (K + 8), "k_refine": (rec + rec2) * P}[name]
 
 
 def kernel_names(variant):
-    """kernel names of the ec_stats.kernel_ms slots: count_part.h's exact path (variant 0) or
-    count_v2.h's fixed-capacity runs (variants 1, 2)"""
+    """kernel names of the ec_stats.kernel_ms slots: count_part.h's exact path (variant 0),
+    count_v2.h's fixed-capacity runs (variants 1, 2) or count_sk2.h's super-k-mers (variant 3)"""
+    if variant == 3:
+        return ("k_prescan", "k_skpart", "k_skbucket", "k_count", "k_skrefine")
     if variant:
         return ("k_prescan", "k_partition", "k_bucket", "k_count", "k_refine2")
     return ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
@@ -274,7 +276,8 @@ def main():
                    "positions": P, "solid_kmers": U,
                    "contigs": int(st.n_contigs if not use_dist else runner.engine.stats().n_contigs),
                    "count_path": ["partitioned", "general", "superkmer"][int(st.count_path)],
-                   "count_variant": ["histogram runs", "fixed-capacity runs", "fixed-capacity runs, 10-B records"][variant],
+                   "count_variant": ["histogram runs", "fixed-capacity runs", "fixed-capacity runs, 10-B records",
+                                     "super-k-mer records, 16 B"][variant],
                    "buckets": int(st.n_buckets), "record_bytes": int(st.record_bytes), "records": int(st.n_records),
                    "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
         "roofline": roof,

@@ -30,6 +30,7 @@
 
 #include "count_part.h"
 #include "count_v2.h"
+#include "count_sk2.h"
 #include "shard.h"
 #include "compact.h"
 #include "count_wide.h"
@@ -369,11 +370,159 @@ BucketPlan plan_buckets(double est, long long limit, bool filt_ok) {
     return p;
 }
 
+// count_sk2.h: super-k-mer records for 21 <= k <= 32 (called by phase_count_v2 after its
+// prescan).  done = false when the input does not qualify, the distinct estimate asks for the
+// seen-twice filter, or a run / bucket / table outgrew its capacity: phase_count_v2 then counts
+// with window records.
+int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads,
+                    uint64_t read_base, int k, long long limit, uint32_t M, uint64_t G, uint64_t gsize, uint64_t P,
+                    int npf, unsigned int &U, SolidIndex &sidx, bool &done) {
+    done = false;
+    if (k < SK_MIN_K || k > 32 || M > 256 || gsize * M >= (1ull << 24) || (read_base + nreads) * M >= (1ull << 32) ||
+        getenv("EULERHIP_NO_SK2"))
+        return EC_OK;
+    hipStream_t st = s->stream;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    auto reset = [&]() -> int {  // scalars as phase_count_v2 expects them after its prescan
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, sizeof(unsigned int), st));
+        EC_HIP(hipMemsetAsync(&dsc->skew, 0, sizeof(unsigned int), st));
+        EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, sizeof(unsigned int), st));
+        EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, sizeof(unsigned long long), st));
+        return EC_OK;
+    };
+    const MinCfg mc = sk_cfg(k);
+    constexpr uint64_t C = 1ull << PT_CBITS;
+    // records per read ~ 2 M / (w + 1) + 1 on random sequence; 40 % headroom per run
+    const double per_read = 2.0 * M / (mc.w + 1) + 2.0;
+    const uint64_t cap = (uint64_t)(gsize * per_read * 1.4 / C) + 256;
+    EC_CHECK(s->recs.ensure((C * G * cap + SK2_ECAP) * 16));
+    EC_CHECK(s->cnt.ensure(C * G * 4));
+    EC_CHECK(s->hll.ensure(G * (1 << HLL_REG_BITS)));
+    EC_CHECK(s->ftot.ensure((1 << HLL_REG_BITS) * 4));
+    uint4 *recs = s->recs.as<uint4>();
+    const uint32_t smask = P >= (1ull << 26) ? 255u : 0u;
+    unsigned int *hreg = s->ftot.as<unsigned int>();
+    EC_HIP(hipMemsetAsync(&dsc->nrec, 0, sizeof(unsigned long long), st));
+    mark(s, 2 * EC_STAGE_COUNT);
+    kmark(s, 1, 0);
+#define EC_SKPART(NPF)                                                                                        \
+    k_skpart<NPF><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, \
+                                                      recs, s->cnt.as<unsigned int>(), s->hll.as<uint8_t>(),      \
+                                                      &dsc->nrec, &dsc->overflow)
+    if (npf == 4) EC_SKPART(4);
+    else if (npf == 7) EC_SKPART(7);
+    else EC_SKPART(10);
+#undef EC_SKPART
+    kmark(s, 1, 1);
+    EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));
+    k_hll_merge<<<dim3((1 << HLL_REG_BITS) / 256, TOT_SLICES), 256, 0, st>>>(s->hll.as<uint8_t>(), G, hreg);
+    k_hll_final<<<1, 1024, 0, st>>>(hreg, HLL_REG_BITS, &dsc->est);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.overflow) return reset();  // a run outgrew its capacity
+    const double est = hsc.est * (smask + 1.0);
+    BucketPlan plan = plan_buckets(est, limit, !getenv("EULERHIP_NO_FILTER"));
+    if (!plan.part || plan.filt) return reset();  // error-rich: window records with the seen-twice filter
+    const int bbits = std::max(plan.bbits, PT_CBITS);
+    const uint64_t Bk = 1ull << bbits;
+    const uint64_t NR = hsc.nrec;
+
+    // ---- refine into fixed-capacity final buckets -------------------------------------------
+    // a bucket gathers whole minimizers (each ~coverage records): ~13 % spread at the headline
+    // size (62 minimizers a bucket), so twice the mean
+    const uint64_t fcap = NR * 2 / Bk + 1024;
+    EC_CHECK(s->recs2.ensure(Bk * fcap * 16));
+    EC_CHECK(s->fcur.ensure(Bk * 8));
+    EC_CHECK(s->bb2.ensure(Bk * 16));
+    EC_HIP(hipMemsetAsync(s->fcur.p, 0, Bk * 8, st));
+    unsigned rs = 8;
+    if (const char *e = getenv("EULERHIP_REFINE_RS")) rs = (unsigned)std::max(1, atoi(e));
+    rs = (unsigned)std::min<uint64_t>(rs, G);
+    kmark(s, 4, 0);
+    k_skrefine<<<dim3((unsigned)C, rs), BUCKET_THREADS, 0, st>>>(recs, s->cnt.as<unsigned int>(), (uint32_t)G, cap, bbits,
+                                                                  s->recs2.as<uint4>(), fcap,
+                                                                  s->fcur.as<unsigned long long>(), &dsc->skew, M,
+                                                                  gsize, read_base);
+    kmark(s, 4, 1);
+    unsigned long long *bbeg = s->bb2.as<unsigned long long>(), *bend = bbeg + Bk;
+    k_fixed_bounds<<<grid_for(Bk, 256), 256, 0, st>>>(s->fcur.as<unsigned long long>(), Bk, fcap, bbeg, bend);
+    mark(s, 2 * EC_STAGE_COUNT + 1);
+
+    // ---- super-k-mers -> bucket tables ----------------------------------------------------------
+    mark(s, 2 * EC_STAGE_COMPACT);
+    const uint64_t umax = Bk * plan.slots;
+    EC_CHECK(s->dkey.ensure(umax * 8));
+    EC_CHECK(s->dcnt.ensure(umax * 4));
+    EC_CHECK(s->dfc.ensure(umax * 8));
+    EC_CHECK(s->dft.ensure(umax * 8));
+    EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
+    kmark(s, 2, 0);
+    const double inv_m = 1.0 / M;
+#ifndef SKB_MODE
+#define SKB_MODE 0
+#endif
+#ifndef SKB_REC_FAST
+#define SKB_REC_FAST true
+#endif
+#if SKB_MODE == 0
+#define EC_SKB(SLOTS, EVEN) k_skbucket_rec<SLOTS, EVEN, SKB_REC_FAST>
+#else
+#define EC_SKB(SLOTS, EVEN) k_skbucket<SLOTS, EVEN, SKB_MODE - 1>
+#endif
+#define EC_SKBUCKET(SLOTS, EVEN)                                                                              \
+    EC_SKB(SLOTS, EVEN)<<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(                                              \
+        s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(),                \
+        s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),          \
+        s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow)
+    if (plan.slots == 2048) {
+        if (k & 1) EC_SKBUCKET(2048, false);
+        else EC_SKBUCKET(2048, true);
+    } else {
+        if (k & 1) EC_SKBUCKET(4096, false);
+        else EC_SKBUCKET(4096, true);
+    }
+#undef EC_SKBUCKET
+#undef EC_SKB
+    kmark(s, 2, 1);
+    mark(s, 2 * EC_STAGE_COMPACT + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (hsc.overflow || hsc.skew) {  // a final bucket or an LDS table overflowed
+        s->stats.table_retries++;
+        return reset();
+    }
+    done = true;
+    s->stats.n_positions = P;
+    s->stats.n_distinct_est = (uint64_t)llround(est);
+    s->stats.record_bytes = 16;
+    s->stats.n_records = NR;
+    s->stats.count_path = EC_PATH_PARTITIONED;
+    s->stats.count_variant = 3;
+    s->stats.n_buckets = (uint32_t)Bk;
+    s->stats.table_capacity = umax;
+    sidx = SolidIndex{};
+    sidx.sub = s->sub.as<SubSlot>();
+    sidx.bbits = bbits;
+    sidx.slots = plan.slots;
+    sidx.sk = 1;
+    sidx.mc = mc;
+    sidx.npb = nullptr;
+    U = hsc.nsolid;
+    s->stats.n_distinct = hsc.ndistinct;
+    s->stats.n_solid = U;
+    if (2ull * U >= (unsigned long long)CYC) {
+        set_error("too many solid k-mers (%u) for 31-bit node ids", U);
+        return EC_ERR_CAPACITY;
+    }
+    return EC_OK;
+}
+
 // count_v2.h: the partitioned count of N-free reads of one length without the histogram
 // upsweep.  ok = false (and nothing decided) when the input does not qualify or a run / final
 // bucket outgrew its fixed capacity: phase_count then takes count_part.h's exact path.
 int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, uint64_t read_base,
-                   int k, long long limit, unsigned int &U, SolidIndex &sidx, bool &ok) {
+                   int k, long long limit, bool allow_sk2, unsigned int &U, SolidIndex &sidx, bool &ok) {
     ok = false;
     hipStream_t st = s->stream;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -406,6 +555,14 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     const uint64_t need16 = (64ull * lall + 30 + 15) / 16;  // 16-B chunks of a 64-read wave tile
     const int npf = need16 <= 4 * 64 ? 4 : need16 <= 7 * 64 ? 7 : need16 <= 10 * 64 ? 10 : 0;
     if (!npf) return EC_OK;
+    if (allow_sk2) {  // super-k-mer records (count_sk2.h) unless window records are asked for
+        bool done = false;
+        EC_CHECK(phase_count_sk2(s, d_reads, d_off, nreads, read_base, k, limit, M, G, gsize, P, npf, U, sidx, done));
+        if (done) {
+            ok = true;
+            return EC_OK;
+        }
+    }
 
     // 10-byte partition records (count_v2.h R10) where the hashed-key remnant and the
     // group-relative meta fit 80 bits (large inputs; EULERHIP_V2_R10 = 1 / 0 forces / disables)
@@ -584,7 +741,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     if (!(flags & (EC_FLAG_GENERAL | EC_FLAG_WIDE_RECORDS | EC_FLAG_SUPERKMER | EC_FLAG_EXACT_COUNT)) && nreads &&
         k <= 32 && !getenv("EULERHIP_NO_V2")) {
         bool ok = false;
-        EC_CHECK(phase_count_v2(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok));
+        EC_CHECK(phase_count_v2(s, d_reads, d_off, nreads, read_base, k, limit, !(flags & EC_FLAG_WINDOW_RECORDS), U,
+                                sidx, ok));
         if (ok) return EC_OK;
         EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
         EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));

@@ -1,0 +1,691 @@
+// count_sk2.h -- super-k-mer records on the count_v2 scaffold (N-free reads of one length,
+// 21 <= k <= 32).
+//
+// count_v2.h moves one 10- or 12-byte record per k-mer position through partition, refine
+// and bucket: ~30 GB of HBM traffic at the headline size.  Consecutive windows of a read that
+// share their minimizer (superkmer.h: the smallest hash over the window's canonical m-mers,
+// the same for a k-mer and its twin) form a super-k-mer; all its k-mers belong to the
+// minimizer's bucket, so the run travels as ONE 16-byte record holding its L = n + k - 1
+// bases (2 bits each, n <= 16 windows) -- about (w + 1) / 2 windows per record:
+//
+//   k_skpart    per read group : lane = read; m-mer hashes and van Herk / Gil-Werman sliding
+//                                minima (block length w, LDS ring), runs of equal minimizer
+//                                buffered as 4-byte entries (read lane, first window, n,
+//                                bucket bits); a flush sorts the wave's entries by coarse
+//                                bucket and writes 16-byte records to the (group, coarse)
+//                                runs, bases read back from the wave's 2-bit stage; sampled
+//                                HyperLogLog of the canonical k-mers
+//   k_skrefine  per coarse slice: runs -> fixed-capacity final buckets (as k_refine2), the
+//                                group-relative position made absolute
+//   k_skbucket  per final bucket: records sorted by window count in LDS, lane = record, the
+//                                k-mers rolled out of the bases into the LDS table of
+//                                count_part.h (lds_insert / lds_table_finish)
+//   SolidIndex (graph.h, sk = 1): a key's bucket = the top bits of min_remix(its minimizer),
+//                                first probe slot = sk_slot(key) -- as k_bucket_sk wrote them
+//
+// Record (uint4): x, y = bases 0..15, 16..31 (base i at bits 2i), z = bases 32..45 in bits
+// 0..27 | (n - 1) << 28; w = partition: bucket-bits-below-coarse (8) << 24 | p_rel (24 bits,
+// (read - g0) * M + first window); refine output: p = (read_base + read) * M + first window.
+// Events as count_part.h: read = p / M, lf = p % M + o for window o, lr = 2M - 1 - lf.
+#pragma once
+#include "count_v2.h"
+#include "superkmer.h"
+
+namespace ec {
+
+constexpr int SK2_NMAX = 16;     // windows per record (n - 1 in 4 bits)
+constexpr int SK2_BASES = 46;    // bases per record (92 bits)
+constexpr int SK2_R = 4;         // windows per lane per round of k_skpart
+constexpr int SK2_ECAP = 896;    // entries a wave buffers before a flush (LDS: 3 workgroups per CU)
+constexpr int SK2_TILE = 4096;   // k_skrefine records per tile (64 KiB of LDS)
+constexpr int SK2_FBITS = FINE_BITS - PT_CBITS;  // bucket bits below the coarse bits in a record
+
+__host__ __device__ inline uint32_t sk2_nmax(int k) {
+    return (uint32_t)(SK2_BASES - k + 1 < SK2_NMAX ? SK2_BASES - k + 1 : SK2_NMAX);
+}
+
+// ---- partition -------------------------------------------------------------------------------
+// Region of (c, g): records [(g * C + c) * cap, + cap) of recs, spill records at C * G * cap
+// (SK2_ECAP of them; *overflow set, the call is redone); cnt[c * G + g] = records stored.
+// Entry (u32): lane | first window << 6 | (n - 1) << 14 | top FINE_BITS of min_remix << 18.
+template <int NPF>
+__global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict__ buf,
+                                                       const uint64_t *__restrict__ off, uint64_t nreads, MinCfg mc,
+                                                       uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
+                                                       uint32_t smask, uint4 *recs, unsigned int *cnt, uint8_t *hll,
+                                                       unsigned long long *nrec, unsigned int *overflow) {
+    constexpr int C = 1 << PT_CBITS;
+    constexpr int NREG = 1 << HLL_REG_BITS;
+    constexpr int SW = NPF * 64 + 4;
+    __shared__ uint32_t s_stage[PT_WAVES][SW];
+    __shared__ uint32_t s_ring[PT_WAVES][SK_W_MAX * 64];  // lane's GW block: [q * 64 + lane]
+    __shared__ uint32_t s_ent[PT_WAVES][SK2_ECAP];
+    __shared__ uint16_t s_srt[PT_WAVES][SK2_ECAP];
+    __shared__ uint32_t s_rel[PT_WAVES][64];
+    __shared__ unsigned long long s_base[PT_WAVES][C];
+    __shared__ unsigned int s_wcnt[PT_WAVES][C];
+    __shared__ unsigned int s_cur[C];
+    __shared__ unsigned int s_hll[NREG / 4];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) s_hll[i] = 0;
+    if (threadIdx.x < C) s_cur[threadIdx.x] = 0;
+    if (lane < C) s_wcnt[wid][lane] = 0;
+    __syncthreads();
+    const uint64_t g = blockIdx.x;
+    const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
+    const uint32_t ntile = (uint32_t)((g1 - g0 + 63) / 64);
+    const int k = mc.k, m = mc.m;
+    const uint32_t w = (uint32_t)mc.w, nmax = sk2_nmax(k);
+    const uint64_t kmask = kmask64(k);
+    const int sh = 2 * (k - 1);
+    uint4 pf[NPF];
+    uint64_t nx_base = 0;
+    uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
+    if (wid < ntile) EC_PT_ISSUE(wid);
+    const unsigned long long gcap = g * C * cap, spill = (unsigned long long)C * G * cap;
+    uint32_t *st = s_stage[wid];
+    uint32_t *ring = s_ring[wid] + lane;
+    uint32_t *ent = s_ent[wid];
+    auto bases16 = [&](uint32_t p) { return __builtin_amdgcn_alignbit(st[(p >> 4) + 1], st[p >> 4], 2 * (p & 15)); };
+    for (uint32_t t = wid; t < ntile; t += PT_WAVES) {
+#pragma unroll
+        for (int q = 0; q < NPF; q++) st[q * 64 + lane] = pack16(pf[q]);
+        const uint32_t tbase = (uint32_t)nx_base, s = nx_s;
+        const uint32_t len = lane < nx_n ? nx_e - nx_s : 0u;
+        const bool more = t + PT_WAVES < ntile;
+        const bool has = len >= (uint32_t)k;  // then len - k + 1 == M
+        const uint32_t rel = has ? s - tbase : 0u;
+        s_rel[wid][lane] = rel;
+        wave_sync();
+        // m-mer / k-mer state over the first k - 1 bases; the GW block starts at m-mer 0
+        uint32_t mf = 0, mr = 0, gi = 0, pm = 0xFFFFFFFFu;
+        uint64_t fwd = 0, rc = 0;
+        // push m-mer hash h (m-mer index j, gi = j mod w): min of the window of w m-mers ending at j
+        auto gw_push = [&](uint32_t h) {
+            pm = gi == 0 ? h : min(pm, h);
+            const uint32_t sn = gi + 1 < w ? ring[(gi + 1) * 64] : 0xFFFFFFFFu;
+            ring[gi * 64] = h;
+            const uint32_t v = min(sn, pm);
+            if (gi + 1 == w) {  // block complete: hashes -> suffix minima (wave-uniform)
+                uint32_t a = 0xFFFFFFFFu;
+                for (int q = (int)w - 1; q >= 0; q--) {
+                    a = min(a, ring[q * 64]);
+                    ring[q * 64] = a;
+                }
+                gi = 0;
+            } else {
+                gi++;
+            }
+            return v;
+        };
+        auto push_base = [&](uint32_t b) {
+            fwd = ((fwd << 2) | b) & kmask;
+            rc = (rc >> 2) | ((uint64_t)(3u - b) << sh);
+            mf = ((mf << 2) | b) & mc.mmask;
+            mr = (mr >> 2) | ((3u - b) << mc.msh);
+        };
+        {
+            const uint32_t x0 = bases16(rel), x1 = bases16(rel + 16);
+            for (int tb = 0; tb < k - 1; tb++) {
+                push_base(tb < 16 ? (x0 >> (2 * tb)) & 3u : (x1 >> (2 * (tb - 16))) & 3u);
+                if (tb >= m - 1) gw_push(mmer_hash(mf < mr ? mf : mr));
+            }
+        }
+        const uint32_t nrounds = __any(has) ? (M + SK2_R - 1) / SK2_R : 0u;
+        if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
+        uint32_t runv = 0, runn = 0, runi = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
+        uint32_t wi = 0;
+        const uint32_t rtile = 64 * t;  // the tile's first read relative to g0
+        for (uint32_t round = 0; round < nrounds; round++) {
+            const uint32_t xb = bases16(rel + (uint32_t)(k - 1) + wi);
+            unsigned int smp = 0;
+            uint32_t shh[SK2_R];
+#pragma unroll
+            for (int j = 0; j < SK2_R; j++) {
+                push_base((xb >> (2 * j)) & 3u);
+                const uint32_t v = gw_push(mmer_hash(mf < mr ? mf : mr));
+                const bool ok = has && wi + j < M;
+                // HyperLogLog sample of the canonical k-mers: a multiplicative test, mix64 for the sampled
+                const uint64_t c = fwd < rc ? fwd : rc;
+                const uint32_t th = (uint32_t)((c * 0x9E3779B97F4A7C15ull) >> 32);
+                shh[j] = 0;
+                if (ok && ((th >> 24) & smask) == 0) {
+                    smp |= 1u << j;
+                    shh[j] = (uint32_t)(mix64(c) >> 32);
+                }
+                const bool close = ok && runn && (v != runv || runn == nmax);
+                const uint64_t bal = __ballot(close);
+                if (close) {
+                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - FINE_BITS)) << 18;
+                }
+                cntw += (uint32_t)__popcll(bal);
+                if (ok) {
+                    if (close || !runn) {
+                        runv = v;
+                        runi = wi + j;
+                        runn = 0;
+                    }
+                    runn++;
+                }
+            }
+            wi += SK2_R;
+            const bool last = round + 1 == nrounds;
+            if (last) {  // the reads' final runs
+                const bool fin = has && runn;
+                const uint64_t bal = __ballot(fin);
+                if (fin) {
+                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - FINE_BITS)) << 18;
+                }
+                cntw += (uint32_t)__popcll(bal);
+                if (more) EC_PT_ISSUE(t + PT_WAVES);
+            }
+            if (smp) {
+#pragma unroll
+                for (int j = 0; j < SK2_R; j++) {
+                    if (!((smp >> j) & 1u)) continue;
+                    const uint32_t hj = shh[j] >> (32 - HLL_REG_BITS);
+                    const uint32_t rho =
+                        (uint32_t)__clz((int)((shh[j] << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+                    const uint32_t hs = (hj & 3) * 8;
+                    uint32_t old = s_hll[hj >> 2];
+                    while (rho > ((old >> hs) & 0xFFu)) {
+                        const uint32_t nw = (old & ~(0xFFu << hs)) | (rho << hs);
+                        const uint32_t prev = atomicCAS(&s_hll[hj >> 2], old, nw);
+                        if (prev == old) break;
+                        old = prev;
+                    }
+                }
+            }
+            // flush: the buffer could not take another round, or the stage is about to change
+            if (last || cntw > (uint32_t)(SK2_ECAP - 64 * (SK2_R + 1))) {
+                wave_sync();
+                for (uint32_t i = lane; i < cntw; i += 64) atomicAdd(&s_wcnt[wid][ent[i] >> 26], 1u);
+                wave_sync();
+                const unsigned int v = lane < (uint32_t)C ? s_wcnt[wid][lane] : 0u;
+                const unsigned int incl = wave_incl_scan(v);
+                const unsigned int beg = incl - v;
+                if (lane < (uint32_t)C) {
+                    s_wcnt[wid][lane] = beg;
+                    unsigned int at = 0;
+                    if (v) at = atomicAdd(&s_cur[lane], v);
+                    unsigned long long b0 = gcap + lane * cap + at - beg;
+                    if (at + v > cap) {  // past the capacity: stores go to the spill records
+                        atomicOr(overflow, 1u);
+                        b0 = spill - beg;
+                    }
+                    s_base[wid][lane] = b0;
+                }
+                wave_sync();
+                for (uint32_t i = lane; i < cntw; i += 64) {
+                    const unsigned int p = atomicAdd(&s_wcnt[wid][ent[i] >> 26], 1u);
+                    s_srt[wid][p] = (uint16_t)i;
+                }
+                wave_sync();
+                for (uint32_t i = lane; i < cntw; i += 64) {
+                    const uint32_t e = ent[s_srt[wid][i]];
+                    const uint32_t lr = e & 63u, i0 = (e >> 6) & 0xFFu, n1 = (e >> 14) & 15u;
+                    const uint32_t p0 = s_rel[wid][lr] + i0;
+                    uint4 o;
+                    o.x = bases16(p0);
+                    o.y = bases16(p0 + 16);
+                    o.z = (bases16(p0 + 32) & 0x0FFFFFFFu) | n1 << 28;
+                    o.w = ((e >> 18) & ((1u << SK2_FBITS) - 1)) << 24 | ((rtile + lr) * M + i0);
+                    recs[s_base[wid][e >> 26] + i] = o;
+                }
+                wave_sync();
+                if (lane < (uint32_t)C) s_wcnt[wid][lane] = 0;
+                cntw = 0;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < C) cnt[(uint64_t)threadIdx.x * G + g] = (unsigned int)min((uint64_t)s_cur[threadIdx.x], cap);
+    if (threadIdx.x == 0) {  // records of the group (one atomic per workgroup)
+        unsigned long long tot = 0;
+        for (int c = 0; c < C; c++) tot += s_cur[c];
+        if (tot) atomicAdd(nrec, tot);
+    }
+    unsigned int *hw = reinterpret_cast<unsigned int *>(hll + g * NREG);
+    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) hw[i] = s_hll[i];
+}
+
+// ---- refine: (group, coarse) runs -> fixed-capacity final buckets ------------------------------
+// As k_refine2: workgroup (c, y) reads the runs of groups [G y / RS, G (y + 1) / RS) of coarse
+// bucket c, sorts SK2_TILE-record tiles by final bucket in LDS and appends each final bucket's
+// run at a cursor reserved by one global atomic: final bucket b holds [b fcap, b fcap + fcur[b]).
+__global__ void __launch_bounds__(BUCKET_THREADS) k_skrefine(const uint4 *recs, const unsigned int *cnt, uint32_t G,
+                                                             uint64_t cap, int bbits, uint4 *out, uint64_t fcap,
+                                                             unsigned long long *fcur, unsigned int *overflow,
+                                                             uint32_t M, uint64_t gsize, uint64_t read_base) {
+    constexpr int TILE = SK2_TILE;
+    constexpr int PER = TILE / BUCKET_THREADS;
+    constexpr uint64_t C = 1 << PT_CBITS;
+    __shared__ uint4 tile[TILE];
+    __shared__ uint8_t tj[TILE];
+    __shared__ unsigned long long base[REFINE_FANOUT];
+    __shared__ unsigned int tcnt[REFINE_FANOUT], tbeg[REFINE_FANOUT], wsum[BUCKET_THREADS / 64];
+    __shared__ unsigned int lst[RF_MAX_RUNS + 1];
+    const int fb = bbits - PT_CBITS;  // final bits below the coarse bits
+    const int F = 1 << fb;
+    const uint64_t c = blockIdx.x;
+    const uint32_t ga = (uint32_t)((uint64_t)G * blockIdx.y / gridDim.y),
+                   gb = (uint32_t)((uint64_t)G * (blockIdx.y + 1) / gridDim.y);
+    const uint32_t nr = gb - ga;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    {
+        const uint32_t i0 = 2 * threadIdx.x;
+        const unsigned int a = i0 < nr ? cnt[c * G + ga + i0] : 0u, b = i0 + 1 < nr ? cnt[c * G + ga + i0 + 1] : 0u;
+        unsigned int incl = a + b;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        unsigned int before = 0;
+        for (int q = 0; q < wid; q++) before += wsum[q];
+        const unsigned int ex = before + incl - (a + b);
+        if (i0 <= nr) lst[i0] = ex;
+        if (i0 + 1 <= nr) lst[i0 + 1] = ex + a;
+        __syncthreads();
+    }
+    const uint64_t N = lst[nr];
+    uint32_t j0 = 0;
+    for (uint64_t t0 = 0; t0 < N; t0 += TILE) {
+        while (j0 + 1 < nr && lst[j0 + 1] <= t0) j0++;
+        const unsigned int n = (unsigned int)min((uint64_t)TILE, N - t0);
+        if (threadIdx.x < REFINE_FANOUT) tcnt[threadIdx.x] = 0;
+        __syncthreads();
+        // (plain u32 arrays: an array of uint4 was kept in memory, not registers)
+        unsigned int rx[PER], ry[PER], rz[PER], rw[PER], lr[PER], jj[PER], rk[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                const uint64_t l = t0 + i;
+                uint32_t jr = j0;
+                while (lst[jr + 1] <= l) jr++;
+                const uint4 v = recs[((ga + jr) * C + c) * cap + (l - lst[jr])];
+                rx[q] = v.x, ry[q] = v.y, rz[q] = v.z, rw[q] = v.w;
+                lr[q] = jr;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                jj[q] = fb ? (rw[q] >> 24) >> (SK2_FBITS - fb) : 0u;
+                rw[q] = (uint32_t)((read_base + (uint64_t)(ga + lr[q]) * gsize) * M) + (rw[q] & 0xFFFFFFu);
+                rk[q] = atomicAdd(&tcnt[jj[q]], 1u);
+            }
+        }
+        __syncthreads();
+        unsigned long long mybase = 0;
+        unsigned int myv = 0;
+        if (threadIdx.x < REFINE_FANOUT) {
+            const unsigned int v = (int)threadIdx.x < F ? tcnt[threadIdx.x] : 0u;
+            unsigned int incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int u = __shfl_up(incl, o);
+                if (lane >= o) incl += u;
+            }
+            tbeg[threadIdx.x] = incl - v;
+            if (lane == 63) wsum[wid] = incl;
+            myv = v;
+            if (v) mybase = atomicAdd(&fcur[c * F + threadIdx.x], (unsigned long long)v);
+        }
+        __syncthreads();
+        if (threadIdx.x >= 64 && threadIdx.x < REFINE_FANOUT) {
+            unsigned int add = 0;
+            for (int q = 0; q < (int)(threadIdx.x >> 6); q++) add += wsum[q];
+            tbeg[threadIdx.x] += add;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int i = threadIdx.x + q * BUCKET_THREADS;
+            if (i < n) {
+                const unsigned int p = tbeg[jj[q]] + rk[q];
+                tile[p] = make_uint4(rx[q], ry[q], rz[q], rw[q]);
+                tj[p] = (uint8_t)jj[q];
+            }
+        }
+        if (threadIdx.x < REFINE_FANOUT) {
+            if (mybase + myv > fcap) atomicOr(overflow, 1u);
+            base[threadIdx.x] = (c * F + threadIdx.x) * fcap + mybase;
+            tcnt[threadIdx.x] = mybase < fcap ? (unsigned int)min<unsigned long long>(fcap - mybase, 0xFFFFFFFFull) : 0u;
+        }
+        __syncthreads();
+        for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
+            const unsigned int j = tj[i];
+            const unsigned int q = i - tbeg[j];
+            if (q < tcnt[j]) out[base[j] + q] = tile[i];
+        }
+        __syncthreads();
+    }
+}
+
+// ---- bucket: super-k-mers -> LDS table
+// One record per lane (records of a chunk sorted by window count, most first, so a wave's
+// lanes run loops of nearly one length); the k-mers are rolled out of the packed bases.
+// FAST: the key at its first or second probe slot (most windows: ~150-fold coverage, tables
+// ~1/4 full) takes count += add and unconditional minima of its events; the other windows (new
+// keys, longer probe chains) are queued per wave as (record, window) and inserted by lds_insert
+// in batches of >= 32 (inline, lds_insert's wave-uniform probe loop runs as long as the slowest
+// of 64 lanes on every window).
+constexpr int SKB_Q = 96;  // queued windows per wave (< 32 before a step + 64 from it)
+template <int SLOTS, bool EVEN_K, bool FAST>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *recs, const unsigned long long *bbeg,
+                                                                 const unsigned long long *bend, int k, uint32_t M,
+                                                                 double inv_m, long long limit, unsigned long long *dkey,
+                                                                 unsigned int *dcnt, unsigned long long *dfc,
+                                                                 unsigned long long *dft, SubSlot *sub,
+                                                                 unsigned int *nsolid, unsigned long long *ndistinct,
+                                                                 unsigned int *overflow) {
+    constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
+    constexpr int NW = BUCKET_THREADS / 64;
+    __shared__ LTab<SLOTS> tab;
+    __shared__ unsigned int s_over[2];
+    // the chunk's records: x, y in the table's id words (LTab::id, unused without DET: keeps
+    // 2048-slot workgroups at two per CU), z, w here
+    __shared__ uint2 s_zw[BUCKET_THREADS];
+    __shared__ unsigned int s_ncnt[SK2_NMAX + 1];
+    __shared__ uint16_t s_q[NW][SKB_Q];  // queued windows: record << 4 | o
+    static_assert(sizeof(tab.id) >= BUCKET_THREADS * sizeof(uint2), "record staging in LTab::id");
+    uint2 *s_xy = reinterpret_cast<uint2 *>(tab.id);
+    const unsigned int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    lds_table_init<SLOTS>(tab, s_over);
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    const uint64_t kmask = kmask64(k);
+    const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
+    const unsigned int m2 = 2 * M - 1;
+    // a record's read (<< 32) and first window in it, from p = read * M + window
+    auto decode = [&](unsigned int p, unsigned long long &rdh, unsigned int &rem) {
+        const unsigned int rd = (unsigned int)((double)p * inv_m);  // p / M, corrected below
+        int rm = (int)(p - rd * M);
+        unsigned int read = rd;
+        if (rm < 0) read--, rm += (int)M;
+        else if (rm >= (int)M) read++, rm -= (int)M;
+        rdh = (unsigned long long)read << 32;
+        rem = (unsigned int)rm;
+    };
+    // events and add of window lf = rem + o given its fwd / rc codes; returns the canonical key
+    auto events = [&](uint64_t fwd, uint64_t rc, unsigned int lf, unsigned long long rdh, unsigned long long &eC,
+                      unsigned long long &eT, unsigned int &add) {
+        const bool tw = fwd > rc;
+        unsigned int lC = tw ? m2 - lf : lf, lT = tw ? lf : m2 - lf;
+        add = 1;
+        if (EVEN_K && fwd == rc) {  // even-k palindrome: inserted twice at the forward event
+            add = 2;
+            lC = lT = lf;
+        }
+        eC = rdh | lC;
+        eT = rdh | lT;
+        return tw ? rc : fwd;
+    };
+    unsigned int qn = 0;  // the wave's queued windows (uniform)
+    auto drain = [&]() {  // queued windows: bases straight out of the record (P = bases o .. o + 31)
+        for (unsigned int q0 = 0; q0 < qn; q0 += 64) {
+            if (q0 + lane < qn) {
+                const unsigned int e = s_q[wid][q0 + lane], r = e >> 4, o = e & 15u;
+                const uint2 xy = s_xy[r], zw = s_zw[r];
+                unsigned long long rdh, eC, eT;
+                unsigned int rem, add;
+                decode(zw.y, rdh, rem);
+                const uint32_t lo = __builtin_amdgcn_alignbit(xy.y, xy.x, 2 * o),
+                               hi = __builtin_amdgcn_alignbit(zw.x, xy.y, 2 * o);
+                const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+                const uint64_t c = events(rev2_64(P) >> fsh, ~P & kmask, rem + o, rdh, eC, eT, add);
+                lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
+            }
+        }
+        qn = 0;
+    };
+    uint4 nx = make_uint4(0, 0, 0, 0);
+    if (r0 + threadIdx.x < r1) nx = recs[r0 + threadIdx.x];
+    for (uint64_t c0 = r0; c0 < r1; c0 += BUCKET_THREADS) {
+        const unsigned int nv = (unsigned int)min<uint64_t>(BUCKET_THREADS, r1 - c0);
+        const uint4 x = nx;
+        if (c0 + BUCKET_THREADS + threadIdx.x < r1) nx = recs[c0 + BUCKET_THREADS + threadIdx.x];  // next chunk
+        if (threadIdx.x <= SK2_NMAX) s_ncnt[threadIdx.x] = 0;
+        __syncthreads();
+        const unsigned int bin = threadIdx.x < nv ? SK2_NMAX - 1 - (x.z >> 28) : SK2_NMAX;  // most windows first
+        const unsigned int rk = atomicAdd(&s_ncnt[bin], 1u);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned int a = 0;
+            for (int q = 0; q <= SK2_NMAX; q++) {
+                const unsigned int v = s_ncnt[q];
+                s_ncnt[q] = a;
+                a += v;
+            }
+        }
+        __syncthreads();
+        s_xy[s_ncnt[bin] + rk] = make_uint2(x.x, x.y);
+        s_zw[s_ncnt[bin] + rk] = make_uint2(x.z, x.w);
+        __syncthreads();
+        const uint2 xy = s_xy[threadIdx.x], zw = s_zw[threadIdx.x];
+        const unsigned int n = threadIdx.x < nv ? (zw.x >> 28) + 1 : 0u;
+        unsigned long long rdh;
+        unsigned int rem;
+        decode(zw.y, rdh, rem);
+        // window 0: bases 0 .. k - 1 (k <= 32: all in x, y)
+        const uint64_t lo = (uint64_t)xy.x | (uint64_t)xy.y << 32;
+        uint64_t fwd = rev2_64(lo) >> fsh;
+        uint64_t rc = ~lo & kmask;
+        const unsigned int nw = __builtin_amdgcn_readfirstlane(n);  // lane 0 has the wave's longest run
+        for (unsigned int o = 0; o < (FAST ? nw : n); o++) {
+            const bool act = o < n;
+            if (o) {
+                const unsigned int tb = o + (unsigned int)k - 1;
+                const uint32_t wd = tb < 32 ? xy.y : zw.x;
+                const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
+                fwd = ((fwd << 2) | bb) & kmask;
+                rc = (rc >> 2) | ((uint64_t)(3u - bb) << sh);
+            }
+            unsigned long long eC, eT;
+            unsigned int add;
+            const uint64_t c = events(fwd, rc, rem + o, rdh, eC, eT, add);
+            if (!FAST) {
+                lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
+                continue;
+            }
+            const unsigned int s0 = (sk_slot(c) >> (32 - SBITS)) & (SLOTS - 1), s1 = (s0 + 1) & (SLOTS - 1);
+            const unsigned long long k0 = tab.key[s0], k1 = tab.key[s1];
+            const bool hit = act && (k0 == c || k1 == c);
+            if (hit) {
+                const unsigned int slot = k0 == c ? s0 : s1;
+                atomicAdd(&tab.count[slot], add);
+                atomicMin(&tab.ev[slot].x, eC);
+                atomicMin(&tab.ev[slot].y, eT);
+            }
+            const bool slow = act && !hit;
+            const uint64_t bal = __ballot(slow);
+            if (slow) {
+                const uint32_t rk2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                s_q[wid][qn + rk2] = (uint16_t)(threadIdx.x << 4 | o);
+            }
+            qn += (unsigned int)__popcll(bal);
+            if (qn >= 32) drain();
+        }
+        if (FAST) drain();
+        __syncthreads();
+    }
+    lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
+}
+
+// -------------------------------------------------------
+// Records go through LDS in chunks of BUCKET_THREADS with the exclusive scan of their window
+// counts; the chunk's T windows are split evenly, lane t taking windows [t q, t q + q) of the
+// concatenation (q = ceil(T / BUCKET_THREADS)), so every wave runs q inserts per lane whatever
+// the run lengths.  Window o of a record is read straight out of its packed bases:
+// P = bases o .. o + 31 (two alignbits), rc = the complement of P's low k bases, fwd = their
+// 2-bit reversal (common.h rev2_64).
+// Insert fast path: the key at its first or second probe slot (most windows: ~150-fold
+// coverage, tables ~1/4 full) takes count += add and unconditional minima of its events.  The
+// other windows (new keys, longer probe chains) are queued per wave as (record, window) and
+// inserted by lds_insert in batches of >= 32: run inline, lds_insert's wave-uniform probe loop
+// ran as long as the slowest of 64 lanes on every window (~130 instructions per window).
+template <int SLOTS, bool EVEN_K, int FAST>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, const unsigned long long *bbeg,
+                                                             const unsigned long long *bend, int k, uint32_t M,
+                                                             double inv_m, long long limit, unsigned long long *dkey,
+                                                             unsigned int *dcnt, unsigned long long *dfc,
+                                                             unsigned long long *dft, SubSlot *sub,
+                                                             unsigned int *nsolid, unsigned long long *ndistinct,
+                                                             unsigned int *overflow) {
+    constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
+    constexpr int NW = BUCKET_THREADS / 64;
+    __shared__ LTab<SLOTS> tab;
+    __shared__ unsigned int s_over[2];
+    // the chunk's records: x, y in the table's id words (LTab::id, unused without DET: keeps
+    // 2048-slot workgroups at two per CU), z, w here; window scan; first record of each lane
+    __shared__ uint2 s_zw[BUCKET_THREADS];
+    __shared__ uint16_t s_pre[BUCKET_THREADS];  // T <= 16 BUCKET_THREADS
+    __shared__ uint16_t s_first[BUCKET_THREADS];
+    __shared__ uint16_t s_q[NW][SKB_Q];  // queued windows: record << 4 | o
+    __shared__ unsigned int s_wsum[NW];
+    static_assert(sizeof(tab.id) >= BUCKET_THREADS * sizeof(uint2), "record staging in LTab::id");
+    uint2 *s_xy = reinterpret_cast<uint2 *>(tab.id);
+    const unsigned int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    lds_table_init<SLOTS>(tab, s_over);
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    const uint64_t kmask = kmask64(k);
+    const int fsh = 64 - 2 * k;
+    const unsigned int m2 = 2 * M - 1;
+    // record r's read (<< 32) and first window in it
+    auto decode = [&](unsigned int p, unsigned long long &rdh, unsigned int &rem) {
+        const unsigned int rd = (unsigned int)((double)p * inv_m);  // p / M, corrected below
+        int rm = (int)(p - rd * M);
+        unsigned int read = rd;
+        if (rm < 0) read--, rm += (int)M;
+        else if (rm >= (int)M) read++, rm -= (int)M;
+        rdh = (unsigned long long)read << 32;
+        rem = (unsigned int)rm;
+    };
+    // window o of the record with bases xy, zw: canonical key, events, add
+    auto window = [&](const uint2 &xy, const uint2 &zw, unsigned int o, unsigned long long rdh, unsigned int rem,
+                      uint64_t &c, unsigned long long &eC, unsigned long long &eT, unsigned int &add) {
+        const uint32_t lo = __builtin_amdgcn_alignbit(xy.y, xy.x, 2 * o), hi = __builtin_amdgcn_alignbit(zw.x, xy.y, 2 * o);
+        const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+        const uint64_t rc = ~P & kmask, fwd = rev2_64(P) >> fsh;
+        const bool tw = fwd > rc;
+        c = tw ? rc : fwd;
+        const unsigned int lf = rem + o;
+        unsigned int lC = tw ? m2 - lf : lf, lT = tw ? lf : m2 - lf;
+        add = 1;
+        if (EVEN_K && fwd == rc) {  // even-k palindrome: inserted twice at the forward event
+            add = 2;
+            lC = lT = lf;
+        }
+        eC = rdh | lC;
+        eT = rdh | lT;
+    };
+    unsigned int qn = 0;  // the wave's queued windows (uniform)
+    auto drain = [&]() {
+        for (unsigned int q0 = 0; q0 < qn; q0 += 64) {
+            if (q0 + lane < qn) {
+                const unsigned int e = s_q[wid][q0 + lane], r = e >> 4, o = e & 15u;
+                unsigned long long rdh, eC, eT;
+                unsigned int rem, add;
+                uint64_t c;
+                decode(s_zw[r].y, rdh, rem);
+                window(s_xy[r], s_zw[r], o, rdh, rem, c, eC, eT, add);
+                lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
+            }
+        }
+        qn = 0;
+    };
+    uint4 nx = make_uint4(0, 0, 0, 0);
+    if (r0 + threadIdx.x < r1) nx = recs[r0 + threadIdx.x];
+    for (uint64_t c0 = r0; c0 < r1; c0 += BUCKET_THREADS) {
+        const unsigned int nv = (unsigned int)min<uint64_t>(BUCKET_THREADS, r1 - c0);
+        const uint4 x = nx;
+        if (c0 + BUCKET_THREADS + threadIdx.x < r1) nx = recs[c0 + BUCKET_THREADS + threadIdx.x];  // next chunk
+        const unsigned int n = threadIdx.x < nv ? (x.z >> 28) + 1 : 0u;
+        s_xy[threadIdx.x] = make_uint2(x.x, x.y);
+        s_zw[threadIdx.x] = make_uint2(x.z, x.w);
+        const unsigned int incl = wave_incl_scan(n);
+        if (lane == 63) s_wsum[wid] = incl;
+        __syncthreads();
+        unsigned int before = 0, T = 0;
+#pragma unroll
+        for (int q = 0; q < NW; q++) {
+            const unsigned int v = s_wsum[q];
+            before += q < (int)wid ? v : 0u;
+            T += v;
+        }
+        const unsigned int pre = before + incl - n;
+        s_pre[threadIdx.x] = (uint16_t)pre;
+        const unsigned int q = (T + BUCKET_THREADS - 1) / BUCKET_THREADS;  // windows per lane
+        for (unsigned int l = (pre + q - 1) / q; l * q < pre + n; l++) s_first[l] = (uint16_t)threadIdx.x;
+        __syncthreads();
+        const unsigned int w0 = threadIdx.x * q, w1 = min(w0 + q, T);
+        unsigned int r = 0, pr = 0, end = 0, rem = 0;
+        uint2 xy = make_uint2(0, 0), zw = make_uint2(0, 0);
+        unsigned long long rdh = 0;
+        auto load = [&]() {
+            xy = s_xy[r];
+            zw = s_zw[r];
+            pr = s_pre[r];
+            end = pr + (zw.x >> 28) + 1;
+            decode(zw.y, rdh, rem);
+        };
+        if (w0 < T) {
+            r = s_first[threadIdx.x];
+            load();
+        }
+        for (unsigned int it = 0; it < q; it++) {  // wave-uniform trip count
+            const unsigned int wi = w0 + it;
+            const bool act = wi < w1;
+            if (act && wi >= end) {  // the next record (n >= 1: one step at most)
+                r++;
+                load();
+            }
+            const unsigned int o = wi - pr;  // < 16
+            unsigned long long eC, eT;
+            unsigned int add;
+            uint64_t c;
+            window(xy, zw, o, rdh, rem, c, eC, eT, add);
+            if (FAST == 0) {
+                if (act) lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
+                continue;
+            }
+            const unsigned int s0 = (sk_slot(c) >> (32 - SBITS)) & (SLOTS - 1), s1 = (s0 + 1) & (SLOTS - 1);
+            const unsigned long long k0 = tab.key[s0], k1 = tab.key[s1];
+            const bool hit = act && (k0 == c || k1 == c);
+            if (hit) {
+                const unsigned int slot = k0 == c ? s0 : s1;
+                atomicAdd(&tab.count[slot], add);
+                if (FAST == 1) {
+                    atomicMin(&tab.ev[slot].x, eC);
+                    atomicMin(&tab.ev[slot].y, eT);
+                } else {
+                    const ulonglong2 ev = tab.ev[slot];
+                    if (eC < ev.x) atomicMin(&tab.ev[slot].x, eC);
+                    if (eT < ev.y) atomicMin(&tab.ev[slot].y, eT);
+                }
+            }
+            const bool slow = act && !hit;
+            const uint64_t bal = __ballot(slow);
+            if (slow) {
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                s_q[wid][qn + rk] = (uint16_t)(r << 4 | o);
+            }
+            qn += (unsigned int)__popcll(bal);
+            if (qn >= 32) drain();
+        }
+        drain();
+        __syncthreads();
+    }
+    lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
+}
+
+}  // namespace ec

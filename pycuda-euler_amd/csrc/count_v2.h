@@ -169,6 +169,27 @@ __device__ inline uint32_t pack16(const uint4 &v) {
     return pack4(v.x) | (pack4(v.y) << 8) | (pack4(v.z) << 16) | (pack4(v.w) << 24);
 }
 
+// Next wave tile's bytes into pf[] and its reads' offsets (k_partition, k_skpart): uses the
+// kernel's g0, g1, off, buf, lane, pf, nx_base, nx_s, nx_e, nx_n
+// (a macro, not a lambda: a lambda capturing pf keeps the array in scratch memory)
+#define EC_PT_ISSUE(T)                                                                                   \
+    do {                                                                                                 \
+        const uint64_t r0_ = g0 + 64ull * (T), r1_ = min(r0_ + 64, g1);                                  \
+        const uint64_t b0_ = off[r0_], b1_ = off[r1_]; /* wave-uniform: scalar loads */                  \
+        const uint8_t *p0_ = buf + b0_ - (((uint64_t)(buf + b0_)) & 15); /* derived from buf: global */  \
+        const uint64_t a1_ = (((uint64_t)(buf + b1_)) + 15) & ~15ull;                                      \
+        const uint32_t n16_ = (uint32_t)((a1_ - (uint64_t)p0_) >> 4); /* <= NPF * 64: host checks */    \
+        const uint4 *src_ = reinterpret_cast<const uint4 *>(p0_);                                         \
+        _Pragma("unroll") for (int q = 0; q < NPF; q++)                                                   \
+            pf[q] = src_[min(q * 64 + lane, n16_ - 1)]; /* in bounds: no branch around the load */       \
+        nx_base = (uint64_t)p0_ - (uint64_t)buf;                                                         \
+        /* low words of the read's offsets (differences mod 2^32; no wait until they are used) */       \
+        const uint64_t ri_ = min(r0_ + lane, r1_ - 1);                                                   \
+        nx_s = reinterpret_cast<const uint32_t *>(off)[2 * ri_];                                         \
+        nx_e = reinterpret_cast<const uint32_t *>(off)[2 * ri_ + 2];                                     \
+        nx_n = (uint32_t)(r1_ - r0_);                                                                    \
+    } while (0)
+
 // Every read with windows has exactly M windows and no N (k_prescan checked).  Record of
 // window w of read r: key = canonical code, meta = (read_base + r) << (ibits + 1) | o << ibits | w
 // (Rec12, count_part.h).  Region of (c, g): records [(g * C + c) * cap, + cap) of keys / meta
@@ -228,24 +249,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
     uint4 pf[NPF];
     uint64_t nx_base = 0;
     uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
-    // (a macro, not a lambda: a lambda capturing pf keeps the array in scratch memory)
-#define EC_PT_ISSUE(T)                                                                                   \
-    do {                                                                                                 \
-        const uint64_t r0_ = g0 + 64ull * (T), r1_ = min(r0_ + 64, g1);                                  \
-        const uint64_t b0_ = off[r0_], b1_ = off[r1_]; /* wave-uniform: scalar loads */                  \
-        const uint8_t *p0_ = buf + b0_ - (((uint64_t)(buf + b0_)) & 15); /* derived from buf: global */  \
-        const uint64_t a1_ = (((uint64_t)(buf + b1_)) + 15) & ~15ull;                                      \
-        const uint32_t n16_ = (uint32_t)((a1_ - (uint64_t)p0_) >> 4); /* <= NPF * 64: host checks */    \
-        const uint4 *src_ = reinterpret_cast<const uint4 *>(p0_);                                         \
-        _Pragma("unroll") for (int q = 0; q < NPF; q++)                                                   \
-            pf[q] = src_[min(q * 64 + lane, n16_ - 1)]; /* in bounds: no branch around the load */       \
-        nx_base = (uint64_t)p0_ - (uint64_t)buf;                                                         \
-        /* low words of the read's offsets (differences mod 2^32; no wait until they are used) */       \
-        const uint64_t ri_ = min(r0_ + lane, r1_ - 1);                                                   \
-        nx_s = reinterpret_cast<const uint32_t *>(off)[2 * ri_];                                         \
-        nx_e = reinterpret_cast<const uint32_t *>(off)[2 * ri_ + 2];                                     \
-        nx_n = (uint32_t)(r1_ - r0_);                                                                    \
-    } while (0)
     if (wid < ntile) EC_PT_ISSUE(wid);
     const unsigned long long gcap = g * C * cap, gstride = cap;
     const unsigned long long spill = (unsigned long long)C * G * cap;
@@ -384,7 +387,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
             wave_sync();
         }
     }
-#undef EC_PT_ISSUE
     __syncthreads();
     if (threadIdx.x < C) cnt[(uint64_t)threadIdx.x * G + g] = (unsigned int)min((uint64_t)s_cur[threadIdx.x], cap);
     unsigned int *hw = reinterpret_cast<unsigned int *>(hll + g * NREG);

@@ -156,15 +156,19 @@ def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode)
     if mode == "superkmer" and 21 <= k <= 32 and nr == 0:
         assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
     if mode in ("partitioned", "window_records") and k <= 32 and nr == 0 \
-            and res.stats.count_path == eulerhip.EC_PATH_PARTITIONED:  # one read length, no N: 12-B records
-        assert res.stats.record_bytes == 12
+            and res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.count_variant != 3:
+        assert res.stats.record_bytes == 12  # one read length, no N: 12-B window records
     if mode == "window_records" and k <= 32:
         assert res.stats.count_path in (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_GENERAL)
     if mode == "wide_records" and k <= 32:
         assert res.stats.record_bytes == 16
     # one read length, no N, k <= 32: the fixed-capacity runs of count_v2.h unless asked otherwise
     if mode in ("partitioned", "window_records") and k <= 32 and nr == 0:
-        assert res.stats.count_variant == 1 and res.stats.record_bytes == 12  # small inputs: 12-B records
+        if mode == "partitioned" and 21 <= k and err <= 0.01:  # 16-B super-k-mer records (count_sk2.h)
+            assert res.stats.count_variant == 3 and res.stats.record_bytes == 16
+            assert 0 < res.stats.n_records < res.stats.n_positions
+        else:  # small inputs: 12-B window records
+            assert res.stats.count_variant == 1 and res.stats.record_bytes == 12
     if mode == "exact":
         assert res.stats.count_variant == 0
 
@@ -424,8 +428,9 @@ def test_v2_skew_falls_back_vs_oracle(gpu_session, k):
 
 
 @pytest.mark.parametrize("L,k", [(40, 11), (63, 31), (100, 17), (111, 27), (150, 31), (159, 32), (200, 31)])
-def test_v2_read_lengths_vs_oracle(gpu_session, L, k):
+def test_v2_read_lengths_vs_oracle(gpu_session, monkeypatch, L, k):
     """wave tiles of 64 reads staged in 4, 7 or 10 KiB per wave; longer reads take the exact path"""
+    monkeypatch.setenv("EULERHIP_NO_SK2", "1")
     buf, off = make_reads(40_000, 9_000 - 30 * L, L, 3000 + L + k, err=0.003)
     ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
     gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
@@ -438,7 +443,8 @@ def test_v2_read_lengths_vs_oracle(gpu_session, L, k):
 
 @pytest.mark.parametrize("pmax,lim", [(2, 1), (3, 0)])
 def test_v2_filter_parts_vs_oracle(gpu_session, monkeypatch, pmax, lim):
-    """seen-twice filter + part tables over the fixed-capacity final buckets"""
+    """seen-twice filter + part tables over the fixed-capacity final buckets (count_sk2.h
+    declines inputs that need the filter)"""
     monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
     monkeypatch.setenv("EULERHIP_FILTER_PMAX", str(pmax))
     monkeypatch.setenv("EULERHIP_FILTER_PMIN", str(pmax))
@@ -451,8 +457,11 @@ def test_v2_filter_parts_vs_oracle(gpu_session, monkeypatch, pmax, lim):
     assert [[x, c] for x, c in res.dict_items] == ref["d"]
 
 
-def test_v2_read_base_and_short_reads_vs_oracle(gpu_session):
+@pytest.mark.parametrize("sk2", [False, True])
+def test_v2_read_base_and_short_reads_vs_oracle(gpu_session, monkeypatch, sk2):
     """reads shorter than k (any length) beside one windowed length; a non-multiple-of-64 count"""
+    if not sk2:
+        monkeypatch.setenv("EULERHIP_NO_SK2", "1")
     rng = np.random.default_rng(5)
     g = "".join("ACGT"[x] for x in rng.integers(0, 4, 20_000))
     reads = []
@@ -462,7 +471,7 @@ def test_v2_read_base_and_short_reads_vs_oracle(gpu_session):
         reads.append(g[p:p + L])
     d, r, gl = oracle.assemble(reads, 31, 1)
     res = gpu_session.assemble(reads, 31, 1, want_dict=True)
-    assert res.stats.count_variant == 1
+    assert res.stats.count_variant == (3 if sk2 else 1)
     assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == gl
 
 
@@ -473,6 +482,7 @@ def test_v2_read_base_and_short_reads_vs_oracle(gpu_session):
     (30_000, 9_000, 120, 8, 0.002, 22), (10_000, 3_333, 64, 9, 0.0, 17)])
 def test_r10_vs_oracle(gpu_session, monkeypatch, g, n, L, seed, err, k):
     monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    monkeypatch.setenv("EULERHIP_NO_SK2", "1")
     buf, off = make_reads(g, n, L, 4000 + seed, err=err)
     want_dict = g <= 50_000
     ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
@@ -489,6 +499,7 @@ def test_r10_vs_oracle(gpu_session, monkeypatch, g, n, L, seed, err, k):
 def test_r10_slices_vs_oracle(gpu_session, monkeypatch, rs):
     """the refine over 8..32 group slices per coarse bucket"""
     monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    monkeypatch.setenv("EULERHIP_NO_SK2", "1")
     monkeypatch.setenv("EULERHIP_REFINE_RS", rs)
     buf, off = make_reads(60_000, 40_000, 100, 4100 + int(rs), err=0.003)
     ref, rc, rl = _oracle_packed(buf, off, 27, 1, True)
@@ -503,6 +514,7 @@ def test_r10_slices_vs_oracle(gpu_session, monkeypatch, rs):
 def test_r10_filter_and_limits_vs_oracle(gpu_session, monkeypatch, lim, pmax):
     """seen-twice filter / part tables and other limits over 10-byte records"""
     monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    monkeypatch.setenv("EULERHIP_NO_SK2", "1")
     if pmax:
         monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
         monkeypatch.setenv("EULERHIP_FILTER_PMAX", str(pmax))
@@ -520,8 +532,83 @@ def test_r10_filter_and_limits_vs_oracle(gpu_session, monkeypatch, lim, pmax):
 def test_r10_palindromes_vs_oracle(gpu_session, monkeypatch):
     """even k: palindromic k-mers (inserted twice by build) recovered from the hashed keys"""
     monkeypatch.setenv("EULERHIP_V2_R10", "1")
+    monkeypatch.setenv("EULERHIP_NO_SK2", "1")
     reads = _low_complexity_reads(1500, 100, 77)
     for k in (16, 20, 24, 32):
         d, r, g = oracle.assemble(reads, k, 1)
         res = gpu_session.assemble(reads, k, 1, want_dict=True)
         assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g, k
+
+
+# ---- super-k-mer records (count_sk2.h) -------------------------------------------------------
+SK2 = [(20_000, 4_000, 100, 1, 0.0, 31), (50_000, 20_000, 100, 2, 0.002, 31), (30_000, 10_000, 80, 3, 0.001, 25),
+       (200_000, 60_000, 100, 6, 0.0, 32), (30_000, 9_000, 120, 8, 0.0, 22), (10_000, 3_333, 64, 9, 0.0, 21),
+       (40_000, 12_000, 150, 10, 0.001, 27), (5_000, 2_000, 40, 11, 0.0, 21), (8_000, 700, 31, 12, 0.0, 31)]
+
+
+@pytest.mark.parametrize("g,n,L,seed,err,k", SK2)
+def test_sk2_vs_oracle(gpu_session, g, n, L, seed, err, k):
+    """16-byte super-k-mer records: partition by minimizer, refine, rolled-out bucket tables"""
+    buf, off = make_reads(g, n, L, 5000 + seed, err=err)
+    want_dict = g <= 50_000
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, want_dict)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT if want_dict else 0)
+    res = gpu_session.fetch(k, want_dict)
+    assert res.stats.count_variant == 3 and res.stats.record_bytes == 16
+    assert 0 < res.stats.n_records <= res.stats.n_positions
+    assert res.stats.n_positions == ref["n_positions"] and res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"] and np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert res.links == rl
+    if want_dict:
+        assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+@pytest.mark.parametrize("rs", ["1", "8", "32"])
+def test_sk2_slices_and_limits_vs_oracle(gpu_session, monkeypatch, rs):
+    """the super-k-mer refine over 1..32 group slices per coarse bucket; limits -1 .. 5"""
+    monkeypatch.setenv("EULERHIP_REFINE_RS", rs)
+    buf, off = make_reads(40_000, 15_000, 100, 5100 + int(rs), err=0.003)
+    for k, lim in ((31, 1), (24, 0), (29, 2), (31, -1), (26, 5)):
+        ref, rc, rl = _oracle_packed(buf, off, k, lim, True)
+        gpu_session.run_host(buf, off, k, lim, eulerhip.EC_FLAG_WANT_DICT)
+        res = gpu_session.fetch(k, True)
+        assert res.stats.count_variant == 3, (k, lim)
+        assert [[x, c] for x, c in res.dict_items] == ref["d"], (k, lim)
+        assert res.contig_bytes == ref["contig_chars"] and res.links == rl, (k, lim)
+
+
+def test_sk2_palindromes_vs_oracle(gpu_session):
+    """even k: palindromic k-mers (inserted twice by build) inside super-k-mers"""
+    rng = np.random.default_rng(17)
+    comp = str.maketrans("ACGT", "TGCA")
+    parts = []
+    for _ in range(60):
+        parts.append("".join("ACGT"[x] for x in rng.integers(0, 4, 300)))
+        x = "".join("ACGT"[x] for x in rng.integers(0, 4, 16))
+        parts.append(x + x.translate(comp)[::-1])  # a 32-base palindrome: its centred even k-mers are too
+    g = "".join(parts)
+    reads = []
+    for _ in range(4000):
+        p = int(rng.integers(0, len(g) - 100))
+        r = g[p:p + 100]
+        reads.append(r if rng.random() < 0.5 else r.translate(comp)[::-1])
+    for k in (22, 24, 32):
+        d, r, gl = oracle.assemble(reads, k, 1)
+        res = gpu_session.assemble(reads, k, 1, want_dict=True)
+        assert res.stats.count_variant == 3, k
+        assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == gl, k
+
+
+def test_sk2_declines_filter_and_window_records(gpu_session, monkeypatch):
+    """inputs that need the seen-twice filter, and EC_FLAG_WINDOW_RECORDS, count window records"""
+    buf, off = make_reads(30_000, 8_000, 100, 5200, err=0.004)
+    ref, rc, rl = _oracle_packed(buf, off, 31, 1, True)
+    gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_WANT_DICT | eulerhip.EC_FLAG_WINDOW_RECORDS)
+    res = gpu_session.fetch(31, True)
+    assert res.stats.count_variant == 1
+    assert [[x, c] for x, c in res.dict_items] == ref["d"] and res.links == rl
+    monkeypatch.setenv("EULERHIP_FORCE_FILTER", "1")
+    gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(31, True)
+    assert res.stats.count_variant == 1
+    assert [[x, c] for x, c in res.dict_items] == ref["d"] and res.links == rl

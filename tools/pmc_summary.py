@@ -3,7 +3,7 @@ import collections
 import csv
 import sys
 
-KEYS = ('k_partition', 'k_refine2', 'k_bucket', 'k_prescan', 'k_link', 'k_walk', 'k_rjump', 'k_final', 'k_starts', 'k_emit')
+KEYS = ('k_sk', 'k_partition', 'k_refine2', 'k_bucket', 'k_prescan', 'k_link', 'k_walk', 'k_rjump', 'k_final', 'k_starts', 'k_emit')
 for path in sys.argv[1:]:
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(path)):
