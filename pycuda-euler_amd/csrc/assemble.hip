@@ -459,19 +459,8 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
     kmark(s, 2, 0);
     const double inv_m = 1.0 / M;
-#ifndef SKB_MODE
-#define SKB_MODE 0
-#endif
-#ifndef SKB_REC_FAST
-#define SKB_REC_FAST true
-#endif
-#if SKB_MODE == 0
-#define EC_SKB(SLOTS, EVEN) k_skbucket_rec<SLOTS, EVEN, SKB_REC_FAST>
-#else
-#define EC_SKB(SLOTS, EVEN) k_skbucket<SLOTS, EVEN, SKB_MODE - 1>
-#endif
 #define EC_SKBUCKET(SLOTS, EVEN)                                                                              \
-    EC_SKB(SLOTS, EVEN)<<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(                                              \
+    k_skbucket<SLOTS, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(                                          \
         s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(),                \
         s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),          \
         s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow)
@@ -483,7 +472,6 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         else EC_SKBUCKET(4096, true);
     }
 #undef EC_SKBUCKET
-#undef EC_SKB
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));

@@ -371,40 +371,36 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skrefine(const uint4 *recs, 
 }
 
 // ---- bucket: super-k-mers -> LDS table
-// One record per lane (records of a chunk sorted by window count, most first, so a wave's
-// lanes run loops of nearly one length); the k-mers are rolled out of the packed bases.
-// FAST: the key at its first or second probe slot (most windows: ~150-fold coverage, tables
-// ~1/4 full) takes count += add and unconditional minima of its events; the other windows (new
-// keys, longer probe chains) are queued per wave as (record, window) and inserted by lds_insert
-// in batches of >= 32 (inline, lds_insert's wave-uniform probe loop runs as long as the slowest
-// of 64 lanes on every window).
-constexpr int SKB_Q = 96;  // queued windows per wave (< 32 before a step + 64 from it)
-template <int SLOTS, bool EVEN_K, bool FAST>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *recs, const unsigned long long *bbeg,
-                                                                 const unsigned long long *bend, int k, uint32_t M,
-                                                                 double inv_m, long long limit, unsigned long long *dkey,
-                                                                 unsigned int *dcnt, unsigned long long *dfc,
-                                                                 unsigned long long *dft, SubSlot *sub,
-                                                                 unsigned int *nsolid, unsigned long long *ndistinct,
-                                                                 unsigned int *overflow) {
+// Records go through LDS in chunks of BUCKET_THREADS, sorted by window count (most first) so a
+// wave's lanes run loops of nearly one length; lane = record: window 0 from the packed bases
+// (fwd = their 2-bit reversal, common.h rev2_64; rc = their complement), later windows rolled.
+// Measured equal or slower: the chunk's windows split evenly over the lanes
+// (each window read straight out of the bases), and a two-slot fast path with the other
+// windows queued for lds_insert.
+template <int SLOTS, bool EVEN_K>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, const unsigned long long *bbeg,
+                                                             const unsigned long long *bend, int k, uint32_t M,
+                                                             double inv_m, long long limit, unsigned long long *dkey,
+                                                             unsigned int *dcnt, unsigned long long *dfc,
+                                                             unsigned long long *dft, SubSlot *sub,
+                                                             unsigned int *nsolid, unsigned long long *ndistinct,
+                                                             unsigned int *overflow) {
     constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
-    constexpr int NW = BUCKET_THREADS / 64;
     __shared__ LTab<SLOTS> tab;
     __shared__ unsigned int s_over[2];
     // the chunk's records: x, y in the table's id words (LTab::id, unused without DET: keeps
     // 2048-slot workgroups at two per CU), z, w here
     __shared__ uint2 s_zw[BUCKET_THREADS];
     __shared__ unsigned int s_ncnt[SK2_NMAX + 1];
-    __shared__ uint16_t s_q[NW][SKB_Q];  // queued windows: record << 4 | o
     static_assert(sizeof(tab.id) >= BUCKET_THREADS * sizeof(uint2), "record staging in LTab::id");
     uint2 *s_xy = reinterpret_cast<uint2 *>(tab.id);
-    const unsigned int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned int b = blockIdx.x;
     lds_table_init<SLOTS>(tab, s_over);
     const uint64_t r0 = bbeg[b], r1 = bend[b];
     const uint64_t kmask = kmask64(k);
     const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
     const unsigned int m2 = 2 * M - 1;
-    // a record's read (<< 32) and first window in it, from p = read * M + window
+    // the record's read (<< 32) and first window in it, from p = read * M + window
     auto decode = [&](unsigned int p, unsigned long long &rdh, unsigned int &rem) {
         const unsigned int rd = (unsigned int)((double)p * inv_m);  // p / M, corrected below
         int rm = (int)(p - rd * M);
@@ -427,24 +423,6 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *re
         eC = rdh | lC;
         eT = rdh | lT;
         return tw ? rc : fwd;
-    };
-    unsigned int qn = 0;  // the wave's queued windows (uniform)
-    auto drain = [&]() {  // queued windows: bases straight out of the record (P = bases o .. o + 31)
-        for (unsigned int q0 = 0; q0 < qn; q0 += 64) {
-            if (q0 + lane < qn) {
-                const unsigned int e = s_q[wid][q0 + lane], r = e >> 4, o = e & 15u;
-                const uint2 xy = s_xy[r], zw = s_zw[r];
-                unsigned long long rdh, eC, eT;
-                unsigned int rem, add;
-                decode(zw.y, rdh, rem);
-                const uint32_t lo = __builtin_amdgcn_alignbit(xy.y, xy.x, 2 * o),
-                               hi = __builtin_amdgcn_alignbit(zw.x, xy.y, 2 * o);
-                const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
-                const uint64_t c = events(rev2_64(P) >> fsh, ~P & kmask, rem + o, rdh, eC, eT, add);
-                lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
-            }
-        }
-        qn = 0;
     };
     uint4 nx = make_uint4(0, 0, 0, 0);
     if (r0 + threadIdx.x < r1) nx = recs[r0 + threadIdx.x];
@@ -478,9 +456,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *re
         const uint64_t lo = (uint64_t)xy.x | (uint64_t)xy.y << 32;
         uint64_t fwd = rev2_64(lo) >> fsh;
         uint64_t rc = ~lo & kmask;
-        const unsigned int nw = __builtin_amdgcn_readfirstlane(n);  // lane 0 has the wave's longest run
-        for (unsigned int o = 0; o < (FAST ? nw : n); o++) {
-            const bool act = o < n;
+        for (unsigned int o = 0; o < n; o++) {
             if (o) {
                 const unsigned int tb = o + (unsigned int)k - 1;
                 const uint32_t wd = tb < 32 ? xy.y : zw.x;
@@ -491,201 +467,12 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *re
             unsigned long long eC, eT;
             unsigned int add;
             const uint64_t c = events(fwd, rc, rem + o, rdh, eC, eT, add);
-            if (!FAST) {
-                lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
-                continue;
-            }
-            const unsigned int s0 = (sk_slot(c) >> (32 - SBITS)) & (SLOTS - 1), s1 = (s0 + 1) & (SLOTS - 1);
-            const unsigned long long k0 = tab.key[s0], k1 = tab.key[s1];
-            const bool hit = act && (k0 == c || k1 == c);
-            if (hit) {
-                const unsigned int slot = k0 == c ? s0 : s1;
-                atomicAdd(&tab.count[slot], add);
-                atomicMin(&tab.ev[slot].x, eC);
-                atomicMin(&tab.ev[slot].y, eT);
-            }
-            const bool slow = act && !hit;
-            const uint64_t bal = __ballot(slow);
-            if (slow) {
-                const uint32_t rk2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                s_q[wid][qn + rk2] = (uint16_t)(threadIdx.x << 4 | o);
-            }
-            qn += (unsigned int)__popcll(bal);
-            if (qn >= 32) drain();
+            lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
         }
-        if (FAST) drain();
         __syncthreads();
     }
     lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
 }
 
 // -------------------------------------------------------
-// Records go through LDS in chunks of BUCKET_THREADS with the exclusive scan of their window
-// counts; the chunk's T windows are split evenly, lane t taking windows [t q, t q + q) of the
-// concatenation (q = ceil(T / BUCKET_THREADS)), so every wave runs q inserts per lane whatever
-// the run lengths.  Window o of a record is read straight out of its packed bases:
-// P = bases o .. o + 31 (two alignbits), rc = the complement of P's low k bases, fwd = their
-// 2-bit reversal (common.h rev2_64).
-// Insert fast path: the key at its first or second probe slot (most windows: ~150-fold
-// coverage, tables ~1/4 full) takes count += add and unconditional minima of its events.  The
-// other windows (new keys, longer probe chains) are queued per wave as (record, window) and
-// inserted by lds_insert in batches of >= 32: run inline, lds_insert's wave-uniform probe loop
-// ran as long as the slowest of 64 lanes on every window (~130 instructions per window).
-template <int SLOTS, bool EVEN_K, int FAST>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, const unsigned long long *bbeg,
-                                                             const unsigned long long *bend, int k, uint32_t M,
-                                                             double inv_m, long long limit, unsigned long long *dkey,
-                                                             unsigned int *dcnt, unsigned long long *dfc,
-                                                             unsigned long long *dft, SubSlot *sub,
-                                                             unsigned int *nsolid, unsigned long long *ndistinct,
-                                                             unsigned int *overflow) {
-    constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
-    constexpr int NW = BUCKET_THREADS / 64;
-    __shared__ LTab<SLOTS> tab;
-    __shared__ unsigned int s_over[2];
-    // the chunk's records: x, y in the table's id words (LTab::id, unused without DET: keeps
-    // 2048-slot workgroups at two per CU), z, w here; window scan; first record of each lane
-    __shared__ uint2 s_zw[BUCKET_THREADS];
-    __shared__ uint16_t s_pre[BUCKET_THREADS];  // T <= 16 BUCKET_THREADS
-    __shared__ uint16_t s_first[BUCKET_THREADS];
-    __shared__ uint16_t s_q[NW][SKB_Q];  // queued windows: record << 4 | o
-    __shared__ unsigned int s_wsum[NW];
-    static_assert(sizeof(tab.id) >= BUCKET_THREADS * sizeof(uint2), "record staging in LTab::id");
-    uint2 *s_xy = reinterpret_cast<uint2 *>(tab.id);
-    const unsigned int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    lds_table_init<SLOTS>(tab, s_over);
-    const uint64_t r0 = bbeg[b], r1 = bend[b];
-    const uint64_t kmask = kmask64(k);
-    const int fsh = 64 - 2 * k;
-    const unsigned int m2 = 2 * M - 1;
-    // record r's read (<< 32) and first window in it
-    auto decode = [&](unsigned int p, unsigned long long &rdh, unsigned int &rem) {
-        const unsigned int rd = (unsigned int)((double)p * inv_m);  // p / M, corrected below
-        int rm = (int)(p - rd * M);
-        unsigned int read = rd;
-        if (rm < 0) read--, rm += (int)M;
-        else if (rm >= (int)M) read++, rm -= (int)M;
-        rdh = (unsigned long long)read << 32;
-        rem = (unsigned int)rm;
-    };
-    // window o of the record with bases xy, zw: canonical key, events, add
-    auto window = [&](const uint2 &xy, const uint2 &zw, unsigned int o, unsigned long long rdh, unsigned int rem,
-                      uint64_t &c, unsigned long long &eC, unsigned long long &eT, unsigned int &add) {
-        const uint32_t lo = __builtin_amdgcn_alignbit(xy.y, xy.x, 2 * o), hi = __builtin_amdgcn_alignbit(zw.x, xy.y, 2 * o);
-        const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
-        const uint64_t rc = ~P & kmask, fwd = rev2_64(P) >> fsh;
-        const bool tw = fwd > rc;
-        c = tw ? rc : fwd;
-        const unsigned int lf = rem + o;
-        unsigned int lC = tw ? m2 - lf : lf, lT = tw ? lf : m2 - lf;
-        add = 1;
-        if (EVEN_K && fwd == rc) {  // even-k palindrome: inserted twice at the forward event
-            add = 2;
-            lC = lT = lf;
-        }
-        eC = rdh | lC;
-        eT = rdh | lT;
-    };
-    unsigned int qn = 0;  // the wave's queued windows (uniform)
-    auto drain = [&]() {
-        for (unsigned int q0 = 0; q0 < qn; q0 += 64) {
-            if (q0 + lane < qn) {
-                const unsigned int e = s_q[wid][q0 + lane], r = e >> 4, o = e & 15u;
-                unsigned long long rdh, eC, eT;
-                unsigned int rem, add;
-                uint64_t c;
-                decode(s_zw[r].y, rdh, rem);
-                window(s_xy[r], s_zw[r], o, rdh, rem, c, eC, eT, add);
-                lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
-            }
-        }
-        qn = 0;
-    };
-    uint4 nx = make_uint4(0, 0, 0, 0);
-    if (r0 + threadIdx.x < r1) nx = recs[r0 + threadIdx.x];
-    for (uint64_t c0 = r0; c0 < r1; c0 += BUCKET_THREADS) {
-        const unsigned int nv = (unsigned int)min<uint64_t>(BUCKET_THREADS, r1 - c0);
-        const uint4 x = nx;
-        if (c0 + BUCKET_THREADS + threadIdx.x < r1) nx = recs[c0 + BUCKET_THREADS + threadIdx.x];  // next chunk
-        const unsigned int n = threadIdx.x < nv ? (x.z >> 28) + 1 : 0u;
-        s_xy[threadIdx.x] = make_uint2(x.x, x.y);
-        s_zw[threadIdx.x] = make_uint2(x.z, x.w);
-        const unsigned int incl = wave_incl_scan(n);
-        if (lane == 63) s_wsum[wid] = incl;
-        __syncthreads();
-        unsigned int before = 0, T = 0;
-#pragma unroll
-        for (int q = 0; q < NW; q++) {
-            const unsigned int v = s_wsum[q];
-            before += q < (int)wid ? v : 0u;
-            T += v;
-        }
-        const unsigned int pre = before + incl - n;
-        s_pre[threadIdx.x] = (uint16_t)pre;
-        const unsigned int q = (T + BUCKET_THREADS - 1) / BUCKET_THREADS;  // windows per lane
-        for (unsigned int l = (pre + q - 1) / q; l * q < pre + n; l++) s_first[l] = (uint16_t)threadIdx.x;
-        __syncthreads();
-        const unsigned int w0 = threadIdx.x * q, w1 = min(w0 + q, T);
-        unsigned int r = 0, pr = 0, end = 0, rem = 0;
-        uint2 xy = make_uint2(0, 0), zw = make_uint2(0, 0);
-        unsigned long long rdh = 0;
-        auto load = [&]() {
-            xy = s_xy[r];
-            zw = s_zw[r];
-            pr = s_pre[r];
-            end = pr + (zw.x >> 28) + 1;
-            decode(zw.y, rdh, rem);
-        };
-        if (w0 < T) {
-            r = s_first[threadIdx.x];
-            load();
-        }
-        for (unsigned int it = 0; it < q; it++) {  // wave-uniform trip count
-            const unsigned int wi = w0 + it;
-            const bool act = wi < w1;
-            if (act && wi >= end) {  // the next record (n >= 1: one step at most)
-                r++;
-                load();
-            }
-            const unsigned int o = wi - pr;  // < 16
-            unsigned long long eC, eT;
-            unsigned int add;
-            uint64_t c;
-            window(xy, zw, o, rdh, rem, c, eC, eT, add);
-            if (FAST == 0) {
-                if (act) lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
-                continue;
-            }
-            const unsigned int s0 = (sk_slot(c) >> (32 - SBITS)) & (SLOTS - 1), s1 = (s0 + 1) & (SLOTS - 1);
-            const unsigned long long k0 = tab.key[s0], k1 = tab.key[s1];
-            const bool hit = act && (k0 == c || k1 == c);
-            if (hit) {
-                const unsigned int slot = k0 == c ? s0 : s1;
-                atomicAdd(&tab.count[slot], add);
-                if (FAST == 1) {
-                    atomicMin(&tab.ev[slot].x, eC);
-                    atomicMin(&tab.ev[slot].y, eT);
-                } else {
-                    const ulonglong2 ev = tab.ev[slot];
-                    if (eC < ev.x) atomicMin(&tab.ev[slot].x, eC);
-                    if (eT < ev.y) atomicMin(&tab.ev[slot].y, eT);
-                }
-            }
-            const bool slow = act && !hit;
-            const uint64_t bal = __ballot(slow);
-            if (slow) {
-                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                s_q[wid][qn + rk] = (uint16_t)(r << 4 | o);
-            }
-            qn += (unsigned int)__popcll(bal);
-            if (qn >= 32) drain();
-        }
-        drain();
-        __syncthreads();
-    }
-    lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
-}
-
 }  // namespace ec
