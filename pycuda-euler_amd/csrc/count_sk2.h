@@ -13,8 +13,8 @@
 //                                buffered as 4-byte entries (read lane, first window, n,
 //                                bucket bits); a flush sorts the wave's entries by coarse
 //                                bucket and writes 16-byte records to the (group, coarse)
-//                                runs, bases read back from the wave's 2-bit stage; sampled
-//                                HyperLogLog of the canonical k-mers
+//                                runs, bases read back from the wave's 2-bit stage;
+//                                HyperLogLog of the k-mers of sampled minimizers
 //   k_skrefine  per coarse slice: runs -> fixed-capacity final buckets (as k_refine2), the
 //                                group-relative position made absolute
 //   k_skbucket  per final bucket: records sorted by window count in LDS, lane = record, the
@@ -78,7 +78,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
     const int k = mc.k, m = mc.m;
     const uint32_t w = (uint32_t)mc.w, nmax = sk2_nmax(k);
     const uint64_t kmask = kmask64(k);
-    const int sh = 2 * (k - 1);
     uint4 pf[NPF];
     uint64_t nx_base = 0;
     uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
@@ -98,9 +97,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
         const uint32_t rel = has ? s - tbase : 0u;
         s_rel[wid][lane] = rel;
         wave_sync();
-        // m-mer / k-mer state over the first k - 1 bases; the GW block starts at m-mer 0
+        // m-mer state over the first k - 1 bases; the GW block starts at m-mer 0
         uint32_t mf = 0, mr = 0, gi = 0, pm = 0xFFFFFFFFu;
-        uint64_t fwd = 0, rc = 0;
         // push m-mer hash h (m-mer index j, gi = j mod w): min of the window of w m-mers ending at j
         auto gw_push = [&](uint32_t h) {
             pm = gi == 0 ? h : min(pm, h);
@@ -120,8 +118,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
             return v;
         };
         auto push_base = [&](uint32_t b) {
-            fwd = ((fwd << 2) | b) & kmask;
-            rc = (rc >> 2) | ((uint64_t)(3u - b) << sh);
             mf = ((mf << 2) | b) & mc.mmask;
             mr = (mr >> 2) | ((3u - b) << mc.msh);
         };
@@ -146,13 +142,16 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
                 push_base((xb >> (2 * j)) & 3u);
                 const uint32_t v = gw_push(mmer_hash(mf < mr ? mf : mr));
                 const bool ok = has && wi + j < M;
-                // HyperLogLog sample of the canonical k-mers: a multiplicative test, mix64 for the sampled
-                const uint64_t c = fwd < rc ? fwd : rc;
-                const uint32_t th = (uint32_t)((c * 0x9E3779B97F4A7C15ull) >> 32);
+                // HyperLogLog over the k-mers whose minimizer hash has its low bits & smask zero (a
+                // sample of the key space: a k-mer and its twin share the minimizer); the
+                // sampled window's canonical k-mer straight out of the stage
                 shh[j] = 0;
-                if (ok && ((th >> 24) & smask) == 0) {
+                if (ok && (v & smask) == 0) {
+                    const uint32_t p = rel + wi + j;
+                    const uint64_t P = (uint64_t)bases16(p) | (uint64_t)bases16(p + 16) << 32;
+                    const uint64_t krc = ~P & kmask, kfw = rev2_64(P) >> (64 - 2 * k);
                     smp |= 1u << j;
-                    shh[j] = (uint32_t)(mix64(c) >> 32);
+                    shh[j] = (uint32_t)(mix64(kfw < krc ? kfw : krc) >> 32);
                 }
                 const bool close = ok && runn && (v != runv || runn == nmax);
                 const uint64_t bal = __ballot(close);
