@@ -14,7 +14,8 @@ import os
 import re
 import sys
 
-KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine", "k_prescan", "k_partition", "k_refine2")
+KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine", "k_prescan", "k_partition", "k_refine2",
+           "k_skpart", "k_skrefine", "k_skbucket")
 
 
 def short(name):
