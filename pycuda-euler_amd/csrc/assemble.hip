@@ -1507,9 +1507,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
-    Scalars hsc;
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    Scalars hsc{};
     const unsigned int N = 2 * U;
     const size_t Nn = std::max<size_t>(N, 1);
 
@@ -1550,7 +1548,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->PL.ensure(Nn * 4));
     EC_CHECK(s->PM.ensure(Nn * 8));
     unsigned int nr = 0;
-    RJump *fin = s->st0.as<RJump>();
+    int rounds = 0;  // Wyllie rounds launched (their convergence is checked with the results)
     s->stats.rank_rounds = 0;
     if (U) {
         EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 8, st));
@@ -1581,7 +1579,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                 return EC_ERR_STATE;
         }
         k_rjump_init<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), nr, s->st0.as<RJump>());
-        int rounds = 1;
+        rounds = 1;
         while ((1ull << (rounds - 1)) < (unsigned long long)nr) rounds++;
         rounds = std::min(rounds + 1, 63);
         RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
@@ -1589,24 +1587,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             k_rjump<<<grid_for(nr, B), B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], nr, N,
                                                   r ? &dsc->active[r - 1] : nullptr, &dsc->active[r],
                                                   &dsc->final_sel, (unsigned)((r + 1) & 1));
-        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
-        unsigned int used = 1;
-        for (int r = 0; r < rounds; r++)
-            if (hsc.active[r]) used = r + 2;
-        s->stats.rank_rounds = std::min<unsigned int>(used, rounds);
-        if (hsc.active[rounds - 1] != 0) {
-            set_error("ruler list ranking did not converge in %d rounds", rounds);
-                return EC_ERR_STATE;
-        }
-        fin = (hsc.final_sel & 1) ? s->st1.as<RJump>() : s->st0.as<RJump>();
         k_finalize<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(),
-                                                s->rid.as<uint2>(),
-                                                s->rlist.as<unsigned int>(), fin, N, s->PK.as<unsigned int>(),
+                                                s->rid.as<uint2>(), s->rlist.as<unsigned int>(), bufs[0], bufs[1],
+                                                &dsc->final_sel, N, s->PK.as<unsigned int>(),
                                                 s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
                                                 s->PM.as<unsigned long long>());
-        k_cycle_len<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), fin, nr,
-                                                  s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+        k_cycle_len<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), bufs[0],
+                                                  bufs[1], &dsc->final_sel, nr, s->PL.as<unsigned int>(),
+                                                  s->PM.as<unsigned long long>());
     }
     s->stats.n_rulers = nr;
     mark(s, 2 * EC_STAGE_RANK + 1);
@@ -1633,8 +1621,18 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                            s->svals.as<unsigned int>());
         EC_HIP(hipMemcpyAsync(&dsc->nstarts, bs + nblk - 1, 4, hipMemcpyDeviceToDevice, st));
     }
-    EC_HIP(hipMemcpyAsync(&hsc.nstarts, &dsc->nstarts, 4, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));  // nstarts, active[]
     EC_HIP(hipStreamSynchronize(st));
+    if (rounds) {
+        unsigned int used = 1;
+        for (int r = 0; r < rounds; r++)
+            if (hsc.active[r]) used = r + 2;
+        s->stats.rank_rounds = std::min<unsigned int>(used, rounds);
+        if (hsc.active[rounds - 1] != 0) {
+            set_error("ruler list ranking did not converge in %d rounds", rounds);
+            return EC_ERR_STATE;
+        }
+    }
     const unsigned int nc = hsc.nstarts;
     s->stats.n_contigs = nc;
     if (nc)
@@ -1652,17 +1650,17 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                    s->cwalk.as<Walk>());
     }
     EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
-    // only the total is needed now; the offsets travel with the other results
+    // the total travels with the other results (no round trip here): the character buffer is
+    // sized for the bound 2U + nc (k - 1) (a walk covers at most its path; a self-twin path's
+    // nodes are up to twice its canonical k-mers)
     EC_CHECK(s->h_coff.resize(nc + 1));
     EC_HIP(hipMemcpyAsync(&s->h_coff[nc], s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
     mark(s, 2 * EC_STAGE_STARTS + 1);
-    const uint64_t nchars = s->h_coff[nc];
-    s->stats.n_contig_chars = nchars;
+    const uint64_t chars_bound = 2ull * U + (uint64_t)nc * (uint64_t)(k - 1);
 
     // ---- emit -----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_EMIT);
-    EC_CHECK(s->chars.ensure(std::max<size_t>(nchars, 1)));
+    EC_CHECK(s->chars.ensure(std::max<size_t>(chars_bound, 1)));
     EC_CHECK(s->cfirst.ensure((size_t)std::max(nc, 1u) * 4));
     EC_CHECK(s->clast.ensure((size_t)std::max(nc, 1u) * 4));
     EC_CHECK(s->headOf.ensure(Nn * 4));
@@ -1691,11 +1689,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     mark(s, 2 * EC_STAGE_GFA + 1);
 
     // ---- results to host (links compacted on the device: only the used entries travel) -----
-    EC_CHECK(s->h_chars.resize(nchars));
     const unsigned int n2 = 2 * nc;
     EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
     s->h_loff[n2] = 0;
-    if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), s->chars.p, nchars, hipMemcpyDeviceToHost, st));
     if (nc) EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, (size_t)nc * 8, hipMemcpyDeviceToHost, st));
     else s->h_coff[0] = 0;
     if (nc) {
@@ -1704,8 +1700,17 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
         EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
     }
+    EC_HIP(hipStreamSynchronize(st));  // h_coff[nc] (the characters), h_loff
+    const uint64_t nchars = s->h_coff[nc];
+    s->stats.n_contig_chars = nchars;
+    if (nchars > chars_bound) {
+        set_error("contig characters %llu past their bound %llu", (unsigned long long)nchars,
+                  (unsigned long long)chars_bound);
+        return EC_ERR_STATE;
+    }
+    EC_CHECK(s->h_chars.resize(nchars));
+    if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), s->chars.p, nchars, hipMemcpyDeviceToHost, st));
     const uint64_t nlinks = s->h_loff[n2];
     EC_CHECK(s->h_links.resize(nlinks));
     if (nlinks) {

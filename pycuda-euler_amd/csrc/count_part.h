@@ -744,12 +744,10 @@ __device__ inline void lds_table_init(LTab<SLOTS> &tab, unsigned int *s_over) {
 // The probe loop is wave-uniform (runs while any lane still misses; lanes that found their
 // slot idle under one exec mask): almost every wave has some lane past its first probe, and a
 // per-lane loop with several exits costs ~40 scalar mask instructions per iteration.
-template <int SLOTS, bool DET = false>
-__device__ inline void lds_insert(LTab<SLOTS> &tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
-                                  unsigned int add, unsigned long long eC, unsigned long long eT,
-                                  unsigned int id = 0) {
-    unsigned int slot = slot0 & (SLOTS - 1);
-    unsigned long long cur = tab.key[slot];
+// lds_locate: the slot of key c given its first probe (slot, cur = the key read there).
+template <int SLOTS>
+__device__ inline unsigned int lds_locate(LTab<SLOTS> &tab, unsigned int *s_over, unsigned long long c,
+                                          unsigned int slot, unsigned long long cur) {
     bool miss = cur != c;
 #pragma unroll 1
     while (__any(miss)) {
@@ -771,6 +769,14 @@ __device__ inline void lds_insert(LTab<SLOTS> &tab, unsigned int *s_over, unsign
             miss = cur != c;
         }
     }
+    return slot;
+}
+template <int SLOTS, bool DET = false>
+__device__ inline void lds_insert(LTab<SLOTS> &tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
+                                  unsigned int add, unsigned long long eC, unsigned long long eT,
+                                  unsigned int id = 0) {
+    unsigned int slot = slot0 & (SLOTS - 1);
+    slot = lds_locate<SLOTS>(tab, s_over, c, slot, tab.key[slot]);
     if (DET) tab.id[slot] = id;  // distinct keys: one writer per slot
     atomicAdd(&tab.count[slot], add);
     const ulonglong2 ev = tab.ev[slot];

@@ -371,8 +371,9 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skrefine(const uint4 *recs, 
 
 // ---- bucket: super-k-mers -> LDS table
 // Records go through LDS in chunks of BUCKET_THREADS, sorted by window count (most first) so a
-// wave's lanes run loops of nearly one length; lane = record: window 0 from the packed bases
-// (fwd = their 2-bit reversal, common.h rev2_64; rc = their complement), later windows rolled.
+// wave's lanes run loops of nearly one length; lane = record, two windows per step (o and
+// o + ceil(n / 2): their LDS probes and updates in flight together, -2.5 %), each read once out
+// of the packed bases (fwd = 2-bit reversal, common.h rev2_64; rc = complement), then rolled.
 // Measured equal or slower: the chunk's windows split evenly over the lanes
 // (each window read straight out of the bases), and a two-slot fast path with the other
 // windows queued for lds_insert.
@@ -451,22 +452,46 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
         unsigned long long rdh;
         unsigned int rem;
         decode(zw.y, rdh, rem);
-        // window 0: bases 0 .. k - 1 (k <= 32: all in x, y)
-        const uint64_t lo = (uint64_t)xy.x | (uint64_t)xy.y << 32;
-        uint64_t fwd = rev2_64(lo) >> fsh;
-        uint64_t rc = ~lo & kmask;
-        for (unsigned int o = 0; o < n; o++) {
-            if (o) {
-                const unsigned int tb = o + (unsigned int)k - 1;
-                const uint32_t wd = tb < 32 ? xy.y : zw.x;
-                const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
-                fwd = ((fwd << 2) | bb) & kmask;
-                rc = (rc >> 2) | ((uint64_t)(3u - bb) << sh);
+        // two windows per step (o and o + h): their LDS probes and updates are in flight together
+        const unsigned int h = (n + 1) >> 1;
+        auto at = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // window o straight out of the bases
+            const uint32_t lo = __builtin_amdgcn_alignbit(xy.y, xy.x, 2 * o), hi = __builtin_amdgcn_alignbit(zw.x, xy.y, 2 * o);
+            const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+            rv = ~P & kmask;
+            fw = rev2_64(P) >> fsh;
+        };
+        uint64_t fA, rA, fB, rB;
+        at(0, fA, rA);
+        at(h, fB, rB);
+        auto roll = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // to window o from o - 1
+            const unsigned int tb = o + (unsigned int)k - 1;
+            const uint32_t wd = tb < 32 ? xy.y : zw.x;
+            const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
+            fw = ((fw << 2) | bb) & kmask;
+            rv = (rv >> 2) | ((uint64_t)(3u - bb) << sh);
+        };
+        for (unsigned int i = 0; i < h; i++) {
+            const unsigned int oB = i + h;
+            const bool bB = oB < n;
+            if (i) {
+                roll(i, fA, rA);
+                roll(oB, fB, rB);
             }
-            unsigned long long eC, eT;
-            unsigned int add;
-            const uint64_t c = events(fwd, rc, rem + o, rdh, eC, eT, add);
-            lds_insert<SLOTS>(tab, s_over, c, sk_slot(c) >> (32 - SBITS), add, eC, eT);
+            unsigned long long eCA, eTA, eCB, eTB;
+            unsigned int addA, addB;
+            const uint64_t cA = events(fA, rA, rem + i, rdh, eCA, eTA, addA);
+            const uint64_t cB = events(fB, rB, rem + oB, rdh, eCB, eTB, addB);
+            unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1), sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
+            const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
+            sA = lds_locate<SLOTS>(tab, s_over, cA, sA, kA);
+            sB = lds_locate<SLOTS>(tab, s_over, cB, sB, bB ? kB : cB);
+            atomicAdd(&tab.count[sA], addA);
+            if (bB) atomicAdd(&tab.count[sB], addB);
+            const ulonglong2 vA = tab.ev[sA], vB = tab.ev[sB];
+            if (eCA < vA.x) atomicMin(&tab.ev[sA].x, eCA);
+            if (eTA < vA.y) atomicMin(&tab.ev[sA].y, eTA);
+            if (bB && eCB < vB.x) atomicMin(&tab.ev[sB].x, eCB);
+            if (bB && eTB < vB.y) atomicMin(&tab.ev[sB].y, eTB);
         }
         __syncthreads();
     }

@@ -455,10 +455,12 @@ __global__ void __launch_bounds__(256) k_rjump(const RJump *src, RJump *dst, uns
 // at the key node: PL = path / cycle length, PM = min first event over it.
 constexpr unsigned int CYC = 0x80000000u;
 
+// The Wyllie rounds' result is in rs0 or rs1 as *sel says (read here: no host round trip).
 __global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const unsigned int *succ, const uint2 *rid,
-                                                  const unsigned int *rlist, const RJump *rs,
-                                                  unsigned int N, unsigned int *PK, unsigned int *RK, unsigned int *PL,
-                                                  unsigned long long *PM) {
+                                                  const unsigned int *rlist, const RJump *rs0, const RJump *rs1,
+                                                  const unsigned int *sel, unsigned int N, unsigned int *PK,
+                                                  unsigned int *RK, unsigned int *PL, unsigned long long *PM) {
+    const RJump *rs = (*sel & 1) ? rs1 : rs0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         if ((x & 1) && upal[x >> 1]) continue;
@@ -481,8 +483,10 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const uns
 }
 
 // cycle length / min: the ruler whose successor ruler is the key ruler closes the ring
-__global__ void __launch_bounds__(256) k_cycle_len(const unsigned int *nextR, const unsigned int *rlist, const RJump *rs,
+__global__ void __launch_bounds__(256) k_cycle_len(const unsigned int *nextR, const unsigned int *rlist,
+                                                   const RJump *rs0, const RJump *rs1, const unsigned int *sel,
                                                    unsigned int nr, unsigned int *PL, unsigned long long *PM) {
+    const RJump *rs = (*sel & 1) ? rs1 : rs0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
         const RJump r = rs[t];
         if (r.a == NONE32) continue;
