@@ -153,6 +153,7 @@ struct ec_session {
     const unsigned long long *bbeg = nullptr, *bend = nullptr;  // launch_bucket: explicit bucket bounds
     uint32_t nseg = 1;          // ... as nseg record ranges per bucket
     DevBuf fcur, bb2;           // count_v2.h: final-bucket cursors, bucket bounds
+    DevBuf nrec;                // graph.h NodeRec: successor + first event per node (k_walk)
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
@@ -463,7 +464,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     k_skbucket<SLOTS, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(                                          \
         s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(),                \
         s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),          \
-        s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow)
+        s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow)
     if (plan.slots == 2048) {
         if (k & 1) EC_SKBUCKET(2048, false);
         else EC_SKBUCKET(2048, true);
@@ -1552,6 +1553,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     s->stats.rank_rounds = 0;
     if (U) {
         EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 8, st));
+        EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
+        k_noderec<<<grid_for(N, B), B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                               s->dft.as<unsigned long long>(), N, s->nrec.as<NodeRec>());
         unsigned int masks[4] = {31u, 7u, 1u, 0u};
         if (const char *e = getenv("EULERHIP_RULER_MASK")) masks[0] = (unsigned int)atoi(e);
         unsigned int r0 = 0;
@@ -1564,8 +1568,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                          s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<uint2>(),
                                          s->rlist.as<unsigned int>());
             k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
-            k_walk<<<2048, B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                      s->dft.as<unsigned long long>(), s->rlist.as<unsigned int>(), r0, &dsc->nr,
+            k_walk<<<2048, B, 0, st>>>(s->nrec.as<NodeRec>(), s->rlist.as<unsigned int>(), r0, &dsc->nr,
                                       masks[it], s->rid.as<uint2>(),
                                       s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
             EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));

@@ -361,10 +361,26 @@ struct alignas(32) RJump {
 };
 static_assert(sizeof(RJump) == 32, "rjump layout");
 
-// Each ruler walks its segment up to the next ruler (a chain of dependent loads).  The next
-// successor is requested before the node's first-event load, so the two latencies overlap.
-__global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const unsigned long long *dfc,
-                                              const unsigned long long *dft, const unsigned int *rlist,
+// A node's successor and first event side by side (k_noderec): the walk's random step then
+// touches one line instead of three (succ, dfc / dft).
+struct alignas(16) NodeRec {
+    unsigned int succ;
+    unsigned int pad;
+    unsigned long long fev;
+};
+__global__ void __launch_bounds__(256) k_noderec(const unsigned int *succ, const unsigned long long *dfc,
+                                                 const unsigned long long *dft, unsigned int N, NodeRec *nrec) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        NodeRec r;
+        r.succ = succ[t];
+        r.pad = 0;
+        r.fev = first_event(dfc, dft, (unsigned int)t);
+        nrec[t] = r;
+    }
+}
+
+// Each ruler walks its segment up to the next ruler (a chain of dependent 16-B loads).
+__global__ void __launch_bounds__(256) k_walk(const NodeRec *nrec, const unsigned int *rlist,
                                               unsigned int r0, const unsigned int *nr, unsigned int smask,
                                               uint2 *rid, unsigned int *nextR, RJump *rs,
                                               unsigned long long *nvisited) {
@@ -373,9 +389,10 @@ __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const un
     for (uint64_t t = r0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < r1; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int i = (unsigned int)t;
         unsigned int v = rlist[i];
-        unsigned long long fm = first_event(dfc, dft, v);
+        const NodeRec a = nrec[v];
+        unsigned long long fm = a.fev;
         unsigned int j = 0, nx = NONE32;
-        unsigned int w = succ[v];
+        unsigned int w = a.succ;
         for (;;) {
             if (w == NONE32) break;
             if (ruler_hash(w, smask)) {  // maybe the next ruler
@@ -387,10 +404,10 @@ __global__ void __launch_bounds__(256) k_walk(const unsigned int *succ, const un
             }
             v = w;
             j++;
-            w = succ[v];  // chain load first
-            const unsigned long long f = first_event(dfc, dft, v);
+            const NodeRec b = nrec[v];
+            w = b.succ;
             rid[v] = make_uint2(i, j);  // (ruler, offset) in one 8-B store
-            fm = f < fm ? f : fm;
+            fm = b.fev < fm ? b.fev : fm;
         }
         nextR[i] = nx;
         RJump r;
