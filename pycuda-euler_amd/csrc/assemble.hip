@@ -393,7 +393,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         return EC_OK;
     };
     const MinCfg mc = sk_cfg(k);
-    constexpr uint64_t C = 1ull << PT_CBITS;
+    constexpr uint64_t C = 1ull << SK2_CBITS;
     // records per read ~ 2 M / (w + 1) + 1 on random sequence; 40 % headroom per run
     const double per_read = 2.0 * M / (mc.w + 1) + 2.0;
     const uint64_t cap = (uint64_t)(gsize * per_read * 1.4 / C) + 256;
@@ -425,7 +425,11 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     const double est = hsc.est * (smask + 1.0);
     BucketPlan plan = plan_buckets(est, limit, !getenv("EULERHIP_NO_FILTER"));
     if (!plan.part || plan.filt) return reset();  // error-rich: window records with the seen-twice filter
-    const int bbits = std::max(plan.bbits, PT_CBITS);
+    // up to 2^SK2_BBITS buckets of <= 1100 estimated keys (2048-slot tables: two workgroups per CU)
+    int bbits = SK2_CBITS;
+    while (bbits < SK2_BBITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
+    plan.bbits = bbits;
+    plan.slots = est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
     const uint64_t Bk = 1ull << bbits;
     const uint64_t NR = hsc.nrec;
 

@@ -36,9 +36,11 @@ namespace ec {
 constexpr int SK2_NMAX = 16;     // windows per record (n - 1 in 4 bits)
 constexpr int SK2_BASES = 46;    // bases per record (92 bits)
 constexpr int SK2_R = 4;         // windows per lane per round of k_skpart
-constexpr int SK2_ECAP = 896;    // entries a wave buffers before a flush (LDS: 3 workgroups per CU)
+constexpr int SK2_ECAP = 864;    // entries a wave buffers before a flush (LDS: 3 workgroups per CU)
 constexpr int SK2_TILE = 4096;   // k_skrefine records per tile (64 KiB of LDS)
-constexpr int SK2_FBITS = FINE_BITS - PT_CBITS;  // bucket bits below the coarse bits in a record
+constexpr int SK2_CBITS = 6;     // coarse buckets of the partition: 64
+constexpr int SK2_BBITS = 14;    // final buckets <= 2^14 (bucket bits in an entry)
+constexpr int SK2_FBITS = SK2_BBITS - SK2_CBITS;  // bucket bits below the coarse bits in a record
 
 __host__ __device__ inline uint32_t sk2_nmax(int k) {
     return (uint32_t)(SK2_BASES - k + 1 < SK2_NMAX ? SK2_BASES - k + 1 : SK2_NMAX);
@@ -47,14 +49,14 @@ __host__ __device__ inline uint32_t sk2_nmax(int k) {
 // ---- partition -------------------------------------------------------------------------------
 // Region of (c, g): records [(g * C + c) * cap, + cap) of recs, spill records at C * G * cap
 // (SK2_ECAP of them; *overflow set, the call is redone); cnt[c * G + g] = records stored.
-// Entry (u32): lane | first window << 6 | (n - 1) << 14 | top FINE_BITS of min_remix << 18.
+// Entry (u32): lane | first window << 6 | (n - 1) << 14 | top SK2_BBITS of min_remix << 18.
 template <int NPF>
 __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict__ buf,
                                                        const uint64_t *__restrict__ off, uint64_t nreads, MinCfg mc,
                                                        uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
                                                        uint32_t smask, uint4 *recs, unsigned int *cnt, uint8_t *hll,
                                                        unsigned long long *nrec, unsigned int *overflow) {
-    constexpr int C = 1 << PT_CBITS;
+    constexpr int C = 1 << SK2_CBITS;
     constexpr int NREG = 1 << HLL_REG_BITS;
     constexpr int SW = NPF * 64 + 4;
     __shared__ uint32_t s_stage[PT_WAVES][SW];
@@ -158,7 +160,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
                 if (close) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - FINE_BITS)) << 18;
+                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
                 }
                 cntw += (uint32_t)__popcll(bal);
                 if (ok) {
@@ -178,7 +180,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
                 if (fin) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - FINE_BITS)) << 18;
+                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
                 }
                 cntw += (uint32_t)__popcll(bal);
                 if (more) EC_PT_ISSUE(t + PT_WAVES);
@@ -263,13 +265,13 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skrefine(const uint4 *recs, 
                                                              uint32_t M, uint64_t gsize, uint64_t read_base) {
     constexpr int TILE = SK2_TILE;
     constexpr int PER = TILE / BUCKET_THREADS;
-    constexpr uint64_t C = 1 << PT_CBITS;
+    constexpr uint64_t C = 1 << SK2_CBITS;
     __shared__ uint4 tile[TILE];
     __shared__ uint8_t tj[TILE];
     __shared__ unsigned long long base[REFINE_FANOUT];
     __shared__ unsigned int tcnt[REFINE_FANOUT], tbeg[REFINE_FANOUT], wsum[BUCKET_THREADS / 64];
     __shared__ unsigned int lst[RF_MAX_RUNS + 1];
-    const int fb = bbits - PT_CBITS;  // final bits below the coarse bits
+    const int fb = bbits - SK2_CBITS;  // final bits below the coarse bits
     const int F = 1 << fb;
     const uint64_t c = blockIdx.x;
     const uint32_t ga = (uint32_t)((uint64_t)G * blockIdx.y / gridDim.y),
