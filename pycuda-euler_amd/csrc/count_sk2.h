@@ -37,7 +37,10 @@ constexpr int SK2_NMAX = 16;     // windows per record (n - 1 in 4 bits)
 constexpr int SK2_BASES = 46;    // bases per record (92 bits)
 constexpr int SK2_R = 4;         // windows per lane per round of k_skpart
 constexpr int SK2_ECAP = 864;    // entries a wave buffers before a flush (LDS: 3 workgroups per CU)
-constexpr int SK2_TILE = 4096;   // k_skrefine records per tile (64 KiB of LDS)
+#ifndef SK2_TILE_DEF
+#define SK2_TILE_DEF 2048
+#endif
+constexpr int SK2_TILE = SK2_TILE_DEF;  // k_skrefine records per tile (A/B: 2048 0.70 ms, 4096 0.81, 8192 0.85)
 constexpr int SK2_CBITS = 6;     // coarse buckets of the partition: 64
 constexpr int SK2_BBITS = 14;    // final buckets <= 2^14 (bucket bits in an entry)
 constexpr int SK2_FBITS = SK2_BBITS - SK2_CBITS;  // bucket bits below the coarse bits in a record
