@@ -421,11 +421,18 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     k_hll_final<<<1, 1024, 0, st>>>(hreg, HLL_REG_BITS, &dsc->est);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
-    if (hsc.overflow) return reset();  // a run outgrew its capacity
+    const bool verbose = getenv("EULERHIP_VERBOSE") != nullptr;
+    if (hsc.overflow) {  // a run outgrew its capacity
+        if (verbose) fprintf(stderr, "count_sk2: partition run overflow (cap %llu)\n", (unsigned long long)cap);
+        return reset();
+    }
     const double est = hsc.est * (smask + 1.0);
     BucketPlan plan = plan_buckets(est, limit, !getenv("EULERHIP_NO_FILTER"));
     if (!plan.part || plan.filt) return reset();  // error-rich: window records with the seen-twice filter
-    // up to 2^SK2_BBITS buckets of <= 1100 estimated keys (2048-slot tables: two workgroups per CU)
+    // up to 2^SK2_BBITS buckets of <= 1100 estimated keys (2048-slot tables: two workgroups per
+    // CU).  Measured: 16384 buckets of 1024 slots (three workgroups per CU) were not faster, and
+    // small tables need lds_insert to count claims after the CAS (reservations of up to 1024
+    // racing lanes overshoot), which cost 8 % in every table
     int bbits = SK2_CBITS;
     while (bbits < SK2_BBITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
     plan.bbits = bbits;
@@ -482,6 +489,10 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     if (hsc.overflow || hsc.skew) {  // a final bucket or an LDS table overflowed
+        if (verbose)
+            fprintf(stderr, "count_sk2: %s overflow (%llu buckets, %u slots, est %.0f, fcap %llu)\n",
+                    hsc.skew ? "final bucket" : "table", (unsigned long long)Bk, plan.slots, est,
+                    (unsigned long long)fcap);
         s->stats.table_retries++;
         return reset();
     }
