@@ -379,7 +379,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
                     uint64_t read_base, int k, long long limit, uint32_t M, uint64_t G, uint64_t gsize, uint64_t P,
                     int npf, unsigned int &U, SolidIndex &sidx, bool &done) {
     done = false;
-    if (k < SK_MIN_K || k > 32 || M > 256 || gsize * M >= (1ull << 24) || (read_base + nreads) * M >= (1ull << 32) ||
+    if (k < SK_MIN_K || k > 32 || M > 256 || gsize * M >= (1ull << 24) || (read_base + nreads) * 2 * M >= (1ull << 32) ||
         getenv("EULERHIP_NO_SK2"))
         return EC_OK;
     hipStream_t st = s->stream;

@@ -745,8 +745,8 @@ __device__ inline void lds_table_init(LTab<SLOTS> &tab, unsigned int *s_over) {
 // slot idle under one exec mask): almost every wave has some lane past its first probe, and a
 // per-lane loop with several exits costs ~40 scalar mask instructions per iteration.
 // lds_locate: the slot of key c given its first probe (slot, cur = the key read there).
-template <int SLOTS>
-__device__ inline unsigned int lds_locate(LTab<SLOTS> &tab, unsigned int *s_over, unsigned long long c,
+template <int SLOTS, typename Tab>
+__device__ inline unsigned int lds_locate(Tab &tab, unsigned int *s_over, unsigned long long c,
                                           unsigned int slot, unsigned long long cur) {
     bool miss = cur != c;
 #pragma unroll 1
@@ -789,12 +789,18 @@ __device__ inline void lds_insert(LTab<SLOTS> &tab, unsigned int *s_over, unsign
 struct KeyId {
     __device__ inline unsigned long long operator()(unsigned long long c) const { return c; }
 };
-template <int SLOTS, bool DET = false, typename KO = KeyId>
-__device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned int *s_over, unsigned int b,
+// the first events of slot i as stored (LTab: (read << 32) | l per orientation)
+struct EvId {
+    template <typename Tab>
+    __device__ inline ulonglong2 operator()(const Tab &tab, int i) const { return tab.ev[i]; }
+};
+template <int SLOTS, bool DET = false, typename KO = KeyId, typename Tab = LTab<SLOTS>, typename EO = EvId>
+__device__ inline void lds_table_finish(const Tab &tab, const unsigned int *s_over, unsigned int b,
                                         long long limit,
                                         unsigned long long *dkey, unsigned int *dcnt, unsigned long long *dfc,
                                         unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
-                                        unsigned long long *ndistinct, unsigned int *overflow, KO ko = KO()) {
+                                        unsigned long long *ndistinct, unsigned int *overflow, KO ko = KO(),
+                                        EO eo = EO()) {
     __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
     __shared__ unsigned int s_base;
     __syncthreads();
@@ -804,7 +810,7 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int PER = SLOTS / BUCKET_THREADS;
-    if (DET) {  // dense ids given by the records (LTab::id): every present key is solid
+    if constexpr (DET) {  // dense ids given by the records (LTab::id): every present key is solid
         SubSlot *region = sub + (uint64_t)b * SLOTS;
         for (int q = 0; q < PER; q++) {
             const int i = threadIdx.x * PER + q;
@@ -815,10 +821,11 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
             o.pad = 0;
             if (key != EMPTY_KEY) {
                 const unsigned int u = tab.id[i];
+                const ulonglong2 ev = eo(tab, i);
                 dkey[u] = ko(key);
                 dcnt[u] = tab.count[i];
-                dfc[u] = tab.ev[i].x;
-                dft[u] = tab.ev[i].y;
+                dfc[u] = ev.x;
+                dft[u] = ev.y;
                 o.id = u;
             }
             region[i] = o;
@@ -866,10 +873,11 @@ __device__ inline void lds_table_finish(const LTab<SLOTS> &tab, const unsigned i
         o.id = NONE32;
         o.pad = 0;
         if (solid[q]) {
+            const ulonglong2 ev = eo(tab, i);
             dkey[u] = ko(o.key);
             dcnt[u] = tab.count[i];
-            dfc[u] = tab.ev[i].x;
-            dft[u] = tab.ev[i].y;
+            dfc[u] = ev.x;
+            dft[u] = ev.y;
             o.id = u;
             u++;
         }

@@ -375,6 +375,26 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skrefine(const uint4 *recs, 
 }
 
 // ---- bucket: super-k-mers -> LDS table
+// The bucket table of k_skbucket: count_part.h's LTab with 32-bit first events
+// e = read * 2M + l (ordered as (read, l); phase_count_sk2 checks (read_base + reads) * 2M <
+// 2^32) and no id words -- 40 KiB for 2048 slots instead of 64, its event read 8 bytes.
+template <int SLOTS>
+struct LTabE {
+    unsigned long long key[SLOTS];
+    uint2 ev[SLOTS];
+    unsigned int count[SLOTS];
+};
+struct EvExpand {  // e -> (read << 32) | l for the dense arrays
+    unsigned int m2;  // 2M
+    __device__ inline unsigned long long one(unsigned int e) const {
+        return ((unsigned long long)(e / m2) << 32) | (e % m2);
+    }
+    template <typename Tab>
+    __device__ inline ulonglong2 operator()(const Tab &tab, int i) const {
+        return make_ulonglong2(one(tab.ev[i].x), one(tab.ev[i].y));
+    }
+};
+
 // Records go through LDS in chunks of BUCKET_THREADS, sorted by window count (most first) so a
 // wave's lanes run loops of nearly one length; lane = record, two windows per step (o and
 // o + ceil(n / 2): their LDS probes and updates in flight together, -2.5 %), each read once out
@@ -391,33 +411,35 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
                                                              unsigned int *nsolid, unsigned long long *ndistinct,
                                                              unsigned int *overflow) {
     constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
-    __shared__ LTab<SLOTS> tab;
+    __shared__ LTabE<SLOTS> tab;
     __shared__ unsigned int s_over[2];
-    // the chunk's records: x, y in the table's id words (LTab::id, unused without DET: keeps
-    // 2048-slot workgroups at two per CU), z, w here
-    __shared__ uint2 s_zw[BUCKET_THREADS];
+    __shared__ uint2 s_xy[BUCKET_THREADS], s_zw[BUCKET_THREADS];  // the chunk's records
     __shared__ unsigned int s_ncnt[SK2_NMAX + 1];
-    static_assert(sizeof(tab.id) >= BUCKET_THREADS * sizeof(uint2), "record staging in LTab::id");
-    uint2 *s_xy = reinterpret_cast<uint2 *>(tab.id);
     const unsigned int b = blockIdx.x;
-    lds_table_init<SLOTS>(tab, s_over);
+    for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
+        tab.key[i] = EMPTY_KEY;
+        tab.count[i] = 0;
+        tab.ev[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    if (threadIdx.x == 0) s_over[0] = s_over[1] = 0;
+    __syncthreads();
     const uint64_t r0 = bbeg[b], r1 = bend[b];
     const uint64_t kmask = kmask64(k);
     const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
     const unsigned int m2 = 2 * M - 1;
-    // the record's read (<< 32) and first window in it, from p = read * M + window
-    auto decode = [&](unsigned int p, unsigned long long &rdh, unsigned int &rem) {
+    // the record's read * 2M and first window in it, from p = read * M + window
+    auto decode = [&](unsigned int p, unsigned int &rd2, unsigned int &rem) {
         const unsigned int rd = (unsigned int)((double)p * inv_m);  // p / M, corrected below
         int rm = (int)(p - rd * M);
         unsigned int read = rd;
         if (rm < 0) read--, rm += (int)M;
         else if (rm >= (int)M) read++, rm -= (int)M;
-        rdh = (unsigned long long)read << 32;
+        rd2 = read * (2 * M);
         rem = (unsigned int)rm;
     };
     // events and add of window lf = rem + o given its fwd / rc codes; returns the canonical key
-    auto events = [&](uint64_t fwd, uint64_t rc, unsigned int lf, unsigned long long rdh, unsigned long long &eC,
-                      unsigned long long &eT, unsigned int &add) {
+    auto events = [&](uint64_t fwd, uint64_t rc, unsigned int lf, unsigned int rd2, unsigned int &eC,
+                      unsigned int &eT, unsigned int &add) {
         const bool tw = fwd > rc;
         unsigned int lC = tw ? m2 - lf : lf, lT = tw ? lf : m2 - lf;
         add = 1;
@@ -425,8 +447,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
             add = 2;
             lC = lT = lf;
         }
-        eC = rdh | lC;
-        eT = rdh | lT;
+        eC = rd2 + lC;
+        eT = rd2 + lT;
         return tw ? rc : fwd;
     };
     uint4 nx = make_uint4(0, 0, 0, 0);
@@ -454,9 +476,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
         __syncthreads();
         const uint2 xy = s_xy[threadIdx.x], zw = s_zw[threadIdx.x];
         const unsigned int n = threadIdx.x < nv ? (zw.x >> 28) + 1 : 0u;
-        unsigned long long rdh;
-        unsigned int rem;
-        decode(zw.y, rdh, rem);
+        unsigned int rd2, rem;
+        decode(zw.y, rd2, rem);
         // two windows per step (o and o + h): their LDS probes and updates are in flight together
         const unsigned int h = (n + 1) >> 1;
         auto at = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // window o straight out of the bases
@@ -482,17 +503,16 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
                 roll(i, fA, rA);
                 roll(oB, fB, rB);
             }
-            unsigned long long eCA, eTA, eCB, eTB;
-            unsigned int addA, addB;
-            const uint64_t cA = events(fA, rA, rem + i, rdh, eCA, eTA, addA);
-            const uint64_t cB = events(fB, rB, rem + oB, rdh, eCB, eTB, addB);
+            unsigned int eCA, eTA, eCB, eTB, addA, addB;
+            const uint64_t cA = events(fA, rA, rem + i, rd2, eCA, eTA, addA);
+            const uint64_t cB = events(fB, rB, rem + oB, rd2, eCB, eTB, addB);
             unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1), sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
             const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
             sA = lds_locate<SLOTS>(tab, s_over, cA, sA, kA);
             sB = lds_locate<SLOTS>(tab, s_over, cB, sB, bB ? kB : cB);
             atomicAdd(&tab.count[sA], addA);
             if (bB) atomicAdd(&tab.count[sB], addB);
-            const ulonglong2 vA = tab.ev[sA], vB = tab.ev[sB];
+            const uint2 vA = tab.ev[sA], vB = tab.ev[sB];
             if (eCA < vA.x) atomicMin(&tab.ev[sA].x, eCA);
             if (eTA < vA.y) atomicMin(&tab.ev[sA].y, eTA);
             if (bB && eCB < vB.x) atomicMin(&tab.ev[sB].x, eCB);
@@ -500,7 +520,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
         }
         __syncthreads();
     }
-    lds_table_finish<SLOTS>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, overflow);
+    lds_table_finish<SLOTS, false, KeyId>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
+                                          overflow, KeyId(), EvExpand{2 * M});
 }
 
 // -------------------------------------------------------
