@@ -51,11 +51,14 @@ typedef struct ec_session ec_session;
 #define EC_FLAG_GENERAL 4u   /* force the general (single HBM hash table) counting path */
 #define EC_FLAG_WIDE_RECORDS 8u /* partitioned path: 16-B window records only (default for k < 21 or
                                   * reads with N: 12-B records when every read is N-free and of one length) */
-#define EC_FLAG_WINDOW_RECORDS 16u /* partitioned path: one record per k-mer window, never super-k-mers */
+#define EC_FLAG_WINDOW_RECORDS 16u /* partitioned path: one record per k-mer window, never super-k-mers
+                                    * (neither count_sk2.h's default 16-B ones nor EC_FLAG_SUPERKMER's) */
 #define EC_FLAG_EXACT_COUNT 64u /* partitioned path: histogram-sized runs only (count_part.h), never the
                                   * fixed-capacity runs of count_v2.h */
-#define EC_FLAG_SUPERKMER 32u /* partitioned path: super-k-mer records (minimizer buckets) where they apply:
-                                * 21 <= k <= 32, N-free reads (else window records) */
+#define EC_FLAG_SUPERKMER 32u /* partitioned path: 32-B super-k-mer records on histogram-sized runs
+                                * (superkmer.h) where they apply: 21 <= k <= 32, N-free reads (else
+                                * window records); without flags, N-free reads of one length get
+                                * count_sk2.h's 16-B super-k-mer records (ec_stats.count_variant 3) */
 
 #define EC_NSTAGES 8
 /* stage ids for ec_stats.stage_ms / ec_stage_name */
@@ -98,10 +101,14 @@ typedef struct {
     uint32_t rank_rounds;    /* Wyllie rounds on the ruler list                               */
     uint32_t count_path;     /* EC_PATH_*                                                     */
     uint32_t n_buckets;      /* partitioned path: B                                           */
-    uint32_t record_bytes;   /* partitioned paths: 12 / 16 per window record, 32 per super-k-mer */
+    uint32_t record_bytes;   /* partitioned paths: 10 / 12 / 16 per window record, 16 or 32 per
+                              * super-k-mer                                                   */
     uint32_t count_variant;  /* partitioned path: 0 = histogram-sized runs (count_part.h),
                               * 1 = fixed-capacity runs without the upsweep (count_v2.h), 12-B
-                              * records; 2 = the same with 10-B records (hashed-key remnants) */
+                              * records; 2 = the same with 10-B records (hashed-key remnants);
+                              * 3 = 16-B super-k-mer records on fixed-capacity runs
+                              * (count_sk2.h; the default for N-free reads of one length,
+                              * 21 <= k <= 32, inputs that need no seen-twice filter)          */
     float stage_ms[EC_NSTAGES];   /* EC_FLAG_TIMING only */
     float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING only */
 } ec_stats;
