@@ -411,9 +411,18 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     k_skpart<NPF><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, \
                                                       recs, s->cnt.as<unsigned int>(), s->hll.as<uint8_t>(),      \
                                                       &dsc->nrec, &dsc->overflow)
-    if (npf == 4) EC_SKPART(4);
+#define EC_SKPART_W(NPF)                                                                                      \
+    k_skpart_w<NPF, 17><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap,     \
+                                                            smask, recs, s->cnt.as<unsigned int>(),                    \
+                                                            s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow)
+    if (mc.w == 17 && !getenv("EULERHIP_SKPART_RING")) {  // k = 31: register-block minima
+        if (npf == 4) EC_SKPART_W(4);
+        else if (npf == 7) EC_SKPART_W(7);
+        else EC_SKPART_W(10);
+    } else if (npf == 4) EC_SKPART(4);
     else if (npf == 7) EC_SKPART(7);
     else EC_SKPART(10);
+#undef EC_SKPART_W
 #undef EC_SKPART
     kmark(s, 1, 1);
     EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));

@@ -50,6 +50,70 @@ __host__ __device__ inline uint32_t sk2_nmax(int k) {
 }
 
 // ---- partition -------------------------------------------------------------------------------
+// A wave's flush: its cntw buffered entries counting-sorted by coarse bucket (the wave's own
+// counters, DPP scan), each bucket's run reserved on the workgroup cursor (spill records past
+// the capacity), the 16-B records built from the wave's 2-bit stage and stored as runs.
+__device__ inline uint32_t sk_bases16(const uint32_t *st, uint32_t p) {
+    return __builtin_amdgcn_alignbit(st[(p >> 4) + 1], st[p >> 4], 2 * (p & 15));
+}
+template <int C>
+__device__ inline void skpart_flush(uint32_t cntw, const uint32_t *ent, uint16_t *srt, unsigned int *wcnt,
+                                    unsigned int *cur, unsigned long long *base, const uint32_t *rel,
+                                    const uint32_t *st, uint32_t lane, unsigned long long gcap, uint64_t cap,
+                                    unsigned long long spill, uint32_t M, uint32_t rtile, uint4 *recs,
+                                    unsigned int *overflow) {
+    wave_sync();
+    for (uint32_t i = lane; i < cntw; i += 64) atomicAdd(&wcnt[ent[i] >> 26], 1u);
+    wave_sync();
+    const unsigned int v = lane < (uint32_t)C ? wcnt[lane] : 0u;
+    const unsigned int incl = wave_incl_scan(v);
+    const unsigned int beg = incl - v;
+    if (lane < (uint32_t)C) {
+        wcnt[lane] = beg;
+        unsigned int at = 0;
+        if (v) at = atomicAdd(&cur[lane], v);
+        unsigned long long b0 = gcap + lane * cap + at - beg;
+        if (at + v > cap) {  // past the capacity: stores go to the spill records
+            atomicOr(overflow, 1u);
+            b0 = spill - beg;
+        }
+        base[lane] = b0;
+    }
+    wave_sync();
+    for (uint32_t i = lane; i < cntw; i += 64) {
+        const unsigned int p = atomicAdd(&wcnt[ent[i] >> 26], 1u);
+        srt[p] = (uint16_t)i;
+    }
+    wave_sync();
+    for (uint32_t i = lane; i < cntw; i += 64) {
+        const uint32_t e = ent[srt[i]];
+        const uint32_t lr = e & 63u, i0 = (e >> 6) & 0xFFu, n1 = (e >> 14) & 15u;
+        const uint32_t p0 = rel[lr] + i0;
+        uint4 o;
+        o.x = sk_bases16(st, p0);
+        o.y = sk_bases16(st, p0 + 16);
+        o.z = (sk_bases16(st, p0 + 32) & 0x0FFFFFFFu) | n1 << 28;
+        o.w = ((e >> 18) & ((1u << SK2_FBITS) - 1)) << 24 | ((rtile + lr) * M + i0);
+        recs[base[e >> 26] + i] = o;
+    }
+    wave_sync();
+    if (lane < (uint32_t)C) wcnt[lane] = 0;
+}
+
+// u8 HyperLogLog register max by CAS on the word holding it
+__device__ inline void sk_hll_put(unsigned int *s_hll, uint32_t hh) {
+    const uint32_t hj = hh >> (32 - HLL_REG_BITS);
+    const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+    const uint32_t hs = (hj & 3) * 8;
+    uint32_t old = s_hll[hj >> 2];
+    while (rho > ((old >> hs) & 0xFFu)) {
+        const uint32_t nw = (old & ~(0xFFu << hs)) | (rho << hs);
+        const uint32_t prev = atomicCAS(&s_hll[hj >> 2], old, nw);
+        if (prev == old) break;
+        old = prev;
+    }
+}
+
 // Region of (c, g): records [(g * C + c) * cap, + cap) of recs, spill records at C * G * cap
 // (SK2_ECAP of them; *overflow set, the call is redone); cnt[c * G + g] = records stored.
 // Entry (u32): lane | first window << 6 | (n - 1) << 14 | top SK2_BBITS of min_remix << 18.
@@ -190,59 +254,163 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
             }
             if (smp) {
 #pragma unroll
-                for (int j = 0; j < SK2_R; j++) {
-                    if (!((smp >> j) & 1u)) continue;
-                    const uint32_t hj = shh[j] >> (32 - HLL_REG_BITS);
-                    const uint32_t rho =
-                        (uint32_t)__clz((int)((shh[j] << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
-                    const uint32_t hs = (hj & 3) * 8;
-                    uint32_t old = s_hll[hj >> 2];
-                    while (rho > ((old >> hs) & 0xFFu)) {
-                        const uint32_t nw = (old & ~(0xFFu << hs)) | (rho << hs);
-                        const uint32_t prev = atomicCAS(&s_hll[hj >> 2], old, nw);
-                        if (prev == old) break;
-                        old = prev;
-                    }
-                }
+                for (int j = 0; j < SK2_R; j++)
+                    if ((smp >> j) & 1u) sk_hll_put(s_hll, shh[j]);
             }
             // flush: the buffer could not take another round, or the stage is about to change
             if (last || cntw > (uint32_t)(SK2_ECAP - 64 * (SK2_R + 1))) {
-                wave_sync();
-                for (uint32_t i = lane; i < cntw; i += 64) atomicAdd(&s_wcnt[wid][ent[i] >> 26], 1u);
-                wave_sync();
-                const unsigned int v = lane < (uint32_t)C ? s_wcnt[wid][lane] : 0u;
-                const unsigned int incl = wave_incl_scan(v);
-                const unsigned int beg = incl - v;
-                if (lane < (uint32_t)C) {
-                    s_wcnt[wid][lane] = beg;
-                    unsigned int at = 0;
-                    if (v) at = atomicAdd(&s_cur[lane], v);
-                    unsigned long long b0 = gcap + lane * cap + at - beg;
-                    if (at + v > cap) {  // past the capacity: stores go to the spill records
-                        atomicOr(overflow, 1u);
-                        b0 = spill - beg;
+                skpart_flush<C>(cntw, ent, s_srt[wid], s_wcnt[wid], s_cur, s_base[wid], s_rel[wid], st, lane, gcap,
+                                cap, spill, M, rtile, recs, overflow);
+                cntw = 0;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < C) cnt[(uint64_t)threadIdx.x * G + g] = (unsigned int)min((uint64_t)s_cur[threadIdx.x], cap);
+    if (threadIdx.x == 0) {  // records of the group (one atomic per workgroup)
+        unsigned long long tot = 0;
+        for (int c = 0; c < C; c++) tot += s_cur[c];
+        if (tot) atomicAdd(nrec, tot);
+    }
+    unsigned int *hw = reinterpret_cast<unsigned int *>(hll + g * NREG);
+    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) hw[i] = s_hll[i];
+}
+
+// k_skpart for one compile-time window width W = k - m + 1 (the headline's k = 31: W = 17):
+// a round is one block of W m-mers, their hashes and the previous block's suffix minima held
+// in registers (van Herk / Gil-Werman: window rW + j = min(suffix_r[j], prefix_{r+1}[j - 1])),
+// so no per-lane LDS ring; the buffer (no ring either) takes a whole round of entries.
+constexpr int SK2_ECAP_W = 1600;  // entries a wave buffers (LDS: 3 workgroups per CU)
+template <int NPF, int W>
+__global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restrict__ buf,
+                                                         const uint64_t *__restrict__ off, uint64_t nreads, MinCfg mc,
+                                                         uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
+                                                         uint32_t smask, uint4 *recs, unsigned int *cnt, uint8_t *hll,
+                                                         unsigned long long *nrec, unsigned int *overflow) {
+    constexpr int C = 1 << SK2_CBITS;
+    constexpr int NREG = 1 << HLL_REG_BITS;
+    constexpr int SW = NPF * 64 + 4;
+    static_assert(SK2_ECAP_W >= 64 * (W + 2), "a round's entries fit the buffer");
+    __shared__ uint32_t s_stage[PT_WAVES][SW];
+    __shared__ uint32_t s_ent[PT_WAVES][SK2_ECAP_W];
+    __shared__ uint16_t s_srt[PT_WAVES][SK2_ECAP_W];
+    __shared__ uint32_t s_rel[PT_WAVES][64];
+    __shared__ unsigned long long s_base[PT_WAVES][C];
+    __shared__ unsigned int s_wcnt[PT_WAVES][C];
+    __shared__ unsigned int s_cur[C];
+    __shared__ unsigned int s_hll[NREG / 4];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) s_hll[i] = 0;
+    if (threadIdx.x < C) s_cur[threadIdx.x] = 0;
+    if (lane < C) s_wcnt[wid][lane] = 0;
+    __syncthreads();
+    const uint64_t g = blockIdx.x;
+    const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
+    const uint32_t ntile = (uint32_t)((g1 - g0 + 63) / 64);
+    const int k = mc.k, m = mc.m;
+    const uint32_t nmax = sk2_nmax(k);
+    const uint64_t kmask = kmask64(k);
+    uint4 pf[NPF];
+    uint64_t nx_base = 0;
+    uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
+    if (wid < ntile) EC_PT_ISSUE(wid);
+    const unsigned long long gcap = g * C * cap, spill = (unsigned long long)C * G * cap;
+    uint32_t *st = s_stage[wid];
+    uint32_t *ent = s_ent[wid];
+    for (uint32_t t = wid; t < ntile; t += PT_WAVES) {
+#pragma unroll
+        for (int q = 0; q < NPF; q++) st[q * 64 + lane] = pack16(pf[q]);
+        const uint32_t tbase = (uint32_t)nx_base, s = nx_s;
+        const uint32_t len = lane < nx_n ? nx_e - nx_s : 0u;
+        const bool more = t + PT_WAVES < ntile;
+        const bool has = len >= (uint32_t)k;  // then len - k + 1 == M
+        const uint32_t rel = has ? s - tbase : 0u;
+        s_rel[wid][lane] = rel;
+        wave_sync();
+        uint32_t mf = 0, mr = 0;
+        auto push_base = [&](uint32_t b) {
+            mf = ((mf << 2) | b) & mc.mmask;
+            mr = (mr >> 2) | ((3u - b) << mc.msh);
+        };
+        // block 0 = m-mers 0 .. W - 1 (bases 0 .. k - 1): its suffix minima
+        uint32_t S[W];
+        {
+            const uint32_t x0 = sk_bases16(st, rel), x1 = sk_bases16(st, rel + 16);
+            for (int tb = 0; tb < m - 1; tb++) push_base(tb < 16 ? (x0 >> (2 * tb)) & 3u : (x1 >> (2 * (tb - 16))) & 3u);
+#pragma unroll
+            for (int j = 0; j < W; j++) {
+                const int tb = m - 1 + j;
+                push_base(tb < 16 ? (x0 >> (2 * tb)) & 3u : (x1 >> (2 * (tb - 16))) & 3u);
+                S[j] = mmer_hash(mf < mr ? mf : mr);
+            }
+#pragma unroll
+            for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
+        }
+        const uint32_t nrounds = __any(has) ? (M + W - 1) / W : 0u;
+        if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
+        uint32_t runv = 0, runn = 0, runi = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
+        const uint32_t rtile = 64 * t;  // the tile's first read relative to g0
+        for (uint32_t round = 0; round < nrounds; round++) {
+            const uint32_t w0 = round * W;  // first window of the round
+            // bases of m-mers (round + 1) W + j: (round + 1) W + m - 1 + j
+            const uint32_t pb = rel + w0 + W + m - 1;
+            const uint32_t xb0 = sk_bases16(st, pb), xb1 = sk_bases16(st, pb + 16);
+            uint32_t H[W];
+            uint32_t P = 0xFFFFFFFFu;  // prefix minimum of the next block so far
+#pragma unroll
+            for (int j = 0; j < W; j++) {
+                if (w0 + j >= M) break;  // uniform
+                const uint32_t v = min(S[j], P);  // window w0 + j
+                push_base(j < 16 ? (xb0 >> (2 * j)) & 3u : (xb1 >> (2 * (j - 16))) & 3u);
+                H[j] = mmer_hash(mf < mr ? mf : mr);
+                P = min(P, H[j]);
+                const bool ok = has;
+                // HyperLogLog over the k-mers of sampled minimizers (their canonical k-mer from the stage)
+                if (ok && (v & smask) == 0) {
+                    const uint32_t p = rel + w0 + j;
+                    const uint64_t K = (uint64_t)sk_bases16(st, p) | (uint64_t)sk_bases16(st, p + 16) << 32;
+                    const uint64_t krc = ~K & kmask, kfw = rev2_64(K) >> (64 - 2 * k);
+                    sk_hll_put(s_hll, (uint32_t)(mix64(kfw < krc ? kfw : krc) >> 32));
+                }
+                const bool close = ok && runn && (v != runv || runn == nmax);
+                const uint64_t bal = __ballot(close);
+                if (close) {
+                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
+                }
+                cntw += (uint32_t)__popcll(bal);
+                if (ok) {
+                    if (close || !runn) {
+                        runv = v;
+                        runi = w0 + j;
+                        runn = 0;
                     }
-                    s_base[wid][lane] = b0;
+                    runn++;
                 }
-                wave_sync();
-                for (uint32_t i = lane; i < cntw; i += 64) {
-                    const unsigned int p = atomicAdd(&s_wcnt[wid][ent[i] >> 26], 1u);
-                    s_srt[wid][p] = (uint16_t)i;
+            }
+            // the next round's suffix minima (the block's unused tail at the read's end is never read)
+#pragma unroll
+            for (int j = 0; j < W; j++) S[j] = H[j];
+#pragma unroll
+            for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
+            const bool last = round + 1 == nrounds;
+            if (last) {  // the reads' final runs
+                const bool fin = has && runn;
+                const uint64_t bal = __ballot(fin);
+                if (fin) {
+                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
                 }
-                wave_sync();
-                for (uint32_t i = lane; i < cntw; i += 64) {
-                    const uint32_t e = ent[s_srt[wid][i]];
-                    const uint32_t lr = e & 63u, i0 = (e >> 6) & 0xFFu, n1 = (e >> 14) & 15u;
-                    const uint32_t p0 = s_rel[wid][lr] + i0;
-                    uint4 o;
-                    o.x = bases16(p0);
-                    o.y = bases16(p0 + 16);
-                    o.z = (bases16(p0 + 32) & 0x0FFFFFFFu) | n1 << 28;
-                    o.w = ((e >> 18) & ((1u << SK2_FBITS) - 1)) << 24 | ((rtile + lr) * M + i0);
-                    recs[s_base[wid][e >> 26] + i] = o;
-                }
-                wave_sync();
-                if (lane < (uint32_t)C) s_wcnt[wid][lane] = 0;
+                cntw += (uint32_t)__popcll(bal);
+                if (more) EC_PT_ISSUE(t + PT_WAVES);
+            }
+            // flush: the buffer could not take another round, or the stage is about to change
+            if (last || cntw > (uint32_t)(SK2_ECAP_W - 64 * (W + 1))) {
+                skpart_flush<C>(cntw, ent, s_srt[wid], s_wcnt[wid], s_cur, s_base[wid], s_rel[wid], st, lane, gcap,
+                                cap, spill, M, rtile, recs, overflow);
                 cntw = 0;
             }
         }
