@@ -411,17 +411,35 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     k_skpart<NPF><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, \
                                                       recs, s->cnt.as<unsigned int>(), s->hll.as<uint8_t>(),      \
                                                       &dsc->nrec, &dsc->overflow)
-#define EC_SKPART_W(NPF)                                                                                      \
-    k_skpart_w<NPF, 17><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap,     \
-                                                            smask, recs, s->cnt.as<unsigned int>(),                    \
-                                                            s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow)
-    if (mc.w == 17 && !getenv("EULERHIP_SKPART_RING")) {  // k = 31: register-block minima
-        if (npf == 4) EC_SKPART_W(4);
-        else if (npf == 7) EC_SKPART_W(7);
-        else EC_SKPART_W(10);
+#define EC_SKPART_W(NPF, W)                                                                                   \
+    k_skpart_w<NPF, W><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap,      \
+                                                           smask, recs, s->cnt.as<unsigned int>(),                     \
+                                                           s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow)
+#define EC_SKPART_NPF(W)              \
+    if (npf == 4) EC_SKPART_W(4, W);  \
+    else if (npf == 7) EC_SKPART_W(7, W); \
+    else EC_SKPART_W(10, W)
+    // register-block minima for every window width of 21 <= k <= 32 (w = k - 14); the LDS-ring
+    // kernel stays for EULERHIP_SKPART_RING (A/B: 2.19 against 1.60 ms at k = 31)
+    if (!getenv("EULERHIP_SKPART_RING")) {
+        switch (mc.w) {
+            case 7: EC_SKPART_NPF(7); break;
+            case 8: EC_SKPART_NPF(8); break;
+            case 9: EC_SKPART_NPF(9); break;
+            case 10: EC_SKPART_NPF(10); break;
+            case 11: EC_SKPART_NPF(11); break;
+            case 12: EC_SKPART_NPF(12); break;
+            case 13: EC_SKPART_NPF(13); break;
+            case 14: EC_SKPART_NPF(14); break;
+            case 15: EC_SKPART_NPF(15); break;
+            case 16: EC_SKPART_NPF(16); break;
+            case 17: EC_SKPART_NPF(17); break;
+            default: EC_SKPART_NPF(18); break;  // k = 32
+        }
     } else if (npf == 4) EC_SKPART(4);
     else if (npf == 7) EC_SKPART(7);
     else EC_SKPART(10);
+#undef EC_SKPART_NPF
 #undef EC_SKPART_W
 #undef EC_SKPART
     kmark(s, 1, 1);

@@ -612,3 +612,19 @@ def test_sk2_declines_filter_and_window_records(gpu_session, monkeypatch):
     res = gpu_session.fetch(31, True)
     assert res.stats.count_variant == 1
     assert [[x, c] for x, c in res.dict_items] == ref["d"] and res.links == rl
+
+
+@pytest.mark.parametrize("k", [21, 28, 31])
+def test_sk2_ring_partition_vs_oracle(gpu_session, monkeypatch, k):
+    """the LDS-ring sliding-minimum partition (EULERHIP_SKPART_RING) against the oracle and
+    against the register-block default: the same records"""
+    buf, off = make_reads(30_000, 10_000, 100, 5300 + k, err=0.002)
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res0 = gpu_session.fetch(k, True)
+    monkeypatch.setenv("EULERHIP_SKPART_RING", "1")
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(k, True)
+    assert res.stats.count_variant == 3 and res.stats.n_records == res0.stats.n_records
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
