@@ -375,10 +375,15 @@ BucketPlan plan_buckets(double est, long long limit, bool filt_ok) {
 // prescan).  done = false when the input does not qualify, the distinct estimate asks for the
 // seen-twice filter, or a run / bucket / table outgrew its capacity: phase_count_v2 then counts
 // with window records.
+// validate: no k_prescan ran (phase_count_v2's fast path): M and npf come from the first read,
+// the partition checks the input and counts the windows; *invalid = the input does not meet
+// the prescan's conditions (the caller then takes the prescan path).
 int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads,
                     uint64_t read_base, int k, long long limit, uint32_t M, uint64_t G, uint64_t gsize, uint64_t P,
-                    int npf, unsigned int &U, SolidIndex &sidx, bool &done) {
+                    int npf, unsigned int &U, SolidIndex &sidx, bool &done, bool validate = false,
+                    bool *invalid = nullptr) {
     done = false;
+    if (invalid) *invalid = false;
     if (k < SK_MIN_K || k > 32 || M > 256 || gsize * M >= (1ull << 24) || (read_base + nreads) * 2 * M >= (1ull << 32) ||
         getenv("EULERHIP_NO_SK2"))
         return EC_OK;
@@ -386,6 +391,11 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc;
     auto reset = [&]() -> int {  // scalars as phase_count_v2 expects them after its prescan
+        if (validate) {  // as begin_call left them: the prescan runs next
+            EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
+            EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
+            return EC_OK;
+        }
         EC_HIP(hipMemsetAsync(&dsc->overflow, 0, sizeof(unsigned int), st));
         EC_HIP(hipMemsetAsync(&dsc->skew, 0, sizeof(unsigned int), st));
         EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, sizeof(unsigned int), st));
@@ -411,10 +421,15 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     k_skpart<NPF><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, \
                                                       recs, s->cnt.as<unsigned int>(), s->hll.as<uint8_t>(),      \
                                                       &dsc->nrec, &dsc->overflow)
-#define EC_SKPART_W(NPF, W)                                                                                   \
-    k_skpart_w<NPF, W><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap,      \
-                                                           smask, recs, s->cnt.as<unsigned int>(),                     \
-                                                           s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow)
+#define EC_SKPART_WV(NPF, W, VAL)                                                                             \
+    k_skpart_w<NPF, W, VAL><<<(unsigned)G, PT_THREADS, 0, st>>>(                                                 \
+        d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, recs, s->cnt.as<unsigned int>(),          \
+        s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow, &dsc->lens[2], &dsc->npos)
+#define EC_SKPART_W(NPF, W)            \
+    if (validate)                      \
+        EC_SKPART_WV(NPF, W, true);    \
+    else                               \
+        EC_SKPART_WV(NPF, W, false)
 #define EC_SKPART_NPF(W)              \
     if (npf == 4) EC_SKPART_W(4, W);  \
     else if (npf == 7) EC_SKPART_W(7, W); \
@@ -441,6 +456,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     else EC_SKPART(10);
 #undef EC_SKPART_NPF
 #undef EC_SKPART_W
+#undef EC_SKPART_WV
 #undef EC_SKPART
     kmark(s, 1, 1);
     EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));
@@ -449,6 +465,14 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     const bool verbose = getenv("EULERHIP_VERBOSE") != nullptr;
+    if (validate) {
+        if (hsc.lens[2]) {  // a read of another length, a byte outside ACGT, an oversized tile
+            if (verbose) fprintf(stderr, "count_sk2: input needs the prescan\n");
+            if (invalid) *invalid = true;
+            return reset();
+        }
+        P = hsc.npos;
+    }
     if (hsc.overflow) {  // a run outgrew its capacity
         if (verbose) fprintf(stderr, "count_sk2: partition run overflow (cap %llu)\n", (unsigned long long)cap);
         return reset();
@@ -563,6 +587,33 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, RF_MAX_RUNS));
     const uint64_t gsize = ((ntiles + G - 1) / G) * 64;
     G = (nreads + gsize - 1) / gsize;
+    auto npf_of = [](uint64_t lall) {  // 16-B chunks of a 64-read wave tile -> staged KiB per wave
+        const uint64_t need16 = (64ull * lall + 30 + 15) / 16;
+        return need16 <= 4 * 64 ? 4 : need16 <= 7 * 64 ? 7 : need16 <= 10 * 64 ? 10 : 0;
+    };
+    // super-k-mer fast path without the prescan (count_sk2.h, k_skpart_w<., ., true>): the
+    // read length of the first read; the partition checks the rest
+    if (allow_sk2 && k >= SK_MIN_K && k <= 32 && !getenv("EULERHIP_NO_SK2") && !getenv("EULERHIP_SKPART_RING") &&
+        !getenv("EULERHIP_NO_FASTSK2")) {
+        uint64_t o2[2] = {0, 0};
+        EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        const uint64_t L = o2[1] - o2[0];
+        const int npf = npf_of(L);
+        if (L >= (uint64_t)k && npf) {
+            const uint32_t M = (uint32_t)(L - k + 1);
+            bool done = false, invalid = false;
+            mark(s, 2 * EC_STAGE_PRESCAN);  // (no prescan: the stage stays empty)
+            mark(s, 2 * EC_STAGE_PRESCAN + 1);
+            EC_CHECK(phase_count_sk2(s, d_reads, d_off, nreads, read_base, k, limit, M, G, gsize, nreads * M, npf, U,
+                                     sidx, done, true, &invalid));
+            if (done) {
+                ok = true;
+                return EC_OK;
+            }
+            if (!invalid) allow_sk2 = false;  // the estimate or a capacity declined: window records
+        }
+    }
     mark(s, 2 * EC_STAGE_PRESCAN);
     kmark(s, 0, 0);
     k_prescan<<<(unsigned)G, 256, 0, st>>>(d_reads, d_off, nreads, k, gsize, &dsc->npos, &dsc->bad, dsc->lens);
@@ -583,8 +634,7 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     int ibits = 1;
     while ((1ull << ibits) < M) ibits++;
     if (ibits > 15 || nreads + read_base > (1ull << (31 - ibits)) || 2ull * M - 1 > MAX_LOCAL_EVENT) return EC_OK;
-    const uint64_t need16 = (64ull * lall + 30 + 15) / 16;  // 16-B chunks of a 64-read wave tile
-    const int npf = need16 <= 4 * 64 ? 4 : need16 <= 7 * 64 ? 7 : need16 <= 10 * 64 ? 10 : 0;
+    const int npf = npf_of(lall);
     if (!npf) return EC_OK;
     if (allow_sk2) {  // super-k-mer records (count_sk2.h) unless window records are asked for
         bool done = false;

@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
     const uint64_t kmask = kmask64(k);
     uint4 pf[NPF];
     uint64_t nx_base = 0;
-    uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
+    uint32_t nx_s = 0, nx_e = 0, nx_n = 0, nx_lo = 0, nx_hi = 0, nx_n16 = 0;
     if (wid < ntile) EC_PT_ISSUE(wid);
     const unsigned long long gcap = g * C * cap, spill = (unsigned long long)C * G * cap;
     uint32_t *st = s_stage[wid];
@@ -281,12 +281,19 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict
 // in registers (van Herk / Gil-Werman: window rW + j = min(suffix_r[j], prefix_{r+1}[j - 1])),
 // so no per-lane LDS ring; the buffer (no ring either) takes a whole round of entries.
 constexpr int SK2_ECAP_W = 1600;  // entries a wave buffers (LDS: 3 workgroups per CU)
-template <int NPF, int W>
+//
+// VAL (no k_prescan ran; M and the stage size come from the first read): the kernel checks
+// what the prescan would have -- every read with windows is L = M + k - 1 bytes long, every
+// byte of a read is A, C, G or T (decode(encode(byte)) == byte: one v_perm per 4 bytes), no
+// tile outgrows the stage -- raises *vfail otherwise (the host then takes the prescan path),
+// and adds the windows to *npos.
+template <int NPF, int W, bool VAL>
 __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restrict__ buf,
                                                          const uint64_t *__restrict__ off, uint64_t nreads, MinCfg mc,
                                                          uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
                                                          uint32_t smask, uint4 *recs, unsigned int *cnt, uint8_t *hll,
-                                                         unsigned long long *nrec, unsigned int *overflow) {
+                                                         unsigned long long *nrec, unsigned int *overflow,
+                                                         unsigned int *vfail, unsigned long long *npos) {
     constexpr int C = 1 << SK2_CBITS;
     constexpr int NREG = 1 << HLL_REG_BITS;
     constexpr int SW = NPF * 64 + 4;
@@ -313,14 +320,53 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
     const uint64_t kmask = kmask64(k);
     uint4 pf[NPF];
     uint64_t nx_base = 0;
-    uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
+    uint32_t nx_s = 0, nx_e = 0, nx_n = 0, nx_lo = 0, nx_hi = 0, nx_n16 = 0;
+    uint32_t nwin = 0;  // VAL: reads with windows (uniform)
     if (wid < ntile) EC_PT_ISSUE(wid);
     const unsigned long long gcap = g * C * cap, spill = (unsigned long long)C * G * cap;
     uint32_t *st = s_stage[wid];
     uint32_t *ent = s_ent[wid];
     for (uint32_t t = wid; t < ntile; t += PT_WAVES) {
+        if (VAL) {
+            // stage and check in one pass: x = the bytes' 2-bit codes (pack4's first step), a byte
+            // is A, C, G or T iff decoding its code gives it back
+            uint32_t diff = 0;
 #pragma unroll
-        for (int q = 0; q < NPF; q++) st[q * 64 + lane] = pack16(pf[q]);
+            for (int q = 0; q < NPF; q++) {
+                const uint32_t wv[4] = {pf[q].x, pf[q].y, pf[q].z, pf[q].w};
+                uint32_t packed = 0, d[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t x = ((wv[u] >> 1) ^ (wv[u] >> 2)) & 0x03030303u;
+                    const uint32_t y = x | (x >> 6);
+                    packed |= ((y | (y >> 12)) & 0xFFu) << (8 * u);
+                    d[u] = __builtin_amdgcn_perm(0u, 0x54474341u, x) ^ wv[u];
+                }
+                st[q * 64 + lane] = packed;
+                const uint32_t lo = 16 * (q * 64 + lane);  // the chunk's bytes relative to nx_base
+                if (lo >= nx_lo && lo + 16 <= nx_hi) {
+                    diff |= d[0] | d[1] | d[2] | d[3];
+                } else if (lo < nx_hi && lo + 16 > nx_lo) {  // a chunk at the tile's ends: its read bytes only
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int b = (int)(lo + 4 * u);
+                        const int from = min(max((int)nx_lo - b, 0), 4), to = min(max((int)nx_hi - b, 0), 4);
+                        const uint32_t keep = to > from ? (0xFFFFFFFFu >> (32 - 8 * (to - from))) << (8 * from) : 0u;
+                        diff |= d[u] & keep;
+                    }
+                }
+            }
+            bool bad = nx_n16 > (uint32_t)NPF * 64 || diff != 0;  // a read longer than the stage, a byte
+            if (lane < nx_n) {
+                const uint32_t ln = nx_e - nx_s;
+                bad |= ln >= (uint32_t)k && ln != M + (uint32_t)k - 1;
+            }
+            if (__any(bad) && lane == 0) atomicOr(vfail, 1u);
+            nwin += (uint32_t)__popcll(__ballot(lane < nx_n && nx_e - nx_s >= (uint32_t)k));
+        } else {
+#pragma unroll
+            for (int q = 0; q < NPF; q++) st[q * 64 + lane] = pack16(pf[q]);
+        }
         const uint32_t tbase = (uint32_t)nx_base, s = nx_s;
         const uint32_t len = lane < nx_n ? nx_e - nx_s : 0u;
         const bool more = t + PT_WAVES < ntile;
@@ -415,12 +461,19 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
             }
         }
     }
+    __shared__ unsigned int s_nwin[PT_WAVES];
+    if (VAL && lane == 0) s_nwin[wid] = nwin;
     __syncthreads();
     if (threadIdx.x < C) cnt[(uint64_t)threadIdx.x * G + g] = (unsigned int)min((uint64_t)s_cur[threadIdx.x], cap);
-    if (threadIdx.x == 0) {  // records of the group (one atomic per workgroup)
+    if (threadIdx.x == 0) {  // records (and VAL: windows) of the group, one atomic each per workgroup
         unsigned long long tot = 0;
         for (int c = 0; c < C; c++) tot += s_cur[c];
         if (tot) atomicAdd(nrec, tot);
+        if (VAL) {
+            unsigned long long wn = 0;
+            for (int q = 0; q < PT_WAVES; q++) wn += s_nwin[q];
+            if (wn) atomicAdd(npos, wn * M);
+        }
     }
     unsigned int *hw = reinterpret_cast<unsigned int *>(hll + g * NREG);
     for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) hw[i] = s_hll[i];

@@ -170,7 +170,8 @@ __device__ inline uint32_t pack16(const uint4 &v) {
 }
 
 // Next wave tile's bytes into pf[] and its reads' offsets (k_partition, k_skpart): uses the
-// kernel's g0, g1, off, buf, lane, pf, nx_base, nx_s, nx_e, nx_n
+// kernel's g0, g1, off, buf, lane, pf, nx_base, nx_s, nx_e, nx_n; nx_lo / nx_hi = the tile's
+// read bytes relative to nx_base, nx_n16 = its 16-B chunks
 // (a macro, not a lambda: a lambda capturing pf keeps the array in scratch memory)
 #define EC_PT_ISSUE(T)                                                                                   \
     do {                                                                                                 \
@@ -183,6 +184,7 @@ __device__ inline uint32_t pack16(const uint4 &v) {
         _Pragma("unroll") for (int q = 0; q < NPF; q++)                                                   \
             pf[q] = src_[min(q * 64 + lane, n16_ - 1)]; /* in bounds: no branch around the load */       \
         nx_base = (uint64_t)p0_ - (uint64_t)buf;                                                         \
+        nx_lo = (uint32_t)(b0_ - nx_base), nx_hi = (uint32_t)(b1_ - nx_base), nx_n16 = n16_;             \
         /* low words of the read's offsets (differences mod 2^32; no wait until they are used) */       \
         const uint64_t ri_ = min(r0_ + lane, r1_ - 1);                                                   \
         nx_s = reinterpret_cast<const uint32_t *>(off)[2 * ri_];                                         \
@@ -248,7 +250,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
     // the next tile's bytes (in flight while the current tile is processed) and its reads
     uint4 pf[NPF];
     uint64_t nx_base = 0;
-    uint32_t nx_s = 0, nx_e = 0, nx_n = 0;
+    uint32_t nx_s = 0, nx_e = 0, nx_n = 0, nx_lo = 0, nx_hi = 0, nx_n16 = 0;
     if (wid < ntile) EC_PT_ISSUE(wid);
     const unsigned long long gcap = g * C * cap, gstride = cap;
     const unsigned long long spill = (unsigned long long)C * G * cap;
