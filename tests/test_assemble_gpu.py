@@ -628,3 +628,30 @@ def test_sk2_ring_partition_vs_oracle(gpu_session, monkeypatch, k):
     assert res.stats.count_variant == 3 and res.stats.n_records == res0.stats.n_records
     assert [[x, c] for x, c in res.dict_items] == ref["d"]
     assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+def test_sk2_fast_path_fallbacks_vs_oracle(gpu_session):
+    """the prescan-free super-k-mer partition takes its read length from the first read and
+    hands anything else back to the prescan path: a longer read later on, an N in the last read,
+    reads shorter than k beside the windowed ones"""
+    rng = np.random.default_rng(77)
+    g = "".join("ACGT"[x] for x in rng.integers(0, 4, 30_000))
+
+    def sample(L):
+        p = int(rng.integers(0, len(g) - L))
+        return g[p:p + L]
+
+    base = [sample(90) for _ in range(5_000)]
+    cases = {
+        "longer_later": base[:2_500] + [sample(140)] + base[2_500:],
+        "n_last": base[:-1] + [base[-1][:40] + "N" + base[-1][41:]],
+        "short_reads": base[:100] + [sample(int(rng.integers(1, 31))) for _ in range(300)] + base[100:],
+    }
+    for name, reads in cases.items():
+        d, r, gl = oracle.assemble(reads, 31, 1)
+        res = gpu_session.assemble(reads, 31, 1, want_dict=True)
+        assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == gl, name
+        if name == "short_reads":
+            assert res.stats.count_variant == 3, name
+        else:
+            assert res.stats.count_variant != 3, name
