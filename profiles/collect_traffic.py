@@ -20,7 +20,7 @@ KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine", "k_pre
 
 def short(name):
     for k in KERNELS:
-        if re.search(r"\b%s(_sk)?\b" % k, name):
+        if re.search(r"\b%s(_sk|_w)?\b" % k, name):
             return k
     return None
 
