@@ -522,8 +522,11 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
     kmark(s, 2, 0);
     const double inv_m = 1.0 / M;
+    // experiments: duplicate records merged before their windows are inserted (EULERHIP_SK2_DEDUPE=1
+    // or 2 records per thread; measured slower)
+    const int dedupe = getenv("EULERHIP_SK2_DEDUPE") ? atoi(getenv("EULERHIP_SK2_DEDUPE")) : 0;
 #define EC_SKBUCKET(SLOTS, EVEN)                                                                              \
-    k_skbucket<SLOTS, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(                                          \
+    (dedupe == 2 ? k_skbucket_dd<SLOTS, EVEN, 2> : dedupe ? k_skbucket_dd<SLOTS, EVEN, 1> : k_skbucket<SLOTS, EVEN>)<<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(   \
         s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(),                \
         s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),          \
         s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow)
@@ -535,6 +538,17 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         else EC_SKBUCKET(4096, true);
     }
 #undef EC_SKBUCKET
+#ifdef SK2_DD_TIMING
+    {
+        unsigned long long t[4];
+        EC_HIP(hipStreamSynchronize(st));
+        EC_HIP(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sk2_dd_t), sizeof(t)));
+        fprintf(stderr, "sk2_dd phases (block-us summed): merge %.0f sort %.0f insert %.0f fin %.0f\n", t[0] / 100.0,
+                t[1] / 100.0, t[2] / 100.0, t[3] / 100.0);
+        memset(t, 0, sizeof(t));
+        EC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sk2_dd_t), t, sizeof(t)));
+    }
+#endif
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));

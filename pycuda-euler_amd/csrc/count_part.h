@@ -771,6 +771,38 @@ __device__ inline unsigned int lds_locate(Tab &tab, unsigned int *s_over, unsign
     }
     return slot;
 }
+// lds_locate of two keys at once (a lane's windows o and o + h): their probe chains run in one
+// loop, so a step waits for the longer chain instead of the sum of both.
+template <int SLOTS, typename Tab>
+__device__ inline void lds_locate2(Tab &tab, unsigned int *s_over, unsigned long long cA, unsigned int &sA,
+                                   unsigned long long curA, unsigned long long cB, unsigned int &sB,
+                                   unsigned long long curB) {
+    bool mA = curA != cA, mB = curB != cB;
+    auto claim = [&](unsigned long long c, unsigned int slot, unsigned long long &cur) {
+        if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {  // table full: the bucket is redone elsewhere
+            s_over[0] = 1;
+            cur = c;
+        } else {
+            cur = atomicCAS(&tab.key[slot], EMPTY_KEY, c);
+            if (cur == EMPTY_KEY) cur = c;
+            else atomicSub(&s_over[1], 1u);
+        }
+    };
+#pragma unroll 1
+    while (__any(mA || mB)) {
+        if (mA && curA == EMPTY_KEY) claim(cA, sA, curA);
+        if (mB && curB == EMPTY_KEY) claim(cB, sB, curB);
+        mA = curA != cA;
+        mB = curB != cB;
+        if (mA) sA = (sA + 1) & (SLOTS - 1);
+        if (mB) sB = (sB + 1) & (SLOTS - 1);
+        const unsigned long long nA = mA ? tab.key[sA] : cA, nB = mB ? tab.key[sB] : cB;
+        curA = nA;
+        curB = nB;
+        mA = curA != cA;
+        mB = curB != cB;
+    }
+}
 template <int SLOTS, bool DET = false>
 __device__ inline void lds_insert(LTab<SLOTS> &tab, unsigned int *s_over, unsigned long long c, unsigned int slot0,
                                   unsigned int add, unsigned long long eC, unsigned long long eT,

@@ -729,8 +729,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
             const uint64_t cB = events(fB, rB, rem + oB, rd2, eCB, eTB, addB);
             unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1), sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
             const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
-            sA = lds_locate<SLOTS>(tab, s_over, cA, sA, kA);
-            sB = lds_locate<SLOTS>(tab, s_over, cB, sB, bB ? kB : cB);
+            lds_locate2<SLOTS>(tab, s_over, cA, sA, kA, cB, sB, bB ? kB : cB);
             atomicAdd(&tab.count[sA], addA);
             if (bB) atomicAdd(&tab.count[sB], addB);
             const uint2 vA = tab.ev[sA], vB = tab.ev[sB];
@@ -746,4 +745,234 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
 }
 
 // -------------------------------------------------------
+// k_skbucket with duplicate records merged first.  At ~150-fold coverage most records of a
+// bucket are the same super-k-mer read by different reads (one in three of a 2048-record chunk
+// is distinct, simulated): a chunk's records go through an LDS table keyed by content (hash of
+// x, y, z; equality checked against the representative's record, re-read from global memory),
+// each entry keeping the multiplicity and two minima over its members' positions -- pa = min p
+// (min read, then min first window) and pb = min (read M + M - 1 - window) (min read, then max
+// window) -- which give every window's first events exactly: a window whose canonical form is
+// the forward string takes eC from pa and eT from pb, the others the reverse.  The distinct
+// records, counting-sorted by window count, then insert their windows with add = multiplicity.
+#ifdef SK2_DD_TIMING  // experiments: per-phase clock totals of k_skbucket_dd (thread 0 of each block)
+__device__ unsigned long long g_sk2_dd_t[4];
+#define SKD_T(i)                                                                                     \
+    do {                                                                                             \
+        if (threadIdx.x == 0) {                                                                      \
+            const unsigned long long t_ = wall_clock64();                                            \
+            if (i) atomicAdd(&g_sk2_dd_t[(i) - 1], t_ - t_last);                                     \
+            t_last = t_;                                                                             \
+        }                                                                                            \
+    } while (0)
+#else
+#define SKD_T(i) (void)0
+#endif
+template <int SLOTS, bool EVEN_K, int PER>  // PER records per thread and chunk
+__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_dd(const uint4 *recs, const unsigned long long *bbeg,
+                                                                const unsigned long long *bend, int k, uint32_t M,
+                                                                double inv_m, long long limit, unsigned long long *dkey,
+                                                                unsigned int *dcnt, unsigned long long *dfc,
+                                                                unsigned long long *dft, SubSlot *sub,
+                                                                unsigned int *nsolid, unsigned long long *ndistinct,
+                                                                unsigned int *overflow) {
+    constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
+    constexpr int SKD_CH = PER * BUCKET_THREADS, SKD_SLOTS = SKD_CH;  // records per chunk, content-table slots
+    constexpr int SKD_BITS = PER == 2 ? 11 : 10;
+    static_assert(SKD_CH < 4096, "index + 1 in the slot word's low 12 bits");
+    __shared__ LTabE<SLOTS> tab;
+    __shared__ unsigned int s_over[2];
+    __shared__ unsigned int d_idx[SKD_SLOTS];  // representative's record index + 1 (0: empty)
+    __shared__ unsigned int d_mult[SKD_SLOTS], d_pa[SKD_SLOTS], d_pb[SKD_SLOTS];
+    __shared__ uint16_t s_ord[SKD_CH];  // distinct records' slots, most windows first
+    __shared__ unsigned int s_ncnt[SK2_NMAX + 1];
+    const unsigned int b = blockIdx.x;
+    for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
+        tab.key[i] = EMPTY_KEY;
+        tab.count[i] = 0;
+        tab.ev[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    if (threadIdx.x == 0) s_over[0] = s_over[1] = 0;
+    __syncthreads();
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    const uint64_t kmask = kmask64(k);
+    const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
+    const unsigned int m2 = 2 * M - 1;
+    auto split = [&](unsigned int p, unsigned int &read, unsigned int &rem) {  // p = read M + rem
+        const unsigned int rd = (unsigned int)((double)p * inv_m);
+        int rm = (int)(p - rd * M);
+        read = rd;
+        if (rm < 0) read--, rm += (int)M;
+        else if (rm >= (int)M) read++, rm -= (int)M;
+        rem = (unsigned int)rm;
+    };
+#ifdef SK2_DD_TIMING
+    unsigned long long t_last = 0;
+#endif
+    uint4 nx[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const uint64_t i = r0 + threadIdx.x + q * BUCKET_THREADS;
+        nx[q] = i < r1 ? recs[i] : make_uint4(0, 0, 0, 0);
+    }
+    for (uint64_t c0 = r0; c0 < r1; c0 += SKD_CH) {
+        const unsigned int nv = (unsigned int)min<uint64_t>(SKD_CH, r1 - c0);
+        uint4 x[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) x[q] = nx[q];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {  // the next chunk
+            const uint64_t i = c0 + SKD_CH + threadIdx.x + q * BUCKET_THREADS;
+            if (i < r1) nx[q] = recs[i];
+        }
+        for (int i = threadIdx.x; i < SKD_SLOTS; i += blockDim.x) {
+            d_idx[i] = 0;
+            d_mult[i] = 0;
+            d_pa[i] = d_pb[i] = 0xFFFFFFFFu;
+        }
+        if (threadIdx.x <= SK2_NMAX) s_ncnt[threadIdx.x] = 0;
+        __syncthreads();
+        SKD_T(0);
+        // merge equal records
+        unsigned int myslot[PER];
+        bool lead[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const unsigned int ri = threadIdx.x + q * BUCKET_THREADS;
+            myslot[q] = 0;
+            lead[q] = false;
+            if (ri >= nv) continue;
+            // slot from the hash's high bits; a 20-bit tag beside the representative's index in
+            // the slot word, so a probe past another record's slot costs no global read
+            unsigned int hh = x[q].x * 0x9E3779B1u;
+            hh = (hh ^ (hh >> 16) ^ x[q].y) * 0x85EBCA77u;
+            hh = (hh ^ (hh >> 13) ^ x[q].z) * 0xC2B2AE3Du;
+            hh ^= hh >> 16;
+            const unsigned int tag = (hh * 0x27D4EB2Fu) & 0xFFFFF000u;
+            unsigned int slot = hh >> (32 - SKD_BITS);
+            const unsigned int mine = tag | (ri + 1);
+            for (;;) {  // <= nv distinct entries in SKD_SLOTS >= nv slots: ends
+                unsigned int cur = d_idx[slot];
+                if (cur == 0) {
+                    cur = atomicCAS(&d_idx[slot], 0u, mine);
+                    if (cur == 0) {
+                        lead[q] = true;
+                        break;
+                    }
+                }
+                if ((cur & 0xFFFFF000u) == tag) {
+                    const uint4 o = recs[c0 + (cur & 0xFFFu) - 1];  // the representative (just loaded: cached)
+                    if (o.x == x[q].x && o.y == x[q].y && o.z == x[q].z) break;
+                }
+                slot = (slot + 1) & (SKD_SLOTS - 1);
+            }
+            myslot[q] = slot;
+            unsigned int read, rem;
+            split(x[q].w, read, rem);
+            atomicAdd(&d_mult[slot], 1u);
+            const unsigned int pb = read * M + (M - 1 - rem);
+            if (x[q].w < d_pa[slot]) atomicMin(&d_pa[slot], x[q].w);
+            if (pb < d_pb[slot]) atomicMin(&d_pb[slot], pb);
+        }
+        __syncthreads();
+        SKD_T(1);
+        // the distinct records by window count (most first)
+        unsigned int bin[PER], rk[PER];
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            bin[q] = lead[q] ? SK2_NMAX - 1 - (x[q].z >> 28) : SK2_NMAX;
+            rk[q] = lead[q] ? atomicAdd(&s_ncnt[bin[q]], 1u) : 0u;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned int a = 0;
+            for (int q = 0; q < SK2_NMAX; q++) {
+                const unsigned int v = s_ncnt[q];
+                s_ncnt[q] = a;
+                a += v;
+            }
+            s_ncnt[SK2_NMAX] = a;  // distinct records
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++)
+            if (lead[q]) s_ord[s_ncnt[bin[q]] + rk[q]] = (uint16_t)myslot[q];
+        __syncthreads();
+        const unsigned int nd = s_ncnt[SK2_NMAX];
+        SKD_T(2);
+        for (unsigned int t = threadIdx.x; t < nd; t += blockDim.x) {
+            const unsigned int slot = s_ord[t];
+            const uint4 y = recs[c0 + (d_idx[slot] & 0xFFFu) - 1];
+            const unsigned int mult = d_mult[slot];
+            unsigned int readA, remA, readB, remB;
+            split(d_pa[slot], readA, remA);
+            split(d_pb[slot], readB, remB);
+            remB = M - 1 - remB;
+            const unsigned int a2 = readA * (2 * M), b2 = readB * (2 * M);
+            const unsigned int n = (y.z >> 28) + 1;
+            // window o: canonical key, its events (forward-canonical: eC from pa, eT from pb)
+            auto events = [&](uint64_t fwd, uint64_t rc, unsigned int o, unsigned int &eC, unsigned int &eT,
+                              unsigned int &add) {
+                const bool tw = fwd > rc;
+                const unsigned int la = remA + o, lb = remB + o;
+                add = mult;
+                if (EVEN_K && fwd == rc) {  // even-k palindrome: inserted twice at the forward event
+                    add = 2 * mult;
+                    eC = eT = a2 + la;
+                } else if (tw) {
+                    eC = b2 + (m2 - lb);
+                    eT = a2 + la;
+                } else {
+                    eC = a2 + la;
+                    eT = b2 + (m2 - lb);
+                }
+                return tw ? rc : fwd;
+            };
+            // two windows per step (o and o + h): their LDS probes and updates in flight together
+            const unsigned int h = (n + 1) >> 1;
+            auto at = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // window o straight out of the bases
+                const uint32_t lo = __builtin_amdgcn_alignbit(y.y, y.x, 2 * o), hi = __builtin_amdgcn_alignbit(y.z, y.y, 2 * o);
+                const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+                rv = ~P & kmask;
+                fw = rev2_64(P) >> fsh;
+            };
+            auto roll = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // to window o from o - 1
+                const unsigned int tb = o + (unsigned int)k - 1;
+                const uint32_t wd = tb < 32 ? y.y : y.z;
+                const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
+                fw = ((fw << 2) | bb) & kmask;
+                rv = (rv >> 2) | ((uint64_t)(3u - bb) << sh);
+            };
+            uint64_t fA, rA, fB, rB;
+            at(0, fA, rA);
+            at(h, fB, rB);
+            for (unsigned int i = 0; i < h; i++) {
+                const unsigned int oB = i + h;
+                const bool bB = oB < n;
+                if (i) {
+                    roll(i, fA, rA);
+                    roll(oB, fB, rB);
+                }
+                unsigned int eCA, eTA, eCB, eTB, addA, addB;
+                const uint64_t cA = events(fA, rA, i, eCA, eTA, addA);
+                const uint64_t cB = events(fB, rB, oB, eCB, eTB, addB);
+                unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1),
+                             sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
+                const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
+                lds_locate2<SLOTS>(tab, s_over, cA, sA, kA, cB, sB, bB ? kB : cB);
+                atomicAdd(&tab.count[sA], addA);
+                if (bB) atomicAdd(&tab.count[sB], addB);
+                const uint2 vA = tab.ev[sA], vB = tab.ev[sB];
+                if (eCA < vA.x) atomicMin(&tab.ev[sA].x, eCA);
+                if (eTA < vA.y) atomicMin(&tab.ev[sA].y, eTA);
+                if (bB && eCB < vB.x) atomicMin(&tab.ev[sB].x, eCB);
+                if (bB && eTB < vB.y) atomicMin(&tab.ev[sB].y, eTB);
+            }
+        }
+        __syncthreads();
+        SKD_T(3);
+    }
+    lds_table_finish<SLOTS, false, KeyId>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
+                                          overflow, KeyId(), EvExpand{2 * M});
+}
+
 }  // namespace ec
