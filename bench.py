@@ -5,6 +5,9 @@ One step = one full fused assembly (encode -> canonical count -> solid filter ->
 list ranking -> contig starts/order -> contig strings -> GFA links, i.e. the reference's
 build() + all_contigs()) of the whole synthetic read set, reads already resident in HBM.
 value = k-mer positions of the whole job / wall time of one step (max over ranks).
+N > 1 is weak-scaled by default: every rank holds its own config-sized read set (10 M x 100 bp
+on the headline) of the same genome, so the job is N x 10 M reads; --strong splits the
+config's reads over the ranks instead.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (read-sharded, RCCL exchange)
@@ -142,6 +145,9 @@ def main():
     ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true", help="use the multi-GPU path even with one rank")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: split the config's reads over the ranks (fixed job) instead of the default "
+                         "weak scaling (every rank samples its own config-sized read set of the same genome)")
     ap.add_argument("--wide-records", action="store_true", help="16-B count records only (EC_FLAG_WIDE_RECORDS)")
     ap.add_argument("--window-records", action="store_true",
                     help="one record per k-mer window, no super-k-mers (EC_FLAG_WINDOW_RECORDS)")
@@ -178,7 +184,12 @@ def main():
     t0 = time.time()
     from synth import make_reads
 
-    buf, off = make_reads(cfg["genome"], cfg["reads"], cfg["read_len"], cfg["seed"], err=cfg.get("err", 0.0))
+    # weak scaling (default): rank r holds reads r*R .. (r+1)*R - 1 of an N*R-read job on the
+    # config's genome, sampled by rank (synth.make_reads part=r); --strong: the config's R reads
+    # are split into contiguous shards (distributed.shard_range)
+    weak = use_dist and not args.strong
+    buf, off = make_reads(cfg["genome"], cfg["reads"], cfg["read_len"], cfg["seed"], err=cfg.get("err", 0.0),
+                          part=(rank if weak else None))
     log("rank %d: generated %d reads in %.1f s" % (rank, cfg["reads"], time.time() - t0))
     k = cfg["k"]
 
@@ -197,7 +208,8 @@ def main():
     else:
         import distributed
 
-        runner = distributed.ShardedAssembler(buf, off, k, 1, rank, world, local)
+        runner = distributed.ShardedAssembler(buf, off, k, 1, rank, world, local,
+                                              read_base=(rank * cfg["reads"] if weak else None))
 
         def step(timing=False):
             runner.run(timing)
@@ -229,7 +241,7 @@ def main():
     st = sess.stats() if not use_dist else runner.stats()
     P = int(st.n_positions) if not use_dist else runner.total_positions
     U = int(st.n_solid) if not use_dist else int(runner.engine.stats().n_solid)
-    R, L = cfg["reads"], cfg["read_len"]
+    R, L = cfg["reads"] * (world if weak else 1), cfg["read_len"]
     value = P / (ms / 1e3)
 
     if rank != 0:
@@ -277,10 +289,11 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "u64" if k <= 32 else "u128",
+        "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "u64" if k <= 32 else "u128",
         "data": "synthetic (iid ACGT genome, uniform %s %d bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)"
                 % ("error-free" if not cfg.get("err") else "%.1f%%-substitution" % (100 * cfg["err"]), L, cfg["seed"]),
-        "config": {"workload": cfg["name"], "genome_bp": cfg["genome"], "reads": R, "read_len": L, "k": k,
+        "config": {"workload": cfg["name"] + ("" if world == 1 or not weak else " per GPU"), "genome_bp": cfg["genome"],
+                   "reads": R, "reads_per_gpu": R // world, "read_len": L, "k": k,
                    "positions": P, "solid_kmers": U,
                    "contigs": int(st.n_contigs if not use_dist else runner.engine.stats().n_contigs),
                    "count_path": ["partitioned", "general", "superkmer"][int(st.count_path)],

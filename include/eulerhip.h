@@ -265,7 +265,9 @@ typedef struct {
     uint64_t first_twin;  /* first insertion event of its twin                                */
 } ec_kmer_record;
 
-/* count the shard (global read ids start at read_base); keeps every distinct k-mer */
+/* count the shard (global read ids start at read_base, read_base + nreads <= 2^32); keeps
+ * every distinct k-mer.  The count runs on shard-relative read ids (every shard qualifies
+ * for the same count path); ec_export_by_owner writes global first events. */
 int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offsets, uint64_t nreads,
                    uint64_t read_base, int k, unsigned flags);
 /* number of dense k-mer records the session holds (after ec_count_shard / ec_merge_owned) */

@@ -146,6 +146,7 @@ struct ec_session {
     unsigned flags = 0;        // flags of the current call
     DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur, cwalk;
     bool no_index = false;      // the call needs dense records only (shard count, owner merge)
+    uint64_t shard_base = 0;    // ec_count_shard: global id of the shard's read 0 (added at export)
     bool filt = false;          // phase_count: k_bucket_filt (more distinct keys than LDS tables hold)
     int pmax = 1, pmin = 0;     // k_bucket_filt: 2^pmax part tables per bucket region
     float part_keys = 1400.0f;  // k_bucket_filt: target keys per part table
@@ -279,6 +280,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     s->k = k;
     s->want_dict = (flags & EC_FLAG_WANT_DICT) != 0;
     s->flags = flags;
+    s->shard_base = 0;
     const bool timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
         for (auto &e : s->ev) EC_HIP(hipEventCreate(&e));
@@ -2042,18 +2044,26 @@ int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offs
         return EC_ERR_ARG;
     }
     EC_CHECK(begin_call(s, k, flags));
+    if (read_base + nreads > (1ull << 32)) {
+        set_error("global read ids reach %llu >= 2^32", (unsigned long long)(read_base + nreads));
+        return EC_ERR_CAPACITY;
+    }
     unsigned int U = 0;
     s->no_index = true;
     int rc = EC_OK;
+    // the shard is counted with shard-relative read ids (so every rank qualifies for the
+    // super-k-mer path's 32-bit positions, count_sk2.h); first events are events
+    // (read << 32) | window, so the export adds read_base << 32 to every real event
     if (k > 32) {
         SolidIndexW sidx{};
-        rc = phase_count_w(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, U, sidx);
+        rc = phase_count_w(s, d_reads, d_offsets, nreads, 0, k, LLONG_MIN, U, sidx);
     } else {
         SolidIndex sidx{};
-        rc = phase_count(s, d_reads, d_offsets, nreads, read_base, k, LLONG_MIN, flags, U, sidx);
+        rc = phase_count(s, d_reads, d_offsets, nreads, 0, k, LLONG_MIN, flags, U, sidx);
     }
     s->no_index = false;
     EC_CHECK(rc);
+    s->shard_base = read_base;
     s->n_dense = U;
     collect_timing(s);
     s->stats_ok = true;
@@ -2091,11 +2101,11 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
         if (wide)
             k_owner_scatter<K128><<<grid_for(n, B, 4096), B, 0, st>>>(
                 s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<AggW *>(d_out));
+                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<AggW *>(d_out), s->shard_base << 32);
         else
             k_owner_scatter<unsigned long long><<<grid_for(n, B, 4096), B, 0, st>>>(
                 s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<Agg *>(d_out));
+                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<Agg *>(d_out), s->shard_base << 32);
         EC_HIP(hipStreamSynchronize(st));
     }
     return EC_OK;

@@ -71,12 +71,14 @@ __global__ void __launch_bounds__(256) k_owner_hist(const K *dkey, unsigned int 
         if (h[i]) atomicAdd(&cnt[i], (unsigned long long)h[i]);
 }
 
-// scatter dense records into owner-major order; cursor[o] starts at the owner's offset
+// scatter dense records into owner-major order; cursor[o] starts at the owner's offset;
+// evbase = the shard's first global read id << 32 (ec_count_shard counts shard-relative)
 template <typename K>
 __global__ void __launch_bounds__(256) k_owner_scatter(const K *dkey, const unsigned int *dcnt,
                                                        const unsigned long long *dfc, const unsigned long long *dft,
                                                        unsigned int n, unsigned int nowners,
-                                                       unsigned long long *cursor, typename RecOf<K>::T *out) {
+                                                       unsigned long long *cursor, typename RecOf<K>::T *out,
+                                                       unsigned long long evbase) {
     __shared__ unsigned int h[MAX_OWNERS];
     __shared__ unsigned long long base[MAX_OWNERS];
     for (uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x; t0 < n; t0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -92,7 +94,11 @@ __global__ void __launch_bounds__(256) k_owner_scatter(const K *dkey, const unsi
         for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x)
             base[i] = h[i] ? atomicAdd(&cursor[i], (unsigned long long)h[i]) : 0ull;
         __syncthreads();
-        if (t < n) out[base[o] + rk] = RecOf<K>::make(dkey[t], dcnt[t], dfc[t], dft[t]);
+        if (t < n) {  // shard-relative first events -> global (NONE64 = no event, kept)
+            const unsigned long long fc = dfc[t], ft = dft[t];
+            out[base[o] + rk] = RecOf<K>::make(dkey[t], dcnt[t], fc == NONE64 ? fc : fc + evbase,
+                                               ft == NONE64 ? ft : ft + evbase);
+        }
         __syncthreads();
     }
 }

@@ -256,13 +256,19 @@ class ShardedAssembler:
     """bench.py / CLI front-end: this rank's shard of a read set already in host memory is
     moved to its GPU once; run() performs one full distributed assembly."""
 
-    def __init__(self, buf, off, k, limit, rank, world, local_rank, comm=None):
+    def __init__(self, buf, off, k, limit, rank, world, local_rank, comm=None, read_base=None):
+        """read_base None: (buf, off) is the whole read set and this rank takes its contiguous
+        shard; otherwise (buf, off) is this rank's shard already, its first read being global
+        read read_base (the ranks' shards in rank order form the job's read set)."""
         import torch
 
-        lo, hi = shard_range(len(off) - 1, rank, world)
+        if read_base is None:
+            lo, hi = shard_range(len(off) - 1, rank, world)
+        else:
+            lo, hi = 0, len(off) - 1
         b0, b1 = int(off[lo]), int(off[hi])
         self.nreads = hi - lo
-        self.read_base = lo
+        self.read_base = lo if read_base is None else int(read_base)
         self.k, self.limit = k, limit
         self.d_reads = torch.from_numpy(np.ascontiguousarray(buf[b0:b1])).to(f"cuda:{local_rank}")
         self.d_off = torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).to(f"cuda:{local_rank}")
@@ -291,21 +297,32 @@ class ShardedAssembler:
 def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None):
     """Simulate the distributed algorithm with len(engines) ranks on the local device(s):
     same engine calls, the collectives done by concatenation.  Returns rank 0's result."""
+    world = len(engines)
+    nreads = len(off) - 1
+    parts = []
+    for r in range(world):
+        lo, hi = shard_range(nreads, r, world)
+        b0, b1 = int(off[lo]), int(off[hi])
+        parts.append((buf[b0:b1], off[lo:hi + 1] - off[lo], lo))
+    return local_sharded_assemble_shards(engines, parts, k, limit, flags, partitioned)
+
+
+def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partitioned=None):
+    """local_sharded_assemble on given shards: parts[r] = (buf, off, read_base) of rank r (host
+    arrays; global read ids read_base.., increasing with r, gaps allowed)."""
     import torch
 
     world = len(engines)
-    nreads = len(off) - 1
     shards = []
-    for r, eng in enumerate(engines):
-        lo, hi = shard_range(nreads, r, world)
-        b0, b1 = int(off[lo]), int(off[hi])
-        d_reads = torch.from_numpy(np.ascontiguousarray(buf[b0:b1]) if b1 > b0 else np.zeros(1, np.uint8)).to(eng.device)
-        d_off = torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).to(eng.device)
-        shards.append((d_reads, d_off, hi - lo, lo))
+    for eng, (b, o, base) in zip(engines, parts):
+        d_reads = torch.from_numpy(np.ascontiguousarray(b) if len(b) else np.zeros(1, np.uint8)).to(eng.device)
+        d_off = torch.from_numpy(np.asarray(o).astype(np.int64)).to(eng.device)
+        shards.append((d_reads, d_off, len(o) - 1, int(base)))
     P = 0
     sends = []
     for eng, (d_reads, d_off, n, lo) in zip(engines, shards):
         st = eng.count_shard(d_reads, d_off, n, lo, k, flags)
+        eng.count_variant = int(st.count_variant)
         P += st.n_positions
         sends.append(eng.export_by_owner(world))
     solids = []

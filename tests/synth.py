@@ -6,10 +6,15 @@ import numpy as np
 LUT = np.frombuffer(b"ACGT", dtype=np.uint8)
 
 
-def make_reads(genome_len, n_reads, read_len, seed, err=0.0, n_rate=0.0, circular=False, rc_frac=0.5):
-    """Returns (buf uint8[n_reads*read_len], offsets uint64[n_reads+1]) of ASCII reads."""
+def make_reads(genome_len, n_reads, read_len, seed, err=0.0, n_rate=0.0, circular=False, rc_frac=0.5,
+               part=None):
+    """Returns (buf uint8[n_reads*read_len], offsets uint64[n_reads+1]) of ASCII reads.
+    part = i >= 1: the i-th further read set of the same genome (weak-scaled multi-GPU bench:
+    rank i samples its own n_reads from the genome of `seed`; part None / 0 = the seed's reads)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     g = rng.integers(0, 4, genome_len, dtype=np.uint8)
+    if part:
+        rng = np.random.Generator(np.random.PCG64([seed, int(part)]))
     if circular:
         g2 = np.concatenate([g, g[:read_len]])
         starts = rng.integers(0, genome_len, n_reads)

@@ -173,3 +173,25 @@ def test_local_sharded_split_tables(engines, monkeypatch, world):
     res, P = distributed.local_sharded_assemble(engines[:world], buf, off, 31, 1)
     assert P == ref["n_positions"]
     assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
+
+
+@pytest.mark.parametrize("k", [31, 25])
+def test_weak_shards_large_read_base(engines, k):
+    """bench.py's weak-scaled shards: every rank its own read set of one genome, global read ids
+    starting at rank * 40 M.  The shard count runs on shard-relative ids, so every rank takes the
+    super-k-mer count (its 32-bit positions read * M + window would overflow at a global
+    id of 80 M), and the export's global first events give the oracle's order of the
+    concatenated reads"""
+    import distributed
+
+    world = 3
+    sets = [make_reads(60_000, 20_000, 100, 7700, part=r) for r in range(world)]
+    buf = np.concatenate([b for b, _ in sets])
+    off = np.arange(world * 20_000 + 1, dtype=np.uint64) * np.uint64(100)
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    res, P = distributed.local_sharded_assemble_shards(
+        engines[:world], [(b, o, r * 40_000_000) for r, (b, o) in enumerate(sets)], k, 1)
+    assert [e.count_variant for e in engines[:world]] == [3] * world
+    assert P == ref["n_positions"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
+    assert res.stats.n_dict == ref["n_dict"]

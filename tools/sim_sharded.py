@@ -20,20 +20,28 @@ def main():
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--err", type=float, default=0.0, help="substitution rate (bench ecoli10m_err: 0.005)")
+    ap.add_argument("--weak", action="store_true",
+                    help="bench.py's default N > 1 mode: every rank its own --reads reads (synth part = rank)")
     a = ap.parse_args()
     import torch
 
     import distributed
     from synth import make_reads
 
-    buf, off = make_reads(4_600_000, a.reads, 100, 20261019, err=a.err)
     world = a.ranks
     engines = [distributed.HipEngine(0) for _ in range(world)]
     shards = []
-    for r in range(world):
-        lo, hi = distributed.shard_range(a.reads, r, world)
-        shards.append((torch.from_numpy(np.ascontiguousarray(buf[int(off[lo]):int(off[hi])])).cuda(),
-                       torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).cuda(), hi - lo, lo))
+    if a.weak:
+        for r in range(world):
+            buf, off = make_reads(4_600_000, a.reads, 100, 20261019, err=a.err, part=r)
+            shards.append((torch.from_numpy(buf).cuda(), torch.from_numpy(off.astype(np.int64)).cuda(), a.reads,
+                           r * a.reads))
+    else:
+        buf, off = make_reads(4_600_000, a.reads, 100, 20261019, err=a.err)
+        for r in range(world):
+            lo, hi = distributed.shard_range(a.reads, r, world)
+            shards.append((torch.from_numpy(np.ascontiguousarray(buf[int(off[lo]):int(off[hi])])).cuda(),
+                           torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).cuda(), hi - lo, lo))
     torch.cuda.synchronize()
     for rep in range(a.reps):
         t = {}
