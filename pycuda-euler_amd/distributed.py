@@ -109,11 +109,11 @@ class HipEngine:
         eulerhip.check(self.L.ec_export_dense(self._h(), ctypes.c_void_p(out.data_ptr())))
         return out[: m * rb]
 
-    def assemble_from_solid(self, recs, k, flags=0):
+    def assemble_from_solid(self, recs, k, flags=0, fetch=True):
         self.k = int(k)
         n = recs.numel() // self.rec_bytes()
         eulerhip.check(self.L.ec_assemble_from_solid(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), flags))
-        return self.sess.fetch(k)
+        return self.sess.fetch(k) if fetch else None
 
     # partitioned graph phase: ec_graph_load / ec_graph_links_part / ec_graph_finish
     def graph_load(self, recs, k, flags=0):
@@ -126,9 +126,11 @@ class HipEngine:
         """successors (uint32) of the oriented nodes of canonical ids [lo, hi) into `out`"""
         eulerhip.check(self.L.ec_graph_links_part(self._h(), int(lo), int(hi), ctypes.c_void_p(out.data_ptr())))
 
-    def graph_finish(self, succ, k, flags=0):
+    def graph_finish(self, succ, k, flags=0, fetch=True):
+        """fetch = False: the results stay in the session's pinned host buffers (as after
+        ec_assemble_device); engine.sess.fetch(k) copies them out later"""
         eulerhip.check(self.L.ec_graph_finish(self._h(), ctypes.c_void_p(succ.data_ptr()), flags))
-        return self.sess.fetch(k)
+        return self.sess.fetch(k) if fetch else None
 
     def stats(self):
         return self.sess.stats()
@@ -194,10 +196,12 @@ class TorchComm:
 
 # ---- the orchestration -----------------------------------------------------------------------
 def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None,
-                     phase_ms=None, partitioned=None):
+                     phase_ms=None, partitioned=None, fetch=True):
     """Run steps 1-4 for this rank; returns (result, n_positions_total).  on_count(stats)
     receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING); phase_ms, a
     dict, receives the wall time of every step (device-synchronised by the engine calls).
+    fetch = False: the result stays in the engine's session (result None; bench.py, like the
+    single-GPU step, which ends with the results in pinned host buffers).
     partitioned (default, unless EC_FLAG_GENERAL): each rank computes the successor links of its own owner
     segment of the gathered solid set only ("each GPU builds its local graph partition");
     the parts are all-gathered and every rank ranks the paths and emits the contigs."""
@@ -224,7 +228,7 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     if not partitioned:
         everything = comm.allgatherv(solid, fill=0xFF)  # filler records: all-ones keys, skipped
         tick("allgather")
-        res = engine.assemble_from_solid(everything, k, flags)
+        res = engine.assemble_from_solid(everything, k, flags, fetch=fetch)
         tick("graph")
     else:
         everything, sizes = comm.allgatherv(solid, fill=0xFF, with_sizes=True)
@@ -244,7 +248,7 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
         else:
             succ = gathered
         tick("gather_links")
-        res = engine.graph_finish(succ, k, flags)
+        res = engine.graph_finish(succ, k, flags, fetch=fetch)
         tick("graph")
     if phase_ms is not None:
         for (_, a), (name, b) in zip(marks, marks[1:]):
@@ -279,11 +283,11 @@ class ShardedAssembler:
         self.result = None
         self.phase_ms = {}
 
-    def run(self, timing=False):
+    def run(self, timing=False, fetch=True):
         flags = eulerhip.EC_FLAG_TIMING if timing else 0
         self.result, self.total_positions = sharded_assemble(self.engine, self.comm, self.d_reads, self.d_off,
                                                              self.nreads, self.read_base, self.k, self.limit, flags,
-                                                             on_count=self._keep, phase_ms=self.phase_ms)
+                                                             on_count=self._keep, phase_ms=self.phase_ms, fetch=fetch)
         return self.result
 
     def _keep(self, st):

@@ -92,7 +92,7 @@ class FakeEngine:
         self.recs = out
         return self._bytes(out)
 
-    def assemble_from_solid(self, recs, k, flags=0):
+    def assemble_from_solid(self, recs, k, flags=0, fetch=True):
         cnt, first = {}, {}
         for r in self._recs(recs):
             if int(r["key"]) == M64:  # all-gather filler record (ec_assemble_from_solid skips it)
@@ -152,7 +152,7 @@ class FakeEngine:
         if part.size:
             out[: part.nbytes] = torch.from_numpy(part.view(np.uint8).copy())
 
-    def graph_finish(self, succ, k, flags=0):
+    def graph_finish(self, succ, k, flags=0, fetch=True):
         got = np.frombuffer(succ.numpy().tobytes(), dtype=np.uint32)[: 2 * len(self.grecs)]
         want = np.array([self._succ_of(x) for x in range(2 * len(self.grecs))], dtype=np.uint32)
         assert np.array_equal(got, want), "gathered successor parts differ from the whole-set links"

@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, reads, k, limit, q, partitioned=None):
+def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None):
     import torch
     import torch.distributed as dist
 
@@ -44,18 +44,19 @@ def _worker(rank, world, port, reads, k, limit, q, partitioned=None):
         off[1:] = np.cumsum([len(r) for r in mine])
         res, P = distributed.sharded_assemble(FakeEngine(k), distributed.TorchComm(),
                                               torch.frombuffer(bytearray(buf or b"\0"), dtype=torch.uint8),
-                                              torch.from_numpy(off), len(mine), lo, k, limit,
+                                              torch.from_numpy(off), len(mine), lo if gap is None else rank * gap,
+                                              k, limit,
                                               partitioned=partitioned)
         q.put((rank, P, res.contigs, res.links))
     finally:
         dist.destroy_process_group()
 
 
-def _run(reads, k, limit, world, partitioned=None):
+def _run(reads, k, limit, world, partitioned=None, gap=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q, partitioned))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q, partitioned, gap))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -84,6 +85,18 @@ def test_sharded_matches_oracle_synthetic():
     P_ref = sum(len(r) - 16 for r in reads)
     for rank, P, contigs, links in out:
         assert P == P_ref
+        assert contigs == rc and links == rl
+
+
+def test_sharded_weak_read_bases():
+    """bench.py's weak scaling: rank r's reads start at global read id r * gap (its own read
+    set, ids with gaps between the ranks); the dict order -- and so the contigs -- is that of
+    the ranks' reads concatenated in rank order"""
+    sets = [make_reads(2_500, 300, 60, 5252, err=0.003, part=r) for r in range(3)]
+    reads = [b[int(o[i]):int(o[i + 1])].tobytes().decode() for b, o in sets for i in range(len(o) - 1)]
+    _, rc, rl = oracle.assemble(reads, 19, 1, want_dict=False)
+    for rank, P, contigs, links in _run(reads, 19, 1, 3, gap=40_000_000):
+        assert P == sum(len(r) - 18 for r in reads)
         assert contigs == rc and links == rl
 
 
