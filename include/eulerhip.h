@@ -273,7 +273,9 @@ int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offs
 /* number of dense k-mer records the session holds (after ec_count_shard / ec_merge_owned) */
 uint64_t ec_dense_count(ec_session *s);
 /* pack the held records owner-major into d_out (ec_kmer_record[ec_dense_count]); owner_counts
- * (host, nowners <= 256) receives the records per owner.  d_out = NULL: counts only. */
+ * (host, nowners <= 256) receives the records per owner.  d_out = NULL: counts only.
+ * Owner of a canonical key: for 21 <= k <= 32 the range of its minimizer ((minimizer * nowners)
+ * >> 32, the merge / load bucket key), else a 64-bit hash of the key (shard.h OwnerFn). */
 int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts);
 /* owner side: aggregate received records, keep count > limit */
 int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags);

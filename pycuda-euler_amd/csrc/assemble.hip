@@ -202,7 +202,7 @@ struct Scalars {  // device scalars block
     unsigned int ndict;
     unsigned int nr;
     unsigned int npal;
-    unsigned int pad;
+    unsigned int ngath;  // phase_load_det: non-filler records of a gathered solid set
     unsigned long long nvisited;
     unsigned int maxlocal;
     unsigned int skew;
@@ -1144,8 +1144,18 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
 // loaded for phase_graph (limit = keep all).
 // The same on the LDS bucket tables of the fused path (k_bucket over the records sorted by
 // bucket): no HBM atomics.  Returns EC_OK with ok = false when a bucket overflows its table.
+// minimizer buckets for the merge / load of 21 <= k <= 32 (shard.h OwnerFn; EULERHIP_MERGE_MIX=1:
+// key-hash buckets and owners, the round-1 layout)
+bool merge_sk(int k) { return k >= SK_MIN_K && k <= 32 && !getenv("EULERHIP_MERGE_MIX"); }
+OwnerFn owner_fn(int k) {
+    OwnerFn f{};
+    f.sk = merge_sk(k) ? 1 : 0;
+    if (f.sk) f.mc = sk_cfg(k);
+    return f;
+}
+
 int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx,
-                     bool &ok, const unsigned int *ids = nullptr, unsigned int nids = 0) {
+                     bool &ok, const unsigned int *ids = nullptr, bool allow_sk = true) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -1156,6 +1166,8 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     if ((double)n / (double)(1ull << bbits) > 2200.0) return EC_OK;  // too large for the LDS tables
     const unsigned int nb = 1u << bbits;
     const unsigned int slots = (double)n / (double)nb > 1100.0 ? 4096u : 2048u;
+    OwnerFn own = owner_fn(s->k);  // minimizer buckets (own.sk) or key-hash buckets
+    if (!allow_sk) own.sk = 0;
     mark(s, 2 * EC_STAGE_COUNT);
     EC_CHECK(s->mbid.ensure(std::max<uint64_t>(n, 1) * 4));
     EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 1) * 4));
@@ -1165,7 +1177,7 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     EC_HIP(hipMemsetAsync(s->bstart.p, 0, (nb + 1ull) * 8, st));
     if (n) {
         k_agg_bucket_ids<<<grid_for(n, B), B, 0, st>>>(d_agg, n, bbits, s->mbid.as<unsigned int>(),
-                                                      s->midx.as<unsigned int>());
+                                                      s->midx.as<unsigned int>(), own.mc, own.sk);
         size_t bytes = 0;
         EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, s->mbid.as<unsigned int>(), s->mbid2.as<unsigned int>(),
                                          s->midx.as<unsigned int>(), s->midx2.as<unsigned int>(), n, 0, bbits + 1, st));
@@ -1187,11 +1199,12 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
     EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
     kmark(s, 2, 0);
+    const int sks = own.sk ? (slots == 2048 ? 11 : 12) : 0;
     if (ids) {  // gathered solid set: dense ids given (partitioned graph phase)
-        const AggDetSource src{d_agg, s->midx2.as<unsigned int>(), ids};
+        const AggDetSource src{d_agg, s->midx2.as<unsigned int>(), ids, sks};
         EC_CHECK(launch_bucket(s, src, nb, slots, limit));
     } else {
-        const AggSource src{d_agg, s->midx2.as<unsigned int>()};
+        const AggSource src{d_agg, s->midx2.as<unsigned int>(), sks};
         EC_CHECK(launch_bucket(s, src, nb, slots, limit));
     }
     kmark(s, 2, 1);
@@ -1203,8 +1216,9 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
         EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
         return EC_OK;
     }
-    U = ids ? nids : hsc.nsolid;
-    s->stats.n_distinct = ids ? nids : hsc.ndistinct;
+    U = ids ? hsc.ngath : hsc.nsolid;  // ids: the dense ids k_det_ids gave (their count in ngath)
+    s->stats.n_distinct = U;
+    if (!ids) s->stats.n_distinct = hsc.ndistinct;
     s->stats.n_solid = U;
     s->stats.count_path = EC_PATH_PARTITIONED;
     s->stats.n_buckets = nb;
@@ -1213,6 +1227,8 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     sidx.sub = s->sub.as<SubSlot>();
     sidx.bbits = bbits;
     sidx.slots = slots;
+    sidx.sk = own.sk;
+    if (own.sk) sidx.mc = own.mc;
     if (2ull * U >= (unsigned long long)CYC) {
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
@@ -1225,6 +1241,7 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
     if (!(s->flags & EC_FLAG_GENERAL)) {
         bool ok = false;
         EC_CHECK(phase_merge_part(s, d_agg, n, limit, U, sidx, ok));
+        if (!ok && merge_sk(s->k)) EC_CHECK(phase_merge_part(s, d_agg, n, limit, U, sidx, ok, nullptr, false));
         if (ok) return EC_OK;
     }
     hipStream_t st = s->stream;
@@ -1286,20 +1303,24 @@ int phase_load_det(ec_session *s, const Agg *d_agg, uint64_t n, unsigned int &U,
     EC_CHECK(s->rbc.ensure((size_t)nblk * 8));
     EC_CHECK(s->nextR.ensure(std::max<uint64_t>(n, 1) * 4));  // ids (nextR is free until the rank stage)
     unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk, *ids = s->nextR.as<unsigned int>();
-    unsigned int tot = 0;
+    // the id count stays on the device (dsc->ngath, read back with phase_merge_part's scalars):
+    // the dense arrays are sized for all n records, so no host round trip here
+    EC_HIP(hipMemsetAsync(&dsc->ngath, 0, 4, st));
     if (n) {
         k_det_count<Agg><<<nblk, 256, 0, st>>>(d_agg, n, bc);
         EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
         k_det_ids<Agg><<<nblk, 256, 0, st>>>(d_agg, n, bs, ids);
-        EC_HIP(hipMemcpyAsync(&tot, bs + nblk - 1, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_HIP(hipMemcpyAsync(&dsc->ngath, bs + nblk - 1, 4, hipMemcpyDeviceToDevice, st));
     }
-    EC_CHECK(s->dkey.ensure(std::max<uint64_t>(tot, 1) * 8));
-    EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(tot, 1) * 4));
-    EC_CHECK(s->dfc.ensure(std::max<uint64_t>(tot, 1) * 8));
-    EC_CHECK(s->dft.ensure(std::max<uint64_t>(tot, 1) * 8));
+    EC_CHECK(s->dkey.ensure(std::max<uint64_t>(n, 1) * 8));
+    EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(n, 1) * 4));
+    EC_CHECK(s->dfc.ensure(std::max<uint64_t>(n, 1) * 8));
+    EC_CHECK(s->dft.ensure(std::max<uint64_t>(n, 1) * 8));
     bool ok = false;
-    EC_CHECK(phase_merge_part(s, d_agg, n, LLONG_MIN, U, sidx, ok, ids, tot));
+    EC_CHECK(phase_merge_part(s, d_agg, n, LLONG_MIN, U, sidx, ok, ids));
+    // a minimizer bucket past its table (low-complexity sequence: many keys, one minimizer):
+    // key-hash buckets instead
+    if (!ok && merge_sk(s->k)) EC_CHECK(phase_merge_part(s, d_agg, n, LLONG_MIN, U, sidx, ok, ids, false));
     if (!ok) {
         set_error("gathered solid set of %llu records does not fit the bucketed index", (unsigned long long)n);
         return EC_ERR_CAPACITY;
@@ -2079,34 +2100,42 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
     hipStream_t st = s->stream;
     const unsigned B = 256;
     const unsigned int n = s->n_dense;
-    EC_CHECK(s->ocnt.ensure(2 * MAX_OWNERS * 8));
-    unsigned long long *cnt = s->ocnt.as<unsigned long long>(), *cur = cnt + MAX_OWNERS;
-    EC_HIP(hipMemsetAsync(cnt, 0, MAX_OWNERS * 8, st));
+    const unsigned int nblk = (unsigned int)std::max<uint64_t>((n + OWN_CHUNK - 1) / OWN_CHUNK, 1);
+    const size_t nbh = (size_t)nowners * nblk;
+    EC_CHECK(s->ocnt.ensure(2 * nbh * 4));
+    unsigned int *bh = s->ocnt.as<unsigned int>(), *bhi = bh + nbh;
     const bool wide = s->k > 32;
-    if (n && wide) k_owner_hist<K128><<<grid_for(n, B, 2048), B, 0, st>>>(s->dkey.as<K128>(), n, nowners, cnt);
-    if (n && !wide)
-        k_owner_hist<unsigned long long><<<grid_for(n, B, 2048), B, 0, st>>>(s->dkey.as<unsigned long long>(), n,
-                                                                            nowners, cnt);
-    std::vector<unsigned long long> h(nowners), o(nowners);
-    EC_HIP(hipMemcpyAsync(h.data(), cnt, nowners * 8, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
-    unsigned long long acc = 0;
-    for (int i = 0; i < nowners; i++) {
-        o[i] = acc;
-        acc += h[i];
-        owner_counts[i] = h[i];
-    }
-    if (n && d_out) {
-        EC_HIP(hipMemcpyAsync(cur, o.data(), nowners * 8, hipMemcpyHostToDevice, st));
+    std::vector<unsigned int> hi(nbh, 0u);
+    const OwnerFn own = owner_fn(s->k);
+    EC_CHECK(s->mbid.ensure(std::max<uint64_t>(n, 1) * 4));  // owner of each record (free until a merge)
+    unsigned int *oid = s->mbid.as<unsigned int>();
+    if (n) {
         if (wide)
-            k_owner_scatter<K128><<<grid_for(n, B, 4096), B, 0, st>>>(
-                s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<AggW *>(d_out), s->shard_base << 32);
+            k_owner_hist<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), n, nowners, nblk, bh, own, oid);
         else
-            k_owner_scatter<unsigned long long><<<grid_for(n, B, 4096), B, 0, st>>>(
+            k_owner_hist<unsigned long long><<<nblk, B, 0, st>>>(s->dkey.as<unsigned long long>(), n, nowners, nblk, bh,
+                                                                own, oid);
+        EC_CHECK(scan_incl_u32(s, bh, bhi, nbh));
+        EC_HIP(hipMemcpyAsync(hi.data(), bhi, nbh * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (n && d_out) {  // the scatter is queued before the host waits for the owner counts
+        if (wide)
+            k_owner_scatter<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), s->dcnt.as<unsigned int>(),
+                                                      s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                      n, nowners, nblk, bhi, reinterpret_cast<AggW *>(d_out),
+                                                      s->shard_base << 32, oid);
+        else
+            k_owner_scatter<unsigned long long><<<nblk, B, 0, st>>>(
                 s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), n, nowners, cur, reinterpret_cast<Agg *>(d_out), s->shard_base << 32);
-        EC_HIP(hipStreamSynchronize(st));
+                s->dft.as<unsigned long long>(), n, nowners, nblk, bhi, reinterpret_cast<Agg *>(d_out),
+                s->shard_base << 32, oid);
+    }
+    EC_HIP(hipStreamSynchronize(st));
+    unsigned long long prev = 0;
+    for (int i = 0; i < nowners; i++) {
+        const unsigned long long end = n ? hi[(size_t)(i + 1) * nblk - 1] : 0ull;
+        owner_counts[i] = end - prev;
+        prev = end;
     }
     return EC_OK;
 }

@@ -29,6 +29,21 @@ constexpr int MAX_OWNERS = 256;
 
 __device__ inline unsigned int owner_of(const K128 &c, unsigned int nowners) { return owner_of_w(c, nowners); }
 
+// The owner rule of the exchange.  For SK_MIN_K <= k <= 32 a key's owner is the range of its
+// minimizer (superkmer.h minimizer_of, uniform 32 bits after min_remix), and the merge and the
+// gathered-set load bucket keys by the same minimizer (SolidIndex::sk): an owner's merged set
+// -- and so its segment of the gathered dense ids -- comes out in bucket order, a node's
+// neighbours mostly share its bucket, and the partitioned links / ranking touch the lookup
+// sub-tables and node arrays with the locality of the one-GPU path.  Other k: a key hash.
+struct OwnerFn {
+    MinCfg mc;
+    int sk;
+    __device__ inline unsigned int operator()(unsigned long long key, unsigned int n) const {
+        return sk ? (unsigned int)(((uint64_t)minimizer_of(key, mc) * n) >> 32) : owner_of(key, n);
+    }
+    __device__ inline unsigned int operator()(const K128 &key, unsigned int n) const { return owner_of(key, n); }
+};
+
 // the exchange record of a key type: Agg (64-bit keys) or AggW (K128)
 template <typename K> struct RecOf;
 template <> struct RecOf<unsigned long long> {
@@ -58,48 +73,55 @@ template <> struct RecOf<K128> {
     }
 };
 
+// Owner-major export in two passes without global atomics (a cursor per owner hit by every
+// block serialised at the memory side: 223 us for 4.6 M records at one owner).
+// Chunk b = records [b OWN_CHUNK, (b + 1) OWN_CHUNK): bh[o * nblk + b] = its records of owner o;
+// after an inclusive scan of bh (owner-major) chunk b's owner-o records start at
+// bh_incl[o * nblk + b - 1] -- the owner's offset in the export included.
+constexpr unsigned int OWN_CHUNK = 8192;
+
 template <typename K>
 __global__ void __launch_bounds__(256) k_owner_hist(const K *dkey, unsigned int n, unsigned int nowners,
-                                                    unsigned long long *cnt) {
+                                                    unsigned int nblk, unsigned int *bh, OwnerFn own,
+                                                    unsigned int *oid) {
     __shared__ unsigned int h[MAX_OWNERS];
     for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
-        atomicAdd(&h[owner_of(dkey[t], nowners)], 1u);
+    const uint64_t c0 = (uint64_t)blockIdx.x * OWN_CHUNK, c1 = min<uint64_t>(c0 + OWN_CHUNK, n);
+    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+        const unsigned int o = own(dkey[t], nowners);  // kept for the scatter (a minimizer is ~250 VALU)
+        oid[t] = o;
+        atomicAdd(&h[o], 1u);
+    }
     __syncthreads();
-    for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x)
-        if (h[i]) atomicAdd(&cnt[i], (unsigned long long)h[i]);
+    for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) bh[(uint64_t)i * nblk + blockIdx.x] = h[i];
 }
 
-// scatter dense records into owner-major order; cursor[o] starts at the owner's offset;
-// evbase = the shard's first global read id << 32 (ec_count_shard counts shard-relative)
+// scatter dense records into owner-major order at the scanned chunk bases (owners from
+// k_owner_hist's oid); evbase = the
+// shard's first global read id << 32 (ec_count_shard counts shard-relative)
 template <typename K>
 __global__ void __launch_bounds__(256) k_owner_scatter(const K *dkey, const unsigned int *dcnt,
                                                        const unsigned long long *dfc, const unsigned long long *dft,
-                                                       unsigned int n, unsigned int nowners,
-                                                       unsigned long long *cursor, typename RecOf<K>::T *out,
-                                                       unsigned long long evbase) {
+                                                       unsigned int n, unsigned int nowners, unsigned int nblk,
+                                                       const unsigned int *bh_incl, typename RecOf<K>::T *out,
+                                                       unsigned long long evbase, const unsigned int *oid) {
     __shared__ unsigned int h[MAX_OWNERS];
-    __shared__ unsigned long long base[MAX_OWNERS];
-    for (uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x; t0 < n; t0 += (uint64_t)gridDim.x * blockDim.x) {
-        for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) h[i] = 0;
-        __syncthreads();
-        const uint64_t t = t0 + threadIdx.x;
-        unsigned int o = 0, rk = 0;
-        if (t < n) {
-            o = owner_of(dkey[t], nowners);
-            rk = atomicAdd(&h[o], 1u);
-        }
-        __syncthreads();
-        for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x)
-            base[i] = h[i] ? atomicAdd(&cursor[i], (unsigned long long)h[i]) : 0ull;
-        __syncthreads();
-        if (t < n) {  // shard-relative first events -> global (NONE64 = no event, kept)
-            const unsigned long long fc = dfc[t], ft = dft[t];
-            out[base[o] + rk] = RecOf<K>::make(dkey[t], dcnt[t], fc == NONE64 ? fc : fc + evbase,
-                                               ft == NONE64 ? ft : ft + evbase);
-        }
-        __syncthreads();
+    __shared__ unsigned int base[MAX_OWNERS];
+    for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) {
+        const uint64_t j = (uint64_t)i * nblk + blockIdx.x;
+        h[i] = 0;
+        base[i] = j ? bh_incl[j - 1] : 0u;
+    }
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * OWN_CHUNK, c1 = min<uint64_t>(c0 + OWN_CHUNK, n);
+    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+        const K key = dkey[t];
+        const unsigned int o = oid[t];
+        const unsigned int rk = atomicAdd(&h[o], 1u);
+        // shard-relative first events -> global (NONE64 = no event, kept)
+        const unsigned long long fc = dfc[t], ft = dft[t];
+        out[base[o] + rk] = RecOf<K>::make(key, dcnt[t], fc == NONE64 ? fc : fc + evbase, ft == NONE64 ? ft : ft + evbase);
     }
 }
 
@@ -143,12 +165,15 @@ __global__ void __launch_bounds__(256) k_export_dense(const K *dkey, const unsig
 
 // ---- bucketed merge: exchange records -> LDS bucket tables (k_bucket over AggSource) -------
 // bucket id = top bbits of mix64(key) (the fused path's bucket hash, so the SolidIndex
-// sub-table layout is shared); filler records (all-ones key) go to bucket 2^bbits, past the end.
+// sub-table layout is shared), or with sk the top bbits of the key's minimizer (OwnerFn);
+// filler records (all-ones key) go to bucket 2^bbits, past the end.
 __global__ void __launch_bounds__(256) k_agg_bucket_ids(const Agg *in, uint64_t n, int bbits, unsigned int *bid,
-                                                        unsigned int *idx) {
+                                                        unsigned int *idx, MinCfg mc, int sk) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned long long key = in[t].key;
-        bid[t] = key == EMPTY_KEY ? (1u << bbits) : (bbits ? (unsigned int)(mix64(key) >> (64 - bbits)) : 0u);
+        bid[t] = key == EMPTY_KEY ? (1u << bbits)
+                 : sk             ? sk_bucket_of(minimizer_of(key, mc), bbits)
+                                  : (bbits ? (unsigned int)(mix64(key) >> (64 - bbits)) : 0u);
         idx[t] = (unsigned int)t;
     }
 }
@@ -164,10 +189,20 @@ __global__ void __launch_bounds__(256) k_bucket_bounds(const unsigned int *sbid,
     }
 }
 
+// first probe slot in the bucket table: mix64 (sks = 0) or, for minimizer buckets, the top sks
+// bits of sk_slot (SolidIndex::slot0 with sk = 1, slots = 2^sks)
+#define EC_AGG_SOURCE                                                                               \
+    __device__ inline void seg(uint32_t, uint32_t) {}                                                \
+    __device__ inline unsigned long long key_out(unsigned long long c) const { return c; }           \
+    __device__ inline uint64_t slot_hash(unsigned long long c) const {                               \
+        return sks ? (uint64_t)(sk_slot(c) >> (32 - sks)) : mix64(c);                                \
+    }
+
 struct AggSource {
-    EC_PLAIN_SOURCE
+    EC_AGG_SOURCE
     const Agg *in;
     const unsigned int *perm;
+    int sks;
     using Raw = Agg;
     static constexpr bool kDet = false;
     __device__ inline Raw fetch(uint64_t i) const { return in[perm[i]]; }
@@ -191,10 +226,11 @@ struct AggDet {
     unsigned int id;
 };
 struct AggDetSource {
-    EC_PLAIN_SOURCE
+    EC_AGG_SOURCE
     const Agg *in;
     const unsigned int *perm;
     const unsigned int *ids;  // dense id of each record (NONE for fillers, which sort past the end)
+    int sks;
     using Raw = AggDet;
     static constexpr bool kDet = true;
     __device__ inline Raw fetch(uint64_t i) const {

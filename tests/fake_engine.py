@@ -3,7 +3,7 @@
 Lets tests drive the real multi-rank orchestration (distributed.sharded_assemble, TorchComm)
 over the gloo backend on CPU.  Its compute comes from the design model (model_parallel.py),
 which is pinned to the reference's golden vectors; the record layout and the owner function
-are the device ones (ec_kmer_record, shard.h owner_of), so the exchange is byte-identical.
+are the device ones (ec_kmer_record, shard.h OwnerFn), so the exchange is byte-identical.
 """
 import numpy as np
 import torch
@@ -16,17 +16,56 @@ CODE = {"A": 0, "C": 1, "G": 2, "T": 3}
 
 
 def mix64(x):
+    """common.h mix64"""
     x &= M64
-    x ^= x >> 33
-    x = (x * 0xff51afd7ed558ccd) & M64
-    x ^= x >> 33
-    x = (x * 0xc4ceb9fe1a85ec53) & M64
-    x ^= x >> 33
+    x ^= x >> 29
+    x = (x * 0xbf58476d1ce4e5b9) & M64
+    x ^= x >> 32
     return x
 
 
 def owner_of(key, n):
     return ((mix64(key ^ 0xD6E8FEB86659FD93) >> 32) * n) >> 32
+
+
+M32 = (1 << 32) - 1
+
+
+def _rev2_32(x):
+    x = ((x >> 2) & 0x33333333) | ((x & 0x33333333) << 2)
+    x = ((x >> 4) & 0x0F0F0F0F) | ((x & 0x0F0F0F0F) << 4)
+    return ((x >> 24) | ((x >> 8) & 0xFF00) | ((x << 8) & 0xFF0000) | (x << 24)) & M32
+
+
+def _mmer_hash(x):
+    x = (x * 0x9E3779B1) & M32
+    return x ^ (x >> 15)
+
+
+def _min_remix(x):
+    x ^= 0x5BD1E995
+    x = (x * 0x2C1B3C6D) & M32
+    x ^= x >> 12
+    x = (x * 0x297A2D39) & M32
+    return x ^ (x >> 15)
+
+
+def minimizer_of(c, k, m=15):
+    """superkmer.h minimizer_of: min over the k-m+1 canonical m-mers of mmer_hash, remixed"""
+    mm = (1 << (2 * m)) - 1
+    v = M32
+    for p in range(k - m + 1):
+        f = (c >> (2 * (k - m - p))) & mm
+        r = _rev2_32(f ^ mm) >> (32 - 2 * m)
+        v = min(v, _mmer_hash(min(f, r)))
+    return _min_remix(v)
+
+
+def owner_fn(key, n, k):
+    """shard.h OwnerFn: the minimizer's range for 21 <= k <= 32, else the key hash"""
+    if 21 <= k <= 32:
+        return (minimizer_of(key, k) * n) >> 32
+    return owner_of(key, n)
 
 
 def encode(s):
@@ -74,7 +113,7 @@ class FakeEngine:
         return _Stats(P)
 
     def export_by_owner(self, nowners):
-        own = np.array([owner_of(int(x), nowners) for x in self.recs["key"]], dtype=np.int64)
+        own = np.array([owner_fn(int(x), nowners, self.k) for x in self.recs["key"]], dtype=np.int64)
         order = np.argsort(own, kind="stable")
         counts = [int((own == o).sum()) for o in range(nowners)]
         return self._bytes(self.recs[order]), counts

@@ -195,3 +195,53 @@ def test_weak_shards_large_read_base(engines, k):
     assert P == ref["n_positions"]
     assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
     assert res.stats.n_dict == ref["n_dict"]
+
+
+@pytest.mark.parametrize("k", [31, 21, 19, 41])
+def test_owner_rule_matches_fake_engine(engines, k):
+    """ec_export_by_owner puts every record in the segment of shard.h OwnerFn's owner -- the
+    minimizer's range for 21 <= k <= 32, a key hash otherwise -- as tests/fake_engine.py
+    restates it for the gloo tests"""
+    import torch
+
+    import distributed
+    from fake_engine import owner_fn
+
+    buf, off = make_reads(5_000, 1_500, 100, 7801)
+    eng = engines[0]
+    eng.count_shard(torch.from_numpy(buf).cuda(), torch.from_numpy(off.astype(np.int64)).cuda(), len(off) - 1, 0, k, 0)
+    recs, counts = eng.export_by_owner(5)
+    rb = distributed.rec_bytes(k)
+    raw = recs.cpu().numpy()
+    o = 0
+    for dst, c in enumerate(counts):
+        for i in range(o, o + c):
+            if k <= 32:
+                key = int(raw[i * rb: i * rb + 8].view(np.uint64)[0])
+                assert owner_fn(key, 5, k) == dst
+        o += c
+    assert o * rb == raw.size
+
+
+def test_sharded_minimizer_skew_falls_back(engines):
+    """~25 K distinct 31-mers share one minimizer (poly-A 15-mers, whose hash is the smallest
+    possible): the minimizer-bucketed merge / load overflow that bucket's table and redo the
+    call on key-hash buckets; the result still equals the oracle"""
+    import distributed
+
+    rng = np.random.Generator(np.random.PCG64(7901))
+    parts = []
+    for _ in range(1_500):
+        parts.append(rng.integers(0, 4, 35, dtype=np.uint8))
+        parts.append(np.zeros(15, np.uint8))
+    g = np.concatenate(parts)
+    L, n = 100, 30_000
+    starts = rng.integers(0, len(g) - L + 1, n)
+    reads = np.frombuffer(b"ACGT", np.uint8)[g[starts[:, None] + np.arange(L)[None, :]]]
+    buf = reads.reshape(-1).copy()
+    off = np.arange(n + 1, dtype=np.uint64) * np.uint64(L)
+    ref = oracle.assemble_packed(buf, off, 31, 1)
+    for world in (1, 2):
+        res, P = distributed.local_sharded_assemble(engines[:world], buf, off, 31, 1)
+        assert P == ref["n_positions"]
+        assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
