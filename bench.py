@@ -199,9 +199,8 @@ def main():
         torch.cuda.synchronize()
         sess = eulerhip.Session(local, stream=torch.cuda.current_stream().cuda_stream)
 
-        def step(timing=False):
-            sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), cfg["reads"], k, 1,
-                            (eulerhip.EC_FLAG_TIMING if timing else 0)
+        def step(timing=0):
+            sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), cfg["reads"], k, 1, timing
                             | (eulerhip.EC_FLAG_WIDE_RECORDS if args.wide_records else 0)
                             | (eulerhip.EC_FLAG_WINDOW_RECORDS if args.window_records else 0)
                             | (eulerhip.EC_FLAG_SUPERKMER if args.superkmer else 0))
@@ -211,23 +210,24 @@ def main():
         runner = distributed.ShardedAssembler(buf, off, k, 1, rank, world, local,
                                               read_base=(rank * cfg["reads"] if weak else None))
 
-        def step(timing=False):  # results left in the session's pinned buffers, as run_device leaves them
+        def step(timing=0):  # results left in the session's pinned buffers, as run_device leaves them
             runner.run(timing, fetch=False)
 
+    # timed steps record the kernel events only (EC_FLAG_KERNEL_TIMING: the roofline's kernel
+    # durations, live over the timed region); the stage breakdown (EC_FLAG_TIMING, ~26 events
+    # a call, ~0.1 ms) comes from one untimed step after it
     for _ in range(args.warmup):
-        step(True)
+        step(eulerhip.EC_FLAG_TIMING)
     if use_dist:
         runner.phase_ms = {}  # per-phase times of the timed steps only
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    stage = np.zeros(eulerhip.EC_NSTAGES)
     kern = np.zeros(eulerhip.EC_NKERNELS)
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step(eulerhip.EC_FLAG_KERNEL_TIMING)
         st = sess.stats() if not use_dist else runner.stats()
-        stage += np.array(list(st.stage_ms))
         kern += np.array(list(st.kernel_ms))
     torch.cuda.synchronize()
     if dist:
@@ -238,6 +238,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
+    timed_phase_ms = dict(runner.phase_ms) if use_dist else None
+    step(eulerhip.EC_FLAG_TIMING)  # untimed (every rank: it has collectives): the per-stage breakdown
+    stage = np.array(list((sess.stats() if not use_dist else runner.stats()).stage_ms))
     st = sess.stats() if not use_dist else runner.stats()
     P = int(st.n_positions) if not use_dist else runner.total_positions
     U = int(st.n_solid) if not use_dist else int(runner.engine.stats().n_solid)
@@ -252,7 +255,7 @@ def main():
     kern /= args.steps
     sharded_ms = None
     if use_dist:
-        sharded_ms = {kk: round(v / args.steps, 3) for kk, v in runner.phase_ms.items()}
+        sharded_ms = {kk: round(v / args.steps, 3) for kk, v in timed_phase_ms.items()}
     kid = int(np.argmax(kern))
     kname = eulerhip.KERNEL_NAMES[kid]  # slot name (kernel_alg_bytes); reported by its variant name
     variant = int(getattr(st, "count_variant", 0))
@@ -303,7 +306,7 @@ def main():
                    "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
         "roofline": roof,
         "cpu_baseline": cpu,
-        "stage_ms": {names[i]: round(stage[i] / args.steps, 3) for i in range(len(names))},
+        "stage_ms": {names[i]: round(stage[i], 3) for i in range(len(names))},
         "sharded_phase_ms": sharded_ms,
     }
     print(json.dumps(out), file=json_out, flush=True)

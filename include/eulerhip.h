@@ -47,7 +47,9 @@ int ec_version(void); /* major*10000 + minor*100 + patch */
 typedef struct ec_session ec_session;
 
 #define EC_FLAG_WANT_DICT 1u /* also keep build()'s ordered dict for ec_copy_dict */
-#define EC_FLAG_TIMING 2u    /* record per-stage HIP-event times (ec_stats.stage_ms) */
+#define EC_FLAG_TIMING 2u    /* record per-stage and per-kernel HIP-event times (stage_ms, kernel_ms) */
+#define EC_FLAG_KERNEL_TIMING 128u /* per-kernel HIP-event times only (kernel_ms): 6-10 events a call
+                                     * instead of ~26, for timed benchmark steps */
 #define EC_FLAG_GENERAL 4u   /* force the general (single HBM hash table) counting path */
 #define EC_FLAG_WIDE_RECORDS 8u /* partitioned path: 16-B window records only (default for k < 21 or
                                   * reads with N: 12-B records when every read is N-free and of one length) */
@@ -110,7 +112,7 @@ typedef struct {
                               * (count_sk2.h; the default for N-free reads of one length,
                               * 21 <= k <= 32, inputs that need no seen-twice filter)          */
     float stage_ms[EC_NSTAGES];   /* EC_FLAG_TIMING only */
-    float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING only */
+    float kernel_ms[EC_NKERNELS]; /* EC_FLAG_TIMING or EC_FLAG_KERNEL_TIMING */
 } ec_stats;
 
 int ec_session_create(ec_session **out, int device);

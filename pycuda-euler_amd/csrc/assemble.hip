@@ -140,7 +140,8 @@ struct ec_session {
     bool kused[EC_NKERNELS] = {};
     bool sused[EC_NSTAGES] = {};
     bool events = false;
-    bool timing = false;
+    bool timing = false;        // kernel events (EC_FLAG_TIMING or EC_FLAG_KERNEL_TIMING)
+    bool stage_timing = false;  // stage events (EC_FLAG_TIMING)
     unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
     unsigned flags = 0;        // flags of the current call
@@ -237,7 +238,7 @@ int sort_pairs(ec_session *s, unsigned long long *kin, unsigned long long *kout,
 }
 
 inline void mark(ec_session *s, int idx) {
-    if (s->timing) {
+    if (s->stage_timing) {
         hipEventRecord(s->ev[idx], s->stream);
         if (idx & 1) s->sused[idx >> 1] = true;
     }
@@ -256,7 +257,7 @@ void collect_timing(ec_session *s) {
     hipStreamSynchronize(s->stream);
     for (int i = 0; i < EC_NSTAGES; i++) {
         float ms = 0;
-        if (s->sused[i]) hipEventElapsedTime(&ms, s->ev[2 * i], s->ev[2 * i + 1]);
+        if (s->stage_timing && s->sused[i]) hipEventElapsedTime(&ms, s->ev[2 * i], s->ev[2 * i + 1]);
         s->stats.stage_ms[i] = ms;
     }
     for (int i = 0; i < EC_NKERNELS; i++) {
@@ -281,7 +282,8 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     s->want_dict = (flags & EC_FLAG_WANT_DICT) != 0;
     s->flags = flags;
     s->shard_base = 0;
-    const bool timing = (flags & EC_FLAG_TIMING) != 0;
+    const bool timing = (flags & (EC_FLAG_TIMING | EC_FLAG_KERNEL_TIMING)) != 0;
+    s->stage_timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
         for (auto &e : s->ev) EC_HIP(hipEventCreate(&e));
         for (auto &e : s->kev) EC_HIP(hipEventCreate(&e));

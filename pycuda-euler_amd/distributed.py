@@ -284,7 +284,8 @@ class ShardedAssembler:
         self.phase_ms = {}
 
     def run(self, timing=False, fetch=True):
-        flags = eulerhip.EC_FLAG_TIMING if timing else 0
+        """timing: True = EC_FLAG_TIMING, or the timing flag bits to pass (EC_FLAG_KERNEL_TIMING)"""
+        flags = eulerhip.EC_FLAG_TIMING if timing is True else int(timing or 0)
         self.result, self.total_positions = sharded_assemble(self.engine, self.comm, self.d_reads, self.d_off,
                                                              self.nreads, self.read_base, self.k, self.limit, flags,
                                                              on_count=self._keep, phase_ms=self.phase_ms, fetch=fetch)

@@ -29,7 +29,7 @@ if HERE not in sys.path:
 def main(argv=None):
     ap = argparse.ArgumentParser(description="MI355X de Bruijn unitig assembler")
     ap.add_argument("-i", "--input", required=True, help="FASTA / FASTQ read file")
-    ap.add_argument("-k", type=int, default=31, help="k-mer (node) length, 1..32")
+    ap.add_argument("-k", type=int, default=31, help="k-mer (node) length, 1..63")
     ap.add_argument("--limit", type=int, default=1, help="keep k-mers seen more than this many times")
     ap.add_argument("-o", "--output", default="", help="contig FASTA ('>contig%%d' records)")
     ap.add_argument("--gfa", default="", help="GFA 1 output")

@@ -30,6 +30,7 @@ EC_ERR_STATE = -6
 
 EC_FLAG_WANT_DICT = 1
 EC_FLAG_TIMING = 2
+EC_FLAG_KERNEL_TIMING = 128  # kernel_ms only (fewer events: bench.py's timed steps)
 EC_FLAG_GENERAL = 4
 EC_FLAG_WIDE_RECORDS = 8
 EC_FLAG_WINDOW_RECORDS = 16
