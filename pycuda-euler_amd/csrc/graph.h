@@ -57,22 +57,27 @@ struct SolidIndex {
         return lookup(table, capmask, c);
     }
     // successors of oriented k-mer xs (k-mers xs << 2 | b): on the super-k-mer path their
-    // minimizers share the w - 1 m-mers of xs's last k - 1 bases
+    // minimizers share the w - 1 m-mers of xs's last k - 1 bases.  txs = twin(xs): the reverse
+    // complement of xs's m-mer p is txs's m-mer at offset p from the end (no per-m-mer reversal)
     struct Nb {
         uint32_t part;
     };
-    __device__ inline Nb nb_begin(uint64_t xs) const {
+    __device__ inline Nb nb_begin(uint64_t xs, uint64_t txs) const {
         Nb nb{0xFFFFFFFFu};
         if (sub && sk)
             for (int p = 1; p < mc.w; p++) {
-                const uint32_t h = mmer_canon_hash((uint32_t)(xs >> (2 * (mc.k - mc.m - p))) & mc.mmask, mc);
+                const uint32_t f = (uint32_t)(xs >> (2 * (mc.k - mc.m - p))) & mc.mmask;
+                const uint32_t r = (uint32_t)(txs >> (2 * p)) & mc.mmask;
+                const uint32_t h = mmer_hash(f < r ? f : r);
                 nb.part = h < nb.part ? h : nb.part;
             }
         return nb;
     }
-    __device__ inline unsigned int find_nb(const Nb &nb, uint64_t y, uint64_t cy) const {
+    // successor y = xs << 2 | b, ty = twin(y), cy = canonical
+    __device__ inline unsigned int find_nb(const Nb &nb, uint64_t y, uint64_t ty, uint64_t cy) const {
         if (sub && sk) {
-            const uint32_t h = mmer_canon_hash((uint32_t)y & mc.mmask, mc);
+            const uint32_t f = (uint32_t)y & mc.mmask, r = (uint32_t)(ty >> (2 * (mc.k - mc.m))) & mc.mmask;
+            const uint32_t h = mmer_hash(f < r ? f : r);
             return find_in(cy, slot0(cy), sk_bucket_of(min_remix(h < nb.part ? h : nb.part), bbits));
         }
         return find(cy);
@@ -128,8 +133,10 @@ struct SolidIndexW {
         return NONE32;
     }
     struct Nb {};
-    __device__ inline Nb nb_begin(const K128 &) const { return Nb{}; }
-    __device__ inline unsigned int find_nb(const Nb &, const K128 &, const K128 &cy) const { return find(cy); }
+    __device__ inline Nb nb_begin(const K128 &, const K128 &) const { return Nb{}; }
+    __device__ inline unsigned int find_nb(const Nb &, const K128 &, const K128 &, const K128 &cy) const {
+        return find(cy);
+    }
 };
 
 // oriented node id: 2u + o (o = 1: twin of the canonical string); palindromes use o = 0 only
@@ -166,12 +173,12 @@ __global__ void __launch_bounds__(256) k_neighbors(Index idx, const typename Ops
         }
         const K xs = (x & 1) ? tc : c, txs = (x & 1) ? c : tc;
         unsigned int n = 0, cd = NONE32;
-        const typename Index::Nb nb = idx.nb_begin(xs);
+        const typename Index::Nb nb = idx.nb_begin(xs, txs);
         for (uint32_t b = 0; b < 4; b++) {
             const K y = Ops::push(xs, b, mask);
             const K ty = Ops::twin_push(txs, b, k);
             const K cy = y < ty ? y : ty;
-            const unsigned int u = idx.find_nb(nb, y, cy);
+            const unsigned int u = idx.find_nb(nb, y, ty, cy);
             if (u != NONE32) {
                 if (n == 0) cd = 2 * u + (y != cy ? 1u : 0u);
                 n++;
@@ -218,12 +225,12 @@ __global__ void __launch_bounds__(256) k_links_part(Index idx, const typename Op
         if (!((x & 1) && pal)) {
             const K xs = (x & 1) ? tc : c, txs = (x & 1) ? c : tc;
             unsigned int nfw = 0, cd = NONE32;
-            const typename Index::Nb nb = idx.nb_begin(xs);
+            const typename Index::Nb nb = idx.nb_begin(xs, txs);
             for (uint32_t b = 0; b < 4; b++) {
                 const K y = Ops::push(xs, b, mask);
                 const K ty = Ops::twin_push(txs, b, k);
                 const K cy = y < ty ? y : ty;
-                const unsigned int u = idx.find_nb(nb, y, cy);
+                const unsigned int u = idx.find_nb(nb, y, ty, cy);
                 if (u != NONE32) {
                     if (nfw == 0) cd = 2 * u + (y != cy ? 1u : 0u);
                     nfw++;
@@ -236,12 +243,12 @@ __global__ void __launch_bounds__(256) k_links_part(Index idx, const typename Op
                 const unsigned int tyn = yt == yc ? cd : (cd ^ 1u);  // twin node of the candidate
                 const K tys = (tyn & 1) ? yt : yc, ttys = (tyn & 1) ? yc : yt;
                 unsigned int nin = 0;
-                const typename Index::Nb nb2 = idx.nb_begin(tys);
+                const typename Index::Nb nb2 = idx.nb_begin(tys, ttys);
                 for (uint32_t b = 0; b < 4; b++) {
                     const K z = Ops::push(tys, b, mask);
                     const K tz = Ops::twin_push(ttys, b, k);
                     const K cz = z < tz ? z : tz;
-                    nin += idx.find_nb(nb2, z, cz) != NONE32;
+                    nin += idx.find_nb(nb2, z, tz, cz) != NONE32;
                 }
                 if (nin == 1) s = cd;
             }

@@ -86,11 +86,17 @@ __host__ __device__ inline uint32_t mmer_canon_hash(uint32_t f, const MinCfg &g)
     return mmer_hash(f < r ? f : r);
 }
 
-// minimizer of k-mer code c (the graph phase's bucket of a key)
+// minimizer of k-mer code c (the graph phase's bucket of a key, the sharded path's owner):
+// the twin's m-mer at offset p is the reverse complement of c's m-mer p, so one 64-bit
+// reversal replaces a 32-bit one per m-mer (= mmer_canon_hash of every m-mer; the
+// minimizer pass over 4.6 M keys of the sharded export 87 -> see DESIGN.md 6)
 __host__ __device__ inline uint32_t minimizer_of(uint64_t c, const MinCfg &g) {
+    const uint64_t tc = twin64(c, g.k);
     uint32_t v = 0xFFFFFFFFu;
     for (int p = 0; p < g.w; p++) {
-        const uint32_t h = mmer_canon_hash((uint32_t)(c >> (2 * (g.k - g.m - p))) & g.mmask, g);
+        const uint32_t f = (uint32_t)(c >> (2 * (g.k - g.m - p))) & g.mmask;
+        const uint32_t r = (uint32_t)(tc >> (2 * p)) & g.mmask;
+        const uint32_t h = mmer_hash(f < r ? f : r);
         v = h < v ? h : v;
     }
     return min_remix(v);
