@@ -88,8 +88,7 @@ __host__ __device__ inline uint32_t mmer_canon_hash(uint32_t f, const MinCfg &g)
 
 // minimizer of k-mer code c (the graph phase's bucket of a key, the sharded path's owner):
 // the twin's m-mer at offset p is the reverse complement of c's m-mer p, so one 64-bit
-// reversal replaces a 32-bit one per m-mer (= mmer_canon_hash of every m-mer; the
-// minimizer pass over 4.6 M keys of the sharded export 87 -> see DESIGN.md 6)
+// reversal replaces a 32-bit one per m-mer (= mmer_canon_hash of every m-mer)
 __host__ __device__ inline uint32_t minimizer_of(uint64_t c, const MinCfg &g) {
     const uint64_t tc = twin64(c, g.k);
     uint32_t v = 0xFFFFFFFFu;
