@@ -283,6 +283,10 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
 int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags);
 /* copy the held records (ec_merge_owned's solid set) to d_out */
 int ec_export_dense(ec_session *s, void *d_out);
+/* ec_merge_owned + ec_export_dense in one call (no host round trip between them); d_out holds
+ * up to n records, ec_dense_count gives how many were written */
+int ec_merge_owned_export(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags,
+                          void *d_out);
 /* all_contigs(d, k) (referenceAssembler.py:79-111) on a caller's dict: n entries of k
  * characters (ACGT) in dict order with their counts; the dict must hold every k-mer together
  * with its twin, as build() returns it.  Results via ec_copy_contigs / ec_copy_links. */
@@ -303,6 +307,9 @@ int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int
  * links, then ranking .. GFA as ec_assemble_from_solid; results via ec_copy_*. */
 int ec_graph_load(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags);
 int ec_graph_links_part(ec_session *s, uint64_t lo, uint64_t hi, uint32_t *d_succ);
+/* ec_graph_load + ec_graph_links_part in one call (no host round trip between them) */
+int ec_graph_load_links(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags, uint64_t lo,
+                        uint64_t hi, uint32_t *d_succ);
 int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags);
 
 #ifdef __cplusplus

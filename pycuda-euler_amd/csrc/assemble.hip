@@ -2186,6 +2186,12 @@ int ec_export_dense(ec_session *s, void *d_out) {
 
 uint64_t ec_dense_count(ec_session *s) { return s ? s->n_dense : 0; }
 
+int ec_merge_owned_export(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags,
+                          void *d_out) {
+    EC_CHECK(ec_merge_owned(s, d_records, n, k, limit, flags));
+    return ec_export_dense(s, d_out);
+}
+
 int ec_assemble_from_solid(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags) {
     if (!s || (n && !d_records)) {
         set_error("null argument");
@@ -2250,6 +2256,12 @@ int ec_graph_links_part(ec_session *s, uint64_t lo, uint64_t hi, uint32_t *d_suc
     }
     EC_HIP(hipStreamSynchronize(s->stream));
     return EC_OK;
+}
+
+int ec_graph_load_links(ec_session *s, const void *d_records, uint64_t n, int k, unsigned flags, uint64_t lo,
+                        uint64_t hi, uint32_t *d_succ) {
+    EC_CHECK(ec_graph_load(s, d_records, n, k, flags));
+    return ec_graph_links_part(s, lo, hi, d_succ);
 }
 
 int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags) {

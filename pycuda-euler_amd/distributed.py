@@ -50,6 +50,8 @@ eulerhip.register("ec_record_bytes", ctypes.c_int, [ctypes.c_int])
 eulerhip.register("ec_graph_load", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_uint])
 eulerhip.register("ec_graph_links_part", ctypes.c_int, [_P, _U64, _U64, _P])
 eulerhip.register("ec_graph_finish", ctypes.c_int, [_P, _P, ctypes.c_uint])
+eulerhip.register("ec_merge_owned_export", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint, _P])
+eulerhip.register("ec_graph_load_links", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _U64, _U64, _P])
 
 
 def shard_range(nreads, rank, world):
@@ -100,13 +102,15 @@ class HipEngine:
         return out[: n * rb], [int(c) for c in counts]
 
     def merge_owned(self, recs, k, limit, flags=0):
+        """ec_merge_owned_export: merge + solid filter + export in one call into a buffer
+        sized for every received record (an upper bound of the solid ones)"""
         self.k = int(k)
         rb = self.rec_bytes()
         n = recs.numel() // rb
-        eulerhip.check(self.L.ec_merge_owned(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), int(limit), flags))
+        out = self.empty(n * rb)
+        eulerhip.check(self.L.ec_merge_owned_export(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k),
+                                                    int(limit), flags, ctypes.c_void_p(out.data_ptr())))
         m = int(self.L.ec_dense_count(self._h()))
-        out = self.empty(m * rb)
-        eulerhip.check(self.L.ec_export_dense(self._h(), ctypes.c_void_p(out.data_ptr())))
         return out[: m * rb]
 
     def assemble_from_solid(self, recs, k, flags=0, fetch=True):
@@ -120,6 +124,14 @@ class HipEngine:
         self.k = int(k)
         n = recs.numel() // self.rec_bytes()
         eulerhip.check(self.L.ec_graph_load(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), flags))
+        return int(self.L.ec_dense_count(self._h()))
+
+    def graph_load_links(self, recs, k, lo, hi, out, flags=0):
+        """graph_load + graph_links_part in one call (ec_graph_load_links)"""
+        self.k = int(k)
+        n = recs.numel() // self.rec_bytes()
+        eulerhip.check(self.L.ec_graph_load_links(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), flags,
+                                                  int(lo), int(hi), ctypes.c_void_p(out.data_ptr())))
         return int(self.L.ec_dense_count(self._h()))
 
     def graph_links_part(self, lo, hi, out):
@@ -166,17 +178,23 @@ class TorchComm:
                                    input_split_sizes=list(counts_bytes), group=self.group)
         return recv[: sum(rcl)], total_tag
 
-    def allgatherv(self, t, fill=0, with_sizes=False):
+    def allgatherv(self, t, fill=0, with_sizes=False, sizes=None):
         """Concatenation of every rank's `t` in rank order, each part padded with `fill` bytes
         to the largest part (no compaction copy: the record consumers skip all-0xFF filler
-        records, ec_assemble_from_solid).  with_sizes: also return every rank's byte count."""
+        records, ec_assemble_from_solid).  with_sizes: also return every rank's byte count.
+        sizes: every rank's byte count when the caller knows them already (no size exchange,
+        no host round trip)."""
         torch, dist = self.torch, self.dist
         if self.world == 1:
             return (t, [t.numel()]) if with_sizes else t
-        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
-        sizes = torch.empty(self.world, dtype=torch.int64, device=t.device)
-        dist.all_gather_into_tensor(sizes, n, group=self.group)
-        szl = [int(x) for x in sizes.tolist()]
+        if sizes is not None:
+            szl = [int(x) for x in sizes]
+            assert szl[self.rank] == t.numel(), "allgatherv: this rank's size differs from sizes[rank]"
+        else:
+            n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+            sz = torch.empty(self.world, dtype=torch.int64, device=t.device)
+            dist.all_gather_into_tensor(sz, n, group=self.group)
+            szl = [int(x) for x in sz.tolist()]
         mx = max(max(szl), 1)
         pad = torch.full((mx,), fill, dtype=torch.uint8, device=t.device)
         pad[: t.numel()] = t
@@ -236,12 +254,18 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
         nrec = [sz // rec_bytes(k) for sz in sizes]
         lo = sum(nrec[: comm.rank])
         hi = lo + nrec[comm.rank]
-        engine.graph_load(everything, k, flags)
-        tick("load")
         part = engine.empty(8 * (hi - lo))
-        engine.graph_links_part(lo, hi, part)
-        tick("links")
-        gathered, psz = comm.allgatherv(part[: 8 * (hi - lo)], fill=0xFF, with_sizes=True)
+        if hasattr(engine, "graph_load_links"):  # one call: no host round trip in between
+            engine.graph_load_links(everything, k, lo, hi, part, flags)
+            tick("load_links")
+        else:
+            engine.graph_load(everything, k, flags)
+            tick("load")
+            engine.graph_links_part(lo, hi, part)
+            tick("links")
+        # every rank's part size is known from the solid-set sizes: no size exchange
+        gathered, psz = comm.allgatherv(part[: 8 * (hi - lo)], fill=0xFF, with_sizes=True,
+                                        sizes=[8 * x for x in nrec])
         if comm.world > 1:  # drop the padding: node order = rank order
             mx = max(max(psz), 1)
             succ = comm.torch.cat([gathered[r * mx: r * mx + psz[r]] for r in range(comm.world)])
