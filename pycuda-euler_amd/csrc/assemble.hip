@@ -148,6 +148,10 @@ struct ec_session {
     DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur, cwalk;
     bool no_index = false;      // the call needs dense records only (shard count, owner merge)
     uint64_t shard_base = 0;    // ec_count_shard: global id of the shard's read 0 (added at export)
+    // the super-k-mer fast path's read length of the last call on (offsets, reads): reused
+    // without a host round trip -- k_skpart_w<., ., true> checks every read against it anyway
+    const uint64_t *lc_off = nullptr;
+    uint64_t lc_n = 0, lc_L = 0;
     bool filt = false;          // phase_count: k_bucket_filt (more distinct keys than LDS tables hold)
     int pmax = 1, pmin = 0;     // k_bucket_filt: 2^pmax part tables per bucket region
     float part_keys = 1400.0f;  // k_bucket_filt: target keys per part table
@@ -613,10 +617,14 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     // read length of the first read; the partition checks the rest
     if (allow_sk2 && k >= SK_MIN_K && k <= 32 && !getenv("EULERHIP_NO_SK2") && !getenv("EULERHIP_SKPART_RING") &&
         !getenv("EULERHIP_NO_FASTSK2")) {
-        uint64_t o2[2] = {0, 0};
-        EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
-        const uint64_t L = o2[1] - o2[0];
+        uint64_t L = s->lc_L;
+        if (!(L && s->lc_off == d_off && s->lc_n == nreads)) {
+            uint64_t o2[2] = {0, 0};
+            EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
+            EC_HIP(hipStreamSynchronize(st));
+            L = o2[1] - o2[0];
+        }
+        s->lc_off = d_off, s->lc_n = nreads, s->lc_L = L;
         const int npf = npf_of(L);
         if (L >= (uint64_t)k && npf) {
             const uint32_t M = (uint32_t)(L - k + 1);
@@ -629,6 +637,7 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
                 ok = true;
                 return EC_OK;
             }
+            if (invalid) s->lc_L = 0;  // (a stale cached length fails the same check: re-read next call)
             if (!invalid) allow_sk2 = false;  // the estimate or a capacity declined: window records
         }
     }

@@ -655,3 +655,34 @@ def test_sk2_fast_path_fallbacks_vs_oracle(gpu_session):
             assert res.stats.count_variant == 3, name
         else:
             assert res.stats.count_variant != 3, name
+
+
+def test_sk2_cached_read_length_same_buffers(gpu_session):
+    """run_device reuses the read length of its last call on the same offsets pointer and read
+    count (no host round trip); new reads of another length in the same device buffers fail the
+    partition's own length check and are redone correctly, as are N-bearing reads"""
+    import torch
+
+    rng = np.random.default_rng(78)
+    g = rng.integers(0, 4, 40_000, dtype=np.uint8)
+    n = 4_000
+
+    def reads_of(L, with_n=False):
+        st = rng.integers(0, len(g) - 120, n)
+        b = np.frombuffer(b"ACGT", np.uint8)[g[st[:, None] + np.arange(L)[None, :]]].reshape(-1).copy()
+        if with_n:
+            b[L * 17 + 5] = ord("N")
+        return b, np.arange(n + 1, dtype=np.uint64) * np.uint64(L)
+
+    d_buf = torch.zeros(n * 100, dtype=torch.uint8, device="cuda")
+    d_off = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    for L, with_n in ((100, False), (100, False), (90, False), (90, False), (100, True), (100, False)):
+        buf, off = reads_of(L, with_n)
+        d_buf[: buf.size].copy_(torch.from_numpy(buf))
+        d_off.copy_(torch.from_numpy(off.astype(np.int64)))
+        torch.cuda.synchronize()
+        gpu_session.run_device(d_buf.data_ptr(), d_off.data_ptr(), n, 31, 1, 0)
+        res = gpu_session.fetch(31)
+        ref = oracle.assemble_packed(buf, off, 31, 1)
+        assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref), (L, with_n)
+        assert res.stats.n_positions == ref["n_positions"], (L, with_n)
