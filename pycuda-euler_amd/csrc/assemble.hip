@@ -617,8 +617,8 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     // read length of the first read; the partition checks the rest
     if (allow_sk2 && k >= SK_MIN_K && k <= 32 && !getenv("EULERHIP_NO_SK2") && !getenv("EULERHIP_SKPART_RING") &&
         !getenv("EULERHIP_NO_FASTSK2")) {
-        uint64_t L = s->lc_L;
-        if (!(L && s->lc_off == d_off && s->lc_n == nreads)) {
+        uint64_t L = s->lc_L;  // (only a length the fast path then validates is reused)
+        if (!(L >= (uint64_t)k && npf_of(L) && s->lc_off == d_off && s->lc_n == nreads)) {
             uint64_t o2[2] = {0, 0};
             EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
             EC_HIP(hipStreamSynchronize(st));
