@@ -606,7 +606,9 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     Scalars hsc;
     // read groups of whole 64-read wave tiles, at most 2048 (k_refine2 run tables)
     const uint64_t ntiles = (nreads + 63) / 64;
-    uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, RF_MAX_RUNS));
+    uint64_t gmax = RF_MAX_RUNS;
+    if (const char *e = getenv("EULERHIP_V2_GROUPS")) gmax = std::min<uint64_t>(RF_MAX_RUNS, std::max(1, atoi(e)));
+    uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, gmax));
     const uint64_t gsize = ((ntiles + G - 1) / G) * 64;
     G = (nreads + gsize - 1) / gsize;
     auto npf_of = [](uint64_t lall) {  // 16-B chunks of a 64-read wave tile -> staged KiB per wave
