@@ -43,6 +43,9 @@ CONFIGS = {
     # BASELINE configs[4]: synthetic 200 Mbp genome, 100M x 150 bp, k = 51 (128-bit keys)
     "genome200m_k51": dict(genome=200_000_000, reads=100_000_000, read_len=150, k=51, seed=20261015 + 5,
                            name="synthetic-200Mbp-100Mx150bp-k51"),
+    # config 5's per-rank shape at 8 ranks: 1/8 of its reads (12.5 M x 150 bp) of the 200 Mbp genome
+    "genome200m_k51_r8": dict(genome=200_000_000, reads=12_500_000, read_len=150, k=51, seed=20261015 + 5,
+                              name="synthetic-200Mbp-12.5Mx150bp-k51"),
     # the same read length / k at a tenth of the size (20 Mbp genome, same 75x coverage)
     "genome20m_k51": dict(genome=20_000_000, reads=10_000_000, read_len=150, k=51, seed=20261015 + 5,
                           name="synthetic-20Mbp-10Mx150bp-k51"),
@@ -101,9 +104,33 @@ def kernel_names(variant):
     return ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine")
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def host_threads():
+    """host cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU boxes; os.cpu_count() there counts the whole machine), else the affinity mask"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
 def cpu_baseline(buf, off, k, sample_reads):
-    """The test-only C restatement (oracle/refasm.c) of the reference CPU assembler, 1 core,
-    on the first `sample_reads` reads of the same workload."""
+    """The test-only C restatement (oracle/refasm.c) of the reference CPU assembler on the first
+    `sample_reads` reads of the same workload, timed twice: 1 core (the
+    reference's build + all_contigs are single-threaded) and N cores (oracle_assemble_mt:
+    map -> reduceByKey counting as src/ref_spark.py:76-84 on N threads, all_contigs
+    single-threaded).  value = the N-core rate."""
     import oracle
 
     n = min(sample_reads, len(off) - 1)
@@ -111,12 +138,57 @@ def cpu_baseline(buf, off, k, sample_reads):
     so = off[: n + 1]
     t0 = time.perf_counter()
     out = oracle.assemble_packed(sb, so, k, 1)
-    dt = time.perf_counter() - t0
+    dt1 = time.perf_counter() - t0
+    nth = host_threads()
+    t0 = time.perf_counter()
+    outn = oracle.assemble_packed(sb, so, k, 1, threads=nth)
+    dtn = time.perf_counter() - t0
+    assert outn["contig_chars"] == out["contig_chars"], "N-core oracle differs from the 1-core oracle"
     P = int(out["n_positions"])
-    return {"value": P / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
-            "sample": "first %d of %d reads (%d k-mer positions), oracle/refasm.c single-threaded, %.1f s"
-                      % (n, len(off) - 1, P, dt),
-            "cpu": platform.processor() or platform.machine()}
+    return {"value": P / dtn, "unit": "k-mers/s", "cores": nth, "kind": "port",
+            "sample": "first %d of %d reads (%d k-mer positions): oracle/refasm.c map->reduceByKey count on %d "
+                      "threads + single-threaded all_contigs %.1f s; single-threaded build+all_contigs %.1f s"
+                      % (n, len(off) - 1, P, nth, dtn, dt1),
+            "one_core": {"value": P / dt1, "unit": "k-mers/s", "cores": 1, "seconds": round(dt1, 2)},
+            "cpu": cpu_model(), "node_cpus": os.cpu_count()}
+
+
+def host_input_legs(sess, buf, off, k, P, steps, warmup):
+    """The drop-in entry from host memory (the reference hands host reads to its GPU path,
+    src/eulercuda.py:484-497; SURVEY 8d: "timer starts after reads are in pinned host memory; H2D
+    is included"): one step = ec_assemble_packed_host on 2-bit codes in page-locked memory (the
+    ingest's output: ec_pack_reads, timed separately as pack_ms), and ec_assemble_host on the ASCII
+    reads in page-locked memory.  Chunked copies on a second stream overlap the partition."""
+    import torch
+    import eulerhip
+
+    pin = lambda n: torch.empty(int(n), dtype=torch.uint8, pin_memory=True).numpy()  # noqa: E731
+    t0 = time.perf_counter()
+    pr = eulerhip.pack_2bit(buf, off, threads=host_threads(), alloc=pin)
+    pack_ms = (time.perf_counter() - t0) * 1e3
+    abuf = pin(buf.size)
+    abuf[:] = buf
+    aoff = torch.empty(len(off), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+    aoff[:] = off
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            fn()  # (each call ends with the results in the session's pinned host buffers)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / steps * 1e3
+
+    ms_packed = timed(lambda: sess.run_packed_host(pr, k, 1, eulerhip.EC_FLAG_KERNEL_TIMING))
+    ms_ascii = timed(lambda: sess.run_host(abuf, aoff, k, 1, eulerhip.EC_FLAG_KERNEL_TIMING))
+    return {"value": round(P / (ms_packed / 1e3), 1), "unit": "k-mers/s", "ms_per_step": round(ms_packed, 3),
+            "input": "2-bit codes in page-locked host memory (%d bytes, one read length: no offsets)" % pr.codes.size,
+            "pack_ms": round(pack_ms, 1),
+            "ascii": {"value": round(P / (ms_ascii / 1e3), 1), "ms_per_step": round(ms_ascii, 3),
+                      "input": "ASCII reads + uint64 offsets in page-locked host memory (%d bytes)"
+                               % (buf.size + 8 * len(off))}}
 
 
 def load_traffic(workload, kernel):
@@ -144,6 +216,8 @@ def main():
     ap.add_argument("--config", default="ecoli10m", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-sample-reads", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-input", action="store_true",
+                    help="skip the host-input legs (reads in pinned host memory, PCIe copy inside the step)")
     ap.add_argument("--sharded", action="store_true", help="use the multi-GPU path even with one rank")
     ap.add_argument("--strong", action="store_true",
                     help="N > 1: split the config's reads over the ranks (fixed job) instead of the default "
@@ -285,6 +359,9 @@ def main():
                 for i in range(len(kern)) if kern[i] > 0},
             "pipeline_alg_bytes": int(alg_bytes(P, R, L, U, K)),
             "pipeline_frac": round(alg_bytes(P, R, L, U, K) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
+    host = None
+    if not use_dist and not args.no_host_input:
+        host = host_input_legs(sess, buf, off, k, P, args.steps, max(2, args.warmup))
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(buf, off, k, args.cpu_sample_reads)
@@ -306,6 +383,7 @@ def main():
                    "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "host_input": host,
         "stage_ms": {names[i]: round(stage[i], 3) for i in range(len(names))},
         "sharded_phase_ms": sharded_ms,
     }

@@ -128,9 +128,28 @@ int ec_session_destroy(ec_session *s);
  * = byte offsets (uint64).  limit: keep k-mers whose dict count > limit (build(limit=1)). */
 int ec_assemble_device(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offsets,
                        uint64_t nreads, int k, int limit, unsigned flags);
-/* Same on host buffers (copies H2D first). */
+/* Same on host buffers: the reference's entry (src/eulercuda.py:484-497 hands the host read
+ * buffer to encode_lmer_device, src/pyencode.py:14, which copies it H2D).  The reads are copied
+ * in chunks on a second stream while the super-k-mer partition runs on the chunks that have
+ * arrived; pinned (page-locked) host memory copies at the full PCIe rate. */
 int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const uint64_t *offsets,
                      uint64_t nreads, int k, int limit, unsigned flags);
+
+/* 2-bit packed host reads (a quarter of ec_assemble_host's PCIe bytes).  Layout: base i of the
+ * concatenated reads at bits 2 (i & 3) of codes[i >> 2] (A=0 C=1 G=2 T=3); every byte that is not
+ * A, C, G or T ('N', anything else) is an exception: exc_pos[] ascending base positions, exc_byte[]
+ * the original bytes (their code bits are ignored).  Read r = bases [offsets[r], offsets[r+1]),
+ * or, offsets = NULL, [r * read_len, (r + 1) * read_len).  Results equal ec_assemble_host's on
+ * the unpacked reads. */
+int ec_assemble_packed_host(ec_session *s, const uint8_t *codes, uint64_t nbases, const uint64_t *offsets,
+                            uint64_t nreads, uint32_t read_len, const uint64_t *exc_pos, const uint8_t *exc_byte,
+                            uint64_t n_exc, int k, int limit, unsigned flags);
+/* ASCII reads (CSR) -> that layout, on `threads` host threads (<= 0: up to 16).  codes holds
+ * ceil(nbases / 4) bytes; exceptions beyond exc_cap are counted but not written (*n_exc = the
+ * total: call again with a larger buffer when it exceeds exc_cap); *read_len = the common read
+ * length, or 0 when the reads differ in length (offsets are then needed). */
+int ec_pack_reads(const uint8_t *reads, const uint64_t *offsets, uint64_t nreads, int threads, uint8_t *codes,
+                  uint64_t *exc_pos, uint8_t *exc_byte, uint64_t exc_cap, uint64_t *n_exc, uint32_t *read_len);
 
 int ec_get_stats(ec_session *s, ec_stats *out);
 const char *ec_stage_name(int stage);

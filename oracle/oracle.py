@@ -45,6 +45,9 @@ def lib():
         _lib.oracle_assemble.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_uint, ctypes.POINTER(_Result)]
         _lib.oracle_assemble.restype = ctypes.c_int
+        _lib.oracle_assemble_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(_Result)]
+        _lib.oracle_assemble_mt.restype = ctypes.c_int
         _lib.oracle_free.argtypes = [ctypes.POINTER(_Result)]
         _lib.oracle_last_error.restype = ctypes.c_char_p
     return _lib
@@ -63,15 +66,21 @@ def pack_reads(reads):
     return np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8), off
 
 
-def assemble_packed(buf, offsets, k, limit=1, want_dict=False):
-    """Run the oracle on a packed read set. Returns dict with d (optional), contigs, links."""
+def assemble_packed(buf, offsets, k, limit=1, want_dict=False, threads=None):
+    """Run the oracle on a packed read set. Returns dict with d (optional), contigs, links.
+    threads = N: the N-core variant (map -> reduceByKey counting as src/ref_spark.py:76-84 on N
+    host threads, all_contigs single-threaded); same results."""
     L = lib()
     res = _Result()
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     nreads = len(offsets) - 1
-    rc = L.oracle_assemble(buf.ctypes.data, offsets.ctypes.data, nreads, k, limit,
-                           1 if want_dict else 0, ctypes.byref(res))
+    if threads:
+        rc = L.oracle_assemble_mt(buf.ctypes.data, offsets.ctypes.data, nreads, k, limit,
+                                  1 if want_dict else 0, int(threads), ctypes.byref(res))
+    else:
+        rc = L.oracle_assemble(buf.ctypes.data, offsets.ctypes.data, nreads, k, limit,
+                               1 if want_dict else 0, ctypes.byref(res))
     if rc != 0:
         raise OracleError("oracle_assemble rc=%d: %s" % (rc, L.oracle_last_error().decode()))
     try:
@@ -115,7 +124,7 @@ def unpack_links(out):
     return res
 
 
-def assemble(reads, k, limit=1, want_dict=True):
+def assemble(reads, k, limit=1, want_dict=True, threads=None):
     buf, off = pack_reads(reads)
-    out = assemble_packed(buf, off, k, limit, want_dict)
+    out = assemble_packed(buf, off, k, limit, want_dict, threads)
     return out.get("d"), unpack_contigs(out), unpack_links(out)

@@ -24,6 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
+#include <pthread.h>
 
 #include "refasm.h"
 
@@ -69,6 +70,14 @@ int oracle_assemble(const char *buf, const uint64_t *offsets, uint64_t nreads, i
     if (k < 1 || k > 64) { snprintf(g_err, sizeof g_err, "k=%d out of range [1,64]", k); return -1; }
     if (k <= 32) return assemble_64(buf, offsets, nreads, k, limit, flags, out);
     return assemble_128(buf, offsets, nreads, k, limit, flags, out);
+}
+
+int oracle_assemble_mt(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
+                       unsigned flags, int threads, oracle_result *out) {
+    memset(out, 0, sizeof(*out));
+    if (k < 1 || k > 64) { snprintf(g_err, sizeof g_err, "k=%d out of range [1,64]", k); return -1; }
+    if (k <= 32) return assemble_mt_64(buf, offsets, nreads, k, limit, flags, threads, out);
+    return assemble_mt_128(buf, offsets, nreads, k, limit, flags, threads, out);
 }
 
 void oracle_free(oracle_result *r) {

@@ -25,6 +25,10 @@ typedef struct {
 /* returns 0 on success, -1 bad argument, -2 byte outside {A,C,G,T,N}, -3 out of memory */
 int oracle_assemble(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
                     unsigned flags, oracle_result *out);
+/* the same result from `threads` host threads: map -> reduceByKey counting as
+ * src/ref_spark.py:76-84, all_contigs single-threaded (BASELINE.md §3 N-core baseline) */
+int oracle_assemble_mt(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
+                       unsigned flags, int threads, oracle_result *out);
 void oracle_free(oracle_result *r);
 const char *oracle_last_error(void);
 

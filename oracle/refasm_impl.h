@@ -176,10 +176,80 @@ static void F(put_kmer)(char *dst, KEY x, int k) {
     for (int i = k - 1; i >= 0; i--) { dst[i] = A[(int)(x & 3)]; x >>= 2; }
 }
 
+/* one read's N-split segments (build:29): calls seg(s + p, q - p) for every segment of >= k
+ * bases; -2 on a byte outside {A,C,G,T,N} */
+#define SEGMENTS(r, s, len, k, SEG_BODY)                                                              \
+    do {                                                                                              \
+        uint64_t p_ = 0;                                                                              \
+        while (p_ <= (len)) {                                                                         \
+            uint64_t q_ = p_;                                                                         \
+            while (q_ < (len) && (s)[q_] != 'N') {                                                    \
+                if (base_code((s)[q_]) < 0) {                                                         \
+                    snprintf(g_err, sizeof g_err, "read %llu byte %llu (0x%02x) outside {A,C,G,T,N}", \
+                             (unsigned long long)(r), (unsigned long long)q_, (s)[q_]);               \
+                    rc = -2;                                                                          \
+                    goto fail;                                                                        \
+                }                                                                                     \
+                q_++;                                                                                 \
+            }                                                                                         \
+            if (q_ - p_ >= (uint64_t)(k)) {                                                           \
+                const unsigned char *seg = (s) + p_;                                                  \
+                const uint64_t seglen = q_ - p_;                                                      \
+                SEG_BODY;                                                                             \
+            }                                                                                         \
+            p_ = q_ + 1;                                                                              \
+        }                                                                                             \
+    } while (0)
+
+/* build:25-42 -> d (insertion-ordered, entries with count > limit) */
+static int F(build)(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit, F(omap) *d,
+                    uint64_t *npos) {
+    int rc = 0;
+    if ((rc = F(om_init)(d, 1 << 16))) return rc;
+    /* build:27-35 -- per read, per N-split segment, forward then twin(seg) k-mers */
+    for (uint64_t r = 0; r < nreads; r++) {
+        const unsigned char *s = (const unsigned char *)buf + offsets[r];
+        uint64_t len = offsets[r + 1] - offsets[r];
+        SEGMENTS(r, s, len, k, {
+            *npos += seglen - k + 1;
+            if ((rc = F(insert_seq)(d, seg, seglen, k, 0))) goto fail;
+            if ((rc = F(insert_seq)(d, seg, seglen, k, 1))) goto fail;
+        });
+    }
+    /* build:37-39 -- delete d[x] <= limit, keeping insertion order */
+    {
+        uint64_t w = 0;
+        for (uint64_t i = 0; i < d->n; i++)
+            if ((int64_t)d->vals[i] > (int64_t)limit) { d->keys[w] = d->keys[i]; d->vals[w] = d->vals[i]; w++; }
+        d->n = w;
+        uint64_t s = 1024;
+        while (s < 2 * (d->n + 1)) s <<= 1;
+        if ((rc = F(om_rehash)(d, s))) goto fail;
+    }
+    return 0;
+fail:
+    return rc;
+}
+
+/* all_contigs:79-111 on d (consumed: freed on return) */
+static int F(all_contigs)(F(omap) *dp, int k, unsigned flags, oracle_result *out);
+
 static int F(assemble)(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
                        unsigned flags, oracle_result *out) {
+    F(omap) d;
+    memset(&d, 0, sizeof d);
+    int rc = F(build)(buf, offsets, nreads, k, limit, &d, &out->n_positions);
+    if (rc) {
+        F(om_free)(&d);
+        if (rc == -3) snprintf(g_err, sizeof g_err, "out of memory");
+        return rc;
+    }
+    return F(all_contigs)(&d, k, flags, out);
+}
+
+static int F(all_contigs)(F(omap) *dp, int k, unsigned flags, oracle_result *out) {
     int rc = 0;
-    F(omap) d, heads, tails;
+    F(omap) d = *dp, heads, tails;
     F(kvec) cf = {0}, cb = {0}, c = {0};
     F(cbuf) chars = {0};
     uint64_t *coff = NULL, *loff = NULL;
@@ -188,41 +258,6 @@ static int F(assemble)(const char *buf, const uint64_t *offsets, uint64_t nreads
     unsigned char *done = NULL;
     memset(&heads, 0, sizeof heads);
     memset(&tails, 0, sizeof tails);
-    if ((rc = F(om_init)(&d, 1 << 16))) return rc;
-
-    /* build:27-35 -- per read, per N-split segment, forward then twin(seg) k-mers */
-    for (uint64_t r = 0; r < nreads; r++) {
-        const unsigned char *s = (const unsigned char *)buf + offsets[r];
-        uint64_t len = offsets[r + 1] - offsets[r], p = 0;
-        while (p <= len) {
-            uint64_t q = p;
-            while (q < len && s[q] != 'N') {
-                if (base_code(s[q]) < 0) {
-                    snprintf(g_err, sizeof g_err, "read %llu byte %llu (0x%02x) outside {A,C,G,T,N}",
-                             (unsigned long long)r, (unsigned long long)q, s[q]);
-                    rc = -2;
-                    goto fail;
-                }
-                q++;
-            }
-            if (q - p >= (uint64_t)k) {
-                out->n_positions += q - p - k + 1;
-                if ((rc = F(insert_seq)(&d, s + p, q - p, k, 0))) goto fail;
-                if ((rc = F(insert_seq)(&d, s + p, q - p, k, 1))) goto fail;
-            }
-            p = q + 1;
-        }
-    }
-    /* build:37-39 -- delete d[x] <= limit, keeping insertion order */
-    {
-        uint64_t w = 0;
-        for (uint64_t i = 0; i < d.n; i++)
-            if ((int64_t)d.vals[i] > (int64_t)limit) { d.keys[w] = d.keys[i]; d.vals[w] = d.vals[i]; w++; }
-        d.n = w;
-        uint64_t s = 1024;
-        while (s < 2 * (d.n + 1)) s <<= 1;
-        if ((rc = F(om_rehash)(&d, s))) goto fail;
-    }
     out->n_dict = d.n;
     if (flags & ORACLE_WANT_DICT) {
         out->dict_kmers = (char *)malloc(d.n * (uint64_t)k + 1);
@@ -331,6 +366,240 @@ fail:
     return rc;
 }
 
+/* ---- N-core variant (bench.py cpu_baseline "cores": N) ---------------------------------------
+ * The reference's distributed CPU path, src/ref_spark.py:76-84: flatMap every read to its
+ * forward and reverse-complement k-mers, map to (k-mer, 1), reduceByKey -- here T map threads
+ * over contiguous read ranges, each combining into P = T hash partitions (Spark's map-side
+ * combine), then P reduce threads merging one partition each.  Unlike ref_spark (whose
+ * per-partition all_contigs loses the global dict), every entry also keeps the minimum
+ * insertion event (read << 32 | index of the insert within the read, build:31-35), so sorting
+ * the solid entries by event restores build()'s insertion order exactly; all_contigs then runs
+ * single-threaded on that dict.  Results equal F(assemble)'s. */
+typedef struct {
+    KEY *keys;
+    uint32_t *cnt;
+    uint64_t *ev;
+    uint64_t n, mask;
+} F(cmap);
+
+static int F(cm_init)(F(cmap) *m, uint64_t cap) {
+    uint64_t s = 1024;
+    while (s < 2 * cap) s <<= 1;
+    m->keys = (KEY *)malloc(s * sizeof(KEY));
+    m->cnt = (uint32_t *)calloc(s, sizeof(uint32_t));
+    m->ev = (uint64_t *)malloc(s * sizeof(uint64_t));
+    m->n = 0;
+    m->mask = s - 1;
+    return (m->keys && m->cnt && m->ev) ? 0 : -3;
+}
+static void F(cm_free)(F(cmap) *m) { free(m->keys); free(m->cnt); free(m->ev); memset(m, 0, sizeof *m); }
+
+static int F(cm_add)(F(cmap) *m, KEY key, uint32_t add, uint64_t ev);
+static int F(cm_grow)(F(cmap) *m) {
+    F(cmap) o = *m;
+    if (F(cm_init)(m, o.mask + 1)) return -3;
+    for (uint64_t i = 0; i <= o.mask; i++)
+        if (o.cnt[i] && F(cm_add)(m, o.keys[i], o.cnt[i], o.ev[i])) return -3;
+    F(cm_free)(&o);
+    return 0;
+}
+/* count += add, event = min (count 0 = empty slot: adds are >= 1) */
+static int F(cm_add)(F(cmap) *m, KEY key, uint32_t add, uint64_t ev) {
+    uint64_t h = KHASH(key) & m->mask;
+    while (m->cnt[h]) {
+        if (m->keys[h] == key) {
+            m->cnt[h] += add;
+            if (ev < m->ev[h]) m->ev[h] = ev;
+            return 0;
+        }
+        h = (h + 1) & m->mask;
+    }
+    m->keys[h] = key;
+    m->cnt[h] = add;
+    m->ev[h] = ev;
+    if (2 * ++m->n > m->mask) return F(cm_grow)(m);
+    return 0;
+}
+
+typedef struct {
+    uint64_t ev;
+    KEY key;
+    uint32_t cnt;
+} F(entry);
+
+typedef struct {
+    const char *buf;
+    const uint64_t *offsets;
+    uint64_t r0, r1, npos;
+    int k, nparts, rc;
+    F(cmap) *parts; /* nparts maps of this map thread */
+    char err[256];
+} F(mapjob);
+
+static inline int F(part_of)(KEY key, int nparts) { return (int)((KHASH(key) >> 40) % (uint64_t)nparts); }
+
+static void *F(map_thread)(void *arg) {
+    F(mapjob) *j = (F(mapjob) *)arg;
+    int rc = 0;
+    const int k = j->k;
+    const KEY mask = F(kmask)(k);
+    static const int comp[4] = {3, 2, 1, 0};
+    for (int p = 0; p < j->nparts; p++)
+        if ((rc = F(cm_init)(&j->parts[p], 1 << 12))) goto fail;
+    for (uint64_t r = j->r0; r < j->r1; r++) {
+        const unsigned char *s = (const unsigned char *)j->buf + j->offsets[r];
+        uint64_t len = j->offsets[r + 1] - j->offsets[r], local = 0;
+        SEGMENTS(r, s, len, k, {
+            j->npos += seglen - k + 1;
+            for (int tw = 0; tw < 2; tw++) { /* ref_spark.py:78 fwd_list, :81-83 rev_list */
+                KEY code = 0;
+                for (uint64_t t = 0; t < seglen; t++) {
+                    const int b = tw ? comp[base_code(seg[seglen - 1 - t])] : base_code(seg[t]);
+                    code = ((code << 2) | (KEY)b) & mask;
+                    if (t + 1 >= (uint64_t)k) {
+                        if ((rc = F(cm_add)(&j->parts[F(part_of)(code, j->nparts)], code, 1, (r << 32) | local)))
+                            goto fail;
+                        local++;
+                    }
+                }
+            }
+        });
+    }
+fail:
+    if (rc == -2) memcpy(j->err, g_err, sizeof j->err);
+    j->rc = rc;
+    return NULL;
+}
+
+typedef struct {
+    F(mapjob) *maps;
+    int nmaps, part, rc;
+    long long limit;
+    F(entry) *out;
+    uint64_t n;
+} F(redjob);
+
+static int F(ev_cmp)(const void *a, const void *b) {
+    const uint64_t x = ((const F(entry) *)a)->ev, y = ((const F(entry) *)b)->ev;
+    return x < y ? -1 : x > y;
+}
+
+/* reduceByKey (ref_spark.py:84) for one partition, then the solid filter (build:37-39) and the
+ * partition's entries in event order */
+static void *F(reduce_thread)(void *arg) {
+    F(redjob) *j = (F(redjob) *)arg;
+    F(cmap) acc;
+    uint64_t est = 0;
+    for (int t = 0; t < j->nmaps; t++) est += j->maps[t].parts[j->part].n;
+    if ((j->rc = F(cm_init)(&acc, est / 2 + 16))) return NULL;
+    for (int t = 0; t < j->nmaps; t++) {
+        F(cmap) *m = &j->maps[t].parts[j->part];
+        for (uint64_t i = 0; i <= m->mask; i++)
+            if (m->cnt[i] && (j->rc = F(cm_add)(&acc, m->keys[i], m->cnt[i], m->ev[i]))) goto done;
+        F(cm_free)(m);
+    }
+    j->out = (F(entry) *)malloc((acc.n + 1) * sizeof(F(entry)));
+    if (!j->out) {
+        j->rc = -3;
+        goto done;
+    }
+    for (uint64_t i = 0; i <= acc.mask; i++)
+        if (acc.cnt[i] && (long long)acc.cnt[i] > j->limit) {
+            j->out[j->n].ev = acc.ev[i];
+            j->out[j->n].key = acc.keys[i];
+            j->out[j->n].cnt = acc.cnt[i];
+            j->n++;
+        }
+    qsort(j->out, j->n, sizeof(F(entry)), F(ev_cmp));
+done:
+    F(cm_free)(&acc);
+    return NULL;
+}
+
+static int F(assemble_mt)(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
+                          unsigned flags, int threads, oracle_result *out) {
+    int rc = 0;
+    const int T = threads < 1 ? 1 : threads > 256 ? 256 : threads;
+    F(mapjob) *maps = (F(mapjob) *)calloc(T, sizeof(F(mapjob)));
+    F(redjob) *reds = (F(redjob) *)calloc(T, sizeof(F(redjob)));
+    pthread_t *th = (pthread_t *)calloc(T, sizeof(pthread_t));
+    uint64_t *head = (uint64_t *)calloc(T, sizeof(uint64_t));
+    F(omap) d;
+    memset(&d, 0, sizeof d);
+    if (!maps || !reds || !th || !head) {
+        rc = -3;
+        goto fail;
+    }
+    for (int t = 0; t < T; t++) {
+        maps[t].buf = buf;
+        maps[t].offsets = offsets;
+        maps[t].r0 = nreads * (uint64_t)t / (uint64_t)T;
+        maps[t].r1 = nreads * (uint64_t)(t + 1) / (uint64_t)T;
+        maps[t].k = k;
+        maps[t].nparts = T;
+        maps[t].parts = (F(cmap) *)calloc(T, sizeof(F(cmap)));
+        if (!maps[t].parts) {
+            rc = -3;
+            goto fail;
+        }
+    }
+    for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, F(map_thread), &maps[t]);
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < T; t++) {
+        out->n_positions += maps[t].npos;
+        if (maps[t].rc && !rc) {
+            rc = maps[t].rc;
+            if (rc == -2) memcpy(g_err, maps[t].err, sizeof g_err);
+        }
+    }
+    if (rc) goto fail;
+    for (int p = 0; p < T; p++) {
+        reds[p].maps = maps;
+        reds[p].nmaps = T;
+        reds[p].part = p;
+        reds[p].limit = limit;
+        pthread_create(&th[p], NULL, F(reduce_thread), &reds[p]);
+    }
+    for (int p = 0; p < T; p++) pthread_join(th[p], NULL);
+    for (int p = 0; p < T; p++)
+        if (reds[p].rc) rc = reds[p].rc;
+    if (rc) goto fail;
+    /* merge the partitions by event: build()'s dict order */
+    {
+        uint64_t total = 0;
+        for (int p = 0; p < T; p++) total += reds[p].n;
+        if ((rc = F(om_init)(&d, total + 16))) goto fail;
+        for (uint64_t i = 0; i < total; i++) {
+            int best = -1;
+            for (int p = 0; p < T; p++)
+                if (head[p] < reds[p].n && (best < 0 || reds[p].out[head[p]].ev < reds[best].out[head[best]].ev))
+                    best = p;
+            const F(entry) *e = &reds[best].out[head[best]++];
+            if ((rc = F(om_add)(&d, e->key, e->cnt))) goto fail;
+        }
+    }
+fail:
+    if (maps)
+        for (int t = 0; t < T; t++) {
+            if (maps[t].parts)
+                for (int p = 0; p < T; p++) F(cm_free)(&maps[t].parts[p]);
+            free(maps[t].parts);
+        }
+    if (reds)
+        for (int p = 0; p < T; p++) free(reds[p].out);
+    free(maps);
+    free(reds);
+    free(th);
+    free(head);
+    if (rc) {
+        F(om_free)(&d);
+        if (rc == -3) snprintf(g_err, sizeof g_err, "out of memory");
+        return rc;
+    }
+    return F(all_contigs)(&d, k, flags, out);
+}
+
+#undef SEGMENTS
 #undef F
 #undef CAT
 #undef CAT2

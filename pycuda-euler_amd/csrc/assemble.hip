@@ -34,6 +34,7 @@
 #include "shard.h"
 #include "compact.h"
 #include "count_wide.h"
+#include "hostin.h"
 
 namespace ec {
 
@@ -163,6 +164,26 @@ struct ec_session {
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
+    // host-input pipeline (ec_assemble_host / ec_assemble_packed_host, hostin.h): the reads are
+    // copied H2D in chunks on cstream; pipe_upto(c) makes chunks .. c visible to the session
+    // stream (event wait + unpack) -- the super-k-mer partition runs on each chunk's read groups
+    // as they arrive, any other count path waits for all of them (pipe_all)
+    hipStream_t cstream = nullptr;
+    struct Pipe {
+        bool active = false;
+        bool packed = false;          // 2-bit codes (k_unpack2 + k_patch) or ASCII
+        int nchunks = 0, done = 0;    // chunks made visible so far
+        std::vector<uint64_t> blo, bhi;   // chunk c = bases [blo[c], bhi[c]) (multiples of 64 inside)
+        std::vector<uint64_t> ravail;     // reads complete after chunk c
+        std::vector<uint64_t> elo, ehi;   // its exceptions (packed)
+        uint64_t first_len = 0;           // length of read 0 (the partition's M before any D2H)
+        const uint32_t *codes = nullptr;  // device 2-bit codes
+        const uint64_t *exc_pos = nullptr;
+        const uint8_t *exc_byte = nullptr;
+        uint8_t *ascii = nullptr;         // device reads (the count kernels' input)
+    } pipe;
+    std::vector<hipEvent_t> pev;  // chunk copy events (created on demand, reused)
+    DevBuf p_codes, p_exc;
 };
 
 namespace ec {
@@ -240,6 +261,26 @@ int sort_pairs(ec_session *s, unsigned long long *kin, unsigned long long *kout,
     EC_HIP(rocprim::radix_sort_pairs(s->tmp.p, bytes, kin, kout, vin, vout, n, 0, 64, s->stream));
     return EC_OK;
 }
+
+// make host-input chunks .. c visible on the session stream (no-op without a pipeline)
+int pipe_upto(ec_session *s, int c) {
+    auto &pp = s->pipe;
+    if (!pp.active) return EC_OK;
+    c = std::min(c, pp.nchunks - 1);
+    for (; pp.done <= c; pp.done++) {
+        const int i = pp.done;
+        EC_HIP(hipStreamWaitEvent(s->stream, s->pev[i], 0));
+        if (pp.packed && pp.bhi[i] > pp.blo[i]) {
+            const uint64_t units = ((pp.bhi[i] + 15) >> 4) - (pp.blo[i] >> 4);
+            k_unpack2<<<grid_for(units, 256, 16384), 256, 0, s->stream>>>(pp.codes, pp.blo[i], pp.bhi[i], pp.ascii);
+            if (pp.ehi[i] > pp.elo[i])
+                k_patch<<<grid_for(pp.ehi[i] - pp.elo[i], 256, 4096), 256, 0, s->stream>>>(
+                    pp.exc_pos, pp.exc_byte, pp.elo[i], pp.ehi[i], pp.ascii);
+        }
+    }
+    return EC_OK;
+}
+int pipe_all(ec_session *s) { return s->pipe.active ? pipe_upto(s, s->pipe.nchunks - 1) : EC_OK; }
 
 inline void mark(ec_session *s, int idx) {
     if (s->stage_timing) {
@@ -430,9 +471,9 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
                                                       recs, s->cnt.as<unsigned int>(), s->hll.as<uint8_t>(),      \
                                                       &dsc->nrec, &dsc->overflow)
 #define EC_SKPART_WV(NPF, W, VAL)                                                                             \
-    k_skpart_w<NPF, W, VAL><<<(unsigned)G, PT_THREADS, 0, st>>>(                                                 \
+    k_skpart_w<NPF, W, VAL><<<lgb - lga, PT_THREADS, 0, st>>>(                                                   \
         d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, recs, s->cnt.as<unsigned int>(),          \
-        s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow, &dsc->lens[2], &dsc->npos)
+        s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow, &dsc->lens[2], &dsc->npos, lga)
 #define EC_SKPART_W(NPF, W)            \
     if (validate)                      \
         EC_SKPART_WV(NPF, W, true);    \
@@ -443,8 +484,19 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     else if (npf == 7) EC_SKPART_W(7, W); \
     else EC_SKPART_W(10, W)
     // register-block minima for every window width of 21 <= k <= 32 (w = k - 14); the LDS-ring
-    // kernel stays for EULERHIP_SKPART_RING (A/B: 2.19 against 1.60 ms at k = 31)
-    if (!getenv("EULERHIP_SKPART_RING")) {
+    // kernel stays for EULERHIP_SKPART_RING (A/B: 2.19 against 1.60 ms at k = 31).
+    // Host input (s->pipe): one launch per arrived chunk, over the groups whose reads it completes
+    const bool chunked = s->pipe.active && s->pipe.done < s->pipe.nchunks && !getenv("EULERHIP_SKPART_RING");
+    if (!chunked) EC_CHECK(pipe_all(s));
+    unsigned lga = 0, lgb = (unsigned)G;
+    for (int pc = chunked ? 0 : s->pipe.nchunks; ; pc++) {
+      if (chunked) {
+        if (pc >= s->pipe.nchunks) break;
+        lgb = pc + 1 == s->pipe.nchunks ? (unsigned)G : (unsigned)std::min<uint64_t>(G, s->pipe.ravail[pc] / gsize);
+        if (lgb <= lga) continue;
+        EC_CHECK(pipe_upto(s, pc));
+      }
+      if (!getenv("EULERHIP_SKPART_RING")) {
         switch (mc.w) {
             case 7: EC_SKPART_NPF(7); break;
             case 8: EC_SKPART_NPF(8); break;
@@ -459,9 +511,12 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
             case 17: EC_SKPART_NPF(17); break;
             default: EC_SKPART_NPF(18); break;  // k = 32
         }
-    } else if (npf == 4) EC_SKPART(4);
-    else if (npf == 7) EC_SKPART(7);
-    else EC_SKPART(10);
+      } else if (npf == 4) EC_SKPART(4);
+      else if (npf == 7) EC_SKPART(7);
+      else EC_SKPART(10);
+      if (!chunked) break;
+      lga = lgb;
+    }
 #undef EC_SKPART_NPF
 #undef EC_SKPART_W
 #undef EC_SKPART_WV
@@ -620,13 +675,15 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     if (allow_sk2 && k >= SK_MIN_K && k <= 32 && !getenv("EULERHIP_NO_SK2") && !getenv("EULERHIP_SKPART_RING") &&
         !getenv("EULERHIP_NO_FASTSK2")) {
         uint64_t L = s->lc_L;  // (only a length the fast path then validates is reused)
-        if (!(L >= (uint64_t)k && npf_of(L) && s->lc_off == d_off && s->lc_n == nreads)) {
+        if (s->pipe.active) {
+            L = s->pipe.first_len;  // host input: the host knows it
+        } else if (!(L >= (uint64_t)k && npf_of(L) && s->lc_off == d_off && s->lc_n == nreads)) {
             uint64_t o2[2] = {0, 0};
             EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
             EC_HIP(hipStreamSynchronize(st));
             L = o2[1] - o2[0];
         }
-        s->lc_off = d_off, s->lc_n = nreads, s->lc_L = L;
+        s->lc_L = 0;  // cached again below only once the partition has validated it
         const int npf = npf_of(L);
         if (L >= (uint64_t)k && npf) {
             const uint32_t M = (uint32_t)(L - k + 1);
@@ -635,14 +692,15 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
             mark(s, 2 * EC_STAGE_PRESCAN + 1);
             EC_CHECK(phase_count_sk2(s, d_reads, d_off, nreads, read_base, k, limit, M, G, gsize, nreads * M, npf, U,
                                      sidx, done, true, &invalid));
-            if (done) {
+            if (done) {  // k_skpart_w<., ., true> checked every read against L
+                if (!s->pipe.active) s->lc_off = d_off, s->lc_n = nreads, s->lc_L = L;
                 ok = true;
                 return EC_OK;
             }
-            if (invalid) s->lc_L = 0;  // (a stale cached length fails the same check: re-read next call)
             if (!invalid) allow_sk2 = false;  // the estimate or a capacity declined: window records
         }
     }
+    EC_CHECK(pipe_all(s));
     mark(s, 2 * EC_STAGE_PRESCAN);
     kmark(s, 0, 0);
     k_prescan<<<(unsigned)G, 256, 0, st>>>(d_reads, d_off, nreads, k, gsize, &dsc->npos, &dsc->bad, dsc->lens);
@@ -857,6 +915,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
         EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
     }
+    EC_CHECK(pipe_all(s));
 
     // ---- prescan = partition upsweep ------------------------------------------------------
     mark(s, 2 * EC_STAGE_PRESCAN);
@@ -1882,12 +1941,82 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     unsigned int U = 0;
     if (k > 32) {
         SolidIndexW sidx{};
+        EC_CHECK(pipe_all(s));
         EC_CHECK(phase_count_w(s, d_reads, d_off, nreads, 0, k, (long long)limit, U, sidx));
         return phase_graph<OpsW>(s, k, U, sidx);
     }
     SolidIndex sidx{};
     EC_CHECK(phase_count(s, d_reads, d_off, nreads, 0, k, (long long)limit, flags, U, sidx));
     return phase_graph<Ops64>(s, k, U, sidx);
+}
+
+// ---- host input -------------------------------------------------------------------------------
+// Chunk plan over nbases bases (chunk boundaries at multiples of 64 bases, ~32 MiB of copied
+// bytes a chunk) and the reads each chunk completes (offsets: host array, or NULL = one length L)
+int pipe_plan(ec_session *s, uint64_t nbases, uint64_t bytes_per_base4, const uint64_t *offsets, uint64_t nreads,
+              uint64_t L) {
+    auto &pp = s->pipe;
+    const uint64_t copy_bytes = bytes_per_base4 ? (nbases + 3) / 4 : nbases;
+    int nc = (int)std::min<uint64_t>(64, std::max<uint64_t>(1, copy_bytes >> 25));
+    if (const char *e = getenv("EULERHIP_HOST_CHUNKS")) nc = std::max(1, std::min(64, atoi(e)));
+    pp.nchunks = nc;
+    pp.done = 0;
+    pp.blo.assign(nc, 0), pp.bhi.assign(nc, 0), pp.ravail.assign(nc, 0), pp.elo.assign(nc, 0), pp.ehi.assign(nc, 0);
+    for (int c = 0; c < nc; c++) {
+        pp.blo[c] = c ? pp.bhi[c - 1] : 0;
+        pp.bhi[c] = c + 1 == nc ? nbases : std::max<uint64_t>(pp.blo[c], (nbases * (uint64_t)(c + 1) / nc) & ~63ull);
+        uint64_t r;  // reads with offsets[r + 1] <= bhi
+        if (c + 1 == nc) r = nreads;
+        else if (!offsets) r = L ? std::min<uint64_t>(nreads, pp.bhi[c] / L) : nreads;
+        else r = (uint64_t)(std::upper_bound(offsets + 1, offsets + nreads + 1, pp.bhi[c]) - (offsets + 1));
+        pp.ravail[c] = r;
+    }
+    if ((int)s->pev.size() < nc) {
+        const size_t have = s->pev.size();
+        s->pev.resize(nc, nullptr);
+        for (size_t i = have; i < (size_t)nc; i++) EC_HIP(hipEventCreateWithFlags(&s->pev[i], hipEventDisableTiming));
+    }
+    if (!s->cstream) EC_HIP(hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking));
+    // the copies overwrite buffers the previous call's kernels may still read
+    EC_HIP(hipEventRecord(s->pev[0], s->stream));
+    EC_HIP(hipStreamWaitEvent(s->cstream, s->pev[0], 0));
+    return EC_OK;
+}
+
+// copy the offsets entries reads [r0, r1] need (chunk by chunk: [ravail[c-1] + 1, ravail[c] + 1))
+int pipe_copy_offsets(ec_session *s, int c, const uint64_t *offsets) {
+    auto &pp = s->pipe;
+    const uint64_t o0 = c ? pp.ravail[c - 1] + 1 : 0, o1 = pp.ravail[c] + 1;
+    if (o1 > o0)
+        EC_HIP(hipMemcpyAsync(s->h_offsets.as<uint64_t>() + o0, offsets + o0, (o1 - o0) * 8, hipMemcpyHostToDevice,
+                              s->cstream));
+    return EC_OK;
+}
+
+int check_offsets(const uint64_t *offsets, uint64_t nreads, uint64_t nbytes) {
+    if (offsets[nreads] > nbytes) {
+        set_error("offsets[nreads]=%llu > nbytes=%llu", (unsigned long long)offsets[nreads], (unsigned long long)nbytes);
+        return EC_ERR_ARG;
+    }
+    for (uint64_t i = 0; i < nreads; i++)
+        if (offsets[i] > offsets[i + 1]) {
+            set_error("offsets not monotone at %llu", (unsigned long long)i);
+            return EC_ERR_ARG;
+        }
+    return EC_OK;
+}
+
+// run assemble() on the pipelined input; the pipeline is drained (every chunk consumed) on any
+// return so no chunk copy is left pending against the next call's buffers
+int assemble_piped(ec_session *s, uint64_t nreads, int k, int limit, unsigned flags) {
+    s->pipe.active = true;
+    int rc = assemble(s, s->h_reads.as<uint8_t>(), s->h_offsets.as<uint64_t>(), nreads, k, limit, flags);
+    if (s->pipe.done < s->pipe.nchunks) {
+        pipe_all(s);
+        hipStreamSynchronize(s->stream);
+    }
+    s->pipe.active = false;
+    return rc;
 }
 
 }  // namespace
@@ -1957,6 +2086,13 @@ int ec_session_destroy(ec_session *s) {
         for (auto &e : s->ev) hipEventDestroy(e);
         for (auto &e : s->kev) hipEventDestroy(e);
     }
+    s->p_codes.release();
+    s->p_exc.release();
+    for (auto &e : s->pev) hipEventDestroy(e);
+    if (s->cstream) {
+        hipStreamSynchronize(s->cstream);
+        hipStreamDestroy(s->cstream);
+    }
     if (s->own_stream && s->stream) hipStreamDestroy(s->stream);
     delete s;
     return EC_OK;
@@ -1977,21 +2113,79 @@ int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const
         set_error("null argument");
         return EC_ERR_ARG;
     }
-    if (offsets[nreads] > nbytes) {
-        set_error("offsets[nreads]=%llu > nbytes=%llu", (unsigned long long)offsets[nreads], (unsigned long long)nbytes);
-        return EC_ERR_ARG;
-    }
-    for (uint64_t i = 0; i < nreads; i++)
-        if (offsets[i] > offsets[i + 1]) {
-            set_error("offsets not monotone at %llu", (unsigned long long)i);
-            return EC_ERR_ARG;
-        }
+    EC_CHECK(check_offsets(offsets, nreads, nbytes));
     EC_HIP(hipSetDevice(s->device));
     EC_CHECK(s->h_reads.ensure(nbytes + 16));
     EC_CHECK(s->h_offsets.ensure((nreads + 1) * 8));
-    if (nbytes) EC_HIP(hipMemcpyAsync(s->h_reads.p, reads, nbytes, hipMemcpyHostToDevice, s->stream));
-    EC_HIP(hipMemcpyAsync(s->h_offsets.p, offsets, (nreads + 1) * 8, hipMemcpyHostToDevice, s->stream));
-    return assemble(s, s->h_reads.as<uint8_t>(), s->h_offsets.as<uint64_t>(), nreads, k, limit, flags);
+    // chunked copies (reads and offsets) on the copy stream, the partition of the reads that
+    // have arrived overlapping the copies of the rest (s->pipe)
+    EC_CHECK(pipe_plan(s, nbytes, 0, offsets, nreads, 0));
+    auto &pp = s->pipe;
+    pp.packed = false;
+    pp.first_len = nreads ? offsets[1] - offsets[0] : 0;
+    pp.ascii = s->h_reads.as<uint8_t>();
+    for (int c = 0; c < pp.nchunks; c++) {
+        if (pp.bhi[c] > pp.blo[c])
+            EC_HIP(hipMemcpyAsync(s->h_reads.as<uint8_t>() + pp.blo[c], reads + pp.blo[c], pp.bhi[c] - pp.blo[c],
+                                  hipMemcpyHostToDevice, s->cstream));
+        EC_CHECK(pipe_copy_offsets(s, c, offsets));
+        EC_HIP(hipEventRecord(s->pev[c], s->cstream));
+    }
+    return assemble_piped(s, nreads, k, limit, flags);
+}
+
+int ec_assemble_packed_host(ec_session *s, const uint8_t *codes, uint64_t nbases, const uint64_t *offsets,
+                            uint64_t nreads, uint32_t read_len, const uint64_t *exc_pos, const uint8_t *exc_byte,
+                            uint64_t n_exc, int k, int limit, unsigned flags) {
+    if (!s || (nbases && !codes) || (n_exc && (!exc_pos || !exc_byte))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (offsets) {
+        EC_CHECK(check_offsets(offsets, nreads, nbases));
+    } else if ((uint64_t)read_len * nreads != nbases) {
+        set_error("%llu reads of %u bases != %llu bases", (unsigned long long)nreads, read_len,
+                  (unsigned long long)nbases);
+        return EC_ERR_ARG;
+    }
+    for (uint64_t i = 0; i < n_exc; i++)
+        if (exc_pos[i] >= nbases || (i && exc_pos[i] <= exc_pos[i - 1])) {
+            set_error("exception %llu: position %llu not ascending inside [0, %llu)", (unsigned long long)i,
+                      (unsigned long long)exc_pos[i], (unsigned long long)nbases);
+            return EC_ERR_ARG;
+        }
+    EC_HIP(hipSetDevice(s->device));
+    const uint64_t ncodes = (nbases + 3) / 4;
+    EC_CHECK(s->h_reads.ensure(nbases + 16));
+    EC_CHECK(s->h_offsets.ensure((nreads + 1) * 8));
+    EC_CHECK(s->p_codes.ensure(((ncodes + 3) & ~3ull) + 16));
+    EC_CHECK(s->p_exc.ensure(n_exc * 9 + 16));
+    EC_CHECK(pipe_plan(s, nbases, 1, offsets, nreads, read_len));
+    auto &pp = s->pipe;
+    pp.packed = true;
+    pp.first_len = nreads ? (offsets ? offsets[1] - offsets[0] : read_len) : 0;
+    pp.ascii = s->h_reads.as<uint8_t>();
+    pp.codes = s->p_codes.as<uint32_t>();
+    pp.exc_pos = s->p_exc.as<uint64_t>();
+    pp.exc_byte = s->p_exc.as<uint8_t>() + n_exc * 8;
+    if (n_exc) {
+        EC_HIP(hipMemcpyAsync(s->p_exc.p, exc_pos, n_exc * 8, hipMemcpyHostToDevice, s->cstream));
+        EC_HIP(hipMemcpyAsync(s->p_exc.as<uint8_t>() + n_exc * 8, exc_byte, n_exc, hipMemcpyHostToDevice, s->cstream));
+    }
+    if (!offsets)  // one read length: the offsets are made on the device
+        k_iota_off<<<grid_for(nreads + 1, 256, 16384), 256, 0, s->stream>>>(s->h_offsets.as<uint64_t>(), nreads + 1,
+                                                                            read_len);
+    for (int c = 0; c < pp.nchunks; c++) {
+        // code bytes of bases [blo, bhi) (blo a multiple of 64: whole 32-bit words)
+        const uint64_t c0 = pp.blo[c] / 4, c1 = c + 1 == pp.nchunks ? ncodes : pp.bhi[c] / 4;
+        if (c1 > c0)
+            EC_HIP(hipMemcpyAsync(s->p_codes.as<uint8_t>() + c0, codes + c0, c1 - c0, hipMemcpyHostToDevice, s->cstream));
+        if (offsets) EC_CHECK(pipe_copy_offsets(s, c, offsets));
+        pp.elo[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.blo[c]) - exc_pos);
+        pp.ehi[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.bhi[c]) - exc_pos);
+        EC_HIP(hipEventRecord(s->pev[c], s->cstream));
+    }
+    return assemble_piped(s, nreads, k, limit, flags);
 }
 
 int ec_get_stats(ec_session *s, ec_stats *out) {

@@ -293,7 +293,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
                                                          uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
                                                          uint32_t smask, uint4 *recs, unsigned int *cnt, uint8_t *hll,
                                                          unsigned long long *nrec, unsigned int *overflow,
-                                                         unsigned int *vfail, unsigned long long *npos) {
+                                                         unsigned int *vfail, unsigned long long *npos,
+                                                         uint32_t g_lo) {
     constexpr int C = 1 << SK2_CBITS;
     constexpr int NREG = 1 << HLL_REG_BITS;
     constexpr int SW = NPF * 64 + 4;
@@ -312,7 +313,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
     if (threadIdx.x < C) s_cur[threadIdx.x] = 0;
     if (lane < C) s_wcnt[wid][lane] = 0;
     __syncthreads();
-    const uint64_t g = blockIdx.x;
+    const uint64_t g = blockIdx.x + (uint64_t)g_lo;  // (host input: launched per chunk of groups)
     const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
     const uint32_t ntile = (uint32_t)((g1 - g0 + 63) / 64);
     const int k = mc.k, m = mc.m;

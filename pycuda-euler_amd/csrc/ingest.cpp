@@ -295,4 +295,74 @@ int ec_reads_copy(const ec_reads *r, uint64_t first, uint64_t count, uint8_t *ba
 
 void ec_reads_free(ec_reads *r) { delete r; }
 
+// ASCII -> 2 bits per base + exceptions (ec_assemble_packed_host's layout).  Threads own
+// base ranges aligned to 4 (whole code bytes); exceptions are counted per range, then written
+// at prefix-summed positions so they stay ascending.
+int ec_pack_reads(const uint8_t *reads, const uint64_t *offsets, uint64_t nreads, int threads, uint8_t *codes,
+                  uint64_t *exc_pos, uint8_t *exc_byte, uint64_t exc_cap, uint64_t *n_exc, uint32_t *read_len) {
+    if (!offsets || !n_exc || !read_len) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    const uint64_t nb = offsets[nreads];
+    if (nb && (!reads || !codes)) {
+        set_error("null reads / codes");
+        return EC_ERR_ARG;
+    }
+    int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (nb < (1u << 22)) T = 1;
+    std::vector<uint64_t> lo(T + 1), nexc(T, 0);
+    for (int t = 0; t <= T; t++) lo[t] = t == T ? nb : (nb * (uint64_t)t / T) & ~3ull;
+    std::vector<uint8_t> uni(T, 1);
+    // code of an ASCII byte (A 0, C 1, G 2, T 3) and whether the byte is exactly that letter
+    auto code = [](uint8_t c) { return (uint8_t)(((c >> 1) ^ (c >> 2)) & 3u); };
+    static const uint8_t letter[4] = {'A', 'C', 'G', 'T'};
+    auto pass = [&](int t, bool write) {
+        uint64_t e = 0, ebase = 0;
+        if (write)
+            for (int q = 0; q < t; q++) ebase += nexc[q];
+        for (uint64_t i = lo[t]; i < lo[t + 1]; i += 4) {
+            uint8_t byte = 0;
+            const int n = (int)std::min<uint64_t>(4, lo[t + 1] - i);
+            for (int j = 0; j < n; j++) {
+                const uint8_t c = reads[i + j], x = code(c);
+                byte |= (uint8_t)(x << (2 * j));
+                if (letter[x] != c) {
+                    if (write && ebase + e < exc_cap) {
+                        exc_pos[ebase + e] = i + j;
+                        exc_byte[ebase + e] = c;
+                    }
+                    e++;
+                }
+            }
+            if (write) codes[i >> 2] = byte;
+        }
+        if (!write) nexc[t] = e;
+        // one read length?  (reads [t n / T, (t + 1) n / T))
+        if (!write && nreads) {
+            const uint64_t r0 = nreads * (uint64_t)t / T, r1 = nreads * (uint64_t)(t + 1) / T;
+            const uint64_t L = offsets[1] - offsets[0];
+            for (uint64_t r = r0; r < r1; r++)
+                if (offsets[r + 1] - offsets[r] != L) {
+                    uni[t] = 0;
+                    break;
+                }
+        }
+    };
+    for (int phase = 0; phase < 2; phase++) {  // count, then write
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; t++) th.emplace_back(pass, t, phase == 1);
+        pass(0, phase == 1);
+        for (auto &x : th) x.join();
+    }
+    uint64_t tot = 0;
+    for (auto v : nexc) tot += v;
+    *n_exc = tot;
+    bool one = true;
+    for (auto v : uni) one &= v != 0;
+    const uint64_t L = nreads ? offsets[1] - offsets[0] : 0;
+    *read_len = (one && nreads && L <= 0xFFFFFFFFull && offsets[0] == 0) ? (uint32_t)L : 0u;
+    return EC_OK;
+}
+
 }  // extern "C"

@@ -100,6 +100,10 @@ _SIGS = {
     "ec_session_destroy": (ctypes.c_int, [_P]),
     "ec_assemble_device": (ctypes.c_int, [_P, _P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_assemble_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
+    "ec_assemble_packed_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_uint32, _P, _P, _U64, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_uint]),
+    "ec_pack_reads": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int, _P, _P, _P, _U64, ctypes.POINTER(_U64),
+                                     ctypes.POINTER(ctypes.c_uint32)]),
     "ec_assemble_from_kmers": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _U64, ctypes.c_int, ctypes.c_uint]),
     "ec_get_stats": (ctypes.c_int, [_P, ctypes.POINTER(Stats)]),
     "ec_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
@@ -164,6 +168,43 @@ def pack_reads(reads):
         off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
     buf = np.frombuffer(b"".join(bs), dtype=np.uint8)
     return buf, off
+
+
+class PackedReads:
+    """Reads 2 bits per base (include/eulerhip.h ec_assemble_packed_host): codes uint8[ceil(n/4)],
+    offsets uint64[nreads + 1] or None with read_len = the common length, and the bytes other than
+    A/C/G/T as (exc_pos uint64[], exc_byte uint8[])."""
+
+    def __init__(self, codes, nbases, nreads, offsets=None, read_len=0, exc_pos=None, exc_byte=None):
+        self.codes, self.nbases, self.nreads = codes, int(nbases), int(nreads)
+        self.offsets, self.read_len = offsets, int(read_len)
+        self.exc_pos = exc_pos if exc_pos is not None else np.zeros(0, np.uint64)
+        self.exc_byte = exc_byte if exc_byte is not None else np.zeros(0, np.uint8)
+
+
+def pack_2bit(buf, offsets, threads=0, alloc=None):
+    """ASCII CSR reads -> PackedReads (ec_pack_reads, host threads).  alloc(n) -> a uint8 array of
+    n bytes for the codes (e.g. page-locked memory); numpy by default."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    nb = int(offsets[-1]) if n >= 0 else 0
+    ncodes = (nb + 3) // 4
+    codes = alloc(max(ncodes, 1)) if alloc else np.empty(max(ncodes, 1), np.uint8)
+    nexc = ctypes.c_uint64(0)
+    rl = ctypes.c_uint32(0)
+    cap = 1 << 16
+    while True:
+        pos = np.empty(cap, np.uint64)
+        byt = np.empty(cap, np.uint8)
+        check(lib().ec_pack_reads(buf.ctypes.data if buf.size else None, offsets.ctypes.data, n, int(threads),
+                                  codes.ctypes.data, pos.ctypes.data, byt.ctypes.data, cap, ctypes.byref(nexc),
+                                  ctypes.byref(rl)))
+        if nexc.value <= cap:
+            break
+        cap = int(nexc.value)
+    ne = int(nexc.value)
+    return PackedReads(codes, nb, n, None if rl.value else offsets, rl.value, pos[:ne].copy(), byt[:ne].copy())
 
 
 class Result:
@@ -251,6 +292,15 @@ class Session:
         n = len(offsets) - 1
         pbuf = buf.ctypes.data if buf.size else None
         check(lib().ec_assemble_host(self._h, pbuf, buf.size, offsets.ctypes.data, n, int(k), int(limit), flags))
+
+    def run_packed_host(self, pr, k, limit=1, flags=0):
+        """Reads 2 bits per base in host memory (PackedReads): a quarter of run_host's PCIe bytes."""
+        off = None if pr.offsets is None else np.ascontiguousarray(pr.offsets, dtype=np.uint64)
+        ne = len(pr.exc_pos)
+        check(lib().ec_assemble_packed_host(
+            self._h, pr.codes.ctypes.data if pr.nbases else None, pr.nbases, None if off is None else off.ctypes.data,
+            pr.nreads, pr.read_len, pr.exc_pos.ctypes.data if ne else None, pr.exc_byte.ctypes.data if ne else None,
+            ne, int(k), int(limit), flags))
 
     def run_device(self, d_reads_ptr, d_offsets_ptr, nreads, k, limit=1, flags=0):
         """Reads already in HBM (e.g. torch uint8 / int64 tensors' data_ptr())."""

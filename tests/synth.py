@@ -6,6 +6,12 @@ import numpy as np
 LUT = np.frombuffer(b"ACGT", dtype=np.uint8)
 
 
+def make_genome(genome_len, seed):
+    """The genome make_reads(genome_len, ..., seed) samples from, as ASCII bytes."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return LUT[rng.integers(0, 4, genome_len, dtype=np.uint8)].tobytes()
+
+
 def make_reads(genome_len, n_reads, read_len, seed, err=0.0, n_rate=0.0, circular=False, rc_frac=0.5,
                part=None):
     """Returns (buf uint8[n_reads*read_len], offsets uint64[n_reads+1]) of ASCII reads.

@@ -1,0 +1,79 @@
+"""BASELINE.json configurations at full size on the HIP path (libeulerhip.so).
+
+* config 2 (4.6 Mbp, 1 M x 100 bp, k = 31) and config 3 (12 Mbp, 5 M x 100 bp, k = 31):
+  contigs, their offsets and the GFA link table bit-exact against the C oracle
+  (oracle/refasm.c, the restatement of referenceAssembler.py:25-111 pinned in test_oracle.py);
+* the headline read set (4.6 Mbp, 10 M x 100 bp, k = 31; config 4's data): size-independent
+  properties -- every k-mer of the error-free genome is solid (n_solid = G - k + 1) and the one
+  contig is the genome itself or its reverse complement (all_contigs:79-111 walks the unique
+  path of a repeat-free genome end to end);
+* config 5's read shape (150 bp reads, k = 51, 128-bit keys, 75-fold coverage) at 10^8
+  positions: bit-exact against the oracle.
+
+Inputs are synth.make_reads with the bench's seeds (20261015 + config#).
+"""
+import numpy as np
+import pytest
+
+import eulerhip
+import oracle
+from synth import make_genome, make_reads
+
+pytestmark = pytest.mark.gpu
+
+COMP = bytes.maketrans(b"ACGT", b"TGCA")
+
+
+def _check_vs_oracle(sess, buf, off, k, limit=1):
+    ref = oracle.assemble_packed(buf, off, k, limit)
+    sess.run_host(buf, off, k, limit)
+    res = sess.fetch(k)
+    assert res.stats.n_positions == ref["n_positions"]
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.stats.n_contigs == len(ref["contig_offsets"]) - 1
+    assert res.contig_bytes == ref["contig_chars"]
+    assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert np.array_equal(res.link_offsets, ref["link_offsets"])
+    assert np.array_equal(res.link_codes, ref["links"])
+    return res
+
+
+def test_config2_ecoli_1m_vs_oracle(gpu_session):
+    """BASELINE configs[1]: E. coli size, 1 M x 100 bp, k = 31"""
+    buf, off = make_reads(4_600_000, 1_000_000, 100, 20261015 + 2)
+    res = _check_vs_oracle(gpu_session, buf, off, 31)
+    assert res.stats.n_positions == 70_000_000
+
+
+def test_config3_yeast_5m_vs_oracle(gpu_session):
+    """BASELINE configs[2]: S. cerevisiae size, 5 M x 100 bp, k = 31"""
+    buf, off = make_reads(12_000_000, 5_000_000, 100, 20261015 + 3)
+    res = _check_vs_oracle(gpu_session, buf, off, 31)
+    assert res.stats.n_positions == 350_000_000
+
+
+def test_headline_10m_contig_is_the_genome(gpu_session):
+    """the metric's workload: 10 M x 100 bp of a 4.6 Mbp genome; the single contig is the
+    genome (or its reverse complement) and every genome k-mer is solid"""
+    G, k, seed = 4_600_000, 31, 20261015 + 4
+    buf, off = make_reads(G, 10_000_000, 100, seed)
+    genome = make_genome(G, seed)
+    gpu_session.run_host(buf, off, k, 1)
+    res = gpu_session.fetch(k)
+    st = res.stats
+    assert st.n_positions == 700_000_000
+    assert st.n_solid == G - k + 1
+    assert st.n_dict == 2 * (G - k + 1)
+    assert st.n_contigs == 1
+    c = res.contig_bytes
+    assert c == genome or c == genome.translate(COMP)[::-1]
+    # a linear contig has no GFA links (all_contigs:90-109: its ends extend nowhere)
+    assert st.n_links == 0
+
+
+def test_config5_shape_k51_vs_oracle(gpu_session):
+    """BASELINE configs[4]'s read shape: 150 bp reads, k = 51 (128-bit keys), 75-fold coverage
+    as 100 M reads of 200 Mbp give; 10^8 positions (1 M reads of a 2 Mbp genome)"""
+    buf, off = make_reads(2_000_000, 1_000_000, 150, 20261015 + 5)
+    res = _check_vs_oracle(gpu_session, buf, off, 51)
+    assert res.stats.n_positions == 100_000_000

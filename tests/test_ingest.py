@@ -104,3 +104,24 @@ def test_detect_format(tmp_path):
     assert ingest.detect_format(str(a)) == ingest.FASTQ
     assert ingest.detect_format("x.fna") == ingest.FASTA_RECORDS
     assert ingest.detect_format("x.fa", "lines") == ingest.FASTA_LINES
+
+
+def test_pack_2bit_roundtrip():
+    """ec_pack_reads (host): codes + exception bytes give the reads back; one-length detection"""
+    import eulerhip
+    from synth import make_reads
+
+    for L, nr in ((100, 0.0), (150, 0.01)):
+        buf, off = make_reads(50_000, 40_000, L, 11 + L, n_rate=nr)
+        buf = buf.copy()
+        buf[[5, 77, 4000]] = [ord("a"), ord("x"), ord("\n")]
+        pr = eulerhip.pack_2bit(buf, off, threads=4)
+        assert pr.read_len == L and pr.offsets is None and pr.nbases == buf.size
+        b = np.arange(pr.nbases)
+        asc = np.frombuffer(b"ACGT", np.uint8)[(pr.codes[b >> 2] >> (2 * (b & 3))) & 3].copy()
+        asc[pr.exc_pos] = pr.exc_byte
+        assert np.array_equal(asc, buf)
+        assert np.all(np.diff(pr.exc_pos.astype(np.int64)) > 0)
+    off2 = off.copy()
+    off2[1] += 1  # ragged
+    assert eulerhip.pack_2bit(buf, off2).read_len == 0

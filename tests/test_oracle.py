@@ -36,3 +36,27 @@ def test_g200_config1_is_empty_at_k21():
     (case,) = [c for c in golden_cases("g200.json") if c["k"] == 21]
     d, r, g = oracle.assemble(case["reads"], 21)
     assert d == [] and r == [] and g == []
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+@pytest.mark.parametrize("case", CASES[::5], ids=[c["name"] for c in CASES[::5]])
+def test_oracle_ncore_matches_reference(case, threads):
+    """the N-core map -> reduceByKey variant (bench.py's N-core CPU baseline) gives build()'s
+    dict order and all_contigs' results"""
+    d, r, g = oracle.assemble(case["reads"], case["k"], case["limit"], threads=threads)
+    assert d == case["d"]
+    assert r == case["contigs"]
+    assert g == case["links"]
+
+
+@pytest.mark.parametrize("k", [21, 31, 51])
+def test_oracle_ncore_synthetic(k):
+    import numpy as np
+    from synth import make_reads
+
+    buf, off = make_reads(60_000, 30_000, 100, 77 + k, err=0.003, n_rate=0.001)
+    a = oracle.assemble_packed(buf, off, k, 1, True)
+    b = oracle.assemble_packed(buf, off, k, 1, True, threads=6)
+    assert a["n_positions"] == b["n_positions"] and a["d"] == b["d"]
+    assert a["contig_chars"] == b["contig_chars"]
+    assert np.array_equal(a["links"], b["links"]) and np.array_equal(a["link_offsets"], b["link_offsets"])
