@@ -225,7 +225,6 @@ def main():
     ap.add_argument("--wide-records", action="store_true", help="16-B count records only (EC_FLAG_WIDE_RECORDS)")
     ap.add_argument("--window-records", action="store_true",
                     help="one record per k-mer window, no super-k-mers (EC_FLAG_WINDOW_RECORDS)")
-    ap.add_argument("--superkmer", action="store_true", help="super-k-mer records (EC_FLAG_SUPERKMER)")
     args = ap.parse_args()
     # stdout carries exactly one JSON line: libraries that print banners (RCCL prints its
     # version block on communicator init) are sent to stderr
@@ -276,8 +275,7 @@ def main():
         def step(timing=0):
             sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), cfg["reads"], k, 1, timing
                             | (eulerhip.EC_FLAG_WIDE_RECORDS if args.wide_records else 0)
-                            | (eulerhip.EC_FLAG_WINDOW_RECORDS if args.window_records else 0)
-                            | (eulerhip.EC_FLAG_SUPERKMER if args.superkmer else 0))
+                            | (eulerhip.EC_FLAG_WINDOW_RECORDS if args.window_records else 0))
     else:
         import distributed
 

@@ -54,13 +54,12 @@ typedef struct ec_session ec_session;
 #define EC_FLAG_WIDE_RECORDS 8u /* partitioned path: 16-B window records only (default for k < 21 or
                                   * reads with N: 12-B records when every read is N-free and of one length) */
 #define EC_FLAG_WINDOW_RECORDS 16u /* partitioned path: one record per k-mer window, never super-k-mers
-                                    * (neither count_sk2.h's default 16-B ones nor EC_FLAG_SUPERKMER's) */
+                                    * (never count_sk2.h's default 16-B super-k-mer records) */
 #define EC_FLAG_EXACT_COUNT 64u /* partitioned path: histogram-sized runs only (count_part.h), never the
                                   * fixed-capacity runs of count_v2.h */
-#define EC_FLAG_SUPERKMER 32u /* partitioned path: 32-B super-k-mer records on histogram-sized runs
-                                * (superkmer.h) where they apply: 21 <= k <= 32, N-free reads (else
-                                * window records); without flags, N-free reads of one length get
-                                * count_sk2.h's 16-B super-k-mer records (ec_stats.count_variant 3) */
+#define EC_FLAG_SUPERKMER 32u /* accepted and ignored: super-k-mer records (count_sk2.h, ec_stats.count_variant 3)
+                                * are the default where they apply -- N-free reads of one length,
+                                * 21 <= k <= 32; the 32-B record path this flag selected was removed */
 
 #define EC_NSTAGES 8
 /* stage ids for ec_stats.stage_ms / ec_stage_name */
@@ -83,7 +82,7 @@ typedef struct ec_session ec_session;
 
 #define EC_PATH_PARTITIONED 0 /* radix-partitioned LDS counting (count_part.h)               */
 #define EC_PATH_GENERAL 1     /* single HBM hash table (count_global.h)                      */
-#define EC_PATH_SUPERKMER 2   /* minimizer-partitioned super-k-mer records (superkmer.h)       */
+#define EC_PATH_SUPERKMER 2   /* no longer reported (the 32-B super-k-mer path was removed)     */
 
 typedef struct {
     uint64_t n_reads;

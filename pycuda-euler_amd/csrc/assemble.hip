@@ -315,6 +315,7 @@ void collect_timing(ec_session *s) {
 // per-call setup shared by every entry point: argument checks, stats reset, timing events,
 // zeroed device scalars
 int begin_call(ec_session *s, int k, unsigned flags) {
+    refresh_knobs();
     s->have = false;
     s->stats_ok = false;
     if (k < 1 || k > EC_MAX_K) {
@@ -412,9 +413,9 @@ BucketPlan plan_buckets(double est, long long limit, bool filt_ok) {
     BucketPlan p;
     const double filt_max = limit >= 1 ? 32768.0 : PART_KEYS * (1 << PMAX);
     p.part = est / FINE <= 2400.0 || (filt_ok && est / FINE <= filt_max);
-    p.filt = p.part && filt_ok && (est / FINE > 2400.0 || getenv("EULERHIP_FORCE_FILTER"));
+    p.filt = p.part && filt_ok && (est / FINE > 2400.0 || kn().force_filter);
     while (p.pmax < PMAX && est / FINE / (double)(1 << p.pmax) > PART_KEYS) p.pmax++;
-    if (const char *e = getenv("EULERHIP_FILTER_PMAX")) p.pmax = std::max(1, std::min(PMAX, atoi(e)));
+    if (kn().filter_pmax) p.pmax = std::max(1, std::min(PMAX, kn().filter_pmax));
     while (p.bbits < FINE_BITS && est / (double)(1ull << p.bbits) > 1100.0) p.bbits++;
     p.slots = p.filt ? (2048u << p.pmax) : est / (double)(1ull << p.bbits) > 1100.0 ? 4096u : 2048u;
     return p;
@@ -434,7 +435,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     done = false;
     if (invalid) *invalid = false;
     if (k < SK_MIN_K || k > 32 || M > 256 || gsize * M >= (1ull << 24) || (read_base + nreads) * 2 * M >= (1ull << 32) ||
-        getenv("EULERHIP_NO_SK2"))
+        kn().no_sk2)
         return EC_OK;
     hipStream_t st = s->stream;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -456,7 +457,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     // records per read ~ 2 M / (w + 1) + 1 on random sequence; 40 % headroom per run
     const double per_read = 2.0 * M / (mc.w + 1) + 2.0;
     const uint64_t cap = (uint64_t)(gsize * per_read * 1.4 / C) + 256;
-    EC_CHECK(s->recs.ensure((C * G * cap + SK2_ECAP) * 16));
+    EC_CHECK(s->recs.ensure((C * G * cap + SK2_ECAP_W) * 16));  // + the spill records
     EC_CHECK(s->cnt.ensure(C * G * 4));
     EC_CHECK(s->hll.ensure(G * (1 << HLL_REG_BITS)));
     EC_CHECK(s->ftot.ensure((1 << HLL_REG_BITS) * 4));
@@ -466,10 +467,6 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_HIP(hipMemsetAsync(&dsc->nrec, 0, sizeof(unsigned long long), st));
     mark(s, 2 * EC_STAGE_COUNT);
     kmark(s, 1, 0);
-#define EC_SKPART(NPF)                                                                                        \
-    k_skpart<NPF><<<(unsigned)G, PT_THREADS, 0, st>>>(d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, \
-                                                      recs, s->cnt.as<unsigned int>(), s->hll.as<uint8_t>(),      \
-                                                      &dsc->nrec, &dsc->overflow)
 #define EC_SKPART_WV(NPF, W, VAL)                                                                             \
     k_skpart_w<NPF, W, VAL><<<lgb - lga, PT_THREADS, 0, st>>>(                                                   \
         d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, recs, s->cnt.as<unsigned int>(),          \
@@ -483,10 +480,10 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     if (npf == 4) EC_SKPART_W(4, W);  \
     else if (npf == 7) EC_SKPART_W(7, W); \
     else EC_SKPART_W(10, W)
-    // register-block minima for every window width of 21 <= k <= 32 (w = k - 14); the LDS-ring
-    // kernel stays for EULERHIP_SKPART_RING (A/B: 2.19 against 1.60 ms at k = 31).
+    // register-block minima for every window width of 21 <= k <= 32 (w = k - 14; an LDS-ring
+    // sliding minimum measured 2.19 against 1.60 ms at k = 31).
     // Host input (s->pipe): one launch per arrived chunk, over the groups whose reads it completes
-    const bool chunked = s->pipe.active && s->pipe.done < s->pipe.nchunks && !getenv("EULERHIP_SKPART_RING");
+    const bool chunked = s->pipe.active && s->pipe.done < s->pipe.nchunks;
     if (!chunked) EC_CHECK(pipe_all(s));
     unsigned lga = 0, lgb = (unsigned)G;
     for (int pc = chunked ? 0 : s->pipe.nchunks; ; pc++) {
@@ -496,7 +493,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         if (lgb <= lga) continue;
         EC_CHECK(pipe_upto(s, pc));
       }
-      if (!getenv("EULERHIP_SKPART_RING")) {
+      {
         switch (mc.w) {
             case 7: EC_SKPART_NPF(7); break;
             case 8: EC_SKPART_NPF(8); break;
@@ -511,23 +508,20 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
             case 17: EC_SKPART_NPF(17); break;
             default: EC_SKPART_NPF(18); break;  // k = 32
         }
-      } else if (npf == 4) EC_SKPART(4);
-      else if (npf == 7) EC_SKPART(7);
-      else EC_SKPART(10);
+      }
       if (!chunked) break;
       lga = lgb;
     }
 #undef EC_SKPART_NPF
 #undef EC_SKPART_W
 #undef EC_SKPART_WV
-#undef EC_SKPART
     kmark(s, 1, 1);
     EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));
     k_hll_merge<<<dim3((1 << HLL_REG_BITS) / 256, TOT_SLICES), 256, 0, st>>>(s->hll.as<uint8_t>(), G, hreg);
     k_hll_final<<<1, 1024, 0, st>>>(hreg, HLL_REG_BITS, &dsc->est);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
-    const bool verbose = getenv("EULERHIP_VERBOSE") != nullptr;
+    const bool verbose = kn().verbose;
     if (validate) {
         if (hsc.lens[2]) {  // a read of another length, a byte outside ACGT, an oversized tile
             if (verbose) fprintf(stderr, "count_sk2: input needs the prescan\n");
@@ -541,7 +535,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         return reset();
     }
     const double est = hsc.est * (smask + 1.0);
-    BucketPlan plan = plan_buckets(est, limit, !getenv("EULERHIP_NO_FILTER"));
+    BucketPlan plan = plan_buckets(est, limit, !kn().no_filter);
     if (!plan.part || plan.filt) return reset();  // error-rich: window records with the seen-twice filter
     // up to 2^SK2_BBITS buckets of <= 1100 estimated keys (2048-slot tables: two workgroups per
     // CU).  Measured: 16384 buckets of 1024 slots (three workgroups per CU) were not faster, and
@@ -563,7 +557,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_CHECK(s->bb2.ensure(Bk * 16));
     EC_HIP(hipMemsetAsync(s->fcur.p, 0, Bk * 8, st));
     unsigned rs = 8;
-    if (const char *e = getenv("EULERHIP_REFINE_RS")) rs = (unsigned)std::max(1, atoi(e));
+    if (kn().refine_rs) rs = (unsigned)std::max(1, kn().refine_rs);
     rs = (unsigned)std::min<uint64_t>(rs, G);
     kmark(s, 4, 0);
     k_skrefine<<<dim3((unsigned)C, rs), BUCKET_THREADS, 0, st>>>(recs, s->cnt.as<unsigned int>(), (uint32_t)G, cap, bbits,
@@ -585,33 +579,49 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
     kmark(s, 2, 0);
     const double inv_m = 1.0 / M;
-    // experiments: duplicate records merged before their windows are inserted (EULERHIP_SK2_DEDUPE=1
-    // or 2 records per thread; measured slower)
-    const int dedupe = getenv("EULERHIP_SK2_DEDUPE") ? atoi(getenv("EULERHIP_SK2_DEDUPE")) : 0;
-#define EC_SKBUCKET(SLOTS, EVEN)                                                                              \
-    (dedupe == 2 ? k_skbucket_dd<SLOTS, EVEN, 2> : dedupe ? k_skbucket_dd<SLOTS, EVEN, 1> : k_skbucket<SLOTS, EVEN>)<<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(   \
-        s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(),                \
+    // records deduplicated per bucket before their windows are rolled out (k_skbucket); the
+    // record-per-lane kernel k_skbucket_rec for A/B (EULERHIP_SK2_NODEDUP=1)
+    const bool nodedup = kn().sk2_nodedup;
+#define EC_SKBUCKET_ARGS                                                                                     \
+    s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(),                    \
         s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),          \
-        s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow)
+        s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow
+#define EC_SKBUCKET(SLOTS, RS, EVEN)                                                                          \
+    do {                                                                                                      \
+        if (nodedup)                                                                                          \
+            k_skbucket_rec<SLOTS, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS);             \
+        else if (kn().sk2_rb == 2)                                                                            \
+            k_skbucket<SLOTS, RS, 2, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg);     \
+        else if (kn().sk2_rb == 1)                                                                            \
+            k_skbucket<SLOTS, RS, 1, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg);     \
+        else                                                                                                  \
+            k_skbucket<SLOTS, RS, 4, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg);     \
+    } while (0)
+    // EULERHIP_SK2_STATS: distinct records, flushes and windows rolled out (stderr)
+    unsigned long long *dbg = nullptr;
+    if (kn().sk2_stats && !nodedup) {
+        EC_CHECK(s->tmp.ensure(64));
+        dbg = s->tmp.as<unsigned long long>();
+        EC_HIP(hipMemsetAsync(dbg, 0, 64, st));
+    }
     if (plan.slots == 2048) {
-        if (k & 1) EC_SKBUCKET(2048, false);
-        else EC_SKBUCKET(2048, true);
+        if (k & 1) EC_SKBUCKET(2048, 3072, false);
+        else EC_SKBUCKET(2048, 3072, true);
     } else {
-        if (k & 1) EC_SKBUCKET(4096, false);
-        else EC_SKBUCKET(4096, true);
+        if (k & 1) EC_SKBUCKET(4096, 2048, false);
+        else EC_SKBUCKET(4096, 2048, true);
     }
 #undef EC_SKBUCKET
-#ifdef SK2_DD_TIMING
-    {
-        unsigned long long t[4];
+#undef EC_SKBUCKET_ARGS
+    if (dbg) {
+        unsigned long long h[8];
+        EC_HIP(hipMemcpyAsync(h, dbg, 64, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
-        EC_HIP(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sk2_dd_t), sizeof(t)));
-        fprintf(stderr, "sk2_dd phases (block-us summed): merge %.0f sort %.0f insert %.0f fin %.0f\n", t[0] / 100.0,
-                t[1] / 100.0, t[2] / 100.0, t[3] / 100.0);
-        memset(t, 0, sizeof(t));
-        EC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sk2_dd_t), t, sizeof(t)));
+        fprintf(stderr, "k_skbucket: %llu records, %llu distinct in %llu flushes (%.2f / bucket), %llu windows rolled "
+                        "(positions %llu); block-us: init %.0f records %.0f sort %.0f roll-out %.0f finish %.0f\n",
+                (unsigned long long)NR, h[0], h[1], (double)h[1] / Bk, h[2], (unsigned long long)P, h[3] / 100.0,
+                h[4] / 100.0, h[5] / 100.0, h[6] / 100.0, h[7] / 100.0);
     }
-#endif
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -662,7 +672,6 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     // read groups of whole 64-read wave tiles, at most 2048 (k_refine2 run tables)
     const uint64_t ntiles = (nreads + 63) / 64;
     uint64_t gmax = RF_MAX_RUNS;
-    if (const char *e = getenv("EULERHIP_V2_GROUPS")) gmax = std::min<uint64_t>(RF_MAX_RUNS, std::max(1, atoi(e)));
     uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, gmax));
     const uint64_t gsize = ((ntiles + G - 1) / G) * 64;
     G = (nreads + gsize - 1) / gsize;
@@ -672,8 +681,7 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     };
     // super-k-mer fast path without the prescan (count_sk2.h, k_skpart_w<., ., true>): the
     // read length of the first read; the partition checks the rest
-    if (allow_sk2 && k >= SK_MIN_K && k <= 32 && !getenv("EULERHIP_NO_SK2") && !getenv("EULERHIP_SKPART_RING") &&
-        !getenv("EULERHIP_NO_FASTSK2")) {
+    if (allow_sk2 && k >= SK_MIN_K && k <= 32 && !kn().no_sk2) {
         uint64_t L = s->lc_L;  // (only a length the fast path then validates is reused)
         if (s->pipe.active) {
             L = s->pipe.first_len;  // host input: the host knows it
@@ -739,7 +747,7 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
         while ((1ull << b) < x) b++;
         return b;
     };
-    const int r10env = getenv("EULERHIP_V2_R10") ? atoi(getenv("EULERHIP_V2_R10")) : -1;
+    const int r10env = kn().v2_r10;
     const bool r10 = r10env != 0 && (r10env == 1 || P >= (1ull << 26)) && k >= 16 &&
                      (2 * k - PT_CBITS) + std::max(0, nbits(gsize) + 1 + ibits - 16) <= 64;
 
@@ -787,7 +795,7 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     EC_HIP(hipStreamSynchronize(st));
     if (hsc.overflow) return EC_OK;  // a run outgrew its capacity (extreme skew)
     const double est = hsc.est * (smask + 1.0);
-    BucketPlan plan = plan_buckets(est, limit, !getenv("EULERHIP_NO_FILTER"));
+    BucketPlan plan = plan_buckets(est, limit, !kn().no_filter);
     if (!plan.part) return EC_OK;
     plan.bbits = std::max(plan.bbits, PT_CBITS);
     const int bbits = plan.bbits;
@@ -800,7 +808,7 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     EC_CHECK(s->bb2.ensure(Bk * 16));
     EC_HIP(hipMemsetAsync(s->fcur.p, 0, Bk * 8, st));
     unsigned rs = 8;
-    if (const char *e = getenv("EULERHIP_REFINE_RS")) rs = (unsigned)std::max(1, atoi(e));
+    if (kn().refine_rs) rs = (unsigned)std::max(1, kn().refine_rs);
     rs = (unsigned)std::min<uint64_t>(rs, G);
     kmark(s, 4, 0);
 #define EC_REFINE(IN10)                                                                                           \
@@ -826,8 +834,8 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     EC_CHECK(s->dft.ensure(umax * 8));
     EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
     s->pmax = plan.pmax;
-    s->part_keys = getenv("EULERHIP_PART_KEYS") ? (float)atof(getenv("EULERHIP_PART_KEYS")) : (float)PART_KEYS;
-    s->pmin = getenv("EULERHIP_FILTER_PMIN") ? std::max(0, std::min(plan.pmax, atoi(getenv("EULERHIP_FILTER_PMIN")))) : 0;
+    s->part_keys = kn().part_keys > 0 ? kn().part_keys : (float)PART_KEYS;
+    s->pmin = kn().filter_pmin >= 0 ? std::max(0, std::min(plan.pmax, kn().filter_pmin)) : 0;
     s->filt = plan.filt;
     s->bbeg = bbeg;
     s->bend = bend;
@@ -906,8 +914,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc;
-    if (!(flags & (EC_FLAG_GENERAL | EC_FLAG_WIDE_RECORDS | EC_FLAG_SUPERKMER | EC_FLAG_EXACT_COUNT)) && nreads &&
-        k <= 32 && !getenv("EULERHIP_NO_V2")) {
+    if (!(flags & (EC_FLAG_GENERAL | EC_FLAG_WIDE_RECORDS | EC_FLAG_EXACT_COUNT)) && nreads &&
+        k <= 32 && !kn().no_v2) {
         bool ok = false;
         EC_CHECK(phase_count_v2(s, d_reads, d_off, nreads, read_base, k, limit, !(flags & EC_FLAG_WINDOW_RECORDS), U,
                                 sidx, ok));
@@ -921,45 +929,18 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     mark(s, 2 * EC_STAGE_PRESCAN);
     const uint64_t ntiles = (nreads + TILE_READS - 1) / TILE_READS;
     uint64_t maxg = 2048;
-    if (const char *e = getenv("EULERHIP_MAX_GROUPS")) maxg = std::max(1, atoi(e));
     uint64_t ngroups = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, maxg));
     const uint64_t gsize = std::max<uint64_t>(1, (ntiles + ngroups - 1) / ngroups) * TILE_READS;
     ngroups = std::max<uint64_t>(1, (nreads + gsize - 1) / gsize);
     EC_CHECK(s->hist.ensure(ngroups * FINE * 4));
     EC_CHECK(s->hll.ensure(ngroups * (1 << HLL_REG_BITS)));
     EC_CHECK(s->ftot.ensure((FINE + (1 << HLL_REG_BITS)) * 8));
-    // super-k-mer counting (superkmer.h) for 21 <= k <= 32 unless window records are asked for;
-    // it needs every read N-free and staged, else the window-record upsweep reruns
-    bool sk = !(flags & (EC_FLAG_GENERAL | EC_FLAG_WIDE_RECORDS | EC_FLAG_WINDOW_RECORDS)) &&
-              ((flags & EC_FLAG_SUPERKMER) || SK_DEFAULT) && k >= SK_MIN_K && k <= 32 && nreads;
-    const MinCfg mc = sk_cfg(k);
     if (nreads) {
         kmark(s, 0, 0);
-        if (sk)
-            k_upsweep_sk<<<(unsigned)ngroups, TILE_READS, 0, st>>>(
-                d_reads, d_off, nreads, mc, gsize, s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), &dsc->npos,
-                &dsc->bad, &dsc->maxlocal, &dsc->skew, dsc->lens, &dsc->nrec);
-        else
-            k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
-                                                               s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
-                                                               &dsc->npos, &dsc->bad, &dsc->maxlocal, &dsc->skew,
-                                                               dsc->lens);
+        k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
+                                                           s->hll.as<uint8_t>(), &dsc->npos, &dsc->bad, &dsc->maxlocal,
+                                                           &dsc->skew, dsc->lens);
         kmark(s, 0, 1);
-        if (sk) {
-            EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-            EC_HIP(hipStreamSynchronize(st));
-            if (hsc.bad == ~0ull && (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT)) {
-                sk = false;
-                EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
-                EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
-                kmark(s, 0, 0);
-                k_upsweep<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
-                                                                   s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
-                                                                   &dsc->npos, &dsc->bad, &dsc->maxlocal,
-                                                                   &dsc->skew, dsc->lens);
-                kmark(s, 0, 1);
-            }
-        }
         EC_HIP(hipMemsetAsync(s->ftot.p, 0, (FINE + (1 << HLL_REG_BITS)) * 8, st));
         k_fine_totals<<<dim3(FINE / 256, TOT_SLICES), 256, 0, st>>>(
             s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), ngroups, s->ftot.as<unsigned long long>(),
@@ -988,17 +969,17 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     // k_bucket_filt also splits a bucket into up to 2^PMAX part tables (large genomes; with
     // limit < 1 -- shard counts, no filter possible -- every key is kept)
     constexpr int PMAX = 3;
-    const bool filt_ok = !sk && !getenv("EULERHIP_NO_FILTER");
+    const bool filt_ok = !kn().no_filter;
     const double filt_max = limit >= 1 ? 32768.0 : PART_KEYS * (1 << PMAX);
     bool part = !(flags & EC_FLAG_GENERAL) && nreads && P && hsc.maxlocal <= MAX_LOCAL_EVENT && !hsc.skew &&
                 (est / FINE <= 2400.0 || (filt_ok && est / FINE <= filt_max));
-    const bool filt = part && filt_ok && (est / FINE > 2400.0 || getenv("EULERHIP_FORCE_FILTER"));
+    const bool filt = part && filt_ok && (est / FINE > 2400.0 || kn().force_filter);
     int pmax = 1;  // part tables per bucket region: 2^pmax (filter mode)
     while (pmax < PMAX && est / FINE / (double)(1 << pmax) > PART_KEYS) pmax++;
-    if (const char *e = getenv("EULERHIP_FILTER_PMAX")) pmax = std::max(1, std::min(PMAX, atoi(e)));
+    if (kn().filter_pmax) pmax = std::max(1, std::min(PMAX, kn().filter_pmax));
     s->pmax = pmax;
-    s->part_keys = getenv("EULERHIP_PART_KEYS") ? (float)atof(getenv("EULERHIP_PART_KEYS")) : (float)PART_KEYS;
-    s->pmin = getenv("EULERHIP_FILTER_PMIN") ? std::max(0, std::min(pmax, atoi(getenv("EULERHIP_FILTER_PMIN")))) : 0;
+    s->part_keys = kn().part_keys > 0 ? kn().part_keys : (float)PART_KEYS;
+    s->pmin = kn().filter_pmin >= 0 ? std::max(0, std::min(pmax, kn().filter_pmin)) : 0;
     int bbits = 0;
     unsigned int slots = 2048;
     sidx = SolidIndex{};
@@ -1006,15 +987,11 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
     if (part) {
         while (bbits < FINE_BITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
         slots = filt ? (2048u << pmax) : est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
-        int maxc = MAX_COARSE_BITS;
-        if (const char *e = getenv("EULERHIP_COARSE_BITS")) maxc = std::max(1, std::min(MAX_COARSE_BITS, atoi(e)));
-        maxc = std::min(maxc, DS_MAX_CBITS);
         // fewest coarse buckets the refine fan-out allows: longer downsweep runs (measured:
         // 128 vs 256 coarse buckets, k_downsweep 5.56 -> 4.98 ms at 10M x 100 bp)
         int fan = 0;
         while ((1 << (fan + 1)) <= REFINE_FANOUT) fan++;
         int cbits = std::min(bbits, std::max(1, bbits - fan));
-        if (getenv("EULERHIP_COARSE_BITS")) cbits = std::min(bbits, std::max(maxc, bbits - fan));
         const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
         mark(s, 2 * EC_STAGE_COUNT);
         EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
@@ -1023,19 +1000,19 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
         // compact 12-B records: every read staged and N-free, one read length, events fit
         const unsigned int lmax = hsc.lens[0], lmin = ~hsc.lens[1];
-        bool compact = !sk && !(flags & EC_FLAG_WIDE_RECORDS) && hsc.lens[2] == 0 && hsc.lens[1] != 0 && lmax == lmin;
+        bool compact = !(flags & EC_FLAG_WIDE_RECORDS) && hsc.lens[2] == 0 && hsc.lens[1] != 0 && lmax == lmin;
         int ibits = 1;
         if (compact) {
             const uint64_t m = (uint64_t)lmax - (uint64_t)k + 1;
             while ((1ull << ibits) < m) ibits++;
             compact = ibits <= 15 && nreads + read_base <= (1ull << (31 - ibits));
         }
-        const uint64_t NR = sk ? hsc.nrec : P;  // records
-        const size_t rsz = sk ? sizeof(SkRec) : compact ? sizeof(Rec12) : sizeof(Rec);
+        const uint64_t NR = P;  // records
+        const size_t rsz = compact ? sizeof(Rec12) : sizeof(Rec);
         s->stats.record_bytes = (uint32_t)rsz;
         s->stats.n_records = NR;
         EC_CHECK(s->recs.ensure(NR * rsz));
-        if (bbits > cbits) EC_CHECK(s->recs2.ensure(NR * (sk ? sizeof(SkRec) : sizeof(Rec))));  // refine output
+        if (bbits > cbits) EC_CHECK(s->recs2.ensure(NR * sizeof(Rec)));  // refine output
         k_coarse<<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
                                                                s->cnt.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ngroups));
@@ -1044,14 +1021,10 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
         // compact records: keys [0, 8P) and meta [8P, 12P) of the first record buffer
         const Store12 c1{s->recs.as<unsigned long long>(), reinterpret_cast<unsigned int *>(s->recs.as<uint8_t>() + P * 8)};
-        // refine output of compact records: packed 12-B records (EULERHIP_PACK12=0: widened to 16 B)
-        const bool pack12 = !(getenv("EULERHIP_PACK12") && atoi(getenv("EULERHIP_PACK12")) == 0);
+        // refine output of compact records: packed 12-B records
+        const bool pack12 = true;
         kmark(s, 1, 0);
-        if (sk)
-            k_downsweep_sk<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, mc, gsize, ngroups, cbits,
-                                                                    s->offs.as<unsigned long long>(),
-                                                                    s->recs.as<SkRec>(), read_base);
-        else if (compact)
+        if (compact)
             k_downsweep<Rec12, MakeRec12, Store12><<<(unsigned)ngroups, TILE_READS, 0, st>>>(
                 d_reads, d_off, nreads, k, gsize, ngroups, cbits, s->offs.as<unsigned long long>(), c1,
                 MakeRec12{read_base, ibits});
@@ -1064,16 +1037,12 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         if (bbits > cbits) {
             // split every coarse bucket over RS workgroups (>= 4 per CU in flight)
             unsigned rsmax = 8;
-            if (const char *e = getenv("EULERHIP_REFINE_RS")) rsmax = (unsigned)std::max(1, atoi(e));
+            if (kn().refine_rs) rsmax = (unsigned)std::max(1, kn().refine_rs);
             const unsigned RS = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(rsmax, 1024 * rsmax / 8 / Ck));
             EC_CHECK(s->gcur.ensure(Bk * 8));
             EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
             kmark(s, 4, 0);
-            if (sk)
-                k_refine<SkRec, StoreSk, StoreSk><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
-                    StoreSk{s->recs.as<SkRec>()}, StoreSk{s->recs2.as<SkRec>()}, s->bstart.as<unsigned long long>(),
-                    s->gcur.as<unsigned long long>(), cbits, bbits);
-            else if (compact && pack12)  // 12-B in, packed 12-B out
+            if (compact && pack12)  // 12-B in, packed 12-B out
                 k_refine<Rec12, Store12, Store12P><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
                     c1, Store12P{s->recs2.as<unsigned int>()}, s->bstart.as<unsigned long long>(),
                     s->gcur.as<unsigned long long>(), cbits, bbits);
@@ -1098,19 +1067,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
         kmark(s, 2, 0);
         s->filt = filt;
-        if (sk) {
-            const SkRec *sr = second ? s->recs2.as<SkRec>() : s->recs.as<SkRec>();
-            if (slots == 2048)
-                k_bucket_sk<2048><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
-                    sr, s->bstart.as<unsigned long long>(), k, (long long)limit, s->dkey.as<unsigned long long>(),
-                    s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-                    s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
-            else
-                k_bucket_sk<4096><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
-                    sr, s->bstart.as<unsigned long long>(), k, (long long)limit, s->dkey.as<unsigned long long>(),
-                    s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-                    s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
-        } else if (compact && second && pack12) {
+        if (compact && second && pack12) {
             const unsigned int m2 = (unsigned int)(2 * ((uint64_t)lmax - k + 1) - 1);
             if (k & 1) {
                 Rec12PSource<false> src;
@@ -1151,11 +1108,10 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
             sidx.sub = s->sub.as<SubSlot>();
             sidx.bbits = bbits;
             sidx.slots = slots;
-            sidx.sk = sk ? 1 : 0;
+            sidx.sk = 0;
             sidx.npb = filt ? s->bnp.as<uint8_t>() : nullptr;
             sidx.pmax = pmax;
-            sidx.mc = mc;
-            s->stats.count_path = sk ? EC_PATH_SUPERKMER : EC_PATH_PARTITIONED;
+            s->stats.count_path = EC_PATH_PARTITIONED;
             s->stats.n_buckets = (uint32_t)Bk;
             s->stats.table_capacity = umax;
         }
@@ -1218,7 +1174,7 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
 // bucket): no HBM atomics.  Returns EC_OK with ok = false when a bucket overflows its table.
 // minimizer buckets for the merge / load of 21 <= k <= 32 (shard.h OwnerFn; EULERHIP_MERGE_MIX=1:
 // key-hash buckets and owners, the round-1 layout)
-bool merge_sk(int k) { return k >= SK_MIN_K && k <= 32 && !getenv("EULERHIP_MERGE_MIX"); }
+bool merge_sk(int k) { return k >= SK_MIN_K && k <= 32 && !kn().merge_mix; }
 OwnerFn owner_fn(int k) {
     OwnerFn f{};
     f.sk = merge_sk(k) ? 1 : 0;
@@ -1492,7 +1448,7 @@ int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, S
 int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads,
                       uint64_t read_base, int k, long long limit, unsigned int &U, SolidIndexW &sidx, bool &ok) {
     ok = false;
-    if ((s->flags & EC_FLAG_GENERAL) || !nreads || getenv("EULERHIP_WIDE_GENERAL")) return EC_OK;
+    if ((s->flags & EC_FLAG_GENERAL) || !nreads || kn().wide_general) return EC_OK;
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -1505,7 +1461,6 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     mark(s, 2 * EC_STAGE_PRESCAN);
     const uint64_t ntiles = (nreads + TILE_READS - 1) / TILE_READS;
     uint64_t maxg = 2048;
-    if (const char *e = getenv("EULERHIP_MAX_GROUPS")) maxg = std::max(1, atoi(e));
     uint64_t ngroups = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, maxg));
     const uint64_t gsize = std::max<uint64_t>(1, (ntiles + ngroups - 1) / ngroups) * TILE_READS;
     ngroups = std::max<uint64_t>(1, (nreads + gsize - 1) / gsize);
@@ -1529,7 +1484,6 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     const uint64_t P = hsc.npos;
     const double est = hsc.est;
     double per_max = 1800.0;  // keys per bucket table (SLOTS_W slots)
-    if (const char *e = getenv("EULERHIP_WIDE_BUCKET_MAX")) per_max = atof(e);
     if (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT || !P || est / FINE_W > per_max) return reset();
     s->stats.n_reads = nreads;
     s->stats.n_positions = P;
@@ -1537,7 +1491,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
 
     int bbits = 0;
     int maxb = FINE_W_BITS;  // (EULERHIP_WIDE_MAX_BBITS: tests force bucket overflow)
-    if (const char *e = getenv("EULERHIP_WIDE_MAX_BBITS")) maxb = std::max(0, std::min(FINE_W_BITS, atoi(e)));
+    if (kn().wide_max_bbits >= 0) maxb = std::max(0, std::min(FINE_W_BITS, kn().wide_max_bbits));
     while (bbits < maxb && est / (double)(1ull << bbits) > 1100.0) bbits++;
     int fan = 0;
     while ((1 << (fan + 1)) <= REFINE_FANOUT) fan++;
@@ -1758,7 +1712,6 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_noderec<<<grid_for(N, B), B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
                                                s->dft.as<unsigned long long>(), N, s->nrec.as<NodeRec>());
         unsigned int masks[4] = {31u, 7u, 1u, 0u};
-        if (const char *e = getenv("EULERHIP_RULER_MASK")) masks[0] = (unsigned int)atoi(e);
         unsigned int r0 = 0;
         for (int it = 0; it < 4; it++) {
             const unsigned int nblk = (unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK);
@@ -1958,7 +1911,7 @@ int pipe_plan(ec_session *s, uint64_t nbases, uint64_t bytes_per_base4, const ui
     auto &pp = s->pipe;
     const uint64_t copy_bytes = bytes_per_base4 ? (nbases + 3) / 4 : nbases;
     int nc = (int)std::min<uint64_t>(64, std::max<uint64_t>(1, copy_bytes >> 25));
-    if (const char *e = getenv("EULERHIP_HOST_CHUNKS")) nc = std::max(1, std::min(64, atoi(e)));
+    if (kn().host_chunks) nc = std::max(1, std::min(64, kn().host_chunks));
     pp.nchunks = nc;
     pp.done = 0;
     pp.blo.assign(nc, 0), pp.bhi.assign(nc, 0), pp.ravail.assign(nc, 0), pp.elo.assign(nc, 0), pp.ehi.assign(nc, 0);
@@ -2109,6 +2062,7 @@ int ec_assemble_device(ec_session *s, const uint8_t *d_reads, const uint64_t *d_
 
 int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const uint64_t *offsets, uint64_t nreads,
                      int k, int limit, unsigned flags) {
+    refresh_knobs();
     if (!s || !offsets || (nbytes && !reads)) {
         set_error("null argument");
         return EC_ERR_ARG;
@@ -2137,6 +2091,7 @@ int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const
 int ec_assemble_packed_host(ec_session *s, const uint8_t *codes, uint64_t nbases, const uint64_t *offsets,
                             uint64_t nreads, uint32_t read_len, const uint64_t *exc_pos, const uint8_t *exc_byte,
                             uint64_t n_exc, int k, int limit, unsigned flags) {
+    refresh_knobs();
     if (!s || (nbases && !codes) || (n_exc && (!exc_pos || !exc_byte))) {
         set_error("null argument");
         return EC_ERR_ARG;
@@ -2299,6 +2254,7 @@ int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offs
 }
 
 int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts) {
+    refresh_knobs();
     if (!s || nowners < 1 || nowners > MAX_OWNERS || !owner_counts) {
         set_error("bad ec_export_by_owner arguments (nowners=%d)", nowners);
         return EC_ERR_ARG;
@@ -2443,6 +2399,7 @@ int ec_graph_load(ec_session *s, const void *d_records, uint64_t n, int k, unsig
 }
 
 int ec_graph_links_part(ec_session *s, uint64_t lo, uint64_t hi, uint32_t *d_succ) {
+    refresh_knobs();
     if (!s || !s->graph_loaded || lo > hi || hi > s->n_dense || (hi > lo && !d_succ)) {
         set_error("ec_graph_links_part: no loaded solid set or bad range [%llu, %llu)", (unsigned long long)lo,
                   (unsigned long long)hi);

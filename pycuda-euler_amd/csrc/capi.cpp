@@ -1,6 +1,7 @@
 // capi.cpp -- error state and version of the libeulerhip C ABI (include/eulerhip.h).
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -12,6 +13,37 @@ void set_error(const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof g_err, fmt, ap);
     va_end(ap);
+}
+
+static thread_local Knobs g_knobs;
+const Knobs &kn() { return g_knobs; }
+void refresh_knobs() {
+    Knobs k;
+    if (getenv("EULERHIP_DEBUG")) {
+        auto flag = [](const char *n) { return getenv(n) != nullptr; };
+        auto num = [](const char *n, int dflt) {
+            const char *e = getenv(n);
+            return e ? atoi(e) : dflt;
+        };
+        k.no_sk2 = flag("EULERHIP_NO_SK2");
+        k.no_v2 = flag("EULERHIP_NO_V2");
+        k.force_filter = flag("EULERHIP_FORCE_FILTER");
+        k.no_filter = flag("EULERHIP_NO_FILTER");
+        k.filter_pmax = num("EULERHIP_FILTER_PMAX", 0);
+        k.filter_pmin = num("EULERHIP_FILTER_PMIN", -1);
+        if (const char *e = getenv("EULERHIP_PART_KEYS")) k.part_keys = (float)atof(e);
+        k.v2_r10 = num("EULERHIP_V2_R10", -1);
+        k.refine_rs = num("EULERHIP_REFINE_RS", 0);
+        k.merge_mix = flag("EULERHIP_MERGE_MIX");
+        k.wide_general = flag("EULERHIP_WIDE_GENERAL");
+        k.wide_max_bbits = num("EULERHIP_WIDE_MAX_BBITS", -1);
+        k.host_chunks = num("EULERHIP_HOST_CHUNKS", 0);
+        k.sk2_nodedup = flag("EULERHIP_SK2_NODEDUP");
+        k.sk2_rb = num("EULERHIP_SK2_RB", 0);
+        k.sk2_stats = flag("EULERHIP_SK2_STATS");
+        k.verbose = flag("EULERHIP_VERBOSE");
+    }
+    g_knobs = k;
 }
 }  // namespace ec
 

@@ -17,6 +17,32 @@ constexpr uint64_t EMPTY_KEY = ~0ull;  // canonical 2-bit keys (k <= 32) never e
 // thread-local last error (ec_last_error)
 void set_error(const char *fmt, ...);
 
+// Test / diagnostic overrides.  Read once per C-ABI call (refresh_knobs) and only when
+// EULERHIP_DEBUG is set: without it the library's behaviour never depends on the environment.
+// Each forces a path the default heuristics would not take on small inputs, so the oracle can
+// check it (tests/conftest.py sets EULERHIP_DEBUG=1).
+struct Knobs {
+    bool no_sk2 = false;        // EULERHIP_NO_SK2: no super-k-mer records (count_sk2.h)
+    bool no_v2 = false;         // EULERHIP_NO_V2: no fixed-capacity runs (count_v2.h)
+    bool force_filter = false;  // EULERHIP_FORCE_FILTER: seen-twice filter buckets at any size
+    bool no_filter = false;     // EULERHIP_NO_FILTER
+    int filter_pmax = 0;        // EULERHIP_FILTER_PMAX: part tables 2^pmax (0 = from the estimate)
+    int filter_pmin = -1;       // EULERHIP_FILTER_PMIN
+    float part_keys = 0.0f;     // EULERHIP_PART_KEYS: keys per part table (0 = PART_KEYS)
+    int v2_r10 = -1;            // EULERHIP_V2_R10: 10-B window records 1 = forced, 0 = never
+    int refine_rs = 0;          // EULERHIP_REFINE_RS: refine slices per coarse bucket (0 = 8)
+    bool merge_mix = false;     // EULERHIP_MERGE_MIX: key-hash buckets / owners instead of minimizers
+    bool wide_general = false;  // EULERHIP_WIDE_GENERAL: k > 32 on the HBM table
+    int wide_max_bbits = -1;    // EULERHIP_WIDE_MAX_BBITS: cap the wide buckets (forces overflow)
+    int host_chunks = 0;        // EULERHIP_HOST_CHUNKS: host-input chunks (0 = ~32 MiB each)
+    bool sk2_nodedup = false;   // EULERHIP_SK2_NODEDUP: record-per-lane k_skbucket_rec (A/B)
+    int sk2_rb = 0;             // EULERHIP_SK2_RB: k_skbucket records per thread and round (A/B)
+    bool sk2_stats = false;     // EULERHIP_SK2_STATS: k_skbucket dedup statistics on stderr
+    bool verbose = false;       // EULERHIP_VERBOSE: count-path fallbacks on stderr
+};
+void refresh_knobs();
+const Knobs &kn();
+
 #define EC_HIP(call)                                                                       \
     do {                                                                                   \
         hipError_t e_ = (call);                                                            \

@@ -34,9 +34,8 @@
 namespace ec {
 
 constexpr int SK2_NMAX = 16;     // windows per record (n - 1 in 4 bits)
+constexpr int SK2_ECAP_W = 1600; // entries a partition wave buffers (LDS: 3 workgroups per CU)
 constexpr int SK2_BASES = 46;    // bases per record (92 bits)
-constexpr int SK2_R = 4;         // windows per lane per round of k_skpart
-constexpr int SK2_ECAP = 864;    // entries a wave buffers before a flush (LDS: 3 workgroups per CU)
 #ifndef SK2_TILE_DEF
 #define SK2_TILE_DEF 2048
 #endif
@@ -115,172 +114,12 @@ __device__ inline void sk_hll_put(unsigned int *s_hll, uint32_t hh) {
 }
 
 // Region of (c, g): records [(g * C + c) * cap, + cap) of recs, spill records at C * G * cap
-// (SK2_ECAP of them; *overflow set, the call is redone); cnt[c * G + g] = records stored.
+// (SK2_ECAP_W of them: a flush stores at most that many; *overflow set, the call is redone); cnt[c * G + g] = records stored.
 // Entry (u32): lane | first window << 6 | (n - 1) << 14 | top SK2_BBITS of min_remix << 18.
-template <int NPF>
-__global__ void __launch_bounds__(PT_THREADS) k_skpart(const uint8_t *__restrict__ buf,
-                                                       const uint64_t *__restrict__ off, uint64_t nreads, MinCfg mc,
-                                                       uint32_t M, uint64_t gsize, uint32_t G, uint64_t cap,
-                                                       uint32_t smask, uint4 *recs, unsigned int *cnt, uint8_t *hll,
-                                                       unsigned long long *nrec, unsigned int *overflow) {
-    constexpr int C = 1 << SK2_CBITS;
-    constexpr int NREG = 1 << HLL_REG_BITS;
-    constexpr int SW = NPF * 64 + 4;
-    __shared__ uint32_t s_stage[PT_WAVES][SW];
-    __shared__ uint32_t s_ring[PT_WAVES][SK_W_MAX * 64];  // lane's GW block: [q * 64 + lane]
-    __shared__ uint32_t s_ent[PT_WAVES][SK2_ECAP];
-    __shared__ uint16_t s_srt[PT_WAVES][SK2_ECAP];
-    __shared__ uint32_t s_rel[PT_WAVES][64];
-    __shared__ unsigned long long s_base[PT_WAVES][C];
-    __shared__ unsigned int s_wcnt[PT_WAVES][C];
-    __shared__ unsigned int s_cur[C];
-    __shared__ unsigned int s_hll[NREG / 4];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) s_hll[i] = 0;
-    if (threadIdx.x < C) s_cur[threadIdx.x] = 0;
-    if (lane < C) s_wcnt[wid][lane] = 0;
-    __syncthreads();
-    const uint64_t g = blockIdx.x;
-    const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
-    const uint32_t ntile = (uint32_t)((g1 - g0 + 63) / 64);
-    const int k = mc.k, m = mc.m;
-    const uint32_t w = (uint32_t)mc.w, nmax = sk2_nmax(k);
-    const uint64_t kmask = kmask64(k);
-    uint4 pf[NPF];
-    uint64_t nx_base = 0;
-    uint32_t nx_s = 0, nx_e = 0, nx_n = 0, nx_lo = 0, nx_hi = 0, nx_n16 = 0;
-    if (wid < ntile) EC_PT_ISSUE(wid);
-    const unsigned long long gcap = g * C * cap, spill = (unsigned long long)C * G * cap;
-    uint32_t *st = s_stage[wid];
-    uint32_t *ring = s_ring[wid] + lane;
-    uint32_t *ent = s_ent[wid];
-    auto bases16 = [&](uint32_t p) { return __builtin_amdgcn_alignbit(st[(p >> 4) + 1], st[p >> 4], 2 * (p & 15)); };
-    for (uint32_t t = wid; t < ntile; t += PT_WAVES) {
-#pragma unroll
-        for (int q = 0; q < NPF; q++) st[q * 64 + lane] = pack16(pf[q]);
-        const uint32_t tbase = (uint32_t)nx_base, s = nx_s;
-        const uint32_t len = lane < nx_n ? nx_e - nx_s : 0u;
-        const bool more = t + PT_WAVES < ntile;
-        const bool has = len >= (uint32_t)k;  // then len - k + 1 == M
-        const uint32_t rel = has ? s - tbase : 0u;
-        s_rel[wid][lane] = rel;
-        wave_sync();
-        // m-mer state over the first k - 1 bases; the GW block starts at m-mer 0
-        uint32_t mf = 0, mr = 0, gi = 0, pm = 0xFFFFFFFFu;
-        // push m-mer hash h (m-mer index j, gi = j mod w): min of the window of w m-mers ending at j
-        auto gw_push = [&](uint32_t h) {
-            pm = gi == 0 ? h : min(pm, h);
-            const uint32_t sn = gi + 1 < w ? ring[(gi + 1) * 64] : 0xFFFFFFFFu;
-            ring[gi * 64] = h;
-            const uint32_t v = min(sn, pm);
-            if (gi + 1 == w) {  // block complete: hashes -> suffix minima (wave-uniform)
-                uint32_t a = 0xFFFFFFFFu;
-                for (int q = (int)w - 1; q >= 0; q--) {
-                    a = min(a, ring[q * 64]);
-                    ring[q * 64] = a;
-                }
-                gi = 0;
-            } else {
-                gi++;
-            }
-            return v;
-        };
-        auto push_base = [&](uint32_t b) {
-            mf = ((mf << 2) | b) & mc.mmask;
-            mr = (mr >> 2) | ((3u - b) << mc.msh);
-        };
-        {
-            const uint32_t x0 = bases16(rel), x1 = bases16(rel + 16);
-            for (int tb = 0; tb < k - 1; tb++) {
-                push_base(tb < 16 ? (x0 >> (2 * tb)) & 3u : (x1 >> (2 * (tb - 16))) & 3u);
-                if (tb >= m - 1) gw_push(mmer_hash(mf < mr ? mf : mr));
-            }
-        }
-        const uint32_t nrounds = __any(has) ? (M + SK2_R - 1) / SK2_R : 0u;
-        if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
-        uint32_t runv = 0, runn = 0, runi = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
-        uint32_t wi = 0;
-        const uint32_t rtile = 64 * t;  // the tile's first read relative to g0
-        for (uint32_t round = 0; round < nrounds; round++) {
-            const uint32_t xb = bases16(rel + (uint32_t)(k - 1) + wi);
-            unsigned int smp = 0;
-            uint32_t shh[SK2_R];
-#pragma unroll
-            for (int j = 0; j < SK2_R; j++) {
-                push_base((xb >> (2 * j)) & 3u);
-                const uint32_t v = gw_push(mmer_hash(mf < mr ? mf : mr));
-                const bool ok = has && wi + j < M;
-                // HyperLogLog over the k-mers whose minimizer hash has its low bits & smask zero (a
-                // sample of the key space: a k-mer and its twin share the minimizer); the
-                // sampled window's canonical k-mer straight out of the stage
-                shh[j] = 0;
-                if (ok && (v & smask) == 0) {
-                    const uint32_t p = rel + wi + j;
-                    const uint64_t P = (uint64_t)bases16(p) | (uint64_t)bases16(p + 16) << 32;
-                    const uint64_t krc = ~P & kmask, kfw = rev2_64(P) >> (64 - 2 * k);
-                    smp |= 1u << j;
-                    shh[j] = (uint32_t)(mix64(kfw < krc ? kfw : krc) >> 32);
-                }
-                const bool close = ok && runn && (v != runv || runn == nmax);
-                const uint64_t bal = __ballot(close);
-                if (close) {
-                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
-                }
-                cntw += (uint32_t)__popcll(bal);
-                if (ok) {
-                    if (close || !runn) {
-                        runv = v;
-                        runi = wi + j;
-                        runn = 0;
-                    }
-                    runn++;
-                }
-            }
-            wi += SK2_R;
-            const bool last = round + 1 == nrounds;
-            if (last) {  // the reads' final runs
-                const bool fin = has && runn;
-                const uint64_t bal = __ballot(fin);
-                if (fin) {
-                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
-                }
-                cntw += (uint32_t)__popcll(bal);
-                if (more) EC_PT_ISSUE(t + PT_WAVES);
-            }
-            if (smp) {
-#pragma unroll
-                for (int j = 0; j < SK2_R; j++)
-                    if ((smp >> j) & 1u) sk_hll_put(s_hll, shh[j]);
-            }
-            // flush: the buffer could not take another round, or the stage is about to change
-            if (last || cntw > (uint32_t)(SK2_ECAP - 64 * (SK2_R + 1))) {
-                skpart_flush<C>(cntw, ent, s_srt[wid], s_wcnt[wid], s_cur, s_base[wid], s_rel[wid], st, lane, gcap,
-                                cap, spill, M, rtile, recs, overflow);
-                cntw = 0;
-            }
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < C) cnt[(uint64_t)threadIdx.x * G + g] = (unsigned int)min((uint64_t)s_cur[threadIdx.x], cap);
-    if (threadIdx.x == 0) {  // records of the group (one atomic per workgroup)
-        unsigned long long tot = 0;
-        for (int c = 0; c < C; c++) tot += s_cur[c];
-        if (tot) atomicAdd(nrec, tot);
-    }
-    unsigned int *hw = reinterpret_cast<unsigned int *>(hll + g * NREG);
-    for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) hw[i] = s_hll[i];
-}
-
-// k_skpart for one compile-time window width W = k - m + 1 (the headline's k = 31: W = 17):
+// k_skpart_w: the partition for one compile-time window width W = k - m + 1 (the headline's k = 31: W = 17):
 // a round is one block of W m-mers, their hashes and the previous block's suffix minima held
 // in registers (van Herk / Gil-Werman: window rW + j = min(suffix_r[j], prefix_{r+1}[j - 1])),
 // so no per-lane LDS ring; the buffer (no ring either) takes a whole round of entries.
-constexpr int SK2_ECAP_W = 1600;  // entries a wave buffers (LDS: 3 workgroups per CU)
 //
 // VAL (no k_prescan ran; M and the stage size come from the first read): the kernel checks
 // what the prescan would have -- every read with windows is L = M + k - 1 bytes long, every
@@ -625,7 +464,7 @@ struct EvExpand {  // e -> (read << 32) | l for the dense arrays
 // (each window read straight out of the bases), and a two-slot fast path with the other
 // windows queued for lds_insert.
 template <int SLOTS, bool EVEN_K>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, const unsigned long long *bbeg,
+__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *recs, const unsigned long long *bbeg,
                                                              const unsigned long long *bend, int k, uint32_t M,
                                                              double inv_m, long long limit, unsigned long long *dkey,
                                                              unsigned int *dcnt, unsigned long long *dfc,
@@ -745,235 +584,285 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
                                           overflow, KeyId(), EvExpand{2 * M});
 }
 
-// -------------------------------------------------------
-// k_skbucket with duplicate records merged first.  At ~150-fold coverage most records of a
-// bucket are the same super-k-mer read by different reads (one in three of a 2048-record chunk
-// is distinct, simulated): a chunk's records go through an LDS table keyed by content (hash of
-// x, y, z; equality checked against the representative's record, re-read from global memory),
-// each entry keeping the multiplicity and two minima over its members' positions -- pa = min p
-// (min read, then min first window) and pb = min (read M + M - 1 - window) (min read, then max
-// window) -- which give every window's first events exactly: a window whose canonical form is
-// the forward string takes eC from pa and eT from pb, the others the reverse.  The distinct
-// records, counting-sorted by window count, then insert their windows with add = multiplicity.
-#ifdef SK2_DD_TIMING  // experiments: per-phase clock totals of k_skbucket_dd (thread 0 of each block)
-__device__ unsigned long long g_sk2_dd_t[4];
-#define SKD_T(i)                                                                                     \
-    do {                                                                                             \
-        if (threadIdx.x == 0) {                                                                      \
-            const unsigned long long t_ = wall_clock64();                                            \
-            if (i) atomicAdd(&g_sk2_dd_t[(i) - 1], t_ - t_last);                                     \
-            t_last = t_;                                                                             \
-        }                                                                                            \
-    } while (0)
-#else
-#define SKD_T(i) (void)0
-#endif
-template <int SLOTS, bool EVEN_K, int PER>  // PER records per thread and chunk
-__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_dd(const uint4 *recs, const unsigned long long *bbeg,
-                                                                const unsigned long long *bend, int k, uint32_t M,
-                                                                double inv_m, long long limit, unsigned long long *dkey,
-                                                                unsigned int *dcnt, unsigned long long *dfc,
-                                                                unsigned long long *dft, SubSlot *sub,
-                                                                unsigned int *nsolid, unsigned long long *ndistinct,
-                                                                unsigned int *overflow) {
+// ---- bucket with the bucket's duplicate super-k-mers merged first (the default) -----------------
+// At ~150-fold coverage a bucket's records are mostly the same few super-k-mers read again and
+// again (each interior super-k-mer of the genome appears in ~130 reads, in two orientations).  The
+// records first go through an LDS table keyed by their CANONICAL content -- the L = n + k - 1
+// bases masked to L (the partition copies bases past the run too) or their reverse complement,
+// whichever is smaller, plus n -- keeping per distinct record its multiplicity and two event
+// minima: with A = read 2M + first window and B = read 2M + 2M - 1 - first window, window o's
+// k-mer string was inserted by build() at A + o and its twin at B - o (count_part.h events); a
+// record taken in reverse complement has A' = B - n + 1, B' = A + n - 1 (window o' of the flip is
+// the twin of window n - 1 - o).  Identical canonical records have identical window strings, so
+// min over copies of (A + o) = min A + o: the distinct records insert their windows once, with
+// add = multiplicity, and every key's count and first events equal the per-record inserts'.
+// The record table holds RS distinct records; before a chunk could overfill it, its records are
+// rolled into the k-mer table and it is cleared (a cache: any split of the copies is exact).
+// Probing claims a slot by CAS on a tag word (20 hash bits | "claimed in this chunk" | claimer's
+// thread); a slot claimed in this chunk is compared against the claimer's staged key (LDS), an
+// older one against the stored key, so one wave-uniform loop resolves every record.
+__device__ inline uint32_t rev2_32b(uint32_t v) {  // superkmer.h rev2_32 with one v_bfrev_b32
+    v = __builtin_bitreverse32(v);
+    return ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+}
+
+template <int SLOTS, int RS, int RB, bool EVEN_K>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, const unsigned long long *bbeg,
+                                                             const unsigned long long *bend, int k, uint32_t M,
+                                                             double inv_m, long long limit, unsigned long long *dkey,
+                                                             unsigned int *dcnt, unsigned long long *dfc,
+                                                             unsigned long long *dft, SubSlot *sub,
+                                                             unsigned int *nsolid, unsigned long long *ndistinct,
+                                                             unsigned int *overflow, unsigned long long *dbg) {
     constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
-    constexpr int SKD_CH = PER * BUCKET_THREADS, SKD_SLOTS = SKD_CH;  // records per chunk, content-table slots
-    constexpr int SKD_BITS = PER == 2 ? 11 : 10;
-    static_assert(SKD_CH < 4096, "index + 1 in the slot word's low 12 bits");
+    constexpr uint32_t PEND = 0x800u;  // tag word: the claimer has not yet stored the key
     __shared__ LTabE<SLOTS> tab;
     __shared__ unsigned int s_over[2];
-    __shared__ unsigned int d_idx[SKD_SLOTS];  // representative's record index + 1 (0: empty)
-    __shared__ unsigned int d_mult[SKD_SLOTS], d_pa[SKD_SLOTS], d_pb[SKD_SLOTS];
-    __shared__ uint16_t s_ord[SKD_CH];  // distinct records' slots, most windows first
-    __shared__ unsigned int s_ncnt[SK2_NMAX + 1];
-    const unsigned int b = blockIdx.x;
-    for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
+    __shared__ uint32_t r_tag[RS], r_x[RS], r_y[RS], r_z[RS], r_mult[RS], r_a[RS], r_b[RS];
+    __shared__ uint16_t s_ord[RS];
+    __shared__ unsigned int s_nent, s_ncnt[SK2_NMAX + 1];
+    const unsigned int b = blockIdx.x, tid = threadIdx.x;
+    for (int i = tid; i < SLOTS; i += BUCKET_THREADS) {
         tab.key[i] = EMPTY_KEY;
         tab.count[i] = 0;
         tab.ev[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
     }
-    if (threadIdx.x == 0) s_over[0] = s_over[1] = 0;
+    for (int i = tid; i < RS; i += BUCKET_THREADS) {
+        r_tag[i] = 0;
+        r_mult[i] = 0;
+        r_a[i] = r_b[i] = 0xFFFFFFFFu;
+    }
+    if (tid <= SK2_NMAX) s_ncnt[tid] = 0;
+    if (tid == 0) s_over[0] = s_over[1] = 0, s_nent = 0;
+    // EULERHIP_SK2_STATS: per-phase wall clock (100 MHz) summed over the blocks, thread 0's view
+    unsigned long long t_last = 0;
+    auto phase = [&](int i) {
+        if (dbg && tid == 0) {
+            const unsigned long long t = wall_clock64();
+            if (i) atomicAdd(&dbg[2 + i], t - t_last);
+            t_last = t;
+        }
+    };
+    phase(0);
     __syncthreads();
     const uint64_t r0 = bbeg[b], r1 = bend[b];
     const uint64_t kmask = kmask64(k);
     const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
-    const unsigned int m2 = 2 * M - 1;
-    auto split = [&](unsigned int p, unsigned int &read, unsigned int &rem) {  // p = read M + rem
-        const unsigned int rd = (unsigned int)((double)p * inv_m);
-        int rm = (int)(p - rd * M);
-        read = rd;
-        if (rm < 0) read--, rm += (int)M;
-        else if (rm >= (int)M) read++, rm -= (int)M;
-        rem = (unsigned int)rm;
+    const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
+
+    // the n windows of a (canonical) record into the k-mer table: window o's string was inserted
+    // at ea + o, its twin at eb - o, mult times each
+    auto roll_out = [&](uint32_t x0, uint32_t x1, uint32_t x2, unsigned int mult, unsigned int ea, unsigned int eb) {
+        const unsigned int n = (x2 >> 28) + 1;
+        if (dbg) atomicAdd(&dbg[2], (unsigned long long)n);
+        auto events = [&](uint64_t fwd, uint64_t rc, unsigned int o, unsigned int &eC, unsigned int &eT,
+                          unsigned int &add) {
+            const bool tw = fwd > rc;
+            const unsigned int ef = ea + o, et = eb - o;
+            add = mult;
+            eC = tw ? et : ef;
+            eT = tw ? ef : et;
+            if (EVEN_K && fwd == rc) {  // even-k palindrome: both inserts at its first event
+                add = 2 * mult;
+                eC = eT = min(ef, et);
+            }
+            return tw ? rc : fwd;
+        };
+        const unsigned int h = (n + 1) >> 1;  // two windows per step (o and o + h)
+        auto at = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // window o straight out of the bases
+            const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, 2 * o), hi = __builtin_amdgcn_alignbit(x2, x1, 2 * o);
+            const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+            rv = ~P & kmask;
+            fw = rev2_64(P) >> fsh;
+        };
+        auto roll = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // to window o from o - 1
+            const unsigned int tb = o + (unsigned int)k - 1;
+            const uint32_t wd = tb < 32 ? x1 : x2;
+            const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
+            fw = ((fw << 2) | bb) & kmask;
+            rv = (rv >> 2) | ((uint64_t)(3u - bb) << sh);
+        };
+        uint64_t fA, rA, fB, rB;
+        at(0, fA, rA);
+        at(h, fB, rB);
+        for (unsigned int i = 0; i < h; i++) {
+            const unsigned int oB = i + h;
+            const bool bB = oB < n;
+            if (i) {
+                roll(i, fA, rA);
+                roll(oB, fB, rB);
+            }
+            unsigned int eCA, eTA, eCB, eTB, addA, addB;
+            const uint64_t cA = events(fA, rA, i, eCA, eTA, addA);
+            const uint64_t cB = events(fB, rB, oB, eCB, eTB, addB);
+            unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1), sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
+            const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
+            lds_locate2<SLOTS>(tab, s_over, cA, sA, kA, cB, sB, bB ? kB : cB);
+            atomicAdd(&tab.count[sA], addA);
+            if (bB) atomicAdd(&tab.count[sB], addB);
+            const uint2 vA = tab.ev[sA], vB = tab.ev[sB];
+            if (eCA < vA.x) atomicMin(&tab.ev[sA].x, eCA);
+            if (eTA < vA.y) atomicMin(&tab.ev[sA].y, eTA);
+            if (bB && eCB < vB.x) atomicMin(&tab.ev[sB].x, eCB);
+            if (bB && eTB < vB.y) atomicMin(&tab.ev[sB].y, eTB);
+        }
     };
-#ifdef SK2_DD_TIMING
-    unsigned long long t_last = 0;
-#endif
-    uint4 nx[PER];
+
+    // ---- records -> record table (no barrier: a slot's key is published by clearing PEND) ----
+    // RB records per thread and round, their loads, canonical forms and probe chains in flight
+    // together (one record per thread waited on its global load and on a chain of dependent
+    // LDS round trips: latency-bound)
+    constexpr unsigned int ROUND = RB * BUCKET_THREADS;
+    phase(1);  // [3] init
+    uint4 nx[RB];
 #pragma unroll
-    for (int q = 0; q < PER; q++) {
-        const uint64_t i = r0 + threadIdx.x + q * BUCKET_THREADS;
-        nx[q] = i < r1 ? recs[i] : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < RB; j++) {
+        const uint64_t ri = r0 + tid + (uint64_t)j * BUCKET_THREADS;
+        nx[j] = ri < r1 ? recs[ri] : make_uint4(0, 0, 0, 0);
     }
-    for (uint64_t c0 = r0; c0 < r1; c0 += SKD_CH) {
-        const unsigned int nv = (unsigned int)min<uint64_t>(SKD_CH, r1 - c0);
-        uint4 x[PER];
+    for (uint64_t c0 = r0; c0 < r1; c0 += ROUND) {
+        uint32_t K0[RB], K1[RB], K2[RB], EA[RB], EB[RB], TG[RB], SL[RB];
+        int ST[RB];  // 0 searching, 1 found / claimed, 2 table full (rolled out on its own)
 #pragma unroll
-        for (int q = 0; q < PER; q++) x[q] = nx[q];
-#pragma unroll
-        for (int q = 0; q < PER; q++) {  // the next chunk
-            const uint64_t i = c0 + SKD_CH + threadIdx.x + q * BUCKET_THREADS;
-            if (i < r1) nx[q] = recs[i];
-        }
-        for (int i = threadIdx.x; i < SKD_SLOTS; i += blockDim.x) {
-            d_idx[i] = 0;
-            d_mult[i] = 0;
-            d_pa[i] = d_pb[i] = 0xFFFFFFFFu;
-        }
-        if (threadIdx.x <= SK2_NMAX) s_ncnt[threadIdx.x] = 0;
-        __syncthreads();
-        SKD_T(0);
-        // merge equal records
-        unsigned int myslot[PER];
-        bool lead[PER];
-#pragma unroll
-        for (int q = 0; q < PER; q++) {
-            const unsigned int ri = threadIdx.x + q * BUCKET_THREADS;
-            myslot[q] = 0;
-            lead[q] = false;
-            if (ri >= nv) continue;
-            // slot from the hash's high bits; a 20-bit tag beside the representative's index in
-            // the slot word, so a probe past another record's slot costs no global read
-            unsigned int hh = x[q].x * 0x9E3779B1u;
-            hh = (hh ^ (hh >> 16) ^ x[q].y) * 0x85EBCA77u;
-            hh = (hh ^ (hh >> 13) ^ x[q].z) * 0xC2B2AE3Du;
+        for (int j = 0; j < RB; j++) {
+            const uint64_t ri = c0 + tid + (uint64_t)j * BUCKET_THREADS;
+            const bool valid = ri < r1;
+            const uint4 x = nx[j];
+            if (ri + ROUND < r1) nx[j] = recs[ri + ROUND];  // next round's records
+            // canonical content of the record
+            const unsigned int n = (x.z >> 28) + 1, L = n + (unsigned int)k - 1;  // L in [k, 46]
+            uint32_t x0 = x.x, x1 = x.y, x2 = x.z & 0x0FFFFFFFu;
+            if (2 * L < 64) x1 &= (1u << (2 * L - 32)) - 1u, x2 = 0;
+            else x2 &= (1u << (2 * L - 64)) - 1u;
+            // reverse complement of the L bases: rev2 of the 96-bit string (base i -> 47 - i), then
+            // down by 2 (48 - L) bits, complemented
+            const uint32_t y0 = rev2_32b(x2), y1 = rev2_32b(x1), y2 = rev2_32b(x0);
+            const unsigned int sft = 2 * (48 - L);  // 4 .. 54
+            uint32_t q0, q1, q2;
+            if (sft < 32) {
+                q0 = __builtin_amdgcn_alignbit(y1, y0, sft), q1 = __builtin_amdgcn_alignbit(y2, y1, sft), q2 = y2 >> sft;
+            } else {
+                q0 = __builtin_amdgcn_alignbit(y2, y1, sft - 32), q1 = y2 >> (sft - 32), q2 = 0;
+            }
+            q0 = ~q0;
+            if (2 * L < 64) q1 = ~q1 & ((1u << (2 * L - 32)) - 1u), q2 = 0;
+            else q1 = ~q1, q2 = ~q2 & ((1u << (2 * L - 64)) - 1u);
+            const bool flip = q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0;
+            // events of window 0: A = read 2M + first window, B = read 2M + 2M - 1 - first window
+            const unsigned int p = x.w;
+            const unsigned int rd0 = (unsigned int)((double)p * inv_m);  // p / M, corrected below
+            int rm = (int)(p - rd0 * M);
+            unsigned int rd = rd0;
+            if (rm < 0) rd--, rm += (int)M;
+            else if (rm >= (int)M) rd++, rm -= (int)M;
+            const unsigned int A = rd * M2 + (unsigned int)rm, B = rd * M2 + m2 - (unsigned int)rm;
+            K0[j] = flip ? q0 : x0, K1[j] = flip ? q1 : x1, K2[j] = (flip ? q2 : x2) | (n - 1) << 28;
+            EA[j] = flip ? B - n + 1 : A, EB[j] = flip ? A + n - 1 : B;
+            // content hash -> first slot, tag
+            uint32_t hh = K0[j] * 0x9E3779B1u;
+            hh = (hh ^ (hh >> 15) ^ K1[j]) * 0x85EBCA77u;
+            hh = (hh ^ (hh >> 13) ^ K2[j]) * 0xC2B2AE3Du;
             hh ^= hh >> 16;
-            const unsigned int tag = (hh * 0x27D4EB2Fu) & 0xFFFFF000u;
-            unsigned int slot = hh >> (32 - SKD_BITS);
-            const unsigned int mine = tag | (ri + 1);
-            for (;;) {  // <= nv distinct entries in SKD_SLOTS >= nv slots: ends
-                unsigned int cur = d_idx[slot];
-                if (cur == 0) {
-                    cur = atomicCAS(&d_idx[slot], 0u, mine);
-                    if (cur == 0) {
-                        lead[q] = true;
-                        break;
+            TG[j] = (hh | 0x1000u) & 0xFFFFF000u;
+            SL[j] = __umulhi(hh * 0x27D4EB2Fu, (unsigned int)RS);
+            ST[j] = valid ? 0 : 1;
+        }
+        auto searching = [&]() {
+            bool a = false;
+#pragma unroll
+            for (int j = 0; j < RB; j++) a |= ST[j] == 0;
+            return a;
+        };
+#pragma unroll 1
+        while (__any(searching())) {
+            uint32_t T[RB];
+#pragma unroll
+            for (int j = 0; j < RB; j++)  // the tag reads of every chain first
+                T[j] = ST[j] == 0 ? __hip_atomic_load(&r_tag[SL[j]], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : 1u;
+#pragma unroll
+            for (int j = 0; j < RB; j++) {
+                if (ST[j] != 0) continue;
+                const unsigned int slot = SL[j];
+                uint32_t t = T[j];
+                if (t == 0) {
+                    if (atomicAdd(&s_nent, 1u) >= (unsigned int)RS - 1) {  // keep one slot free
+                        atomicSub(&s_nent, 1u);
+                        ST[j] = 2;
+                    } else {
+                        t = atomicCAS(&r_tag[slot], 0u, TG[j] | PEND);
+                        if (t == 0) {  // claimed: store the key, then publish it
+                            r_x[slot] = K0[j], r_y[slot] = K1[j], r_z[slot] = K2[j];
+                            __hip_atomic_store(&r_tag[slot], TG[j], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            ST[j] = 1;
+                        } else {
+                            atomicSub(&s_nent, 1u);
+                        }
                     }
                 }
-                if ((cur & 0xFFFFF000u) == tag) {
-                    const uint4 o = recs[c0 + (cur & 0xFFFu) - 1];  // the representative (just loaded: cached)
-                    if (o.x == x[q].x && o.y == x[q].y && o.z == x[q].z) break;
-                }
-                slot = (slot + 1) & (SKD_SLOTS - 1);
+                // a slot whose key is still pending counts as another key: at worst the record
+                // gets a second entry (both are rolled out: still exact)
+                if (ST[j] == 0 && t == TG[j] && r_x[slot] == K0[j] && r_y[slot] == K1[j] && r_z[slot] == K2[j])
+                    ST[j] = 1;
+                if (ST[j] == 0) SL[j] = slot + 1 == (unsigned int)RS ? 0u : slot + 1;
             }
-            myslot[q] = slot;
-            unsigned int read, rem;
-            split(x[q].w, read, rem);
-            atomicAdd(&d_mult[slot], 1u);
-            const unsigned int pb = read * M + (M - 1 - rem);
-            if (x[q].w < d_pa[slot]) atomicMin(&d_pa[slot], x[q].w);
-            if (pb < d_pb[slot]) atomicMin(&d_pb[slot], pb);
         }
-        __syncthreads();
-        SKD_T(1);
-        // the distinct records by window count (most first)
-        unsigned int bin[PER], rk[PER];
+#pragma unroll
+        for (int j = 0; j < RB; j++) {
+            const bool valid = c0 + tid + (uint64_t)j * BUCKET_THREADS < r1;
+            if (valid && ST[j] == 1) {
+                const unsigned int slot = SL[j];
+                atomicAdd(&r_mult[slot], 1u);
+                if (EA[j] < r_a[slot]) atomicMin(&r_a[slot], EA[j]);
+                if (EB[j] < r_b[slot]) atomicMin(&r_b[slot], EB[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RB; j++)
+            if (ST[j] == 2) roll_out(K0[j], K1[j], K2[j], 1u, EA[j], EB[j]);
+    }
+    __syncthreads();
+    phase(2);  // [4] records (thread 0 + the barrier)
+    // ---- the distinct records into the k-mer table, by window count (most first) -------------
+    {
+        constexpr int PER = (RS + BUCKET_THREADS - 1) / BUCKET_THREADS;
+        unsigned int sl[PER], rk[PER];
 #pragma unroll
         for (int q = 0; q < PER; q++) {
-            bin[q] = lead[q] ? SK2_NMAX - 1 - (x[q].z >> 28) : SK2_NMAX;
-            rk[q] = lead[q] ? atomicAdd(&s_ncnt[bin[q]], 1u) : 0u;
+            const unsigned int i = tid + q * BUCKET_THREADS;
+            sl[q] = SK2_NMAX;
+            if (i < (unsigned)RS && r_tag[i]) {
+                sl[q] = SK2_NMAX - 1 - (r_z[i] >> 28);
+                rk[q] = atomicAdd(&s_ncnt[sl[q]], 1u);
+            }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             unsigned int a = 0;
             for (int q = 0; q < SK2_NMAX; q++) {
                 const unsigned int v = s_ncnt[q];
                 s_ncnt[q] = a;
                 a += v;
             }
-            s_ncnt[SK2_NMAX] = a;  // distinct records
+            s_ncnt[SK2_NMAX] = a;
+            if (dbg) atomicAdd(&dbg[0], (unsigned long long)a), atomicAdd(&dbg[1], 1ull);
         }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < PER; q++)
-            if (lead[q]) s_ord[s_ncnt[bin[q]] + rk[q]] = (uint16_t)myslot[q];
+            if (sl[q] < SK2_NMAX) s_ord[s_ncnt[sl[q]] + rk[q]] = (uint16_t)(tid + q * BUCKET_THREADS);
         __syncthreads();
-        const unsigned int nd = s_ncnt[SK2_NMAX];
-        SKD_T(2);
-        for (unsigned int t = threadIdx.x; t < nd; t += blockDim.x) {
-            const unsigned int slot = s_ord[t];
-            const uint4 y = recs[c0 + (d_idx[slot] & 0xFFFu) - 1];
-            const unsigned int mult = d_mult[slot];
-            unsigned int readA, remA, readB, remB;
-            split(d_pa[slot], readA, remA);
-            split(d_pb[slot], readB, remB);
-            remB = M - 1 - remB;
-            const unsigned int a2 = readA * (2 * M), b2 = readB * (2 * M);
-            const unsigned int n = (y.z >> 28) + 1;
-            // window o: canonical key, its events (forward-canonical: eC from pa, eT from pb)
-            auto events = [&](uint64_t fwd, uint64_t rc, unsigned int o, unsigned int &eC, unsigned int &eT,
-                              unsigned int &add) {
-                const bool tw = fwd > rc;
-                const unsigned int la = remA + o, lb = remB + o;
-                add = mult;
-                if (EVEN_K && fwd == rc) {  // even-k palindrome: inserted twice at the forward event
-                    add = 2 * mult;
-                    eC = eT = a2 + la;
-                } else if (tw) {
-                    eC = b2 + (m2 - lb);
-                    eT = a2 + la;
-                } else {
-                    eC = a2 + la;
-                    eT = b2 + (m2 - lb);
-                }
-                return tw ? rc : fwd;
-            };
-            // two windows per step (o and o + h): their LDS probes and updates in flight together
-            const unsigned int h = (n + 1) >> 1;
-            auto at = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // window o straight out of the bases
-                const uint32_t lo = __builtin_amdgcn_alignbit(y.y, y.x, 2 * o), hi = __builtin_amdgcn_alignbit(y.z, y.y, 2 * o);
-                const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
-                rv = ~P & kmask;
-                fw = rev2_64(P) >> fsh;
-            };
-            auto roll = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // to window o from o - 1
-                const unsigned int tb = o + (unsigned int)k - 1;
-                const uint32_t wd = tb < 32 ? y.y : y.z;
-                const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
-                fw = ((fw << 2) | bb) & kmask;
-                rv = (rv >> 2) | ((uint64_t)(3u - bb) << sh);
-            };
-            uint64_t fA, rA, fB, rB;
-            at(0, fA, rA);
-            at(h, fB, rB);
-            for (unsigned int i = 0; i < h; i++) {
-                const unsigned int oB = i + h;
-                const bool bB = oB < n;
-                if (i) {
-                    roll(i, fA, rA);
-                    roll(oB, fB, rB);
-                }
-                unsigned int eCA, eTA, eCB, eTB, addA, addB;
-                const uint64_t cA = events(fA, rA, i, eCA, eTA, addA);
-                const uint64_t cB = events(fB, rB, oB, eCB, eTB, addB);
-                unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1),
-                             sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
-                const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
-                lds_locate2<SLOTS>(tab, s_over, cA, sA, kA, cB, sB, bB ? kB : cB);
-                atomicAdd(&tab.count[sA], addA);
-                if (bB) atomicAdd(&tab.count[sB], addB);
-                const uint2 vA = tab.ev[sA], vB = tab.ev[sB];
-                if (eCA < vA.x) atomicMin(&tab.ev[sA].x, eCA);
-                if (eTA < vA.y) atomicMin(&tab.ev[sA].y, eTA);
-                if (bB && eCB < vB.x) atomicMin(&tab.ev[sB].x, eCB);
-                if (bB && eTB < vB.y) atomicMin(&tab.ev[sB].y, eTB);
-            }
+        const unsigned int ne = s_ncnt[SK2_NMAX];
+        phase(3);  // [5] sort
+        for (unsigned int t = tid; t < ne; t += BUCKET_THREADS) {
+            const unsigned int e = s_ord[t];
+            roll_out(r_x[e], r_y[e], r_z[e], r_mult[e], r_a[e], r_b[e]);
         }
-        __syncthreads();
-        SKD_T(3);
     }
+    __syncthreads();
+    phase(4);  // [6] roll-out
     lds_table_finish<SLOTS, false, KeyId>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
                                           overflow, KeyId(), EvExpand{2 * M});
+    phase(5);  // [7] finish
 }
 
 }  // namespace ec

@@ -12,6 +12,10 @@ for p in (PKG, os.path.join(ROOT, "oracle"), os.path.dirname(os.path.abspath(__f
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# the library's test / diagnostic overrides (EULERHIP_NO_SK2, EULERHIP_FORCE_FILTER, ...) take
+# effect only with EULERHIP_DEBUG set (csrc/common.h Knobs)
+os.environ.setdefault("EULERHIP_DEBUG", "1")
+
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 

@@ -35,20 +35,17 @@ def _sk_applies(reads, k):
 
 
 def _want_paths(reads, k, superkmer):
-    """super-k-mer records (default or EC_FLAG_SUPERKMER) for 21 <= k <= 32 and N-free reads,
-    else window records (k <= 32); k > 32: 24-B records without N, else the general table"""
+    """partitioned counting (super-k-mer or window records) for k <= 32; k > 32: 24-B records
+    without N, else the general table.  EC_FLAG_SUPERKMER is accepted and changes nothing
+    (super-k-mer records are the default where they apply)."""
     if k > 32:  # partitioned 24-B records for N-free reads (count_wide.h)
         return (eulerhip.EC_PATH_GENERAL,) if any("N" in r for r in reads) else (eulerhip.EC_PATH_PARTITIONED,)
-    if not _sk_applies(reads, k):
-        return (eulerhip.EC_PATH_PARTITIONED,)
-    if superkmer:
-        return (eulerhip.EC_PATH_SUPERKMER,)
-    return (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_SUPERKMER)
+    return (eulerhip.EC_PATH_PARTITIONED,)
 
 
 @pytest.mark.parametrize("case", CASES32[1::3], ids=[c["name"] for c in CASES32[1::3]])
 def test_golden_superkmer(gpu_session, case):
-    """super-k-mer records asked for (EC_FLAG_SUPERKMER)"""
+    """EC_FLAG_SUPERKMER (accepted, the default behaviour)"""
     res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True, superkmer=True)
     assert [[x, c] for x, c in res.dict_items] == case["d"]
     assert res.contigs == case["contigs"]
@@ -151,10 +148,6 @@ def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode)
     assert res.links == rl
     if want_dict:
         assert [[x, c] for x, c in res.dict_items] == ref["d"]
-    if res.stats.count_path == eulerhip.EC_PATH_SUPERKMER:  # 32-B super-k-mer records
-        assert res.stats.record_bytes == 32 and 0 < res.stats.n_records < res.stats.n_positions
-    if mode == "superkmer" and 21 <= k <= 32 and nr == 0:
-        assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
     if mode in ("partitioned", "window_records") and k <= 32 and nr == 0 \
             and res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.count_variant != 3:
         assert res.stats.record_bytes == 12  # one read length, no N: 12-B window records
@@ -163,8 +156,8 @@ def test_synthetic_vs_oracle(gpu_session, g, n, L, seed, err, nr, circ, k, mode)
     if mode == "wide_records" and k <= 32:
         assert res.stats.record_bytes == 16
     # one read length, no N, k <= 32: the fixed-capacity runs of count_v2.h unless asked otherwise
-    if mode in ("partitioned", "window_records") and k <= 32 and nr == 0:
-        if mode == "partitioned" and 21 <= k and err <= 0.01:  # 16-B super-k-mer records (count_sk2.h)
+    if mode in ("partitioned", "window_records", "superkmer") and k <= 32 and nr == 0:
+        if mode != "window_records" and 21 <= k and err <= 0.01:  # 16-B super-k-mer records (count_sk2.h)
             assert res.stats.count_variant == 3 and res.stats.record_bytes == 16
             assert 0 < res.stats.n_records < res.stats.n_positions
         else:  # small inputs: 12-B window records
@@ -229,12 +222,12 @@ def test_many_buckets_vs_oracle(gpu_session):
     ref, rc, rl = _oracle_packed(buf, off, 31)
     gpu_session.run_host(buf, off, 31, 1)
     res = gpu_session.fetch(31)
-    assert res.stats.count_path in (eulerhip.EC_PATH_PARTITIONED, eulerhip.EC_PATH_SUPERKMER)
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
     assert res.stats.n_buckets > 64
     assert res.contig_bytes == ref["contig_chars"] and res.links == rl
     gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_SUPERKMER)
     res = gpu_session.fetch(31)
-    assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER and res.stats.n_buckets > 64
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED and res.stats.n_buckets > 64
     assert res.contig_bytes == ref["contig_chars"] and res.links == rl
     gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_WINDOW_RECORDS)
     res = gpu_session.fetch(31)
@@ -266,8 +259,8 @@ def _low_complexity_reads(n, L, seed):
 def test_superkmer_low_complexity_vs_oracle(gpu_session, k):
     reads = _low_complexity_reads(400, 120, 40 + k)
     d, r, g = oracle.assemble(reads, k, 1)
-    res = gpu_session.assemble(reads, k, 1, want_dict=True, superkmer=True)
-    assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
+    res = gpu_session.assemble(reads, k, 1, want_dict=True)
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
     assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g
 
 
@@ -286,9 +279,9 @@ def test_superkmer_ragged_lengths_vs_oracle(gpu_session, k):
     off = np.zeros(len(reads) + 1, np.uint64)
     off[1:] = np.cumsum([len(x) for x in reads])
     ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
-    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT | eulerhip.EC_FLAG_SUPERKMER)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
     res = gpu_session.fetch(k, True)
-    assert res.stats.count_path == eulerhip.EC_PATH_SUPERKMER
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
     assert [[x, c] for x, c in res.dict_items] == ref["d"]
     assert res.contig_bytes == ref["contig_chars"] and res.links == rl
 
@@ -612,22 +605,6 @@ def test_sk2_declines_filter_and_window_records(gpu_session, monkeypatch):
     res = gpu_session.fetch(31, True)
     assert res.stats.count_variant == 1
     assert [[x, c] for x, c in res.dict_items] == ref["d"] and res.links == rl
-
-
-@pytest.mark.parametrize("k", [21, 28, 31])
-def test_sk2_ring_partition_vs_oracle(gpu_session, monkeypatch, k):
-    """the LDS-ring sliding-minimum partition (EULERHIP_SKPART_RING) against the oracle and
-    against the register-block default: the same records"""
-    buf, off = make_reads(30_000, 10_000, 100, 5300 + k, err=0.002)
-    ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
-    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
-    res0 = gpu_session.fetch(k, True)
-    monkeypatch.setenv("EULERHIP_SKPART_RING", "1")
-    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
-    res = gpu_session.fetch(k, True)
-    assert res.stats.count_variant == 3 and res.stats.n_records == res0.stats.n_records
-    assert [[x, c] for x, c in res.dict_items] == ref["d"]
-    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
 
 
 def test_sk2_fast_path_fallbacks_vs_oracle(gpu_session):
