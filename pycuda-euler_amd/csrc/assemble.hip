@@ -541,8 +541,11 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     // CU).  Measured: 16384 buckets of 1024 slots (three workgroups per CU) were not faster, and
     // small tables need lds_insert to count claims after the CAS (reservations of up to 1024
     // racing lanes overshoot), which cost 8 % in every table
+    // (<= 800 estimated keys a bucket: the estimate is +-3 %, and a bucket past ~1100 keys makes
+    // both the count and the graph phase's probes measurably slower -- headline A/B 8192 against
+    // 4096 buckets: k_skbucket 1.65 / 2.37 ms, links 0.56 / 1.07 ms)
     int bbits = SK2_CBITS;
-    while (bbits < SK2_BBITS && est / (double)(1ull << bbits) > 1100.0) bbits++;
+    while (bbits < SK2_BBITS && est / (double)(1ull << bbits) > 800.0) bbits++;
     plan.bbits = bbits;
     plan.slots = est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
     const uint64_t Bk = 1ull << bbits;
@@ -590,12 +593,8 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     do {                                                                                                      \
         if (nodedup)                                                                                          \
             k_skbucket_rec<SLOTS, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS);             \
-        else if (kn().sk2_rb == 2)                                                                            \
-            k_skbucket<SLOTS, RS, 2, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg);     \
-        else if (kn().sk2_rb == 1)                                                                            \
-            k_skbucket<SLOTS, RS, 1, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg);     \
         else                                                                                                  \
-            k_skbucket<SLOTS, RS, 4, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg);     \
+            k_skbucket<SLOTS, RS, 1, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg, kn().sk2_exp);     \
     } while (0)
     // EULERHIP_SK2_STATS: distinct records, flushes and windows rolled out (stderr)
     unsigned long long *dbg = nullptr;
@@ -1824,13 +1823,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->tailOf.ensure(Nn * 4));
     EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
     EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->skew, 0, 4, st));  // k_emit: a position past the character bound
     if (U)
         k_emit<Ops><<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
                                             s->PL.as<unsigned int>(), s->dkey.as<typename Ops::K>(),
                                             s->cidxOf.as<unsigned int>(), s->cwalk.as<Walk>(), s->coff.as<unsigned long long>(),
-                                            N, k, s->chars.as<char>(), s->cfirst.as<unsigned int>(),
-                                            s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
-                                            s->tailOf.as<unsigned int>());
+                                            N, k, s->chars.as<char>(), std::max<uint64_t>(chars_bound, 1),
+                                            s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(),
+                                            s->headOf.as<unsigned int>(), s->tailOf.as<unsigned int>(), &dsc->skew);
     mark(s, 2 * EC_STAGE_EMIT + 1);
 
     // ---- GFA ------------------------------------------------------------------------------
@@ -1858,8 +1858,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
         EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, st));
     }
+    unsigned int emit_bad = 0;
+    EC_HIP(hipMemcpyAsync(&emit_bad, &dsc->skew, 4, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));  // h_coff[nc] (the characters), h_loff
     const uint64_t nchars = s->h_coff[nc];
+    if (emit_bad) {
+        set_error("contig characters past their bound %llu (inconsistent ranking)", (unsigned long long)chars_bound);
+        return EC_ERR_STATE;
+    }
     s->stats.n_contig_chars = nchars;
     if (nchars > chars_bound) {
         set_error("contig characters %llu past their bound %llu", (unsigned long long)nchars,

@@ -39,7 +39,7 @@ void refresh_knobs() {
         k.wide_max_bbits = num("EULERHIP_WIDE_MAX_BBITS", -1);
         k.host_chunks = num("EULERHIP_HOST_CHUNKS", 0);
         k.sk2_nodedup = flag("EULERHIP_SK2_NODEDUP");
-        k.sk2_rb = num("EULERHIP_SK2_RB", 0);
+        k.sk2_exp = num("EULERHIP_SK2_EXP", 0);
         k.sk2_stats = flag("EULERHIP_SK2_STATS");
         k.verbose = flag("EULERHIP_VERBOSE");
     }

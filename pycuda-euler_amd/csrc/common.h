@@ -36,7 +36,8 @@ struct Knobs {
     int wide_max_bbits = -1;    // EULERHIP_WIDE_MAX_BBITS: cap the wide buckets (forces overflow)
     int host_chunks = 0;        // EULERHIP_HOST_CHUNKS: host-input chunks (0 = ~32 MiB each)
     bool sk2_nodedup = false;   // EULERHIP_SK2_NODEDUP: record-per-lane k_skbucket_rec (A/B)
-    int sk2_rb = 0;             // EULERHIP_SK2_RB: k_skbucket records per thread and round (A/B)
+    int sk2_exp = 0;            // EULERHIP_SK2_EXP bit 2: no reverse complement in k_skbucket's record
+                                // keys (A/B; results stay exact)
     bool sk2_stats = false;     // EULERHIP_SK2_STATS: k_skbucket dedup statistics on stderr
     bool verbose = false;       // EULERHIP_VERBOSE: count-path fallbacks on stderr
 };

@@ -55,12 +55,27 @@ __host__ __device__ inline uint32_t sk2_nmax(int k) {
 __device__ inline uint32_t sk_bases16(const uint32_t *st, uint32_t p) {
     return __builtin_amdgcn_alignbit(st[(p >> 4) + 1], st[p >> 4], 2 * (p & 15));
 }
+// u8 HyperLogLog register max by CAS on the word holding it
+__device__ inline void sk_hll_put(unsigned int *s_hll, uint32_t hh) {
+    const uint32_t hj = hh >> (32 - HLL_REG_BITS);
+    const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+    const uint32_t hs = (hj & 3) * 8;
+    uint32_t old = s_hll[hj >> 2];
+    while (rho > ((old >> hs) & 0xFFu)) {
+        const uint32_t nw = (old & ~(0xFFu << hs)) | (rho << hs);
+        const uint32_t prev = atomicCAS(&s_hll[hj >> 2], old, nw);
+        if (prev == old) break;
+        old = prev;
+    }
+}
+
 template <int C>
 __device__ inline void skpart_flush(uint32_t cntw, const uint32_t *ent, uint16_t *srt, unsigned int *wcnt,
                                     unsigned int *cur, unsigned long long *base, const uint32_t *rel,
                                     const uint32_t *st, uint32_t lane, unsigned long long gcap, uint64_t cap,
                                     unsigned long long spill, uint32_t M, uint32_t rtile, uint4 *recs,
-                                    unsigned int *overflow) {
+                                    unsigned int *overflow, unsigned int *s_hll, uint32_t smaskb, int k,
+                                    uint64_t kmask) {
     wave_sync();
     for (uint32_t i = lane; i < cntw; i += 64) atomicAdd(&wcnt[ent[i] >> 26], 1u);
     wave_sync();
@@ -94,23 +109,19 @@ __device__ inline void skpart_flush(uint32_t cntw, const uint32_t *ent, uint16_t
         o.z = (sk_bases16(st, p0 + 32) & 0x0FFFFFFFu) | n1 << 28;
         o.w = ((e >> 18) & ((1u << SK2_FBITS) - 1)) << 24 | ((rtile + lr) * M + i0);
         recs[base[e >> 26] + i] = o;
+        // HyperLogLog over the k-mers of the runs whose minimizer's low bucket bits & smaskb are 0
+        // (a sample of minimizer space; a k-mer and its twin share the minimizer): each window's
+        // canonical k-mer out of the stage
+        if (((e >> 18) & smaskb) == 0) {
+            for (uint32_t q = 0; q <= n1; q++) {
+                const uint64_t K = (uint64_t)sk_bases16(st, p0 + q) | (uint64_t)sk_bases16(st, p0 + q + 16) << 32;
+                const uint64_t krc = ~K & kmask, kfw = rev2_64(K) >> (64 - 2 * k);
+                sk_hll_put(s_hll, (uint32_t)(mix64(kfw < krc ? kfw : krc) >> 32));
+            }
+        }
     }
     wave_sync();
     if (lane < (uint32_t)C) wcnt[lane] = 0;
-}
-
-// u8 HyperLogLog register max by CAS on the word holding it
-__device__ inline void sk_hll_put(unsigned int *s_hll, uint32_t hh) {
-    const uint32_t hj = hh >> (32 - HLL_REG_BITS);
-    const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
-    const uint32_t hs = (hj & 3) * 8;
-    uint32_t old = s_hll[hj >> 2];
-    while (rho > ((old >> hs) & 0xFFu)) {
-        const uint32_t nw = (old & ~(0xFFu << hs)) | (rho << hs);
-        const uint32_t prev = atomicCAS(&s_hll[hj >> 2], old, nw);
-        if (prev == old) break;
-        old = prev;
-    }
 }
 
 // Region of (c, g): records [(g * C + c) * cap, + cap) of recs, spill records at C * G * cap
@@ -235,7 +246,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
         }
         const uint32_t nrounds = __any(has) ? (M + W - 1) / W : 0u;
         if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
-        uint32_t runv = 0, runn = 0, runi = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
+        uint32_t runv = 0, runn = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
+        const uint32_t inc = has ? 1u : 0u;
         const uint32_t rtile = 64 * t;  // the tile's first read relative to g0
         for (uint32_t round = 0; round < nrounds; round++) {
             const uint32_t w0 = round * W;  // first window of the round
@@ -251,30 +263,23 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
                 push_base(j < 16 ? (xb0 >> (2 * j)) & 3u : (xb1 >> (2 * (j - 16))) & 3u);
                 H[j] = mmer_hash(mf < mr ? mf : mr);
                 P = min(P, H[j]);
-                const bool ok = has;
-                // HyperLogLog over the k-mers of sampled minimizers (their canonical k-mer from the stage)
-                if (ok && (v & smask) == 0) {
-                    const uint32_t p = rel + w0 + j;
-                    const uint64_t K = (uint64_t)sk_bases16(st, p) | (uint64_t)sk_bases16(st, p + 16) << 32;
-                    const uint64_t krc = ~K & kmask, kfw = rev2_64(K) >> (64 - 2 * k);
-                    sk_hll_put(s_hll, (uint32_t)(mix64(kfw < krc ? kfw : krc) >> 32));
-                }
-                const bool close = ok && runn && (v != runv || runn == nmax);
-                const uint64_t bal = __ballot(close);
-                if (close) {
-                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
-                }
-                cntw += (uint32_t)__popcll(bal);
-                if (ok) {
-                    if (close || !runn) {
-                        runv = v;
-                        runi = w0 + j;
-                        runn = 0;
+                // the run of windows [w0 + j - runn, w0 + j) closes when the minimizer changes or it
+                // holds nmax windows; a lane without a read keeps runn = 0 and never closes.  Between
+                // closes v == runv, so runv = v every window (no select), and the run's first window
+                // is derived at the close (no per-window bookkeeping for it)
+                const bool close = runn != 0 && (v != runv || runn == nmax);
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(close);
+                if (bal) {
+                    if (close) {
+                        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                        ent[cntw + rk] = lane | (w0 + j - runn) << 6 | (runn - 1) << 14 |
+                                         (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
                     }
-                    runn++;
+                    cntw += (uint32_t)__popcll(bal);
                 }
+                runv = v;
+                runn = (close ? 0u : runn) + inc;
             }
             // the next round's suffix minima (the block's unused tail at the read's end is never read)
 #pragma unroll
@@ -282,13 +287,13 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
 #pragma unroll
             for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
             const bool last = round + 1 == nrounds;
-            if (last) {  // the reads' final runs
-                const bool fin = has && runn;
+            if (last) {  // the reads' final runs: windows [M - runn, M)
+                const bool fin = runn != 0;
                 const uint64_t bal = __ballot(fin);
                 if (fin) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = lane | runi << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
+                    ent[cntw + rk] = lane | (M - runn) << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
                 }
                 cntw += (uint32_t)__popcll(bal);
                 if (more) EC_PT_ISSUE(t + PT_WAVES);
@@ -296,7 +301,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
             // flush: the buffer could not take another round, or the stage is about to change
             if (last || cntw > (uint32_t)(SK2_ECAP_W - 64 * (W + 1))) {
                 skpart_flush<C>(cntw, ent, s_srt[wid], s_wcnt[wid], s_cur, s_base[wid], s_rel[wid], st, lane, gcap,
-                                cap, spill, M, rtile, recs, overflow);
+                                cap, spill, M, rtile, recs, overflow, s_hll, smask ? 0xFFu : 0u, k, kmask);
                 cntw = 0;
             }
         }
@@ -596,11 +601,13 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *re
 // the twin of window n - 1 - o).  Identical canonical records have identical window strings, so
 // min over copies of (A + o) = min A + o: the distinct records insert their windows once, with
 // add = multiplicity, and every key's count and first events equal the per-record inserts'.
-// The record table holds RS distinct records; before a chunk could overfill it, its records are
-// rolled into the k-mer table and it is cleared (a cache: any split of the copies is exact).
-// Probing claims a slot by CAS on a tag word (20 hash bits | "claimed in this chunk" | claimer's
-// thread); a slot claimed in this chunk is compared against the claimer's staged key (LDS), an
-// older one against the stored key, so one wave-uniform loop resolves every record.
+// The record table takes up to RS / 2 distinct records; a record that finds no entry once it is
+// that full is rolled out on its own (any split of the copies between entries is exact).
+// Probing claims a slot by CAS on a tag word (20 hash bits | PEND), stores the key and publishes
+// it by clearing PEND (release); a prober compares keys only behind a published tag (acquire), so
+// no barrier is needed -- a record that meets a pending slot of its own key just takes another
+// entry.  Each thread takes RB records per round: their loads, canonical forms and probe chains
+// overlap (one record per thread was bound by the latency of its dependent LDS round trips).
 __device__ inline uint32_t rev2_32b(uint32_t v) {  // superkmer.h rev2_32 with one v_bfrev_b32
     v = __builtin_bitreverse32(v);
     return ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
@@ -613,9 +620,14 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
                                                              unsigned int *dcnt, unsigned long long *dfc,
                                                              unsigned long long *dft, SubSlot *sub,
                                                              unsigned int *nsolid, unsigned long long *ndistinct,
-                                                             unsigned int *overflow, unsigned long long *dbg) {
+                                                             unsigned int *overflow, unsigned long long *dbg,
+                                                             int exp) {
     constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
     constexpr uint32_t PEND = 0x800u;  // tag word: the claimer has not yet stored the key
+    // entries claimed at most: half the slots, and low enough that the claims a block can have in
+    // flight past the check (one per record being probed) still leave a free slot
+    constexpr unsigned int CLAIM_MAX = RS / 2 < RS - 1 - RB * BUCKET_THREADS ? RS / 2 : RS - 1 - RB * BUCKET_THREADS;
+    static_assert(RS > RB * BUCKET_THREADS + 1, "record table too small for the records in flight");
     __shared__ LTabE<SLOTS> tab;
     __shared__ unsigned int s_over[2];
     __shared__ uint32_t r_tag[RS], r_x[RS], r_y[RS], r_z[RS], r_mult[RS], r_a[RS], r_b[RS];
@@ -729,25 +741,20 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
             const bool valid = ri < r1;
             const uint4 x = nx[j];
             if (ri + ROUND < r1) nx[j] = recs[ri + ROUND];  // next round's records
-            // canonical content of the record
-            const unsigned int n = (x.z >> 28) + 1, L = n + (unsigned int)k - 1;  // L in [k, 46]
-            uint32_t x0 = x.x, x1 = x.y, x2 = x.z & 0x0FFFFFFFu;
-            if (2 * L < 64) x1 &= (1u << (2 * L - 32)) - 1u, x2 = 0;
-            else x2 &= (1u << (2 * L - 64)) - 1u;
+            // canonical content of the record (branch-free: selects, no divergent paths)
+            const unsigned int n = (x.z >> 28) + 1, L2 = 2 * (n + (unsigned int)k - 1);  // 2L in [2k, 92]
+            const uint32_t m1 = L2 >= 64 ? 0xFFFFFFFFu : (1u << ((L2 - 32) & 31)) - 1u;  // bits of word 1
+            const uint32_t mw2 = L2 > 64 ? (1u << ((L2 - 64) & 31)) - 1u : 0u;           // bits of word 2
+            const uint32_t x0 = x.x, x1 = x.y & m1, x2 = x.z & mw2;
             // reverse complement of the L bases: rev2 of the 96-bit string (base i -> 47 - i), then
-            // down by 2 (48 - L) bits, complemented
+            // down by 96 - 2L bits (4 .. 54), complemented
             const uint32_t y0 = rev2_32b(x2), y1 = rev2_32b(x1), y2 = rev2_32b(x0);
-            const unsigned int sft = 2 * (48 - L);  // 4 .. 54
-            uint32_t q0, q1, q2;
-            if (sft < 32) {
-                q0 = __builtin_amdgcn_alignbit(y1, y0, sft), q1 = __builtin_amdgcn_alignbit(y2, y1, sft), q2 = y2 >> sft;
-            } else {
-                q0 = __builtin_amdgcn_alignbit(y2, y1, sft - 32), q1 = y2 >> (sft - 32), q2 = 0;
-            }
-            q0 = ~q0;
-            if (2 * L < 64) q1 = ~q1 & ((1u << (2 * L - 32)) - 1u), q2 = 0;
-            else q1 = ~q1, q2 = ~q2 & ((1u << (2 * L - 64)) - 1u);
-            const bool flip = q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0;
+            const unsigned int sft = 96 - L2, s5 = sft & 31;
+            const bool lo = sft < 32;
+            const uint32_t a0 = __builtin_amdgcn_alignbit(y1, y0, s5), a1 = __builtin_amdgcn_alignbit(y2, y1, s5),
+                           a2 = y2 >> s5;
+            const uint32_t q0 = ~(lo ? a0 : a1), q1 = ~(lo ? a1 : a2) & m1, q2 = lo ? ~a2 & mw2 : 0u;
+            const bool flip = !(exp & 4) && (q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0);
             // events of window 0: A = read 2M + first window, B = read 2M + 2M - 1 - first window
             const unsigned int p = x.w;
             const unsigned int rd0 = (unsigned int)((double)p * inv_m);  // p / M, corrected below
@@ -773,37 +780,48 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
             for (int j = 0; j < RB; j++) a |= ST[j] == 0;
             return a;
         };
+        // a step reads every chain's tag and key words (in program order: a published tag read
+        // first implies the key words read after it are the stored key -- DS operations of a wave
+        // complete in order), compares branch-free, and only the rare empty slot takes the claim
+        // path; a chain that is done re-reads its slot harmlessly
+        const volatile uint32_t *vt = r_tag, *vx = r_x, *vy = r_y, *vz = r_z;
 #pragma unroll 1
         while (__any(searching())) {
-            uint32_t T[RB];
+            uint32_t T[RB], X[RB], Y[RB], Z[RB];
 #pragma unroll
-            for (int j = 0; j < RB; j++)  // the tag reads of every chain first
-                T[j] = ST[j] == 0 ? __hip_atomic_load(&r_tag[SL[j]], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : 1u;
+            for (int j = 0; j < RB; j++) T[j] = vt[SL[j]];
+#pragma unroll
+            for (int j = 0; j < RB; j++) X[j] = vx[SL[j]], Y[j] = vy[SL[j]], Z[j] = vz[SL[j]];
+            bool claim = false;
 #pragma unroll
             for (int j = 0; j < RB; j++) {
-                if (ST[j] != 0) continue;
-                const unsigned int slot = SL[j];
-                uint32_t t = T[j];
-                if (t == 0) {
-                    if (atomicAdd(&s_nent, 1u) >= (unsigned int)RS - 1) {  // keep one slot free
-                        atomicSub(&s_nent, 1u);
+                const bool hit = T[j] == TG[j] && X[j] == K0[j] && Y[j] == K1[j] && Z[j] == K2[j];
+                const bool go = ST[j] == 0;
+                ST[j] = go && hit ? 1 : ST[j];
+                claim |= go && !hit && T[j] == 0;
+                // a published tag of another key, or a pending one of other tag bits: the next slot;
+                // a pending slot of this tag is read again (its claimer publishes within a few
+                // instructions), so concurrent copies of a new record share one entry
+                if (go && !hit && T[j] != 0 && T[j] != (TG[j] | PEND))
+                    SL[j] = SL[j] + 1 == (unsigned int)RS ? 0u : SL[j] + 1;
+            }
+            if (claim) {
+#pragma unroll
+                for (int j = 0; j < RB; j++) {
+                    if (ST[j] != 0 || T[j] != 0) continue;
+                    const unsigned int slot = SL[j];
+                    // claims stop at CLAIM_MAX entries (a plain read: at most a block's worth of
+                    // claims in flight overshoot it, so free slots always remain and a miss meets
+                    // one within a few probes -- linear probing near full scans the table)
+                    if (*(volatile unsigned int *)&s_nent >= CLAIM_MAX) {
                         ST[j] = 2;
-                    } else {
-                        t = atomicCAS(&r_tag[slot], 0u, TG[j] | PEND);
-                        if (t == 0) {  // claimed: store the key, then publish it
-                            r_x[slot] = K0[j], r_y[slot] = K1[j], r_z[slot] = K2[j];
-                            __hip_atomic_store(&r_tag[slot], TG[j], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            ST[j] = 1;
-                        } else {
-                            atomicSub(&s_nent, 1u);
-                        }
-                    }
+                    } else if (atomicCAS(&r_tag[slot], 0u, TG[j] | PEND) == 0) {  // store the key, publish
+                        r_x[slot] = K0[j], r_y[slot] = K1[j], r_z[slot] = K2[j];
+                        __hip_atomic_store(&r_tag[slot], TG[j], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        atomicAdd(&s_nent, 1u);
+                        ST[j] = 1;
+                    }  // (lost the race: the slot is read again next step)
                 }
-                // a slot whose key is still pending counts as another key: at worst the record
-                // gets a second entry (both are rolled out: still exact)
-                if (ST[j] == 0 && t == TG[j] && r_x[slot] == K0[j] && r_y[slot] == K1[j] && r_z[slot] == K2[j])
-                    ST[j] = 1;
-                if (ST[j] == 0) SL[j] = slot + 1 == (unsigned int)RS ? 0u : slot + 1;
             }
         }
 #pragma unroll

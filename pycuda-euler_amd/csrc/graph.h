@@ -665,8 +665,9 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
                                               const unsigned int *PL, const typename Ops::K *dkey,
                                               const unsigned int *cidxOf, const Walk *cwalk,
                                               const unsigned long long *coff, unsigned int N, int k, char *chars,
-                                              unsigned int *cfirst, unsigned int *clast, unsigned int *headOf,
-                                              unsigned int *tailOf) {
+                                              unsigned long long chars_bound, unsigned int *cfirst,
+                                              unsigned int *clast, unsigned int *headOf, unsigned int *tailOf,
+                                              unsigned int *bad) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         if ((x & 1) && upal[x >> 1]) continue;
@@ -690,6 +691,12 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
             }
         }
         if (pos < 0) continue;
+        // the buffer holds the bound 2U + nc (k - 1) the host sized it for: a position past it
+        // (never, for a consistent ranking) is reported instead of written
+        if (coff[ci] + (unsigned long long)(k - 1) + (unsigned long long)pos >= chars_bound) {
+            atomicOr(bad, 1u);
+            continue;
+        }
         const typename Ops::K code = node_code<Ops>(dkey, x, k);
         char *dst = chars + coff[ci];
         if (pos == 0) {
