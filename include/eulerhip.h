@@ -297,9 +297,14 @@ uint64_t ec_dense_count(ec_session *s);
  * Owner of a canonical key: for 21 <= k <= 32 the range of its minimizer ((minimizer * nowners)
  * >> 32, the merge / load bucket key), else a 64-bit hash of the key (shard.h OwnerFn). */
 int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts);
+/* owner rule of ec_export_by_owner: 0 (default) = the minimizer's range for 21 <= k <= 32, else a
+ * key hash; 1 = the key hash always (distributed.py switches every rank to it when the job's
+ * minimizer-range counts, all-reduced, show one owner past twice the mean -- low-complexity
+ * input).  A counts-only call (d_out = NULL) followed by the scatter call reuses the owner ids. */
+int ec_session_set_owner_rule(ec_session *s, int rule);
 /* owner side: aggregate received records, keep count > limit */
 int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags);
-/* copy the held records (ec_merge_owned's solid set) to d_out */
+/* copy the held records to d_out (after ec_count_shard with global first events, as the export) */
 int ec_export_dense(ec_session *s, void *d_out);
 /* ec_merge_owned + ec_export_dense in one call (no host round trip between them); d_out holds
  * up to n records, ec_dense_count gives how many were written */

@@ -164,6 +164,13 @@ struct ec_session {
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
+    int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 32), 1 key hash
+    // ec_export_by_owner's owner ids / scanned chunk histogram of the last call, reused by a
+    // following call with the same records, owners and rule (counts first, then the scatter)
+    bool own_valid = false;
+    int own_rule = 0, own_nowners = 0;
+    unsigned int own_n = 0, own_nblk = 0;
+    std::vector<unsigned int> own_hi;
     // host-input pipeline (ec_assemble_host / ec_assemble_packed_host, hostin.h): the reads are
     // copied H2D in chunks on cstream; pipe_upto(c) makes chunks .. c visible to the session
     // stream (event wait + unpack) -- the super-k-mer partition runs on each chunk's read groups
@@ -328,6 +335,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     s->want_dict = (flags & EC_FLAG_WANT_DICT) != 0;
     s->flags = flags;
     s->shard_base = 0;
+    s->own_valid = false;
     const bool timing = (flags & (EC_FLAG_TIMING | EC_FLAG_KERNEL_TIMING)) != 0;
     s->stage_timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
@@ -2259,6 +2267,16 @@ int ec_count_shard(ec_session *s, const uint8_t *d_reads, const uint64_t *d_offs
     return EC_OK;
 }
 
+int ec_session_set_owner_rule(ec_session *s, int rule) {
+    if (!s || rule < 0 || rule > 1) {
+        set_error("bad owner rule %d", rule);
+        return EC_ERR_ARG;
+    }
+    if (rule != s->owner_rule) s->own_valid = false;
+    s->owner_rule = rule;
+    return EC_OK;
+}
+
 int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts) {
     refresh_knobs();
     if (!s || nowners < 1 || nowners > MAX_OWNERS || !owner_counts) {
@@ -2274,18 +2292,23 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
     EC_CHECK(s->ocnt.ensure(2 * nbh * 4));
     unsigned int *bh = s->ocnt.as<unsigned int>(), *bhi = bh + nbh;
     const bool wide = s->k > 32;
-    std::vector<unsigned int> hi(nbh, 0u);
-    const OwnerFn own = owner_fn(s->k);
+    OwnerFn own = owner_fn(s->k);
+    if (s->owner_rule == 1) own.sk = 0;  // key-hash owners (a skewed minimizer distribution)
     EC_CHECK(s->mbid.ensure(std::max<uint64_t>(n, 1) * 4));  // owner of each record (free until a merge)
     unsigned int *oid = s->mbid.as<unsigned int>();
-    if (n) {
-        if (wide)
-            k_owner_hist<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), n, nowners, nblk, bh, own, oid);
-        else
-            k_owner_hist<unsigned long long><<<nblk, B, 0, st>>>(s->dkey.as<unsigned long long>(), n, nowners, nblk, bh,
-                                                                own, oid);
-        EC_CHECK(scan_incl_u32(s, bh, bhi, nbh));
-        EC_HIP(hipMemcpyAsync(hi.data(), bhi, nbh * 4, hipMemcpyDeviceToHost, st));
+    const bool reuse = s->own_valid && s->own_rule == s->owner_rule && s->own_nowners == nowners && s->own_n == n &&
+                       s->own_nblk == nblk;
+    if (!reuse) {
+        s->own_hi.assign(nbh, 0u);
+        if (n) {
+            if (wide)
+                k_owner_hist<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), n, nowners, nblk, bh, own, oid);
+            else
+                k_owner_hist<unsigned long long><<<nblk, B, 0, st>>>(s->dkey.as<unsigned long long>(), n, nowners, nblk,
+                                                                    bh, own, oid);
+            EC_CHECK(scan_incl_u32(s, bh, bhi, nbh));
+            EC_HIP(hipMemcpyAsync(s->own_hi.data(), bhi, nbh * 4, hipMemcpyDeviceToHost, st));
+        }
     }
     if (n && d_out) {  // the scatter is queued before the host waits for the owner counts
         if (wide)
@@ -2300,9 +2323,10 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
                 s->shard_base << 32, oid);
     }
     EC_HIP(hipStreamSynchronize(st));
+    s->own_valid = true, s->own_rule = s->owner_rule, s->own_nowners = nowners, s->own_n = n, s->own_nblk = nblk;
     unsigned long long prev = 0;
     for (int i = 0; i < nowners; i++) {
-        const unsigned long long end = n ? hi[(size_t)(i + 1) * nblk - 1] : 0ull;
+        const unsigned long long end = n ? s->own_hi[(size_t)(i + 1) * nblk - 1] : 0ull;
         owner_counts[i] = end - prev;
         prev = end;
     }
@@ -2341,11 +2365,11 @@ int ec_export_dense(ec_session *s, void *d_out) {
         if (s->k > 32)
             k_export_dense<K128><<<grid_for(n, 256), 256, 0, s->stream>>>(
                 s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), n, reinterpret_cast<AggW *>(d_out));
+                s->dft.as<unsigned long long>(), n, reinterpret_cast<AggW *>(d_out), s->shard_base << 32);
         else
             k_export_dense<unsigned long long><<<grid_for(n, 256), 256, 0, s->stream>>>(
                 s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                s->dft.as<unsigned long long>(), n, reinterpret_cast<Agg *>(d_out));
+                s->dft.as<unsigned long long>(), n, reinterpret_cast<Agg *>(d_out), s->shard_base << 32);
         EC_HIP(hipStreamSynchronize(s->stream));
     }
     return EC_OK;

@@ -154,12 +154,17 @@ __global__ void __launch_bounds__(256) k_merge_agg(const Agg *in, uint64_t n, Sl
     }
 }
 
+// evbase: after ec_count_shard the first events are shard-relative (+ read_base << 32 makes them
+// global, as k_owner_scatter does); after a merge they are global already (evbase 0)
 template <typename K>
 __global__ void __launch_bounds__(256) k_export_dense(const K *dkey, const unsigned int *dcnt,
                                                       const unsigned long long *dfc, const unsigned long long *dft,
-                                                      unsigned int n, typename RecOf<K>::T *out) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
-        out[t] = RecOf<K>::make(dkey[t], dcnt[t], dfc[t], dft[t]);
+                                                      unsigned int n, typename RecOf<K>::T *out,
+                                                      unsigned long long evbase) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long fc = dfc[t], ft = dft[t];
+        out[t] = RecOf<K>::make(dkey[t], dcnt[t], fc == NONE64 ? fc : fc + evbase, ft == NONE64 ? ft : ft + evbase);
+    }
 }
 
 

@@ -43,6 +43,22 @@ _U64 = ctypes.c_uint64
 eulerhip.register("ec_count_shard", ctypes.c_int, [_P, _P, _P, _U64, _U64, ctypes.c_int, ctypes.c_uint])
 eulerhip.register("ec_dense_count", ctypes.c_uint64, [_P])
 eulerhip.register("ec_export_by_owner", ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.POINTER(ctypes.c_uint64)])
+eulerhip.register("ec_session_set_owner_rule", ctypes.c_int, [_P, ctypes.c_int])
+
+# owner rules (ec_session_set_owner_rule): minimizer ranges (21 <= k <= 32), or a key hash when
+# the job's minimizer-range counts are skewed past SKEW times the mean owner (low-complexity input:
+# one minimizer can own most records; the merge then falls to the HBM table and every rank pays
+# the all-gather padding of the largest part)
+OWNER_MINIMIZER, OWNER_HASH = 0, 1
+SKEW = 2.0
+
+
+def owner_rule_for(totals, k):
+    """the rule every rank takes, from the all-reduced per-owner record counts"""
+    if not 21 <= k <= 32 or len(totals) < 2:
+        return OWNER_MINIMIZER
+    mean = sum(totals) / len(totals)
+    return OWNER_HASH if mean > 0 and max(totals) > SKEW * mean else OWNER_MINIMIZER
 eulerhip.register("ec_merge_owned", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint])
 eulerhip.register("ec_export_dense", ctypes.c_int, [_P, _P])
 eulerhip.register("ec_assemble_from_solid", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_uint])
@@ -92,6 +108,15 @@ class HipEngine:
 
     def rec_bytes(self):
         return int(self.L.ec_record_bytes(self.k))
+
+    def owner_counts(self, nowners):
+        """records per owner under the current rule (no export; the owner ids are kept for it)"""
+        counts = (ctypes.c_uint64 * nowners)()
+        eulerhip.check(self.L.ec_export_by_owner(self._h(), int(nowners), None, counts))
+        return [int(c) for c in counts]
+
+    def set_owner_rule(self, rule):
+        eulerhip.check(self.L.ec_session_set_owner_rule(self._h(), int(rule)))
 
     def export_by_owner(self, nowners):
         n = int(self.L.ec_dense_count(self._h()))
@@ -202,6 +227,13 @@ class TorchComm:
         dist.all_gather_into_tensor(out, pad, group=self.group)
         return (out, szl) if with_sizes else out
 
+    def allreduce_vec(self, vals):
+        """element-wise sum over the ranks of a list of integers"""
+        dev = "cuda" if self.dist.get_backend(self.group) == "nccl" else "cpu"
+        t = self.torch.tensor([int(v) for v in vals], dtype=self.torch.int64, device=dev)
+        self.dist.all_reduce(t, group=self.group)
+        return [int(x) for x in t.tolist()]
+
     def allreduce_sum(self, v):
         dev = "cuda" if self.dist.get_backend(self.group) == "nccl" else "cpu"
         t = self.torch.tensor([int(v)], dtype=self.torch.int64, device=dev)
@@ -236,6 +268,11 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     tick("count")
     if on_count:
         on_count(st)
+    if comm.world > 1 and 21 <= k <= 32:  # one owner rule for every rank, from the job's counts
+        engine.set_owner_rule(OWNER_MINIMIZER)
+        rule = owner_rule_for(comm.allreduce_vec(engine.owner_counts(comm.world)), k)
+        if rule != OWNER_MINIMIZER:
+            engine.set_owner_rule(rule)
     recs, counts = engine.export_by_owner(comm.world)
     tick("export")
     # the job's k-mer positions ride along with the exchange's byte counts
@@ -353,7 +390,16 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
         st = eng.count_shard(d_reads, d_off, n, lo, k, flags)
         eng.count_variant = int(st.count_variant)
         P += st.n_positions
+    rule = OWNER_MINIMIZER
+    if world > 1 and 21 <= k <= 32:  # as sharded_assemble: the summed owner counts decide the rule
+        for eng in engines:
+            eng.set_owner_rule(OWNER_MINIMIZER)
+        rule = owner_rule_for([sum(c) for c in zip(*[eng.owner_counts(world) for eng in engines])], k)
+    for eng in engines:
+        eng.set_owner_rule(rule)
         sends.append(eng.export_by_owner(world))
+    local_sharded_assemble_shards.last_rule = rule
+    local_sharded_assemble_shards.last_counts = [c for _, c in sends]
     solids = []
     for dst, eng in enumerate(engines):
         parts = []

@@ -61,9 +61,9 @@ def minimizer_of(c, k, m=15):
     return _min_remix(v)
 
 
-def owner_fn(key, n, k):
-    """shard.h OwnerFn: the minimizer's range for 21 <= k <= 32, else the key hash"""
-    if 21 <= k <= 32:
+def owner_fn(key, n, k, rule=0):
+    """shard.h OwnerFn: the minimizer's range for 21 <= k <= 32 (rule 0), else the key hash"""
+    if 21 <= k <= 32 and rule == 0:
         return (minimizer_of(key, k) * n) >> 32
     return owner_of(key, n)
 
@@ -112,10 +112,21 @@ class FakeEngine:
         self.recs = out
         return _Stats(P)
 
+    rule = 0
+    last_counts = None
+
+    def set_owner_rule(self, rule):
+        self.rule = rule
+
+    def owner_counts(self, nowners):
+        own = [owner_fn(int(x), nowners, self.k, self.rule) for x in self.recs["key"]]
+        return [own.count(o) for o in range(nowners)]
+
     def export_by_owner(self, nowners):
-        own = np.array([owner_fn(int(x), nowners, self.k) for x in self.recs["key"]], dtype=np.int64)
+        own = np.array([owner_fn(int(x), nowners, self.k, self.rule) for x in self.recs["key"]], dtype=np.int64)
         order = np.argsort(own, kind="stable")
         counts = [int((own == o).sum()) for o in range(nowners)]
+        self.last_counts = counts
         return self._bytes(self.recs[order]), counts
 
     def merge_owned(self, recs, k, limit, flags=0):

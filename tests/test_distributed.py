@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None):
+def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None, want_counts=False):
     import torch
     import torch.distributed as dist
 
@@ -42,21 +42,22 @@ def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None):
         buf = "".join(mine).encode()
         off = np.zeros(len(mine) + 1, np.int64)
         off[1:] = np.cumsum([len(r) for r in mine])
-        res, P = distributed.sharded_assemble(FakeEngine(k), distributed.TorchComm(),
+        eng = FakeEngine(k)
+        res, P = distributed.sharded_assemble(eng, distributed.TorchComm(),
                                               torch.frombuffer(bytearray(buf or b"\0"), dtype=torch.uint8),
                                               torch.from_numpy(off), len(mine), lo if gap is None else rank * gap,
                                               k, limit,
                                               partitioned=partitioned)
-        q.put((rank, P, res.contigs, res.links))
+        q.put((rank, P, res.contigs, res.links) + ((eng.rule, eng.last_counts) if want_counts else ()))
     finally:
         dist.destroy_process_group()
 
 
-def _run(reads, k, limit, world, partitioned=None, gap=None):
+def _run(reads, k, limit, world, partitioned=None, gap=None, want_counts=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q, partitioned, gap))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q, partitioned, gap, want_counts))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -108,3 +109,37 @@ def test_shard_range_partitions_reads():
             spans = [distributed.shard_range(n, r, w) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def test_sharded_skewed_minimizers_take_hash_owners():
+    """low-complexity reads: most k-mers share a few minimizers, so minimizer-range owners would
+    put most records on one rank; the all-reduced owner counts switch every rank to key-hash
+    owners (ec_session_set_owner_rule), and the exchange is balanced"""
+    rng = np.random.default_rng(61)
+    # 15 A's (mmer_hash 0, the global minimum m-mer) every 17 bases: every 31-mer holds one, so
+    # every k-mer of g1 has the same minimizer; g2 is ordinary random sequence
+    g1 = "".join("A" * 15 + "".join("ACGT"[x] for x in rng.integers(0, 4, 2)) for _ in range(180))
+    g2 = "".join("ACGT"[x] for x in rng.integers(0, 4, 1500))
+    reads = []
+    for g, n in ((g1, 200), (g2, 80)):
+        for _ in range(n):
+            p = int(rng.integers(0, len(g) - 70))
+            reads.append(g[p:p + 70])
+    _, rc, rl = oracle.assemble(reads, 31, 1, want_dict=False)
+    world = 3
+    out = _run(reads, 31, 1, world, want_counts=True)
+    rules = {o[4] for o in out}
+    assert rules == {1}, rules  # every rank switched
+    totals = [sum(o[5][d] for o in out) for d in range(world)]
+    assert max(totals) <= 2.0 * (sum(totals) / world), totals
+    for rank, P, contigs, links, _, _ in out:
+        assert contigs == rc and links == rl
+
+
+def test_owner_rule_balanced_input_keeps_minimizers():
+    import distributed
+
+    assert distributed.owner_rule_for([100, 110, 95], 31) == distributed.OWNER_MINIMIZER
+    assert distributed.owner_rule_for([300, 10, 5], 31) == distributed.OWNER_HASH
+    assert distributed.owner_rule_for([300, 10, 5], 45) == distributed.OWNER_MINIMIZER  # key hash already
+    assert distributed.owner_rule_for([300], 31) == distributed.OWNER_MINIMIZER

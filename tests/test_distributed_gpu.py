@@ -210,17 +210,22 @@ def test_owner_rule_matches_fake_engine(engines, k):
     buf, off = make_reads(5_000, 1_500, 100, 7801)
     eng = engines[0]
     eng.count_shard(torch.from_numpy(buf).cuda(), torch.from_numpy(off.astype(np.int64)).cuda(), len(off) - 1, 0, k, 0)
-    recs, counts = eng.export_by_owner(5)
-    rb = distributed.rec_bytes(k)
-    raw = recs.cpu().numpy()
-    o = 0
-    for dst, c in enumerate(counts):
-        for i in range(o, o + c):
-            if k <= 32:
-                key = int(raw[i * rb: i * rb + 8].view(np.uint64)[0])
-                assert owner_fn(key, 5, k) == dst
-        o += c
-    assert o * rb == raw.size
+    for rule in (0, 1, 0):
+        eng.set_owner_rule(rule)
+        pre = eng.owner_counts(5)
+        recs, counts = eng.export_by_owner(5)
+        assert counts == pre
+        rb = distributed.rec_bytes(k)
+        raw = recs.cpu().numpy()
+        o = 0
+        for dst, c in enumerate(counts):
+            for i in range(o, o + c):
+                if k <= 32:
+                    key = int(raw[i * rb: i * rb + 8].view(np.uint64)[0])
+                    assert owner_fn(key, 5, k, rule) == dst
+            o += c
+        assert o * rb == raw.size
+    eng.set_owner_rule(0)
 
 
 def test_sharded_minimizer_skew_falls_back(engines):
@@ -245,3 +250,32 @@ def test_sharded_minimizer_skew_falls_back(engines):
         res, P = distributed.local_sharded_assemble(engines[:world], buf, off, 31, 1)
         assert P == ref["n_positions"]
         assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
+
+
+def test_sharded_owner_rule_switches_on_skew(engines):
+    """every 31-mer of this genome holds 15 A's, so they all share one minimizer and minimizer-range
+    owners would send every record to one rank; the summed owner counts switch all ranks to key-hash
+    owners, whose parts are balanced, and the result still equals the oracle"""
+    import distributed
+
+    rng = np.random.Generator(np.random.PCG64(7902))
+    parts = []
+    for _ in range(3_000):
+        parts.append(np.zeros(15, np.uint8))
+        parts.append(rng.integers(0, 4, 2, dtype=np.uint8))
+    g = np.concatenate(parts)
+    L, n = 100, 20_000
+    starts = rng.integers(0, len(g) - L + 1, n)
+    reads = np.frombuffer(b"ACGT", np.uint8)[g[starts[:, None] + np.arange(L)[None, :]]]
+    buf = reads.reshape(-1).copy()
+    off = np.arange(n + 1, dtype=np.uint64) * np.uint64(L)
+    ref = oracle.assemble_packed(buf, off, 31, 1)
+    world = 3
+    res, P = distributed.local_sharded_assemble(engines[:world], buf, off, 31, 1)
+    assert distributed.local_sharded_assemble_shards.last_rule == distributed.OWNER_HASH
+    totals = [sum(c[d] for c in distributed.local_sharded_assemble_shards.last_counts) for d in range(world)]
+    assert max(totals) <= 1.25 * sum(totals) / world, totals
+    assert P == ref["n_positions"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
+    for e in engines:
+        e.set_owner_rule(distributed.OWNER_MINIMIZER)
