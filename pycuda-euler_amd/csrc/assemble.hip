@@ -436,12 +436,46 @@ BucketPlan plan_buckets(double est, long long limit, bool filt_ok) {
 // validate: no k_prescan ran (phase_count_v2's fast path): M and npf come from the first read,
 // the partition checks the input and counts the windows; *invalid = the input does not meet
 // the prescan's conditions (the caller then takes the prescan path).
+// workgroups of k_skpart_w<npf, w, val> the device runs at once (CUs x resident per CU)
+static uint64_t skpart_slots(int npf, int w, bool val) {
+    static thread_local int cache[3][SK_W_MAX + 1][2] = {};
+    const int ni = npf == 4 ? 0 : npf == 7 ? 1 : 2;
+    int &c = cache[ni][w][val];
+    if (!c) {
+        const void *fn = nullptr;
+#define EC_SKF(NPF, W)                                                                                        \
+    if (npf == NPF && w == W) fn = val ? (const void *)&k_skpart_w<NPF, W, true> : (const void *)&k_skpart_w<NPF, W, false>;
+#define EC_SKF_W(W) EC_SKF(4, W) EC_SKF(7, W) EC_SKF(10, W)
+        EC_SKF_W(7) EC_SKF_W(8) EC_SKF_W(9) EC_SKF_W(10) EC_SKF_W(11) EC_SKF_W(12)
+        EC_SKF_W(13) EC_SKF_W(14) EC_SKF_W(15) EC_SKF_W(16) EC_SKF_W(17) EC_SKF_W(18)
+#undef EC_SKF_W
+#undef EC_SKF
+        int dev = 0, ncu = 0, per = 0;
+        if (!fn || hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, PT_THREADS, 0) != hipSuccess || per < 1)
+            return 1;
+        c = ncu * per;
+    }
+    return (uint64_t)c;
+}
+
 int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads,
                     uint64_t read_base, int k, long long limit, uint32_t M, uint64_t G, uint64_t gsize, uint64_t P,
                     int npf, unsigned int &U, SolidIndex &sidx, bool &done, bool validate = false,
                     bool *invalid = nullptr) {
     done = false;
     if (invalid) *invalid = false;
+    if (k >= SK_MIN_K && k <= 32) {
+        // read groups: a multiple of the workgroups resident at once when there are more tiles
+        // than that (2030 groups of 77 tiles on 768 slots ran 2.64 waves of workgroups, the last
+        // one a third idle; 1536 of 102 tiles run 2 full ones), at most RF_MAX_RUNS (k_skrefine)
+        const uint64_t ntiles = (nreads + 63) / 64, slots = skpart_slots(npf, k - SK_M + 1, validate);
+        uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>(ntiles, RF_MAX_RUNS));
+        if (g > slots && !kn().no_slot_groups) g = g / slots * slots;
+        gsize = ((ntiles + g - 1) / g) * 64;
+        G = (nreads + gsize - 1) / gsize;
+    }
     if (k < SK_MIN_K || k > 32 || M > 256 || gsize * M >= (1ull << 24) || (read_base + nreads) * 2 * M >= (1ull << 32) ||
         kn().no_sk2)
         return EC_OK;

@@ -35,6 +35,7 @@ namespace ec {
 
 constexpr int SK2_NMAX = 16;     // windows per record (n - 1 in 4 bits)
 constexpr int SK2_ECAP_W = 1600; // entries a partition wave buffers (LDS: 3 workgroups per CU)
+constexpr int SK2_HQ = 128;      // sampled runs a partition wave queues for the HyperLogLog
 constexpr int SK2_BASES = 46;    // bases per record (92 bits)
 #ifndef SK2_TILE_DEF
 #define SK2_TILE_DEF 2048
@@ -44,7 +45,7 @@ constexpr int SK2_CBITS = 6;     // coarse buckets of the partition: 64
 constexpr int SK2_BBITS = 14;    // final buckets <= 2^14 (bucket bits in an entry)
 constexpr int SK2_FBITS = SK2_BBITS - SK2_CBITS;  // bucket bits below the coarse bits in a record
 
-__host__ __device__ inline uint32_t sk2_nmax(int k) {
+__host__ __device__ constexpr inline uint32_t sk2_nmax(int k) {
     return (uint32_t)(SK2_BASES - k + 1 < SK2_NMAX ? SK2_BASES - k + 1 : SK2_NMAX);
 }
 
@@ -74,8 +75,8 @@ __device__ inline void skpart_flush(uint32_t cntw, const uint32_t *ent, uint16_t
                                     unsigned int *cur, unsigned long long *base, const uint32_t *rel,
                                     const uint32_t *st, uint32_t lane, unsigned long long gcap, uint64_t cap,
                                     unsigned long long spill, uint32_t M, uint32_t rtile, uint4 *recs,
-                                    unsigned int *overflow, unsigned int *s_hll, uint32_t smaskb, int k,
-                                    uint64_t kmask) {
+                                    unsigned int *overflow, unsigned int *s_hll, uint32_t *hq, uint32_t smaskb,
+                                    int k, uint64_t kmask) {
     wave_sync();
     for (uint32_t i = lane; i < cntw; i += 64) atomicAdd(&wcnt[ent[i] >> 26], 1u);
     wave_sync();
@@ -99,27 +100,49 @@ __device__ inline void skpart_flush(uint32_t cntw, const uint32_t *ent, uint16_t
         srt[p] = (uint16_t)i;
     }
     wave_sync();
-    for (uint32_t i = lane; i < cntw; i += 64) {
-        const uint32_t e = ent[srt[i]];
-        const uint32_t lr = e & 63u, i0 = (e >> 6) & 0xFFu, n1 = (e >> 14) & 15u;
-        const uint32_t p0 = rel[lr] + i0;
-        uint4 o;
-        o.x = sk_bases16(st, p0);
-        o.y = sk_bases16(st, p0 + 16);
-        o.z = (sk_bases16(st, p0 + 32) & 0x0FFFFFFFu) | n1 << 28;
-        o.w = ((e >> 18) & ((1u << SK2_FBITS) - 1)) << 24 | ((rtile + lr) * M + i0);
-        recs[base[e >> 26] + i] = o;
-        // HyperLogLog over the k-mers of the runs whose minimizer's low bucket bits & smaskb are 0
-        // (a sample of minimizer space; a k-mer and its twin share the minimizer): each window's
-        // canonical k-mer out of the stage
-        if (((e >> 18) & smaskb) == 0) {
-            for (uint32_t q = 0; q <= n1; q++) {
-                const uint64_t K = (uint64_t)sk_bases16(st, p0 + q) | (uint64_t)sk_bases16(st, p0 + q + 16) << 32;
+    // HyperLogLog over the k-mers of the runs whose minimizer's low bucket bits & smaskb are 0 (a
+    // sample of minimizer space; a k-mer and its twin share the minimizer): sampled runs are
+    // queued (stage position | (n - 1) << 16) and their windows spread over the lanes when the
+    // queue fills -- a per-lane loop over its run's windows held the whole wave whenever one
+    // lane of 64 had a sampled run
+    uint32_t nq = 0;  // (uniform)
+    auto hll_drain = [&]() {
+        wave_sync();
+        for (uint32_t x = lane; x < nq * SK2_NMAX; x += 64) {
+            const uint32_t qe = hq[x / SK2_NMAX], q = x % SK2_NMAX;
+            if (q <= (qe >> 16)) {
+                const uint32_t p = (qe & 0xFFFFu) + q;
+                const uint64_t K = (uint64_t)sk_bases16(st, p) | (uint64_t)sk_bases16(st, p + 16) << 32;
                 const uint64_t krc = ~K & kmask, kfw = rev2_64(K) >> (64 - 2 * k);
                 sk_hll_put(s_hll, (uint32_t)(mix64(kfw < krc ? kfw : krc) >> 32));
             }
         }
+        wave_sync();
+        nq = 0;
+    };
+    for (uint32_t i0 = 0; i0 < cntw; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        bool samp = false;
+        uint32_t qv = 0;
+        if (i < cntw) {
+            const uint32_t e = ent[srt[i]];
+            const uint32_t lr = e & 63u, w0 = (e >> 6) & 0xFFu, n1 = (e >> 14) & 15u;
+            const uint32_t p0 = rel[lr] + w0;
+            uint4 o;
+            o.x = sk_bases16(st, p0);
+            o.y = sk_bases16(st, p0 + 16);
+            o.z = (sk_bases16(st, p0 + 32) & 0x0FFFFFFFu) | n1 << 28;
+            o.w = ((e >> 18) & ((1u << SK2_FBITS) - 1)) << 24 | ((rtile + lr) * M + w0);
+            recs[base[e >> 26] + i] = o;
+            samp = ((e >> 18) & smaskb) == 0;
+            qv = p0 | n1 << 16;
+        }
+        const uint64_t sb = __builtin_amdgcn_ballot_w64(samp);
+        if (samp) hq[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(sb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sb, 0u))] = qv;
+        nq += (uint32_t)__popcll(sb);
+        if (nq > (uint32_t)(SK2_HQ - 64)) hll_drain();
     }
+    if (nq) hll_drain();
     wave_sync();
     if (lane < (uint32_t)C) wcnt[lane] = 0;
 }
@@ -157,6 +180,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
     __shared__ unsigned int s_wcnt[PT_WAVES][C];
     __shared__ unsigned int s_cur[C];
     __shared__ unsigned int s_hll[NREG / 4];
+    __shared__ uint32_t s_hq[PT_WAVES][SK2_HQ];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (int i = threadIdx.x; i < NREG / 4; i += PT_THREADS) s_hll[i] = 0;
@@ -166,8 +190,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
     const uint64_t g = blockIdx.x + (uint64_t)g_lo;  // (host input: launched per chunk of groups)
     const uint64_t g0 = min(g * gsize, nreads), g1 = min(g0 + gsize, nreads);
     const uint32_t ntile = (uint32_t)((g1 - g0 + 63) / 64);
-    const int k = mc.k, m = mc.m;
-    const uint32_t nmax = sk2_nmax(k);
+    const int k = mc.k;
+    constexpr uint32_t nmax = sk2_nmax(W + SK_M - 1);  // k = W + m - 1
     const uint64_t kmask = kmask64(k);
     uint4 pf[NPF];
     uint64_t nx_base = 0;
@@ -225,15 +249,18 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
         const uint32_t rel = has ? s - tbase : 0u;
         s_rel[wid][lane] = rel;
         wave_sync();
+        constexpr int m = SK_M;
+        constexpr uint32_t MMASK = (1u << (2 * SK_M)) - 1;
         uint32_t mf = 0, mr = 0;
         auto push_base = [&](uint32_t b) {
-            mf = ((mf << 2) | b) & mc.mmask;
-            mr = (mr >> 2) | ((3u - b) << mc.msh);
+            mf = ((mf << 2) | b) & MMASK;
+            mr = (mr >> 2) | ((3u - b) << (2 * SK_M - 2));
         };
         // block 0 = m-mers 0 .. W - 1 (bases 0 .. k - 1): its suffix minima
         uint32_t S[W];
         {
             const uint32_t x0 = sk_bases16(st, rel), x1 = sk_bases16(st, rel + 16);
+#pragma unroll
             for (int tb = 0; tb < m - 1; tb++) push_base(tb < 16 ? (x0 >> (2 * tb)) & 3u : (x1 >> (2 * (tb - 16))) & 3u);
 #pragma unroll
             for (int j = 0; j < W; j++) {
@@ -246,9 +273,17 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
         }
         const uint32_t nrounds = __any(has) ? (M + W - 1) / W : 0u;
         if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
-        uint32_t runv = 0, runn = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
-        const uint32_t inc = has ? 1u : 0u;
-        const uint32_t rtile = 64 * t;  // the tile's first read relative to g0
+        // the open run of a lane: windows [rs, w) of minimizer runv.  runv starts as window 0's
+        // value, so window 0 never closes a run; a lane without a read never closes one (has)
+        uint32_t runv = S[0], rs = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
+        const uint64_t hasm = __builtin_amdgcn_ballot_w64(has);
+        const uint32_t rtile = 64 * t;            // the tile's first read relative to g0
+        // entry of the run [rs, end) closing at window end: lane | rs << 6 | (n - 1) << 14 |
+        // bucket bits << 18 with n = end - rs (fields disjoint, so a sum), the bucket bits the
+        // top 14 of min_remix(runv) = its low 14 (the shift drops the rest)
+        auto entry = [&](uint32_t end) {
+            return (runv << 18) + (lane + ((end - 1u) << 14)) + (uint32_t)__mul24((int)rs, -16320);
+        };
         for (uint32_t round = 0; round < nrounds; round++) {
             const uint32_t w0 = round * W;  // first window of the round
             // bases of m-mers (round + 1) W + j: (round + 1) W + m - 1 + j
@@ -256,30 +291,38 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
             const uint32_t xb0 = sk_bases16(st, pb), xb1 = sk_bases16(st, pb + 16);
             uint32_t H[W];
             uint32_t P = 0xFFFFFFFFu;  // prefix minimum of the next block so far
-#pragma unroll
-            for (int j = 0; j < W; j++) {
-                if (w0 + j >= M) break;  // uniform
+            // one window: its minimizer v, the next block's hash j, and the run bookkeeping.  A run
+            // closes when the minimizer changes or it holds nmax windows: the closing lanes append
+            // their entries (ballot rank), the others only move rs
+            auto window = [&](int j) {
                 const uint32_t v = min(S[j], P);  // window w0 + j
                 push_base(j < 16 ? (xb0 >> (2 * j)) & 3u : (xb1 >> (2 * (j - 16))) & 3u);
                 H[j] = mmer_hash(mf < mr ? mf : mr);
                 P = min(P, H[j]);
-                // the run of windows [w0 + j - runn, w0 + j) closes when the minimizer changes or it
-                // holds nmax windows; a lane without a read keeps runn = 0 and never closes.  Between
-                // closes v == runv, so runv = v every window (no select), and the run's first window
-                // is derived at the close (no per-window bookkeeping for it)
-                const bool close = runn != 0 && (v != runv || runn == nmax);
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(close);
-                if (bal) {
-                    if (close) {
-                        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                        ent[cntw + rk] = lane | (w0 + j - runn) << 6 | (runn - 1) << 14 |
-                                         (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
-                    }
-                    cntw += (uint32_t)__popcll(bal);
+                const uint32_t end = w0 + j;  // uniform
+                // (the mask from the compares' own ballots: a ballot of the combined bool was
+                // materialised through a VGPR)
+                const bool c1 = v != runv, c2 = rs == end - nmax;
+                const bool close = has & (c1 | c2);
+                const uint64_t bal = (__builtin_amdgcn_ballot_w64(c1) | __builtin_amdgcn_ballot_w64(c2)) & hasm;
+                if (close) {
+                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    ent[cntw + rk] = entry(end);
+                    rs = end;
                 }
+                cntw += (uint32_t)__popcll(bal);
                 runv = v;
-                runn = (close ? 0u : runn) + inc;
+            };
+            if (w0 + W <= M) {  // a whole round: no bound checks
+#pragma unroll
+                for (int j = 0; j < W; j++) window(j);
+            } else {
+#pragma unroll
+                for (int j = 0; j < W; j++) {
+                    if (w0 + j >= M) break;  // uniform
+                    window(j);
+                }
             }
             // the next round's suffix minima (the block's unused tail at the read's end is never read)
 #pragma unroll
@@ -287,13 +330,12 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
 #pragma unroll
             for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
             const bool last = round + 1 == nrounds;
-            if (last) {  // the reads' final runs: windows [M - runn, M)
-                const bool fin = runn != 0;
-                const uint64_t bal = __ballot(fin);
-                if (fin) {
+            if (last) {  // the reads' final runs: windows [rs, M)
+                const uint64_t bal = hasm;
+                if (has) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = lane | (M - runn) << 6 | (runn - 1) << 14 | (min_remix(runv) >> (32 - SK2_BBITS)) << 18;
+                    ent[cntw + rk] = entry(M);
                 }
                 cntw += (uint32_t)__popcll(bal);
                 if (more) EC_PT_ISSUE(t + PT_WAVES);
@@ -301,7 +343,8 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
             // flush: the buffer could not take another round, or the stage is about to change
             if (last || cntw > (uint32_t)(SK2_ECAP_W - 64 * (W + 1))) {
                 skpart_flush<C>(cntw, ent, s_srt[wid], s_wcnt[wid], s_cur, s_base[wid], s_rel[wid], st, lane, gcap,
-                                cap, spill, M, rtile, recs, overflow, s_hll, smask ? 0xFFu : 0u, k, kmask);
+                                cap, spill, M, rtile, recs, overflow, s_hll, s_hq[wid], smask ? 0xFFu : 0u, k,
+                                kmask);
                 cntw = 0;
             }
         }

@@ -41,17 +41,11 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t x) {
     return x ^ (x >> 15);
 }
 
-// the minimizer's identity as used downstream: the minimum hash remixed, so that its top bits
-// (fine bin, coarse and final bucket) are uniform -- the minimum of w hashes itself crowds
-// towards 0.  Bijective: runs still split exactly where the minimizer changes.
-__host__ __device__ inline uint32_t min_remix(uint32_t x) {
-    x ^= 0x5BD1E995u;
-    x *= 0x2C1B3C6Du;
-    x ^= x >> 12;
-    x *= 0x297A2D39u;
-    x ^= x >> 15;
-    return x;
-}
+// the minimizer's identity as used downstream: the minimum hash rotated so that its LOW 14
+// bits are the top ones -- the minimum of w hashes crowds its high bits towards 0, its low bits
+// stay uniform -- so the fine bin, coarse and final bucket (top bits) and the owner ranges are
+// even.  Bijective; k_skpart_w takes the bucket bits as runv << 18 (no remix per run).
+__host__ __device__ inline uint32_t min_remix(uint32_t x) { return (x >> 14) | (x << 18); }
 
 __host__ __device__ inline uint32_t rev2_32(uint32_t x) {
     x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);

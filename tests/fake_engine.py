@@ -43,11 +43,8 @@ def _mmer_hash(x):
 
 
 def _min_remix(x):
-    x ^= 0x5BD1E995
-    x = (x * 0x2C1B3C6D) & M32
-    x ^= x >> 12
-    x = (x * 0x297A2D39) & M32
-    return x ^ (x >> 15)
+    """superkmer.h min_remix: rotate right by 14 (the minimum's uniform low bits on top)"""
+    return ((x >> 14) | (x << 18)) & M32
 
 
 def minimizer_of(c, k, m=15):
