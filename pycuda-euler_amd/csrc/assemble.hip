@@ -587,9 +587,13 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     // both the count and the graph phase's probes measurably slower -- headline A/B 8192 against
     // 4096 buckets: k_skbucket 1.65 / 2.37 ms, links 0.56 / 1.07 ms)
     int bbits = SK2_CBITS;
-    while (bbits < SK2_BBITS && est / (double)(1ull << bbits) > 800.0) bbits++;
+    // k_skbucket3 (three workgroups per CU, 1024-slot tables) while its buckets stay at <= 380
+    // estimated keys; larger inputs take k_skbucket's 2048- / 4096-slot tables
+    const bool b3 = !kn().no_skb3 && est / (double)(1ull << SK2_BBITS) <= 380.0;
+    const double per_bucket = b3 ? 380.0 : 800.0;
+    while (bbits < SK2_BBITS && est / (double)(1ull << bbits) > per_bucket) bbits++;
     plan.bbits = bbits;
-    plan.slots = est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
+    plan.slots = b3 ? 1024u : est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
     const uint64_t Bk = 1ull << bbits;
     const uint64_t NR = hsc.nrec;
 
@@ -641,11 +645,17 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     // EULERHIP_SK2_STATS: distinct records, flushes and windows rolled out (stderr)
     unsigned long long *dbg = nullptr;
     if (kn().sk2_stats && !nodedup) {
-        EC_CHECK(s->tmp.ensure(64));
+        EC_CHECK(s->tmp.ensure(128));
         dbg = s->tmp.as<unsigned long long>();
-        EC_HIP(hipMemsetAsync(dbg, 0, 64, st));
+        EC_HIP(hipMemsetAsync(dbg, 0, 128, st));
     }
-    if (plan.slots == 2048) {
+    if (plan.slots == 1024) {
+        constexpr int NT3 = 512;
+        if (k & 1)
+            k_skbucket3<1024, 1664, NT3, false><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg);
+        else
+            k_skbucket3<1024, 1664, NT3, true><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg);
+    } else if (plan.slots == 2048) {
         if (k & 1) EC_SKBUCKET(2048, 3072, false);
         else EC_SKBUCKET(2048, 3072, true);
     } else {
@@ -655,9 +665,13 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
 #undef EC_SKBUCKET
 #undef EC_SKBUCKET_ARGS
     if (dbg) {
-        unsigned long long h[8];
-        EC_HIP(hipMemcpyAsync(h, dbg, 64, hipMemcpyDeviceToHost, st));
+        unsigned long long h[16];
+        EC_HIP(hipMemcpyAsync(h, dbg, 128, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
+        const double nw = (double)Bk * (BUCKET_THREADS / 64);  // waves
+        fprintf(stderr, "k_skbucket per wave (shader clocks): records phase canon %.0f probe %.0f (%.1f iterations) "
+                        "post %.0f barrier %.0f over %.1f rounds; roll-out %.0f barrier %.0f\n",
+                h[8] / nw, h[9] / nw, h[11] / nw, h[10] / nw, h[12] / nw, h[13] / nw, h[14] / nw, h[15] / nw);
         fprintf(stderr, "k_skbucket: %llu records, %llu distinct in %llu flushes (%.2f / bucket), %llu windows rolled "
                         "(positions %llu); block-us: init %.0f records %.0f sort %.0f roll-out %.0f finish %.0f\n",
                 (unsigned long long)NR, h[0], h[1], (double)h[1] / Bk, h[2], (unsigned long long)P, h[3] / 100.0,

@@ -42,6 +42,7 @@ void refresh_knobs() {
         k.sk2_exp = num("EULERHIP_SK2_EXP", 0);
         k.sk2_stats = flag("EULERHIP_SK2_STATS");
         k.no_slot_groups = flag("EULERHIP_NO_SLOT_GROUPS");
+        k.no_skb3 = flag("EULERHIP_NO_SKB3");
         k.verbose = flag("EULERHIP_VERBOSE");
     }
     g_knobs = k;

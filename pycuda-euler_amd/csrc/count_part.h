@@ -826,14 +826,15 @@ struct EvId {
     template <typename Tab>
     __device__ inline ulonglong2 operator()(const Tab &tab, int i) const { return tab.ev[i]; }
 };
-template <int SLOTS, bool DET = false, typename KO = KeyId, typename Tab = LTab<SLOTS>, typename EO = EvId>
+template <int SLOTS, bool DET = false, typename KO = KeyId, typename Tab = LTab<SLOTS>, typename EO = EvId,
+          int NT = BUCKET_THREADS>
 __device__ inline void lds_table_finish(const Tab &tab, const unsigned int *s_over, unsigned int b,
                                         long long limit,
                                         unsigned long long *dkey, unsigned int *dcnt, unsigned long long *dfc,
                                         unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
                                         unsigned long long *ndistinct, unsigned int *overflow, KO ko = KO(),
                                         EO eo = EO()) {
-    __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
+    __shared__ unsigned int s_wave[NT / 64], s_pres[NT / 64];
     __shared__ unsigned int s_base;
     __syncthreads();
     if (*s_over) {
@@ -841,7 +842,7 @@ __device__ inline void lds_table_finish(const Tab &tab, const unsigned int *s_ov
         return;
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int PER = SLOTS / BUCKET_THREADS;
+    constexpr int PER = SLOTS / NT;
     if constexpr (DET) {  // dense ids given by the records (LTab::id): every present key is solid
         SubSlot *region = sub + (uint64_t)b * SLOTS;
         for (int q = 0; q < PER; q++) {
@@ -886,7 +887,7 @@ __device__ inline void lds_table_finish(const Tab &tab, const unsigned int *s_ov
     __syncthreads();
     if (threadIdx.x == 0) {  // one global atomic each per block (a per-wave atomic on one word serialises)
         unsigned int tot = 0, np = 0;
-        for (int w = 0; w < BUCKET_THREADS / 64; w++) {
+        for (int w = 0; w < NT / 64; w++) {
             const unsigned int c = s_wave[w];
             s_wave[w] = tot;
             tot += c;

@@ -35,6 +35,10 @@ namespace ec {
 
 constexpr int SK2_NMAX = 16;     // windows per record (n - 1 in 4 bits)
 constexpr int SK2_ECAP_W = 1600; // entries a partition wave buffers (LDS: 3 workgroups per CU)
+#ifndef SK2_PD_DEF
+#define SK2_PD_DEF 4
+#endif
+constexpr int SK2_PD = SK2_PD_DEF;  // k_skbucket record rounds in flight per thread
 constexpr int SK2_HQ = 128;      // sampled runs a partition wave queues for the HyperLogLog
 constexpr int SK2_BASES = 46;    // bases per record (92 bits)
 #ifndef SK2_TILE_DEF
@@ -705,11 +709,13 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
     const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
     const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
 
+    unsigned long long n_rolled = 0;  // (EULERHIP_SK2_STATS; no global atomics in the loops: they
+                                      // would hold the record loads' counter at vmcnt(0))
     // the n windows of a (canonical) record into the k-mer table: window o's string was inserted
     // at ea + o, its twin at eb - o, mult times each
     auto roll_out = [&](uint32_t x0, uint32_t x1, uint32_t x2, unsigned int mult, unsigned int ea, unsigned int eb) {
         const unsigned int n = (x2 >> 28) + 1;
-        if (dbg) atomicAdd(&dbg[2], (unsigned long long)n);
+        if (dbg) n_rolled += n;
         auto events = [&](uint64_t fwd, uint64_t rc, unsigned int o, unsigned int &eC, unsigned int &eT,
                           unsigned int &add) {
             const bool tw = fwd > rc;
@@ -769,21 +775,40 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
     // LDS round trips: latency-bound)
     constexpr unsigned int ROUND = RB * BUCKET_THREADS;
     phase(1);  // [3] init
-    uint4 nx[RB];
+    // records PD rounds ahead in flight per thread (one round ahead left the loads' latency
+    // exposed once the probes were cheap: ~16 KiB in flight per CU); the round loop is unrolled
+    // PD times so each slot is consumed and reloaded in place (no register moves that would wait)
+    constexpr int PD = SK2_PD;
+    uint4 nx[PD][RB];
 #pragma unroll
-    for (int j = 0; j < RB; j++) {
-        const uint64_t ri = r0 + tid + (uint64_t)j * BUCKET_THREADS;
-        nx[j] = ri < r1 ? recs[ri] : make_uint4(0, 0, 0, 0);
-    }
-    for (uint64_t c0 = r0; c0 < r1; c0 += ROUND) {
+    for (int d = 0; d < PD; d++)
+#pragma unroll
+        for (int j = 0; j < RB; j++) {
+            const uint64_t ri = r0 + tid + (uint64_t)j * BUCKET_THREADS + (uint64_t)d * ROUND;
+            nx[d][j] = recs[r1 > r0 ? min(ri, r1 - 1) : r0];  // (an empty bucket reads its own start)
+        }
+    // EULERHIP_SK2_STATS: per-wave shader-clock split of the records phase (dbg[8..13])
+    unsigned long long c_canon = 0, c_probe = 0, c_post = 0, n_iter = 0, n_rounds = 0, c_t = 0;
+    auto tick = [&](unsigned long long &acc) {
+        if (dbg) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            acc += t - c_t;
+            c_t = t;
+        }
+    };
+    if (dbg) c_t = __builtin_amdgcn_s_memtime();
+    auto record_round = [&](uint4 (&nxd)[RB], uint64_t c0) {
+        if (dbg) n_rounds++;
         uint32_t K0[RB], K1[RB], K2[RB], EA[RB], EB[RB], TG[RB], SL[RB];
         int ST[RB];  // 0 searching, 1 found / claimed, 2 table full (rolled out on its own)
 #pragma unroll
         for (int j = 0; j < RB; j++) {
             const uint64_t ri = c0 + tid + (uint64_t)j * BUCKET_THREADS;
             const bool valid = ri < r1;
-            const uint4 x = nx[j];
-            if (ri + ROUND < r1) nx[j] = recs[ri + ROUND];  // next round's records
+            const uint4 x = nxd[j];
+            // the records PD rounds on; unconditional (clamped; the value past the end is not
+            // used), so the loads stay in order in flight and the wait before use is vmcnt(PD - 1)
+            nxd[j] = recs[min(ri + PD * ROUND, r1 - 1)];
             // canonical content of the record (branch-free: selects, no divergent paths)
             const unsigned int n = (x.z >> 28) + 1, L2 = 2 * (n + (unsigned int)k - 1);  // 2L in [2k, 92]
             const uint32_t m1 = L2 >= 64 ? 0xFFFFFFFFu : (1u << ((L2 - 32) & 31)) - 1u;  // bits of word 1
@@ -827,14 +852,19 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
         // first implies the key words read after it are the stored key -- DS operations of a wave
         // complete in order), compares branch-free, and only the rare empty slot takes the claim
         // path; a chain that is done re-reads its slot harmlessly
-        const volatile uint32_t *vt = r_tag, *vx = r_x, *vy = r_y, *vz = r_z;
+        // (relaxed atomic loads stay ds_read_b32 with one wait for all four; volatile pointers
+        // had lost the LDS address space: flat loads with a full wait after each, 4x slower)
+        auto ld = [](uint32_t *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+        tick(c_canon);
 #pragma unroll 1
         while (__any(searching())) {
+            if (dbg) n_iter++;
             uint32_t T[RB], X[RB], Y[RB], Z[RB];
 #pragma unroll
-            for (int j = 0; j < RB; j++) T[j] = vt[SL[j]];
+            for (int j = 0; j < RB; j++) T[j] = ld(&r_tag[SL[j]]);
+            asm volatile("" ::: "memory");  // the key words are read after the tag (issue order)
 #pragma unroll
-            for (int j = 0; j < RB; j++) X[j] = vx[SL[j]], Y[j] = vy[SL[j]], Z[j] = vz[SL[j]];
+            for (int j = 0; j < RB; j++) X[j] = ld(&r_x[SL[j]]), Y[j] = ld(&r_y[SL[j]]), Z[j] = ld(&r_z[SL[j]]);
             bool claim = false;
 #pragma unroll
             for (int j = 0; j < RB; j++) {
@@ -856,7 +886,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
                     // claims stop at CLAIM_MAX entries (a plain read: at most a block's worth of
                     // claims in flight overshoot it, so free slots always remain and a miss meets
                     // one within a few probes -- linear probing near full scans the table)
-                    if (*(volatile unsigned int *)&s_nent >= CLAIM_MAX) {
+                    if (ld(&s_nent) >= CLAIM_MAX) {
                         ST[j] = 2;
                     } else if (atomicCAS(&r_tag[slot], 0u, TG[j] | PEND) == 0) {  // store the key, publish
                         r_x[slot] = K0[j], r_y[slot] = K1[j], r_z[slot] = K2[j];
@@ -867,6 +897,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
                 }
             }
         }
+        tick(c_probe);
 #pragma unroll
         for (int j = 0; j < RB; j++) {
             const bool valid = c0 + tid + (uint64_t)j * BUCKET_THREADS < r1;
@@ -880,8 +911,22 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
 #pragma unroll
         for (int j = 0; j < RB; j++)
             if (ST[j] == 2) roll_out(K0[j], K1[j], K2[j], 1u, EA[j], EB[j]);
+        tick(c_post);
+    };
+    for (uint64_t c0 = r0; c0 < r1; c0 += PD * ROUND) {
+#pragma unroll
+        for (int d = 0; d < PD; d++) {
+            if (c0 + (uint64_t)d * ROUND >= r1) break;  // uniform
+            record_round(nx[d], c0 + (uint64_t)d * ROUND);
+        }
     }
+    unsigned long long c_bar = 0;
     __syncthreads();
+    tick(c_bar);
+    if (dbg && (tid & 63) == 0) {
+        atomicAdd(&dbg[8], c_canon), atomicAdd(&dbg[9], c_probe), atomicAdd(&dbg[10], c_post);
+        atomicAdd(&dbg[11], n_iter), atomicAdd(&dbg[12], c_bar), atomicAdd(&dbg[13], n_rounds);
+    }
     phase(2);  // [4] records (thread 0 + the barrier)
     // ---- the distinct records into the k-mer table, by window count (most first) -------------
     {
@@ -914,16 +959,270 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
         __syncthreads();
         const unsigned int ne = s_ncnt[SK2_NMAX];
         phase(3);  // [5] sort
+        if (dbg) c_t = __builtin_amdgcn_s_memtime();
+        unsigned long long c_roll = 0, c_bar2 = 0;
         for (unsigned int t = tid; t < ne; t += BUCKET_THREADS) {
             const unsigned int e = s_ord[t];
             roll_out(r_x[e], r_y[e], r_z[e], r_mult[e], r_a[e], r_b[e]);
         }
+        tick(c_roll);
+        __syncthreads();
+        tick(c_bar2);
+        if (dbg && (tid & 63) == 0) atomicAdd(&dbg[14], c_roll), atomicAdd(&dbg[15], c_bar2);
+        if (dbg) atomicAdd(&dbg[2], n_rolled);
     }
-    __syncthreads();
     phase(4);  // [6] roll-out
     lds_table_finish<SLOTS, false, KeyId>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
                                           overflow, KeyId(), EvExpand{2 * M});
     phase(5);  // [7] finish
+}
+
+
+// ---- k_skbucket3: small buckets, several workgroups per CU ------------------------------------
+// k_skbucket's 133 KiB of LDS (the 3072-entry record table beside the 2048-slot k-mer table) held
+// one workgroup per CU: its barriers, the init and the per-bucket tail were exposed.  Here a
+// bucket is half as large (2^14 buckets, ~280 keys: a 1024-slot k-mer table) and the two tables
+// share one region: the record table in the records phase, then the k-mer table beside the
+// distinct records compacted (sorted by window count) out of it.  NT = 512 threads and ~50 KiB
+// of LDS: three workgroups per CU.  Records the record table cannot take (past CLAIM_MAX
+// entries) wait in a small overflow list and are rolled out after the distinct ones; a full
+// list raises *overflow (the call is redone on another path).
+template <int SLOTS, int RS, int NT>
+struct SkB3Lds {
+    static constexpr int NC = RS / 2;  // compact records (CLAIM_MAX <= RS / 2)
+    struct Rec {
+        uint32_t tag[RS], x[RS], y[RS], z[RS], mult[RS], a[RS], b[RS];
+    };
+    struct Roll {
+        LTabE<SLOTS> tab;
+        uint32_t x[NC], y[NC], z[NC], mult[NC], a[NC], b[NC];
+    };
+    union {
+        Rec r;
+        Roll k;
+    };
+};
+
+template <int SLOTS, int RS, int NT, bool EVEN_K>
+__global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsigned long long *bbeg,
+                                                  const unsigned long long *bend, int k, uint32_t M, double inv_m,
+                                                  long long limit, unsigned long long *dkey, unsigned int *dcnt,
+                                                  unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
+                                                  unsigned int *nsolid, unsigned long long *ndistinct,
+                                                  unsigned int *overflow, unsigned long long *dbg) {
+    constexpr int SBITS = __builtin_ctz(SLOTS);
+    constexpr uint32_t PEND = 0x800u;
+    constexpr unsigned int CLAIM_MAX = RS / 2 < RS - 1 - NT ? RS / 2 : RS - 1 - NT;
+    static_assert(RS > NT + 1, "record table too small for the records in flight");
+    static_assert(sizeof(typename SkB3Lds<SLOTS, RS, NT>::Roll) <= sizeof(typename SkB3Lds<SLOTS, RS, NT>::Rec),
+                  "the k-mer table and the compact records fit the record table's space");
+    constexpr int OV = 256;  // overflow list
+    __shared__ SkB3Lds<SLOTS, RS, NT> L;
+    __shared__ uint32_t o_x[OV], o_y[OV], o_z[OV], o_a[OV], o_b[OV];
+    __shared__ unsigned int s_over[2];
+    __shared__ unsigned int s_nent, s_nov, s_ncnt[SK2_NMAX + 1];
+    auto &R = L.r;
+    auto &tab = L.k.tab;
+    const unsigned int b = blockIdx.x, tid = threadIdx.x;
+    for (int i = tid; i < RS; i += NT) {
+        R.tag[i] = 0;
+        R.mult[i] = 0;
+        R.a[i] = R.b[i] = 0xFFFFFFFFu;
+    }
+    if (tid <= SK2_NMAX) s_ncnt[tid] = 0;
+    if (tid == 0) s_over[0] = s_over[1] = 0, s_nent = 0, s_nov = 0;
+    __syncthreads();
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    const uint64_t kmask = kmask64(k);
+    const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
+    const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
+    unsigned long long n_rolled = 0;
+
+    // the n windows of a canonical record into the k-mer table (as k_skbucket's roll_out)
+    auto roll_out = [&](uint32_t x0, uint32_t x1, uint32_t x2, unsigned int mult, unsigned int ea, unsigned int eb) {
+        const unsigned int n = (x2 >> 28) + 1;
+        if (dbg) n_rolled += n;
+        auto events = [&](uint64_t fwd, uint64_t rc, unsigned int o, unsigned int &eC, unsigned int &eT,
+                          unsigned int &add) {
+            const bool tw = fwd > rc;
+            const unsigned int ef = ea + o, et = eb - o;
+            add = mult;
+            eC = tw ? et : ef;
+            eT = tw ? ef : et;
+            if (EVEN_K && fwd == rc) {
+                add = 2 * mult;
+                eC = eT = min(ef, et);
+            }
+            return tw ? rc : fwd;
+        };
+        const unsigned int h = (n + 1) >> 1;
+        auto at = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {
+            const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, 2 * o), hi = __builtin_amdgcn_alignbit(x2, x1, 2 * o);
+            const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+            rv = ~P & kmask;
+            fw = rev2_64(P) >> fsh;
+        };
+        auto roll = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {
+            const unsigned int tb = o + (unsigned int)k - 1;
+            const uint32_t wd = tb < 32 ? x1 : x2;
+            const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
+            fw = ((fw << 2) | bb) & kmask;
+            rv = (rv >> 2) | ((uint64_t)(3u - bb) << sh);
+        };
+        uint64_t fA, rA, fB, rB;
+        at(0, fA, rA);
+        at(h, fB, rB);
+        for (unsigned int i = 0; i < h; i++) {
+            const unsigned int oB = i + h;
+            const bool bB = oB < n;
+            if (i) {
+                roll(i, fA, rA);
+                roll(oB, fB, rB);
+            }
+            unsigned int eCA, eTA, eCB, eTB, addA, addB;
+            const uint64_t cA = events(fA, rA, i, eCA, eTA, addA);
+            const uint64_t cB = events(fB, rB, oB, eCB, eTB, addB);
+            unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1), sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
+            const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
+            lds_locate2<SLOTS>(tab, s_over, cA, sA, kA, cB, sB, bB ? kB : cB);
+            atomicAdd(&tab.count[sA], addA);
+            if (bB) atomicAdd(&tab.count[sB], addB);
+            const uint2 vA = tab.ev[sA], vB = tab.ev[sB];
+            if (eCA < vA.x) atomicMin(&tab.ev[sA].x, eCA);
+            if (eTA < vA.y) atomicMin(&tab.ev[sA].y, eTA);
+            if (bB && eCB < vB.x) atomicMin(&tab.ev[sB].x, eCB);
+            if (bB && eTB < vB.y) atomicMin(&tab.ev[sB].y, eTB);
+        }
+    };
+
+    // ---- records -> record table (k_skbucket's protocol; PD rounds of loads in flight) --------
+    constexpr int PD = SK2_PD;
+    uint4 nx[PD];
+#pragma unroll
+    for (int d = 0; d < PD; d++) nx[d] = recs[r1 > r0 ? min(r0 + tid + (uint64_t)d * NT, r1 - 1) : r0];
+    auto ld = [](uint32_t *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto record_round = [&](uint4 &nxd, uint64_t c0) {
+        const uint64_t ri = c0 + tid;
+        const bool valid = ri < r1;
+        const uint4 x = nxd;
+        nxd = recs[min(ri + PD * NT, r1 - 1)];
+        const unsigned int n = (x.z >> 28) + 1, L2 = 2 * (n + (unsigned int)k - 1);
+        const uint32_t m1 = L2 >= 64 ? 0xFFFFFFFFu : (1u << ((L2 - 32) & 31)) - 1u;
+        const uint32_t mw2 = L2 > 64 ? (1u << ((L2 - 64) & 31)) - 1u : 0u;
+        const uint32_t x0 = x.x, x1 = x.y & m1, x2 = x.z & mw2;
+        const uint32_t y0 = rev2_32b(x2), y1 = rev2_32b(x1), y2 = rev2_32b(x0);
+        const unsigned int sft = 96 - L2, s5 = sft & 31;
+        const bool lo = sft < 32;
+        const uint32_t a0 = __builtin_amdgcn_alignbit(y1, y0, s5), a1 = __builtin_amdgcn_alignbit(y2, y1, s5),
+                       a2 = y2 >> s5;
+        const uint32_t q0 = ~(lo ? a0 : a1), q1 = ~(lo ? a1 : a2) & m1, q2 = lo ? ~a2 & mw2 : 0u;
+        const bool flip = q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0;
+        const unsigned int p = x.w;
+        const unsigned int rd0 = (unsigned int)((double)p * inv_m);
+        int rm = (int)(p - rd0 * M);
+        unsigned int rd = rd0;
+        if (rm < 0) rd--, rm += (int)M;
+        else if (rm >= (int)M) rd++, rm -= (int)M;
+        const unsigned int A = rd * M2 + (unsigned int)rm, B = rd * M2 + m2 - (unsigned int)rm;
+        const uint32_t K0 = flip ? q0 : x0, K1 = flip ? q1 : x1, K2 = (flip ? q2 : x2) | (n - 1) << 28;
+        const uint32_t EA = flip ? B - n + 1 : A, EB = flip ? A + n - 1 : B;
+        uint32_t hh = K0 * 0x9E3779B1u;
+        hh = (hh ^ (hh >> 15) ^ K1) * 0x85EBCA77u;
+        hh = (hh ^ (hh >> 13) ^ K2) * 0xC2B2AE3Du;
+        hh ^= hh >> 16;
+        const uint32_t TG = (hh | 0x1000u) & 0xFFFFF000u;
+        uint32_t SL = __umulhi(hh * 0x27D4EB2Fu, (unsigned int)RS);
+        int ST = valid ? 0 : 1;  // 0 searching, 1 found / claimed, 2 past the claim cap
+#pragma unroll 1
+        while (__any(ST == 0)) {
+            const uint32_t T = ld(&R.tag[SL]);
+            asm volatile("" ::: "memory");  // the key words are read after the tag (issue order)
+            const uint32_t X = ld(&R.x[SL]), Y = ld(&R.y[SL]), Z = ld(&R.z[SL]);
+            const bool hit = T == TG && X == K0 && Y == K1 && Z == K2;
+            const bool go = ST == 0;
+            ST = go && hit ? 1 : ST;
+            const bool claim = go && !hit && T == 0;
+            if (go && !hit && T != 0 && T != (TG | PEND)) SL = SL + 1 == (unsigned int)RS ? 0u : SL + 1;
+            if (claim) {
+                if (ld(&s_nent) >= CLAIM_MAX) {
+                    ST = 2;
+                } else if (atomicCAS(&R.tag[SL], 0u, TG | PEND) == 0) {
+                    R.x[SL] = K0, R.y[SL] = K1, R.z[SL] = K2;
+                    __hip_atomic_store(&R.tag[SL], TG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    atomicAdd(&s_nent, 1u);
+                    ST = 1;
+                }
+            }
+        }
+        if (valid && ST == 1) {
+            atomicAdd(&R.mult[SL], 1u);
+            if (EA < R.a[SL]) atomicMin(&R.a[SL], EA);
+            if (EB < R.b[SL]) atomicMin(&R.b[SL], EB);
+        }
+        if (ST == 2) {  // the overflow list (full: the call is redone elsewhere)
+            const unsigned int o = atomicAdd(&s_nov, 1u);
+            if (o < (unsigned int)OV) o_x[o] = K0, o_y[o] = K1, o_z[o] = K2, o_a[o] = EA, o_b[o] = EB;
+            else s_over[0] = 1;
+        }
+    };
+    for (uint64_t c0 = r0; c0 < r1; c0 += PD * NT) {
+#pragma unroll
+        for (int d = 0; d < PD; d++) {
+            if (c0 + (uint64_t)d * NT >= r1) break;  // uniform
+            record_round(nx[d], c0 + (uint64_t)d * NT);
+        }
+    }
+    __syncthreads();
+    // ---- distinct records out of the record table, counted by window count --------------------
+    constexpr int PER = (RS + NT - 1) / NT;
+    uint32_t cx[PER], cy[PER], cz[PER], cm[PER], ca[PER], cb[PER], bin[PER], rk[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const unsigned int i = tid + q * NT;
+        bin[q] = SK2_NMAX;
+        if (i < (unsigned)RS && R.tag[i]) {
+            cx[q] = R.x[i], cy[q] = R.y[i], cz[q] = R.z[i], cm[q] = R.mult[i], ca[q] = R.a[i], cb[q] = R.b[i];
+            bin[q] = SK2_NMAX - 1 - (cz[q] >> 28);  // most windows first
+            rk[q] = atomicAdd(&s_ncnt[bin[q]], 1u);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned int a = 0;
+        for (int q = 0; q < SK2_NMAX; q++) {
+            const unsigned int v = s_ncnt[q];
+            s_ncnt[q] = a;
+            a += v;
+        }
+        s_ncnt[SK2_NMAX] = a;
+        if (dbg) atomicAdd(&dbg[0], (unsigned long long)a), atomicAdd(&dbg[1], 1ull);
+    }
+    // the k-mer table over the record table's space (its reads are done)
+    for (int i = tid; i < SLOTS; i += NT) {
+        tab.key[i] = EMPTY_KEY;
+        tab.count[i] = 0;
+        tab.ev[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++)
+        if (bin[q] < SK2_NMAX) {
+            const unsigned int o = s_ncnt[bin[q]] + rk[q];
+            L.k.x[o] = cx[q], L.k.y[o] = cy[q], L.k.z[o] = cz[q], L.k.mult[o] = cm[q], L.k.a[o] = ca[q], L.k.b[o] = cb[q];
+        }
+    __syncthreads();
+    const unsigned int ne = s_ncnt[SK2_NMAX], nov = min(s_nov, (unsigned int)OV);
+    for (unsigned int t = tid; t < ne + nov; t += NT) {
+        if (t < ne) roll_out(L.k.x[t], L.k.y[t], L.k.z[t], L.k.mult[t], L.k.a[t], L.k.b[t]);
+        else {
+            const unsigned int o = t - ne;
+            roll_out(o_x[o], o_y[o], o_z[o], 1u, o_a[o], o_b[o]);
+        }
+    }
+    if (dbg) atomicAdd(&dbg[2], n_rolled);
+    lds_table_finish<SLOTS, false, KeyId, LTabE<SLOTS>, EvExpand, NT>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub,
+                                                                      nsolid, ndistinct, overflow, KeyId(),
+                                                                      EvExpand{2 * M});
 }
 
 }  // namespace ec
