@@ -651,10 +651,11 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     }
     if (plan.slots == 1024) {
         constexpr int NT3 = 512;
+        const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
         if (k & 1)
-            k_skbucket3<1024, 1664, NT3, false><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg);
+            k_skbucket3<1024, 1664, NT3, false><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg, claim_cap);
         else
-            k_skbucket3<1024, 1664, NT3, true><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg);
+            k_skbucket3<1024, 1664, NT3, true><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg, claim_cap);
     } else if (plan.slots == 2048) {
         if (k & 1) EC_SKBUCKET(2048, 3072, false);
         else EC_SKBUCKET(2048, 3072, true);

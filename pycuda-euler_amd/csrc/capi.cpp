@@ -43,6 +43,7 @@ void refresh_knobs() {
         k.sk2_stats = flag("EULERHIP_SK2_STATS");
         k.no_slot_groups = flag("EULERHIP_NO_SLOT_GROUPS");
         k.no_skb3 = flag("EULERHIP_NO_SKB3");
+        k.sk2_claim = num("EULERHIP_SK2_CLAIM", 0);
         k.verbose = flag("EULERHIP_VERBOSE");
     }
     g_knobs = k;

@@ -39,6 +39,7 @@ struct Knobs {
     int sk2_exp = 0;            // EULERHIP_SK2_EXP bit 2: no reverse complement in k_skbucket's record
                                 // keys (A/B; results stay exact)
     bool sk2_stats = false;     // EULERHIP_SK2_STATS: k_skbucket dedup statistics on stderr
+    int sk2_claim = 0;          // EULERHIP_SK2_CLAIM: k_skbucket3 record-table claim cap (tests: overflow list)
     bool no_skb3 = false;       // EULERHIP_NO_SKB3: k_skbucket's 8192-bucket plan instead of k_skbucket3 (A/B)
     bool no_slot_groups = false; // EULERHIP_NO_SLOT_GROUPS: k_skpart_w read groups not rounded to resident slots (A/B)
     bool verbose = false;       // EULERHIP_VERBOSE: count-path fallbacks on stderr

@@ -1009,7 +1009,8 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
                                                   long long limit, unsigned long long *dkey, unsigned int *dcnt,
                                                   unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
                                                   unsigned int *nsolid, unsigned long long *ndistinct,
-                                                  unsigned int *overflow, unsigned long long *dbg) {
+                                                  unsigned int *overflow, unsigned long long *dbg,
+                                                  unsigned int claim_cap) {
     constexpr int SBITS = __builtin_ctz(SLOTS);
     constexpr uint32_t PEND = 0x800u;
     constexpr unsigned int CLAIM_MAX = RS / 2 < RS - 1 - NT ? RS / 2 : RS - 1 - NT;
@@ -1144,7 +1145,7 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
             const bool claim = go && !hit && T == 0;
             if (go && !hit && T != 0 && T != (TG | PEND)) SL = SL + 1 == (unsigned int)RS ? 0u : SL + 1;
             if (claim) {
-                if (ld(&s_nent) >= CLAIM_MAX) {
+                if (ld(&s_nent) >= min(CLAIM_MAX, claim_cap)) {  // (claim_cap: tests of the overflow list)
                     ST = 2;
                 } else if (atomicCAS(&R.tag[SL], 0u, TG | PEND) == 0) {
                     R.x[SL] = K0, R.y[SL] = K1, R.z[SL] = K2;

@@ -570,6 +570,35 @@ def test_sk2_slices_and_limits_vs_oracle(gpu_session, monkeypatch, rs):
         assert res.contig_bytes == ref["contig_chars"] and res.links == rl, (k, lim)
 
 
+@pytest.mark.parametrize("cap,variant", [("400", 3), ("8", None)])
+def test_sk2_record_overflow_list_vs_oracle(gpu_session, monkeypatch, cap, variant):
+    """k_skbucket3 with its record-table claims capped (EULERHIP_SK2_CLAIM): records past the cap
+    go to the overflow list and are rolled out one by one (cap 400 of ~530 distinct records a
+    bucket); a full list (cap 8) redoes the call on another path -- exact either way"""
+    monkeypatch.setenv("EULERHIP_SK2_CLAIM", cap)
+    buf, off = make_reads(20_000, 4_000, 100, 5300, err=0.0)
+    ref, rc, rl = _oracle_packed(buf, off, 31, 1, True)
+    gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(31, True)
+    if variant is not None:
+        assert res.stats.count_variant == variant
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
+@pytest.mark.parametrize("k", [31, 24])
+def test_sk2_large_table_kernel_vs_oracle(gpu_session, monkeypatch, k):
+    """EULERHIP_NO_SKB3: k_skbucket's 2048-slot tables (the plan for inputs past ~6 M keys)"""
+    monkeypatch.setenv("EULERHIP_NO_SKB3", "1")
+    buf, off = make_reads(50_000, 15_000, 100, 5310 + k, err=0.001)
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(k, True)
+    assert res.stats.count_variant == 3
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
 def test_sk2_palindromes_vs_oracle(gpu_session):
     """even k: palindromic k-mers (inserted twice by build) inside super-k-mers"""
     rng = np.random.default_rng(17)
