@@ -355,6 +355,13 @@ def main():
                 kernel_alg_bytes(eulerhip.KERNEL_NAMES[i], int(st.n_positions), int(st.n_reads), L, K, rec,
                                  int(st.n_records), nsub, rec2) / (float(kern[i]) / 1e3) / (HBM_PEAK_GBS * 1e9), 5)
                 for i in range(len(kern)) if kern[i] > 0},
+            # measured HBM bytes (PMC traffic) per launch / launch time / peak: the HBM roofline on
+            # what the kernels really move (k_skbucket's §8d basis counts LDS insert work)
+            "frac_hbm": (round(tr["kernel_bytes_per_launch"] / (kms / 1e3) / (HBM_PEAK_GBS * 1e9), 5) if tr else None),
+            "kernels_frac_hbm": {names_v[i]: round(t["kernel_bytes_per_launch"] / (float(kern[i]) / 1e3)
+                                                   / (HBM_PEAK_GBS * 1e9), 5)
+                                 for i in range(len(kern)) if kern[i] > 0
+                                 for t in [load_traffic(cfg["name"], names_v[i])] if t},
             "pipeline_alg_bytes": int(alg_bytes(P, R, L, U, K)),
             "pipeline_frac": round(alg_bytes(P, R, L, U, K) / (ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5)}
     host = None

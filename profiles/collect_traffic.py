@@ -15,27 +15,41 @@ import re
 import sys
 
 KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine", "k_prescan", "k_partition", "k_refine2",
-           "k_skpart", "k_skrefine", "k_skbucket")
+           "k_skpart", "k_skrefine", "k_skbucket", "k_neighbors", "k_walk")
 
 
 def short(name):
     for k in KERNELS:
-        if re.search(r"\b%s(_sk|_w)?\b" % k, name):
+        if re.search(r"\b%s(_sk|_w|3)?\b" % k, name):
             return k
     return None
 
 
-def per_kernel(d, counter):
-    vals = {}
+def rows(d, counter):
+    """(kernel name, dispatch id, value) of `counter`: rocprofv3 CSV output or its rocpd SQLite
+    database (run_results.db, the default output format of newer rocprofv3)."""
+    import sqlite3
+
     for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(fn) as f:
             for row in csv.DictReader(f):
-                if row["Counter_Name"] != counter:
-                    continue
-                k = short(row["Kernel_Name"])
-                if k:
-                    vals.setdefault(k, {}).setdefault(row["Dispatch_Id"], 0.0)
-                    vals[k][row["Dispatch_Id"]] += float(row["Counter_Value"])
+                if row["Counter_Name"] == counter:
+                    yield row["Kernel_Name"], row["Dispatch_Id"], float(row["Counter_Value"])
+    for fn in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
+        con = sqlite3.connect(fn)
+        for name, disp, val in con.execute(
+                "select kernel_name, dispatch_id, value from counters_collection where counter_name = ?", (counter,)):
+            yield name, str(disp), float(val)
+        con.close()
+
+
+def per_kernel(d, counter):
+    vals = {}
+    for name, disp, val in rows(d, counter):
+        k = short(name)
+        if k:
+            vals.setdefault(k, {}).setdefault(disp, 0.0)
+            vals[k][disp] += val
     return {k: sum(v.values()) / len(v) * 1024.0 for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
 
 
