@@ -222,6 +222,9 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="N > 1: split the config's reads over the ranks (fixed job) instead of the default "
                          "weak scaling (every rank samples its own config-sized read set of the same genome)")
+    ap.add_argument("--no-strong-leg", action="store_true",
+                    help="N > 1 weak-scaled runs: skip the strong-scaled leg (the config's read set split over "
+                         "the ranks, reported under \"strong\")")
     ap.add_argument("--wide-records", action="store_true", help="16-B count records only (EC_FLAG_WIDE_RECORDS)")
     ap.add_argument("--window-records", action="store_true",
                     help="one record per k-mer window, no super-k-mers (EC_FLAG_WINDOW_RECORDS)")
@@ -319,6 +322,33 @@ def main():
     R, L = cfg["reads"] * (world if weak else 1), cfg["read_len"]
     value = P / (ms / 1e3)
 
+    # strong-scaled leg (N > 1, weak mode): the config's own read set (rank 0's) split into
+    # contiguous shards over the ranks (BASELINE config 4: "10M x 100 bp reads, read-sharded"),
+    # timed the same way; reported beside the weak-scaled value
+    strong = None
+    if weak and world > 1 and not args.no_strong_leg:
+        import distributed
+
+        lo, hi = distributed.shard_range(cfg["reads"], rank, world)
+        sbuf, soff = make_reads(cfg["genome"], cfg["reads"], cfg["read_len"], cfg["seed"], err=cfg.get("err", 0.0),
+                                rows=(lo, hi))
+        srun = distributed.ShardedAssembler(sbuf, soff, k, 1, rank, world, local, comm=runner.comm, read_base=lo)
+        for _ in range(max(1, args.warmup)):
+            srun.run(eulerhip.EC_FLAG_KERNEL_TIMING, fetch=False)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            srun.run(eulerhip.EC_FLAG_KERNEL_TIMING, fetch=False)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t1], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sms = float(t.item()) / args.steps * 1e3
+        strong = {"value": round(srun.total_positions / (sms / 1e3), 1), "unit": "k-mers/s",
+                  "ms_per_step": round(sms, 3), "reads": cfg["reads"], "reads_per_gpu": hi - lo,
+                  "positions": int(srun.total_positions), "scaling": "strong"}
+
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -391,6 +421,7 @@ def main():
         "host_input": host,
         "stage_ms": {names[i]: round(stage[i], 3) for i in range(len(names))},
         "sharded_phase_ms": sharded_ms,
+        "strong": strong,
     }
     print(json.dumps(out), file=json_out, flush=True)
     if dist:

@@ -1539,8 +1539,19 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_HIP(hipStreamSynchronize(st));
     const uint64_t P = hsc.npos;
     const double est = hsc.est;
-    double per_max = 1800.0;  // keys per bucket table (SLOTS_W slots)
-    if (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT || !P || est / FINE_W > per_max) return reset();
+    // Up to 2^FINE_W_BITS buckets of <= 1100 estimated keys in 3328-slot tables (156 KB: one
+    // workgroup per CU), sized exactly by the fine histogram.  Past that (~1.8e7 keys: config
+    // 5's 200 Mbp genome has 2e8) a third level splits every fine bucket into 2^sbits
+    // fixed-capacity sub-buckets of <= 800 estimated keys in 1664-slot tables (78 KB: two
+    // workgroups per CU); measured before: such inputs fell to the HBM table (k_count 130 ms of
+    // a 335 ms step at 1.25e9 positions).
+    if (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT || !P) return reset();
+    int sbits = 0;
+    if (est / FINE_W > 1800.0) {
+        while (sbits < 6 && est / (double)(FINE_W << sbits) > 800.0) sbits++;
+        if (est / (double)(FINE_W << sbits) > 800.0) return reset();
+    }
+    if (kn().wide_l3 > 0) sbits = std::min(6, kn().wide_l3);
     s->stats.n_reads = nreads;
     s->stats.n_positions = P;
     s->stats.n_distinct_est = (uint64_t)llround(est);
@@ -1548,18 +1559,24 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     int bbits = 0;
     int maxb = FINE_W_BITS;  // (EULERHIP_WIDE_MAX_BBITS: tests force bucket overflow)
     if (kn().wide_max_bbits >= 0) maxb = std::max(0, std::min(FINE_W_BITS, kn().wide_max_bbits));
+    if (sbits) bbits = FINE_W_BITS;
     while (bbits < maxb && est / (double)(1ull << bbits) > 1100.0) bbits++;
     int fan = 0;
     while ((1 << (fan + 1)) <= REFINE_FANOUT) fan++;
     const int cbits = std::min(bbits, std::min(DS_MAX_CBITS, std::max(1, bbits - fan)));
     const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
-    constexpr unsigned int SLOTS = SLOTS_W;
+    const uint64_t Bt = Bk << sbits;  // tables
+    // third-level capacity: mean + 30 % + 1024 (a sub-bucket's records are a sum over its
+    // ~800 keys of their multiplicities: its spread is a few % of the mean)
+    uint64_t fcap3 = sbits ? P / Bt + P / Bt * 3 / 10 + 1024 : 0;
+    if (sbits && kn().wide_l3_cap > 0) fcap3 = (uint64_t)kn().wide_l3_cap;
+    const unsigned int SLOTS = sbits ? 1664u : (unsigned int)SLOTS_W;
     mark(s, 2 * EC_STAGE_COUNT);
     EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
     EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
     EC_CHECK(s->tot.ensure((Bk + 1) * 8));
     EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
-    EC_CHECK(s->recs.ensure(P * sizeof(RecW)));
+    EC_CHECK(s->recs.ensure(std::max<uint64_t>(P, Bt * fcap3) * sizeof(RecW)));
     const bool second = bbits > cbits;
     if (second) EC_CHECK(s->recs2.ensure(P * sizeof(RecW)));
     s->stats.record_bytes = (uint32_t)sizeof(RecW);
@@ -1581,21 +1598,43 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
             StoreW{s->recs.as<RecW>()}, StoreW{s->recs2.as<RecW>()}, s->bstart.as<unsigned long long>(),
             s->gcur.as<unsigned long long>(), cbits, bbits);
+        if (sbits) {  // fine buckets (recs2) -> fixed-capacity sub-buckets (recs)
+            EC_CHECK(s->bb2.ensure((Bt + 1) * 8 * 2));
+            EC_CHECK(s->gcur.ensure(Bt * 8));
+            EC_CHECK(s->fcur.ensure((Bt + 1) * 8));
+            unsigned long long *b3 = s->fcur.as<unsigned long long>();
+            k_level3_init<<<grid_for(Bt + 1, B, 8192), B, 0, st>>>(s->bstart.as<unsigned long long>(), Bk, sbits, fcap3,
+                                                                   b3, s->gcur.as<unsigned long long>());
+            k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Bk, 1), BUCKET_THREADS, 0, st>>>(
+                StoreW{s->recs2.as<RecW>()}, StoreW{s->recs.as<RecW>()}, b3, s->gcur.as<unsigned long long>(), bbits,
+                bbits + sbits, fcap3, &dsc->overflow);
+            k_level3_ends<<<grid_for(Bt, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), Bt, fcap3,
+                                                               s->bb2.as<unsigned long long>(),
+                                                               s->bb2.as<unsigned long long>() + Bt + 1);
+        }
         kmark(s, 4, 1);
     }
     mark(s, 2 * EC_STAGE_COUNT + 1);
     mark(s, 2 * EC_STAGE_COMPACT);
-    const uint64_t umax = Bk * SLOTS;
+    const uint64_t umax = Bt * SLOTS;
     EC_CHECK(s->dkey.ensure(umax * sizeof(K128)));
     EC_CHECK(s->dcnt.ensure(umax * 4));
     EC_CHECK(s->dfc.ensure(umax * 8));
     EC_CHECK(s->dft.ensure(umax * 8));
     if (!s->no_index) EC_CHECK(s->sub.ensure(umax * sizeof(SubSlotW)));
     kmark(s, 2, 0);
-    k_bucket_w<SLOTS><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(
-        second ? s->recs2.as<RecW>() : s->recs.as<RecW>(), s->bstart.as<unsigned long long>(), limit, s->dkey.as<K128>(),
-        s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-        s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow);
+#define EC_BUCKET_W(SL, SRC, BEG, END)                                                                          \
+    k_bucket_w<SL><<<(unsigned)Bt, BUCKET_THREADS, 0, st>>>(                                                     \
+        SRC, BEG, END, limit, s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),    \
+        s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
+        &dsc->ndistinct, &dsc->overflow)
+    if (sbits)
+        EC_BUCKET_W(1664, s->recs.as<RecW>(), s->bb2.as<unsigned long long>(),
+                    s->bb2.as<unsigned long long>() + Bt + 1);
+    else
+        EC_BUCKET_W(SLOTS_W, second ? s->recs2.as<RecW>() : s->recs.as<RecW>(), s->bstart.as<unsigned long long>(),
+                    nullptr);
+#undef EC_BUCKET_W
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
@@ -1608,12 +1647,12 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     s->stats.n_distinct = hsc.ndistinct;
     s->stats.n_solid = U;
     s->stats.count_path = EC_PATH_PARTITIONED;
-    s->stats.n_buckets = (uint32_t)Bk;
+    s->stats.n_buckets = (uint32_t)Bt;
     s->stats.table_capacity = umax;
     sidx.table = nullptr;
     sidx.capmask = 0;
     sidx.sub = s->sub.as<SubSlotW>();
-    sidx.bbits = bbits;
+    sidx.bbits = bbits + sbits;
     sidx.slots = SLOTS;
     if (2ull * U >= (unsigned long long)CYC) {
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
@@ -1738,12 +1777,17 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_neighbors<Ops, Index><<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
                                                  s->cand.as<unsigned int>(), &dsc->npal);
+        EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
         k_succ<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(),
-                                            N, s->succ.as<unsigned int>());
+                                            N, s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                            s->dft.as<unsigned long long>(), s->nrec.as<NodeRec>());
     }
     if (U) {
-        k_pred<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
-                                            s->pred.as<unsigned int>());
+        // (with the first ruler pass's counts: k_rulers_count at it = 0 below is skipped)
+        EC_CHECK(s->rbc.ensure(((Nn + RULER_CHUNK - 1) / RULER_CHUNK) * 8));
+        k_pred_rc<<<(unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK), B, 0, st>>>(
+            s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, 31u, s->pred.as<unsigned int>(),
+            s->rbc.as<unsigned int>());
     }
     mark(s, 2 * EC_STAGE_LINKS + 1);
 
@@ -1765,14 +1809,16 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (U) {
         EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 8, st));
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
-        k_noderec<<<grid_for(N, B), B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                               s->dft.as<unsigned long long>(), N, s->nrec.as<NodeRec>());
+        if (ext_succ)  // (k_succ wrote the node records otherwise)
+            k_noderec<<<grid_for(N, B), B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                                   s->dft.as<unsigned long long>(), N, s->nrec.as<NodeRec>());
         unsigned int masks[4] = {31u, 7u, 1u, 0u};
         unsigned int r0 = 0;
         for (int it = 0; it < 4; it++) {
             const unsigned int nblk = (unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK);
-            k_rulers_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it], it == 0,
-                                               s->rid.as<uint2>(), s->rbc.as<unsigned int>());
+            if (it)  // (it = 0: counted by k_pred_rc with masks[0])
+                k_rulers_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it],
+                                                   it == 0, s->rid.as<uint2>(), s->rbc.as<unsigned int>());
             EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
             k_rulers<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it], it == 0,
                                          s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<uint2>(),
@@ -1802,11 +1848,12 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                   &dsc->final_sel, (unsigned)((r + 1) & 1));
         k_finalize<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(),
                                                 s->rid.as<uint2>(), s->rlist.as<unsigned int>(), bufs[0], bufs[1],
-                                                &dsc->final_sel, N, s->PK.as<unsigned int>(),
+                                                &dsc->final_sel, &dsc->active[rounds - 1], N, s->PK.as<unsigned int>(),
                                                 s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
                                                 s->PM.as<unsigned long long>());
         k_cycle_len<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), bufs[0],
-                                                  bufs[1], &dsc->final_sel, nr, s->PL.as<unsigned int>(),
+                                                  bufs[1], &dsc->final_sel, &dsc->active[rounds - 1], nr,
+                                                  s->PL.as<unsigned int>(),
                                                   s->PM.as<unsigned long long>());
     }
     s->stats.n_rulers = nr;

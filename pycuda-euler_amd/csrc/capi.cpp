@@ -37,6 +37,8 @@ void refresh_knobs() {
         k.merge_mix = flag("EULERHIP_MERGE_MIX");
         k.wide_general = flag("EULERHIP_WIDE_GENERAL");
         k.wide_max_bbits = num("EULERHIP_WIDE_MAX_BBITS", -1);
+        k.wide_l3 = num("EULERHIP_WIDE_L3", 0);
+        if (const char *e = getenv("EULERHIP_WIDE_L3_CAP")) k.wide_l3_cap = atoll(e);
         k.host_chunks = num("EULERHIP_HOST_CHUNKS", 0);
         k.sk2_nodedup = flag("EULERHIP_SK2_NODEDUP");
         k.sk2_exp = num("EULERHIP_SK2_EXP", 0);

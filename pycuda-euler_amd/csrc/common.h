@@ -34,6 +34,8 @@ struct Knobs {
     bool merge_mix = false;     // EULERHIP_MERGE_MIX: key-hash buckets / owners instead of minimizers
     bool wide_general = false;  // EULERHIP_WIDE_GENERAL: k > 32 on the HBM table
     int wide_max_bbits = -1;    // EULERHIP_WIDE_MAX_BBITS: cap the wide buckets (forces overflow)
+    int wide_l3 = 0;            // EULERHIP_WIDE_L3: third partition level of 2^n sub-buckets at any size
+    long long wide_l3_cap = 0;  // EULERHIP_WIDE_L3_CAP: its sub-bucket capacity (forces its overflow)
     int host_chunks = 0;        // EULERHIP_HOST_CHUNKS: host-input chunks (0 = ~32 MiB each)
     bool sk2_nodedup = false;   // EULERHIP_SK2_NODEDUP: record-per-lane k_skbucket_rec (A/B)
     int sk2_exp = 0;            // EULERHIP_SK2_EXP bit 2: no reverse complement in k_skbucket's record

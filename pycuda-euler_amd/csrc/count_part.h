@@ -502,9 +502,13 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
 // gridDim.y workgroups share a coarse bucket (contiguous tile ranges); each tile reserves its
 // runs in the final buckets with one global atomic per final bucket (cursor gcur, initialised
 // to bstart).  Run order inside a final bucket is then arbitrary -- k_bucket is order-free.
+// fcap != 0: the final buckets have a fixed capacity of fcap records from d * fcap (count_wide.h's
+// third level, whose bucket sizes nothing counted): a record past its bucket's end is dropped
+// and *over set (the caller then counts on the HBM table).
 template <typename RecT, typename StoreIn, typename StoreOut>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut out, const unsigned long long *bstart,
-                                                          unsigned long long *gcur, int cbits, int bbits) {
+                                                          unsigned long long *gcur, int cbits, int bbits,
+                                                          uint64_t fcap = 0, unsigned int *over = nullptr) {
     constexpr int TILE = sizeof(RecT) > 16 ? REFINE_TILE / 2 : REFINE_TILE;  // <= 64 KiB of LDS
     __shared__ RecT tile[TILE];
     __shared__ uint8_t tj[TILE];  // final bucket of each sorted record (the store loop needs no rehash)
@@ -582,9 +586,20 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
         if (threadIdx.x < REFINE_FANOUT) base[threadIdx.x] = mybase;
         __syncthreads();
         if (PIPE && t0 + TILE < tend) load_tile(t0 + TILE);
-        for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
-            const unsigned int j = tj[i];
-            out.store(base[j] + (i - tbeg[j]), tile[i]);
+        if (fcap) {
+            bool lost = false;
+            for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
+                const unsigned int j = tj[i];
+                const uint64_t pos = base[j] + (i - tbeg[j]);
+                if (pos < (c * F + j + 1) * fcap) out.store(pos, tile[i]);
+                else lost = true;
+            }
+            if (lost) *over = 1u;
+        } else {
+            for (unsigned int i = threadIdx.x; i < n; i += BUCKET_THREADS) {
+                const unsigned int j = tj[i];
+                out.store(base[j] + (i - tbeg[j]), tile[i]);
+            }
         }
         __syncthreads();
     }

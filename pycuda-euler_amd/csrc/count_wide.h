@@ -302,9 +302,34 @@ __device__ inline void lds_insert_w(LSlotW *tab, unsigned int *s_over, const K12
     if (eT < ev.y) atomicMin(&sl.fT, eT);
 }
 
+// ---- third partition level (more keys than 2^FINE_W_BITS tables hold) ---------------------
+// The upsweep's fine histogram sizes 2^FINE_W_BITS buckets exactly; past ~1.8e7 distinct keys
+// each of them is split again by the next hash bits into 2^s sub-buckets of fixed capacity
+// (k_refine with fcap: the hash is uniform, so a sub-bucket holds its mean +- a few sigma).
+// bstart3[c << s] = bstart[c] gives k_refine its input ranges; cursors start at d * fcap.
+__global__ void __launch_bounds__(256) k_level3_init(const unsigned long long *bstart, uint64_t nfine, int s,
+                                                     uint64_t fcap, unsigned long long *bstart3,
+                                                     unsigned long long *gcur) {
+    const uint64_t F = 1ull << s;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t <= nfine * F;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        if ((t & (F - 1)) == 0) bstart3[t] = bstart[t >> s];
+        if (t < nfine * F) gcur[t] = t * fcap;
+    }
+}
+// bucket d's records: [d * fcap, min(gcur[d], (d + 1) * fcap))
+__global__ void __launch_bounds__(256) k_level3_ends(const unsigned long long *gcur, uint64_t nb, uint64_t fcap,
+                                                     unsigned long long *bbeg, unsigned long long *bend) {
+    for (uint64_t d = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; d < nb; d += (uint64_t)gridDim.x * blockDim.x) {
+        bbeg[d] = d * fcap;
+        bend[d] = min((uint64_t)gcur[d], (d + 1) * fcap);
+    }
+}
+
+// bend != nullptr: bucket b is [bstart[b], bend[b]) (third level), else [bstart[b], bstart[b + 1])
 template <int SLOTS>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, const unsigned long long *bstart,
-                                                            long long limit, K128 *dkey, unsigned int *dcnt,
+                                                            const unsigned long long *bend, long long limit, K128 *dkey, unsigned int *dcnt,
                                                             unsigned long long *dfc, unsigned long long *dft,
                                                             SubSlotW *sub, unsigned int *nsolid,
                                                             unsigned long long *ndistinct, unsigned int *overflow) {
@@ -325,7 +350,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, c
         s_over[1] = 0;
     }
     __syncthreads();
-    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    const uint64_t r0 = bstart[b], r1 = bend ? bend[b] : bstart[b + 1];
     constexpr int U = 4;  // loads of U records issued before any insert
     auto ins = [&](const RecW &x) {
         const unsigned int lC = x.ev & 0xFFFFu, lT = x.ev >> 16;

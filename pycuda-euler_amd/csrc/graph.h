@@ -192,8 +192,22 @@ __global__ void __launch_bounds__(256) k_neighbors(Index idx, const typename Ops
 // links phase 2: x -> y iff |fw(x) in d| == 1, |bw(y) in d| == 1 and y != twin(x)
 // (get_contig_forward:63-73; the cand == km / twin(km) stop is applied by the walk emulation)
 // |bw(y) in d| == |fw(twin y) in d| == outdeg[twin y].
+__device__ inline unsigned long long first_event(const unsigned long long *dfc, const unsigned long long *dft,
+                                                 unsigned int x) {
+    return (x & 1) ? dft[x >> 1] : dfc[x >> 1];
+}
+
+// A node's successor and first event side by side (k_noderec): the walk's random step then
+// touches one line instead of three (succ, dfc / dft).
+struct alignas(16) NodeRec {
+    unsigned int succ;
+    unsigned int pad;
+    unsigned long long fev;
+};
+// nrec != nullptr: also the ruler walk's node records (succ + first event, k_noderec's output)
 __global__ void __launch_bounds__(256) k_succ(const uint8_t *upal, const uint8_t *outdeg, const unsigned int *cand,
-                                              unsigned int N, unsigned int *succ) {
+                                              unsigned int N, unsigned int *succ, const unsigned long long *dfc,
+                                              const unsigned long long *dft, NodeRec *nrec) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         unsigned int s = NONE32;
@@ -203,6 +217,13 @@ __global__ void __launch_bounds__(256) k_succ(const uint8_t *upal, const uint8_t
             if (outdeg[ty] == 1 && y != twin_node(upal, x)) s = y;
         }
         succ[x] = s;
+        if (nrec) {
+            NodeRec r;
+            r.succ = s;
+            r.pad = 0;
+            r.fev = first_event(dfc, dft, x);
+            nrec[t] = r;
+        }
     }
 }
 
@@ -272,24 +293,6 @@ __global__ void __launch_bounds__(256) k_upal(const typename Ops::K *dkey, unsig
     if ((threadIdx.x & 63) == 0 && np) atomicAdd(npal, np);
 }
 
-__device__ inline unsigned long long first_event(const unsigned long long *dfc, const unsigned long long *dft,
-                                                 unsigned int x) {
-    return (x & 1) ? dft[x >> 1] : dfc[x >> 1];
-}
-
-// pred(x) = twin(succ(twin(x))): the links are closed under twin-reversal
-__global__ void __launch_bounds__(256) k_pred(const uint8_t *upal, const unsigned int *succ, unsigned int N,
-                                              unsigned int *pred) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int x = (unsigned int)t;
-        unsigned int p = NONE32;
-        if (!((x & 1) && upal[x >> 1])) {
-            const unsigned int sx = succ[twin_node(upal, x)];
-            if (sx != NONE32) p = twin_node(upal, sx);
-        }
-        pred[x] = p;
-    }
-}
 
 // ---- list ranking by a sparse ruling set ------------------------------------------------
 // Rulers: every path head plus every node whose hash hits the sampling mask.  Each ruler
@@ -309,6 +312,32 @@ __device__ inline bool ruler_sel(const uint8_t *upal, const unsigned int *pred, 
                                  unsigned int smask, int first) {
     if (((x & 1) && upal[x >> 1]) || rid[x].x != NONE32) return false;
     return (first && pred[x] == NONE32) || ruler_hash(x, smask);
+}
+
+// pred(x) = twin(succ(twin(x))) (the links are closed under twin-reversal), fused with the
+// first ruler pass's counting (k_rulers_count with first = 1: every node's
+// rid is still NONE then): block b handles the RULER_CHUNK nodes of chunk b
+__global__ void __launch_bounds__(256) k_pred_rc(const uint8_t *upal, const unsigned int *succ, unsigned int N,
+                                                 unsigned int smask, unsigned int *pred, unsigned int *bc) {
+    const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
+    const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
+    unsigned int c = 0;
+    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+        const unsigned int x = (unsigned int)t;
+        unsigned int p = NONE32;
+        const bool skip = (x & 1) && upal[x >> 1];
+        if (!skip) {
+            const unsigned int sx = succ[twin_node(upal, x)];
+            if (sx != NONE32) p = twin_node(upal, sx);
+        }
+        pred[x] = p;
+        c += !skip && (p == NONE32 || ruler_hash(x, smask));
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    __shared__ unsigned int w[4];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bc[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
 }
 
 __global__ void __launch_bounds__(256) k_rulers_count(const uint8_t *upal, const unsigned int *pred, unsigned int N,
@@ -368,13 +397,6 @@ struct alignas(32) RJump {
 };
 static_assert(sizeof(RJump) == 32, "rjump layout");
 
-// A node's successor and first event side by side (k_noderec): the walk's random step then
-// touches one line instead of three (succ, dfc / dft).
-struct alignas(16) NodeRec {
-    unsigned int succ;
-    unsigned int pad;
-    unsigned long long fev;
-};
 __global__ void __launch_bounds__(256) k_noderec(const unsigned int *succ, const unsigned long long *dfc,
                                                  const unsigned long long *dft, unsigned int N, NodeRec *nrec) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -482,8 +504,19 @@ constexpr unsigned int CYC = 0x80000000u;
 // The Wyllie rounds' result is in rs0 or rs1 as *sel says (read here: no host round trip).
 __global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const unsigned int *succ, const uint2 *rid,
                                                   const unsigned int *rlist, const RJump *rs0, const RJump *rs1,
-                                                  const unsigned int *sel, unsigned int N, unsigned int *PK,
+                                                  const unsigned int *sel, const unsigned int *unconverged,
+                                                  unsigned int N, unsigned int *PK,
                                                   unsigned int *RK, unsigned int *PL, unsigned long long *PM) {
+    if (*unconverged) {  // the last Wyllie round still moved pointers (the host reports it):
+        // in-range placeholders, so the later kernels index nothing outside their arrays
+        for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+            PK[t] = (unsigned int)t;
+            RK[t] = 0;
+            PL[t] = 1;
+            PM[t] = 0;
+        }
+        return;
+    }
     const RJump *rs = (*sel & 1) ? rs1 : rs0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
@@ -509,7 +542,9 @@ __global__ void __launch_bounds__(256) k_finalize(const uint8_t *upal, const uns
 // cycle length / min: the ruler whose successor ruler is the key ruler closes the ring
 __global__ void __launch_bounds__(256) k_cycle_len(const unsigned int *nextR, const unsigned int *rlist,
                                                    const RJump *rs0, const RJump *rs1, const unsigned int *sel,
-                                                   unsigned int nr, unsigned int *PL, unsigned long long *PM) {
+                                                   const unsigned int *unconverged, unsigned int nr, unsigned int *PL,
+                                                   unsigned long long *PM) {
+    if (*unconverged) return;
     const RJump *rs = (*sel & 1) ? rs1 : rs0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
         const RJump r = rs[t];

@@ -391,6 +391,35 @@ def test_wide_fallbacks_vs_oracle(gpu_session, monkeypatch):
         assert res.contig_bytes == ref["contig_chars"] and res.links == rl
 
 
+@pytest.mark.parametrize("k,sbits", [(51, 2), (45, 1), (63, 3)])
+def test_wide_third_level_vs_oracle(gpu_session, monkeypatch, k, sbits):
+    """k > 32 past 2^14 bucket tables (config 5: 2e8 keys): every fine bucket split again into
+    2^sbits fixed-capacity sub-buckets (k_refine with fcap) counted in 1664-slot tables; forced
+    here on small inputs"""
+    monkeypatch.setenv("EULERHIP_WIDE_L3", str(sbits))
+    buf, off = make_reads(60_000, 25_000, 150, 70 + k, err=0.003)
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(k, True)
+    assert res.stats.count_path == eulerhip.EC_PATH_PARTITIONED
+    assert res.stats.n_buckets == (1 << 14) << sbits
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+
+
+def test_wide_third_level_overflow_falls_back(gpu_session, monkeypatch):
+    """a third-level sub-bucket past its capacity drops nothing silently: the call is redone on
+    the HBM table"""
+    monkeypatch.setenv("EULERHIP_WIDE_L3", "2")
+    monkeypatch.setenv("EULERHIP_WIDE_L3_CAP", "8")
+    buf, off = make_reads(40_000, 20_000, 150, 91, err=0.002)
+    ref, rc, rl = _oracle_packed(buf, off, 51, 1)
+    gpu_session.run_host(buf, off, 51, 1)
+    res = gpu_session.fetch(51)
+    assert res.stats.count_path == eulerhip.EC_PATH_GENERAL and res.stats.table_retries >= 1
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+
+
 @pytest.mark.parametrize("pmax,lim", [(2, 1), (3, 1), (3, 0), (2, -1)])
 def test_filter_bucket_parts_vs_oracle(gpu_session, monkeypatch, pmax, lim):
     """buckets split into 2^pmax part tables (hash bits 11..; SolidIndex::npb), as for genomes
