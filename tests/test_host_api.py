@@ -99,3 +99,22 @@ def test_oracle_partial_contigs_paths_and_cycles():
     out = R.partial_contigs(ev, ee, 3)
     g = [R.get_string(2, i) for i in range(6)]
     assert out == [[g[0], g[1], g[2], g[3]], [g[5], g[0]], [g[3], g[4], g[3]]]
+
+
+def test_get_optimal_launch_configuration():
+    """E4 (src/pyencode.py:237-255): block = (threadPerBlock, 1, 1); grid y = ceil(threads /
+    threadPerBlock) capped at 65535, grid x = y_uncapped // 65535 + 1 -- values worked out by hand
+    from the reference's arithmetic"""
+    import pyencode
+
+    cases = [
+        ((10, 32), ((32, 1, 1), (1, 1, 1))),            # threadCount <= threadPerBlock
+        ((32, 32), ((32, 1, 1), (1, 1, 1))),
+        ((33, 32), ((32, 1, 1), (1, 2, 1))),
+        ((100, 32), ((32, 1, 1), (1, 4, 1))),
+        ((65535 * 32, 32), ((32, 1, 1), (2, 65535, 1))),  # y = 65535 exactly: x = 65535 // 65535 + 1
+        ((65535 * 32 + 1, 32), ((32, 1, 1), (2, 65535, 1))),
+        ((200_000_000, 100), ((100, 1, 1), (31, 65535, 1))),
+    ]
+    for args, want in cases:
+        assert pyencode.getOptimalLaunchConfiguration(*args) == want, args
