@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <climits>
+#include <type_traits>
 #include <vector>
 
 #include "count_part.h"
@@ -35,6 +36,7 @@
 #include "compact.h"
 #include "count_wide.h"
 #include "hostin.h"
+#include "join_w.h"
 
 namespace ec {
 
@@ -1752,6 +1754,69 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
     return finish_wide(s, cap, limit, U, sidx);
 }
 
+// Links of 128-bit keys by the (k-1)-mer half-edge join (join_w.h).  ok = false (succ and npal
+// left for the caller's k_neighbors / k_succ) when a level region or a join table overflowed.
+int links_join_w(ec_session *s, int k, unsigned int U, bool &ok) {
+    ok = false;
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const uint64_t N = 2ull * U;
+    // final buckets of <= 900 (k-1)-mer groups (~U of them) in 2048-slot tables; levels of <= 256
+    int bt = 1;
+    while ((double)U / (double)(1ull << bt) > 900.0) bt++;
+    std::vector<int> lv;
+    for (int rem = bt; rem > 0; rem -= std::min(8, rem)) lv.push_back(std::min(8, rem));
+    const uint64_t extra_cap = U;  // palindromic (k-1)-mers' second records
+    uint64_t needA = N + extra_cap, needB = 0, nbmax = 1;
+    std::vector<uint64_t> fc(lv.size());
+    for (size_t l = 0, cb = 0; l < lv.size(); l++) {
+        cb += lv[l];
+        const uint64_t nb = 1ull << cb, mean = N / nb;
+        fc[l] = mean + mean * 3 / 10 + 1024;
+        (l & 1 ? needA : needB) = std::max(l & 1 ? needA : needB, nb * fc[l]);
+        nbmax = std::max(nbmax, nb);
+    }
+    EC_CHECK(s->recs.ensure(needA * sizeof(RecJ)));
+    EC_CHECK(s->recs2.ensure(needB * sizeof(RecJ)));
+    EC_CHECK(s->bb2.ensure(2 * nbmax * 8));
+    EC_CHECK(s->gcur.ensure(nbmax * 8));
+    EC_CHECK(s->tmp.ensure(16));
+    unsigned int *flags = s->tmp.as<unsigned int>();  // [0] extras, [1] overflow
+    unsigned long long *ibeg = s->bb2.as<unsigned long long>(), *iend = ibeg + nbmax;
+    EC_HIP(hipMemsetAsync(flags, 0, 8, st));
+    k_upal<OpsW><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<K128>(), U, k, s->upal.as<uint8_t>(), &dsc->npal);
+    RecJ *src = s->recs.as<RecJ>(), *dst = s->recs2.as<RecJ>();
+    k_half_emit<<<grid_for(U, B, 8192), B, 0, st>>>(s->dkey.as<K128>(), U, k, s->upal.as<uint8_t>(), src, &flags[0],
+                                                    extra_cap, &flags[1]);
+    k_half_range<<<1, 1, 0, st>>>(&flags[0], N, extra_cap, ibeg, iend);
+    int cb = 0;
+    for (size_t l = 0; l < lv.size(); l++) {
+        const uint64_t nc = 1ull << cb, nb = 1ull << (cb + lv[l]);
+        k_cursor_init<<<grid_for(nb, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), nb, fc[l]);
+        const unsigned rs = (unsigned)std::max<uint64_t>(1, 1024 / nc);
+        k_refine<RecJ, StoreJ, StoreJ><<<dim3((unsigned)nc, rs), BUCKET_THREADS, 0, st>>>(
+            StoreJ{src}, StoreJ{dst}, nullptr, s->gcur.as<unsigned long long>(), cb, cb + lv[l], fc[l], &flags[1], ibeg,
+            iend);
+        k_level3_ends<<<grid_for(nb, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), nb, fc[l], ibeg, iend);
+        std::swap(src, dst);
+        cb += lv[l];
+    }
+    EC_HIP(hipMemsetAsync(s->succ.p, 0xFF, N * 4, st));
+    k_half_join<2048, 512><<<(unsigned)(1ull << cb), 512, 0, st>>>(src, ibeg, iend, s->upal.as<uint8_t>(),
+                                                                  s->succ.as<unsigned int>(), &flags[1]);
+    unsigned int h[2];
+    EC_HIP(hipMemcpyAsync(h, flags, 8, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (h[1]) {  // the caller recounts npal with k_neighbors
+        if (kn().verbose) fprintf(stderr, "links_join_w: overflow (U %u, %d bucket bits), probing instead\n", U, cb);
+        EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
+        return EC_OK;
+    }
+    ok = true;
+    return EC_OK;
+}
+
 // all_contigs:79-111 on the device from the solid set of phase_count / phase_merge
 template <typename Ops, typename Index>
 int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const unsigned int *ext_succ = nullptr) {
@@ -1773,7 +1838,13 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<typename Ops::K>(), U, k, s->upal.as<uint8_t>(),
                                                  &dsc->npal);
         EC_HIP(hipMemcpyAsync(s->succ.p, ext_succ, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
-    } else if (U) {
+    }
+    bool joined = false;  // links of 128-bit keys by the half-edge join (join_w.h): from ~2e6 keys on
+    if constexpr (std::is_same<Ops, OpsW>::value) {
+        if (U && !ext_succ && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
+            EC_CHECK(links_join_w(s, k, U, joined));
+    }
+    if (U && !ext_succ && !joined) {
         k_neighbors<Ops, Index><<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
                                                  s->cand.as<unsigned int>(), &dsc->npal);
@@ -1809,7 +1880,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (U) {
         EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 8, st));
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
-        if (ext_succ)  // (k_succ wrote the node records otherwise)
+        if (ext_succ || joined)  // (k_succ wrote the node records otherwise)
             k_noderec<<<grid_for(N, B), B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
                                                    s->dft.as<unsigned long long>(), N, s->nrec.as<NodeRec>());
         unsigned int masks[4] = {31u, 7u, 1u, 0u};

@@ -508,7 +508,9 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep(const uint8_t *buf, co
 template <typename RecT, typename StoreIn, typename StoreOut>
 __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut out, const unsigned long long *bstart,
                                                           unsigned long long *gcur, int cbits, int bbits,
-                                                          uint64_t fcap = 0, unsigned int *over = nullptr) {
+                                                          uint64_t fcap = 0, unsigned int *over = nullptr,
+                                                          const unsigned long long *ibeg = nullptr,
+                                                          const unsigned long long *iend = nullptr) {
     constexpr int TILE = sizeof(RecT) > 16 ? REFINE_TILE / 2 : REFINE_TILE;  // <= 64 KiB of LDS
     __shared__ RecT tile[TILE];
     __shared__ uint8_t tj[TILE];  // final bucket of each sorted record (the store loop needs no rehash)
@@ -516,7 +518,9 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_refine(StoreIn in, StoreOut 
     __shared__ unsigned int tcnt[REFINE_FANOUT], tbeg[REFINE_FANOUT], wsum[REFINE_FANOUT / 64];
     const int F = 1 << (bbits - cbits);
     const uint64_t c = blockIdx.x;
-    const uint64_t r0 = bstart[c * F], r1 = bstart[(c + 1) * F];
+    // input: coarse bucket c's records [bstart[c F], bstart[(c + 1) F]), or [ibeg[c], iend[c])
+    // when the coarse buckets are themselves fixed-capacity regions (join_w.h's levels)
+    const uint64_t r0 = ibeg ? ibeg[c] : bstart[c * F], r1 = ibeg ? iend[c] : bstart[(c + 1) * F];
     const uint64_t nt = (r1 - r0 + TILE - 1) / TILE;
     const uint64_t tb = nt * blockIdx.y / gridDim.y, te = nt * (blockIdx.y + 1) / gridDim.y;
     constexpr int PER = TILE / BUCKET_THREADS;

@@ -1,0 +1,202 @@
+// join_w.h -- successor links of 128-bit keys (32 < k <= 63) by a (k-1)-mer half-edge join.
+//
+// get_contig_forward (referenceAssembler.py:59-73): oriented x -> y iff |fw(x) in d| = 1 (= y),
+// |bw(y) in d| = 1 and y != twin(x).  k_neighbors answers it with 8 hash probes per canonical
+// key; at config 5's 2e8 keys those are 1.6e9 random sub-table probes (67 ms of a 222 ms step).
+// Here the same relation comes out of a bucketed join, every pass sequential:
+//
+// For an oriented (k-1)-mer o let A(o) = {oriented k-mers in d whose suffix is o} and
+// B(o) = {oriented k-mers whose prefix is o}; for x in A(o): fw(x) in d = B(o), and for y in
+// B(o): bw(y) in d = A(o).  So x -> y iff A(o) = {x}, B(o) = {y} and y != twin(x).  Twin
+// symmetry: A(twin o) = twin(B(o)), B(twin o) = twin(A(o)), so one group per canonical (k-1)-mer
+// o^ holds both, and a link x -> y found there also gives twin(y) -> twin(x).
+//
+//   k_half_emit  per canonical key c (node 2u, twin node 2u+1): two records -- c's suffix s
+//                (s < twin s: (s, A, c); else (twin s, B, twin c)) and prefix p (p < twin p:
+//                (p, B, c); else (twin p, A, twin c)); a palindromic (k-1)-mer is both its own
+//                twin and canonical, so it gets both records (appended after the 2U)
+//   k_refine     2-3 levels of <= 256-way LDS bucket sorts into fixed-capacity regions (the
+//                count's refine kernel, fcap mode), by the top bits of mix128(o^)
+//   k_half_join  per final bucket: an LDS table keyed by o^ collects the distinct node ids of
+//                each side (a second distinct id marks the side "many"); every group with one
+//                id on each side and y != twin(x) writes succ[x] = y and succ[twin y] = twin x
+//
+// Record traffic: 2U records of 24 B written once and read + written once per level, then read
+// by the join: ~(2 + 2 L) * 48 B per key instead of 8 random probes.  A region or table past
+// its capacity makes the caller fall back to k_neighbors / k_succ (same result).
+#pragma once
+#include "count_wide.h"
+#include "graph.h"
+
+namespace ec {
+
+struct alignas(8) RecJ {
+    unsigned long long lo, hi;  // canonical (k-1)-mer
+    unsigned int tag;           // oriented node id | side << 31 (side 0 = A: suffix, 1 = B: prefix)
+    unsigned int pad;
+};
+static_assert(sizeof(RecJ) == 24, "join record layout");
+__device__ inline unsigned int rec_bucket(const RecJ &r, int bbits) {
+    return (unsigned int)(mix128(K128{r.lo, r.hi}) >> 32) >> (32 - bbits);
+}
+struct StoreJ {
+    RecJ *p;
+    __device__ inline RecJ load(uint64_t i) const { return p[i]; }
+    __device__ inline void store(uint64_t i, const RecJ &r) const { p[i] = r; }
+};
+
+// reverse complement of a j-mer, 32 <= j <= 62
+__device__ inline K128 twin_j(const K128 &x, int j) {
+    if (j <= 32) return K128{twin64(x.lo, j), 0ull};
+    return twin128(x, j);
+}
+
+__device__ inline RecJ make_recj(const K128 &o, unsigned int node, unsigned int side) {
+    RecJ r;
+    r.lo = o.lo;
+    r.hi = o.hi;
+    r.tag = node | (side << 31);
+    r.pad = 0;
+    return r;
+}
+
+// records 2u (suffix) and 2u + 1 (prefix) of key u; palindromic (k-1)-mers' second records
+// appended at 2U + wave_append(nextra) (at most extra_cap of them, else *over)
+__global__ void __launch_bounds__(256) k_half_emit(const K128 *dkey, unsigned int U, int k, const uint8_t *upal,
+                                                   RecJ *out, unsigned int *nextra, uint64_t extra_cap,
+                                                   unsigned int *over) {
+    const int j = k - 1;
+    const K128 mj = kmask128(j);
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < U; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        const bool valid = t < U;  // (every lane stays in the loop: wave_append is convergent)
+        bool e1 = false, e2 = false;
+        RecJ x1{}, x2{};
+        if (valid) {
+            const K128 c = dkey[t];
+            const unsigned int ic = 2u * (unsigned int)t, itc = upal[t] ? ic : ic + 1u;
+            const K128 s{c.lo & mj.lo, c.hi & mj.hi};
+            const K128 p{(c.lo >> 2) | (c.hi << 62), c.hi >> 2};
+            const K128 ts = twin_j(s, j), tp = twin_j(p, j);
+            out[2 * t] = s < ts ? make_recj(s, ic, 0) : make_recj(ts, itc, 1);
+            out[2 * t + 1] = p < tp ? make_recj(p, ic, 1) : make_recj(tp, itc, 0);
+            e1 = s == ts;  // (s, B, twin c) above; also (s, A, c)
+            e2 = p == tp;  // (p, A, twin c) above; also (p, B, c)
+            if (e1) x1 = make_recj(s, ic, 0);
+            if (e2) x2 = make_recj(p, ic, 1);
+        }
+        const unsigned int q1 = wave_append(nextra, e1);
+        if (e1) {
+            if (q1 < extra_cap) out[2ull * U + q1] = x1;
+            else *over = 1u;
+        }
+        const unsigned int q2 = wave_append(nextra, e2);
+        if (e2) {
+            if (q2 < extra_cap) out[2ull * U + q2] = x2;
+            else *over = 1u;
+        }
+    }
+}
+
+// level-1 input range [0, 2U + extras) and cursors d * fcap
+__global__ void k_half_range(const unsigned int *nextra, uint64_t n2, uint64_t extra_cap, unsigned long long *ibeg,
+                             unsigned long long *iend) {
+    ibeg[0] = 0;
+    iend[0] = n2 + min((uint64_t)*nextra, extra_cap);
+}
+__global__ void __launch_bounds__(256) k_cursor_init(unsigned long long *gcur, uint64_t nb, uint64_t fcap) {
+    for (uint64_t d = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; d < nb; d += (uint64_t)gridDim.x * blockDim.x)
+        gcur[d] = d * fcap;
+}
+
+// per final bucket: group the records by (k-1)-mer in LDS, then write the links
+template <int SLOTS, int NT>
+__global__ void __launch_bounds__(NT) k_half_join(const RecJ *recs, const unsigned long long *bbeg,
+                                                  const unsigned long long *bend, const uint8_t *upal,
+                                                  unsigned int *succ, unsigned int *overflow) {
+    __shared__ unsigned long long w1[SLOTS], w2[SLOTS];
+    __shared__ unsigned int ida[SLOTS], idb[SLOTS], many[SLOTS];
+    __shared__ unsigned int s_over[2];
+    const unsigned int b = blockIdx.x;
+    for (int i = threadIdx.x; i < SLOTS; i += NT) {
+        w1[i] = 0;
+        w2[i] = 0;
+        ida[i] = NONE32;
+        idb[i] = NONE32;
+        many[i] = 0;
+    }
+    if (threadIdx.x == 0) {
+        s_over[0] = 0;
+        s_over[1] = 0;
+    }
+    __syncthreads();
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    for (uint64_t base = r0; base < r1; base += NT) {
+        const uint64_t i = base + threadIdx.x;
+        const bool valid = i < r1;
+        RecJ r{};
+        if (valid) r = recs[i];
+        const K128 o{r.lo, r.hi};
+        const unsigned long long a1 = wide_w1(o), a2 = wide_w2(o);
+        unsigned int slot = (unsigned int)(((uint64_t)(uint32_t)mix128(o) * SLOTS) >> 32);
+        unsigned long long a = 0, bw = 0;
+        bool miss = valid;
+        if (valid) {
+            a = w1[slot];
+            bw = w2[slot];
+            miss = !(a == a1 && bw == a2);
+        }
+        // claim by two CASes on the key's 63-bit halves (as lds_insert_w), wave-uniform loop
+#pragma unroll 1
+        while (__any(miss)) {
+            if (miss) {
+                if (a == 0) {
+                    if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {
+                        s_over[0] = 1;
+                        a = a1;
+                        bw = a2;
+                    } else {
+                        a = atomicCAS(&w1[slot], 0ull, a1);
+                        if (a == 0) a = a1;
+                        else atomicSub(&s_over[1], 1u);
+                    }
+                }
+                if (a == a1 && bw != a2) {
+                    bw = w2[slot];
+                    if (bw == 0) {
+                        bw = atomicCAS(&w2[slot], 0ull, a2);
+                        if (bw == 0) bw = a2;
+                    }
+                }
+                if (!(a == a1 && bw == a2)) {
+                    slot = slot + 1 == SLOTS ? 0u : slot + 1;
+                    a = w1[slot];
+                    bw = w2[slot];
+                }
+                miss = !(a == a1 && bw == a2);
+            }
+        }
+        if (valid) {
+            const unsigned int side = r.tag >> 31, id = r.tag & 0x7FFFFFFFu;
+            unsigned int *ids = side ? idb : ida;
+            const unsigned int old = atomicCAS(&ids[slot], NONE32, id);
+            if (old != NONE32 && old != id) atomicOr(&many[slot], 1u << side);
+        }
+    }
+    __syncthreads();
+    if (s_over[0]) {
+        if (threadIdx.x == 0) atomicAdd(overflow, 1u);
+        return;
+    }
+    for (int i = threadIdx.x; i < SLOTS; i += NT) {
+        if (w1[i] == 0 || many[i]) continue;
+        const unsigned int x = ida[i], y = idb[i];
+        if (x == NONE32 || y == NONE32) continue;
+        const unsigned int tx = twin_node(upal, x), ty = twin_node(upal, y);
+        if (y == tx) continue;
+        succ[x] = y;
+        succ[ty] = tx;
+    }
+}
+
+}  // namespace ec

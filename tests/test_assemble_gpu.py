@@ -407,6 +407,35 @@ def test_wide_third_level_vs_oracle(gpu_session, monkeypatch, k, sbits):
     assert [[x, c] for x, c in res.dict_items] == ref["d"]
 
 
+@pytest.mark.parametrize("case", [c for c in CASES32 if c["k"] > 32], ids=lambda c: c["name"])
+def test_golden_wide_join_links(gpu_session, monkeypatch, case):
+    """k > 32 links by the (k-1)-mer half-edge join (join_w.h), forced at any size: golden
+    vectors of the imported reference"""
+    monkeypatch.setenv("EULERHIP_JOIN_LINKS", "1")
+    res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True)
+    assert [[x, c] for x, c in res.dict_items] == case["d"]
+    assert res.contigs == case["contigs"] and res.links == case["links"]
+
+
+@pytest.mark.parametrize("k", [33, 34, 40, 51, 62, 63])
+def test_wide_join_links_vs_oracle(gpu_session, monkeypatch, k):
+    """the half-edge join against the oracle: k = 33 (32-base junctions), even k (palindromic
+    k-mers), odd k (palindromic (k-1)-mer junctions), random reads with errors and tandem
+    repeats; and the probe path (EULERHIP_JOIN_LINKS=0) on the same input"""
+    buf, off = make_reads(40_000, 15_000, 150, 300 + k, err=0.004)
+    ref, rc, rl = _oracle_packed(buf, off, k, 1)
+    for mode in ("1", "0"):
+        monkeypatch.setenv("EULERHIP_JOIN_LINKS", mode)
+        gpu_session.run_host(buf, off, k, 1)
+        res = gpu_session.fetch(k)
+        assert res.contig_bytes == ref["contig_chars"] and res.links == rl, mode
+    monkeypatch.setenv("EULERHIP_JOIN_LINKS", "1")
+    reads = _low_complexity_reads(300, 140, 90 + k)
+    d, r, g = oracle.assemble(reads, k, 1)
+    res = gpu_session.assemble(reads, k, 1, want_dict=True)
+    assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g
+
+
 def test_wide_third_level_overflow_falls_back(gpu_session, monkeypatch):
     """a third-level sub-bucket past its capacity drops nothing silently: the call is redone on
     the HBM table"""
