@@ -1803,8 +1803,12 @@ int links_join_w(ec_session *s, int k, unsigned int U, bool &ok) {
         cb += lv[l];
     }
     EC_HIP(hipMemsetAsync(s->succ.p, 0xFF, N * 4, st));
-    k_half_join<2048, 512><<<(unsigned)(1ull << cb), 512, 0, st>>>(src, ibeg, iend, s->upal.as<uint8_t>(),
-                                                                  s->succ.as<unsigned int>(), &flags[1]);
+    if (k & 1)
+        k_half_join<2048, 512, true><<<(unsigned)(1ull << cb), 512, 0, st>>>(src, ibeg, iend, s->upal.as<uint8_t>(),
+                                                                            s->succ.as<unsigned int>(), &flags[1]);
+    else
+        k_half_join<2048, 512, false><<<(unsigned)(1ull << cb), 512, 0, st>>>(src, ibeg, iend, s->upal.as<uint8_t>(),
+                                                                             s->succ.as<unsigned int>(), &flags[1]);
     unsigned int h[2];
     EC_HIP(hipMemcpyAsync(h, flags, 8, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));

@@ -109,21 +109,24 @@ __global__ void __launch_bounds__(256) k_cursor_init(unsigned long long *gcur, u
         gcur[d] = d * fcap;
 }
 
-// per final bucket: group the records by (k-1)-mer in LDS, then write the links
-template <int SLOTS, int NT>
+// per final bucket: group the records by (k-1)-mer in LDS, then write the links.  Slots are
+// 24 B (key halves, one id word per side whose bit 31 marks a second distinct id): 2048 slots in
+// 48 KB, three workgroups per CU.  ODD_K: no palindromic k-mers, twin(x) = x ^ 1 without the
+// palindrome flags' random reads.
+template <int SLOTS, int NT, bool ODD_K>
 __global__ void __launch_bounds__(NT) k_half_join(const RecJ *recs, const unsigned long long *bbeg,
                                                   const unsigned long long *bend, const uint8_t *upal,
                                                   unsigned int *succ, unsigned int *overflow) {
+    constexpr unsigned int MANY = 0x80000000u;
     __shared__ unsigned long long w1[SLOTS], w2[SLOTS];
-    __shared__ unsigned int ida[SLOTS], idb[SLOTS], many[SLOTS];
+    __shared__ unsigned int ids[2][SLOTS];
     __shared__ unsigned int s_over[2];
     const unsigned int b = blockIdx.x;
     for (int i = threadIdx.x; i < SLOTS; i += NT) {
         w1[i] = 0;
         w2[i] = 0;
-        ida[i] = NONE32;
-        idb[i] = NONE32;
-        many[i] = 0;
+        ids[0][i] = NONE32;
+        ids[1][i] = NONE32;
     }
     if (threadIdx.x == 0) {
         s_over[0] = 0;
@@ -178,9 +181,8 @@ __global__ void __launch_bounds__(NT) k_half_join(const RecJ *recs, const unsign
         }
         if (valid) {
             const unsigned int side = r.tag >> 31, id = r.tag & 0x7FFFFFFFu;
-            unsigned int *ids = side ? idb : ida;
-            const unsigned int old = atomicCAS(&ids[slot], NONE32, id);
-            if (old != NONE32 && old != id) atomicOr(&many[slot], 1u << side);
+            const unsigned int old = atomicCAS(&ids[side][slot], NONE32, id);
+            if (old != NONE32 && (old & ~MANY) != id) atomicOr(&ids[side][slot], MANY);
         }
     }
     __syncthreads();
@@ -189,10 +191,9 @@ __global__ void __launch_bounds__(NT) k_half_join(const RecJ *recs, const unsign
         return;
     }
     for (int i = threadIdx.x; i < SLOTS; i += NT) {
-        if (w1[i] == 0 || many[i]) continue;
-        const unsigned int x = ida[i], y = idb[i];
-        if (x == NONE32 || y == NONE32) continue;
-        const unsigned int tx = twin_node(upal, x), ty = twin_node(upal, y);
+        const unsigned int x = ids[0][i], y = ids[1][i];  // (NONE32 has bit 31 set too)
+        if ((x | y) & MANY) continue;
+        const unsigned int tx = ODD_K ? x ^ 1u : twin_node(upal, x), ty = ODD_K ? y ^ 1u : twin_node(upal, y);
         if (y == tx) continue;
         succ[x] = y;
         succ[ty] = tx;
