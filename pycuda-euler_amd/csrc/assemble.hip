@@ -630,23 +630,17 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
     kmark(s, 2, 0);
     const double inv_m = 1.0 / M;
-    // records deduplicated per bucket before their windows are rolled out (k_skbucket); the
-    // record-per-lane kernel k_skbucket_rec for A/B (EULERHIP_SK2_NODEDUP=1)
-    const bool nodedup = kn().sk2_nodedup;
+    // records deduplicated per bucket before their windows are rolled out (k_skbucket3 /
+    // k_skbucket: 10x fewer k-mer inserts than one per record window on the headline)
 #define EC_SKBUCKET_ARGS                                                                                     \
     s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(),                    \
         s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),          \
         s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow
-#define EC_SKBUCKET(SLOTS, RS, EVEN)                                                                          \
-    do {                                                                                                      \
-        if (nodedup)                                                                                          \
-            k_skbucket_rec<SLOTS, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS);             \
-        else                                                                                                  \
-            k_skbucket<SLOTS, RS, 1, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg, kn().sk2_exp);     \
-    } while (0)
+#define EC_SKBUCKET(SLOTS, RS, EVEN) \
+    k_skbucket<SLOTS, RS, 1, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg)
     // EULERHIP_SK2_STATS: distinct records, flushes and windows rolled out (stderr)
     unsigned long long *dbg = nullptr;
-    if (kn().sk2_stats && !nodedup) {
+    if (kn().sk2_stats) {
         EC_CHECK(s->tmp.ensure(128));
         dbg = s->tmp.as<unsigned long long>();
         EC_HIP(hipMemsetAsync(dbg, 0, 128, st));

@@ -41,8 +41,6 @@ void refresh_knobs() {
         k.join_links = num("EULERHIP_JOIN_LINKS", -1);
         if (const char *e = getenv("EULERHIP_WIDE_L3_CAP")) k.wide_l3_cap = atoll(e);
         k.host_chunks = num("EULERHIP_HOST_CHUNKS", 0);
-        k.sk2_nodedup = flag("EULERHIP_SK2_NODEDUP");
-        k.sk2_exp = num("EULERHIP_SK2_EXP", 0);
         k.sk2_stats = flag("EULERHIP_SK2_STATS");
         k.no_slot_groups = flag("EULERHIP_NO_SLOT_GROUPS");
         k.no_skb3 = flag("EULERHIP_NO_SKB3");

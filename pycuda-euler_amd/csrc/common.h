@@ -38,9 +38,6 @@ struct Knobs {
     long long wide_l3_cap = 0;  // EULERHIP_WIDE_L3_CAP: its sub-bucket capacity (forces its overflow)
     int join_links = -1;        // EULERHIP_JOIN_LINKS: k > 32 links by the half-edge join 1 = always, 0 = never
     int host_chunks = 0;        // EULERHIP_HOST_CHUNKS: host-input chunks (0 = ~32 MiB each)
-    bool sk2_nodedup = false;   // EULERHIP_SK2_NODEDUP: record-per-lane k_skbucket_rec (A/B)
-    int sk2_exp = 0;            // EULERHIP_SK2_EXP bit 2: no reverse complement in k_skbucket's record
-                                // keys (A/B; results stay exact)
     bool sk2_stats = false;     // EULERHIP_SK2_STATS: k_skbucket dedup statistics on stderr
     int sk2_claim = 0;          // EULERHIP_SK2_CLAIM: k_skbucket3 record-table claim cap (tests: overflow list)
     bool no_skb3 = false;       // EULERHIP_NO_SKB3: k_skbucket's 8192-bucket plan instead of k_skbucket3 (A/B)

@@ -508,133 +508,6 @@ struct EvExpand {  // e -> (read << 32) | l for the dense arrays
     }
 };
 
-// Records go through LDS in chunks of BUCKET_THREADS, sorted by window count (most first) so a
-// wave's lanes run loops of nearly one length; lane = record, two windows per step (o and
-// o + ceil(n / 2): their LDS probes and updates in flight together, -2.5 %), each read once out
-// of the packed bases (fwd = 2-bit reversal, common.h rev2_64; rc = complement), then rolled.
-// Measured equal or slower: the chunk's windows split evenly over the lanes
-// (each window read straight out of the bases), and a two-slot fast path with the other
-// windows queued for lds_insert.
-template <int SLOTS, bool EVEN_K>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket_rec(const uint4 *recs, const unsigned long long *bbeg,
-                                                             const unsigned long long *bend, int k, uint32_t M,
-                                                             double inv_m, long long limit, unsigned long long *dkey,
-                                                             unsigned int *dcnt, unsigned long long *dfc,
-                                                             unsigned long long *dft, SubSlot *sub,
-                                                             unsigned int *nsolid, unsigned long long *ndistinct,
-                                                             unsigned int *overflow) {
-    constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
-    __shared__ LTabE<SLOTS> tab;
-    __shared__ unsigned int s_over[2];
-    __shared__ uint2 s_xy[BUCKET_THREADS], s_zw[BUCKET_THREADS];  // the chunk's records
-    __shared__ unsigned int s_ncnt[SK2_NMAX + 1];
-    const unsigned int b = blockIdx.x;
-    for (int i = threadIdx.x; i < SLOTS; i += blockDim.x) {
-        tab.key[i] = EMPTY_KEY;
-        tab.count[i] = 0;
-        tab.ev[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-    }
-    if (threadIdx.x == 0) s_over[0] = s_over[1] = 0;
-    __syncthreads();
-    const uint64_t r0 = bbeg[b], r1 = bend[b];
-    const uint64_t kmask = kmask64(k);
-    const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
-    const unsigned int m2 = 2 * M - 1;
-    // the record's read * 2M and first window in it, from p = read * M + window
-    auto decode = [&](unsigned int p, unsigned int &rd2, unsigned int &rem) {
-        const unsigned int rd = (unsigned int)((double)p * inv_m);  // p / M, corrected below
-        int rm = (int)(p - rd * M);
-        unsigned int read = rd;
-        if (rm < 0) read--, rm += (int)M;
-        else if (rm >= (int)M) read++, rm -= (int)M;
-        rd2 = read * (2 * M);
-        rem = (unsigned int)rm;
-    };
-    // events and add of window lf = rem + o given its fwd / rc codes; returns the canonical key
-    auto events = [&](uint64_t fwd, uint64_t rc, unsigned int lf, unsigned int rd2, unsigned int &eC,
-                      unsigned int &eT, unsigned int &add) {
-        const bool tw = fwd > rc;
-        unsigned int lC = tw ? m2 - lf : lf, lT = tw ? lf : m2 - lf;
-        add = 1;
-        if (EVEN_K && fwd == rc) {  // even-k palindrome: inserted twice at the forward event
-            add = 2;
-            lC = lT = lf;
-        }
-        eC = rd2 + lC;
-        eT = rd2 + lT;
-        return tw ? rc : fwd;
-    };
-    uint4 nx = make_uint4(0, 0, 0, 0);
-    if (r0 + threadIdx.x < r1) nx = recs[r0 + threadIdx.x];
-    for (uint64_t c0 = r0; c0 < r1; c0 += BUCKET_THREADS) {
-        const unsigned int nv = (unsigned int)min<uint64_t>(BUCKET_THREADS, r1 - c0);
-        const uint4 x = nx;
-        if (c0 + BUCKET_THREADS + threadIdx.x < r1) nx = recs[c0 + BUCKET_THREADS + threadIdx.x];  // next chunk
-        if (threadIdx.x <= SK2_NMAX) s_ncnt[threadIdx.x] = 0;
-        __syncthreads();
-        const unsigned int bin = threadIdx.x < nv ? SK2_NMAX - 1 - (x.z >> 28) : SK2_NMAX;  // most windows first
-        const unsigned int rk = atomicAdd(&s_ncnt[bin], 1u);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned int a = 0;
-            for (int q = 0; q <= SK2_NMAX; q++) {
-                const unsigned int v = s_ncnt[q];
-                s_ncnt[q] = a;
-                a += v;
-            }
-        }
-        __syncthreads();
-        s_xy[s_ncnt[bin] + rk] = make_uint2(x.x, x.y);
-        s_zw[s_ncnt[bin] + rk] = make_uint2(x.z, x.w);
-        __syncthreads();
-        const uint2 xy = s_xy[threadIdx.x], zw = s_zw[threadIdx.x];
-        const unsigned int n = threadIdx.x < nv ? (zw.x >> 28) + 1 : 0u;
-        unsigned int rd2, rem;
-        decode(zw.y, rd2, rem);
-        // two windows per step (o and o + h): their LDS probes and updates are in flight together
-        const unsigned int h = (n + 1) >> 1;
-        auto at = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // window o straight out of the bases
-            const uint32_t lo = __builtin_amdgcn_alignbit(xy.y, xy.x, 2 * o), hi = __builtin_amdgcn_alignbit(zw.x, xy.y, 2 * o);
-            const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
-            rv = ~P & kmask;
-            fw = rev2_64(P) >> fsh;
-        };
-        uint64_t fA, rA, fB, rB;
-        at(0, fA, rA);
-        at(h, fB, rB);
-        auto roll = [&](unsigned int o, uint64_t &fw, uint64_t &rv) {  // to window o from o - 1
-            const unsigned int tb = o + (unsigned int)k - 1;
-            const uint32_t wd = tb < 32 ? xy.y : zw.x;
-            const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
-            fw = ((fw << 2) | bb) & kmask;
-            rv = (rv >> 2) | ((uint64_t)(3u - bb) << sh);
-        };
-        for (unsigned int i = 0; i < h; i++) {
-            const unsigned int oB = i + h;
-            const bool bB = oB < n;
-            if (i) {
-                roll(i, fA, rA);
-                roll(oB, fB, rB);
-            }
-            unsigned int eCA, eTA, eCB, eTB, addA, addB;
-            const uint64_t cA = events(fA, rA, rem + i, rd2, eCA, eTA, addA);
-            const uint64_t cB = events(fB, rB, rem + oB, rd2, eCB, eTB, addB);
-            unsigned int sA = (sk_slot(cA) >> (32 - SBITS)) & (SLOTS - 1), sB = (sk_slot(cB) >> (32 - SBITS)) & (SLOTS - 1);
-            const unsigned long long kA = tab.key[sA], kB = tab.key[sB];
-            lds_locate2<SLOTS>(tab, s_over, cA, sA, kA, cB, sB, bB ? kB : cB);
-            atomicAdd(&tab.count[sA], addA);
-            if (bB) atomicAdd(&tab.count[sB], addB);
-            const uint2 vA = tab.ev[sA], vB = tab.ev[sB];
-            if (eCA < vA.x) atomicMin(&tab.ev[sA].x, eCA);
-            if (eTA < vA.y) atomicMin(&tab.ev[sA].y, eTA);
-            if (bB && eCB < vB.x) atomicMin(&tab.ev[sB].x, eCB);
-            if (bB && eTB < vB.y) atomicMin(&tab.ev[sB].y, eTB);
-        }
-        __syncthreads();
-    }
-    lds_table_finish<SLOTS, false, KeyId>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
-                                          overflow, KeyId(), EvExpand{2 * M});
-}
 
 // ---- bucket with the bucket's duplicate super-k-mers merged first (the default) -----------------
 // At ~150-fold coverage a bucket's records are mostly the same few super-k-mers read again and
@@ -667,8 +540,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
                                                              unsigned int *dcnt, unsigned long long *dfc,
                                                              unsigned long long *dft, SubSlot *sub,
                                                              unsigned int *nsolid, unsigned long long *ndistinct,
-                                                             unsigned int *overflow, unsigned long long *dbg,
-                                                             int exp) {
+                                                             unsigned int *overflow, unsigned long long *dbg) {
     constexpr int SBITS = SLOTS == 2048 ? 11 : 12;
     constexpr uint32_t PEND = 0x800u;  // tag word: the claimer has not yet stored the key
     // entries claimed at most: half the slots, and low enough that the claims a block can have in
@@ -822,7 +694,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_skbucket(const uint4 *recs, 
             const uint32_t a0 = __builtin_amdgcn_alignbit(y1, y0, s5), a1 = __builtin_amdgcn_alignbit(y2, y1, s5),
                            a2 = y2 >> s5;
             const uint32_t q0 = ~(lo ? a0 : a1), q1 = ~(lo ? a1 : a2) & m1, q2 = lo ? ~a2 & mw2 : 0u;
-            const bool flip = !(exp & 4) && (q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0);
+            const bool flip = q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0;
             // events of window 0: A = read 2M + first window, B = read 2M + 2M - 1 - first window
             const unsigned int p = x.w;
             const unsigned int rd0 = (unsigned int)((double)p * inv_m);  // p / M, corrected below
