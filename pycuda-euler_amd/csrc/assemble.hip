@@ -1748,9 +1748,42 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
     return finish_wide(s, cap, limit, U, sidx);
 }
 
-// Links of 128-bit keys by the (k-1)-mer half-edge join (join_w.h).  ok = false (succ and npal
-// left for the caller's k_neighbors / k_succ) when a level region or a join table overflowed.
-int links_join_w(ec_session *s, int k, unsigned int U, bool &ok) {
+// Links by the (k-1)-mer half-edge join (join_w.h), 128-bit (OpsW) or 64-bit (Ops64) keys.
+// ok = false (succ and npal left for the caller's k_neighbors / k_succ) when a level region or
+// a join table overflowed.
+template <typename Ops> struct JoinT;
+template <> struct JoinT<OpsW> {
+    using R = RecJ;
+    using S = StoreJ;
+    static void emit(const K128 *d, unsigned U, int k, const uint8_t *up, R *o, unsigned *ne, uint64_t cap, unsigned *ov,
+                     hipStream_t st) {
+        k_half_emit<<<grid_for(U, 256, 8192), 256, 0, st>>>(d, U, k, up, o, ne, cap, ov);
+    }
+    template <bool ODD>
+    static void join(unsigned nb, const R *r, const unsigned long long *bb, const unsigned long long *be,
+                     const uint8_t *up, unsigned *succ, unsigned *ov, hipStream_t st) {
+        k_half_join<2048, 512, ODD><<<nb, 512, 0, st>>>(r, bb, be, up, succ, ov);
+    }
+};
+template <> struct JoinT<Ops64> {
+    using R = RecJ64;
+    using S = StoreJ64;
+    static void emit(const unsigned long long *d, unsigned U, int k, const uint8_t *up, R *o, unsigned *ne, uint64_t cap,
+                     unsigned *ov, hipStream_t st) {
+        k_half_emit64<<<grid_for(U, 256, 8192), 256, 0, st>>>(d, U, k, up, o, ne, cap, ov);
+    }
+    template <bool ODD>
+    static void join(unsigned nb, const R *r, const unsigned long long *bb, const unsigned long long *be,
+                     const uint8_t *up, unsigned *succ, unsigned *ov, hipStream_t st) {
+        k_half_join64<2048, 512, ODD><<<nb, 512, 0, st>>>(r, bb, be, up, succ, ov);
+    }
+};
+
+template <typename Ops>
+int links_join(ec_session *s, int k, unsigned int U, bool &ok) {
+    using J = JoinT<Ops>;
+    using R = typename J::R;
+    using S = typename J::S;
     ok = false;
     hipStream_t st = s->stream;
     const unsigned B = 256;
@@ -1771,43 +1804,42 @@ int links_join_w(ec_session *s, int k, unsigned int U, bool &ok) {
         (l & 1 ? needA : needB) = std::max(l & 1 ? needA : needB, nb * fc[l]);
         nbmax = std::max(nbmax, nb);
     }
-    EC_CHECK(s->recs.ensure(needA * sizeof(RecJ)));
-    EC_CHECK(s->recs2.ensure(needB * sizeof(RecJ)));
+    EC_CHECK(s->recs.ensure(needA * sizeof(R)));
+    EC_CHECK(s->recs2.ensure(needB * sizeof(R)));
     EC_CHECK(s->bb2.ensure(2 * nbmax * 8));
     EC_CHECK(s->gcur.ensure(nbmax * 8));
     EC_CHECK(s->tmp.ensure(16));
     unsigned int *flags = s->tmp.as<unsigned int>();  // [0] extras, [1] overflow
     unsigned long long *ibeg = s->bb2.as<unsigned long long>(), *iend = ibeg + nbmax;
     EC_HIP(hipMemsetAsync(flags, 0, 8, st));
-    k_upal<OpsW><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<K128>(), U, k, s->upal.as<uint8_t>(), &dsc->npal);
-    RecJ *src = s->recs.as<RecJ>(), *dst = s->recs2.as<RecJ>();
-    k_half_emit<<<grid_for(U, B, 8192), B, 0, st>>>(s->dkey.as<K128>(), U, k, s->upal.as<uint8_t>(), src, &flags[0],
-                                                    extra_cap, &flags[1]);
+    const typename Ops::K *dkey = s->dkey.as<typename Ops::K>();
+    k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(dkey, U, k, s->upal.as<uint8_t>(), &dsc->npal);
+    R *src = s->recs.as<R>(), *dst = s->recs2.as<R>();
+    J::emit(dkey, U, k, s->upal.as<uint8_t>(), src, &flags[0], extra_cap, &flags[1], st);
     k_half_range<<<1, 1, 0, st>>>(&flags[0], N, extra_cap, ibeg, iend);
     int cb = 0;
     for (size_t l = 0; l < lv.size(); l++) {
         const uint64_t nc = 1ull << cb, nb = 1ull << (cb + lv[l]);
         k_cursor_init<<<grid_for(nb, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), nb, fc[l]);
         const unsigned rs = (unsigned)std::max<uint64_t>(1, 1024 / nc);
-        k_refine<RecJ, StoreJ, StoreJ><<<dim3((unsigned)nc, rs), BUCKET_THREADS, 0, st>>>(
-            StoreJ{src}, StoreJ{dst}, nullptr, s->gcur.as<unsigned long long>(), cb, cb + lv[l], fc[l], &flags[1], ibeg,
-            iend);
+        k_refine<R, S, S><<<dim3((unsigned)nc, rs), BUCKET_THREADS, 0, st>>>(
+            S{src}, S{dst}, nullptr, s->gcur.as<unsigned long long>(), cb, cb + lv[l], fc[l], &flags[1], ibeg, iend);
         k_level3_ends<<<grid_for(nb, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), nb, fc[l], ibeg, iend);
         std::swap(src, dst);
         cb += lv[l];
     }
     EC_HIP(hipMemsetAsync(s->succ.p, 0xFF, N * 4, st));
     if (k & 1)
-        k_half_join<2048, 512, true><<<(unsigned)(1ull << cb), 512, 0, st>>>(src, ibeg, iend, s->upal.as<uint8_t>(),
-                                                                            s->succ.as<unsigned int>(), &flags[1]);
+        J::template join<true>((unsigned)(1ull << cb), src, ibeg, iend, s->upal.as<uint8_t>(), s->succ.as<unsigned int>(),
+                               &flags[1], st);
     else
-        k_half_join<2048, 512, false><<<(unsigned)(1ull << cb), 512, 0, st>>>(src, ibeg, iend, s->upal.as<uint8_t>(),
-                                                                             s->succ.as<unsigned int>(), &flags[1]);
+        J::template join<false>((unsigned)(1ull << cb), src, ibeg, iend, s->upal.as<uint8_t>(),
+                                s->succ.as<unsigned int>(), &flags[1], st);
     unsigned int h[2];
     EC_HIP(hipMemcpyAsync(h, flags, 8, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     if (h[1]) {  // the caller recounts npal with k_neighbors
-        if (kn().verbose) fprintf(stderr, "links_join_w: overflow (U %u, %d bucket bits), probing instead\n", U, cb);
+        if (kn().verbose) fprintf(stderr, "links_join: overflow (U %u, %d bucket bits), probing instead\n", U, cb);
         EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
         return EC_OK;
     }
@@ -1837,10 +1869,16 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                  &dsc->npal);
         EC_HIP(hipMemcpyAsync(s->succ.p, ext_succ, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
     }
-    bool joined = false;  // links of 128-bit keys by the half-edge join (join_w.h): from ~2e6 keys on
-    if constexpr (std::is_same<Ops, OpsW>::value) {
-        if (U && !ext_succ && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
-            EC_CHECK(links_join_w(s, k, U, joined));
+    // links by the half-edge join (join_w.h) instead of neighbour probes: 128-bit keys from ~2e6
+    // keys on (their sub-tables have no locality); 64-bit keys only on the k-mer-hash indexes
+    // (the window-record counts) from ~4e6 keys -- the minimizer index's probes (super-k-mer
+    // count) stay in a bucket's sub-table and are cheaper than the join's random link writes
+    bool joined = false;
+    if (U && !ext_succ && k >= 8 && kn().join_links != 0) {
+        bool use = kn().join_links == 1;
+        if constexpr (std::is_same<Ops, OpsW>::value) use = use || U >= (1u << 21);
+        else use = use || (!sidx.sk && U >= (1u << 22));
+        if (use) EC_CHECK(links_join<Ops>(s, k, U, joined));
     }
     if (U && !ext_succ && !joined) {
         k_neighbors<Ops, Index><<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,

@@ -200,4 +200,134 @@ __global__ void __launch_bounds__(NT) k_half_join(const RecJ *recs, const unsign
     }
 }
 
+// ---- 64-bit keys (k <= 32): the same join on 16-B records --------------------------------------
+// For the window-record count paths (k-mer-hash sub-tables: no minimizer locality for the
+// neighbour probes) on large sets -- error-rich reads (1.3e7 solid keys), big genomes.
+struct alignas(8) RecJ64 {
+    unsigned long long key;  // canonical (k-1)-mer
+    unsigned int tag;        // oriented node id | side << 31
+    unsigned int pad;
+};
+static_assert(sizeof(RecJ64) == 16, "join record layout");
+__device__ inline unsigned int rec_bucket(const RecJ64 &r, int bbits) {
+    return (unsigned int)(mix64(r.key) >> 32) >> (32 - bbits);
+}
+struct StoreJ64 {
+    RecJ64 *p;
+    __device__ inline RecJ64 load(uint64_t i) const { return p[i]; }
+    __device__ inline void store(uint64_t i, const RecJ64 &r) const { p[i] = r; }
+};
+__device__ inline RecJ64 make_recj64(unsigned long long o, unsigned int node, unsigned int side) {
+    RecJ64 r;
+    r.key = o;
+    r.tag = node | (side << 31);
+    r.pad = 0;
+    return r;
+}
+
+__global__ void __launch_bounds__(256) k_half_emit64(const unsigned long long *dkey, unsigned int U, int k,
+                                                     const uint8_t *upal, RecJ64 *out, unsigned int *nextra,
+                                                     uint64_t extra_cap, unsigned int *over) {
+    const int j = k - 1;
+    const unsigned long long mj = kmask64(j);
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < U; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        const bool valid = t < U;
+        bool e1 = false, e2 = false;
+        RecJ64 x1{}, x2{};
+        if (valid) {
+            const unsigned long long c = dkey[t];
+            const unsigned int ic = 2u * (unsigned int)t, itc = upal[t] ? ic : ic + 1u;
+            const unsigned long long s = c & mj, p = c >> 2;
+            const unsigned long long ts = twin64(s, j), tp = twin64(p, j);
+            out[2 * t] = s < ts ? make_recj64(s, ic, 0) : make_recj64(ts, itc, 1);
+            out[2 * t + 1] = p < tp ? make_recj64(p, ic, 1) : make_recj64(tp, itc, 0);
+            e1 = s == ts;
+            e2 = p == tp;
+            if (e1) x1 = make_recj64(s, ic, 0);
+            if (e2) x2 = make_recj64(p, ic, 1);
+        }
+        const unsigned int q1 = wave_append(nextra, e1);
+        if (e1) {
+            if (q1 < extra_cap) out[2ull * U + q1] = x1;
+            else *over = 1u;
+        }
+        const unsigned int q2 = wave_append(nextra, e2);
+        if (e2) {
+            if (q2 < extra_cap) out[2ull * U + q2] = x2;
+            else *over = 1u;
+        }
+    }
+}
+
+// 16-B slots (key, one id word per side): 2048 slots in 32 KB
+template <int SLOTS, int NT, bool ODD_K>
+__global__ void __launch_bounds__(NT) k_half_join64(const RecJ64 *recs, const unsigned long long *bbeg,
+                                                    const unsigned long long *bend, const uint8_t *upal,
+                                                    unsigned int *succ, unsigned int *overflow) {
+    constexpr unsigned int MANY = 0x80000000u;
+    __shared__ unsigned long long kt[SLOTS];
+    __shared__ unsigned int ids[2][SLOTS];
+    __shared__ unsigned int s_over[2];
+    const unsigned int b = blockIdx.x;
+    for (int i = threadIdx.x; i < SLOTS; i += NT) {
+        kt[i] = EMPTY_KEY;  // (a (k-1)-mer of <= 62 bits never equals it)
+        ids[0][i] = NONE32;
+        ids[1][i] = NONE32;
+    }
+    if (threadIdx.x == 0) {
+        s_over[0] = 0;
+        s_over[1] = 0;
+    }
+    __syncthreads();
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    for (uint64_t base = r0; base < r1; base += NT) {
+        const uint64_t i = base + threadIdx.x;
+        const bool valid = i < r1;
+        RecJ64 r{};
+        if (valid) r = recs[i];
+        unsigned int slot = (unsigned int)(((uint64_t)(uint32_t)mix64(r.key) * SLOTS) >> 32);
+        unsigned long long cur = valid ? kt[slot] : 0ull;
+        bool miss = valid && cur != r.key;
+#pragma unroll 1
+        while (__any(miss)) {
+            if (miss) {
+                if (cur == EMPTY_KEY) {
+                    if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {
+                        s_over[0] = 1;
+                        cur = r.key;
+                    } else {
+                        cur = atomicCAS(&kt[slot], EMPTY_KEY, r.key);
+                        if (cur == EMPTY_KEY) cur = r.key;
+                        else atomicSub(&s_over[1], 1u);
+                    }
+                }
+                if (cur != r.key) {
+                    slot = slot + 1 == SLOTS ? 0u : slot + 1;
+                    cur = kt[slot];
+                }
+                miss = cur != r.key;
+            }
+        }
+        if (valid) {
+            const unsigned int side = r.tag >> 31, id = r.tag & 0x7FFFFFFFu;
+            const unsigned int old = atomicCAS(&ids[side][slot], NONE32, id);
+            if (old != NONE32 && (old & ~MANY) != id) atomicOr(&ids[side][slot], MANY);
+        }
+    }
+    __syncthreads();
+    if (s_over[0]) {
+        if (threadIdx.x == 0) atomicAdd(overflow, 1u);
+        return;
+    }
+    for (int i = threadIdx.x; i < SLOTS; i += NT) {
+        const unsigned int x = ids[0][i], y = ids[1][i];
+        if ((x | y) & MANY) continue;
+        const unsigned int tx = ODD_K ? x ^ 1u : twin_node(upal, x), ty = ODD_K ? y ^ 1u : twin_node(upal, y);
+        if (y == tx) continue;
+        succ[x] = y;
+        succ[ty] = tx;
+    }
+}
+
 }  // namespace ec

@@ -407,14 +407,32 @@ def test_wide_third_level_vs_oracle(gpu_session, monkeypatch, k, sbits):
     assert [[x, c] for x, c in res.dict_items] == ref["d"]
 
 
-@pytest.mark.parametrize("case", [c for c in CASES32 if c["k"] > 32], ids=lambda c: c["name"])
-def test_golden_wide_join_links(gpu_session, monkeypatch, case):
-    """k > 32 links by the (k-1)-mer half-edge join (join_w.h), forced at any size: golden
-    vectors of the imported reference"""
+@pytest.mark.parametrize("case", [c for c in CASES32 if c["k"] >= 8], ids=lambda c: c["name"])
+def test_golden_join_links(gpu_session, monkeypatch, case):
+    """links by the (k-1)-mer half-edge join (join_w.h; 64-bit records for k <= 32, 128-bit
+    above), forced at any size: golden vectors of the imported reference"""
     monkeypatch.setenv("EULERHIP_JOIN_LINKS", "1")
     res = gpu_session.assemble(case["reads"], case["k"], case["limit"], want_dict=True)
     assert [[x, c] for x, c in res.dict_items] == case["d"]
     assert res.contigs == case["contigs"] and res.links == case["links"]
+
+
+@pytest.mark.parametrize("k", [8, 15, 16, 21, 22, 31, 32])
+def test_join_links_vs_oracle(gpu_session, monkeypatch, k):
+    """64-bit half-edge join against the oracle on error-rich reads with N (the window-record
+    count paths it serves by default from 4e6 keys), both parities of k; and the probe path"""
+    buf, off = make_reads(60_000, 30_000, 100, 500 + k, err=0.006, n_rate=0.0005)
+    ref, rc, rl = _oracle_packed(buf, off, k, 1)
+    for mode in ("1", "0"):
+        monkeypatch.setenv("EULERHIP_JOIN_LINKS", mode)
+        gpu_session.run_host(buf, off, k, 1)
+        res = gpu_session.fetch(k)
+        assert res.contig_bytes == ref["contig_chars"] and res.links == rl, mode
+    monkeypatch.setenv("EULERHIP_JOIN_LINKS", "1")
+    reads = _low_complexity_reads(300, 140, 40 + k)
+    d, r, g = oracle.assemble(reads, k, 1)
+    res = gpu_session.assemble(reads, k, 1, want_dict=True)
+    assert [[x, c] for x, c in res.dict_items] == d and res.contigs == r and res.links == g
 
 
 @pytest.mark.parametrize("k", [33, 34, 40, 51, 62, 63])
