@@ -1749,8 +1749,8 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
 }
 
 // Links by the (k-1)-mer half-edge join (join_w.h), 128-bit (OpsW) or 64-bit (Ops64) keys.
-// ok = false (succ and npal left for the caller's k_neighbors / k_succ) when a level region or
-// a join table overflowed.
+// gate: a device flag set when a level region or a join table overflowed; the caller then
+// launches k_neighbors / k_succ gated on it (they return at once unless it is set).
 template <typename Ops> struct JoinT;
 template <> struct JoinT<OpsW> {
     using R = RecJ;
@@ -1780,7 +1780,7 @@ template <> struct JoinT<Ops64> {
 };
 
 template <typename Ops>
-int links_join(ec_session *s, int k, unsigned int U, bool &ok) {
+int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned int *&gate) {
     using J = JoinT<Ops>;
     using R = typename J::R;
     using S = typename J::S;
@@ -1800,7 +1800,7 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok) {
     for (size_t l = 0, cb = 0; l < lv.size(); l++) {
         cb += lv[l];
         const uint64_t nb = 1ull << cb, mean = N / nb;
-        fc[l] = mean + mean * 3 / 10 + 1024;
+        fc[l] = kn().join_cap > 0 ? (uint64_t)kn().join_cap : mean + mean * 3 / 10 + 1024;
         (l & 1 ? needA : needB) = std::max(l & 1 ? needA : needB, nb * fc[l]);
         nbmax = std::max(nbmax, nb);
     }
@@ -1835,14 +1835,9 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok) {
     else
         J::template join<false>((unsigned)(1ull << cb), src, ibeg, iend, s->upal.as<uint8_t>(),
                                 s->succ.as<unsigned int>(), &flags[1], st);
-    unsigned int h[2];
-    EC_HIP(hipMemcpyAsync(h, flags, 8, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
-    if (h[1]) {  // the caller recounts npal with k_neighbors
-        if (kn().verbose) fprintf(stderr, "links_join: overflow (U %u, %d bucket bits), probing instead\n", U, cb);
-        EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
-        return EC_OK;
-    }
+    // no host round trip: the caller's probe kernels run gated on flags[1] (a level region or a
+    // join table that overflowed) and then rewrite every successor
+    gate = &flags[1];
     ok = true;
     return EC_OK;
 }
@@ -1874,20 +1869,18 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     // (the window-record counts) from ~4e6 keys -- the minimizer index's probes (super-k-mer
     // count) stay in a bucket's sub-table and are cheaper than the join's random link writes
     bool joined = false;
-    if (U && !ext_succ && k >= 8 && kn().join_links != 0) {
-        bool use = kn().join_links == 1;
-        if constexpr (std::is_same<Ops, OpsW>::value) use = use || U >= (1u << 21);
-        else use = use || (!sidx.sk && U >= (1u << 22));
-        if (use) EC_CHECK(links_join<Ops>(s, k, U, joined));
-    }
-    if (U && !ext_succ && !joined) {
+    const unsigned int *gate = nullptr;
+    if (U && !ext_succ && k >= 8 && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
+        EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
+    if (U && !ext_succ) {  // (after a join: only if it overflowed, decided on the device)
         k_neighbors<Ops, Index><<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
-                                                 s->cand.as<unsigned int>(), &dsc->npal);
+                                                 s->cand.as<unsigned int>(), joined ? nullptr : &dsc->npal, gate);
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
         k_succ<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(),
                                             N, s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                            s->dft.as<unsigned long long>(), s->nrec.as<NodeRec>());
+                                            s->dft.as<unsigned long long>(), joined ? nullptr : s->nrec.as<NodeRec>(),
+                                            gate);
     }
     if (U) {
         // (with the first ruler pass's counts: k_rulers_count at it = 0 below is skipped)

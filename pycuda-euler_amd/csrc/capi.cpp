@@ -39,6 +39,7 @@ void refresh_knobs() {
         k.wide_max_bbits = num("EULERHIP_WIDE_MAX_BBITS", -1);
         k.wide_l3 = num("EULERHIP_WIDE_L3", 0);
         k.join_links = num("EULERHIP_JOIN_LINKS", -1);
+        k.join_cap = num("EULERHIP_JOIN_CAP", 0);
         if (const char *e = getenv("EULERHIP_WIDE_L3_CAP")) k.wide_l3_cap = atoll(e);
         k.host_chunks = num("EULERHIP_HOST_CHUNKS", 0);
         k.sk2_stats = flag("EULERHIP_SK2_STATS");

@@ -36,7 +36,8 @@ struct Knobs {
     int wide_max_bbits = -1;    // EULERHIP_WIDE_MAX_BBITS: cap the wide buckets (forces overflow)
     int wide_l3 = 0;            // EULERHIP_WIDE_L3: third partition level of 2^n sub-buckets at any size
     long long wide_l3_cap = 0;  // EULERHIP_WIDE_L3_CAP: its sub-bucket capacity (forces its overflow)
-    int join_links = -1;        // EULERHIP_JOIN_LINKS: k > 32 links by the half-edge join 1 = always, 0 = never
+    int join_links = -1;        // EULERHIP_JOIN_LINKS: links by the half-edge join 1 = always, 0 = never
+    int join_cap = 0;           // EULERHIP_JOIN_CAP: its level regions' capacity (forces the fallback)
     int host_chunks = 0;        // EULERHIP_HOST_CHUNKS: host-input chunks (0 = ~32 MiB each)
     bool sk2_stats = false;     // EULERHIP_SK2_STATS: k_skbucket dedup statistics on stderr
     int sk2_claim = 0;          // EULERHIP_SK2_CLAIM: k_skbucket3 record-table claim cap (tests: overflow list)

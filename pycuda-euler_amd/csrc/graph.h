@@ -153,9 +153,10 @@ __device__ inline unsigned int twin_node(const uint8_t *upal, unsigned int x) {
 template <typename Ops, typename Index>
 __global__ void __launch_bounds__(256) k_neighbors(Index idx, const typename Ops::K *dkey, unsigned int U, int k,
                                                    uint8_t *upal, uint8_t *outdeg, unsigned int *cand,
-                                                   unsigned int *npal) {
+                                                   unsigned int *npal, const unsigned int *gate = nullptr) {
     using K = typename Ops::K;
     const K mask = Ops::mask(k);
+    if (gate && *gate == 0) return;  // (gated: the fallback of the half-edge join, join_w.h)
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < 2ull * U; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         const K c = dkey[x >> 1];
@@ -169,7 +170,7 @@ __global__ void __launch_bounds__(256) k_neighbors(Index idx, const typename Ops
             }
         } else {
             upal[x >> 1] = pal ? 1 : 0;
-            if (pal) atomicAdd(npal, 1u);
+            if (pal && npal) atomicAdd(npal, 1u);
         }
         const K xs = (x & 1) ? tc : c, txs = (x & 1) ? c : tc;
         unsigned int n = 0, cd = NONE32;
@@ -207,7 +208,9 @@ struct alignas(16) NodeRec {
 // nrec != nullptr: also the ruler walk's node records (succ + first event, k_noderec's output)
 __global__ void __launch_bounds__(256) k_succ(const uint8_t *upal, const uint8_t *outdeg, const unsigned int *cand,
                                               unsigned int N, unsigned int *succ, const unsigned long long *dfc,
-                                              const unsigned long long *dft, NodeRec *nrec) {
+                                              const unsigned long long *dft, NodeRec *nrec,
+                                              const unsigned int *gate = nullptr) {
+    if (gate && *gate == 0) return;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         unsigned int s = NONE32;

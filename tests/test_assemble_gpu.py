@@ -417,6 +417,20 @@ def test_golden_join_links(gpu_session, monkeypatch, case):
     assert res.contigs == case["contigs"] and res.links == case["links"]
 
 
+@pytest.mark.parametrize("k", [31, 51])
+def test_join_links_overflow_falls_back(gpu_session, monkeypatch, k):
+    """a join level region past its capacity: the probe kernels, gated on the device-side flag,
+    rewrite every successor (no host round trip decides it)"""
+    monkeypatch.setenv("EULERHIP_JOIN_LINKS", "1")
+    monkeypatch.setenv("EULERHIP_JOIN_CAP", "64")
+    buf, off = make_reads(30_000, 10_000, 120, 800 + k, err=0.003)
+    ref, rc, rl = _oracle_packed(buf, off, k, 1, True)
+    gpu_session.run_host(buf, off, k, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(k, True)
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    assert [[x, c] for x, c in res.dict_items] == ref["d"] and res.stats.n_dict == ref["n_dict"]
+
+
 @pytest.mark.parametrize("k", [8, 15, 16, 21, 22, 31, 32])
 def test_join_links_vs_oracle(gpu_session, monkeypatch, k):
     """64-bit half-edge join against the oracle on error-rich reads with N (the window-record
