@@ -1883,11 +1883,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                             gate);
     }
     if (U) {
-        // (with the first ruler pass's counts: k_rulers_count at it = 0 below is skipped)
+        // (with the first ruler pass's counts: k_rulers_count at it = 0 below is skipped, and the
+        // node records when k_succ did not write them)
+        EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
         EC_CHECK(s->rbc.ensure(((Nn + RULER_CHUNK - 1) / RULER_CHUNK) * 8));
         k_pred_rc<<<(unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK), B, 0, st>>>(
             s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, 31u, s->pred.as<unsigned int>(),
-            s->rbc.as<unsigned int>());
+            s->rbc.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+            (ext_succ || joined) ? s->nrec.as<NodeRec>() : nullptr);
     }
     mark(s, 2 * EC_STAGE_LINKS + 1);
 
@@ -1909,9 +1912,6 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (U) {
         EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 8, st));
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
-        if (ext_succ || joined)  // (k_succ wrote the node records otherwise)
-            k_noderec<<<grid_for(N, B), B, 0, st>>>(s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                                   s->dft.as<unsigned long long>(), N, s->nrec.as<NodeRec>());
         unsigned int masks[4] = {31u, 7u, 1u, 0u};
         unsigned int r0 = 0;
         for (int it = 0; it < 4; it++) {

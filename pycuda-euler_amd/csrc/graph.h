@@ -198,14 +198,14 @@ __device__ inline unsigned long long first_event(const unsigned long long *dfc, 
     return (x & 1) ? dft[x >> 1] : dfc[x >> 1];
 }
 
-// A node's successor and first event side by side (k_noderec): the walk's random step then
+// A node's successor and first event side by side (k_succ / k_pred_rc): the walk's random step then
 // touches one line instead of three (succ, dfc / dft).
 struct alignas(16) NodeRec {
     unsigned int succ;
     unsigned int pad;
     unsigned long long fev;
 };
-// nrec != nullptr: also the ruler walk's node records (succ + first event, k_noderec's output)
+// nrec != nullptr: also the ruler walk's node records (succ + first event)
 __global__ void __launch_bounds__(256) k_succ(const uint8_t *upal, const uint8_t *outdeg, const unsigned int *cand,
                                               unsigned int N, unsigned int *succ, const unsigned long long *dfc,
                                               const unsigned long long *dft, NodeRec *nrec,
@@ -320,8 +320,11 @@ __device__ inline bool ruler_sel(const uint8_t *upal, const unsigned int *pred, 
 // pred(x) = twin(succ(twin(x))) (the links are closed under twin-reversal), fused with the
 // first ruler pass's counting (k_rulers_count with first = 1: every node's
 // rid is still NONE then): block b handles the RULER_CHUNK nodes of chunk b
+// nrec != nullptr: also the ruler walk's node records (when k_succ did not write them)
 __global__ void __launch_bounds__(256) k_pred_rc(const uint8_t *upal, const unsigned int *succ, unsigned int N,
-                                                 unsigned int smask, unsigned int *pred, unsigned int *bc) {
+                                                 unsigned int smask, unsigned int *pred, unsigned int *bc,
+                                                 const unsigned long long *dfc, const unsigned long long *dft,
+                                                 NodeRec *nrec) {
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
     unsigned int c = 0;
@@ -335,6 +338,13 @@ __global__ void __launch_bounds__(256) k_pred_rc(const uint8_t *upal, const unsi
         }
         pred[x] = p;
         c += !skip && (p == NONE32 || ruler_hash(x, smask));
+        if (nrec) {
+            NodeRec r;
+            r.succ = succ[x];
+            r.pad = 0;
+            r.fev = first_event(dfc, dft, x);
+            nrec[x] = r;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     __shared__ unsigned int w[4];
@@ -400,16 +410,6 @@ struct alignas(32) RJump {
 };
 static_assert(sizeof(RJump) == 32, "rjump layout");
 
-__global__ void __launch_bounds__(256) k_noderec(const unsigned int *succ, const unsigned long long *dfc,
-                                                 const unsigned long long *dft, unsigned int N, NodeRec *nrec) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
-        NodeRec r;
-        r.succ = succ[t];
-        r.pad = 0;
-        r.fev = first_event(dfc, dft, (unsigned int)t);
-        nrec[t] = r;
-    }
-}
 
 // Each ruler walks its segment up to the next ruler (a chain of dependent 16-B loads).
 __global__ void __launch_bounds__(256) k_walk(const NodeRec *nrec, const unsigned int *rlist,
