@@ -15,7 +15,7 @@ import re
 import sys
 
 KERNELS = ("k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine", "k_prescan", "k_partition", "k_refine2",
-           "k_skpart", "k_skrefine", "k_skbucket", "k_neighbors", "k_walk")
+           "k_skpart", "k_skrefine", "k_skbucket", "k_neighbors", "k_walk", "k_half_join64", "k_half_join", "k_half_emit64", "k_half_emit", "k_pred_rc")
 
 
 def short(name):
