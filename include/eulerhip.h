@@ -206,6 +206,11 @@ int ec_find_euler(const void *ev, uint64_t vcount, const uint32_t *l, const uint
 int ec_execute_swipe(const void *ev, uint64_t vcount, const uint32_t *e, void *ee, uint64_t E, const void *cg_edges,
                      uint64_t cg_edge_count, const uint32_t *tree, uint64_t tree_count, unsigned flags,
                      uint32_t *mark_out);
+/* T4 findSpanningTree (src/eulercuda.py:266-305): the spanning forest of the circuit graph
+ * (CircuitEdge[cg_edge_count], circuits 0..cg_vertex_count-1) that Kruskal takes in edge-index
+ * order, as ascending circuit-edge indices in tree[*tree_count] (capacity cg_edge_count) */
+int ec_spanning_forest(const void *cg_edges, uint64_t cg_edge_count, uint64_t cg_vertex_count, uint32_t *tree,
+                       uint64_t *tree_count);
 /* T6 identify_contig_start (src/pyeulertour.py:667-706): contig_start[ee[i].s] = 0 for s < E */
 int ec_identify_contig_start(const void *ee, uint64_t E, uint32_t *contig_start);
 

@@ -334,3 +334,25 @@ def partial_contigs(ev, ee, l):
         if visited[i] == 0:
             walk(i)
     return output
+
+
+def spanning_forest(cg, E, V):
+    """T4 findSpanningTree (src/eulercuda.py:266-305, graph_tool Kruskal with unit weights):
+    restated as Kruskal over the circuit edges in index order -- circuit-edge indices of the
+    forest, ascending (the module returns edge indices; parity unpinned: graph_tool's
+    tie-breaking among equal weights is unversioned)."""
+    parent = list(range(int(V)))
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    tree = []
+    for j in range(int(E)):
+        a, b = find(int(cg[j]["c1"])), find(int(cg[j]["c2"]))
+        if a != b:
+            parent[max(a, b)] = min(a, b)
+            tree.append(j)
+    return tree

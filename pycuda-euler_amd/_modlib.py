@@ -27,6 +27,7 @@ for name, res, args in [
     ("ec_find_euler", INT, [P, U64, P, P, P, U64, P, ctypes.POINTER(U64), ctypes.POINTER(U32)]),
     ("ec_execute_swipe", INT, [P, U64, P, P, U64, P, U64, P, U64, UINT, P]),
     ("ec_identify_contig_start", INT, [P, U64, P]),
+    ("ec_spanning_forest", INT, [P, U64, U64, P, ctypes.POINTER(U64)]),
     ("ec_assign_successor", INT, [P, U64, P, P, P, U64]),
     ("ec_db_counts", INT, [P, P, U64, U32, P, P, P, U32, U64, P, P]),
     ("ec_db_vertices", INT, [P, U64, P, P, P, U32, P, P, P, P, P]),

@@ -1873,14 +1873,16 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (U && !ext_succ && k >= 8 && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
         EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
     if (U && !ext_succ) {  // (after a join: only if it overflowed, decided on the device)
-        k_neighbors<Ops, Index><<<grid_for(N, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,
+        // gated: a small grid-stride grid, so the normal case (the gate closed) costs ~2 us a
+        // launch instead of one exiting block per 256 nodes
+        const unsigned gn = joined ? std::min(grid_for(N, B), 2048u) : grid_for(N, B);
+        k_neighbors<Ops, Index><<<gn, B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), U, k,
                                                  s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(),
                                                  s->cand.as<unsigned int>(), joined ? nullptr : &dsc->npal, gate);
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
-        k_succ<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(),
-                                            N, s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                            s->dft.as<unsigned long long>(), joined ? nullptr : s->nrec.as<NodeRec>(),
-                                            gate);
+        k_succ<<<gn, B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(), N,
+                                s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                s->dft.as<unsigned long long>(), joined ? nullptr : s->nrec.as<NodeRec>(), gate);
     }
     if (U) {
         // (with the first ruler pass's counts: k_rulers_count at it = 0 below is skipped, and the

@@ -957,6 +957,94 @@ int ec_identify_contig_start(const void *ee, uint64_t E, uint32_t *contig_start)
     return EC_OK;
 }
 
+// ---- T4 findSpanningTree (src/eulercuda.py:266-305) -----------------------------------------
+// The reference asks graph_tool for a minimum spanning tree of the circuit graph with unit
+// weights (Kruskal); the result here is the forest Kruskal takes in edge-index order, i.e. the
+// minimum spanning forest for weights = edge index -- unique, since those weights are distinct,
+// so Boruvka rounds find it in parallel: every component picks its lowest-index outgoing edge,
+// components hook along them (of a mutual pick, the larger root hooks to the smaller), then
+// every vertex chases its new root.  Each round at least halves the components.
+__global__ void __launch_bounds__(256) k_sf_best(const CircuitEdge *cg, uint64_t E, const unsigned int *comp,
+                                                 unsigned int *best, unsigned int *any) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < E; j += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int a = comp[cg[j].c1], b = comp[cg[j].c2];
+        if (a != b) {
+            atomicMin(&best[a], (unsigned int)j);
+            atomicMin(&best[b], (unsigned int)j);
+            *any = 1u;
+        }
+    }
+}
+__global__ void __launch_bounds__(256) k_sf_hook(const CircuitEdge *cg, uint64_t n, const unsigned int *comp,
+                                                 const unsigned int *best, unsigned int *nxt, uint8_t *intree) {
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+        nxt[r] = comp[r];
+        if (comp[r] != r || best[r] == NONE32) continue;
+        const unsigned int j = best[r];
+        const unsigned int a = comp[cg[j].c1], b = comp[cg[j].c2];
+        const unsigned int o = a == (unsigned int)r ? b : a;
+        intree[j] = 1;
+        if (best[o] == j && o > (unsigned int)r) continue;  // mutual pick: the larger root hooks
+        nxt[r] = o;
+    }
+}
+__global__ void __launch_bounds__(256) k_sf_chase(uint64_t n, const unsigned int *nxt, unsigned int *comp,
+                                                  unsigned int *best) {
+    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned int r = nxt[v];
+        for (uint64_t it = 0; nxt[r] != r && it < n; it++) r = nxt[r];  // (hooks form trees: bounded)
+        comp[v] = r;
+        best[v] = NONE32;
+    }
+}
+
+int ec_spanning_forest(const void *cg_edges, uint64_t cg_edge_count, uint64_t cg_vertex_count, uint32_t *tree,
+                       uint64_t *tree_count) {
+    if (!tree_count || (cg_edge_count && (!cg_edges || !tree))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    *tree_count = 0;
+    const uint64_t E = cg_edge_count, n = cg_vertex_count;
+    if (!E || !n) return EC_OK;
+    const CircuitEdge *h = static_cast<const CircuitEdge *>(cg_edges);
+    for (uint64_t j = 0; j < E; j++)
+        if (h[j].c1 >= n || h[j].c2 >= n) {
+            set_error("circuit edge %llu joins circuit %u / %u of %llu", (unsigned long long)j, h[j].c1, h[j].c2,
+                      (unsigned long long)n);
+            return EC_ERR_ARG;
+        }
+    EC_DEV(dcg, E * sizeof(CircuitEdge));
+    EC_DEV(dcomp, n * 4);
+    EC_DEV(dnxt, n * 4);
+    EC_DEV(dbest, n * 4);
+    EC_DEV(din, E);
+    EC_DEV(dany, 4);
+    EC_HIP(hipMemcpy(dcg.p, cg_edges, E * sizeof(CircuitEdge), hipMemcpyHostToDevice));
+    EC_HIP(hipMemset(din.p, 0, E));
+    EC_HIP(hipMemset(dbest.p, 0xFF, n * 4));
+    k_iota<<<grid_for(n, 256), 256>>>(dcomp.as<unsigned int>(), n);
+    for (int round = 0; round < 64; round++) {  // (<= log2(n) rounds)
+        EC_HIP(hipMemset(dany.p, 0, 4));
+        k_sf_best<<<grid_for(E, 256), 256>>>(dcg.as<CircuitEdge>(), E, dcomp.as<unsigned int>(),
+                                             dbest.as<unsigned int>(), dany.as<unsigned int>());
+        unsigned int any = 0;
+        EC_HIP(hipMemcpy(&any, dany.p, 4, hipMemcpyDeviceToHost));
+        if (!any) break;
+        k_sf_hook<<<grid_for(n, 256), 256>>>(dcg.as<CircuitEdge>(), n, dcomp.as<unsigned int>(),
+                                             dbest.as<unsigned int>(), dnxt.as<unsigned int>(), din.as<uint8_t>());
+        k_sf_chase<<<grid_for(n, 256), 256>>>(n, dnxt.as<unsigned int>(), dcomp.as<unsigned int>(),
+                                              dbest.as<unsigned int>());
+    }
+    std::vector<uint8_t> in(E);
+    EC_HIP(hipMemcpy(in.data(), din.p, E, hipMemcpyDeviceToHost));
+    uint64_t c = 0;
+    for (uint64_t j = 0; j < E; j++)
+        if (in[j]) tree[c++] = (uint32_t)j;
+    *tree_count = c;
+    return EC_OK;
+}
+
 
 // ---- step-level drop-ins (the reference's intermediate module functions) ---------------------
 // phase1_device (src/pygpuhash.py:18-73): per-key offset within its bucket + bucket sizes

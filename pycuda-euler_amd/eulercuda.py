@@ -146,24 +146,16 @@ def constructDebruijnGraph(readBuffer, partitionReadCount, readLength, lmerLengt
 
 def findSpanningTree(cg_edge, cg_edgecount, cg_vertexcount):
     """src/eulercuda.py:266-305: a spanning forest of the circuit graph (unit weights, Kruskal in
-    the (c1, c2)-sorted edge order).  Returns circuit-graph EDGE indices -- what
+    the (c1, c2)-sorted edge order), on the device (ec_spanning_forest: Boruvka rounds that find
+    the forest Kruskal takes in edge-index order).  Returns circuit-graph EDGE indices -- what
     markSpanningEulerEdges indexes with (the reference returned vertex pairs).
     The reference's graph_tool tie-breaking is unversioned: parity unpinned."""
-    parent = list(range(int(cg_vertexcount)))
-
-    def find(x):
-        while parent[x] != x:
-            parent[x] = parent[parent[x]]
-            x = parent[x]
-        return x
-
-    tree = []
-    for j in range(int(cg_edgecount)):
-        a, b = find(int(cg_edge[j]["c1"])), find(int(cg_edge[j]["c2"]))
-        if a != b:
-            parent[max(a, b)] = min(a, b)
-            tree.append(j)
-    return np.array(tree, dtype=np.uint32)
+    E = int(cg_edgecount)
+    cg = M.as_struct(np.asarray(cg_edge)[:E], M.CE) if E else np.zeros(0, M.CE)
+    tree = np.zeros(max(E, 1), np.uint32)
+    nt = ctypes.c_uint64(0)
+    M.call("ec_spanning_forest", M.ptr(cg), E, int(cg_vertexcount), M.ptr(tree), ctypes.byref(nt))
+    return tree[: nt.value].copy()
 
 
 def partial_contigs_device(d_ev, vcount, d_ee, ecount, l):

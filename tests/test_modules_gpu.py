@@ -207,3 +207,27 @@ def test_components_random(mods):
                 v[s[i]]["n2"] = i
         D = cc.find_component_device(v, np.zeros(n, np.uint32), n)
         assert np.array_equal(D, R.components(v))
+
+
+def test_spanning_forest_vs_kruskal():
+    """T4 on the device (ec_spanning_forest, Boruvka) = Kruskal in edge-index order (the
+    restatement of src/eulercuda.py:266-305): the KAT forest, random multigraphs with self-loops
+    and isolated circuits, a long path (many rounds), empty input"""
+    import eulercuda
+
+    cg = np.zeros(6, R.CE)
+    cg["c1"] = [0, 0, 1, 2, 3, 3]
+    cg["c2"] = [1, 2, 2, 3, 4, 4]
+    assert eulercuda.findSpanningTree(cg, 6, 6).tolist() == [0, 1, 3, 4]
+    rng = np.random.default_rng(4)
+    for V, E in [(10, 30), (1000, 800), (1000, 5000), (50_000, 120_000), (3, 0)]:
+        cg = np.zeros(E, R.CE)
+        cg["c1"] = rng.integers(0, V, E)
+        cg["c2"] = rng.integers(0, V, E)
+        cg["ceid"] = np.arange(E)
+        assert eulercuda.findSpanningTree(cg, E, V).tolist() == R.spanning_forest(cg, E, V), (V, E)
+    V = 20_000  # a path given in reverse: every round merges pairs only
+    cg = np.zeros(V - 1, R.CE)
+    cg["c1"] = np.arange(V - 1)[::-1]
+    cg["c2"] = np.arange(1, V)[::-1]
+    assert eulercuda.findSpanningTree(cg, V - 1, V).tolist() == list(range(V - 1))
