@@ -1973,14 +1973,17 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     {
         const unsigned int nblk = (unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK);
         unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk;
+        // the start bits between the two passes live in `cand` (free after the links)
+        EC_CHECK(s->cand.ensure(std::max<size_t>(Nn * 4, (Nn / 64 + 8) * 8)));
+        unsigned long long *smask = s->cand.as<unsigned long long>();
         k_starts_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
                                            s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
-                                           s->PM.as<unsigned long long>(), N, bc);
+                                           s->PM.as<unsigned long long>(), N, bc, smask);
         EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
         k_starts_write<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
                                            s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
-                                           s->PM.as<unsigned long long>(), N, bs, s->skeys.as<unsigned long long>(),
-                                           s->svals.as<unsigned int>());
+                                           s->PM.as<unsigned long long>(), N, bs, smask,
+                                           s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>());
         EC_HIP(hipMemcpyAsync(&dsc->nstarts, bs + nblk - 1, 4, hipMemcpyDeviceToDevice, st));
     }
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));  // nstarts, active[]

@@ -581,13 +581,20 @@ __device__ inline bool is_start(const uint8_t *upal, const unsigned long long *d
 // ~88 atomics / us -- 4.6 ms for the 1.1 M contigs of reads with 0.5 % errors).
 __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const unsigned long long *dfc,
                                                       const unsigned long long *dft, const unsigned int *PK,
-                                                      const unsigned long long *PM, unsigned int N, unsigned int *bc) {
+                                                      const unsigned long long *PM, unsigned int N, unsigned int *bc,
+                                                      unsigned long long *smask) {
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
     unsigned int c = 0;
-    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+    // one bit per node (a wave's 64 consecutive nodes per word): k_starts_write reads the
+    // decisions instead of repeating the path-minimum gathers
+    for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
+        const uint64_t t = t0 + threadIdx.x;
         unsigned long long f;
-        c += is_start(upal, dfc, dft, PK, PM, (unsigned int)t, f);
+        const bool sel = t < c1 && is_start(upal, dfc, dft, PK, PM, (unsigned int)t, f);
+        const unsigned long long m = __ballot(sel);
+        if ((threadIdx.x & 63) == 0 && t < c1) smask[t >> 6] = m;
+        c += sel;
     }
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     __shared__ unsigned int w[4];
@@ -600,8 +607,8 @@ __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const
 __global__ void __launch_bounds__(256) k_starts_write(const uint8_t *upal, const unsigned long long *dfc,
                                                       const unsigned long long *dft, const unsigned int *PK,
                                                       const unsigned long long *PM, unsigned int N,
-                                                      const unsigned int *bs, unsigned long long *skeys,
-                                                      unsigned int *svals) {
+                                                      const unsigned int *bs, const unsigned long long *smask,
+                                                      unsigned long long *skeys, unsigned int *svals) {
     __shared__ unsigned int wsum[4];
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
@@ -609,9 +616,9 @@ __global__ void __launch_bounds__(256) k_starts_write(const uint8_t *upal, const
     const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
         const uint64_t t = t0 + threadIdx.x;
-        unsigned long long f = 0;
-        const bool sel = t < c1 && is_start(upal, dfc, dft, PK, PM, (unsigned int)t, f);
-        const unsigned long long m = __ballot(sel);
+        const unsigned long long m = t0 < c1 ? smask[t0 >> 6 | (threadIdx.x >> 6)] : 0ull;  // (wave-uniform)
+        const bool sel = t < c1 && ((m >> lane) & 1ull);
+        const unsigned long long f = sel ? first_event(dfc, dft, (unsigned int)t) : 0ull;
         if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
         __syncthreads();
         unsigned int off = base;
