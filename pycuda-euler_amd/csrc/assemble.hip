@@ -1755,9 +1755,9 @@ template <typename Ops> struct JoinT;
 template <> struct JoinT<OpsW> {
     using R = RecJ;
     using S = StoreJ;
-    static void emit(const K128 *d, unsigned U, int k, const uint8_t *up, R *o, unsigned *ne, uint64_t cap, unsigned *ov,
-                     hipStream_t st) {
-        k_half_emit<<<grid_for(U, 256, 8192), 256, 0, st>>>(d, U, k, up, o, ne, cap, ov);
+    static void emit_l1(const K128 *d, unsigned U, int k, const uint8_t *up, int lb, uint64_t fc, unsigned long long *gc,
+                        R *o, unsigned *ov, hipStream_t st) {
+        k_half_emit_l1<K128, R><<<grid_for(U, 1024, 2048), 1024, 0, st>>>(d, U, k, up, lb, fc, gc, o, ov);
     }
     template <bool ODD>
     static void join(unsigned nb, const R *r, const unsigned long long *bb, const unsigned long long *be,
@@ -1768,9 +1768,9 @@ template <> struct JoinT<OpsW> {
 template <> struct JoinT<Ops64> {
     using R = RecJ64;
     using S = StoreJ64;
-    static void emit(const unsigned long long *d, unsigned U, int k, const uint8_t *up, R *o, unsigned *ne, uint64_t cap,
-                     unsigned *ov, hipStream_t st) {
-        k_half_emit64<<<grid_for(U, 256, 8192), 256, 0, st>>>(d, U, k, up, o, ne, cap, ov);
+    static void emit_l1(const unsigned long long *d, unsigned U, int k, const uint8_t *up, int lb, uint64_t fc,
+                        unsigned long long *gc, R *o, unsigned *ov, hipStream_t st) {
+        k_half_emit_l1<unsigned long long, R><<<grid_for(U, 1024, 2048), 1024, 0, st>>>(d, U, k, up, lb, fc, gc, o, ov);
     }
     template <bool ODD>
     static void join(unsigned nb, const R *r, const unsigned long long *bb, const unsigned long long *be,
@@ -1794,8 +1794,7 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
     while ((double)U / (double)(1ull << bt) > 900.0) bt++;
     std::vector<int> lv;
     for (int rem = bt; rem > 0; rem -= std::min(8, rem)) lv.push_back(std::min(8, rem));
-    const uint64_t extra_cap = U;  // palindromic (k-1)-mers' second records
-    uint64_t needA = N + extra_cap, needB = 0, nbmax = 1;
+    uint64_t needA = 0, needB = 0, nbmax = 1;
     std::vector<uint64_t> fc(lv.size());
     for (size_t l = 0, cb = 0; l < lv.size(); l++) {
         cb += lv[l];
@@ -1815,10 +1814,14 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
     const typename Ops::K *dkey = s->dkey.as<typename Ops::K>();
     k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(dkey, U, k, s->upal.as<uint8_t>(), &dsc->npal);
     R *src = s->recs.as<R>(), *dst = s->recs2.as<R>();
-    J::emit(dkey, U, k, s->upal.as<uint8_t>(), src, &flags[0], extra_cap, &flags[1], st);
-    k_half_range<<<1, 1, 0, st>>>(&flags[0], N, extra_cap, ibeg, iend);
-    int cb = 0;
-    for (size_t l = 0; l < lv.size(); l++) {
+    // level 0 fused with the emit (k_half_emit_l1), its regions in dst
+    const uint64_t nb0 = 1ull << lv[0];
+    k_cursor_init<<<grid_for(nb0, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), nb0, fc[0]);
+    J::emit_l1(dkey, U, k, s->upal.as<uint8_t>(), lv[0], fc[0], s->gcur.as<unsigned long long>(), dst, &flags[1], st);
+    k_level3_ends<<<grid_for(nb0, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), nb0, fc[0], ibeg, iend);
+    std::swap(src, dst);
+    int cb = lv[0];
+    for (size_t l = 1; l < lv.size(); l++) {
         const uint64_t nc = 1ull << cb, nb = 1ull << (cb + lv[l]);
         k_cursor_init<<<grid_for(nb, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), nb, fc[l]);
         const unsigned rs = (unsigned)std::max<uint64_t>(1, 1024 / nc);
@@ -1855,7 +1858,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     // ---- links ----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_LINKS);
     EC_CHECK(s->upal.ensure(std::max<size_t>(U, 1)));
-    EC_CHECK(s->outdeg.ensure(Nn));
+    EC_CHECK(s->outdeg.ensure(std::max<size_t>(Nn, (Nn / 64 + 8) * 8)));  // (later: k_pred_rc's ruler bits)
     EC_CHECK(s->cand.ensure(Nn * 4));
     EC_CHECK(s->succ.ensure(Nn * 4));
     EC_CHECK(s->pred.ensure(Nn * 4));
@@ -1892,7 +1895,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_pred_rc<<<(unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK), B, 0, st>>>(
             s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, 31u, s->pred.as<unsigned int>(),
             s->rbc.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-            (ext_succ || joined) ? s->nrec.as<NodeRec>() : nullptr);
+            (ext_succ || joined) ? s->nrec.as<NodeRec>() : nullptr, s->outdeg.as<unsigned long long>());
     }
     mark(s, 2 * EC_STAGE_LINKS + 1);
 
@@ -1924,7 +1927,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
             k_rulers<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->pred.as<unsigned int>(), N, masks[it], it == 0,
                                          s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<uint2>(),
-                                         s->rlist.as<unsigned int>());
+                                         s->rlist.as<unsigned int>(),
+                                         it == 0 ? s->outdeg.as<unsigned long long>() : nullptr);
             k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
             k_walk<<<2048, B, 0, st>>>(s->nrec.as<NodeRec>(), s->rlist.as<unsigned int>(), r0, &dsc->nr,
                                       masks[it], s->rid.as<uint2>(),

@@ -324,21 +324,28 @@ __device__ inline bool ruler_sel(const uint8_t *upal, const unsigned int *pred, 
 __global__ void __launch_bounds__(256) k_pred_rc(const uint8_t *upal, const unsigned int *succ, unsigned int N,
                                                  unsigned int smask, unsigned int *pred, unsigned int *bc,
                                                  const unsigned long long *dfc, const unsigned long long *dft,
-                                                 NodeRec *nrec) {
+                                                 NodeRec *nrec, unsigned long long *rbits) {
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
     unsigned int c = 0;
-    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+    // the first pass's ruler decisions, one bit per node (a wave's 64 consecutive nodes a word),
+    // for k_rulers to read instead of re-deriving them from upal / pred / rid
+    for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
+        const uint64_t t = t0 + threadIdx.x;
+        const bool valid = t < c1;
         const unsigned int x = (unsigned int)t;
         unsigned int p = NONE32;
-        const bool skip = (x & 1) && upal[x >> 1];
+        const bool skip = !valid || ((x & 1) && upal[x >> 1]);
         if (!skip) {
             const unsigned int sx = succ[twin_node(upal, x)];
             if (sx != NONE32) p = twin_node(upal, sx);
         }
-        pred[x] = p;
-        c += !skip && (p == NONE32 || ruler_hash(x, smask));
-        if (nrec) {
+        if (valid) pred[x] = p;
+        const bool rul = !skip && (p == NONE32 || ruler_hash(x, smask));
+        const unsigned long long m = __ballot(rul);
+        if ((threadIdx.x & 63) == 0 && valid) rbits[t >> 6] = m;
+        c += rul;
+        if (nrec && valid) {
             NodeRec r;
             r.succ = succ[x];
             r.pad = 0;
@@ -371,7 +378,7 @@ __global__ void __launch_bounds__(256) k_rulers_count(const uint8_t *upal, const
 __global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsigned int *pred, unsigned int N,
                                                 unsigned int smask, int first, const unsigned int *bs,
                                                 const unsigned int *nr, uint2 *rid,
-                                                unsigned int *rlist) {
+                                                unsigned int *rlist, const unsigned long long *rbits) {
     __shared__ unsigned int wsum[4];
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
@@ -379,7 +386,11 @@ __global__ void __launch_bounds__(256) k_rulers(const uint8_t *upal, const unsig
     const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
         const uint64_t t = t0 + threadIdx.x;
-        const bool sel = t < c1 && ruler_sel(upal, pred, rid, (unsigned int)t, smask, first);
+        bool sel;
+        if (rbits)  // (first pass: k_pred_rc's bits; a wave-uniform word)
+            sel = t < c1 && ((rbits[(t0 >> 6) + wid] >> lane) & 1ull);
+        else
+            sel = t < c1 && ruler_sel(upal, pred, rid, (unsigned int)t, smask, first);
         const unsigned long long m = __ballot(sel);
         if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
         __syncthreads();

@@ -11,12 +11,13 @@
 // symmetry: A(twin o) = twin(B(o)), B(twin o) = twin(A(o)), so one group per canonical (k-1)-mer
 // o^ holds both, and a link x -> y found there also gives twin(y) -> twin(x).
 //
-//   k_half_emit  per canonical key c (node 2u, twin node 2u+1): two records -- c's suffix s
+//   k_half_emit_l1  per canonical key c (node 2u, twin node 2u+1): two records -- c's suffix s
 //                (s < twin s: (s, A, c); else (twin s, B, twin c)) and prefix p (p < twin p:
 //                (p, B, c); else (twin p, A, twin c)); a palindromic (k-1)-mer is both its own
-//                twin and canonical, so it gets both records (appended after the 2U)
-//   k_refine     2-3 levels of <= 256-way LDS bucket sorts into fixed-capacity regions (the
-//                count's refine kernel, fcap mode), by the top bits of mix128(o^)
+//                twin and canonical, so it gets both records -- sorted in LDS straight into the
+//                first level's fixed-capacity regions by the top bits of the junction's hash
+//   k_refine     1-2 more levels of <= 256-way LDS bucket sorts (the count's refine kernel, fcap
+//                mode)
 //   k_half_join  per final bucket: an LDS table keyed by o^ collects the distinct node ids of
 //                each side (a second distinct id marks the side "many"); every group with one
 //                id on each side and y != twin(x) writes succ[x] = y and succ[twin y] = twin x
@@ -60,50 +61,6 @@ __device__ inline RecJ make_recj(const K128 &o, unsigned int node, unsigned int 
     return r;
 }
 
-// records 2u (suffix) and 2u + 1 (prefix) of key u; palindromic (k-1)-mers' second records
-// appended at 2U + wave_append(nextra) (at most extra_cap of them, else *over)
-__global__ void __launch_bounds__(256) k_half_emit(const K128 *dkey, unsigned int U, int k, const uint8_t *upal,
-                                                   RecJ *out, unsigned int *nextra, uint64_t extra_cap,
-                                                   unsigned int *over) {
-    const int j = k - 1;
-    const K128 mj = kmask128(j);
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < U; base += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t t = base + threadIdx.x;
-        const bool valid = t < U;  // (every lane stays in the loop: wave_append is convergent)
-        bool e1 = false, e2 = false;
-        RecJ x1{}, x2{};
-        if (valid) {
-            const K128 c = dkey[t];
-            const unsigned int ic = 2u * (unsigned int)t, itc = upal[t] ? ic : ic + 1u;
-            const K128 s{c.lo & mj.lo, c.hi & mj.hi};
-            const K128 p{(c.lo >> 2) | (c.hi << 62), c.hi >> 2};
-            const K128 ts = twin_j(s, j), tp = twin_j(p, j);
-            out[2 * t] = s < ts ? make_recj(s, ic, 0) : make_recj(ts, itc, 1);
-            out[2 * t + 1] = p < tp ? make_recj(p, ic, 1) : make_recj(tp, itc, 0);
-            e1 = s == ts;  // (s, B, twin c) above; also (s, A, c)
-            e2 = p == tp;  // (p, A, twin c) above; also (p, B, c)
-            if (e1) x1 = make_recj(s, ic, 0);
-            if (e2) x2 = make_recj(p, ic, 1);
-        }
-        const unsigned int q1 = wave_append(nextra, e1);
-        if (e1) {
-            if (q1 < extra_cap) out[2ull * U + q1] = x1;
-            else *over = 1u;
-        }
-        const unsigned int q2 = wave_append(nextra, e2);
-        if (e2) {
-            if (q2 < extra_cap) out[2ull * U + q2] = x2;
-            else *over = 1u;
-        }
-    }
-}
-
-// level-1 input range [0, 2U + extras) and cursors d * fcap
-__global__ void k_half_range(const unsigned int *nextra, uint64_t n2, uint64_t extra_cap, unsigned long long *ibeg,
-                             unsigned long long *iend) {
-    ibeg[0] = 0;
-    iend[0] = n2 + min((uint64_t)*nextra, extra_cap);
-}
 __global__ void __launch_bounds__(256) k_cursor_init(unsigned long long *gcur, uint64_t nb, uint64_t fcap) {
     for (uint64_t d = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; d < nb; d += (uint64_t)gridDim.x * blockDim.x)
         gcur[d] = d * fcap;
@@ -225,41 +182,6 @@ __device__ inline RecJ64 make_recj64(unsigned long long o, unsigned int node, un
     return r;
 }
 
-__global__ void __launch_bounds__(256) k_half_emit64(const unsigned long long *dkey, unsigned int U, int k,
-                                                     const uint8_t *upal, RecJ64 *out, unsigned int *nextra,
-                                                     uint64_t extra_cap, unsigned int *over) {
-    const int j = k - 1;
-    const unsigned long long mj = kmask64(j);
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < U; base += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t t = base + threadIdx.x;
-        const bool valid = t < U;
-        bool e1 = false, e2 = false;
-        RecJ64 x1{}, x2{};
-        if (valid) {
-            const unsigned long long c = dkey[t];
-            const unsigned int ic = 2u * (unsigned int)t, itc = upal[t] ? ic : ic + 1u;
-            const unsigned long long s = c & mj, p = c >> 2;
-            const unsigned long long ts = twin64(s, j), tp = twin64(p, j);
-            out[2 * t] = s < ts ? make_recj64(s, ic, 0) : make_recj64(ts, itc, 1);
-            out[2 * t + 1] = p < tp ? make_recj64(p, ic, 1) : make_recj64(tp, itc, 0);
-            e1 = s == ts;
-            e2 = p == tp;
-            if (e1) x1 = make_recj64(s, ic, 0);
-            if (e2) x2 = make_recj64(p, ic, 1);
-        }
-        const unsigned int q1 = wave_append(nextra, e1);
-        if (e1) {
-            if (q1 < extra_cap) out[2ull * U + q1] = x1;
-            else *over = 1u;
-        }
-        const unsigned int q2 = wave_append(nextra, e2);
-        if (e2) {
-            if (q2 < extra_cap) out[2ull * U + q2] = x2;
-            else *over = 1u;
-        }
-    }
-}
-
 // 16-B slots (key, one id word per side): 2048 slots in 32 KB
 template <int SLOTS, int NT, bool ODD_K>
 __global__ void __launch_bounds__(NT) k_half_join64(const RecJ64 *recs, const unsigned long long *bbeg,
@@ -327,6 +249,121 @@ __global__ void __launch_bounds__(NT) k_half_join64(const RecJ64 *recs, const un
         if (y == tx) continue;
         succ[x] = y;
         succ[ty] = tx;
+    }
+}
+
+// ---- emit fused with the first level ----------------------------------------------------------
+// The junction records go straight into the 2^lb1 first-level regions: each workgroup sorts
+// its tile's records by region in LDS and stores them as runs reserved with one global atomic per
+// region and tile (k_refine's scheme), so the level-1 pass over all 2U records disappears.  The
+// rare second records of palindromic junctions take one global atomic each.
+__device__ inline void half_recs(const K128 &c, unsigned int t, int j, const K128 &mj, const uint8_t *upal, RecJ &r1,
+                                 RecJ &r2, bool &e1, bool &e2, RecJ &x1, RecJ &x2) {
+    const unsigned int ic = 2u * t, itc = upal[t] ? ic : ic + 1u;
+    const K128 s{c.lo & mj.lo, c.hi & mj.hi};
+    const K128 p{(c.lo >> 2) | (c.hi << 62), c.hi >> 2};
+    const K128 ts = twin_j(s, j), tp = twin_j(p, j);
+    r1 = s < ts ? make_recj(s, ic, 0) : make_recj(ts, itc, 1);
+    r2 = p < tp ? make_recj(p, ic, 1) : make_recj(tp, itc, 0);
+    e1 = s == ts;
+    e2 = p == tp;
+    x1 = make_recj(s, ic, 0);
+    x2 = make_recj(p, ic, 1);
+}
+__device__ inline void half_recs(unsigned long long c, unsigned int t, int j, unsigned long long mj,
+                                 const uint8_t *upal, RecJ64 &r1, RecJ64 &r2, bool &e1, bool &e2, RecJ64 &x1,
+                                 RecJ64 &x2) {
+    const unsigned int ic = 2u * t, itc = upal[t] ? ic : ic + 1u;
+    const unsigned long long s = c & mj, p = c >> 2;
+    const unsigned long long ts = twin64(s, j), tp = twin64(p, j);
+    r1 = s < ts ? make_recj64(s, ic, 0) : make_recj64(ts, itc, 1);
+    r2 = p < tp ? make_recj64(p, ic, 1) : make_recj64(tp, itc, 0);
+    e1 = s == ts;
+    e2 = p == tp;
+    x1 = make_recj64(s, ic, 0);
+    x2 = make_recj64(p, ic, 1);
+}
+__device__ inline K128 kmask_j(int j, K128 *) { return kmask128(j); }
+__device__ inline unsigned long long kmask_j(int j, unsigned long long *) { return kmask64(j); }
+
+template <typename K, typename R>
+__global__ void __launch_bounds__(1024) k_half_emit_l1(const K *dkey, unsigned int U, int k, const uint8_t *upal,
+                                                       int lb1, uint64_t fcap, unsigned long long *gcur, R *out,
+                                                       unsigned int *over) {
+    constexpr int NT = 1024, TILE = 2 * NT;
+    __shared__ R tile[TILE];
+    __shared__ uint8_t tj[TILE];
+    __shared__ unsigned long long base[256];
+    __shared__ unsigned int tcnt[256], tbeg[256], wsum[4];
+    const int j = k - 1;
+    const K mj = kmask_j(j, (K *)nullptr);
+    const unsigned int F = 1u << lb1;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * NT; t0 < U; t0 += (uint64_t)gridDim.x * NT) {
+        const uint64_t t = t0 + threadIdx.x;
+        const bool valid = t < U;
+        const unsigned int n = (unsigned int)min((uint64_t)NT, U - t0) * 2;
+        if (threadIdx.x < 256) tcnt[threadIdx.x] = 0;
+        __syncthreads();
+        R r1{}, r2{}, x1{}, x2{};
+        bool e1 = false, e2 = false;
+        unsigned int j1 = 0, j2 = 0, k1 = 0, k2 = 0;
+        if (valid) {
+            half_recs(dkey[t], (unsigned int)t, j, mj, upal, r1, r2, e1, e2, x1, x2);
+            j1 = rec_bucket(r1, lb1);
+            j2 = rec_bucket(r2, lb1);
+            k1 = atomicAdd(&tcnt[j1], 1u);
+            k2 = atomicAdd(&tcnt[j2], 1u);
+            if (e1) {  // (palindromic junctions: rare) one global atomic each
+                const unsigned int jx = rec_bucket(x1, lb1);
+                const unsigned long long pos = atomicAdd(&gcur[jx], 1ull);
+                if (pos < (jx + 1ull) * fcap) out[pos] = x1;
+                else *over = 1u;
+            }
+            if (e2) {
+                const unsigned int jx = rec_bucket(x2, lb1);
+                const unsigned long long pos = atomicAdd(&gcur[jx], 1ull);
+                if (pos < (jx + 1ull) * fcap) out[pos] = x2;
+                else *over = 1u;
+            }
+        }
+        __syncthreads();
+        unsigned long long mybase = 0;
+        if (threadIdx.x < 256) {  // exclusive scan of the tile counts + run reservations
+            const unsigned int v = threadIdx.x < F ? tcnt[threadIdx.x] : 0u;
+            unsigned int incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int u = __shfl_up(incl, o);
+                if ((int)(threadIdx.x & 63) >= o) incl += u;
+            }
+            tbeg[threadIdx.x] = incl - v;
+            if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+            if (v) mybase = atomicAdd(&gcur[threadIdx.x], (unsigned long long)v);
+        }
+        __syncthreads();
+        if (threadIdx.x >= 64 && threadIdx.x < 256) {
+            unsigned int add = 0;
+            for (unsigned int w = 0; w < (threadIdx.x >> 6); w++) add += wsum[w];
+            tbeg[threadIdx.x] += add;
+        }
+        __syncthreads();
+        if (valid) {
+            const unsigned int p1 = tbeg[j1] + k1, p2 = tbeg[j2] + k2;
+            tile[p1] = r1;
+            tj[p1] = (uint8_t)j1;
+            tile[p2] = r2;
+            tj[p2] = (uint8_t)j2;
+        }
+        if (threadIdx.x < 256) base[threadIdx.x] = mybase;
+        __syncthreads();
+        bool lost = false;
+        for (unsigned int i = threadIdx.x; i < n; i += NT) {
+            const unsigned int b = tj[i];
+            const uint64_t pos = base[b] + (i - tbeg[b]);
+            if (pos < (b + 1ull) * fcap) out[pos] = tile[i];
+            else lost = true;
+        }
+        if (lost) *over = 1u;
+        __syncthreads();
     }
 }
 
