@@ -1808,7 +1808,7 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
     EC_CHECK(s->bb2.ensure(2 * nbmax * 8));
     EC_CHECK(s->gcur.ensure(nbmax * 8));
     EC_CHECK(s->tmp.ensure(16));
-    unsigned int *flags = s->tmp.as<unsigned int>();  // [0] extras, [1] overflow
+    unsigned int *flags = s->tmp.as<unsigned int>();  // [1]: a level region or a join table overflowed
     unsigned long long *ibeg = s->bb2.as<unsigned long long>(), *iend = ibeg + nbmax;
     EC_HIP(hipMemsetAsync(flags, 0, 8, st));
     const typename Ops::K *dkey = s->dkey.as<typename Ops::K>();
