@@ -81,13 +81,12 @@ def kernel_alg_bytes(name, P, R, L, K=8, rec=16, NR=None, nsub=0, rec2=None):
     k_count     general path: read once + one insert per position R*L + P*(K+8)
     Super-k-mer records (rec = 32 or 16 bytes, NR records):
     k_downsweep / k_skpart R*L + rec*NR;  k_refine / k_skrefine 2*rec*NR
-    k_bucket (rec 32) rec*NR + nsub
-    k_skbucket (rec 16)    P*(K+8): SURVEY 8d's per-position canonical insert, the work this
-                           kernel does (in LDS); its HBM bytes (the 16-B records, ~P/7 of them,
-                           and the sub-tables) are the measured `traffic`, far below"""
+    k_bucket / k_skbucket rec*NR + nsub: the records read, the sub-tables written (SURVEY 8d's
+                           per-position insert, P*(K+8), overstates it: the kernel inserts each
+                           distinct super-k-mer's windows once, ~P/10 inserts, in LDS)"""
     if NR is not None and NR < P and rec in (16, 32):
         return {"k_upsweep": R * L, "k_downsweep": R * L + rec * NR,
-                "k_bucket": (P * (K + 8) if rec == 16 else rec * NR + nsub),
+                "k_bucket": rec * NR + nsub,
                 "k_count": R * L + P * (K + 8), "k_refine": 2 * rec * NR}[name]
     rec2 = rec2 or rec
     return {"k_upsweep": R * L, "k_downsweep": R * L + rec * P, "k_bucket": rec2 * P + nsub,
@@ -375,9 +374,7 @@ def main():
             "traffic": (tr["kernel_bytes_per_launch"] if tr else None),
             "traffic_source": (tr["file"] if tr else None),
             "kernel": names_v[kid], "kernel_ms": round(kms, 4), "alg_bytes_per_launch": int(kb),
-            "alg_basis": ("SURVEY 8d P*(K+8): one canonical insert per position (LDS tables); "
-                          "traffic = HBM bytes moved" if names_v[kid] == "k_skbucket"
-                          else "bytes the kernel must move through HBM"),
+            "alg_basis": "bytes the kernel must move through HBM",
             "kernels_ms": {names_v[i]: round(float(kern[i]), 4) for i in range(len(kern)) if kern[i] > 0},
             # every counting kernel against the same roofline (k_downsweep and k_refine run within
             # a few % of each other on the headline, so the dominant one can change between runs)
