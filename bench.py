@@ -221,6 +221,8 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="N > 1: split the config's reads over the ranks (fixed job) instead of the default "
                          "weak scaling (every rank samples its own config-sized read set of the same genome)")
+    ap.add_argument("--strong-leg", action="store_true",
+                    help="run the strong-scaled leg at any N (with --sharded at N = 1: rehearses its code path)")
     ap.add_argument("--no-strong-leg", action="store_true",
                     help="N > 1 weak-scaled runs: skip the strong-scaled leg (the config's read set split over "
                          "the ranks, reported under \"strong\")")
@@ -325,7 +327,7 @@ def main():
     # contiguous shards over the ranks (BASELINE config 4: "10M x 100 bp reads, read-sharded"),
     # timed the same way; reported beside the weak-scaled value
     strong = None
-    if weak and world > 1 and not args.no_strong_leg:
+    if weak and (world > 1 or args.strong_leg) and not args.no_strong_leg:
         import distributed
 
         lo, hi = distributed.shard_range(cfg["reads"], rank, world)
