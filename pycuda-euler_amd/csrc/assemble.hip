@@ -666,6 +666,9 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         EC_HIP(hipMemcpyAsync(h, dbg, 128, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
         const double nw = (double)Bk * (BUCKET_THREADS / 64);  // waves
+        if (plan.slots == 1024)
+            fprintf(stderr, "k_skbucket3: %llu buckets, most distinct records in a bucket %llu\n",
+                    (unsigned long long)Bk, h[3]);
         fprintf(stderr, "k_skbucket per wave (shader clocks): records phase canon %.0f probe %.0f (%.1f iterations) "
                         "post %.0f barrier %.0f over %.1f rounds; roll-out %.0f barrier %.0f\n",
                 h[8] / nw, h[9] / nw, h[11] / nw, h[10] / nw, h[12] / nw, h[13] / nw, h[14] / nw, h[15] / nw);

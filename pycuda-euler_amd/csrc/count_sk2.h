@@ -1017,13 +1017,19 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
             const bool claim = go && !hit && T == 0;
             if (go && !hit && T != 0 && T != (TG | PEND)) SL = SL + 1 == (unsigned int)RS ? 0u : SL + 1;
             if (claim) {
-                if (ld(&s_nent) >= min(CLAIM_MAX, claim_cap)) {  // (claim_cap: tests of the overflow list)
+                // reserve an entry first, so the table never holds more than the cap (the compact
+                // arrays below hold NC = RS / 2 entries): a lane past it, or one whose CAS loses,
+                // gives its reservation back (claim_cap: tests of the overflow list)
+                const unsigned int o = atomicAdd(&s_nent, 1u);
+                if (o >= min(CLAIM_MAX, claim_cap)) {
+                    atomicSub(&s_nent, 1u);
                     ST = 2;
                 } else if (atomicCAS(&R.tag[SL], 0u, TG | PEND) == 0) {
                     R.x[SL] = K0, R.y[SL] = K1, R.z[SL] = K2;
                     __hip_atomic_store(&R.tag[SL], TG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    atomicAdd(&s_nent, 1u);
                     ST = 1;
+                } else {
+                    atomicSub(&s_nent, 1u);
                 }
             }
         }
@@ -1068,7 +1074,10 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
             a += v;
         }
         s_ncnt[SK2_NMAX] = a;
-        if (dbg) atomicAdd(&dbg[0], (unsigned long long)a), atomicAdd(&dbg[1], 1ull);
+        if (dbg) {
+            atomicAdd(&dbg[0], (unsigned long long)a), atomicAdd(&dbg[1], 1ull);
+            atomicMax(&dbg[3], (unsigned long long)(a + min(s_nov, (unsigned int)OV)));  // distinct, overflow incl.
+        }
     }
     // the k-mer table over the record table's space (its reads are done)
     for (int i = tid; i < SLOTS; i += NT) {

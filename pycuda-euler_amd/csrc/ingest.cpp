@@ -304,6 +304,19 @@ int ec_pack_reads(const uint8_t *reads, const uint64_t *offsets, uint64_t nreads
         set_error("null argument");
         return EC_ERR_ARG;
     }
+    if (nreads == UINT64_MAX) {  // (nreads + 1 offsets: an empty offsets array passed as -1)
+        set_error("bad read count");
+        return EC_ERR_ARG;
+    }
+    if (offsets[0] != 0) {
+        set_error("offsets[0] = %llu, not 0", (unsigned long long)offsets[0]);
+        return EC_ERR_ARG;
+    }
+    for (uint64_t r = 0; r < nreads; r++)
+        if (offsets[r + 1] < offsets[r]) {
+            set_error("offsets not monotone at read %llu", (unsigned long long)r);
+            return EC_ERR_ARG;
+        }
     const uint64_t nb = offsets[nreads];
     if (nb && (!reads || !codes)) {
         set_error("null reads / codes");

@@ -988,12 +988,25 @@ __global__ void __launch_bounds__(256) k_sf_hook(const CircuitEdge *cg, uint64_t
         nxt[r] = o;
     }
 }
-__global__ void __launch_bounds__(256) k_sf_chase(uint64_t n, const unsigned int *nxt, unsigned int *comp,
-                                                  unsigned int *best) {
+// the hooks form trees whose roots point to themselves, but not shallow ones: on a path whose
+// edges are sorted by (c1, c2) every vertex hooks to its neighbour, one chain of length n.
+// Pointer jumping (nxt[v] = nxt[nxt[v]], in place: a racing read only sees a pointer further up
+// the same tree) reaches every root in ceil(log2(depth)) launches.
+__global__ void __launch_bounds__(256) k_sf_jump(uint64_t n, unsigned int *nxt, unsigned int *changed) {
+    bool ch = false;
     for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
-        unsigned int r = nxt[v];
-        for (uint64_t it = 0; nxt[r] != r && it < n; it++) r = nxt[r];  // (hooks form trees: bounded)
-        comp[v] = r;
+        const unsigned int p = nxt[v], q = nxt[p];
+        if (p != q) {
+            nxt[v] = q;
+            ch = true;
+        }
+    }
+    if (__any(ch) && (threadIdx.x & 63) == 0) *changed = 1u;
+}
+__global__ void __launch_bounds__(256) k_sf_settle(uint64_t n, const unsigned int *nxt, unsigned int *comp,
+                                                   unsigned int *best) {
+    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < n; v += (uint64_t)gridDim.x * blockDim.x) {
+        comp[v] = nxt[v];
         best[v] = NONE32;
     }
 }
@@ -1033,8 +1046,14 @@ int ec_spanning_forest(const void *cg_edges, uint64_t cg_edge_count, uint64_t cg
         if (!any) break;
         k_sf_hook<<<grid_for(n, 256), 256>>>(dcg.as<CircuitEdge>(), n, dcomp.as<unsigned int>(),
                                              dbest.as<unsigned int>(), dnxt.as<unsigned int>(), din.as<uint8_t>());
-        k_sf_chase<<<grid_for(n, 256), 256>>>(n, dnxt.as<unsigned int>(), dcomp.as<unsigned int>(),
-                                              dbest.as<unsigned int>());
+        for (int j = 0; j < 64; j++) {  // (<= log2(n) + 1 launches)
+            EC_HIP(hipMemset(dany.p, 0, 4));
+            k_sf_jump<<<grid_for(n, 256), 256>>>(n, dnxt.as<unsigned int>(), dany.as<unsigned int>());
+            EC_HIP(hipMemcpy(&any, dany.p, 4, hipMemcpyDeviceToHost));
+            if (!any) break;
+        }
+        k_sf_settle<<<grid_for(n, 256), 256>>>(n, dnxt.as<unsigned int>(), dcomp.as<unsigned int>(),
+                                               dbest.as<unsigned int>());
     }
     std::vector<uint8_t> in(E);
     EC_HIP(hipMemcpy(in.data(), din.p, E, hipMemcpyDeviceToHost));

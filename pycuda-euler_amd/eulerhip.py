@@ -187,8 +187,10 @@ def pack_2bit(buf, offsets, threads=0, alloc=None):
     n bytes for the codes (e.g. page-locked memory); numpy by default."""
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if offsets.size == 0:
+        raise ValueError("offsets must hold nreads + 1 entries (at least [0])")
     n = len(offsets) - 1
-    nb = int(offsets[-1]) if n >= 0 else 0
+    nb = int(offsets[-1])
     ncodes = (nb + 3) // 4
     codes = alloc(max(ncodes, 1)) if alloc else np.empty(max(ncodes, 1), np.uint8)
     nexc = ctypes.c_uint64(0)

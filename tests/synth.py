@@ -12,6 +12,14 @@ def make_genome(genome_len, seed):
     return LUT[rng.integers(0, 4, genome_len, dtype=np.uint8)].tobytes()
 
 
+def read_starts(genome_len, n_reads, read_len, seed):
+    """Genome start of every read of make_reads(genome_len, n_reads, read_len, seed) (linear,
+    part None): the same draws in the same order."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rng.integers(0, 4, genome_len, dtype=np.uint8)
+    return rng.integers(0, max(1, genome_len - read_len + 1), n_reads)
+
+
 def make_reads(genome_len, n_reads, read_len, seed, err=0.0, n_rate=0.0, circular=False, rc_frac=0.5,
                part=None, rows=None):
     """Returns (buf uint8[n_reads*read_len], offsets uint64[n_reads+1]) of ASCII reads.

@@ -676,6 +676,26 @@ def test_sk2_record_overflow_list_vs_oracle(gpu_session, monkeypatch, cap, varia
     assert res.contig_bytes == ref["contig_chars"] and res.links == rl
 
 
+@pytest.mark.parametrize("g,n,L,seed", [(22_000, 80_000, 60, 1), (23_000, 60_000, 50, 2), (21_000, 90_000, 70, 3)])
+def test_sk2_record_table_full_default_cap_vs_oracle(gpu_session, monkeypatch, capfd, g, n, L, seed):
+    """k_skbucket3 at its default claim cap with buckets of more than 832 distinct records (the
+    compact arrays' size, RS / 2): short reads at high coverage, so nearly every start position
+    adds two read-truncated records.  The cap must be a hard bound -- records past it go to the
+    overflow list, never past the compact arrays (a racing wave used to overshoot)."""
+    monkeypatch.setenv("EULERHIP_SK2_STATS", "1")
+    buf, off = make_reads(g, n, L, 5400 + seed, err=0.0)
+    ref, rc, rl = _oracle_packed(buf, off, 31, 1, True)
+    capfd.readouterr()
+    gpu_session.run_host(buf, off, 31, 1, eulerhip.EC_FLAG_WANT_DICT)
+    res = gpu_session.fetch(31, True)
+    err = capfd.readouterr().err
+    assert [[x, c] for x, c in res.dict_items] == ref["d"]
+    assert res.contig_bytes == ref["contig_chars"] and res.links == rl
+    most = [int(l.rsplit(" ", 1)[1]) for l in err.splitlines() if l.startswith("k_skbucket3:")]
+    assert res.stats.count_variant == 3 and most, err
+    assert most[-1] > 832, err
+
+
 @pytest.mark.parametrize("k", [31, 24])
 def test_sk2_large_table_kernel_vs_oracle(gpu_session, monkeypatch, k):
     """EULERHIP_NO_SKB3: k_skbucket's 2048-slot tables (the plan for inputs past ~6 M keys)"""

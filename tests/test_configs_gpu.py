@@ -17,7 +17,7 @@ import pytest
 
 import eulerhip
 import oracle
-from synth import make_genome, make_reads
+from synth import make_genome, make_reads, read_starts
 
 pytestmark = pytest.mark.gpu
 
@@ -77,3 +77,78 @@ def test_config5_shape_k51_vs_oracle(gpu_session):
     buf, off = make_reads(2_000_000, 1_000_000, 150, 20261015 + 5)
     res = _check_vs_oracle(gpu_session, buf, off, 51)
     assert res.stats.n_positions == 100_000_000
+
+
+def _solid_runs(G, starts, L, k, limit=1):
+    """For error-free reads of a repeat-free genome, the count of a canonical k-mer is the number
+    of read windows covering its genome position (a read and its reverse complement insert the
+    same canonical k-mers, build:25-42), so the solid k-mers are the positions covered by more
+    than `limit` windows; all_contigs:79-111 walks each maximal run of consecutive solid positions
+    as one contig (no branches: every (k - 1)-mer is unique).  Returns (n_solid, run starts,
+    run ends) with runs [a, b) of k-mer positions."""
+    W = L - k + 1
+    C = np.cumsum(np.bincount(starts, minlength=G - k + 1), dtype=np.int64)
+    cov = C.copy()
+    cov[W:] -= C[:-W]
+    solid = cov > limit
+    e = np.diff(np.concatenate([[0], solid.view(np.int8), [0]]).astype(np.int8))
+    return int(solid.sum()), np.flatnonzero(e == 1), np.flatnonzero(e == -1)
+
+
+def _canon(s):
+    t = s.translate(COMP)[::-1]
+    return s if s <= t else t
+
+
+def test_config5_rank_shape_solid_runs():
+    """BASELINE configs[4] at its per-rank shape (8 ranks: 12.5 M x 150 bp of the 200 Mbp genome,
+    k = 51, 128-bit keys, third partition level, 1.9 * 10^9 positions): n_solid equals the
+    solid positions computed from the read starts, and the contigs, each in canonical
+    orientation, are exactly the genome substrings of the maximal solid runs (a size-independent
+    property; the oracle is bit-exact on the same path below at 10^9 positions)"""
+    import torch
+
+    G, n, L, k, seed = 200_000_000, 12_500_000, 150, 51, 20261015 + 5
+    buf, off = make_reads(G, n, L, seed)
+    s = eulerhip.Session(0)
+    try:
+        free0, total = torch.cuda.mem_get_info()
+        s.run_host(buf, off, k, 1)
+        res = s.fetch(k)
+        free1, _ = torch.cuda.mem_get_info()
+        print("config-5 rank shape: session HBM %.1f GB of %.1f GB" % ((free0 - free1) / 1e9, total / 1e9))
+    finally:
+        s.close()
+    del buf, off
+    st = res.stats
+    assert st.n_positions == n * (L - k + 1)
+    n_solid, a, b = _solid_runs(G, read_starts(G, n, L, seed), L, k)
+    assert st.n_solid == n_solid and st.n_dict == 2 * n_solid
+    assert st.n_contigs == len(a)
+    assert st.n_links == 0  # a run's ends extend nowhere
+    genome = make_genome(G, seed)
+    ch, co = res.contig_bytes, res.contig_offsets
+    got = sorted(_canon(ch[int(co[i]):int(co[i + 1])]) for i in range(len(co) - 1))
+    want = sorted(_canon(genome[int(x):int(y) - 1 + k]) for x, y in zip(a, b))
+    assert got == want
+
+
+def test_genome20m_k51_third_level_vs_oracle(gpu_session, monkeypatch):
+    """config 5's read shape at a tenth of its genome (20 Mbp, 10 M x 150 bp, k = 51: 10^9
+    positions, 2 * 10^7 solid 51-mers) through the wide path's third partition level (forced:
+    2^2 sub-buckets per fine bucket), bit-exact against the oracle (N-core count)"""
+    import os
+
+    monkeypatch.setenv("EULERHIP_WIDE_L3", "2")
+    buf, off = make_reads(20_000_000, 10_000_000, 150, 20261015 + 5)
+    th = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    ref = oracle.assemble_packed(buf, off, 51, 1, threads=th)
+    gpu_session.run_host(buf, off, 51, 1)
+    res = gpu_session.fetch(51)
+    assert res.stats.n_buckets == (1 << 14) << 2
+    assert res.stats.n_positions == ref["n_positions"] == 10 ** 9
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert np.array_equal(res.link_offsets, ref["link_offsets"])
+    assert np.array_equal(res.link_codes, ref["links"])

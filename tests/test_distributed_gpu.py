@@ -279,3 +279,25 @@ def test_sharded_owner_rule_switches_on_skew(engines):
     assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref)
     for e in engines:
         e.set_owner_rule(distributed.OWNER_MINIMIZER)
+
+
+@pytest.mark.parametrize("partitioned", [True, False])
+def test_local_sharded_8_ranks_k51_vs_oracle(partitioned):
+    """BASELINE config 5's path (128-bit keys, "8xMI355X partitioned graph") at 8 simulated ranks
+    on a k = 51 slice of 1.0 * 10^7 positions: the owners' merges, the gathered set's HBM lookup
+    table and the partitioned links equal the oracle (contigs, links, dict size)"""
+    import distributed
+
+    es = [distributed.HipEngine(0) for _ in range(8)]
+    try:
+        buf, off = make_reads(200_000, 100_000, 150, 20261015 + 5, err=0.001)
+        ref = oracle.assemble_packed(buf, off, 51, 1)
+        assert ref["n_positions"] >= 10 ** 7 - 10 ** 5
+        res, P = distributed.local_sharded_assemble(es, buf, off, 51, 1, partitioned=partitioned)
+        assert P == ref["n_positions"]
+        assert res.stats.n_dict == ref["n_dict"]
+        assert res.contig_bytes == ref["contig_chars"]
+        assert res.links == oracle.unpack_links(ref)
+    finally:
+        for e in es:
+            e.sess.close()

@@ -125,3 +125,20 @@ def test_pack_2bit_roundtrip():
     off2 = off.copy()
     off2[1] += 1  # ragged
     assert eulerhip.pack_2bit(buf, off2).read_len == 0
+
+
+def test_pack_2bit_rejects_bad_offsets():
+    """empty offsets (no nreads + 1 entries), offsets not starting at 0 or not monotone are
+    rejected before any read is touched"""
+    import pytest
+
+    import eulerhip
+
+    buf = np.frombuffer(b"ACGTACGT", np.uint8)
+    with pytest.raises(ValueError):
+        eulerhip.pack_2bit(buf, np.zeros(0, np.uint64))
+    for bad in ([0, 5, 3, 8], [1, 4, 8]):
+        with pytest.raises(eulerhip.EulerHipError):
+            eulerhip.pack_2bit(buf, np.array(bad, np.uint64))
+    pr = eulerhip.pack_2bit(buf[:0], np.zeros(1, np.uint64))
+    assert pr.nreads == 0 and pr.nbases == 0

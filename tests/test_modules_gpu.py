@@ -226,8 +226,37 @@ def test_spanning_forest_vs_kruskal():
         cg["c2"] = rng.integers(0, V, E)
         cg["ceid"] = np.arange(E)
         assert eulercuda.findSpanningTree(cg, E, V).tolist() == R.spanning_forest(cg, E, V), (V, E)
-    V = 20_000  # a path given in reverse: every round merges pairs only
+    V = 20_000  # a path given in reverse: every vertex hooks to v + 1, one chain of length V
     cg = np.zeros(V - 1, R.CE)
     cg["c1"] = np.arange(V - 1)[::-1]
     cg["c2"] = np.arange(1, V)[::-1]
     assert eulercuda.findSpanningTree(cg, V - 1, V).tolist() == list(range(V - 1))
+
+
+def test_spanning_forest_long_chain_time():
+    """10^6 circuits on a forward-sorted path: round 1 hooks every vertex to v - 1, a single
+    chain of length 10^6; the roots are found by pointer jumping (log2 launches), not by a serial
+    chase per vertex (O(n^2))"""
+    import time
+
+    import eulercuda
+
+    for V in (1_000_000, 300_001):
+        cg = np.zeros(V - 1, R.CE)
+        cg["c1"] = np.arange(V - 1)
+        cg["c2"] = np.arange(1, V)
+        cg["ceid"] = np.arange(V - 1)
+        t = time.perf_counter()
+        tree = eulercuda.findSpanningTree(cg, V - 1, V)
+        dt = time.perf_counter() - t
+        assert np.array_equal(tree, np.arange(V - 1)), V
+        assert dt < 10.0, (V, dt)
+    # two interleaved chains joined at the end, plus isolated circuits
+    rng = np.random.default_rng(9)
+    V = 200_000
+    perm = rng.permutation(V)
+    cg = np.zeros(V - 2, R.CE)
+    cg["c1"] = perm[:-2]
+    cg["c2"] = perm[1:-1]
+    cg["ceid"] = np.arange(V - 2)
+    assert eulercuda.findSpanningTree(cg, V - 2, V).tolist() == R.spanning_forest(cg, V - 2, V)

@@ -60,3 +60,24 @@ def test_oracle_ncore_synthetic(k):
     assert a["n_positions"] == b["n_positions"] and a["d"] == b["d"]
     assert a["contig_chars"] == b["contig_chars"]
     assert np.array_equal(a["links"], b["links"]) and np.array_equal(a["link_offsets"], b["link_offsets"])
+
+
+def test_solid_run_property_matches_oracle():
+    """The size-independent property test_configs_gpu.py checks config 5's per-rank shape with
+    (solid k-mers = positions covered by > limit read windows; contigs = maximal solid runs as
+    genome substrings) agrees with the oracle on a small error-free set of the same shape"""
+    import numpy as np
+
+    from synth import make_genome, make_reads, read_starts
+    from test_configs_gpu import _canon, _solid_runs
+
+    G, n, L, k, seed = 300_000, 20_000, 150, 51, 99
+    buf, off = make_reads(G, n, L, seed)
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    n_solid, a, b = _solid_runs(G, read_starts(G, n, L, seed), L, k)
+    assert ref["n_dict"] == 2 * n_solid
+    genome = make_genome(G, seed)
+    ch, co = ref["contig_chars"], ref["contig_offsets"]
+    got = sorted(_canon(ch[int(co[i]):int(co[i + 1])]) for i in range(len(co) - 1))
+    assert got == sorted(_canon(genome[int(x):int(y) - 1 + k]) for x, y in zip(a, b))
+    assert len(got) > 10
