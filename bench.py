@@ -270,6 +270,7 @@ def main():
     log("rank %d: generated %d reads in %.1f s" % (rank, cfg["reads"], time.time() - t0))
     k = cfg["k"]
 
+    hbm_free0 = torch.cuda.mem_get_info()[0]  # device memory before the inputs and the session
     if not use_dist:
         d_buf = torch.from_numpy(buf).cuda()
         d_off = torch.from_numpy(off.astype(np.int64)).cuda()
@@ -314,6 +315,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
+    # HBM held after the steps: inputs + the session's buffers (sized by their largest use and
+    # kept between calls, so this is the run's peak allocation)
+    hbm_used = hbm_free0 - torch.cuda.mem_get_info()[0]
     timed_phase_ms = dict(runner.phase_ms) if use_dist else None
     step(eulerhip.EC_FLAG_TIMING)  # untimed (every rank: it has collectives): the per-stage breakdown
     stage = np.array(list((sess.stats() if not use_dist else runner.stats()).stage_ms))
@@ -403,7 +407,8 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "u64" if k <= 32 else "u128",
+        "scaling": "none" if world == 1 and not use_dist else ("strong" if args.strong else "weak"),
+        "vs_baseline": None, "dtype": "u64" if k <= 32 else "u128",
         "data": "synthetic (iid ACGT genome, uniform %s %d bp reads, 50%% reverse-complemented, numpy PCG64 seed %d)"
                 % ("error-free" if not cfg.get("err") else "%.1f%%-substitution" % (100 * cfg["err"]), L, cfg["seed"]),
         "config": {"workload": cfg["name"] + ("" if world == 1 or not weak else " per GPU"), "genome_bp": cfg["genome"],
@@ -414,7 +419,8 @@ def main():
                    "count_variant": ["histogram runs", "fixed-capacity runs", "fixed-capacity runs, 10-B records",
                                      "super-k-mer records, 16 B"][variant],
                    "buckets": int(st.n_buckets), "record_bytes": int(st.record_bytes), "records": int(st.n_records),
-                   "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else "")},
+                   "parallelism": ("dp%d" % world) + ("-sharded" if use_dist else ""),
+                   "hbm_used_gb": round(hbm_used / 1e9, 2)},
         "roofline": roof,
         "cpu_baseline": cpu,
         "host_input": host,
