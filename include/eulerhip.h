@@ -16,8 +16,11 @@
  *     reference function it replaces.
  *
  * k-mer codes are 2-bit, MSB-first (A=0 C=1 G=2 T=3), exactly the reference encoding
- * (src/pyencode.py:40,62-69).  Reads are ASCII over {A,C,G,T,N}; 'N' splits a read into
- * segments (referenceAssembler.py:29).  Other bytes -> EC_ERR_ALPHABET.
+ * (src/pyencode.py:40,62-69).  Reads are ASCII; 'N' splits a read into segments
+ * (referenceAssembler.py:29).  Any other byte (lowercase, IUPAC codes) is an opaque symbol that
+ * is its own complement, as the reference's twin() keeps it (:7-10): such inputs take the
+ * extended-alphabet path (csrc/extended.h) with sb-bit symbol codes (sb = 4 / 5 / 8 for up to
+ * 16 / 32 / 256 distinct symbols) and need sb * k <= 126, else EC_ERR_ALPHABET.
  */
 #ifndef EULERHIP_H
 #define EULERHIP_H
@@ -32,11 +35,13 @@ extern "C" {
 /* ---- status codes ---------------------------------------------------------------------- */
 #define EC_OK 0
 #define EC_ERR_ARG (-1)      /* bad argument (k range, null pointer, size)                   */
-#define EC_ERR_ALPHABET (-2) /* read byte outside {A,C,G,T,N}                                 */
+#define EC_ERR_ALPHABET (-2) /* extended alphabet: sb * k > 126 (see above)                    */
 #define EC_ERR_NOMEM (-3)    /* device or host allocation failed                              */
 #define EC_ERR_HIP (-4)      /* HIP runtime error (message in ec_last_error)                  */
 #define EC_ERR_CAPACITY (-5) /* table overflow that survived the retries                       */
-#define EC_ERR_STATE (-6)    /* result requested before a successful ec_assemble_*            */
+#define EC_ERR_STATE (-6)    /* result requested before a successful ec_assemble_*, or an
+                              * extended-alphabet input on which the reference's
+                              * get_contig_forward never returns (referenceAssembler.py:59-77) */
 
 #define EC_MAX_K 63 /* k <= 32: 64-bit keys; 32 < k <= 63: 128-bit keys */
 

@@ -48,6 +48,9 @@ def lib():
         _lib.oracle_assemble_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(_Result)]
         _lib.oracle_assemble_mt.restype = ctypes.c_int
+        _lib.oracle_assemble_str.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_uint, ctypes.POINTER(_Result)]
+        _lib.oracle_assemble_str.restype = ctypes.c_int
         _lib.oracle_free.argtypes = [ctypes.POINTER(_Result)]
         _lib.oracle_last_error.restype = ctypes.c_char_p
     return _lib
@@ -66,16 +69,20 @@ def pack_reads(reads):
     return np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8), off
 
 
-def assemble_packed(buf, offsets, k, limit=1, want_dict=False, threads=None):
+def assemble_packed(buf, offsets, k, limit=1, want_dict=False, threads=None, string=False):
     """Run the oracle on a packed read set. Returns dict with d (optional), contigs, links.
     threads = N: the N-core variant (map -> reduceByKey counting as src/ref_spark.py:76-84 on N
-    host threads, all_contigs single-threaded); same results."""
+    host threads, all_contigs single-threaded); same results.  Reads with bytes outside
+    {A,C,G,T,N} take the string-keyed restatement (refasm_str.c); string=True forces it."""
     L = lib()
     res = _Result()
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     nreads = len(offsets) - 1
-    if threads:
+    if string:
+        rc = L.oracle_assemble_str(buf.ctypes.data, offsets.ctypes.data, nreads, k, limit,
+                                   1 if want_dict else 0, ctypes.byref(res))
+    elif threads:
         rc = L.oracle_assemble_mt(buf.ctypes.data, offsets.ctypes.data, nreads, k, limit,
                                   1 if want_dict else 0, int(threads), ctypes.byref(res))
     else:
@@ -124,7 +131,7 @@ def unpack_links(out):
     return res
 
 
-def assemble(reads, k, limit=1, want_dict=True, threads=None):
+def assemble(reads, k, limit=1, want_dict=True, threads=None, string=False):
     buf, off = pack_reads(reads)
-    out = assemble_packed(buf, off, k, limit, want_dict, threads)
+    out = assemble_packed(buf, off, k, limit, want_dict, threads, string)
     return out.get("d"), unpack_contigs(out), unpack_links(out)

@@ -14,11 +14,11 @@
  * Pinned: tests/test_oracle.py checks it against every golden vector generated from the
  * real reference (the JSON fixtures in tests/golden/, made by tests/golden/make_golden.py).
  *
- * Alphabet: k-mers are 2-bit packed (A=0,C=1,G=2,T=3, first base most significant), so
- * reads must be over {A,C,G,T,N}; 'N' splits a read into segments exactly like
- * `read.split('N')` (build:29).  Any other byte makes the call return -2 (the reference
- * would keep such k-mers as opaque strings -- the documented alphabet deviation shared
- * with the product path).  k <= 32 uses 64-bit keys, 32 < k <= 64 uses 128-bit keys.
+ * Alphabet: over {A,C,G,T,N} k-mers are 2-bit packed (A=0,C=1,G=2,T=3, first base most
+ * significant); 'N' splits a read into segments exactly like `read.split('N')` (build:29).
+ * k <= 32 uses 64-bit keys, 32 < k <= 64 uses 128-bit keys.  Reads holding any other byte
+ * (lowercase, IUPAC codes: the reference keeps them as opaque symbols, twin:7-10) go to the
+ * string-keyed restatement in refasm_str.c.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -32,6 +32,11 @@ typedef unsigned __int128 u128;
 
 static __thread char g_err[256];
 const char *oracle_last_error(void) { return g_err; }
+void oracle_set_error(const char *msg) { snprintf(g_err, sizeof g_err, "%s", msg); }
+
+int oracle_assemble_str(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
+                        unsigned flags, oracle_result *out);
+
 
 static inline uint64_t mix64(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
@@ -45,6 +50,14 @@ static inline int base_code(unsigned char c) {
     case 'N': return -1;
     default: return -2;
     }
+}
+
+/* a byte outside {A,C,G,T,N} in the reads: the string-keyed restatement */
+static int extended_alphabet(const char *buf, const uint64_t *offsets, uint64_t nreads) {
+    if (!nreads) return 0;
+    for (uint64_t i = offsets[0]; i < offsets[nreads]; i++)
+        if (base_code((unsigned char)buf[i]) == -2) return 1;
+    return 0;
 }
 
 /* two instantiations: KEY = uint64_t (k <= 32) and KEY = u128 (k <= 64) */
@@ -68,6 +81,7 @@ int oracle_assemble(const char *buf, const uint64_t *offsets, uint64_t nreads, i
                     unsigned flags, oracle_result *out) {
     memset(out, 0, sizeof(*out));
     if (k < 1 || k > 64) { snprintf(g_err, sizeof g_err, "k=%d out of range [1,64]", k); return -1; }
+    if (extended_alphabet(buf, offsets, nreads)) return oracle_assemble_str(buf, offsets, nreads, k, limit, flags, out);
     if (k <= 32) return assemble_64(buf, offsets, nreads, k, limit, flags, out);
     return assemble_128(buf, offsets, nreads, k, limit, flags, out);
 }
@@ -76,6 +90,7 @@ int oracle_assemble_mt(const char *buf, const uint64_t *offsets, uint64_t nreads
                        unsigned flags, int threads, oracle_result *out) {
     memset(out, 0, sizeof(*out));
     if (k < 1 || k > 64) { snprintf(g_err, sizeof g_err, "k=%d out of range [1,64]", k); return -1; }
+    if (extended_alphabet(buf, offsets, nreads)) return oracle_assemble_str(buf, offsets, nreads, k, limit, flags, out);
     if (k <= 32) return assemble_mt_64(buf, offsets, nreads, k, limit, flags, threads, out);
     return assemble_mt_128(buf, offsets, nreads, k, limit, flags, threads, out);
 }

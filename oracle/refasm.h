@@ -22,7 +22,8 @@ typedef struct {
     int64_t *links;           /* entry = 2*j + (orientation == '-')                      */
 } oracle_result;
 
-/* returns 0 on success, -1 bad argument, -2 byte outside {A,C,G,T,N}, -3 out of memory */
+/* returns 0 on success, -1 bad argument, -3 out of memory, -4 a contig walk that the reference
+ * would never finish (reads with bytes outside {A,C,G,T,N} only: see refasm_str.c) */
 int oracle_assemble(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
                     unsigned flags, oracle_result *out);
 /* the same result from `threads` host threads: map -> reduceByKey counting as
@@ -30,6 +31,9 @@ int oracle_assemble(const char *buf, const uint64_t *offsets, uint64_t nreads, i
 int oracle_assemble_mt(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
                        unsigned flags, int threads, oracle_result *out);
 void oracle_free(oracle_result *r);
+/* the string-keyed restatement (any bytes; refasm_str.c), also reached through the two above */
+int oracle_assemble_str(const char *buf, const uint64_t *offsets, uint64_t nreads, int k, int limit,
+                        unsigned flags, oracle_result *out);
 const char *oracle_last_error(void);
 
 #ifdef __cplusplus

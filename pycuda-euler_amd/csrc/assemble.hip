@@ -37,6 +37,10 @@
 #include "count_wide.h"
 #include "hostin.h"
 #include "join_w.h"
+#include "extended.h"
+#include "rank_tile.h"
+
+#include <mutex>
 
 namespace ec {
 
@@ -193,6 +197,13 @@ struct ec_session {
     } pipe;
     std::vector<hipEvent_t> pev;  // chunk copy events (created on demand, reused)
     DevBuf p_codes, p_exc;
+    // extended alphabet (extended.h): its symbol table, and the one-way-link components'
+    // union-find / cut / emulation buffers
+    bool xalpha = false;
+    XAlpha xa{};
+    DevBuf x_par, x_irr, x_in, x_succ, x_done, x_lk, x_lv, x_lk2, x_lv2, x_len, x_m, x_cid, x_head, x_tail;
+    // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
+    DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp;
 };
 
 namespace ec {
@@ -243,6 +254,8 @@ struct Scalars {  // device scalars block
     unsigned int skew;
     unsigned int lens[4];  // k_upsweep: max read length, ~min read length (reads with windows), any slow-path read
     unsigned long long nrec;  // k_upsweep_sk: super-k-mer records
+    unsigned int nasym, nxl, nxs;  // extended.h: one-way links, entries of their components, their starts
+    unsigned int xbad;             // extended.h: a walk that never reaches its start again
     unsigned int active[64];
 };
 
@@ -324,6 +337,7 @@ void collect_timing(ec_session *s) {
 // per-call setup shared by every entry point: argument checks, stats reset, timing events,
 // zeroed device scalars
 int begin_call(ec_session *s, int k, unsigned flags) {
+    s->xalpha = false;  // (set by the extended-alphabet path, extended.h)
     refresh_knobs();
     s->have = false;
     s->stats_ok = false;
@@ -1848,6 +1862,53 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
     return EC_OK;
 }
 
+// extended alphabet (extended.h): links without their twin link make their components'
+// walks overlap; those components are cut out of the parallel ranking (their successors saved
+// in x_succ) and their dict entries listed in (component, first event) order for k_x_emulate.
+// nx = the entries listed (0: every link has its twin link, nothing to do)
+int x_cut(ec_session *s, unsigned int U, unsigned int &nx) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int N = 2 * U;
+    nx = 0;
+    EC_HIP(hipMemsetAsync(&dsc->nasym, 0, 16, st));  // nasym, nxl, nxs, xbad
+    k_x_asym<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, &dsc->nasym);
+    unsigned int nasym = 0;
+    EC_HIP(hipMemcpyAsync(&nasym, &dsc->nasym, 4, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (!nasym) return EC_OK;
+    EC_CHECK(s->x_par.ensure((size_t)U * 4));
+    EC_CHECK(s->x_irr.ensure(U));
+    EC_CHECK(s->x_in.ensure(U));
+    EC_CHECK(s->x_succ.ensure((size_t)N * 4));
+    EC_CHECK(s->x_lk.ensure((size_t)N * 8));
+    EC_CHECK(s->x_lk2.ensure((size_t)N * 8));
+    EC_CHECK(s->x_lv.ensure((size_t)N * 4));
+    EC_CHECK(s->x_lv2.ensure((size_t)N * 4));
+    unsigned int *par = s->x_par.as<unsigned int>();
+    k_x_iota<<<grid_for(U, B), B, 0, st>>>(par, U);
+    k_x_uf_link<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, par);
+    k_x_uf_flatten<<<grid_for(U, B), B, 0, st>>>(U, par);
+    EC_HIP(hipMemsetAsync(s->x_irr.p, 0, U, st));
+    k_x_mark_irr<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, par,
+                                              s->x_irr.as<uint8_t>());
+    k_x_cut<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), N, par, s->x_irr.as<uint8_t>(), s->x_in.as<uint8_t>(),
+                                         s->succ.as<unsigned int>(), s->x_succ.as<unsigned int>(),
+                                         s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                         s->x_lk.as<unsigned long long>(), s->x_lv.as<unsigned int>(), &dsc->nxl);
+    EC_HIP(hipMemcpyAsync(&nx, &dsc->nxl, 4, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (kn().verbose) fprintf(stderr, "extended: %u one-way links, %u dict entries in their components\n", nasym, nx);
+    // (component, first event) order: by event, then stably by component root
+    EC_CHECK(sort_pairs(s, s->x_lk.as<unsigned long long>(), s->x_lk2.as<unsigned long long>(), s->x_lv.as<unsigned int>(),
+                        s->x_lv2.as<unsigned int>(), nx));
+    k_x_rekey<<<grid_for(nx, B), B, 0, st>>>(s->x_lv2.as<unsigned int>(), nx, par, s->x_lk.as<unsigned long long>());
+    EC_CHECK(sort_pairs(s, s->x_lk.as<unsigned long long>(), s->x_lk2.as<unsigned long long>(),
+                        s->x_lv2.as<unsigned int>(), s->x_lv.as<unsigned int>(), nx));
+    return EC_OK;
+}
+
 // all_contigs:79-111 on the device from the solid set of phase_count / phase_merge
 template <typename Ops, typename Index>
 int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const unsigned int *ext_succ = nullptr) {
@@ -1857,6 +1918,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     Scalars hsc{};
     const unsigned int N = 2 * U;
     const size_t Nn = std::max<size_t>(N, 1);
+    // list ranking by tile contraction (rank_tile.h) unless EULERHIP_RANK=1 asks for the
+    // node-level ruling set: neither needs pred / the node walk records then
+    const bool tile_rank = kn().rank != 1;
 
     // ---- links ----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_LINKS);
@@ -1876,8 +1940,11 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     // count) stay in a bucket's sub-table and are cheaper than the join's random link writes
     bool joined = false;
     const unsigned int *gate = nullptr;
-    if (U && !ext_succ && k >= 8 && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
-        EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
+    constexpr bool XT = std::is_same<Ops, OpsX>::value;  // extended alphabet (extended.h)
+    if constexpr (!XT) {
+        if (U && !ext_succ && k >= 8 && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
+            EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
+    }
     if (U && !ext_succ) {  // (after a join: only if it overflowed, decided on the device)
         // gated: a small grid-stride grid, so the normal case (the gate closed) costs ~2 us a
         // launch instead of one exiting block per 256 nodes
@@ -1888,17 +1955,22 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
         k_succ<<<gn, B, 0, st>>>(s->upal.as<uint8_t>(), s->outdeg.as<uint8_t>(), s->cand.as<unsigned int>(), N,
                                 s->succ.as<unsigned int>(), s->dfc.as<unsigned long long>(),
-                                s->dft.as<unsigned long long>(), joined ? nullptr : s->nrec.as<NodeRec>(), gate);
+                                s->dft.as<unsigned long long>(), (joined || tile_rank) ? nullptr : s->nrec.as<NodeRec>(),
+                                gate);
     }
-    if (U) {
+    unsigned int nx = 0;  // extended alphabet: dict entries of components with one-way links
+    if constexpr (XT) {
+        if (U) EC_CHECK(x_cut(s, U, nx));
+    }
+    if (U && !tile_rank) {
         // (with the first ruler pass's counts: k_rulers_count at it = 0 below is skipped, and the
-        // node records when k_succ did not write them)
+        // node records when k_succ did not write them, or wrote successors x_cut has cut since)
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
         EC_CHECK(s->rbc.ensure(((Nn + RULER_CHUNK - 1) / RULER_CHUNK) * 8));
         k_pred_rc<<<(unsigned int)((N + RULER_CHUNK - 1) / RULER_CHUNK), B, 0, st>>>(
             s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, 31u, s->pred.as<unsigned int>(),
             s->rbc.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-            (ext_succ || joined) ? s->nrec.as<NodeRec>() : nullptr, s->outdeg.as<unsigned long long>());
+            (ext_succ || joined || nx) ? s->nrec.as<NodeRec>() : nullptr, s->outdeg.as<unsigned long long>());
     }
     mark(s, 2 * EC_STAGE_LINKS + 1);
 
@@ -1917,7 +1989,89 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     unsigned int nr = 0;
     int rounds = 0;  // Wyllie rounds launched (their convergence is checked with the results)
     s->stats.rank_rounds = 0;
-    if (U) {
+    if (U && tile_rank) {
+        // (1) chains of in-tile links ranked in LDS, in-tile cycles finished (rank_tile.h)
+        const unsigned int ntiles = (N + RT_TN - 1) / RT_TN;
+        EC_CHECK(s->rt_tcnt.ensure(((size_t)ntiles + 1) * 8));
+        EC_CHECK(s->rt_tbase.ensure(((size_t)ntiles + 1) * 8));
+        EC_CHECK(s->rt_srec.ensure(Nn * sizeof(SuperRec)));
+        EC_CHECK(s->rt_sidx.ensure(Nn * 4));
+        unsigned int *LH = s->pred.as<unsigned int>(), *LR = s->rid.as<unsigned int>() + Nn;  // (free here)
+        SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);  // (dead before the Wyllie rounds)
+        static_assert(sizeof(SuperRec) == sizeof(RJump), "tile scratch in the ruler state buffer");
+        unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
+        EC_HIP(hipMemsetAsync(tcnt + ntiles, 0, 8, st));
+        k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
+                                                s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), LH,
+                                                LR, tcnt, scratch, s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
+                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+        EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
+        unsigned long long M64 = 0;
+        EC_HIP(hipMemcpyAsync(&M64, tbase + ntiles, 8, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        const unsigned int M = (unsigned int)M64;
+        // (2) the super list: compacted in tile order, linked, ranked by the weighted ruling set
+        if (M) {
+            SuperRec *srec = s->rt_srec.as<SuperRec>();
+            unsigned int *SIDX = s->rt_sidx.as<unsigned int>();
+            k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, srec, SIDX);
+            EC_CHECK(s->rt_snrec.ensure((size_t)M * sizeof(SNodeRec)));
+            EC_CHECK(s->rt_hasp.ensure(M));
+            EC_CHECK(s->rt_pks.ensure((size_t)M * 4));
+            EC_CHECK(s->rt_rks.ensure((size_t)M * 4));
+            EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
+            SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
+            k_super_link<<<grid_for(M, B), B, 0, st>>>(srec, M, SIDX, snrec, s->rt_hasp.as<uint8_t>());
+            EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
+            EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
+            EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
+            const unsigned int masks[4] = {15u, 3u, 1u, 0u};
+            unsigned int r0 = 0;
+            const unsigned int nblk = (M + RULER_CHUNK - 1) / RULER_CHUNK;
+            for (int it = 0; it < 4; it++) {
+                k_srulers_count<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), M, masks[it], it == 0, s->rid.as<uint2>(),
+                                                    s->rbc.as<unsigned int>());
+                EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
+                k_srulers<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), M, masks[it], it == 0,
+                                              s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<uint2>(),
+                                              s->rlist.as<unsigned int>());
+                k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
+                k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), r0, &dsc->nr, masks[it],
+                                             s->rid.as<uint2>(), s->nextR.as<unsigned int>(), s->st0.as<RJump>(),
+                                             &dsc->nvisited);
+                EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+                EC_HIP(hipStreamSynchronize(st));
+                r0 = hsc.nr;
+                if (hsc.nvisited >= M) break;
+            }
+            nr = hsc.nr;
+            if (hsc.nvisited != M) {
+                set_error("ruling set covered %llu of %u chains", (unsigned long long)hsc.nvisited, M);
+                return EC_ERR_STATE;
+            }
+            k_rjump_init<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), nr, s->st0.as<RJump>());
+            rounds = 1;
+            while ((1ull << (rounds - 1)) < (unsigned long long)nr) rounds++;
+            rounds = std::min(rounds + 1, 63);
+            RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
+            for (int r = 0; r < rounds; r++)
+                k_rjump<<<grid_for(nr, B), B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], nr, N,
+                                                      r ? &dsc->active[r - 1] : nullptr, &dsc->active[r],
+                                                      &dsc->final_sel, (unsigned)((r + 1) & 1));
+            k_finalize_s<<<grid_for(M, B), B, 0, st>>>(snrec, srec, s->rid.as<uint2>(), s->rlist.as<unsigned int>(),
+                                                      bufs[0], bufs[1], &dsc->final_sel, &dsc->active[rounds - 1], M,
+                                                      s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
+                                                      s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+            k_cycle_len_s<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), srec,
+                                                        bufs[0], bufs[1], &dsc->final_sel, &dsc->active[rounds - 1], nr,
+                                                        s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+            // (3) every node: its chain's key and rank + its offset in the chain
+            k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, SIDX, s->rt_pks.as<unsigned int>(),
+                                                  s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
+                                                  s->RK.as<unsigned int>());
+        }
+    }
+    if (U && !tile_rank) {
         EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, Nn * 8, st));
         EC_CHECK(s->nrec.ensure(Nn * sizeof(NodeRec)));
         unsigned int masks[4] = {31u, 7u, 1u, 0u};
@@ -1985,7 +2139,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         unsigned long long *smask = s->cand.as<unsigned long long>();
         k_starts_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
                                            s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
-                                           s->PM.as<unsigned long long>(), N, bc, smask);
+                                           s->PM.as<unsigned long long>(), N, bc, smask,
+                                           nx ? s->x_in.as<uint8_t>() : nullptr);
         EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
         k_starts_write<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
                                            s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
@@ -2005,11 +2160,35 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             return EC_ERR_STATE;
         }
     }
-    const unsigned int nc = hsc.nstarts;
+    unsigned int nc = hsc.nstarts;
+    unsigned int nsort = nc;
+    if (nx) {  // all_contigs on the components with one-way links, their starts after the others
+        EC_CHECK(s->x_done.ensure(Nn));
+        EC_CHECK(s->x_len.ensure((size_t)nx * 4));
+        EC_CHECK(s->x_m.ensure((size_t)nx * 4));
+        EC_CHECK(s->x_cid.ensure((size_t)nx * 4));
+        EC_HIP(hipMemsetAsync(s->x_done.p, 0, Nn, st));
+        k_x_emulate<<<grid_for(nx, 64), 64, 0, st>>>(
+            s->x_lv.as<unsigned int>(), nx, s->x_par.as<unsigned int>(), s->upal.as<uint8_t>(),
+            s->x_succ.as<unsigned int>(), s->dkey.as<K128>(), k, N, s->dfc.as<unsigned long long>(),
+            s->dft.as<unsigned long long>(), s->x_done.as<uint8_t>(), s->skeys.as<unsigned long long>() + nc,
+            s->svals.as<unsigned int>() + nc, s->x_len.as<unsigned int>(), s->x_m.as<unsigned int>(), &dsc->nxs,
+            &dsc->xbad);
+        unsigned int xs[2] = {0, 0};
+        EC_HIP(hipMemcpyAsync(xs, &dsc->nxs, 8, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (xs[1]) {
+            set_error("a contig walk enters a cycle without its start: the reference's get_contig_forward "
+                      "(referenceAssembler.py:59-77) never returns on this input");
+            return EC_ERR_STATE;
+        }
+        nsort = nc + nx;  // (the emulation's non-starts carry key NONE: sorted past the starts)
+        nc += xs[0];
+    }
     s->stats.n_contigs = nc;
-    if (nc)
+    if (nsort)
         EC_CHECK(sort_pairs(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(),
-                            s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nc));
+                            s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nsort));
     const unsigned int *sorted_nodes = s->svals2.as<unsigned int>();
     EC_CHECK(s->clen.ensure((size_t)(nc + 1) * 8));
     EC_CHECK(s->cwalk.ensure((size_t)std::max(nc, 1u) * sizeof(Walk)));
@@ -2019,7 +2198,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_contig_len<<<grid_for(nc, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(),
                                                    s->RK.as<unsigned int>(), s->PL.as<unsigned int>(), sorted_nodes, nc,
                                                    k, s->cidxOf.as<unsigned int>(), s->clen.as<unsigned long long>(),
-                                                   s->cwalk.as<Walk>());
+                                                   s->cwalk.as<Walk>(), nx ? s->x_len.as<unsigned int>() : nullptr,
+                                                   nx ? s->x_cid.as<unsigned int>() : nullptr);
     }
     EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
     // the total travels with the other results (no round trip here): the character buffer is
@@ -2028,7 +2208,13 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->h_coff.resize(nc + 1));
     EC_HIP(hipMemcpyAsync(&s->h_coff[nc], s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
     mark(s, 2 * EC_STAGE_STARTS + 1);
-    const uint64_t chars_bound = 2ull * U + (uint64_t)nc * (uint64_t)(k - 1);
+    uint64_t chars_bound = 2ull * U + (uint64_t)nc * (uint64_t)(k - 1);
+    if (nx) {  // emulated contigs may overlap: the bound is their exact total
+        unsigned long long tot = 0;
+        EC_HIP(hipMemcpyAsync(&tot, s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        chars_bound = std::max<uint64_t>(chars_bound, tot);
+    }
 
     // ---- emit -----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_EMIT);
@@ -2047,6 +2233,22 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                             N, k, s->chars.as<char>(), std::max<uint64_t>(chars_bound, 1),
                                             s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(),
                                             s->headOf.as<unsigned int>(), s->tailOf.as<unsigned int>(), &dsc->skew);
+    if constexpr (XT) {
+        if (nx) {
+            EC_CHECK(s->x_head.ensure(Nn * 4));
+            EC_CHECK(s->x_tail.ensure(Nn * 4));
+            EC_HIP(hipMemsetAsync(s->x_head.p, 0, Nn * 4, st));
+            EC_HIP(hipMemsetAsync(s->x_tail.p, 0, Nn * 4, st));
+            k_x_emit<<<grid_for(nx, B), B, 0, st>>>(
+                s->x_lv.as<unsigned int>(), s->x_len.as<unsigned int>(), s->x_m.as<unsigned int>(),
+                s->x_cid.as<unsigned int>(), s->skeys.as<unsigned long long>() + hsc.nstarts, nx, s->upal.as<uint8_t>(),
+                s->x_succ.as<unsigned int>(), s->dkey.as<K128>(), k, s->coff.as<unsigned long long>(),
+                s->chars.as<char>(), s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(),
+                s->x_head.as<unsigned int>(), s->x_tail.as<unsigned int>());
+            k_x_heads<<<grid_for(N, B), B, 0, st>>>(N, s->x_head.as<unsigned int>(), s->x_tail.as<unsigned int>(),
+                                                    s->headOf.as<unsigned int>(), s->tailOf.as<unsigned int>());
+        }
+    }
     mark(s, 2 * EC_STAGE_EMIT + 1);
 
     // ---- GFA ------------------------------------------------------------------------------
@@ -2110,6 +2312,132 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     return EC_OK;
 }
 
+// ---- extended alphabet (extended.h) -----------------------------------------------------------
+// c_xa (the symbol table the OpsX kernels read) is one per process: extended-alphabet calls
+// of different sessions are serialised (each call ends with its stream synchronised)
+std::mutex g_xmu;
+
+int x_upload(ec_session *s) {
+    EC_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xa), &s->xa, sizeof(XAlpha), 0, hipMemcpyHostToDevice, s->stream));
+    return EC_OK;
+}
+
+// the symbol table from the bytes present (bit c of pm): A C G T = 0..3, 'N' the segment split
+// (split_n) or an opaque symbol, every other byte an opaque symbol in byte order
+int x_alphabet(ec_session *s, const unsigned int *pm, bool split_n, int k) {
+    XAlpha &xa = s->xa;
+    memset(&xa, 0, sizeof xa);
+    const char *acgt = "ACGT";
+    for (int c = 0; c < 256; c++) xa.code[c] = 0xFE;
+    for (int b = 0; b < 4; b++) xa.code[(int)acgt[b]] = (uint8_t)b, xa.dec[b] = (uint8_t)acgt[b];
+    if (split_n) xa.code[(int)'N'] = 0xFF;
+    unsigned int nsym = 4;
+    for (int c = 0; c < 256; c++)
+        if (((pm[c >> 5] >> (c & 31)) & 1u) && xa.code[c] == 0xFE) {
+            xa.code[c] = (uint8_t)nsym;
+            xa.dec[nsym++] = (uint8_t)c;
+        }
+    xa.nsym = nsym;
+    xa.sb = nsym <= 16 ? 4 : nsym <= 32 ? 5 : 8;
+    if (xa.sb * (unsigned)k > 126) {
+        set_error("the input holds %u symbols besides A/C/G/T%s (%u bits each): k = %d needs %u-bit keys, more than "
+                  "126 (k <= %u for this alphabet)", nsym - 4, split_n ? "/N" : "", xa.sb, k, xa.sb * k, 126 / xa.sb);
+        return EC_ERR_ALPHABET;
+    }
+    EC_CHECK(x_upload(s));
+    s->xalpha = true;
+    return EC_OK;
+}
+
+// all_contigs on a caller's dict holding bytes other than A/C/G/T (ec_assemble_from_kmers)
+int assemble_kmers_extended(ec_session *s, const char *kmers, uint64_t n, int k) {
+    std::lock_guard<std::mutex> lock(g_xmu);
+    unsigned int pm[8] = {};
+    for (uint64_t i = 0; i < n * (uint64_t)k; i++) {
+        const unsigned char c = (unsigned char)kmers[i];
+        pm[c >> 5] |= 1u << (c & 31);
+    }
+    EC_CHECK(x_alphabet(s, pm, false, k));
+    hipStream_t st = s->stream;
+    k_x_kmers_to_agg<<<grid_for(n, 256), 256, 0, st>>>(s->dchars.as<char>(), s->dcounts.as<unsigned int>(), n, k,
+                                                       s->recs2.as<AggW>());
+    unsigned int U = 0;
+    SolidIndexW sidx{};
+    EC_CHECK(phase_merge_w(s, s->recs2.as<AggW>(), n, LLONG_MIN, U, sidx));
+    return phase_graph<OpsX>(s, k, U, sidx);
+}
+
+// reads with bytes other than A/C/G/T/N: symbol table from the bytes present, count into the
+// wide HBM table (128-bit keys of sb-bit symbols), then the graph phase over OpsX
+int assemble_extended(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, int k,
+                      long long limit) {
+    std::lock_guard<std::mutex> lock(g_xmu);
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc;
+    EC_CHECK(s->tmp.ensure(64));
+    unsigned int *present = s->tmp.as<unsigned int>();
+    EC_HIP(hipMemsetAsync(present, 0, 32, st));
+    if (nreads) k_x_alphabet<<<grid_for(nreads, B, 4096), B, 0, st>>>(d_reads, d_off, nreads, present);
+    unsigned int pm[8];
+    EC_HIP(hipMemcpyAsync(pm, present, 32, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(x_alphabet(s, pm, true, k));
+    s->stats.count_variant = 0;
+    s->stats.n_buckets = 0;
+    s->stats.record_bytes = 0;
+    s->stats.n_records = 0;
+    s->stats.n_reads = nreads;
+    // prescan (positions, HyperLogLog of the canonical keys) + count (phase_count_w's table)
+    mark(s, 2 * EC_STAGE_PRESCAN);
+    EC_CHECK(s->hll.ensure(HLL_M * 4));
+    EC_HIP(hipMemsetAsync(s->hll.p, 0, HLL_M * 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->npos, 0, 8, st));
+    EC_HIP(hipMemsetAsync(&dsc->est, 0, 8, st));
+    if (nreads) {
+        k_x_prescan<<<grid_for(nreads, B, 4096), B, 0, st>>>(d_reads, d_off, nreads, k, s->hll.as<unsigned int>(),
+                                                            &dsc->npos);
+        k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<unsigned int>(), HLL_BITS, &dsc->est);
+    }
+    mark(s, 2 * EC_STAGE_PRESCAN + 1);
+    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    const uint64_t P = nreads ? hsc.npos : 0;
+    s->stats.n_positions = P;
+    const double est = nreads ? hsc.est : 0.0;
+    s->stats.n_distinct_est = (uint64_t)llround(est);
+    uint64_t cap = 1024;
+    const double want = std::min((double)P, 1.05 * est) * 1.6 + 1024;
+    while ((double)cap < want) cap <<= 1;
+    for (int attempt = 0;; attempt++) {
+        EC_CHECK(s->table.ensure(cap * sizeof(SlotW)));
+        mark(s, 2 * EC_STAGE_COUNT);
+        k_table_clear_w<<<grid_for(cap, B, 8192), B, 0, st>>>(s->table.as<SlotW>(), cap);
+        EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+        if (nreads) {
+            kmark(s, 3, 0);
+            k_x_count<<<grid_for(nreads, B), B, 0, st>>>(d_reads, d_off, nreads, k, s->table.as<SlotW>(), cap - 1,
+                                                        &dsc->overflow);
+            kmark(s, 3, 1);
+        }
+        mark(s, 2 * EC_STAGE_COUNT + 1);
+        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (!hsc.overflow) break;
+        if (attempt >= 4) {
+            set_error("hash table overflow at capacity %llu", (unsigned long long)cap);
+            return EC_ERR_CAPACITY;
+        }
+        cap <<= 2;
+        s->stats.table_retries++;
+    }
+    unsigned int U = 0;
+    SolidIndexW sidx{};
+    EC_CHECK(finish_wide(s, cap, limit, U, sidx));
+    return phase_graph<OpsX>(s, k, U, sidx);
+}
+
 int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads, int k, int limit,
              unsigned flags) {
     EC_CHECK(begin_call(s, k, flags));
@@ -2117,11 +2445,18 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
     if (k > 32) {
         SolidIndexW sidx{};
         EC_CHECK(pipe_all(s));
-        EC_CHECK(phase_count_w(s, d_reads, d_off, nreads, 0, k, (long long)limit, U, sidx));
+        const int rc = phase_count_w(s, d_reads, d_off, nreads, 0, k, (long long)limit, U, sidx);
+        if (rc == EC_ERR_ALPHABET) return assemble_extended(s, d_reads, d_off, nreads, k, (long long)limit);
+        EC_CHECK(rc);
         return phase_graph<OpsW>(s, k, U, sidx);
     }
     SolidIndex sidx{};
-    EC_CHECK(phase_count(s, d_reads, d_off, nreads, 0, k, (long long)limit, flags, U, sidx));
+    const int rc = phase_count(s, d_reads, d_off, nreads, 0, k, (long long)limit, flags, U, sidx);
+    if (rc == EC_ERR_ALPHABET) {  // bytes other than A/C/G/T/N: opaque symbols (extended.h)
+        EC_CHECK(pipe_all(s));
+        return assemble_extended(s, d_reads, d_off, nreads, k, (long long)limit);
+    }
+    EC_CHECK(rc);
     return phase_graph<Ops64>(s, k, U, sidx);
 }
 
@@ -2251,7 +2586,10 @@ int ec_session_destroy(ec_session *s) {
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
                      &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->bnp, &s->rbc,
-                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk};
+                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
+                     &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
+                     &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->h_coff.release();
@@ -2426,7 +2764,14 @@ int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts) {
                         s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nd));
     EC_CHECK(s->dchars.ensure((size_t)nd * s->k));
     EC_CHECK(s->dcounts.ensure((size_t)nd * 4));
-    if (s->k > 32)
+    std::unique_lock<std::mutex> xlock(g_xmu, std::defer_lock);
+    if (s->xalpha) {  // (c_xa may hold another session's alphabet by now)
+        xlock.lock();
+        EC_CHECK(x_upload(s));
+        k_dict_render<OpsX><<<grid_for(nd, B), B, 0, st>>>(s->svals2.as<unsigned int>(), nd, s->dkey.as<K128>(),
+                                                          s->dcnt.as<unsigned int>(), s->k, s->dchars.as<char>(),
+                                                          s->dcounts.as<unsigned int>());
+    } else if (s->k > 32)
         k_dict_render<OpsW><<<grid_for(nd, B), B, 0, st>>>(s->svals2.as<unsigned int>(), nd, s->dkey.as<K128>(),
                                                           s->dcnt.as<unsigned int>(), s->k, s->dchars.as<char>(),
                                                           s->dcounts.as<unsigned int>());
@@ -2704,10 +3049,8 @@ int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *cou
         unsigned long long bad = 0;
         EC_HIP(hipMemcpyAsync(&bad, &dsc->bad, 8, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
-        if (bad != ~0ull) {
-            set_error("dict entry %llu holds a byte outside ACGT", bad);
-            return EC_ERR_ALPHABET;
-        }
+        if (bad != ~0ull)  // bytes other than A/C/G/T: opaque symbols (extended.h)
+            return assemble_kmers_extended(s, kmers, n, k);
     }
     unsigned int U = 0;
     if (wide) {

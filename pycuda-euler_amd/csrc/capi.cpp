@@ -47,6 +47,7 @@ void refresh_knobs() {
         k.no_skb3 = flag("EULERHIP_NO_SKB3");
         k.sk2_claim = num("EULERHIP_SK2_CLAIM", 0);
         k.verbose = flag("EULERHIP_VERBOSE");
+        k.rank = num("EULERHIP_RANK", -1);
     }
     g_knobs = k;
 }

@@ -44,6 +44,7 @@ struct Knobs {
     bool no_skb3 = false;       // EULERHIP_NO_SKB3: k_skbucket's 8192-bucket plan instead of k_skbucket3 (A/B)
     bool no_slot_groups = false; // EULERHIP_NO_SLOT_GROUPS: k_skpart_w read groups not rounded to resident slots (A/B)
     bool verbose = false;       // EULERHIP_VERBOSE: count-path fallbacks on stderr
+    int rank = -1;              // EULERHIP_RANK: list ranking 0 = tile contraction (rank_tile.h), 1 = node ruling set
 };
 void refresh_knobs();
 const Knobs &kn();

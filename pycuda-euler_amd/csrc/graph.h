@@ -95,6 +95,7 @@ struct Ops64 {
     }
     __device__ static inline uint32_t base(const K &x, int k, int i) { return (uint32_t)(x >> (2 * (k - 1 - i))) & 3u; }
     __device__ static inline uint32_t last(const K &x) { return (uint32_t)x & 3u; }
+    __device__ static inline char chr(uint32_t b) { return "ACGT"[b]; }  // symbol code -> byte
 };
 struct OpsW {
     using K = K128;
@@ -109,6 +110,7 @@ struct OpsW {
     }
     __device__ static inline uint32_t base(const K &x, int k, int i) { return base_at128(x, k, i); }
     __device__ static inline uint32_t last(const K &x) { return (uint32_t)x.lo & 3u; }
+    __device__ static inline char chr(uint32_t b) { return "ACGT"[b]; }
 };
 
 // canonical K128 key -> dense solid id in the wide table
@@ -579,8 +581,9 @@ __device__ inline unsigned long long path_min(const unsigned int *PK, const unsi
 // event over the path and its twin path (= the first dict entry not yet `done`).
 __device__ inline bool is_start(const uint8_t *upal, const unsigned long long *dfc, const unsigned long long *dft,
                                 const unsigned int *PK, const unsigned long long *PM, unsigned int x,
-                                unsigned long long &f) {
+                                unsigned long long &f, const uint8_t *excl = nullptr) {
     if ((x & 1) && upal[x >> 1]) return false;
+    if (excl && excl[x >> 1]) return false;  // (extended.h: a component with one-way links)
     f = first_event(dfc, dft, x);
     const unsigned long long a = path_min(PK, PM, x);
     const unsigned long long b = path_min(PK, PM, twin_node(upal, x));
@@ -593,7 +596,7 @@ __device__ inline bool is_start(const uint8_t *upal, const unsigned long long *d
 __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const unsigned long long *dfc,
                                                       const unsigned long long *dft, const unsigned int *PK,
                                                       const unsigned long long *PM, unsigned int N, unsigned int *bc,
-                                                      unsigned long long *smask) {
+                                                      unsigned long long *smask, const uint8_t *excl = nullptr) {
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
     unsigned int c = 0;
@@ -602,7 +605,7 @@ __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const
     for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
         const uint64_t t = t0 + threadIdx.x;
         unsigned long long f;
-        const bool sel = t < c1 && is_start(upal, dfc, dft, PK, PM, (unsigned int)t, f);
+        const bool sel = t < c1 && is_start(upal, dfc, dft, PK, PM, (unsigned int)t, f, excl);
         const unsigned long long m = __ballot(sel);
         if ((threadIdx.x & 63) == 0 && t < c1) smask[t >> 6] = m;
         c += sel;
@@ -704,9 +707,16 @@ __device__ inline Walk walk_of(const uint8_t *upal, const unsigned int *PK, cons
 __global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
                                                     const unsigned int *PL, const unsigned int *sorted_nodes,
                                                     unsigned int nc, int k, unsigned int *cidxOf,
-                                                    unsigned long long *clen, Walk *cwalk) {
+                                                    unsigned long long *clen, Walk *cwalk,
+                                                    const unsigned int *xlen = nullptr, unsigned int *xcid = nullptr) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int s = sorted_nodes[i];
+        if (xlen && (s & 0x80000000u)) {  // a start the extended path's emulation found (extended.h)
+            const unsigned int j = s & 0x7FFFFFFFu;
+            clen[i] = (unsigned long long)(k - 1) + xlen[j];
+            xcid[j] = (unsigned int)i;
+            continue;
+        }
         cidxOf[PK[s] & ~CYC] = (unsigned int)i;
         const Walk w = walk_of(upal, PK, RK, PL, s);
         clen[i] = (unsigned long long)(k - 1) + w.len;
@@ -756,11 +766,11 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
         const typename Ops::K code = node_code<Ops>(dkey, x, k);
         char *dst = chars + coff[ci];
         if (pos == 0) {
-            for (int i = 0; i < k; i++) dst[i] = "ACGT"[Ops::base(code, k, i)];
+            for (int i = 0; i < k; i++) dst[i] = Ops::chr(Ops::base(code, k, i));
             cfirst[ci] = x;
             headOf[x] = ci;
         } else {
-            dst[k - 1 + pos] = "ACGT"[Ops::last(code)];
+            dst[k - 1 + pos] = Ops::chr(Ops::last(code));
         }
         if ((unsigned long long)pos == (unsigned long long)w.len - 1) {
             clast[ci] = x;
@@ -837,7 +847,7 @@ __global__ void __launch_bounds__(256) k_dict_render(const unsigned int *nodes, 
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = nodes[i];
         const typename Ops::K c = node_code<Ops>(dkey, x, k);
-        for (int p = 0; p < k; p++) out[i * k + p] = "ACGT"[Ops::base(c, k, p)];
+        for (int p = 0; p < k; p++) out[i * k + p] = Ops::chr(Ops::base(c, k, p));
         counts[i] = dcnt[x >> 1];
     }
 }

@@ -1,0 +1,420 @@
+// rank_tile.h -- list ranking of the successor paths / cycles by tile contraction (round 4).
+//
+// The dense ids of the solid k-mers come out of the count bucket by bucket, each bucket a
+// contiguous id range, and on the super-k-mer path a bucket holds whole minimizers: ~90 % of
+// the links join two k-mers of one bucket, so they stay inside a tile of TN consecutive
+// oriented node ids.  Ranking therefore runs in three steps:
+//   1. k_tile_chains, one workgroup per tile: the tile's successors staged in LDS; the chains
+//      of in-tile links are ranked there by pointer jumping (ceil(log2 TN) rounds, no HBM
+//      traffic); a chain closed into a cycle inside the tile is finished on the spot (key = its
+//      smallest node); every other chain becomes one weighted super node {head, length, min
+//      first event, successor of its tail};
+//   2. the super nodes (compacted in tile order) are ranked by the ruling set of graph.h with
+//      weights: rulers walk their segments summing chain lengths (k_walk_s), the rulers by
+//      weighted Wyllie (k_rjump, shared), cycles across tiles keyed by their smallest ruler;
+//   3. k_expand: every node's path key and rank = its chain's + its offset in the chain.
+// The outputs are graph.h's PK / RK / PL / PM, so starts, emission and GFA are unchanged.
+// HBM traffic per node: its successor and first event read once in tile order, 8 bytes of
+// chain position written and read back, PK / RK written; the random accesses of the ruler walk
+// touch only the ~N/9 super nodes (one 16-B record each).
+#pragma once
+#include "graph.h"
+
+namespace ec {
+
+constexpr int RT_TN = 2048;        // oriented nodes per tile
+constexpr int RT_NT = 512;         // threads per tile workgroup
+constexpr int RT_PER = RT_TN / RT_NT;
+constexpr int RT_ROUNDS = 11;      // 2^11 = RT_TN: chains and cycles of a tile are covered
+constexpr unsigned int RT_FIN = 0x80000000u;  // LH flag: node of an in-tile cycle, finished
+constexpr uint16_t RT_NONE = 0xFFFFu;
+
+// super node of a chain: head node, successor of its tail (node id or NONE), length, min event
+struct alignas(16) SuperRec {
+    unsigned int head, succ, w, pad;
+    unsigned long long fmin;
+    unsigned long long pad2;
+};
+// the super list's walk record
+struct alignas(16) SNodeRec {
+    unsigned int succ;  // super index or NONE
+    unsigned int w;     // chain length (nodes)
+    unsigned long long fev;  // min first event over the chain
+};
+
+__global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, const unsigned int *succ, unsigned int N,
+                                                       const unsigned long long *dfc, const unsigned long long *dft,
+                                                       unsigned int *LH, unsigned int *LR, unsigned long long *tcnt,
+                                                       SuperRec *scratch, unsigned int *PK, unsigned int *RK,
+                                                       unsigned int *PL, unsigned long long *PM) {
+    __shared__ uint16_t s_ls[RT_TN], s_lp[RT_TN], s_p[RT_TN], s_mn[RT_TN];
+    __shared__ unsigned int s_d[RT_TN], s_cl[RT_TN];
+    __shared__ unsigned long long s_cm[RT_TN];
+    __shared__ unsigned int s_wsum[RT_NT / 64];
+    const unsigned int tile = blockIdx.x, base = tile * RT_TN, tid = threadIdx.x;
+    unsigned int ext[RT_PER];
+    unsigned long long fev[RT_PER];
+    bool valid[RT_PER];
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        const unsigned int i = tid + q * RT_NT, x = base + i;
+        valid[q] = x < N && !((x & 1) && upal[x >> 1]);
+        const unsigned int s = valid[q] ? succ[x] : NONE32;
+        fev[q] = valid[q] ? first_event(dfc, dft, x) : NONE64;
+        const bool in = s != NONE32 && s / RT_TN == tile;
+        s_ls[i] = in ? (uint16_t)(s - base) : RT_NONE;
+        ext[q] = in ? NONE32 : s;
+        s_lp[i] = RT_NONE;
+        s_cl[i] = 0;
+        s_cm[i] = NONE64;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        const unsigned int i = tid + q * RT_NT;
+        if (s_ls[i] != RT_NONE) s_lp[s_ls[i]] = (uint16_t)i;  // (in-degree <= 1)
+    }
+    __syncthreads();
+    // pointer jumping towards the chain head (heads point to themselves); s_mn: the smallest
+    // node passed (on a cycle, after the rounds: the cycle's smallest node)
+    uint16_t p[RT_PER], mn[RT_PER];
+    unsigned int d[RT_PER];
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        const unsigned int i = tid + q * RT_NT;
+        const uint16_t lp = s_lp[i];
+        p[q] = lp == RT_NONE ? (uint16_t)i : lp;
+        d[q] = lp == RT_NONE ? 0u : 1u;
+        mn[q] = p[q] < i ? p[q] : (uint16_t)i;
+        s_p[i] = p[q];
+        s_d[i] = d[q];
+        s_mn[i] = mn[q];
+    }
+    __syncthreads();
+    for (int r = 0; r < RT_ROUNDS; r++) {
+#pragma unroll
+        for (int q = 0; q < RT_PER; q++) {
+            const uint16_t a = p[q];
+            d[q] += s_d[a];
+            const uint16_t m2 = s_mn[a];
+            mn[q] = m2 < mn[q] ? m2 : mn[q];
+            p[q] = s_p[a];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RT_PER; q++) {
+            const unsigned int i = tid + q * RT_NT;
+            s_p[i] = p[q];
+            s_d[i] = d[q];
+            s_mn[i] = mn[q];
+        }
+        __syncthreads();
+    }
+    // nodes of in-tile cycles: their "head" still has a predecessor.  Rank them again from the
+    // cycle's smallest node (the cycle cut in front of it)
+    bool cyc[RT_PER];
+    bool anyc = false;
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        const unsigned int i = tid + q * RT_NT;
+        cyc[q] = valid[q] && s_lp[p[q]] != RT_NONE;
+        anyc |= cyc[q];
+    }
+    if (__syncthreads_or(anyc)) {
+#pragma unroll
+        for (int q = 0; q < RT_PER; q++) {
+            const unsigned int i = tid + q * RT_NT;
+            if (cyc[q]) {
+                const bool key = i == mn[q];
+                p[q] = key ? (uint16_t)i : s_lp[i];
+                d[q] = key ? 0u : 1u;
+            }
+            s_p[i] = p[q];
+            s_d[i] = d[q];
+        }
+        __syncthreads();
+        for (int r = 0; r < RT_ROUNDS; r++) {
+#pragma unroll
+            for (int q = 0; q < RT_PER; q++) {
+                if (!cyc[q]) continue;
+                const uint16_t a = p[q];
+                d[q] += s_d[a];
+                p[q] = s_p[a];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < RT_PER; q++) {
+                const unsigned int i = tid + q * RT_NT;
+                if (!cyc[q]) continue;
+                s_p[i] = p[q];
+                s_d[i] = d[q];
+            }
+            __syncthreads();
+        }
+    }
+    // per chain / cycle at its head: length, min first event; the successor of a chain's tail
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        if (!valid[q]) continue;
+        const uint16_t h = p[q];
+        atomicMax(&s_cl[h], d[q] + 1);
+        if (fev[q] < s_cm[h]) atomicMin(&s_cm[h], fev[q]);
+    }
+    __syncthreads();
+    unsigned int nh = 0;  // chain heads of this thread (super nodes)
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        const unsigned int i = tid + q * RT_NT, x = base + i;
+        if (!valid[q]) {
+            if (x < N) LH[x] = NONE32;
+            continue;
+        }
+        const unsigned int h = base + p[q];
+        if (cyc[q]) {  // finished here: path key = the cycle's smallest node
+            LH[x] = h | RT_FIN;
+            PK[x] = h | CYC;
+            RK[x] = d[q];
+            if (d[q] == 0) {
+                PL[h] = s_cl[p[q]];
+                PM[h] = s_cm[p[q]];
+            }
+        } else {
+            LH[x] = h;
+            nh += d[q] == 0;
+        }
+        LR[x] = d[q];
+    }
+    // compaction of the heads in node order (q-major: node i = tid + q * NT)
+    const unsigned int lane = tid & 63, wid = tid >> 6;
+    unsigned int off = 0;
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        const unsigned int i = tid + q * RT_NT;
+        const bool hd = valid[q] && !cyc[q] && d[q] == 0;
+        const unsigned long long m = __ballot(hd);
+        if (lane == 0) s_wsum[wid] = (unsigned int)__popcll(m);
+        __syncthreads();
+        unsigned int o = off;
+        for (unsigned int w = 0; w < wid; w++) o += s_wsum[w];
+        unsigned int tot = 0;
+        for (unsigned int w = 0; w < RT_NT / 64; w++) tot += s_wsum[w];
+        if (hd) {
+            const unsigned int j = o + (unsigned int)__popcll(m & ((1ull << lane) - 1));
+            // the chain's tail: the node at distance len - 1 from the head has no in-tile successor;
+            // its successor is filled in below by the tail's thread
+            SuperRec r;
+            r.head = base + i;
+            r.succ = NONE32;
+            r.w = s_cl[i];
+            r.pad = 0;
+            r.fmin = s_cm[i];
+            r.pad2 = 0;
+            scratch[(uint64_t)tile * RT_TN + j] = r;
+            s_ls[i] = (uint16_t)j;  // (reused: head -> its index among the tile's heads)
+        }
+        off += tot;
+        __syncthreads();
+    }
+    // a chain's tail writes its external successor into the chain's record
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        if (!valid[q] || cyc[q]) continue;
+        const unsigned int i = tid + q * RT_NT;
+        if (d[q] + 1 == s_cl[p[q]] && ext[q] != NONE32) scratch[(uint64_t)tile * RT_TN + s_ls[p[q]]].succ = ext[q];
+        (void)i;
+    }
+    if (tid == 0) tcnt[tile] = off;
+}
+
+// tile heads -> the compact super list (tbase = exclusive scan of tcnt); SIDX[head] = its index
+__global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, const unsigned long long *tcnt,
+                                                      const unsigned long long *tbase, SuperRec *srec,
+                                                      unsigned int *SIDX) {
+    const unsigned int t = blockIdx.x;
+    const unsigned int n = (unsigned int)tcnt[t];
+    const unsigned long long b = tbase[t];
+    for (unsigned int j = threadIdx.x; j < n; j += blockDim.x) {
+        const SuperRec r = scratch[(uint64_t)t * RT_TN + j];
+        srec[b + j] = r;
+        SIDX[r.head] = (unsigned int)(b + j);
+    }
+}
+
+// super successors as super indices (a tail's external successor starts its own chain), the
+// walk records, and which super nodes have a predecessor (the path heads: none)
+__global__ void __launch_bounds__(256) k_super_link(const SuperRec *srec, unsigned int M, const unsigned int *SIDX,
+                                                    SNodeRec *nrec, uint8_t *hasp) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < M; t += (uint64_t)gridDim.x * blockDim.x) {
+        const SuperRec r = srec[t];
+        const unsigned int s = r.succ == NONE32 ? NONE32 : SIDX[r.succ];
+        SNodeRec o;
+        o.succ = s;
+        o.w = r.w;
+        o.fev = r.fmin;
+        nrec[t] = o;
+        if (s != NONE32) hasp[s] = 1;
+    }
+}
+
+// ruler selection on the super list (graph.h k_rulers_count / k_rulers without palindromes)
+__device__ inline bool sruler_sel(const uint8_t *hasp, const uint2 *rid, unsigned int i, unsigned int smask,
+                                  int first) {
+    if (rid[i].x != NONE32) return false;
+    return (first && !hasp[i]) || ruler_hash(i, smask);
+}
+__global__ void __launch_bounds__(256) k_srulers_count(const uint8_t *hasp, unsigned int M, unsigned int smask,
+                                                       int first, const uint2 *rid, unsigned int *bc) {
+    const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
+    const uint64_t c1 = c0 + RULER_CHUNK < M ? c0 + RULER_CHUNK : M;
+    unsigned int c = 0;
+    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) c += sruler_sel(hasp, rid, (unsigned int)t, smask, first);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    __shared__ unsigned int w[4];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bc[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+}
+__global__ void __launch_bounds__(256) k_srulers(const uint8_t *hasp, unsigned int M, unsigned int smask, int first,
+                                                 const unsigned int *bs, const unsigned int *nr, uint2 *rid,
+                                                 unsigned int *rlist) {
+    __shared__ unsigned int wsum[4];
+    const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
+    const uint64_t c1 = c0 + RULER_CHUNK < M ? c0 + RULER_CHUNK : M;
+    unsigned int base = *nr + (blockIdx.x ? bs[blockIdx.x - 1] : 0u);
+    const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
+        const uint64_t t = t0 + threadIdx.x;
+        const bool sel = t < c1 && sruler_sel(hasp, rid, (unsigned int)t, smask, first);
+        const unsigned long long m = __ballot(sel);
+        if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
+        __syncthreads();
+        unsigned int off = base;
+        for (unsigned int q = 0; q < wid; q++) off += wsum[q];
+        const unsigned int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (sel) {
+            const unsigned int i = off + (unsigned int)__popcll(m & ((1ull << lane) - 1));
+            rlist[i] = (unsigned int)t;
+            rid[t] = make_uint2(i, 0u);
+        }
+        base += tot;
+        __syncthreads();
+    }
+}
+
+// each ruler walks its segment of super nodes, offsets in nodes (chain lengths summed)
+__global__ void __launch_bounds__(256) k_walk_s(const SNodeRec *nrec, const unsigned int *rlist, unsigned int r0,
+                                                const unsigned int *nr, unsigned int smask, uint2 *rid,
+                                                unsigned int *nextR, RJump *rs, unsigned long long *nvisited) {
+    const unsigned int r1 = *nr;
+    unsigned long long seen = 0;
+    for (uint64_t t = r0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < r1; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int i = (unsigned int)t;
+        unsigned int v = rlist[i];
+        const SNodeRec a = nrec[v];
+        unsigned long long fm = a.fev;
+        unsigned int j = 0, wl = a.w, cnt = 1, nx = NONE32;
+        unsigned int w = a.succ;
+        for (;;) {
+            if (w == NONE32) break;
+            if (ruler_hash(w, smask)) {  // maybe the next ruler
+                const unsigned int q = rid[w].x;
+                if (q != NONE32) {
+                    nx = q;
+                    break;
+                }
+            }
+            v = w;
+            j += wl;
+            const SNodeRec b = nrec[v];
+            w = b.succ;
+            wl = b.w;
+            rid[v] = make_uint2(i, j);
+            fm = b.fev < fm ? b.fev : fm;
+            cnt++;
+        }
+        nextR[i] = nx;
+        RJump r;
+        r.a = NONE32;  // set from prevR by k_rjump_init
+        r.s = 0;
+        r.h = i;
+        r.cm = rlist[i];
+        r.cd = 0;
+        r.len = j + wl;  // nodes of the segment
+        r.fm = fm;
+        rs[i] = r;
+        seen += cnt;
+    }
+    for (int o = 32; o > 0; o >>= 1) seen += __shfl_down(seen, o);
+    __shared__ unsigned long long bseen[4];
+    if ((threadIdx.x & 63) == 0) bseen[threadIdx.x >> 6] = seen;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long v = bseen[0] + bseen[1] + bseen[2] + bseen[3];
+        if (v) atomicAdd(nvisited, v);
+    }
+}
+
+// per super node: path key (head node of the path, or the cycle's smallest ruler's head node |
+// CYC) and rank of its chain's head; the path's length / min event at the key node
+__global__ void __launch_bounds__(256) k_finalize_s(const SNodeRec *nrec, const SuperRec *srec, const uint2 *rid,
+                                                    const unsigned int *rlist, const RJump *rs0, const RJump *rs1,
+                                                    const unsigned int *sel, const unsigned int *unconverged,
+                                                    unsigned int M, unsigned int *PKs, unsigned int *RKs,
+                                                    unsigned int *PL, unsigned long long *PM) {
+    const bool bad = *unconverged != 0;  // (the host reports it; placeholders stay in range)
+    const RJump *rs = (*sel & 1) ? rs1 : rs0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < M; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int v = (unsigned int)t;
+        if (bad) {
+            PKs[v] = srec[v].head;
+            RKs[v] = 0;
+            continue;
+        }
+        const uint2 ro = rid[v];
+        const RJump r = rs[ro.x];
+        if (r.a == NONE32) {  // path
+            const unsigned int pk = srec[rlist[r.h]].head, rk = r.s + ro.y;
+            PKs[v] = pk;
+            RKs[v] = rk;
+            if (nrec[v].succ == NONE32) {  // tail chain: its ruler's window spans the path
+                PL[pk] = rk + nrec[v].w;
+                PM[pk] = r.fm;
+            }
+        } else {
+            PKs[v] = srec[r.cm].head | CYC;
+            RKs[v] = r.cd + ro.y;
+        }
+    }
+}
+__global__ void __launch_bounds__(256) k_cycle_len_s(const unsigned int *nextR, const unsigned int *rlist,
+                                                     const SuperRec *srec, const RJump *rs0, const RJump *rs1,
+                                                     const unsigned int *sel, const unsigned int *unconverged,
+                                                     unsigned int nr, unsigned int *PL, unsigned long long *PM) {
+    if (*unconverged) return;
+    const RJump *rs = (*sel & 1) ? rs1 : rs0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
+        const RJump r = rs[t];
+        if (r.a == NONE32) continue;
+        const unsigned int n = nextR[t];
+        if (n != NONE32 && rlist[n] == r.cm) {
+            const unsigned int key = srec[r.cm].head;
+            PL[key] = r.cd + r.len;
+            PM[key] = r.fm;
+        }
+    }
+}
+
+// every node: its chain's path key and rank + its offset in the chain
+__global__ void __launch_bounds__(256) k_expand(const unsigned int *LH, const unsigned int *LR, unsigned int N,
+                                                const unsigned int *SIDX, const unsigned int *PKs,
+                                                const unsigned int *RKs, unsigned int *PK, unsigned int *RK) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int h = LH[t];
+        if (h == NONE32 || (h & RT_FIN)) continue;  // palindrome twin / in-tile cycle (done)
+        const unsigned int si = SIDX[h];
+        PK[t] = PKs[si];
+        RK[t] = RKs[si] + LR[t];
+    }
+}
+
+}  // namespace ec

@@ -13,6 +13,11 @@ Fixtures written (all plain JSON, data only):
                  even-k palindromes / hairpins, lowercase + IUPAC pass-through, limit variants
   fuzz.json      seeded random small cases (low-complexity alphabets force branching,
                  cycles, Moebius paths and palindromes)
+  extended.json  reads with bytes outside {A,C,G,T,N} (soft-masked lowercase runs, IUPAC codes,
+                 lowercase n): opaque symbols that are their own complement (twin:7-10), odd-k
+                 palindromes, and k-mers with an opaque first symbol whose one fw neighbour has a
+                 different single bw neighbour (one-way links, get_contig_forward:63-73);
+                 cases where the reference's walk never returns are skipped (alarm)
   kat.json       known-answer values for the per-kernel rows (E1/E2/E3/H1) + the
                  pinned hash_tk.txt layout summary (src/hash_tk.txt)
 
@@ -150,6 +155,71 @@ def fuzz_cases(ra, n=400):
     return cases
 
 
+def extended_cases(ra, n=240):
+    import signal
+
+    def on_alarm(*a):
+        raise TimeoutError
+
+    signal.signal(signal.SIGALRM, on_alarm)
+    cases = []
+    rng = np.random.default_rng(4711)
+    lower = str.maketrans("ACGT", "acgt")
+    iupac = "RYKMSWBDHVrykmswbdhvn"
+    i = 0
+    skipped = 0
+    while len(cases) < n:
+        i += 1
+        k = int(rng.integers(3, 14))
+        mode = len(cases) % 5
+        g = rand_seq(rng, int(rng.integers(20, 150)), "ACGT", p=[0.4, 0.2, 0.2, 0.2] if i % 3 == 0 else None)
+        L = int(rng.integers(max(2, k), k + 25))
+        circ = bool(rng.random() < 0.25)
+        rs = sample_reads(rng, g, int(rng.integers(2, 40)), L, circular=circ)
+        if mode == 0:    # soft-masked runs (lowercase), as in repeat-masked FASTA
+            out = []
+            for r in rs:
+                if rng.random() < 0.6:
+                    a = int(rng.integers(0, len(r) + 1))
+                    b = int(rng.integers(a, len(r) + 1))
+                    r = r[:a] + r[a:b].translate(lower) + r[b:]
+                out.append(r)
+            rs = out
+        elif mode == 1:  # sparse IUPAC / lowercase n bytes
+            rs = ["".join(iupac[int(rng.integers(0, len(iupac)))] if rng.random() < 0.04 else c for c in r)
+                  for r in rs]
+        elif mode == 2:  # one-way links: a read copy whose first base is lowercased
+            out = list(rs)
+            for r in rs[: max(1, len(rs) // 3)]:
+                j = int(rng.integers(0, max(1, len(r) - k)))
+                t = r[j:]
+                if t:
+                    out += [t[0].lower() + t[1:]] * int(rng.integers(1, 3))
+            rs = out
+        elif mode == 3:  # odd-k palindromes around an opaque middle symbol
+            a = rand_seq(rng, int(rng.integers(1, 8)))
+            mid = iupac[int(rng.integers(0, len(iupac)))]
+            pal = a + mid + rc(a)
+            rs = rs + [rand_seq(rng, 4) + pal + rand_seq(rng, 4) for _ in range(3)] + [pal] * 2
+        else:            # everything at once, with N splits
+            rs = ["".join("N" if rng.random() < 0.03 else
+                          (c.lower() if rng.random() < 0.15 else
+                           (iupac[int(rng.integers(0, len(iupac)))] if rng.random() < 0.03 else c)) for c in r)
+                  for r in rs]
+        rs = rs + rs[: len(rs) // 2]  # coverage: most k-mers seen twice
+        lim = 1 if rng.random() < 0.85 else int(rng.integers(0, 3))
+        signal.alarm(2)
+        try:
+            c = run_case(ra, rs, k, limit=lim, name=f"ext{len(cases)}")
+        except TimeoutError:
+            skipped += 1
+            continue
+        finally:
+            signal.alarm(0)
+        cases.append(c)
+    return cases, skipped
+
+
 def kat_values():
     """Known answers for the per-kernel rows, computed by the definitions in SURVEY §8a rows
     E1 (src/pyencode.py:43-74), E2 (:110-133), E3 intended (:171-207), H1 (src/pygpuhash.py:32-35),
@@ -177,6 +247,12 @@ def kat_values():
 
 def main():
     ra = load_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "extended":  # (added in round 4: only this file)
+        cases, skipped = extended_cases(ra)
+        with open(os.path.join(HERE, "extended.json"), "w") as f:
+            json.dump({"cases": cases, "skipped_nonterminating": skipped}, f, separators=(",", ":"))
+        print("extended.json", len(cases), "cases;", skipped, "skipped (the reference's walk does not return)")
+        return
     reads = [l.strip() for l in open(os.path.join(REF, "tests", "g200reads.fa")) if not l.startswith(">")]
     g200 = [run_case(ra, reads, k, name=f"g200_k{k}") for k in (9, 11, 15, 20, 21)]
     # also the even / small k on g200 (palindromes exist at even k)

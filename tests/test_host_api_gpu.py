@@ -61,11 +61,25 @@ def test_all_contigs_any_dict_order(asm, seed):
     assert [[[list(x) for x in G[i][0]], [list(x) for x in G[i][1]]] for i in range(len(r))] == ml
 
 
+EXT = golden_cases("synthetic.json", alphabet="extended") + golden_cases("extended.json", alphabet="all")[::4]
+
+
+@pytest.mark.parametrize("case", EXT, ids=[c["name"] for c in EXT])
+def test_all_contigs_extended_dict(asm, case):
+    """all_contigs on build()'s dict of reads with opaque bytes (a caller's dict of arbitrary
+    strings: ec_assemble_from_kmers on the extended alphabet) gives the reference's contigs and G"""
+    k = case["k"]
+    d = collections.OrderedDict((x, v) for x, v in case["d"])
+    G, r = asm.all_contigs(d, k)
+    assert r == case["contigs"]
+    assert [[[list(x) for x in G[i][0]], [list(x) for x in G[i][1]]] for i in range(len(r))] == case["links"]
+
+
 def test_all_contigs_rejects_bad_input(asm):
     import eulerhip
 
-    with pytest.raises(eulerhip.AlphabetError):
-        asm.all_contigs({"ACGR": 2, "RCGT": 2}, 4)
+    G, r = asm.all_contigs({"ACGR": 2, "RCGT": 2}, 4)  # opaque R: its own complement, no links
+    assert r == ["ACGR", "RCGT"] and G == {0: ([], []), 1: ([], [])}
     with pytest.raises(eulerhip.EulerHipError):
         asm.all_contigs({"ACG": 2}, 4)
     assert asm.all_contigs({}, 5) == ({}, [])

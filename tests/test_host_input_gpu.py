@@ -71,19 +71,22 @@ def test_packed_ragged_reads_vs_oracle(gpu_session, monkeypatch, chunks):
         _same(gpu_session.fetch(k), ref, rl)
 
 
-def test_packed_alphabet_error(gpu_session, monkeypatch):
-    """a byte outside {A,C,G,T,N} travels as an exception and is rejected as in ASCII input"""
+def test_packed_extended_alphabet(gpu_session, monkeypatch):
+    """a byte outside {A,C,G,T,N} travels as an exception and, as in ASCII input, is an opaque
+    symbol (extended.h): both host-input paths equal the oracle's string-keyed restatement"""
     monkeypatch.setenv("EULERHIP_HOST_CHUNKS", "3")
     buf, off = make_reads(20_000, 4_000, 100, 7100)
     buf = buf.copy()
     buf[250_123] = ord("a")
+    buf[[5, 300_001, 399_999]] = [ord("R"), ord("n"), ord("y")]
     pr = eulerhip.pack_2bit(buf, off)
-    assert list(pr.exc_pos) == [250_123] and list(pr.exc_byte) == [ord("a")]
-    with pytest.raises(eulerhip.AlphabetError):
-        gpu_session.run_packed_host(pr, 31, 1)
-    with pytest.raises(eulerhip.AlphabetError):
-        gpu_session.run_host(buf, off, 31, 1)
-    # the session still works afterwards (the pipeline was drained)
+    assert list(pr.exc_pos) == [5, 250_123, 300_001, 399_999]
+    ref, rl = _ref(buf, off, 31)
+    gpu_session.run_packed_host(pr, 31, 1)
+    _same(gpu_session.fetch(31), ref, rl)
+    gpu_session.run_host(buf, off, 31, 1)
+    _same(gpu_session.fetch(31), ref, rl)
+    # the session still works afterwards on ordinary input (the pipeline was drained)
     buf2, off2 = make_reads(20_000, 4_000, 100, 7101)
     ref, rl = _ref(buf2, off2, 31)
     gpu_session.run_packed_host(eulerhip.pack_2bit(buf2, off2), 31, 1)

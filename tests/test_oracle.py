@@ -8,6 +8,7 @@ from conftest import golden_cases
 from model_parallel import model_assemble
 
 CASES = golden_cases("g200.json", "synthetic.json", "fuzz.json")
+ALL = golden_cases("g200.json", "synthetic.json", "fuzz.json", alphabet="all")
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
@@ -26,10 +27,24 @@ def test_parallel_model_matches_reference(case):
     assert g == case["links"]
 
 
-def test_oracle_rejects_extended_alphabet():
-    for case in golden_cases("synthetic.json", alphabet="extended"):
-        with pytest.raises(oracle.OracleError):
-            oracle.assemble(case["reads"], case["k"], case["limit"])
+def test_oracle_extended_alphabet_matches_reference():
+    """lowercase and IUPAC bytes are opaque symbols, their own complement (twin:7-10): the
+    oracle takes its string-keyed restatement (refasm_str.c) for such reads"""
+    cases = golden_cases("synthetic.json", alphabet="extended")
+    assert cases
+    for case in cases:
+        for th in (None, 4):
+            d, r, g = oracle.assemble(case["reads"], case["k"], case["limit"], threads=th)
+            assert d == case["d"] and r == case["contigs"] and g == case["links"], case["name"]
+
+
+@pytest.mark.parametrize("case", ALL, ids=[c["name"] for c in ALL])
+def test_string_oracle_matches_reference(case):
+    """the string-keyed restatement on every golden case (forced: string=True)"""
+    d, r, g = oracle.assemble(case["reads"], case["k"], case["limit"], string=True)
+    assert d == case["d"]
+    assert r == case["contigs"]
+    assert g == case["links"]
 
 
 def test_g200_config1_is_empty_at_k21():
