@@ -594,7 +594,12 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     }
     const double est = hsc.est * (smask + 1.0);
     BucketPlan plan = plan_buckets(est, limit, !kn().no_filter);
-    if (!plan.part || plan.filt) return reset();  // error-rich: window records with the seen-twice filter
+    // error-rich input (the estimate asks for the seen-twice filter): super-k-mer buckets behind
+    // the filter (k_skbucket_filt) while a bucket's distinct keys stay within its 2^16 filter
+    // cells (limit >= 1); otherwise window records with count_part.h's filter
+    const bool skfilt = plan.part && plan.filt && limit >= 1 && kn().sk_filt != 0 &&
+                        est / (double)(1ull << SK2_BBITS) <= 16000.0;
+    if (!plan.part || (plan.filt && !skfilt)) return reset();
     // up to 2^SK2_BBITS buckets of <= 1100 estimated keys (2048-slot tables: two workgroups per
     // CU).  Measured: 16384 buckets of 1024 slots (three workgroups per CU) were not faster, and
     // small tables need lds_insert to count claims after the CAS (reservations of up to 1024
@@ -605,11 +610,12 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     int bbits = SK2_CBITS;
     // k_skbucket3 (three workgroups per CU, 1024-slot tables) while its buckets stay at <= 380
     // estimated keys; larger inputs take k_skbucket's 2048- / 4096-slot tables
-    const bool b3 = !kn().no_skb3 && est / (double)(1ull << SK2_BBITS) <= 380.0;
+    const bool b3 = !skfilt && !kn().no_skb3 && est / (double)(1ull << SK2_BBITS) <= 380.0;
     const double per_bucket = b3 ? 380.0 : 800.0;
     while (bbits < SK2_BBITS && est / (double)(1ull << bbits) > per_bucket) bbits++;
+    if (skfilt) bbits = SK2_BBITS;
     plan.bbits = bbits;
-    plan.slots = b3 ? 1024u : est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
+    plan.slots = skfilt ? 2048u : b3 ? 1024u : est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
     const uint64_t Bk = 1ull << bbits;
     const uint64_t NR = hsc.nrec;
 
@@ -659,7 +665,14 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         dbg = s->tmp.as<unsigned long long>();
         EC_HIP(hipMemsetAsync(dbg, 0, 128, st));
     }
-    if (plan.slots == 1024) {
+    if (skfilt) {
+        constexpr int NTF = 512;
+        const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 2048u * 72 / 100;
+        if (k & 1)
+            k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys);
+        else
+            k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys);
+    } else if (plan.slots == 1024) {
         constexpr int NT3 = 512;
         const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
         if (k & 1)
@@ -1877,6 +1890,7 @@ int x_cut(ec_session *s, unsigned int U, unsigned int &nx) {
     unsigned int nasym = 0;
     EC_HIP(hipMemcpyAsync(&nasym, &dsc->nasym, 4, hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
+    if (kn().verbose) fprintf(stderr, "extended: %u one-way links among %u nodes\n", nasym, N);
     if (!nasym) return EC_OK;
     EC_CHECK(s->x_par.ensure((size_t)U * 4));
     EC_CHECK(s->x_irr.ensure(U));
@@ -1886,10 +1900,11 @@ int x_cut(ec_session *s, unsigned int U, unsigned int &nx) {
     EC_CHECK(s->x_lk2.ensure((size_t)N * 8));
     EC_CHECK(s->x_lv.ensure((size_t)N * 4));
     EC_CHECK(s->x_lv2.ensure((size_t)N * 4));
-    unsigned int *par = s->x_par.as<unsigned int>();
-    k_x_iota<<<grid_for(U, B), B, 0, st>>>(par, U);
-    k_x_uf_link<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, par);
-    k_x_uf_flatten<<<grid_for(U, B), B, 0, st>>>(U, par);
+    // union-find over canonical ids (CAS hooks); par then holds the roots (the tree in x_lv2)
+    unsigned int *par = s->x_par.as<unsigned int>(), *tree = s->x_lv2.as<unsigned int>();
+    k_x_iota<<<grid_for(U, B), B, 0, st>>>(tree, U);
+    k_x_uf_link<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, tree);
+    k_x_uf_flatten<<<grid_for(U, B), B, 0, st>>>(U, tree, par);
     EC_HIP(hipMemsetAsync(s->x_irr.p, 0, U, st));
     k_x_mark_irr<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, par,
                                               s->x_irr.as<uint8_t>());

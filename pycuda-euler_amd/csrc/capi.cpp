@@ -48,6 +48,8 @@ void refresh_knobs() {
         k.sk2_claim = num("EULERHIP_SK2_CLAIM", 0);
         k.verbose = flag("EULERHIP_VERBOSE");
         k.rank = num("EULERHIP_RANK", -1);
+        k.sk_filt = num("EULERHIP_SK_FILT", -1);
+        k.skf_keys = num("EULERHIP_SKF_KEYS", 0);
     }
     g_knobs = k;
 }

@@ -45,6 +45,8 @@ struct Knobs {
     bool no_slot_groups = false; // EULERHIP_NO_SLOT_GROUPS: k_skpart_w read groups not rounded to resident slots (A/B)
     bool verbose = false;       // EULERHIP_VERBOSE: count-path fallbacks on stderr
     int rank = -1;              // EULERHIP_RANK: list ranking 0 = tile contraction (rank_tile.h), 1 = node ruling set
+    int sk_filt = -1;           // EULERHIP_SK_FILT: 0 = error-rich inputs on window records, not k_skbucket_filt
+    int skf_keys = 0;           // EULERHIP_SKF_KEYS: k_skbucket_filt's keys-per-table cap (forces its overflow)
 };
 void refresh_knobs();
 const Knobs &kn();

@@ -1107,4 +1107,124 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
                                                                       EvExpand{2 * M});
 }
 
+
+// ---- error-rich input: super-k-mer buckets behind a seen-twice filter (round 4) ----------------
+// With sequencing errors most distinct k-mers occur once (ecoli10m_err: 1.6e8 distinct, 1.3e7
+// solid) and a bucket's records are mostly unique, so k_skbucket3's record merge finds nothing
+// to merge and its tables would overflow.  Here every record's windows are rolled out twice, as
+// k_bucket_filt (count_part.h) does for window records: pass 0 marks two cells per canonical
+// key in LDS bitmaps (seen once / seen twice); pass 1 inserts a window only if both of its
+// cells were seen twice (every key occurring >= 2 times passes; a singleton passes with the
+// probability of a double cell collision, and is then counted exactly and dropped by the solid
+// filter) or if its own insert already exceeds the limit (an even-k palindrome adds 2).  The
+// table holds the bucket's solid keys plus those few singletons; a bucket whose twice-seen
+// cells estimate more keys than the table takes reports an overflow (the call is redone on
+// window records).  Requires limit >= 1 (with limit < 1 every key is solid).
+constexpr int SKF_BITS = 16;  // filter cells per bitmap
+template <int SLOTS, int NT, bool EVEN_K>
+__global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const unsigned long long *bbeg,
+                                                      const unsigned long long *bend, int k, uint32_t M, double inv_m,
+                                                      long long limit, unsigned long long *dkey, unsigned int *dcnt,
+                                                      unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
+                                                      unsigned int *nsolid, unsigned long long *ndistinct,
+                                                      unsigned int *overflow, unsigned int max_keys) {
+    constexpr int SBITS = __builtin_ctz(SLOTS);
+    constexpr unsigned int NW = 1u << (SKF_BITS - 5), CM = (1u << SKF_BITS) - 1;
+    __shared__ LTabE<SLOTS> tab;
+    __shared__ unsigned int s_over[2];
+    __shared__ unsigned int seen1[NW], seen2[NW];
+    __shared__ unsigned int s_cells[2];
+    const unsigned int b = blockIdx.x, tid = threadIdx.x;
+    for (int i = tid; i < SLOTS; i += NT) {
+        tab.key[i] = EMPTY_KEY;
+        tab.count[i] = 0;
+        tab.ev[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+    for (unsigned int i = tid; i < NW; i += NT) seen1[i] = seen2[i] = 0;
+    if (tid == 0) s_over[0] = s_over[1] = 0, s_cells[0] = s_cells[1] = 0;
+    __syncthreads();
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    const uint64_t kmask = kmask64(k);
+    const int fsh = 64 - 2 * k;
+    const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
+    // the windows of a record as stored (window o = bases o .. o + k - 1, o < n <= 16): canonical
+    // key, add, first events of the canonical / twin string (k_skbucket3's roll-out, unflipped)
+    auto windows = [&](const uint4 &x, auto &&fn) {
+        const unsigned int n = (x.z >> 28) + 1;
+        const unsigned int p = x.w;
+        const unsigned int rd0 = (unsigned int)((double)p * inv_m);
+        int rm = (int)(p - rd0 * M);
+        unsigned int rd = rd0;
+        if (rm < 0) rd--, rm += (int)M;
+        else if (rm >= (int)M) rd++, rm -= (int)M;
+        const unsigned int A = rd * M2 + (unsigned int)rm, B = rd * M2 + m2 - (unsigned int)rm;
+        for (unsigned int o = 0; o < n; o++) {
+            const uint32_t lo = __builtin_amdgcn_alignbit(x.y, x.x, 2 * o), hi = __builtin_amdgcn_alignbit(x.z, x.y, 2 * o);
+            const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+            const uint64_t rv = ~P & kmask, fw = rev2_64(P) >> fsh;
+            const bool tw = fw > rv;
+            const unsigned int ef = A + o, et = B - o;
+            unsigned int add = 1, eC = tw ? et : ef, eT = tw ? ef : et;
+            if (EVEN_K && fw == rv) {
+                add = 2;
+                eC = eT = min(ef, et);
+            }
+            fn(tw ? rv : fw, add, eC, eT);
+        }
+    };
+    auto cells = [](unsigned long long c, unsigned int &c1, unsigned int &c2) {
+        const uint64_t h = mix64(c);
+        c1 = (unsigned int)(h >> 12) & CM;
+        c2 = (unsigned int)(h >> 30) & CM;
+    };
+    // pass 0: the filter
+    for (uint64_t i = r0 + tid; i < r1; i += NT) {
+        windows(recs[i], [&](unsigned long long c, unsigned int, unsigned int, unsigned int) {
+            unsigned int c1, c2;
+            cells(c, c1, c2);
+            const unsigned int m1 = 1u << (c1 & 31), mm2 = 1u << (c2 & 31);
+            if (atomicOr(&seen1[c1 >> 5], m1) & m1) atomicOr(&seen2[c1 >> 5], m1);
+            if (atomicOr(&seen1[c2 >> 5], mm2) & mm2) atomicOr(&seen2[c2 >> 5], mm2);
+        });
+    }
+    __syncthreads();
+    {  // keys that will be inserted, and the bucket's distinct keys, by linear counting
+        unsigned int n2 = 0, n1 = 0;
+        for (unsigned int i = tid; i < NW; i += NT) n2 += __popc(seen2[i]), n1 += __popc(seen1[i]);
+        for (int o = 32; o > 0; o >>= 1) n2 += __shfl_down(n2, o), n1 += __shfl_down(n1, o);
+        if ((tid & 63) == 0) atomicAdd(&s_cells[0], n2), atomicAdd(&s_cells[1], n1);
+        __syncthreads();
+        if (tid == 0) {
+            const double m = (double)(1u << SKF_BITS);
+            const double k2 = -m * log(1.0 - (double)min(s_cells[0], CM) / m) / 2.0;
+            const double k1 = -m * log(1.0 - (double)min(s_cells[1], CM) / m) / 2.0;
+            if (k2 > (double)max_keys) s_over[0] = 1;  // (default: the table would pass ~3/4 full)
+            else atomicAdd(ndistinct, (unsigned long long)llround(k1));
+        }
+        __syncthreads();
+    }
+    if (s_over[0]) {
+        if (tid == 0) atomicAdd(overflow, 1u);
+        return;
+    }
+    // pass 1: the keys seen twice (or solid by their own insert) into the table
+    for (uint64_t i = r0 + tid; i < r1; i += NT) {
+        windows(recs[i], [&](unsigned long long c, unsigned int add, unsigned int eC, unsigned int eT) {
+            unsigned int c1, c2;
+            cells(c, c1, c2);
+            const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
+            if (!twice && (long long)add <= limit) return;
+            const unsigned int s0 = (sk_slot(c) >> (32 - SBITS)) & (SLOTS - 1);
+            const unsigned int sl = lds_locate<SLOTS>(tab, s_over, c, s0, tab.key[s0]);
+            atomicAdd(&tab.count[sl], add);
+            const uint2 v = tab.ev[sl];
+            if (eC < v.x) atomicMin(&tab.ev[sl].x, eC);
+            if (eT < v.y) atomicMin(&tab.ev[sl].y, eT);
+        });
+    }
+    lds_table_finish<SLOTS, false, KeyId, LTabE<SLOTS>, EvExpand, NT>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub,
+                                                                      nsolid, nullptr, overflow, KeyId(),
+                                                                      EvExpand{2 * M});
+}
+
 }  // namespace ec

@@ -272,10 +272,15 @@ __global__ void __launch_bounds__(256) k_x_uf_link(const uint8_t *upal, const un
     }
 }
 
-// canonical id -> its component's root; roots of components holding a one-way link get irr = 1
-__global__ void __launch_bounds__(256) k_x_uf_flatten(unsigned int U, unsigned int *par) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < U; t += (uint64_t)gridDim.x * blockDim.x)
-        par[t] = uf_find(par, (unsigned int)t);
+// canonical id -> its component's root (into a separate array: path halving by other threads
+// while flattening in place could overwrite a node's root with an intermediate ancestor); roots
+// of components holding a one-way link get irr = 1
+__global__ void __launch_bounds__(256) k_x_uf_flatten(unsigned int U, const unsigned int *par, unsigned int *root) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < U; t += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned int x = (unsigned int)t;
+        for (unsigned int p = par[x]; p != x; p = par[x]) x = p;
+        root[t] = x;
+    }
 }
 __global__ void __launch_bounds__(256) k_x_mark_irr(const uint8_t *upal, const unsigned int *succ, unsigned int N,
                                                     const unsigned int *par, uint8_t *irr) {

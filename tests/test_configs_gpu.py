@@ -152,3 +152,23 @@ def test_genome20m_k51_third_level_vs_oracle(gpu_session, monkeypatch):
     assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
     assert np.array_equal(res.link_offsets, ref["link_offsets"])
     assert np.array_equal(res.link_codes, ref["links"])
+
+
+def test_ecoli10m_err_vs_oracle(gpu_session):
+    """the headline read set with 0.5 % substitution errors (SURVEY §8d's error variant: 1.6·10^8
+    distinct k-mers, mostly singletons) at full size, bit-exact against the oracle (N-core
+    count): the super-k-mer count behind the seen-twice filter (k_skbucket_filt)"""
+    import os
+
+    buf, off = make_reads(4_600_000, 10_000_000, 100, 20261015 + 4, err=0.005)
+    th = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    ref = oracle.assemble_packed(buf, off, 31, 1, threads=th)
+    gpu_session.run_host(buf, off, 31, 1)
+    res = gpu_session.fetch(31)
+    assert res.stats.count_variant == 3
+    assert res.stats.n_positions == ref["n_positions"] == 700_000_000
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert np.array_equal(res.link_offsets, ref["link_offsets"])
+    assert np.array_equal(res.link_codes, ref["links"])
