@@ -176,6 +176,9 @@ int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts);
 #define EC_MOD_TAIL_DROP 1u  /* pygpuhash: floor(n/1024)-block grid drops the tail (src/pygpuhash.py:57-61) */
 #define EC_MOD_REF_BOUNDS 2u /* pydebruijn: setupEdges' `< lmerCount` bounds (src/pydebruijn.py:449)     */
 #define EC_MOD_SWIPE 4u      /* pyeulertour: run the commented-out swipe body (src/pyeulertour.py:539-552) */
+#define EC_MOD_TREE_MARKS 8u /* pyeulertour: mark only the spanning tree's edges (mark starts at zero, not at
+                              * one as :659; mark[e1] of each tree edge): with EC_MOD_SWIPE every connected
+                              * component's circuits merge into one Euler tour */
 #define EC_HASH_BUCKET_ITEMS 520 /* MAX_BUCKET_ITEM (src/pygpuhash.py:14) */
 
 /* E1 encode_lmer_device (src/pyencode.py:14-98): out[p] = MSB-first 2-bit code of buf[p..p+L-1]

@@ -225,20 +225,23 @@ def contig_start(ee):
     return cs
 
 
-def mark_spanning(cg, tree, E):
+def mark_spanning(cg, tree, E, tree_marks=False):
     """T5 markSpanningEulerEdges (src/pyeulertour.py:613-632): mark starts all ones (:659);
-    tree holds circuit-graph EDGE indices."""
-    mark = np.ones(E, np.uint32)
+    tree holds circuit-graph EDGE indices.  tree_marks (EC_MOD_TREE_MARKS, the
+    intended merge): mark starts at zero and each tree edge marks e1, the first of the two
+    consecutive entering edges it joins (assignCircuitGraphEdgeData :458-463)."""
+    mark = np.zeros(E, np.uint32) if tree_marks else np.ones(E, np.uint32)
     for t in tree:
         c = cg[int(t)]
-        m = min(int(c["e1"]), int(c["e2"]))
+        m = int(c["e1"]) if tree_marks else min(int(c["e1"]), int(c["e2"]))
         if m < E:
             mark[m] = 1
     return mark
 
 
 def swipe(ev, e, ee, mark):
-    """T5 executeSwipe, the body the reference comments out (src/pyeulertour.py:539-552)."""
+    """T5 executeSwipe, the body the reference comments out (src/pyeulertour.py:534-555): every
+    run of marked entering edges of a vertex rotates its successors."""
     ee = ee.copy()
     E = len(ee)
     for v in ev:
@@ -248,14 +251,40 @@ def swipe(ev, e, ee, mark):
         mx = index + int(v["ecount"]) - 1
         if mx >= E:
             continue
-        if mark[int(ee[int(e[index])]["eid"])] == 1:
-            t0, s = index, int(ee[int(e[index])]["s"])
-            while mark[int(ee[int(e[index])]["eid"])] == 1 and index < mx:
-                ee[int(e[index])]["s"] = ee[int(e[index + 1])]["s"]
-                index += 1
-            if t0 != index:
-                ee[int(e[index])]["s"] = s
+        while index < mx and int(ee[int(e[index])]["eid"]) < E:
+            if mark[int(ee[int(e[index])]["eid"])] == 1:
+                t0, s = index, int(ee[int(e[index])]["s"])
+                while mark[int(ee[int(e[index])]["eid"])] == 1 and index < mx:
+                    ee[int(e[index])]["s"] = ee[int(e[index + 1])]["s"]
+                    index += 1
+                if t0 != index:
+                    ee[int(e[index])]["s"] = s
+            index += 1
     return ee
+
+
+def successor_cycles(ee):
+    """The successor structure of the edges as cycles / paths of edge indices (each edge once):
+    paths from the edges no edge points to, then cycles from their smallest edge.  After the
+    merge (EC_MOD_TREE_MARKS + swipe) every connected component is one of them."""
+    E = len(ee)
+    s = [int(x) for x in ee["s"]]
+    has_pred = [False] * E
+    for x in s:
+        if x < E:
+            has_pred[x] = True
+    seen = [False] * E
+    out = []
+    for start in [i for i in range(E) if not has_pred[i]] + list(range(E)):
+        if seen[start]:
+            continue
+        walk, x = [], start
+        while x < E and not seen[x]:
+            seen[x] = True
+            walk.append(x)
+            x = s[x]
+        out.append(walk)
+    return out
 
 
 def lmer_table(buf, l):

@@ -42,6 +42,7 @@ for name, res, args in [
 EC_MOD_TAIL_DROP = 1
 EC_MOD_REF_BOUNDS = 2
 EC_MOD_SWIPE = 4
+EC_MOD_TREE_MARKS = 8
 BUCKET_ITEMS = 520
 
 # the reference's structured dtypes (src/pydebruijn.py:604-606, src/pyeulertour.py:734,785)

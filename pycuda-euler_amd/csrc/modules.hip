@@ -370,17 +370,21 @@ __global__ void __launch_bounds__(256) k_circuit_edges(const EulerVertex *ev, ui
 }
 
 // markSpanningEulerEdges (:613-632) and executeSwipe (:518-557)
+// tree_first = 0: mark[min(e1, e2)] (:627); 1 (EC_MOD_TREE_MARKS): mark[e1], the first of the
+// two consecutive entering edges the circuit-graph edge joins (e1 = e[i], e2 = e[i + 1],
+// k_circuit_edges), which is the edge whose run the swipe rotates
 __global__ void __launch_bounds__(256) k_mark_spanning(const CircuitEdge *cg, const unsigned int *tree, uint64_t nt,
-                                                       uint64_t E, unsigned int *mark) {
+                                                       uint64_t E, unsigned int *mark, int tree_first) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nt; t += (uint64_t)gridDim.x * blockDim.x) {
         const CircuitEdge c = cg[tree[t]];
-        const unsigned int m = min(c.e1, c.e2);
+        const unsigned int m = tree_first ? c.e1 : min(c.e1, c.e2);
         if (m < E) mark[m] = 1;
     }
 }
 
-// the swipe body the reference comments out (:539-552): rotate the successors of a run of
-// marked entering edges of a vertex
+// the swipe body the reference comments out (:534-555): at every vertex, each run of marked
+// entering edges e_t .. e_{j-1} (and the edge e_j that ends it) rotates its successors,
+// s(e_i) = s(e_{i+1}), s(e_j) = old s(e_t) -- merging the circuits of e_t .. e_j into one
 __global__ void __launch_bounds__(256) k_swipe(const EulerVertex *ev, uint64_t vcount, const unsigned int *e,
                                                EulerEdge *ee, const unsigned int *mark, uint64_t E) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < vcount; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -389,14 +393,17 @@ __global__ void __launch_bounds__(256) k_swipe(const EulerVertex *ev, uint64_t v
         uint64_t index = v.ep;
         const uint64_t maxIndex = index + v.ecount - 1;
         if (maxIndex >= E) continue;
-        if (mark[ee[e[index]].eid] == 1) {
-            const uint64_t t0 = index;
-            const unsigned int s = ee[e[index]].s;
-            while (mark[ee[e[index]].eid] == 1 && index < maxIndex) {
-                ee[e[index]].s = ee[e[index + 1]].s;
-                index++;
+        while (index < maxIndex && ee[e[index]].eid < E) {
+            if (mark[ee[e[index]].eid] == 1) {
+                const uint64_t t0 = index;
+                const unsigned int s = ee[e[index]].s;
+                while (mark[ee[e[index]].eid] == 1 && index < maxIndex) {
+                    ee[e[index]].s = ee[e[index + 1]].s;
+                    index++;
+                }
+                if (t0 != index) ee[e[index]].s = s;
             }
-            if (t0 != index) ee[e[index]].s = s;
+            index++;
         }
     }
 }
@@ -928,12 +935,13 @@ int ec_execute_swipe(const void *ev, uint64_t vcount, const uint32_t *e, void *e
     EC_HIP(hipMemcpy(dee.p, ee, E * sizeof(EulerEdge), hipMemcpyHostToDevice));
     if (cg_edge_count) EC_HIP(hipMemcpy(dcg.p, cg_edges, cg_edge_count * sizeof(CircuitEdge), hipMemcpyHostToDevice));
     if (tree_count) EC_HIP(hipMemcpy(dt.p, tree, tree_count * 4, hipMemcpyHostToDevice));
-    // mark starts as all ones (src/pyeulertour.py:659)
-    std::vector<uint32_t> ones(E, 1u);
-    EC_HIP(hipMemcpy(dm.p, ones.data(), E * 4, hipMemcpyHostToDevice));
+    // mark starts as all ones (src/pyeulertour.py:659) -- or all zeros with EC_MOD_TREE_MARKS, so
+    // only the spanning tree's edges rotate and each component's circuits merge into one tour
+    std::vector<uint32_t> init(E, (flags & EC_MOD_TREE_MARKS) ? 0u : 1u);
+    EC_HIP(hipMemcpy(dm.p, init.data(), E * 4, hipMemcpyHostToDevice));
     if (tree_count)
         k_mark_spanning<<<grid_for(tree_count, 256), 256>>>(dcg.as<CircuitEdge>(), dt.as<unsigned int>(), tree_count, E,
-                                                           dm.as<unsigned int>());
+                                                           dm.as<unsigned int>(), (flags & EC_MOD_TREE_MARKS) ? 1 : 0);
     if ((flags & EC_MOD_SWIPE) && vcount)
         k_swipe<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), vcount, de.as<unsigned int>(),
                                                dee.as<EulerEdge>(), dm.as<unsigned int>(), E);

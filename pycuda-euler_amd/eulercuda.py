@@ -191,12 +191,35 @@ def generatePartialContig(outfile, d_ev, vcount, d_ee, ecount, l):
     return output
 
 
-def findEulerTour(d_ev, d_ee, d_levEdge, d_entEdge, edgeCountList, vertexCount, lmerLength, outfile, swipe=False):
-    """src/eulercuda.py:405-434, with the de Bruijn counts kept (SURVEY §A8: the reference
-    overwrote them with the circuit-graph counts and left outstrings unbound without circuit
-    edges).  swipe=True runs the swipe body the reference leaves commented out."""
+def mergeEulerCircuits(d_ev, d_ee, d_levEdge, d_entEdge, edgeCountList, vertexCount):
+    """The Euler-circuit merge the reference sets up and leaves as a no-op (src/eulercuda.py:
+    425-431, src/pyeulertour.py:495-664), on the device: successor pairing
+    and circuits (findEulerDevice), the spanning forest of the circuit graph (findSpanningTree,
+    Boruvka on the device), then the swipe with only the forest's edges marked.  Returns the
+    edges with merged successors: every connected component of the circuit graph is one tour."""
     import pyeulertour as et
 
+    ee = np.array(d_ee, copy=True)
+    cg_edge, cg_edgeCount, cg_vertexCount = et.findEulerDevice(d_ev, d_levEdge, d_entEdge, vertexCount, ee,
+                                                               edgeCountList, None, 0, 0)
+    if cg_edgeCount > 0:
+        tree = findSpanningTree(cg_edge, cg_edgeCount, cg_vertexCount)
+        ee = et.executeSwipeDevice(d_ev, d_entEdge, vertexCount, ee, edgeCountList, cg_edge, cg_edgeCount, tree,
+                                   len(tree), swipe=True, merge=True)
+    return ee
+
+
+def findEulerTour(d_ev, d_ee, d_levEdge, d_entEdge, edgeCountList, vertexCount, lmerLength, outfile, swipe=False,
+                  merge=False):
+    """src/eulercuda.py:405-434, with the de Bruijn counts kept (SURVEY §A8: the reference
+    overwrote them with the circuit-graph counts and left outstrings unbound without circuit
+    edges).  swipe=True runs the swipe body the reference leaves commented out; merge=True
+    merges each component's circuits into one tour first (mergeEulerCircuits)."""
+    import pyeulertour as et
+
+    if merge:
+        ee = mergeEulerCircuits(d_ev, d_ee, d_levEdge, d_entEdge, edgeCountList, vertexCount)
+        return generatePartialContig(outfile, d_ev, vertexCount, ee, edgeCountList, lmerLength)
     ee = np.array(d_ee, copy=True)
     cg_edge, cg_edgeCount, cg_vertexCount = et.findEulerDevice(d_ev, d_levEdge, d_entEdge, vertexCount, ee,
                                                                edgeCountList, None, 0, 0)

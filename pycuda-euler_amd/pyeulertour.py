@@ -80,7 +80,7 @@ def mark_spanning_euler_edges(d_ee, d_mark, ecount, d_cg_edge, cg_edgeCount, d_t
     return _swipe(None, 0, None, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, treeCount, False)[1]
 
 
-def _swipe(d_ev, vcount, d_e, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, treeCount, swipe):
+def _swipe(d_ev, vcount, d_e, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, treeCount, swipe, merge=False):
     E = int(ecount)
     ee = _ee(d_ee)
     ev = _ev(d_ev) if d_ev is not None else np.zeros(0, M.EV)
@@ -89,7 +89,8 @@ def _swipe(d_ev, vcount, d_e, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, tre
     tree = M.arr(d_tree, np.uint32).reshape(-1)[: int(treeCount)] if treeCount else np.zeros(0, np.uint32)
     mark = np.zeros(max(E, 1), np.uint32)
     M.call("ec_execute_swipe", M.ptr(ev), int(vcount), M.ptr(e), M.ptr(ee), E, M.ptr(cg), int(cg_edgeCount),
-           M.ptr(tree), len(tree), M.EC_MOD_SWIPE if swipe else 0, M.ptr(mark))
+           M.ptr(tree), len(tree), (M.EC_MOD_SWIPE if swipe else 0) | (M.EC_MOD_TREE_MARKS if merge else 0),
+           M.ptr(mark))
     return _copy_fields(d_ee, ee), mark[:E]
 
 
@@ -99,10 +100,13 @@ def execute_swipe(d_ev, d_e, vcount, d_ee, d_mark, ecount, swipe=False):
     return _swipe(d_ev, vcount, d_e, d_ee, ecount, None, 0, None, 0, swipe)
 
 
-def executeSwipeDevice(d_ev, d_e, vcount, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, treeCount, swipe=False):
+def executeSwipeDevice(d_ev, d_e, vcount, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, treeCount, swipe=False,
+                       merge=False):
     """src/pyeulertour.py:656-664: mark spanning-tree edges, swipe; returns ee.  d_tree holds
-    circuit-graph edge indices (the reference passed vertex pairs)."""
-    return _swipe(d_ev, vcount, d_e, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, treeCount, swipe)[0]
+    circuit-graph edge indices (the reference passed vertex pairs).  merge=True
+    (with swipe=True): marks start at zero and only the tree's edges rotate, so every connected
+    component's circuits merge into one Euler tour (the reference's intent; its merge is a no-op)."""
+    return _swipe(d_ev, vcount, d_e, d_ee, ecount, d_cg_edge, cg_edgeCount, d_tree, treeCount, swipe, merge)[0]
 
 
 def identify_contig_start(d_ee, d_contigStart, ecount):

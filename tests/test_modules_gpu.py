@@ -260,3 +260,74 @@ def test_spanning_forest_long_chain_time():
     cg["c2"] = perm[1:-1]
     cg["ceid"] = np.arange(V - 2)
     assert eulercuda.findSpanningTree(cg, V - 2, V).tolist() == R.spanning_forest(cg, V - 2, V)
+
+
+def _euler_graph(seqs, l):
+    """de Bruijn multigraph of circular sequences (every vertex balanced: an Euler graph), laid
+    out by the pydebruijn restatement: l-mer keys / multiplicities / (l-1)-mer vertex keys"""
+    code = {"A": 0, "C": 1, "G": 2, "T": 3}
+    cnt = {}
+    for s in seqs:
+        t = s + s[: l - 1]
+        for i in range(len(s)):
+            x = 0
+            for c in t[i:i + l]:
+                x = (x << 2) | code[c]
+            cnt[x] = cnt.get(x, 0) + 1
+    keys = np.array(sorted(cnt), dtype=np.uint64)
+    counts = np.array([cnt[int(x)] for x in keys], dtype=np.uint32)
+    mask = (1 << (2 * (l - 1))) - 1
+    kmers = np.unique(np.concatenate([(keys >> np.uint64(2)) & np.uint64(mask), keys & np.uint64(mask)]))
+    table = R.hash_build(kmers, np.arange(len(kmers), dtype=np.uint32))
+    ev, ee, L, Ee, E = R.debruijn(keys, counts, kmers, l, table)
+    return ev, ee, L, Ee, E
+
+
+@pytest.mark.parametrize("seed,nseq,n,l", [(1, 1, 400, 8), (2, 5, 300, 7), (3, 20, 200, 6), (4, 3, 3000, 10),
+                                           (5, 40, 60, 5)])
+def test_euler_circuit_merge(mods, seed, nseq, n, l):
+    """SURVEY §8f row 4, the merge the reference leaves as a no-op: successor pairing, circuits,
+    spanning forest of the circuit graph, then the swipe with only the forest's edges marked
+    (EC_MOD_TREE_MARKS).  Every connected component of the Euler graph becomes ONE tour whose
+    consecutive edges meet (v2(e) = v1(s(e))); the swipe equals its restatement on the same tree"""
+    import eulercuda
+
+    enc, gh, db, cc, et = mods
+    rng = np.random.default_rng(60 + seed)
+    seqs = []
+    while len(seqs) < nseq:
+        s = "".join(rng.choice(list("ACGT"), n))
+        if "A" * l not in s + s[: l]:  # (the all-A l-mer is the reference's empty key, SURVEY §A4)
+            seqs.append(s)
+    ev, ee, L, Ee, E = _euler_graph(seqs, l)
+    merged = eulercuda.mergeEulerCircuits(ev, ee, L, Ee, E, len(ev))
+    # components of the graph (edges' vertices united)
+    par = list(range(len(ev)))
+
+    def find(x):
+        while par[x] != x:
+            par[x] = par[par[x]]
+            x = par[x]
+        return x
+
+    for x in ee:
+        a, b = find(int(x["v1"])), find(int(x["v2"]))
+        if a != b:
+            par[max(a, b)] = min(a, b)
+    ncomp = len({find(int(x["v1"])) for x in ee})
+    tours = R.successor_cycles(merged)
+    assert sorted(i for t in tours for i in t) == list(range(E))
+    assert len(tours) == ncomp, (len(tours), ncomp)
+    for t in tours:
+        assert int(merged[t[-1]]["s"]) == t[0]  # closed: a circuit
+        for a, b in zip(t, t[1:] + t[:1]):
+            assert int(merged[a]["v2"]) == int(merged[b]["v1"])
+    # the swipe itself against its restatement, on the device's circuit graph and forest
+    ree, _, _ = R.find_euler(ev, L, Ee, ee)
+    work = ee.copy()
+    cg, ncg, cgV = et.findEulerDevice(ev, L, Ee, len(ev), work, E, None, 0, 0)
+    if ncg:
+        tree = eulercuda.findSpanningTree(cg, ncg, cgV)
+        sw = et.executeSwipeDevice(ev, Ee, len(ev), work.copy(), E, cg, ncg, tree, len(tree), swipe=True, merge=True)
+        assert np.array_equal(sw, R.swipe(ev, Ee, work, R.mark_spanning(cg, tree, E, tree_marks=True)))
+        assert len(R.successor_cycles(sw)) == ncomp
