@@ -348,6 +348,34 @@ int ec_graph_load_links(ec_session *s, const void *d_records, uint64_t n, int k,
                         uint64_t hi, uint32_t *d_succ);
 int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags);
 
+/* partitioned FINISH (round 4): instead of all-gathering the successor parts and ranking /
+ * emitting the whole set on every rank (ec_graph_finish), each rank ranks and emits its own
+ * segment [lo, hi) of the loaded set (csrc/rank_tile.h):
+ *   1. ec_graph_chains_part: its successors' chains ranked in LDS tiles; its chains as super
+ *      records (ec_super_record_bytes() = 32 B each, up to 2(hi-lo)) into d_super, *n_super;
+ *   2. ec_graph_rank_supers: every rank, on ALL ranks' super records concatenated in rank
+ *      order (n of them): the chains' list ranking (weighted ruling set);
+ *   3. ec_graph_starts_part: its nodes' path keys / ranks, its contig starts as start records
+ *      (ec_start_record_bytes() = 48 B, up to 2(hi-lo)) into d_starts, *n_starts (have_supers:
+ *      the job had any super records);
+ *   4. ec_graph_layout: every rank, on ALL start records (any order, n): contig order by first
+ *      event, *n_chars = the job's contig characters;
+ *      ec_graph_emit_part: its nodes' characters at their global positions into d_chars
+ *      (n_chars bytes, zeroed by the caller) and the contigs' first / last node + 1 it holds
+ *      into d_ends (2 * contigs uint32, zeroed) -- summed over the ranks they give every byte
+ *      and end exactly once;
+ *   5. ec_graph_collect (one rank): the summed characters / ends -> GFA links (all_contigs:90-109)
+ *      and the results (ec_copy_*, ec_get_stats). */
+int ec_graph_chains_part(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ, void *d_super,
+                         uint64_t *n_super);
+int ec_graph_rank_supers(ec_session *s, const void *d_supers, uint64_t n);
+int ec_graph_starts_part(ec_session *s, int have_supers, void *d_starts, uint64_t *n_starts);
+int ec_graph_layout(ec_session *s, const void *d_starts, uint64_t n, uint64_t *n_chars);
+int ec_graph_emit_part(ec_session *s, char *d_chars, uint32_t *d_ends);
+int ec_graph_collect(ec_session *s, const char *d_chars, const uint32_t *d_ends);
+int ec_super_record_bytes(void);
+int ec_start_record_bytes(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -203,7 +203,11 @@ struct ec_session {
     XAlpha xa{};
     DevBuf x_par, x_irr, x_in, x_succ, x_done, x_lk, x_lv, x_lk2, x_lv2, x_len, x_m, x_cid, x_head, x_tail;
     // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
-    DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp;
+    DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr;
+    // multi-GPU partitioned finish (ec_graph_chains_part ..): this rank's segment of oriented nodes
+    uint64_t seg_n0 = 0, seg_n1 = 0;
+    unsigned int seg_nc = 0;     // contigs of the job (ec_graph_layout)
+    uint64_t seg_nchars = 0;
 };
 
 namespace ec {
@@ -1875,6 +1879,72 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
     return EC_OK;
 }
 
+// rank_tile.h (2): the super list srec (M chains, SIDX[head] = index) linked and ranked by the
+// weighted ruling set; per chain its path key / rank (rt_pks / rt_rks), paths' and cycles'
+// length / min first event at their key nodes (PL / PM)
+int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr, int &rounds) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    Scalars hsc{};
+    SuperRec *srec = s->rt_srec.as<SuperRec>();
+    unsigned int *SIDX = s->rt_sidx.as<unsigned int>();
+    EC_CHECK(s->rt_snrec.ensure((size_t)M * sizeof(SNodeRec)));
+    EC_CHECK(s->rt_hasp.ensure(M));
+    EC_CHECK(s->rt_pks.ensure((size_t)M * 4));
+    EC_CHECK(s->rt_rks.ensure((size_t)M * 4));
+    EC_CHECK(s->rid.ensure((size_t)M * 8));
+    EC_CHECK(s->rlist.ensure((size_t)M * 4));
+    EC_CHECK(s->nextR.ensure((size_t)M * 4));
+    EC_CHECK(s->st0.ensure((size_t)M * sizeof(RJump)));
+    EC_CHECK(s->st1.ensure((size_t)M * sizeof(RJump)));
+    EC_CHECK(s->rbc.ensure(((M + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
+    EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
+    SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
+    k_super_link<<<grid_for(M, B), B, 0, st>>>(srec, M, SIDX, snrec, s->rt_hasp.as<uint8_t>());
+    EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
+    EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
+    const unsigned int masks[4] = {15u, 3u, 1u, 0u};
+    unsigned int r0 = 0;
+    const unsigned int nblk = (M + RULER_CHUNK - 1) / RULER_CHUNK;
+    for (int it = 0; it < 4; it++) {
+        k_srulers_count<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), M, masks[it], it == 0, s->rid.as<uint2>(),
+                                            s->rbc.as<unsigned int>());
+        EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
+        k_srulers<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), M, masks[it], it == 0, s->rbc.as<unsigned int>() + nblk,
+                                      &dsc->nr, s->rid.as<uint2>(), s->rlist.as<unsigned int>());
+        k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
+        k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), r0, &dsc->nr, masks[it], s->rid.as<uint2>(),
+                                     s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
+        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        r0 = hsc.nr;
+        if (hsc.nvisited >= M) break;
+    }
+    nr = hsc.nr;
+    if (hsc.nvisited != M) {
+        set_error("ruling set covered %llu of %u chains", (unsigned long long)hsc.nvisited, M);
+        return EC_ERR_STATE;
+    }
+    k_rjump_init<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), nr, s->st0.as<RJump>());
+    rounds = 1;
+    while ((1ull << (rounds - 1)) < (unsigned long long)nr) rounds++;
+    rounds = std::min(rounds + 1, 63);
+    RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
+    for (int r = 0; r < rounds; r++)
+        k_rjump<<<grid_for(nr, B), B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], nr, N, r ? &dsc->active[r - 1] : nullptr,
+                                              &dsc->active[r], &dsc->final_sel, (unsigned)((r + 1) & 1));
+    k_finalize_s<<<grid_for(M, B), B, 0, st>>>(snrec, srec, s->rid.as<uint2>(), s->rlist.as<unsigned int>(), bufs[0],
+                                              bufs[1], &dsc->final_sel, &dsc->active[rounds - 1], M,
+                                              s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
+                                              s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+    k_cycle_len_s<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), srec, bufs[0],
+                                                bufs[1], &dsc->final_sel, &dsc->active[rounds - 1], nr,
+                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+    return EC_OK;
+}
+
 // extended alphabet (extended.h): links without their twin link make their components'
 // walks overlap; those components are cut out of the parallel ranking (their successors saved
 // in x_succ) and their dict entries listed in (component, first event) order for k_x_emulate.
@@ -2011,7 +2081,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(s->rt_tbase.ensure(((size_t)ntiles + 1) * 8));
         EC_CHECK(s->rt_srec.ensure(Nn * sizeof(SuperRec)));
         EC_CHECK(s->rt_sidx.ensure(Nn * 4));
-        unsigned int *LH = s->pred.as<unsigned int>(), *LR = s->rid.as<unsigned int>() + Nn;  // (free here)
+        EC_CHECK(s->rt_lr.ensure(Nn * 4));
+        unsigned int *LH = s->pred.as<unsigned int>(), *LR = s->rt_lr.as<unsigned int>();  // (pred: free here)
         SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);  // (dead before the Wyllie rounds)
         static_assert(sizeof(SuperRec) == sizeof(RJump), "tile scratch in the ruler state buffer");
         unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
@@ -2027,61 +2098,11 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         const unsigned int M = (unsigned int)M64;
         // (2) the super list: compacted in tile order, linked, ranked by the weighted ruling set
         if (M) {
-            SuperRec *srec = s->rt_srec.as<SuperRec>();
-            unsigned int *SIDX = s->rt_sidx.as<unsigned int>();
-            k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, srec, SIDX);
-            EC_CHECK(s->rt_snrec.ensure((size_t)M * sizeof(SNodeRec)));
-            EC_CHECK(s->rt_hasp.ensure(M));
-            EC_CHECK(s->rt_pks.ensure((size_t)M * 4));
-            EC_CHECK(s->rt_rks.ensure((size_t)M * 4));
-            EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
-            SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
-            k_super_link<<<grid_for(M, B), B, 0, st>>>(srec, M, SIDX, snrec, s->rt_hasp.as<uint8_t>());
-            EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
-            EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
-            EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
-            const unsigned int masks[4] = {15u, 3u, 1u, 0u};
-            unsigned int r0 = 0;
-            const unsigned int nblk = (M + RULER_CHUNK - 1) / RULER_CHUNK;
-            for (int it = 0; it < 4; it++) {
-                k_srulers_count<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), M, masks[it], it == 0, s->rid.as<uint2>(),
-                                                    s->rbc.as<unsigned int>());
-                EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
-                k_srulers<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), M, masks[it], it == 0,
-                                              s->rbc.as<unsigned int>() + nblk, &dsc->nr, s->rid.as<uint2>(),
-                                              s->rlist.as<unsigned int>());
-                k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
-                k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), r0, &dsc->nr, masks[it],
-                                             s->rid.as<uint2>(), s->nextR.as<unsigned int>(), s->st0.as<RJump>(),
-                                             &dsc->nvisited);
-                EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-                EC_HIP(hipStreamSynchronize(st));
-                r0 = hsc.nr;
-                if (hsc.nvisited >= M) break;
-            }
-            nr = hsc.nr;
-            if (hsc.nvisited != M) {
-                set_error("ruling set covered %llu of %u chains", (unsigned long long)hsc.nvisited, M);
-                return EC_ERR_STATE;
-            }
-            k_rjump_init<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), nr, s->st0.as<RJump>());
-            rounds = 1;
-            while ((1ull << (rounds - 1)) < (unsigned long long)nr) rounds++;
-            rounds = std::min(rounds + 1, 63);
-            RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
-            for (int r = 0; r < rounds; r++)
-                k_rjump<<<grid_for(nr, B), B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], nr, N,
-                                                      r ? &dsc->active[r - 1] : nullptr, &dsc->active[r],
-                                                      &dsc->final_sel, (unsigned)((r + 1) & 1));
-            k_finalize_s<<<grid_for(M, B), B, 0, st>>>(snrec, srec, s->rid.as<uint2>(), s->rlist.as<unsigned int>(),
-                                                      bufs[0], bufs[1], &dsc->final_sel, &dsc->active[rounds - 1], M,
-                                                      s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
-                                                      s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
-            k_cycle_len_s<<<grid_for(nr, B), B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), srec,
-                                                        bufs[0], bufs[1], &dsc->final_sel, &dsc->active[rounds - 1], nr,
-                                                        s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+            k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
+                                                   s->rt_sidx.as<unsigned int>());
+            EC_CHECK(rank_supers(s, M, N, nr, rounds));
             // (3) every node: its chain's key and rank + its offset in the chain
-            k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, SIDX, s->rt_pks.as<unsigned int>(),
+            k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
                                                   s->RK.as<unsigned int>());
         }
@@ -2322,6 +2343,254 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     s->stats.n_dict = 2ull * U - hsc.npal;  // len(build()): palindromes have one entry
 
     collect_timing(s);
+    s->have = true;
+    s->stats_ok = true;
+    return EC_OK;
+}
+
+// ---- multi-GPU partitioned finish (distributed.py): each rank ranks and emits its own segment --
+// of the loaded (gathered) solid set, canonical ids [lo, hi) = oriented nodes [n0, n1):
+//   ec_graph_chains_part  its links' chains ranked in LDS (rank_tile.h) -> its super records
+//   ec_graph_rank_supers  every rank: the job's super list (all-gathered, rank order) ranked
+//   ec_graph_starts_part  its nodes' keys / ranks, its contig starts -> start records
+//   ec_graph_layout       every rank: the job's starts (all-gathered) in event order, offsets
+//   ec_graph_emit_part    its nodes' characters at their global positions, its contig ends
+//   ec_graph_collect      rank 0: the summed characters / ends -> GFA links and the results
+template <typename Ops>
+int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ, SuperRec *d_super,
+                uint64_t *n_super) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int U = (unsigned int)s->n_dense, N = 2 * U;
+    const size_t Nn = std::max<size_t>(N, 1);
+    const unsigned int n0 = (unsigned int)(2 * lo), n1 = (unsigned int)(2 * hi);
+    EC_CHECK(s->upal.ensure(std::max<size_t>(U, 1)));
+    EC_CHECK(s->succ.ensure(Nn * 4));
+    EC_CHECK(s->PK.ensure(Nn * 4));
+    EC_CHECK(s->RK.ensure(Nn * 4));
+    EC_CHECK(s->PL.ensure(Nn * 4));
+    EC_CHECK(s->PM.ensure(Nn * 8));
+    EC_CHECK(s->pred.ensure(Nn * 4));
+    EC_CHECK(s->rt_lr.ensure(Nn * 4));
+    EC_CHECK(s->rt_sidx.ensure(Nn * 4));
+    EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
+    if (U) k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<typename Ops::K>(), U, s->k, s->upal.as<uint8_t>(),
+                                                     &dsc->npal);
+    if (n1 > n0)
+        EC_HIP(hipMemcpyAsync(s->succ.as<unsigned int>() + n0, d_succ, (size_t)(n1 - n0) * 4, hipMemcpyDeviceToDevice,
+                              st));
+    const unsigned int ntiles = (n1 - n0 + RT_TN - 1) / RT_TN;
+    EC_CHECK(s->rt_tcnt.ensure(((size_t)ntiles + 1) * 8));
+    EC_CHECK(s->rt_tbase.ensure(((size_t)ntiles + 1) * 8));
+    EC_CHECK(s->st1.ensure(std::max<size_t>((size_t)ntiles * RT_TN, 1) * sizeof(SuperRec)));
+    unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
+    SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);
+    EC_HIP(hipMemsetAsync(tcnt + ntiles, 0, 8, st));
+    if (ntiles)
+        k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), n1,
+                                                s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                s->pred.as<unsigned int>(), s->rt_lr.as<unsigned int>(), tcnt, scratch,
+                                                s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
+                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>(), n0);
+    EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
+    unsigned long long M = 0;
+    EC_HIP(hipMemcpyAsync(&M, tbase + ntiles, 8, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (M) k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, d_super, s->rt_sidx.as<unsigned int>());
+    EC_HIP(hipStreamSynchronize(st));
+    *n_super = M;
+    s->seg_n0 = n0;
+    s->seg_n1 = n1;
+    return EC_OK;
+}
+
+int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
+    hipStream_t st = s->stream;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int N = 2 * (unsigned int)s->n_dense;
+    s->stats.n_rulers = 0;
+    if (!M) return EC_OK;
+    EC_CHECK(s->rt_srec.ensure((size_t)M * sizeof(SuperRec)));
+    EC_HIP(hipMemcpyAsync(s->rt_srec.p, d_all, (size_t)M * sizeof(SuperRec), hipMemcpyDeviceToDevice, st));
+    k_super_index<<<grid_for(M, 256), 256, 0, st>>>(s->rt_srec.as<SuperRec>(), (unsigned int)M,
+                                                    s->rt_sidx.as<unsigned int>());
+    unsigned int nr = 0;
+    int rounds = 0;
+    EC_CHECK(rank_supers(s, (unsigned int)M, N, nr, rounds));
+    s->stats.n_rulers = nr;
+    unsigned int act = 0;
+    EC_HIP(hipMemcpyAsync(&act, &dsc->active[rounds - 1], 4, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (act) {
+        set_error("chain list ranking did not converge in %d rounds", rounds);
+        return EC_ERR_STATE;
+    }
+    s->stats.rank_rounds = rounds;
+    return EC_OK;
+}
+
+int part_starts(ec_session *s, bool have_supers, StartRec *d_starts, uint64_t *n_starts) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    const unsigned int n0 = (unsigned int)s->seg_n0, n1 = (unsigned int)s->seg_n1;
+    const size_t Nn = std::max<size_t>(2 * (size_t)s->n_dense, 1);
+    *n_starts = 0;
+    if (n1 <= n0) return EC_OK;
+    if (have_supers)
+        k_expand<<<grid_for(n1 - n0, B), B, 0, st>>>(s->pred.as<unsigned int>(), s->rt_lr.as<unsigned int>(), n1,
+                                                     s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
+                                                     s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
+                                                     s->RK.as<unsigned int>(), n0);
+    const unsigned int nblk = (n1 - n0 + RULER_CHUNK - 1) / RULER_CHUNK;
+    EC_CHECK(s->rbc.ensure((size_t)nblk * 8 + 8));
+    EC_CHECK(s->cand.ensure(((size_t)(n1 - n0) / 64 + 8) * 8));
+    EC_CHECK(s->skeys.ensure(Nn * 8));
+    EC_CHECK(s->svals.ensure(Nn * 4));
+    unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk;
+    k_starts_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
+                                       s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                       s->PM.as<unsigned long long>(), n1, bc, s->cand.as<unsigned long long>(), nullptr,
+                                       n0);
+    EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
+    k_starts_write<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
+                                       s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                       s->PM.as<unsigned long long>(), n1, bs, s->cand.as<unsigned long long>(),
+                                       s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(), n0);
+    unsigned int cnt = 0;
+    EC_HIP(hipMemcpyAsync(&cnt, bs + nblk - 1, 4, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (cnt)
+        k_start_recs<<<grid_for(cnt, B), B, 0, st>>>(s->svals.as<unsigned int>(), cnt, s->upal.as<uint8_t>(),
+                                                     s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                     s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
+                                                     s->PL.as<unsigned int>(), s->k, d_starts);
+    EC_HIP(hipStreamSynchronize(st));
+    *n_starts = cnt;
+    return EC_OK;
+}
+
+int part_layout(ec_session *s, const StartRec *d_all, uint64_t nc, uint64_t *n_chars) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    const size_t Nn = std::max<size_t>(2 * (size_t)s->n_dense, 1), nn = std::max<size_t>(nc, 1);
+    EC_CHECK(s->skeys.ensure(nn * 8));
+    EC_CHECK(s->svals.ensure(nn * 4));
+    EC_CHECK(s->skeys2.ensure(nn * 8));
+    EC_CHECK(s->svals2.ensure(nn * 4));
+    EC_CHECK(s->clen.ensure((nn + 1) * 8));
+    EC_CHECK(s->coff.ensure((nn + 1) * 8));
+    EC_CHECK(s->cwalk.ensure(nn * sizeof(Walk)));
+    EC_CHECK(s->cidxOf.ensure(Nn * 4));
+    EC_HIP(hipMemsetAsync(s->cidxOf.p, 0xFF, Nn * 4, st));
+    EC_HIP(hipMemsetAsync(s->clen.as<unsigned long long>() + nc, 0, 8, st));
+    if (nc) {
+        k_start_keys<<<grid_for(nc, B), B, 0, st>>>(d_all, (unsigned int)nc, s->skeys.as<unsigned long long>(),
+                                                    s->svals.as<unsigned int>());
+        EC_CHECK(sort_pairs(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(),
+                            s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nc));
+        k_layout<<<grid_for(nc, B), B, 0, st>>>(d_all, s->svals2.as<unsigned int>(), (unsigned int)nc,
+                                                s->clen.as<unsigned long long>(), s->cidxOf.as<unsigned int>(),
+                                                s->cwalk.as<Walk>());
+    }
+    EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
+    unsigned long long tot = 0;
+    EC_HIP(hipMemcpyAsync(&tot, s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    s->seg_nc = (unsigned int)nc;
+    s->seg_nchars = tot;
+    *n_chars = tot;
+    return EC_OK;
+}
+
+template <typename Ops>
+int part_emit(ec_session *s, char *d_chars, uint32_t *d_ends) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int n0 = (unsigned int)s->seg_n0, n1 = (unsigned int)s->seg_n1, nc = s->seg_nc;
+    const size_t Nn = std::max<size_t>(2 * (size_t)s->n_dense, 1), nn = std::max<size_t>(nc, 1);
+    EC_CHECK(s->cfirst.ensure(nn * 4));
+    EC_CHECK(s->clast.ensure(nn * 4));
+    EC_CHECK(s->headOf.ensure(Nn * 4));
+    EC_CHECK(s->tailOf.ensure(Nn * 4));
+    EC_HIP(hipMemsetAsync(s->cfirst.p, 0xFF, nn * 4, st));
+    EC_HIP(hipMemsetAsync(s->clast.p, 0xFF, nn * 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->skew, 0, 4, st));
+    if (n1 > n0 && nc)
+        k_emit<Ops><<<grid_for(n1 - n0, B), B, 0, st>>>(
+            s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
+            s->dkey.as<typename Ops::K>(), s->cidxOf.as<unsigned int>(), s->cwalk.as<Walk>(),
+            s->coff.as<unsigned long long>(), n1, s->k, d_chars, std::max<uint64_t>(s->seg_nchars, 1),
+            s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
+            s->tailOf.as<unsigned int>(), &dsc->skew, n0);
+    if (nc) k_ends_export<<<grid_for(nc, B), B, 0, st>>>(s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), nc, d_ends);
+    unsigned int bad = 0;
+    EC_HIP(hipMemcpyAsync(&bad, &dsc->skew, 4, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    if (bad) {
+        set_error("contig characters past their bound %llu (inconsistent ranking)", (unsigned long long)s->seg_nchars);
+        return EC_ERR_STATE;
+    }
+    return EC_OK;
+}
+
+template <typename Ops, typename Index>
+int part_collect(ec_session *s, const Index &sidx, const char *d_chars, const uint32_t *d_ends) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const unsigned int U = (unsigned int)s->n_dense, nc = s->seg_nc;
+    const size_t Nn = std::max<size_t>(2 * (size_t)U, 1), nn = std::max<size_t>(nc, 1);
+    const uint64_t nchars = s->seg_nchars;
+    EC_CHECK(s->cfirst.ensure(nn * 4));
+    EC_CHECK(s->clast.ensure(nn * 4));
+    EC_CHECK(s->headOf.ensure(Nn * 4));
+    EC_CHECK(s->tailOf.ensure(Nn * 4));
+    EC_CHECK(s->lk.ensure(nn * 16 * 8));
+    EC_CHECK(s->lcnt.ensure(nn * 2 * 4));
+    EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
+    EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
+    if (nc) {
+        k_heads_from_ends<<<grid_for(nc, B), B, 0, st>>>(d_ends, nc, s->upal.as<uint8_t>(), s->cfirst.as<unsigned int>(),
+                                                         s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
+                                                         s->tailOf.as<unsigned int>());
+        k_gfa<Ops, Index><<<grid_for(nc, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), s->upal.as<uint8_t>(),
+                                                         s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(),
+                                                         s->headOf.as<unsigned int>(), s->tailOf.as<unsigned int>(), nc,
+                                                         s->k, s->lk.as<long long>(), s->lcnt.as<unsigned int>());
+    }
+    const unsigned int n2 = 2 * nc;
+    EC_CHECK(s->h_coff.resize((size_t)nc + 1));
+    EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
+    s->h_loff[n2] = 0;
+    EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, ((size_t)nc + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (nc) {
+        EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));
+        EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));
+        k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>());
+        EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
+        EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, st));
+    }
+    unsigned int npal = 0;
+    EC_HIP(hipMemcpyAsync(&npal, &dsc->npal, 4, hipMemcpyDeviceToHost, st));
+    EC_CHECK(s->h_chars.resize(nchars));
+    if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), d_chars, nchars, hipMemcpyDeviceToHost, st));
+    EC_HIP(hipStreamSynchronize(st));
+    const uint64_t nlinks = s->h_loff[n2];
+    EC_CHECK(s->h_links.resize(nlinks));
+    if (nlinks) {
+        EC_CHECK(s->dcounts.ensure(nlinks * 8));
+        k_links_compact<<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
+                                                      s->skeys2.as<unsigned long long>(), n2, s->dcounts.as<long long>());
+        EC_HIP(hipMemcpyAsync(s->h_links.data(), s->dcounts.p, nlinks * 8, hipMemcpyDeviceToHost, st));
+    }
+    EC_HIP(hipStreamSynchronize(st));
+    s->stats.n_solid = U;
+    s->stats.n_contigs = nc;
+    s->stats.n_contig_chars = nchars;
+    s->stats.n_links = nlinks;
+    s->stats.n_dict = 2ull * U - npal;
     s->have = true;
     s->stats_ok = true;
     return EC_OK;
@@ -2604,7 +2873,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp};
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->h_coff.release();
@@ -3039,6 +3308,70 @@ int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags) {
     if (s->k > 32) return phase_graph<OpsW>(s, s->k, U, s->gidxw, d_succ);
     return phase_graph<Ops64>(s, s->k, U, s->gidx, d_succ);
 }
+
+// multi-GPU partitioned finish (see part_chains above); include/eulerhip.h
+int ec_graph_chains_part(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ, void *d_super,
+                         uint64_t *n_super) {
+    refresh_knobs();
+    if (!s || !s->graph_loaded || lo > hi || hi > s->n_dense || !n_super || (hi > lo && (!d_succ || !d_super))) {
+        set_error("ec_graph_chains_part: no loaded solid set or bad range [%llu, %llu)", (unsigned long long)lo,
+                  (unsigned long long)hi);
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    SuperRec *out = static_cast<SuperRec *>(d_super);
+    return s->k > 32 ? part_chains<OpsW>(s, lo, hi, d_succ, out, n_super)
+                     : part_chains<Ops64>(s, lo, hi, d_succ, out, n_super);
+}
+
+int ec_graph_rank_supers(ec_session *s, const void *d_supers, uint64_t n) {
+    if (!s || !s->graph_loaded || (n && !d_supers)) {
+        set_error("ec_graph_rank_supers: no loaded solid set");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return part_rank(s, static_cast<const SuperRec *>(d_supers), n);
+}
+
+int ec_graph_starts_part(ec_session *s, int have_supers, void *d_starts, uint64_t *n_starts) {
+    if (!s || !s->graph_loaded || !n_starts || (s->seg_n1 > s->seg_n0 && !d_starts)) {
+        set_error("ec_graph_starts_part: no loaded solid set");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return part_starts(s, have_supers != 0, static_cast<StartRec *>(d_starts), n_starts);
+}
+
+int ec_graph_layout(ec_session *s, const void *d_starts, uint64_t n, uint64_t *n_chars) {
+    if (!s || !s->graph_loaded || !n_chars || (n && !d_starts)) {
+        set_error("ec_graph_layout: no loaded solid set");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return part_layout(s, static_cast<const StartRec *>(d_starts), n, n_chars);
+}
+
+int ec_graph_emit_part(ec_session *s, char *d_chars, uint32_t *d_ends) {
+    if (!s || !s->graph_loaded || (s->seg_nchars && !d_chars) || (s->seg_nc && !d_ends)) {
+        set_error("ec_graph_emit_part: no layout");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return s->k > 32 ? part_emit<OpsW>(s, d_chars, d_ends) : part_emit<Ops64>(s, d_chars, d_ends);
+}
+
+int ec_graph_collect(ec_session *s, const char *d_chars, const uint32_t *d_ends) {
+    if (!s || !s->graph_loaded || (s->seg_nchars && !d_chars) || (s->seg_nc && !d_ends)) {
+        set_error("ec_graph_collect: no layout");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return s->k > 32 ? part_collect<OpsW, SolidIndexW>(s, s->gidxw, d_chars, d_ends)
+                     : part_collect<Ops64, SolidIndex>(s, s->gidx, d_chars, d_ends);
+}
+
+int ec_super_record_bytes(void) { return (int)sizeof(SuperRec); }
+int ec_start_record_bytes(void) { return (int)sizeof(StartRec); }
 
 int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *counts, uint64_t n, int k, unsigned flags) {
     if (!s || (n && (!kmers || !counts))) {

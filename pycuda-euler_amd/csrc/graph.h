@@ -596,8 +596,10 @@ __device__ inline bool is_start(const uint8_t *upal, const unsigned long long *d
 __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const unsigned long long *dfc,
                                                       const unsigned long long *dft, const unsigned int *PK,
                                                       const unsigned long long *PM, unsigned int N, unsigned int *bc,
-                                                      unsigned long long *smask, const uint8_t *excl = nullptr) {
-    const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
+                                                      unsigned long long *smask, const uint8_t *excl = nullptr,
+                                                      unsigned int n0 = 0) {
+    // nodes [n0, N) (n0 > 0: a segment of the multi-GPU finish; smask bits relative to n0)
+    const uint64_t c0 = n0 + (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
     unsigned int c = 0;
     // one bit per node (a wave's 64 consecutive nodes per word): k_starts_write reads the
@@ -607,7 +609,7 @@ __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const
         unsigned long long f;
         const bool sel = t < c1 && is_start(upal, dfc, dft, PK, PM, (unsigned int)t, f, excl);
         const unsigned long long m = __ballot(sel);
-        if ((threadIdx.x & 63) == 0 && t < c1) smask[t >> 6] = m;
+        if ((threadIdx.x & 63) == 0 && t < c1) smask[(t - n0) >> 6] = m;
         c += sel;
     }
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
@@ -622,15 +624,16 @@ __global__ void __launch_bounds__(256) k_starts_write(const uint8_t *upal, const
                                                       const unsigned long long *dft, const unsigned int *PK,
                                                       const unsigned long long *PM, unsigned int N,
                                                       const unsigned int *bs, const unsigned long long *smask,
-                                                      unsigned long long *skeys, unsigned int *svals) {
+                                                      unsigned long long *skeys, unsigned int *svals,
+                                                      unsigned int n0 = 0) {
     __shared__ unsigned int wsum[4];
-    const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
+    const uint64_t c0 = n0 + (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
     unsigned int base = blockIdx.x ? bs[blockIdx.x - 1] : 0u;
     const unsigned int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint64_t t0 = c0; t0 < c1; t0 += blockDim.x) {
         const uint64_t t = t0 + threadIdx.x;
-        const unsigned long long m = t0 < c1 ? smask[t0 >> 6 | (threadIdx.x >> 6)] : 0ull;  // (wave-uniform)
+        const unsigned long long m = t0 < c1 ? smask[(t0 - n0) >> 6 | (threadIdx.x >> 6)] : 0ull;  // (wave-uniform)
         const bool sel = t < c1 && ((m >> lane) & 1ull);
         const unsigned long long f = sel ? first_event(dfc, dft, (unsigned int)t) : 0ull;
         if (lane == 0) wsum[wid] = (unsigned int)__popcll(m);
@@ -733,8 +736,8 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
                                               const unsigned long long *coff, unsigned int N, int k, char *chars,
                                               unsigned long long chars_bound, unsigned int *cfirst,
                                               unsigned int *clast, unsigned int *headOf, unsigned int *tailOf,
-                                              unsigned int *bad) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+                                              unsigned int *bad, unsigned int n0 = 0) {
+    for (uint64_t t = n0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         if ((x & 1) && upal[x >> 1]) continue;
         const unsigned int pk = PK[x], rk = RK[x];

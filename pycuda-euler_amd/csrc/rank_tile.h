@@ -42,16 +42,19 @@ struct alignas(16) SNodeRec {
     unsigned long long fev;  // min first event over the chain
 };
 
+// nodes [n0, N): the tiles of a segment (the multi-GPU finish ranks its own segment's chains;
+// a successor outside the segment is external like one outside the tile)
 __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, const unsigned int *succ, unsigned int N,
                                                        const unsigned long long *dfc, const unsigned long long *dft,
                                                        unsigned int *LH, unsigned int *LR, unsigned long long *tcnt,
                                                        SuperRec *scratch, unsigned int *PK, unsigned int *RK,
-                                                       unsigned int *PL, unsigned long long *PM) {
+                                                       unsigned int *PL, unsigned long long *PM, unsigned int n0 = 0) {
     __shared__ uint16_t s_ls[RT_TN], s_lp[RT_TN], s_p[RT_TN], s_mn[RT_TN];
     __shared__ unsigned int s_d[RT_TN], s_cl[RT_TN];
     __shared__ unsigned long long s_cm[RT_TN];
     __shared__ unsigned int s_wsum[RT_NT / 64];
-    const unsigned int tile = blockIdx.x, base = tile * RT_TN, tid = threadIdx.x;
+    const unsigned int tile = blockIdx.x, base = n0 + tile * RT_TN, tid = threadIdx.x;
+    const unsigned int tend = base + RT_TN < N ? base + RT_TN : N;
     unsigned int ext[RT_PER];
     unsigned long long fev[RT_PER];
     bool valid[RT_PER];
@@ -61,7 +64,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         valid[q] = x < N && !((x & 1) && upal[x >> 1]);
         const unsigned int s = valid[q] ? succ[x] : NONE32;
         fev[q] = valid[q] ? first_event(dfc, dft, x) : NONE64;
-        const bool in = s != NONE32 && s / RT_TN == tile;
+        const bool in = s != NONE32 && s >= base && s < tend;
         s_ls[i] = in ? (uint16_t)(s - base) : RT_NONE;
         ext[q] = in ? NONE32 : s;
         s_lp[i] = RT_NONE;
@@ -240,6 +243,12 @@ __global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, c
     }
 }
 
+// SIDX[head] = index of a chain in a gathered super list (the multi-GPU finish)
+__global__ void __launch_bounds__(256) k_super_index(const SuperRec *srec, unsigned int M, unsigned int *SIDX) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < M; t += (uint64_t)gridDim.x * blockDim.x)
+        SIDX[srec[t].head] = (unsigned int)t;
+}
+
 // super successors as super indices (a tail's external successor starts its own chain), the
 // walk records, and which super nodes have a predecessor (the path heads: none)
 __global__ void __launch_bounds__(256) k_super_link(const SuperRec *srec, unsigned int M, const unsigned int *SIDX,
@@ -407,13 +416,80 @@ __global__ void __launch_bounds__(256) k_cycle_len_s(const unsigned int *nextR, 
 // every node: its chain's path key and rank + its offset in the chain
 __global__ void __launch_bounds__(256) k_expand(const unsigned int *LH, const unsigned int *LR, unsigned int N,
                                                 const unsigned int *SIDX, const unsigned int *PKs,
-                                                const unsigned int *RKs, unsigned int *PK, unsigned int *RK) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
+                                                const unsigned int *RKs, unsigned int *PK, unsigned int *RK,
+                                                unsigned int n0 = 0) {
+    for (uint64_t t = n0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int h = LH[t];
         if (h == NONE32 || (h & RT_FIN)) continue;  // palindrome twin / in-tile cycle (done)
         const unsigned int si = SIDX[h];
         PK[t] = PKs[si];
         RK[t] = RKs[si] + LR[t];
+    }
+}
+
+
+// ---- multi-GPU partitioned finish (ec_graph_*_part): contig starts travel as records ----------
+// a contig start found by the rank owning its node: its first event (the contig order), node,
+// path key, walk geometry (graph.h walk_of, from the owner's PK / RK and the replicated PL)
+struct alignas(16) StartRec {
+    unsigned long long ev;
+    unsigned int node, pk;
+    Walk w;
+    unsigned int clen, pad;
+};
+static_assert(sizeof(StartRec) == 48, "start record layout");
+
+__global__ void __launch_bounds__(256) k_start_recs(const unsigned int *nodes, unsigned int n, const uint8_t *upal,
+                                                    const unsigned long long *dfc, const unsigned long long *dft,
+                                                    const unsigned int *PK, const unsigned int *RK,
+                                                    const unsigned int *PL, int k, StartRec *out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int x = nodes[i];
+        StartRec r;
+        r.ev = first_event(dfc, dft, x);
+        r.node = x;
+        r.pk = PK[x] & ~CYC;
+        r.w = walk_of(upal, PK, RK, PL, x);
+        r.clen = (unsigned int)(k - 1) + r.w.len;
+        r.pad = 0;
+        out[i] = r;
+    }
+}
+__global__ void __launch_bounds__(256) k_start_keys(const StartRec *recs, unsigned int n, unsigned long long *keys,
+                                                    unsigned int *vals) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        keys[i] = recs[i].ev;
+        vals[i] = (unsigned int)i;
+    }
+}
+// contig i = the i-th start in event order: its length, key -> index map, walk geometry
+__global__ void __launch_bounds__(256) k_layout(const StartRec *recs, const unsigned int *order, unsigned int nc,
+                                                unsigned long long *clen, unsigned int *cidxOf, Walk *cwalk) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
+        const StartRec r = recs[order[i]];
+        clen[i] = r.clen;
+        cidxOf[r.pk] = (unsigned int)i;
+        cwalk[i] = r.w;
+    }
+}
+// contig ends found by this rank as node + 1 (0 elsewhere: a sum over the ranks combines them)
+__global__ void __launch_bounds__(256) k_ends_export(const unsigned int *cfirst, const unsigned int *clast, unsigned int nc,
+                                                     unsigned int *ends) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
+        ends[i] = cfirst[i] == NONE32 ? 0u : cfirst[i] + 1;
+        ends[nc + i] = clast[i] == NONE32 ? 0u : clast[i] + 1;
+    }
+}
+// ... and back: first / last node per contig, heads / tails for the GFA lookups (k_emit's)
+__global__ void __launch_bounds__(256) k_heads_from_ends(const unsigned int *ends, unsigned int nc, const uint8_t *upal,
+                                                         unsigned int *cfirst, unsigned int *clast, unsigned int *headOf,
+                                                         unsigned int *tailOf) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int f = ends[i] - 1, l = ends[nc + i] - 1;
+        cfirst[i] = f;
+        clast[i] = l;
+        headOf[f] = (unsigned int)i;
+        tailOf[twin_node(upal, l)] = (unsigned int)i;
     }
 }
 

@@ -11,9 +11,12 @@ result (the reference's per-partition contigs were never merged):
      key) and exchanged with ONE all-to-all-v (torch.distributed, backend "nccl" = RCCL);
   3. each owner merges what it received (sum of counts, min of first events) and applies the
      solid filter count > limit (build:37-39) -- the reduceByKey of ref_spark.py:84;
-  4. the solid sets are all-gathered and every rank runs the graph phase (links, list ranking,
-     contig starts / order, contig strings, GFA links) on the full set, so every rank holds
-     the complete, reference-identical result.
+  4. the solid sets are all-gathered; every rank computes the successor links of its own
+     segment of them, ranks the chains of its segment in LDS tiles, and only the chains (~1/9
+     of the nodes) and then the contig starts are all-gathered: each rank emits its own nodes'
+     characters and rank 0 collects them (one reduce) with the GFA links -- the complete,
+     reference-identical result (finish="replicated": the successor parts all-gathered and
+     every rank ranks / emits the whole set).
 
 The compute steps go through an *engine* (HipEngine = libeulerhip.so on the rank's GPU) and
 the collectives through a *comm* (TorchComm = torch.distributed).  Tests drive the same
@@ -68,6 +71,17 @@ eulerhip.register("ec_graph_links_part", ctypes.c_int, [_P, _U64, _U64, _P])
 eulerhip.register("ec_graph_finish", ctypes.c_int, [_P, _P, ctypes.c_uint])
 eulerhip.register("ec_merge_owned_export", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint, _P])
 eulerhip.register("ec_graph_load_links", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _U64, _U64, _P])
+# partitioned finish (each rank ranks / emits its own segment; include/eulerhip.h)
+eulerhip.register("ec_graph_chains_part", ctypes.c_int, [_P, _U64, _U64, _P, _P, ctypes.POINTER(_U64)])
+eulerhip.register("ec_graph_rank_supers", ctypes.c_int, [_P, _P, _U64])
+eulerhip.register("ec_graph_starts_part", ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.POINTER(_U64)])
+eulerhip.register("ec_graph_layout", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)])
+eulerhip.register("ec_graph_emit_part", ctypes.c_int, [_P, _P, _P])
+eulerhip.register("ec_graph_collect", ctypes.c_int, [_P, _P, _P])
+eulerhip.register("ec_super_record_bytes", ctypes.c_int, [])
+eulerhip.register("ec_start_record_bytes", ctypes.c_int, [])
+SUPER_BYTES = 32  # ec_super_record_bytes()
+START_BYTES = 48  # ec_start_record_bytes()
 
 
 def shard_range(nreads, rank, world):
@@ -169,6 +183,43 @@ class HipEngine:
         eulerhip.check(self.L.ec_graph_finish(self._h(), ctypes.c_void_p(succ.data_ptr()), flags))
         return self.sess.fetch(k) if fetch else None
 
+    # partitioned finish: ec_graph_chains_part .. ec_graph_collect
+    def graph_chains_part(self, lo, hi, succ_part):
+        """this rank's chains as super records (uint8 tensor of n * SUPER_BYTES) and n"""
+        out = self.empty(2 * (hi - lo) * SUPER_BYTES)
+        n = ctypes.c_uint64(0)
+        eulerhip.check(self.L.ec_graph_chains_part(self._h(), int(lo), int(hi), ctypes.c_void_p(succ_part.data_ptr()),
+                                                   ctypes.c_void_p(out.data_ptr()), ctypes.byref(n)))
+        return out[: n.value * SUPER_BYTES], int(n.value)
+
+    def graph_rank_supers(self, supers, n):
+        eulerhip.check(self.L.ec_graph_rank_supers(self._h(), ctypes.c_void_p(supers.data_ptr()), int(n)))
+
+    def graph_starts_part(self, have_supers, lo, hi):
+        out = self.empty(2 * (hi - lo) * START_BYTES)
+        n = ctypes.c_uint64(0)
+        eulerhip.check(self.L.ec_graph_starts_part(self._h(), 1 if have_supers else 0, ctypes.c_void_p(out.data_ptr()),
+                                                   ctypes.byref(n)))
+        return out[: n.value * START_BYTES], int(n.value)
+
+    def graph_layout(self, starts, n):
+        nchars = ctypes.c_uint64(0)
+        eulerhip.check(self.L.ec_graph_layout(self._h(), ctypes.c_void_p(starts.data_ptr()), int(n),
+                                              ctypes.byref(nchars)))
+        return int(nchars.value)
+
+    def graph_emit_part(self, chars, ends):
+        eulerhip.check(self.L.ec_graph_emit_part(self._h(), ctypes.c_void_p(chars.data_ptr()),
+                                                 ctypes.c_void_p(ends.data_ptr())))
+
+    def graph_collect(self, chars, ends, k, fetch=True):
+        eulerhip.check(self.L.ec_graph_collect(self._h(), ctypes.c_void_p(chars.data_ptr()),
+                                               ctypes.c_void_p(ends.data_ptr())))
+        return self.sess.fetch(k) if fetch else None
+
+    def zeros(self, nbytes):
+        return self.torch.zeros(max(int(nbytes), 1), dtype=self.torch.uint8, device=self.device)
+
     def stats(self):
         return self.sess.stats()
 
@@ -227,6 +278,13 @@ class TorchComm:
         dist.all_gather_into_tensor(out, pad, group=self.group)
         return (out, szl) if with_sizes else out
 
+    def reduce_sum(self, t, dst=0):
+        """element-wise sum of every rank's uint8 tensor `t` into rank dst's (in place); the
+        partitioned finish's characters / contig ends, each byte set by exactly one rank"""
+        if self.world > 1:
+            self.dist.reduce(t, dst=dst, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t
+
     def allreduce_vec(self, vals):
         """element-wise sum over the ranks of a list of integers"""
         dev = "cuda" if self.dist.get_backend(self.group) == "nccl" else "cpu"
@@ -245,8 +303,45 @@ class TorchComm:
 
 
 # ---- the orchestration -----------------------------------------------------------------------
+def _gather_concat(comm, t, nbytes_each=None):
+    """all-gather of variable-size uint8 parts, padding dropped (rank order); returns (tensor, sizes)"""
+    g, sz = comm.allgatherv(t, fill=0, with_sizes=True)
+    if comm.world == 1:
+        return g, sz
+    mx = max(max(sz), 1)
+    return comm.torch.cat([g[r * mx: r * mx + sz[r]] for r in range(comm.world)]), sz
+
+
+def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None):
+    """The graph finish with every rank ranking / emitting its own segment (ec_graph_chains_part ..
+    ec_graph_collect): all-gathers of the chains' super records (~1/9 of the nodes on the
+    super-k-mer path) and of the contig starts, one reduce of the contig characters to rank 0.
+    Returns rank 0's result (None elsewhere)."""
+    tick = tick or (lambda name: None)
+    sup, _ = engine.graph_chains_part(lo, hi, part)
+    tick("chains")
+    supers, _ = _gather_concat(comm, sup)
+    M = supers.numel() // SUPER_BYTES
+    engine.graph_rank_supers(supers, M)
+    tick("rank")
+    st, _ = engine.graph_starts_part(M > 0, lo, hi)
+    starts, _ = _gather_concat(comm, st)
+    nc = starts.numel() // START_BYTES
+    nchars = engine.graph_layout(starts, nc)
+    tick("starts")
+    chars = engine.zeros(nchars)
+    ends = engine.zeros(max(8 * nc, 8))
+    engine.graph_emit_part(chars, ends)
+    comm.reduce_sum(chars)
+    comm.reduce_sum(ends)
+    tick("emit")
+    res = engine.graph_collect(chars, ends, k, fetch=fetch) if comm.rank == 0 else None
+    tick("collect")
+    return res
+
+
 def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None,
-                     phase_ms=None, partitioned=None, fetch=True):
+                     phase_ms=None, partitioned=None, fetch=True, finish="partitioned"):
     """Run steps 1-4 for this rank; returns (result, n_positions_total).  on_count(stats)
     receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING); phase_ms, a
     dict, receives the wall time of every step (device-synchronised by the engine calls).
@@ -300,17 +395,20 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
             tick("load")
             engine.graph_links_part(lo, hi, part)
             tick("links")
-        # every rank's part size is known from the solid-set sizes: no size exchange
-        gathered, psz = comm.allgatherv(part[: 8 * (hi - lo)], fill=0xFF, with_sizes=True,
-                                        sizes=[8 * x for x in nrec])
-        if comm.world > 1:  # drop the padding: node order = rank order
-            mx = max(max(psz), 1)
-            succ = comm.torch.cat([gathered[r * mx: r * mx + psz[r]] for r in range(comm.world)])
-        else:
-            succ = gathered
-        tick("gather_links")
-        res = engine.graph_finish(succ, k, flags, fetch=fetch)
-        tick("graph")
+        if finish == "partitioned" and hasattr(engine, "graph_chains_part"):
+            res = partitioned_finish(engine, comm, k, lo, hi, part, fetch=fetch, tick=tick)
+        else:  # replicated finish: the successor parts all-gathered, every rank ranks / emits everything
+            # every rank's part size is known from the solid-set sizes: no size exchange
+            gathered, psz = comm.allgatherv(part[: 8 * (hi - lo)], fill=0xFF, with_sizes=True,
+                                            sizes=[8 * x for x in nrec])
+            if comm.world > 1:  # drop the padding: node order = rank order
+                mx = max(max(psz), 1)
+                succ = comm.torch.cat([gathered[r * mx: r * mx + psz[r]] for r in range(comm.world)])
+            else:
+                succ = gathered
+            tick("gather_links")
+            res = engine.graph_finish(succ, k, flags, fetch=fetch)
+            tick("graph")
     if phase_ms is not None:
         for (_, a), (name, b) in zip(marks, marks[1:]):
             phase_ms[name] = phase_ms.get(name, 0.0) + (b - a) * 1e3
@@ -360,7 +458,7 @@ class ShardedAssembler:
         return self.count_stats
 
 
-def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None):
+def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None, finish="partitioned"):
     """Simulate the distributed algorithm with len(engines) ranks on the local device(s):
     same engine calls, the collectives done by concatenation.  Returns rank 0's result."""
     world = len(engines)
@@ -370,10 +468,10 @@ def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=N
         lo, hi = shard_range(nreads, r, world)
         b0, b1 = int(off[lo]), int(off[hi])
         parts.append((buf[b0:b1], off[lo:hi + 1] - off[lo], lo))
-    return local_sharded_assemble_shards(engines, parts, k, limit, flags, partitioned)
+    return local_sharded_assemble_shards(engines, parts, k, limit, flags, partitioned, finish)
 
 
-def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partitioned=None):
+def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partitioned=None, finish="partitioned"):
     """local_sharded_assemble on given shards: parts[r] = (buf, off, read_base) of rank r (host
     arrays; global read ids read_base.., increasing with r, gaps allowed)."""
     import torch
@@ -423,12 +521,39 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
     rb = rec_bytes(k)
     nrec = [x.numel() // rb for x in solids]
     parts = []
+    segs = []
     for r, eng in enumerate(engines):
         lo = sum(nrec[:r])
         eng.graph_load(allsolid.to(eng.device), k, flags)
         part = eng.empty(8 * nrec[r])
         eng.graph_links_part(lo, lo + nrec[r], part)
+        segs.append((lo, lo + nrec[r], part))
         parts.append(part[: 8 * nrec[r]].to(engines[0].device))
+    if finish == "partitioned" and hasattr(engines[0], "graph_chains_part"):
+        return local_partitioned_finish(engines, segs, k), P
     succ = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=engines[0].device)
     res = engines[0].graph_finish(succ if succ.numel() else engines[0].empty(4), k, flags)
     return res, P
+
+
+def local_partitioned_finish(engines, segs, k):
+    """partitioned_finish with the collectives done by concatenation / summation (simulated ranks)"""
+    import torch
+
+    dev = engines[0].device
+    sups = [eng.graph_chains_part(lo, hi, part)[0] for eng, (lo, hi, part) in zip(engines, segs)]
+    supers = torch.cat([x.to(dev) for x in sups])
+    M = supers.numel() // SUPER_BYTES
+    for eng in engines:
+        eng.graph_rank_supers(supers.to(eng.device), M)
+    sts = [eng.graph_starts_part(M > 0, lo, hi)[0] for eng, (lo, hi, _) in zip(engines, segs)]
+    starts = torch.cat([x.to(dev) for x in sts])
+    nc = starts.numel() // START_BYTES
+    chars, ends = None, None
+    for eng in engines:
+        nchars = eng.graph_layout(starts.to(eng.device), nc)
+        c, e = eng.zeros(nchars), eng.zeros(max(8 * nc, 8))
+        eng.graph_emit_part(c, e)
+        chars = c.to(dev) if chars is None else chars + c.to(dev)
+        ends = e.view(torch.int32).to(dev) if ends is None else ends + e.view(torch.int32).to(dev)
+    return engines[0].graph_collect(chars, ends.view(torch.uint8), k)

@@ -205,3 +205,68 @@ class FakeEngine:
         assert np.array_equal(got, want), "gathered successor parts differ from the whole-set links"
         return self.assemble_from_solid(self._bytes(self.grecs), k, flags)
 
+
+    # ---- partitioned finish (distributed.partitioned_finish): the same records / collectives,
+    # computed on the whole set by the design model -- every node is its own chain; contig i is
+    # emitted by the rank whose segment holds the canonical id of its first k-mer
+    SUP = np.dtype([("head", "<u4"), ("succ", "<u4"), ("w", "<u4"), ("pad", "<u4"), ("fmin", "<u8"), ("pad2", "<u8")])
+    ST = np.dtype([("ev", "<u8"), ("node", "<u4"), ("pk", "<u4"), ("walk", "<u4", 6), ("clen", "<u4"), ("pad", "<u4")])
+
+    def zeros(self, nbytes):
+        return torch.zeros(max(int(nbytes), 1), dtype=torch.uint8)
+
+    def graph_chains_part(self, lo, hi, part):
+        self.lo, self.hi = lo, hi
+        succ = np.frombuffer(part.numpy().tobytes(), dtype=np.uint32)[: 2 * (hi - lo)]
+        out = np.zeros(2 * (hi - lo), self.SUP)
+        out["head"] = np.arange(2 * lo, 2 * hi, dtype=np.uint32)
+        out["succ"] = succ
+        out["w"] = 1
+        return self._bytes(out), len(out)
+
+    def graph_rank_supers(self, supers, M):
+        sup = np.frombuffer(supers.numpy().tobytes(), dtype=self.SUP)[:M]
+        N = 2 * len(self.grecs)
+        assert M == N and np.array_equal(sup["head"], np.arange(N)), "super records out of rank order"
+        want = np.array([self._succ_of(x) for x in range(N)], dtype=np.uint32)
+        assert np.array_equal(sup["succ"], want), "gathered chains differ from the whole-set links"
+        self.full = self.assemble_from_solid(self._bytes(self.grecs), self.gk)
+
+    def _first_id(self, c):
+        x = encode(c[: self.gk])
+        return self.gid[min(x, self._tw(x))]
+
+    def graph_starts_part(self, have_supers, lo, hi):
+        own = [i for i, c in enumerate(self.full.contigs) if lo <= self._first_id(c) < hi]
+        out = np.zeros(len(own), self.ST)
+        out["ev"] = own
+        out["node"] = own
+        out["pk"] = own
+        out["clen"] = [len(self.full.contigs[i]) for i in own]
+        self.own = own
+        return self._bytes(out), len(out)
+
+    def graph_layout(self, starts, n):
+        st = np.frombuffer(starts.numpy().tobytes(), dtype=self.ST)[:n]
+        st = st[np.argsort(st["ev"], kind="stable")]
+        assert list(st["ev"]) == list(range(len(self.full.contigs))), "gathered starts miss contigs"
+        self.coff = np.concatenate([[0], np.cumsum(st["clen"].astype(np.int64))])
+        self.nc = n
+        return int(self.coff[-1])
+
+    def graph_emit_part(self, chars, ends):
+        e = np.zeros(max(2 * self.nc, 2), np.uint32)
+        c = chars.numpy()
+        for i in self.own:
+            s = self.full.contigs[i].encode()
+            c[self.coff[i]:self.coff[i] + len(s)] = np.frombuffer(s, np.uint8)
+            e[i] = e[self.nc + i] = i + 1
+        ends[: 8 * self.nc] = torch.from_numpy(e[: 2 * self.nc].view(np.uint8).copy())
+
+    def graph_collect(self, chars, ends, k, fetch=True):
+        e = np.frombuffer(ends.numpy().tobytes(), dtype=np.uint32)[: 2 * self.nc]
+        assert list(e) == list(range(1, self.nc + 1)) * 2, "contig ends not set exactly once"
+        ch = chars.numpy().tobytes()
+        contigs = [ch[self.coff[i]:self.coff[i + 1]].decode() for i in range(self.nc)]
+        assert contigs == self.full.contigs
+        return _Result(self.full.dict_items, contigs, self.full.links)

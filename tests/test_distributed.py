@@ -23,7 +23,8 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None, want_counts=False):
+def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None, want_counts=False,
+            finish="partitioned"):
     import torch
     import torch.distributed as dist
 
@@ -47,17 +48,22 @@ def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None, w
                                               torch.frombuffer(bytearray(buf or b"\0"), dtype=torch.uint8),
                                               torch.from_numpy(off), len(mine), lo if gap is None else rank * gap,
                                               k, limit,
-                                              partitioned=partitioned)
-        q.put((rank, P, res.contigs, res.links) + ((eng.rule, eng.last_counts) if want_counts else ()))
+                                              partitioned=partitioned, finish=finish)
+        # the partitioned finish leaves the result on rank 0 only
+        q.put((rank, P, res.contigs if res else None, res.links if res else None)
+              + ((eng.rule, eng.last_counts) if want_counts else ()))
     finally:
         dist.destroy_process_group()
 
 
-def _run(reads, k, limit, world, partitioned=None, gap=None, want_counts=False):
+def _run(reads, k, limit, world, partitioned=None, gap=None, want_counts=False, finish="partitioned"):
+    """every rank's (rank, P, contigs, links[, rule, counts]); with the partitioned finish
+    (the default, partitioned links) only rank 0 holds contigs / links (None elsewhere)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q, partitioned, gap, want_counts))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, reads, k, limit, q, partitioned, gap, want_counts,
+                                               finish))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -65,16 +71,25 @@ def _run(reads, k, limit, world, partitioned=None, gap=None, want_counts=False):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    return sorted(out)
+    out = sorted(out, key=lambda o: o[0])
+    assert out[0][2] is not None, "rank 0 holds no result"
+    part_finish = finish == "partitioned" and partitioned is not False
+    return [o for o in out if not (part_finish and o[0] != 0 and o[2] is None)]
 
 
 # partitioned: each rank computes the links of its own owner segment (ec_graph_links_part's
 # rule restated in fake_engine) and the parts are all-gathered; replicated: one rank-local
 # graph phase on the gathered set (ec_assemble_from_solid)
-@pytest.mark.parametrize("world,partitioned", [(2, True), (3, True), (2, False)])
-def test_sharded_matches_reference_g200(world, partitioned):
+@pytest.mark.parametrize("world,partitioned,finish", [(2, True, "partitioned"), (3, True, "partitioned"),
+                                                     (3, True, "replicated"), (2, False, "replicated")])
+def test_sharded_matches_reference_g200(world, partitioned, finish):
+    """partitioned finish: every rank ranks / emits its own segment, the chains, the contig
+    starts and the characters travel (distributed.partitioned_finish); replicated: the successor
+    parts are all-gathered and every rank finishes the whole set"""
     (case,) = [c for c in golden_cases("g200.json") if c["k"] == 15]
-    for rank, P, contigs, links in _run(case["reads"], 15, 1, world, partitioned):
+    out = _run(case["reads"], 15, 1, world, partitioned, finish=finish)
+    assert len(out) == (1 if finish == "partitioned" else world)
+    for rank, P, contigs, links in out:
         assert contigs == case["contigs"] and links == case["links"]
 
 
