@@ -301,3 +301,31 @@ def test_local_sharded_8_ranks_k51_vs_oracle(partitioned):
     finally:
         for e in es:
             e.sess.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 5])
+@pytest.mark.parametrize("seed,g,n,L,err,k,circ", [(11, 20_000, 6_000, 100, 0.002, 31, False),
+                                                   (12, 3_000, 1_500, 60, 0.0, 25, True),
+                                                   (13, 30_000, 8_000, 150, 0.002, 51, False),
+                                                   (14, 2_000, 800, 40, 0.01, 16, False)])
+def test_partitioned_finish_equals_replicated(world, seed, g, n, L, err, k, circ):
+    """distributed.partitioned_finish (each rank ranks its own segment's chains, the chains and
+    contig starts all-gathered, every rank emits its own nodes, rank 0 collects) against the
+    replicated finish and the oracle: cycles (circular genomes) across the segments, k <= 32
+    and k > 32, error-rich reads"""
+    import distributed
+
+    es = [distributed.HipEngine(0) for _ in range(world)]
+    try:
+        buf, off = make_reads(g, n, L, 7900 + seed, err=err, n_rate=0.001, circular=circ)
+        ref = oracle.assemble_packed(buf, off, k, 1)
+        for finish in ("partitioned", "replicated"):
+            res, P = distributed.local_sharded_assemble(es, buf, off, k, 1, finish=finish)
+            assert P == ref["n_positions"], finish
+            assert res.contig_bytes == ref["contig_chars"], finish
+            assert np.array_equal(res.contig_offsets, ref["contig_offsets"]), finish
+            assert res.links == oracle.unpack_links(ref), finish
+            assert res.stats.n_dict == ref["n_dict"], finish
+    finally:
+        for e in es:
+            e.sess.close()

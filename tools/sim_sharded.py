@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--err", type=float, default=0.0, help="substitution rate (bench ecoli10m_err: 0.005)")
+    ap.add_argument("--finish", default="partitioned", choices=["partitioned", "replicated"],
+                    help="partitioned: every rank ranks / emits its own segment (distributed.partitioned_finish)")
     ap.add_argument("--weak", action="store_true",
                     help="bench.py's default N > 1 mode: every rank its own --reads reads (synth part = rank)")
     a = ap.parse_args()
@@ -86,23 +88,62 @@ def main():
             eng.graph_links_part(lo, lo + nrec[r], part)
             tick("links", t0)
             parts.append(part[: 8 * nrec[r]])
-        succ = torch.cat(parts)
-        eng = engines[0]
-        t0 = time.perf_counter()
         import ctypes
         import eulerhip
-        eulerhip.check(eng.L.ec_graph_finish(eng._h(), ctypes.c_void_p(succ.data_ptr()), eulerhip.EC_FLAG_TIMING))
-        tick("finish", t0)
-        t0 = time.perf_counter()
-        res = eng.sess.fetch(31)
-        tick("fetch", t0)
-        st = eng.stats()
-        print("finish stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
+        segs = [(sum(nrec[:r]), sum(nrec[:r + 1]), parts[r]) for r in range(world)]
+        extra = ""
+        if a.finish == "replicated":
+            succ = torch.cat(parts)
+            eng = engines[0]
+            t0 = time.perf_counter()
+            eulerhip.check(eng.L.ec_graph_finish(eng._h(), ctypes.c_void_p(succ.data_ptr()), eulerhip.EC_FLAG_TIMING))
+            tick("finish", t0)
+            t0 = time.perf_counter()
+            res = eng.sess.fetch(31)
+            tick("fetch", t0)
+            st = eng.stats()
+            print("finish stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
+        else:  # distributed.partitioned_finish, every rank's calls timed
+            sups = []
+            for eng, (lo, hi, part) in zip(engines, segs):
+                t0 = time.perf_counter()
+                sups.append(eng.graph_chains_part(lo, hi, part)[0])
+                tick("chains", t0)
+            supers = torch.cat(sups)
+            M = supers.numel() // distributed.SUPER_BYTES
+            for eng in engines:
+                t0 = time.perf_counter()
+                eng.graph_rank_supers(supers, M)
+                tick("rank_supers", t0)
+            sts = []
+            for eng, (lo, hi, _) in zip(engines, segs):
+                t0 = time.perf_counter()
+                sts.append(eng.graph_starts_part(M > 0, lo, hi)[0])
+                tick("starts", t0)
+            starts = torch.cat(sts)
+            nc = starts.numel() // distributed.START_BYTES
+            chars = ends = None
+            for eng in engines:
+                t0 = time.perf_counter()
+                nchars = eng.graph_layout(starts, nc)
+                tick("layout", t0)
+                t0 = time.perf_counter()
+                c, e = eng.zeros(nchars), eng.zeros(max(8 * nc, 8))
+                eng.graph_emit_part(c, e)
+                tick("emit", t0)
+                chars = c if chars is None else chars + c
+                ends = e.view(torch.int32) if ends is None else ends + e.view(torch.int32)
+            t0 = time.perf_counter()
+            res = engines[0].graph_collect(chars, ends.view(torch.uint8), 31)
+            tick("collect", t0)
+            extra = ", chains gathered %.1f MB (%d), starts %.2f MB, chars %.1f MB" % (
+                supers.numel() / 1e6, M, starts.numel() / 1e6, chars.numel() / 1e6)
         print("export per rank:", [round(x, 2) for x in t["export"]], "count per rank:", [round(x, 2) for x in t["count"]])
-        print("rep %d  ranks %d  per-rank max ms: %s  exchanged bytes/rank ~%.0f MB, gathered %.0f MB" % (
-            rep, world, {k: round(max(v), 2) for k, v in t.items()},
-            sum(c for c in sends[0][1]) * rb / 1e6, allsolid.numel() / 1e6))
-    print("contigs", len(res.contig_offsets) - 1)
+        mx_ph = {k: round(max(v), 2) for k, v in t.items()}
+        print("rep %d  ranks %d  per-rank max ms: %s  sum %.2f  exchanged bytes/rank ~%.0f MB, gathered %.0f MB%s" % (
+            rep, world, mx_ph, sum(mx_ph.values()),
+            sum(c for c in sends[0][1]) * rb / 1e6, allsolid.numel() / 1e6, extra))
+    print("contigs", len(res.contig_offsets) - 1, "chars", len(res.contig_bytes))
 
 
 if __name__ == "__main__":
