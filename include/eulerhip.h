@@ -284,6 +284,15 @@ uint64_t ec_reads_span(const ec_reads *r, uint64_t first, uint64_t count);
 /* copy reads [first, first+count): their bases and count+1 offsets rebased to 0 */
 int ec_reads_copy(const ec_reads *r, uint64_t first, uint64_t count, uint8_t *bases, uint64_t *offsets);
 void ec_reads_free(ec_reads *r);
+/* format | EC_READS_PACKED: ec_reads_load writes the bases straight as 2-bit codes (4 a byte, the
+ * layout of ec_assemble_packed_host) into page-locked memory plus the bytes other than A/C/G/T as
+ * (position, byte) exceptions -- no ASCII copy, no separate ec_pack_reads pass; read_len = the
+ * common read length (0 if the lengths differ; then the offsets travel too) */
+#define EC_READS_PACKED 0x100
+int ec_reads_packed_info(const ec_reads *r, uint64_t *nbases, uint32_t *read_len, uint64_t *n_exc);
+int ec_reads_packed_copy(const ec_reads *r, uint8_t *codes, uint64_t *exc_pos, uint8_t *exc_byte);
+/* ec_assemble_packed_host on a packed read set (FASTA / FASTQ file -> contigs in two calls) */
+int ec_assemble_packed_reads(ec_session *s, const ec_reads *r, int k, int limit, unsigned flags);
 
 /* ---- read-sharded multi-GPU building blocks (pycuda-euler_amd/distributed.py) ------------
  * Replace the reference's distribution layer (Spark mapPartitions of assemble2,

@@ -14,6 +14,8 @@
 // then copy at prefix-summed offsets), so a multi-GB read set is ingested at memory speed.
 #include "common.h"
 
+#include <hip/hip_runtime.h>
+
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -29,6 +31,19 @@ using ec::set_error;
 struct ec_reads {
     std::vector<uint8_t> bases;
     std::vector<uint64_t> offsets;  // n_reads + 1
+    // EC_READS_PACKED: the bases as 2-bit codes (4 a byte, ec_assemble_packed_host's layout) in
+    // page-locked memory, the bytes other than A/C/G/T as exceptions; bases stays empty
+    bool packed = false;
+    uint8_t *codes = nullptr;
+    uint64_t nbases = 0;
+    uint32_t read_len = 0;  // every read this long (0: lengths differ)
+    bool pinned = true;     // codes from hipHostMalloc (else malloc)
+    std::vector<uint64_t> exc_pos;
+    std::vector<uint8_t> exc_byte;
+    ~ec_reads() {
+        if (codes && pinned) (void)hipHostFree(codes);
+        else free(codes);
+    }
 };
 
 namespace {
@@ -45,7 +60,20 @@ struct Chunk {
     uint64_t lo = 0, hi = 0;       // byte range [lo, hi), starts at a line start
     uint64_t lines_before = 0;     // FASTQ: global index of the first line of the chunk
     uint64_t reads = 0, bases = 0; // pass-1 counts
+    uint64_t exc = 0;              // packed: bytes other than A/C/G/T among its bases
 };
+
+// 2-bit code of an ASCII base (A 0, C 1, G 2, T 3) and whether the byte is exactly that letter
+inline uint8_t code2(uint8_t c) { return (uint8_t)(((c >> 1) ^ (c >> 2)) & 3u); }
+inline bool is_exc(uint8_t c) {
+    static const uint8_t letter[4] = {'A', 'C', 'G', 'T'};
+    return letter[code2(c)] != c;
+}
+inline uint64_t count_exc(const uint8_t *p, uint64_t n) {
+    uint64_t e = 0;
+    for (uint64_t i = 0; i < n; i++) e += is_exc(p[i]);
+    return e;
+}
 
 // visit the lines of [lo, hi): fn(line_begin, line_end_excl_newline)
 template <typename Fn>
@@ -64,6 +92,8 @@ void for_lines(const uint8_t *p, uint64_t lo, uint64_t hi, Fn fn) {
 extern "C" {
 
 int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
+    const bool pack = (format & EC_READS_PACKED) != 0;
+    format &= ~EC_READS_PACKED;
     if (!path || !out || format < EC_FASTA_RECORDS || format > EC_FASTQ) {
         set_error("bad arguments");
         return EC_ERR_ARG;
@@ -125,6 +155,7 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
                 strip(p, b, e);
                 c.reads++;
                 c.bases += e - b;
+                if (pack) c.exc += count_exc(p + b, e - b);
             });
         } else {
             for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
@@ -134,6 +165,7 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
                 }
                 strip(p, b, e);
                 c.bases += e - b;  // bases before the chunk's first header are resolved below
+                if (pack) c.exc += count_exc(p + b, e - b);
             });
         }
     };
@@ -163,6 +195,7 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
                     if (e > b && p[e - 1] == '\r') e--;  // rstrip('\n') of a CRLF line keeps '\r'; drop it
                     c.reads++;
                     c.bases += e - b;
+                    if (pack) c.exc += count_exc(p + b, e - b);
                 }
                 li++;
             });
@@ -174,10 +207,10 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
     }
     // FASTA records: sequence bytes before a chunk's first header belong to the previous
     // chunk's last record (or to no record at the file start)
-    std::vector<uint64_t> lead(T, 0);
+    std::vector<uint64_t> lead(T, 0), lead_exc(T, 0);
     if (format == EC_FASTA_RECORDS) {
         auto lead_of = [&](int t) {  // stripped bytes before the chunk's first header
-            uint64_t sum = 0, q = ch[t].lo;
+            uint64_t sum = 0, q = ch[t].lo, ex = 0;
             while (q < ch[t].hi) {
                 const void *nl = memchr(p + q, '\n', ch[t].hi - q);
                 uint64_t e = nl ? (uint64_t)((const uint8_t *)nl - p) : ch[t].hi;
@@ -186,28 +219,49 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
                 const uint64_t next = e + 1;
                 strip(p, b, e);
                 sum += e - b;
+                if (pack) ex += count_exc(p + b, e - b);
                 q = next;
             }
             lead[t] = sum;
+            lead_exc[t] = ex;
         };
         for (int t = 0; t < T; t++) lead_of(t);
         // chunk t's leading bytes: counted by chunk t, belong to the last record before it
         bool any_header_before = false;
         for (int t = 0; t < T; t++) {
-            if (!any_header_before) ch[t].bases -= lead[t];  // no record yet: ignored text
+            if (!any_header_before) ch[t].bases -= lead[t], ch[t].exc -= lead_exc[t];  // no record yet: ignored text
             any_header_before |= ch[t].reads > 0;
         }
     }
-    uint64_t R = 0, B = 0;
-    std::vector<uint64_t> r0(T), b0(T);
+    uint64_t R = 0, B = 0, X = 0;
+    std::vector<uint64_t> r0(T), b0(T), x0(T);
     for (int t = 0; t < T; t++) {
         r0[t] = R;
         b0[t] = B;
+        x0[t] = X;
         R += ch[t].reads;
         B += ch[t].bases;
+        X += ch[t].exc;
     }
     try {
-        r->bases.resize(std::max<uint64_t>(B, 1));
+        if (pack) {
+            r->packed = true;
+            r->nbases = B;
+            const uint64_t nc = (B + 3) / 4 + 16;
+            // page-locked so the codes go over PCIe at DMA speed; a host without a usable GPU
+            // (ingest tests on CPU) gets ordinary memory
+            if (hipHostMalloc((void **)&r->codes, nc, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                r->codes = static_cast<uint8_t *>(malloc(nc));
+                if (!r->codes) throw std::bad_alloc();
+                r->pinned = false;
+            }
+            memset(r->codes, 0, nc);
+            r->exc_pos.resize(X);
+            r->exc_byte.resize(X);
+        } else {
+            r->bases.resize(std::max<uint64_t>(B, 1));
+        }
         r->offsets.resize(R + 1);
     } catch (...) {
         delete r;
@@ -217,19 +271,39 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
     }
     uint8_t *ob = r->bases.data();
     uint64_t *oo = r->offsets.data();
+    uint8_t *oc = r->codes;
+    uint64_t *xp = r->exc_pos.data();
+    uint8_t *xb = r->exc_byte.data();
     // pass 2: copy.  Record reads get offsets[i] at their header; their bytes follow contiguously
     // across chunk boundaries because b0 is a prefix sum in file order.
     auto pass2 = [&](int t) {
         const Chunk &c = ch[t];
-        uint64_t ri = r0[t], bi = b0[t];
+        uint64_t ri = r0[t], bi = b0[t], xi = x0[t];
+        // packed: the code bytes of bases [b0[t], b0[t + 1]) -- the first and the last may be
+        // shared with the neighbouring chunks' bases: atomic OR there
+        const uint64_t cb0 = b0[t] >> 2, cb1 = t + 1 < T ? (b0[t + 1] + 3) >> 2 : 0;
+        auto put = [&](const uint8_t *src, uint64_t n) {
+            if (!pack) {
+                memcpy(ob + bi, src, n);
+                bi += n;
+                return;
+            }
+            for (uint64_t i = 0; i < n; i++, bi++) {
+                const uint8_t ch8 = src[i];
+                const uint8_t v = (uint8_t)(code2(ch8) << (2 * (bi & 3)));
+                const uint64_t cb = bi >> 2;
+                if (cb == cb0 || cb + 1 >= cb1) __atomic_fetch_or(oc + cb, v, __ATOMIC_RELAXED);
+                else oc[cb] |= v;
+                if (is_exc(ch8)) xp[xi] = bi, xb[xi++] = ch8;
+            }
+        };
         if (format == EC_FASTQ) {
             uint64_t li = c.lines_before;
             for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
                 if (li % 4 == 1) {
                     if (e > b && p[e - 1] == '\r') e--;
                     oo[ri++] = bi;
-                    memcpy(ob + bi, p + b, e - b);
-                    bi += e - b;
+                    put(p + b, e - b);
                 }
                 li++;
             });
@@ -238,8 +312,7 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
                 if (b < e && p[b] == '>') return;
                 strip(p, b, e);
                 oo[ri++] = bi;
-                memcpy(ob + bi, p + b, e - b);
-                bi += e - b;
+                put(p + b, e - b);
             });
         } else {
             const bool owned_lead = ri > 0;  // leading bytes continue the previous record
@@ -252,8 +325,7 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
                 }
                 if (in_lead && !owned_lead) return;
                 strip(p, b, e);
-                memcpy(ob + bi, p + b, e - b);
-                bi += e - b;
+                put(p + b, e - b);
             });
         }
     };
@@ -265,8 +337,49 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
     }
     oo[R] = B;
     if (p) munmap((void *)p, n);
+    if (pack && R) {  // one read length: no offsets travel
+        const uint64_t L = oo[1] - oo[0];
+        bool one = L <= 0xFFFFFFFFull;
+        for (uint64_t i = 0; i < R && one; i++) one = oo[i + 1] - oo[i] == L;
+        r->read_len = one ? (uint32_t)L : 0u;
+    }
     *out = r;
     return EC_OK;
+}
+
+int ec_reads_packed_info(const ec_reads *r, uint64_t *nbases, uint32_t *read_len, uint64_t *n_exc) {
+    if (!r || !r->packed) {
+        set_error("not a packed read set (ec_reads_load with EC_READS_PACKED)");
+        return EC_ERR_ARG;
+    }
+    if (nbases) *nbases = r->nbases;
+    if (read_len) *read_len = r->read_len;
+    if (n_exc) *n_exc = r->exc_pos.size();
+    return EC_OK;
+}
+
+int ec_reads_packed_copy(const ec_reads *r, uint8_t *codes, uint64_t *exc_pos, uint8_t *exc_byte) {
+    if (!r || !r->packed) {
+        set_error("not a packed read set (ec_reads_load with EC_READS_PACKED)");
+        return EC_ERR_ARG;
+    }
+    if (codes && r->nbases) memcpy(codes, r->codes, (r->nbases + 3) / 4);
+    if (exc_pos && !r->exc_pos.empty()) memcpy(exc_pos, r->exc_pos.data(), r->exc_pos.size() * 8);
+    if (exc_byte && !r->exc_byte.empty()) memcpy(exc_byte, r->exc_byte.data(), r->exc_byte.size());
+    return EC_OK;
+}
+
+// the fused assembly straight from a packed read set (its page-locked codes go over PCIe)
+int ec_assemble_packed_reads(ec_session *s, const ec_reads *r, int k, int limit, unsigned flags) {
+    if (!r || !r->packed) {
+        set_error("not a packed read set (ec_reads_load with EC_READS_PACKED)");
+        return EC_ERR_ARG;
+    }
+    const uint64_t R = r->offsets.size() - 1;
+    return ec_assemble_packed_host(s, r->codes, r->nbases, r->read_len ? nullptr : r->offsets.data(), R, r->read_len,
+                                   r->exc_pos.empty() ? nullptr : r->exc_pos.data(),
+                                   r->exc_byte.empty() ? nullptr : r->exc_byte.data(), r->exc_pos.size(), k, limit,
+                                   flags);
 }
 
 uint64_t ec_reads_count(const ec_reads *r) { return r ? r->offsets.size() - 1 : 0; }
@@ -279,16 +392,20 @@ uint64_t ec_reads_span(const ec_reads *r, uint64_t first, uint64_t count) {
 }
 
 int ec_reads_copy(const ec_reads *r, uint64_t first, uint64_t count, uint8_t *bases, uint64_t *offsets) {
+    if (r && r->packed && bases && count) {
+        set_error("a packed read set holds no ASCII bases (ec_reads_packed_copy)");
+        return EC_ERR_ARG;
+    }
     if (!r || first + count > r->offsets.size() - 1 || (count && !offsets)) {
         set_error("bad shard [%llu, +%llu)", (unsigned long long)first, (unsigned long long)count);
         return EC_ERR_ARG;
     }
     const uint64_t b0 = r->offsets[first], b1 = r->offsets[first + count];
-    if (b1 > b0 && !bases) {
+    if (b1 > b0 && !bases && !r->packed) {
         set_error("null base buffer");
         return EC_ERR_ARG;
     }
-    if (b1 > b0) memcpy(bases, r->bases.data() + b0, b1 - b0);
+    if (b1 > b0 && bases) memcpy(bases, r->bases.data() + b0, b1 - b0);
     for (uint64_t i = 0; i <= count; i++) offsets[i] = r->offsets[first + i] - b0;
     return EC_OK;
 }

@@ -21,6 +21,10 @@ eulerhip.register("ec_reads_bases", _U64, [_P])
 eulerhip.register("ec_reads_span", _U64, [_P, _U64, _U64])
 eulerhip.register("ec_reads_copy", ctypes.c_int, [_P, _U64, _U64, _P, _P])
 eulerhip.register("ec_reads_free", None, [_P])
+eulerhip.register("ec_reads_packed_info", ctypes.c_int, [_P, _P, _P, _P])
+eulerhip.register("ec_reads_packed_copy", ctypes.c_int, [_P, _P, _P, _P])
+eulerhip.register("ec_assemble_packed_reads", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_uint])
+READS_PACKED = 0x100  # EC_READS_PACKED
 
 
 def detect_format(path, fasta_mode="records"):
@@ -36,13 +40,18 @@ def detect_format(path, fasta_mode="records"):
 
 
 class ReadSet:
-    """A read file parsed by the native reader (host memory, freed on close)."""
+    """A read file parsed by the native reader (host memory, freed on close).
 
-    def __init__(self, path, fmt=None, threads=0, fasta_mode="records"):
+    packed=True: the reader writes the bases straight as 2-bit codes into page-locked memory
+    (EC_READS_PACKED) -- the input of assemble(); packed_reads() copies them out."""
+
+    def __init__(self, path, fmt=None, threads=0, fasta_mode="records", packed=False):
         self.path = path
         self.format = detect_format(path, fasta_mode) if fmt is None else fmt
+        self.is_packed = bool(packed)
         h = _P()
-        eulerhip.check(eulerhip.lib().ec_reads_load(os.fsencode(path), int(self.format), int(threads), ctypes.byref(h)))
+        f = int(self.format) | (READS_PACKED if packed else 0)
+        eulerhip.check(eulerhip.lib().ec_reads_load(os.fsencode(path), f, int(threads), ctypes.byref(h)))
         self._h = h
 
     def __len__(self):
@@ -61,6 +70,28 @@ class ReadSet:
         off = np.zeros(count + 1, np.uint64)
         eulerhip.check(eulerhip.lib().ec_reads_copy(self._h, int(first), count, buf.ctypes.data, off.ctypes.data))
         return buf[:nb], off
+
+    def packed_reads(self):
+        """the packed set as an eulerhip.PackedReads (numpy copies; packed=True sets only)"""
+        nb, rl, ne = ctypes.c_uint64(0), ctypes.c_uint32(0), ctypes.c_uint64(0)
+        eulerhip.check(eulerhip.lib().ec_reads_packed_info(self._h, ctypes.byref(nb), ctypes.byref(rl),
+                                                           ctypes.byref(ne)))
+        nb, rl, ne = nb.value, rl.value, ne.value
+        codes = np.zeros(max((nb + 3) // 4, 1), np.uint8)
+        pos = np.zeros(max(ne, 1), np.uint64)
+        byt = np.zeros(max(ne, 1), np.uint8)
+        eulerhip.check(eulerhip.lib().ec_reads_packed_copy(self._h, codes.ctypes.data, pos.ctypes.data,
+                                                           byt.ctypes.data))
+        off = None
+        if not rl:
+            off = np.zeros(len(self) + 1, np.uint64)
+            eulerhip.check(eulerhip.lib().ec_reads_copy(self._h, 0, len(self), None, off.ctypes.data))
+        return eulerhip.PackedReads(codes, nb, len(self), off, rl, pos[:ne], byt[:ne])
+
+    def assemble(self, session, k, limit=1, flags=0):
+        """the fused assembly on session straight from the packed set (ec_assemble_packed_reads);
+        session.fetch(k) then returns the Result"""
+        eulerhip.check(eulerhip.lib().ec_assemble_packed_reads(session._h, self._h, int(k), int(limit), int(flags)))
 
     def reads(self):
         """the reads as Python strings (small inputs / tests)"""

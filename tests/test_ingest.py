@@ -142,3 +142,57 @@ def test_pack_2bit_rejects_bad_offsets():
             eulerhip.pack_2bit(buf, np.array(bad, np.uint64))
     pr = eulerhip.pack_2bit(buf[:0], np.zeros(1, np.uint64))
     assert pr.nreads == 0 and pr.nbases == 0
+
+
+def _same_packed(pr, ref):
+    nc = (ref.nbases + 3) // 4
+    assert pr.nbases == ref.nbases and pr.nreads == ref.nreads and pr.read_len == ref.read_len
+    assert np.array_equal(pr.codes[:nc], ref.codes[:nc])
+    assert np.array_equal(pr.exc_pos, ref.exc_pos) and np.array_equal(pr.exc_byte, ref.exc_byte)
+    assert (pr.offsets is None) == (ref.offsets is None)
+    if pr.offsets is not None:
+        assert np.array_equal(pr.offsets, ref.offsets)
+
+
+@pytest.mark.parametrize("threads", [1, 5, 16])
+def test_packed_load_equals_pack_2bit(tmp_path, threads):
+    """EC_READS_PACKED (2-bit codes written by the parser itself, chunk-boundary code bytes by
+    atomic OR) == ec_pack_reads of the ASCII load, for every format; one read length -> no offsets"""
+    rng = np.random.default_rng(40 + threads)
+    for uniform in (False, True):
+        recs = []
+        for i in range(9000):
+            n = 150 if uniform else int(rng.integers(0, 400))
+            recs.append("".join(rng.choice(list("ACGTACGTACGTNacgx"), n)))
+        fa = tmp_path / "p.fa"
+        with open(fa, "w") as f:
+            f.write("ACGTjunk before\n")
+            for i, r in enumerate(recs):
+                f.write(">r%d\n" % i)
+                for j in range(0, len(r), 61):
+                    f.write(r[j:j + 61] + ("\n" if i % 7 else "\r\n"))
+        fq = tmp_path / "p.fastq"
+        with open(fq, "w") as f:
+            for i, r in enumerate(recs):
+                f.write("@r%d\n%s\n+\n%s\n" % (i, r, ("@>" * len(r))[:len(r)]))
+        for path, fmt in ((fa, ingest.FASTA_RECORDS), (fa, ingest.FASTA_LINES), (fq, ingest.FASTQ)):
+            with ingest.ReadSet(str(path), fmt, threads) as rs:
+                buf, off = rs.packed()
+            import eulerhip
+
+            ref = eulerhip.pack_2bit(buf, off)
+            with ingest.ReadSet(str(path), fmt, threads, packed=True) as rs:
+                assert len(rs) == len(off) - 1 and rs.n_bases == len(buf)
+                _same_packed(rs.packed_reads(), ref)
+                with pytest.raises(eulerhip.EulerHipError):
+                    rs.packed(0, 1)  # no ASCII bases in a packed set
+            if uniform and fmt != ingest.FASTA_LINES:
+                assert ref.read_len == 150
+
+
+def test_packed_load_empty(tmp_path):
+    p = tmp_path / "e.fa"
+    p.write_text(">a\n>b\n")
+    with ingest.ReadSet(str(p), packed=True) as rs:
+        pr = rs.packed_reads()
+        assert len(rs) == 2 and pr.nbases == 0 and len(pr.exc_pos) == 0
