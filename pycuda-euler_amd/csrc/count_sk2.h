@@ -1120,7 +1120,11 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
 // table holds the bucket's solid keys plus those few singletons; a bucket whose twice-seen
 // cells estimate more keys than the table takes reports an overflow (the call is redone on
 // window records).  Requires limit >= 1 (with limit < 1 every key is solid).
-constexpr int SKF_BITS = 16;  // filter cells per bitmap
+// 2^17 cells a bitmap (2 x 16 KiB of LDS beside the 40 KiB table: two workgroups per CU).  At the
+// error-rich headline (~9800 distinct keys, ~800 solid a bucket) a singleton passes with
+// p^2, p = 1 - exp(-2D/m) = 0.14: ~170 singletons a table; 2^16 cells passed ~600 and overflowed
+// the 1474-key budget in many buckets
+constexpr int SKF_BITS = 17;  // filter cells per bitmap
 template <int SLOTS, int NT, bool EVEN_K>
 __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const unsigned long long *bbeg,
                                                       const unsigned long long *bend, int k, uint32_t M, double inv_m,
@@ -1195,11 +1199,17 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
         if ((tid & 63) == 0) atomicAdd(&s_cells[0], n2), atomicAdd(&s_cells[1], n1);
         __syncthreads();
         if (tid == 0) {
+            // D distinct keys (linear counting on the seen-once cells, 2 marks a key); the
+            // seen-twice cells beyond those of random collisions, m (1 - e^-l (1 + l)), l = 2D/m,
+            // are ~2 per repeated key S; a singleton passes when both its cells hold another
+            // mark, (1 - e^-l)^2: the table receives S + (D - S) (1 - e^-l)^2 keys
             const double m = (double)(1u << SKF_BITS);
-            const double k2 = -m * log(1.0 - (double)min(s_cells[0], CM) / m) / 2.0;
-            const double k1 = -m * log(1.0 - (double)min(s_cells[1], CM) / m) / 2.0;
-            if (k2 > (double)max_keys) s_over[0] = 1;  // (default: the table would pass ~3/4 full)
-            else atomicAdd(ndistinct, (unsigned long long)llround(k1));
+            const double D = -m * log(1.0 - (double)min(s_cells[1], CM) / m) / 2.0;
+            const double l = 2.0 * D / m, el = exp(-l);
+            const double S = fmax(0.0, ((double)s_cells[0] - m * (1.0 - el * (1.0 + l))) / 2.0);
+            const double pass = 1.1 * (S + fmax(0.0, D - S) * (1.0 - el) * (1.0 - el));  // (~10 % low: solid cells hit by collisions)
+            if (pass > (double)max_keys) s_over[0] = 1;  // (default: the table would pass ~3/4 full)
+            else atomicAdd(ndistinct, (unsigned long long)llround(D));
         }
         __syncthreads();
     }

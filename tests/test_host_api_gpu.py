@@ -78,8 +78,10 @@ def test_all_contigs_extended_dict(asm, case):
 def test_all_contigs_rejects_bad_input(asm):
     import eulerhip
 
-    G, r = asm.all_contigs({"ACGR": 2, "RCGT": 2}, 4)  # opaque R: its own complement, no links
-    assert r == ["ACGR", "RCGT"] and G == {0: ([], []), 1: ([], [])}
+    # opaque R is its own complement, so RCGT is ACGR's twin: all_contigs marks the twin of every
+    # contig k-mer done (tests/referenceAssembler.py all_contigs), one contig, no links
+    G, r = asm.all_contigs({"ACGR": 2, "RCGT": 2}, 4)
+    assert r == ["ACGR"] and G == {0: ([], [])}
     with pytest.raises(eulerhip.EulerHipError):
         asm.all_contigs({"ACG": 2}, 4)
     assert asm.all_contigs({}, 5) == ({}, [])
