@@ -1994,6 +1994,15 @@ int x_cut(ec_session *s, unsigned int U, unsigned int &nx) {
     return EC_OK;
 }
 
+// dense ids with minimizer locality (a bucket's ids contiguous, a bucket = whole minimizers:
+// the super-k-mer count, the sharded load on minimizer buckets): most links stay inside a
+// rank_tile.h tile.  Hash-bucketed ids (window records, 128-bit keys, extended alphabet) have
+// none -- every link would leave its tile and the contraction only add work
+template <typename Index>
+inline bool ids_minimizer_local(const Index &) { return false; }
+template <>
+inline bool ids_minimizer_local<SolidIndex>(const SolidIndex &x) { return x.sk != 0; }
+
 // all_contigs:79-111 on the device from the solid set of phase_count / phase_merge
 template <typename Ops, typename Index>
 int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const unsigned int *ext_succ = nullptr) {
@@ -2003,9 +2012,10 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     Scalars hsc{};
     const unsigned int N = 2 * U;
     const size_t Nn = std::max<size_t>(N, 1);
-    // list ranking by tile contraction (rank_tile.h) unless EULERHIP_RANK=1 asks for the
-    // node-level ruling set: neither needs pred / the node walk records then
-    const bool tile_rank = kn().rank != 1;
+    // list ranking by tile contraction (rank_tile.h) on minimizer-local ids, the node-level
+    // ruling set otherwise (EULERHIP_RANK=1 / 2 force one or the other); tile ranking needs
+    // neither pred nor the node walk records
+    const bool tile_rank = kn().rank == 2 || (kn().rank != 1 && ids_minimizer_local(sidx));
 
     // ---- links ----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_LINKS);
