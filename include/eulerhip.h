@@ -148,6 +148,18 @@ int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const
 int ec_assemble_packed_host(ec_session *s, const uint8_t *codes, uint64_t nbases, const uint64_t *offsets,
                             uint64_t nreads, uint32_t read_len, const uint64_t *exc_pos, const uint8_t *exc_byte,
                             uint64_t n_exc, int k, int limit, unsigned flags);
+/* Staged packed batches (round 4): a pipeline over consecutive read batches.  ec_stage_packed_host
+ * queues one batch's H2D copies (same arguments as ec_assemble_packed_host; the host buffers must
+ * stay valid and unchanged until the batch is assembled) into one of two device slots and returns
+ * at once; ec_assemble_staged assembles the oldest staged batch (results as ec_assemble_*).
+ * Staging batch i + 1 before assembling batch i overlaps its PCIe copy with batch i's kernels:
+ *   stage(b0); stage(b1); assemble -> b0; stage(b2); assemble -> b1; ...
+ * EC_ERR_STATE: a third batch staged, or ec_assemble_staged with none (ec_assemble_packed_host
+ * also refuses while batches are staged). */
+int ec_stage_packed_host(ec_session *s, const uint8_t *codes, uint64_t nbases, const uint64_t *offsets,
+                         uint64_t nreads, uint32_t read_len, const uint64_t *exc_pos, const uint8_t *exc_byte,
+                         uint64_t n_exc);
+int ec_assemble_staged(ec_session *s, int k, int limit, unsigned flags);
 /* ASCII reads (CSR) -> that layout, on `threads` host threads (<= 0: up to 16).  codes holds
  * ceil(nbases / 4) bytes; exceptions beyond exc_cap are counted but not written (*n_exc = the
  * total: call again with a larger buffer when it exceeds exc_cap); *read_len = the common read
@@ -293,6 +305,8 @@ int ec_reads_packed_info(const ec_reads *r, uint64_t *nbases, uint32_t *read_len
 int ec_reads_packed_copy(const ec_reads *r, uint8_t *codes, uint64_t *exc_pos, uint8_t *exc_byte);
 /* ec_assemble_packed_host on a packed read set (FASTA / FASTQ file -> contigs in two calls) */
 int ec_assemble_packed_reads(ec_session *s, const ec_reads *r, int k, int limit, unsigned flags);
+/* a packed read set as a staged batch (ec_stage_packed_host; r must outlive its assembly) */
+int ec_stage_packed_reads(ec_session *s, const ec_reads *r);
 
 /* ---- read-sharded multi-GPU building blocks (pycuda-euler_amd/distributed.py) ------------
  * Replace the reference's distribution layer (Spark mapPartitions of assemble2,

@@ -194,9 +194,19 @@ struct ec_session {
         const uint64_t *exc_pos = nullptr;
         const uint8_t *exc_byte = nullptr;
         uint8_t *ascii = nullptr;         // device reads (the count kernels' input)
+        std::vector<hipEvent_t> ev;       // chunk copy events (created on demand, reused)
     } pipe;
-    std::vector<hipEvent_t> pev;  // chunk copy events (created on demand, reused)
     DevBuf p_codes, p_exc;
+    // staged packed batches (ec_stage_packed_host / ec_assemble_staged): two slots, so the copy
+    // of batch i + 1 runs on cstream while batch i is assembled; free_ev = the slot's last
+    // reader (its assemble call) done on the session stream
+    struct Staged {
+        Pipe pipe;
+        DevBuf codes, exc, off;
+        hipEvent_t free_ev = nullptr;
+        uint64_t nreads = 0, nbases = 0;
+    } stg[2];
+    int stg_head = 0, stg_n = 0;
     // extended alphabet (extended.h): its symbol table, and the one-way-link components'
     // union-find / cut / emulation buffers
     bool xalpha = false;
@@ -295,7 +305,7 @@ int pipe_upto(ec_session *s, int c) {
     c = std::min(c, pp.nchunks - 1);
     for (; pp.done <= c; pp.done++) {
         const int i = pp.done;
-        EC_HIP(hipStreamWaitEvent(s->stream, s->pev[i], 0));
+        EC_HIP(hipStreamWaitEvent(s->stream, pp.ev[i], 0));
         if (pp.packed && pp.bhi[i] > pp.blo[i]) {
             const uint64_t units = ((pp.bhi[i] + 15) >> 4) - (pp.blo[i] >> 4);
             k_unpack2<<<grid_for(units, 256, 16384), 256, 0, s->stream>>>(pp.codes, pp.blo[i], pp.bhi[i], pp.ascii);
@@ -2755,11 +2765,11 @@ int assemble(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint6
 }
 
 // ---- host input -------------------------------------------------------------------------------
+using Pipe = ec_session::Pipe;
 // Chunk plan over nbases bases (chunk boundaries at multiples of 64 bases, ~32 MiB of copied
 // bytes a chunk) and the reads each chunk completes (offsets: host array, or NULL = one length L)
-int pipe_plan(ec_session *s, uint64_t nbases, uint64_t bytes_per_base4, const uint64_t *offsets, uint64_t nreads,
-              uint64_t L) {
-    auto &pp = s->pipe;
+int pipe_plan(ec_session *s, Pipe &pp, uint64_t nbases, uint64_t bytes_per_base4, const uint64_t *offsets,
+              uint64_t nreads, uint64_t L, hipEvent_t after = nullptr) {
     const uint64_t copy_bytes = bytes_per_base4 ? (nbases + 3) / 4 : nbases;
     int nc = (int)std::min<uint64_t>(64, std::max<uint64_t>(1, copy_bytes >> 25));
     if (kn().host_chunks) nc = std::max(1, std::min(64, kn().host_chunks));
@@ -2775,25 +2785,27 @@ int pipe_plan(ec_session *s, uint64_t nbases, uint64_t bytes_per_base4, const ui
         else r = (uint64_t)(std::upper_bound(offsets + 1, offsets + nreads + 1, pp.bhi[c]) - (offsets + 1));
         pp.ravail[c] = r;
     }
-    if ((int)s->pev.size() < nc) {
-        const size_t have = s->pev.size();
-        s->pev.resize(nc, nullptr);
-        for (size_t i = have; i < (size_t)nc; i++) EC_HIP(hipEventCreateWithFlags(&s->pev[i], hipEventDisableTiming));
+    if ((int)pp.ev.size() < nc) {
+        const size_t have = pp.ev.size();
+        pp.ev.resize(nc, nullptr);
+        for (size_t i = have; i < (size_t)nc; i++) EC_HIP(hipEventCreateWithFlags(&pp.ev[i], hipEventDisableTiming));
     }
     if (!s->cstream) EC_HIP(hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking));
-    // the copies overwrite buffers the previous call's kernels may still read
-    EC_HIP(hipEventRecord(s->pev[0], s->stream));
-    EC_HIP(hipStreamWaitEvent(s->cstream, s->pev[0], 0));
+    // the copies overwrite buffers a previous call's kernels may still read: after = the event
+    // of their last reader (a staged slot), else everything queued on the session stream
+    if (!after) {
+        EC_HIP(hipEventRecord(pp.ev[0], s->stream));
+        after = pp.ev[0];
+    }
+    EC_HIP(hipStreamWaitEvent(s->cstream, after, 0));
     return EC_OK;
 }
 
 // copy the offsets entries reads [r0, r1] need (chunk by chunk: [ravail[c-1] + 1, ravail[c] + 1))
-int pipe_copy_offsets(ec_session *s, int c, const uint64_t *offsets) {
-    auto &pp = s->pipe;
+int pipe_copy_offsets(ec_session *s, const Pipe &pp, int c, const uint64_t *offsets, uint64_t *d_off) {
     const uint64_t o0 = c ? pp.ravail[c - 1] + 1 : 0, o1 = pp.ravail[c] + 1;
     if (o1 > o0)
-        EC_HIP(hipMemcpyAsync(s->h_offsets.as<uint64_t>() + o0, offsets + o0, (o1 - o0) * 8, hipMemcpyHostToDevice,
-                              s->cstream));
+        EC_HIP(hipMemcpyAsync(d_off + o0, offsets + o0, (o1 - o0) * 8, hipMemcpyHostToDevice, s->cstream));
     return EC_OK;
 }
 
@@ -2812,15 +2824,72 @@ int check_offsets(const uint64_t *offsets, uint64_t nreads, uint64_t nbytes) {
 
 // run assemble() on the pipelined input; the pipeline is drained (every chunk consumed) on any
 // return so no chunk copy is left pending against the next call's buffers
-int assemble_piped(ec_session *s, uint64_t nreads, int k, int limit, unsigned flags) {
+int assemble_piped(ec_session *s, const uint64_t *d_off, uint64_t nreads, int k, int limit, unsigned flags) {
     s->pipe.active = true;
-    int rc = assemble(s, s->h_reads.as<uint8_t>(), s->h_offsets.as<uint64_t>(), nreads, k, limit, flags);
+    s->pipe.ascii = s->h_reads.as<uint8_t>();  // (staged batches: h_reads may have grown since)
+    int rc = assemble(s, s->h_reads.as<uint8_t>(), d_off, nreads, k, limit, flags);
     if (s->pipe.done < s->pipe.nchunks) {
         pipe_all(s);
         hipStreamSynchronize(s->stream);
     }
     s->pipe.active = false;
     return rc;
+}
+
+int check_packed(const uint8_t *codes, uint64_t nbases, const uint64_t *offsets, uint64_t nreads, uint32_t read_len,
+                 const uint64_t *exc_pos, const uint8_t *exc_byte, uint64_t n_exc) {
+    if ((nbases && !codes) || (n_exc && (!exc_pos || !exc_byte))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (offsets) {
+        EC_CHECK(check_offsets(offsets, nreads, nbases));
+    } else if ((uint64_t)read_len * nreads != nbases) {
+        set_error("%llu reads of %u bases != %llu bases", (unsigned long long)nreads, read_len,
+                  (unsigned long long)nbases);
+        return EC_ERR_ARG;
+    }
+    for (uint64_t i = 0; i < n_exc; i++)
+        if (exc_pos[i] >= nbases || (i && exc_pos[i] <= exc_pos[i - 1])) {
+            set_error("exception %llu: position %llu not ascending inside [0, %llu)", (unsigned long long)i,
+                      (unsigned long long)exc_pos[i], (unsigned long long)nbases);
+            return EC_ERR_ARG;
+        }
+    return EC_OK;
+}
+
+// a packed batch's copies into (codes_b, exc_b, off_b) on cstream, chunk events in pp (the
+// plan of assemble_piped); after = the event the copies wait for (nullptr: the session stream)
+int stage_packed(ec_session *s, Pipe &pp, DevBuf &codes_b, DevBuf &exc_b, DevBuf &off_b, hipEvent_t after,
+                 const uint8_t *codes, uint64_t nbases, const uint64_t *offsets, uint64_t nreads, uint32_t read_len,
+                 const uint64_t *exc_pos, const uint8_t *exc_byte, uint64_t n_exc) {
+    const uint64_t ncodes = (nbases + 3) / 4;
+    EC_CHECK(off_b.ensure((nreads + 1) * 8));
+    EC_CHECK(codes_b.ensure(((ncodes + 3) & ~3ull) + 16));
+    EC_CHECK(exc_b.ensure(n_exc * 9 + 16));
+    EC_CHECK(pipe_plan(s, pp, nbases, 1, offsets, nreads, read_len, after));
+    pp.packed = true;
+    pp.first_len = nreads ? (offsets ? offsets[1] - offsets[0] : read_len) : 0;
+    pp.codes = codes_b.as<uint32_t>();
+    pp.exc_pos = exc_b.as<uint64_t>();
+    pp.exc_byte = exc_b.as<uint8_t>() + n_exc * 8;
+    if (n_exc) {
+        EC_HIP(hipMemcpyAsync(exc_b.p, exc_pos, n_exc * 8, hipMemcpyHostToDevice, s->cstream));
+        EC_HIP(hipMemcpyAsync(exc_b.as<uint8_t>() + n_exc * 8, exc_byte, n_exc, hipMemcpyHostToDevice, s->cstream));
+    }
+    if (!offsets)  // one read length: the offsets are made on the device (ordered before chunk 0's event)
+        k_iota_off<<<grid_for(nreads + 1, 256, 16384), 256, 0, s->cstream>>>(off_b.as<uint64_t>(), nreads + 1, read_len);
+    for (int c = 0; c < pp.nchunks; c++) {
+        // code bytes of bases [blo, bhi) (blo a multiple of 64: whole 32-bit words)
+        const uint64_t c0 = pp.blo[c] / 4, c1 = c + 1 == pp.nchunks ? ncodes : pp.bhi[c] / 4;
+        if (c1 > c0)
+            EC_HIP(hipMemcpyAsync(codes_b.as<uint8_t>() + c0, codes + c0, c1 - c0, hipMemcpyHostToDevice, s->cstream));
+        if (offsets) EC_CHECK(pipe_copy_offsets(s, pp, c, offsets, off_b.as<uint64_t>()));
+        pp.elo[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.blo[c]) - exc_pos);
+        pp.ehi[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.bhi[c]) - exc_pos);
+        EC_HIP(hipEventRecord(pp.ev[c], s->cstream));
+    }
+    return EC_OK;
 }
 
 }  // namespace
@@ -2895,7 +2964,14 @@ int ec_session_destroy(ec_session *s) {
     }
     s->p_codes.release();
     s->p_exc.release();
-    for (auto &e : s->pev) hipEventDestroy(e);
+    for (auto &e : s->pipe.ev) hipEventDestroy(e);
+    for (auto &sl : s->stg) {
+        for (auto &e : sl.pipe.ev) hipEventDestroy(e);
+        if (sl.free_ev) hipEventDestroy(sl.free_ev);
+        sl.codes.release();
+        sl.exc.release();
+        sl.off.release();
+    }
     if (s->cstream) {
         hipStreamSynchronize(s->cstream);
         hipStreamDestroy(s->cstream);
@@ -2927,7 +3003,7 @@ int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const
     EC_CHECK(s->h_offsets.ensure((nreads + 1) * 8));
     // chunked copies (reads and offsets) on the copy stream, the partition of the reads that
     // have arrived overlapping the copies of the rest (s->pipe)
-    EC_CHECK(pipe_plan(s, nbytes, 0, offsets, nreads, 0));
+    EC_CHECK(pipe_plan(s, s->pipe, nbytes, 0, offsets, nreads, 0));
     auto &pp = s->pipe;
     pp.packed = false;
     pp.first_len = nreads ? offsets[1] - offsets[0] : 0;
@@ -2936,65 +3012,86 @@ int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const
         if (pp.bhi[c] > pp.blo[c])
             EC_HIP(hipMemcpyAsync(s->h_reads.as<uint8_t>() + pp.blo[c], reads + pp.blo[c], pp.bhi[c] - pp.blo[c],
                                   hipMemcpyHostToDevice, s->cstream));
-        EC_CHECK(pipe_copy_offsets(s, c, offsets));
-        EC_HIP(hipEventRecord(s->pev[c], s->cstream));
+        EC_CHECK(pipe_copy_offsets(s, pp, c, offsets, s->h_offsets.as<uint64_t>()));
+        EC_HIP(hipEventRecord(pp.ev[c], s->cstream));
     }
-    return assemble_piped(s, nreads, k, limit, flags);
+    return assemble_piped(s, s->h_offsets.as<uint64_t>(), nreads, k, limit, flags);
 }
 
 int ec_assemble_packed_host(ec_session *s, const uint8_t *codes, uint64_t nbases, const uint64_t *offsets,
                             uint64_t nreads, uint32_t read_len, const uint64_t *exc_pos, const uint8_t *exc_byte,
                             uint64_t n_exc, int k, int limit, unsigned flags) {
     refresh_knobs();
-    if (!s || (nbases && !codes) || (n_exc && (!exc_pos || !exc_byte))) {
-        set_error("null argument");
+    if (!s) {
+        set_error("null session");
         return EC_ERR_ARG;
     }
-    if (offsets) {
-        EC_CHECK(check_offsets(offsets, nreads, nbases));
-    } else if ((uint64_t)read_len * nreads != nbases) {
-        set_error("%llu reads of %u bases != %llu bases", (unsigned long long)nreads, read_len,
-                  (unsigned long long)nbases);
-        return EC_ERR_ARG;
+    if (s->stg_n) {
+        set_error("staged batches pending (ec_assemble_staged first)");
+        return EC_ERR_STATE;
     }
-    for (uint64_t i = 0; i < n_exc; i++)
-        if (exc_pos[i] >= nbases || (i && exc_pos[i] <= exc_pos[i - 1])) {
-            set_error("exception %llu: position %llu not ascending inside [0, %llu)", (unsigned long long)i,
-                      (unsigned long long)exc_pos[i], (unsigned long long)nbases);
-            return EC_ERR_ARG;
-        }
+    EC_CHECK(check_packed(codes, nbases, offsets, nreads, read_len, exc_pos, exc_byte, n_exc));
     EC_HIP(hipSetDevice(s->device));
-    const uint64_t ncodes = (nbases + 3) / 4;
     EC_CHECK(s->h_reads.ensure(nbases + 16));
-    EC_CHECK(s->h_offsets.ensure((nreads + 1) * 8));
-    EC_CHECK(s->p_codes.ensure(((ncodes + 3) & ~3ull) + 16));
-    EC_CHECK(s->p_exc.ensure(n_exc * 9 + 16));
-    EC_CHECK(pipe_plan(s, nbases, 1, offsets, nreads, read_len));
-    auto &pp = s->pipe;
-    pp.packed = true;
-    pp.first_len = nreads ? (offsets ? offsets[1] - offsets[0] : read_len) : 0;
-    pp.ascii = s->h_reads.as<uint8_t>();
-    pp.codes = s->p_codes.as<uint32_t>();
-    pp.exc_pos = s->p_exc.as<uint64_t>();
-    pp.exc_byte = s->p_exc.as<uint8_t>() + n_exc * 8;
-    if (n_exc) {
-        EC_HIP(hipMemcpyAsync(s->p_exc.p, exc_pos, n_exc * 8, hipMemcpyHostToDevice, s->cstream));
-        EC_HIP(hipMemcpyAsync(s->p_exc.as<uint8_t>() + n_exc * 8, exc_byte, n_exc, hipMemcpyHostToDevice, s->cstream));
+    EC_CHECK(stage_packed(s, s->pipe, s->p_codes, s->p_exc, s->h_offsets, nullptr, codes, nbases, offsets, nreads,
+                          read_len, exc_pos, exc_byte, n_exc));
+    return assemble_piped(s, s->h_offsets.as<uint64_t>(), nreads, k, limit, flags);
+}
+
+int ec_stage_packed_host(ec_session *s, const uint8_t *codes, uint64_t nbases, const uint64_t *offsets,
+                         uint64_t nreads, uint32_t read_len, const uint64_t *exc_pos, const uint8_t *exc_byte,
+                         uint64_t n_exc) {
+    refresh_knobs();
+    if (!s) {
+        set_error("null session");
+        return EC_ERR_ARG;
     }
-    if (!offsets)  // one read length: the offsets are made on the device
-        k_iota_off<<<grid_for(nreads + 1, 256, 16384), 256, 0, s->stream>>>(s->h_offsets.as<uint64_t>(), nreads + 1,
-                                                                            read_len);
-    for (int c = 0; c < pp.nchunks; c++) {
-        // code bytes of bases [blo, bhi) (blo a multiple of 64: whole 32-bit words)
-        const uint64_t c0 = pp.blo[c] / 4, c1 = c + 1 == pp.nchunks ? ncodes : pp.bhi[c] / 4;
-        if (c1 > c0)
-            EC_HIP(hipMemcpyAsync(s->p_codes.as<uint8_t>() + c0, codes + c0, c1 - c0, hipMemcpyHostToDevice, s->cstream));
-        if (offsets) EC_CHECK(pipe_copy_offsets(s, c, offsets));
-        pp.elo[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.blo[c]) - exc_pos);
-        pp.ehi[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.bhi[c]) - exc_pos);
-        EC_HIP(hipEventRecord(s->pev[c], s->cstream));
+    if (s->stg_n >= 2) {
+        set_error("two batches already staged (ec_assemble_staged first)");
+        return EC_ERR_STATE;
     }
-    return assemble_piped(s, nreads, k, limit, flags);
+    EC_CHECK(check_packed(codes, nbases, offsets, nreads, read_len, exc_pos, exc_byte, n_exc));
+    EC_HIP(hipSetDevice(s->device));
+    auto &sl = s->stg[(s->stg_head + s->stg_n) & 1];
+    if (!sl.free_ev) {  // first use: free once the session stream's current work is done
+        EC_HIP(hipEventCreateWithFlags(&sl.free_ev, hipEventDisableTiming));
+        EC_HIP(hipEventRecord(sl.free_ev, s->stream));
+    }
+    EC_CHECK(stage_packed(s, sl.pipe, sl.codes, sl.exc, sl.off, sl.free_ev, codes, nbases, offsets, nreads, read_len,
+                          exc_pos, exc_byte, n_exc));
+    sl.nreads = nreads;
+    sl.nbases = nbases;
+    s->stg_n++;
+    return EC_OK;
+}
+
+int ec_assemble_staged(ec_session *s, int k, int limit, unsigned flags) {
+    refresh_knobs();
+    if (!s) {
+        set_error("null session");
+        return EC_ERR_ARG;
+    }
+    if (!s->stg_n) {
+        set_error("no staged batch (ec_stage_packed_host)");
+        return EC_ERR_STATE;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    auto &sl = s->stg[s->stg_head];
+    int rc = s->h_reads.ensure(sl.nbases + 16);
+    if (rc == EC_OK) {
+        std::swap(s->pipe, sl.pipe);
+        rc = assemble_piped(s, sl.off.as<uint64_t>(), sl.nreads, k, limit, flags);
+        std::swap(s->pipe, sl.pipe);
+    }
+    // the slot is free for the next staged batch once this call's kernels are done with it
+    // (drained on every return, so also after a failure)
+    if (sl.pipe.done < sl.pipe.nchunks) {  // (a failure before any chunk was consumed)
+        for (int c = 0; c < sl.pipe.nchunks; c++) hipStreamWaitEvent(s->stream, sl.pipe.ev[c], 0);
+    }
+    hipEventRecord(sl.free_ev, s->stream);
+    s->stg_head ^= 1;
+    s->stg_n--;
+    return rc;
 }
 
 int ec_get_stats(ec_session *s, ec_stats *out) {

@@ -369,6 +369,18 @@ int ec_reads_packed_copy(const ec_reads *r, uint8_t *codes, uint64_t *exc_pos, u
     return EC_OK;
 }
 
+// a packed read set as a staged batch (ec_stage_packed_host)
+int ec_stage_packed_reads(ec_session *s, const ec_reads *r) {
+    if (!r || !r->packed) {
+        set_error("not a packed read set (ec_reads_load with EC_READS_PACKED)");
+        return EC_ERR_ARG;
+    }
+    const uint64_t R = r->offsets.size() - 1;
+    return ec_stage_packed_host(s, r->codes, r->nbases, r->read_len ? nullptr : r->offsets.data(), R, r->read_len,
+                                r->exc_pos.empty() ? nullptr : r->exc_pos.data(),
+                                r->exc_byte.empty() ? nullptr : r->exc_byte.data(), r->exc_pos.size());
+}
+
 // the fused assembly straight from a packed read set (its page-locked codes go over PCIe)
 int ec_assemble_packed_reads(ec_session *s, const ec_reads *r, int k, int limit, unsigned flags) {
     if (!r || !r->packed) {

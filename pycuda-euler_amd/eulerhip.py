@@ -102,6 +102,8 @@ _SIGS = {
     "ec_assemble_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_assemble_packed_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_uint32, _P, _P, _U64, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_uint]),
+    "ec_stage_packed_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_uint32, _P, _P, _U64]),
+    "ec_assemble_staged": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_pack_reads": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int, _P, _P, _P, _U64, ctypes.POINTER(_U64),
                                      ctypes.POINTER(ctypes.c_uint32)]),
     "ec_assemble_from_kmers": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _U64, ctypes.c_int, ctypes.c_uint]),
@@ -303,6 +305,23 @@ class Session:
             self._h, pr.codes.ctypes.data if pr.nbases else None, pr.nbases, None if off is None else off.ctypes.data,
             pr.nreads, pr.read_len, pr.exc_pos.ctypes.data if ne else None, pr.exc_byte.ctypes.data if ne else None,
             ne, int(k), int(limit), flags))
+
+    def stage_packed(self, pr):
+        """Queue a PackedReads batch's H2D copies (ec_stage_packed_host; two slots).  pr must stay
+        alive and unchanged until assemble_staged() has consumed it."""
+        off = None if pr.offsets is None else np.ascontiguousarray(pr.offsets, dtype=np.uint64)
+        if off is not None:
+            pr.offsets = off  # (kept alive with pr)
+        ne = len(pr.exc_pos)
+        check(lib().ec_stage_packed_host(
+            self._h, pr.codes.ctypes.data if pr.nbases else None, pr.nbases, None if off is None else off.ctypes.data,
+            pr.nreads, pr.read_len, pr.exc_pos.ctypes.data if ne else None, pr.exc_byte.ctypes.data if ne else None,
+            ne))
+
+    def assemble_staged(self, k, limit=1, flags=0):
+        """Assemble the oldest staged batch (ec_assemble_staged): staging batch i + 1 before this
+        call overlaps its PCIe copy with batch i's kernels."""
+        check(lib().ec_assemble_staged(self._h, int(k), int(limit), flags))
 
     def run_device(self, d_reads_ptr, d_offsets_ptr, nreads, k, limit=1, flags=0):
         """Reads already in HBM (e.g. torch uint8 / int64 tensors' data_ptr())."""

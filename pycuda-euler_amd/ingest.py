@@ -24,6 +24,7 @@ eulerhip.register("ec_reads_free", None, [_P])
 eulerhip.register("ec_reads_packed_info", ctypes.c_int, [_P, _P, _P, _P])
 eulerhip.register("ec_reads_packed_copy", ctypes.c_int, [_P, _P, _P, _P])
 eulerhip.register("ec_assemble_packed_reads", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_uint])
+eulerhip.register("ec_stage_packed_reads", ctypes.c_int, [_P, _P])
 READS_PACKED = 0x100  # EC_READS_PACKED
 
 
@@ -92,6 +93,11 @@ class ReadSet:
         """the fused assembly on session straight from the packed set (ec_assemble_packed_reads);
         session.fetch(k) then returns the Result"""
         eulerhip.check(eulerhip.lib().ec_assemble_packed_reads(session._h, self._h, int(k), int(limit), int(flags)))
+
+    def stage(self, session):
+        """queue this packed set as session's next staged batch (ec_stage_packed_reads); keep the
+        ReadSet open until session.assemble_staged() has consumed it"""
+        eulerhip.check(eulerhip.lib().ec_stage_packed_reads(session._h, self._h))
 
     def reads(self):
         """the reads as Python strings (small inputs / tests)"""

@@ -114,3 +114,66 @@ def test_packed_headline_shape_pinned(gpu_session):
     res = gpu_session.fetch(31)
     assert res.stats.count_variant == 3
     _same(res, ref, rl)
+
+
+@pytest.mark.parametrize("chunks", ["1", "6"])
+def test_staged_batches_vs_oracle(gpu_session, monkeypatch, chunks):
+    """ec_stage_packed_host / ec_assemble_staged: a pipeline of batches of different shapes (one
+    length, ragged with offsets, N exceptions, k = 31 / 25 / 51), batch i + 1 staged before batch
+    i is assembled, each result equal to the oracle; misuse is refused (EC_ERR_STATE)"""
+    monkeypatch.setenv("EULERHIP_HOST_CHUNKS", chunks)
+    batches = []
+    for i, (g, n, L, err, nr, k) in enumerate([(40_000, 20_000, 100, 0.0, 0.0, 31), (30_000, 10_000, 90, 0.002, 0.003, 25),
+                                                (20_000, 6_000, 150, 0.002, 0.0, 51), (40_000, 12_000, 100, 0.0, 0.0, 31)]):
+        buf, off = make_reads(g, n, L, 7300 + i, err=err, n_rate=nr)
+        if i == 3:  # ragged: drop the tail of every 7th read
+            reads = [buf[int(off[j]):int(off[j + 1])].tobytes().decode()[: (60 if j % 7 == 0 else L)] for j in range(n)]
+            buf, off = eulerhip.pack_reads(reads)
+        pr = eulerhip.pack_2bit(buf, off)
+        batches.append((pr, k, _ref(buf, off, k)))
+    with pytest.raises(eulerhip.EulerHipError):
+        gpu_session.assemble_staged(31)  # nothing staged
+    gpu_session.stage_packed(batches[0][0])
+    gpu_session.stage_packed(batches[1][0])
+    with pytest.raises(eulerhip.EulerHipError):
+        gpu_session.stage_packed(batches[2][0])  # both slots taken
+    with pytest.raises(eulerhip.EulerHipError):
+        gpu_session.run_packed_host(batches[2][0], 31, 1)  # batches pending
+    for i in range(len(batches)):
+        pr, k, (ref, rl) = batches[i]
+        gpu_session.assemble_staged(k, 1)
+        if i + 2 < len(batches):
+            gpu_session.stage_packed(batches[i + 2][0])
+        _same(gpu_session.fetch(k), ref, rl)
+    # the immediate entry works again once the pipeline is empty
+    pr, k, (ref, rl) = batches[0]
+    gpu_session.run_packed_host(pr, k, 1)
+    _same(gpu_session.fetch(k), ref, rl)
+
+
+def test_staged_read_set_from_file(gpu_session, tmp_path):
+    """FASTA file -> page-locked 2-bit codes (EC_READS_PACKED) -> staged batches -> contigs"""
+    import ingest
+
+    paths = []
+    for i in range(3):
+        buf, off = make_reads(30_000, 8_000, 100, 7400 + i, err=0.001)
+        p = tmp_path / ("r%d.fa" % i)
+        with open(p, "wb") as f:
+            for j in range(len(off) - 1):
+                f.write(b">r\n" + buf[int(off[j]):int(off[j + 1])].tobytes() + b"\n")
+        paths.append((str(p), _ref(buf, off, 31)))
+    sets = [ingest.ReadSet(p, packed=True) for p, _ in paths]
+    sets[0].stage(gpu_session)
+    sets[1].stage(gpu_session)
+    for i in range(3):
+        gpu_session.assemble_staged(31, 1)
+        if i + 2 < 3:
+            sets[i + 2].stage(gpu_session)
+        ref, rl = paths[i][1]
+        _same(gpu_session.fetch(31), ref, rl)
+    # and the one-call form
+    sets[2].assemble(gpu_session, 31, 1)
+    _same(gpu_session.fetch(31), *paths[2][1])
+    for rs in sets:
+        rs.close()
