@@ -213,7 +213,8 @@ struct ec_session {
     XAlpha xa{};
     DevBuf x_par, x_irr, x_in, x_succ, x_done, x_lk, x_lv, x_lk2, x_lv2, x_len, x_m, x_cid, x_head, x_tail;
     // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
-    DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr;
+    DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr, rt_coop;
+    unsigned int coop_grid = 0;  // blocks of the cooperative ranking launch (all resident)
     // multi-GPU partitioned finish (ec_graph_chains_part ..): this rank's segment of oriented nodes
     uint64_t seg_n0 = 0, seg_n1 = 0;
     unsigned int seg_nc = 0;     // contigs of the job (ec_graph_layout)
@@ -683,9 +684,9 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         constexpr int NTF = 512;
         const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 2048u * 72 / 100;
         if (k & 1)
-            k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys);
+            k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
         else
-            k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys);
+            k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
     } else if (plan.slots == 1024) {
         constexpr int NT3 = 512;
         const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
@@ -707,6 +708,12 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         EC_HIP(hipMemcpyAsync(h, dbg, 128, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
         const double nw = (double)Bk * (BUCKET_THREADS / 64);  // waves
+        if (skfilt)
+            fprintf(stderr, "k_skbucket_filt: %llu buckets: max distinct est %llu, max predicted inserts %llu, max "
+                            "seen-twice cells %llu, max records %llu; refused by the predictor %llu, tables filled "
+                            "%llu, most keys inserted %llu (max_keys %u)\n",
+                    (unsigned long long)Bk, h[0], h[1], h[2], h[3], h[4], h[5], h[6],
+                    kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 2048u * 72 / 100);
         if (plan.slots == 1024)
             fprintf(stderr, "k_skbucket3: %llu buckets, most distinct records in a bucket %llu\n",
                     (unsigned long long)Bk, h[3]);
@@ -1911,6 +1918,36 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
     EC_CHECK(s->rbc.ensure(((M + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
     EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
     SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
+    if (kn().rank_coop != 0) {  // one cooperative launch (rank_tile.h k_rank_supers_coop)
+        if (!s->coop_grid) {
+            int per = 0, cus = 0;
+            EC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_rank_supers_coop, 256, 0));
+            EC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
+            s->coop_grid = (unsigned int)std::max(1, std::min(per, 4) * cus);
+        }
+        const unsigned int G = s->coop_grid;
+        EC_CHECK(s->rt_coop.ensure(((size_t)G + 16) * 4));
+        unsigned int *flags = s->rt_coop.as<unsigned int>(), *bcnt = flags + 16;
+        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
+        EC_HIP(hipMemsetAsync(flags, 0, 16 * 4, st));
+        EC_HIP(hipMemsetAsync(dsc->active, 0, sizeof(dsc->active), st));
+        CoopRank a{srec, SIDX, snrec, s->rt_hasp.as<uint8_t>(), s->rid.as<uint2>(), s->rlist.as<unsigned int>(),
+                   s->nextR.as<unsigned int>(), s->st0.as<RJump>(), s->st1.as<RJump>(), bcnt, flags, dsc->active,
+                   &dsc->final_sel, M, N, s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
+                   s->PL.as<unsigned int>(), s->PM.as<unsigned long long>()};
+        void *args[] = {&a};
+        EC_HIP(hipLaunchCooperativeKernel((const void *)k_rank_supers_coop, dim3(G), dim3(256), args, 0, st));
+        unsigned int hf[16];
+        EC_HIP(hipMemcpyAsync(hf, flags, sizeof hf, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        if (hf[8]) {
+            set_error("ruling set left chains unvisited (%u chains)", M);
+            return EC_ERR_STATE;
+        }
+        nr = hf[9];
+        rounds = 63;  // (the callers' convergence flag: active[62])
+        return EC_OK;
+    }
     k_super_link<<<grid_for(M, B), B, 0, st>>>(srec, M, SIDX, snrec, s->rt_hasp.as<uint8_t>());
     EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
     EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
@@ -2952,7 +2989,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr};
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->h_coff.release();

@@ -50,6 +50,7 @@ void refresh_knobs() {
         k.rank = num("EULERHIP_RANK", -1);
         k.sk_filt = num("EULERHIP_SK_FILT", -1);
         k.skf_keys = num("EULERHIP_SKF_KEYS", 0);
+        k.rank_coop = num("EULERHIP_RANK_COOP", -1);
     }
     g_knobs = k;
 }

@@ -47,6 +47,7 @@ struct Knobs {
     int rank = -1;              // EULERHIP_RANK: list ranking 0 = tile contraction (rank_tile.h), 1 = node ruling set
     int sk_filt = -1;           // EULERHIP_SK_FILT: 0 = error-rich inputs on window records, not k_skbucket_filt
     int skf_keys = 0;           // EULERHIP_SKF_KEYS: k_skbucket_filt's keys-per-table cap (forces its overflow)
+    int rank_coop = -1;      // EULERHIP_RANK_COOP=0: the super list ranked by separate launches
 };
 void refresh_knobs();
 const Knobs &kn();

@@ -1131,7 +1131,8 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
                                                       long long limit, unsigned long long *dkey, unsigned int *dcnt,
                                                       unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
                                                       unsigned int *nsolid, unsigned long long *ndistinct,
-                                                      unsigned int *overflow, unsigned int max_keys) {
+                                                      unsigned int *overflow, unsigned int max_keys,
+                                                      unsigned long long *dbg = nullptr) {
     constexpr int SBITS = __builtin_ctz(SLOTS);
     constexpr unsigned int NW = 1u << (SKF_BITS - 5), CM = (1u << SKF_BITS) - 1;
     __shared__ LTabE<SLOTS> tab;
@@ -1210,6 +1211,13 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
             const double pass = 1.1 * (S + fmax(0.0, D - S) * (1.0 - el) * (1.0 - el));  // (~10 % low: solid cells hit by collisions)
             if (pass > (double)max_keys) s_over[0] = 1;  // (default: the table would pass ~3/4 full)
             else atomicAdd(ndistinct, (unsigned long long)llround(D));
+            if (dbg) {  // EULERHIP_SK2_STATS: the largest estimates, the predictor's refusals
+                atomicMax(&dbg[0], (unsigned long long)D);
+                atomicMax(&dbg[1], (unsigned long long)pass);
+                atomicMax(&dbg[2], (unsigned long long)s_cells[0]);
+                atomicMax(&dbg[3], (unsigned long long)(bend[b] - bbeg[b]));
+                if (s_over[0]) atomicAdd(&dbg[4], 1ull);
+            }
         }
         __syncthreads();
     }
@@ -1231,6 +1239,13 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
             if (eC < v.x) atomicMin(&tab.ev[sl].x, eC);
             if (eT < v.y) atomicMin(&tab.ev[sl].y, eT);
         });
+    }
+    if (dbg) {
+        __syncthreads();
+        if (tid == 0) {
+            if (s_over[0]) atomicAdd(&dbg[5], 1ull);  // tables that filled up in pass 1
+            atomicMax(&dbg[6], (unsigned long long)s_over[1]);  // most keys inserted
+        }
     }
     lds_table_finish<SLOTS, false, KeyId, LTabE<SLOTS>, EvExpand, NT>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub,
                                                                       nsolid, nullptr, overflow, KeyId(),
