@@ -271,6 +271,7 @@ struct Scalars {  // device scalars block
     unsigned long long nrec;  // k_upsweep_sk: super-k-mer records
     unsigned int nasym, nxl, nxs;  // extended.h: one-way links, entries of their components, their starts
     unsigned int xbad;             // extended.h: a walk that never reaches its start again
+    unsigned int coop_bad, coop_nr;  // k_rank_supers_coop: chains left unvisited, rulers
     unsigned int active[64];
 };
 
@@ -1899,26 +1900,27 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
 // rank_tile.h (2): the super list srec (M chains, SIDX[head] = index) linked and ranked by the
 // weighted ruling set; per chain its path key / rank (rt_pks / rt_rks), paths' and cycles'
 // length / min first event at their key nodes (PL / PM)
-int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr, int &rounds) {
+int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr, int &rounds,
+                const unsigned long long *dM = nullptr, bool defer = false) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc{};
     SuperRec *srec = s->rt_srec.as<SuperRec>();
     unsigned int *SIDX = s->rt_sidx.as<unsigned int>();
-    EC_CHECK(s->rt_snrec.ensure((size_t)M * sizeof(SNodeRec)));
-    EC_CHECK(s->rt_hasp.ensure(M));
-    EC_CHECK(s->rt_pks.ensure((size_t)M * 4));
-    EC_CHECK(s->rt_rks.ensure((size_t)M * 4));
-    EC_CHECK(s->rid.ensure((size_t)M * 8));
-    EC_CHECK(s->rlist.ensure((size_t)M * 4));
-    EC_CHECK(s->nextR.ensure((size_t)M * 4));
-    EC_CHECK(s->st0.ensure((size_t)M * sizeof(RJump)));
-    EC_CHECK(s->st1.ensure((size_t)M * sizeof(RJump)));
-    EC_CHECK(s->rbc.ensure(((M + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
-    EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
+    const size_t cap = dM ? std::max<size_t>(N, 1) : std::max<size_t>(M, 1);  // (dM: M <= N chains)
+    EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec)));
+    EC_CHECK(s->rt_hasp.ensure(cap));
+    EC_CHECK(s->rt_pks.ensure(cap * 4));
+    EC_CHECK(s->rt_rks.ensure(cap * 4));
+    EC_CHECK(s->rid.ensure(cap * 8));
+    EC_CHECK(s->rlist.ensure(cap * 4));
+    EC_CHECK(s->nextR.ensure(cap * 4));
+    EC_CHECK(s->st0.ensure(cap * sizeof(RJump)));
+    EC_CHECK(s->st1.ensure(cap * sizeof(RJump)));
+    EC_CHECK(s->rbc.ensure(((cap + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
     SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
-    if (kn().rank_coop != 0) {  // one cooperative launch (rank_tile.h k_rank_supers_coop)
+    if (kn().rank_coop != 0 || dM) {  // one cooperative launch (rank_tile.h k_rank_supers_coop)
         if (!s->coop_grid) {
             int per = 0, cus = 0;
             EC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_rank_supers_coop, 256, 0));
@@ -1928,26 +1930,28 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
         const unsigned int G = s->coop_grid;
         EC_CHECK(s->rt_coop.ensure(((size_t)G + 16) * 4));
         unsigned int *flags = s->rt_coop.as<unsigned int>(), *bcnt = flags + 16;
-        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
         EC_HIP(hipMemsetAsync(flags, 0, 16 * 4, st));
         EC_HIP(hipMemsetAsync(dsc->active, 0, sizeof(dsc->active), st));
+        EC_HIP(hipMemsetAsync(&dsc->coop_bad, 0, 8, st));
         CoopRank a{srec, SIDX, snrec, s->rt_hasp.as<uint8_t>(), s->rid.as<uint2>(), s->rlist.as<unsigned int>(),
                    s->nextR.as<unsigned int>(), s->st0.as<RJump>(), s->st1.as<RJump>(), bcnt, flags, dsc->active,
-                   &dsc->final_sel, M, N, s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
+                   &dsc->final_sel, &dsc->coop_bad, &dsc->coop_nr, M, N, dM, s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
                    s->PL.as<unsigned int>(), s->PM.as<unsigned long long>()};
         void *args[] = {&a};
         EC_HIP(hipLaunchCooperativeKernel((const void *)k_rank_supers_coop, dim3(G), dim3(256), args, 0, st));
-        unsigned int hf[16];
-        EC_HIP(hipMemcpyAsync(hf, flags, sizeof hf, hipMemcpyDeviceToHost, st));
+        rounds = 63;  // (the callers' convergence flag: active[62])
+        nr = 0;
+        if (defer) return EC_OK;  // (coop_bad / coop_nr checked with the caller's next scalar read)
+        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
-        if (hf[8]) {
+        if (hsc.coop_bad) {
             set_error("ruling set left chains unvisited (%u chains)", M);
             return EC_ERR_STATE;
         }
-        nr = hf[9];
-        rounds = 63;  // (the callers' convergence flag: active[62])
+        nr = hsc.coop_nr;
         return EC_OK;
     }
+    EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
     k_super_link<<<grid_for(M, B), B, 0, st>>>(srec, M, SIDX, snrec, s->rt_hasp.as<uint8_t>());
     EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
     EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
@@ -2130,6 +2134,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->PM.ensure(Nn * 8));
     unsigned int nr = 0;
     int rounds = 0;  // Wyllie rounds launched (their convergence is checked with the results)
+    bool coop_deferred = false;  // the cooperative ranking's checks wait for the next scalar read
     s->stats.rank_rounds = 0;
     if (U && tile_rank) {
         // (1) chains of in-tile links ranked in LDS, in-tile cycles finished (rank_tile.h)
@@ -2149,15 +2154,22 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                 LR, tcnt, scratch, s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
                                                 s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
         EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
-        unsigned long long M64 = 0;
-        EC_HIP(hipMemcpyAsync(&M64, tbase + ntiles, 8, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
-        const unsigned int M = (unsigned int)M64;
         // (2) the super list: compacted in tile order, linked, ranked by the weighted ruling set
-        if (M) {
+        // -- in one cooperative launch that reads the chain count on the device (no host round
+        // trip; its checks ride on the scalar read after the starts), or by separate launches
+        unsigned int M = 0;
+        const bool coop = kn().rank_coop != 0;
+        if (!coop) {
+            unsigned long long M64 = 0;
+            EC_HIP(hipMemcpyAsync(&M64, tbase + ntiles, 8, hipMemcpyDeviceToHost, st));
+            EC_HIP(hipStreamSynchronize(st));
+            M = (unsigned int)M64;
+        }
+        coop_deferred = coop;
+        if (coop || M) {
             k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
                                                    s->rt_sidx.as<unsigned int>());
-            EC_CHECK(rank_supers(s, M, N, nr, rounds));
+            EC_CHECK(rank_supers(s, M, N, nr, rounds, coop ? tbase + ntiles : nullptr, coop));
             // (3) every node: its chain's key and rank + its offset in the chain
             k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
@@ -2243,6 +2255,13 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     }
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));  // nstarts, active[]
     EC_HIP(hipStreamSynchronize(st));
+    if (coop_deferred) {
+        if (hsc.coop_bad) {
+            set_error("ruling set left chains unvisited");
+            return EC_ERR_STATE;
+        }
+        s->stats.n_rulers = nr = hsc.coop_nr;
+    }
     if (rounds) {
         unsigned int used = 1;
         for (int r = 0; r < rounds; r++)

@@ -432,10 +432,12 @@ struct CoopRank {
     unsigned int *rlist, *nextR;
     RJump *rs0, *rs1;
     unsigned int *bcnt;    // per block: rulers selected
-    unsigned int *flags;   // [it] = a node unvisited after ruler pass it; [8] = not covered; [9] = nr
+    unsigned int *flags;   // [it] = a node unvisited after ruler pass it
     unsigned int *active;  // [r] = a pointer moved in Wyllie round r; [62] = not converged
     unsigned int *final_sel;
+    unsigned int *out_bad, *out_nr;  // (the session's scalars: read with its next scalar read)
     unsigned int M, N;
+    const unsigned long long *dM;  // if set: M read on the device (the tile compaction's total)
     unsigned int *PKs, *RKs, *PL;
     unsigned long long *PM;
 };
@@ -453,7 +455,12 @@ __global__ void __launch_bounds__(256) k_rank_supers_coop(CoopRank a) {
     __shared__ unsigned int s_w[4];
     const unsigned int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
     const uint64_t gt = (uint64_t)b * 256 + tid, gs = (uint64_t)G * 256;
-    const unsigned int M = a.M;
+    const unsigned int M = a.dM ? (unsigned int)*a.dM : a.M;
+    for (uint64_t t = gt; t < M; t += gs) {  // (no host memsets: M may be known only here)
+        a.hasp[t] = 0;
+        a.rid[t] = make_uint2(NONE32, NONE32);
+    }
+    grid.sync();
     // super links (k_super_link)
     for (uint64_t t = gt; t < M; t += gs) {
         const SuperRec r = a.srec[t];
@@ -550,11 +557,11 @@ __global__ void __launch_bounds__(256) k_rank_supers_coop(CoopRank a) {
         if (!a.flags[it]) break;
     }
     if (it == 4) {  // (mask 0 selects every unvisited node: cannot happen)
-        if (gt == 0) a.flags[8] = 1u;
+        if (gt == 0) *a.out_bad = 1u;
         return;
     }
     const unsigned int nr = r0;
-    if (gt == 0) a.flags[9] = nr;
+    if (gt == 0) *a.out_nr = nr;
     for (uint64_t t = gt; t < nr; t += gs) {  // k_rjump_init
         const unsigned int n = a.nextR[t];
         if (n != NONE32) a.rs0[n].a = (unsigned int)t;
