@@ -214,6 +214,7 @@ struct ec_session {
     DevBuf x_par, x_irr, x_in, x_succ, x_done, x_lk, x_lv, x_lk2, x_lv2, x_len, x_m, x_cid, x_head, x_tail;
     // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
     DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr, rt_coop;
+    DevBuf wbv;  // count_wide.h minimizer buckets: every window's minimizer
     unsigned int coop_grid = 0;  // blocks of the cooperative ranking launch (all resident)
     // multi-GPU partitioned finish (ec_graph_chains_part ..): this rank's segment of oriented nodes
     uint64_t seg_n0 = 0, seg_n1 = 0;
@@ -272,6 +273,7 @@ struct Scalars {  // device scalars block
     unsigned int nasym, nxl, nxs;  // extended.h: one-way links, entries of their components, their starts
     unsigned int xbad;             // extended.h: a walk that never reaches its start again
     unsigned int coop_bad, coop_nr;  // k_rank_supers_coop: chains left unvisited, rulers
+    unsigned int wbv_long, wpad;     // k_wbv: a read past its length limit
     unsigned int active[64];
 };
 
@@ -1550,7 +1552,8 @@ int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, S
 // bucket, as phase_count for k <= 32.  ok = false (scalars reset) when the input needs the
 // HBM table: reads with 'N' or other bytes, tiles over the 40 KB stage, a bucket past its table.
 int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, uint64_t nreads,
-                      uint64_t read_base, int k, long long limit, unsigned int &U, SolidIndexW &sidx, bool &ok) {
+                      uint64_t read_base, int k, long long limit, unsigned int &U, SolidIndexW &sidx, bool &ok,
+                      bool mb = false, bool *mb_declined = nullptr) {
     ok = false;
     if ((s->flags & EC_FLAG_GENERAL) || !nreads || kn().wide_general) return EC_OK;
     hipStream_t st = s->stream;
@@ -1573,9 +1576,26 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_CHECK(s->hll.ensure(ngroups * HR));
     EC_CHECK(s->ftot.ensure((FINE_W + HR) * 8));
     kmark(s, 0, 0);
-    k_upsweep_w<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, s->hist.as<unsigned int>(),
-                                                         s->hll.as<uint8_t>(), &dsc->npos, &dsc->maxlocal, &dsc->skew,
-                                                         dsc->lens);
+    // minimizer buckets (count_wide.h k_wbv): every window's minimizer, indexed by its base offset
+    uint32_t *wbv = nullptr;
+    if (mb) {
+        uint64_t nb = 0;
+        EC_HIP(hipMemcpyAsync(&nb, d_off + nreads, 8, hipMemcpyDeviceToHost, st));
+        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(s->wbv.ensure(std::max<uint64_t>(nb, 1) * 4));
+        wbv = s->wbv.as<uint32_t>();
+        k_wbv<<<(unsigned)((nreads + 63) / 64), 64, 0, st>>>(d_reads, d_off, nreads, k, wbv, &dsc->wbv_long);
+    }
+    if (mb)
+        k_upsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
+                                                                   s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
+                                                                   &dsc->npos, &dsc->maxlocal, &dsc->skew, dsc->lens,
+                                                                   wbv);
+    else
+        k_upsweep_w<false><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
+                                                                    s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
+                                                                    &dsc->npos, &dsc->maxlocal, &dsc->skew, dsc->lens,
+                                                                    nullptr);
     kmark(s, 0, 1);
     unsigned long long *ftot = s->ftot.as<unsigned long long>();
     EC_HIP(hipMemsetAsync(ftot, 0, (FINE_W + HR) * 8, st));
@@ -1593,6 +1613,10 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     // fixed-capacity sub-buckets of <= 800 estimated keys in 1664-slot tables (78 KB: two
     // workgroups per CU); measured before: such inputs fell to the HBM table (k_count 130 ms of
     // a 335 ms step at 1.25e9 positions).
+    if (mb && hsc.wbv_long) {  // a read past k_wbv's length: hash buckets instead
+        if (mb_declined) *mb_declined = true;
+        return reset();
+    }
     if (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT || !P) return reset();
     int sbits = 0;
     if (est / FINE_W > 1800.0) {
@@ -1635,17 +1659,28 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     k_bucket_totals<FINE_W_BITS><<<grid_for(Bk + 1, B), B, 0, st>>>(ftot, bbits, s->tot.as<unsigned long long>());
     EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
     kmark(s, 1, 0);
-    k_downsweep_w<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups, cbits,
-                                                           s->offs.as<unsigned long long>(), s->recs.as<RecW>(), read_base);
+    if (mb)
+        k_downsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups, cbits,
+                                                                     s->offs.as<unsigned long long>(),
+                                                                     s->recs.as<RecW>(), read_base, wbv);
+    else
+        k_downsweep_w<false><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups,
+                                                                      cbits, s->offs.as<unsigned long long>(),
+                                                                      s->recs.as<RecW>(), read_base, nullptr);
     kmark(s, 1, 1);
     if (second) {
         const unsigned RS = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8, 1024 / Ck));
         EC_CHECK(s->gcur.ensure(Bk * 8));
         EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
         kmark(s, 4, 0);
-        k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
-            StoreW{s->recs.as<RecW>()}, StoreW{s->recs2.as<RecW>()}, s->bstart.as<unsigned long long>(),
-            s->gcur.as<unsigned long long>(), cbits, bbits);
+        if (mb)
+            k_refine<RecWM, StoreWM, StoreWM><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                StoreWM{s->recs.as<RecWM>()}, StoreWM{s->recs2.as<RecWM>()}, s->bstart.as<unsigned long long>(),
+                s->gcur.as<unsigned long long>(), cbits, bbits);
+        else
+            k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                StoreW{s->recs.as<RecW>()}, StoreW{s->recs2.as<RecW>()}, s->bstart.as<unsigned long long>(),
+                s->gcur.as<unsigned long long>(), cbits, bbits);
         if (sbits) {  // fine buckets (recs2) -> fixed-capacity sub-buckets (recs)
             EC_CHECK(s->bb2.ensure((Bt + 1) * 8 * 2));
             EC_CHECK(s->gcur.ensure(Bt * 8));
@@ -1653,9 +1688,14 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
             unsigned long long *b3 = s->fcur.as<unsigned long long>();
             k_level3_init<<<grid_for(Bt + 1, B, 8192), B, 0, st>>>(s->bstart.as<unsigned long long>(), Bk, sbits, fcap3,
                                                                    b3, s->gcur.as<unsigned long long>());
-            k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Bk, 1), BUCKET_THREADS, 0, st>>>(
-                StoreW{s->recs2.as<RecW>()}, StoreW{s->recs.as<RecW>()}, b3, s->gcur.as<unsigned long long>(), bbits,
-                bbits + sbits, fcap3, &dsc->overflow);
+            if (mb)
+                k_refine<RecWM, StoreWM, StoreWM><<<dim3((unsigned)Bk, 1), BUCKET_THREADS, 0, st>>>(
+                    StoreWM{s->recs2.as<RecWM>()}, StoreWM{s->recs.as<RecWM>()}, b3, s->gcur.as<unsigned long long>(),
+                    bbits, bbits + sbits, fcap3, &dsc->overflow);
+            else
+                k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Bk, 1), BUCKET_THREADS, 0, st>>>(
+                    StoreW{s->recs2.as<RecW>()}, StoreW{s->recs.as<RecW>()}, b3, s->gcur.as<unsigned long long>(),
+                    bbits, bbits + sbits, fcap3, &dsc->overflow);
             k_level3_ends<<<grid_for(Bt, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), Bt, fcap3,
                                                                s->bb2.as<unsigned long long>(),
                                                                s->bb2.as<unsigned long long>() + Bt + 1);
@@ -1671,16 +1711,22 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_CHECK(s->dft.ensure(umax * 8));
     if (!s->no_index) EC_CHECK(s->sub.ensure(umax * sizeof(SubSlotW)));
     kmark(s, 2, 0);
-#define EC_BUCKET_W(SL, SRC, BEG, END)                                                                          \
-    k_bucket_w<SL><<<(unsigned)Bt, BUCKET_THREADS, 0, st>>>(                                                     \
+#define EC_BUCKET_W(SL, R, SRC, BEG, END)                                                                       \
+    k_bucket_w<SL, R><<<(unsigned)Bt, BUCKET_THREADS, 0, st>>>(                                                  \
         SRC, BEG, END, limit, s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),    \
         s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
         &dsc->ndistinct, &dsc->overflow)
-    if (sbits)
-        EC_BUCKET_W(1664, s->recs.as<RecW>(), s->bb2.as<unsigned long long>(),
+    if (sbits && mb)
+        EC_BUCKET_W(1664, RecWM, s->recs.as<RecWM>(), s->bb2.as<unsigned long long>(),
                     s->bb2.as<unsigned long long>() + Bt + 1);
+    else if (sbits)
+        EC_BUCKET_W(1664, RecW, s->recs.as<RecW>(), s->bb2.as<unsigned long long>(),
+                    s->bb2.as<unsigned long long>() + Bt + 1);
+    else if (mb)
+        EC_BUCKET_W(SLOTS_W, RecWM, second ? s->recs2.as<RecWM>() : s->recs.as<RecWM>(),
+                    s->bstart.as<unsigned long long>(), nullptr);
     else
-        EC_BUCKET_W(SLOTS_W, second ? s->recs2.as<RecW>() : s->recs.as<RecW>(), s->bstart.as<unsigned long long>(),
+        EC_BUCKET_W(SLOTS_W, RecW, second ? s->recs2.as<RecW>() : s->recs.as<RecW>(), s->bstart.as<unsigned long long>(),
                     nullptr);
 #undef EC_BUCKET_W
     kmark(s, 2, 1);
@@ -1702,6 +1748,8 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     sidx.sub = s->sub.as<SubSlotW>();
     sidx.bbits = bbits + sbits;
     sidx.slots = SLOTS;
+    sidx.mb = mb ? 1 : 0;
+    sidx.k = k;
     if (2ull * U >= (unsigned long long)CYC) {
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
@@ -1717,7 +1765,13 @@ int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, 
         return EC_ERR_ARG;
     }
     bool ok = false;
-    EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok));
+    {
+        // minimizer buckets for k <= 52 (count_wide.h; EULERHIP_WIDE_MB=0: hash buckets)
+        bool declined = false;
+        const bool mb = k <= WMB_MAX_K && kn().wide_mb != 0;
+        EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok, mb, &declined));
+        if (declined) EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok));
+    }
     if (ok) return EC_OK;
     s->stats.n_reads = nreads;
     hipStream_t st = s->stream;
@@ -2053,6 +2107,8 @@ template <typename Index>
 inline bool ids_minimizer_local(const Index &) { return false; }
 template <>
 inline bool ids_minimizer_local<SolidIndex>(const SolidIndex &x) { return x.sk != 0; }
+template <>
+inline bool ids_minimizer_local<SolidIndexW>(const SolidIndexW &x) { return x.mb != 0; }
 
 // all_contigs:79-111 on the device from the solid set of phase_count / phase_merge
 template <typename Ops, typename Index>
@@ -3008,7 +3064,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop};
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->h_coff.release();

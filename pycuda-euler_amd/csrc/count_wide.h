@@ -8,9 +8,76 @@
 // path of wide.h.
 #pragma once
 #include "count_part.h"
+#include "graph.h"
+#include "superkmer.h"
 #include "wide.h"
 
 namespace ec {
+
+// ---- minimizer buckets for 128-bit keys (round 4) ------------------------------------------
+// With the bucket of a key = its minimizer (the smallest hash over its w = k - 14 canonical
+// 15-mers, superkmer.h) instead of mix128, a bucket holds whole minimizers, so the dense ids a
+// bucket gets are the k-mers of ~(w + 1) / 2-window runs of the genome: consecutive nodes of a
+// path mostly share a tile of ids (rank_tile.h ranks them in LDS) -- on hash buckets every link
+// leaves its tile.  The placement hash keeps mix128's low 32 bits for the slot inside a table:
+//   wide_place(c) = min_remix(minimizer) << 32 | low 32 bits of mix128(c).
+// Records carry the top 24 placement bits in the unused top bits of the key's high word (2k <=
+// 104: k <= 52), so the refine levels need not recompute the minimizer (graph.h wide_place).
+constexpr int WMB_MAX_K = 52;
+constexpr int WMB_SHIFT = 40;  // record hi: key bits below, placement bits 32..55 above
+
+// Per-window minimizers of the reads (one wave per 64 reads, lane = read): wbv[off[r] + w] =
+// min_remix(minimizer of window w of read r), read by k_upsweep_w / k_downsweep_w<true>.  The
+// m-mer hashes of a read go to LDS (lane-interleaved), suffix minima over blocks of w in place,
+// then a forward pass recomputes the hashes for the blocks' prefix minima (van Herk / Gil-Werman:
+// window = min(suffix[start], prefix[end])).  Reads longer than WMB_MAXL take no part: the wide
+// partitioned path stages reads of <= 159 bases anyway.
+constexpr int WMB_MAXL = 160;
+constexpr int WMB_MAXH = WMB_MAXL - SK_M + 1;
+__global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *off, uint64_t nreads, int k,
+                                            uint32_t *wbv, unsigned int *too_long) {
+    __shared__ uint32_t hs[WMB_MAXH * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t r = (uint64_t)blockIdx.x * 64 + lane;
+    if (r >= nreads) return;
+    const uint64_t s = off[r], len = off[r + 1] - s;
+    if (len < (uint64_t)k) return;
+    if (len > (uint64_t)WMB_MAXL) {
+        *too_long = 1u;
+        return;
+    }
+    const uint8_t *rd = buf + s;
+    const int nh = (int)len - SK_M + 1, W = k - SK_M + 1, nw = (int)len - k + 1;
+    constexpr uint32_t MM = (1u << (2 * SK_M)) - 1;
+    uint32_t mf = 0, mr = 0;
+    auto push = [&](uint32_t b) {
+        mf = ((mf << 2) | b) & MM;
+        mr = (mr >> 2) | ((3u - b) << (2 * SK_M - 2));
+    };
+    for (int t = 0; t < SK_M - 1; t++) push(code2(rd[t]));
+    for (int j = 0; j < nh; j++) {
+        push(code2(rd[j + SK_M - 1]));
+        hs[j * 64 + lane] = mmer_hash(mf < mr ? mf : mr);
+    }
+    for (int b0 = 0; b0 < nh; b0 += W) {  // suffix minima inside each block of W
+        const int b1 = min(b0 + W, nh);
+        uint32_t m = 0xFFFFFFFFu;
+        for (int j = b1 - 1; j >= b0; j--) {
+            m = min(m, hs[j * 64 + lane]);
+            hs[j * 64 + lane] = m;
+        }
+    }
+    mf = mr = 0;
+    for (int t = 0; t < SK_M - 1; t++) push(code2(rd[t]));
+    uint32_t pre = 0xFFFFFFFFu;
+    for (int e = 0; e < nh; e++) {  // e = a window's last m-mer: prefix minimum of e's block
+        push(code2(rd[e + SK_M - 1]));
+        const uint32_t h = mmer_hash(mf < mr ? mf : mr);
+        pre = (e % W == 0) ? h : min(pre, h);
+        const int w = e - W + 1;
+        if (w >= 0 && w < nw) wbv[s + w] = min_remix(min(hs[w * 64 + lane], pre));
+    }
+}
 
 constexpr int STAGE_W = 40896;  // LDS stage of the wide kernels (256 reads of <= 159 bases; upsweep in 80 KB)
 constexpr int FINE_W_BITS = 14;  // fine histogram bins (16384 buckets: up to ~30 M distinct keys)
@@ -29,6 +96,18 @@ __device__ inline K128 rkey(const RecW &r) { return K128{r.lo, r.hi}; }
 __device__ inline unsigned int rec_bucket(const RecW &r, int bbits) {
     return (unsigned int)(mix128(rkey(r)) >> 32) >> (32 - bbits);
 }
+// minimizer-bucketed records (k <= WMB_MAX_K): placement bits 32..55 in hi's top 24 bits
+struct alignas(8) RecWM : RecW {};
+static_assert(sizeof(RecWM) == 24, "wide record layout");
+__device__ inline K128 rkey(const RecWM &r) { return K128{r.lo, r.hi & ((1ull << WMB_SHIFT) - 1)}; }
+__device__ inline unsigned int rec_bucket(const RecWM &r, int bbits) {
+    return bbits ? ((unsigned int)(r.hi >> WMB_SHIFT) << 8) >> (32 - bbits) : 0u;
+}
+struct StoreWM {
+    RecWM *p;
+    __device__ inline RecWM load(uint64_t i) const { return p[i]; }
+    __device__ inline void store(uint64_t i, const RecWM &r) const { p[i] = r; }
+};
 struct StoreW {
     RecW *p;
     __device__ inline RecW load(uint64_t i) const { return p[i]; }
@@ -59,11 +138,12 @@ __device__ inline void roll_w(K128 &fwd, K128 &rc, uint32_t b, const K128 &mask,
 // ---- upsweep: fine histogram (16384 bins by mix128) + HyperLogLog, per read group ----------
 // lens[2] is set when a read has an 'N' / another byte, or a tile does not fit the stage:
 // the host then counts on the HBM table instead.
+template <bool MB>
 __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                           int k, uint64_t gsize, unsigned int *hist,
                                                           uint8_t *hll_blocks, unsigned long long *npos,
                                                           unsigned int *maxlocal, unsigned int *skew,
-                                                          unsigned int *lens) {
+                                                          unsigned int *lens, const uint32_t *wbv) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
     __shared__ unsigned int h_cnt[FINE_W / 2];
     __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
@@ -108,7 +188,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
             const uint32_t hh = (uint32_t)(mix128(c) >> 32);  // as k_upsweep
             const uint32_t j = hh >> (32 - HLL_REG_BITS);
             const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
-            const uint32_t f = hh >> (32 - FINE_W_BITS);
+            const uint32_t f = (MB ? wbv[s + t + 1 - k] : hh) >> (32 - FINE_W_BITS);
             atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
             if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
         }
@@ -140,10 +220,11 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
 
 // ---- downsweep: records to their (coarse bucket, group) runs (count_part.h k_downsweep for
 // clean reads, 24-B records, DS_RW windows per lane per round) -------------------------------
+template <bool MB>
 __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                             int k, uint64_t gsize, uint64_t ngroups, int cbits,
                                                             const unsigned long long *offs, RecW *recs,
-                                                            uint64_t read_base) {
+                                                            uint64_t read_base, const uint32_t *wbv) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
     __shared__ RecW sorted[DS_BATCH_W];
     __shared__ uint8_t sbk[DS_BATCH_W];
@@ -194,11 +275,12 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, 
                     const bool f = fwd < rc, pal = fwd == rc;
                     const K128 c = f ? fwd : rc;
                     uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
+                    const uint32_t pv = MB ? wbv[s + w] : (uint32_t)(mix128(c) >> 32);
                     rr[j].lo = c.lo;
-                    rr[j].hi = c.hi;
+                    rr[j].hi = MB ? (c.hi | ((unsigned long long)(pv >> 8) << WMB_SHIFT)) : c.hi;
                     rr[j].read = (unsigned int)(r + read_base);
                     rr[j].ev = lC | (lT << 16);
-                    cb[j] = cbits ? ((unsigned int)(mix128(c) >> 32) >> (32 - cbits)) : 0u;
+                    cb[j] = cbits ? (pv >> (32 - cbits)) : 0u;
                     rk[j] = atomicAdd(&bcnt[cb[j]], 1u);
                     t++;
                     w++;
@@ -327,8 +409,8 @@ __global__ void __launch_bounds__(256) k_level3_ends(const unsigned long long *g
 }
 
 // bend != nullptr: bucket b is [bstart[b], bend[b]) (third level), else [bstart[b], bstart[b + 1])
-template <int SLOTS>
-__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, const unsigned long long *bstart,
+template <int SLOTS, typename R = RecW>
+__global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const R *recs, const unsigned long long *bstart,
                                                             const unsigned long long *bend, long long limit, K128 *dkey, unsigned int *dcnt,
                                                             unsigned long long *dfc, unsigned long long *dft,
                                                             SubSlotW *sub, unsigned int *nsolid,
@@ -352,7 +434,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, c
     __syncthreads();
     const uint64_t r0 = bstart[b], r1 = bend ? bend[b] : bstart[b + 1];
     constexpr int U = 4;  // loads of U records issued before any insert
-    auto ins = [&](const RecW &x) {
+    auto ins = [&](const R &x) {
         const unsigned int lC = x.ev & 0xFFFFu, lT = x.ev >> 16;
         const K128 c = rkey(x);
         const unsigned long long rd = (unsigned long long)x.read << 32;
@@ -360,7 +442,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const RecW *recs, c
     };
     uint64_t i = r0 + threadIdx.x;
     for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
-        RecW raw[U];
+        R raw[U];
 #pragma unroll
         for (int u = 0; u < U; u++) raw[u] = recs[i + u * (uint64_t)blockDim.x];
 #pragma unroll

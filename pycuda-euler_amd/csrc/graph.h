@@ -114,16 +114,41 @@ struct OpsW {
 };
 
 // canonical K128 key -> dense solid id in the wide table
+// minimizer buckets of 128-bit keys (count_wide.h, round 4): a key's placement hash
+__host__ __device__ inline uint32_t bits30_128(const K128 &x, int sh) {  // 0 <= sh <= 98
+    const uint64_t v = sh >= 64 ? (x.hi >> (sh - 64)) : sh == 0 ? x.lo : ((x.lo >> sh) | (x.hi << (64 - sh)));
+    return (uint32_t)v & ((1u << (2 * SK_M)) - 1);
+}
+// minimizer of a 128-bit k-mer code (the twin's m-mer p is the reverse complement of c's m-mer
+// w - 1 - p: one 128-bit reversal instead of one per m-mer)
+__host__ __device__ inline uint32_t minimizer_of_w(const K128 &c, int k) {
+    const K128 tc = twin128(c, k);
+    const int w = k - SK_M + 1;
+    uint32_t v = 0xFFFFFFFFu;
+    for (int p = 0; p < w; p++) {
+        const uint32_t f = bits30_128(c, 2 * (k - SK_M - p)), r = bits30_128(tc, 2 * p);
+        const uint32_t h = mmer_hash(f < r ? f : r);
+        v = h < v ? h : v;
+    }
+    return min_remix(v);
+}
+__host__ __device__ inline uint64_t wide_place(const K128 &c, int k, bool mb) {
+    const uint64_t h = mix128(c);
+    return mb ? ((uint64_t)minimizer_of_w(c, k) << 32) | (h & 0xFFFFFFFFull) : h;
+}
+
 struct SolidIndexW {
     const SlotW *table;  // general count: the HBM table
     uint64_t capmask;
     const SubSlotW *sub;  // partitioned count (count_wide.h): bucket sub-tables of `slots` slots
     int bbits;
     unsigned int slots;
+    int mb = 0;  // buckets by minimizer (count_wide.h): placement = wide_place(c, k, true)
+    int k = 0;
     __device__ inline unsigned int find(const K128 &c) const {
         if (!sub) return lookup_w(table, capmask, c);
         const unsigned long long w1 = wide_w1(c), w2 = wide_w2(c);
-        const uint64_t h = mix128(c);
+        const uint64_t h = wide_place(c, k, mb != 0);
         const SubSlotW *r = sub + (bbits ? (h >> (64 - bbits)) : 0ull) * slots;
         unsigned int slot = (unsigned int)(((uint64_t)(uint32_t)h * slots) >> 32);  // wide_slot0
         for (unsigned int probe = 0; probe < slots; probe++) {
