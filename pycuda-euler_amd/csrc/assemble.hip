@@ -1871,6 +1871,19 @@ template <> struct JoinT<OpsW> {
         k_half_join<2048, 512, ODD><<<nb, 512, 0, st>>>(r, bb, be, up, succ, ov);
     }
 };
+struct JoinTM {  // 128-bit keys on minimizer-bucketed ids: junctions bucketed by their minimizer
+    using R = RecJM;
+    using S = StoreJM;
+    static void emit_l1(const K128 *d, unsigned U, int k, const uint8_t *up, int lb, uint64_t fc, unsigned long long *gc,
+                        R *o, unsigned *ov, hipStream_t st) {
+        k_half_emit_l1<K128, R><<<grid_for(U, 1024, 2048), 1024, 0, st>>>(d, U, k, up, lb, fc, gc, o, ov);
+    }
+    template <bool ODD>
+    static void join(unsigned nb, const R *r, const unsigned long long *bb, const unsigned long long *be,
+                     const uint8_t *up, unsigned *succ, unsigned *ov, hipStream_t st) {
+        k_half_join<2048, 512, ODD, RecJM><<<nb, 512, 0, st>>>(r, bb, be, up, succ, ov);
+    }
+};
 template <> struct JoinT<Ops64> {
     using R = RecJ64;
     using S = StoreJ64;
@@ -1885,9 +1898,8 @@ template <> struct JoinT<Ops64> {
     }
 };
 
-template <typename Ops>
+template <typename Ops, typename J = JoinT<Ops>>
 int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned int *&gate) {
-    using J = JoinT<Ops>;
     using R = typename J::R;
     using S = typename J::S;
     ok = false;
@@ -2145,7 +2157,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     constexpr bool XT = std::is_same<Ops, OpsX>::value;  // extended alphabet (extended.h)
     if constexpr (!XT) {
         if (U && !ext_succ && k >= 8 && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
-            EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
+        {
+            if constexpr (std::is_same<Index, SolidIndexW>::value) {
+                if (sidx.mb && kn().join_mb != 0) EC_CHECK((links_join<Ops, JoinTM>(s, k, U, joined, gate)));
+                else EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
+            } else {
+                EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
+            }
+        }
     }
     if (U && !ext_succ) {  // (after a join: only if it overflowed, decided on the device)
         // gated: a small grid-stride grid, so the normal case (the gate closed) costs ~2 us a

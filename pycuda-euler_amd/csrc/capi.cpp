@@ -52,6 +52,7 @@ void refresh_knobs() {
         k.skf_keys = num("EULERHIP_SKF_KEYS", 0);
         k.rank_coop = num("EULERHIP_RANK_COOP", -1);
         k.wide_mb = num("EULERHIP_WIDE_MB", -1);
+        k.join_mb = num("EULERHIP_JOIN_MB", -1);
     }
     g_knobs = k;
 }

@@ -45,6 +45,17 @@ struct StoreJ {
     __device__ inline RecJ load(uint64_t i) const { return p[i]; }
     __device__ inline void store(uint64_t i, const RecJ &r) const { p[i] = r; }
 };
+// minimizer-bucketed ids (count_wide.h, round 4): a junction's bucket = its own minimizer
+// (pad = min_remix of it), which is the minimizer of most k-mers holding it -- a join bucket's
+// nodes then sit in a few id ranges, so the link writes succ[x] stay local instead of spraying
+// the whole node array (config 5: 3.9e8 random 4-B writes)
+struct alignas(8) RecJM : RecJ {};
+__device__ inline unsigned int rec_bucket(const RecJM &r, int bbits) { return bbits ? r.pad >> (32 - bbits) : 0u; }
+struct StoreJM {
+    RecJM *p;
+    __device__ inline RecJM load(uint64_t i) const { return p[i]; }
+    __device__ inline void store(uint64_t i, const RecJM &r) const { p[i] = r; }
+};
 
 // reverse complement of a j-mer, 32 <= j <= 62
 __device__ inline K128 twin_j(const K128 &x, int j) {
@@ -70,8 +81,8 @@ __global__ void __launch_bounds__(256) k_cursor_init(unsigned long long *gcur, u
 // 24 B (key halves, one id word per side whose bit 31 marks a second distinct id): 2048 slots in
 // 48 KB, three workgroups per CU.  ODD_K: no palindromic k-mers, twin(x) = x ^ 1 without the
 // palindrome flags' random reads.
-template <int SLOTS, int NT, bool ODD_K>
-__global__ void __launch_bounds__(NT) k_half_join(const RecJ *recs, const unsigned long long *bbeg,
+template <int SLOTS, int NT, bool ODD_K, typename R = RecJ>
+__global__ void __launch_bounds__(NT) k_half_join(const R *recs, const unsigned long long *bbeg,
                                                   const unsigned long long *bend, const uint8_t *upal,
                                                   unsigned int *succ, unsigned int *overflow) {
     constexpr unsigned int MANY = 0x80000000u;
@@ -94,7 +105,7 @@ __global__ void __launch_bounds__(NT) k_half_join(const RecJ *recs, const unsign
     for (uint64_t base = r0; base < r1; base += NT) {
         const uint64_t i = base + threadIdx.x;
         const bool valid = i < r1;
-        RecJ r{};
+        R r{};
         if (valid) r = recs[i];
         const K128 o{r.lo, r.hi};
         const unsigned long long a1 = wide_w1(o), a2 = wide_w2(o);
@@ -282,6 +293,27 @@ __device__ inline void half_recs(unsigned long long c, unsigned int t, int j, un
     e2 = p == tp;
     x1 = make_recj64(s, ic, 0);
     x2 = make_recj64(p, ic, 1);
+}
+// the same records with their junctions' minimizers (k = j + 1 <= 63: the prefix junction holds
+// m-mers 0 .. w - 2 of the key, the suffix junction m-mers 1 .. w - 1)
+__device__ inline void half_recs(const K128 &c, unsigned int t, int j, const K128 &mj, const uint8_t *upal, RecJM &r1,
+                                 RecJM &r2, bool &e1, bool &e2, RecJM &x1, RecJM &x2) {
+    half_recs(c, t, j, mj, upal, static_cast<RecJ &>(r1), static_cast<RecJ &>(r2), e1, e2, static_cast<RecJ &>(x1),
+              static_cast<RecJ &>(x2));
+    const int k = j + 1, w = k - SK_M + 1;
+    const K128 tc = twin128(c, k);
+    uint32_t mp = 0xFFFFFFFFu, ms = 0xFFFFFFFFu;
+    for (int p = 0; p < w; p++) {
+        const uint32_t f = bits30_128(c, 2 * (k - SK_M - p)), r = bits30_128(tc, 2 * p);
+        const uint32_t h = mmer_hash(f < r ? f : r);
+        if (p < w - 1) mp = h < mp ? h : mp;
+        if (p > 0) ms = h < ms ? h : ms;
+    }
+    const uint32_t vs = min_remix(ms), vp = min_remix(mp);
+    r1.pad = vs;  // (r1 / x1: the suffix junction, r2 / x2: the prefix)
+    x1.pad = vs;
+    r2.pad = vp;
+    x2.pad = vp;
 }
 __device__ inline K128 kmask_j(int j, K128 *) { return kmask128(j); }
 __device__ inline unsigned long long kmask_j(int j, unsigned long long *) { return kmask64(j); }
