@@ -340,8 +340,18 @@ def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None):
     return res
 
 
+def finish_mode(finish, k, rule):
+    """"auto": the partitioned finish where the gathered ids have minimizer locality (21 <= k <=
+    32 on minimizer owners: a segment's chains are ~1/9 of its nodes), else the replicated one
+    (on hash-ordered ids every node is its own chain and the all-gathered chain records would
+    outweigh the successor array 8 : 1)"""
+    if finish != "auto":
+        return finish
+    return "partitioned" if 21 <= k <= 32 and rule == OWNER_MINIMIZER else "replicated"
+
+
 def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None,
-                     phase_ms=None, partitioned=None, fetch=True, finish="partitioned"):
+                     phase_ms=None, partitioned=None, fetch=True, finish="auto"):
     """Run steps 1-4 for this rank; returns (result, n_positions_total).  on_count(stats)
     receives the shard-count statistics (per-kernel times with EC_FLAG_TIMING); phase_ms, a
     dict, receives the wall time of every step (device-synchronised by the engine calls).
@@ -363,11 +373,13 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     tick("count")
     if on_count:
         on_count(st)
+    rule = OWNER_MINIMIZER
     if comm.world > 1 and 21 <= k <= 32:  # one owner rule for every rank, from the job's counts
         engine.set_owner_rule(OWNER_MINIMIZER)
         rule = owner_rule_for(comm.allreduce_vec(engine.owner_counts(comm.world)), k)
         if rule != OWNER_MINIMIZER:
             engine.set_owner_rule(rule)
+    finish = finish_mode(finish, k, rule)
     recs, counts = engine.export_by_owner(comm.world)
     tick("export")
     # the job's k-mer positions ride along with the exchange's byte counts
@@ -458,7 +470,7 @@ class ShardedAssembler:
         return self.count_stats
 
 
-def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None, finish="partitioned"):
+def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None, finish="auto"):
     """Simulate the distributed algorithm with len(engines) ranks on the local device(s):
     same engine calls, the collectives done by concatenation.  Returns rank 0's result."""
     world = len(engines)
@@ -471,7 +483,7 @@ def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=N
     return local_sharded_assemble_shards(engines, parts, k, limit, flags, partitioned, finish)
 
 
-def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partitioned=None, finish="partitioned"):
+def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partitioned=None, finish="auto"):
     """local_sharded_assemble on given shards: parts[r] = (buf, off, read_base) of rank r (host
     arrays; global read ids read_base.., increasing with r, gaps allowed)."""
     import torch
@@ -497,6 +509,7 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
         eng.set_owner_rule(rule)
         sends.append(eng.export_by_owner(world))
     local_sharded_assemble_shards.last_rule = rule
+    finish = finish_mode(finish, k, rule)
     local_sharded_assemble_shards.last_counts = [c for _, c in sends]
     solids = []
     for dst, eng in enumerate(engines):
