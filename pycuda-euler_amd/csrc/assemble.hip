@@ -1312,14 +1312,16 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     if (n) {
         k_agg_bucket_ids<<<grid_for(n, B), B, 0, st>>>(d_agg, n, bbits, s->mbid.as<unsigned int>(),
                                                       s->midx.as<unsigned int>(), own.mc, own.sk);
-        size_t bytes = 0;
-        EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, s->mbid.as<unsigned int>(), s->mbid2.as<unsigned int>(),
-                                         s->midx.as<unsigned int>(), s->midx2.as<unsigned int>(), n, 0, bbits + 1, st));
-        EC_CHECK(s->tmp.ensure(bytes));
-        EC_HIP(rocprim::radix_sort_pairs(s->tmp.p, bytes, s->mbid.as<unsigned int>(), s->mbid2.as<unsigned int>(),
-                                         s->midx.as<unsigned int>(), s->midx2.as<unsigned int>(), n, 0, bbits + 1, st));
-        k_bucket_bounds<<<grid_for(n, B), B, 0, st>>>(s->mbid2.as<unsigned int>(), n, nb,
-                                                     s->bstart.as<unsigned long long>());
+        // indices by bucket: counting sort (shard.h k_cs_*), buckets 0..nb (nb: filler records)
+        const unsigned int nbins = nb + 1, nch = (unsigned int)((n + CS_CHUNK - 1) / CS_CHUNK);
+        const uint64_t cells = (uint64_t)nbins * nch;
+        EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 2 * cells) * 4));
+        unsigned int *hist = s->mbid2.as<unsigned int>(), *incl = hist + cells;
+        k_cs_hist<<<nch, 256, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist);
+        EC_CHECK(scan_incl_u32(s, hist, incl, cells));
+        k_cs_scatter<<<nch, 256, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist, incl,
+                                                  s->midx2.as<unsigned int>());
+        k_cs_bounds<<<grid_for(nbins, B), B, 0, st>>>(hist, incl, nbins, nch, s->bstart.as<unsigned long long>());
     }
     mark(s, 2 * EC_STAGE_COUNT + 1);
     mark(s, 2 * EC_STAGE_COMPACT);

@@ -183,6 +183,42 @@ __global__ void __launch_bounds__(256) k_agg_bucket_ids(const Agg *in, uint64_t 
     }
 }
 
+// Counting sort of record indices by bucket id (round 4; a rocPRIM radix sort of (id, index)
+// pairs took 4 x 55 us a call): per chunk of CS_CHUNK records an LDS histogram of the nbins
+// ids, stored bucket-major; one scan over (bucket, chunk); per chunk LDS cursors place the
+// indices.  The order inside a (bucket, chunk) cell is not deterministic -- the bucket tables
+// do not depend on it.
+constexpr unsigned int CS_CHUNK = 16384;
+__global__ void __launch_bounds__(256) k_cs_hist(const unsigned int *bid, uint64_t n, unsigned int nbins, unsigned int nch,
+                                                 unsigned int *hist) {
+    extern __shared__ unsigned int csh[];
+    for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) csh[i] = 0;
+    __syncthreads();
+    const uint64_t c = blockIdx.x, t0 = c * CS_CHUNK, t1 = t0 + CS_CHUNK < n ? t0 + CS_CHUNK : n;
+    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) atomicAdd(&csh[bid[t]], 1u);
+    __syncthreads();
+    for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) hist[(uint64_t)i * nch + c] = csh[i];
+}
+__global__ void __launch_bounds__(256) k_cs_scatter(const unsigned int *bid, uint64_t n, unsigned int nbins,
+                                                    unsigned int nch, const unsigned int *hist,
+                                                    const unsigned int *incl, unsigned int *out) {
+    extern __shared__ unsigned int csh[];
+    const uint64_t c = blockIdx.x, t0 = c * CS_CHUNK, t1 = t0 + CS_CHUNK < n ? t0 + CS_CHUNK : n;
+    for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) {
+        const uint64_t q = (uint64_t)i * nch + c;
+        csh[i] = incl[q] - hist[q];
+    }
+    __syncthreads();
+    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) out[atomicAdd(&csh[bid[t]], 1u)] = (unsigned int)t;
+}
+__global__ void __launch_bounds__(256) k_cs_bounds(const unsigned int *hist, const unsigned int *incl, unsigned int nbins,
+                                                   unsigned int nch, unsigned long long *bstart) {
+    for (unsigned int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
+        const uint64_t q = (uint64_t)b * nch;
+        bstart[b] = incl[q] - hist[q];
+    }
+}
+
 // bstart[b] = first position of bucket b in the sorted ids (b = 0..nb; bstart[nb] = real records)
 __global__ void __launch_bounds__(256) k_bucket_bounds(const unsigned int *sbid, uint64_t n, unsigned int nb,
                                                        unsigned long long *bstart) {
