@@ -1640,17 +1640,13 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     const int cbits = std::min(bbits, std::min(DS_MAX_CBITS, std::max(1, bbits - fan)));
     const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
     const uint64_t Bt = Bk << sbits;  // tables
-    // third-level capacity: mean + 30 % + 1024 (a sub-bucket's records are a sum over its
-    // ~800 keys of their multiplicities: its spread is a few % of the mean)
-    uint64_t fcap3 = sbits ? P / Bt + P / Bt * 3 / 10 + 1024 : 0;
-    if (sbits && kn().wide_l3_cap > 0) fcap3 = (uint64_t)kn().wide_l3_cap;
     const unsigned int SLOTS = sbits ? 1664u : (unsigned int)SLOTS_W;
     mark(s, 2 * EC_STAGE_COUNT);
     EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
     EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
     EC_CHECK(s->tot.ensure((Bk + 1) * 8));
     EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
-    EC_CHECK(s->recs.ensure(std::max<uint64_t>(P, Bt * fcap3) * sizeof(RecW)));
+    EC_CHECK(s->recs.ensure(std::max<uint64_t>(P, 1) * sizeof(RecW)));
     const bool second = bbits > cbits;
     if (second) EC_CHECK(s->recs2.ensure(P * sizeof(RecW)));
     s->stats.record_bytes = (uint32_t)sizeof(RecW);
@@ -1683,24 +1679,17 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
             k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
                 StoreW{s->recs.as<RecW>()}, StoreW{s->recs2.as<RecW>()}, s->bstart.as<unsigned long long>(),
                 s->gcur.as<unsigned long long>(), cbits, bbits);
-        if (sbits) {  // fine buckets (recs2) -> fixed-capacity sub-buckets (recs)
-            EC_CHECK(s->bb2.ensure((Bt + 1) * 8 * 2));
-            EC_CHECK(s->gcur.ensure(Bt * 8));
-            EC_CHECK(s->fcur.ensure((Bt + 1) * 8));
-            unsigned long long *b3 = s->fcur.as<unsigned long long>();
-            k_level3_init<<<grid_for(Bt + 1, B, 8192), B, 0, st>>>(s->bstart.as<unsigned long long>(), Bk, sbits, fcap3,
-                                                                   b3, s->gcur.as<unsigned long long>());
+        if (sbits) {  // fine buckets (recs2) -> their sub-buckets (recs), exact (k_split3)
+            EC_CHECK(s->bb2.ensure((Bt + 1) * 8));
+            const unsigned long long cap3 = kn().wide_l3_cap > 0 ? (unsigned long long)kn().wide_l3_cap : 0ull;
             if (mb)
-                k_refine<RecWM, StoreWM, StoreWM><<<dim3((unsigned)Bk, 1), BUCKET_THREADS, 0, st>>>(
-                    StoreWM{s->recs2.as<RecWM>()}, StoreWM{s->recs.as<RecWM>()}, b3, s->gcur.as<unsigned long long>(),
-                    bbits, bbits + sbits, fcap3, &dsc->overflow);
+                k_split3<RecWM><<<(unsigned)Bk, 512, 0, st>>>(s->recs2.as<RecWM>(), s->bstart.as<unsigned long long>(),
+                                                              bbits, sbits, s->recs.as<RecWM>(),
+                                                              s->bb2.as<unsigned long long>(), cap3, &dsc->overflow);
             else
-                k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Bk, 1), BUCKET_THREADS, 0, st>>>(
-                    StoreW{s->recs2.as<RecW>()}, StoreW{s->recs.as<RecW>()}, b3, s->gcur.as<unsigned long long>(),
-                    bbits, bbits + sbits, fcap3, &dsc->overflow);
-            k_level3_ends<<<grid_for(Bt, B, 8192), B, 0, st>>>(s->gcur.as<unsigned long long>(), Bt, fcap3,
-                                                               s->bb2.as<unsigned long long>(),
-                                                               s->bb2.as<unsigned long long>() + Bt + 1);
+                k_split3<RecW><<<(unsigned)Bk, 512, 0, st>>>(s->recs2.as<RecW>(), s->bstart.as<unsigned long long>(),
+                                                             bbits, sbits, s->recs.as<RecW>(),
+                                                             s->bb2.as<unsigned long long>(), cap3, &dsc->overflow);
         }
         kmark(s, 4, 1);
     }
@@ -1720,10 +1709,10 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         &dsc->ndistinct, &dsc->overflow)
     if (sbits && mb)
         EC_BUCKET_W(1664, RecWM, s->recs.as<RecWM>(), s->bb2.as<unsigned long long>(),
-                    s->bb2.as<unsigned long long>() + Bt + 1);
+                    s->bb2.as<unsigned long long>() + 1);
     else if (sbits)
         EC_BUCKET_W(1664, RecW, s->recs.as<RecW>(), s->bb2.as<unsigned long long>(),
-                    s->bb2.as<unsigned long long>() + Bt + 1);
+                    s->bb2.as<unsigned long long>() + 1);
     else if (mb)
         EC_BUCKET_W(SLOTS_W, RecWM, second ? s->recs2.as<RecWM>() : s->recs.as<RecWM>(),
                     s->bstart.as<unsigned long long>(), nullptr);

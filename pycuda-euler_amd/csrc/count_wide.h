@@ -324,6 +324,42 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, 
     }
 }
 
+// ---- third level, exact (round 4): fine bucket b's records split into its 2^sbits sub-buckets
+// by two passes in one workgroup (LDS counts, then LDS cursors), written back to back from
+// bstart[b]: b3[b 2^sbits + j] = first record of sub-bucket j.  The fixed-capacity regions of
+// round 3 (mean + 30 % + 1024) assumed uniform hash buckets; minimizer buckets group whole
+// minimizers (~(w + 1) / 2 k-mers x coverage records each), whose spread sent config-5-sized
+// inputs past a few hundred sub-bucket capacities.  cap != 0 (tests): a sub-bucket past cap
+// records raises *over, as the capacity did.
+template <typename R>
+__global__ void __launch_bounds__(512) k_split3(const R *in, const unsigned long long *bstart, int bbits, int sbits,
+                                                R *out, unsigned long long *b3, unsigned long long cap,
+                                                unsigned int *over) {
+    __shared__ unsigned int cnt[64], cur[64];
+    const unsigned int b = blockIdx.x, F = 1u << sbits, tid = threadIdx.x;
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    if (tid < 64) cnt[tid] = 0;
+    __syncthreads();
+    for (uint64_t i = r0 + tid; i < r1; i += 512) atomicAdd(&cnt[rec_bucket(in[i], bbits + sbits) & (F - 1)], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        unsigned int run = 0;
+        for (unsigned int j = 0; j < F; j++) {
+            cur[j] = run;
+            b3[(uint64_t)b * F + j] = r0 + run;
+            if (cap && cnt[j] > cap) *over = 1u;
+            run += cnt[j];
+        }
+        if (b + 1 == gridDim.x) b3[(uint64_t)gridDim.x * F] = r1;
+    }
+    __syncthreads();
+    for (uint64_t i = r0 + tid; i < r1; i += 512) {
+        const R r = in[i];
+        const unsigned int p = atomicAdd(&cur[rec_bucket(r, bbits + sbits) & (F - 1)], 1u);
+        out[r0 + p] = r;
+    }
+}
+
 // ---- bucket pass: one LDS table of 128-bit keys per final bucket ----------------------------
 // Slots claim a key with two 64-bit CASes on its claim words (wide_w1 / wide_w2, never 0),
 // as wide_slot does in HBM; a slot whose first word matches but whose second word went to
