@@ -20,14 +20,14 @@ namespace ec {
 // bucket gets are the k-mers of ~(w + 1) / 2-window runs of the genome: consecutive nodes of a
 // path mostly share a tile of ids (rank_tile.h ranks them in LDS) -- on hash buckets every link
 // leaves its tile.  The placement hash keeps mix128's low 32 bits for the slot inside a table:
-//   wide_place(c) = min_remix(minimizer) << 32 | low 32 bits of mix128(c).
+//   wide_place(c) = min_remix_w(minimizer) << 32 | low 32 bits of mix128(c).
 // Records carry the top 24 placement bits in the unused top bits of the key's high word (2k <=
 // 104: k <= 52), so the refine levels need not recompute the minimizer (graph.h wide_place).
 constexpr int WMB_MAX_K = 52;
 constexpr int WMB_SHIFT = 40;  // record hi: key bits below, placement bits 32..55 above
 
 // Per-window minimizers of the reads (one wave per 64 reads, lane = read): wbv[off[r] + w] =
-// min_remix(minimizer of window w of read r), read by k_upsweep_w / k_downsweep_w<true>.  The
+// min_remix_w(minimizer of window w of read r), read by k_upsweep_w / k_downsweep_w<true>.  The
 // m-mer hashes of a read go to LDS (lane-interleaved), suffix minima over blocks of w in place,
 // then a forward pass recomputes the hashes for the blocks' prefix minima (van Herk / Gil-Werman:
 // window = min(suffix[start], prefix[end])).  Reads longer than WMB_MAXL take no part: the wide
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *
         const uint32_t h = mmer_hash(mf < mr ? mf : mr);
         pre = (e % W == 0) ? h : min(pre, h);
         const int w = e - W + 1;
-        if (w >= 0 && w < nw) wbv[s + w] = min_remix(min(hs[w * 64 + lane], pre));
+        if (w >= 0 && w < nw) wbv[s + w] = min_remix_w(min(hs[w * 64 + lane], pre));
     }
 }
 

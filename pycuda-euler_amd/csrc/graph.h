@@ -130,7 +130,7 @@ __host__ __device__ inline uint32_t minimizer_of_w(const K128 &c, int k) {
         const uint32_t h = mmer_hash(f < r ? f : r);
         v = h < v ? h : v;
     }
-    return min_remix(v);
+    return min_remix_w(v);
 }
 __host__ __device__ inline uint64_t wide_place(const K128 &c, int k, bool mb) {
     const uint64_t h = mix128(c);

@@ -46,7 +46,7 @@ struct StoreJ {
     __device__ inline void store(uint64_t i, const RecJ &r) const { p[i] = r; }
 };
 // minimizer-bucketed ids (count_wide.h, round 4): a junction's bucket = its own minimizer
-// (pad = min_remix of it), which is the minimizer of most k-mers holding it -- a join bucket's
+// (pad = min_remix_w of it), which is the minimizer of most k-mers holding it -- a join bucket's
 // nodes then sit in a few id ranges, so the link writes succ[x] stay local instead of spraying
 // the whole node array (config 5: 3.9e8 random 4-B writes)
 struct alignas(8) RecJM : RecJ {};
@@ -309,7 +309,7 @@ __device__ inline void half_recs(const K128 &c, unsigned int t, int j, const K12
         if (p < w - 1) mp = h < mp ? h : mp;
         if (p > 0) ms = h < ms ? h : ms;
     }
-    const uint32_t vs = min_remix(ms), vp = min_remix(mp);
+    const uint32_t vs = min_remix_w(ms), vp = min_remix_w(mp);
     r1.pad = vs;  // (r1 / x1: the suffix junction, r2 / x2: the prefix)
     x1.pad = vs;
     r2.pad = vp;

@@ -46,6 +46,12 @@ __host__ __device__ inline uint32_t mmer_hash(uint32_t x) {
 // stay uniform -- so the fine bin, coarse and final bucket (top bits) and the owner ranges are
 // even.  Bijective; k_skpart_w takes the bucket bits as runv << 18 (no remix per run).
 __host__ __device__ inline uint32_t min_remix(uint32_t x) { return (x >> 14) | (x << 18); }
+// the same for placements that use up to ~20 bucket bits (count_wide.h minimizer buckets: 14
+// fine + up to 6 third-level bits, join_w.h junction buckets): min_remix's bits after the top 14
+// are the minimum's HIGH bits -- almost always 0 (the minimum of w ~ 37 hashes is ~2^32 / 38) --
+// so they put every key of a fine bucket into its first sub-bucket.  Here the top 20 bits are
+// the minimum's low 20 bits, uniform
+__host__ __device__ inline uint32_t min_remix_w(uint32_t x) { return (x >> 20) | (x << 12); }
 
 __host__ __device__ inline uint32_t rev2_32(uint32_t x) {
     x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
