@@ -685,7 +685,9 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     }
     if (skfilt) {
         constexpr int NTF = 512;
-        const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 2048u * 72 / 100;
+        // (the table takes up to 2047 keys; the prediction runs ~10 % high.  ecoli10m_err's
+        // fullest bucket: 1525 predicted, 1485 inserted)
+        const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 1900u;
         if (k & 1)
             k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
         else
@@ -1615,6 +1617,9 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     // fixed-capacity sub-buckets of <= 800 estimated keys in 1664-slot tables (78 KB: two
     // workgroups per CU); measured before: such inputs fell to the HBM table (k_count 130 ms of
     // a 335 ms step at 1.25e9 positions).
+    if (kn().verbose)
+        fprintf(stderr, "count_wpart: mb %d P %llu est %.0f lens2 %u skew %u maxlocal %u wbv_long %u\n", (int)mb,
+                (unsigned long long)hsc.npos, hsc.est, hsc.lens[2], hsc.skew, hsc.maxlocal, hsc.wbv_long);
     if (mb && hsc.wbv_long) {  // a read past k_wbv's length: hash buckets instead
         if (mb_declined) *mb_declined = true;
         return reset();
@@ -1725,6 +1730,9 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
     EC_HIP(hipStreamSynchronize(st));
     if (hsc.overflow) {  // a bucket outgrew its LDS table: the caller counts on the HBM table
+        if (kn().verbose)
+            fprintf(stderr, "count_wpart: %u tables overflowed (%llu tables of %u slots, sbits %d, mb %d)\n",
+                    hsc.overflow, (unsigned long long)Bt, SLOTS, sbits, (int)mb);
         s->stats.table_retries++;
         return reset();
     }
@@ -1759,7 +1767,7 @@ int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, 
     {
         // minimizer buckets for k <= 52 (count_wide.h; EULERHIP_WIDE_MB=0: hash buckets)
         bool declined = false;
-        const bool mb = k <= WMB_MAX_K && kn().wide_mb != 0;
+        const bool mb = k <= WMB_MAX_K && kn().wide_mb == 1;  // (opt-in until config 5 runs on it)
         EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok, mb, &declined));
         if (declined) EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok));
     }
@@ -1977,7 +1985,7 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
     EC_CHECK(s->st1.ensure(cap * sizeof(RJump)));
     EC_CHECK(s->rbc.ensure(((cap + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
     SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
-    if (kn().rank_coop != 0 || dM) {  // one cooperative launch (rank_tile.h k_rank_supers_coop)
+    if (kn().rank_coop == 1 || dM) {  // one cooperative launch (rank_tile.h k_rank_supers_coop)
         if (!s->coop_grid) {
             int per = 0, cus = 0;
             EC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_rank_supers_coop, 256, 0));
@@ -2224,7 +2232,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         // -- in one cooperative launch that reads the chain count on the device (no host round
         // trip; its checks ride on the scalar read after the starts), or by separate launches
         unsigned int M = 0;
-        const bool coop = kn().rank_coop != 0;
+        // (measured: the cooperative launch took the headline's rank stage 0.63 -> 3.3 ms, its
+        // grid barriers far slower than the launches they replace -- opt-in only)
+        const bool coop = kn().rank_coop == 1;
         if (!coop) {
             unsigned long long M64 = 0;
             EC_HIP(hipMemcpyAsync(&M64, tbase + ntiles, 8, hipMemcpyDeviceToHost, st));

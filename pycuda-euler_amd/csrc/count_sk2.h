@@ -1209,7 +1209,7 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
             const double l = 2.0 * D / m, el = exp(-l);
             const double S = fmax(0.0, ((double)s_cells[0] - m * (1.0 - el * (1.0 + l))) / 2.0);
             const double pass = 1.1 * (S + fmax(0.0, D - S) * (1.0 - el) * (1.0 - el));  // (~10 % low: solid cells hit by collisions)
-            if (pass > (double)max_keys) s_over[0] = 1;  // (default: the table would pass ~3/4 full)
+            if (pass > (double)max_keys) s_over[0] = 1;  // (default 1900 of the table's 2048 slots)
             else atomicAdd(ndistinct, (unsigned long long)llround(D));
             if (dbg) {  // EULERHIP_SK2_STATS: the largest estimates, the predictor's refusals
                 atomicMax(&dbg[0], (unsigned long long)D);
