@@ -2021,7 +2021,8 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
     EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
     EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
     EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
-    const unsigned int masks[4] = {15u, 3u, 1u, 0u};
+    unsigned int masks[4] = {15u, 3u, 1u, 0u};
+    if (kn().sruler_mask > 0) masks[0] = (unsigned int)kn().sruler_mask;  // (A/B: first-pass ruler density)
     unsigned int r0 = 0;
     const unsigned int nblk = (M + RULER_CHUNK - 1) / RULER_CHUNK;
     for (int it = 0; it < 4; it++) {

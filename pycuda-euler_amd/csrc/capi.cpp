@@ -53,6 +53,7 @@ void refresh_knobs() {
         k.rank_coop = num("EULERHIP_RANK_COOP", -1);
         k.wide_mb = num("EULERHIP_WIDE_MB", -1);
         k.join_mb = num("EULERHIP_JOIN_MB", -1);
+        k.sruler_mask = num("EULERHIP_SRULER_MASK", 0);
     }
     g_knobs = k;
 }

@@ -96,7 +96,10 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         s_mn[i] = mn[q];
     }
     __syncthreads();
+    // (until every pointer reached its chain's head: ~log2 of the tile's longest chain rounds,
+    // all RT_ROUNDS only in a tile holding a cycle, whose minimum needs them)
     for (int r = 0; r < RT_ROUNDS; r++) {
+        bool more = false;
 #pragma unroll
         for (int q = 0; q < RT_PER; q++) {
             const uint16_t a = p[q];
@@ -104,6 +107,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
             const uint16_t m2 = s_mn[a];
             mn[q] = m2 < mn[q] ? m2 : mn[q];
             p[q] = s_p[a];
+            more |= s_lp[p[q]] != RT_NONE;
         }
         __syncthreads();
 #pragma unroll
@@ -113,7 +117,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
             s_d[i] = d[q];
             s_mn[i] = mn[q];
         }
-        __syncthreads();
+        if (!__syncthreads_or(more)) break;
     }
     // nodes of in-tile cycles: their "head" still has a predecessor.  Rank them again from the
     // cycle's smallest node (the cycle cut in front of it)
