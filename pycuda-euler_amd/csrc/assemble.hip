@@ -1588,7 +1588,16 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         EC_HIP(hipStreamSynchronize(st));
         EC_CHECK(s->wbv.ensure(std::max<uint64_t>(nb, 1) * 4));
         wbv = s->wbv.as<uint32_t>();
-        k_wbv<<<(unsigned)((nreads + 63) / 64), 64, 0, st>>>(d_reads, d_off, nreads, k, wbv, &dsc->wbv_long);
+        const unsigned g = (unsigned)((nreads + 255) / 256);
+        switch (k - SK_M + 1) {  // (WMB_MAX_K = 52: w <= 38)
+#define EC_WBV(W) \
+    case W: k_wbv<W><<<g, 256, 0, st>>>(d_reads, d_off, nreads, wbv); break;
+            EC_WBV(19) EC_WBV(20) EC_WBV(21) EC_WBV(22) EC_WBV(23) EC_WBV(24) EC_WBV(25) EC_WBV(26) EC_WBV(27)
+            EC_WBV(28) EC_WBV(29) EC_WBV(30) EC_WBV(31) EC_WBV(32) EC_WBV(33) EC_WBV(34) EC_WBV(35) EC_WBV(36)
+            EC_WBV(37) EC_WBV(38)
+#undef EC_WBV
+            default: set_error("minimizer buckets: k = %d out of range", k); return EC_ERR_ARG;
+        }
     }
     if (mb)
         k_upsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
@@ -1626,9 +1635,14 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     }
     if (hsc.lens[2] || hsc.skew || hsc.maxlocal > MAX_LOCAL_EVENT || !P) return reset();
     int sbits = 0;
+    // keys per third-level table: <= 800 on hash buckets; <= 400 on minimizer buckets, whose
+    // tables hold whole minimizers (~25 k-mers each): config 5's 2^18 tables of mean 763 keys
+    // reached 1808, past the 1664 slots (a numpy model of its genome reproduces the five
+    // overflowing tables); 2^19 of mean 381 top out at 1421
+    const double per3 = mb ? 400.0 : 800.0;
     if (est / FINE_W > 1800.0) {
-        while (sbits < 6 && est / (double)(FINE_W << sbits) > 800.0) sbits++;
-        if (est / (double)(FINE_W << sbits) > 800.0) return reset();
+        while (sbits < 6 && est / (double)(FINE_W << sbits) > per3) sbits++;
+        if (est / (double)(FINE_W << sbits) > per3) return reset();
     }
     if (kn().wide_l3 > 0) sbits = std::min(6, kn().wide_l3);
     s->stats.n_reads = nreads;

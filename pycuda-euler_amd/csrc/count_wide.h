@@ -26,56 +26,69 @@ namespace ec {
 constexpr int WMB_MAX_K = 52;
 constexpr int WMB_SHIFT = 40;  // record hi: key bits below, placement bits 32..55 above
 
-// Per-window minimizers of the reads (one wave per 64 reads, lane = read): wbv[off[r] + w] =
-// min_remix_w(minimizer of window w of read r), read by k_upsweep_w / k_downsweep_w<true>.  The
-// m-mer hashes of a read go to LDS (lane-interleaved), suffix minima over blocks of w in place,
-// then a forward pass recomputes the hashes for the blocks' prefix minima (van Herk / Gil-Werman:
-// window = min(suffix[start], prefix[end])).  Reads longer than WMB_MAXL take no part: the wide
-// partitioned path stages reads of <= 159 bases anyway.
-constexpr int WMB_MAXL = 160;
-constexpr int WMB_MAXH = WMB_MAXL - SK_M + 1;
-__global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *off, uint64_t nreads, int k,
-                                            uint32_t *wbv, unsigned int *too_long) {
-    __shared__ uint32_t hs[WMB_MAXH * 64];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t r = (uint64_t)blockIdx.x * 64 + lane;
+// Per-window minimizers of the reads (lane = read): wbv[off[r] + w] = min_remix_w(minimizer of
+// window w of read r), read by k_upsweep_w / k_downsweep_w<true>.  Van Herk / Gil-Werman with
+// the block length W = k - 14 a template parameter, as k_skpart_w: a round is one block of W
+// m-mers, their hashes and the previous block's suffix minima in registers (window rW + j =
+// min(suffix_r[j], prefix_{r+1}[j - 1])).  The bases come through a 16-byte register window.
+// (A first version kept every hash of a read in LDS: 35 KB a wave, one wave per SIMD, 20 ms at
+// config 5.)
+template <int W>
+__global__ void __launch_bounds__(256) k_wbv(const uint8_t *buf, const uint64_t *off, uint64_t nreads, uint32_t *wbv) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nreads) return;
+    constexpr int K = W + SK_M - 1;
     const uint64_t s = off[r], len = off[r + 1] - s;
-    if (len < (uint64_t)k) return;
-    if (len > (uint64_t)WMB_MAXL) {
-        *too_long = 1u;
-        return;
-    }
-    const uint8_t *rd = buf + s;
-    const int nh = (int)len - SK_M + 1, W = k - SK_M + 1, nw = (int)len - k + 1;
+    if (len < (uint64_t)K) return;
+    const uint32_t nh = (uint32_t)len - SK_M + 1, nw = (uint32_t)len - K + 1;
+    // bytes of the read in order through an aligned 16-B window
+    const uint8_t *p0 = buf + s;
+    uint64_t cur = ~0ull;  // address of the loaded window
+    uint4 win = make_uint4(0, 0, 0, 0);
+    auto byte_at = [&](uint32_t t) -> uint32_t {
+        const uint64_t a = (uint64_t)(p0 + t);
+        const uint64_t al = a & ~15ull;
+        if (al != cur) {
+            win = *reinterpret_cast<const uint4 *>(al);
+            cur = al;
+        }
+        const uint32_t o = (uint32_t)(a & 15), wd = o < 8 ? (o < 4 ? win.x : win.y) : (o < 12 ? win.z : win.w);
+        return (wd >> (8 * (o & 3))) & 0xFFu;
+    };
     constexpr uint32_t MM = (1u << (2 * SK_M)) - 1;
     uint32_t mf = 0, mr = 0;
     auto push = [&](uint32_t b) {
         mf = ((mf << 2) | b) & MM;
         mr = (mr >> 2) | ((3u - b) << (2 * SK_M - 2));
     };
-    for (int t = 0; t < SK_M - 1; t++) push(code2(rd[t]));
-    for (int j = 0; j < nh; j++) {
-        push(code2(rd[j + SK_M - 1]));
-        hs[j * 64 + lane] = mmer_hash(mf < mr ? mf : mr);
+    for (uint32_t t = 0; t < SK_M - 1; t++) push(code2(byte_at(t)));
+    uint32_t S[W];
+#pragma unroll
+    for (int j = 0; j < W; j++) {  // block 0: m-mers 0 .. W - 1 (all exist: len >= K)
+        push(code2(byte_at(SK_M - 1 + j)));
+        S[j] = mmer_hash(mf < mr ? mf : mr);
     }
-    for (int b0 = 0; b0 < nh; b0 += W) {  // suffix minima inside each block of W
-        const int b1 = min(b0 + W, nh);
-        uint32_t m = 0xFFFFFFFFu;
-        for (int j = b1 - 1; j >= b0; j--) {
-            m = min(m, hs[j * 64 + lane]);
-            hs[j * 64 + lane] = m;
+#pragma unroll
+    for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
+    for (uint32_t w0 = 0; w0 < nw; w0 += W) {
+        uint32_t H[W];
+        uint32_t P = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            const uint32_t w = w0 + j;
+            if (w < nw) wbv[s + w] = min_remix_w(min(S[j], P));
+            const uint32_t e = w0 + W + j;  // m-mer of the next block
+            H[j] = 0xFFFFFFFFu;
+            if (e < nh) {
+                push(code2(byte_at(e + SK_M - 1)));
+                H[j] = mmer_hash(mf < mr ? mf : mr);
+            }
+            P = min(P, H[j]);
         }
-    }
-    mf = mr = 0;
-    for (int t = 0; t < SK_M - 1; t++) push(code2(rd[t]));
-    uint32_t pre = 0xFFFFFFFFu;
-    for (int e = 0; e < nh; e++) {  // e = a window's last m-mer: prefix minimum of e's block
-        push(code2(rd[e + SK_M - 1]));
-        const uint32_t h = mmer_hash(mf < mr ? mf : mr);
-        pre = (e % W == 0) ? h : min(pre, h);
-        const int w = e - W + 1;
-        if (w >= 0 && w < nw) wbv[s + w] = min_remix_w(min(hs[w * 64 + lane], pre));
+#pragma unroll
+        for (int j = 0; j < W; j++) S[j] = H[j];
+#pragma unroll
+        for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
     }
 }
 
