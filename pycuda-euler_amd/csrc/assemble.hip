@@ -2173,7 +2173,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         if (U && !ext_succ && k >= 8 && kn().join_links != 0 && (kn().join_links == 1 || U >= (1u << 21)))
         {
             if constexpr (std::is_same<Index, SolidIndexW>::value) {
-                if (sidx.mb && kn().join_mb != 0) EC_CHECK((links_join<Ops, JoinTM>(s, k, U, joined, gate)));
+                // (opt-in: config 5's junction groups overflowed the join's fixed-capacity regions,
+                // sized for uniform hashes, and the probe fallback took links 39 -> 81 ms)
+                if (sidx.mb && kn().join_mb == 1) EC_CHECK((links_join<Ops, JoinTM>(s, k, U, joined, gate)));
                 else EC_CHECK(links_join<Ops>(s, k, U, joined, gate));
             } else {
                 EC_CHECK(links_join<Ops>(s, k, U, joined, gate));

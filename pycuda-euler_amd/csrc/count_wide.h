@@ -33,14 +33,28 @@ constexpr int WMB_SHIFT = 40;  // record hi: key bits below, placement bits 32..
 // min(suffix_r[j], prefix_{r+1}[j - 1])).  The bases come through a 16-byte register window.
 // (A first version kept every hash of a read in LDS: 35 KB a wave, one wave per SIMD, 20 ms at
 // config 5.)
+// Stores: a lane's W values of a round are consecutive, the lanes' runs ~a read length apart,
+// so per-lane stores touch 64 lines an instruction (config 5: 1.9e9 partial-line writes).  The
+// round's values go through LDS instead and each wave writes the runs one after the other, a
+// run per instruction (contiguous bytes).
 template <int W>
 __global__ void __launch_bounds__(256) k_wbv(const uint8_t *buf, const uint64_t *off, uint64_t nreads, uint32_t *wbv) {
+    __shared__ uint32_t s_out[4][64 * (W + 1)];  // per wave: lane l's run at l (W + 1) (+1: no bank conflicts)
+    __shared__ unsigned long long s_at[4][64];
+    __shared__ uint32_t s_n[4][64];
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nreads) return;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     constexpr int K = W + SK_M - 1;
-    const uint64_t s = off[r], len = off[r + 1] - s;
-    if (len < (uint64_t)K) return;
-    const uint32_t nh = (uint32_t)len - SK_M + 1, nw = (uint32_t)len - K + 1;
+    uint64_t s = 0, len = 0;
+    if (r < nreads) {
+        s = off[r];
+        len = off[r + 1] - s;
+    }
+    const bool act = len >= (uint64_t)K;
+    const uint32_t nh = act ? (uint32_t)len - SK_M + 1 : 0u, nw = act ? (uint32_t)len - K + 1 : 0u;
+    uint32_t maxw = nw;  // (the wave loops over its longest read's rounds: barriers inside)
+    for (int o = 32; o > 0; o >>= 1) maxw = max(maxw, (uint32_t)__shfl_xor(maxw, o));
+    uint32_t *out = s_out[wid];
     // bytes of the read in order through an aligned 16-B window
     const uint8_t *p0 = buf + s;
     uint64_t cur = ~0ull;  // address of the loaded window
@@ -61,22 +75,23 @@ __global__ void __launch_bounds__(256) k_wbv(const uint8_t *buf, const uint64_t 
         mf = ((mf << 2) | b) & MM;
         mr = (mr >> 2) | ((3u - b) << (2 * SK_M - 2));
     };
-    for (uint32_t t = 0; t < SK_M - 1; t++) push(code2(byte_at(t)));
     uint32_t S[W];
+    if (act) {
+        for (uint32_t t = 0; t < SK_M - 1; t++) push(code2(byte_at(t)));
 #pragma unroll
-    for (int j = 0; j < W; j++) {  // block 0: m-mers 0 .. W - 1 (all exist: len >= K)
-        push(code2(byte_at(SK_M - 1 + j)));
-        S[j] = mmer_hash(mf < mr ? mf : mr);
+        for (int j = 0; j < W; j++) {  // block 0: m-mers 0 .. W - 1 (all exist: len >= K)
+            push(code2(byte_at(SK_M - 1 + j)));
+            S[j] = mmer_hash(mf < mr ? mf : mr);
+        }
+#pragma unroll
+        for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
     }
-#pragma unroll
-    for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
-    for (uint32_t w0 = 0; w0 < nw; w0 += W) {
+    for (uint32_t w0 = 0; w0 < maxw; w0 += W) {
         uint32_t H[W];
         uint32_t P = 0xFFFFFFFFu;
 #pragma unroll
         for (int j = 0; j < W; j++) {
-            const uint32_t w = w0 + j;
-            if (w < nw) wbv[s + w] = min_remix_w(min(S[j], P));
+            out[lane * (W + 1) + j] = min_remix_w(min(S[j], P));
             const uint32_t e = w0 + W + j;  // m-mer of the next block
             H[j] = 0xFFFFFFFFu;
             if (e < nh) {
@@ -85,6 +100,14 @@ __global__ void __launch_bounds__(256) k_wbv(const uint8_t *buf, const uint64_t 
             }
             P = min(P, H[j]);
         }
+        s_at[wid][lane] = s + w0;
+        s_n[wid][lane] = w0 < nw ? min((uint32_t)W, nw - w0) : 0u;
+        wave_sync();
+        for (uint32_t l = 0; l < 64; l++) {  // run of lane l: one contiguous store
+            const uint32_t n = s_n[wid][l];
+            if (lane < n) wbv[s_at[wid][l] + lane] = out[l * (W + 1) + lane];
+        }
+        wave_sync();
 #pragma unroll
         for (int j = 0; j < W; j++) S[j] = H[j];
 #pragma unroll
