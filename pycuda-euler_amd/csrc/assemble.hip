@@ -273,7 +273,7 @@ struct Scalars {  // device scalars block
     unsigned int nasym, nxl, nxs;  // extended.h: one-way links, entries of their components, their starts
     unsigned int xbad;             // extended.h: a walk that never reaches its start again
     unsigned int coop_bad, coop_nr;  // k_rank_supers_coop: chains left unvisited, rulers
-    unsigned int wbv_long, wpad;     // k_wbv: a read past its length limit
+    unsigned int wbv_long, wpad;     // k_wbv: a read of another length
     unsigned int active[64];
 };
 
@@ -1582,16 +1582,24 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     kmark(s, 0, 0);
     // minimizer buckets (count_wide.h k_wbv): every window's minimizer, indexed by its base offset
     uint32_t *wbv = nullptr;
-    if (mb) {
-        uint64_t nb = 0;
-        EC_HIP(hipMemcpyAsync(&nb, d_off + nreads, 8, hipMemcpyDeviceToHost, st));
+    uint32_t mbM = 0;
+    if (mb) {  // reads of one length L <= WMB_MAXL only (k_wbv checks the others)
+        uint64_t o2[2] = {0, 0};
+        EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
         EC_HIP(hipStreamSynchronize(st));
-        EC_CHECK(s->wbv.ensure(std::max<uint64_t>(nb, 1) * 4));
+        const uint64_t L = o2[1] - o2[0];
+        if (L < (uint64_t)k || L > WMB_MAXL) {
+            if (mb_declined) *mb_declined = true;
+            return reset();
+        }
+        mbM = (uint32_t)(L - k + 1);
+        EC_HIP(hipMemsetAsync(&dsc->wbv_long, 0, 4, st));
+        EC_CHECK(s->wbv.ensure(((nreads + 255) / 256) * 256 * (uint64_t)mbM * 4));
         wbv = s->wbv.as<uint32_t>();
-        const unsigned g = (unsigned)((nreads + 255) / 256);
+        const unsigned g = (unsigned)((nreads + 63) / 64);
         switch (k - SK_M + 1) {  // (WMB_MAX_K = 52: w <= 38)
 #define EC_WBV(W) \
-    case W: k_wbv<W><<<g, 256, 0, st>>>(d_reads, d_off, nreads, wbv); break;
+    case W: k_wbv<W><<<g, 64, 0, st>>>(d_reads, d_off, nreads, (uint32_t)L, wbv, &dsc->wbv_long); break;
             EC_WBV(19) EC_WBV(20) EC_WBV(21) EC_WBV(22) EC_WBV(23) EC_WBV(24) EC_WBV(25) EC_WBV(26) EC_WBV(27)
             EC_WBV(28) EC_WBV(29) EC_WBV(30) EC_WBV(31) EC_WBV(32) EC_WBV(33) EC_WBV(34) EC_WBV(35) EC_WBV(36)
             EC_WBV(37) EC_WBV(38)
@@ -1603,12 +1611,12 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         k_upsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
                                                                    s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
                                                                    &dsc->npos, &dsc->maxlocal, &dsc->skew, dsc->lens,
-                                                                   wbv);
+                                                                   wbv, mbM);
     else
         k_upsweep_w<false><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
                                                                     s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
                                                                     &dsc->npos, &dsc->maxlocal, &dsc->skew, dsc->lens,
-                                                                    nullptr);
+                                                                    nullptr, 0u);
     kmark(s, 0, 1);
     unsigned long long *ftot = s->ftot.as<unsigned long long>();
     EC_HIP(hipMemsetAsync(ftot, 0, (FINE_W + HR) * 8, st));
@@ -1629,7 +1637,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     if (kn().verbose)
         fprintf(stderr, "count_wpart: mb %d P %llu est %.0f lens2 %u skew %u maxlocal %u wbv_long %u\n", (int)mb,
                 (unsigned long long)hsc.npos, hsc.est, hsc.lens[2], hsc.skew, hsc.maxlocal, hsc.wbv_long);
-    if (mb && hsc.wbv_long) {  // a read past k_wbv's length: hash buckets instead
+    if (mb && hsc.wbv_long) {  // reads of several lengths: hash buckets instead
         if (mb_declined) *mb_declined = true;
         return reset();
     }
@@ -1679,11 +1687,11 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     if (mb)
         k_downsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups, cbits,
                                                                      s->offs.as<unsigned long long>(),
-                                                                     s->recs.as<RecW>(), read_base, wbv);
+                                                                     s->recs.as<RecW>(), read_base, wbv, mbM);
     else
         k_downsweep_w<false><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups,
                                                                       cbits, s->offs.as<unsigned long long>(),
-                                                                      s->recs.as<RecW>(), read_base, nullptr);
+                                                                      s->recs.as<RecW>(), read_base, nullptr, 0u);
     kmark(s, 1, 1);
     if (second) {
         const unsigned RS = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8, 1024 / Ck));

@@ -26,88 +26,77 @@ namespace ec {
 constexpr int WMB_MAX_K = 52;
 constexpr int WMB_SHIFT = 40;  // record hi: key bits below, placement bits 32..55 above
 
-// Per-window minimizers of the reads (lane = read): wbv[off[r] + w] = min_remix_w(minimizer of
-// window w of read r), read by k_upsweep_w / k_downsweep_w<true>.  Van Herk / Gil-Werman with
-// the block length W = k - 14 a template parameter, as k_skpart_w: a round is one block of W
+// Per-window minimizers of reads of one length L (lane = read): window w of read r at
+// wbv_at(r, w) = (r / 256) 256 M + w 256 + r % 256 (M = L - k + 1 windows): the layout the
+// upsweep / downsweep read it in (lane = read of a 256-read tile, one window at a time), so
+// their loads and these stores are contiguous across the lanes.  Van Herk / Gil-Werman with the
+// block length W = k - 14 a template parameter, as k_skpart_w: a round is one block of W
 // m-mers, their hashes and the previous block's suffix minima in registers (window rW + j =
-// min(suffix_r[j], prefix_{r+1}[j - 1])).  The bases come through a 16-byte register window.
-// (A first version kept every hash of a read in LDS: 35 KB a wave, one wave per SIMD, 20 ms at
-// config 5.)
-// Stores: a lane's W values of a round are consecutive, the lanes' runs ~a read length apart,
-// so per-lane stores touch 64 lines an instruction (config 5: 1.9e9 partial-line writes).  The
-// round's values go through LDS instead and each wave writes the runs one after the other, a
-// run per instruction (contiguous bytes).
+// min(suffix_r[j], prefix_{r+1}[j - 1])).  One wave per 64 reads, staged in LDS by 16-byte
+// loads.  A read of another length raises *bad (the call takes mix128 buckets).
+// (First versions: every hash of a read in LDS, 35 KB a wave -- 20 ms at config 5; then
+// per-lane byte loads through a register window -- 9.5 ms, divergent dependent loads.)
+constexpr uint32_t WMB_MAXL = 160;
+__host__ __device__ inline uint64_t wbv_at(uint64_t r, uint32_t w, uint32_t M) {
+    return (r >> 8) * 256ull * M + (uint64_t)w * 256u + (r & 255u);
+}
 template <int W>
-__global__ void __launch_bounds__(256) k_wbv(const uint8_t *buf, const uint64_t *off, uint64_t nreads, uint32_t *wbv) {
-    __shared__ uint32_t s_out[4][64 * (W + 1)];  // per wave: lane l's run at l (W + 1) (+1: no bank conflicts)
-    __shared__ unsigned long long s_at[4][64];
-    __shared__ uint32_t s_n[4][64];
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+__global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *off, uint64_t nreads, uint32_t L,
+                                            uint32_t *wbv, unsigned int *bad) {
+    __shared__ __attribute__((aligned(16))) uint8_t st[64 * WMB_MAXL + 32];
     constexpr int K = W + SK_M - 1;
-    uint64_t s = 0, len = 0;
-    if (r < nreads) {
-        s = off[r];
-        len = off[r + 1] - s;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * 64, r1 = r0 + 64 < nreads ? r0 + 64 : nreads;
+    const uint64_t b0 = off[r0], b1 = off[r1];
+    const uint64_t a0 = ((uint64_t)(buf + b0)) & ~15ull, a1 = (((uint64_t)(buf + b1)) + 15) & ~15ull;
+    const uint32_t n16 = (uint32_t)((a1 - a0) >> 4);
+    if (n16 * 16 > sizeof st) {  // (reads of length L > WMB_MAXL are not sent here)
+        if (lane == 0) *bad = 1u;
+        return;
     }
-    const bool act = len >= (uint64_t)K;
-    const uint32_t nh = act ? (uint32_t)len - SK_M + 1 : 0u, nw = act ? (uint32_t)len - K + 1 : 0u;
-    uint32_t maxw = nw;  // (the wave loops over its longest read's rounds: barriers inside)
-    for (int o = 32; o > 0; o >>= 1) maxw = max(maxw, (uint32_t)__shfl_xor(maxw, o));
-    uint32_t *out = s_out[wid];
-    // bytes of the read in order through an aligned 16-B window
-    const uint8_t *p0 = buf + s;
-    uint64_t cur = ~0ull;  // address of the loaded window
-    uint4 win = make_uint4(0, 0, 0, 0);
-    auto byte_at = [&](uint32_t t) -> uint32_t {
-        const uint64_t a = (uint64_t)(p0 + t);
-        const uint64_t al = a & ~15ull;
-        if (al != cur) {
-            win = *reinterpret_cast<const uint4 *>(al);
-            cur = al;
-        }
-        const uint32_t o = (uint32_t)(a & 15), wd = o < 8 ? (o < 4 ? win.x : win.y) : (o < 12 ? win.z : win.w);
-        return (wd >> (8 * (o & 3))) & 0xFFu;
-    };
+    for (uint32_t i = lane; i < n16; i += 64)
+        reinterpret_cast<uint4 *>(st)[i] = reinterpret_cast<const uint4 *>(a0)[i];
+    __syncthreads();
+    const uint64_t r = r0 + lane;
+    if (r >= r1) return;
+    const uint64_t s = off[r];
+    if (off[r + 1] - s != L) {
+        *bad = 1u;
+        return;
+    }
+    const uint8_t *rd = st + ((uint64_t)(buf + s) - a0);
+    const uint32_t M = L - K + 1, nh = L - SK_M + 1;
     constexpr uint32_t MM = (1u << (2 * SK_M)) - 1;
     uint32_t mf = 0, mr = 0;
     auto push = [&](uint32_t b) {
         mf = ((mf << 2) | b) & MM;
         mr = (mr >> 2) | ((3u - b) << (2 * SK_M - 2));
     };
+    for (uint32_t t = 0; t < SK_M - 1; t++) push(code2(rd[t]));
     uint32_t S[W];
-    if (act) {
-        for (uint32_t t = 0; t < SK_M - 1; t++) push(code2(byte_at(t)));
 #pragma unroll
-        for (int j = 0; j < W; j++) {  // block 0: m-mers 0 .. W - 1 (all exist: len >= K)
-            push(code2(byte_at(SK_M - 1 + j)));
-            S[j] = mmer_hash(mf < mr ? mf : mr);
-        }
-#pragma unroll
-        for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
+    for (int j = 0; j < W; j++) {  // block 0: m-mers 0 .. W - 1 (all exist: L >= K)
+        push(code2(rd[SK_M - 1 + j]));
+        S[j] = mmer_hash(mf < mr ? mf : mr);
     }
-    for (uint32_t w0 = 0; w0 < maxw; w0 += W) {
+#pragma unroll
+    for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
+    uint32_t *outp = wbv + wbv_at(r, 0, M);
+    for (uint32_t w0 = 0; w0 < M; w0 += W) {
         uint32_t H[W];
         uint32_t P = 0xFFFFFFFFu;
 #pragma unroll
         for (int j = 0; j < W; j++) {
-            out[lane * (W + 1) + j] = min_remix_w(min(S[j], P));
+            const uint32_t w = w0 + j;
+            if (w < M) outp[(uint64_t)w * 256u] = min_remix_w(min(S[j], P));
             const uint32_t e = w0 + W + j;  // m-mer of the next block
             H[j] = 0xFFFFFFFFu;
             if (e < nh) {
-                push(code2(byte_at(e + SK_M - 1)));
+                push(code2(rd[e + SK_M - 1]));
                 H[j] = mmer_hash(mf < mr ? mf : mr);
             }
             P = min(P, H[j]);
         }
-        s_at[wid][lane] = s + w0;
-        s_n[wid][lane] = w0 < nw ? min((uint32_t)W, nw - w0) : 0u;
-        wave_sync();
-        for (uint32_t l = 0; l < 64; l++) {  // run of lane l: one contiguous store
-            const uint32_t n = s_n[wid][l];
-            if (lane < n) wbv[s_at[wid][l] + lane] = out[l * (W + 1) + lane];
-        }
-        wave_sync();
 #pragma unroll
         for (int j = 0; j < W; j++) S[j] = H[j];
 #pragma unroll
@@ -179,7 +168,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
                                                           int k, uint64_t gsize, unsigned int *hist,
                                                           uint8_t *hll_blocks, unsigned long long *npos,
                                                           unsigned int *maxlocal, unsigned int *skew,
-                                                          unsigned int *lens, const uint32_t *wbv) {
+                                                          unsigned int *lens, const uint32_t *wbv, uint32_t mbM) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
     __shared__ unsigned int h_cnt[FINE_W / 2];
     __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
@@ -224,7 +213,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
             const uint32_t hh = (uint32_t)(mix128(c) >> 32);  // as k_upsweep
             const uint32_t j = hh >> (32 - HLL_REG_BITS);
             const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
-            const uint32_t f = (MB ? wbv[s + t + 1 - k] : hh) >> (32 - FINE_W_BITS);
+            const uint32_t f = (MB ? wbv[wbv_at(r, t + 1 - (uint32_t)k, mbM)] : hh) >> (32 - FINE_W_BITS);
             atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
             if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
         }
@@ -260,7 +249,7 @@ template <bool MB>
 __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                             int k, uint64_t gsize, uint64_t ngroups, int cbits,
                                                             const unsigned long long *offs, RecW *recs,
-                                                            uint64_t read_base, const uint32_t *wbv) {
+                                                            uint64_t read_base, const uint32_t *wbv, uint32_t mbM) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
     __shared__ RecW sorted[DS_BATCH_W];
     __shared__ uint8_t sbk[DS_BATCH_W];
@@ -311,7 +300,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, 
                     const bool f = fwd < rc, pal = fwd == rc;
                     const K128 c = f ? fwd : rc;
                     uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
-                    const uint32_t pv = MB ? wbv[s + w] : (uint32_t)(mix128(c) >> 32);
+                    const uint32_t pv = MB ? wbv[wbv_at(r, w, mbM)] : (uint32_t)(mix128(c) >> 32);
                     rr[j].lo = c.lo;
                     rr[j].hi = MB ? (c.hi | ((unsigned long long)(pv >> 8) << WMB_SHIFT)) : c.hi;
                     rr[j].read = (unsigned int)(r + read_base);
