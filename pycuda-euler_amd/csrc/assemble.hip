@@ -1789,7 +1789,9 @@ int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, 
     {
         // minimizer buckets for k <= 52 (count_wide.h; EULERHIP_WIDE_MB=0: hash buckets)
         bool declined = false;
-        const bool mb = k <= WMB_MAX_K && kn().wide_mb == 1;  // (opt-in until config 5 runs on it)
+        // (config-5 rank shape: 141 ms a step against 169 ms on mix128 buckets --
+        // profiles/r04_l_config5_rank_shape_minimizer_buckets.json)
+        const bool mb = k <= WMB_MAX_K && kn().wide_mb != 0;
         EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok, mb, &declined));
         if (declined) EC_CHECK(phase_count_wpart(s, d_reads, d_off, nreads, read_base, k, limit, U, sidx, ok));
     }
