@@ -215,6 +215,7 @@ struct ec_session {
     // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
     DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr, rt_coop;
     DevBuf wbv;  // count_wide.h minimizer buckets: every window's minimizer
+    DevBuf skrej;  // k_skbucket_filtd: records its record tables had no room for
     unsigned int coop_grid = 0;  // blocks of the cooperative ranking launch (all resident)
     // multi-GPU partitioned finish (ec_graph_chains_part ..): this rank's segment of oriented nodes
     uint64_t seg_n0 = 0, seg_n1 = 0;
@@ -688,10 +689,21 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         // (the table takes up to 2047 keys; the prediction runs ~10 % high.  ecoli10m_err's
         // fullest bucket: 1525 predicted, 1485 inserted)
         const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 1900u;
-        if (k & 1)
-            k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
-        else
-            k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
+        if (kn().skf_dedup == 0) {  // (A/B: every record occurrence rolled out twice)
+            if (k & 1)
+                k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
+            else
+                k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
+        } else {  // rejected records (no room in the record table) in a scratch array laid out as recs2
+            EC_CHECK(s->skrej.ensure(Bk * fcap * 16));
+            uint4 *rej = s->skrej.as<uint4>();
+            if (k & 1)
+                k_skbucket_filtd<2048, 2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, rej,
+                                                                                      dbg);
+            else
+                k_skbucket_filtd<2048, 2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, rej,
+                                                                                     dbg);
+        }
     } else if (plan.slots == 1024) {
         constexpr int NT3 = 512;
         const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
@@ -716,9 +728,8 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         if (skfilt)
             fprintf(stderr, "k_skbucket_filt: %llu buckets: max distinct est %llu, max predicted inserts %llu, max "
                             "seen-twice cells %llu, max records %llu; refused by the predictor %llu, tables filled "
-                            "%llu, most keys inserted %llu (max_keys %u)\n",
-                    (unsigned long long)Bk, h[0], h[1], h[2], h[3], h[4], h[5], h[6],
-                    kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 2048u * 72 / 100);
+                            "%llu, most keys inserted %llu; most merged records %llu, most rejected %llu\n",
+                    (unsigned long long)Bk, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
         if (plan.slots == 1024)
             fprintf(stderr, "k_skbucket3: %llu buckets, most distinct records in a bucket %llu\n",
                     (unsigned long long)Bk, h[3]);
@@ -3111,7 +3122,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv};
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv, &s->skrej};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->h_coff.release();

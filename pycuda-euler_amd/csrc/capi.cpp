@@ -54,6 +54,7 @@ void refresh_knobs() {
         k.wide_mb = num("EULERHIP_WIDE_MB", -1);
         k.join_mb = num("EULERHIP_JOIN_MB", -1);
         k.sruler_mask = num("EULERHIP_SRULER_MASK", 0);
+        k.skf_dedup = num("EULERHIP_SKF_DEDUP", -1);
     }
     g_knobs = k;
 }
