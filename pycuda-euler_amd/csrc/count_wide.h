@@ -289,9 +289,25 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, 
         if (m)
             for (; t < (uint32_t)(k - 1); t++) roll_w(fwd, rc, code2(stage[rel + t]), mask, sh);
         const uint32_t m2 = 2 * m - 1;
+        // MB: the round's minimizers are loaded one round ahead (a load per window right
+        // before its use exposed its latency four times a round)
+        uint32_t pvn[DS_RW];
+        if (MB) {
+#pragma unroll
+            for (int j = 0; j < DS_RW; j++) pvn[j] = (uint32_t)j < m ? wbv[wbv_at(r, j, mbM)] : 0u;
+        }
         for (unsigned int round = 0; round < nrounds; round++) {
             RecW rr[DS_RW];
             unsigned int cb[DS_RW], rk[DS_RW];
+            uint32_t pvc[DS_RW];
+            if (MB) {
+#pragma unroll
+                for (int j = 0; j < DS_RW; j++) {
+                    pvc[j] = pvn[j];
+                    const uint32_t wn = w + DS_RW + j;
+                    pvn[j] = wn < m ? wbv[wbv_at(r, wn, mbM)] : 0u;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < DS_RW; j++) {
                 cb[j] = 0xFFFFFFFFu;
@@ -300,7 +316,7 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, 
                     const bool f = fwd < rc, pal = fwd == rc;
                     const K128 c = f ? fwd : rc;
                     uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
-                    const uint32_t pv = MB ? wbv[wbv_at(r, w, mbM)] : (uint32_t)(mix128(c) >> 32);
+                    const uint32_t pv = MB ? pvc[j] : (uint32_t)(mix128(c) >> 32);
                     rr[j].lo = c.lo;
                     rr[j].hi = MB ? (c.hi | ((unsigned long long)(pv >> 8) << WMB_SHIFT)) : c.hi;
                     rr[j].read = (unsigned int)(r + read_base);
