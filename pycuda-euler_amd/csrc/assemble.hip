@@ -689,7 +689,10 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         // (the table takes up to 2047 keys; the prediction runs ~10 % high.  ecoli10m_err's
         // fullest bucket: 1525 predicted, 1485 inserted)
         const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 1900u;
-        if (kn().skf_dedup == 0) {  // (A/B: every record occurrence rolled out twice)
+        // (measured on ecoli10m_err: the record merge filled its 1535-entry tables -- up to 915
+        // records a bucket rejected -- and its 131 KB of LDS held one workgroup per CU: compact
+        // 8.26 ms against 7.75 without it; opt-in, EULERHIP_SKF_DEDUP=1)
+        if (kn().skf_dedup != 1) {
             if (k & 1)
                 k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
             else
