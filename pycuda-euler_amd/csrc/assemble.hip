@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <climits>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -138,6 +139,25 @@ struct ec_session {
     int k = 0;
     ec_stats stats{};
     HostBuf h_chars;
+    // small device -> host reads (scalars, counts) go through this page-locked bounce buffer and
+    // are delivered by host_sync: a pageable destination cost ~11 us more per round trip
+    // (tools/micro/sync_lat.hip on MI355X: 27.2 vs 16.3 us), and a step has ~6 of them
+    HostBuf bounce;
+    struct Pend {
+        void *dst;
+        size_t off, n;
+    };
+    std::vector<Pend> pend;
+    size_t bused = 0;
+    hipEvent_t rd_ev = nullptr;  // host_wait: a read-back's event (created on first use)
+    // count_sk2's refine plan of the previous call: launched speculatively on the next call of
+    // the same shape while the host reads the partition's scalars back (phase_count_sk2)
+    struct SkSpec {
+        bool valid = false;
+        uint64_t G = 0, cap = 0, nreads = 0, read_base = 0, fcap = 0;
+        uint32_t M = 0;
+        int k = 0, bbits = 0;
+    } skspec;
     PinnedVec<uint64_t> h_coff;  // result readbacks land in pinned host memory
     PinnedVec<uint64_t> h_loff;
     PinnedVec<int64_t> h_links;
@@ -222,6 +242,52 @@ struct ec_session {
     unsigned int seg_nc = 0;     // contigs of the job (ec_graph_layout)
     uint64_t seg_nchars = 0;
 };
+
+namespace {
+constexpr size_t BOUNCE_CAP = 64 << 10, BOUNCE_MAX = 16 << 10;  // bytes; larger reads go direct
+
+// queue a device -> host copy of n bytes to dst on st; dst is valid after host_sync(s, st)
+int d2h(ec_session *s, void *dst, const void *src, size_t n, hipStream_t st) {
+    if (!n) return EC_OK;
+    const size_t off = (s->bused + 15) & ~size_t(15);
+    if (n > BOUNCE_MAX || off + n > BOUNCE_CAP) {
+        EC_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
+        return EC_OK;
+    }
+    if (!s->bounce.p) EC_CHECK(s->bounce.resize(BOUNCE_CAP));
+    EC_HIP(hipMemcpyAsync(s->bounce.p + off, src, n, hipMemcpyDeviceToHost, st));
+    s->pend.push_back({dst, off, n});
+    s->bused = off + n;
+    return EC_OK;
+}
+
+// wait for event ev (recorded after the d2h copies), then deliver the queued d2h reads: the
+// stream may run on past it
+int host_wait(ec_session *s, hipEvent_t ev) {
+    const hipError_t e = hipEventSynchronize(ev);
+    for (const auto &q : s->pend) std::memcpy(q.dst, s->bounce.p + q.off, q.n);
+    s->pend.clear();
+    s->bused = 0;
+    if (e != hipSuccess) {
+        set_error("HIP error %s", hipGetErrorString(e));
+        return EC_ERR_HIP;
+    }
+    return EC_OK;
+}
+
+// wait for st, then deliver the queued d2h reads
+int host_sync(ec_session *s, hipStream_t st) {
+    const hipError_t e = hipStreamSynchronize(st);
+    for (const auto &q : s->pend) std::memcpy(q.dst, s->bounce.p + q.off, q.n);
+    s->pend.clear();
+    s->bused = 0;
+    if (e != hipSuccess) {
+        set_error("HIP error %s", hipGetErrorString(e));
+        return EC_ERR_HIP;
+    }
+    return EC_OK;
+}
+}  // namespace
 
 namespace ec {
 
@@ -596,8 +662,45 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));
     k_hll_merge<<<dim3((1 << HLL_REG_BITS) / 256, TOT_SLICES), 256, 0, st>>>(s->hll.as<uint8_t>(), G, hreg);
     k_hll_final<<<1, 1024, 0, st>>>(hreg, HLL_REG_BITS, &dsc->est);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    // ---- refine into fixed-capacity final buckets (launched below, or here on speculation) ----
+    // a bucket gathers whole minimizers (each ~coverage records): ~13 % spread at the headline
+    // size (62 minimizers a bucket), so twice the mean: fcap = 2 NR / buckets + 1024
+    auto launch_refine = [&](int bb, uint64_t fc) -> int {
+        const uint64_t nb = 1ull << bb;
+        EC_CHECK(s->recs2.ensure(nb * fc * 16));
+        EC_CHECK(s->fcur.ensure(nb * 8));
+        EC_CHECK(s->bb2.ensure(nb * 16));
+        EC_HIP(hipMemsetAsync(s->fcur.p, 0, nb * 8, st));
+        unsigned rs = 8;
+        if (kn().refine_rs) rs = (unsigned)std::max(1, kn().refine_rs);
+        rs = (unsigned)std::min<uint64_t>(rs, G);
+        kmark(s, 4, 0);
+        k_skrefine<<<dim3((unsigned)C, rs), BUCKET_THREADS, 0, st>>>(recs, s->cnt.as<unsigned int>(), (uint32_t)G, cap,
+                                                                      bb, s->recs2.as<uint4>(), fc,
+                                                                      s->fcur.as<unsigned long long>(), &dsc->skew, M,
+                                                                      gsize, read_base);
+        kmark(s, 4, 1);
+        unsigned long long *b0 = s->bb2.as<unsigned long long>();
+        k_fixed_bounds<<<grid_for(nb, 256), 256, 0, st>>>(s->fcur.as<unsigned long long>(), nb, fc, b0, b0 + nb);
+        return EC_OK;
+    };
+    // the previous call's plan for an input of this shape (a stream of equal batches, the bench's
+    // steps) runs the refine while the host waits for the scalars -- the host's wake-up and the
+    // plan below overlap the refine instead of idling the device (~40 us a call); a plan that
+    // turns out different launches the refine again (it only writes recs2 / fcur / bb2)
+    const auto sp = s->skspec;
+    const bool spec = sp.valid && sp.G == G && sp.cap == cap && sp.nreads == nreads && sp.read_base == read_base &&
+                      sp.M == M && sp.k == k && !chunked && kn().no_spec == 0;
+    s->skspec.valid = false;
+    if (spec) {
+        if (!s->rd_ev) EC_HIP(hipEventCreateWithFlags(&s->rd_ev, hipEventDisableTiming));
+        EC_HIP(hipEventRecord(s->rd_ev, st));
+        EC_CHECK(launch_refine(sp.bbits, sp.fcap));
+        EC_CHECK(host_wait(s, s->rd_ev));
+    } else {
+        EC_CHECK(host_sync(s, st));
+    }
     const bool verbose = kn().verbose;
     if (validate) {
         if (hsc.lens[2]) {  // a read of another length, a byte outside ACGT, an oversized tile
@@ -637,26 +740,24 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     plan.slots = skfilt ? 2048u : b3 ? 1024u : est / (double)(1ull << bbits) > 1100.0 ? 4096u : 2048u;
     const uint64_t Bk = 1ull << bbits;
     const uint64_t NR = hsc.nrec;
-
-    // ---- refine into fixed-capacity final buckets -------------------------------------------
-    // a bucket gathers whole minimizers (each ~coverage records): ~13 % spread at the headline
-    // size (62 minimizers a bucket), so twice the mean
-    const uint64_t fcap = NR * 2 / Bk + 1024;
-    EC_CHECK(s->recs2.ensure(Bk * fcap * 16));
-    EC_CHECK(s->fcur.ensure(Bk * 8));
-    EC_CHECK(s->bb2.ensure(Bk * 16));
-    EC_HIP(hipMemsetAsync(s->fcur.p, 0, Bk * 8, st));
-    unsigned rs = 8;
-    if (kn().refine_rs) rs = (unsigned)std::max(1, kn().refine_rs);
-    rs = (unsigned)std::min<uint64_t>(rs, G);
-    kmark(s, 4, 0);
-    k_skrefine<<<dim3((unsigned)C, rs), BUCKET_THREADS, 0, st>>>(recs, s->cnt.as<unsigned int>(), (uint32_t)G, cap, bbits,
-                                                                  s->recs2.as<uint4>(), fcap,
-                                                                  s->fcur.as<unsigned long long>(), &dsc->skew, M,
-                                                                  gsize, read_base);
-    kmark(s, 4, 1);
+    uint64_t fcap = NR * 2 / Bk + 1024;
+    if (spec && sp.bbits == bbits && sp.fcap >= fcap && sp.fcap <= fcap + fcap / 8) {
+        fcap = sp.fcap;  // the speculative refine stands
+    } else {
+        if (spec && verbose) fprintf(stderr, "count_sk2: refine plan changed (bits %d -> %d), refined again\n", sp.bbits, bbits);
+        fcap += fcap / 16;  // (headroom: the next call of this shape keeps the plan)
+        EC_CHECK(launch_refine(bbits, fcap));
+    }
+    s->skspec.valid = true;
+    s->skspec.G = G;
+    s->skspec.cap = cap;
+    s->skspec.nreads = nreads;
+    s->skspec.read_base = read_base;
+    s->skspec.fcap = fcap;
+    s->skspec.M = M;
+    s->skspec.k = k;
+    s->skspec.bbits = bbits;
     unsigned long long *bbeg = s->bb2.as<unsigned long long>(), *bend = bbeg + Bk;
-    k_fixed_bounds<<<grid_for(Bk, 256), 256, 0, st>>>(s->fcur.as<unsigned long long>(), Bk, fcap, bbeg, bend);
     mark(s, 2 * EC_STAGE_COUNT + 1);
 
     // ---- super-k-mers -> bucket tables ----------------------------------------------------------
@@ -725,8 +826,8 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
 #undef EC_SKBUCKET_ARGS
     if (dbg) {
         unsigned long long h[16];
-        EC_HIP(hipMemcpyAsync(h, dbg, 128, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, h, dbg, 128, st));
+        EC_CHECK(host_sync(s, st));
         const double nw = (double)Bk * (BUCKET_THREADS / 64);  // waves
         if (skfilt)
             fprintf(stderr, "k_skbucket_filt: %llu buckets: max distinct est %llu, max predicted inserts %llu, max "
@@ -746,8 +847,8 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     }
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.overflow || hsc.skew) {  // a final bucket or an LDS table overflowed
         if (verbose)
             fprintf(stderr, "count_sk2: %s overflow (%llu buckets, %u slots, est %.0f, fcap %llu)\n",
@@ -809,8 +910,8 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
             L = s->pipe.first_len;  // host input: the host knows it
         } else if (!(L >= (uint64_t)k && npf_of(L) && s->lc_off == d_off && s->lc_n == nreads)) {
             uint64_t o2[2] = {0, 0};
-            EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
-            EC_HIP(hipStreamSynchronize(st));
+            EC_CHECK(d2h(s, o2, d_off, 16, st));
+            EC_CHECK(host_sync(s, st));
             L = o2[1] - o2[0];
         }
         s->lc_L = 0;  // cached again below only once the partition has validated it
@@ -836,8 +937,8 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     k_prescan<<<(unsigned)G, 256, 0, st>>>(d_reads, d_off, nreads, k, gsize, &dsc->npos, &dsc->bad, dsc->lens);
     kmark(s, 0, 1);
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.bad != ~0ull) {
         uint8_t byte = 0;
         hipMemcpy(&byte, d_reads + hsc.bad, 1, hipMemcpyDeviceToHost);
@@ -913,8 +1014,8 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     EC_HIP(hipMemsetAsync(hreg, 0, (1 << HLL_REG_BITS) * 4, st));
     k_hll_merge<<<dim3((1 << HLL_REG_BITS) / 256, TOT_SLICES), 256, 0, st>>>(s->hll.as<uint8_t>(), G, hreg);
     k_hll_final<<<1, 1024, 0, st>>>(hreg, HLL_REG_BITS, &dsc->est);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.overflow) return EC_OK;  // a run outgrew its capacity (extreme skew)
     const double est = hsc.est * (smask + 1.0);
     BucketPlan plan = plan_buckets(est, limit, !kn().no_filter);
@@ -987,8 +1088,8 @@ int phase_count_v2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off,
     EC_CHECK(rc);
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.overflow || hsc.skew) {  // a final bucket or an LDS table overflowed: redo on the exact path
         EC_HIP(hipMemsetAsync(dsc, 0, sizeof(Scalars), st));
         EC_HIP(hipMemsetAsync(&dsc->bad, 0xFF, sizeof(unsigned long long), st));
@@ -1071,8 +1172,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
                                         HLL_REG_BITS, &dsc->est);
     }
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.bad != ~0ull) {
         uint8_t byte = 0;
         hipMemcpy(&byte, d_reads + hsc.bad, 1, hipMemcpyDeviceToHost);
@@ -1218,8 +1319,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         s->filt = false;
         kmark(s, 2, 1);
         mark(s, 2 * EC_STAGE_COMPACT + 1);
-        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+        EC_CHECK(host_sync(s, st));
         if (hsc.overflow) {  // a bucket outgrew its LDS table: redo on the general path
             part = false;
             s->stats.table_retries++;
@@ -1254,8 +1355,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
                                                           &dsc->overflow, read_base);
             kmark(s, 3, 1);
             mark(s, 2 * EC_STAGE_COUNT + 1);
-            EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
-            EC_HIP(hipStreamSynchronize(st));
+            EC_CHECK(d2h(s, &hsc.overflow, &dsc->overflow, 4, st));
+            EC_CHECK(host_sync(s, st));
             if (!hsc.overflow) break;
             if (attempt >= 4) {
                 set_error("hash table overflow at capacity %llu", (unsigned long long)cap);
@@ -1273,8 +1374,8 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
         EC_CHECK(s->dft.ensure(umax * 8));
         EC_CHECK(compact_table(s, s->table.as<Slot>(), cap, (long long)limit, s->dkey.as<unsigned long long>()));
         mark(s, 2 * EC_STAGE_COMPACT + 1);
-        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+        EC_CHECK(host_sync(s, st));
         sidx.table = s->table.as<Slot>();
         sidx.capmask = cap - 1;
         s->stats.count_path = EC_PATH_GENERAL;
@@ -1361,8 +1462,8 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     }
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.overflow) {
         s->stats.table_retries++;
         EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
@@ -1409,8 +1510,8 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
         EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
         if (n) k_merge_agg<<<grid_for(n, B), B, 0, st>>>(d_agg, n, s->table.as<Slot>(), cap - 1, &dsc->overflow);
         mark(s, 2 * EC_STAGE_COUNT + 1);
-        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc.overflow, &dsc->overflow, 4, st));
+        EC_CHECK(host_sync(s, st));
         if (!hsc.overflow) break;
         if (attempt >= 4) {
             set_error("merge table overflow at capacity %llu", (unsigned long long)cap);
@@ -1429,8 +1530,8 @@ int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, un
     EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
     EC_CHECK(compact_table(s, s->table.as<Slot>(), cap, limit, s->dkey.as<unsigned long long>()));
     mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     U = hsc.nsolid;
     s->stats.n_distinct = hsc.ndistinct;
     s->stats.n_solid = U;
@@ -1495,8 +1596,8 @@ int phase_load_det_w(ec_session *s, const AggW *d_agg, uint64_t n, unsigned int 
         k_det_count<AggW><<<nblk, 256, 0, st>>>(d_agg, n, bc);
         EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
         k_det_ids<AggW><<<nblk, 256, 0, st>>>(d_agg, n, bs, ids);
-        EC_HIP(hipMemcpyAsync(&tot, bs + nblk - 1, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &tot, bs + nblk - 1, 4, st));
+        EC_CHECK(host_sync(s, st));
     }
     EC_CHECK(s->dkey.ensure(std::max<uint64_t>(tot, 1) * sizeof(K128)));
     EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(tot, 1) * 4));
@@ -1515,8 +1616,8 @@ int phase_load_det_w(ec_session *s, const AggW *d_agg, uint64_t n, unsigned int 
                                                       s->dft.as<unsigned long long>(), &dsc->overflow);
         mark(s, 2 * EC_STAGE_COUNT + 1);
         unsigned int of = 0;
-        EC_HIP(hipMemcpyAsync(&of, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &of, &dsc->overflow, 4, st));
+        EC_CHECK(host_sync(s, st));
         if (!of) break;
         if (attempt >= 4) {
             set_error("load table overflow at capacity %llu", (unsigned long long)cap);
@@ -1549,8 +1650,8 @@ int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, S
     EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
     EC_CHECK(compact_table(s, s->table.as<SlotW>(), cap, limit, s->dkey.as<K128>()));
     mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     U = hsc.nsolid;
     s->stats.n_distinct = hsc.ndistinct;
     s->stats.n_solid = U;
@@ -1599,8 +1700,8 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     uint32_t mbM = 0;
     if (mb) {  // reads of one length L <= WMB_MAXL only (k_wbv checks the others)
         uint64_t o2[2] = {0, 0};
-        EC_HIP(hipMemcpyAsync(o2, d_off, 16, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, o2, d_off, 16, st));
+        EC_CHECK(host_sync(s, st));
         const uint64_t L = o2[1] - o2[0];
         if (L < (uint64_t)k || L > WMB_MAXL) {
             if (mb_declined) *mb_declined = true;
@@ -1638,8 +1739,8 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), ngroups, ftot, reinterpret_cast<unsigned int *>(ftot + FINE_W));
     k_hll_final<<<1, 1024, 0, st>>>(reinterpret_cast<unsigned int *>(ftot + FINE_W), HLL_REG_BITS, &dsc->est);
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     const uint64_t P = hsc.npos;
     const double est = hsc.est;
     // Up to 2^FINE_W_BITS buckets of <= 1100 estimated keys in 3328-slot tables (156 KB: one
@@ -1763,8 +1864,8 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
 #undef EC_BUCKET_W
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.overflow) {  // a bucket outgrew its LDS table: the caller counts on the HBM table
         if (kn().verbose)
             fprintf(stderr, "count_wpart: %u tables overflowed (%llu tables of %u slots, sbits %d, mb %d)\n",
@@ -1824,8 +1925,8 @@ int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, 
         k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<unsigned int>(), HLL_BITS, &dsc->est);
     }
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     if (hsc.bad != ~0ull) {
         uint8_t byte = 0;
         hipMemcpy(&byte, d_reads + hsc.bad, 1, hipMemcpyDeviceToHost);
@@ -1851,8 +1952,8 @@ int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, 
             kmark(s, 3, 1);
         }
         mark(s, 2 * EC_STAGE_COUNT + 1);
-        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc.overflow, &dsc->overflow, 4, st));
+        EC_CHECK(host_sync(s, st));
         if (!hsc.overflow) break;
         if (attempt >= 4) {
             set_error("hash table overflow at capacity %llu", (unsigned long long)cap);
@@ -1878,8 +1979,8 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
         EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
         if (n) k_merge_agg_w<<<grid_for(n, B), B, 0, st>>>(d_agg, n, s->table.as<SlotW>(), cap - 1, &dsc->overflow);
         mark(s, 2 * EC_STAGE_COUNT + 1);
-        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc.overflow, &dsc->overflow, 4, st));
+        EC_CHECK(host_sync(s, st));
         if (!hsc.overflow) break;
         if (attempt >= 4) {
             set_error("merge table overflow at capacity %llu", (unsigned long long)cap);
@@ -2004,7 +2105,7 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
 // weighted ruling set; per chain its path key / rank (rt_pks / rt_rks), paths' and cycles'
 // length / min first event at their key nodes (PL / PM)
 int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr, int &rounds,
-                const unsigned long long *dM = nullptr, bool defer = false) {
+                const unsigned long long *dM = nullptr, bool defer = false, bool pre_init = false) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -2045,8 +2146,8 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
         rounds = 63;  // (the callers' convergence flag: active[62])
         nr = 0;
         if (defer) return EC_OK;  // (coop_bad / coop_nr checked with the caller's next scalar read)
-        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+        EC_CHECK(host_sync(s, st));
         if (hsc.coop_bad) {
             set_error("ruling set left chains unvisited (%u chains)", M);
             return EC_ERR_STATE;
@@ -2054,11 +2155,13 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
         nr = hsc.coop_nr;
         return EC_OK;
     }
-    EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
+    if (!pre_init) EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));  // (pre_init: k_tile_compact did these)
     k_super_link<<<grid_for(M, B), B, 0, st>>>(srec, M, SIDX, snrec, s->rt_hasp.as<uint8_t>());
-    EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
-    EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
-    EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
+    if (!pre_init) {
+        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
+        EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
+        EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
+    }
     unsigned int masks[4] = {15u, 3u, 1u, 0u};
     if (kn().sruler_mask > 0) masks[0] = (unsigned int)kn().sruler_mask;  // (A/B: first-pass ruler density)
     unsigned int r0 = 0;
@@ -2072,8 +2175,8 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
         k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
         k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), r0, &dsc->nr, masks[it], s->rid.as<uint2>(),
                                      s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
-        EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+        EC_CHECK(host_sync(s, st));
         r0 = hsc.nr;
         if (hsc.nvisited >= M) break;
     }
@@ -2113,8 +2216,8 @@ int x_cut(ec_session *s, unsigned int U, unsigned int &nx) {
     EC_HIP(hipMemsetAsync(&dsc->nasym, 0, 16, st));  // nasym, nxl, nxs, xbad
     k_x_asym<<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N, &dsc->nasym);
     unsigned int nasym = 0;
-    EC_HIP(hipMemcpyAsync(&nasym, &dsc->nasym, 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &nasym, &dsc->nasym, 4, st));
+    EC_CHECK(host_sync(s, st));
     if (kn().verbose) fprintf(stderr, "extended: %u one-way links among %u nodes\n", nasym, N);
     if (!nasym) return EC_OK;
     EC_CHECK(s->x_par.ensure((size_t)U * 4));
@@ -2137,8 +2240,8 @@ int x_cut(ec_session *s, unsigned int U, unsigned int &nx) {
                                          s->succ.as<unsigned int>(), s->x_succ.as<unsigned int>(),
                                          s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
                                          s->x_lk.as<unsigned long long>(), s->x_lv.as<unsigned int>(), &dsc->nxl);
-    EC_HIP(hipMemcpyAsync(&nx, &dsc->nxl, 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &nx, &dsc->nxl, 4, st));
+    EC_CHECK(host_sync(s, st));
     if (kn().verbose) fprintf(stderr, "extended: %u one-way links, %u dict entries in their components\n", nasym, nx);
     // (component, first event) order: by event, then stably by component root
     EC_CHECK(sort_pairs(s, s->x_lk.as<unsigned long long>(), s->x_lk2.as<unsigned long long>(), s->x_lv.as<unsigned int>(),
@@ -2263,7 +2366,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);  // (dead before the Wyllie rounds)
         static_assert(sizeof(SuperRec) == sizeof(RJump), "tile scratch in the ruler state buffer");
         unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
-        EC_HIP(hipMemsetAsync(tcnt + ntiles, 0, 8, st));
+        EC_CHECK(s->rt_hasp.ensure(Nn));  // (sized here: k_tile_compact initialises it for rank_supers)
         k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
                                                 s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), LH,
                                                 LR, tcnt, scratch, s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
@@ -2276,17 +2379,25 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         // (measured: the cooperative launch took the headline's rank stage 0.63 -> 3.3 ms, its
         // grid barriers far slower than the launches they replace -- opt-in only)
         const bool coop = kn().rank_coop == 1;
-        if (!coop) {
-            unsigned long long M64 = 0;
-            EC_HIP(hipMemcpyAsync(&M64, tbase + ntiles, 8, hipMemcpyDeviceToHost, st));
-            EC_HIP(hipStreamSynchronize(st));
-            M = (unsigned int)M64;
-        }
         coop_deferred = coop;
-        if (coop || M) {
+        if (coop) {
             k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
                                                    s->rt_sidx.as<unsigned int>());
-            EC_CHECK(rank_supers(s, M, N, nr, rounds, coop ? tbase + ntiles : nullptr, coop));
+        } else {
+            // the chain count read back while k_tile_compact (sized by the tiles, not by M) runs:
+            // the host's wake-up and next launches overlap the compaction
+            unsigned long long M64 = 0;
+            if (!s->rd_ev) EC_HIP(hipEventCreateWithFlags(&s->rd_ev, hipEventDisableTiming));
+            EC_CHECK(d2h(s, &M64, tbase + ntiles, 8, st));
+            EC_HIP(hipEventRecord(s->rd_ev, st));
+            k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
+                                                   s->rt_sidx.as<unsigned int>(), s->rt_hasp.as<uint8_t>(),
+                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited);
+            EC_CHECK(host_wait(s, s->rd_ev));
+            M = (unsigned int)M64;
+        }
+        if (coop || M) {
+            EC_CHECK(rank_supers(s, M, N, nr, rounds, coop ? tbase + ntiles : nullptr, coop, !coop));
             // (3) every node: its chain's key and rank + its offset in the chain
             k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
@@ -2312,8 +2423,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             k_walk<<<2048, B, 0, st>>>(s->nrec.as<NodeRec>(), s->rlist.as<unsigned int>(), r0, &dsc->nr,
                                       masks[it], s->rid.as<uint2>(),
                                       s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
-            EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-            EC_HIP(hipStreamSynchronize(st));
+            EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+            EC_CHECK(host_sync(s, st));
             r0 = hsc.nr;
             if (hsc.nvisited + hsc.npal >= N) break;
         }
@@ -2370,8 +2481,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                            s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>());
         EC_HIP(hipMemcpyAsync(&dsc->nstarts, bs + nblk - 1, 4, hipMemcpyDeviceToDevice, st));
     }
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));  // nstarts, active[]
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));  // nstarts, active[]
+    EC_CHECK(host_sync(s, st));
     if (coop_deferred) {
         if (hsc.coop_bad) {
             set_error("ruling set left chains unvisited");
@@ -2404,8 +2515,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             s->svals.as<unsigned int>() + nc, s->x_len.as<unsigned int>(), s->x_m.as<unsigned int>(), &dsc->nxs,
             &dsc->xbad);
         unsigned int xs[2] = {0, 0};
-        EC_HIP(hipMemcpyAsync(xs, &dsc->nxs, 8, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, xs, &dsc->nxs, 8, st));
+        EC_CHECK(host_sync(s, st));
         if (xs[1]) {
             set_error("a contig walk enters a cycle without its start: the reference's get_contig_forward "
                       "(referenceAssembler.py:59-77) never returns on this input");
@@ -2435,13 +2546,13 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     // sized for the bound 2U + nc (k - 1) (a walk covers at most its path; a self-twin path's
     // nodes are up to twice its canonical k-mers)
     EC_CHECK(s->h_coff.resize(nc + 1));
-    EC_HIP(hipMemcpyAsync(&s->h_coff[nc], s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
+    EC_CHECK(d2h(s, &s->h_coff[nc], s->coff.as<unsigned long long>() + nc, 8, st));
     mark(s, 2 * EC_STAGE_STARTS + 1);
     uint64_t chars_bound = 2ull * U + (uint64_t)nc * (uint64_t)(k - 1);
     if (nx) {  // emulated contigs may overlap: the bound is their exact total
         unsigned long long tot = 0;
-        EC_HIP(hipMemcpyAsync(&tot, s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &tot, s->coff.as<unsigned long long>() + nc, 8, st));
+        EC_CHECK(host_sync(s, st));
         chars_bound = std::max<uint64_t>(chars_bound, tot);
     }
 
@@ -2496,18 +2607,18 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     const unsigned int n2 = 2 * nc;
     EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
     s->h_loff[n2] = 0;
-    if (nc) EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, (size_t)nc * 8, hipMemcpyDeviceToHost, st));
+    if (nc) EC_CHECK(d2h(s, s->h_coff.data(), s->coff.p, (size_t)nc * 8, st));
     else s->h_coff[0] = 0;
     if (nc) {
         EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));   // per-side counts as u64 (starts sorted)
         EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));  // their exclusive scan = link offsets
         k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
-        EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, st));
+        EC_CHECK(d2h(s, s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, st));
     }
     unsigned int emit_bad = 0;
-    EC_HIP(hipMemcpyAsync(&emit_bad, &dsc->skew, 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));  // h_coff[nc] (the characters), h_loff
+    EC_CHECK(d2h(s, &emit_bad, &dsc->skew, 4, st));
+    EC_CHECK(host_sync(s, st));  // h_coff[nc] (the characters), h_loff
     const uint64_t nchars = s->h_coff[nc];
     if (emit_bad) {
         set_error("contig characters past their bound %llu (inconsistent ranking)", (unsigned long long)chars_bound);
@@ -2520,7 +2631,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         return EC_ERR_STATE;
     }
     EC_CHECK(s->h_chars.resize(nchars));
-    if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), s->chars.p, nchars, hipMemcpyDeviceToHost, st));
+    if (nchars) EC_CHECK(d2h(s, s->h_chars.data(), s->chars.p, nchars, st));
     const uint64_t nlinks = s->h_loff[n2];
     EC_CHECK(s->h_links.resize(nlinks));
     if (nlinks) {
@@ -2528,9 +2639,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_links_compact<<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
                                                       s->skeys2.as<unsigned long long>(), n2,
                                                       s->dcounts.as<long long>());
-        EC_HIP(hipMemcpyAsync(s->h_links.data(), s->dcounts.p, nlinks * 8, hipMemcpyDeviceToHost, st));
+        EC_CHECK(d2h(s, s->h_links.data(), s->dcounts.p, nlinks * 8, st));
     }
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(host_sync(s, st));
     s->stats.n_links = nlinks;
 
     s->stats.n_dict = 2ull * U - hsc.npal;  // len(build()): palindromes have one entry
@@ -2579,7 +2690,7 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
     EC_CHECK(s->st1.ensure(std::max<size_t>((size_t)ntiles * RT_TN, 1) * sizeof(SuperRec)));
     unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
     SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);
-    EC_HIP(hipMemsetAsync(tcnt + ntiles, 0, 8, st));
+    if (!ntiles) EC_HIP(hipMemsetAsync(tcnt, 0, 8, st));  // (k_tile_chains zeroes tcnt[ntiles])
     if (ntiles)
         k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), n1,
                                                 s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
@@ -2588,10 +2699,10 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
                                                 s->PL.as<unsigned int>(), s->PM.as<unsigned long long>(), n0);
     EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
     unsigned long long M = 0;
-    EC_HIP(hipMemcpyAsync(&M, tbase + ntiles, 8, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &M, tbase + ntiles, 8, st));
+    EC_CHECK(host_sync(s, st));
     if (M) k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, d_super, s->rt_sidx.as<unsigned int>());
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(host_sync(s, st));
     *n_super = M;
     s->seg_n0 = n0;
     s->seg_n1 = n1;
@@ -2613,8 +2724,8 @@ int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
     EC_CHECK(rank_supers(s, (unsigned int)M, N, nr, rounds));
     s->stats.n_rulers = nr;
     unsigned int act = 0;
-    EC_HIP(hipMemcpyAsync(&act, &dsc->active[rounds - 1], 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &act, &dsc->active[rounds - 1], 4, st));
+    EC_CHECK(host_sync(s, st));
     if (act) {
         set_error("chain list ranking did not converge in %d rounds", rounds);
         return EC_ERR_STATE;
@@ -2651,14 +2762,14 @@ int part_starts(ec_session *s, bool have_supers, StartRec *d_starts, uint64_t *n
                                        s->PM.as<unsigned long long>(), n1, bs, s->cand.as<unsigned long long>(),
                                        s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(), n0);
     unsigned int cnt = 0;
-    EC_HIP(hipMemcpyAsync(&cnt, bs + nblk - 1, 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &cnt, bs + nblk - 1, 4, st));
+    EC_CHECK(host_sync(s, st));
     if (cnt)
         k_start_recs<<<grid_for(cnt, B), B, 0, st>>>(s->svals.as<unsigned int>(), cnt, s->upal.as<uint8_t>(),
                                                      s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
                                                      s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
                                                      s->PL.as<unsigned int>(), s->k, d_starts);
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(host_sync(s, st));
     *n_starts = cnt;
     return EC_OK;
 }
@@ -2688,8 +2799,8 @@ int part_layout(ec_session *s, const StartRec *d_all, uint64_t nc, uint64_t *n_c
     }
     EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
     unsigned long long tot = 0;
-    EC_HIP(hipMemcpyAsync(&tot, s->coff.as<unsigned long long>() + nc, 8, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &tot, s->coff.as<unsigned long long>() + nc, 8, st));
+    EC_CHECK(host_sync(s, st));
     s->seg_nc = (unsigned int)nc;
     s->seg_nchars = tot;
     *n_chars = tot;
@@ -2719,8 +2830,8 @@ int part_emit(ec_session *s, char *d_chars, uint32_t *d_ends) {
             s->tailOf.as<unsigned int>(), &dsc->skew, n0);
     if (nc) k_ends_export<<<grid_for(nc, B), B, 0, st>>>(s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), nc, d_ends);
     unsigned int bad = 0;
-    EC_HIP(hipMemcpyAsync(&bad, &dsc->skew, 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &bad, &dsc->skew, 4, st));
+    EC_CHECK(host_sync(s, st));
     if (bad) {
         set_error("contig characters past their bound %llu (inconsistent ranking)", (unsigned long long)s->seg_nchars);
         return EC_ERR_STATE;
@@ -2757,28 +2868,28 @@ int part_collect(ec_session *s, const Index &sidx, const char *d_chars, const ui
     EC_CHECK(s->h_coff.resize((size_t)nc + 1));
     EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
     s->h_loff[n2] = 0;
-    EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, ((size_t)nc + 1) * 8, hipMemcpyDeviceToHost, st));
+    EC_CHECK(d2h(s, s->h_coff.data(), s->coff.p, ((size_t)nc + 1) * 8, st));
     if (nc) {
         EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));
         EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));
         k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
-        EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, st));
+        EC_CHECK(d2h(s, s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, st));
     }
     unsigned int npal = 0;
-    EC_HIP(hipMemcpyAsync(&npal, &dsc->npal, 4, hipMemcpyDeviceToHost, st));
+    EC_CHECK(d2h(s, &npal, &dsc->npal, 4, st));
     EC_CHECK(s->h_chars.resize(nchars));
-    if (nchars) EC_HIP(hipMemcpyAsync(s->h_chars.data(), d_chars, nchars, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    if (nchars) EC_CHECK(d2h(s, s->h_chars.data(), d_chars, nchars, st));
+    EC_CHECK(host_sync(s, st));
     const uint64_t nlinks = s->h_loff[n2];
     EC_CHECK(s->h_links.resize(nlinks));
     if (nlinks) {
         EC_CHECK(s->dcounts.ensure(nlinks * 8));
         k_links_compact<<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
                                                       s->skeys2.as<unsigned long long>(), n2, s->dcounts.as<long long>());
-        EC_HIP(hipMemcpyAsync(s->h_links.data(), s->dcounts.p, nlinks * 8, hipMemcpyDeviceToHost, st));
+        EC_CHECK(d2h(s, s->h_links.data(), s->dcounts.p, nlinks * 8, st));
     }
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(host_sync(s, st));
     s->stats.n_solid = U;
     s->stats.n_contigs = nc;
     s->stats.n_contig_chars = nchars;
@@ -2858,8 +2969,8 @@ int assemble_extended(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_HIP(hipMemsetAsync(present, 0, 32, st));
     if (nreads) k_x_alphabet<<<grid_for(nreads, B, 4096), B, 0, st>>>(d_reads, d_off, nreads, present);
     unsigned int pm[8];
-    EC_HIP(hipMemcpyAsync(pm, present, 32, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, pm, present, 32, st));
+    EC_CHECK(host_sync(s, st));
     EC_CHECK(x_alphabet(s, pm, true, k));
     s->stats.count_variant = 0;
     s->stats.n_buckets = 0;
@@ -2878,8 +2989,8 @@ int assemble_extended(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         k_hll_final<<<1, 1024, 0, st>>>(s->hll.as<unsigned int>(), HLL_BITS, &dsc->est);
     }
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
-    EC_HIP(hipMemcpyAsync(&hsc, dsc, sizeof(Scalars), hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+    EC_CHECK(host_sync(s, st));
     const uint64_t P = nreads ? hsc.npos : 0;
     s->stats.n_positions = P;
     const double est = nreads ? hsc.est : 0.0;
@@ -2899,8 +3010,8 @@ int assemble_extended(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
             kmark(s, 3, 1);
         }
         mark(s, 2 * EC_STAGE_COUNT + 1);
-        EC_HIP(hipMemcpyAsync(&hsc.overflow, &dsc->overflow, 4, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &hsc.overflow, &dsc->overflow, 4, st));
+        EC_CHECK(host_sync(s, st));
         if (!hsc.overflow) break;
         if (attempt >= 4) {
             set_error("hash table overflow at capacity %llu", (unsigned long long)cap);
@@ -3003,7 +3114,7 @@ int assemble_piped(ec_session *s, const uint64_t *d_off, uint64_t nreads, int k,
     int rc = assemble(s, s->h_reads.as<uint8_t>(), d_off, nreads, k, limit, flags);
     if (s->pipe.done < s->pipe.nchunks) {
         pipe_all(s);
-        hipStreamSynchronize(s->stream);
+        (void)host_sync(s, s->stream);
     }
     s->pipe.active = false;
     return rc;
@@ -3104,7 +3215,7 @@ int ec_session_set_stream(ec_session *s, void *hip_stream) {
         return EC_OK;
     }
     if (s->own_stream && s->stream) {
-        hipStreamSynchronize(s->stream);
+        (void)host_sync(s, s->stream);
         hipStreamDestroy(s->stream);
     }
     s->own_stream = false;
@@ -3128,6 +3239,8 @@ int ec_session_destroy(ec_session *s) {
                      &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv, &s->skrej};
     for (auto *b : all) b->release();
     s->h_chars.release();
+    s->bounce.release();
+    s->pend.clear();
     s->h_coff.release();
     s->h_loff.release();
     s->h_links.release();
@@ -3137,6 +3250,7 @@ int ec_session_destroy(ec_session *s) {
     }
     s->p_codes.release();
     s->p_exc.release();
+    if (s->rd_ev) hipEventDestroy(s->rd_ev);
     for (auto &e : s->pipe.ev) hipEventDestroy(e);
     for (auto &sl : s->stg) {
         for (auto &e : sl.pipe.ev) hipEventDestroy(e);
@@ -3322,8 +3436,8 @@ int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts) {
                                               s->dft.as<unsigned long long>(), N, s->skeys.as<unsigned long long>(),
                                               s->svals.as<unsigned int>(), &dsc->ndict);
     unsigned int nd = 0;
-    EC_HIP(hipMemcpyAsync(&nd, &dsc->ndict, 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(d2h(s, &nd, &dsc->ndict, 4, st));
+    EC_CHECK(host_sync(s, st));
     EC_CHECK(sort_pairs(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(),
                         s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nd));
     EC_CHECK(s->dchars.ensure((size_t)nd * s->k));
@@ -3343,9 +3457,9 @@ int ec_copy_dict(ec_session *s, char *kmers, uint32_t *counts) {
         k_dict_render<Ops64><<<grid_for(nd, B), B, 0, st>>>(s->svals2.as<unsigned int>(), nd,
                                                            s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
                                                            s->k, s->dchars.as<char>(), s->dcounts.as<unsigned int>());
-    if (kmers) EC_HIP(hipMemcpyAsync(kmers, s->dchars.p, (size_t)nd * s->k, hipMemcpyDeviceToHost, st));
-    if (counts) EC_HIP(hipMemcpyAsync(counts, s->dcounts.p, (size_t)nd * 4, hipMemcpyDeviceToHost, st));
-    EC_HIP(hipStreamSynchronize(st));
+    if (kmers) EC_CHECK(d2h(s, kmers, s->dchars.p, (size_t)nd * s->k, st));
+    if (counts) EC_CHECK(d2h(s, counts, s->dcounts.p, (size_t)nd * 4, st));
+    EC_CHECK(host_sync(s, st));
     return EC_OK;
 }
 
@@ -3424,7 +3538,7 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
                 k_owner_hist<unsigned long long><<<nblk, B, 0, st>>>(s->dkey.as<unsigned long long>(), n, nowners, nblk,
                                                                     bh, own, oid);
             EC_CHECK(scan_incl_u32(s, bh, bhi, nbh));
-            EC_HIP(hipMemcpyAsync(s->own_hi.data(), bhi, nbh * 4, hipMemcpyDeviceToHost, st));
+            EC_CHECK(d2h(s, s->own_hi.data(), bhi, nbh * 4, st));
         }
     }
     if (n && d_out) {  // the scatter is queued before the host waits for the owner counts
@@ -3439,7 +3553,7 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
                 s->dft.as<unsigned long long>(), n, nowners, nblk, bhi, reinterpret_cast<Agg *>(d_out),
                 s->shard_base << 32, oid);
     }
-    EC_HIP(hipStreamSynchronize(st));
+    EC_CHECK(host_sync(s, st));
     s->own_valid = true, s->own_rule = s->owner_rule, s->own_nowners = nowners, s->own_n = n, s->own_nblk = nblk;
     unsigned long long prev = 0;
     for (int i = 0; i < nowners; i++) {
@@ -3487,7 +3601,7 @@ int ec_export_dense(ec_session *s, void *d_out) {
             k_export_dense<unsigned long long><<<grid_for(n, 256), 256, 0, s->stream>>>(
                 s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
                 s->dft.as<unsigned long long>(), n, reinterpret_cast<Agg *>(d_out), s->shard_base << 32);
-        EC_HIP(hipStreamSynchronize(s->stream));
+        EC_CHECK(host_sync(s, s->stream));
     }
     return EC_OK;
 }
@@ -3563,7 +3677,7 @@ int ec_graph_links_part(ec_session *s, uint64_t lo, uint64_t hi, uint32_t *d_suc
                 s->gidx, s->dkey.as<unsigned long long>(), (unsigned int)lo, (unsigned int)hi, s->k, d_succ);
         EC_HIP(hipGetLastError());
     }
-    EC_HIP(hipStreamSynchronize(s->stream));
+    EC_CHECK(host_sync(s, s->stream));
     return EC_OK;
 }
 
@@ -3675,8 +3789,8 @@ int ec_assemble_from_kmers(ec_session *s, const char *kmers, const uint32_t *cou
             k_kmers_to_agg<Ops64><<<grid_for(n, 256), 256, 0, st>>>(s->dchars.as<char>(), s->dcounts.as<unsigned int>(),
                                                                    n, k, s->recs2.as<Agg>(), &dsc->bad);
         unsigned long long bad = 0;
-        EC_HIP(hipMemcpyAsync(&bad, &dsc->bad, 8, hipMemcpyDeviceToHost, st));
-        EC_HIP(hipStreamSynchronize(st));
+        EC_CHECK(d2h(s, &bad, &dsc->bad, 8, st));
+        EC_CHECK(host_sync(s, st));
         if (bad != ~0ull)  // bytes other than A/C/G/T: opaque symbols (extended.h)
             return assemble_kmers_extended(s, kmers, n, k);
     }

@@ -278,21 +278,27 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
         const uint32_t nrounds = __any(has) ? (M + W - 1) / W : 0u;
         if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
         // the open run of a lane: windows [rs, w) of minimizer runv.  runv starts as window 0's
-        // value, so window 0 never closes a run; a lane without a read never closes one (has)
-        uint32_t runv = S[0], rs = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
+        // value, so window 0 never closes a run; a lane without a read never closes one (has).
+        // The run start is kept as its entry term rsx = -16320 rs (below): the close test
+        // rs == end - nmax compares it with a uniform constant and the entry needs no multiply
+        uint32_t runv = S[0], rsx = 0, cntw = 0;  // cntw: the wave's buffered entries (uniform)
         const uint64_t hasm = __builtin_amdgcn_ballot_w64(has);
         const uint32_t rtile = 64 * t;            // the tile's first read relative to g0
         // entry of the run [rs, end) closing at window end: lane | rs << 6 | (n - 1) << 14 |
-        // bucket bits << 18 with n = end - rs (fields disjoint, so a sum), the bucket bits the
-        // top 14 of min_remix(runv) = its low 14 (the shift drops the rest)
-        auto entry = [&](uint32_t end) {
-            return (runv << 18) + (lane + ((end - 1u) << 14)) + (uint32_t)__mul24((int)rs, -16320);
-        };
+        // bucket bits << 18 with n = end - rs (fields disjoint, so a sum: (end - 1) << 14 -
+        // 16320 rs), the bucket bits the top 14 of min_remix(runv) = its low 14 (the shift drops
+        // the rest)
+        auto entry = [&](uint32_t end) { return (runv << 18) + lane + (((end - 1u) << 14) + rsx); };
+        auto rs_term = [](uint32_t w) { return (uint32_t)((int)w * -16320); };
         for (uint32_t round = 0; round < nrounds; round++) {
             const uint32_t w0 = round * W;  // first window of the round
-            // bases of m-mers (round + 1) W + j: (round + 1) W + m - 1 + j
-            const uint32_t pb = rel + w0 + W + m - 1;
-            const uint32_t xb0 = sk_bases16(st, pb), xb1 = sk_bases16(st, pb + 16);
+            // m-mer (round + 1) W + j covers bases q + j .. q + j + m - 1: a0, a1 = bases q .. q + 31
+            // (W + m - 1 <= 32).  Its forward code rolls in base q + m - 1 + j; its reverse
+            // complement's code is the complement of the m bases read little-endian (base i at
+            // bits 2i), one alignbit -- no second rolling register
+            const uint32_t q = rel + w0 + W;
+            const uint32_t a0 = sk_bases16(st, q), a1 = sk_bases16(st, q + 16);
+            const uint32_t rw0 = rs_term(w0);  // (uniform: window w0 + j's term is rw0 + rs_term(j))
             uint32_t H[W];
             uint32_t P = 0xFFFFFFFFu;  // prefix minimum of the next block so far
             // one window: its minimizer v, the next block's hash j, and the run bookkeeping.  A run
@@ -300,20 +306,25 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
             // their entries (ballot rank), the others only move rs
             auto window = [&](int j) {
                 const uint32_t v = min(S[j], P);  // window w0 + j
-                push_base(j < 16 ? (xb0 >> (2 * j)) & 3u : (xb1 >> (2 * (j - 16))) & 3u);
-                H[j] = mmer_hash(mf < mr ? mf : mr);
+                const int tb = m - 1 + j;  // the rolled-in base, relative to q
+                const uint32_t b = tb < 16 ? (a0 >> (2 * tb)) & 3u : (a1 >> (2 * (tb - 16))) & 3u;
+                mf = (mf << 2) | b;  // (bits past the m-mer's 2m are dropped where it is used)
+                const uint32_t fw = mf & MMASK;
+                const uint32_t le = j == 0 ? a0 : j < 16 ? __builtin_amdgcn_alignbit(a1, a0, 2 * j) : a1 >> (2 * (j - 16));
+                const uint32_t rc = ~le & MMASK;
+                H[j] = mmer_hash(fw < rc ? fw : rc);
                 P = min(P, H[j]);
                 const uint32_t end = w0 + j;  // uniform
                 // (the mask from the compares' own ballots: a ballot of the combined bool was
                 // materialised through a VGPR)
-                const bool c1 = v != runv, c2 = rs == end - nmax;
+                const bool c1 = v != runv, c2 = rsx == rw0 + (uint32_t)((j - (int)nmax) * -16320);
                 const bool close = has & (c1 | c2);
                 const uint64_t bal = (__builtin_amdgcn_ballot_w64(c1) | __builtin_amdgcn_ballot_w64(c2)) & hasm;
                 if (close) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
                     ent[cntw + rk] = entry(end);
-                    rs = end;
+                    rsx = rw0 + (uint32_t)(j * -16320);
                 }
                 cntw += (uint32_t)__popcll(bal);
                 runv = v;

@@ -57,6 +57,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
     __shared__ unsigned int s_wsum[RT_NT / 64];
     const unsigned int tile = blockIdx.x, base = n0 + tile * RT_TN, tid = threadIdx.x;
     const unsigned int tend = base + RT_TN < N ? base + RT_TN : N;
+    if (tile == 0 && tid == 0) tcnt[gridDim.x] = 0;  // the scan's last element (no memset launch)
     unsigned int ext[RT_PER];
     unsigned long long fev[RT_PER];
     bool valid[RT_PER];
@@ -235,10 +236,15 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
     if (tid == 0) tcnt[tile] = off;
 }
 
-// tile heads -> the compact super list (tbase = exclusive scan of tcnt); SIDX[head] = its index
+// tile heads -> the compact super list (tbase = exclusive scan of tcnt); SIDX[head] = its index.
+// With hasp / rid (the one-GPU ranking): the super list's ruler state initialised on the way --
+// hasp = 0, rid = NONE per super, the ruler count and visit total zeroed -- instead of four
+// memset launches sized by a count the host has not read yet
 __global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, const unsigned long long *tcnt,
                                                       const unsigned long long *tbase, SuperRec *srec,
-                                                      unsigned int *SIDX) {
+                                                      unsigned int *SIDX, uint8_t *hasp = nullptr,
+                                                      uint2 *rid = nullptr, unsigned int *nr = nullptr,
+                                                      unsigned long long *nvisited = nullptr) {
     const unsigned int t = blockIdx.x;
     const unsigned int n = (unsigned int)tcnt[t];
     const unsigned long long b = tbase[t];
@@ -246,6 +252,14 @@ __global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, c
         const SuperRec r = scratch[(uint64_t)t * RT_TN + j];
         srec[b + j] = r;
         SIDX[r.head] = (unsigned int)(b + j);
+        if (hasp) {
+            hasp[b + j] = 0;
+            rid[b + j] = make_uint2(NONE32, NONE32);
+        }
+    }
+    if (nr && t == 0 && threadIdx.x == 0) {
+        *nr = 0;
+        *nvisited = 0;
     }
 }
 
