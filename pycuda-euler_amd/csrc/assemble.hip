@@ -2203,6 +2203,60 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
     return EC_OK;
 }
 
+// rank_supers without host read-backs: the chain count M and the ruler count stay on the device
+// (dM, Scalars::nr), grids are sized by the node count N >= M and read the counts in-kernel,
+// one ruler pass only (mask 15 plus every head), Wyllie rounds for N rulers (rounds past
+// convergence exit at once).  The whole ranking is queued while the device still runs the links:
+// after a read-back the host issued these ~25 launches slower than the device ran them
+// (~0.25 ms from the walk to finalize on the headline).  Chains no ruler reached (a cycle of
+// chains without a sampled one) are caught by the caller's next scalar read (nvisited < M),
+// which redoes the ranking with rank_supers.  Needs k_tile_compact's initialisation (pre_init).
+int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *dM, int &rounds) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    SuperRec *srec = s->rt_srec.as<SuperRec>();
+    const size_t cap = std::max<size_t>(N, 1);
+    EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec)));
+    EC_CHECK(s->rt_pks.ensure(cap * 4));
+    EC_CHECK(s->rt_rks.ensure(cap * 4));
+    EC_CHECK(s->rlist.ensure(cap * 4));
+    EC_CHECK(s->nextR.ensure(cap * 4));
+    EC_CHECK(s->rbc.ensure(((cap + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
+    SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
+    const unsigned int *dnr = &dsc->nr;
+    const unsigned int gs = std::min(grid_for(N, B), 4096u);  // grid-stride grids over <= N items
+    k_super_link<<<gs, B, 0, st>>>(srec, 0, s->rt_sidx.as<unsigned int>(), snrec, s->rt_hasp.as<uint8_t>(), dM);
+    const unsigned int smask = kn().sruler_mask > 0 ? (unsigned int)kn().sruler_mask : 15u;
+    const unsigned int nblk = (N + RULER_CHUNK - 1) / RULER_CHUNK;
+    k_srulers_count<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), 0, smask, 1, s->rid.as<uint2>(),
+                                        s->rbc.as<unsigned int>(), dM);
+    EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
+    k_srulers<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), 0, smask, 1, s->rbc.as<unsigned int>() + nblk, &dsc->nr,
+                                  s->rid.as<uint2>(), s->rlist.as<unsigned int>(), dM);
+    k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
+    k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), 0, &dsc->nr, smask, s->rid.as<uint2>(),
+                                 s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
+    // rulers <= chains <= N: rounds for N (a round after convergence returns at its first load)
+    const unsigned int gr = std::min(grid_for(N / 8 + 1, B), 2048u);
+    k_rjump_init<<<gr, B, 0, st>>>(s->nextR.as<unsigned int>(), 0, s->st0.as<RJump>(), dnr);
+    rounds = 1;
+    while ((1ull << (rounds - 1)) < (unsigned long long)N) rounds++;
+    rounds = std::min(rounds + 1, 63);
+    RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
+    for (int r = 0; r < rounds; r++)
+        k_rjump<<<gr, B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], 0, N, r ? &dsc->active[r - 1] : nullptr,
+                                  &dsc->active[r], &dsc->final_sel, (unsigned)((r + 1) & 1), dnr);
+    k_finalize_s<<<gs, B, 0, st>>>(snrec, srec, s->rid.as<uint2>(), s->rlist.as<unsigned int>(), bufs[0], bufs[1],
+                                   &dsc->final_sel, &dsc->active[rounds - 1], 0, s->rt_pks.as<unsigned int>(),
+                                   s->rt_rks.as<unsigned int>(), s->PL.as<unsigned int>(),
+                                   s->PM.as<unsigned long long>(), dM);
+    k_cycle_len_s<<<gr, B, 0, st>>>(s->nextR.as<unsigned int>(), s->rlist.as<unsigned int>(), srec, bufs[0], bufs[1],
+                                    &dsc->final_sel, &dsc->active[rounds - 1], 0, s->PL.as<unsigned int>(),
+                                    s->PM.as<unsigned long long>(), dnr);
+    return EC_OK;
+}
+
 // extended alphabet (extended.h): links without their twin link make their components'
 // walks overlap; those components are cut out of the parallel ranking (their successors saved
 // in x_succ) and their dict entries listed in (component, first event) order for k_x_emulate.
@@ -2353,6 +2407,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     unsigned int nr = 0;
     int rounds = 0;  // Wyllie rounds launched (their convergence is checked with the results)
     bool coop_deferred = false;  // the cooperative ranking's checks wait for the next scalar read
+    bool rank_async = false;     // rank_supers_async: its checks wait for the next scalar read
+    const unsigned long long *async_M = nullptr;  // (the chain count on the device)
+    unsigned int *async_LH = nullptr, *async_LR = nullptr;
     s->stats.rank_rounds = 0;
     if (U && tile_rank) {
         // (1) chains of in-tile links ranked in LDS, in-tile cycles finished (rank_tile.h)
@@ -2380,7 +2437,19 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         // grid barriers far slower than the launches they replace -- opt-in only)
         const bool coop = kn().rank_coop == 1;
         coop_deferred = coop;
-        if (coop) {
+        rank_async = !coop && kn().rank_sync != 1;
+        async_M = tbase + ntiles;
+        async_LH = LH;
+        async_LR = LR;
+        if (rank_async) {  // no read-back: the checks ride on the scalar read after the starts
+            k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
+                                                   s->rt_sidx.as<unsigned int>(), s->rt_hasp.as<uint8_t>(),
+                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited);
+            EC_CHECK(rank_supers_async(s, N, async_M, rounds));
+            k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
+                                                  s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
+                                                  s->RK.as<unsigned int>());
+        } else if (coop) {
             k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
                                                    s->rt_sidx.as<unsigned int>());
         } else {
@@ -2396,7 +2465,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             EC_CHECK(host_wait(s, s->rd_ev));
             M = (unsigned int)M64;
         }
-        if (coop || M) {
+        if (!rank_async && (coop || M)) {
             EC_CHECK(rank_supers(s, M, N, nr, rounds, coop ? tbase + ntiles : nullptr, coop, !coop));
             // (3) every node: its chain's key and rank + its offset in the chain
             k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
@@ -2462,6 +2531,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->svals.ensure(Nn * 4));
     EC_CHECK(s->skeys2.ensure(Nn * 8));
     EC_CHECK(s->svals2.ensure(Nn * 4));
+    unsigned long long async_M64 = 0;
+    auto starts_pass = [&]() -> int {
     EC_HIP(hipMemsetAsync(s->cidxOf.p, 0xFF, Nn * 4, st));
     if (U)
     {
@@ -2482,7 +2553,33 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_HIP(hipMemcpyAsync(&dsc->nstarts, bs + nblk - 1, 4, hipMemcpyDeviceToDevice, st));
     }
     EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));  // nstarts, active[]
+    if (rank_async) EC_CHECK(d2h(s, &async_M64, async_M, 8, st));
     EC_CHECK(host_sync(s, st));
+    return EC_OK;
+    };
+    EC_CHECK(starts_pass());
+    if (rank_async) {
+        const unsigned int Ma = (unsigned int)async_M64;
+        nr = hsc.nr;
+        s->stats.n_rulers = nr;
+        if (kn().verbose)
+            fprintf(stderr, "rank: %u oriented nodes, %u chains (tile contraction), %u rulers, %llu visited\n", N, Ma,
+                    nr, (unsigned long long)hsc.nvisited);
+        if (hsc.nvisited != Ma || (Ma && hsc.active[rounds - 1] != 0)) {
+            // a cycle of chains no ruler reached (or unconverged rounds): the ranking with its
+            // host-checked ruler passes, then the starts again
+            if (kn().verbose)
+                fprintf(stderr, "rank: one ruler pass covered %llu of %u chains, ranking again\n",
+                        (unsigned long long)hsc.nvisited, Ma);
+            rank_async = false;
+            EC_CHECK(rank_supers(s, Ma, N, nr, rounds));
+            k_expand<<<grid_for(N, B), B, 0, st>>>(async_LH, async_LR, N, s->rt_sidx.as<unsigned int>(),
+                                                  s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
+                                                  s->PK.as<unsigned int>(), s->RK.as<unsigned int>());
+            s->stats.n_rulers = nr;
+            EC_CHECK(starts_pass());
+        }
+    }
     if (coop_deferred) {
         if (hsc.coop_bad) {
             set_error("ruling set left chains unvisited");

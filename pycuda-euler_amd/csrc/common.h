@@ -31,6 +31,7 @@ struct Knobs {
     float part_keys = 0.0f;     // EULERHIP_PART_KEYS: keys per part table (0 = PART_KEYS)
     int v2_r10 = -1;            // EULERHIP_V2_R10: 10-B window records 1 = forced, 0 = never
     int refine_rs = 0;          // EULERHIP_REFINE_RS: refine slices per coarse bucket (0 = 8)
+    int rank_sync = 0;          // EULERHIP_RANK_SYNC=1: tile ranking with host-read counts (A/B)
     int no_spec = 0;            // EULERHIP_NO_SPEC=1: no speculative refine launch (count_sk2, A/B)
     bool merge_mix = false;     // EULERHIP_MERGE_MIX: key-hash buckets / owners instead of minimizers
     bool wide_general = false;  // EULERHIP_WIDE_GENERAL: k > 32 on the HBM table

@@ -501,7 +501,9 @@ __global__ void __launch_bounds__(256) k_walk(const NodeRec *nrec, const unsigne
     }
 }
 
-__global__ void __launch_bounds__(256) k_rjump_init(const unsigned int *nextR, unsigned int nr, RJump *rs) {
+__global__ void __launch_bounds__(256) k_rjump_init(const unsigned int *nextR, unsigned int nr, RJump *rs,
+                                                    const unsigned int *dnr = nullptr) {
+    if (dnr) nr = *dnr;  // (the ruler count on the device: no host read-back)
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int n = nextR[t];
         if (n != NONE32) rs[n].a = (unsigned int)t;  // prevR[next] = me (unique predecessor)
@@ -511,8 +513,10 @@ __global__ void __launch_bounds__(256) k_rjump_init(const unsigned int *nextR, u
 // one weighted Wyllie round on the ruler list
 __global__ void __launch_bounds__(256) k_rjump(const RJump *src, RJump *dst, unsigned int nr, unsigned int N,
                                                const unsigned int *active_in, unsigned int *active_out,
-                                               unsigned int *final_sel, unsigned int sel) {
+                                               unsigned int *final_sel, unsigned int sel,
+                                               const unsigned int *dnr = nullptr) {
     if (active_in && *active_in == 0) return;
+    if (dnr) nr = *dnr;
     unsigned int act = 0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
         RJump j = src[t];

@@ -272,7 +272,9 @@ __global__ void __launch_bounds__(256) k_super_index(const SuperRec *srec, unsig
 // super successors as super indices (a tail's external successor starts its own chain), the
 // walk records, and which super nodes have a predecessor (the path heads: none)
 __global__ void __launch_bounds__(256) k_super_link(const SuperRec *srec, unsigned int M, const unsigned int *SIDX,
-                                                    SNodeRec *nrec, uint8_t *hasp) {
+                                                    SNodeRec *nrec, uint8_t *hasp,
+                                                    const unsigned long long *dM = nullptr) {
+    if (dM) M = (unsigned int)*dM;  // (the count on the device: no host read-back)
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < M; t += (uint64_t)gridDim.x * blockDim.x) {
         const SuperRec r = srec[t];
         const unsigned int s = r.succ == NONE32 ? NONE32 : SIDX[r.succ];
@@ -292,7 +294,9 @@ __device__ inline bool sruler_sel(const uint8_t *hasp, const uint2 *rid, unsigne
     return (first && !hasp[i]) || ruler_hash(i, smask);
 }
 __global__ void __launch_bounds__(256) k_srulers_count(const uint8_t *hasp, unsigned int M, unsigned int smask,
-                                                       int first, const uint2 *rid, unsigned int *bc) {
+                                                       int first, const uint2 *rid, unsigned int *bc,
+                                                       const unsigned long long *dM = nullptr) {
+    if (dM) M = (unsigned int)*dM;
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < M ? c0 + RULER_CHUNK : M;
     unsigned int c = 0;
@@ -305,7 +309,8 @@ __global__ void __launch_bounds__(256) k_srulers_count(const uint8_t *hasp, unsi
 }
 __global__ void __launch_bounds__(256) k_srulers(const uint8_t *hasp, unsigned int M, unsigned int smask, int first,
                                                  const unsigned int *bs, const unsigned int *nr, uint2 *rid,
-                                                 unsigned int *rlist) {
+                                                 unsigned int *rlist, const unsigned long long *dM = nullptr) {
+    if (dM) M = (unsigned int)*dM;
     __shared__ unsigned int wsum[4];
     const uint64_t c0 = (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < M ? c0 + RULER_CHUNK : M;
@@ -389,17 +394,19 @@ __global__ void __launch_bounds__(256) k_finalize_s(const SNodeRec *nrec, const 
                                                     const unsigned int *rlist, const RJump *rs0, const RJump *rs1,
                                                     const unsigned int *sel, const unsigned int *unconverged,
                                                     unsigned int M, unsigned int *PKs, unsigned int *RKs,
-                                                    unsigned int *PL, unsigned long long *PM) {
+                                                    unsigned int *PL, unsigned long long *PM,
+                                                    const unsigned long long *dM = nullptr) {
+    if (dM) M = (unsigned int)*dM;
     const bool bad = *unconverged != 0;  // (the host reports it; placeholders stay in range)
     const RJump *rs = (*sel & 1) ? rs1 : rs0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < M; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int v = (unsigned int)t;
-        if (bad) {
+        const uint2 ro = rid[v];
+        if (bad || ro.x == NONE32) {  // (NONE: a chain no ruler reached -- the deferred check redoes the ranking)
             PKs[v] = srec[v].head;
             RKs[v] = 0;
             continue;
         }
-        const uint2 ro = rid[v];
         const RJump r = rs[ro.x];
         if (r.a == NONE32) {  // path
             const unsigned int pk = srec[rlist[r.h]].head, rk = r.s + ro.y;
@@ -418,8 +425,10 @@ __global__ void __launch_bounds__(256) k_finalize_s(const SNodeRec *nrec, const 
 __global__ void __launch_bounds__(256) k_cycle_len_s(const unsigned int *nextR, const unsigned int *rlist,
                                                      const SuperRec *srec, const RJump *rs0, const RJump *rs1,
                                                      const unsigned int *sel, const unsigned int *unconverged,
-                                                     unsigned int nr, unsigned int *PL, unsigned long long *PM) {
+                                                     unsigned int nr, unsigned int *PL, unsigned long long *PM,
+                                                     const unsigned int *dnr = nullptr) {
     if (*unconverged) return;
+    if (dnr) nr = *dnr;
     const RJump *rs = (*sel & 1) ? rs1 : rs0;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nr; t += (uint64_t)gridDim.x * blockDim.x) {
         const RJump r = rs[t];
