@@ -155,6 +155,10 @@ struct ec_session {
     hipStream_t ostream = nullptr;
     hipEvent_t oev[2] = {nullptr, nullptr};
     uint64_t last_nchars = 0;
+    // bucket starts of the dense ids (k_skbucket3 marks each bucket's first id): the tile
+    // ranking cuts its tiles there (k_tile_plan); valid from a super-k-mer count to its graph phase
+    DevBuf bmark, rt_tb;
+    bool bmark_ok = false;
     // count_sk2's refine plan of the previous call: launched speculatively on the next call of
     // the same shape while the host reads the partition's scalars back (phase_count_sk2)
     struct SkSpec {
@@ -442,6 +446,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     s->flags = flags;
     s->shard_base = 0;
     s->own_valid = false;
+    s->bmark_ok = false;
     const bool timing = (flags & (EC_FLAG_TIMING | EC_FLAG_KERNEL_TIMING)) != 0;
     s->stage_timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
@@ -784,6 +789,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
 #define EC_SKBUCKET(SLOTS, RS, EVEN) \
     k_skbucket<SLOTS, RS, 1, EVEN><<<(unsigned)Bk, BUCKET_THREADS, 0, st>>>(EC_SKBUCKET_ARGS, dbg)
     // EULERHIP_SK2_STATS: distinct records, flushes and windows rolled out (stderr)
+    bool b3_marked = false;
     unsigned long long *dbg = nullptr;
     if (kn().sk2_stats) {
         EC_CHECK(s->tmp.ensure(128));
@@ -816,10 +822,18 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     } else if (plan.slots == 1024) {
         constexpr int NT3 = 512;
         const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
+        unsigned int *bm = nullptr;
+        if (kn().tile_plan != 0) {  // (bucket starts for the tile ranking: one bit per dense id)
+            const size_t words = umax / 32 + 2;
+            EC_CHECK(s->bmark.ensure(words * 4));
+            EC_HIP(hipMemsetAsync(s->bmark.p, 0, words * 4, st));
+            bm = s->bmark.as<unsigned int>();
+        }
         if (k & 1)
-            k_skbucket3<1024, 1664, NT3, false><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg, claim_cap);
+            k_skbucket3<1024, 1664, NT3, false><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg, claim_cap, bm);
         else
-            k_skbucket3<1024, 1664, NT3, true><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg, claim_cap);
+            k_skbucket3<1024, 1664, NT3, true><<<(unsigned)Bk, NT3, 0, st>>>(EC_SKBUCKET_ARGS, dbg, claim_cap, bm);
+        b3_marked = bm != nullptr;
     } else if (plan.slots == 2048) {
         if (k & 1) EC_SKBUCKET(2048, 3072, false);
         else EC_SKBUCKET(2048, 3072, true);
@@ -863,6 +877,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         return reset();
     }
     done = true;
+    s->bmark_ok = b3_marked;
     s->stats.n_positions = P;
     s->stats.n_distinct_est = (uint64_t)llround(est);
     s->stats.record_bytes = 16;
@@ -2243,7 +2258,7 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), 0, &dsc->nr, smask, s->rid.as<uint2>(),
                                  s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
     // rulers <= chains <= N: rounds for N (a round after convergence returns at its first load)
-    const unsigned int gr = std::min(grid_for(N / 8 + 1, B), 2048u);
+    const unsigned int gr = std::min(grid_for(N / (kn().rj_div > 0 ? (unsigned)kn().rj_div : 8u) + 1, B), 2048u);
     k_rjump_init<<<gr, B, 0, st>>>(s->nextR.as<unsigned int>(), 0, s->st0.as<RJump>(), dnr);
     rounds = 1;
     while ((1ull << (rounds - 1)) < (unsigned long long)N) rounds++;
@@ -2418,13 +2433,25 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     s->stats.rank_rounds = 0;
     if (U && tile_rank) {
         // (1) chains of in-tile links ranked in LDS, in-tile cycles finished (rank_tile.h)
-        const unsigned int ntiles = (N + RT_TN - 1) / RT_TN;
+        // tiles cut at bucket starts where the count marked them (k_tile_plan), else fixed
+        const bool planned = std::is_same<Index, SolidIndex>::value && s->bmark_ok;
+        s->bmark_ok = false;
+        const unsigned int ntiles = planned ? (U + RT_STEP - 1) / RT_STEP : (N + RT_TN - 1) / RT_TN;
+        const unsigned int *tbp = nullptr;
+        if (planned) {
+            EC_CHECK(s->rt_tb.ensure(((size_t)ntiles + 1) * 4));
+            k_tile_plan<<<grid_for(ntiles + 1ull, B), B, 0, st>>>(s->bmark.as<unsigned int>(), U, ntiles,
+                                                               s->rt_tb.as<unsigned int>());
+            tbp = s->rt_tb.as<unsigned int>();
+        }
         EC_CHECK(s->rt_tcnt.ensure(((size_t)ntiles + 1) * 8));
         EC_CHECK(s->rt_tbase.ensure(((size_t)ntiles + 1) * 8));
         EC_CHECK(s->rt_srec.ensure(Nn * sizeof(SuperRec)));
         EC_CHECK(s->rt_sidx.ensure(Nn * 4));
         EC_CHECK(s->rt_lr.ensure(Nn * 4));
         unsigned int *LH = s->pred.as<unsigned int>(), *LR = s->rt_lr.as<unsigned int>();  // (pred: free here)
+        // (a tile's chains at scratch[tile * RT_TN ..]: planned tiles are more than N / RT_TN)
+        EC_CHECK(s->st1.ensure(std::max<size_t>(Nn, (size_t)ntiles * RT_TN) * sizeof(RJump)));
         SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);  // (dead before the Wyllie rounds)
         static_assert(sizeof(SuperRec) == sizeof(RJump), "tile scratch in the ruler state buffer");
         unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
@@ -2432,7 +2459,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
                                                 s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), LH,
                                                 LR, tcnt, scratch, s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
-                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>());
+                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>(), 0u, tbp);
         EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
         // (2) the super list: compacted in tile order, linked, ranked by the weighted ruling set
         // -- in one cooperative launch that reads the chain count on the device (no host round
@@ -2844,6 +2871,35 @@ int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
                                                     s->rt_sidx.as<unsigned int>());
     unsigned int nr = 0;
     int rounds = 0;
+    if (kn().rank_sync != 1) {
+        // rank_supers_async (one read-back at the end instead of one per ruler pass plus the
+        // launch backlog after it): M on the device, the ruler state initialised here
+        const size_t Nn = std::max<size_t>(N, 1);
+        EC_CHECK(s->rt_hasp.ensure(Nn));
+        EC_CHECK(s->rid.ensure(Nn * 8));
+        EC_CHECK(s->st0.ensure(Nn * sizeof(RJump)));
+        EC_CHECK(s->st1.ensure(Nn * sizeof(RJump)));
+        EC_CHECK(s->rt_tbase.ensure(8));
+        unsigned int *dM32 = s->rt_tbase.as<unsigned int>();
+        EC_HIP(hipMemsetD32Async(dM32, (int)(unsigned int)M, 1, st));
+        EC_HIP(hipMemsetD32Async(dM32 + 1, 0, 1, st));
+        EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
+        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
+        EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
+        EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
+        EC_CHECK(rank_supers_async(s, N, s->rt_tbase.as<unsigned long long>(), rounds));
+        Scalars hsc{};
+        EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
+        EC_CHECK(host_sync(s, st));
+        if (hsc.nvisited == M && hsc.active[rounds - 1] == 0) {
+            s->stats.n_rulers = hsc.nr;
+            s->stats.rank_rounds = rounds;
+            return EC_OK;
+        }
+        if (kn().verbose)
+            fprintf(stderr, "part_rank: one ruler pass covered %llu of %llu chains, ranking again\n",
+                    (unsigned long long)hsc.nvisited, (unsigned long long)M);
+    }
     EC_CHECK(rank_supers(s, (unsigned int)M, N, nr, rounds));
     s->stats.n_rulers = nr;
     unsigned int act = 0;
@@ -3359,7 +3415,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv, &s->skrej};
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv, &s->skrej, &s->bmark, &s->rt_tb};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->bounce.release();

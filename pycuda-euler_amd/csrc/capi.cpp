@@ -35,6 +35,8 @@ void refresh_knobs() {
         k.v2_r10 = num("EULERHIP_V2_R10", -1);
         k.refine_rs = num("EULERHIP_REFINE_RS", 0);
         k.no_spec = num("EULERHIP_NO_SPEC", 0);
+        k.tile_plan = num("EULERHIP_TILE_PLAN", -1);
+        k.rj_div = num("EULERHIP_RJ_DIV", 0);
         k.rank_sync = num("EULERHIP_RANK_SYNC", 0);
         k.merge_mix = flag("EULERHIP_MERGE_MIX");
         k.wide_general = flag("EULERHIP_WIDE_GENERAL");

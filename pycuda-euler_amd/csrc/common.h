@@ -32,6 +32,8 @@ struct Knobs {
     int v2_r10 = -1;            // EULERHIP_V2_R10: 10-B window records 1 = forced, 0 = never
     int refine_rs = 0;          // EULERHIP_REFINE_RS: refine slices per coarse bucket (0 = 8)
     int rank_sync = 0;          // EULERHIP_RANK_SYNC=1: tile ranking with host-read counts (A/B)
+    int rj_div = 0;             // EULERHIP_RJ_DIV: rank_supers_async's Wyllie grids cover N / RJ_DIV rulers (A/B)
+    int tile_plan = -1;         // EULERHIP_TILE_PLAN=0: fixed rank tiles, not cut at bucket starts (A/B)
     int no_spec = 0;            // EULERHIP_NO_SPEC=1: no speculative refine launch (count_sk2, A/B)
     bool merge_mix = false;     // EULERHIP_MERGE_MIX: key-hash buckets / owners instead of minimizers
     bool wide_general = false;  // EULERHIP_WIDE_GENERAL: k > 32 on the HBM table

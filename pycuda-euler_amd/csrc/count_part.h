@@ -852,7 +852,7 @@ __device__ inline void lds_table_finish(const Tab &tab, const unsigned int *s_ov
                                         unsigned long long *dkey, unsigned int *dcnt, unsigned long long *dfc,
                                         unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
                                         unsigned long long *ndistinct, unsigned int *overflow, KO ko = KO(),
-                                        EO eo = EO()) {
+                                        EO eo = EO(), unsigned int *bmark = nullptr) {
     __shared__ unsigned int s_wave[NT / 64], s_pres[NT / 64];
     __shared__ unsigned int s_base;
     __syncthreads();
@@ -913,6 +913,7 @@ __device__ inline void lds_table_finish(const Tab &tab, const unsigned int *s_ov
             np += s_pres[w];
         }
         s_base = tot ? atomicAdd(nsolid, tot) : 0;
+        if (bmark && tot) atomicOr(&bmark[s_base >> 5], 1u << (s_base & 31));  // (the bucket's first id: k_tile_plan)
         if (np && ndistinct) atomicAdd(ndistinct, (unsigned long long)np);
     }
     __syncthreads();

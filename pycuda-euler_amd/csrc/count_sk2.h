@@ -893,7 +893,7 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
                                                   unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
                                                   unsigned int *nsolid, unsigned long long *ndistinct,
                                                   unsigned int *overflow, unsigned long long *dbg,
-                                                  unsigned int claim_cap) {
+                                                  unsigned int claim_cap, unsigned int *bmark = nullptr) {
     constexpr int SBITS = __builtin_ctz(SLOTS);
     constexpr uint32_t PEND = 0x800u;
     constexpr unsigned int CLAIM_MAX = RS / 2 < RS - 1 - NT ? RS / 2 : RS - 1 - NT;
@@ -1115,7 +1115,7 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
     if (dbg) atomicAdd(&dbg[2], n_rolled);
     lds_table_finish<SLOTS, false, KeyId, LTabE<SLOTS>, EvExpand, NT>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub,
                                                                       nsolid, ndistinct, overflow, KeyId(),
-                                                                      EvExpand{2 * M});
+                                                                      EvExpand{2 * M}, bmark);
 }
 
 

@@ -50,13 +50,16 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
                                                        const unsigned long long *dfc, const unsigned long long *dft,
                                                        unsigned int *LH, unsigned int *LR, unsigned long long *tcnt,
                                                        SuperRec *scratch, unsigned int *PK, unsigned int *RK,
-                                                       unsigned int *PL, unsigned long long *PM, unsigned int n0 = 0) {
+                                                       unsigned int *PL, unsigned long long *PM, unsigned int n0 = 0,
+                                                       const unsigned int *tb = nullptr) {
     __shared__ uint16_t s_ls[RT_TN], s_lp[RT_TN], s_p[RT_TN], s_mn[RT_TN];
     __shared__ unsigned int s_d[RT_TN], s_cl[RT_TN];
     __shared__ unsigned long long s_cm[RT_TN];
     __shared__ unsigned int s_wsum[RT_NT / 64];
-    const unsigned int tile = blockIdx.x, base = n0 + tile * RT_TN, tid = threadIdx.x;
-    const unsigned int tend = base + RT_TN < N ? base + RT_TN : N;
+    // tiles of RT_TN nodes from n0, or tb's tiles (k_tile_plan: cut at bucket starts, <= RT_TN)
+    const unsigned int tile = blockIdx.x, tid = threadIdx.x;
+    const unsigned int base = tb ? tb[tile] : n0 + tile * RT_TN;
+    const unsigned int tend = tb ? tb[tile + 1] : (base + RT_TN < N ? base + RT_TN : N);
     if (tile == 0 && tid == 0) tcnt[gridDim.x] = 0;  // the scan's last element (no memset launch)
     unsigned int ext[RT_PER];
     unsigned long long fev[RT_PER];
@@ -64,7 +67,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
 #pragma unroll
     for (int q = 0; q < RT_PER; q++) {
         const unsigned int i = tid + q * RT_NT, x = base + i;
-        valid[q] = x < N && !((x & 1) && upal[x >> 1]);
+        valid[q] = x < tend && !((x & 1) && upal[x >> 1]);
         const unsigned int s = valid[q] ? succ[x] : NONE32;
         fev[q] = valid[q] ? first_event(dfc, dft, x) : NONE64;
         const bool in = s != NONE32 && s >= base && s < tend;
@@ -176,7 +179,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
     for (int q = 0; q < RT_PER; q++) {
         const unsigned int i = tid + q * RT_NT, x = base + i;
         if (!valid[q]) {
-            if (x < N) LH[x] = NONE32;
+            if (x < tend) LH[x] = NONE32;
             continue;
         }
         const unsigned int h = base + p[q];
@@ -234,6 +237,35 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         (void)i;
     }
     if (tid == 0) tcnt[tile] = off;
+}
+
+// Tiles cut at bucket starts (the super-k-mer count marks each bucket's first dense id in
+// bmark): a minimizer's k-mers share a bucket, so a chain leaves its tile only where its path
+// changes minimizer, not where a fixed RT_TN boundary splits a bucket (~37 % of the headline's
+// chains).  Tile t starts at canonical id t * RT_STEP rounded down to the nearest bucket start
+// at most RT_TN / 2 - RT_STEP below it (else not rounded): tiles hold <= RT_TN oriented nodes.
+// tb[t] = oriented start of tile t, tb[ntiles] = 2 U
+constexpr unsigned int RT_STEP = 768;  // canonical ids per tile stride (RT_TN / 2 = 1024 at most)
+__global__ void __launch_bounds__(256) k_tile_plan(const unsigned int *bmark, unsigned int U, unsigned int ntiles,
+                                                   unsigned int *tb) {
+    const unsigned int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    if (t == 0 || t == ntiles) {
+        tb[t] = t ? 2 * U : 0u;
+        return;
+    }
+    const unsigned int c = t * RT_STEP, lo = c - (RT_TN / 2 - RT_STEP);
+    unsigned int cut = c;
+    for (int w = (int)(c >> 5); w >= (int)(lo >> 5); w--) {  // the highest bucket start in [lo, c]
+        unsigned int m = bmark[w];
+        if ((unsigned int)w == (c >> 5)) m &= (c & 31) == 31 ? ~0u : ((2u << (c & 31)) - 1);
+        if (m) {
+            const unsigned int pos = (unsigned int)w * 32 + 31 - (unsigned int)__clz((int)m);
+            if (pos >= lo) cut = pos;
+            break;
+        }
+    }
+    tb[t] = 2 * cut;
 }
 
 // tile heads -> the compact super list (tbase = exclusive scan of tcnt); SIDX[head] = its index.
