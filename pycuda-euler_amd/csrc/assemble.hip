@@ -159,6 +159,9 @@ struct ec_session {
     // ranking cuts its tiles there (k_tile_plan); valid from a super-k-mer count to its graph phase
     DevBuf bmark, rt_tb;
     bool bmark_ok = false;
+    // the owner merge's marks (phase_merge_part): its solid count, 0 = none -- the partitioned
+    // finish cuts its segment's tiles there when the segment is that merge's output
+    uint64_t seg_marks = 0;
     // count_sk2's refine plan of the previous call: launched speculatively on the next call of
     // the same shape while the host reads the partition's scalars back (phase_count_sk2)
     struct SkSpec {
@@ -486,7 +489,7 @@ int compact_table(ec_session *s, SlotT *table, uint64_t cap, long long limit, Ke
 
 
 template <typename Src>
-int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long limit) {
+int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long limit, unsigned int *bmark = nullptr) {
     Scalars *dsc = s->scal.as<Scalars>();
     hipStream_t st = s->stream;
     // bucket b = records [bb[b], be[b]): the exact path's scanned starts, or the fixed-capacity
@@ -508,12 +511,12 @@ int launch_bucket(ec_session *s, Src src, unsigned nb, unsigned slots, long long
         k_bucket<Src, 2048><<<nb, BUCKET_THREADS, 0, st>>>(
             src, bb, be, ns, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
             s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
-            &dsc->ndistinct, &dsc->overflow);
+            &dsc->ndistinct, &dsc->overflow, bmark);
     else
         k_bucket<Src, 4096><<<nb, BUCKET_THREADS, 0, st>>>(
             src, bb, be, ns, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),
             s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid,
-            &dsc->ndistinct, &dsc->overflow);
+            &dsc->ndistinct, &dsc->overflow, bmark);
     return EC_OK;
 }
 
@@ -1473,12 +1476,23 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
     kmark(s, 2, 0);
     const int sks = own.sk ? (slots == 2048 ? 11 : 12) : 0;
+    bool merge_marked = false;
+    if (!ids) s->seg_marks = 0;
     if (ids) {  // gathered solid set: dense ids given (partitioned graph phase)
         const AggDetSource src{d_agg, s->midx2.as<unsigned int>(), ids, sks};
         EC_CHECK(launch_bucket(s, src, nb, slots, limit));
     } else {
+        // (minimizer buckets: their first ids marked for the partitioned finish's tiles)
+        unsigned int *bm = nullptr;
+        if (own.sk && !s->filt && kn().tile_plan != 0) {
+            const size_t words = umax / 32 + 2;
+            EC_CHECK(s->bmark.ensure(words * 4));
+            EC_HIP(hipMemsetAsync(s->bmark.p, 0, words * 4, st));
+            bm = s->bmark.as<unsigned int>();
+        }
         const AggSource src{d_agg, s->midx2.as<unsigned int>(), sks};
-        EC_CHECK(launch_bucket(s, src, nb, slots, limit));
+        EC_CHECK(launch_bucket(s, src, nb, slots, limit, bm));
+        merge_marked = bm != nullptr;
     }
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
@@ -1506,6 +1520,7 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
     }
+    if (merge_marked) s->seg_marks = U;  // (bmark holds this merge's bucket starts, U ids)
     ok = true;
     return EC_OK;
 }
@@ -2834,7 +2849,18 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
     if (n1 > n0)
         EC_HIP(hipMemcpyAsync(s->succ.as<unsigned int>() + n0, d_succ, (size_t)(n1 - n0) * 4, hipMemcpyDeviceToDevice,
                               st));
-    const unsigned int ntiles = (n1 - n0 + RT_TN - 1) / RT_TN;
+    // tiles cut at the bucket starts this rank's owner merge marked (its output is this segment)
+    const bool planned = s->seg_marks && s->seg_marks == hi - lo && hi > lo;
+    const unsigned int ntiles =
+        planned ? (unsigned int)((hi - lo + RT_STEP_SEG - 1) / RT_STEP_SEG) : (n1 - n0 + RT_TN - 1) / RT_TN;
+    const unsigned int *tbp = nullptr;
+    if (planned) {
+        EC_CHECK(s->rt_tb.ensure(((size_t)ntiles + 1) * 4));
+        k_tile_plan<<<grid_for(ntiles + 1ull, B), B, 0, st>>>(s->bmark.as<unsigned int>(), (unsigned int)(hi - lo),
+                                                           ntiles, s->rt_tb.as<unsigned int>(), (unsigned int)lo,
+                                                           RT_STEP_SEG);
+        tbp = s->rt_tb.as<unsigned int>();
+    }
     EC_CHECK(s->rt_tcnt.ensure(((size_t)ntiles + 1) * 8));
     EC_CHECK(s->rt_tbase.ensure(((size_t)ntiles + 1) * 8));
     EC_CHECK(s->st1.ensure(std::max<size_t>((size_t)ntiles * RT_TN, 1) * sizeof(SuperRec)));
@@ -2846,7 +2872,7 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
                                                 s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
                                                 s->pred.as<unsigned int>(), s->rt_lr.as<unsigned int>(), tcnt, scratch,
                                                 s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
-                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>(), n0);
+                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>(), n0, tbp);
     EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
     unsigned long long M = 0;
     EC_CHECK(d2h(s, &M, tbase + ntiles, 8, st));

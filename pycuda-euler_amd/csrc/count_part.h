@@ -953,7 +953,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
                                                           unsigned long long *dkey, unsigned int *dcnt,
                                                           unsigned long long *dfc, unsigned long long *dft,
                                                           SubSlot *sub, unsigned int *nsolid,
-                                                          unsigned long long *ndistinct, unsigned int *overflow) {
+                                                          unsigned long long *ndistinct, unsigned int *overflow,
+                                                          unsigned int *bmark = nullptr) {
     __shared__ LTab<SLOTS> tab;
     __shared__ unsigned int s_over[2];
     const unsigned int b = blockIdx.x;
@@ -987,7 +988,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket(Src src, const unsign
         }
     }
     lds_table_finish<SLOTS, Src::kDet>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct,
-                                       overflow, KeyOutOf<Src>{src});
+                                       overflow, KeyOutOf<Src>{src}, EvId(), bmark);
 }
 
 // ---- buckets with more distinct k-mers than an LDS table holds -----------------------------

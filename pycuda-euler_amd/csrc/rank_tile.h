@@ -246,15 +246,20 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
 // at most RT_TN / 2 - RT_STEP below it (else not rounded): tiles hold <= RT_TN oriented nodes.
 // tb[t] = oriented start of tile t, tb[ntiles] = 2 U
 constexpr unsigned int RT_STEP = 768;  // canonical ids per tile stride (RT_TN / 2 = 1024 at most)
+// the owner merge's buckets hold ~600 solid keys (k_agg_bucket_ids: <= 1100 records), twice the
+// count's: its segments are cut on a finer stride that may round down further
+constexpr unsigned int RT_STEP_SEG = 512;
+// (c0: the segment's first canonical id -- the multi-GPU finish plans its own segment, whose
+// bucket starts its merge marked in segment-relative ids)
 __global__ void __launch_bounds__(256) k_tile_plan(const unsigned int *bmark, unsigned int U, unsigned int ntiles,
-                                                   unsigned int *tb) {
+                                                   unsigned int *tb, unsigned int c0 = 0, unsigned int step = RT_STEP) {
     const unsigned int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t > ntiles) return;
     if (t == 0 || t == ntiles) {
-        tb[t] = t ? 2 * U : 0u;
+        tb[t] = 2 * (c0 + (t ? U : 0u));
         return;
     }
-    const unsigned int c = t * RT_STEP, lo = c - (RT_TN / 2 - RT_STEP);
+    const unsigned int c = t * step, lo = c - (RT_TN / 2 - step);  // (step >= RT_TN / 4: monotone cuts)
     unsigned int cut = c;
     for (int w = (int)(c >> 5); w >= (int)(lo >> 5); w--) {  // the highest bucket start in [lo, c]
         unsigned int m = bmark[w];
@@ -265,7 +270,7 @@ __global__ void __launch_bounds__(256) k_tile_plan(const unsigned int *bmark, un
             break;
         }
     }
-    tb[t] = 2 * cut;
+    tb[t] = 2 * (c0 + cut);
 }
 
 // tile heads -> the compact super list (tbase = exclusive scan of tcnt); SIDX[head] = its index.
