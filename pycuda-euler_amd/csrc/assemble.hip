@@ -1878,12 +1878,20 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_CHECK(s->dfc.ensure(umax * 8));
     EC_CHECK(s->dft.ensure(umax * 8));
     if (!s->no_index) EC_CHECK(s->sub.ensure(umax * sizeof(SubSlotW)));
+    // minimizer buckets: each bucket's first dense id marked for the tile ranking (k_tile_plan)
+    unsigned int *bm = nullptr;
+    if (mb && kn().tile_plan != 0) {
+        const size_t words = umax / 32 + 2;
+        EC_CHECK(s->bmark.ensure(words * 4));
+        EC_HIP(hipMemsetAsync(s->bmark.p, 0, words * 4, st));
+        bm = s->bmark.as<unsigned int>();
+    }
     kmark(s, 2, 0);
 #define EC_BUCKET_W(SL, R, SRC, BEG, END)                                                                       \
     k_bucket_w<SL, R><<<(unsigned)Bt, BUCKET_THREADS, 0, st>>>(                                                  \
         SRC, BEG, END, limit, s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),    \
         s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
-        &dsc->ndistinct, &dsc->overflow)
+        &dsc->ndistinct, &dsc->overflow, bm)
     if (sbits && mb)
         EC_BUCKET_W(1664, RecWM, s->recs.as<RecWM>(), s->bb2.as<unsigned long long>(),
                     s->bb2.as<unsigned long long>() + 1);
@@ -1925,6 +1933,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         set_error("too many solid k-mers (%u) for 31-bit node ids", U);
         return EC_ERR_CAPACITY;
     }
+    s->bmark_ok = bm != nullptr;
     ok = true;
     return EC_OK;
 }
@@ -2449,7 +2458,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (U && tile_rank) {
         // (1) chains of in-tile links ranked in LDS, in-tile cycles finished (rank_tile.h)
         // tiles cut at bucket starts where the count marked them (k_tile_plan), else fixed
-        const bool planned = std::is_same<Index, SolidIndex>::value && s->bmark_ok;
+        const bool planned = ids_minimizer_local(sidx) && s->bmark_ok;
         s->bmark_ok = false;
         const unsigned int ntiles = planned ? (U + RT_STEP - 1) / RT_STEP : (N + RT_TN - 1) / RT_TN;
         const unsigned int *tbp = nullptr;

@@ -491,7 +491,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const R *recs, cons
                                                             const unsigned long long *bend, long long limit, K128 *dkey, unsigned int *dcnt,
                                                             unsigned long long *dfc, unsigned long long *dft,
                                                             SubSlotW *sub, unsigned int *nsolid,
-                                                            unsigned long long *ndistinct, unsigned int *overflow) {
+                                                            unsigned long long *ndistinct, unsigned int *overflow,
+                                                            unsigned int *bmark = nullptr) {
     __shared__ LSlotW tab[SLOTS];
     __shared__ unsigned int s_over[2];
     __shared__ unsigned int s_wave[BUCKET_THREADS / 64], s_pres[BUCKET_THREADS / 64];
@@ -567,6 +568,7 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const R *recs, cons
         }
         s_base = tot ? atomicAdd(nsolid, tot) : 0;
         if (np) atomicAdd(ndistinct, (unsigned long long)np);
+        if (bmark && tot) atomicOr(&bmark[s_base >> 5], 1u << (s_base & 31));  // (the tile ranking's cuts)
     }
     __syncthreads();
     unsigned int u = s_base + s_wave[wid] + incl - mine;
