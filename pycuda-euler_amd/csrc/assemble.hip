@@ -808,10 +808,14 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         // records a bucket rejected -- and its 131 KB of LDS held one workgroup per CU: compact
         // 8.26 ms against 7.75 without it; opt-in, EULERHIP_SKF_DEDUP=1)
         if (kn().skf_dedup != 1) {
+            // (no tile planning here: measured on ecoli10m_err the planned tiles left more chains,
+            // 11.2 M against 10.9 M -- its graph is cut by error branches, not by tile edges)
+            unsigned int *bm = nullptr;
             if (k & 1)
-                k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
+                k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
             else
-                k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg);
+                k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
+            b3_marked = bm != nullptr;
         } else {  // rejected records (no room in the record table) in a scratch array laid out as recs2
             EC_CHECK(s->skrej.ensure(Bk * fcap * 16));
             uint4 *rej = s->skrej.as<uint4>();

@@ -1143,7 +1143,7 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
                                                       unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
                                                       unsigned int *nsolid, unsigned long long *ndistinct,
                                                       unsigned int *overflow, unsigned int max_keys,
-                                                      unsigned long long *dbg = nullptr) {
+                                                      unsigned long long *dbg = nullptr, unsigned int *bmark = nullptr) {
     constexpr int SBITS = __builtin_ctz(SLOTS);
     constexpr unsigned int NW = 1u << (SKF_BITS - 5), CM = (1u << SKF_BITS) - 1;
     __shared__ LTabE<SLOTS> tab;
@@ -1260,7 +1260,7 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
     }
     lds_table_finish<SLOTS, false, KeyId, LTabE<SLOTS>, EvExpand, NT>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub,
                                                                       nsolid, nullptr, overflow, KeyId(),
-                                                                      EvExpand{2 * M});
+                                                                      EvExpand{2 * M}, bmark);
 }
 
 // ---- the same behind a record merge (round 4) ------------------------------------------------
