@@ -353,6 +353,7 @@ struct Scalars {  // device scalars block
     unsigned int xbad;             // extended.h: a walk that never reaches its start again
     unsigned int coop_bad, coop_nr;  // k_rank_supers_coop: chains left unvisited, rulers
     unsigned int wbv_long, wpad;     // k_wbv: a read of another length
+    unsigned long long chains;       // k_tile_compact: the tile contraction's chain count
     unsigned int active[64];
 };
 
@@ -2503,7 +2504,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         if (rank_async) {  // no read-back: the checks ride on the scalar read after the starts
             k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
                                                    s->rt_sidx.as<unsigned int>(), s->rt_hasp.as<uint8_t>(),
-                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited);
+                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited, &dsc->chains);
             EC_CHECK(rank_supers_async(s, N, async_M, rounds));
             k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
@@ -2608,12 +2609,12 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_starts_write<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
                                            s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
                                            s->PM.as<unsigned long long>(), N, bs, smask,
-                                           s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>());
-        EC_HIP(hipMemcpyAsync(&dsc->nstarts, bs + nblk - 1, 4, hipMemcpyDeviceToDevice, st));
+                                           s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(), 0u,
+                                           &dsc->nstarts);
     }
-    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));  // nstarts, active[]
-    if (rank_async) EC_CHECK(d2h(s, &async_M64, async_M, 8, st));
+    EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));  // nstarts, active[], the chain count
     EC_CHECK(host_sync(s, st));
+    async_M64 = hsc.chains;
     return EC_OK;
     };
     EC_CHECK(starts_pass());

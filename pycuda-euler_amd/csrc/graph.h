@@ -654,8 +654,9 @@ __global__ void __launch_bounds__(256) k_starts_write(const uint8_t *upal, const
                                                       const unsigned long long *PM, unsigned int N,
                                                       const unsigned int *bs, const unsigned long long *smask,
                                                       unsigned long long *skeys, unsigned int *svals,
-                                                      unsigned int n0 = 0) {
+                                                      unsigned int n0 = 0, unsigned int *nstarts = nullptr) {
     __shared__ unsigned int wsum[4];
+    if (nstarts && blockIdx.x == 0 && threadIdx.x == 0) *nstarts = bs[gridDim.x - 1];  // (no copy launch)
     const uint64_t c0 = n0 + (uint64_t)blockIdx.x * RULER_CHUNK;
     const uint64_t c1 = c0 + RULER_CHUNK < N ? c0 + RULER_CHUNK : N;
     unsigned int base = blockIdx.x ? bs[blockIdx.x - 1] : 0u;

@@ -281,7 +281,8 @@ __global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, c
                                                       const unsigned long long *tbase, SuperRec *srec,
                                                       unsigned int *SIDX, uint8_t *hasp = nullptr,
                                                       uint2 *rid = nullptr, unsigned int *nr = nullptr,
-                                                      unsigned long long *nvisited = nullptr) {
+                                                      unsigned long long *nvisited = nullptr,
+                                                      unsigned long long *nchains = nullptr) {
     const unsigned int t = blockIdx.x;
     const unsigned int n = (unsigned int)tcnt[t];
     const unsigned long long b = tbase[t];
@@ -298,6 +299,7 @@ __global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, c
         *nr = 0;
         *nvisited = 0;
     }
+    if (nchains && t == 0 && threadIdx.x == 0) *nchains = tbase[gridDim.x];  // (rides on the next scalar read)
 }
 
 // SIDX[head] = index of a chain in a gathered super list (the multi-GPU finish)
