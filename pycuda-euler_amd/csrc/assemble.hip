@@ -2464,12 +2464,17 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         // tiles cut at bucket starts where the count marked them (k_tile_plan), else fixed
         const bool planned = ids_minimizer_local(sidx) && s->bmark_ok;
         s->bmark_ok = false;
-        const unsigned int ntiles = planned ? (U + RT_STEP - 1) / RT_STEP : (N + RT_TN - 1) / RT_TN;
+        // (buckets of more than ~300 keys -- config 5's 2^19 tables hold ~376 -- are cut on the
+        // finer stride that may round down by up to 512: a cut inside a bucket splits nearly every
+        // minimizer run of it, whose k-mers lie in hash order across the bucket's ids)
+        const double per_bucket = s->stats.n_buckets ? (double)U / s->stats.n_buckets : 0.0;
+        const unsigned int step = per_bucket > 300.0 ? RT_STEP_SEG : RT_STEP;
+        const unsigned int ntiles = planned ? (U + step - 1) / step : (N + RT_TN - 1) / RT_TN;
         const unsigned int *tbp = nullptr;
         if (planned) {
             EC_CHECK(s->rt_tb.ensure(((size_t)ntiles + 1) * 4));
             k_tile_plan<<<grid_for(ntiles + 1ull, B), B, 0, st>>>(s->bmark.as<unsigned int>(), U, ntiles,
-                                                               s->rt_tb.as<unsigned int>());
+                                                               s->rt_tb.as<unsigned int>(), 0u, step);
             tbp = s->rt_tb.as<unsigned int>();
         }
         EC_CHECK(s->rt_tcnt.ensure(((size_t)ntiles + 1) * 8));
