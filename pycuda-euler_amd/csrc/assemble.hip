@@ -2484,7 +2484,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(s->rt_lr.ensure(Nn * 4));
         unsigned int *LH = s->pred.as<unsigned int>(), *LR = s->rt_lr.as<unsigned int>();  // (pred: free here)
         // (a tile's chains at scratch[tile * RT_TN ..]: planned tiles are more than N / RT_TN)
-        EC_CHECK(s->st1.ensure(std::max<size_t>(Nn, (size_t)ntiles * RT_TN) * sizeof(RJump)));
+        EC_CHECK(s->st1.ensure(std::max<size_t>(Nn, planned ? 0 : (size_t)ntiles * RT_TN) * sizeof(RJump)));
         SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);  // (dead before the Wyllie rounds)
         static_assert(sizeof(SuperRec) == sizeof(RJump), "tile scratch in the ruler state buffer");
         unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
@@ -2509,14 +2509,16 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         if (rank_async) {  // no read-back: the checks ride on the scalar read after the starts
             k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
                                                    s->rt_sidx.as<unsigned int>(), s->rt_hasp.as<uint8_t>(),
-                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited, &dsc->chains);
+                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited, &dsc->chains,
+                                                   tbp);
             EC_CHECK(rank_supers_async(s, N, async_M, rounds));
             k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
                                                   s->RK.as<unsigned int>());
         } else if (coop) {
             k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
-                                                   s->rt_sidx.as<unsigned int>());
+                                                   s->rt_sidx.as<unsigned int>(), nullptr, nullptr, nullptr, nullptr,
+                                                   nullptr, tbp);
         } else {
             // the chain count read back while k_tile_compact (sized by the tiles, not by M) runs:
             // the host's wake-up and next launches overlap the compaction
@@ -2526,7 +2528,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             EC_HIP(hipEventRecord(s->rd_ev, st));
             k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
                                                    s->rt_sidx.as<unsigned int>(), s->rt_hasp.as<uint8_t>(),
-                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited);
+                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited, nullptr, tbp);
             EC_CHECK(host_wait(s, s->rd_ev));
             M = (unsigned int)M64;
         }
@@ -2895,7 +2897,9 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
     unsigned long long M = 0;
     EC_CHECK(d2h(s, &M, tbase + ntiles, 8, st));
     EC_CHECK(host_sync(s, st));
-    if (M) k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, d_super, s->rt_sidx.as<unsigned int>());
+    if (M)
+        k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, d_super, s->rt_sidx.as<unsigned int>(), nullptr,
+                                               nullptr, nullptr, nullptr, nullptr, tbp);
     EC_CHECK(host_sync(s, st));
     *n_super = M;
     s->seg_n0 = n0;

@@ -60,6 +60,9 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
     const unsigned int tile = blockIdx.x, tid = threadIdx.x;
     const unsigned int base = tb ? tb[tile] : n0 + tile * RT_TN;
     const unsigned int tend = tb ? tb[tile + 1] : (base + RT_TN < N ? base + RT_TN : N);
+    // the tile's chain records at scratch[soff ..]: a tile's chains <= its nodes, so planned
+    // tiles use their node offset (scratch of N records) and fixed ones tile * RT_TN
+    const uint64_t soff = tb ? (uint64_t)(base - tb[0]) : (uint64_t)tile * RT_TN;
     if (tile == 0 && tid == 0) tcnt[gridDim.x] = 0;  // the scan's last element (no memset launch)
     unsigned int ext[RT_PER];
     unsigned long long fev[RT_PER];
@@ -222,7 +225,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
             r.pad = 0;
             r.fmin = s_cm[i];
             r.pad2 = 0;
-            scratch[(uint64_t)tile * RT_TN + j] = r;
+            scratch[soff + j] = r;
             s_ls[i] = (uint16_t)j;  // (reused: head -> its index among the tile's heads)
         }
         off += tot;
@@ -233,7 +236,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
     for (int q = 0; q < RT_PER; q++) {
         if (!valid[q] || cyc[q]) continue;
         const unsigned int i = tid + q * RT_NT;
-        if (d[q] + 1 == s_cl[p[q]] && ext[q] != NONE32) scratch[(uint64_t)tile * RT_TN + s_ls[p[q]]].succ = ext[q];
+        if (d[q] + 1 == s_cl[p[q]] && ext[q] != NONE32) scratch[soff + s_ls[p[q]]].succ = ext[q];
         (void)i;
     }
     if (tid == 0) tcnt[tile] = off;
@@ -282,12 +285,14 @@ __global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, c
                                                       unsigned int *SIDX, uint8_t *hasp = nullptr,
                                                       uint2 *rid = nullptr, unsigned int *nr = nullptr,
                                                       unsigned long long *nvisited = nullptr,
-                                                      unsigned long long *nchains = nullptr) {
+                                                      unsigned long long *nchains = nullptr,
+                                                      const unsigned int *tb = nullptr) {
     const unsigned int t = blockIdx.x;
     const unsigned int n = (unsigned int)tcnt[t];
     const unsigned long long b = tbase[t];
+    const uint64_t soff = tb ? (uint64_t)(tb[t] - tb[0]) : (uint64_t)t * RT_TN;  // (as k_tile_chains)
     for (unsigned int j = threadIdx.x; j < n; j += blockDim.x) {
-        const SuperRec r = scratch[(uint64_t)t * RT_TN + j];
+        const SuperRec r = scratch[soff + j];
         srec[b + j] = r;
         SIDX[r.head] = (unsigned int)(b + j);
         if (hasp) {
