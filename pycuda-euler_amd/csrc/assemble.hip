@@ -2883,7 +2883,9 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
     }
     EC_CHECK(s->rt_tcnt.ensure(((size_t)ntiles + 1) * 8));
     EC_CHECK(s->rt_tbase.ensure(((size_t)ntiles + 1) * 8));
-    EC_CHECK(s->st1.ensure(std::max<size_t>((size_t)ntiles * RT_TN, 1) * sizeof(SuperRec)));
+    // (planned tiles keep their chain records at node offsets: 2 (hi - lo) records)
+    EC_CHECK(s->st1.ensure(std::max<size_t>(planned ? 2 * (size_t)(hi - lo) : (size_t)ntiles * RT_TN, 1) *
+                           sizeof(SuperRec)));
     unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
     SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);
     if (!ntiles) EC_HIP(hipMemsetAsync(tcnt, 0, 8, st));  // (k_tile_chains zeroes tcnt[ntiles])
