@@ -202,7 +202,7 @@ struct ec_session {
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
-    int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 32), 1 key hash
+    int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 52), 1 key hash
     // ec_export_by_owner's owner ids / scanned chunk histogram of the last call, reused by a
     // following call with the same records, owners and rule (counts first, then the scatter)
     bool own_valid = false;
@@ -451,6 +451,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     s->shard_base = 0;
     s->own_valid = false;
     s->bmark_ok = false;
+    s->seg_marks = 0;  // bucket marks of an earlier call never plan this call's tiles
     const bool timing = (flags & (EC_FLAG_TIMING | EC_FLAG_KERNEL_TIMING)) != 0;
     s->stage_timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
@@ -1426,10 +1427,13 @@ int phase_count(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, ui
 // minimizer buckets for the merge / load of 21 <= k <= 32 (shard.h OwnerFn; EULERHIP_MERGE_MIX=1:
 // key-hash buckets and owners, the round-1 layout)
 bool merge_sk(int k) { return k >= SK_MIN_K && k <= 32 && !kn().merge_mix; }
+// 128-bit keys on minimizer owners (the count's minimizer buckets, count_wide.h)
+bool merge_wmb(int k) { return k > 32 && k <= WMB_MAX_K && kn().wide_mb != 0 && !kn().merge_mix; }
 OwnerFn owner_fn(int k) {
     OwnerFn f{};
     f.sk = merge_sk(k) ? 1 : 0;
     if (f.sk) f.mc = sk_cfg(k);
+    f.wk = merge_wmb(k) ? k : 0;
     return f;
 }
 
@@ -2014,6 +2018,46 @@ int phase_count_w(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off, 
     return finish_wide(s, cap, limit, U, sidx);
 }
 
+// The owner merge's dense set (U ids in table order) reordered by minimizer (shard.h k_wplace /
+// k_wpermute), the minimizers' first ids marked for the partitioned finish's tiles: the
+// gathered ids of 128-bit keys get the locality minimizer owners give (round 5)
+int order_by_minimizer_w(ec_session *s, unsigned int U) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    if (!U) return EC_OK;
+    EC_CHECK(s->skeys.ensure((size_t)U * 8));
+    EC_CHECK(s->skeys2.ensure((size_t)U * 8));
+    EC_CHECK(s->svals.ensure((size_t)U * 4));
+    EC_CHECK(s->svals2.ensure((size_t)U * 4));
+    k_wplace<<<grid_for(U, B), B, 0, st>>>(s->dkey.as<K128>(), U, s->k, s->skeys.as<unsigned long long>(),
+                                           s->svals.as<unsigned int>());
+    EC_CHECK(sort_pairs(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(),
+                        s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), U));
+    // permuted into the count-phase record buffers (free on the owner side), then swapped in
+    EC_CHECK(s->recs.ensure((size_t)U * sizeof(K128)));
+    EC_CHECK(s->recs2.ensure((size_t)U * 16));
+    EC_CHECK(s->mbid2.ensure((size_t)U * 4));
+    unsigned long long *nfc = s->recs2.as<unsigned long long>(), *nft = nfc + U;
+    k_wpermute<<<grid_for(U, B), B, 0, st>>>(s->svals2.as<unsigned int>(), U, s->dkey.as<K128>(),
+                                             s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                                             s->dft.as<unsigned long long>(), s->recs.as<K128>(),
+                                             s->mbid2.as<unsigned int>(), nfc, nft);
+    std::swap(s->dkey, s->recs);
+    std::swap(s->dcnt, s->mbid2);
+    EC_CHECK(s->dfc.ensure((size_t)U * 8));
+    EC_CHECK(s->dft.ensure((size_t)U * 8));
+    EC_HIP(hipMemcpyAsync(s->dfc.p, nfc, (size_t)U * 8, hipMemcpyDeviceToDevice, st));
+    EC_HIP(hipMemcpyAsync(s->dft.p, nft, (size_t)U * 8, hipMemcpyDeviceToDevice, st));
+    if (kn().tile_plan != 0) {
+        const unsigned int words = U / 32 + 2;
+        EC_CHECK(s->bmark.ensure((size_t)words * 4));
+        k_wmarks<<<grid_for(words, B), B, 0, st>>>(s->skeys2.as<unsigned long long>(), U, s->bmark.as<unsigned int>(),
+                                                   words);
+        s->seg_marks = U;
+    }
+    return EC_OK;
+}
+
 int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndexW &sidx) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
@@ -2038,7 +2082,13 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
         cap <<= 2;
         s->stats.table_retries++;
     }
-    return finish_wide(s, cap, limit, U, sidx);
+    EC_CHECK(finish_wide(s, cap, limit, U, sidx));
+    // an owner merge (no lookup index wanted) on minimizer owners: ids in minimizer order
+    if (s->no_index && s->owner_rule == 0 && merge_wmb(s->k) && !(s->flags & EC_FLAG_GENERAL)) {
+        EC_CHECK(order_by_minimizer_w(s, U));
+        sidx.table = nullptr;  // (the table's ids are the pre-order ones)
+    }
+    return EC_OK;
 }
 
 // Links by the (k-1)-mer half-edge join (join_w.h), 128-bit (OpsW) or 64-bit (Ops64) keys.
@@ -2483,7 +2533,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(s->rt_sidx.ensure(Nn * 4));
         EC_CHECK(s->rt_lr.ensure(Nn * 4));
         unsigned int *LH = s->pred.as<unsigned int>(), *LR = s->rt_lr.as<unsigned int>();  // (pred: free here)
-        // (a tile's chains at scratch[tile * RT_TN ..]: planned tiles are more than N / RT_TN)
+        // (a planned tile keeps its chain records at its first node's offset, tb[t] - tb[0]: its
+        // chains fit in its nodes, so N records suffice; fixed tiles at scratch[tile * RT_TN ..])
         EC_CHECK(s->st1.ensure(std::max<size_t>(Nn, planned ? 0 : (size_t)ntiles * RT_TN) * sizeof(RJump)));
         SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);  // (dead before the Wyllie rounds)
         static_assert(sizeof(SuperRec) == sizeof(RJump), "tile scratch in the ruler state buffer");
@@ -3455,7 +3506,11 @@ int ec_session_set_stream(ec_session *s, void *hip_stream) {
 int ec_session_destroy(ec_session *s) {
     if (!s) return EC_OK;
     hipSetDevice(s->device);
+    // every stream that may still copy into / out of the session's buffers (the speculative
+    // contig copy on ostream, staged batches on cstream) drains before anything is released
     if (s->stream) hipStreamSynchronize(s->stream);
+    if (s->ostream) hipStreamSynchronize(s->ostream);
+    if (s->cstream) hipStreamSynchronize(s->cstream);
     DevBuf *all[] = {&s->h_reads, &s->h_offsets, &s->hll, &s->scal, &s->table, &s->dkey, &s->dcnt, &s->dfc, &s->dft,
                      &s->upal, &s->outdeg, &s->cand, &s->succ, &s->pred, &s->st0, &s->st1, &s->startOf, &s->skeys,
                      &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
@@ -3759,7 +3814,7 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
     unsigned int *bh = s->ocnt.as<unsigned int>(), *bhi = bh + nbh;
     const bool wide = s->k > 32;
     OwnerFn own = owner_fn(s->k);
-    if (s->owner_rule == 1) own.sk = 0;  // key-hash owners (a skewed minimizer distribution)
+    if (s->owner_rule == 1) own.sk = 0, own.wk = 0;  // key-hash owners (a skewed minimizer distribution)
     EC_CHECK(s->mbid.ensure(std::max<uint64_t>(n, 1) * 4));  // owner of each record (free until a merge)
     unsigned int *oid = s->mbid.as<unsigned int>();
     const bool reuse = s->own_valid && s->own_rule == s->owner_rule && s->own_nowners == nowners && s->own_n == n &&
@@ -3877,7 +3932,10 @@ int ec_graph_load(ec_session *s, const void *d_records, uint64_t n, int k, unsig
         return EC_ERR_ARG;
     }
     s->graph_loaded = false;
+    // the owner merge's bucket marks (this rank's segment of the set loaded here) outlive the load
+    const uint64_t marks = s->seg_marks;
     EC_CHECK(begin_call(s, k, flags));
+    s->seg_marks = marks;
     unsigned int U = 0;
     if (k > 32)
         EC_CHECK(phase_load_det_w(s, reinterpret_cast<const AggW *>(d_records), n, U, s->gidxw));

@@ -1592,3 +1592,361 @@ extern "C" int ec_partial_contigs(const void *ev, uint64_t vcount, const void *e
     *n_chars = total;
     return EC_OK;
 }
+
+// ---- Shiloach-Vishkin steps of find_component_device, one launch each (round 5) ---------------
+// src/pycomponent.py:16-665: the ten step kernels the reference's component loop is made of,
+// exposed step by step (ec_component_step) with the reference's arguments and in-place
+// semantics.  Every step is elementwise over tid < length; the atomics of steps 2/3 (P2) are
+// minima and same-value stores, so the result does not depend on thread order.  Indices the
+// reference would read out of bounds (a D / prevD / val entry >= length) are skipped.
+namespace ec {
+enum SvStep : int {
+    SV_INIT = 0,      // componentStepInit (:34-43): D = tid, Q = 0
+    SV_S1P1 = 1,      // componentStepOne_ShortCuttingP1 (:87-94): D = prevD[prevD]
+    SV_S1P2 = 2,      // componentStepOne_ShortCuttingP2 (:148-158): D != prevD -> Q[D] = s
+    SV_S2P1 = 3,      // componentStepTwoP1 (:212-242): hook candidates of unchanged roots
+    SV_S2P2 = 4,      // componentStepTwoP2 (:301-330): atomicMin(D + t, val), Q[val] = s
+    SV_S3P1 = 5,      // componentStepThreeP1 (:394-414): hook candidates of stagnant stars
+    SV_S3P2 = 6,      // componentStepThreeP2 (:474-494): atomicMin(D + t, val)
+    SV_S4P1 = 7,      // componentStepFourP1 (:548-553): val1 = D[D]
+    SV_S4P2 = 8,      // componentStepFourP2 (:595-601): D = val1
+    SV_S5 = 9,        // componentStepFive (:638-646): any Q == s -> *sptemp = 1
+};
+
+__global__ void __launch_bounds__(256) k_sv_step(int step, const Vtx *v, const unsigned int *prevD, unsigned int *D,
+                                                 unsigned int *Q, unsigned int *t1, unsigned int *val1,
+                                                 unsigned int *t2, unsigned int *val2, unsigned int *sptemp,
+                                                 unsigned int n, unsigned int s) {
+    for (unsigned int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        switch (step) {
+        case SV_INIT:
+            D[t] = t;
+            Q[t] = 0;
+            break;
+        case SV_S1P1: {
+            const unsigned int p = prevD[t];
+            if (p < n) D[t] = prevD[p];
+            break;
+        }
+        case SV_S1P2:
+            if (D[t] != prevD[t] && D[t] < n) Q[D[t]] = s;
+            break;
+        case SV_S2P1:
+        case SV_S3P1: {
+            const unsigned int d = D[t];
+            t1[t] = n;
+            t2[t] = n;
+            bool live;
+            if (step == SV_S2P1) live = d == prevD[t];
+            else live = d < n && d == D[d] && Q[d] < s;
+            if (!live) break;
+            const unsigned int nb[2] = {v[t].n1, v[t].n2};
+            for (int q = 0; q < 2; q++) {
+                if (nb[q] >= n) continue;
+                const unsigned int dn = D[nb[q]];
+                if (step == SV_S2P1 ? dn < d : dn != d) {
+                    (q ? t2 : t1)[t] = d;
+                    (q ? val2 : val1)[t] = dn;
+                }
+            }
+            break;
+        }
+        case SV_S2P2:
+        case SV_S3P2:
+            for (int q = 0; q < 2; q++) {
+                const unsigned int a = (q ? t2 : t1)[t], val = (q ? val2 : val1)[t];
+                if (a >= n) continue;
+                atomicMin(D + a, val);
+                if (step == SV_S2P2 && val < n) Q[val] = s;  // (atomicExch of one value s)
+            }
+            break;
+        case SV_S4P1: {
+            const unsigned int d = D[t];
+            if (d < n) val1[t] = D[d];
+            break;
+        }
+        case SV_S4P2:
+            D[t] = val1[t];
+            break;
+        case SV_S5:
+            if (Q[t] == s) *sptemp = 1;  // (atomicExch of one value)
+            break;
+        }
+    }
+}
+
+// calculateCircuitGraphVertexData (src/pyeulertour.py:223-231): C[D[tid]] = 1
+__global__ void __launch_bounds__(256) k_circuit_mark_checked(const unsigned int *D, uint64_t n, unsigned int *C,
+                                                              uint64_t nc, unsigned int *bad) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        if (D[t] < nc) C[D[t]] = 1;
+        else atomicOr(bad, 1u);
+    }
+}
+// constructCircuitGraphVertex (:280-288): cv[offset[tid]] = tid where C[tid] != 0
+__global__ void __launch_bounds__(256) k_cg_vertex(const unsigned int *C, const unsigned int *offset, unsigned int n,
+                                                   unsigned int *cv, unsigned int ncv) {
+    for (unsigned int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+        if (C[t] != 0 && offset[t] < ncv) cv[offset[t]] = t;
+}
+
+// calculateCircuitGraphEdgeData (:331-371) / assignCircuitGraphEdgeData (:428-469), per vertex:
+// the candidate circuit-graph edges (consecutive entering edges on different circuits) in
+// the order a sequential run of the kernel's threads meets them (vertex, then entry index)
+__device__ inline bool cg_pair(const unsigned int *e, const unsigned int *D, const unsigned int *map, unsigned int E,
+                               unsigned int nmap, unsigned int index, unsigned int &c1, unsigned int &c2) {
+    if (index + 1 >= E || e[index] >= E || e[index + 1] >= E) return false;
+    const unsigned int d1 = D[e[index]], d2 = D[e[index + 1]];
+    if (d1 >= nmap || d2 >= nmap) return false;
+    c1 = map[d1];
+    c2 = map[d2];
+    return c1 != c2;
+}
+__global__ void __launch_bounds__(256) k_cg_count(const EulerVertex *ev, unsigned int vcount, const unsigned int *e,
+                                                  const unsigned int *D, const unsigned int *map, unsigned int E,
+                                                  unsigned int nmap, unsigned int *per_vertex,
+                                                  unsigned int *cedge_count, unsigned int ngroups, unsigned int *bad) {
+    for (unsigned int t = blockIdx.x * blockDim.x + threadIdx.x; t < vcount; t += gridDim.x * blockDim.x) {
+        const EulerVertex v = ev[t];
+        unsigned int c = 0;
+        if (v.ecount > 0) {
+            const unsigned int maxIndex = v.ep + v.ecount - 1;
+            for (unsigned int index = v.ep; index < maxIndex && index < E; index++) {
+                unsigned int c1, c2;
+                if (!cg_pair(e, D, map, E, nmap, index, c1, c2)) continue;
+                c++;
+                if (cedge_count) {  // (atomicInc(.., ecount): the count stays below its bound)
+                    if (min(c1, c2) < ngroups) atomicAdd(cedge_count + min(c1, c2), 1u);
+                    else atomicOr(bad, 1u);
+                }
+            }
+        }
+        if (per_vertex) per_vertex[t] = c;
+    }
+}
+// the candidates of vertex t at slots base[t] .. (exclusive scan of k_cg_count's per-vertex
+// counts): key = the group c = min(c1, c2), value = the candidate's sequential position
+__global__ void __launch_bounds__(256) k_cg_list(const EulerVertex *ev, unsigned int vcount, const unsigned int *e,
+                                                 const unsigned int *D, const unsigned int *map, unsigned int E,
+                                                 unsigned int nmap, const unsigned int *base, unsigned int *gkey,
+                                                 unsigned int *gpos, uint4 *cand) {
+    for (unsigned int t = blockIdx.x * blockDim.x + threadIdx.x; t < vcount; t += gridDim.x * blockDim.x) {
+        const EulerVertex v = ev[t];
+        unsigned int o = base[t];
+        if (v.ecount == 0) continue;
+        const unsigned int maxIndex = v.ep + v.ecount - 1;
+        for (unsigned int index = v.ep; index < maxIndex && index < E; index++) {
+            unsigned int c1, c2;
+            if (!cg_pair(e, D, map, E, nmap, index, c1, c2)) continue;
+            gkey[o] = min(c1, c2);
+            gpos[o] = o;
+            cand[o] = make_uint4(e[index], e[index + 1], min(c1, c2), max(c1, c2));
+            o++;
+        }
+    }
+}
+// group-sorted candidates (stable: sequential order inside a group); the r-th candidate of
+// group c takes atomicDec's r-th return, i = count[c] - 1 - r, at cedge[offset[c] + i]
+__global__ void __launch_bounds__(256) k_cg_assign(const unsigned int *skey, const unsigned int *spos, unsigned int nc,
+                                                   const uint4 *cand, const unsigned int *cedge_offset,
+                                                   const unsigned int *cedge_count, unsigned int ngroups,
+                                                   CircuitEdge *cedge, unsigned int cecount) {
+    for (unsigned int j = blockIdx.x * blockDim.x + threadIdx.x; j < nc; j += gridDim.x * blockDim.x) {
+        const unsigned int c = skey[j];
+        if (c >= ngroups) continue;
+        unsigned int lo = 0, hi = j;  // first position of group c (binary search)
+        while (lo < hi) {
+            const unsigned int mid = (lo + hi) / 2;
+            if (skey[mid] < c) lo = mid + 1;
+            else hi = mid;
+        }
+        const unsigned int r = j - lo;
+        if (r >= cedge_count[c]) continue;  // (the reference's atomicDec would wrap)
+        const unsigned int slot = cedge_offset[c] + cedge_count[c] - 1 - r;
+        if (slot >= cecount) continue;
+        const uint4 x = cand[spos[j]];
+        CircuitEdge &o = cedge[slot];
+        o.c1 = x.z;
+        o.c2 = x.w;
+        o.e1 = x.x;
+        o.e2 = x.y;  // (ceid is left as the caller set it, as the reference kernel does)
+    }
+}
+}  // namespace ec
+
+extern "C" {
+
+int ec_component_step(int step, const void *vertices, uint32_t *prevD, uint32_t *D, uint32_t *Q, uint32_t *t1,
+                      uint32_t *val1, uint32_t *t2, uint32_t *val2, uint32_t *sptemp, uint64_t length, uint32_t s) {
+    if (step < SV_INIT || step > SV_S5 || length >= 0xFFFFFFFFull) {
+        set_error("bad component step %d / length %llu", step, (unsigned long long)length);
+        return EC_ERR_ARG;
+    }
+    const uint64_t n = length;
+    // which arrays the step reads (r) / writes (w)
+    const bool need_v = step == SV_S2P1 || step == SV_S3P1;
+    const bool need_prev = step == SV_S1P1 || step == SV_S1P2 || step == SV_S2P1;
+    const bool need_D = step != SV_S5;
+    const bool need_Q = step == SV_INIT || step == SV_S1P2 || step == SV_S2P2 || step == SV_S3P1 || step == SV_S5;
+    const bool need_t = step == SV_S2P1 || step == SV_S2P2 || step == SV_S3P1 || step == SV_S3P2;
+    const bool need_val1 = need_t || step == SV_S4P1 || step == SV_S4P2;
+    const bool need_s5 = step == SV_S5;
+    if (n && ((need_v && !vertices) || (need_prev && !prevD) || (need_D && !D) || (need_Q && !Q) ||
+              (need_t && (!t1 || !t2 || !val2)) || (need_val1 && !val1) || (need_s5 && !sptemp))) {
+        set_error("component step %d: a required array is null", step);
+        return EC_ERR_ARG;
+    }
+    if (!n) return EC_OK;
+    EC_DEV(dv, need_v ? n * sizeof(Vtx) : 16);
+    EC_DEV(dprev, need_prev ? n * 4 : 16);
+    EC_DEV(dD, n * 4);
+    EC_DEV(dQ, n * 4);
+    EC_DEV(dt, need_t ? n * 16 : 16);  // t1, val1, t2, val2
+    EC_DEV(dval1, n * 4);
+    EC_DEV(dsp, 4);
+    unsigned int *dt1 = dt.as<unsigned int>(), *dt2 = dt1 + (need_t ? n : 0), *dval2 = dt2 + (need_t ? n : 0);
+    if (need_v) EC_HIP(hipMemcpy(dv.p, vertices, n * sizeof(Vtx), hipMemcpyHostToDevice));
+    if (need_prev) EC_HIP(hipMemcpy(dprev.p, prevD, n * 4, hipMemcpyHostToDevice));
+    if (need_D && step != SV_INIT) EC_HIP(hipMemcpy(dD.p, D, n * 4, hipMemcpyHostToDevice));
+    if (need_Q && step != SV_INIT) EC_HIP(hipMemcpy(dQ.p, Q, n * 4, hipMemcpyHostToDevice));
+    if (need_t) {  // (P1 leaves val1 / val2 alone where no candidate: their inputs stay)
+        EC_HIP(hipMemcpy(dt1, t1, n * 4, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dt2, t2, n * 4, hipMemcpyHostToDevice));
+        EC_HIP(hipMemcpy(dval2, val2, n * 4, hipMemcpyHostToDevice));
+    }
+    if (need_val1) EC_HIP(hipMemcpy(dval1.p, val1, n * 4, hipMemcpyHostToDevice));
+    if (need_s5) EC_HIP(hipMemcpy(dsp.p, sptemp, 4, hipMemcpyHostToDevice));
+    k_sv_step<<<grid_for(n, 256), 256>>>(step, dv.as<Vtx>(), dprev.as<unsigned int>(), dD.as<unsigned int>(),
+                                        dQ.as<unsigned int>(), dt1, dval1.as<unsigned int>(), dt2, dval2,
+                                        dsp.as<unsigned int>(), (unsigned int)n, s);
+    EC_HIP(hipGetLastError());
+    if (need_D) EC_HIP(hipMemcpy(D, dD.p, n * 4, hipMemcpyDeviceToHost));
+    if (need_Q) EC_HIP(hipMemcpy(Q, dQ.p, n * 4, hipMemcpyDeviceToHost));
+    if (need_t) {
+        EC_HIP(hipMemcpy(t1, dt1, n * 4, hipMemcpyDeviceToHost));
+        EC_HIP(hipMemcpy(t2, dt2, n * 4, hipMemcpyDeviceToHost));
+        EC_HIP(hipMemcpy(val2, dval2, n * 4, hipMemcpyDeviceToHost));
+    }
+    if (need_val1) EC_HIP(hipMemcpy(val1, dval1.p, n * 4, hipMemcpyDeviceToHost));
+    if (need_s5) EC_HIP(hipMemcpy(sptemp, dsp.p, 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+int ec_cg_vertex_data(const uint32_t *D, uint64_t length, uint32_t *C, uint64_t ncount) {
+    if (length && (!D || !C)) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!length) return EC_OK;
+    EC_DEV(dD, length * 4);
+    EC_DEV(dC, ncount * 4);
+    EC_HIP(hipMemcpy(dD.p, D, length * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dC.p, C, ncount * 4, hipMemcpyHostToDevice));
+    EC_DEV(dbad, 4);
+    EC_HIP(hipMemset(dbad.p, 0, 4));
+    k_circuit_mark_checked<<<grid_for(length, 256), 256>>>(dD.as<unsigned int>(), length, dC.as<unsigned int>(), ncount,
+                                                          dbad.as<unsigned int>());
+    unsigned int bad = 0;
+    EC_HIP(hipMemcpy(&bad, dbad.p, 4, hipMemcpyDeviceToHost));
+    if (bad) {
+        set_error("a component label D[i] is outside C[0..%llu)", (unsigned long long)ncount);
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipMemcpy(C, dC.p, ncount * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+int ec_cg_vertices(const uint32_t *C, const uint32_t *offset, uint64_t ecount, uint32_t *cv, uint64_t ncv) {
+    if (ecount && (!C || !offset || (ncv && !cv))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!ecount || !ncv) return EC_OK;
+    EC_DEV(dC, ecount * 4);
+    EC_DEV(dO, ecount * 4);
+    EC_DEV(dcv, ncv * 4);
+    EC_HIP(hipMemcpy(dC.p, C, ecount * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dO.p, offset, ecount * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dcv.p, cv, ncv * 4, hipMemcpyHostToDevice));
+    k_cg_vertex<<<grid_for(ecount, 256), 256>>>(dC.as<unsigned int>(), dO.as<unsigned int>(), (unsigned int)ecount,
+                                               dcv.as<unsigned int>(), (unsigned int)ncv);
+    EC_HIP(hipMemcpy(cv, dcv.p, ncv * 4, hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+// calculateCircuitGraphEdgeData (cedge_count += per group) when cedge is null, else
+// assignCircuitGraphEdgeData (cedge_count read-only: the reference passes it drv.In)
+int ec_cg_edges_step(const void *ev, uint64_t vcount, const uint32_t *e, const uint32_t *D, const uint32_t *map,
+                     uint64_t nmap, uint64_t ecount, const uint32_t *cedge_offset, uint32_t *cedge_count,
+                     uint64_t ngroups, void *cedge, uint64_t cecount) {
+    if ((vcount && !ev) || (ecount && (!e || !D)) || (nmap && !map) || !cedge_count ||
+        (cedge && (!cedge_offset || (cecount && !cedge)))) {
+        set_error("null argument");
+        return EC_ERR_ARG;
+    }
+    if (!vcount || !ecount) return EC_OK;
+    EC_DEV(dev, vcount * sizeof(EulerVertex));
+    EC_DEV(de, ecount * 4);
+    EC_DEV(dD, ecount * 4);
+    EC_DEV(dmap, nmap * 4);
+    EC_DEV(dcnt, ngroups * 4);
+    EC_DEV(dper, vcount * 4);
+    EC_HIP(hipMemcpy(dev.p, ev, vcount * sizeof(EulerVertex), hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(de.p, e, ecount * 4, hipMemcpyHostToDevice));
+    EC_HIP(hipMemcpy(dD.p, D, ecount * 4, hipMemcpyHostToDevice));
+    if (nmap) EC_HIP(hipMemcpy(dmap.p, map, nmap * 4, hipMemcpyHostToDevice));
+    if (ngroups) EC_HIP(hipMemcpy(dcnt.p, cedge_count, ngroups * 4, hipMemcpyHostToDevice));
+    if (!cedge) {  // calculate: the groups' counts added to cedge_count
+        EC_DEV(dbad, 4);
+        EC_HIP(hipMemset(dbad.p, 0, 4));
+        k_cg_count<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), (unsigned int)vcount, de.as<unsigned int>(),
+                                                  dD.as<unsigned int>(), dmap.as<unsigned int>(), (unsigned int)ecount,
+                                                  (unsigned int)nmap, nullptr, dcnt.as<unsigned int>(),
+                                                  (unsigned int)ngroups, dbad.as<unsigned int>());
+        unsigned int bad = 0;
+        EC_HIP(hipMemcpy(&bad, dbad.p, 4, hipMemcpyDeviceToHost));
+        if (bad) {
+            set_error("a circuit id is outside cedgeCount[0..%llu)", (unsigned long long)ngroups);
+            return EC_ERR_ARG;
+        }
+        if (ngroups) EC_HIP(hipMemcpy(cedge_count, dcnt.p, ngroups * 4, hipMemcpyDeviceToHost));
+        return EC_OK;
+    }
+    // assign: the candidates in sequential order, stably sorted by group
+    k_cg_count<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), (unsigned int)vcount, de.as<unsigned int>(),
+                                              dD.as<unsigned int>(), dmap.as<unsigned int>(), (unsigned int)ecount,
+                                              (unsigned int)nmap, dper.as<unsigned int>(), nullptr, 0u, nullptr);
+    EC_DEV(dbase, (vcount + 1) * 4);
+    EC_CHECK(exscan_u32(dper.as<unsigned int>(), dbase.as<unsigned int>(), vcount));
+    unsigned int last = 0, lastc = 0;
+    EC_HIP(hipMemcpy(&last, dbase.as<unsigned int>() + vcount - 1, 4, hipMemcpyDeviceToHost));
+    EC_HIP(hipMemcpy(&lastc, dper.as<unsigned int>() + vcount - 1, 4, hipMemcpyDeviceToHost));
+    const uint64_t nc = (uint64_t)last + lastc;
+    if (!nc) return EC_OK;
+    EC_DEV(dkey, nc * 4);
+    EC_DEV(dpos, nc * 4);
+    EC_DEV(dkey2, nc * 4);
+    EC_DEV(dpos2, nc * 4);
+    EC_DEV(dcand, nc * 16);
+    EC_DEV(doff, ngroups * 4);
+    EC_DEV(dce, cecount * sizeof(CircuitEdge));
+    k_cg_list<<<grid_for(vcount, 256), 256>>>(dev.as<EulerVertex>(), (unsigned int)vcount, de.as<unsigned int>(),
+                                             dD.as<unsigned int>(), dmap.as<unsigned int>(), (unsigned int)ecount,
+                                             (unsigned int)nmap, dbase.as<unsigned int>(), dkey.as<unsigned int>(),
+                                             dpos.as<unsigned int>(), dcand.as<uint4>());
+    size_t bytes = 0;
+    EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, dkey.as<unsigned int>(), dkey2.as<unsigned int>(),
+                                     dpos.as<unsigned int>(), dpos2.as<unsigned int>(), nc, 0, 32, (hipStream_t)0));
+    EC_DEV(tmp, bytes);
+    EC_HIP(rocprim::radix_sort_pairs(tmp.p, bytes, dkey.as<unsigned int>(), dkey2.as<unsigned int>(),
+                                     dpos.as<unsigned int>(), dpos2.as<unsigned int>(), nc, 0, 32, (hipStream_t)0));
+    if (ngroups) EC_HIP(hipMemcpy(doff.p, cedge_offset, ngroups * 4, hipMemcpyHostToDevice));
+    if (cecount) EC_HIP(hipMemcpy(dce.p, cedge, cecount * sizeof(CircuitEdge), hipMemcpyHostToDevice));
+    k_cg_assign<<<grid_for(nc, 256), 256>>>(dkey2.as<unsigned int>(), dpos2.as<unsigned int>(), (unsigned int)nc,
+                                           dcand.as<uint4>(), doff.as<unsigned int>(), dcnt.as<unsigned int>(),
+                                           (unsigned int)ngroups, dce.as<CircuitEdge>(), (unsigned int)cecount);
+    if (cecount) EC_HIP(hipMemcpy(cedge, dce.p, cecount * sizeof(CircuitEdge), hipMemcpyDeviceToHost));
+    return EC_OK;
+}
+
+}  // extern "C"

@@ -8,6 +8,7 @@
 #include "count_global.h"
 #include "wide.h"
 #include "count_part.h"
+#include "graph.h"
 
 namespace ec {
 
@@ -34,15 +35,57 @@ __device__ inline unsigned int owner_of(const K128 &c, unsigned int nowners) { r
 // gathered-set load bucket keys by the same minimizer (SolidIndex::sk): an owner's merged set
 // -- and so its segment of the gathered dense ids -- comes out in bucket order, a node's
 // neighbours mostly share its bucket, and the partitioned links / ranking touch the lookup
-// sub-tables and node arrays with the locality of the one-GPU path.  Other k: a key hash.
+// sub-tables and node arrays with the locality of the one-GPU path.  128-bit keys with
+// 33 <= k <= 52 (round 5): the range of the key's 128-bit minimizer (graph.h minimizer_of_w, the
+// count_wide.h bucket minimizer), and the owner merge emits its set in minimizer order
+// (order_by_minimizer_w), so config 5's gathered ids have the same locality and take the
+// partitioned finish.  Other k: a key hash.
 struct OwnerFn {
     MinCfg mc;
     int sk;
+    int wk = 0;  // 128-bit keys: k when owners are minimizer ranges, 0 for key-hash owners
     __device__ inline unsigned int operator()(unsigned long long key, unsigned int n) const {
         return sk ? (unsigned int)(((uint64_t)minimizer_of(key, mc) * n) >> 32) : owner_of(key, n);
     }
-    __device__ inline unsigned int operator()(const K128 &key, unsigned int n) const { return owner_of(key, n); }
+    __device__ inline unsigned int operator()(const K128 &key, unsigned int n) const {
+        return wk ? (unsigned int)(((uint64_t)minimizer_of_w(key, wk) * n) >> 32) : owner_of(key, n);
+    }
 };
+
+// owner merge of 128-bit keys on minimizer owners: the dense set reordered by placement
+// (minimizer << 32 | low half of mix128, graph.h wide_place), each minimizer's first id marked
+// in bmark for the partitioned finish's tile plan (k_tile_plan)
+__global__ void __launch_bounds__(256) k_wplace(const K128 *dkey, unsigned int U, int k, unsigned long long *place,
+                                                unsigned int *idx) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < U; t += (uint64_t)gridDim.x * blockDim.x) {
+        place[t] = wide_place(dkey[t], k, true);
+        idx[t] = (unsigned int)t;
+    }
+}
+__global__ void __launch_bounds__(256) k_wpermute(const unsigned int *perm, unsigned int U, const K128 *ik,
+                                                  const unsigned int *ic, const unsigned long long *ifc,
+                                                  const unsigned long long *ift, K128 *ok, unsigned int *oc,
+                                                  unsigned long long *ofc, unsigned long long *oft) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < U; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int j = perm[t];
+        ok[t] = ik[j];
+        oc[t] = ic[j];
+        ofc[t] = ifc[j];
+        oft[t] = ift[j];
+    }
+}
+// one thread per 32 ids: bit i of bmark set iff id i starts a minimizer (sorted placements)
+__global__ void __launch_bounds__(256) k_wmarks(const unsigned long long *place, unsigned int U, unsigned int *bmark,
+                                                unsigned int words) {
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < words; w += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned int m = 0;
+        for (unsigned int b = 0; b < 32; b++) {
+            const uint64_t i = w * 32 + b;
+            if (i < U && (i == 0 || (place[i] >> 32) != (place[i - 1] >> 32))) m |= 1u << b;
+        }
+        bmark[w] = m;
+    }
+}
 
 // the exchange record of a key type: Agg (64-bit keys) or AggW (K128)
 template <typename K> struct RecOf;

@@ -48,7 +48,7 @@ eulerhip.register("ec_dense_count", ctypes.c_uint64, [_P])
 eulerhip.register("ec_export_by_owner", ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.POINTER(ctypes.c_uint64)])
 eulerhip.register("ec_session_set_owner_rule", ctypes.c_int, [_P, ctypes.c_int])
 
-# owner rules (ec_session_set_owner_rule): minimizer ranges (21 <= k <= 32), or a key hash when
+# owner rules (ec_session_set_owner_rule): minimizer ranges (21 <= k <= 52), or a key hash when
 # the job's minimizer-range counts are skewed past SKEW times the mean owner (low-complexity input:
 # one minimizer can own most records; the merge then falls to the HBM table and every rank pays
 # the all-gather padding of the largest part)
@@ -56,9 +56,15 @@ OWNER_MINIMIZER, OWNER_HASH = 0, 1
 SKEW = 2.0
 
 
+def minimizer_owners(k):
+    """k with minimizer-range owners under OWNER_MINIMIZER (shard.h OwnerFn: 64-bit keys from
+    k = 21, 128-bit keys up to count_wide.h's WMB_MAX_K = 52); other k use key-hash owners"""
+    return 21 <= k <= 52
+
+
 def owner_rule_for(totals, k):
     """the rule every rank takes, from the all-reduced per-owner record counts"""
-    if not 21 <= k <= 32 or len(totals) < 2:
+    if not minimizer_owners(k) or len(totals) < 2:
         return OWNER_MINIMIZER
     mean = sum(totals) / len(totals)
     return OWNER_HASH if mean > 0 and max(totals) > SKEW * mean else OWNER_MINIMIZER
@@ -342,12 +348,13 @@ def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None):
 
 def finish_mode(finish, k, rule):
     """"auto": the partitioned finish where the gathered ids have minimizer locality (21 <= k <=
-    32 on minimizer owners: a segment's chains are ~1/9 of its nodes), else the replicated one
-    (on hash-ordered ids every node is its own chain and the all-gathered chain records would
+    52 on minimizer owners: a segment's chains are a fraction of its nodes; 128-bit keys since
+    round 5, the owner merge emitting its set in minimizer order), else the replicated one (on
+    hash-ordered ids every node is its own chain and the all-gathered chain records would
     outweigh the successor array 8 : 1)"""
     if finish != "auto":
         return finish
-    return "partitioned" if 21 <= k <= 32 and rule == OWNER_MINIMIZER else "replicated"
+    return "partitioned" if minimizer_owners(k) and rule == OWNER_MINIMIZER else "replicated"
 
 
 def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1, flags=0, on_count=None,
@@ -358,8 +365,10 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     fetch = False: the result stays in the engine's session (result None; bench.py, like the
     single-GPU step, which ends with the results in pinned host buffers).
     partitioned (default, unless EC_FLAG_GENERAL): each rank computes the successor links of its own owner
-    segment of the gathered solid set only ("each GPU builds its local graph partition");
-    the parts are all-gathered and every rank ranks the paths and emits the contigs."""
+    segment of the gathered solid set only ("each GPU builds its local graph partition").
+    finish "partitioned" (the "auto" choice where the ids have minimizer locality): every rank
+    ranks / emits its own segment and ONLY RANK 0 returns the result (None on the others);
+    "replicated": the successor parts are all-gathered and every rank returns the result."""
     import time
 
     if partitioned is None:
@@ -374,7 +383,7 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     if on_count:
         on_count(st)
     rule = OWNER_MINIMIZER
-    if comm.world > 1 and 21 <= k <= 32:  # one owner rule for every rank, from the job's counts
+    if comm.world > 1 and minimizer_owners(k):  # one owner rule for every rank, from the job's counts
         engine.set_owner_rule(OWNER_MINIMIZER)
         rule = owner_rule_for(comm.allreduce_vec(engine.owner_counts(comm.world)), k)
         if rule != OWNER_MINIMIZER:
@@ -501,7 +510,7 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
         eng.count_variant = int(st.count_variant)
         P += st.n_positions
     rule = OWNER_MINIMIZER
-    if world > 1 and 21 <= k <= 32:  # as sharded_assemble: the summed owner counts decide the rule
+    if world > 1 and minimizer_owners(k):  # as sharded_assemble: the summed owner counts decide the rule
         for eng in engines:
             eng.set_owner_rule(OWNER_MINIMIZER)
         rule = owner_rule_for([sum(c) for c in zip(*[eng.owner_counts(world) for eng in engines])], k)

@@ -58,10 +58,24 @@ def minimizer_of(c, k, m=15):
     return _min_remix(v)
 
 
+def minimizer_of_w(c, k, m=15):
+    """graph.h minimizer_of_w: minimizer of a 128-bit code c (< 4^k), remixed by min_remix_w"""
+    mm = (1 << (2 * m)) - 1
+    v = M32
+    for p in range(k - m + 1):
+        f = (c >> (2 * (k - m - p))) & mm
+        r = _rev2_32(f ^ mm) >> (32 - 2 * m)
+        v = min(v, _mmer_hash(min(f, r)))
+    return ((v >> 20) | (v << 12)) & M32
+
+
 def owner_fn(key, n, k, rule=0):
-    """shard.h OwnerFn: the minimizer's range for 21 <= k <= 32 (rule 0), else the key hash"""
+    """shard.h OwnerFn: the minimizer's range for 21 <= k <= 52 (rule 0), else the key hash
+    (64-bit keys; the 128-bit key hash is wide.h owner_of_w, not restated here)"""
     if 21 <= k <= 32 and rule == 0:
         return (minimizer_of(key, k) * n) >> 32
+    if 32 < k <= 52 and rule == 0:
+        return (minimizer_of_w(key, k) * n) >> 32
     return owner_of(key, n)
 
 

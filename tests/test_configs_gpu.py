@@ -172,3 +172,76 @@ def test_ecoli10m_err_vs_oracle(gpu_session):
     assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
     assert np.array_equal(res.link_offsets, ref["link_offsets"])
     assert np.array_equal(res.link_codes, ref["links"])
+
+
+# ---- BASELINE config 4: the headline read set read-sharded over 8 ranks ----------------------
+@pytest.fixture(scope="module")
+def engines8():
+    import distributed
+
+    es = [distributed.HipEngine(0) for _ in range(8)]
+    yield es
+    for e in es:
+        e.sess.close()
+
+
+@pytest.mark.parametrize("finish", ["partitioned", "replicated"])
+def test_config4_sharded_8_ranks_contig_is_the_genome(engines8, finish):
+    """BASELINE configs[3]: E. coli 10 M x 100 bp, k = 31, read-sharded over 8 ranks (8 simulated
+    HipEngines on one GPU: every rank's count / export / owner merge / load / partitioned links
+    and finish, the collectives by concatenation -- distributed.local_sharded_assemble, the same
+    engine calls sharded_assemble makes over RCCL).  Size-independent properties of the
+    error-free repeat-free genome: every genome k-mer is solid, the one contig is the genome or
+    its reverse complement, no GFA links (src/cli_spark_gpu.py:37, src/ref_spark.py:76-88)"""
+    import distributed
+
+    G, k, seed = 4_600_000, 31, 20261015 + 4
+    buf, off = make_reads(G, 10_000_000, 100, seed)
+    res, P = distributed.local_sharded_assemble(engines8, buf, off, k, 1, finish=finish)
+    del buf, off
+    assert distributed.local_sharded_assemble_shards.last_rule == distributed.OWNER_MINIMIZER
+    st = res.stats
+    assert P == 700_000_000
+    assert st.n_solid == G - k + 1
+    assert st.n_dict == 2 * (G - k + 1)
+    assert st.n_contigs == 1
+    genome = make_genome(G, seed)
+    c = res.contig_bytes
+    assert c == genome or c == genome.translate(COMP)[::-1]
+    assert st.n_links == 0
+
+
+@pytest.mark.parametrize("finish", ["partitioned", "replicated"])
+def test_config2_sharded_8_ranks_vs_oracle(engines8, finish):
+    """BASELINE configs[1] (4.6 Mbp, 1 M x 100 bp, k = 31) read-sharded over 8 simulated ranks,
+    bit-exact against the oracle: contigs, offsets, GFA links and dict size"""
+    import distributed
+
+    buf, off = make_reads(4_600_000, 1_000_000, 100, 20261015 + 2)
+    ref = oracle.assemble_packed(buf, off, 31, 1)
+    res, P = distributed.local_sharded_assemble(engines8, buf, off, 31, 1, finish=finish)
+    assert P == ref["n_positions"] == 70_000_000
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert np.array_equal(res.link_offsets, ref["link_offsets"])
+    assert np.array_equal(res.link_codes, ref["links"])
+
+
+def test_config4_err_sharded_8_ranks_vs_oracle(engines8):
+    """the headline read set with 0.5 % substitutions (1.3 * 10^7 solid k-mers in ~10^6 contigs,
+    so GFA links everywhere) read-sharded over 8 simulated ranks, bit-exact vs the oracle"""
+    import os
+
+    import distributed
+
+    buf, off = make_reads(4_600_000, 10_000_000, 100, 20261015 + 4, err=0.005)
+    th = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    ref = oracle.assemble_packed(buf, off, 31, 1, threads=th)
+    res, P = distributed.local_sharded_assemble(engines8, buf, off, 31, 1)
+    assert P == ref["n_positions"] == 700_000_000
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert np.array_equal(res.link_offsets, ref["link_offsets"])
+    assert np.array_equal(res.link_codes, ref["links"])

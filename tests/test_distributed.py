@@ -1,7 +1,9 @@
 """The N > 1 path (pycuda-euler_amd/distributed.py) on CPU: world_size 2 and 3 over gloo, the
 real orchestration and collectives (TorchComm: all-to-all-v, all-gather-v, all-reduce), the
-compute from tests/fake_engine.py.  Every rank must hold the reference's result for the
-whole read set (checked against the oracle, itself pinned to the golden vectors)."""
+compute from tests/fake_engine.py.  Rank 0 (every rank under the replicated finish) must hold
+the reference's result for the whole read set (checked against the oracle, itself pinned to the
+golden vectors); the partitioned finish leaves the other ranks without a result.  Owner-rule
+and exchange checks read every rank's values, whatever its result."""
 import os
 import socket
 import sys
@@ -56,9 +58,11 @@ def _worker(rank, world, port, reads, k, limit, q, partitioned=None, gap=None, w
         dist.destroy_process_group()
 
 
-def _run(reads, k, limit, world, partitioned=None, gap=None, want_counts=False, finish="partitioned"):
-    """every rank's (rank, P, contigs, links[, rule, counts]); with the partitioned finish
-    (the default, partitioned links) only rank 0 holds contigs / links (None elsewhere)"""
+def _run(reads, k, limit, world, partitioned=None, gap=None, want_counts=False, finish="partitioned",
+         all_ranks=False):
+    """(rank, P, contigs, links[, rule, counts]) of the ranks holding a result; all_ranks: of
+    every rank (with the partitioned finish -- the default, partitioned links -- only rank 0
+    holds contigs / links, None elsewhere)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -74,6 +78,8 @@ def _run(reads, k, limit, world, partitioned=None, gap=None, want_counts=False, 
     out = sorted(out, key=lambda o: o[0])
     assert out[0][2] is not None, "rank 0 holds no result"
     part_finish = finish == "partitioned" and partitioned is not False
+    if all_ranks:
+        return out
     return [o for o in out if not (part_finish and o[0] != 0 and o[2] is None)]
 
 
@@ -142,13 +148,16 @@ def test_sharded_skewed_minimizers_take_hash_owners():
             reads.append(g[p:p + 70])
     _, rc, rl = oracle.assemble(reads, 31, 1, want_dict=False)
     world = 3
-    out = _run(reads, 31, 1, world, want_counts=True)
+    out = _run(reads, 31, 1, world, want_counts=True, all_ranks=True)
+    assert len(out) == world
     rules = {o[4] for o in out}
     assert rules == {1}, rules  # every rank switched
-    totals = [sum(o[5][d] for o in out) for d in range(world)]
+    totals = [sum(o[5][d] for o in out) for d in range(world)]  # the job's records per owner
     assert max(totals) <= 2.0 * (sum(totals) / world), totals
+    assert out[0][2] is not None
     for rank, P, contigs, links, _, _ in out:
-        assert contigs == rc and links == rl
+        if contigs is not None:
+            assert contigs == rc and links == rl
 
 
 def test_owner_rule_balanced_input_keeps_minimizers():
@@ -156,5 +165,6 @@ def test_owner_rule_balanced_input_keeps_minimizers():
 
     assert distributed.owner_rule_for([100, 110, 95], 31) == distributed.OWNER_MINIMIZER
     assert distributed.owner_rule_for([300, 10, 5], 31) == distributed.OWNER_HASH
-    assert distributed.owner_rule_for([300, 10, 5], 45) == distributed.OWNER_MINIMIZER  # key hash already
+    assert distributed.owner_rule_for([300, 10, 5], 45) == distributed.OWNER_HASH  # 128-bit minimizers
+    assert distributed.owner_rule_for([300, 10, 5], 55) == distributed.OWNER_MINIMIZER  # key hash already
     assert distributed.owner_rule_for([300], 31) == distributed.OWNER_MINIMIZER

@@ -197,11 +197,11 @@ def test_weak_shards_large_read_base(engines, k):
     assert res.stats.n_dict == ref["n_dict"]
 
 
-@pytest.mark.parametrize("k", [31, 21, 19, 41])
+@pytest.mark.parametrize("k", [31, 21, 19, 41, 51])
 def test_owner_rule_matches_fake_engine(engines, k):
     """ec_export_by_owner puts every record in the segment of shard.h OwnerFn's owner -- the
-    minimizer's range for 21 <= k <= 32, a key hash otherwise -- as tests/fake_engine.py
-    restates it for the gloo tests"""
+    minimizer's range for 21 <= k <= 52 (128-bit keys: minimizer_of_w), a key hash otherwise --
+    as tests/fake_engine.py restates it for the gloo tests"""
     import torch
 
     import distributed
@@ -223,6 +223,9 @@ def test_owner_rule_matches_fake_engine(engines, k):
                 if k <= 32:
                     key = int(raw[i * rb: i * rb + 8].view(np.uint64)[0])
                     assert owner_fn(key, 5, k, rule) == dst
+                elif rule == 0:  # 128-bit key: lo, hi words
+                    lo, hi = (int(x) for x in raw[i * rb: i * rb + 16].view(np.uint64))
+                    assert owner_fn((hi << 64) | lo, 5, k, rule) == dst
             o += c
         assert o * rb == raw.size
     eng.set_owner_rule(0)
