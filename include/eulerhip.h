@@ -277,6 +277,28 @@ int ec_read_lmers_kmers(const uint8_t *buf, uint64_t B, uint32_t L, uint64_t *lm
 int ec_partial_contigs(const void *ev, uint64_t vcount, const void *ee, uint64_t E, uint32_t l, char *chars,
                        uint64_t *coff, uint64_t *n_contigs, uint64_t *n_chars);
 
+/* ---- step-level drop-ins of C1 and T3 (round 5) ------------------------------------------
+ * One Shiloach-Vishkin step kernel of find_component_device (src/pycomponent.py:16-665) over
+ * tid < length, in place on the caller's uint32 host arrays: step 0 componentStepInit (:34),
+ * 1 / 2 ShortCuttingP1 / P2 (:87, :148), 3 / 4 StepTwoP1 / P2 (:212, :301), 5 / 6 StepThreeP1 /
+ * P2 (:394, :474), 7 / 8 StepFourP1 / P2 (:548, :595), 9 StepFive (:638, sets *sptemp = 1).
+ * Arrays a step does not touch may be null.  Replaces component_step_init ..
+ * component_step5 (src/pycomponent.py:16, 66, 126, 187, 277, 369, 450, 529, 576, 625). */
+int ec_component_step(int step, const void *vertices, uint32_t *prevD, uint32_t *D, uint32_t *Q, uint32_t *t1,
+                      uint32_t *val1, uint32_t *t2, uint32_t *val2, uint32_t *sptemp, uint64_t length, uint32_t s);
+/* calculate_circuit_graph_vertex_data_device (src/pyeulertour.py:219): C[D[i]] = 1, i < length
+ * (EC_ERR_ARG if a label is >= ncount) */
+int ec_cg_vertex_data(const uint32_t *D, uint64_t length, uint32_t *C, uint64_t ncount);
+/* construct_circuit_Graph_vertex (src/pyeulertour.py:268): cv[offset[i]] = i where C[i] != 0 */
+int ec_cg_vertices(const uint32_t *C, const uint32_t *offset, uint64_t ecount, uint32_t *cv, uint64_t ncv);
+/* calculate_circuit_graph_edge_data (src/pyeulertour.py:307; cedge null: cedge_count[c] += the
+ * circuit-graph edges of smaller end c) and assign_circuit_graph_edge_data (:393; cedge given:
+ * the r-th edge of group c in sequential thread order at cedge[cedge_offset[c] + cedge_count[c]
+ * - 1 - r], ceid untouched, cedge_count read only).  map = cg_offset (circuit label -> index). */
+int ec_cg_edges_step(const void *ev, uint64_t vcount, const uint32_t *e, const uint32_t *D, const uint32_t *map,
+                     uint64_t nmap, uint64_t ecount, const uint32_t *cedge_offset, uint32_t *cedge_count,
+                     uint64_t ngroups, void *cedge, uint64_t cecount);
+
 /* ---- native read ingest -----------------------------------------------
  * FASTA / FASTQ file -> packed bases + uint64 offsets (the CSR layout ec_assemble_* takes).
  * EC_FASTA_RECORDS: one read per '>' record, lines stripped and joined (SeqIO parse of

@@ -385,3 +385,135 @@ def spanning_forest(cg, E, V):
             parent[max(a, b)] = min(a, b)
             tree.append(j)
     return tree
+
+
+# ---- C1 step kernels (src/pycomponent.py:16-665), restated one by one ----------------------
+SV_INIT, SV_S1P1, SV_S1P2, SV_S2P1, SV_S2P2, SV_S3P1, SV_S3P2, SV_S4P1, SV_S4P2, SV_S5 = range(10)
+
+
+def sv_step(step, v, prevD, D, Q, t1, val1, t2, val2, sptemp, n, s):
+    """One Shiloach-Vishkin step kernel of the reference over tid < n, in place on the given
+    uint32 arrays (elementwise; the P2 atomics are minima / one-value stores, so a sequential
+    pass equals the parallel kernel).  Indices past n, which the reference would read out of
+    bounds, are skipped (the device restatement does the same)."""
+    for t in range(n):
+        if step == SV_INIT:  # componentStepInit (:34-43)
+            D[t] = t
+            Q[t] = 0
+        elif step == SV_S1P1:  # componentStepOne_ShortCuttingP1 (:87-94)
+            if prevD[t] < n:
+                D[t] = prevD[prevD[t]]
+        elif step == SV_S1P2:  # componentStepOne_ShortCuttingP2 (:148-158)
+            if D[t] != prevD[t] and D[t] < n:
+                Q[D[t]] = s
+        elif step in (SV_S2P1, SV_S3P1):  # componentStepTwoP1 (:212-242) / ThreeP1 (:394-414)
+            d = int(D[t])
+            t1[t] = n
+            t2[t] = n
+            live = d == prevD[t] if step == SV_S2P1 else (d < n and d == D[d] and Q[d] < s)
+            if not live:
+                continue
+            for q, nb in enumerate((int(v[t]["n1"]), int(v[t]["n2"]))):
+                if nb >= n:
+                    continue
+                dn = int(D[nb])
+                if (dn < d) if step == SV_S2P1 else (dn != d):
+                    (t2 if q else t1)[t] = d
+                    (val2 if q else val1)[t] = dn
+        elif step in (SV_S2P2, SV_S3P2):  # componentStepTwoP2 (:301-330) / ThreeP2 (:474-494)
+            for a, val in ((int(t1[t]), int(val1[t])), (int(t2[t]), int(val2[t]))):
+                if a >= n:
+                    continue
+                D[a] = min(int(D[a]), val)
+                if step == SV_S2P2 and val < n:
+                    Q[val] = s
+        elif step == SV_S4P1:  # componentStepFourP1 (:548-553)
+            if D[t] < n:
+                val1[t] = D[D[t]]
+        elif step == SV_S4P2:  # componentStepFourP2 (:595-601)
+            D[t] = val1[t]
+        elif step == SV_S5:  # componentStepFive (:638-646)
+            if Q[t] == s:
+                sptemp[0] = 1
+
+
+def sv_components(v):
+    """find_component_device's intended loop (:689-720, with step 5 called as intended, §A6)
+    driven through sv_step; returns D"""
+    n = len(v)
+    D = np.zeros(n, np.uint32)
+    Q = np.zeros(n, np.uint32)
+    prevD = np.zeros(n, np.uint32)
+    t1, t2, val1, val2 = (np.zeros(n, np.uint32) for _ in range(4))
+    sv_step(SV_INIT, v, prevD, D, Q, t1, val1, t2, val2, None, n, 0)
+    s, sp = 1, 1
+    while s == sp:
+        D, prevD = prevD, D
+        for st in (SV_S1P1, SV_S1P2, SV_S2P1, SV_S2P2, SV_S3P1, SV_S3P2, SV_S4P1, SV_S4P2):
+            sv_step(st, v, prevD, D, Q, t1, val1, t2, val2, None, n, s)
+        sp_t = np.zeros(1, np.uint32)
+        sv_step(SV_S5, v, prevD, D, Q, t1, val1, t2, val2, sp_t, n, s)
+        sp += int(sp_t[0])
+        s += 1
+    return D
+
+
+# ---- T3 circuit-graph step kernels (src/pyeulertour.py:219-493) ----------------------------
+def cg_vertex_data(D, C):
+    """calculateCircuitGraphVertexData (:223-231): C[D[tid]] = 1"""
+    C = C.copy()
+    for d in D:
+        C[d] = 1
+    return C
+
+
+def cg_vertices(C, offset, cv):
+    """constructCircuitGraphVertex (:280-288): cv[offset[tid]] = tid where C[tid] != 0"""
+    cv = cv.copy()
+    for t in range(len(C)):
+        if C[t] != 0 and offset[t] < len(cv):
+            cv[offset[t]] = t
+    return cv
+
+
+def _cg_pairs(ev, e, D, mp, E):
+    """the candidate circuit-graph edges in the order a sequential run of the kernel's threads
+    meets them: (c = min, t = max, e1, e2)"""
+    out = []
+    for v in ev:
+        if int(v["ecount"]) == 0:
+            continue
+        idx, mx = int(v["ep"]), int(v["ep"]) + int(v["ecount"]) - 1
+        while idx < mx and idx < E:
+            if idx + 1 < E and int(e[idx]) < E and int(e[idx + 1]) < E:
+                d1, d2 = int(D[e[idx]]), int(D[e[idx + 1]])
+                if d1 < len(mp) and d2 < len(mp):
+                    c1, c2 = int(mp[d1]), int(mp[d2])
+                    if c1 != c2:
+                        out.append((min(c1, c2), max(c1, c2), int(e[idx]), int(e[idx + 1])))
+            idx += 1
+    return out
+
+
+def cg_edge_count(ev, e, D, mp, E, cedge_count):
+    """calculateCircuitGraphEdgeData (:331-371): atomicInc(cedgeCount + min(c1, c2))"""
+    cnt = cedge_count.copy()
+    for c, _, _, _ in _cg_pairs(ev, e, D, mp, E):
+        cnt[c] += 1
+    return cnt
+
+
+def cg_edge_assign(ev, e, D, mp, E, cedge_offset, cedge_count, cg_edge):
+    """assignCircuitGraphEdgeData (:428-469): the r-th candidate of group c (sequential order)
+    takes atomicDec's r-th return, slot offset[c] + count[c] - 1 - r; ceid untouched"""
+    cg = cg_edge.copy()
+    seen = {}
+    for c, t, e1, e2 in _cg_pairs(ev, e, D, mp, E):
+        r = seen.get(c, 0)
+        seen[c] = r + 1
+        if r >= int(cedge_count[c]):
+            continue
+        slot = int(cedge_offset[c]) + int(cedge_count[c]) - 1 - r
+        if slot < len(cg):
+            cg[slot]["c1"], cg[slot]["c2"], cg[slot]["e1"], cg[slot]["e2"] = c, t, e1, e2
+    return cg

@@ -36,6 +36,10 @@ for name, res, args in [
     ("ec_read_lmers_kmers", INT, [P, U64, U32, P, P, ctypes.POINTER(U64), ctypes.POINTER(U64), P,
                                   ctypes.POINTER(U64)]),
     ("ec_partial_contigs", INT, [P, U64, P, U64, U32, P, P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+    ("ec_component_step", INT, [INT, P, P, P, P, P, P, P, P, P, U64, U32]),
+    ("ec_cg_vertex_data", INT, [P, U64, P, U64]),
+    ("ec_cg_vertices", INT, [P, P, U64, P, U64]),
+    ("ec_cg_edges_step", INT, [P, U64, P, P, P, U64, U64, P, P, U64, P, U64]),
 ]:
     eulerhip.register(name, res, args)
 

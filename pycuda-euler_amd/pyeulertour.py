@@ -59,6 +59,59 @@ def construct_successor_graphP2_device(d_ee, d_v, ecount):
     return construct_successor_graph_device(d_ee, d_v, ecount)
 
 
+# ---- circuit-graph step kernels (src/pyeulertour.py:219-493), one device launch each; the
+# reference's arguments, in-place updates and return values.  findEulerDevice runs them fused.
+def _u32v(x):
+    return np.ascontiguousarray(np.asarray(x).reshape(-1), dtype=np.uint32)
+
+
+def _into(dst, src):
+    if dst is not src:
+        np.asarray(dst).reshape(-1)[: src.size] = src
+    return dst
+
+
+def calculate_circuit_graph_vertex_data_device(d_D, d_C, length):
+    """src/pyeulertour.py:219-250 (:223-231): C[D[i]] = 1 for i < length; returns (D, C)"""
+    D, C = _u32v(d_D)[: int(length)], _u32v(d_C)
+    M.call("ec_cg_vertex_data", M.ptr(D), int(length), M.ptr(C), C.size)
+    return d_D, _into(d_C, C)
+
+
+def construct_circuit_Graph_vertex(d_C, d_cg_offset, ecount, d_cv):
+    """src/pyeulertour.py:268-304 (:280-288): cv[offset[i]] = i where C[i] != 0; returns cv"""
+    C, off, cv = _u32v(d_C)[: int(ecount)], _u32v(d_cg_offset)[: int(ecount)], _u32v(d_cv)
+    M.call("ec_cg_vertices", M.ptr(C), M.ptr(off), int(ecount), M.ptr(cv), cv.size)
+    return _into(d_cv, cv)
+
+
+def calculate_circuit_graph_edge_data(d_ev, d_e, vcount, d_D, d_cg_offset, ecount, d_cedgeCount):
+    """src/pyeulertour.py:307-390 (:331-371): per circuit c, the circuit-graph edges whose
+    smaller end is c (consecutive entering edges on different circuits) added to cedgeCount[c];
+    returns cedgeCount"""
+    ev, e, D, mp = _ev(np.asarray(d_ev)[: int(vcount)]), _u32v(d_e), _u32v(d_D), _u32v(d_cg_offset)
+    cnt = _u32v(d_cedgeCount)
+    M.call("ec_cg_edges_step", M.ptr(ev), int(vcount), M.ptr(e), M.ptr(D), M.ptr(mp), mp.size, int(ecount), None,
+           M.ptr(cnt), cnt.size, None, 0)
+    return _into(d_cedgeCount, cnt)
+
+
+def assign_circuit_graph_edge_data(d_ev, d_e, vcount, d_D, d_cg_offset, ecount, d_cg_edge_start, d_cedgeCount,
+                                   circuitVertexSize, d_cg_edge, circuitGraphEdgeCount):
+    """src/pyeulertour.py:393-493 (:428-469): every circuit-graph edge written at
+    cg_edge[cg_edge_start[c] + i] with i = atomicDec's return - 1 on cedgeCount[c] (c = min(c1,
+    c2)); ceid untouched; cedgeCount is an input only (the reference passes it drv.In).  The
+    reference's slot order inside a group is a race; here it is that of a sequential run of its
+    threads (vertex, then entry order).  Returns cg_edge."""
+    ev, e, D, mp = _ev(np.asarray(d_ev)[: int(vcount)]), _u32v(d_e), _u32v(d_D), _u32v(d_cg_offset)
+    start, cnt = _u32v(d_cg_edge_start), _u32v(d_cedgeCount).copy()
+    cg = M.as_struct(np.asarray(d_cg_edge).reshape(-1), M.CE)
+    ng = min(start.size, cnt.size)
+    M.call("ec_cg_edges_step", M.ptr(ev), int(vcount), M.ptr(e), M.ptr(D), M.ptr(mp), mp.size, int(ecount),
+           M.ptr(start), M.ptr(cnt), ng, M.ptr(cg), cg.size)  # (slots bounded by the array)
+    return _copy_fields(d_cg_edge, cg) if isinstance(d_cg_edge, np.ndarray) and d_cg_edge.dtype.names else cg
+
+
 def findEulerDevice(d_ev, d_l, d_e, vcount, d_ee, ecount, d_cg_edge, cg_edgeCount, cg_vertexCount):
     """src/pyeulertour.py:714-792: successors (written into d_ee in place), circuits and the
     circuit graph; returns (cg_edge sorted by (c1, c2), cg_edgeCount, cg_vertexCount)."""

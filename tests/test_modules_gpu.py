@@ -331,3 +331,116 @@ def test_euler_circuit_merge(mods, seed, nseq, n, l):
         sw = et.executeSwipeDevice(ev, Ee, len(ev), work.copy(), E, cg, ncg, tree, len(tree), swipe=True, merge=True)
         assert np.array_equal(sw, R.swipe(ev, Ee, work, R.mark_spanning(cg, tree, E, tree_marks=True)))
         assert len(R.successor_cycles(sw)) == ncomp
+
+
+# ---- step-level drop-ins of C1 / T3 (round 5): pycomponent.component_* and the circuit-graph
+# steps of pyeulertour, each against its restatement in oracle/modules_ref.py
+def _sv_vertices(n, seed, cut=0.03):
+    rng = np.random.default_rng(seed)
+    s = rng.permutation(n).astype(np.uint32)
+    s[rng.random(n) < cut] = n
+    v = np.zeros(n, R.VTX)
+    v["vid"] = np.arange(n)
+    v["n1"] = s
+    v["n2"] = n
+    for i in range(n):
+        if s[i] < n:
+            v[s[i]]["n2"] = i
+    return v
+
+
+@pytest.mark.parametrize("n,seed", [(1, 1), (9, 2), (300, 3), (4000, 4)])
+def test_component_steps_vs_restatement(mods, n, seed):
+    """every SV step kernel (src/pycomponent.py:16-665) on the states the intended loop
+    (:689-720) passes through, in place, against modules_ref.sv_step"""
+    cc = mods[3]
+    v = _sv_vertices(n, seed)
+    rng = np.random.default_rng(seed)
+    # device and reference states side by side
+    st = {k: np.zeros(n, np.uint32) for k in ("D", "Q", "prevD", "t1", "t2", "val1", "val2")}
+    ref = {k: a.copy() for k, a in st.items()}
+    # garbage in val1 / val2: P1 must leave them where it writes no candidate
+    for d in (st, ref):
+        d["val1"][:] = d["val2"][:] = 0
+    junk = rng.integers(0, max(n, 1), n).astype(np.uint32)
+    st["val1"][:] = junk
+    ref["val1"][:] = junk
+    out = cc.component_step_init(v, st["D"], st["Q"], n)
+    assert out[0] is st["D"] and out[1] is st["Q"]
+    R.sv_step(R.SV_INIT, v, ref["prevD"], ref["D"], ref["Q"], ref["t1"], ref["val1"], ref["t2"], ref["val2"], None, n, 0)
+    s, sp = 1, 1
+    calls = [
+        (R.SV_S1P1, lambda: cc.component_step1_shortcutting_p1(v, st["prevD"], st["D"], st["Q"], n, s)),
+        (R.SV_S1P2, lambda: cc.component_step1_shortcutting_p2(v, st["prevD"], st["D"], st["Q"], n, s)),
+        (R.SV_S2P1, lambda: cc.component_Step2_P1(v, st["prevD"], st["D"], st["Q"], st["t1"], st["val1"], st["t2"],
+                                                  st["val2"], n, s)),
+        (R.SV_S2P2, lambda: cc.component_Step2_P2(v, st["prevD"], st["D"], st["Q"], st["t1"], st["val1"], st["t2"],
+                                                  st["val2"], n, s)),
+        (R.SV_S3P1, lambda: cc.component_Step3_P1(v, st["prevD"], st["D"], st["Q"], st["t1"], st["val1"], st["t2"],
+                                                  st["val2"], n, s)),
+        (R.SV_S3P2, lambda: cc.component_Step3_P2(v, st["prevD"], st["D"], st["Q"], st["t1"], st["val1"], st["t2"],
+                                                  st["val2"], n, s)),
+        (R.SV_S4P1, lambda: cc.component_step4_P1(v, st["D"], st["val1"], n)),
+        (R.SV_S4P2, lambda: cc.component_step4_P2(v, st["D"], st["val1"], n)),
+    ]
+    rounds = 0
+    while s == sp:
+        st["D"], st["prevD"] = st["prevD"], st["D"]
+        ref["D"], ref["prevD"] = ref["prevD"], ref["D"]
+        for step, call in calls:
+            call()
+            R.sv_step(step, v, ref["prevD"], ref["D"], ref["Q"], ref["t1"], ref["val1"], ref["t2"], ref["val2"], None,
+                      n, s)
+            for k in st:
+                assert np.array_equal(st[k], ref[k]), (step, k, s)
+        sptemp = np.zeros(1, np.uint32)
+        assert cc.component_step5(st["Q"], n, sptemp, s) is sptemp
+        rsp = np.zeros(1, np.uint32)
+        R.sv_step(R.SV_S5, v, ref["prevD"], ref["D"], ref["Q"], ref["t1"], ref["val1"], ref["t2"], ref["val2"], rsp, n, s)
+        assert sptemp[0] == rsp[0]
+        sp += int(sptemp[0])
+        s += 1
+        rounds += 1
+        assert rounds < 64
+    # the loop run as intended labels the components
+    first = {}
+    want = [first.setdefault(int(d), i) for i, d in enumerate(R.components(v))]
+    first = {}
+    assert [first.setdefault(int(d), i) for i, d in enumerate(st["D"])] == want
+
+
+@pytest.mark.parametrize("l,nreads", [(10, 40), (12, 200), (21, 200)])
+def test_circuit_graph_steps_vs_restatement(kat, mods, l, nreads):
+    """calculate_circuit_graph_vertex_data_device / construct_circuit_Graph_vertex /
+    calculate_circuit_graph_edge_data / assign_circuit_graph_edge_data (src/pyeulertour.py:219-493)
+    one launch each against their restatements, and composed into findEulerDevice's circuit
+    graph"""
+    enc, gh, db, cc, et = mods
+    buf = "".join(kat["g200_reads"][:nreads]).encode()
+    keys, counts, kmers, table, ev, ee, L, Ee, E = _ref_pipeline(buf, l, False)
+    ree, rcg, rcgV = R.find_euler(ev, L, Ee, ee)
+    v = et.construct_successor_graph_device(ree, None, E)
+    D = cc.find_component_device(v, np.zeros(E, np.uint32), E)
+    C = np.zeros(E, np.uint32)
+    D2, C2 = et.calculate_circuit_graph_vertex_data_device(D, C, E)
+    assert C2 is C and np.array_equal(C, R.cg_vertex_data(D, np.zeros(E, np.uint32)))
+    mp = np.concatenate([[0], np.cumsum(C)[:-1]]).astype(np.uint32)
+    cgV = int(mp[-1] + C[-1]) if E else 0
+    assert cgV == rcgV
+    cv = np.zeros(max(cgV, 1), np.uint32)
+    assert et.construct_circuit_Graph_vertex(C, mp, E, cv) is cv
+    assert np.array_equal(cv, R.cg_vertices(C, mp, np.zeros(max(cgV, 1), np.uint32)))
+    cnt = np.zeros(max(cgV, 1), np.uint32)
+    assert et.calculate_circuit_graph_edge_data(ev, Ee, len(ev), D, mp, E, cnt) is cnt
+    assert np.array_equal(cnt, R.cg_edge_count(ev, Ee, D, mp, E, np.zeros(max(cgV, 1), np.uint32)))
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint32)
+    ncg = int(cnt.sum())
+    cg = np.zeros(max(ncg, 1), R.CE)
+    cg["ceid"] = 7  # the kernel leaves ceid alone
+    cnt_in = cnt.copy()
+    got = et.assign_circuit_graph_edge_data(ev, Ee, len(ev), D, mp, E, start, cnt, cgV, cg, ncg)
+    assert got is cg and np.array_equal(cnt, cnt_in)  # cedgeCount is an input (drv.In)
+    want = R.cg_edge_assign(ev, Ee, D, mp, E, start, cnt, np.array([(7, 0, 0, 0, 0)] * max(ncg, 1), R.CE))
+    assert np.array_equal(cg, want)
+    key = lambda a: np.sort(a[:ncg], order=["c1", "c2", "e1", "e2"])[["e1", "e2", "c1", "c2"]]  # noqa: E731
+    assert ncg == len(rcg) and np.array_equal(key(cg), key(rcg))

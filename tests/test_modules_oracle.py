@@ -146,3 +146,58 @@ def test_components_and_swipe():
     assert R.components(vtx).tolist() == [0, 0, 0, 3, 3, 5, 5]
     mark = R.mark_spanning(np.array([(0, 5, 2, 0, 1)], R.CE), [0], 6)
     assert mark.tolist() == [1] * 6
+
+
+def _succ_vertices(n, seed, cut=0.05):
+    rng = np.random.default_rng(seed)
+    s = rng.permutation(n).astype(np.uint32)
+    s[rng.random(n) < cut] = n
+    v = np.zeros(n, R.VTX)
+    v["vid"] = np.arange(n)
+    v["n1"] = s
+    v["n2"] = n
+    for i in range(n):
+        if s[i] < n:
+            v[s[i]]["n2"] = i
+    return v
+
+
+def _partition(D):
+    """component labels -> canonical form (first index of each label)"""
+    first = {}
+    return [first.setdefault(int(d), i) for i, d in enumerate(D)]
+
+
+def test_sv_step_loop_is_components():
+    """find_component_device's intended loop (src/pycomponent.py:689-720, step 5 called as
+    intended) over the restated step kernels labels the same components as the fixpoint"""
+    for n, seed in ((1, 0), (7, 1), (200, 2), (1500, 3)):
+        v = _succ_vertices(n, seed)
+        assert _partition(R.sv_components(v)) == _partition(R.components(v))
+
+
+def test_cg_step_restatements_compose_to_find_euler(kat):
+    """the circuit-graph step kernels restated one by one (src/pyeulertour.py:219-493) give the
+    circuit graph find_euler builds in one piece"""
+    buf = "".join(kat["g200_reads"][:60]).encode()
+    keys, counts, kmers, table, ev, ee, L, Ee, E = _pipeline(buf, 12)
+    ree, rcg, cgV = R.find_euler(ev, L, Ee, ee)
+    vtx = np.zeros(E, R.VTX)
+    vtx["vid"] = ree["eid"].astype(np.uint32)
+    vtx["n1"] = ree["s"]
+    vtx["n2"] = E
+    for i in range(E):
+        if vtx[i]["n1"] < E:
+            vtx[int(vtx[i]["n1"])]["n2"] = vtx[i]["vid"]
+    D = R.components(vtx)
+    C = R.cg_vertex_data(D, np.zeros(E, np.uint32))
+    mp = np.concatenate([[0], np.cumsum(C)[:-1]]).astype(np.uint32)
+    assert int(mp[-1] + C[-1]) == cgV
+    cv = R.cg_vertices(C, mp, np.zeros(cgV, np.uint32))
+    assert list(cv) == [i for i in range(E) if C[i]]
+    cnt = R.cg_edge_count(ev, Ee, D, mp, E, np.zeros(cgV, np.uint32))
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint32)
+    cg = R.cg_edge_assign(ev, Ee, D, mp, E, start, cnt, np.zeros(int(cnt.sum()), R.CE))
+    assert len(cg) == len(rcg)
+    key = lambda a: np.sort(a, order=["c1", "c2", "e1", "e2"])  # noqa: E731
+    assert np.array_equal(key(cg), key(rcg))

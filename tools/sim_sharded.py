@@ -20,6 +20,10 @@ def main():
     ap.add_argument("--reads", type=int, default=10_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--err", type=float, default=0.0, help="substitution rate (bench ecoli10m_err: 0.005)")
+    ap.add_argument("--genome", type=int, default=4_600_000, help="genome length (genome20m_k51 shape: 20000000)")
+    ap.add_argument("--len", type=int, default=100, help="read length (config 5 shape: 150)")
+    ap.add_argument("--k", type=int, default=31, help="node length (config 5: 51, 128-bit keys)")
+    ap.add_argument("--seed", type=int, default=20261019)
     ap.add_argument("--finish", default="partitioned", choices=["partitioned", "replicated"],
                     help="partitioned: every rank ranks / emits its own segment (distributed.partitioned_finish)")
     ap.add_argument("--weak", action="store_true",
@@ -35,11 +39,11 @@ def main():
     shards = []
     if a.weak:
         for r in range(world):
-            buf, off = make_reads(4_600_000, a.reads, 100, 20261019, err=a.err, part=r)
+            buf, off = make_reads(a.genome, a.reads, a.len, a.seed, err=a.err, part=r)
             shards.append((torch.from_numpy(buf).cuda(), torch.from_numpy(off.astype(np.int64)).cuda(), a.reads,
                            r * a.reads))
     else:
-        buf, off = make_reads(4_600_000, a.reads, 100, 20261019, err=a.err)
+        buf, off = make_reads(a.genome, a.reads, a.len, a.seed, err=a.err)
         for r in range(world):
             lo, hi = distributed.shard_range(a.reads, r, world)
             shards.append((torch.from_numpy(np.ascontiguousarray(buf[int(off[lo]):int(off[hi])])).cuda(),
@@ -55,13 +59,13 @@ def main():
         sends = []
         for eng, (d_reads, d_off, n, lo) in zip(engines, shards):
             t0 = time.perf_counter()
-            eng.count_shard(d_reads, d_off, n, lo, 31, 0)
+            eng.count_shard(d_reads, d_off, n, lo, a.k, 0)
             tick("count", t0)
             t0 = time.perf_counter()
             sends.append(eng.export_by_owner(world))
             tick("export", t0)
         solids = []
-        rb = distributed.rec_bytes(31)
+        rb = distributed.rec_bytes(a.k)
         for dst, eng in enumerate(engines):
             parts = []
             for src in range(world):
@@ -70,7 +74,7 @@ def main():
                 parts.append(recs[o:o + counts[dst] * rb])
             recv = torch.cat(parts)
             t0 = time.perf_counter()
-            solids.append(eng.merge_owned(recv, 31, 1, 0))
+            solids.append(eng.merge_owned(recv, a.k, 1, 0))
             tick("merge", t0)
         mx = max(x.numel() for x in solids)
         allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device="cuda")
@@ -81,7 +85,7 @@ def main():
         for r, eng in enumerate(engines):
             lo = sum(nrec[:r])
             t0 = time.perf_counter()
-            eng.graph_load(allsolid, 31)
+            eng.graph_load(allsolid, a.k)
             tick("load", t0)
             t0 = time.perf_counter()
             part = eng.empty(8 * nrec[r])
@@ -99,7 +103,7 @@ def main():
             eulerhip.check(eng.L.ec_graph_finish(eng._h(), ctypes.c_void_p(succ.data_ptr()), eulerhip.EC_FLAG_TIMING))
             tick("finish", t0)
             t0 = time.perf_counter()
-            res = eng.sess.fetch(31)
+            res = eng.sess.fetch(a.k)
             tick("fetch", t0)
             st = eng.stats()
             print("finish stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
@@ -134,7 +138,7 @@ def main():
                 chars = c if chars is None else chars + c
                 ends = e.view(torch.int32) if ends is None else ends + e.view(torch.int32)
             t0 = time.perf_counter()
-            res = engines[0].graph_collect(chars, ends.view(torch.uint8), 31)
+            res = engines[0].graph_collect(chars, ends.view(torch.uint8), a.k)
             tick("collect", t0)
             extra = ", chains gathered %.1f MB (%d), starts %.2f MB, chars %.1f MB" % (
                 supers.numel() / 1e6, M, starts.numel() / 1e6, chars.numel() / 1e6)
