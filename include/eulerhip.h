@@ -393,12 +393,36 @@ int ec_graph_load_links(ec_session *s, const void *d_records, uint64_t n, int k,
                         uint64_t hi, uint32_t *d_succ);
 int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags);
 
+/* JUNCTION-PARTITIONED graph (round 5, csrc/junction.h): no rank holds the job's solid set.
+ * After ec_merge_owned (this rank's owner segment, Ur keys):
+ *   a. ec_graph_place: the segment placed at global canonical ids [lo, lo + Ur) of U (lo = the
+ *      earlier ranks' segment sizes), its palindromes counted into *n_pal, and its (k-1)-mer
+ *      junction records (ec_junction_record_bytes(k): 16 / 24 B, up to 4 Ur) written into d_jrecs
+ *      grouped by the junction's owner (the keys' owner rule), owner_counts[r] records for rank r;
+ *   b. (all-to-all-v of the records) ec_graph_join on everything this rank received (n records):
+ *      the get_contig_forward links (referenceAssembler.py:59-73) of the junctions it owns --
+ *      links of its own nodes kept, the others into d_links (ec_link_record_bytes() = 8 B, up
+ *      to n) grouped by the node's rank, owner_counts[r] for rank r; seg_lo: the nowners + 1
+ *      canonical id bounds of the segments (seg_lo[nowners] = U);
+ *   c. (all-to-all-v of the link records) ec_graph_links_apply: the received links of its nodes.
+ * The segment's successors are then in the session: ec_graph_chains_part takes d_succ = NULL.
+ * Replaces the all-gather + ec_graph_load_links of the solid set (north_star: "redistributes
+ * k-mers by hash prefix before each GPU builds its local graph partition"). */
+int ec_graph_place(ec_session *s, uint64_t lo, uint64_t U, int nowners, void *d_jrecs, uint64_t *owner_counts,
+                   uint64_t *n_pal);
+int ec_graph_join(ec_session *s, const void *d_jrecs, uint64_t n, int nowners, const uint64_t *seg_lo, void *d_links,
+                  uint64_t *owner_counts);
+int ec_graph_links_apply(ec_session *s, const void *d_links, uint64_t n);
+int ec_junction_record_bytes(int k);
+int ec_link_record_bytes(void);
+
 /* partitioned FINISH (round 4): instead of all-gathering the successor parts and ranking /
  * emitting the whole set on every rank (ec_graph_finish), each rank ranks and emits its own
- * segment [lo, hi) of the loaded set (csrc/rank_tile.h):
- *   1. ec_graph_chains_part: its successors' chains ranked in LDS tiles; its chains as super
- *      records (ec_super_record_bytes() = 32 B each, up to 2(hi-lo)) into d_super, *n_super;
- *   2. ec_graph_rank_supers: every rank, on ALL ranks' super records concatenated in rank
+ * segment [lo, hi) (a placed segment, or one of a loaded set) (csrc/rank_tile.h):
+ *   1. ec_graph_chains_part: its successors' chains ranked in LDS tiles (d_succ: the segment's
+ *      successors, or NULL for a placed segment, which holds them); its chains as super
+ *      records (ec_super_record_bytes() = 32 B, up to 2(hi-lo)) into d_super, *n_super;
+ *   2. ec_graph_rank_supers: every rank, on ALL super records (all-gathered, rank order) -- the
  *      order (n of them): the chains' list ranking (weighted ruling set);
  *   3. ec_graph_starts_part: its nodes' path keys / ranks, its contig starts as start records
  *      (ec_start_record_bytes() = 48 B, up to 2(hi-lo)) into d_starts, *n_starts (have_supers:
@@ -406,18 +430,20 @@ int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags);
  *   4. ec_graph_layout: every rank, on ALL start records (any order, n): contig order by first
  *      event, *n_chars = the job's contig characters;
  *      ec_graph_emit_part: its nodes' characters at their global positions into d_chars
- *      (n_chars bytes, zeroed by the caller) and the contigs' first / last node + 1 it holds
- *      into d_ends (2 * contigs uint32, zeroed) -- summed over the ranks they give every byte
- *      and end exactly once;
- *   5. ec_graph_collect (one rank): the summed characters / ends -> GFA links (all_contigs:90-109)
- *      and the results (ec_copy_*, ec_get_stats). */
+ *      (n_chars bytes, zeroed by the caller) and the k-mer codes of the contigs' first / last
+ *      nodes it holds into d_ends (2 * contigs codes of ec_end_record_bytes(k) = 8 / 16 B,
+ *      zeroed) -- summed over the ranks they give every byte and end exactly once;
+ *   5. ec_graph_collect (one rank): the summed characters / end codes -> GFA links
+ *      (all_contigs:90-109, from the end codes alone) and the results (ec_copy_*,
+ *      ec_get_stats; n_dict = 2 U - n_pal, n_pal = the job's palindromic solid k-mers). */
 int ec_graph_chains_part(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ, void *d_super,
                          uint64_t *n_super);
 int ec_graph_rank_supers(ec_session *s, const void *d_supers, uint64_t n);
 int ec_graph_starts_part(ec_session *s, int have_supers, void *d_starts, uint64_t *n_starts);
 int ec_graph_layout(ec_session *s, const void *d_starts, uint64_t n, uint64_t *n_chars);
-int ec_graph_emit_part(ec_session *s, char *d_chars, uint32_t *d_ends);
-int ec_graph_collect(ec_session *s, const char *d_chars, const uint32_t *d_ends);
+int ec_graph_emit_part(ec_session *s, char *d_chars, void *d_ends);
+int ec_graph_collect(ec_session *s, const char *d_chars, const void *d_ends, uint64_t n_pal);
+int ec_end_record_bytes(int k);
 int ec_super_record_bytes(void);
 int ec_start_record_bytes(void);
 

@@ -40,6 +40,7 @@
 #include "join_w.h"
 #include "extended.h"
 #include "rank_tile.h"
+#include "junction.h"
 
 #include <mutex>
 
@@ -202,6 +203,11 @@ struct ec_session {
     SolidIndex gidx{};          // index of the loaded solid set (ec_graph_load, k <= 32)
     SolidIndexW gidxw{};        // the same for k > 32
     bool graph_loaded = false;  // ec_graph_load held: ec_graph_links_part / ec_graph_finish valid
+    // junction-partitioned graph (junction.h, round 5): the segment placed at its global ids
+    // (ec_graph_place), no global set held; record / outbox scratch of the distributed join
+    bool placed = false;
+    uint64_t seg_lo = 0, seg_Ur = 0;
+    DevBuf jrec, joid, jout, jseg, jcnt;
     int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 52), 1 key hash
     // ec_export_by_owner's owner ids / scanned chunk histogram of the last call, reused by a
     // following call with the same records, owners and rule (counts first, then the scatter)
@@ -452,6 +458,7 @@ int begin_call(ec_session *s, int k, unsigned flags) {
     s->own_valid = false;
     s->bmark_ok = false;
     s->seg_marks = 0;  // bucket marks of an earlier call never plan this call's tiles
+    s->placed = false;
     const bool timing = (flags & (EC_FLAG_TIMING | EC_FLAG_KERNEL_TIMING)) != 0;
     s->stage_timing = (flags & EC_FLAG_TIMING) != 0;
     if (timing && !s->events) {
@@ -2914,10 +2921,12 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
     EC_CHECK(s->pred.ensure(Nn * 4));
     EC_CHECK(s->rt_lr.ensure(Nn * 4));
     EC_CHECK(s->rt_sidx.ensure(Nn * 4));
-    EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
-    if (U) k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<typename Ops::K>(), U, s->k, s->upal.as<uint8_t>(),
-                                                     &dsc->npal);
-    if (n1 > n0)
+    if (!s->placed) {  // (a placed segment has its flags and links already: ec_graph_place / join)
+        EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
+        if (U) k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<typename Ops::K>(), U, s->k, s->upal.as<uint8_t>(),
+                                                         &dsc->npal);
+    }
+    if (n1 > n0 && d_succ)
         EC_HIP(hipMemcpyAsync(s->succ.as<unsigned int>() + n0, d_succ, (size_t)(n1 - n0) * 4, hipMemcpyDeviceToDevice,
                               st));
     // tiles cut at the bucket starts this rank's owner merge marked (its output is this segment)
@@ -3088,7 +3097,7 @@ int part_layout(ec_session *s, const StartRec *d_all, uint64_t nc, uint64_t *n_c
 }
 
 template <typename Ops>
-int part_emit(ec_session *s, char *d_chars, uint32_t *d_ends) {
+int part_emit(ec_session *s, char *d_chars, void *d_ends) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -3108,7 +3117,12 @@ int part_emit(ec_session *s, char *d_chars, uint32_t *d_ends) {
             s->coff.as<unsigned long long>(), n1, s->k, d_chars, std::max<uint64_t>(s->seg_nchars, 1),
             s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
             s->tailOf.as<unsigned int>(), &dsc->skew, n0);
-    if (nc) k_ends_export<<<grid_for(nc, B), B, 0, st>>>(s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), nc, d_ends);
+    // contig ends as k-mer codes (the collecting rank holds no global set): 2 nc codes, each
+    // written by the rank that emitted the node, zeros elsewhere
+    if (nc)
+        k_ends_codes<Ops><<<grid_for(nc, B), B, 0, st>>>(s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), nc,
+                                                         s->dkey.as<typename Ops::K>(), s->k,
+                                                         reinterpret_cast<typename Ops::K *>(d_ends));
     unsigned int bad = 0;
     EC_CHECK(d2h(s, &bad, &dsc->skew, 4, st));
     EC_CHECK(host_sync(s, st));
@@ -3119,30 +3133,28 @@ int part_emit(ec_session *s, char *d_chars, uint32_t *d_ends) {
     return EC_OK;
 }
 
-template <typename Ops, typename Index>
-int part_collect(ec_session *s, const Index &sidx, const char *d_chars, const uint32_t *d_ends) {
+template <typename Ops>
+int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint64_t n_pal) {
+    using K = typename Ops::K;
+    using T = typename EndSlotOf<K>::T;
     hipStream_t st = s->stream;
     const unsigned B = 256;
-    Scalars *dsc = s->scal.as<Scalars>();
     const unsigned int U = (unsigned int)s->n_dense, nc = s->seg_nc;
-    const size_t Nn = std::max<size_t>(2 * (size_t)U, 1), nn = std::max<size_t>(nc, 1);
+    const size_t nn = std::max<size_t>(nc, 1);
     const uint64_t nchars = s->seg_nchars;
-    EC_CHECK(s->cfirst.ensure(nn * 4));
-    EC_CHECK(s->clast.ensure(nn * 4));
-    EC_CHECK(s->headOf.ensure(Nn * 4));
-    EC_CHECK(s->tailOf.ensure(Nn * 4));
+    const K *d_ends = static_cast<const K *>(d_ends_v);
     EC_CHECK(s->lk.ensure(nn * 16 * 8));
     EC_CHECK(s->lcnt.ensure(nn * 2 * 4));
-    EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
-    EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
-    if (nc) {
-        k_heads_from_ends<<<grid_for(nc, B), B, 0, st>>>(d_ends, nc, s->upal.as<uint8_t>(), s->cfirst.as<unsigned int>(),
-                                                         s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
-                                                         s->tailOf.as<unsigned int>());
-        k_gfa<Ops, Index><<<grid_for(nc, B), B, 0, st>>>(sidx, s->dkey.as<typename Ops::K>(), s->upal.as<uint8_t>(),
-                                                         s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(),
-                                                         s->headOf.as<unsigned int>(), s->tailOf.as<unsigned int>(), nc,
-                                                         s->k, s->lk.as<long long>(), s->lcnt.as<unsigned int>());
+    if (nc) {  // GFA links from the contig-end codes (junction.h): a table of 2 nc entries
+        uint64_t cap = 1024;
+        while (cap < 4ull * nc) cap <<= 1;
+        EC_CHECK(s->table.ensure(cap * sizeof(T)));
+        T *t = s->table.as<T>();
+        if (sizeof(K) == 8) k_end_clear64<<<grid_for(cap, B, 8192), B, 0, st>>>(reinterpret_cast<EndSlot64 *>(t), cap);
+        else k_end_clearW<<<grid_for(cap, B, 8192), B, 0, st>>>(reinterpret_cast<EndSlotW *>(t), cap);
+        k_end_insert<Ops><<<grid_for(nc, B), B, 0, st>>>(d_ends, nc, s->k, t, cap - 1);
+        k_gfa_codes<Ops><<<grid_for(nc, B), B, 0, st>>>(d_ends, nc, s->k, t, cap - 1, s->lk.as<long long>(),
+                                                        s->lcnt.as<unsigned int>());
     }
     const unsigned int n2 = 2 * nc;
     EC_CHECK(s->h_coff.resize((size_t)nc + 1));
@@ -3156,8 +3168,6 @@ int part_collect(ec_session *s, const Index &sidx, const char *d_chars, const ui
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
         EC_CHECK(d2h(s, s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, st));
     }
-    unsigned int npal = 0;
-    EC_CHECK(d2h(s, &npal, &dsc->npal, 4, st));
     EC_CHECK(s->h_chars.resize(nchars));
     if (nchars) EC_CHECK(d2h(s, s->h_chars.data(), d_chars, nchars, st));
     EC_CHECK(host_sync(s, st));
@@ -3174,7 +3184,7 @@ int part_collect(ec_session *s, const Index &sidx, const char *d_chars, const ui
     s->stats.n_contigs = nc;
     s->stats.n_contig_chars = nchars;
     s->stats.n_links = nlinks;
-    s->stats.n_dict = 2ull * U - npal;
+    s->stats.n_dict = 2ull * U - n_pal;
     s->have = true;
     s->stats_ok = true;
     return EC_OK;
@@ -3520,7 +3530,8 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv, &s->skrej, &s->bmark, &s->rt_tb};
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv, &s->skrej, &s->bmark, &s->rt_tb,
+                     &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->bounce.release();
@@ -3981,7 +3992,7 @@ int ec_graph_load_links(ec_session *s, const void *d_records, uint64_t n, int k,
 }
 
 int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags) {
-    if (!s || !s->graph_loaded || (s->n_dense && !d_succ)) {
+    if (!s || !s->graph_loaded || s->placed || (s->n_dense && !d_succ)) {
         set_error("ec_graph_finish: no loaded solid set");
         return EC_ERR_ARG;
     }
@@ -4000,7 +4011,9 @@ int ec_graph_finish(ec_session *s, const uint32_t *d_succ, unsigned flags) {
 int ec_graph_chains_part(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ, void *d_super,
                          uint64_t *n_super) {
     refresh_knobs();
-    if (!s || !s->graph_loaded || lo > hi || hi > s->n_dense || !n_super || (hi > lo && (!d_succ || !d_super))) {
+    if (!s || !s->graph_loaded || lo > hi || hi > s->n_dense || !n_super ||
+        (hi > lo && ((!d_succ && !s->placed) || !d_super)) ||
+        (s->placed && (lo != s->seg_lo || hi != s->seg_lo + s->seg_Ur))) {
         set_error("ec_graph_chains_part: no loaded solid set or bad range [%llu, %llu)", (unsigned long long)lo,
                   (unsigned long long)hi);
         return EC_ERR_ARG;
@@ -4038,7 +4051,7 @@ int ec_graph_layout(ec_session *s, const void *d_starts, uint64_t n, uint64_t *n
     return part_layout(s, static_cast<const StartRec *>(d_starts), n, n_chars);
 }
 
-int ec_graph_emit_part(ec_session *s, char *d_chars, uint32_t *d_ends) {
+int ec_graph_emit_part(ec_session *s, char *d_chars, void *d_ends) {
     if (!s || !s->graph_loaded || (s->seg_nchars && !d_chars) || (s->seg_nc && !d_ends)) {
         set_error("ec_graph_emit_part: no layout");
         return EC_ERR_ARG;
@@ -4047,14 +4060,249 @@ int ec_graph_emit_part(ec_session *s, char *d_chars, uint32_t *d_ends) {
     return s->k > 32 ? part_emit<OpsW>(s, d_chars, d_ends) : part_emit<Ops64>(s, d_chars, d_ends);
 }
 
-int ec_graph_collect(ec_session *s, const char *d_chars, const uint32_t *d_ends) {
-    if (!s || !s->graph_loaded || (s->seg_nchars && !d_chars) || (s->seg_nc && !d_ends)) {
+int ec_graph_collect(ec_session *s, const char *d_chars, const void *d_ends, uint64_t n_pal) {
+    if (!s || !s->graph_loaded || (s->seg_nchars && !d_chars) || (s->seg_nc && !d_ends) || 2 * n_pal > 2 * s->n_dense) {
         set_error("ec_graph_collect: no layout");
         return EC_ERR_ARG;
     }
     EC_HIP(hipSetDevice(s->device));
-    return s->k > 32 ? part_collect<OpsW, SolidIndexW>(s, s->gidxw, d_chars, d_ends)
-                     : part_collect<Ops64, SolidIndex>(s, s->gidx, d_chars, d_ends);
+    return s->k > 32 ? part_collect<OpsW>(s, d_chars, d_ends, n_pal) : part_collect<Ops64>(s, d_chars, d_ends, n_pal);
+}
+
+int ec_end_record_bytes(int k) { return k > 32 ? 16 : 8; }
+int ec_junction_record_bytes(int k) { return k > 32 ? (int)sizeof(RecJ) : (int)sizeof(RecJ64); }
+int ec_link_record_bytes(void) { return (int)sizeof(LinkRec); }
+
+}  // extern "C"
+
+// ---- junction-partitioned graph (junction.h) ------------------------------------------------
+// counting sort of n ids (bins 0..nbins-1) -> perm (midx2) and bin starts bstart[0..nbins]
+int bin_sort(ec_session *s, const unsigned int *bid, uint64_t n, unsigned int nbins, unsigned long long *bstart) {
+    hipStream_t st = s->stream;
+    const unsigned int nch = (unsigned int)std::max<uint64_t>((n + CS_CHUNK - 1) / CS_CHUNK, 1);
+    const uint64_t cells = (uint64_t)nbins * nch;
+    EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(2 * cells, 2) * 4));
+    EC_CHECK(s->midx2.ensure(std::max<uint64_t>(n, 1) * 4));
+    unsigned int *hist = s->mbid2.as<unsigned int>(), *incl = hist + cells;
+    if (!n) {
+        EC_HIP(hipMemsetAsync(bstart, 0, (nbins + 1ull) * 8, st));
+        return EC_OK;
+    }
+    k_cs_hist<<<nch, 256, nbins * 4, st>>>(bid, n, nbins, nch, hist);
+    EC_CHECK(scan_incl_u32(s, hist, incl, cells));
+    k_cs_scatter<<<nch, 256, nbins * 4, st>>>(bid, n, nbins, nch, hist, incl, s->midx2.as<unsigned int>());
+    k_cs_bounds<<<grid_for(nbins, 256), 256, 0, st>>>(hist, incl, nbins, nch, bstart);
+    EC_HIP(hipMemcpyAsync(bstart + nbins, &incl[cells - 1], 4, hipMemcpyDeviceToDevice, st));  // (low word)
+    EC_HIP(hipMemsetAsync(reinterpret_cast<unsigned int *>(bstart + nbins) + 1, 0, 4, st));
+    return EC_OK;
+}
+
+template <typename K>
+int graph_place(ec_session *s, uint64_t lo, uint64_t U, int nowners, void *d_out, uint64_t *owner_counts,
+                uint64_t *n_pal) {
+    using R = typename JRecOf<K>::R;
+    using Ops = typename std::conditional<sizeof(K) == 8, Ops64, OpsW>::type;
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const uint64_t Ur = s->n_dense, Uu = std::max<uint64_t>(U, 1);
+    // the merge's dense arrays [0, Ur) -> global ids [lo, lo + Ur) of U-sized arrays
+    EC_CHECK(s->recs.ensure(std::max<uint64_t>(Ur, 1) * sizeof(K)));
+    EC_CHECK(s->recs2.ensure(std::max<uint64_t>(Ur, 1) * 16));
+    EC_CHECK(s->midx.ensure(std::max<uint64_t>(Ur, 1) * 4));
+    unsigned long long *tfc = s->recs2.as<unsigned long long>(), *tft = tfc + Ur;
+    if (Ur) {
+        EC_HIP(hipMemcpyAsync(s->recs.p, s->dkey.p, Ur * sizeof(K), hipMemcpyDeviceToDevice, st));
+        EC_HIP(hipMemcpyAsync(s->midx.p, s->dcnt.p, Ur * 4, hipMemcpyDeviceToDevice, st));
+        EC_HIP(hipMemcpyAsync(tfc, s->dfc.p, Ur * 8, hipMemcpyDeviceToDevice, st));
+        EC_HIP(hipMemcpyAsync(tft, s->dft.p, Ur * 8, hipMemcpyDeviceToDevice, st));
+    }
+    EC_HIP(hipStreamSynchronize(st));  // (ensure() may free the sources below)
+    EC_CHECK(s->dkey.ensure(Uu * sizeof(K)));
+    EC_CHECK(s->dcnt.ensure(Uu * 4));
+    EC_CHECK(s->dfc.ensure(Uu * 8));
+    EC_CHECK(s->dft.ensure(Uu * 8));
+    EC_CHECK(s->upal.ensure(Uu));
+    EC_CHECK(s->succ.ensure(2 * Uu * 4));
+    if (Ur) {
+        EC_HIP(hipMemcpyAsync(s->dkey.as<K>() + lo, s->recs.p, Ur * sizeof(K), hipMemcpyDeviceToDevice, st));
+        EC_HIP(hipMemcpyAsync(s->dcnt.as<unsigned int>() + lo, s->midx.p, Ur * 4, hipMemcpyDeviceToDevice, st));
+        EC_HIP(hipMemcpyAsync(s->dfc.as<unsigned long long>() + lo, tfc, Ur * 8, hipMemcpyDeviceToDevice, st));
+        EC_HIP(hipMemcpyAsync(s->dft.as<unsigned long long>() + lo, tft, Ur * 8, hipMemcpyDeviceToDevice, st));
+        EC_HIP(hipMemsetAsync(s->succ.as<unsigned int>() + 2 * lo, 0xFF, 2 * Ur * 4, st));
+    }
+    EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
+    if (Ur)
+        k_upal<Ops><<<grid_for(Ur, B), B, 0, st>>>(s->dkey.as<K>() + lo, (unsigned int)Ur, s->k,
+                                                   s->upal.as<uint8_t>() + lo, &dsc->npal);
+    // junction records routed to the junctions' owners (the keys' rule, shard.h OwnerFn)
+    OwnerFn own = owner_fn(s->k);
+    if (s->owner_rule == 1) own.sk = 0, own.wk = 0;
+    JOwnerFn jown{};
+    jown.sk = own.sk;
+    if (own.sk) jown.mcj = sk_cfg(s->k - 1);
+    jown.wj = own.wk ? s->k - 1 : 0;
+    const uint64_t nslot = 4 * Ur;
+    EC_CHECK(s->jrec.ensure(std::max<uint64_t>(nslot, 1) * sizeof(R)));
+    EC_CHECK(s->joid.ensure(std::max<uint64_t>(nslot, 1) * 4));
+    EC_CHECK(s->jseg.ensure(((size_t)nowners + 2) * 8));
+    unsigned long long *ostart = s->jseg.as<unsigned long long>();
+    if (Ur)
+        k_junction_emit<K><<<grid_for(Ur, B), B, 0, st>>>(s->dkey.as<K>(), s->upal.as<uint8_t>(), (unsigned int)lo,
+                                                         (unsigned int)Ur, s->k, jown, (unsigned int)nowners,
+                                                         s->jrec.as<R>(), s->joid.as<unsigned int>());
+    // owner-major order: counting sort by owner (NONE slots in the last bin, dropped)
+    EC_CHECK(s->joid.ensure(std::max<uint64_t>(nslot, 1) * 4));
+    if (nslot) k_none_to_bin<<<grid_for(nslot, B), B, 0, st>>>(s->joid.as<unsigned int>(), nslot, (unsigned int)nowners);
+    EC_CHECK(bin_sort(s, s->joid.as<unsigned int>(), nslot, (unsigned int)nowners + 1, ostart));
+    if (nslot)
+        k_gather_recs<R><<<grid_for(nslot, B), B, 0, st>>>(s->jrec.as<R>(), s->midx2.as<unsigned int>(), nslot,
+                                                          static_cast<R *>(d_out));
+    std::vector<unsigned long long> hs((size_t)nowners + 2);
+    EC_CHECK(d2h(s, hs.data(), ostart, ((size_t)nowners + 2) * 8, st));
+    unsigned int npal = 0;
+    EC_CHECK(d2h(s, &npal, &dsc->npal, 4, st));
+    EC_CHECK(host_sync(s, st));
+    for (int r = 0; r < nowners; r++) owner_counts[r] = hs[r + 1] - hs[r];
+    *n_pal = npal;
+    s->seg_lo = lo;
+    s->seg_Ur = Ur;
+    s->n_dense = (unsigned int)U;
+    s->placed = true;
+    s->graph_loaded = true;  // (the part_* steps' state: the placed segment)
+    s->seg_n0 = 2 * lo;
+    s->seg_n1 = 2 * (lo + Ur);
+    return EC_OK;
+}
+
+template <typename R>
+int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const uint64_t *seg_lo, LinkRec *d_links,
+               uint64_t *owner_counts) {
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    EC_CHECK(s->jseg.ensure(((size_t)nowners + 2) * 8 + (size_t)(1u << 14) * 8 + 64));
+    unsigned long long *dseg = s->jseg.as<unsigned long long>();
+    unsigned long long *bstart = dseg + nowners + 2;
+    EC_HIP(hipMemcpyAsync(dseg, seg_lo, ((size_t)nowners + 1) * 8, hipMemcpyHostToDevice, st));
+    EC_CHECK(s->jcnt.ensure(16));
+    unsigned int *flag = s->jcnt.as<unsigned int>(), *nout = flag + 1;
+    EC_CHECK(s->jout.ensure(std::max<uint64_t>(n, 1) * sizeof(LinkRec)));
+    LinkRec *outbox = s->jout.as<LinkRec>();
+    // join buckets: ~n / 2 junction groups, <= ~900 a 2048-slot table (<= 2^14 buckets), 4096
+    // slots past that
+    int bt = 0;
+    while (bt < 14 && (double)n / 2.0 / (double)(1ull << bt) > 900.0) bt++;
+    for (int attempt = 0;; attempt++) {
+        const bool big = (double)n / 2.0 / (double)(1ull << bt) > 1500.0 || attempt > 0;
+        const unsigned int nb = 1u << bt;
+        EC_CHECK(s->joid.ensure(std::max<uint64_t>(n, 1) * 4));
+        EC_HIP(hipMemsetAsync(flag, 0, 8, st));
+        if (n) k_junction_bucket<R><<<grid_for(n, B), B, 0, st>>>(d_recs, n, bt, s->joid.as<unsigned int>());
+        EC_CHECK(bin_sort(s, s->joid.as<unsigned int>(), n, nb, bstart));
+        const unsigned int n0 = (unsigned int)(2 * s->seg_lo), n1 = (unsigned int)(2 * (s->seg_lo + s->seg_Ur));
+        if (n) {
+            if (big)
+                k_junction_join<4096, 512, R><<<nb, 512, 0, st>>>(d_recs, s->midx2.as<unsigned int>(), bstart, n0, n1,
+                                                                  s->succ.as<unsigned int>(), outbox, nout,
+                                                                  (unsigned int)n, flag);
+            else
+                k_junction_join<2048, 512, R><<<nb, 512, 0, st>>>(d_recs, s->midx2.as<unsigned int>(), bstart, n0, n1,
+                                                                  s->succ.as<unsigned int>(), outbox, nout,
+                                                                  (unsigned int)n, flag);
+        }
+        unsigned int hf[2] = {0, 0};
+        EC_CHECK(d2h(s, hf, flag, 8, st));
+        EC_CHECK(host_sync(s, st));
+        if (hf[0] & 2u) {
+            set_error("junction join: link outbox overflow");
+            return EC_ERR_STATE;
+        }
+        if (hf[0] & 1u) {  // a table past its slots (skewed junction hashes): finer buckets, bigger tables
+            if (attempt >= 2 || bt >= 14) {
+                set_error("junction join: a bucket of %llu records overflows its table", (unsigned long long)n);
+                return EC_ERR_CAPACITY;
+            }
+            bt++;
+            s->stats.table_retries++;
+            continue;
+        }
+        // outbox -> destination-major link records
+        const unsigned int no = hf[1];
+        if (no) {
+            EC_CHECK(s->joid.ensure((uint64_t)no * 4));
+            k_link_dest<<<grid_for(no, B), B, 0, st>>>(outbox, nout, no, dseg, (unsigned int)nowners,
+                                                       s->joid.as<unsigned int>());
+            EC_CHECK(bin_sort(s, s->joid.as<unsigned int>(), no, (unsigned int)nowners, bstart));
+            k_gather_recs<LinkRec><<<grid_for(no, B), B, 0, st>>>(outbox, s->midx2.as<unsigned int>(), no, d_links);
+            std::vector<unsigned long long> hs((size_t)nowners + 1);
+            EC_CHECK(d2h(s, hs.data(), bstart, ((size_t)nowners + 1) * 8, st));
+            EC_CHECK(host_sync(s, st));
+            for (int r = 0; r < nowners; r++) owner_counts[r] = hs[r + 1] - hs[r];
+        } else {
+            for (int r = 0; r < nowners; r++) owner_counts[r] = 0;
+        }
+        return EC_OK;
+    }
+}
+
+extern "C" {
+
+int ec_graph_place(ec_session *s, uint64_t lo, uint64_t U, int nowners, void *d_jrecs, uint64_t *owner_counts,
+                   uint64_t *n_pal) {
+    refresh_knobs();
+    if (!s || nowners < 1 || nowners > MAX_OWNERS || !owner_counts || !n_pal || lo + s->n_dense > U ||
+        2 * U >= (uint64_t)CYC || (s->n_dense && !d_jrecs)) {
+        set_error("ec_graph_place: bad arguments (segment [%llu, +%u) of %llu ids)", (unsigned long long)lo,
+                  s ? s->n_dense : 0u, (unsigned long long)U);
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return s->k > 32 ? graph_place<K128>(s, lo, U, nowners, d_jrecs, owner_counts, n_pal)
+                     : graph_place<unsigned long long>(s, lo, U, nowners, d_jrecs, owner_counts, n_pal);
+}
+
+int ec_graph_join(ec_session *s, const void *d_jrecs, uint64_t n, int nowners, const uint64_t *seg_lo, void *d_links,
+                  uint64_t *owner_counts) {
+    if (!s || !s->placed || nowners < 1 || nowners > MAX_OWNERS || !seg_lo || !owner_counts ||
+        (n && (!d_jrecs || !d_links))) {
+        set_error("ec_graph_join: no placed segment or bad arguments");
+        return EC_ERR_ARG;
+    }
+    for (int r = 0; r < nowners; r++)
+        if (seg_lo[r] > seg_lo[r + 1] || seg_lo[nowners] != s->n_dense) {
+            set_error("ec_graph_join: segment bounds not ascending up to %u", s->n_dense);
+            return EC_ERR_ARG;
+        }
+    EC_HIP(hipSetDevice(s->device));
+    return s->k > 32 ? graph_join<RecJ>(s, static_cast<const RecJ *>(d_jrecs), n, nowners, seg_lo,
+                                        static_cast<LinkRec *>(d_links), owner_counts)
+                     : graph_join<RecJ64>(s, static_cast<const RecJ64 *>(d_jrecs), n, nowners, seg_lo,
+                                          static_cast<LinkRec *>(d_links), owner_counts);
+}
+
+int ec_graph_links_apply(ec_session *s, const void *d_links, uint64_t n) {
+    if (!s || !s->placed || (n && !d_links)) {
+        set_error("ec_graph_links_apply: no placed segment");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    EC_CHECK(s->jcnt.ensure(16));
+    unsigned int *bad = s->jcnt.as<unsigned int>();
+    EC_HIP(hipMemsetAsync(bad, 0, 4, st));
+    if (n)
+        k_links_apply<<<grid_for(n, 256), 256, 0, st>>>(static_cast<const LinkRec *>(d_links), n,
+                                                        (unsigned int)(2 * s->seg_lo),
+                                                        (unsigned int)(2 * (s->seg_lo + s->seg_Ur)),
+                                                        s->succ.as<unsigned int>(), bad);
+    unsigned int hb = 0;
+    EC_CHECK(d2h(s, &hb, bad, 4, st));
+    EC_CHECK(host_sync(s, st));
+    if (hb) {
+        set_error("ec_graph_links_apply: a link record names a node outside this segment");
+        return EC_ERR_ARG;
+    }
+    return EC_OK;
 }
 
 int ec_super_record_bytes(void) { return (int)sizeof(SuperRec); }

@@ -21,8 +21,15 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)  // (host pass only)
+#include <emmintrin.h>
+#endif
+
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -38,12 +45,10 @@ struct ec_reads {
     uint64_t nbases = 0;
     uint32_t read_len = 0;  // every read this long (0: lengths differ)
     bool pinned = true;     // codes from hipHostMalloc (else malloc)
+    size_t codes_cap = 0;
     std::vector<uint64_t> exc_pos;
     std::vector<uint8_t> exc_byte;
-    ~ec_reads() {
-        if (codes && pinned) (void)hipHostFree(codes);
-        else free(codes);
-    }
+    ~ec_reads();
 };
 
 namespace {
@@ -69,10 +74,102 @@ inline bool is_exc(uint8_t c) {
     static const uint8_t letter[4] = {'A', 'C', 'G', 'T'};
     return letter[code2(c)] != c;
 }
+// SWAR over 8 bytes: 0x80 in every byte that is not exactly A, C, G or T (exact per byte: no
+// borrow crosses bytes), and the 2-bit codes of 8 bases packed into 2 code bytes
+inline uint64_t zero_bytes(uint64_t x) {
+    const uint64_t m = 0x7F7F7F7F7F7F7F7Full;
+    return ~(((x & m) + m) | x | m);
+}
+inline uint64_t exc_mask8(uint64_t w) {
+    const uint64_t one = 0x0101010101010101ull;
+    const uint64_t ok = zero_bytes(w ^ ('A' * one)) | zero_bytes(w ^ ('C' * one)) | zero_bytes(w ^ ('G' * one)) |
+                        zero_bytes(w ^ ('T' * one));
+    return ~ok & 0x8080808080808080ull;
+}
+inline uint16_t pack8(uint64_t w) {  // base j's code at bits 2 (j mod 4) of code byte j / 4
+    const uint64_t c = ((w >> 1) ^ (w >> 2)) & 0x0303030303030303ull;
+    const uint64_t x = c | (c >> 6) | (c >> 12) | (c >> 18);
+    return (uint16_t)((x & 0xFF) | ((x >> 24) & 0xFF00));
+}
+inline uint64_t load8(const uint8_t *p) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    return w;
+}
+#if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)  // (host pass only)
+// 16 bytes at a time (SSE2 is baseline x86-64): bit i set iff byte i is not A/C/G/T
+inline unsigned exc_mask16(__m128i v) {
+    const __m128i ok = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, _mm_set1_epi8('A')), _mm_cmpeq_epi8(v, _mm_set1_epi8('C'))),
+                                    _mm_or_si128(_mm_cmpeq_epi8(v, _mm_set1_epi8('G')), _mm_cmpeq_epi8(v, _mm_set1_epi8('T'))));
+    return ~(unsigned)_mm_movemask_epi8(ok) & 0xFFFFu;
+}
+// 16 bases -> 4 code bytes (base j at bits 2 (j mod 4) of byte j / 4)
+inline uint32_t pack16(__m128i v) {
+    const __m128i m3 = _mm_set1_epi8(3);
+    const __m128i c = _mm_and_si128(_mm_xor_si128(_mm_srli_epi16(v, 1), _mm_srli_epi16(v, 2)), m3);
+    __m128i x = _mm_or_si128(_mm_or_si128(c, _mm_srli_epi32(c, 6)), _mm_or_si128(_mm_srli_epi32(c, 12), _mm_srli_epi32(c, 18)));
+    x = _mm_and_si128(x, _mm_set1_epi32(0xFF));
+    x = _mm_packs_epi32(x, x);
+    x = _mm_packus_epi16(x, x);
+    return (uint32_t)_mm_cvtsi128_si32(x);
+}
+#endif
 inline uint64_t count_exc(const uint8_t *p, uint64_t n) {
-    uint64_t e = 0;
-    for (uint64_t i = 0; i < n; i++) e += is_exc(p[i]);
+    uint64_t e = 0, i = 0;
+#if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)  // (host pass only)
+    for (; i + 16 <= n; i += 16) e += (uint64_t)__builtin_popcount(exc_mask16(_mm_loadu_si128((const __m128i *)(p + i))));
+#endif
+    for (; i + 8 <= n; i += 8) e += (uint64_t)__builtin_popcountll(exc_mask8(load8(p + i)));
+    for (; i < n; i++) e += is_exc(p[i]);
     return e;
+}
+// the next '\n' at or after s (hi if none): inline, no call per short line
+inline uint64_t find_nl(const uint8_t *p, uint64_t s, uint64_t hi) {
+#if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)  // (host pass only)
+    const __m128i nl = _mm_set1_epi8('\n');
+    for (; s + 16 <= hi; s += 16) {
+        const unsigned m = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i *)(p + s)), nl));
+        if (m) return s + (uint64_t)__builtin_ctz(m);
+    }
+#endif
+    for (; s < hi; s++)
+        if (p[s] == '\n') return s;
+    return hi;
+}
+
+// page-locked code buffers are reused across loads (pinning ~250 MB costs tens of ms): one
+// cached buffer, handed out when large enough and returned by ec_reads_free
+std::mutex g_pool_mu;
+uint8_t *g_pool_p = nullptr;
+size_t g_pool_cap = 0;
+uint8_t *pinned_take(size_t n, size_t *cap) {
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_pool_p && g_pool_cap >= n) {
+            uint8_t *q = g_pool_p;
+            *cap = g_pool_cap;
+            g_pool_p = nullptr;
+            g_pool_cap = 0;
+            return q;
+        }
+    }
+    uint8_t *q = nullptr;
+    if (hipHostMalloc((void **)&q, n, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    *cap = n;
+    return q;
+}
+void pinned_give(uint8_t *q, size_t cap) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_pool_p && g_pool_cap >= cap) {
+        (void)hipHostFree(q);
+        return;
+    }
+    if (g_pool_p) (void)hipHostFree(g_pool_p);
+    g_pool_p = q;
+    g_pool_cap = cap;
 }
 
 // visit the lines of [lo, hi): fn(line_begin, line_end_excl_newline)
@@ -80,14 +177,28 @@ template <typename Fn>
 void for_lines(const uint8_t *p, uint64_t lo, uint64_t hi, Fn fn) {
     uint64_t s = lo;
     while (s < hi) {
-        const void *nl = memchr(p + s, '\n', hi - s);
-        const uint64_t e = nl ? (uint64_t)((const uint8_t *)nl - p) : hi;
+        const uint64_t e = find_nl(p, s, hi);
         fn(s, e);
         s = e + 1;
     }
 }
 
+// worker threads: the caller's count, else OMP_NUM_THREADS / the hardware (a GPU box's share
+// of a many-core host is what OMP_NUM_THREADS says)
+int host_threads(int threads) {
+    if (threads > 0) return threads;
+    const char *e = getenv("OMP_NUM_THREADS");
+    const int env = e ? atoi(e) : 0;
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    return std::max(1, std::min(env > 0 ? env : hw, 64));
+}
+
 }  // namespace
+
+ec_reads::~ec_reads() {
+    if (codes && pinned) pinned_give(codes, codes_cap);
+    else free(codes);
+}
 
 extern "C" {
 
@@ -99,6 +210,9 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
         return EC_ERR_ARG;
     }
     *out = nullptr;
+    const bool tdbg = getenv("EULERHIP_INGEST_TIMING") != nullptr;
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_start = now();
     const int fd = open(path, O_RDONLY);
     if (fd < 0) {
         set_error("cannot open %s", path);
@@ -129,7 +243,7 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
         set_error("out of host memory");
         return EC_ERR_NOMEM;
     }
-    int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    int T = host_threads(threads);
     if (n < (1u << 20)) T = 1;
     // chunk boundaries at line starts
     std::vector<Chunk> ch(T);
@@ -205,6 +319,7 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
         pass1b(0);
         for (auto &x : th) x.join();
     }
+    const double t_p1 = now();
     // FASTA records: sequence bytes before a chunk's first header belong to the previous
     // chunk's last record (or to no record at the file start)
     std::vector<uint64_t> lead(T, 0), lead_exc(T, 0);
@@ -250,13 +365,13 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
             const uint64_t nc = (B + 3) / 4 + 16;
             // page-locked so the codes go over PCIe at DMA speed; a host without a usable GPU
             // (ingest tests on CPU) gets ordinary memory
-            if (hipHostMalloc((void **)&r->codes, nc, hipHostMallocDefault) != hipSuccess) {
-                (void)hipGetLastError();
+            r->codes = pinned_take(nc, &r->codes_cap);
+            if (!r->codes) {
                 r->codes = static_cast<uint8_t *>(malloc(nc));
                 if (!r->codes) throw std::bad_alloc();
                 r->pinned = false;
             }
-            memset(r->codes, 0, nc);
+            // (zeroed by the copy threads: each its own code bytes, pass 2 below)
             r->exc_pos.resize(X);
             r->exc_byte.resize(X);
         } else {
@@ -280,23 +395,57 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
         const Chunk &c = ch[t];
         uint64_t ri = r0[t], bi = b0[t], xi = x0[t];
         // packed: the code bytes of bases [b0[t], b0[t + 1]) -- the first and the last may be
-        // shared with the neighbouring chunks' bases: atomic OR there
-        const uint64_t cb0 = b0[t] >> 2, cb1 = t + 1 < T ? (b0[t + 1] + 3) >> 2 : 0;
+        // shared with the neighbouring chunks' bases (atomic OR there; the last chunk shares
+        // none at its end).  Whole code bytes (4 bases of this chunk) are plain stores.
+        const uint64_t cb0 = b0[t] >> 2, cbl = t + 1 < T ? b0[t + 1] >> 2 : ~0ull;
+        auto put1 = [&](uint8_t ch8) {
+            const uint8_t v = (uint8_t)(code2(ch8) << (2 * (bi & 3)));
+            const uint64_t cb = bi >> 2;
+            if (cb == cb0 || cb == cbl) __atomic_fetch_or(oc + cb, v, __ATOMIC_RELAXED);
+            else oc[cb] |= v;
+            if (is_exc(ch8)) xp[xi] = bi, xb[xi++] = ch8;
+            bi++;
+        };
         auto put = [&](const uint8_t *src, uint64_t n) {
             if (!pack) {
                 memcpy(ob + bi, src, n);
                 bi += n;
                 return;
             }
-            for (uint64_t i = 0; i < n; i++, bi++) {
-                const uint8_t ch8 = src[i];
-                const uint8_t v = (uint8_t)(code2(ch8) << (2 * (bi & 3)));
-                const uint64_t cb = bi >> 2;
-                if (cb == cb0 || cb + 1 >= cb1) __atomic_fetch_or(oc + cb, v, __ATOMIC_RELAXED);
-                else oc[cb] |= v;
-                if (is_exc(ch8)) xp[xi] = bi, xb[xi++] = ch8;
+            uint64_t i = 0;
+            for (; i < n && (bi & 3); i++) put1(src[i]);
+#if defined(__SSE2__) && !defined(__HIP_DEVICE_COMPILE__)  // (host pass only)
+            for (; i + 16 <= n; i += 16) {  // 16 bases -> 4 whole code bytes
+                const __m128i v = _mm_loadu_si128((const __m128i *)(src + i));
+                const uint32_t c = pack16(v);
+                memcpy(oc + (bi >> 2), &c, 4);
+                unsigned bad = exc_mask16(v);
+                while (bad) {
+                    const int j = __builtin_ctz(bad);
+                    xp[xi] = bi + j, xb[xi++] = src[i + j];
+                    bad &= bad - 1;
+                }
+                bi += 16;
             }
+#endif
+            for (; i + 8 <= n; i += 8) {  // 8 bases -> 2 whole code bytes
+                const uint64_t w = load8(src + i);
+                const uint16_t c = pack8(w);
+                memcpy(oc + (bi >> 2), &c, 2);
+                uint64_t bad = exc_mask8(w);
+                while (bad) {
+                    const int j = __builtin_ctzll(bad) >> 3;
+                    xp[xi] = bi + j, xb[xi++] = src[i + j];
+                    bad &= bad - 1;
+                }
+                bi += 8;
+            }
+            for (; i < n; i++) put1(src[i]);
         };
+        if (pack) {  // zero this chunk's code bytes (whole ones; the shared boundary bytes were zeroed before)
+            const uint64_t z0 = (b0[t] + 3) >> 2, z1 = t + 1 < T ? b0[t + 1] >> 2 : (B + 3) / 4 + 16;
+            if (z1 > z0) memset(oc + z0, 0, z1 - z0);
+        }
         if (format == EC_FASTQ) {
             uint64_t li = c.lines_before;
             for_lines(p, c.lo, c.hi, [&](uint64_t b, uint64_t e) {
@@ -329,6 +478,10 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
             });
         }
     };
+    const double t_alloc = now();
+    if (pack)  // code bytes shared by two chunks' bases: zeroed before the chunks OR into them
+        for (int t = 0; t < T; t++)
+            if (b0[t] & 3) oc[b0[t] >> 2] = 0;
     {
         std::vector<std::thread> th;
         for (int t = 1; t < T; t++) th.emplace_back(pass2, t);
@@ -336,7 +489,11 @@ int ec_reads_load(const char *path, int format, int threads, ec_reads **out) {
         for (auto &x : th) x.join();
     }
     oo[R] = B;
+    const double t_p2 = now();
     if (p) munmap((void *)p, n);
+    if (tdbg)
+        fprintf(stderr, "ingest: T %d pass1 %.1f alloc %.1f pass2 %.1f munmap %.1f ms\n", T, t_p1 - t_start,
+                t_alloc - t_p1, t_p2 - t_alloc, now() - t_p2);
     if (pack && R) {  // one read length: no offsets travel
         const uint64_t L = oo[1] - oo[0];
         bool one = L <= 0xFFFFFFFFull;
@@ -451,7 +608,7 @@ int ec_pack_reads(const uint8_t *reads, const uint64_t *offsets, uint64_t nreads
         set_error("null reads / codes");
         return EC_ERR_ARG;
     }
-    int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    int T = host_threads(threads);
     if (nb < (1u << 22)) T = 1;
     std::vector<uint64_t> lo(T + 1), nexc(T, 0);
     for (int t = 0; t <= T; t++) lo[t] = t == T ? nb : (nb * (uint64_t)t / T) & ~3ull;

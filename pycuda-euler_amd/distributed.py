@@ -83,7 +83,27 @@ eulerhip.register("ec_graph_rank_supers", ctypes.c_int, [_P, _P, _U64])
 eulerhip.register("ec_graph_starts_part", ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.POINTER(_U64)])
 eulerhip.register("ec_graph_layout", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)])
 eulerhip.register("ec_graph_emit_part", ctypes.c_int, [_P, _P, _P])
-eulerhip.register("ec_graph_collect", ctypes.c_int, [_P, _P, _P])
+eulerhip.register("ec_graph_collect", ctypes.c_int, [_P, _P, _P, _U64])
+eulerhip.register("ec_end_record_bytes", ctypes.c_int, [ctypes.c_int])
+# junction-partitioned graph (round 5, csrc/junction.h): no rank holds the job's solid set
+eulerhip.register("ec_graph_place", ctypes.c_int, [_P, _U64, _U64, ctypes.c_int, _P, ctypes.POINTER(_U64),
+                                                   ctypes.POINTER(_U64)])
+eulerhip.register("ec_graph_join", ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.POINTER(_U64), _P,
+                                                  ctypes.POINTER(_U64)])
+eulerhip.register("ec_graph_links_apply", ctypes.c_int, [_P, _P, _U64])
+eulerhip.register("ec_junction_record_bytes", ctypes.c_int, [ctypes.c_int])
+eulerhip.register("ec_link_record_bytes", ctypes.c_int, [])
+LINK_BYTES = 8  # ec_link_record_bytes()
+
+
+def junction_bytes(k):
+    """ec_junction_record_bytes: RecJ64 (k <= 32) / RecJ"""
+    return 16 if k <= 32 else 24
+
+
+def end_bytes(k):
+    """ec_end_record_bytes: one contig-end k-mer code"""
+    return 8 if k <= 32 else 16
 eulerhip.register("ec_super_record_bytes", ctypes.c_int, [])
 eulerhip.register("ec_start_record_bytes", ctypes.c_int, [])
 SUPER_BYTES = 32  # ec_super_record_bytes()
@@ -146,12 +166,17 @@ class HipEngine:
         eulerhip.check(self.L.ec_export_by_owner(self._h(), int(nowners), ctypes.c_void_p(out.data_ptr()), counts))
         return out[: n * rb], [int(c) for c in counts]
 
-    def merge_owned(self, recs, k, limit, flags=0):
+    def merge_owned(self, recs, k, limit, flags=0, export=True):
         """ec_merge_owned_export: merge + solid filter + export in one call into a buffer
-        sized for every received record (an upper bound of the solid ones)"""
+        sized for every received record (an upper bound of the solid ones).  export=False
+        (the junction-partitioned graph): ec_merge_owned only, returns the solid count"""
         self.k = int(k)
         rb = self.rec_bytes()
         n = recs.numel() // rb
+        if not export:
+            eulerhip.check(self.L.ec_merge_owned(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k), int(limit),
+                                                 flags))
+            return int(self.L.ec_dense_count(self._h()))
         out = self.empty(n * rb)
         eulerhip.check(self.L.ec_merge_owned_export(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(k),
                                                     int(limit), flags, ctypes.c_void_p(out.data_ptr())))
@@ -190,11 +215,44 @@ class HipEngine:
         return self.sess.fetch(k) if fetch else None
 
     # partitioned finish: ec_graph_chains_part .. ec_graph_collect
-    def graph_chains_part(self, lo, hi, succ_part):
-        """this rank's chains as super records (uint8 tensor of n * SUPER_BYTES) and n"""
+    # junction-partitioned graph: ec_graph_place / ec_graph_join / ec_graph_links_apply
+    def graph_place(self, lo, U, nowners):
+        """this rank's merged segment at global ids [lo, lo + Ur); returns (junction records
+        grouped by owner, records per owner, palindromic keys of the segment)"""
+        ur = int(self.L.ec_dense_count(self._h()))
+        jb = junction_bytes(self.k)
+        out = self.empty(4 * ur * jb)
+        counts = (_U64 * nowners)()
+        npal = _U64(0)
+        eulerhip.check(self.L.ec_graph_place(self._h(), int(lo), int(U), int(nowners), ctypes.c_void_p(out.data_ptr()),
+                                             counts, ctypes.byref(npal)))
+        tot = sum(int(c) for c in counts)
+        return out[: tot * jb], [int(c) for c in counts], int(npal.value)
+
+    def graph_join(self, recs, seg_lo):
+        """the links of the junctions this rank owns (recs: every record it received); returns
+        (link records of other ranks' nodes grouped by rank, records per rank)"""
+        nowners = len(seg_lo) - 1
+        n = recs.numel() // junction_bytes(self.k)
+        out = self.empty(n * LINK_BYTES)
+        counts = (_U64 * nowners)()
+        bounds = (_U64 * len(seg_lo))(*[int(x) for x in seg_lo])
+        eulerhip.check(self.L.ec_graph_join(self._h(), ctypes.c_void_p(recs.data_ptr()), n, int(nowners), bounds,
+                                            ctypes.c_void_p(out.data_ptr()), counts))
+        tot = sum(int(c) for c in counts)
+        return out[: tot * LINK_BYTES], [int(c) for c in counts]
+
+    def graph_links_apply(self, links):
+        eulerhip.check(self.L.ec_graph_links_apply(self._h(), ctypes.c_void_p(links.data_ptr()),
+                                                   links.numel() // LINK_BYTES))
+
+    def graph_chains_part(self, lo, hi, succ_part=None):
+        """this rank's chains as super records (uint8 tensor of n * SUPER_BYTES) and n
+        (succ_part None: a placed segment, whose links the session holds)"""
         out = self.empty(2 * (hi - lo) * SUPER_BYTES)
         n = ctypes.c_uint64(0)
-        eulerhip.check(self.L.ec_graph_chains_part(self._h(), int(lo), int(hi), ctypes.c_void_p(succ_part.data_ptr()),
+        sp = ctypes.c_void_p(succ_part.data_ptr()) if succ_part is not None else None
+        eulerhip.check(self.L.ec_graph_chains_part(self._h(), int(lo), int(hi), sp,
                                                    ctypes.c_void_p(out.data_ptr()), ctypes.byref(n)))
         return out[: n.value * SUPER_BYTES], int(n.value)
 
@@ -218,9 +276,10 @@ class HipEngine:
         eulerhip.check(self.L.ec_graph_emit_part(self._h(), ctypes.c_void_p(chars.data_ptr()),
                                                  ctypes.c_void_p(ends.data_ptr())))
 
-    def graph_collect(self, chars, ends, k, fetch=True):
+    def graph_collect(self, chars, ends, k, npal, fetch=True):
+        """npal: the job's palindromic solid k-mers (n_dict = 2 U - npal)"""
         eulerhip.check(self.L.ec_graph_collect(self._h(), ctypes.c_void_p(chars.data_ptr()),
-                                               ctypes.c_void_p(ends.data_ptr())))
+                                               ctypes.c_void_p(ends.data_ptr()), int(npal)))
         return self.sess.fetch(k) if fetch else None
 
     def zeros(self, nbytes):
@@ -284,6 +343,16 @@ class TorchComm:
         dist.all_gather_into_tensor(out, pad, group=self.group)
         return (out, szl) if with_sizes else out
 
+    def allgather_int(self, v):
+        """every rank's integer v, in rank order (one small all-gather)"""
+        if self.world == 1:
+            return [int(v)]
+        dev = "cuda" if self.dist.get_backend(self.group) == "nccl" else "cpu"
+        t = self.torch.tensor([int(v)], dtype=self.torch.int64, device=dev)
+        out = self.torch.empty(self.world, dtype=self.torch.int64, device=dev)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return [int(x) for x in out.tolist()]
+
     def reduce_sum(self, t, dst=0):
         """element-wise sum of every rank's uint8 tensor `t` into rank dst's (in place); the
         partitioned finish's characters / contig ends, each byte set by exactly one rank"""
@@ -318,10 +387,33 @@ def _gather_concat(comm, t, nbytes_each=None):
     return comm.torch.cat([g[r * mx: r * mx + sz[r]] for r in range(comm.world)]), sz
 
 
-def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None):
+def junction_links(engine, comm, k, ur, tick=None):
+    """The junction-partitioned graph (csrc/junction.h): this rank's merged segment (ur keys)
+    placed at its global ids, the (k-1)-mer junction records exchanged by junction owner (one
+    all-to-all-v; with minimizer owners nearly all stay local), the links of the owned
+    junctions joined, the other ranks' link records exchanged (a second all-to-all-v) and
+    applied.  No rank holds the job's solid set.  Returns (lo, hi, U, job palindromes)."""
+    tick = tick or (lambda name: None)
+    sizes = comm.allgather_int(ur)
+    lo = sum(sizes[: comm.rank])
+    U = sum(sizes)
+    seg_lo = [sum(sizes[:r]) for r in range(comm.world + 1)]
+    jrecs, jcounts, npal = engine.graph_place(lo, U, comm.world)
+    jb = junction_bytes(k)
+    recv, npal_job = comm.alltoallv(jrecs, [c * jb for c in jcounts], tag=npal)  # (the palindromes ride along)
+    tick("place")
+    links, lcounts = engine.graph_join(recv, seg_lo)
+    lrecv, _ = comm.alltoallv(links, [c * LINK_BYTES for c in lcounts])
+    engine.graph_links_apply(lrecv)
+    tick("join")
+    return lo, lo + ur, U, npal_job
+
+
+def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None, npal=None):
     """The graph finish with every rank ranking / emitting its own segment (ec_graph_chains_part ..
     ec_graph_collect): all-gathers of the chains' super records (~1/9 of the nodes on the
-    super-k-mer path) and of the contig starts, one reduce of the contig characters to rank 0.
+    super-k-mer path) and of the contig starts, one reduce of the contig characters and end
+    codes to rank 0.  part None: a placed segment (junction_links), npal its job palindromes.
     Returns rank 0's result (None elsewhere)."""
     tick = tick or (lambda name: None)
     sup, _ = engine.graph_chains_part(lo, hi, part)
@@ -336,12 +428,12 @@ def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None):
     nchars = engine.graph_layout(starts, nc)
     tick("starts")
     chars = engine.zeros(nchars)
-    ends = engine.zeros(max(8 * nc, 8))
+    ends = engine.zeros(max(2 * nc * end_bytes(k), 8))
     engine.graph_emit_part(chars, ends)
     comm.reduce_sum(chars)
     comm.reduce_sum(ends)
     tick("emit")
-    res = engine.graph_collect(chars, ends, k, fetch=fetch) if comm.rank == 0 else None
+    res = engine.graph_collect(chars, ends, k, npal, fetch=fetch) if comm.rank == 0 else None
     tick("collect")
     return res
 
@@ -394,6 +486,16 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     # the job's k-mer positions ride along with the exchange's byte counts
     received, P = comm.alltoallv(recs, [c * rec_bytes(k) for c in counts], tag=st.n_positions)
     tick("alltoall")
+    junction = partitioned and finish == "partitioned" and hasattr(engine, "graph_place")
+    if junction:  # each rank keeps its own segment: the links come out of the junction join
+        ur = engine.merge_owned(received, k, limit, flags, export=False)
+        tick("merge")
+        lo, hi, _, npal = junction_links(engine, comm, k, ur, tick=tick)
+        res = partitioned_finish(engine, comm, k, lo, hi, None, fetch=fetch, tick=tick, npal=npal)
+        if phase_ms is not None:
+            for (_, a), (name, b) in zip(marks, marks[1:]):
+                phase_ms[name] = phase_ms.get(name, 0.0) + (b - a) * 1e3
+        return res, P
     solid = engine.merge_owned(received, k, limit, flags)
     tick("merge")
     if not partitioned:
@@ -416,20 +518,18 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
             tick("load")
             engine.graph_links_part(lo, hi, part)
             tick("links")
-        if finish == "partitioned" and hasattr(engine, "graph_chains_part"):
-            res = partitioned_finish(engine, comm, k, lo, hi, part, fetch=fetch, tick=tick)
-        else:  # replicated finish: the successor parts all-gathered, every rank ranks / emits everything
-            # every rank's part size is known from the solid-set sizes: no size exchange
-            gathered, psz = comm.allgatherv(part[: 8 * (hi - lo)], fill=0xFF, with_sizes=True,
-                                            sizes=[8 * x for x in nrec])
-            if comm.world > 1:  # drop the padding: node order = rank order
-                mx = max(max(psz), 1)
-                succ = comm.torch.cat([gathered[r * mx: r * mx + psz[r]] for r in range(comm.world)])
-            else:
-                succ = gathered
-            tick("gather_links")
-            res = engine.graph_finish(succ, k, flags, fetch=fetch)
-            tick("graph")
+        # replicated finish: the successor parts all-gathered, every rank ranks / emits everything
+        # (every rank's part size is known from the solid-set sizes: no size exchange)
+        gathered, psz = comm.allgatherv(part[: 8 * (hi - lo)], fill=0xFF, with_sizes=True,
+                                        sizes=[8 * x for x in nrec])
+        if comm.world > 1:  # drop the padding: node order = rank order
+            mx = max(max(psz), 1)
+            succ = comm.torch.cat([gathered[r * mx: r * mx + psz[r]] for r in range(comm.world)])
+        else:
+            succ = gathered
+        tick("gather_links")
+        res = engine.graph_finish(succ, k, flags, fetch=fetch)
+        tick("graph")
     if phase_ms is not None:
         for (_, a), (name, b) in zip(marks, marks[1:]):
             phase_ms[name] = phase_ms.get(name, 0.0) + (b - a) * 1e3
@@ -520,45 +620,58 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
     local_sharded_assemble_shards.last_rule = rule
     finish = finish_mode(finish, k, rule)
     local_sharded_assemble_shards.last_counts = [c for _, c in sends]
-    solids = []
-    for dst, eng in enumerate(engines):
+    rb = rec_bytes(k)
+
+    def received(dst, eng):
         parts = []
         for src in range(world):
             recs, counts = sends[src]
-            rb = rec_bytes(k)
             o = sum(counts[:dst]) * rb
             parts.append(recs[o:o + counts[dst] * rb].to(eng.device))
-        solids.append(eng.merge_owned(torch.cat(parts), k, limit, flags))
+        return torch.cat(parts)
+
+    if partitioned is None:
+        partitioned = not (flags & eulerhip.EC_FLAG_GENERAL)
+    if partitioned and finish == "partitioned":  # the junction-partitioned graph (junction_links)
+        urs = [eng.merge_owned(received(dst, eng), k, limit, flags, export=False) for dst, eng in enumerate(engines)]
+        seg_lo = [sum(urs[:r]) for r in range(world + 1)]
+        U = seg_lo[-1]
+        placed = [eng.graph_place(seg_lo[r], U, world) for r, eng in enumerate(engines)]
+        npal = sum(p[2] for p in placed)
+        jb = junction_bytes(k)
+        links = []
+        for dst, eng in enumerate(engines):
+            got = [rec[sum(c[:dst]) * jb:sum(c[:dst + 1]) * jb].to(eng.device) for rec, c, _ in placed]
+            links.append(eng.graph_join(torch.cat(got), seg_lo))
+        for dst, eng in enumerate(engines):
+            got = [rec[sum(c[:dst]) * LINK_BYTES:sum(c[:dst + 1]) * LINK_BYTES].to(eng.device) for rec, c in links]
+            eng.graph_links_apply(torch.cat(got))
+        segs = [(seg_lo[r], seg_lo[r + 1], None) for r in range(world)]
+        return local_partitioned_finish(engines, segs, k, npal), P
+    solids = [eng.merge_owned(received(dst, eng), k, limit, flags) for dst, eng in enumerate(engines)]
     mx = max(max(x.numel() for x in solids), 1)  # padded like TorchComm.allgatherv (0xFF filler records)
     allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device=engines[0].device)
     for i, x in enumerate(solids):
         allsolid[i * mx: i * mx + x.numel()] = x.to(engines[0].device)
-    if partitioned is None:
-        partitioned = not (flags & eulerhip.EC_FLAG_GENERAL)
     if not partitioned:
         res = engines[0].assemble_from_solid(allsolid, k, flags)
         return res, P
-    # partitioned graph phase: every simulated rank loads the gathered set and computes the
-    # links of its own segment; the parts are concatenated in rank order
-    rb = rec_bytes(k)
+    # partitioned links, replicated finish: every simulated rank loads the gathered set and
+    # computes the links of its own segment; the parts are concatenated in rank order
     nrec = [x.numel() // rb for x in solids]
     parts = []
-    segs = []
     for r, eng in enumerate(engines):
         lo = sum(nrec[:r])
         eng.graph_load(allsolid.to(eng.device), k, flags)
         part = eng.empty(8 * nrec[r])
         eng.graph_links_part(lo, lo + nrec[r], part)
-        segs.append((lo, lo + nrec[r], part))
         parts.append(part[: 8 * nrec[r]].to(engines[0].device))
-    if finish == "partitioned" and hasattr(engines[0], "graph_chains_part"):
-        return local_partitioned_finish(engines, segs, k), P
     succ = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=engines[0].device)
     res = engines[0].graph_finish(succ if succ.numel() else engines[0].empty(4), k, flags)
     return res, P
 
 
-def local_partitioned_finish(engines, segs, k):
+def local_partitioned_finish(engines, segs, k, npal):
     """partitioned_finish with the collectives done by concatenation / summation (simulated ranks)"""
     import torch
 
@@ -574,8 +687,8 @@ def local_partitioned_finish(engines, segs, k):
     chars, ends = None, None
     for eng in engines:
         nchars = eng.graph_layout(starts.to(eng.device), nc)
-        c, e = eng.zeros(nchars), eng.zeros(max(8 * nc, 8))
+        c, e = eng.zeros(nchars), eng.zeros(max(2 * nc * end_bytes(k), 8))
         eng.graph_emit_part(c, e)
         chars = c.to(dev) if chars is None else chars + c.to(dev)
         ends = e.view(torch.int32).to(dev) if ends is None else ends + e.view(torch.int32).to(dev)
-    return engines[0].graph_collect(chars, ends.view(torch.uint8), k)
+    return engines[0].graph_collect(chars, ends.view(torch.uint8), k, npal)

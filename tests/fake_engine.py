@@ -8,6 +8,8 @@ are the device ones (ec_kmer_record, shard.h OwnerFn), so the exchange is byte-i
 import numpy as np
 import torch
 
+import bisect
+
 from distributed import REC_BYTES, REC_DTYPE
 from model_parallel import model_count, model_graph, twin
 
@@ -140,7 +142,7 @@ class FakeEngine:
         self.last_counts = counts
         return self._bytes(self.recs[order]), counts
 
-    def merge_owned(self, recs, k, limit, flags=0):
+    def merge_owned(self, recs, k, limit, flags=0, export=True):
         agg = {}
         for r in self._recs(recs):
             key = int(r["key"])
@@ -151,7 +153,7 @@ class FakeEngine:
         for i, (key, c, a, b) in enumerate(keep):
             out[i] = (key, c, 0, a, b)
         self.recs = out
-        return self._bytes(out)
+        return self._bytes(out) if export else len(out)
 
     def assemble_from_solid(self, recs, k, flags=0, fetch=True):
         cnt, first = {}, {}
@@ -220,32 +222,117 @@ class FakeEngine:
         return self.assemble_from_solid(self._bytes(self.grecs), k, flags)
 
 
+    # ---- junction-partitioned graph (distributed.junction_links; csrc/junction.h) ----------
+    # RecJ64 {key u64, tag u32 = oriented global node | side << 31, pad u32 = palindrome flag},
+    # LinkRec {node u32, value u32}; junction owners as JOwnerFn (the keys' rule on k - 1 bases)
+    JREC = np.dtype([("key", "<u8"), ("tag", "<u4"), ("pad", "<u4")])
+    LINK = np.dtype([("node", "<u4"), ("value", "<u4")])
+
+    def _jowner(self, o, n):
+        if 21 <= self.k <= 32 and self.rule == 0:
+            return (minimizer_of(o, self.k - 1) * n) >> 32
+        return owner_of(o, n)
+
+    def graph_place(self, lo, U, nowners):
+        k = self.k
+        self.lo, self.U = lo, U
+        self.seg = self.recs.copy()  # the merge's segment, global ids lo..
+        self.succ_seg = {}
+        recs, npal = [], 0
+        for i, r in enumerate(self.seg):
+            c = decode(int(r["key"]), k)
+            pal = twin(c) == c
+            npal += pal
+            g = lo + i
+            ic, itc = 2 * g, (2 * g if pal else 2 * g + 1)
+            s_, p_ = c[1:], c[:-1]  # suffix / prefix junctions (half_recs)
+            for (j, side, node, tnode) in ((s_, 0, ic, itc), (p_, 1, ic, itc)):
+                tj = twin(j)
+                if j < tj:
+                    recs.append((encode(j), node | (side << 31), int(pal)))
+                elif j > tj:
+                    recs.append((encode(tj), tnode | ((1 - side) << 31), int(pal)))
+                else:  # palindromic junction: both records
+                    recs.append((encode(j), tnode | ((1 - side) << 31), int(pal)))
+                    recs.append((encode(j), node | (side << 31), int(pal)))
+        own = [self._jowner(key, nowners) for key, _, _ in recs]
+        order = sorted(range(len(recs)), key=lambda q: own[q])
+        out = np.array([recs[q] for q in order], dtype=self.JREC) if recs else np.zeros(0, self.JREC)
+        return self._bytes(out), [own.count(o) for o in range(nowners)], npal
+
+    def graph_join(self, recs, seg_lo):
+        groups = {}
+        for r in np.frombuffer(recs.numpy().tobytes(), dtype=self.JREC):
+            g = groups.setdefault(int(r["key"]), ([set(), set()], {}))
+            tag = int(r["tag"])
+            node = tag & 0x7FFFFFFF
+            g[0][tag >> 31].add(node)
+            g[1][node] = int(r["pad"])
+        n0, n1 = 2 * self.lo, 2 * (self.lo + len(self.seg))
+        out = []
+        for a, pal in groups.values():
+            if len(a[0]) != 1 or len(a[1]) != 1:
+                continue
+            (x,), (y,) = a[0], a[1]
+            tx, ty = (x if pal[x] else x ^ 1), (y if pal[y] else y ^ 1)
+            if y == tx:
+                continue
+            for t, v in ((x, y), (ty, tx)):
+                if n0 <= t < n1:
+                    self.succ_seg[t] = v
+                else:
+                    out.append((t, v))
+        own = [bisect.bisect_right(seg_lo, t >> 1) - 1 for t, _ in out]
+        order = sorted(range(len(out)), key=lambda q: own[q])
+        arr = np.array([out[q] for q in order], dtype=self.LINK) if out else np.zeros(0, self.LINK)
+        return self._bytes(arr), [own.count(o) for o in range(len(seg_lo) - 1)]
+
+    def graph_links_apply(self, links):
+        n0, n1 = 2 * self.lo, 2 * (self.lo + len(self.seg))
+        for r in np.frombuffer(links.numpy().tobytes(), dtype=self.LINK):
+            assert n0 <= int(r["node"]) < n1, "a link record for another rank's node"
+            self.succ_seg[int(r["node"])] = int(r["value"])
+
     # ---- partitioned finish (distributed.partitioned_finish): the same records / collectives,
-    # computed on the whole set by the design model -- every node is its own chain; contig i is
-    # emitted by the rank whose segment holds the canonical id of its first k-mer
+    # computed by the design model -- every node is its own chain; its super record carries its
+    # key and count in the spare fields, so the all-gathered supers rebuild the job's solid set
+    # and check the junction join's links against the direct rule; contig i is emitted by the
+    # rank whose segment holds the canonical id of its first k-mer
     SUP = np.dtype([("head", "<u4"), ("succ", "<u4"), ("w", "<u4"), ("pad", "<u4"), ("fmin", "<u8"), ("pad2", "<u8")])
     ST = np.dtype([("ev", "<u8"), ("node", "<u4"), ("pk", "<u4"), ("walk", "<u4", 6), ("clen", "<u4"), ("pad", "<u4")])
 
     def zeros(self, nbytes):
         return torch.zeros(max(int(nbytes), 1), dtype=torch.uint8)
 
-    def graph_chains_part(self, lo, hi, part):
-        self.lo, self.hi = lo, hi
-        succ = np.frombuffer(part.numpy().tobytes(), dtype=np.uint32)[: 2 * (hi - lo)]
+    def graph_chains_part(self, lo, hi, part=None):
+        assert part is None and lo == self.lo and hi == lo + len(self.seg)
         out = np.zeros(2 * (hi - lo), self.SUP)
         out["head"] = np.arange(2 * lo, 2 * hi, dtype=np.uint32)
-        out["succ"] = succ
+        out["succ"] = [self.succ_seg.get(x, 0xFFFFFFFF) for x in range(2 * lo, 2 * hi)]
         out["w"] = 1
+        out["pad"] = np.repeat(self.seg["count"], 2)
+        out["pad2"] = np.repeat(self.seg["key"], 2)
+        fm = np.zeros(2 * (hi - lo), np.uint64)
+        fm[0::2] = self.seg["first_canon"]
+        fm[1::2] = self.seg["first_twin"]
+        out["fmin"] = fm
         return self._bytes(out), len(out)
 
     def graph_rank_supers(self, supers, M):
         sup = np.frombuffer(supers.numpy().tobytes(), dtype=self.SUP)[:M]
-        N = 2 * len(self.grecs)
+        N = 2 * self.U
         assert M == N and np.array_equal(sup["head"], np.arange(N)), "super records out of rank order"
+        g = np.zeros(self.U, REC_DTYPE)
+        g["key"] = sup["pad2"][0::2]
+        g["count"] = sup["pad"][0::2]
+        g["first_canon"] = sup["fmin"][0::2]
+        g["first_twin"] = sup["fmin"][1::2]
+        self.grecs = g
+        self.gid = {int(x): i for i, x in enumerate(g["key"])}
+        self.gk = self.k
         want = np.array([self._succ_of(x) for x in range(N)], dtype=np.uint32)
-        assert np.array_equal(sup["succ"], want), "gathered chains differ from the whole-set links"
-        self.full = self.assemble_from_solid(self._bytes(self.grecs), self.gk)
-
+        assert np.array_equal(sup["succ"], want), "junction-joined links differ from the whole-set rule"
+        self.full = self.assemble_from_solid(self._bytes(g), self.k)
     def _first_id(self, c):
         x = encode(c[: self.gk])
         return self.gid[min(x, self._tw(x))]
@@ -269,16 +356,17 @@ class FakeEngine:
         return int(self.coff[-1])
 
     def graph_emit_part(self, chars, ends):
-        e = np.zeros(max(2 * self.nc, 2), np.uint32)
+        e = np.zeros(max(2 * self.nc, 2), np.uint64)  # (the device writes end codes; one set per end)
         c = chars.numpy()
         for i in self.own:
             s = self.full.contigs[i].encode()
             c[self.coff[i]:self.coff[i] + len(s)] = np.frombuffer(s, np.uint8)
             e[i] = e[self.nc + i] = i + 1
-        ends[: 8 * self.nc] = torch.from_numpy(e[: 2 * self.nc].view(np.uint8).copy())
+        ends[: 16 * self.nc] = torch.from_numpy(e[: 2 * self.nc].view(np.uint8).copy())
 
-    def graph_collect(self, chars, ends, k, fetch=True):
-        e = np.frombuffer(ends.numpy().tobytes(), dtype=np.uint32)[: 2 * self.nc]
+    def graph_collect(self, chars, ends, k, npal, fetch=True):
+        assert npal == sum(decode(int(x), k) == twin(decode(int(x), k)) for x in self.grecs["key"])
+        e = np.frombuffer(ends.numpy().tobytes(), dtype=np.uint64)[: 2 * self.nc]
         assert list(e) == list(range(1, self.nc + 1)) * 2, "contig ends not set exactly once"
         ch = chars.numpy().tobytes()
         contigs = [ch[self.coff[i]:self.coff[i + 1]].decode() for i in range(self.nc)]

@@ -64,39 +64,40 @@ def main():
             t0 = time.perf_counter()
             sends.append(eng.export_by_owner(world))
             tick("export", t0)
-        solids = []
         rb = distributed.rec_bytes(a.k)
+        recvs = []
         for dst, eng in enumerate(engines):
             parts = []
             for src in range(world):
                 recs, counts = sends[src]
                 o = sum(counts[:dst]) * rb
                 parts.append(recs[o:o + counts[dst] * rb])
-            recv = torch.cat(parts)
-            t0 = time.perf_counter()
-            solids.append(eng.merge_owned(recv, a.k, 1, 0))
-            tick("merge", t0)
-        mx = max(x.numel() for x in solids)
-        allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device="cuda")
-        for i, x in enumerate(solids):
-            allsolid[i * mx: i * mx + x.numel()] = x
-        nrec = [x.numel() // rb for x in solids]
-        parts = []
-        for r, eng in enumerate(engines):
-            lo = sum(nrec[:r])
-            t0 = time.perf_counter()
-            eng.graph_load(allsolid, a.k)
-            tick("load", t0)
-            t0 = time.perf_counter()
-            part = eng.empty(8 * nrec[r])
-            eng.graph_links_part(lo, lo + nrec[r], part)
-            tick("links", t0)
-            parts.append(part[: 8 * nrec[r]])
+            recvs.append(torch.cat(parts))
         import ctypes
         import eulerhip
-        segs = [(sum(nrec[:r]), sum(nrec[:r + 1]), parts[r]) for r in range(world)]
         extra = ""
-        if a.finish == "replicated":
+        if a.finish == "replicated":  # the round-4 layout: gathered solid set, loaded on every rank
+            solids = []
+            for eng, recv in zip(engines, recvs):
+                t0 = time.perf_counter()
+                solids.append(eng.merge_owned(recv, a.k, 1, 0))
+                tick("merge", t0)
+            mx = max(x.numel() for x in solids)
+            allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device="cuda")
+            for i, x in enumerate(solids):
+                allsolid[i * mx: i * mx + x.numel()] = x
+            nrec = [x.numel() // rb for x in solids]
+            parts = []
+            for r, eng in enumerate(engines):
+                lo = sum(nrec[:r])
+                t0 = time.perf_counter()
+                eng.graph_load(allsolid, a.k)
+                tick("load", t0)
+                t0 = time.perf_counter()
+                part = eng.empty(8 * nrec[r])
+                eng.graph_links_part(lo, lo + nrec[r], part)
+                tick("links", t0)
+                parts.append(part[: 8 * nrec[r]])
             succ = torch.cat(parts)
             eng = engines[0]
             t0 = time.perf_counter()
@@ -107,11 +108,43 @@ def main():
             tick("fetch", t0)
             st = eng.stats()
             print("finish stages ms:", {n: round(v, 3) for n, v in zip(eulerhip.stage_names(), st.stage_ms)})
-        else:  # distributed.partitioned_finish, every rank's calls timed
-            sups = []
-            for eng, (lo, hi, part) in zip(engines, segs):
+            xb = allsolid.numel()
+        else:  # the junction-partitioned graph and the partitioned finish, every rank's calls timed
+            urs = []
+            for eng, recv in zip(engines, recvs):
                 t0 = time.perf_counter()
-                sups.append(eng.graph_chains_part(lo, hi, part)[0])
+                urs.append(eng.merge_owned(recv, a.k, 1, 0, export=False))
+                tick("merge", t0)
+            seg_lo = [sum(urs[:r]) for r in range(world + 1)]
+            U = seg_lo[-1]
+            placed = []
+            for r, eng in enumerate(engines):
+                t0 = time.perf_counter()
+                placed.append(eng.graph_place(seg_lo[r], U, world))
+                tick("place", t0)
+            npal = sum(p[2] for p in placed)
+            jb = distributed.junction_bytes(a.k)
+            links = []
+            jx = 0
+            for dst, eng in enumerate(engines):
+                got = [rec[sum(c[:dst]) * jb:sum(c[:dst + 1]) * jb] for rec, c, _ in placed]
+                jx = max(jx, sum(g.numel() for i, g in enumerate(got) if i != dst))
+                recv = torch.cat(got)
+                t0 = time.perf_counter()
+                links.append(eng.graph_join(recv, seg_lo))
+                tick("join", t0)
+            lx = 0
+            for dst, eng in enumerate(engines):
+                got = [rec[sum(c[:dst]) * 8:sum(c[:dst + 1]) * 8] for rec, c in links]
+                lx = max(lx, sum(g.numel() for g in got))
+                t0 = time.perf_counter()
+                eng.graph_links_apply(torch.cat(got))
+                tick("apply", t0)
+            segs = [(seg_lo[r], seg_lo[r + 1]) for r in range(world)]
+            sups = []
+            for eng, (lo, hi) in zip(engines, segs):
+                t0 = time.perf_counter()
+                sups.append(eng.graph_chains_part(lo, hi)[0])
                 tick("chains", t0)
             supers = torch.cat(sups)
             M = supers.numel() // distributed.SUPER_BYTES
@@ -120,7 +153,7 @@ def main():
                 eng.graph_rank_supers(supers, M)
                 tick("rank_supers", t0)
             sts = []
-            for eng, (lo, hi, _) in zip(engines, segs):
+            for eng, (lo, hi) in zip(engines, segs):
                 t0 = time.perf_counter()
                 sts.append(eng.graph_starts_part(M > 0, lo, hi)[0])
                 tick("starts", t0)
@@ -132,21 +165,23 @@ def main():
                 nchars = eng.graph_layout(starts, nc)
                 tick("layout", t0)
                 t0 = time.perf_counter()
-                c, e = eng.zeros(nchars), eng.zeros(max(8 * nc, 8))
+                c, e = eng.zeros(nchars), eng.zeros(max(2 * nc * distributed.end_bytes(a.k), 8))
                 eng.graph_emit_part(c, e)
                 tick("emit", t0)
                 chars = c if chars is None else chars + c
                 ends = e.view(torch.int32) if ends is None else ends + e.view(torch.int32)
             t0 = time.perf_counter()
-            res = engines[0].graph_collect(chars, ends.view(torch.uint8), a.k)
+            res = engines[0].graph_collect(chars, ends.view(torch.uint8), a.k, npal)
             tick("collect", t0)
-            extra = ", chains gathered %.1f MB (%d), starts %.2f MB, chars %.1f MB" % (
-                supers.numel() / 1e6, M, starts.numel() / 1e6, chars.numel() / 1e6)
+            extra = (", junction records off-rank %.2f MB, link records %.2f MB, chains gathered %.1f MB (%d), "
+                     "starts %.2f MB, chars %.1f MB" % (jx / 1e6, lx / 1e6, supers.numel() / 1e6, M,
+                                                        starts.numel() / 1e6, chars.numel() / 1e6))
+            xb = 0
         print("export per rank:", [round(x, 2) for x in t["export"]], "count per rank:", [round(x, 2) for x in t["count"]])
         mx_ph = {k: round(max(v), 2) for k, v in t.items()}
         print("rep %d  ranks %d  per-rank max ms: %s  sum %.2f  exchanged bytes/rank ~%.0f MB, gathered %.0f MB%s" % (
             rep, world, mx_ph, sum(mx_ph.values()),
-            sum(c for c in sends[0][1]) * rb / 1e6, allsolid.numel() / 1e6, extra))
+            sum(c for c in sends[0][1]) * rb / 1e6, xb / 1e6, extra))
     print("contigs", len(res.contig_offsets) - 1, "chars", len(res.contig_bytes))
 
 
