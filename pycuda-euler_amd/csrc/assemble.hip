@@ -251,10 +251,8 @@ struct ec_session {
     XAlpha xa{};
     DevBuf x_par, x_irr, x_in, x_succ, x_done, x_lk, x_lv, x_lk2, x_lv2, x_len, x_m, x_cid, x_head, x_tail;
     // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
-    DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr, rt_coop;
+    DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr;
     DevBuf wbv;  // count_wide.h minimizer buckets: every window's minimizer
-    DevBuf skrej;  // k_skbucket_filtd: records its record tables had no room for
-    unsigned int coop_grid = 0;  // blocks of the cooperative ranking launch (all resident)
     // multi-GPU partitioned finish (ec_graph_chains_part ..): this rank's segment of oriented nodes
     uint64_t seg_n0 = 0, seg_n1 = 0;
     unsigned int seg_nc = 0;     // contigs of the job (ec_graph_layout)
@@ -357,7 +355,6 @@ struct Scalars {  // device scalars block
     unsigned long long nrec;  // k_upsweep_sk: super-k-mer records
     unsigned int nasym, nxl, nxs;  // extended.h: one-way links, entries of their components, their starts
     unsigned int xbad;             // extended.h: a walk that never reaches its start again
-    unsigned int coop_bad, coop_nr;  // k_rank_supers_coop: chains left unvisited, rulers
     unsigned int wbv_long, wpad;     // k_wbv: a read of another length
     unsigned long long chains;       // k_tile_compact: the tile contraction's chain count
     unsigned int active[64];
@@ -813,28 +810,17 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         // (the table takes up to 2047 keys; the prediction runs ~10 % high.  ecoli10m_err's
         // fullest bucket: 1525 predicted, 1485 inserted)
         const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 1900u;
-        // (measured on ecoli10m_err: the record merge filled its 1535-entry tables -- up to 915
-        // records a bucket rejected -- and its 131 KB of LDS held one workgroup per CU: compact
-        // 8.26 ms against 7.75 without it; opt-in, EULERHIP_SKF_DEDUP=1)
-        if (kn().skf_dedup != 1) {
-            // (no tile planning here: measured on ecoli10m_err the planned tiles left more chains,
-            // 11.2 M against 10.9 M -- its graph is cut by error branches, not by tile edges)
-            unsigned int *bm = nullptr;
-            if (k & 1)
-                k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
-            else
-                k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
-            b3_marked = bm != nullptr;
-        } else {  // rejected records (no room in the record table) in a scratch array laid out as recs2
-            EC_CHECK(s->skrej.ensure(Bk * fcap * 16));
-            uint4 *rej = s->skrej.as<uint4>();
-            if (k & 1)
-                k_skbucket_filtd<2048, 2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, rej,
-                                                                                      dbg);
-            else
-                k_skbucket_filtd<2048, 2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, rej,
-                                                                                     dbg);
-        }
+        // (round 4 measured a record merge in front of the filter on ecoli10m_err: its 1535-entry
+        // tables filled -- up to 915 records a bucket rejected -- and its 131 KB of LDS held one
+        // workgroup per CU: compact 8.26 ms against 7.75 without it; removed in round 5.
+        // No tile planning here: measured on ecoli10m_err the planned tiles left more chains,
+        // 11.2 M against 10.9 M -- its graph is cut by error branches, not by tile edges)
+        unsigned int *bm = nullptr;
+        if (k & 1)
+            k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
+        else
+            k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
+        b3_marked = bm != nullptr;
     } else if (plan.slots == 1024) {
         constexpr int NT3 = 512;
         const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
@@ -2211,14 +2197,14 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
 // weighted ruling set; per chain its path key / rank (rt_pks / rt_rks), paths' and cycles'
 // length / min first event at their key nodes (PL / PM)
 int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr, int &rounds,
-                const unsigned long long *dM = nullptr, bool defer = false, bool pre_init = false) {
+                bool pre_init = false) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc{};
     SuperRec *srec = s->rt_srec.as<SuperRec>();
     unsigned int *SIDX = s->rt_sidx.as<unsigned int>();
-    const size_t cap = dM ? std::max<size_t>(N, 1) : std::max<size_t>(M, 1);  // (dM: M <= N chains)
+    const size_t cap = std::max<size_t>(M, 1);
     EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec)));
     EC_CHECK(s->rt_hasp.ensure(cap));
     EC_CHECK(s->rt_pks.ensure(cap * 4));
@@ -2230,37 +2216,6 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
     EC_CHECK(s->st1.ensure(cap * sizeof(RJump)));
     EC_CHECK(s->rbc.ensure(((cap + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
     SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
-    if (kn().rank_coop == 1 || dM) {  // one cooperative launch (rank_tile.h k_rank_supers_coop)
-        if (!s->coop_grid) {
-            int per = 0, cus = 0;
-            EC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_rank_supers_coop, 256, 0));
-            EC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device));
-            s->coop_grid = (unsigned int)std::max(1, std::min(per, 4) * cus);
-        }
-        const unsigned int G = s->coop_grid;
-        EC_CHECK(s->rt_coop.ensure(((size_t)G + 16) * 4));
-        unsigned int *flags = s->rt_coop.as<unsigned int>(), *bcnt = flags + 16;
-        EC_HIP(hipMemsetAsync(flags, 0, 16 * 4, st));
-        EC_HIP(hipMemsetAsync(dsc->active, 0, sizeof(dsc->active), st));
-        EC_HIP(hipMemsetAsync(&dsc->coop_bad, 0, 8, st));
-        CoopRank a{srec, SIDX, snrec, s->rt_hasp.as<uint8_t>(), s->rid.as<uint2>(), s->rlist.as<unsigned int>(),
-                   s->nextR.as<unsigned int>(), s->st0.as<RJump>(), s->st1.as<RJump>(), bcnt, flags, dsc->active,
-                   &dsc->final_sel, &dsc->coop_bad, &dsc->coop_nr, M, N, dM, s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
-                   s->PL.as<unsigned int>(), s->PM.as<unsigned long long>()};
-        void *args[] = {&a};
-        EC_HIP(hipLaunchCooperativeKernel((const void *)k_rank_supers_coop, dim3(G), dim3(256), args, 0, st));
-        rounds = 63;  // (the callers' convergence flag: active[62])
-        nr = 0;
-        if (defer) return EC_OK;  // (coop_bad / coop_nr checked with the caller's next scalar read)
-        EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
-        EC_CHECK(host_sync(s, st));
-        if (hsc.coop_bad) {
-            set_error("ruling set left chains unvisited (%u chains)", M);
-            return EC_ERR_STATE;
-        }
-        nr = hsc.coop_nr;
-        return EC_OK;
-    }
     if (!pre_init) EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));  // (pre_init: k_tile_compact did these)
     k_super_link<<<grid_for(M, B), B, 0, st>>>(srec, M, SIDX, snrec, s->rt_hasp.as<uint8_t>());
     if (!pre_init) {
@@ -2511,7 +2466,6 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->PM.ensure(Nn * 8));
     unsigned int nr = 0;
     int rounds = 0;  // Wyllie rounds launched (their convergence is checked with the results)
-    bool coop_deferred = false;  // the cooperative ranking's checks wait for the next scalar read
     bool rank_async = false;     // rank_supers_async: its checks wait for the next scalar read
     const unsigned long long *async_M = nullptr;  // (the chain count on the device)
     unsigned int *async_LH = nullptr, *async_LR = nullptr;
@@ -2553,14 +2507,10 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                 s->PL.as<unsigned int>(), s->PM.as<unsigned long long>(), 0u, tbp);
         EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
         // (2) the super list: compacted in tile order, linked, ranked by the weighted ruling set
-        // -- in one cooperative launch that reads the chain count on the device (no host round
-        // trip; its checks ride on the scalar read after the starts), or by separate launches
+        // (round 4 measured the same sequence as one cooperative launch: rank stage 0.63 -> 3.3
+        // ms, its grid barriers far slower than the launches they replace; removed in round 5)
         unsigned int M = 0;
-        // (measured: the cooperative launch took the headline's rank stage 0.63 -> 3.3 ms, its
-        // grid barriers far slower than the launches they replace -- opt-in only)
-        const bool coop = kn().rank_coop == 1;
-        coop_deferred = coop;
-        rank_async = !coop && kn().rank_sync != 1;
+        rank_async = kn().rank_sync != 1;
         async_M = tbase + ntiles;
         async_LH = LH;
         async_LR = LR;
@@ -2573,10 +2523,6 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
                                                   s->RK.as<unsigned int>());
-        } else if (coop) {
-            k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
-                                                   s->rt_sidx.as<unsigned int>(), nullptr, nullptr, nullptr, nullptr,
-                                                   nullptr, tbp);
         } else {
             // the chain count read back while k_tile_compact (sized by the tiles, not by M) runs:
             // the host's wake-up and next launches overlap the compaction
@@ -2590,8 +2536,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             EC_CHECK(host_wait(s, s->rd_ev));
             M = (unsigned int)M64;
         }
-        if (!rank_async && (coop || M)) {
-            EC_CHECK(rank_supers(s, M, N, nr, rounds, coop ? tbase + ntiles : nullptr, coop, !coop));
+        if (!rank_async && M) {
+            EC_CHECK(rank_supers(s, M, N, nr, rounds, true));
             // (3) every node: its chain's key and rank + its offset in the chain
             k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
@@ -2704,13 +2650,6 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             s->stats.n_rulers = nr;
             EC_CHECK(starts_pass());
         }
-    }
-    if (coop_deferred) {
-        if (hsc.coop_bad) {
-            set_error("ruling set left chains unvisited");
-            return EC_ERR_STATE;
-        }
-        s->stats.n_rulers = nr = hsc.coop_nr;
     }
     if (rounds) {
         unsigned int used = 1;
@@ -3530,7 +3469,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->rt_coop, &s->wbv, &s->skrej, &s->bmark, &s->rt_tb,
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
                      &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt};
     for (auto *b : all) b->release();
     s->h_chars.release();

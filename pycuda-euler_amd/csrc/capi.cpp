@@ -54,11 +54,9 @@ void refresh_knobs() {
         k.rank = num("EULERHIP_RANK", -1);
         k.sk_filt = num("EULERHIP_SK_FILT", -1);
         k.skf_keys = num("EULERHIP_SKF_KEYS", 0);
-        k.rank_coop = num("EULERHIP_RANK_COOP", -1);
         k.wide_mb = num("EULERHIP_WIDE_MB", -1);
         k.join_mb = num("EULERHIP_JOIN_MB", -1);
         k.sruler_mask = num("EULERHIP_SRULER_MASK", 0);
-        k.skf_dedup = num("EULERHIP_SKF_DEDUP", -1);
     }
     g_knobs = k;
 }

@@ -51,9 +51,7 @@ struct Knobs {
     int rank = -1;              // EULERHIP_RANK: list ranking 0 = tile contraction (rank_tile.h), 1 = node ruling set
     int sk_filt = -1;           // EULERHIP_SK_FILT: 0 = error-rich inputs on window records, not k_skbucket_filt
     int skf_keys = 0;           // EULERHIP_SKF_KEYS: k_skbucket_filt's keys-per-table cap (forces its overflow)
-    int rank_coop = -1;      // EULERHIP_RANK_COOP=0: the super list ranked by separate launches
     int wide_mb = -1;        // EULERHIP_WIDE_MB=0: 128-bit keys bucketed by mix128, not by minimizer
-    int skf_dedup = -1;      // EULERHIP_SKF_DEDUP=1: the seen-twice super-k-mer filter behind a record merge
     int sruler_mask = 0;     // EULERHIP_SRULER_MASK: first ruler pass of the super list takes 1 / (mask + 1)
     int join_mb = -1;        // EULERHIP_JOIN_MB=0: junctions of minimizer-bucketed keys bucketed by mix128
 };

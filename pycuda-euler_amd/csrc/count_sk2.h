@@ -1263,277 +1263,5 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
                                                                       EvExpand{2 * M}, bmark);
 }
 
-// ---- the same behind a record merge (round 4) ------------------------------------------------
-// k_skbucket_filt rolls out every record occurrence twice: at ecoli10m_err ~1e9 windows a pass,
-// 7.7 ms.  Most records there are still error-free super-k-mers seen ~coverage times, so a
-// bucket's records are first merged in an LDS record table (k_skbucket3's protocol: canonical
-// content, tag claim by CAS, multiplicity, min events); the filter passes then run over the
-// distinct records (a record seen twice or more has only keys seen twice: its cells are marked
-// seen-twice directly, its windows inserted with count += multiplicity) and over the records the
-// table had no room for, which go to the bucket's range of a scratch array (rej, laid out as the
-// records) and are rolled out one occurrence at a time.
-template <int SLOTS, int RS, int NT, bool EVEN_K>
-__global__ void __launch_bounds__(NT) k_skbucket_filtd(const uint4 *recs_in, const unsigned long long *bbeg,
-                                                       const unsigned long long *bend, int k, uint32_t M,
-                                                       double inv_m, long long limit, unsigned long long *dkey,
-                                                       unsigned int *dcnt, unsigned long long *dfc,
-                                                       unsigned long long *dft, SubSlot *sub, unsigned int *nsolid,
-                                                       unsigned long long *ndistinct, unsigned int *overflow,
-                                                       unsigned int max_keys, uint4 *rej,
-                                                       unsigned long long *dbg = nullptr) {
-    constexpr int SBITS = __builtin_ctz(SLOTS);
-    constexpr uint32_t PEND = 0x800u;
-    constexpr unsigned int CLAIM_MAX = RS - 1 - NT;
-    static_assert(RS > NT + 1, "record table too small for the records in flight");
-    constexpr unsigned int NW = 1u << (SKF_BITS - 5), CM = (1u << SKF_BITS) - 1;
-    __shared__ uint32_t r_tag[RS], r_x[RS], r_y[RS], r_z[RS], r_mult[RS], r_a[RS], r_b[RS];
-    __shared__ LTabE<SLOTS> tab;
-    __shared__ unsigned int seen1[NW], seen2[NW];
-    __shared__ unsigned int s_over[2], s_cells[2], s_nent, s_nrej;
-    const uint4 *recs = recs_in;
-    const unsigned int b = blockIdx.x, tid = threadIdx.x;
-    for (int i = tid; i < RS; i += NT) {
-        r_tag[i] = 0;
-        r_mult[i] = 0;
-        r_a[i] = r_b[i] = 0xFFFFFFFFu;
-    }
-    for (int i = tid; i < SLOTS; i += NT) {
-        tab.key[i] = EMPTY_KEY;
-        tab.count[i] = 0;
-        tab.ev[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-    }
-    for (unsigned int i = tid; i < NW; i += NT) seen1[i] = seen2[i] = 0;
-    if (tid == 0) s_over[0] = s_over[1] = 0, s_cells[0] = s_cells[1] = 0, s_nent = 0, s_nrej = 0;
-    __syncthreads();
-    const uint64_t r0 = bbeg[b], r1 = bend[b];
-    const uint64_t kmask = kmask64(k);
-    const int sh = 2 * (k - 1), fsh = 64 - 2 * k;
-    const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
-
-    // ---- records -> record table (k_skbucket3's record_round; rejected records kept in place)
-    constexpr int PD = SK2_PD;
-    uint4 nx[PD];
-#pragma unroll
-    for (int d = 0; d < PD; d++) nx[d] = recs[r1 > r0 ? min(r0 + tid + (uint64_t)d * NT, r1 - 1) : r0];
-    auto ld = [](uint32_t *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    auto record_round = [&](uint4 &nxd, uint64_t c0) {
-        const uint64_t ri = c0 + tid;
-        const bool valid = ri < r1;
-        const uint4 x = nxd;
-        nxd = recs[min(ri + PD * NT, r1 - 1)];
-        const unsigned int n = (x.z >> 28) + 1, L2 = 2 * (n + (unsigned int)k - 1);
-        const uint32_t m1 = L2 >= 64 ? 0xFFFFFFFFu : (1u << ((L2 - 32) & 31)) - 1u;
-        const uint32_t mw2 = L2 > 64 ? (1u << ((L2 - 64) & 31)) - 1u : 0u;
-        const uint32_t x0 = x.x, x1 = x.y & m1, x2 = x.z & mw2;
-        const uint32_t y0 = rev2_32b(x2), y1 = rev2_32b(x1), y2 = rev2_32b(x0);
-        const unsigned int sft = 96 - L2, s5 = sft & 31;
-        const bool lo = sft < 32;
-        const uint32_t a0 = __builtin_amdgcn_alignbit(y1, y0, s5), a1 = __builtin_amdgcn_alignbit(y2, y1, s5),
-                       a2 = y2 >> s5;
-        const uint32_t q0 = ~(lo ? a0 : a1), q1 = ~(lo ? a1 : a2) & m1, q2 = lo ? ~a2 & mw2 : 0u;
-        const bool flip = q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0;
-        const unsigned int p = x.w;
-        const unsigned int rd0 = (unsigned int)((double)p * inv_m);
-        int rm = (int)(p - rd0 * M);
-        unsigned int rd = rd0;
-        if (rm < 0) rd--, rm += (int)M;
-        else if (rm >= (int)M) rd++, rm -= (int)M;
-        const unsigned int A = rd * M2 + (unsigned int)rm, B = rd * M2 + m2 - (unsigned int)rm;
-        const uint32_t K0 = flip ? q0 : x0, K1 = flip ? q1 : x1, K2 = (flip ? q2 : x2) | (n - 1) << 28;
-        const uint32_t EA = flip ? B - n + 1 : A, EB = flip ? A + n - 1 : B;
-        uint32_t hh = K0 * 0x9E3779B1u;
-        hh = (hh ^ (hh >> 15) ^ K1) * 0x85EBCA77u;
-        hh = (hh ^ (hh >> 13) ^ K2) * 0xC2B2AE3Du;
-        hh ^= hh >> 16;
-        const uint32_t TG = (hh | 0x1000u) & 0xFFFFF000u;
-        uint32_t SL = __umulhi(hh * 0x27D4EB2Fu, (unsigned int)RS);
-        int ST = valid ? 0 : 1;  // 0 searching, 1 found / claimed, 2 no room
-#pragma unroll 1
-        while (__any(ST == 0)) {
-            const uint32_t T = ld(&r_tag[SL]);
-            asm volatile("" ::: "memory");
-            const uint32_t X = ld(&r_x[SL]), Y = ld(&r_y[SL]), Z = ld(&r_z[SL]);
-            const bool hit = T == TG && X == K0 && Y == K1 && Z == K2;
-            const bool go = ST == 0;
-            ST = go && hit ? 1 : ST;
-            const bool claim = go && !hit && T == 0;
-            if (go && !hit && T != 0 && T != (TG | PEND)) SL = SL + 1 == (unsigned int)RS ? 0u : SL + 1;
-            if (claim) {
-                const unsigned int o = atomicAdd(&s_nent, 1u);
-                if (o >= CLAIM_MAX) {
-                    atomicSub(&s_nent, 1u);
-                    ST = 2;
-                } else if (atomicCAS(&r_tag[SL], 0u, TG | PEND) == 0) {
-                    r_x[SL] = K0, r_y[SL] = K1, r_z[SL] = K2;
-                    __hip_atomic_store(&r_tag[SL], TG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    ST = 1;
-                } else {
-                    atomicSub(&s_nent, 1u);
-                }
-            }
-        }
-        if (valid && ST == 1) {
-            atomicAdd(&r_mult[SL], 1u);
-            if (EA < r_a[SL]) atomicMin(&r_a[SL], EA);
-            if (EB < r_b[SL]) atomicMin(&r_b[SL], EB);
-        }
-        if (ST == 2) rej[r0 + atomicAdd(&s_nrej, 1u)] = x;
-    };
-    for (uint64_t c0 = r0; c0 < r1; c0 += PD * NT) {
-#pragma unroll
-        for (int d = 0; d < PD; d++) {
-            if (c0 + (uint64_t)d * NT >= r1) break;  // uniform
-            record_round(nx[d], c0 + (uint64_t)d * NT);
-        }
-    }
-    __syncthreads();
-    const unsigned int nrej = s_nrej;  // (rej: written by this workgroup before the barrier)
-
-    // windows of a merged (canonical) record: key, add (2 for an even-k palindrome), events
-    auto merged_windows = [&](uint32_t x0, uint32_t x1, uint32_t x2, unsigned int ea, unsigned int eb, auto &&fn) {
-        const unsigned int n = (x2 >> 28) + 1;
-        uint64_t fw = 0, rv = 0;
-        for (unsigned int o = 0; o < n; o++) {
-            if (o == 0) {
-                const uint64_t P = (uint64_t)x0 | (uint64_t)x1 << 32;
-                rv = ~P & kmask;
-                fw = rev2_64(P) >> fsh;
-            } else {
-                const unsigned int tb = o + (unsigned int)k - 1;
-                const uint32_t wd = tb < 32 ? x1 : x2;
-                const uint32_t bb = (wd >> (2 * (tb & 15))) & 3u;
-                fw = ((fw << 2) | bb) & kmask;
-                rv = (rv >> 2) | ((uint64_t)(3u - bb) << sh);
-            }
-            const bool tw = fw > rv;
-            const unsigned int ef = ea + o, et = eb - o;
-            unsigned int add = 1, eC = tw ? et : ef, eT = tw ? ef : et;
-            if (EVEN_K && fw == rv) {
-                add = 2;
-                eC = eT = min(ef, et);
-            }
-            fn(tw ? rv : fw, add, eC, eT);
-        }
-    };
-    // windows of a raw record as stored (k_skbucket_filt's)
-    auto raw_windows = [&](const uint4 &x, auto &&fn) {
-        const unsigned int n = (x.z >> 28) + 1;
-        const unsigned int p = x.w;
-        const unsigned int rd0 = (unsigned int)((double)p * inv_m);
-        int rm = (int)(p - rd0 * M);
-        unsigned int rd = rd0;
-        if (rm < 0) rd--, rm += (int)M;
-        else if (rm >= (int)M) rd++, rm -= (int)M;
-        const unsigned int A = rd * M2 + (unsigned int)rm, B = rd * M2 + m2 - (unsigned int)rm;
-        for (unsigned int o = 0; o < n; o++) {
-            const uint32_t lo = __builtin_amdgcn_alignbit(x.y, x.x, 2 * o), hi = __builtin_amdgcn_alignbit(x.z, x.y, 2 * o);
-            const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
-            const uint64_t rv = ~P & kmask, fw = rev2_64(P) >> fsh;
-            const bool tw = fw > rv;
-            const unsigned int ef = A + o, et = B - o;
-            unsigned int add = 1, eC = tw ? et : ef, eT = tw ? ef : et;
-            if (EVEN_K && fw == rv) {
-                add = 2;
-                eC = eT = min(ef, et);
-            }
-            fn(tw ? rv : fw, add, eC, eT);
-        }
-    };
-    auto cells = [](unsigned long long c, unsigned int &c1, unsigned int &c2) {
-        const uint64_t h = mix64(c);
-        c1 = (unsigned int)(h >> 12) & CM;
-        c2 = (unsigned int)(h >> 30) & CM;
-    };
-    auto mark = [&](unsigned long long c, bool many) {
-        unsigned int c1, c2;
-        cells(c, c1, c2);
-        const unsigned int m1 = 1u << (c1 & 31), mm2 = 1u << (c2 & 31);
-        if (many) {
-            atomicOr(&seen1[c1 >> 5], m1), atomicOr(&seen2[c1 >> 5], m1);
-            atomicOr(&seen1[c2 >> 5], mm2), atomicOr(&seen2[c2 >> 5], mm2);
-        } else {
-            if (atomicOr(&seen1[c1 >> 5], m1) & m1) atomicOr(&seen2[c1 >> 5], m1);
-            if (atomicOr(&seen1[c2 >> 5], mm2) & mm2) atomicOr(&seen2[c2 >> 5], mm2);
-        }
-    };
-    auto twice = [&](unsigned long long c) {
-        unsigned int c1, c2;
-        cells(c, c1, c2);
-        return ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
-    };
-    auto insert = [&](unsigned long long c, unsigned int add, unsigned int eC, unsigned int eT) {
-        const unsigned int s0 = (sk_slot(c) >> (32 - SBITS)) & (SLOTS - 1);
-        const unsigned int sl = lds_locate<SLOTS>(tab, s_over, c, s0, tab.key[s0]);
-        atomicAdd(&tab.count[sl], add);
-        const uint2 v = tab.ev[sl];
-        if (eC < v.x) atomicMin(&tab.ev[sl].x, eC);
-        if (eT < v.y) atomicMin(&tab.ev[sl].y, eT);
-    };
-    // pass 0: the filter, from the merged records and the rejected ones
-    for (int i = tid; i < RS; i += NT) {
-        if (!r_tag[i]) continue;
-        const bool many = r_mult[i] >= 2u;
-        merged_windows(r_x[i], r_y[i], r_z[i], r_a[i], r_b[i],
-                       [&](unsigned long long c, unsigned int, unsigned int, unsigned int) { mark(c, many); });
-    }
-    for (uint64_t i = r0 + tid; i < r0 + nrej; i += NT)
-        raw_windows(rej[i], [&](unsigned long long c, unsigned int, unsigned int, unsigned int) { mark(c, false); });
-    __syncthreads();
-    {  // the predictor of k_skbucket_filt
-        unsigned int n2 = 0, n1 = 0;
-        for (unsigned int i = tid; i < NW; i += NT) n2 += __popc(seen2[i]), n1 += __popc(seen1[i]);
-        for (int o = 32; o > 0; o >>= 1) n2 += __shfl_down(n2, o), n1 += __shfl_down(n1, o);
-        if ((tid & 63) == 0) atomicAdd(&s_cells[0], n2), atomicAdd(&s_cells[1], n1);
-        __syncthreads();
-        if (tid == 0) {
-            const double m = (double)(1u << SKF_BITS);
-            const double D = -m * log(1.0 - (double)min(s_cells[1], CM) / m) / 2.0;
-            const double l = 2.0 * D / m, el = exp(-l);
-            const double S = fmax(0.0, ((double)s_cells[0] - m * (1.0 - el * (1.0 + l))) / 2.0);
-            const double pass = 1.1 * (S + fmax(0.0, D - S) * (1.0 - el) * (1.0 - el));
-            if (pass > (double)max_keys) s_over[0] = 1;
-            else atomicAdd(ndistinct, (unsigned long long)llround(D));
-            if (dbg) {
-                atomicMax(&dbg[0], (unsigned long long)D);
-                atomicMax(&dbg[1], (unsigned long long)pass);
-                atomicMax(&dbg[2], (unsigned long long)s_cells[0]);
-                atomicMax(&dbg[3], (unsigned long long)(bend[b] - bbeg[b]));
-                if (s_over[0]) atomicAdd(&dbg[4], 1ull);
-                atomicMax(&dbg[7], (unsigned long long)s_nent);  // most merged records
-                atomicMax(&dbg[8], (unsigned long long)nrej);    // most rejected records
-            }
-        }
-        __syncthreads();
-    }
-    if (s_over[0]) {
-        if (tid == 0) atomicAdd(overflow, 1u);
-        return;
-    }
-    // pass 1: keys seen twice (or solid by their own insert) into the table
-    for (int i = tid; i < RS; i += NT) {
-        if (!r_tag[i]) continue;
-        const unsigned int mu = r_mult[i];
-        merged_windows(r_x[i], r_y[i], r_z[i], r_a[i], r_b[i],
-                       [&](unsigned long long c, unsigned int add, unsigned int eC, unsigned int eT) {
-                           if (mu < 2u && !twice(c) && (long long)add <= limit) return;
-                           insert(c, add * mu, eC, eT);
-                       });
-    }
-    for (uint64_t i = r0 + tid; i < r0 + nrej; i += NT)
-        raw_windows(rej[i], [&](unsigned long long c, unsigned int add, unsigned int eC, unsigned int eT) {
-            if (!twice(c) && (long long)add <= limit) return;
-            insert(c, add, eC, eT);
-        });
-    if (dbg) {
-        __syncthreads();
-        if (tid == 0) {
-            if (s_over[0]) atomicAdd(&dbg[5], 1ull);
-            atomicMax(&dbg[6], (unsigned long long)s_over[1]);
-        }
-    }
-    lds_table_finish<SLOTS, false, KeyId, LTabE<SLOTS>, EvExpand, NT>(tab, s_over, b, limit, dkey, dcnt, dfc, dft, sub,
-                                                                      nsolid, nullptr, overflow, KeyId(),
-                                                                      EvExpand{2 * M});
-}
 
 }  // namespace ec

@@ -251,6 +251,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_partition(const uint8_t *__restr
     uint4 pf[NPF];
     uint64_t nx_base = 0;
     uint32_t nx_s = 0, nx_e = 0, nx_n = 0, nx_lo = 0, nx_hi = 0, nx_n16 = 0;
+    (void)nx_lo;
     if (wid < ntile) EC_PT_ISSUE(wid);
     const unsigned long long gcap = g * C * cap, gstride = cap;
     const unsigned long long spill = (unsigned long long)C * G * cap;

@@ -18,7 +18,6 @@
 // chain position written and read back, PK / RK written; the random accesses of the ruler walk
 // touch only the ~N/9 super nodes (one 16-B record each).
 #pragma once
-#include <hip/hip_cooperative_groups.h>
 
 #include "graph.h"
 
@@ -132,7 +131,6 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
     bool anyc = false;
 #pragma unroll
     for (int q = 0; q < RT_PER; q++) {
-        const unsigned int i = tid + q * RT_NT;
         cyc[q] = valid[q] && s_lp[p[q]] != RT_NONE;
         anyc |= cyc[q];
     }
@@ -177,7 +175,6 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         if (fev[q] < s_cm[h]) atomicMin(&s_cm[h], fev[q]);
     }
     __syncthreads();
-    unsigned int nh = 0;  // chain heads of this thread (super nodes)
 #pragma unroll
     for (int q = 0; q < RT_PER; q++) {
         const unsigned int i = tid + q * RT_NT, x = base + i;
@@ -196,7 +193,6 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
             }
         } else {
             LH[x] = h;
-            nh += d[q] == 0;
         }
         LR[x] = d[q];
     }
@@ -482,222 +478,6 @@ __global__ void __launch_bounds__(256) k_cycle_len_s(const unsigned int *nextR, 
             const unsigned int key = srec[r.cm].head;
             PL[key] = r.cd + r.len;
             PM[key] = r.fm;
-        }
-    }
-}
-
-// ---- the super list ranked in one cooperative launch (round 4) -----------------------------
-// rank_supers' sequence -- super links, up to four ruler selections each followed by the
-// rulers' walks, the weighted Wyllie rounds, finalize -- as phases of one grid separated by
-// grid-wide barriers (hipLaunchCooperativeKernel: every block resident).  Launched as separate
-// kernels it was ~30 launches plus a host round trip per ruler pass (~0.3 ms of gaps on the
-// headline); here ruler ids come from per-block counts prefix-summed by every block (no
-// contended counter), "any node unvisited" and "any pointer still moving" are plain flag
-// stores read after the barrier, so every block takes the same branch.
-struct CoopRank {
-    const SuperRec *srec;
-    const unsigned int *SIDX;
-    SNodeRec *nrec;
-    uint8_t *hasp;
-    uint2 *rid;
-    unsigned int *rlist, *nextR;
-    RJump *rs0, *rs1;
-    unsigned int *bcnt;    // per block: rulers selected
-    unsigned int *flags;   // [it] = a node unvisited after ruler pass it
-    unsigned int *active;  // [r] = a pointer moved in Wyllie round r; [62] = not converged
-    unsigned int *final_sel;
-    unsigned int *out_bad, *out_nr;  // (the session's scalars: read with its next scalar read)
-    unsigned int M, N;
-    const unsigned long long *dM;  // if set: M read on the device (the tile compaction's total)
-    unsigned int *PKs, *RKs, *PL;
-    unsigned long long *PM;
-};
-
-__device__ inline unsigned int coop_block_sum(unsigned int v, unsigned int *s_w) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
-    __syncthreads();
-    return s_w[0] + s_w[1] + s_w[2] + s_w[3];
-}
-
-__global__ void __launch_bounds__(256) k_rank_supers_coop(CoopRank a) {
-    auto grid = cooperative_groups::this_grid();
-    __shared__ unsigned int s_w[4];
-    const unsigned int G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
-    const uint64_t gt = (uint64_t)b * 256 + tid, gs = (uint64_t)G * 256;
-    const unsigned int M = a.dM ? (unsigned int)*a.dM : a.M;
-    for (uint64_t t = gt; t < M; t += gs) {  // (no host memsets: M may be known only here)
-        a.hasp[t] = 0;
-        a.rid[t] = make_uint2(NONE32, NONE32);
-    }
-    grid.sync();
-    // super links (k_super_link)
-    for (uint64_t t = gt; t < M; t += gs) {
-        const SuperRec r = a.srec[t];
-        const unsigned int sx = r.succ == NONE32 ? NONE32 : a.SIDX[r.succ];
-        SNodeRec o;
-        o.succ = sx;
-        o.w = r.w;
-        o.fev = r.fmin;
-        a.nrec[t] = o;
-        if (sx != NONE32) a.hasp[sx] = 1;
-    }
-    grid.sync();
-    // ruler passes: select (deterministic ids: block b's range [lo, hi) in order), walk, check
-    const unsigned int masks[4] = {15u, 3u, 1u, 0u};
-    const unsigned int lo = (unsigned int)((uint64_t)M * b / G), hi = (unsigned int)((uint64_t)M * (b + 1) / G);
-    const unsigned int lane = tid & 63, wid = tid >> 6;
-    unsigned int r0 = 0;
-    int it = 0;
-    for (; it < 4; it++) {
-        const unsigned int mk = masks[it];
-        const int first = it == 0;
-        unsigned int c = 0;
-        for (unsigned int t = lo + tid; t < hi; t += 256) c += sruler_sel(a.hasp, a.rid, t, mk, first);
-        c = coop_block_sum(c, s_w);
-        if (tid == 0) a.bcnt[b] = c;
-        grid.sync();
-        unsigned int pre = 0, tot = 0;
-        for (unsigned int q = tid; q < G; q += 256) {
-            const unsigned int v = a.bcnt[q];
-            tot += v;
-            if (q < b) pre += v;
-        }
-        pre = coop_block_sum(pre, s_w);
-        tot = coop_block_sum(tot, s_w);
-        unsigned int base = r0 + pre;
-        for (unsigned int t0 = lo; t0 < hi; t0 += 256) {
-            const unsigned int t = t0 + tid;
-            const bool sel = t < hi && sruler_sel(a.hasp, a.rid, t, mk, first);
-            const unsigned long long m = __ballot(sel);
-            __syncthreads();
-            if (lane == 0) s_w[wid] = (unsigned int)__popcll(m);
-            __syncthreads();
-            unsigned int off = base;
-            for (unsigned int q = 0; q < wid; q++) off += s_w[q];
-            if (sel) {
-                const unsigned int i = off + (unsigned int)__popcll(m & ((1ull << lane) - 1));
-                a.rlist[i] = t;
-                a.rid[t] = make_uint2(i, 0u);
-            }
-            base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        }
-        const unsigned int r1 = r0 + tot;
-        grid.sync();
-        for (uint64_t t = r0 + gt; t < r1; t += gs) {  // k_walk_s
-            const unsigned int i = (unsigned int)t;
-            unsigned int v = a.rlist[i];
-            const SNodeRec s0 = a.nrec[v];
-            unsigned long long fm = s0.fev;
-            unsigned int j = 0, wl = s0.w, nx = NONE32, w = s0.succ;
-            for (;;) {
-                if (w == NONE32) break;
-                if (ruler_hash(w, mk)) {
-                    const unsigned int q = a.rid[w].x;
-                    if (q != NONE32) {
-                        nx = q;
-                        break;
-                    }
-                }
-                v = w;
-                j += wl;
-                const SNodeRec s1 = a.nrec[v];
-                w = s1.succ;
-                wl = s1.w;
-                a.rid[v] = make_uint2(i, j);
-                fm = s1.fev < fm ? s1.fev : fm;
-            }
-            a.nextR[i] = nx;
-            RJump r;
-            r.a = NONE32;
-            r.s = 0;
-            r.h = i;
-            r.cm = a.rlist[i];
-            r.cd = 0;
-            r.len = j + wl;
-            r.fm = fm;
-            a.rs0[i] = r;
-        }
-        grid.sync();
-        bool any = false;
-        for (unsigned int t = lo + tid; t < hi; t += 256) any |= a.rid[t].x == NONE32;
-        if (__syncthreads_or(any) && tid == 0) a.flags[it] = 1u;
-        r0 = r1;
-        grid.sync();
-        if (!a.flags[it]) break;
-    }
-    if (it == 4) {  // (mask 0 selects every unvisited node: cannot happen)
-        if (gt == 0) *a.out_bad = 1u;
-        return;
-    }
-    const unsigned int nr = r0;
-    if (gt == 0) *a.out_nr = nr;
-    for (uint64_t t = gt; t < nr; t += gs) {  // k_rjump_init
-        const unsigned int n = a.nextR[t];
-        if (n != NONE32) a.rs0[n].a = (unsigned int)t;
-    }
-    grid.sync();
-    // weighted Wyllie rounds (k_rjump) until no pointer moves
-    unsigned int sel = 0;
-    int r = 0;
-    for (; r < 62; r++) {
-        const RJump *src = (r & 1) ? a.rs1 : a.rs0;
-        RJump *dst = (r & 1) ? a.rs0 : a.rs1;
-        unsigned int act = 0;
-        for (uint64_t t = gt; t < nr; t += gs) {
-            RJump j = src[t];
-            if (j.a != NONE32 && j.s < a.N) {
-                const RJump y = src[j.a];
-                const unsigned int back = j.s + y.len;
-                if (y.cm < j.cm) {
-                    j.cm = y.cm;
-                    j.cd = back + y.cd;
-                }
-                j.s = back + y.s;
-                j.a = y.a;
-                j.h = y.h;
-                j.fm = y.fm < j.fm ? y.fm : j.fm;
-                act += (j.a != NONE32 && j.s < a.N);
-            }
-            dst[t] = j;
-        }
-        if (__syncthreads_or(act != 0) && tid == 0) a.active[r] = 1u;
-        sel = (unsigned int)((r + 1) & 1);
-        grid.sync();
-        if (!a.active[r]) break;
-    }
-    if (gt == 0) {
-        *a.final_sel = sel;
-        if (r == 62) a.active[62] = 1u;  // still moving after 62 rounds: not converged
-    }
-    if (r == 62) return;  // (the host reports it; the callers' finalize placeholders run there)
-    const RJump *rs = sel ? a.rs1 : a.rs0;
-    for (uint64_t t = gt; t < M; t += gs) {  // k_finalize_s
-        const unsigned int v = (unsigned int)t;
-        const uint2 ro = a.rid[v];
-        const RJump rr = rs[ro.x];
-        if (rr.a == NONE32) {
-            const unsigned int pk = a.srec[a.rlist[rr.h]].head, rk = rr.s + ro.y;
-            a.PKs[v] = pk;
-            a.RKs[v] = rk;
-            if (a.nrec[v].succ == NONE32) {
-                a.PL[pk] = rk + a.nrec[v].w;
-                a.PM[pk] = rr.fm;
-            }
-        } else {
-            a.PKs[v] = a.srec[rr.cm].head | CYC;
-            a.RKs[v] = rr.cd + ro.y;
-        }
-    }
-    for (uint64_t t = gt; t < nr; t += gs) {  // k_cycle_len_s
-        const RJump rr = rs[t];
-        if (rr.a == NONE32) continue;
-        const unsigned int n = a.nextR[t];
-        if (n != NONE32 && a.rlist[n] == rr.cm) {
-            const unsigned int key = a.srec[rr.cm].head;
-            a.PL[key] = rr.cd + rr.len;
-            a.PM[key] = rr.fm;
         }
     }
 }
