@@ -355,6 +355,17 @@ uint64_t ec_dense_count(ec_session *s);
  * Owner of a canonical key: for 21 <= k <= 32 the range of its minimizer ((minimizer * nowners)
  * >> 32, the merge / load bucket key), else a 64-bit hash of the key (shard.h OwnerFn). */
 int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts);
+/* the same with compact = 1 (round 5): where this shard's events fit, 20-B records (28 B for
+ * k > 32: key, count, the two first events shard-relative as (read << *lf_bits) | position)
+ * instead of 32 / 48 B, *lf_bits >= 0; else full records with global events, *lf_bits = -1.
+ * d_out is sized for full records either way.  The receiver merges with ec_merge_owned_from. */
+int ec_export_by_owner_ex(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts, int compact,
+                          int *lf_bits);
+int ec_compact_record_bytes(int k);
+/* ec_merge_owned on what nsrc ranks sent (source q: src_bytes[q] bytes, its global read base
+ * and its records' lf_bits from ec_export_by_owner_ex; the sources in rank order) */
+int ec_merge_owned_from(ec_session *s, const void *d_records, int nsrc, const uint64_t *src_bytes,
+                        const int64_t *src_read_base, const int32_t *src_lf_bits, int k, int limit, unsigned flags);
 /* owner rule of ec_export_by_owner: 0 (default) = the minimizer's range for 21 <= k <= 32, else a
  * key hash; 1 = the key hash always (distributed.py switches every rank to it when the job's
  * minimizer-range counts, all-reduced, show one owner past twice the mean -- low-complexity

@@ -208,6 +208,7 @@ struct ec_session {
     bool placed = false;
     uint64_t seg_lo = 0, seg_Ur = 0;
     DevBuf jrec, joid, jout, jseg, jcnt;
+    DevBuf xrec;  // ec_merge_owned_from: the received records decoded
     int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 52), 1 key hash
     // ec_export_by_owner's owner ids / scanned chunk histogram of the last call, reused by a
     // following call with the same records, owners and rule (counts first, then the scatter)
@@ -3470,7 +3471,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
                      &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
-                     &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt};
+                     &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->bounce.release();
@@ -3749,6 +3750,11 @@ int ec_session_set_owner_rule(ec_session *s, int rule) {
 }
 
 int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts) {
+    return ec_export_by_owner_ex(s, nowners, d_out, owner_counts, 0, nullptr);
+}
+
+int ec_export_by_owner_ex(ec_session *s, int nowners, void *d_out, uint64_t *owner_counts, int compact,
+                          int *lf_bits) {
     refresh_knobs();
     if (!s || nowners < 1 || nowners > MAX_OWNERS || !owner_counts) {
         set_error("bad ec_export_by_owner arguments (nowners=%d)", nowners);
@@ -3766,22 +3772,49 @@ int ec_export_by_owner(ec_session *s, int nowners, void *d_out, uint64_t *owner_
     OwnerFn own = owner_fn(s->k);
     if (s->owner_rule == 1) own.sk = 0, own.wk = 0;  // key-hash owners (a skewed minimizer distribution)
     EC_CHECK(s->mbid.ensure(std::max<uint64_t>(n, 1) * 4));  // owner of each record (free until a merge)
+    EC_CHECK(s->ocnt.ensure(2 * nbh * 4 + 16));
+    bh = s->ocnt.as<unsigned int>(), bhi = bh + nbh;
+    unsigned int *evmax = bhi + nbh;  // largest shard-relative read id / position of the events
     unsigned int *oid = s->mbid.as<unsigned int>();
     const bool reuse = s->own_valid && s->own_rule == s->owner_rule && s->own_nowners == nowners && s->own_n == n &&
                        s->own_nblk == nblk;
     if (!reuse) {
-        s->own_hi.assign(nbh, 0u);
+        s->own_hi.assign(nbh + 2, 0u);
         if (n) {
+            EC_HIP(hipMemsetAsync(evmax, 0, 8, st));
             if (wide)
-                k_owner_hist<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), n, nowners, nblk, bh, own, oid);
+                k_owner_hist<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), n, nowners, nblk, bh, own, oid,
+                                                       s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                       evmax);
             else
                 k_owner_hist<unsigned long long><<<nblk, B, 0, st>>>(s->dkey.as<unsigned long long>(), n, nowners, nblk,
-                                                                    bh, own, oid);
+                                                                    bh, own, oid, s->dfc.as<unsigned long long>(),
+                                                                    s->dft.as<unsigned long long>(), evmax);
             EC_CHECK(scan_incl_u32(s, bh, bhi, nbh));
-            EC_CHECK(d2h(s, s->own_hi.data(), bhi, nbh * 4, st));
+            EC_CHECK(d2h(s, s->own_hi.data(), bhi, nbh * 4 + 8, st));  // (+ the event maxima)
         }
+        if (compact && n) EC_CHECK(host_sync(s, st));  // (the event widths choose the record format)
     }
-    if (n && d_out) {  // the scatter is queued before the host waits for the owner counts
+    int lfb = -1;  // compact records: bits of the window position (the read id above them), else full
+    if (compact && lf_bits) {
+        const unsigned int mr = n ? s->own_hi[nbh] : 0u, ml = n ? s->own_hi[nbh + 1] : 0u;
+        int lb = 1, rb = 0;
+        while (lb < 31 && (ml >> lb)) lb++;
+        while (rb < 32 && (mr >> rb)) rb++;
+        // (the all-ones code is "no event": it must stay out of range)
+        if (lb + rb <= 32 && !(lb + rb == 32 && mr == (0xFFFFFFFFu >> lb) && ml == (1u << lb) - 1)) lfb = lb;
+        *lf_bits = lfb;
+    }
+    if (n && d_out && lfb >= 0) {  // compact records (shard-relative events)
+        if (wide)
+            k_owner_scatter_c<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), s->dcnt.as<unsigned int>(),
+                                                        s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                        n, nowners, nblk, bhi, reinterpret_cast<CRecW *>(d_out), lfb, oid);
+        else
+            k_owner_scatter_c<unsigned long long><<<nblk, B, 0, st>>>(
+                s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),
+                s->dft.as<unsigned long long>(), n, nowners, nblk, bhi, reinterpret_cast<CRec *>(d_out), lfb, oid);
+    } else if (n && d_out) {  // the scatter is queued before the host waits for the owner counts
         if (wide)
             k_owner_scatter<K128><<<nblk, B, 0, st>>>(s->dkey.as<K128>(), s->dcnt.as<unsigned int>(),
                                                       s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
@@ -3827,6 +3860,66 @@ int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int 
     s->stats_ok = true;
     return EC_OK;
 }
+
+// the merge of records received from nsrc ranks (ec_export_by_owner_ex: compact or full per
+// source) -- decoded to exchange records with global events, then ec_merge_owned
+int ec_merge_owned_from(ec_session *s, const void *d_records, int nsrc, const uint64_t *src_bytes,
+                        const int64_t *src_read_base, const int32_t *src_lf_bits, int k, int limit, unsigned flags) {
+    if (!s || nsrc < 1 || nsrc > MAX_OWNERS || !src_bytes || !src_read_base || !src_lf_bits || k < 1 || k > EC_MAX_K) {
+        set_error("ec_merge_owned_from: bad arguments");
+        return EC_ERR_ARG;
+    }
+    const size_t full = k > 32 ? sizeof(AggW) : sizeof(Agg), comp = k > 32 ? sizeof(CRecW) : sizeof(CRec);
+    std::vector<unsigned long long> hoff(2 * (size_t)nsrc + 2);
+    std::vector<long long> hb(nsrc);
+    std::vector<int> hl(nsrc);
+    unsigned long long bsum = 0, rsum = 0;
+    for (int q = 0; q < nsrc; q++) {
+        const size_t rb = src_lf_bits[q] >= 0 ? comp : full;
+        if (src_bytes[q] % rb || src_lf_bits[q] > 31) {
+            set_error("ec_merge_owned_from: source %d sends %llu bytes of %zu-B records", q,
+                      (unsigned long long)src_bytes[q], rb);
+            return EC_ERR_ARG;
+        }
+        hoff[q] = bsum;
+        hoff[nsrc + 1 + q] = rsum;
+        bsum += src_bytes[q];
+        rsum += src_bytes[q] / rb;
+        hb[q] = src_read_base[q];
+        hl[q] = src_lf_bits[q];
+    }
+    hoff[nsrc] = bsum;
+    hoff[2 * (size_t)nsrc + 1] = rsum;
+    if (bsum && !d_records) {
+        set_error("null records");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    EC_CHECK(s->xrec.ensure(std::max<uint64_t>(rsum, 1) * full + hoff.size() * 8 + (size_t)nsrc * 12 + 64));
+    uint8_t *meta = s->xrec.as<uint8_t>() + std::max<uint64_t>(rsum, 1) * full;
+    unsigned long long *doff = reinterpret_cast<unsigned long long *>(meta);
+    long long *dbase = reinterpret_cast<long long *>(doff + hoff.size());
+    int *dlfb = reinterpret_cast<int *>(dbase + nsrc);
+    EC_HIP(hipMemcpyAsync(doff, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, st));
+    EC_HIP(hipMemcpyAsync(dbase, hb.data(), (size_t)nsrc * 8, hipMemcpyHostToDevice, st));
+    EC_HIP(hipMemcpyAsync(dlfb, hl.data(), (size_t)nsrc * 4, hipMemcpyHostToDevice, st));
+    if (rsum) {
+        if (k > 32)
+            k_uncompact<K128><<<grid_for(rsum, 256), 256, 0, st>>>(static_cast<const uint8_t *>(d_records), doff,
+                                                                  doff + nsrc + 1, dbase, dlfb, nsrc, rsum,
+                                                                  s->xrec.as<AggW>());
+        else
+            k_uncompact<unsigned long long><<<grid_for(rsum, 256), 256, 0, st>>>(
+                static_cast<const uint8_t *>(d_records), doff, doff + nsrc + 1, dbase, dlfb, nsrc, rsum, s->xrec.as<Agg>());
+    }
+    // (the host arrays above live until the copies ran: ec_merge_owned reads back on this stream)
+    const int rc = ec_merge_owned(s, s->xrec.p, rsum, k, limit, flags);
+    EC_HIP(hipStreamSynchronize(st));
+    return rc;
+}
+
+int ec_compact_record_bytes(int k) { return k > 32 ? (int)sizeof(CRecW) : (int)sizeof(CRec); }
 
 int ec_export_dense(ec_session *s, void *d_out) {
     if (!s) return EC_ERR_ARG;

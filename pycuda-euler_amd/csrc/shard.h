@@ -126,18 +126,131 @@ constexpr unsigned int OWN_CHUNK = 8192;
 template <typename K>
 __global__ void __launch_bounds__(256) k_owner_hist(const K *dkey, unsigned int n, unsigned int nowners,
                                                     unsigned int nblk, unsigned int *bh, OwnerFn own,
-                                                    unsigned int *oid) {
+                                                    unsigned int *oid, const unsigned long long *dfc = nullptr,
+                                                    const unsigned long long *dft = nullptr,
+                                                    unsigned int *evmax = nullptr) {
     __shared__ unsigned int h[MAX_OWNERS];
+    __shared__ unsigned int s_mx[2];
     for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) h[i] = 0;
+    if (threadIdx.x < 2) s_mx[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t c0 = (uint64_t)blockIdx.x * OWN_CHUNK, c1 = min<uint64_t>(c0 + OWN_CHUNK, n);
+    unsigned int mr = 0, ml = 0;  // largest shard-relative read id / window position of the events
     for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
         const unsigned int o = own(dkey[t], nowners);  // kept for the scatter (a minimizer is ~250 VALU)
         oid[t] = o;
         atomicAdd(&h[o], 1u);
+        if (evmax) {
+            const unsigned long long a = dfc[t], b = dft[t];
+            if (a != NONE64) mr = max(mr, (unsigned int)(a >> 32)), ml = max(ml, (unsigned int)a);
+            if (b != NONE64) mr = max(mr, (unsigned int)(b >> 32)), ml = max(ml, (unsigned int)b);
+        }
+    }
+    if (evmax) {
+        for (int o = 32; o > 0; o >>= 1) mr = max(mr, (unsigned int)__shfl_xor(mr, o)), ml = max(ml, (unsigned int)__shfl_xor(ml, o));
+        if ((threadIdx.x & 63) == 0) atomicMax(&s_mx[0], mr), atomicMax(&s_mx[1], ml);
     }
     __syncthreads();
     for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) bh[(uint64_t)i * nblk + blockIdx.x] = h[i];
+    if (evmax && threadIdx.x == 0) atomicMax(&evmax[0], s_mx[0]), atomicMax(&evmax[1], s_mx[1]);
+}
+
+// ---- compact exchange records (round 5) ---------------------------------------------------------
+// The all-to-all carries every rank's distinct k-mers (config 4: 4.6 M per rank whatever N is).
+// Events of a shard count are shard-relative, (read << 32) | window position, with reads <
+// 2^24 and positions < 2^9 at the bench's shapes, so a record carries them as 32-bit
+// (read << lf_bits) | lf (0xFFFFFFFF: no event) and the receiver adds the source's global read
+// base: 20-B records (k <= 32; 28 B for 128-bit keys) instead of 32 / 48 B.  A rank whose events
+// do not fit sends full records (lf_bits -1); the receiver decodes per source.
+struct CRec {
+    uint32_t w[5];  // key lo, key hi, count, eC, eT
+};
+struct CRecW {
+    uint32_t w[7];  // key lo.lo, lo.hi, hi.lo, hi.hi, count, eC, eT
+};
+static_assert(sizeof(CRec) == 20 && sizeof(CRecW) == 28, "compact record layout");
+template <typename K> struct CRecOf;
+template <> struct CRecOf<unsigned long long> {
+    using T = CRec;
+    static constexpr int KW = 2;
+};
+template <> struct CRecOf<K128> {
+    using T = CRecW;
+    static constexpr int KW = 4;
+};
+__device__ inline void key_words(unsigned long long k, uint32_t *w) { w[0] = (uint32_t)k, w[1] = (uint32_t)(k >> 32); }
+__device__ inline void key_words(const K128 &k, uint32_t *w) {
+    w[0] = (uint32_t)k.lo, w[1] = (uint32_t)(k.lo >> 32), w[2] = (uint32_t)k.hi, w[3] = (uint32_t)(k.hi >> 32);
+}
+__device__ inline uint32_t ev_pack(unsigned long long e, int lfb) {
+    return e == NONE64 ? 0xFFFFFFFFu : (uint32_t)(((e >> 32) << lfb) | (e & 0xFFFFFFFFull));
+}
+__device__ inline unsigned long long ev_unpack(uint32_t v, int lfb, unsigned long long read_base) {
+    if (v == 0xFFFFFFFFu) return NONE64;
+    return ((read_base + (v >> lfb)) << 32) | (v & ((1u << lfb) - 1u));
+}
+
+template <typename K>
+__global__ void __launch_bounds__(256) k_owner_scatter_c(const K *dkey, const unsigned int *dcnt,
+                                                         const unsigned long long *dfc, const unsigned long long *dft,
+                                                         unsigned int n, unsigned int nowners, unsigned int nblk,
+                                                         const unsigned int *bh_incl, typename CRecOf<K>::T *out,
+                                                         int lfb, const unsigned int *oid) {
+    constexpr int KW = CRecOf<K>::KW;
+    __shared__ unsigned int h[MAX_OWNERS];
+    __shared__ unsigned int base[MAX_OWNERS];
+    for (unsigned int i = threadIdx.x; i < nowners; i += blockDim.x) {
+        const uint64_t j = (uint64_t)i * nblk + blockIdx.x;
+        h[i] = 0;
+        base[i] = j ? bh_incl[j - 1] : 0u;
+    }
+    __syncthreads();
+    const uint64_t c0 = (uint64_t)blockIdx.x * OWN_CHUNK, c1 = min<uint64_t>(c0 + OWN_CHUNK, n);
+    for (uint64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+        const unsigned int o = oid[t];
+        const unsigned int rk = atomicAdd(&h[o], 1u);
+        typename CRecOf<K>::T r;
+        key_words(dkey[t], r.w);
+        r.w[KW] = dcnt[t];
+        r.w[KW + 1] = ev_pack(dfc[t], lfb);
+        r.w[KW + 2] = ev_pack(dft[t], lfb);
+        out[base[o] + rk] = r;
+    }
+}
+
+// received records of every source -> exchange records with global events (the merge's input);
+// source s: records [roff[s], roff[s + 1]) at byte boffs[s], compact (lfb[s] >= 0) or full
+template <typename K>
+__global__ void __launch_bounds__(256) k_uncompact(const uint8_t *in, const unsigned long long *boff,
+                                                   const unsigned long long *roff, const long long *rbase,
+                                                   const int *lfb, int nsrc, uint64_t n,
+                                                   typename RecOf<K>::T *out) {
+    using R = typename RecOf<K>::T;
+    using C = typename CRecOf<K>::T;
+    constexpr int KW = CRecOf<K>::KW;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+        int a = 0, b = nsrc;  // roff[a] <= t < roff[b]
+        while (b - a > 1) {
+            const int m = (a + b) >> 1;
+            if (t >= roff[m]) a = m;
+            else b = m;
+        }
+        const uint64_t i = t - roff[a];
+        if (lfb[a] < 0) {  // full records (word copies: a source segment is 4-B aligned only)
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(in + boff[a]) + i * (sizeof(R) / 4);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(out + t);
+#pragma unroll
+            for (int q = 0; q < (int)(sizeof(R) / 4); q++) dst[q] = src[q];
+            continue;
+        }
+        const C c = reinterpret_cast<const C *>(in + boff[a])[i];
+        K key;
+        if constexpr (KW == 2) key = (unsigned long long)c.w[0] | (unsigned long long)c.w[1] << 32;
+        else key = K128{(unsigned long long)c.w[0] | (unsigned long long)c.w[1] << 32,
+                        (unsigned long long)c.w[2] | (unsigned long long)c.w[3] << 32};
+        out[t] = RecOf<K>::make(key, c.w[KW], ev_unpack(c.w[KW + 1], lfb[a], (unsigned long long)rbase[a]),
+                                ev_unpack(c.w[KW + 2], lfb[a], (unsigned long long)rbase[a]));
+    }
 }
 
 // scatter dense records into owner-major order at the scanned chunk bases (owners from

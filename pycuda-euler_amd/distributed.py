@@ -47,6 +47,18 @@ eulerhip.register("ec_count_shard", ctypes.c_int, [_P, _P, _P, _U64, _U64, ctype
 eulerhip.register("ec_dense_count", ctypes.c_uint64, [_P])
 eulerhip.register("ec_export_by_owner", ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.POINTER(ctypes.c_uint64)])
 eulerhip.register("ec_session_set_owner_rule", ctypes.c_int, [_P, ctypes.c_int])
+# compact exchange records (round 5): 20 / 28 B, events shard-relative (the receiver adds bases)
+eulerhip.register("ec_export_by_owner_ex", ctypes.c_int, [_P, ctypes.c_int, _P, ctypes.POINTER(ctypes.c_uint64),
+                                                          ctypes.c_int, ctypes.POINTER(ctypes.c_int)])
+eulerhip.register("ec_compact_record_bytes", ctypes.c_int, [ctypes.c_int])
+eulerhip.register("ec_merge_owned_from", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
+                                                        ctypes.c_int, ctypes.c_int, ctypes.c_uint])
+
+
+def compact_bytes(k):
+    """ec_compact_record_bytes"""
+    return 20 if k <= 32 else 28
 
 # owner rules (ec_session_set_owner_rule): minimizer ranges (21 <= k <= 52), or a key hash when
 # the job's minimizer-range counts are skewed past SKEW times the mean owner (low-complexity input:
@@ -158,13 +170,38 @@ class HipEngine:
     def set_owner_rule(self, rule):
         eulerhip.check(self.L.ec_session_set_owner_rule(self._h(), int(rule)))
 
-    def export_by_owner(self, nowners):
+    def export_by_owner(self, nowners, compact=False):
+        """records grouped by owner and the records per owner; compact=True: also the records'
+        lf_bits (compact_bytes(k)-B records with shard-relative events, or -1: full records)"""
         n = int(self.L.ec_dense_count(self._h()))
         rb = self.rec_bytes()
         counts = (ctypes.c_uint64 * nowners)()
         out = self.empty(n * rb)
-        eulerhip.check(self.L.ec_export_by_owner(self._h(), int(nowners), ctypes.c_void_p(out.data_ptr()), counts))
-        return out[: n * rb], [int(c) for c in counts]
+        if not compact:
+            eulerhip.check(self.L.ec_export_by_owner(self._h(), int(nowners), ctypes.c_void_p(out.data_ptr()), counts))
+            return out[: n * rb], [int(c) for c in counts]
+        lfb = ctypes.c_int(-1)
+        eulerhip.check(self.L.ec_export_by_owner_ex(self._h(), int(nowners), ctypes.c_void_p(out.data_ptr()), counts, 1,
+                                                    ctypes.byref(lfb)))
+        rb = compact_bytes(self.k) if lfb.value >= 0 else rb
+        return out[: n * rb], [int(c) for c in counts], int(lfb.value)
+
+    def merge_owned_from(self, recs, src_bytes, src_base, src_lfb, k, limit, flags=0, export=True):
+        """ec_merge_owned_from on the records of every source (rank order); export as merge_owned"""
+        self.k = int(k)
+        ns = len(src_bytes)
+        eulerhip.check(self.L.ec_merge_owned_from(self._h(), ctypes.c_void_p(recs.data_ptr()), ns,
+                                                  (ctypes.c_uint64 * ns)(*[int(x) for x in src_bytes]),
+                                                  (ctypes.c_int64 * ns)(*[int(x) for x in src_base]),
+                                                  (ctypes.c_int32 * ns)(*[int(x) for x in src_lfb]), int(k), int(limit),
+                                                  flags))
+        m = int(self.L.ec_dense_count(self._h()))
+        if not export:
+            return m
+        rb = self.rec_bytes()
+        out = self.empty(m * rb)
+        eulerhip.check(self.L.ec_export_dense(self._h(), ctypes.c_void_p(out.data_ptr())))
+        return out[: m * rb]
 
     def merge_owned(self, recs, k, limit, flags=0, export=True):
         """ec_merge_owned_export: merge + solid filter + export in one call into a buffer
@@ -301,18 +338,27 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
 
-    def alltoallv(self, send, counts_bytes, tag=0):
+    def alltoallv(self, send, counts_bytes, tag=0, meta=None):
         """send: uint8 tensor laid out destination-major with counts_bytes[d] bytes for rank d.
         Returns (received bytes, sum over ranks of `tag`): the per-rank integer rides along with
-        the byte-count exchange, so no separate all-reduce (and host sync) is needed for it."""
+        the byte-count exchange, so no separate all-reduce (and host sync) is needed for it.
+        meta (a list of ints): rides along too; then also returns every source's byte count
+        and meta list (rank order)."""
         torch, dist = self.torch, self.dist
         dev = send.device
-        sc = torch.tensor([[int(c), int(tag)] for c in counts_bytes], dtype=torch.int64, device=dev)
+        m = [int(x) for x in (meta or [])]
+        sc = torch.tensor([[int(c), int(tag)] + m for c in counts_bytes], dtype=torch.int64, device=dev)
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=self.group)
         rcv = rc.tolist()
         rcl = [int(x[0]) for x in rcv]
         total_tag = sum(int(x[1]) for x in rcv)
+        if meta is not None:
+            recv = torch.empty(max(sum(rcl), 1), dtype=torch.uint8, device=dev)
+            if sum(rcl) or sum(counts_bytes):
+                dist.all_to_all_single(recv[: sum(rcl)], send[: sum(counts_bytes)], output_split_sizes=rcl,
+                                       input_split_sizes=list(counts_bytes), group=self.group)
+            return recv[: sum(rcl)], total_tag, rcl, [[int(v) for v in x[2:]] for x in rcv]
         recv = torch.empty(max(sum(rcl), 1), dtype=torch.uint8, device=dev)
         if sum(rcl) or sum(counts_bytes):
             dist.all_to_all_single(recv[: sum(rcl)], send[: sum(counts_bytes)], output_split_sizes=rcl,
@@ -481,14 +527,19 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
         if rule != OWNER_MINIMIZER:
             engine.set_owner_rule(rule)
     finish = finish_mode(finish, k, rule)
-    recs, counts = engine.export_by_owner(comm.world)
+    # compact records where the events fit (the receivers add this shard's read base)
+    recs, counts, lfb = engine.export_by_owner(comm.world, compact=True)
+    rb = compact_bytes(k) if lfb >= 0 else rec_bytes(k)
     tick("export")
-    # the job's k-mer positions ride along with the exchange's byte counts
-    received, P = comm.alltoallv(recs, [c * rec_bytes(k) for c in counts], tag=st.n_positions)
+    # the job's k-mer positions, this shard's read base and record format ride along with the
+    # exchange's byte counts
+    received, P, src_bytes, metas = comm.alltoallv(recs, [c * rb for c in counts], tag=st.n_positions,
+                                                   meta=[read_base, lfb])
+    src_base, src_lfb = [m[0] for m in metas], [m[1] for m in metas]
     tick("alltoall")
     junction = partitioned and finish == "partitioned" and hasattr(engine, "graph_place")
     if junction:  # each rank keeps its own segment: the links come out of the junction join
-        ur = engine.merge_owned(received, k, limit, flags, export=False)
+        ur = engine.merge_owned_from(received, src_bytes, src_base, src_lfb, k, limit, flags, export=False)
         tick("merge")
         lo, hi, _, npal = junction_links(engine, comm, k, ur, tick=tick)
         res = partitioned_finish(engine, comm, k, lo, hi, None, fetch=fetch, tick=tick, npal=npal)
@@ -496,7 +547,7 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
             for (_, a), (name, b) in zip(marks, marks[1:]):
                 phase_ms[name] = phase_ms.get(name, 0.0) + (b - a) * 1e3
         return res, P
-    solid = engine.merge_owned(received, k, limit, flags)
+    solid = engine.merge_owned_from(received, src_bytes, src_base, src_lfb, k, limit, flags)
     tick("merge")
     if not partitioned:
         everything = comm.allgatherv(solid, fill=0xFF)  # filler records: all-ones keys, skipped
@@ -579,7 +630,7 @@ class ShardedAssembler:
         return self.count_stats
 
 
-def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None, finish="auto"):
+def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None, finish="auto", compact=True):
     """Simulate the distributed algorithm with len(engines) ranks on the local device(s):
     same engine calls, the collectives done by concatenation.  Returns rank 0's result."""
     world = len(engines)
@@ -589,12 +640,13 @@ def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=N
         lo, hi = shard_range(nreads, r, world)
         b0, b1 = int(off[lo]), int(off[hi])
         parts.append((buf[b0:b1], off[lo:hi + 1] - off[lo], lo))
-    return local_sharded_assemble_shards(engines, parts, k, limit, flags, partitioned, finish)
+    return local_sharded_assemble_shards(engines, parts, k, limit, flags, partitioned, finish, compact)
 
 
-def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partitioned=None, finish="auto"):
+def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partitioned=None, finish="auto", compact=True):
     """local_sharded_assemble on given shards: parts[r] = (buf, off, read_base) of rank r (host
-    arrays; global read ids read_base.., increasing with r, gaps allowed)."""
+    arrays; global read ids read_base.., increasing with r, gaps allowed).  compact: the
+    exchange's record format per rank (a bool for all; compact records where events fit)."""
     import torch
 
     world = len(engines)
@@ -614,26 +666,30 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
         for eng in engines:
             eng.set_owner_rule(OWNER_MINIMIZER)
         rule = owner_rule_for([sum(c) for c in zip(*[eng.owner_counts(world) for eng in engines])], k)
-    for eng in engines:
+    comp = compact if isinstance(compact, (list, tuple)) else [compact] * world
+    for eng, c in zip(engines, comp):
         eng.set_owner_rule(rule)
-        sends.append(eng.export_by_owner(world))
+        sends.append(eng.export_by_owner(world, compact=True) if c else eng.export_by_owner(world) + (-1,))
     local_sharded_assemble_shards.last_rule = rule
     finish = finish_mode(finish, k, rule)
-    local_sharded_assemble_shards.last_counts = [c for _, c in sends]
-    rb = rec_bytes(k)
+    local_sharded_assemble_shards.last_counts = [c for _, c, _ in sends]
+    local_sharded_assemble_shards.last_lf_bits = [b for _, _, b in sends]
+    rbs = [compact_bytes(k) if b >= 0 else rec_bytes(k) for _, _, b in sends]
+    bases = [int(base) for _, _, base in parts]
 
-    def received(dst, eng):
-        parts = []
+    def merge(dst, eng, export):
+        got = []
         for src in range(world):
-            recs, counts = sends[src]
-            o = sum(counts[:dst]) * rb
-            parts.append(recs[o:o + counts[dst] * rb].to(eng.device))
-        return torch.cat(parts)
+            recs, counts, _ = sends[src]
+            o = sum(counts[:dst]) * rbs[src]
+            got.append(recs[o:o + counts[dst] * rbs[src]].to(eng.device))
+        return eng.merge_owned_from(torch.cat(got), [g.numel() for g in got], bases,
+                                    [b for _, _, b in sends], k, limit, flags, export=export)
 
     if partitioned is None:
         partitioned = not (flags & eulerhip.EC_FLAG_GENERAL)
     if partitioned and finish == "partitioned":  # the junction-partitioned graph (junction_links)
-        urs = [eng.merge_owned(received(dst, eng), k, limit, flags, export=False) for dst, eng in enumerate(engines)]
+        urs = [merge(dst, eng, False) for dst, eng in enumerate(engines)]
         seg_lo = [sum(urs[:r]) for r in range(world + 1)]
         U = seg_lo[-1]
         placed = [eng.graph_place(seg_lo[r], U, world) for r, eng in enumerate(engines)]
@@ -648,7 +704,8 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
             eng.graph_links_apply(torch.cat(got))
         segs = [(seg_lo[r], seg_lo[r + 1], None) for r in range(world)]
         return local_partitioned_finish(engines, segs, k, npal), P
-    solids = [eng.merge_owned(received(dst, eng), k, limit, flags) for dst, eng in enumerate(engines)]
+    solids = [merge(dst, eng, True) for dst, eng in enumerate(engines)]
+    rb = rec_bytes(k)
     mx = max(max(x.numel() for x in solids), 1)  # padded like TorchComm.allgatherv (0xFF filler records)
     allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device=engines[0].device)
     for i, x in enumerate(solids):

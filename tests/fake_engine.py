@@ -135,12 +135,19 @@ class FakeEngine:
         own = [owner_fn(int(x), nowners, self.k, self.rule) for x in self.recs["key"]]
         return [own.count(o) for o in range(nowners)]
 
-    def export_by_owner(self, nowners):
+    def export_by_owner(self, nowners, compact=False):
+        """(compact: the device's compact records carry shard-relative events; this engine always
+        sends full records, lf_bits -1, with global events -- the exchange's mixed-format case)"""
         own = np.array([owner_fn(int(x), nowners, self.k, self.rule) for x in self.recs["key"]], dtype=np.int64)
         order = np.argsort(own, kind="stable")
         counts = [int((own == o).sum()) for o in range(nowners)]
         self.last_counts = counts
-        return self._bytes(self.recs[order]), counts
+        out = self._bytes(self.recs[order])
+        return (out, counts, -1) if compact else (out, counts)
+
+    def merge_owned_from(self, recs, src_bytes, src_base, src_lfb, k, limit, flags=0, export=True):
+        assert all(b == -1 for b in src_lfb) and sum(src_bytes) == recs.numel()
+        return self.merge_owned(recs, k, limit, flags, export)
 
     def merge_owned(self, recs, k, limit, flags=0, export=True):
         agg = {}

@@ -332,3 +332,28 @@ def test_partitioned_finish_equals_replicated(world, seed, g, n, L, err, k, circ
     finally:
         for e in es:
             e.sess.close()
+
+
+@pytest.mark.parametrize("compact", [True, False, [True, False, True]])
+@pytest.mark.parametrize("k", [31, 51])
+def test_exchange_record_formats(engines, compact, k):
+    """the all-to-all's records: compact (shard-relative events in 32 bits, 20 / 28 B), full
+    (global events, 32 / 48 B) and both at once (ec_merge_owned_from decodes per source), at
+    read bases 0 / 40 M / 80 M, equal to the oracle on the concatenated reads"""
+    import distributed
+
+    world = 3
+    sets = [make_reads(60_000, 20_000, 150 if k > 32 else 100, 8100 + k, part=r, err=0.002) for r in range(world)]
+    buf = np.concatenate([b for b, _ in sets])
+    L = 150 if k > 32 else 100
+    off = np.arange(world * 20_000 + 1, dtype=np.uint64) * np.uint64(L)
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    for finish in ("partitioned", "replicated"):
+        res, P = distributed.local_sharded_assemble_shards(
+            engines[:world], [(b, o, r * 40_000_000) for r, (b, o) in enumerate(sets)], k, 1, finish=finish,
+            compact=compact)
+        want = [compact] * world if isinstance(compact, bool) else compact
+        assert [b >= 0 for b in distributed.local_sharded_assemble_shards.last_lf_bits] == want
+        assert P == ref["n_positions"]
+        assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref), finish
+        assert res.stats.n_dict == ref["n_dict"]

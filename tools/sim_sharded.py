@@ -62,25 +62,28 @@ def main():
             eng.count_shard(d_reads, d_off, n, lo, a.k, 0)
             tick("count", t0)
             t0 = time.perf_counter()
-            sends.append(eng.export_by_owner(world))
+            sends.append(eng.export_by_owner(world, compact=True))
             tick("export", t0)
         rb = distributed.rec_bytes(a.k)
+        rbs = [distributed.compact_bytes(a.k) if b >= 0 else rb for _, _, b in sends]
         recvs = []
         for dst, eng in enumerate(engines):
             parts = []
             for src in range(world):
-                recs, counts = sends[src]
-                o = sum(counts[:dst]) * rb
-                parts.append(recs[o:o + counts[dst] * rb])
-            recvs.append(torch.cat(parts))
+                recs, counts, _ = sends[src]
+                o = sum(counts[:dst]) * rbs[src]
+                parts.append(recs[o:o + counts[dst] * rbs[src]])
+            recvs.append((torch.cat(parts), [x.numel() for x in parts]))
+        bases = [sh[3] for sh in shards]
+        lfbs = [b for _, _, b in sends]
         import ctypes
         import eulerhip
         extra = ""
         if a.finish == "replicated":  # the round-4 layout: gathered solid set, loaded on every rank
             solids = []
-            for eng, recv in zip(engines, recvs):
+            for eng, (recv, sb) in zip(engines, recvs):
                 t0 = time.perf_counter()
-                solids.append(eng.merge_owned(recv, a.k, 1, 0))
+                solids.append(eng.merge_owned_from(recv, sb, bases, lfbs, a.k, 1, 0))
                 tick("merge", t0)
             mx = max(x.numel() for x in solids)
             allsolid = torch.full((world * mx,), 0xFF, dtype=torch.uint8, device="cuda")
@@ -111,9 +114,9 @@ def main():
             xb = allsolid.numel()
         else:  # the junction-partitioned graph and the partitioned finish, every rank's calls timed
             urs = []
-            for eng, recv in zip(engines, recvs):
+            for eng, (recv, sb) in zip(engines, recvs):
                 t0 = time.perf_counter()
-                urs.append(eng.merge_owned(recv, a.k, 1, 0, export=False))
+                urs.append(eng.merge_owned_from(recv, sb, bases, lfbs, a.k, 1, 0, export=False))
                 tick("merge", t0)
             seg_lo = [sum(urs[:r]) for r in range(world + 1)]
             U = seg_lo[-1]
@@ -181,7 +184,7 @@ def main():
         mx_ph = {k: round(max(v), 2) for k, v in t.items()}
         print("rep %d  ranks %d  per-rank max ms: %s  sum %.2f  exchanged bytes/rank ~%.0f MB, gathered %.0f MB%s" % (
             rep, world, mx_ph, sum(mx_ph.values()),
-            sum(c for c in sends[0][1]) * rb / 1e6, xb / 1e6, extra))
+            sum(c for c in sends[0][1]) * rbs[0] / 1e6, xb / 1e6, extra))
     print("contigs", len(res.contig_offsets) - 1, "chars", len(res.contig_bytes))
 
 
