@@ -208,7 +208,8 @@ struct ec_session {
     bool placed = false;
     uint64_t seg_lo = 0, seg_Ur = 0;
     DevBuf jrec, joid, jout, jseg, jcnt;
-    DevBuf xrec;  // ec_merge_owned_from: the received records decoded
+    DevBuf xrec;     // ec_merge_owned_from: the received records decoded
+    HostBuf hmeta;   // ... and its per-source table, staged page-locked
     int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 52), 1 key hash
     // ec_export_by_owner's owner ids / scanned chunk histogram of the last call, reused by a
     // following call with the same records, owners and rule (counts first, then the scatter)
@@ -1460,9 +1461,9 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
         const uint64_t cells = (uint64_t)nbins * nch;
         EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 2 * cells) * 4));
         unsigned int *hist = s->mbid2.as<unsigned int>(), *incl = hist + cells;
-        k_cs_hist<<<nch, 256, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist);
+        k_cs_hist<<<nch, 1024, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist);
         EC_CHECK(scan_incl_u32(s, hist, incl, cells));
-        k_cs_scatter<<<nch, 256, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist, incl,
+        k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist, incl,
                                                   s->midx2.as<unsigned int>());
         k_cs_bounds<<<grid_for(nbins, B), B, 0, st>>>(hist, incl, nbins, nch, s->bstart.as<unsigned long long>());
     }
@@ -2273,12 +2274,17 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
 // (~0.25 ms from the walk to finalize on the headline).  Chains no ruler reached (a cycle of
 // chains without a sampled one) are caught by the caller's next scalar read (nvisited < M),
 // which redoes the ranking with rank_supers.  Needs k_tile_compact's initialisation (pre_init).
-int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *dM, int &rounds) {
+int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *dM, int &rounds,
+                      unsigned int mcap = 0) {
+    // mcap: a bound of the chain count known on the host (the partitioned finish's gathered
+    // list) -- grids and Wyllie rounds sized by it instead of the node count N, which stays the
+    // cycle bound of the jumps (j.s < N)
+    const unsigned int G = mcap ? mcap : N;
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     SuperRec *srec = s->rt_srec.as<SuperRec>();
-    const size_t cap = std::max<size_t>(N, 1);
+    const size_t cap = std::max<size_t>(G, 1);
     EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec)));
     EC_CHECK(s->rt_pks.ensure(cap * 4));
     EC_CHECK(s->rt_rks.ensure(cap * 4));
@@ -2287,10 +2293,10 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     EC_CHECK(s->rbc.ensure(((cap + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
     SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
     const unsigned int *dnr = &dsc->nr;
-    const unsigned int gs = std::min(grid_for(N, B), 4096u);  // grid-stride grids over <= N items
+    const unsigned int gs = std::min(grid_for(G, B), 4096u);  // grid-stride grids over <= G items
     k_super_link<<<gs, B, 0, st>>>(srec, 0, s->rt_sidx.as<unsigned int>(), snrec, s->rt_hasp.as<uint8_t>(), dM);
     const unsigned int smask = kn().sruler_mask > 0 ? (unsigned int)kn().sruler_mask : 15u;
-    const unsigned int nblk = (N + RULER_CHUNK - 1) / RULER_CHUNK;
+    const unsigned int nblk = (G + RULER_CHUNK - 1) / RULER_CHUNK;
     k_srulers_count<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), 0, smask, 1, s->rid.as<uint2>(),
                                         s->rbc.as<unsigned int>(), dM);
     EC_CHECK(scan_incl_u32(s, s->rbc.as<unsigned int>(), s->rbc.as<unsigned int>() + nblk, nblk));
@@ -2300,10 +2306,10 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), 0, &dsc->nr, smask, s->rid.as<uint2>(),
                                  s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
     // rulers <= chains <= N: rounds for N (a round after convergence returns at its first load)
-    const unsigned int gr = std::min(grid_for(N / (kn().rj_div > 0 ? (unsigned)kn().rj_div : 8u) + 1, B), 2048u);
+    const unsigned int gr = std::min(grid_for(G / (kn().rj_div > 0 ? (unsigned)kn().rj_div : 8u) + 1, B), 2048u);
     k_rjump_init<<<gr, B, 0, st>>>(s->nextR.as<unsigned int>(), 0, s->st0.as<RJump>(), dnr);
     rounds = 1;
-    while ((1ull << (rounds - 1)) < (unsigned long long)N) rounds++;
+    while ((1ull << (rounds - 1)) < (unsigned long long)G) rounds++;
     rounds = std::min(rounds + 1, 63);
     RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
     for (int r = 0; r < rounds; r++)
@@ -2930,14 +2936,12 @@ int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
         EC_CHECK(s->st0.ensure(Nn * sizeof(RJump)));
         EC_CHECK(s->st1.ensure(Nn * sizeof(RJump)));
         EC_CHECK(s->rt_tbase.ensure(8));
-        unsigned int *dM32 = s->rt_tbase.as<unsigned int>();
-        EC_HIP(hipMemsetD32Async(dM32, (int)(unsigned int)M, 1, st));
-        EC_HIP(hipMemsetD32Async(dM32 + 1, 0, 1, st));
-        EC_HIP(hipMemsetAsync(s->rt_hasp.p, 0, M, st));
-        EC_HIP(hipMemsetAsync(s->rid.p, 0xFF, (size_t)M * 8, st));
-        EC_HIP(hipMemsetAsync(&dsc->nr, 0, 4, st));
-        EC_HIP(hipMemsetAsync(&dsc->nvisited, 0, 8, st));
-        EC_CHECK(rank_supers_async(s, N, s->rt_tbase.as<unsigned long long>(), rounds));
+        // the chain count on the device, the ruler state initialised: one launch (six memsets
+        // cost ~40 us of launch gaps)
+        k_part_rank_init<<<std::min(grid_for(M, 256), 2048u), 256, 0, st>>>(
+            s->rt_tbase.as<unsigned long long>(), (unsigned int)M, s->rt_hasp.as<uint8_t>(), s->rid.as<uint2>(), &dsc->nr,
+            &dsc->nvisited);
+        EC_CHECK(rank_supers_async(s, N, s->rt_tbase.as<unsigned long long>(), rounds, (unsigned int)M));
         Scalars hsc{};
         EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
         EC_CHECK(host_sync(s, st));
@@ -3474,6 +3478,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec};
     for (auto *b : all) b->release();
     s->h_chars.release();
+    s->hmeta.release();
     s->bounce.release();
     s->pend.clear();
     s->h_coff.release();
@@ -3896,14 +3901,19 @@ int ec_merge_owned_from(ec_session *s, const void *d_records, int nsrc, const ui
     }
     EC_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
-    EC_CHECK(s->xrec.ensure(std::max<uint64_t>(rsum, 1) * full + hoff.size() * 8 + (size_t)nsrc * 12 + 64));
+    const size_t mbytes = hoff.size() * 8 + (size_t)nsrc * 12;
+    EC_CHECK(s->xrec.ensure(std::max<uint64_t>(rsum, 1) * full + mbytes + 64));
     uint8_t *meta = s->xrec.as<uint8_t>() + std::max<uint64_t>(rsum, 1) * full;
     unsigned long long *doff = reinterpret_cast<unsigned long long *>(meta);
     long long *dbase = reinterpret_cast<long long *>(doff + hoff.size());
     int *dlfb = reinterpret_cast<int *>(dbase + nsrc);
-    EC_HIP(hipMemcpyAsync(doff, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice, st));
-    EC_HIP(hipMemcpyAsync(dbase, hb.data(), (size_t)nsrc * 8, hipMemcpyHostToDevice, st));
-    EC_HIP(hipMemcpyAsync(dlfb, hl.data(), (size_t)nsrc * 4, hipMemcpyHostToDevice, st));
+    // one H2D copy from page-locked staging (three pageable copies cost ~0.1 ms a call)
+    EC_HIP(hipStreamSynchronize(st));  // (the staging of an earlier call has been read)
+    EC_CHECK(s->hmeta.resize(mbytes));
+    memcpy(s->hmeta.data(), hoff.data(), hoff.size() * 8);
+    memcpy(s->hmeta.data() + hoff.size() * 8, hb.data(), (size_t)nsrc * 8);
+    memcpy(s->hmeta.data() + hoff.size() * 8 + (size_t)nsrc * 8, hl.data(), (size_t)nsrc * 4);
+    EC_HIP(hipMemcpyAsync(doff, s->hmeta.data(), mbytes, hipMemcpyHostToDevice, st));
     if (rsum) {
         if (k > 32)
             k_uncompact<K128><<<grid_for(rsum, 256), 256, 0, st>>>(static_cast<const uint8_t *>(d_records), doff,
@@ -3913,10 +3923,7 @@ int ec_merge_owned_from(ec_session *s, const void *d_records, int nsrc, const ui
             k_uncompact<unsigned long long><<<grid_for(rsum, 256), 256, 0, st>>>(
                 static_cast<const uint8_t *>(d_records), doff, doff + nsrc + 1, dbase, dlfb, nsrc, rsum, s->xrec.as<Agg>());
     }
-    // (the host arrays above live until the copies ran: ec_merge_owned reads back on this stream)
-    const int rc = ec_merge_owned(s, s->xrec.p, rsum, k, limit, flags);
-    EC_HIP(hipStreamSynchronize(st));
-    return rc;
+    return ec_merge_owned(s, s->xrec.p, rsum, k, limit, flags);
 }
 
 int ec_compact_record_bytes(int k) { return k > 32 ? (int)sizeof(CRecW) : (int)sizeof(CRec); }
@@ -4120,9 +4127,9 @@ int bin_sort(ec_session *s, const unsigned int *bid, uint64_t n, unsigned int nb
         EC_HIP(hipMemsetAsync(bstart, 0, (nbins + 1ull) * 8, st));
         return EC_OK;
     }
-    k_cs_hist<<<nch, 256, nbins * 4, st>>>(bid, n, nbins, nch, hist);
+    k_cs_hist<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist);
     EC_CHECK(scan_incl_u32(s, hist, incl, cells));
-    k_cs_scatter<<<nch, 256, nbins * 4, st>>>(bid, n, nbins, nch, hist, incl, s->midx2.as<unsigned int>());
+    k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist, incl, s->midx2.as<unsigned int>());
     k_cs_bounds<<<grid_for(nbins, 256), 256, 0, st>>>(hist, incl, nbins, nch, bstart);
     EC_HIP(hipMemcpyAsync(bstart + nbins, &incl[cells - 1], 4, hipMemcpyDeviceToDevice, st));  // (low word)
     EC_HIP(hipMemsetAsync(reinterpret_cast<unsigned int *>(bstart + nbins) + 1, 0, 4, st));
@@ -4149,7 +4156,8 @@ int graph_place(ec_session *s, uint64_t lo, uint64_t U, int nowners, void *d_out
         EC_HIP(hipMemcpyAsync(tfc, s->dfc.p, Ur * 8, hipMemcpyDeviceToDevice, st));
         EC_HIP(hipMemcpyAsync(tft, s->dft.p, Ur * 8, hipMemcpyDeviceToDevice, st));
     }
-    EC_HIP(hipStreamSynchronize(st));  // (ensure() may free the sources below)
+    if (s->dkey.cap < Uu * sizeof(K) || s->dcnt.cap < Uu * 4 || s->dfc.cap < Uu * 8 || s->dft.cap < Uu * 8)
+        EC_HIP(hipStreamSynchronize(st));  // (the ensure()s below free the copies' sources)
     EC_CHECK(s->dkey.ensure(Uu * sizeof(K)));
     EC_CHECK(s->dcnt.ensure(Uu * 4));
     EC_CHECK(s->dfc.ensure(Uu * 8));
@@ -4242,8 +4250,20 @@ int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const ui
                                                                   s->succ.as<unsigned int>(), outbox, nout,
                                                                   (unsigned int)n, flag);
         }
+        // outbox -> destination-major link records, sized by n on the host (the count stays on
+        // the device: one read-back for the flags and the destinations' counts)
+        if (n) {
+            k_link_dest<<<grid_for(n, B), B, 0, st>>>(outbox, nout, (unsigned int)n, dseg, (unsigned int)nowners,
+                                                      s->joid.as<unsigned int>());
+            EC_CHECK(bin_sort(s, s->joid.as<unsigned int>(), n, (unsigned int)nowners + 1, bstart));
+            k_gather_recs<LinkRec><<<grid_for(n, B), B, 0, st>>>(outbox, s->midx2.as<unsigned int>(), n, d_links);
+        } else {
+            EC_HIP(hipMemsetAsync(bstart, 0, ((size_t)nowners + 2) * 8, st));
+        }
         unsigned int hf[2] = {0, 0};
+        std::vector<unsigned long long> hs((size_t)nowners + 2);
         EC_CHECK(d2h(s, hf, flag, 8, st));
+        EC_CHECK(d2h(s, hs.data(), bstart, ((size_t)nowners + 2) * 8, st));
         EC_CHECK(host_sync(s, st));
         if (hf[0] & 2u) {
             set_error("junction join: link outbox overflow");
@@ -4258,21 +4278,7 @@ int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const ui
             s->stats.table_retries++;
             continue;
         }
-        // outbox -> destination-major link records
-        const unsigned int no = hf[1];
-        if (no) {
-            EC_CHECK(s->joid.ensure((uint64_t)no * 4));
-            k_link_dest<<<grid_for(no, B), B, 0, st>>>(outbox, nout, no, dseg, (unsigned int)nowners,
-                                                       s->joid.as<unsigned int>());
-            EC_CHECK(bin_sort(s, s->joid.as<unsigned int>(), no, (unsigned int)nowners, bstart));
-            k_gather_recs<LinkRec><<<grid_for(no, B), B, 0, st>>>(outbox, s->midx2.as<unsigned int>(), no, d_links);
-            std::vector<unsigned long long> hs((size_t)nowners + 1);
-            EC_CHECK(d2h(s, hs.data(), bstart, ((size_t)nowners + 1) * 8, st));
-            EC_CHECK(host_sync(s, st));
-            for (int r = 0; r < nowners; r++) owner_counts[r] = hs[r + 1] - hs[r];
-        } else {
-            for (int r = 0; r < nowners; r++) owner_counts[r] = 0;
-        }
+        for (int r = 0; r < nowners; r++) owner_counts[r] = hs[r + 1] - hs[r];
         return EC_OK;
     }
 }

@@ -213,34 +213,42 @@ __global__ void __launch_bounds__(NT) k_junction_join(const R *recs, const unsig
         if (threadIdx.x == 0) atomicAdd(overflow, 1u);
         return;
     }
-    for (int i0 = 0; i0 < SLOTS; i0 += NT) {  // (whole waves: the outbox append is wave-aggregated)
-        const int i = i0 + threadIdx.x;
-        unsigned int t0 = NONE32, v0 = 0, t1 = NONE32, v1 = 0;
-        if (i < SLOTS) {
-            const unsigned long long ex = ids[0][i], ey = ids[1][i];
-            if (ex != EMPTY && ey != EMPTY && !((ex | ey) & MANY)) {
-                const unsigned int x = (unsigned int)ex, y = (unsigned int)ey;
-                const unsigned int tx = (ex >> 32) ? x : (x ^ 1u), ty = (ey >> 32) ? y : (y ^ 1u);
-                if (y != tx) {
-                    t0 = x, v0 = y;
-                    t1 = ty, v1 = tx;
-                }
-            }
-        }
-        const bool l0 = t0 != NONE32 && t0 >= n0 && t0 < n1, l1 = t1 != NONE32 && t1 >= n0 && t1 < n1;
-        if (l0) succ[t0] = v0;
-        if (l1) succ[t1] = v1;
-        const bool o0 = t0 != NONE32 && !l0, o1 = t1 != NONE32 && !l1;
-        const unsigned int p0 = wave_append(nout, o0);
-        if (o0) {
-            if (p0 < outcap) outbox[p0] = LinkRec{t0, v0};
-            else atomicOr(overflow, 2u);
-        }
-        const unsigned int p1 = wave_append(nout, o1);
-        if (o1) {
-            if (p1 < outcap) outbox[p1] = LinkRec{t1, v1};
-            else atomicOr(overflow, 2u);
-        }
+    // links: local ones written at once; the other ranks' into the outbox at one global
+    // reservation per workgroup (a counter hit by every wave serialises at the memory side: ~60 K
+    // appends a rank took 0.46 ms)
+    constexpr int PER = (SLOTS + NT - 1) / NT;
+    unsigned int rt[2 * PER], rv[2 * PER], nr = 0;  // (static indices: registers, no scratch)
+    bool rf[2 * PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int i = threadIdx.x + q * NT;
+        rf[2 * q] = rf[2 * q + 1] = false;
+        if (i >= SLOTS) continue;
+        const unsigned long long ex = ids[0][i], ey = ids[1][i];
+        if (ex == EMPTY || ey == EMPTY || ((ex | ey) & MANY)) continue;
+        const unsigned int x = (unsigned int)ex, y = (unsigned int)ey;
+        const unsigned int tx = (ex >> 32) ? x : (x ^ 1u), ty = (ey >> 32) ? y : (y ^ 1u);
+        if (y == tx) continue;
+        rt[2 * q] = x, rv[2 * q] = y, rf[2 * q] = !(x >= n0 && x < n1);
+        rt[2 * q + 1] = ty, rv[2 * q + 1] = tx, rf[2 * q + 1] = !(ty >= n0 && ty < n1);
+        if (!rf[2 * q]) succ[x] = y;
+        if (!rf[2 * q + 1]) succ[ty] = tx;
+        nr += rf[2 * q] + rf[2 * q + 1];
+    }
+    __shared__ unsigned int s_cnt, s_base;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const unsigned int my = nr ? atomicAdd(&s_cnt, nr) : 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(nout, s_cnt) : 0u;
+    __syncthreads();
+    unsigned int p = s_base + my;
+#pragma unroll
+    for (int j = 0; j < 2 * PER; j++) {
+        if (!rf[j]) continue;
+        if (p < outcap) outbox[p] = LinkRec{rt[j], rv[j]};
+        else atomicOr(overflow, 2u);
+        p++;
     }
 }
 

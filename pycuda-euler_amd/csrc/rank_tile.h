@@ -303,6 +303,16 @@ __global__ void __launch_bounds__(256) k_tile_compact(const SuperRec *scratch, c
     if (nchains && t == 0 && threadIdx.x == 0) *nchains = tbase[gridDim.x];  // (rides on the next scalar read)
 }
 
+// the partitioned finish's ranking state: chain count M on the device, hasp = 0, rid = NONE
+__global__ void __launch_bounds__(256) k_part_rank_init(unsigned long long *dM, unsigned int M, uint8_t *hasp, uint2 *rid,
+                                                        unsigned int *nr, unsigned long long *nvisited) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *dM = M, *nr = 0, *nvisited = 0;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < M; t += (uint64_t)gridDim.x * blockDim.x) {
+        hasp[t] = 0;
+        rid[t] = make_uint2(NONE32, NONE32);
+    }
+}
+
 // SIDX[head] = index of a chain in a gathered super list (the multi-GPU finish)
 __global__ void __launch_bounds__(256) k_super_index(const SuperRec *srec, unsigned int M, unsigned int *SIDX) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < M; t += (uint64_t)gridDim.x * blockDim.x)

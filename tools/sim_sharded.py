@@ -182,6 +182,8 @@ def main():
             xb = 0
         print("export per rank:", [round(x, 2) for x in t["export"]], "count per rank:", [round(x, 2) for x in t["count"]])
         mx_ph = {k: round(max(v), 2) for k, v in t.items()}
+        med = {k: round(float(np.median(v)), 2) for k, v in t.items()}
+        print("rep %d  per-rank median ms: %s  sum %.2f" % (rep, med, sum(med.values())))
         print("rep %d  ranks %d  per-rank max ms: %s  sum %.2f  exchanged bytes/rank ~%.0f MB, gathered %.0f MB%s" % (
             rep, world, mx_ph, sum(mx_ph.values()),
             sum(c for c in sends[0][1]) * rbs[0] / 1e6, xb / 1e6, extra))
