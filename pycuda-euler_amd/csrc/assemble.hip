@@ -53,10 +53,14 @@ struct DevBuf {
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap) return EC_OK;
+        // a buffer that grows gets 1/8 of headroom: sizes that vary a little from call to call
+        // (chain counts, received records) would otherwise reallocate -- ~1 ms a hipFree /
+        // hipMalloc pair -- on every call that is a little larger than the last
+        size_t want = std::max<size_t>(bytes, 256);
+        if (cap) want += want / 8;
         if (p) hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t want = std::max<size_t>(bytes, 256);
         if (hipMalloc(&p, want) != hipSuccess) {
             set_error("hipMalloc(%zu) failed", want);
             return EC_ERR_NOMEM;
@@ -2284,7 +2288,9 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     SuperRec *srec = s->rt_srec.as<SuperRec>();
-    const size_t cap = std::max<size_t>(G, 1);
+    // (buffers sized by N, not by the chain count: a count a little above the last call's would
+    // reallocate them -- a hipFree / hipMalloc pair of ~1 ms in the partitioned finish)
+    const size_t cap = std::max<size_t>(std::max(N, G), 1);
     EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec)));
     EC_CHECK(s->rt_pks.ensure(cap * 4));
     EC_CHECK(s->rt_rks.ensure(cap * 4));
@@ -2921,7 +2927,7 @@ int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
     const unsigned int N = 2 * (unsigned int)s->n_dense;
     s->stats.n_rulers = 0;
     if (!M) return EC_OK;
-    EC_CHECK(s->rt_srec.ensure((size_t)M * sizeof(SuperRec)));
+    EC_CHECK(s->rt_srec.ensure(std::max<size_t>(M, N) * sizeof(SuperRec)));
     EC_HIP(hipMemcpyAsync(s->rt_srec.p, d_all, (size_t)M * sizeof(SuperRec), hipMemcpyDeviceToDevice, st));
     k_super_index<<<grid_for(M, 256), 256, 0, st>>>(s->rt_srec.as<SuperRec>(), (unsigned int)M,
                                                     s->rt_sidx.as<unsigned int>());

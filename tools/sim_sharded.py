@@ -52,16 +52,20 @@ def main():
     for rep in range(a.reps):
         t = {}
 
+        def t_start():  # the host-side copies between calls are not charged to the next call
+            torch.cuda.synchronize()
+            return time.perf_counter()
+
         def tick(name, t0):
             torch.cuda.synchronize()
             t[name] = t.get(name, []) + [(time.perf_counter() - t0) * 1e3]
 
         sends = []
         for eng, (d_reads, d_off, n, lo) in zip(engines, shards):
-            t0 = time.perf_counter()
+            t0 = t_start()
             eng.count_shard(d_reads, d_off, n, lo, a.k, 0)
             tick("count", t0)
-            t0 = time.perf_counter()
+            t0 = t_start()
             sends.append(eng.export_by_owner(world, compact=True))
             tick("export", t0)
         rb = distributed.rec_bytes(a.k)
@@ -82,7 +86,7 @@ def main():
         if a.finish == "replicated":  # the round-4 layout: gathered solid set, loaded on every rank
             solids = []
             for eng, (recv, sb) in zip(engines, recvs):
-                t0 = time.perf_counter()
+                t0 = t_start()
                 solids.append(eng.merge_owned_from(recv, sb, bases, lfbs, a.k, 1, 0))
                 tick("merge", t0)
             mx = max(x.numel() for x in solids)
@@ -93,20 +97,20 @@ def main():
             parts = []
             for r, eng in enumerate(engines):
                 lo = sum(nrec[:r])
-                t0 = time.perf_counter()
+                t0 = t_start()
                 eng.graph_load(allsolid, a.k)
                 tick("load", t0)
-                t0 = time.perf_counter()
+                t0 = t_start()
                 part = eng.empty(8 * nrec[r])
                 eng.graph_links_part(lo, lo + nrec[r], part)
                 tick("links", t0)
                 parts.append(part[: 8 * nrec[r]])
             succ = torch.cat(parts)
             eng = engines[0]
-            t0 = time.perf_counter()
+            t0 = t_start()
             eulerhip.check(eng.L.ec_graph_finish(eng._h(), ctypes.c_void_p(succ.data_ptr()), eulerhip.EC_FLAG_TIMING))
             tick("finish", t0)
-            t0 = time.perf_counter()
+            t0 = t_start()
             res = eng.sess.fetch(a.k)
             tick("fetch", t0)
             st = eng.stats()
@@ -115,14 +119,14 @@ def main():
         else:  # the junction-partitioned graph and the partitioned finish, every rank's calls timed
             urs = []
             for eng, (recv, sb) in zip(engines, recvs):
-                t0 = time.perf_counter()
+                t0 = t_start()
                 urs.append(eng.merge_owned_from(recv, sb, bases, lfbs, a.k, 1, 0, export=False))
                 tick("merge", t0)
             seg_lo = [sum(urs[:r]) for r in range(world + 1)]
             U = seg_lo[-1]
             placed = []
             for r, eng in enumerate(engines):
-                t0 = time.perf_counter()
+                t0 = t_start()
                 placed.append(eng.graph_place(seg_lo[r], U, world))
                 tick("place", t0)
             npal = sum(p[2] for p in placed)
@@ -133,47 +137,47 @@ def main():
                 got = [rec[sum(c[:dst]) * jb:sum(c[:dst + 1]) * jb] for rec, c, _ in placed]
                 jx = max(jx, sum(g.numel() for i, g in enumerate(got) if i != dst))
                 recv = torch.cat(got)
-                t0 = time.perf_counter()
+                t0 = t_start()
                 links.append(eng.graph_join(recv, seg_lo))
                 tick("join", t0)
             lx = 0
             for dst, eng in enumerate(engines):
                 got = [rec[sum(c[:dst]) * 8:sum(c[:dst + 1]) * 8] for rec, c in links]
                 lx = max(lx, sum(g.numel() for g in got))
-                t0 = time.perf_counter()
+                t0 = t_start()
                 eng.graph_links_apply(torch.cat(got))
                 tick("apply", t0)
             segs = [(seg_lo[r], seg_lo[r + 1]) for r in range(world)]
             sups = []
             for eng, (lo, hi) in zip(engines, segs):
-                t0 = time.perf_counter()
+                t0 = t_start()
                 sups.append(eng.graph_chains_part(lo, hi)[0])
                 tick("chains", t0)
             supers = torch.cat(sups)
             M = supers.numel() // distributed.SUPER_BYTES
             for eng in engines:
-                t0 = time.perf_counter()
+                t0 = t_start()
                 eng.graph_rank_supers(supers, M)
                 tick("rank_supers", t0)
             sts = []
             for eng, (lo, hi) in zip(engines, segs):
-                t0 = time.perf_counter()
+                t0 = t_start()
                 sts.append(eng.graph_starts_part(M > 0, lo, hi)[0])
                 tick("starts", t0)
             starts = torch.cat(sts)
             nc = starts.numel() // distributed.START_BYTES
             chars = ends = None
             for eng in engines:
-                t0 = time.perf_counter()
+                t0 = t_start()
                 nchars = eng.graph_layout(starts, nc)
                 tick("layout", t0)
-                t0 = time.perf_counter()
+                t0 = t_start()
                 c, e = eng.zeros(nchars), eng.zeros(max(2 * nc * distributed.end_bytes(a.k), 8))
                 eng.graph_emit_part(c, e)
                 tick("emit", t0)
                 chars = c if chars is None else chars + c
                 ends = e.view(torch.int32) if ends is None else ends + e.view(torch.int32)
-            t0 = time.perf_counter()
+            t0 = t_start()
             res = engines[0].graph_collect(chars, ends.view(torch.uint8), a.k, npal)
             tick("collect", t0)
             extra = (", junction records off-rank %.2f MB, link records %.2f MB, chains gathered %.1f MB (%d), "
