@@ -27,6 +27,8 @@
 #include <cmath>
 #include <climits>
 #include <cstring>
+#include <cstddef>
+#include <functional>
 #include <type_traits>
 #include <vector>
 
@@ -213,6 +215,7 @@ struct ec_session {
     uint64_t seg_lo = 0, seg_Ur = 0;
     DevBuf jrec, joid, jout, jseg, jcnt;
     DevBuf xrec;     // ec_merge_owned_from: the received records decoded
+    DevBuf skm_rec, skm_ev, skm_end;  // k_skdedup: the merged records of the error-rich count
     HostBuf hmeta;   // ... and its per-source table, staged page-locked
     int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 52), 1 key hash
     // ec_export_by_owner's owner ids / scanned chunk histogram of the last call, reused by a
@@ -258,6 +261,11 @@ struct ec_session {
     DevBuf x_par, x_irr, x_in, x_succ, x_done, x_lk, x_lv, x_lk2, x_lv2, x_len, x_m, x_cid, x_head, x_tail;
     // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
     DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr;
+    // Wyllie rounds the last converged super ranking needed + 1 (0: none yet, or it did not
+    // converge): rank_supers_async queues that many instead of ceil(log2 N) + 2 -- a round after
+    // convergence still costs its launch (~5 us; the headline needs ~18 of 26) -- and a shortfall
+    // is caught by the convergence check that already follows (the ranking redone, host-checked)
+    int spec_rounds = 0;
     DevBuf wbv;  // count_wide.h minimizer buckets: every window's minimizer
     // multi-GPU partitioned finish (ec_graph_chains_part ..): this rank's segment of oriented nodes
     uint64_t seg_n0 = 0, seg_n1 = 0;
@@ -816,13 +824,40 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         // (the table takes up to 2047 keys; the prediction runs ~10 % high.  ecoli10m_err's
         // fullest bucket: 1525 predicted, 1485 inserted)
         const unsigned int max_keys = kn().skf_keys > 0 ? (unsigned int)kn().skf_keys : 1900u;
-        // (round 4 measured a record merge in front of the filter on ecoli10m_err: its 1535-entry
+        // (round 4 measured a record merge inside the filter kernel on ecoli10m_err: its 1535-entry
         // tables filled -- up to 915 records a bucket rejected -- and its 131 KB of LDS held one
-        // workgroup per CU: compact 8.26 ms against 7.75 without it; removed in round 5.
+        // workgroup per CU: compact 8.26 ms against 7.75 without it; round 5 merges in a kernel
+        // of its own, k_skdedup, EULERHIP_SKF_MERGE=0 the filter alone.
         // No tile planning here: measured on ecoli10m_err the planned tiles left more chains,
         // 11.2 M against 10.9 M -- its graph is cut by error branches, not by tile edges)
         unsigned int *bm = nullptr;
-        if (k & 1)
+        if (kn().skf_merge != 0) {
+            // the bucket's duplicate records merged first (k_skdedup), the filter on the merged ones
+            // (bucket b's merged records at its refine region [bbeg[b], ..): Bk x fcap records)
+            EC_CHECK(s->skm_rec.ensure(Bk * fcap * sizeof(uint4)));
+            EC_CHECK(s->skm_ev.ensure(Bk * fcap * sizeof(uint2)));
+            EC_CHECK(s->skm_end.ensure(Bk * 8));
+            uint4 *mrec = s->skm_rec.as<uint4>();
+            uint2 *mev = s->skm_ev.as<uint2>();
+            unsigned long long *mend = s->skm_end.as<unsigned long long>();
+            const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
+            if (kn().skf_merge == 2)
+                k_skdedup<4096, 1024><<<(unsigned)Bk, 1024, 0, st>>>(s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, mrec,
+                                                                     mev, mend, claim_cap);
+            else
+                k_skdedup<2560, 512><<<(unsigned)Bk, 512, 0, st>>>(s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, mrec,
+                                                                   mev, mend, claim_cap);
+#define EC_SKF_MERGED_ARGS                                                                                   \
+    mrec, bbeg, mend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),      \
+        s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),                                    \
+        s->no_index ? nullptr : s->sub.as<SubSlot>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow, max_keys, \
+        dbg, bm, mev
+            if (k & 1)
+                k_skbucket_filt<2048, NTF, false, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKF_MERGED_ARGS);
+            else
+                k_skbucket_filt<2048, NTF, true, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKF_MERGED_ARGS);
+#undef EC_SKF_MERGED_ARGS
+        } else if (k & 1)
             k_skbucket_filt<2048, NTF, false><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
         else
             k_skbucket_filt<2048, NTF, true><<<(unsigned)Bk, NTF, 0, st>>>(EC_SKBUCKET_ARGS, max_keys, dbg, bm);
@@ -1437,7 +1472,8 @@ OwnerFn owner_fn(int k) {
 }
 
 int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx,
-                     bool &ok, const unsigned int *ids = nullptr, bool allow_sk = true) {
+                     bool &ok, const unsigned int *ids = nullptr, bool allow_sk = true, const XIn *xin = nullptr) {
+    // (xin: the received records read in place, ec_merge_owned_from; d_agg unused)
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -1453,22 +1489,25 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     mark(s, 2 * EC_STAGE_COUNT);
     EC_CHECK(s->mbid.ensure(std::max<uint64_t>(n, 1) * 4));
     EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 1) * 4));
-    EC_CHECK(s->midx.ensure(std::max<uint64_t>(n, 1) * 4));
     EC_CHECK(s->midx2.ensure(std::max<uint64_t>(n, 1) * 4));
     EC_CHECK(s->bstart.ensure((nb + 1ull) * 8));
-    EC_HIP(hipMemsetAsync(s->bstart.p, 0, (nb + 1ull) * 8, st));
+    if (!n) EC_HIP(hipMemsetAsync(s->bstart.p, 0, (nb + 1ull) * 8, st));  // (else k_cs_bounds writes them all)
     if (n) {
-        k_agg_bucket_ids<<<grid_for(n, B), B, 0, st>>>(d_agg, n, bbits, s->mbid.as<unsigned int>(),
-                                                      s->midx.as<unsigned int>(), own.mc, own.sk);
+        if (xin)
+            k_agg_bucket_ids<XIn><<<grid_for(n, B), B, 0, st>>>(*xin, n, bbits, s->mbid.as<unsigned int>(), own.mc,
+                                                               own.sk);
+        else
+            k_agg_bucket_ids<PlainIn><<<grid_for(n, B), B, 0, st>>>(PlainIn{d_agg}, n, bbits, s->mbid.as<unsigned int>(),
+                                                                   own.mc, own.sk);
         // indices by bucket: counting sort (shard.h k_cs_*), buckets 0..nb (nb: filler records)
-        const unsigned int nbins = nb + 1, nch = (unsigned int)((n + CS_CHUNK - 1) / CS_CHUNK);
+        const unsigned int nbins = nb + 1, chunk = cs_chunk(nbins), nch = (unsigned int)((n + chunk - 1) / chunk);
         const uint64_t cells = (uint64_t)nbins * nch;
         EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 2 * cells) * 4));
         unsigned int *hist = s->mbid2.as<unsigned int>(), *incl = hist + cells;
-        k_cs_hist<<<nch, 1024, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist);
+        k_cs_hist<<<nch, 1024, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist, chunk);
         EC_CHECK(scan_incl_u32(s, hist, incl, cells));
         k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist, incl,
-                                                  s->midx2.as<unsigned int>());
+                                                  s->midx2.as<unsigned int>(), chunk);
         k_cs_bounds<<<grid_for(nbins, B), B, 0, st>>>(hist, incl, nbins, nch, s->bstart.as<unsigned long long>());
     }
     mark(s, 2 * EC_STAGE_COUNT + 1);
@@ -1479,9 +1518,9 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     EC_CHECK(s->dfc.ensure(umax * 8));
     EC_CHECK(s->dft.ensure(umax * 8));
     EC_CHECK(s->sub.ensure(umax * sizeof(SubSlot)));
-    EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
-    EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
-    EC_HIP(hipMemsetAsync(&dsc->overflow, 0, 4, st));
+    // ndistinct, est, overflow, nsolid: one fill (they are adjacent; est is the count's alone)
+    static_assert(offsetof(Scalars, nsolid) + 4 - offsetof(Scalars, ndistinct) == 24, "Scalars layout");
+    EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 24, st));
     kmark(s, 2, 0);
     const int sks = own.sk ? (slots == 2048 ? 11 : 12) : 0;
     bool merge_marked = false;
@@ -1498,8 +1537,13 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
             EC_HIP(hipMemsetAsync(s->bmark.p, 0, words * 4, st));
             bm = s->bmark.as<unsigned int>();
         }
-        const AggSource src{d_agg, s->midx2.as<unsigned int>(), sks};
-        EC_CHECK(launch_bucket(s, src, nb, slots, limit, bm));
+        if (xin) {
+            const XAggSource src{*xin, s->midx2.as<unsigned int>(), sks};
+            EC_CHECK(launch_bucket(s, src, nb, slots, limit, bm));
+        } else {
+            const AggSource src{d_agg, s->midx2.as<unsigned int>(), sks};
+            EC_CHECK(launch_bucket(s, src, nb, slots, limit, bm));
+        }
         merge_marked = bm != nullptr;
     }
     kmark(s, 2, 1);
@@ -1533,13 +1577,15 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     return EC_OK;
 }
 
-int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx) {
+int phase_merge(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx,
+                const XIn *xin = nullptr, const std::function<int(const Agg *&)> &decode = nullptr) {
     if (!(s->flags & EC_FLAG_GENERAL)) {
         bool ok = false;
-        EC_CHECK(phase_merge_part(s, d_agg, n, limit, U, sidx, ok));
-        if (!ok && merge_sk(s->k)) EC_CHECK(phase_merge_part(s, d_agg, n, limit, U, sidx, ok, nullptr, false));
+        EC_CHECK(phase_merge_part(s, d_agg, n, limit, U, sidx, ok, nullptr, true, xin));
+        if (!ok && merge_sk(s->k)) EC_CHECK(phase_merge_part(s, d_agg, n, limit, U, sidx, ok, nullptr, false, xin));
         if (ok) return EC_OK;
     }
+    if (xin) EC_CHECK(decode(d_agg));  // the HBM table reads decoded records
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -2317,6 +2363,7 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     rounds = 1;
     while ((1ull << (rounds - 1)) < (unsigned long long)G) rounds++;
     rounds = std::min(rounds + 1, 63);
+    if (s->spec_rounds > 0 && s->spec_rounds < rounds) rounds = s->spec_rounds;
     RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
     for (int r = 0; r < rounds; r++)
         k_rjump<<<gr, B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], 0, N, r ? &dsc->active[r - 1] : nullptr,
@@ -2329,6 +2376,20 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
                                     &dsc->final_sel, &dsc->active[rounds - 1], 0, s->PL.as<unsigned int>(),
                                     s->PM.as<unsigned long long>(), dnr);
     return EC_OK;
+}
+
+// the rounds a ranking used (the last round that still moved a pointer + 1), for the next
+// call's speculation; 0 when the last round still moved one (not converged)
+int rounds_used(const Scalars &h, int rounds) {
+    if (rounds <= 0 || h.active[rounds - 1]) return 0;
+    int used = 1;
+    for (int r = 0; r < rounds; r++)
+        if (h.active[r]) used = r + 2;
+    return std::min(used, rounds);
+}
+void note_rounds(ec_session *s, const Scalars &h, int rounds) {
+    const int used = rounds_used(h, rounds);
+    s->spec_rounds = used ? used + 1 : 0;
 }
 
 // extended alphabet (extended.h): links without their twin link make their components'
@@ -2649,6 +2710,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         if (kn().verbose)
             fprintf(stderr, "rank: %u oriented nodes, %u chains (tile contraction), %u rulers, %llu visited\n", N, Ma,
                     nr, (unsigned long long)hsc.nvisited);
+        if (Ma) note_rounds(s, hsc, rounds);
         if (hsc.nvisited != Ma || (Ma && hsc.active[rounds - 1] != 0)) {
             // a cycle of chains no ruler reached (or unconverged rounds): the ranking with its
             // host-checked ruler passes, then the starts again
@@ -2951,9 +3013,10 @@ int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
         Scalars hsc{};
         EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
         EC_CHECK(host_sync(s, st));
+        note_rounds(s, hsc, rounds);
         if (hsc.nvisited == M && hsc.active[rounds - 1] == 0) {
             s->stats.n_rulers = hsc.nr;
-            s->stats.rank_rounds = rounds;
+            s->stats.rank_rounds = rounds_used(hsc, rounds);
             return EC_OK;
         }
         if (kn().verbose)
@@ -3481,7 +3544,8 @@ int ec_session_destroy(ec_session *s) {
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
                      &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
-                     &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec};
+                     &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec,
+                     &s->skm_rec, &s->skm_ev, &s->skm_end};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->hmeta.release();
@@ -3848,7 +3912,11 @@ int ec_export_by_owner_ex(ec_session *s, int nowners, void *d_out, uint64_t *own
     return EC_OK;
 }
 
-int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags) {
+}  // extern "C"
+
+// the owner merge; xin: k <= 32 records read in place (decode: the decoded copy, for the HBM table)
+int merge_owned_impl(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags,
+                     const XIn *xin = nullptr, const std::function<int(const Agg *&)> &decode = nullptr) {
     if (!s || (n && !d_records)) {
         set_error("null argument");
         return EC_ERR_ARG;
@@ -3862,7 +3930,7 @@ int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int 
         rc = phase_merge_w(s, reinterpret_cast<const AggW *>(d_records), n, (long long)limit, U, sidx);
     } else {
         SolidIndex sidx{};
-        rc = phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx);
+        rc = phase_merge(s, reinterpret_cast<const Agg *>(d_records), n, (long long)limit, U, sidx, xin, decode);
     }
     s->no_index = false;
     EC_CHECK(rc);
@@ -3870,6 +3938,12 @@ int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int 
     collect_timing(s);
     s->stats_ok = true;
     return EC_OK;
+}
+
+extern "C" {
+
+int ec_merge_owned(ec_session *s, const void *d_records, uint64_t n, int k, int limit, unsigned flags) {
+    return merge_owned_impl(s, d_records, n, k, limit, flags);
 }
 
 // the merge of records received from nsrc ranks (ec_export_by_owner_ex: compact or full per
@@ -3920,6 +3994,18 @@ int ec_merge_owned_from(ec_session *s, const void *d_records, int nsrc, const ui
     memcpy(s->hmeta.data() + hoff.size() * 8, hb.data(), (size_t)nsrc * 8);
     memcpy(s->hmeta.data() + hoff.size() * 8 + (size_t)nsrc * 8, hl.data(), (size_t)nsrc * 4);
     EC_HIP(hipMemcpyAsync(doff, s->hmeta.data(), mbytes, hipMemcpyHostToDevice, st));
+    if (k <= 32 && rsum && !kn().merge_decode) {
+        // k <= 32: the merge reads the received records in place; the decoded copy only for the
+        // HBM-table fallback (a bucket past its LDS table, or EC_FLAG_GENERAL)
+        const XIn xin{static_cast<const uint8_t *>(d_records), doff, doff + nsrc + 1, dbase, dlfb, nsrc};
+        auto decode = [&](const Agg *&out) -> int {
+            k_uncompact<unsigned long long><<<grid_for(rsum, 256), 256, 0, s->stream>>>(
+                static_cast<const uint8_t *>(d_records), doff, doff + nsrc + 1, dbase, dlfb, nsrc, rsum, s->xrec.as<Agg>());
+            out = s->xrec.as<Agg>();
+            return EC_OK;
+        };
+        return merge_owned_impl(s, s->xrec.p, rsum, k, limit, flags, &xin, decode);
+    }
     if (rsum) {
         if (k > 32)
             k_uncompact<K128><<<grid_for(rsum, 256), 256, 0, st>>>(static_cast<const uint8_t *>(d_records), doff,
@@ -4124,7 +4210,7 @@ int ec_link_record_bytes(void) { return (int)sizeof(LinkRec); }
 // counting sort of n ids (bins 0..nbins-1) -> perm (midx2) and bin starts bstart[0..nbins]
 int bin_sort(ec_session *s, const unsigned int *bid, uint64_t n, unsigned int nbins, unsigned long long *bstart) {
     hipStream_t st = s->stream;
-    const unsigned int nch = (unsigned int)std::max<uint64_t>((n + CS_CHUNK - 1) / CS_CHUNK, 1);
+    const unsigned int chunk = cs_chunk(nbins), nch = (unsigned int)std::max<uint64_t>((n + chunk - 1) / chunk, 1);
     const uint64_t cells = (uint64_t)nbins * nch;
     EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(2 * cells, 2) * 4));
     EC_CHECK(s->midx2.ensure(std::max<uint64_t>(n, 1) * 4));
@@ -4133,9 +4219,9 @@ int bin_sort(ec_session *s, const unsigned int *bid, uint64_t n, unsigned int nb
         EC_HIP(hipMemsetAsync(bstart, 0, (nbins + 1ull) * 8, st));
         return EC_OK;
     }
-    k_cs_hist<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist);
+    k_cs_hist<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist, chunk);
     EC_CHECK(scan_incl_u32(s, hist, incl, cells));
-    k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist, incl, s->midx2.as<unsigned int>());
+    k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist, incl, s->midx2.as<unsigned int>(), chunk);
     k_cs_bounds<<<grid_for(nbins, 256), 256, 0, st>>>(hist, incl, nbins, nch, bstart);
     EC_HIP(hipMemcpyAsync(bstart + nbins, &incl[cells - 1], 4, hipMemcpyDeviceToDevice, st));  // (low word)
     EC_HIP(hipMemsetAsync(reinterpret_cast<unsigned int *>(bstart + nbins) + 1, 0, 4, st));

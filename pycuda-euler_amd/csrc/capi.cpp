@@ -39,6 +39,8 @@ void refresh_knobs() {
         k.rj_div = num("EULERHIP_RJ_DIV", 0);
         k.rank_sync = num("EULERHIP_RANK_SYNC", 0);
         k.merge_mix = flag("EULERHIP_MERGE_MIX");
+        k.merge_decode = flag("EULERHIP_MERGE_DECODE");
+        k.skf_merge = num("EULERHIP_SKF_MERGE", 1);
         k.wide_general = flag("EULERHIP_WIDE_GENERAL");
         k.wide_max_bbits = num("EULERHIP_WIDE_MAX_BBITS", -1);
         k.wide_l3 = num("EULERHIP_WIDE_L3", 0);

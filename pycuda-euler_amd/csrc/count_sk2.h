@@ -1136,14 +1136,19 @@ __global__ void __launch_bounds__(NT) k_skbucket3(const uint4 *recs, const unsig
 // p^2, p = 1 - exp(-2D/m) = 0.14: ~170 singletons a table; 2^16 cells passed ~600 and overflowed
 // the 1474-key budget in many buckets
 constexpr int SKF_BITS = 17;  // filter cells per bitmap
-template <int SLOTS, int NT, bool EVEN_K>
+// MERGED (round 5): the bucket's records merged by k_skdedup first -- {canonical bases | (n - 1)
+// << 28, multiplicity} with their event minima {A, B} in mev -- so a super-k-mer read ~130 times
+// rolls out its windows once, with add = multiplicity (a key of a record seen twice is repeated:
+// its cells are marked seen twice at once, and it is inserted without the filter's test)
+template <int SLOTS, int NT, bool EVEN_K, bool MERGED = false>
 __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const unsigned long long *bbeg,
                                                       const unsigned long long *bend, int k, uint32_t M, double inv_m,
                                                       long long limit, unsigned long long *dkey, unsigned int *dcnt,
                                                       unsigned long long *dfc, unsigned long long *dft, SubSlot *sub,
                                                       unsigned int *nsolid, unsigned long long *ndistinct,
                                                       unsigned int *overflow, unsigned int max_keys,
-                                                      unsigned long long *dbg = nullptr, unsigned int *bmark = nullptr) {
+                                                      unsigned long long *dbg = nullptr, unsigned int *bmark = nullptr,
+                                                      const uint2 *mev = nullptr) {
     constexpr int SBITS = __builtin_ctz(SLOTS);
     constexpr unsigned int NW = 1u << (SKF_BITS - 5), CM = (1u << SKF_BITS) - 1;
     __shared__ LTabE<SLOTS> tab;
@@ -1165,8 +1170,26 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
     const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
     // the windows of a record as stored (window o = bases o .. o + k - 1, o < n <= 16): canonical
     // key, add, first events of the canonical / twin string (k_skbucket3's roll-out, unflipped)
-    auto windows = [&](const uint4 &x, auto &&fn) {
+    auto windows = [&](uint64_t ri, const uint4 &x, auto &&fn) {
         const unsigned int n = (x.z >> 28) + 1;
+        if constexpr (MERGED) {  // canonical record: window o at A + o, its twin at B - o
+            const uint2 e = mev[ri];
+            const unsigned int mult = x.w;
+            for (unsigned int o = 0; o < n; o++) {
+                const uint32_t lo = __builtin_amdgcn_alignbit(x.y, x.x, 2 * o), hi = __builtin_amdgcn_alignbit(x.z, x.y, 2 * o);
+                const uint64_t P = (uint64_t)lo | (uint64_t)hi << 32;
+                const uint64_t rv = ~P & kmask, fw = rev2_64(P) >> fsh;
+                const bool tw = fw > rv;
+                const unsigned int ef = e.x + o, et = e.y - o;
+                unsigned int add = mult, eC = tw ? et : ef, eT = tw ? ef : et;
+                if (EVEN_K && fw == rv) {
+                    add = 2 * mult;
+                    eC = eT = min(ef, et);
+                }
+                fn(tw ? rv : fw, add, eC, eT);
+            }
+            return;
+        }
         const unsigned int p = x.w;
         const unsigned int rd0 = (unsigned int)((double)p * inv_m);
         int rm = (int)(p - rd0 * M);
@@ -1195,10 +1218,17 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
     };
     // pass 0: the filter
     for (uint64_t i = r0 + tid; i < r1; i += NT) {
-        windows(recs[i], [&](unsigned long long c, unsigned int, unsigned int, unsigned int) {
+        const uint4 x = recs[i];
+        const bool rep = MERGED && x.w > 1;  // (a merged record seen twice: its keys are repeated)
+        windows(i, x, [&](unsigned long long c, unsigned int, unsigned int, unsigned int) {
             unsigned int c1, c2;
             cells(c, c1, c2);
             const unsigned int m1 = 1u << (c1 & 31), mm2 = 1u << (c2 & 31);
+            if (rep) {
+                atomicOr(&seen1[c1 >> 5], m1), atomicOr(&seen2[c1 >> 5], m1);
+                atomicOr(&seen1[c2 >> 5], mm2), atomicOr(&seen2[c2 >> 5], mm2);
+                return;
+            }
             if (atomicOr(&seen1[c1 >> 5], m1) & m1) atomicOr(&seen2[c1 >> 5], m1);
             if (atomicOr(&seen1[c2 >> 5], mm2) & mm2) atomicOr(&seen2[c2 >> 5], mm2);
         });
@@ -1238,11 +1268,13 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
     }
     // pass 1: the keys seen twice (or solid by their own insert) into the table
     for (uint64_t i = r0 + tid; i < r1; i += NT) {
-        windows(recs[i], [&](unsigned long long c, unsigned int add, unsigned int eC, unsigned int eT) {
-            unsigned int c1, c2;
-            cells(c, c1, c2);
-            const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
-            if (!twice && (long long)add <= limit) return;
+        windows(i, recs[i], [&](unsigned long long c, unsigned int add, unsigned int eC, unsigned int eT) {
+            if ((long long)add <= limit) {  // (add > limit: solid by this insert alone)
+                unsigned int c1, c2;
+                cells(c, c1, c2);
+                const bool twice = ((seen2[c1 >> 5] >> (c1 & 31)) & (seen2[c2 >> 5] >> (c2 & 31)) & 1u) != 0;
+                if (!twice) return;
+            }
             const unsigned int s0 = (sk_slot(c) >> (32 - SBITS)) & (SLOTS - 1);
             const unsigned int sl = lds_locate<SLOTS>(tab, s_over, c, s0, tab.key[s0]);
             atomicAdd(&tab.count[sl], add);
@@ -1263,5 +1295,113 @@ __global__ void __launch_bounds__(NT) k_skbucket_filt(const uint4 *recs, const u
                                                                       EvExpand{2 * M}, bmark);
 }
 
+
+// ---- error-rich input: the bucket's duplicate records merged in front of the filter (round 5) -----
+// At 0.5 % substitutions ~60 % of the reads are error-free and most super-k-mers of the others
+// are too: ecoli10m_err's buckets hold ~6300 records of which ~1200 are distinct.  k_skdedup merges
+// a bucket's records by canonical content (k_skbucket3's record table and claim protocol) and
+// writes the distinct ones -- {bases | (n - 1) << 28, multiplicity} + {A, B} -- at the bucket's
+// start in mrec / mev; a record past the table's claim cap is written as it is (multiplicity 1,
+// any split of the copies between entries is exact).  k_skbucket_filt<MERGED> then rolls out
+// ~6x fewer windows, twice.  mend[b] = the end of bucket b's merged records.  (Round 4 merged in
+// the filter kernel itself: its 131 KB of LDS held one workgroup per CU, slower than no merge.)
+template <int RS, int NT>
+__global__ void __launch_bounds__(NT) k_skdedup(const uint4 *recs, const unsigned long long *bbeg,
+                                                const unsigned long long *bend, int k, uint32_t M, double inv_m,
+                                                uint4 *mrec, uint2 *mev, unsigned long long *mend,
+                                                unsigned int claim_cap = ~0u) {
+    constexpr uint32_t PEND = 0x800u;
+    constexpr unsigned int CLAIM_MAX = RS - 1 - NT;  // (probes of the records in flight end)
+    static_assert(RS > NT + 1, "record table too small for the records in flight");
+    __shared__ uint32_t tag[RS], tx[RS], ty[RS], tz[RS], tm[RS], ta[RS], tb[RS];
+    __shared__ unsigned int s_nent, s_nout;
+    const unsigned int b = blockIdx.x, tid = threadIdx.x;
+    for (int i = tid; i < RS; i += NT) {
+        tag[i] = 0;
+        tm[i] = 0;
+        ta[i] = tb[i] = 0xFFFFFFFFu;
+    }
+    if (tid == 0) s_nent = 0, s_nout = 0;
+    __syncthreads();
+    const uint64_t r0 = bbeg[b], r1 = bend[b];
+    const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
+    auto ld = [](uint32_t *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    for (uint64_t c0 = r0; c0 < r1; c0 += NT) {
+        const uint64_t ri = c0 + tid;
+        const bool valid = ri < r1;
+        const uint4 x = recs[valid ? ri : r0];
+        // canonical content (k_skbucket3's record round)
+        const unsigned int n = (x.z >> 28) + 1, L2 = 2 * (n + (unsigned int)k - 1);
+        const uint32_t m1 = L2 >= 64 ? 0xFFFFFFFFu : (1u << ((L2 - 32) & 31)) - 1u;
+        const uint32_t mw2 = L2 > 64 ? (1u << ((L2 - 64) & 31)) - 1u : 0u;
+        const uint32_t x0 = x.x, x1 = x.y & m1, x2 = x.z & mw2;
+        const uint32_t y0 = rev2_32b(x2), y1 = rev2_32b(x1), y2 = rev2_32b(x0);
+        const unsigned int sft = 96 - L2, s5 = sft & 31;
+        const bool lo = sft < 32;
+        const uint32_t a0 = __builtin_amdgcn_alignbit(y1, y0, s5), a1 = __builtin_amdgcn_alignbit(y2, y1, s5),
+                       a2 = y2 >> s5;
+        const uint32_t q0 = ~(lo ? a0 : a1), q1 = ~(lo ? a1 : a2) & m1, q2 = lo ? ~a2 & mw2 : 0u;
+        const bool flip = q2 != x2 ? q2 < x2 : q1 != x1 ? q1 < x1 : q0 < x0;
+        const unsigned int p = x.w;
+        const unsigned int rd0 = (unsigned int)((double)p * inv_m);
+        int rm = (int)(p - rd0 * M);
+        unsigned int rd = rd0;
+        if (rm < 0) rd--, rm += (int)M;
+        else if (rm >= (int)M) rd++, rm -= (int)M;
+        const unsigned int A = rd * M2 + (unsigned int)rm, B = rd * M2 + m2 - (unsigned int)rm;
+        const uint32_t K0 = flip ? q0 : x0, K1 = flip ? q1 : x1, K2 = (flip ? q2 : x2) | (n - 1) << 28;
+        const uint32_t EA = flip ? B - n + 1 : A, EB = flip ? A + n - 1 : B;
+        uint32_t hh = K0 * 0x9E3779B1u;
+        hh = (hh ^ (hh >> 15) ^ K1) * 0x85EBCA77u;
+        hh = (hh ^ (hh >> 13) ^ K2) * 0xC2B2AE3Du;
+        hh ^= hh >> 16;
+        const uint32_t TG = (hh | 0x1000u) & 0xFFFFF000u;
+        uint32_t SL = __umulhi(hh * 0x27D4EB2Fu, (unsigned int)RS);
+        int ST = valid ? 0 : 1;  // 0 searching, 1 found / claimed, 2 past the claim cap
+#pragma unroll 1
+        while (__any(ST == 0)) {
+            const uint32_t T = ld(&tag[SL]);
+            asm volatile("" ::: "memory");  // the key words are read after the tag (issue order)
+            const uint32_t X = ld(&tx[SL]), Y = ld(&ty[SL]), Z = ld(&tz[SL]);
+            const bool hit = T == TG && X == K0 && Y == K1 && Z == K2;
+            const bool go = ST == 0;
+            ST = go && hit ? 1 : ST;
+            const bool claim = go && !hit && T == 0;
+            if (go && !hit && T != 0 && T != (TG | PEND)) SL = SL + 1 == (unsigned int)RS ? 0u : SL + 1;
+            if (claim) {
+                const unsigned int o = atomicAdd(&s_nent, 1u);
+                if (o >= min(CLAIM_MAX, claim_cap)) {  // (claim_cap: tests of the records past the cap)
+                    atomicSub(&s_nent, 1u);
+                    ST = 2;
+                } else if (atomicCAS(&tag[SL], 0u, TG | PEND) == 0) {
+                    tx[SL] = K0, ty[SL] = K1, tz[SL] = K2;
+                    __hip_atomic_store(&tag[SL], TG, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ST = 1;
+                } else {
+                    atomicSub(&s_nent, 1u);
+                }
+            }
+        }
+        if (valid && ST == 1) {
+            atomicAdd(&tm[SL], 1u);
+            if (EA < ta[SL]) atomicMin(&ta[SL], EA);
+            if (EB < tb[SL]) atomicMin(&tb[SL], EB);
+        }
+        if (ST == 2) {  // past the cap: written on its own
+            const uint64_t o = r0 + atomicAdd(&s_nout, 1u);
+            mrec[o] = make_uint4(K0, K1, K2, 1u);
+            mev[o] = make_uint2(EA, EB);
+        }
+    }
+    __syncthreads();
+    for (unsigned int i = tid; i < (unsigned int)RS; i += NT) {
+        if (!tag[i]) continue;
+        const uint64_t o = r0 + atomicAdd(&s_nout, 1u);
+        mrec[o] = make_uint4(tx[i], ty[i], tz[i], tm[i]);
+        mev[o] = make_uint2(ta[i], tb[i]);
+    }
+    __syncthreads();
+    if (tid == 0) mend[b] = r0 + s_nout;
+}
 
 }  // namespace ec

@@ -253,6 +253,56 @@ __global__ void __launch_bounds__(256) k_uncompact(const uint8_t *in, const unsi
     }
 }
 
+// The received records read in place (round 5, k <= 32): record t's source by a search over
+// roff, compact records decoded with their source's read base.  The owner merge's bucket ids and
+// bucket tables read them directly (XAggSource) instead of a decoded copy (k_uncompact wrote and
+// read back 147 MB a rank at 8 weak ranks: 55 us + the gather of 32-B records).
+struct XIn {
+    const uint8_t *in;
+    const unsigned long long *boff, *roff;
+    const long long *rbase;
+    const int *lfb;
+    int nsrc;
+    __device__ inline int src_of(uint64_t t) const {
+        int a = 0, b = nsrc;  // roff[a] <= t < roff[b]
+        while (b - a > 1) {
+            const int m = (a + b) >> 1;
+            if (t >= roff[m]) a = m;
+            else b = m;
+        }
+        return a;
+    }
+    __device__ inline Agg get(uint64_t t) const {
+        const int a = src_of(t);
+        const uint64_t i = t - roff[a];
+        const int lb = lfb[a];
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(in + boff[a]);  // (4-B aligned only)
+        Agg r;
+        if (lb < 0) {
+            uint32_t *d = reinterpret_cast<uint32_t *>(&r);
+#pragma unroll
+            for (int q = 0; q < (int)(sizeof(Agg) / 4); q++) d[q] = w[i * (sizeof(Agg) / 4) + q];
+            return r;
+        }
+        const uint32_t *c = w + i * 5;
+        const unsigned long long rb = (unsigned long long)rbase[a];
+        r = RecOf<unsigned long long>::make((unsigned long long)c[0] | (unsigned long long)c[1] << 32, c[2],
+                                            ev_unpack(c[3], lb, rb), ev_unpack(c[4], lb, rb));
+        return r;
+    }
+    __device__ inline unsigned long long key(uint64_t t) const {
+        const int a = src_of(t);
+        const uint64_t i = t - roff[a];
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(in + boff[a]) + i * (lfb[a] < 0 ? sizeof(Agg) / 4 : 5);
+        return (unsigned long long)w[0] | (unsigned long long)w[1] << 32;
+    }
+};
+static_assert(sizeof(CRec) == 20, "XIn decodes 5-word records");
+struct PlainIn {
+    const Agg *p;
+    __device__ inline unsigned long long key(uint64_t t) const { return p[t].key; }
+};
+
 // scatter dense records into owner-major order at the scanned chunk bases (owners from
 // k_owner_hist's oid); evbase = the
 // shard's first global read id << 32 (ec_count_shard counts shard-relative)
@@ -328,39 +378,46 @@ __global__ void __launch_bounds__(256) k_export_dense(const K *dkey, const unsig
 // bucket id = top bbits of mix64(key) (the fused path's bucket hash, so the SolidIndex
 // sub-table layout is shared), or with sk the top bbits of the key's minimizer (OwnerFn);
 // filler records (all-ones key) go to bucket 2^bbits, past the end.
-__global__ void __launch_bounds__(256) k_agg_bucket_ids(const Agg *in, uint64_t n, int bbits, unsigned int *bid,
-                                                        unsigned int *idx, MinCfg mc, int sk) {
+template <typename In>
+__global__ void __launch_bounds__(256) k_agg_bucket_ids(In in, uint64_t n, int bbits, unsigned int *bid, MinCfg mc,
+                                                        int sk) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned long long key = in[t].key;
+        const unsigned long long key = in.key(t);
         bid[t] = key == EMPTY_KEY ? (1u << bbits)
                  : sk             ? sk_bucket_of(minimizer_of(key, mc), bbits)
                                   : (bbits ? (unsigned int)(mix64(key) >> (64 - bbits)) : 0u);
-        idx[t] = (unsigned int)t;
     }
 }
 
 // Counting sort of record indices by bucket id (round 4; a rocPRIM radix sort of (id, index)
-// pairs took 4 x 55 us a call): per chunk of CS_CHUNK records an LDS histogram of the nbins
-// ids, stored bucket-major; one scan over (bucket, chunk); per chunk LDS cursors place the
-// indices.  The order inside a (bucket, chunk) cell is not deterministic -- the bucket tables
-// do not depend on it.  1024 threads a chunk (round 5: 256 left ~280 workgroups on 256 CUs for
-// 4.6 M records).
+// pairs took 4 x 55 us a call): per chunk of records an LDS histogram of the nbins ids, stored
+// bucket-major; one scan over (bucket, chunk); per chunk LDS cursors place the indices.  The
+// order inside a (bucket, chunk) cell is not deterministic -- the bucket tables do not depend on
+// it.  1024 threads a chunk (round 5: 256 left ~280 workgroups on 256 CUs for 4.6 M records).
+// The chunk grows with nbins (cs_chunk): the bucket-major cells are written and read back with
+// a stride of one cell per chunk, so nbins x chunks strided accesses -- 8193 buckets x 281
+// chunks of 16 K cost the owner merge 46 + 21 + 64 us for the histogram, scan and scatter.
 constexpr unsigned int CS_CHUNK = 16384;
+inline unsigned int cs_chunk(unsigned int nbins) {
+    unsigned int c = CS_CHUNK;
+    while (c < 262144u && c < 8ull * nbins) c <<= 1;
+    return c;
+}
 __global__ void __launch_bounds__(1024) k_cs_hist(const unsigned int *bid, uint64_t n, unsigned int nbins, unsigned int nch,
-                                                 unsigned int *hist) {
+                                                 unsigned int *hist, unsigned int chunk) {
     extern __shared__ unsigned int csh[];
     for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) csh[i] = 0;
     __syncthreads();
-    const uint64_t c = blockIdx.x, t0 = c * CS_CHUNK, t1 = t0 + CS_CHUNK < n ? t0 + CS_CHUNK : n;
+    const uint64_t c = blockIdx.x, t0 = c * chunk, t1 = t0 + chunk < n ? t0 + chunk : n;
     for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) atomicAdd(&csh[bid[t]], 1u);
     __syncthreads();
     for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) hist[(uint64_t)i * nch + c] = csh[i];
 }
 __global__ void __launch_bounds__(1024) k_cs_scatter(const unsigned int *bid, uint64_t n, unsigned int nbins,
                                                     unsigned int nch, const unsigned int *hist,
-                                                    const unsigned int *incl, unsigned int *out) {
+                                                    const unsigned int *incl, unsigned int *out, unsigned int chunk) {
     extern __shared__ unsigned int csh[];
-    const uint64_t c = blockIdx.x, t0 = c * CS_CHUNK, t1 = t0 + CS_CHUNK < n ? t0 + CS_CHUNK : n;
+    const uint64_t c = blockIdx.x, t0 = c * chunk, t1 = t0 + chunk < n ? t0 + chunk : n;
     for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) {
         const uint64_t q = (uint64_t)i * nch + c;
         csh[i] = incl[q] - hist[q];
@@ -415,6 +472,24 @@ struct AggSource {
 };
 
 
+// AggSource over the received records in place (XIn)
+struct XAggSource {
+    EC_AGG_SOURCE
+    XIn in;
+    const unsigned int *perm;
+    int sks;
+    using Raw = Agg;
+    static constexpr bool kDet = false;
+    __device__ inline Raw fetch(uint64_t i) const { return in.get(perm[i]); }
+    __device__ inline unsigned int id(const Raw &) const { return 0; }
+    __device__ inline void decode(const Agg &a, unsigned long long &key, unsigned int &add, unsigned long long &eC,
+                                  unsigned long long &eT) const {
+        key = a.key;
+        add = a.count;
+        eC = a.fC;
+        eT = a.fT;
+    }
+};
 
 // ---- partitioned graph phase (k <= 32): every rank loads the all-gathered solid set with the
 // SAME dense ids (position among the non-filler records, i.e. owner-major), computes the links
