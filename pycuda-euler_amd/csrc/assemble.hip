@@ -160,7 +160,8 @@ struct ec_session {
     // the contig characters' early copy to host memory (phase_graph): its stream and events, and
     // the previous call's character total that sizes it
     hipStream_t ostream = nullptr;
-    hipEvent_t oev[2] = {nullptr, nullptr};
+    // oev[0] / [1]: emission done / characters copied; [2] contig offsets final; [3] link offsets final
+    hipEvent_t oev[4] = {nullptr, nullptr, nullptr, nullptr};
     uint64_t last_nchars = 0;
     // bucket starts of the dense ids (k_skbucket3 marks each bucket's first id): the tile
     // ranking cuts its tiles there (k_tile_plan); valid from a super-k-mer count to its graph phase
@@ -461,6 +462,8 @@ int begin_call(ec_session *s, int k, unsigned flags) {
         return EC_ERR_ARG;
     }
     EC_HIP(hipSetDevice(s->device));
+    // (an earlier call that failed may have left a results copy in flight on the output stream)
+    if (s->ostream) EC_HIP(hipStreamSynchronize(s->ostream));
     memset(&s->stats, 0, sizeof(s->stats));
     s->k = k;
     s->want_dict = (flags & EC_FLAG_WANT_DICT) != 0;
@@ -1471,6 +1474,23 @@ OwnerFn owner_fn(int k) {
     return f;
 }
 
+// counting sort of n > 0 bin ids (shard.h k_cs_*): perm in midx2, bin starts bstart[0..nbins)
+// (end: and bstart[nbins] = n)
+int cs_sort(ec_session *s, const unsigned int *bid, uint64_t n, unsigned int nbins, unsigned long long *bstart,
+            bool end = false) {
+    hipStream_t st = s->stream;
+    const unsigned int nch = (unsigned int)((n + CS_CHUNK - 1) / CS_CHUNK);
+    EC_CHECK(s->midx2.ensure(std::max<uint64_t>(n, 1) * 4));
+    EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 3ull * nbins) * 4));  // (mbid2 is free here)
+    unsigned int *tot = s->mbid2.as<unsigned int>(), *incl = tot + nbins, *cur = incl + nbins;
+    EC_HIP(hipMemsetAsync(tot, 0, (size_t)nbins * 4, st));
+    k_cs_hist<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, tot);
+    EC_CHECK(scan_incl_u32(s, tot, incl, nbins));
+    k_cs_starts<<<grid_for(nbins, 256), 256, 0, st>>>(tot, incl, nbins, bstart, cur, end);
+    k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, cur, s->midx2.as<unsigned int>());
+    return EC_OK;
+}
+
 int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limit, unsigned int &U, SolidIndex &sidx,
                      bool &ok, const unsigned int *ids = nullptr, bool allow_sk = true, const XIn *xin = nullptr) {
     // (xin: the received records read in place, ec_merge_owned_from; d_agg unused)
@@ -1491,7 +1511,7 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
     EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 1) * 4));
     EC_CHECK(s->midx2.ensure(std::max<uint64_t>(n, 1) * 4));
     EC_CHECK(s->bstart.ensure((nb + 1ull) * 8));
-    if (!n) EC_HIP(hipMemsetAsync(s->bstart.p, 0, (nb + 1ull) * 8, st));  // (else k_cs_bounds writes them all)
+    if (!n) EC_HIP(hipMemsetAsync(s->bstart.p, 0, (nb + 1ull) * 8, st));  // (else k_cs_starts writes them all)
     if (n) {
         if (xin)
             k_agg_bucket_ids<XIn><<<grid_for(n, B), B, 0, st>>>(*xin, n, bbits, s->mbid.as<unsigned int>(), own.mc,
@@ -1500,15 +1520,7 @@ int phase_merge_part(ec_session *s, const Agg *d_agg, uint64_t n, long long limi
             k_agg_bucket_ids<PlainIn><<<grid_for(n, B), B, 0, st>>>(PlainIn{d_agg}, n, bbits, s->mbid.as<unsigned int>(),
                                                                    own.mc, own.sk);
         // indices by bucket: counting sort (shard.h k_cs_*), buckets 0..nb (nb: filler records)
-        const unsigned int nbins = nb + 1, chunk = cs_chunk(nbins), nch = (unsigned int)((n + chunk - 1) / chunk);
-        const uint64_t cells = (uint64_t)nbins * nch;
-        EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(n, 2 * cells) * 4));
-        unsigned int *hist = s->mbid2.as<unsigned int>(), *incl = hist + cells;
-        k_cs_hist<<<nch, 1024, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist, chunk);
-        EC_CHECK(scan_incl_u32(s, hist, incl, cells));
-        k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(s->mbid.as<unsigned int>(), n, nbins, nch, hist, incl,
-                                                  s->midx2.as<unsigned int>(), chunk);
-        k_cs_bounds<<<grid_for(nbins, B), B, 0, st>>>(hist, incl, nbins, nch, s->bstart.as<unsigned long long>());
+        EC_CHECK(cs_sort(s, s->mbid.as<unsigned int>(), n, nb + 1, s->bstart.as<unsigned long long>()));
     }
     mark(s, 2 * EC_STAGE_COUNT + 1);
     mark(s, 2 * EC_STAGE_COMPACT);
@@ -2287,7 +2299,7 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
                                       &dsc->nr, s->rid.as<uint2>(), s->rlist.as<unsigned int>());
         k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
         k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), r0, &dsc->nr, masks[it], s->rid.as<uint2>(),
-                                     s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
+                                     s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited, srec);
         EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
         EC_CHECK(host_sync(s, st));
         r0 = hsc.nr;
@@ -2356,7 +2368,7 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
                                   s->rid.as<uint2>(), s->rlist.as<unsigned int>(), dM);
     k_rulers_total<<<1, 1, 0, st>>>(s->rbc.as<unsigned int>() + nblk, nblk, &dsc->nr);
     k_walk_s<<<2048, B, 0, st>>>(snrec, s->rlist.as<unsigned int>(), 0, &dsc->nr, smask, s->rid.as<uint2>(),
-                                 s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited);
+                                 s->nextR.as<unsigned int>(), s->st0.as<RJump>(), &dsc->nvisited, srec);
     // rulers <= chains <= N: rounds for N (a round after convergence returns at its first load)
     const unsigned int gr = std::min(grid_for(G / (kn().rj_div > 0 ? (unsigned)kn().rj_div : 8u) + 1, B), 2048u);
     k_rjump_init<<<gr, B, 0, st>>>(s->nextR.as<unsigned int>(), 0, s->st0.as<RJump>(), dnr);
@@ -2783,6 +2795,22 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     // nodes are up to twice its canonical k-mers)
     EC_CHECK(s->h_coff.resize(nc + 1));
     EC_CHECK(d2h(s, &s->h_coff[nc], s->coff.as<unsigned long long>() + nc, 8, st));
+    // the results' copies to host memory run on the output stream, each as soon as its data is
+    // final: the contig offsets here (overlapping emission and GFA), the characters after the
+    // emission, the link offsets after the GFA counts (ecoli10m_err: 1.1 M contigs, 47 MB of
+    // results copied after GFA took ~1 ms in line)
+    auto ostream_ready = [&]() -> int {
+        if (!s->ostream) EC_HIP(hipStreamCreateWithFlags(&s->ostream, hipStreamNonBlocking));
+        for (auto &e : s->oev)
+            if (!e) EC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        return EC_OK;
+    };
+    EC_CHECK(ostream_ready());
+    if (nc) {
+        EC_HIP(hipEventRecord(s->oev[2], st));
+        EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[2], 0));
+        EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, (size_t)nc * 8, hipMemcpyDeviceToHost, s->ostream));
+    }
     mark(s, 2 * EC_STAGE_STARTS + 1);
     uint64_t chars_bound = 2ull * U + (uint64_t)nc * (uint64_t)(k - 1);
     if (nx) {  // emulated contigs may overlap: the bound is their exact total
@@ -2832,9 +2860,6 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     uint64_t pre = 0;
     if (s->last_nchars && s->last_nchars <= chars_bound && kn().no_spec == 0) {
         pre = s->last_nchars;
-        if (!s->ostream) EC_HIP(hipStreamCreateWithFlags(&s->ostream, hipStreamNonBlocking));
-        for (auto &e : s->oev)
-            if (!e) EC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         EC_CHECK(s->h_chars.resize(pre));
         EC_HIP(hipEventRecord(s->oev[0], st));
         EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[0], 0));
@@ -2860,20 +2885,23 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     const unsigned int n2 = 2 * nc;
     EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
     s->h_loff[n2] = 0;
-    if (nc) EC_CHECK(d2h(s, s->h_coff.data(), s->coff.p, (size_t)nc * 8, st));
-    else s->h_coff[0] = 0;
+    if (!nc) s->h_coff[0] = 0;
+    unsigned long long nlinks64 = 0;
     if (nc) {
         EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));   // per-side counts as u64 (starts sorted)
         EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));  // their exclusive scan = link offsets
         k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>());
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
-        EC_CHECK(d2h(s, s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, st));
+        EC_HIP(hipEventRecord(s->oev[3], st));
+        EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[3], 0));
+        EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, s->ostream));
+        EC_CHECK(d2h(s, &nlinks64, s->skeys2.as<unsigned long long>() + n2, 8, st));
     }
     unsigned int emit_bad = 0;
     EC_CHECK(d2h(s, &emit_bad, &dsc->skew, 4, st));
-    EC_CHECK(host_sync(s, st));  // h_coff[nc] (the characters), h_loff
+    EC_CHECK(host_sync(s, st));  // h_coff[nc] (the characters), the link total
     const uint64_t nchars = s->h_coff[nc];
-    if (pre && (emit_bad || nchars > chars_bound)) hipEventSynchronize(s->oev[1]);  // (no copy left in flight)
+    if (emit_bad || nchars > chars_bound) EC_HIP(hipStreamSynchronize(s->ostream));  // (no copy left in flight)
     if (emit_bad) {
         set_error("contig characters past their bound %llu (inconsistent ranking)", (unsigned long long)chars_bound);
         return EC_ERR_STATE;
@@ -2887,7 +2915,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (pre && nchars > pre) EC_HIP(hipEventSynchronize(s->oev[1]));  // (before h_chars may move)
     EC_CHECK(s->h_chars.resize(nchars));
     if (nchars > pre) EC_CHECK(d2h(s, s->h_chars.data(), s->chars.p, nchars, st));
-    const uint64_t nlinks = s->h_loff[n2];
+    const uint64_t nlinks = nlinks64;
     EC_CHECK(s->h_links.resize(nlinks));
     if (nlinks) {
         EC_CHECK(s->dcounts.ensure(nlinks * 8));
@@ -2897,7 +2925,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(d2h(s, s->h_links.data(), s->dcounts.p, nlinks * 8, st));
     }
     EC_CHECK(host_sync(s, st));
-    if (pre) EC_HIP(hipEventSynchronize(s->oev[1]));
+    EC_HIP(hipStreamSynchronize(s->ostream));  // (offsets, characters, link offsets)
     s->last_nchars = nchars;
     s->stats.n_links = nlinks;
 
@@ -4209,23 +4237,12 @@ int ec_link_record_bytes(void) { return (int)sizeof(LinkRec); }
 // ---- junction-partitioned graph (junction.h) ------------------------------------------------
 // counting sort of n ids (bins 0..nbins-1) -> perm (midx2) and bin starts bstart[0..nbins]
 int bin_sort(ec_session *s, const unsigned int *bid, uint64_t n, unsigned int nbins, unsigned long long *bstart) {
-    hipStream_t st = s->stream;
-    const unsigned int chunk = cs_chunk(nbins), nch = (unsigned int)std::max<uint64_t>((n + chunk - 1) / chunk, 1);
-    const uint64_t cells = (uint64_t)nbins * nch;
-    EC_CHECK(s->mbid2.ensure(std::max<uint64_t>(2 * cells, 2) * 4));
     EC_CHECK(s->midx2.ensure(std::max<uint64_t>(n, 1) * 4));
-    unsigned int *hist = s->mbid2.as<unsigned int>(), *incl = hist + cells;
     if (!n) {
-        EC_HIP(hipMemsetAsync(bstart, 0, (nbins + 1ull) * 8, st));
+        EC_HIP(hipMemsetAsync(bstart, 0, (nbins + 1ull) * 8, s->stream));
         return EC_OK;
     }
-    k_cs_hist<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist, chunk);
-    EC_CHECK(scan_incl_u32(s, hist, incl, cells));
-    k_cs_scatter<<<nch, 1024, nbins * 4, st>>>(bid, n, nbins, nch, hist, incl, s->midx2.as<unsigned int>(), chunk);
-    k_cs_bounds<<<grid_for(nbins, 256), 256, 0, st>>>(hist, incl, nbins, nch, bstart);
-    EC_HIP(hipMemcpyAsync(bstart + nbins, &incl[cells - 1], 4, hipMemcpyDeviceToDevice, st));  // (low word)
-    EC_HIP(hipMemsetAsync(reinterpret_cast<unsigned int *>(bstart + nbins) + 1, 0, 4, st));
-    return EC_OK;
+    return cs_sort(s, bid, n, nbins, bstart, true);
 }
 
 template <typename K>

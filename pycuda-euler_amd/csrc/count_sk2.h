@@ -1326,10 +1326,14 @@ __global__ void __launch_bounds__(NT) k_skdedup(const uint4 *recs, const unsigne
     const uint64_t r0 = bbeg[b], r1 = bend[b];
     const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
     auto ld = [](uint32_t *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    // (the next round's record loaded before this round's probes: one load in flight per
+    // thread left the kernel waiting on HBM latency)
+    uint4 nxt = r1 > r0 ? recs[min(r0 + tid, r1 - 1)] : make_uint4(0u, 0u, 0u, 0u);
     for (uint64_t c0 = r0; c0 < r1; c0 += NT) {
         const uint64_t ri = c0 + tid;
         const bool valid = ri < r1;
-        const uint4 x = recs[valid ? ri : r0];
+        const uint4 x = nxt;
+        if (c0 + NT < r1) nxt = recs[min(ri + NT, r1 - 1)];
         // canonical content (k_skbucket3's record round)
         const unsigned int n = (x.z >> 28) + 1, L2 = 2 * (n + (unsigned int)k - 1);
         const uint32_t m1 = L2 >= 64 ? 0xFFFFFFFFu : (1u << ((L2 - 32) & 31)) - 1u;

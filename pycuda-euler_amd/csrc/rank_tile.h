@@ -386,9 +386,12 @@ __global__ void __launch_bounds__(256) k_srulers(const uint8_t *hasp, unsigned i
 }
 
 // each ruler walks its segment of super nodes, offsets in nodes (chain lengths summed)
+// (RJump::h carries the ruler's chain head NODE, not its ruler index: the Wyllie rounds copy it
+// from the head ruler, and k_finalize_s reads a path's key without two dependent gathers)
 __global__ void __launch_bounds__(256) k_walk_s(const SNodeRec *nrec, const unsigned int *rlist, unsigned int r0,
                                                 const unsigned int *nr, unsigned int smask, uint2 *rid,
-                                                unsigned int *nextR, RJump *rs, unsigned long long *nvisited) {
+                                                unsigned int *nextR, RJump *rs, unsigned long long *nvisited,
+                                                const SuperRec *srec) {
     const unsigned int r1 = *nr;
     unsigned long long seen = 0;
     for (uint64_t t = r0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < r1; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -420,7 +423,7 @@ __global__ void __launch_bounds__(256) k_walk_s(const SNodeRec *nrec, const unsi
         RJump r;
         r.a = NONE32;  // set from prevR by k_rjump_init
         r.s = 0;
-        r.h = i;
+        r.h = srec[rlist[i]].head;
         r.cm = rlist[i];
         r.cd = 0;
         r.len = j + wl;  // nodes of the segment
@@ -459,7 +462,7 @@ __global__ void __launch_bounds__(256) k_finalize_s(const SNodeRec *nrec, const 
         }
         const RJump r = rs[ro.x];
         if (r.a == NONE32) {  // path
-            const unsigned int pk = srec[rlist[r.h]].head, rk = r.s + ro.y;
+            const unsigned int pk = r.h, rk = r.s + ro.y;
             PKs[v] = pk;
             RKs[v] = rk;
             if (nrec[v].succ == NONE32) {  // tail chain: its ruler's window spans the path

@@ -390,47 +390,52 @@ __global__ void __launch_bounds__(256) k_agg_bucket_ids(In in, uint64_t n, int b
 }
 
 // Counting sort of record indices by bucket id (round 4; a rocPRIM radix sort of (id, index)
-// pairs took 4 x 55 us a call): per chunk of records an LDS histogram of the nbins ids, stored
-// bucket-major; one scan over (bucket, chunk); per chunk LDS cursors place the indices.  The
-// order inside a (bucket, chunk) cell is not deterministic -- the bucket tables do not depend on
-// it.  1024 threads a chunk (round 5: 256 left ~280 workgroups on 256 CUs for 4.6 M records).
-// The chunk grows with nbins (cs_chunk): the bucket-major cells are written and read back with
-// a stride of one cell per chunk, so nbins x chunks strided accesses -- 8193 buckets x 281
-// chunks of 16 K cost the owner merge 46 + 21 + 64 us for the histogram, scan and scatter.
+// pairs took 4 x 55 us a call).  Round 5: per chunk of CS_CHUNK records an LDS histogram whose
+// nonzero bins are added to job-wide bin totals (k_cs_hist), one exclusive scan of the nbins
+// totals (k_cs_starts: the bin starts and the scatter cursors), and per chunk the histogram
+// again, each nonzero bin's range reserved with one global atomic and the indices placed
+// through LDS cursors (k_cs_scatter).  Round 4 stored the per-chunk histograms bin-major and
+// scanned all nbins x chunks cells: 8193 bins x 281 chunks, written and read back at a stride
+// of one cell per chunk, cost the owner merge 46 + 21 + 64 us.  The order inside a bin is not
+// deterministic -- the bucket tables do not depend on it.  1024 threads a chunk (256 left ~280
+// workgroups on 256 CUs for 4.6 M records).
 constexpr unsigned int CS_CHUNK = 16384;
-inline unsigned int cs_chunk(unsigned int nbins) {
-    unsigned int c = CS_CHUNK;
-    while (c < 262144u && c < 8ull * nbins) c <<= 1;
-    return c;
-}
-__global__ void __launch_bounds__(1024) k_cs_hist(const unsigned int *bid, uint64_t n, unsigned int nbins, unsigned int nch,
-                                                 unsigned int *hist, unsigned int chunk) {
+__global__ void __launch_bounds__(1024) k_cs_hist(const unsigned int *bid, uint64_t n, unsigned int nbins,
+                                                 unsigned int *tot) {
     extern __shared__ unsigned int csh[];
     for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) csh[i] = 0;
     __syncthreads();
-    const uint64_t c = blockIdx.x, t0 = c * chunk, t1 = t0 + chunk < n ? t0 + chunk : n;
+    const uint64_t t0 = (uint64_t)blockIdx.x * CS_CHUNK, t1 = t0 + CS_CHUNK < n ? t0 + CS_CHUNK : n;
     for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) atomicAdd(&csh[bid[t]], 1u);
     __syncthreads();
-    for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) hist[(uint64_t)i * nch + c] = csh[i];
+    for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x)
+        if (csh[i]) atomicAdd(&tot[i], csh[i]);
+}
+// excl = exclusive scan of tot (scan_incl_u32 gives incl): bin starts (u64) and cursors
+// (end: bstart[nbins] = n as well)
+__global__ void __launch_bounds__(256) k_cs_starts(const unsigned int *tot, const unsigned int *incl, unsigned int nbins,
+                                                   unsigned long long *bstart, unsigned int *cur, bool end) {
+    if (end && blockIdx.x == 0 && threadIdx.x == 0) bstart[nbins] = incl[nbins - 1];
+    for (unsigned int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
+        const unsigned int e = incl[b] - tot[b];
+        bstart[b] = e;
+        cur[b] = e;
+    }
 }
 __global__ void __launch_bounds__(1024) k_cs_scatter(const unsigned int *bid, uint64_t n, unsigned int nbins,
-                                                    unsigned int nch, const unsigned int *hist,
-                                                    const unsigned int *incl, unsigned int *out, unsigned int chunk) {
+                                                    unsigned int *cur, unsigned int *out) {
     extern __shared__ unsigned int csh[];
-    const uint64_t c = blockIdx.x, t0 = c * chunk, t1 = t0 + chunk < n ? t0 + chunk : n;
+    for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) csh[i] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * CS_CHUNK, t1 = t0 + CS_CHUNK < n ? t0 + CS_CHUNK : n;
+    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) atomicAdd(&csh[bid[t]], 1u);
+    __syncthreads();
     for (unsigned int i = threadIdx.x; i < nbins; i += blockDim.x) {
-        const uint64_t q = (uint64_t)i * nch + c;
-        csh[i] = incl[q] - hist[q];
+        const unsigned int c = csh[i];
+        if (c) csh[i] = atomicAdd(&cur[i], c);  // this chunk's range of bin i
     }
     __syncthreads();
     for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) out[atomicAdd(&csh[bid[t]], 1u)] = (unsigned int)t;
-}
-__global__ void __launch_bounds__(256) k_cs_bounds(const unsigned int *hist, const unsigned int *incl, unsigned int nbins,
-                                                   unsigned int nch, unsigned long long *bstart) {
-    for (unsigned int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
-        const uint64_t q = (uint64_t)b * nch;
-        bstart[b] = incl[q] - hist[q];
-    }
 }
 
 // bstart[b] = first position of bucket b in the sorted ids (b = 0..nb; bstart[nb] = real records)
