@@ -844,12 +844,14 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
             uint2 *mev = s->skm_ev.as<uint2>();
             unsigned long long *mend = s->skm_end.as<unsigned long long>();
             const unsigned int claim_cap = kn().sk2_claim > 0 ? (unsigned int)kn().sk2_claim : ~0u;
-            if (kn().skf_merge == 2)
+            // (4096-entry tables, 1024 threads, one workgroup per CU: compact 2.87-2.92 ms on
+            // ecoli10m_err against 3.03-3.06 with 2560 entries and two workgroups per CU)
+            if (kn().skf_merge != 2)
                 k_skdedup<4096, 1024><<<(unsigned)Bk, 1024, 0, st>>>(s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, mrec,
-                                                                     mev, mend, claim_cap);
+                                                                     mev, mend, claim_cap, dbg);
             else
                 k_skdedup<2560, 512><<<(unsigned)Bk, 512, 0, st>>>(s->recs2.as<uint4>(), bbeg, bend, k, M, inv_m, mrec,
-                                                                   mev, mend, claim_cap);
+                                                                   mev, mend, claim_cap, dbg);
 #define EC_SKF_MERGED_ARGS                                                                                   \
     mrec, bbeg, mend, k, M, inv_m, limit, s->dkey.as<unsigned long long>(), s->dcnt.as<unsigned int>(),      \
         s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),                                    \
@@ -897,8 +899,10 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
         if (skfilt)
             fprintf(stderr, "k_skbucket_filt: %llu buckets: max distinct est %llu, max predicted inserts %llu, max "
                             "seen-twice cells %llu, max records %llu; refused by the predictor %llu, tables filled "
-                            "%llu, most keys inserted %llu; most merged records %llu, most rejected %llu\n",
-                    (unsigned long long)Bk, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
+                            "%llu, most keys inserted %llu; most merged records %llu, most past the claim cap %llu, "
+                            "merged records %llu of %llu\n",
+                    (unsigned long long)Bk, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9],
+                    (unsigned long long)NR);
         if (plan.slots == 1024)
             fprintf(stderr, "k_skbucket3: %llu buckets, most distinct records in a bucket %llu\n",
                     (unsigned long long)Bk, h[3]);

@@ -36,7 +36,7 @@ struct Knobs {
     int tile_plan = -1;         // EULERHIP_TILE_PLAN=0: fixed rank tiles, not cut at bucket starts (A/B)
     int no_spec = 0;            // EULERHIP_NO_SPEC=1: no speculative refine launch (count_sk2, A/B)
     bool merge_mix = false;     // EULERHIP_MERGE_MIX: key-hash buckets / owners instead of minimizers
-    int skf_merge = 1;          // EULERHIP_SKF_MERGE: error-rich records merged before the filter (0 off, 2 wide tables)
+    int skf_merge = 1;          // EULERHIP_SKF_MERGE: error-rich records merged before the filter (0 off, 2 2560-entry tables)
     bool merge_decode = false;  // EULERHIP_MERGE_DECODE: the owner merge reads a decoded copy of the received records
     bool wide_general = false;  // EULERHIP_WIDE_GENERAL: k > 32 on the HBM table
     int wide_max_bbits = -1;    // EULERHIP_WIDE_MAX_BBITS: cap the wide buckets (forces overflow)

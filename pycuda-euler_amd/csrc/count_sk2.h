@@ -1309,19 +1309,20 @@ template <int RS, int NT>
 __global__ void __launch_bounds__(NT) k_skdedup(const uint4 *recs, const unsigned long long *bbeg,
                                                 const unsigned long long *bend, int k, uint32_t M, double inv_m,
                                                 uint4 *mrec, uint2 *mev, unsigned long long *mend,
-                                                unsigned int claim_cap = ~0u) {
+                                                unsigned int claim_cap = ~0u, unsigned long long *dbg = nullptr) {
     constexpr uint32_t PEND = 0x800u;
     constexpr unsigned int CLAIM_MAX = RS - 1 - NT;  // (probes of the records in flight end)
     static_assert(RS > NT + 1, "record table too small for the records in flight");
     __shared__ uint32_t tag[RS], tx[RS], ty[RS], tz[RS], tm[RS], ta[RS], tb[RS];
-    __shared__ unsigned int s_nent, s_nout;
+    __shared__ unsigned int s_nent, s_nout, s_nrej, s_ncnt[SK2_NMAX];
     const unsigned int b = blockIdx.x, tid = threadIdx.x;
     for (int i = tid; i < RS; i += NT) {
         tag[i] = 0;
         tm[i] = 0;
         ta[i] = tb[i] = 0xFFFFFFFFu;
     }
-    if (tid == 0) s_nent = 0, s_nout = 0;
+    if (tid == 0) s_nent = 0, s_nout = 0, s_nrej = 0;
+    if (tid < (unsigned int)SK2_NMAX) s_ncnt[tid] = 0;
     __syncthreads();
     const uint64_t r0 = bbeg[b], r1 = bend[b];
     const unsigned int m2 = 2 * M - 1, M2 = 2 * M;
@@ -1392,20 +1393,55 @@ __global__ void __launch_bounds__(NT) k_skdedup(const uint4 *recs, const unsigne
             if (EB < tb[SL]) atomicMin(&tb[SL], EB);
         }
         if (ST == 2) {  // past the cap: written on its own
+            if (dbg) atomicAdd(&s_nrej, 1u);
             const uint64_t o = r0 + atomicAdd(&s_nout, 1u);
             mrec[o] = make_uint4(K0, K1, K2, 1u);
             mev[o] = make_uint2(EA, EB);
         }
     }
     __syncthreads();
-    for (unsigned int i = tid; i < (unsigned int)RS; i += NT) {
-        if (!tag[i]) continue;
-        const uint64_t o = r0 + atomicAdd(&s_nout, 1u);
+    // the distinct records out by window count, most windows first (after those past the cap):
+    // the filter rolls a record's windows out in one lane, so a wave of mixed counts ran at the
+    // pace of its longest record (~42 % of its lanes busy on ecoli10m_err)
+    constexpr int PER = (RS + NT - 1) / NT;
+    uint32_t bin[PER], rk[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const unsigned int i = tid + q * NT;
+        bin[q] = SK2_NMAX;
+        if (i < (unsigned int)RS && tag[i]) {
+            bin[q] = SK2_NMAX - 1 - (tz[i] >> 28);
+            rk[q] = atomicAdd(&s_ncnt[bin[q]], 1u);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned int a = s_nout;  // (the records past the cap come first)
+        for (int q = 0; q < SK2_NMAX; q++) {
+            const unsigned int v = s_ncnt[q];
+            s_ncnt[q] = a;
+            a += v;
+        }
+        s_nout = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        if (bin[q] == SK2_NMAX) continue;
+        const unsigned int i = tid + q * NT;
+        const uint64_t o = r0 + s_ncnt[bin[q]] + rk[q];
         mrec[o] = make_uint4(tx[i], ty[i], tz[i], tm[i]);
         mev[o] = make_uint2(ta[i], tb[i]);
     }
     __syncthreads();
-    if (tid == 0) mend[b] = r0 + s_nout;
+    if (tid == 0) {
+        mend[b] = r0 + s_nout;
+        if (dbg) {  // EULERHIP_SK2_STATS: most merged records / records past the cap a bucket, all merged
+            atomicMax(&dbg[7], (unsigned long long)s_nout);
+            atomicMax(&dbg[8], (unsigned long long)s_nrej);
+            atomicAdd(&dbg[9], (unsigned long long)s_nout);
+        }
+    }
 }
 
 }  // namespace ec

@@ -1,11 +1,11 @@
 #!/bin/bash
-# A/B of debug knobs on the headline bench: gpu_ab.sh TAG "name:ENV=v ENV2=v" ... (2 reps each,
-# interleaved); prints ms/step and the stages per variant
+# A/B of debug knobs on a bench config (CFG, default the headline): gpu_ab.sh TAG "name:ENV=v ENV2=v" ...
+# (2 reps each, interleaved); prints ms/step and the stages per variant
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 T=$1; shift
-B="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-input"
+B="bench.py --config ${CFG:-ecoli10m} --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --no-host-input"
 for rep in 1 2; do
   for v in "$@"; do
     name=${v%%:*}; envs=${v#*:}
