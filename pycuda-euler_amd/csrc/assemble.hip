@@ -181,6 +181,12 @@ struct ec_session {
     PinnedVec<uint64_t> h_coff;  // result readbacks land in pinned host memory
     PinnedVec<uint64_t> h_loff;
     PinnedVec<int64_t> h_links;
+    // the one-GPU results' links in transfer form (links_compact): per-side link counts as bytes
+    // and the links as u32 (2 contig + end < 2^32) -- ec_copy_links widens them (ecoli10m_err:
+    // 18 + 18 MB of u64 offsets and links after GFA cost ~0.65 ms of PCIe; now 2.2 + 9 MB)
+    PinnedVec<uint8_t> h_lc8;
+    PinnedVec<uint32_t> h_links32;
+    bool links_compact = false;
     bool want_dict = false;
     hipEvent_t ev[2 * EC_NSTAGES] = {};
     hipEvent_t kev[2 * EC_NKERNELS] = {};
@@ -192,7 +198,7 @@ struct ec_session {
     unsigned int n_dense = 0;  // dense k-mer arrays held by the session (shard / merge steps)
     bool stats_ok = false;     // ec_get_stats valid (any successful call)
     unsigned flags = 0;        // flags of the current call
-    DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur, cwalk;
+    DevBuf ocnt, rbc, mbid, mbid2, midx, midx2, gcur, cwalk, ewalk, lc8;
     bool no_index = false;      // the call needs dense records only (shard count, owner merge)
     uint64_t shard_base = 0;    // ec_count_shard: global id of the shard's read 0 (added at export)
     // the super-k-mer fast path's read length of the last call on (offsets, reads): reused
@@ -2834,10 +2840,14 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
     EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
     EC_HIP(hipMemsetAsync(&dsc->skew, 0, 4, st));  // k_emit: a position past the character bound
+    EC_CHECK(s->ewalk.ensure((size_t)std::max(nc, 1u) * sizeof(EWalk)));
+    if (nc)
+        k_ewalk<<<grid_for(nc, B), B, 0, st>>>(s->cwalk.as<Walk>(), s->coff.as<unsigned long long>(), nc,
+                                              s->ewalk.as<EWalk>());
     if (U)
         k_emit<Ops><<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
                                             s->PL.as<unsigned int>(), s->dkey.as<typename Ops::K>(),
-                                            s->cidxOf.as<unsigned int>(), s->cwalk.as<Walk>(), s->coff.as<unsigned long long>(),
+                                            s->cidxOf.as<unsigned int>(), s->ewalk.as<EWalk>(),
                                             N, k, s->chars.as<char>(), std::max<uint64_t>(chars_bound, 1),
                                             s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(),
                                             s->headOf.as<unsigned int>(), s->tailOf.as<unsigned int>(), &dsc->skew);
@@ -2887,18 +2897,21 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
 
     // ---- results to host (links compacted on the device: only the used entries travel) -----
     const unsigned int n2 = 2 * nc;
-    EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
-    s->h_loff[n2] = 0;
+    s->links_compact = true;
+    EC_CHECK(s->h_lc8.resize(n2));
     if (!nc) s->h_coff[0] = 0;
     unsigned long long nlinks64 = 0;
     if (nc) {
         EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));   // per-side counts as u64 (starts sorted)
         EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));  // their exclusive scan = link offsets
-        k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>());
-        EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
+        // (the counts as bytes in a buffer of their own: the scan's temporary storage is s->tmp)
+        EC_CHECK(s->lc8.ensure(n2));
+        k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>(),
+                                                       s->lc8.as<uint8_t>());
         EC_HIP(hipEventRecord(s->oev[3], st));
         EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[3], 0));
-        EC_HIP(hipMemcpyAsync(s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, hipMemcpyDeviceToHost, s->ostream));
+        EC_HIP(hipMemcpyAsync(s->h_lc8.data(), s->lc8.p, n2, hipMemcpyDeviceToHost, s->ostream));
+        EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
         EC_CHECK(d2h(s, &nlinks64, s->skeys2.as<unsigned long long>() + n2, 8, st));
     }
     unsigned int emit_bad = 0;
@@ -2920,13 +2933,13 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->h_chars.resize(nchars));
     if (nchars > pre) EC_CHECK(d2h(s, s->h_chars.data(), s->chars.p, nchars, st));
     const uint64_t nlinks = nlinks64;
-    EC_CHECK(s->h_links.resize(nlinks));
+    EC_CHECK(s->h_links32.resize(nlinks));
     if (nlinks) {
-        EC_CHECK(s->dcounts.ensure(nlinks * 8));
-        k_links_compact<<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
-                                                      s->skeys2.as<unsigned long long>(), n2,
-                                                      s->dcounts.as<long long>());
-        EC_CHECK(d2h(s, s->h_links.data(), s->dcounts.p, nlinks * 8, st));
+        EC_CHECK(s->dcounts.ensure(nlinks * 4));
+        k_links_compact<uint32_t><<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
+                                                                s->skeys2.as<unsigned long long>(), n2,
+                                                                s->dcounts.as<uint32_t>());
+        EC_CHECK(d2h(s, s->h_links32.data(), s->dcounts.p, nlinks * 4, st));
     }
     EC_CHECK(host_sync(s, st));
     EC_HIP(hipStreamSynchronize(s->ostream));  // (offsets, characters, link offsets)
@@ -3155,11 +3168,15 @@ int part_emit(ec_session *s, char *d_chars, void *d_ends) {
     EC_HIP(hipMemsetAsync(s->cfirst.p, 0xFF, nn * 4, st));
     EC_HIP(hipMemsetAsync(s->clast.p, 0xFF, nn * 4, st));
     EC_HIP(hipMemsetAsync(&dsc->skew, 0, 4, st));
+    EC_CHECK(s->ewalk.ensure(nn * sizeof(EWalk)));
+    if (nc)
+        k_ewalk<<<grid_for(nc, B), B, 0, st>>>(s->cwalk.as<Walk>(), s->coff.as<unsigned long long>(), nc,
+                                              s->ewalk.as<EWalk>());
     if (n1 > n0 && nc)
         k_emit<Ops><<<grid_for(n1 - n0, B), B, 0, st>>>(
             s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
-            s->dkey.as<typename Ops::K>(), s->cidxOf.as<unsigned int>(), s->cwalk.as<Walk>(),
-            s->coff.as<unsigned long long>(), n1, s->k, d_chars, std::max<uint64_t>(s->seg_nchars, 1),
+            s->dkey.as<typename Ops::K>(), s->cidxOf.as<unsigned int>(), s->ewalk.as<EWalk>(),
+            n1, s->k, d_chars, std::max<uint64_t>(s->seg_nchars, 1),
             s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
             s->tailOf.as<unsigned int>(), &dsc->skew, n0);
     // contig ends as k-mer codes (the collecting rank holds no global set): 2 nc codes, each
@@ -3202,6 +3219,7 @@ int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint6
                                                         s->lcnt.as<unsigned int>());
     }
     const unsigned int n2 = 2 * nc;
+    s->links_compact = false;
     EC_CHECK(s->h_coff.resize((size_t)nc + 1));
     EC_CHECK(s->h_loff.resize((size_t)n2 + 1));
     s->h_loff[n2] = 0;
@@ -3220,8 +3238,9 @@ int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint6
     EC_CHECK(s->h_links.resize(nlinks));
     if (nlinks) {
         EC_CHECK(s->dcounts.ensure(nlinks * 8));
-        k_links_compact<<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
-                                                      s->skeys2.as<unsigned long long>(), n2, s->dcounts.as<long long>());
+        k_links_compact<long long><<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
+                                                                 s->skeys2.as<unsigned long long>(), n2,
+                                                                 s->dcounts.as<long long>());
         EC_CHECK(d2h(s, s->h_links.data(), s->dcounts.p, nlinks * 8, st));
     }
     EC_CHECK(host_sync(s, st));
@@ -3572,7 +3591,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
                      &s->rid, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
                      &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->bnp, &s->rbc,
-                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->x_par, &s->x_irr,
+                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->ewalk, &s->lc8, &s->x_par, &s->x_irr,
                      &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
                      &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
@@ -3586,6 +3605,8 @@ int ec_session_destroy(ec_session *s) {
     s->h_coff.release();
     s->h_loff.release();
     s->h_links.release();
+    s->h_lc8.release();
+    s->h_links32.release();
     if (s->events) {
         for (auto &e : s->ev) hipEventDestroy(e);
         for (auto &e : s->kev) hipEventDestroy(e);
@@ -3760,6 +3781,20 @@ int ec_copy_links(ec_session *s, uint64_t *link_offsets, int64_t *links) {
     if (!s->have) {
         set_error("no successful assembly in this session");
         return EC_ERR_STATE;
+    }
+    if (s->links_compact) {  // (phase_graph's transfer form: widened here)
+        if (link_offsets) {
+            uint64_t o = 0;
+            const size_t n2 = s->h_lc8.size();
+            for (size_t i = 0; i < n2; i++) {
+                link_offsets[i] = o;
+                o += s->h_lc8[i];
+            }
+            link_offsets[n2] = o;
+        }
+        if (links)
+            for (size_t i = 0; i < s->h_links32.size(); i++) links[i] = (int64_t)s->h_links32[i];
+        return EC_OK;
     }
     if (link_offsets) memcpy(link_offsets, s->h_loff.data(), s->h_loff.size() * 8);
     if (links && !s->h_links.empty()) memcpy(links, s->h_links.data(), s->h_links.size() * 8);

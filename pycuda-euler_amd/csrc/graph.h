@@ -757,13 +757,30 @@ __global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const u
     }
 }
 
+// a contig's walk geometry with its character offset: k_emit's one gather per node (the walk
+// and the offset as two gathers cost ecoli10m_err's 26.8 M nodes a dependent random read each)
+struct EWalk {
+    Walk w;
+    unsigned long long coff;
+};
+static_assert(sizeof(EWalk) == 32, "EWalk layout");
+__global__ void __launch_bounds__(256) k_ewalk(const Walk *cwalk, const unsigned long long *coff, unsigned int nc,
+                                               EWalk *ew) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
+        EWalk e;
+        e.w = cwalk[i];
+        e.coff = coff[i];
+        ew[i] = e;
+    }
+}
+
 // emit: every node finds its contig through its path key, computes its walk position and
 // writes its chars (contig_to_string:44-45: first node k chars, later nodes their last base).
 template <typename Ops>
 __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
                                               const unsigned int *PL, const typename Ops::K *dkey,
-                                              const unsigned int *cidxOf, const Walk *cwalk,
-                                              const unsigned long long *coff, unsigned int N, int k, char *chars,
+                                              const unsigned int *cidxOf, const EWalk *ew,
+                                              unsigned int N, int k, char *chars,
                                               unsigned long long chars_bound, unsigned int *cfirst,
                                               unsigned int *clast, unsigned int *headOf, unsigned int *tailOf,
                                               unsigned int *bad, unsigned int n0 = 0) {
@@ -773,7 +790,8 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
         const unsigned int pk = PK[x], rk = RK[x];
         const unsigned int ci = cidxOf[pk & ~CYC];
         if (ci == NONE32) continue;  // the twin path of a disjoint pair carries the contig
-        const Walk w = cwalk[ci];
+        const EWalk e = ew[ci];
+        const Walk &w = e.w;
         long long pos = -1;
         if (w.kind == 0) {
             pos = rk;
@@ -792,12 +810,12 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
         if (pos < 0) continue;
         // the buffer holds the bound 2U + nc (k - 1) the host sized it for: a position past it
         // (never, for a consistent ranking) is reported instead of written
-        if (coff[ci] + (unsigned long long)(k - 1) + (unsigned long long)pos >= chars_bound) {
+        if (e.coff + (unsigned long long)(k - 1) + (unsigned long long)pos >= chars_bound) {
             atomicOr(bad, 1u);
             continue;
         }
         const typename Ops::K code = node_code<Ops>(dkey, x, k);
-        char *dst = chars + coff[ci];
+        char *dst = chars + e.coff;
         if (pos == 0) {
             for (int i = 0; i < k; i++) dst[i] = Ops::chr(Ops::base(code, k, i));
             cfirst[ci] = x;
@@ -847,16 +865,21 @@ __global__ void __launch_bounds__(256) k_gfa(Index idx, const typename Ops::K *d
 }
 
 // GFA links to a dense array: loff = exclusive scan of the per-side counts (u64, 2nc + 1)
-__global__ void __launch_bounds__(256) k_lcnt64(const unsigned int *lcnt, unsigned int n2, unsigned long long *out) {
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t <= n2; t += (uint64_t)gridDim.x * blockDim.x)
-        out[t] = t < n2 ? lcnt[t] : 0ull;
+// (c8: the counts as bytes as well, <= 8 a side -- what travels to host memory)
+__global__ void __launch_bounds__(256) k_lcnt64(const unsigned int *lcnt, unsigned int n2, unsigned long long *out,
+                                                uint8_t *c8 = nullptr) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t <= n2; t += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int c = t < n2 ? lcnt[t] : 0u;
+        out[t] = c;
+        if (c8 && t < n2) c8[t] = (uint8_t)c;
+    }
 }
+template <typename T>
 __global__ void __launch_bounds__(256) k_links_compact(const long long *lk, const unsigned int *lcnt,
-                                                       const unsigned long long *loff, unsigned int n2,
-                                                       long long *out) {
+                                                       const unsigned long long *loff, unsigned int n2, T *out) {
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n2; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int c = lcnt[t];
-        for (unsigned int j = 0; j < c; j++) out[loff[t] + j] = lk[t * 8 + j];
+        for (unsigned int j = 0; j < c; j++) out[loff[t] + j] = (T)lk[t * 8 + j];
     }
 }
 

@@ -23,6 +23,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
 
 
+def pytest_assertrepr_compare(config, op, left, right):
+    """A failed == on large results (contig strings, link lists, dicts of 10^5+ entries) is
+    reported by its first difference: pytest's own diff runs difflib over them for minutes,
+    and a GPU run that prints nothing that long is taken for a hang."""
+    sized = (list, tuple, bytes, str, dict)
+    if op != "==" or not isinstance(left, sized) or not isinstance(right, sized):
+        return None
+    if max(len(left), len(right)) <= 200:
+        return None
+    a = list(left.items()) if isinstance(left, dict) else left
+    b = list(right.items()) if isinstance(right, dict) else right
+    i = next((j for j, (x, y) in enumerate(zip(a, b)) if x != y), min(len(a), len(b)))
+    show = lambda v: repr(v[i:i + 3])[:200]
+    return ["%s of %d == %s of %d fails" % (type(left).__name__, len(left), type(right).__name__, len(right)),
+            "first difference at index %d: %s != %s" % (i, show(a), show(b))]
+
+
 def load_golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)
