@@ -1833,7 +1833,14 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
             default: set_error("minimizer buckets: k = %d out of range", k); return EC_ERR_ARG;
         }
     }
-    if (mb)
+    // minimizer runs as the partition records (count_wide.h RunWM; EULERHIP_WIDE_RUNS=0: windows)
+    const bool runs = mb && kn().wide_runs != 0;
+    if (runs)
+        k_upsweep_w<true, true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
+                                                                         s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
+                                                                         &dsc->npos, &dsc->maxlocal, &dsc->skew,
+                                                                         dsc->lens, wbv, mbM);
+    else if (mb)
         k_upsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
                                                                    s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
                                                                    &dsc->npos, &dsc->maxlocal, &dsc->skew, dsc->lens,
@@ -1899,10 +1906,13 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
     EC_CHECK(s->tot.ensure((Bk + 1) * 8));
     EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
+    // (runs: P windows bound the run records; their count comes back with the bucket pass's
+    // scalars.  Both buffers take P window records: the runs are expanded into the other one)
+    const size_t rbytes = runs ? sizeof(RunWM) : sizeof(RecW);
     EC_CHECK(s->recs.ensure(std::max<uint64_t>(P, 1) * sizeof(RecW)));
     const bool second = bbits > cbits;
-    if (second) EC_CHECK(s->recs2.ensure(P * sizeof(RecW)));
-    s->stats.record_bytes = (uint32_t)sizeof(RecW);
+    if (second || runs) EC_CHECK(s->recs2.ensure(std::max<uint64_t>(P, 1) * sizeof(RecW)));
+    s->stats.record_bytes = (uint32_t)rbytes;
     s->stats.n_records = P;
     k_coarse<FINE_W_BITS><<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
                                                                         s->cnt.as<unsigned long long>());
@@ -1910,7 +1920,11 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     k_bucket_totals<FINE_W_BITS><<<grid_for(Bk + 1, B), B, 0, st>>>(ftot, bbits, s->tot.as<unsigned long long>());
     EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->bstart.as<unsigned long long>(), Bk + 1));
     kmark(s, 1, 0);
-    if (mb)
+    if (runs)
+        k_downsweep_wr<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_off, nreads, k, gsize, ngroups, cbits,
+                                                                s->offs.as<unsigned long long>(), s->recs.as<RunWM>(),
+                                                                wbv, mbM);
+    else if (mb)
         k_downsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize, ngroups, cbits,
                                                                      s->offs.as<unsigned long long>(),
                                                                      s->recs.as<RecW>(), read_base, wbv, mbM);
@@ -1924,7 +1938,11 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         EC_CHECK(s->gcur.ensure(Bk * 8));
         EC_HIP(hipMemcpyAsync(s->gcur.p, s->bstart.p, Bk * 8, hipMemcpyDeviceToDevice, st));
         kmark(s, 4, 0);
-        if (mb)
+        if (runs)
+            k_refine<RunWM, StoreRM, StoreRM><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
+                StoreRM{s->recs.as<RunWM>()}, StoreRM{s->recs2.as<RunWM>()}, s->bstart.as<unsigned long long>(),
+                s->gcur.as<unsigned long long>(), cbits, bbits);
+        else if (mb)
             k_refine<RecWM, StoreWM, StoreWM><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
                 StoreWM{s->recs.as<RecWM>()}, StoreWM{s->recs2.as<RecWM>()}, s->bstart.as<unsigned long long>(),
                 s->gcur.as<unsigned long long>(), cbits, bbits);
@@ -1932,7 +1950,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
             k_refine<RecW, StoreW, StoreW><<<dim3((unsigned)Ck, RS), BUCKET_THREADS, 0, st>>>(
                 StoreW{s->recs.as<RecW>()}, StoreW{s->recs2.as<RecW>()}, s->bstart.as<unsigned long long>(),
                 s->gcur.as<unsigned long long>(), cbits, bbits);
-        if (sbits) {  // fine buckets (recs2) -> their sub-buckets (recs), exact (k_split3)
+        if (sbits && !runs) {  // fine buckets (recs2) -> their sub-buckets (recs), exact (k_split3)
             EC_CHECK(s->bb2.ensure((Bt + 1) * 8));
             const unsigned long long cap3 = kn().wide_l3_cap > 0 ? (unsigned long long)kn().wide_l3_cap : 0ull;
             if (mb)
@@ -1944,6 +1962,31 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
                                                              bbits, sbits, s->recs.as<RecW>(),
                                                              s->bb2.as<unsigned long long>(), cap3, &dsc->overflow);
         }
+        kmark(s, 4, 1);
+    }
+    RecWM *rwin = nullptr;  // runs: the window records of the expansion, bucket bounds in bb2
+    if (runs) {
+        // each fine bucket's runs -> its windows' records, split into its sub-buckets on the way
+        const RunWM *rin = second ? s->recs2.as<RunWM>() : s->recs.as<RunWM>();
+        rwin = second ? s->recs.as<RecWM>() : s->recs2.as<RecWM>();
+        EC_CHECK(s->bb2.ensure((Bt + 1) * 8));
+        EC_CHECK(s->tot.ensure((Bk + 1) * 8));
+        EC_CHECK(s->gcur.ensure((Bk + 1) * 8));
+        kmark(s, 4, 0);
+        k_run_wsum<<<(unsigned)(Bk + 1), 256, 0, st>>>(rin, s->bstart.as<unsigned long long>(),
+                                                      s->tot.as<unsigned long long>(), Bk);
+        EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->gcur.as<unsigned long long>(), Bk + 1));
+        // (dynamic LDS only to bound the workgroups a CU holds: each lane writes its own stream of
+        // window records, and past ~2 MB of open lines per XCD the L2 evicts them half written --
+        // EULERHIP_WRUN_LDS: bytes, A/B)
+        const unsigned wlds = kn().wrun_lds >= 0 ? (unsigned)kn().wrun_lds : 0u;
+        k_split3_runs<<<(unsigned)Bk, 512, wlds, st>>>(rin, s->bstart.as<unsigned long long>(), bbits, sbits,
+                                                    s->gcur.as<unsigned long long>(), rwin,
+                                                    s->bb2.as<unsigned long long>(),
+                                                    RunReads{d_reads, d_off, k, mbM, read_base},
+                                                    sbits && kn().wide_l3_cap > 0 ? (unsigned long long)kn().wide_l3_cap
+                                                                                  : 0ull,
+                                                    &dsc->overflow);
         kmark(s, 4, 1);
     }
     mark(s, 2 * EC_STAGE_COUNT + 1);
@@ -1968,7 +2011,11 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         SRC, BEG, END, limit, s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),    \
         s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
         &dsc->ndistinct, &dsc->overflow, bm)
-    if (sbits && mb)
+    if (sbits && runs)
+        EC_BUCKET_W(1664, RecWM, rwin, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1);
+    else if (runs)
+        EC_BUCKET_W(SLOTS_W, RecWM, rwin, s->bb2.as<unsigned long long>(), nullptr);
+    else if (sbits && mb)
         EC_BUCKET_W(1664, RecWM, s->recs.as<RecWM>(), s->bb2.as<unsigned long long>(),
                     s->bb2.as<unsigned long long>() + 1);
     else if (sbits)
@@ -1983,8 +2030,11 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
 #undef EC_BUCKET_W
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
+    unsigned long long nruns = 0;
+    if (runs) EC_CHECK(d2h(s, &nruns, s->bstart.as<unsigned long long>() + Bk, 8, st));
     EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
     EC_CHECK(host_sync(s, st));
+    if (runs) s->stats.n_records = nruns;
     if (hsc.overflow) {  // a bucket outgrew its LDS table: the caller counts on the HBM table
         if (kn().verbose)
             fprintf(stderr, "count_wpart: %u tables overflowed (%llu tables of %u slots, sbits %d, mb %d)\n",

@@ -7,6 +7,7 @@
 // 256-read tiles fit the 40 KB stage (reads up to ~160 bp); other inputs keep the HBM-table
 // path of wide.h.
 #pragma once
+#include <type_traits>
 #include "count_part.h"
 #include "graph.h"
 #include "superkmer.h"
@@ -139,6 +140,29 @@ struct StoreW {
     __device__ inline void store(uint64_t i, const RecW &r) const { p[i] = r; }
 };
 
+// ---- minimizer runs (round 5): one 16-B record per run of windows sharing a minimizer -------
+// On minimizer buckets all windows of a read's run of one minimizer go to the same bucket, so
+// the partition passes can carry the RUN {read, first window, windows, placement bits} instead
+// of its windows' 24-B records: config 5's 1.25e9 windows are ~6.6e7 runs (~19 windows each),
+// so the downsweep writes and the refine / third level move ~1 GB instead of 30 GB.  The bucket
+// pass gathers a run's bases from the reads (still in HBM) and rolls its windows out itself.
+struct alignas(16) RunWM {
+    unsigned int read;   // read index of the call (0-based; + read_base in the events)
+    unsigned int wn;     // first window | windows << 16
+    unsigned int place;  // placement bits 32..55 (the minimizer's top 24 bits, as RecWM)
+    unsigned int pad;
+};
+static_assert(sizeof(RunWM) == 16, "run record layout");
+__device__ inline unsigned int rec_bucket(const RunWM &r, int bbits) {
+    return bbits ? (r.place << 8) >> (32 - bbits) : 0u;
+}
+struct StoreRM {
+    RunWM *p;
+    __device__ inline RunWM load(uint64_t i) const { return p[i]; }
+    __device__ inline void store(uint64_t i, const RunWM &r) const { p[i] = r; }
+};
+constexpr uint32_t RUN_MAXW = 255;  // windows a run record holds at most
+
 __device__ inline bool stage_tile_w(const uint8_t *buf, const uint64_t *off, uint64_t r0, uint64_t r1, uint8_t *stage,
                                     uint64_t &base) {
     const uint64_t b0 = off[r0], b1 = off[r1];
@@ -163,12 +187,15 @@ __device__ inline void roll_w(K128 &fwd, K128 &rc, uint32_t b, const K128 &mask,
 // ---- upsweep: fine histogram (16384 bins by mix128) + HyperLogLog, per read group ----------
 // lens[2] is set when a read has an 'N' / another byte, or a tile does not fit the stage:
 // the host then counts on the HBM table instead.
-template <bool MB>
+// RUNS (minimizer runs, MB only): the histogram counts run records -- a window opens one
+// where its minimizer differs from the previous window's, or the open run holds RUN_MAXW
+template <bool MB, bool RUNS = false>
 __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, const uint64_t *off, uint64_t nreads,
                                                           int k, uint64_t gsize, unsigned int *hist,
                                                           uint8_t *hll_blocks, unsigned long long *npos,
                                                           unsigned int *maxlocal, unsigned int *skew,
                                                           unsigned int *lens, const uint32_t *wbv, uint32_t mbM) {
+    static_assert(MB || !RUNS, "runs need minimizer buckets");
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
     __shared__ unsigned int h_cnt[FINE_W / 2];
     __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
@@ -178,7 +205,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
     const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
     const K128 mask = kmask128(k);
     const int sh = 2 * (k - 1);
-    unsigned long long mypos = 0;
+    unsigned long long mypos = 0, myrec = 0;
     unsigned int mymax = 0, mynonclean = 0;
     for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
         const uint64_t r1 = min(r0 + TILE_READS, g1);
@@ -205,6 +232,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
         mymax = max(mymax, 2 * m - 1);
         K128 fwd{0, 0}, rc{0, 0};
         uint32_t c4 = 0;
+        uint32_t runv = 0, runl = 0;  // RUNS: the open run's minimizer and windows
         for (uint32_t t = 0; t < (uint32_t)len; t++) {
             if ((t & 3) == 0) c4 = rv.chunk(t >> 2);
             roll_w(fwd, rc, code2(c4 >> (8 * (t & 3))), mask, sh);
@@ -213,16 +241,26 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
             const uint32_t hh = (uint32_t)(mix128(c) >> 32);  // as k_upsweep
             const uint32_t j = hh >> (32 - HLL_REG_BITS);
             const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
-            const uint32_t f = (MB ? wbv[wbv_at(r, t + 1 - (uint32_t)k, mbM)] : hh) >> (32 - FINE_W_BITS);
-            atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
+            const uint32_t pv = MB ? wbv[wbv_at(r, t + 1 - (uint32_t)k, mbM)] : hh;
+            const uint32_t f = pv >> (32 - FINE_W_BITS);
+            bool open = true;
+            if (RUNS) {
+                open = t + 1 == (uint32_t)k || pv != runv || runl == RUN_MAXW;
+                runl = open ? 1u : runl + 1;
+                runv = pv;
+                myrec += open;
+            }
+            if (open) atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
             if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
         }
     }
     unsigned long long binsum = 0;  // bin-sum overflow check of k_upsweep
     __syncthreads();
     for (int i = threadIdx.x; i < FINE_W / 2; i += blockDim.x) binsum += (h_cnt[i] & 0xFFFFu) + (h_cnt[i] >> 16);
+    if (!RUNS) myrec = mypos;
     for (int o = 32; o > 0; o >>= 1) {
         mypos += __shfl_down(mypos, o);
+        myrec += __shfl_down(myrec, o);
         binsum += __shfl_down(binsum, o);
         mymax = max(mymax, (unsigned int)__shfl_down(mymax, o));
         mynonclean |= (unsigned int)__shfl_down(mynonclean, o);
@@ -231,7 +269,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
     if (threadIdx.x == 0) s_diff = 0;
     __syncthreads();
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&s_diff, mypos - binsum);
+        atomicAdd(&s_diff, myrec - binsum);
         if (mypos) atomicAdd(npos, mypos);
         if (mymax) atomicMax(maxlocal, mymax);
         if (mynonclean) atomicOr(&lens[2], 1u);
@@ -365,6 +403,125 @@ __global__ void __launch_bounds__(TILE_READS) k_downsweep_w(const uint8_t *buf, 
     }
 }
 
+// ---- downsweep of minimizer runs (RUNS): a lane's read closes a run where its minimizer
+// changes (or the run holds RUN_MAXW windows) and at its last window; the runs go to their
+// (coarse bucket, group) ranges through the same LDS counting sort as k_downsweep_w.  No read
+// bytes are staged: a run needs only the window minimizers (k_wbv).
+__global__ void __launch_bounds__(TILE_READS) k_downsweep_wr(const uint64_t *off, uint64_t nreads, int k,
+                                                             uint64_t gsize, uint64_t ngroups, int cbits,
+                                                             const unsigned long long *offs, RunWM *recs,
+                                                             const uint32_t *wbv, uint32_t mbM) {
+    constexpr int RW = DS_RW;
+    constexpr int E = RW + 1;  // emissions a lane can make in a round (the last run closes extra)
+    __shared__ RunWM sorted[TILE_READS * E];
+    __shared__ uint8_t sbk[TILE_READS * E];
+    __shared__ unsigned int bcnt[1 << DS_MAX_CBITS], bbeg[1 << DS_MAX_CBITS];
+    __shared__ unsigned long long cur[1 << DS_MAX_CBITS], gbase[1 << DS_MAX_CBITS];
+    __shared__ unsigned int s_rounds, s_total, s_wave[TILE_READS / 64];
+    const uint64_t g = blockIdx.x;
+    const int C = 1 << cbits;
+    const unsigned int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
+    for (uint64_t r0 = g0; r0 < g1; r0 += TILE_READS) {
+        const uint64_t r1 = min(r0 + TILE_READS, g1);
+        __syncthreads();
+        for (int c = tid; c < C; c += TILE_READS) {
+            if (r0 == g0) cur[c] = offs[(uint64_t)c * ngroups + g];
+            bcnt[c] = 0;
+        }
+        if (tid == 0) s_rounds = 0;
+        __syncthreads();
+        const uint64_t r = r0 + tid;
+        uint32_t m = 0;
+        if (r < r1) {
+            const uint64_t len = off[r + 1] - off[r];
+            m = len >= (uint64_t)k ? (uint32_t)(len - k + 1) : 0u;
+        }
+        if (m) atomicMax(&s_rounds, (m + RW - 1) / RW);
+        __syncthreads();
+        const unsigned int nrounds = s_rounds;
+        uint32_t w = 0, rs = 0, runv = 0;
+        bool closed = m == 0;
+        uint32_t pvn[RW];  // the next round's minimizers, loaded a round ahead
+#pragma unroll
+        for (int j = 0; j < RW; j++) pvn[j] = (uint32_t)j < m ? wbv[wbv_at(r, j, mbM)] : 0u;
+        for (unsigned int round = 0; round < nrounds; round++) {
+            RunWM rr[E];
+            unsigned int cb[E], rk[E];
+            uint32_t pvc[RW];
+#pragma unroll
+            for (int j = 0; j < RW; j++) {
+                pvc[j] = pvn[j];
+                const uint32_t wn = w + RW + j;
+                pvn[j] = wn < m ? wbv[wbv_at(r, wn, mbM)] : 0u;
+            }
+            auto emit = [&](int j, uint32_t end) {  // the run [rs, end) of minimizer runv
+                rr[j].read = (unsigned int)r;
+                rr[j].wn = rs | ((end - rs) << 16);
+                rr[j].place = runv >> 8;
+                rr[j].pad = 0;
+                cb[j] = cbits ? (runv >> (32 - cbits)) : 0u;
+                rk[j] = atomicAdd(&bcnt[cb[j]], 1u);
+            };
+#pragma unroll
+            for (int j = 0; j < E; j++) cb[j] = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < RW; j++) {
+                if (w < m) {
+                    const uint32_t pv = pvc[j];
+                    if (w == 0) {
+                        rs = 0;
+                        runv = pv;
+                    } else if (pv != runv || w - rs == RUN_MAXW) {
+                        emit(j, w);
+                        rs = w;
+                        runv = pv;
+                    }
+                    w++;
+                }
+            }
+            if (!closed && w == m) {
+                emit(RW, m);
+                closed = true;
+            }
+            __syncthreads();
+            const unsigned int v = (int)tid < C ? bcnt[tid] : 0u;
+            unsigned int incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int u = __shfl_up(incl, o);
+                if ((int)lane >= o) incl += u;
+            }
+            if (lane == 63) s_wave[wid] = incl;
+            __syncthreads();
+            unsigned int before = 0;
+            for (unsigned int q = 0; q < wid; q++) before += s_wave[q];
+            if ((int)tid < C) {
+                bbeg[tid] = before + incl - v;
+                gbase[tid] = cur[tid];
+                cur[tid] += v;
+            }
+            if (tid == TILE_READS - 1) s_total = before + incl;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < E; j++) {
+                if (cb[j] != 0xFFFFFFFFu) {
+                    const unsigned int p = bbeg[cb[j]] + rk[j];
+                    sorted[p] = rr[j];
+                    sbk[p] = (uint8_t)cb[j];
+                }
+            }
+            __syncthreads();
+            const unsigned int total = s_total;
+            for (unsigned int i = tid; i < total; i += TILE_READS) {
+                const unsigned int c = sbk[i];
+                recs[gbase[c] + (i - bbeg[c])] = sorted[i];
+            }
+            if ((int)tid < C) bcnt[tid] = 0;
+            __syncthreads();
+        }
+    }
+}
+
 // ---- third level, exact (round 4): fine bucket b's records split into its 2^sbits sub-buckets
 // by two passes in one workgroup (LDS counts, then LDS cursors), written back to back from
 // bstart[b]: b3[b 2^sbits + j] = first record of sub-bucket j.  The fixed-capacity regions of
@@ -398,6 +555,107 @@ __global__ void __launch_bounds__(512) k_split3(const R *in, const unsigned long
         const R r = in[i];
         const unsigned int p = atomicAdd(&cur[rec_bucket(r, bbits + sbits) & (F - 1)], 1u);
         out[r0 + p] = r;
+    }
+}
+
+// ---- minimizer runs back to window records (RUNS): after the refine, each fine bucket's runs
+// are expanded into its windows' RecWM records -- split into the bucket's 2^sbits sub-buckets on
+// the way (the third level; sbits = 0: one) -- so the bucket pass reads window records as before.
+// Expanding inside the LDS-table kernel instead (one workgroup per table, a run's bases gathered
+// as it rolls) took config 5's bucket pass from 16 to 70 ms: too few waves to hide the gathers.
+struct RunReads {
+    const uint8_t *buf;
+    const uint64_t *off;
+    int k;
+    uint32_t m;          // windows per read (minimizer buckets: one read length)
+    uint64_t read_base;  // global id of read 0
+};
+// windows per fine bucket (the expansion's output bases after a scan)
+__global__ void __launch_bounds__(256) k_run_wsum(const RunWM *runs, const unsigned long long *bstart,
+                                                  unsigned long long *wsum, uint64_t nb) {
+    const uint64_t b = blockIdx.x;
+    if (b >= nb) {  // (the scan's last element)
+        if (threadIdx.x == 0) wsum[b] = 0;
+        return;
+    }
+    unsigned long long w = 0;
+    for (uint64_t i = bstart[b] + threadIdx.x; i < bstart[b + 1]; i += blockDim.x) w += runs[i].wn >> 16;
+    for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o);
+    __shared__ unsigned long long s[4];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) wsum[b] = s[0] + s[1] + s[2] + s[3];
+}
+// fine bucket b's runs [bstart[b], bstart[b + 1]) -> the window records of its sub-buckets at
+// wstart[b] ..; b3[b 2^sbits + j] = first window record of sub-bucket j
+__global__ void __launch_bounds__(512) k_split3_runs(const RunWM *runs, const unsigned long long *bstart, int bbits,
+                                                     int sbits, const unsigned long long *wstart, RecWM *out,
+                                                     unsigned long long *b3, RunReads rr, unsigned long long cap,
+                                                     unsigned int *over) {
+    __shared__ unsigned int cnt[64], cur[64];
+    const unsigned int b = blockIdx.x, F = 1u << sbits, tid = threadIdx.x;
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    if (tid < 64) cnt[tid] = 0;
+    __syncthreads();
+    for (uint64_t i = r0 + tid; i < r1; i += 512) {
+        const RunWM x = runs[i];
+        atomicAdd(&cnt[rec_bucket(x, bbits + sbits) & (F - 1)], x.wn >> 16);
+    }
+    __syncthreads();
+    const uint64_t w0 = wstart[b];
+    if (tid == 0) {
+        unsigned int run = 0;
+        for (unsigned int j = 0; j < F; j++) {
+            cur[j] = run;
+            b3[(uint64_t)b * F + j] = w0 + run;
+            if (cap && cnt[j] > cap) *over = 1u;  // (tests: as k_split3's capacity)
+            run += cnt[j];
+        }
+        if (b + 1 == gridDim.x) b3[(uint64_t)gridDim.x * F] = w0 + run;
+    }
+    __syncthreads();
+    const int k = rr.k;
+    const K128 mask = kmask128(k);
+    const int sh = 2 * (k - 1);
+    const uint32_t m2 = 2 * rr.m - 1;
+    for (uint64_t i = r0 + tid; i < r1; i += 512) {
+        const RunWM x = runs[i];
+        const uint32_t ws = x.wn & 0xFFFFu, n = x.wn >> 16;
+        RecWM *o = out + w0 + atomicAdd(&cur[rec_bucket(x, bbits + sbits) & (F - 1)], n);
+        // the run's n + k - 1 bases by chunks of 8 dwords (loads issued together; the byte
+        // steps unrolled so the chunk stays in registers)
+        const uint64_t s0 = rr.off[x.read] + ws;
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(rr.buf + (s0 & ~3ull));
+        const uint32_t skip = (uint32_t)(s0 & 3), nb = n + (uint32_t)k - 1, nw = (skip + nb + 3) >> 2;
+        const unsigned int rd = (unsigned int)(rr.read_base + x.read);
+        const unsigned long long pbits = (unsigned long long)x.place << WMB_SHIFT;
+        K128 fwd{0, 0}, rc{0, 0};
+        for (uint32_t q0 = 0; q0 < nw; q0 += 8) {
+            uint32_t ch[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) ch[u] = q0 + u < nw ? wp[q0 + u] : 0u;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+#pragma unroll
+                for (int bt = 0; bt < 4; bt++) {
+                    const uint32_t bpos = (q0 + u) * 4 + bt;
+                    if (bpos < skip || bpos >= skip + nb) continue;
+                    roll_w(fwd, rc, code2((ch[u] >> (8 * bt)) & 0xFFu), mask, sh);
+                    const uint32_t tt = bpos - skip;  // the run's base index
+                    if (tt + 1 < (uint32_t)k) continue;
+                    const uint32_t j = tt + 1 - (uint32_t)k, w = ws + j;
+                    const bool f = fwd < rc, pal = fwd == rc;
+                    const K128 c = f ? fwd : rc;
+                    const uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
+                    RecWM r;
+                    r.lo = c.lo;
+                    r.hi = c.hi | pbits;
+                    r.read = rd;
+                    r.ev = lC | (lT << 16);
+                    o[j] = r;
+                }
+            }
+        }
     }
 }
 
@@ -511,22 +769,24 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const R *recs, cons
     }
     __syncthreads();
     const uint64_t r0 = bstart[b], r1 = bend ? bend[b] : bstart[b + 1];
-    constexpr int U = 4;  // loads of U records issued before any insert
-    auto ins = [&](const R &x) {
-        const unsigned int lC = x.ev & 0xFFFFu, lT = x.ev >> 16;
-        const K128 c = rkey(x);
-        const unsigned long long rd = (unsigned long long)x.read << 32;
-        lds_insert_w<SLOTS>(tab, s_over, c, wide_slot0(mix128(c), SLOTS), lC == lT ? 2u : 1u, rd | lC, rd | lT);
-    };
-    uint64_t i = r0 + threadIdx.x;
-    for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
-        R raw[U];
+    {
+        constexpr int U = 4;  // loads of U records issued before any insert
+        auto ins = [&](const R &x) {
+            const unsigned int lC = x.ev & 0xFFFFu, lT = x.ev >> 16;
+            const K128 c = rkey(x);
+            const unsigned long long rd = (unsigned long long)x.read << 32;
+            lds_insert_w<SLOTS>(tab, s_over, c, wide_slot0(mix128(c), SLOTS), lC == lT ? 2u : 1u, rd | lC, rd | lT);
+        };
+        uint64_t i = r0 + threadIdx.x;
+        for (; i + (U - 1) * (uint64_t)blockDim.x < r1; i += U * (uint64_t)blockDim.x) {
+            R raw[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) raw[u] = recs[i + u * (uint64_t)blockDim.x];
+            for (int u = 0; u < U; u++) raw[u] = recs[i + u * (uint64_t)blockDim.x];
 #pragma unroll
-        for (int u = 0; u < U; u++) ins(raw[u]);
+            for (int u = 0; u < U; u++) ins(raw[u]);
+        }
+        for (; i < r1; i += blockDim.x) ins(recs[i]);
     }
-    for (; i < r1; i += blockDim.x) ins(recs[i]);
     __syncthreads();
     if (s_over[0]) {
         if (threadIdx.x == 0) atomicAdd(overflow, 1u);
