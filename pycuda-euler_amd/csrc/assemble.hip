@@ -223,6 +223,7 @@ struct ec_session {
     DevBuf jrec, joid, jout, jseg, jcnt;
     DevBuf xrec;     // ec_merge_owned_from: the received records decoded
     DevBuf skm_rec, skm_ev, skm_end;  // k_skdedup: the merged records of the error-rich count
+    DevBuf wcodes_tab;                // k_run_codes: each third-level table's first code dword
     HostBuf hmeta;   // ... and its per-source table, staged page-locked
     int owner_rule = 0;         // ec_session_set_owner_rule: 0 minimizer ranges (21 <= k <= 52), 1 key hash
     // ec_export_by_owner's owner ids / scanned chunk histogram of the last call, reused by a
@@ -1965,10 +1966,38 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         kmark(s, 4, 1);
     }
     RecWM *rwin = nullptr;  // runs: the window records of the expansion, bucket bounds in bb2
-    if (runs) {
-        // each fine bucket's runs -> its windows' records, split into its sub-buckets on the way
-        const RunWM *rin = second ? s->recs2.as<RunWM>() : s->recs.as<RunWM>();
-        rwin = second ? s->recs.as<RecWM>() : s->recs2.as<RecWM>();
+    RunWM *rdirect = nullptr;  // runs on third-level tables: sorted runs, bounds in run units (bb2)
+    uint32_t *wcodes = nullptr;  // ... and their bases as 2-bit codes, table t's from wcodes_tab[t]
+    if (runs && sbits && kn().wide_runs != 2) {
+        // each fine bucket's runs split into its sub-buckets (run units); the bucket pass rolls
+        // the windows out itself (k_bucket_wr)
+        RunWM *rin = second ? s->recs2.as<RunWM>() : s->recs.as<RunWM>();
+        rdirect = second ? s->recs.as<RunWM>() : s->recs2.as<RunWM>();
+        EC_CHECK(s->bb2.ensure((Bt + 1) * 8));
+        const unsigned long long cap3 = kn().wide_l3_cap > 0 ? (unsigned long long)kn().wide_l3_cap : 0ull;
+        kmark(s, 4, 0);
+        k_split3<RunWM><<<(unsigned)Bk, 512, 0, st>>>(rin, s->bstart.as<unsigned long long>(), bbits, sbits, rdirect,
+                                                      s->bb2.as<unsigned long long>(), cap3, &dsc->overflow);
+        // the sorted runs' bases as 2-bit codes (the refined runs' buffer is free: P 24-B records
+        // hold them -- at most 20 code dwords a run)
+        EC_CHECK(s->tot.ensure((Bk + 1) * 8));
+        EC_CHECK(s->gcur.ensure((Bk + 1) * 8));
+        EC_CHECK(s->wcodes_tab.ensure((Bt + 1) * 8));
+        k_run_ccount<<<(unsigned)(Bk + 1), 256, 0, st>>>(rdirect, s->bstart.as<unsigned long long>(), k,
+                                                        s->tot.as<unsigned long long>(), Bk);
+        EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->gcur.as<unsigned long long>(), Bk + 1));
+        wcodes = reinterpret_cast<uint32_t *>(rin);
+        k_run_codes<<<(unsigned)Bk, 512, 0, st>>>(rdirect, s->bstart.as<unsigned long long>(),
+                                                  s->gcur.as<unsigned long long>(), s->bb2.as<unsigned long long>(),
+                                                  sbits, wcodes, s->wcodes_tab.as<unsigned long long>(),
+                                                  RunReads{d_reads, d_off, k, mbM, read_base});
+        kmark(s, 4, 1);
+    } else if (runs) {
+        // each fine bucket's runs sorted by sub-bucket (k_split3_runs, run units), then expanded
+        // into its windows' records (k_expand_runs, window units; bb2 = sub-bucket bounds)
+        RunWM *rin = second ? s->recs2.as<RunWM>() : s->recs.as<RunWM>();
+        RunWM *rsorted = second ? s->recs.as<RunWM>() : s->recs2.as<RunWM>();
+        rwin = reinterpret_cast<RecWM *>(rin);  // (the refined runs are dead after the sort)
         EC_CHECK(s->bb2.ensure((Bt + 1) * 8));
         EC_CHECK(s->tot.ensure((Bk + 1) * 8));
         EC_CHECK(s->gcur.ensure((Bk + 1) * 8));
@@ -1976,17 +2005,15 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         k_run_wsum<<<(unsigned)(Bk + 1), 256, 0, st>>>(rin, s->bstart.as<unsigned long long>(),
                                                       s->tot.as<unsigned long long>(), Bk);
         EC_CHECK(scan_u64(s, s->tot.as<unsigned long long>(), s->gcur.as<unsigned long long>(), Bk + 1));
-        // (dynamic LDS only to bound the workgroups a CU holds: each lane writes its own stream of
-        // window records, and past ~2 MB of open lines per XCD the L2 evicts them half written --
-        // EULERHIP_WRUN_LDS: bytes, A/B)
-        const unsigned wlds = kn().wrun_lds >= 0 ? (unsigned)kn().wrun_lds : 0u;
-        k_split3_runs<<<(unsigned)Bk, 512, wlds, st>>>(rin, s->bstart.as<unsigned long long>(), bbits, sbits,
-                                                    s->gcur.as<unsigned long long>(), rwin,
+        k_split3_runs<<<(unsigned)Bk, 512, 0, st>>>(rin, s->bstart.as<unsigned long long>(), bbits, sbits,
+                                                    s->gcur.as<unsigned long long>(), rsorted,
                                                     s->bb2.as<unsigned long long>(),
-                                                    RunReads{d_reads, d_off, k, mbM, read_base},
                                                     sbits && kn().wide_l3_cap > 0 ? (unsigned long long)kn().wide_l3_cap
                                                                                   : 0ull,
                                                     &dsc->overflow);
+        k_expand_runs<<<(unsigned)Bk, 512, 0, st>>>(rsorted, s->bstart.as<unsigned long long>(),
+                                                    s->gcur.as<unsigned long long>(), rwin,
+                                                    RunReads{d_reads, d_off, k, mbM, read_base});
         kmark(s, 4, 1);
     }
     mark(s, 2 * EC_STAGE_COUNT + 1);
@@ -2011,7 +2038,13 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         SRC, BEG, END, limit, s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),    \
         s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
         &dsc->ndistinct, &dsc->overflow, bm)
-    if (sbits && runs)
+    if (rdirect)
+        k_bucket_wr<1664><<<(unsigned)Bt, WR_NT, 0, st>>>(
+            rdirect, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1, limit, s->dkey.as<K128>(),
+            s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+            s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow, bm,
+            RunReads{d_reads, d_off, k, mbM, read_base}, wcodes, s->wcodes_tab.as<unsigned long long>());
+    else if (sbits && runs)
         EC_BUCKET_W(1664, RecWM, rwin, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1);
     else if (runs)
         EC_BUCKET_W(SLOTS_W, RecWM, rwin, s->bb2.as<unsigned long long>(), nullptr);
@@ -3646,7 +3679,7 @@ int ec_session_destroy(ec_session *s) {
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
                      &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
                      &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec,
-                     &s->skm_rec, &s->skm_ev, &s->skm_end};
+                     &s->skm_rec, &s->skm_ev, &s->skm_end, &s->wcodes_tab};
     for (auto *b : all) b->release();
     s->h_chars.release();
     s->hmeta.release();

@@ -586,76 +586,155 @@ __global__ void __launch_bounds__(256) k_run_wsum(const RunWM *runs, const unsig
     __syncthreads();
     if (threadIdx.x == 0) wsum[b] = s[0] + s[1] + s[2] + s[3];
 }
-// fine bucket b's runs [bstart[b], bstart[b + 1]) -> the window records of its sub-buckets at
-// wstart[b] ..; b3[b 2^sbits + j] = first window record of sub-bucket j
-__global__ void __launch_bounds__(512) k_split3_runs(const RunWM *runs, const unsigned long long *bstart, int bbits,
-                                                     int sbits, const unsigned long long *wstart, RecWM *out,
-                                                     unsigned long long *b3, RunReads rr, unsigned long long cap,
+// fine bucket b's runs [bstart[b], bstart[b + 1]) -> out (same positions), sorted by their
+// sub-bucket (the third level; sbits = 0: one); b3w[b 2^sbits + j] = first WINDOW record of
+// sub-bucket j in the expansion's output (wstart[b] = the fine bucket's first)
+__global__ void __launch_bounds__(512) k_split3_runs(const RunWM *in, const unsigned long long *bstart, int bbits,
+                                                     int sbits, const unsigned long long *wstart, RunWM *out,
+                                                     unsigned long long *b3w, unsigned long long cap,
                                                      unsigned int *over) {
     __shared__ unsigned int cnt[64], cur[64];
+    __shared__ unsigned long long wc[64];
     const unsigned int b = blockIdx.x, F = 1u << sbits, tid = threadIdx.x;
     const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
-    if (tid < 64) cnt[tid] = 0;
+    if (tid < 64) cnt[tid] = 0, wc[tid] = 0;
     __syncthreads();
     for (uint64_t i = r0 + tid; i < r1; i += 512) {
-        const RunWM x = runs[i];
-        atomicAdd(&cnt[rec_bucket(x, bbits + sbits) & (F - 1)], x.wn >> 16);
+        const RunWM x = in[i];
+        const unsigned int j = rec_bucket(x, bbits + sbits) & (F - 1);
+        atomicAdd(&cnt[j], 1u);
+        atomicAdd(&wc[j], (unsigned long long)(x.wn >> 16));
     }
     __syncthreads();
-    const uint64_t w0 = wstart[b];
     if (tid == 0) {
         unsigned int run = 0;
+        unsigned long long w = wstart[b];
         for (unsigned int j = 0; j < F; j++) {
             cur[j] = run;
-            b3[(uint64_t)b * F + j] = w0 + run;
-            if (cap && cnt[j] > cap) *over = 1u;  // (tests: as k_split3's capacity)
+            b3w[(uint64_t)b * F + j] = w;
+            if (cap && wc[j] > cap) *over = 1u;  // (tests: as k_split3's capacity)
             run += cnt[j];
+            w += wc[j];
         }
-        if (b + 1 == gridDim.x) b3[(uint64_t)gridDim.x * F] = w0 + run;
+        if (b + 1 == gridDim.x) b3w[(uint64_t)gridDim.x * F] = w;
     }
     __syncthreads();
+    for (uint64_t i = r0 + tid; i < r1; i += 512) {
+        const RunWM x = in[i];
+        out[r0 + atomicAdd(&cur[rec_bucket(x, bbits + sbits) & (F - 1)], 1u)] = x;
+    }
+}
+
+// fine bucket b's runs (in sub-bucket order) -> its windows' records at wstart[b] .., in run
+// order: a workgroup takes the runs in batches, their window offsets scanned in LDS, and each
+// thread a chunk of RUN_CHUNK consecutive windows -- its first run found by binary search, the
+// k-mer rolled from the read's bases (RunReads), re-rolled where the chunk enters the next run.
+// Consecutive threads write consecutive records, so a wave fills whole lines: with a lane per
+// run, each lane wrote a stream of its own and the L2 evicted ~0.5 M open lines half written
+// (27-39 ms at config 5, against ~10 ms here).
+constexpr int RUN_BATCH = 2048;
+constexpr int RUN_CHUNK = 16;
+constexpr int RUN_DW = (RUN_CHUNK + WMB_MAX_K - 1 + 3 + 3) / 4;  // dwords a segment's bases span
+static_assert(RUN_DW == 18, "segment dwords");
+__global__ void __launch_bounds__(512) k_expand_runs(const RunWM *runs, const unsigned long long *bstart,
+                                                     const unsigned long long *wstart, RecWM *out, RunReads rr) {
+    __shared__ unsigned int pre[RUN_BATCH + 1];
+    __shared__ unsigned int s_w[8];
+    const unsigned int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
     const int k = rr.k;
     const K128 mask = kmask128(k);
     const int sh = 2 * (k - 1);
     const uint32_t m2 = 2 * rr.m - 1;
-    for (uint64_t i = r0 + tid; i < r1; i += 512) {
-        const RunWM x = runs[i];
-        const uint32_t ws = x.wn & 0xFFFFu, n = x.wn >> 16;
-        RecWM *o = out + w0 + atomicAdd(&cur[rec_bucket(x, bbits + sbits) & (F - 1)], n);
-        // the run's n + k - 1 bases by chunks of 8 dwords (loads issued together; the byte
-        // steps unrolled so the chunk stays in registers)
-        const uint64_t s0 = rr.off[x.read] + ws;
-        const uint32_t *wp = reinterpret_cast<const uint32_t *>(rr.buf + (s0 & ~3ull));
-        const uint32_t skip = (uint32_t)(s0 & 3), nb = n + (uint32_t)k - 1, nw = (skip + nb + 3) >> 2;
-        const unsigned int rd = (unsigned int)(rr.read_base + x.read);
-        const unsigned long long pbits = (unsigned long long)x.place << WMB_SHIFT;
-        K128 fwd{0, 0}, rc{0, 0};
-        for (uint32_t q0 = 0; q0 < nw; q0 += 8) {
-            uint32_t ch[8];
+    uint64_t wout = wstart[b];
+    auto code_at = [&](uint64_t pos) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(rr.buf + (pos & ~3ull));
+        return code2((w >> (8 * (pos & 3))) & 0xFFu);
+    };
+    for (uint64_t rb = r0; rb < r1; rb += RUN_BATCH) {
+        const unsigned int nb = (unsigned int)min<uint64_t>(RUN_BATCH, r1 - rb);
+        // window offsets of the batch's runs: 4 runs a thread, a block scan
+        unsigned int v[4], sum = 0;
 #pragma unroll
-            for (int u = 0; u < 8; u++) ch[u] = q0 + u < nw ? wp[q0 + u] : 0u;
+        for (int u = 0; u < 4; u++) {
+            const unsigned int i = tid * 4 + u;
+            v[u] = i < nb ? runs[rb + i].wn >> 16 : 0u;
+            sum += v[u];
+        }
+        unsigned int incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int t = __shfl_up(incl, o);
+            if ((int)lane >= o) incl += t;
+        }
+        if (lane == 63) s_w[wid] = incl;
+        __syncthreads();
+        unsigned int before = 0;
+        for (unsigned int q = 0; q < wid; q++) before += s_w[q];
+        unsigned int run = before + incl - sum;
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 4; u++) {
+            const unsigned int i = tid * 4 + u;
+            if (i < nb) pre[i] = run;
+            run += v[u];
+        }
+        if (tid == 511) pre[nb] = run;  // (tid 511's run is the batch total: nb <= 4 * 512)
+        __syncthreads();
+        const unsigned int W = pre[nb];
+        for (unsigned int q0 = tid * RUN_CHUNK; q0 < W; q0 += 512 * RUN_CHUNK) {
+            const unsigned int q1 = min(q0 + RUN_CHUNK, W);
+            unsigned int lo = 0, hi = nb;  // the run holding window q0: pre[lo] <= q0 < pre[lo + 1]
+            while (hi - lo > 1) {
+                const unsigned int md = (lo + hi) >> 1;
+                if (pre[md] <= q0) lo = md;
+                else hi = md;
+            }
+            unsigned int i = lo, j = q0 - pre[lo];
+            // segments: the chunk's windows within one run -- their n + k - 1 bases loaded as
+            // dwords at once (RUN_DW of them: k <= WMB_MAX_K), the byte steps unrolled over
+            // registers (a load per base left each step waiting on its latency: 85 ms at config 5)
+            for (unsigned int q = q0; q < q1;) {
+                const RunWM x = runs[rb + i];
+                const uint32_t ws = x.wn & 0xFFFFu, n = x.wn >> 16;
+                const uint32_t cnt = min(n - j, q1 - q);
+                const uint64_t s0 = rr.off[x.read] + ws + j;
+                const uint32_t skip = (uint32_t)(s0 & 3), nbytes = cnt + (uint32_t)k - 1;
+                const uint32_t nw = (skip + nbytes + 3) >> 2;
+                const uint32_t *wp = reinterpret_cast<const uint32_t *>(rr.buf + (s0 & ~3ull));
+                uint32_t d[RUN_DW];
 #pragma unroll
-                for (int bt = 0; bt < 4; bt++) {
-                    const uint32_t bpos = (q0 + u) * 4 + bt;
-                    if (bpos < skip || bpos >= skip + nb) continue;
-                    roll_w(fwd, rc, code2((ch[u] >> (8 * bt)) & 0xFFu), mask, sh);
-                    const uint32_t tt = bpos - skip;  // the run's base index
-                    if (tt + 1 < (uint32_t)k) continue;
-                    const uint32_t j = tt + 1 - (uint32_t)k, w = ws + j;
-                    const bool f = fwd < rc, pal = fwd == rc;
-                    const K128 c = f ? fwd : rc;
-                    const uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
-                    RecWM r;
-                    r.lo = c.lo;
-                    r.hi = c.hi | pbits;
-                    r.read = rd;
-                    r.ev = lC | (lT << 16);
-                    o[j] = r;
+                for (int u = 0; u < RUN_DW; u++) d[u] = (uint32_t)u < nw ? wp[u] : 0u;
+                const unsigned int rd = (unsigned int)(rr.read_base + x.read);
+                const unsigned long long pbits = (unsigned long long)x.place << WMB_SHIFT;
+                RecWM *o = out + wout + q;
+                K128 fwd{0, 0}, rc{0, 0};
+#pragma unroll
+                for (int u = 0; u < RUN_DW; u++) {
+#pragma unroll
+                    for (int bt = 0; bt < 4; bt++) {
+                        const uint32_t bpos = (uint32_t)(u * 4 + bt);
+                        if (bpos < skip || bpos >= skip + nbytes) continue;
+                        roll_w(fwd, rc, code2((d[u] >> (8 * bt)) & 0xFFu), mask, sh);
+                        const uint32_t tt = bpos - skip;
+                        if (tt + 1 < (uint32_t)k) continue;
+                        const uint32_t jj = tt + 1 - (uint32_t)k, w = ws + j + jj;
+                        const bool f = fwd < rc, pal = fwd == rc;
+                        const K128 c = f ? fwd : rc;
+                        const uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
+                        RecWM r;
+                        r.lo = c.lo;
+                        r.hi = c.hi | pbits;
+                        r.read = rd;
+                        r.ev = lC | (lT << 16);
+                        o[jj] = r;
+                    }
                 }
+                q += cnt;
+                j += cnt;
+                if (j == n) i++, j = 0;
             }
         }
+        wout += W;
+        __syncthreads();  // (pre is rewritten by the next batch)
     }
 }
 
@@ -719,6 +798,216 @@ __device__ inline void lds_insert_w(LSlotW *tab, unsigned int *s_over, const K12
     if (eT < ev.y) atomicMin(&sl.fT, eT);
 }
 
+// ---- bucket pass on minimizer runs (RUNS, third level) ------------------------------------------
+// One workgroup per table as k_bucket_w, but the table's records are its RUNS (k_split3<RunWM>:
+// sorted by sub-bucket, bounds in run units): their bases are gathered once into LDS as 2-bit
+// codes (a thread a run, 16 bases a dword), then every window of the table is a thread's -- its
+// run by binary search over the window offsets, its k-mer extracted from the codes (the reverse
+// complement is ~codes, the forward string its twin) -- and inserted.  The window records never
+// exist: config 5's expansion wrote and the bucket pass read back 30 GB of them (29 + 16 ms).
+constexpr int WR_NT = 1024;        // threads a table (one workgroup per CU: 104 KB of LDS)
+constexpr int WR_CODES = 2048;     // code dwords a batch of runs stages (32 K bases)
+__device__ inline K128 extract_codes(const uint32_t *c, uint32_t bitpos) {  // bits [bitpos, bitpos + 128)
+    const uint32_t w = bitpos >> 5, sft = bitpos & 31;
+    uint32_t d[5];
+#pragma unroll
+    for (int u = 0; u < 5; u++) d[u] = c[w + u];
+    uint32_t o[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) o[u] = sft ? __builtin_amdgcn_alignbit(d[u + 1], d[u], sft) : d[u];
+    return K128{(unsigned long long)o[0] | (unsigned long long)o[1] << 32, (unsigned long long)o[2] | (unsigned long long)o[3] << 32};
+}
+// the runs' bases as 2-bit codes in global memory, run after run in their (sub-bucket sorted)
+// order: per fine bucket b its code dwords (k_run_ccount, scanned -> cbase[b]), then each run's
+// codes at cbase[b] + the prefix of its fine bucket's runs (k_run_codes: a thread a run, all
+// lanes busy, the gathers' latency hidden by full occupancy); ctab[t] = first code dword of
+// table t (sub-bucket bounds b3 in run units).  The bucket pass then loads a table's codes as
+// one contiguous block -- gathering them itself, one workgroup per CU, it waited on them
+// (k_bucket_wr 55 ms at config 5).
+__device__ inline unsigned int run_cdw(const RunWM &x, int k) { return ((x.wn >> 16) + (unsigned int)k - 1 + 15) >> 4; }
+__global__ void __launch_bounds__(256) k_run_ccount(const RunWM *runs, const unsigned long long *bstart, int k,
+                                                    unsigned long long *csum, uint64_t nb) {
+    const uint64_t b = blockIdx.x;
+    if (b >= nb) {
+        if (threadIdx.x == 0) csum[b] = 0;
+        return;
+    }
+    unsigned long long c = 0;
+    for (uint64_t i = bstart[b] + threadIdx.x; i < bstart[b + 1]; i += blockDim.x) c += run_cdw(runs[i], k);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+    __shared__ unsigned long long sm[4];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) csum[b] = sm[0] + sm[1] + sm[2] + sm[3];
+}
+__global__ void __launch_bounds__(512) k_run_codes(const RunWM *runs, const unsigned long long *bstart,
+                                                   const unsigned long long *cbase, const unsigned long long *b3, int sbits,
+                                                   uint32_t *codes, unsigned long long *ctab, RunReads rr) {
+    __shared__ unsigned int s_w[8];
+    __shared__ unsigned long long s_off;
+    const unsigned int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, F = 1u << sbits;
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    const int k = rr.k;
+    if (tid == 0) s_off = cbase[b];
+    __syncthreads();
+    for (uint64_t rb = r0; rb < r1; rb += 512) {
+        const uint64_t ri = rb + tid;
+        RunWM x{};
+        unsigned int nc = 0;
+        if (ri < r1) x = runs[ri], nc = run_cdw(x, k);
+        unsigned int incl = nc;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int t = __shfl_up(incl, o);
+            if ((int)lane >= o) incl += t;
+        }
+        if (lane == 63) s_w[wid] = incl;
+        __syncthreads();
+        unsigned int before = 0, tot = 0;
+        for (unsigned int q = 0; q < 8; q++) {
+            if (q < wid) before += s_w[q];
+            tot += s_w[q];
+        }
+        const unsigned long long od0 = s_off + before + incl - nc;
+        if (ri < r1) {
+            // a table's first run: its code base (the sub-bucket bounds are runs of this bucket)
+            for (unsigned int j = 0; j < F; j++)
+                if (b3[(uint64_t)b * F + j] == ri) ctab[(uint64_t)b * F + j] = od0;
+            const unsigned int nwin = x.wn >> 16, nbases = nwin + (unsigned int)k - 1;
+            const uint64_t s0 = rr.off[x.read] + (x.wn & 0xFFFFu);
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(rr.buf + (s0 & ~3ull));
+            const unsigned int skip = (unsigned int)(s0 & 3), nw = (skip + nbases + 3) >> 2;
+            uint32_t acc = 0;
+            unsigned int i = 0;
+            unsigned long long od = od0;
+            for (unsigned int q = 0; q < nw; q += 8) {
+                uint32_t d[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) d[u] = q + u < nw ? wp[q + u] : 0u;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+#pragma unroll
+                    for (int bt = 0; bt < 4; bt++) {
+                        const unsigned int bp = (q + u) * 4 + bt;
+                        if (bp < skip || bp >= skip + nbases) continue;
+                        acc |= code2((d[u] >> (8 * bt)) & 0xFFu) << (2 * (i & 15));
+                        if ((i & 15) == 15) codes[od++] = acc, acc = 0;
+                        i++;
+                    }
+            }
+            if (i & 15) codes[od] = acc;
+        }
+        __syncthreads();
+        if (tid == 0) s_off += tot;
+        __syncthreads();
+    }
+    if (tid == 0 && b + 1 == gridDim.x) ctab[(uint64_t)gridDim.x * F] = s_off;
+}
+
+template <int SLOTS>
+__global__ void __launch_bounds__(WR_NT) k_bucket_wr(const RunWM *runs, const unsigned long long *bstart,
+                                                    const unsigned long long *bend, long long limit, K128 *dkey,
+                                                    unsigned int *dcnt, unsigned long long *dfc, unsigned long long *dft,
+                                                    SubSlotW *sub, unsigned int *nsolid, unsigned long long *ndistinct,
+                                                    unsigned int *overflow, unsigned int *bmark, RunReads rr,
+                                                    const uint32_t *gcodes, const unsigned long long *ctab) {
+    __shared__ LSlotW tab[SLOTS];
+    __shared__ unsigned int s_over[2];
+    __shared__ unsigned int s_wave[WR_NT / 64], s_pres[WR_NT / 64], s_wave2[WR_NT / 64];
+    __shared__ unsigned int s_base, s_nb;
+    __shared__ unsigned int wpre[WR_NT + 1], cpre[WR_NT + 1];  // window / code-dword offsets of the batch's runs
+    __shared__ uint2 rmeta[WR_NT];                              // read, first window
+    __shared__ uint32_t codes[WR_CODES + 8];
+    const unsigned int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int i = tid; i < SLOTS; i += WR_NT) {
+        tab[i].w1 = 0;
+        tab[i].w2 = 0;
+        tab[i].count = 0;
+        tab[i].fC = NONE64;
+        tab[i].fT = NONE64;
+    }
+    if (tid == 0) s_over[0] = 0, s_over[1] = 0;
+    __syncthreads();
+    const uint64_t r0 = bstart[b], r1 = bend ? bend[b] : bstart[b + 1];
+    const int k = rr.k;
+    const K128 mask = kmask128(k);
+    const uint32_t m2 = 2 * rr.m - 1;
+    unsigned long long gco = ctab[b];  // the batch's first code dword in gcodes
+    for (uint64_t rb = r0; rb < r1;) {
+        // the batch: up to WR_NT runs whose codes fit WR_CODES dwords (a run of n windows: n + k - 1 bases)
+        const uint64_t ri = rb + tid;
+        RunWM x{};
+        unsigned int nwin = 0, ncd = 0;
+        if (ri < r1) {
+            x = runs[ri];
+            nwin = x.wn >> 16;
+            ncd = (nwin + (unsigned int)k - 1 + 15) >> 4;
+        }
+        // two block scans at once (windows, code dwords)
+        unsigned int iw = nwin, ic = ncd;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int tw = __shfl_up(iw, o), tc = __shfl_up(ic, o);
+            if ((int)lane >= o) iw += tw, ic += tc;
+        }
+        if (lane == 63) s_wave[wid] = iw, s_wave2[wid] = ic;
+        __syncthreads();
+        unsigned int bw = 0, bc = 0;
+        for (unsigned int q = 0; q < wid; q++) bw += s_wave[q], bc += s_wave2[q];
+        const unsigned int cw = bw + iw - nwin, cc = bc + ic - ncd;  // exclusive offsets
+        const bool in = ri < r1 && cc + ncd <= WR_CODES;             // (runs past the codes wait for the next batch)
+        if (tid == 0) s_nb = 0;
+        __syncthreads();
+        if (in) atomicMax(&s_nb, tid + 1);  // (a prefix: offsets grow with tid)
+        __syncthreads();
+        const unsigned int nb = s_nb;
+        if (tid < nb) {
+            wpre[tid] = cw;
+            cpre[tid] = cc;
+            rmeta[tid] = make_uint2(x.read, x.wn & 0xFFFFu);
+            if (tid + 1 == nb) wpre[nb] = cw + nwin, cpre[nb] = cc + ncd;
+        }
+        __syncthreads();
+        // the batch's codes: one contiguous block of gcodes (k_run_codes)
+        const unsigned int ncodes = cpre[nb];
+        for (unsigned int i = tid; i < ncodes; i += WR_NT) codes[i] = gcodes[gco + i];
+        gco += ncodes;
+        __syncthreads();
+        // the batch's windows, a thread each
+        const unsigned int W = wpre[nb];
+        for (unsigned int q = tid; q < W; q += WR_NT) {
+            unsigned int lo = 0, hi = nb;
+            while (hi - lo > 1) {
+                const unsigned int md = (lo + hi) >> 1;
+                if (wpre[md] <= q) lo = md;
+                else hi = md;
+            }
+            const unsigned int j = q - wpre[lo];
+            const uint2 mt = rmeta[lo];
+            const K128 V = extract_codes(codes, cpre[lo] * 32 + 2 * j);  // bases j .., first least significant
+            const K128 rc{~V.lo & mask.lo, ~V.hi & mask.hi};
+            const K128 fwd = twin128(rc, k);
+            const uint32_t w = mt.y + j;
+            const bool f = fwd < rc, pal = fwd == rc;
+            const K128 c = f ? fwd : rc;
+            const uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
+            const unsigned long long rd = (unsigned long long)(rr.read_base + mt.x) << 32;
+            lds_insert_w<SLOTS>(tab, s_over, c, wide_slot0(mix128(c), SLOTS), lC == lT ? 2u : 1u, rd | lC, rd | lT);
+        }
+        rb += nb;
+        if (nb == 0) {  // (one run past WR_CODES: never for k <= 52 and reads <= 160 bp -- reported)
+            if (tid == 0) s_over[0] = 1;
+            __syncthreads();
+            break;
+        }
+        __syncthreads();  // (the batch's staging is rewritten by the next)
+    }
+    if (s_over[0]) {
+        if (tid == 0) atomicAdd(overflow, 1u);
+        return;
+    }
+    bucket_w_finish<SLOTS, WR_NT>(tab, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, bmark, s_wave, s_pres,
+                                  s_base);
+}
+
 // ---- third partition level (more keys than 2^FINE_W_BITS tables hold) ---------------------
 // The upsweep's fine histogram sizes 2^FINE_W_BITS buckets exactly; past ~1.8e7 distinct keys
 // each of them is split again by the next hash bits into 2^s sub-buckets of fixed capacity
@@ -740,6 +1029,75 @@ __global__ void __launch_bounds__(256) k_level3_ends(const unsigned long long *g
     for (uint64_t d = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; d < nb; d += (uint64_t)gridDim.x * blockDim.x) {
         bbeg[d] = d * fcap;
         bend[d] = min((uint64_t)gcur[d], (d + 1) * fcap);
+    }
+}
+
+// solid filter + compaction of a filled table (as lds_table_finish): the solid keys to the
+// dense arrays at a block-reserved base, the slots to the bucket's sub-table region
+template <int SLOTS, int NT>
+__device__ inline void bucket_w_finish(const LSlotW *tab, unsigned int b, long long limit, K128 *dkey, unsigned int *dcnt,
+                                       unsigned long long *dfc, unsigned long long *dft, SubSlotW *sub,
+                                       unsigned int *nsolid, unsigned long long *ndistinct, unsigned int *bmark,
+                                       unsigned int *s_wave, unsigned int *s_pres, unsigned int &s_base) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int PER = (SLOTS + NT - 1) / NT;
+    bool solid[PER];
+    unsigned int mine = 0, present = 0;
+    for (int q = 0; q < PER; q++) {
+        const int idx = threadIdx.x * PER + q;
+        if (idx >= SLOTS) {
+            solid[q] = false;
+            continue;
+        }
+        const LSlotW &sl = tab[idx];
+        present += sl.w1 != 0;
+        solid[q] = sl.w1 != 0 && (long long)sl.count > limit;
+        mine += solid[q];
+    }
+    unsigned int incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) s_wave[wid] = incl;
+    unsigned int pres = present;
+    for (int o = 32; o > 0; o >>= 1) pres += __shfl_down(pres, o);
+    if (lane == 0) s_pres[wid] = pres;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int tot = 0, np = 0;
+        for (int w = 0; w < NT / 64; w++) {
+            const unsigned int c = s_wave[w];
+            s_wave[w] = tot;
+            tot += c;
+            np += s_pres[w];
+        }
+        s_base = tot ? atomicAdd(nsolid, tot) : 0;
+        if (np) atomicAdd(ndistinct, (unsigned long long)np);
+        if (bmark && tot) atomicOr(&bmark[s_base >> 5], 1u << (s_base & 31));  // (the tile ranking's cuts)
+    }
+    __syncthreads();
+    unsigned int u = s_base + s_wave[wid] + incl - mine;
+    SubSlotW *region = sub ? sub + (uint64_t)b * SLOTS : nullptr;
+    for (int q = 0; q < PER; q++) {
+        const int idx = threadIdx.x * PER + q;
+        if (idx >= SLOTS) break;
+        const LSlotW &sl = tab[idx];
+        SubSlotW o;
+        o.w1 = sl.w1;
+        o.w2 = sl.w2;
+        o.id = NONE32;
+        o.pad = 0;
+        o.pad2 = 0;
+        if (solid[q]) {
+            dkey[u] = wide_key(sl.w1, sl.w2);
+            dcnt[u] = sl.count;
+            dfc[u] = sl.fC;
+            dft[u] = sl.fT;
+            o.id = u;
+            u++;
+        }
+        if (region) region[idx] = o;
     }
 }
 
@@ -792,67 +1150,8 @@ __global__ void __launch_bounds__(BUCKET_THREADS) k_bucket_w(const R *recs, cons
         if (threadIdx.x == 0) atomicAdd(overflow, 1u);
         return;
     }
-    // solid filter + compaction (as lds_table_finish)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int PER = (SLOTS + BUCKET_THREADS - 1) / BUCKET_THREADS;
-    bool solid[PER];
-    unsigned int mine = 0, present = 0;
-    for (int q = 0; q < PER; q++) {
-        const int idx = threadIdx.x * PER + q;
-        if (idx >= SLOTS) {
-            solid[q] = false;
-            continue;
-        }
-        const LSlotW &sl = tab[idx];
-        present += sl.w1 != 0;
-        solid[q] = sl.w1 != 0 && (long long)sl.count > limit;
-        mine += solid[q];
-    }
-    unsigned int incl = mine;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
-    }
-    if (lane == 63) s_wave[wid] = incl;
-    unsigned int pres = present;
-    for (int o = 32; o > 0; o >>= 1) pres += __shfl_down(pres, o);
-    if (lane == 0) s_pres[wid] = pres;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned int tot = 0, np = 0;
-        for (int w = 0; w < BUCKET_THREADS / 64; w++) {
-            const unsigned int c = s_wave[w];
-            s_wave[w] = tot;
-            tot += c;
-            np += s_pres[w];
-        }
-        s_base = tot ? atomicAdd(nsolid, tot) : 0;
-        if (np) atomicAdd(ndistinct, (unsigned long long)np);
-        if (bmark && tot) atomicOr(&bmark[s_base >> 5], 1u << (s_base & 31));  // (the tile ranking's cuts)
-    }
-    __syncthreads();
-    unsigned int u = s_base + s_wave[wid] + incl - mine;
-    SubSlotW *region = sub ? sub + (uint64_t)b * SLOTS : nullptr;
-    for (int q = 0; q < PER; q++) {
-        const int idx = threadIdx.x * PER + q;
-        if (idx >= SLOTS) break;
-        const LSlotW &sl = tab[idx];
-        SubSlotW o;
-        o.w1 = sl.w1;
-        o.w2 = sl.w2;
-        o.id = NONE32;
-        o.pad = 0;
-        o.pad2 = 0;
-        if (solid[q]) {
-            dkey[u] = wide_key(sl.w1, sl.w2);
-            dcnt[u] = sl.count;
-            dfc[u] = sl.fC;
-            dft[u] = sl.fT;
-            o.id = u;
-            u++;
-        }
-        if (region) region[idx] = o;
-    }
+    bucket_w_finish<SLOTS, BUCKET_THREADS>(tab, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, bmark, s_wave,
+                                           s_pres, s_base);
 }
 
 }  // namespace ec
