@@ -1881,7 +1881,11 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     // tables hold whole minimizers (~25 k-mers each): config 5's 2^18 tables of mean 763 keys
     // reached 1808, past the 1664 slots (a numpy model of its genome reproduces the five
     // overflowing tables); 2^19 of mean 381 top out at 1421
-    const double per3 = mb ? 400.0 : 800.0;
+    // runs rolled out in the tables (k_bucket_wr): 1024-slot tables of <= 200 keys, so two
+    // workgroups a CU hold their tables (48 KB) beside the staged codes
+    bool rdir = runs && kn().wide_runs != 2 && kn().wr_slots != 1664;
+    if (rdir && est / (double)(FINE_W << 6) > 200.0) rdir = false;  // (past 2^20 tables: 1664 slots)
+    const double per3 = mb ? (rdir ? 200.0 : 400.0) : 800.0;
     if (est / FINE_W > 1800.0) {
         while (sbits < 6 && est / (double)(FINE_W << sbits) > per3) sbits++;
         if (est / (double)(FINE_W << sbits) > per3) return reset();
@@ -1901,7 +1905,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     const int cbits = std::min(bbits, std::min(DS_MAX_CBITS, std::max(1, bbits - fan)));
     const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
     const uint64_t Bt = Bk << sbits;  // tables
-    const unsigned int SLOTS = sbits ? 1664u : (unsigned int)SLOTS_W;
+    const unsigned int SLOTS = sbits ? (rdir ? 1024u : 1664u) : (unsigned int)SLOTS_W;
     mark(s, 2 * EC_STAGE_COUNT);
     EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
     EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
@@ -2039,11 +2043,16 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
         &dsc->ndistinct, &dsc->overflow, bm)
     if (rdirect)
-        k_bucket_wr<1664><<<(unsigned)Bt, WR_NT, 0, st>>>(
-            rdirect, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1, limit, s->dkey.as<K128>(),
-            s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-            s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow, bm,
-            RunReads{d_reads, d_off, k, mbM, read_base}, wcodes, s->wcodes_tab.as<unsigned long long>());
+#define EC_BUCKET_WR(SL)                                                                                         \
+    k_bucket_wr<SL><<<(unsigned)Bt, WR_NT, 0, st>>>(                                                                \
+        rdirect, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1, limit, s->dkey.as<K128>(),      \
+        s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),                \
+        s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow, bm,            \
+        RunReads{d_reads, d_off, k, mbM, read_base}, wcodes, s->wcodes_tab.as<unsigned long long>())
+    if (rdirect && SLOTS == 1024)
+        EC_BUCKET_WR(1024);
+    else if (rdirect)
+        EC_BUCKET_WR(1664);
     else if (sbits && runs)
         EC_BUCKET_W(1664, RecWM, rwin, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1);
     else if (runs)
@@ -2061,6 +2070,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         EC_BUCKET_W(SLOTS_W, RecW, second ? s->recs2.as<RecW>() : s->recs.as<RecW>(), s->bstart.as<unsigned long long>(),
                     nullptr);
 #undef EC_BUCKET_W
+#undef EC_BUCKET_WR
     kmark(s, 2, 1);
     mark(s, 2 * EC_STAGE_COMPACT + 1);
     unsigned long long nruns = 0;
