@@ -2042,7 +2042,6 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         SRC, BEG, END, limit, s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),    \
         s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
         &dsc->ndistinct, &dsc->overflow, bm)
-    if (rdirect)
 #define EC_BUCKET_WR(SL)                                                                                         \
     k_bucket_wr<SL><<<(unsigned)Bt, WR_NT, 0, st>>>(                                                                \
         rdirect, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1, limit, s->dkey.as<K128>(),      \
@@ -2495,6 +2494,7 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
 
 // the rounds a ranking used (the last round that still moved a pointer + 1), for the next
 // call's speculation; 0 when the last round still moved one (not converged)
+constexpr unsigned int OCOPY_MIN = 1u << 16;  // contigs past which results copy on the output stream
 int rounds_used(const Scalars &h, int rounds) {
     if (rounds <= 0 || h.active[rounds - 1]) return 0;
     int used = 1;
@@ -2908,8 +2908,11 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
             if (!e) EC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         return EC_OK;
     };
+    // (only for many contigs: the event / stream-wait / copy calls cost the host ~30 us, more
+    // than the headline's few bytes of offsets and link counts take in line)
+    const bool ocopy = nc >= OCOPY_MIN;
     EC_CHECK(ostream_ready());
-    if (nc) {
+    if (ocopy) {
         EC_HIP(hipEventRecord(s->oev[2], st));
         EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[2], 0));
         EC_HIP(hipMemcpyAsync(s->h_coff.data(), s->coff.p, (size_t)nc * 8, hipMemcpyDeviceToHost, s->ostream));
@@ -2993,6 +2996,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     s->links_compact = true;
     EC_CHECK(s->h_lc8.resize(n2));
     if (!nc) s->h_coff[0] = 0;
+    if (nc && !ocopy) EC_CHECK(d2h(s, s->h_coff.data(), s->coff.p, (size_t)nc * 8, st));
     unsigned long long nlinks64 = 0;
     if (nc) {
         EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));   // per-side counts as u64 (starts sorted)
@@ -3001,9 +3005,13 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(s->lc8.ensure(n2));
         k_lcnt64<<<grid_for(n2 + 1ull, B), B, 0, st>>>(s->lcnt.as<unsigned int>(), n2, s->skeys.as<unsigned long long>(),
                                                        s->lc8.as<uint8_t>());
-        EC_HIP(hipEventRecord(s->oev[3], st));
-        EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[3], 0));
-        EC_HIP(hipMemcpyAsync(s->h_lc8.data(), s->lc8.p, n2, hipMemcpyDeviceToHost, s->ostream));
+        if (ocopy) {
+            EC_HIP(hipEventRecord(s->oev[3], st));
+            EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[3], 0));
+            EC_HIP(hipMemcpyAsync(s->h_lc8.data(), s->lc8.p, n2, hipMemcpyDeviceToHost, s->ostream));
+        } else {
+            EC_CHECK(d2h(s, s->h_lc8.data(), s->lc8.p, n2, st));
+        }
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
         EC_CHECK(d2h(s, &nlinks64, s->skeys2.as<unsigned long long>() + n2, 8, st));
     }
@@ -3035,7 +3043,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(d2h(s, s->h_links32.data(), s->dcounts.p, nlinks * 4, st));
     }
     EC_CHECK(host_sync(s, st));
-    EC_HIP(hipStreamSynchronize(s->ostream));  // (offsets, characters, link offsets)
+    if (ocopy || pre) EC_HIP(hipStreamSynchronize(s->ostream));  // (offsets, characters, link counts)
     s->last_nchars = nchars;
     s->stats.n_links = nlinks;
 

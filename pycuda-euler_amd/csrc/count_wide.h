@@ -647,10 +647,6 @@ __global__ void __launch_bounds__(512) k_expand_runs(const RunWM *runs, const un
     const int sh = 2 * (k - 1);
     const uint32_t m2 = 2 * rr.m - 1;
     uint64_t wout = wstart[b];
-    auto code_at = [&](uint64_t pos) {
-        const uint32_t w = *reinterpret_cast<const uint32_t *>(rr.buf + (pos & ~3ull));
-        return code2((w >> (8 * (pos & 3))) & 0xFFu);
-    };
     for (uint64_t rb = r0; rb < r1; rb += RUN_BATCH) {
         const unsigned int nb = (unsigned int)min<uint64_t>(RUN_BATCH, r1 - rb);
         // window offsets of the batch's runs: 4 runs a thread, a block scan
@@ -902,6 +898,12 @@ __global__ void __launch_bounds__(512) k_run_codes(const RunWM *runs, const unsi
     }
     if (tid == 0 && b + 1 == gridDim.x) ctab[(uint64_t)gridDim.x * F] = s_off;
 }
+
+template <int SLOTS, int NT>
+__device__ inline void bucket_w_finish(const LSlotW *tab, unsigned int b, long long limit, K128 *dkey, unsigned int *dcnt,
+                                       unsigned long long *dfc, unsigned long long *dft, SubSlotW *sub,
+                                       unsigned int *nsolid, unsigned long long *ndistinct, unsigned int *bmark,
+                                       unsigned int *s_wave, unsigned int *s_pres, unsigned int &s_base);
 
 template <int SLOTS>
 __global__ void __launch_bounds__(WR_NT) k_bucket_wr(const RunWM *runs, const unsigned long long *bstart,
