@@ -1881,11 +1881,9 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     // tables hold whole minimizers (~25 k-mers each): config 5's 2^18 tables of mean 763 keys
     // reached 1808, past the 1664 slots (a numpy model of its genome reproduces the five
     // overflowing tables); 2^19 of mean 381 top out at 1421
-    // runs rolled out in the tables (k_bucket_wr): 1024-slot tables of <= 200 keys, so two
-    // workgroups a CU hold their tables (48 KB) beside the staged codes
-    bool rdir = runs && kn().wide_runs != 2 && kn().wr_slots != 1664;
-    if (rdir && est / (double)(FINE_W << 6) > 200.0) rdir = false;  // (past 2^20 tables: 1664 slots)
-    const double per3 = mb ? (rdir ? 200.0 : 400.0) : 800.0;
+    // (1024-slot tables of <= 200 keys for the run tables, two workgroups a CU, measured 3x
+    // slower on config 5's shape: 355 vs 117 ms)
+    const double per3 = mb ? 400.0 : 800.0;
     if (est / FINE_W > 1800.0) {
         while (sbits < 6 && est / (double)(FINE_W << sbits) > per3) sbits++;
         if (est / (double)(FINE_W << sbits) > per3) return reset();
@@ -1905,7 +1903,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     const int cbits = std::min(bbits, std::min(DS_MAX_CBITS, std::max(1, bbits - fan)));
     const uint64_t Bk = 1ull << bbits, Ck = 1ull << cbits;
     const uint64_t Bt = Bk << sbits;  // tables
-    const unsigned int SLOTS = sbits ? (rdir ? 1024u : 1664u) : (unsigned int)SLOTS_W;
+    const unsigned int SLOTS = sbits ? 1664u : (unsigned int)SLOTS_W;
     mark(s, 2 * EC_STAGE_COUNT);
     EC_CHECK(s->cnt.ensure(Ck * ngroups * 8));
     EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
@@ -2048,9 +2046,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),                \
         s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow, bm,            \
         RunReads{d_reads, d_off, k, mbM, read_base}, wcodes, s->wcodes_tab.as<unsigned long long>())
-    if (rdirect && SLOTS == 1024)
-        EC_BUCKET_WR(1024);
-    else if (rdirect)
+    if (rdirect)
         EC_BUCKET_WR(1664);
     else if (sbits && runs)
         EC_BUCKET_W(1664, RecWM, rwin, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1);

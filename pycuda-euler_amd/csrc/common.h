@@ -38,7 +38,6 @@ struct Knobs {
     bool merge_mix = false;     // EULERHIP_MERGE_MIX: key-hash buckets / owners instead of minimizers
     int skf_merge = 1;          // EULERHIP_SKF_MERGE: error-rich records merged before the filter (0 off, 2 2560-entry tables)
     bool merge_decode = false;  // EULERHIP_MERGE_DECODE: the owner merge reads a decoded copy of the received records
-    int wr_slots = 0;           // EULERHIP_WR_SLOTS=1664: the run-bucket tables at 1664 slots (A/B)
     int wide_runs = 1;          // EULERHIP_WIDE_RUNS: 128-bit keys on minimizer buckets partition runs (0: windows, 2: runs expanded to windows)
     bool wide_general = false;  // EULERHIP_WIDE_GENERAL: k > 32 on the HBM table
     int wide_max_bbits = -1;    // EULERHIP_WIDE_MAX_BBITS: cap the wide buckets (forces overflow)
