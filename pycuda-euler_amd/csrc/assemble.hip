@@ -2787,6 +2787,13 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->svals.ensure(Nn * 4));
     EC_CHECK(s->skeys2.ensure(Nn * 8));
     EC_CHECK(s->svals2.ensure(Nn * 4));
+    // the emission's node maps, cleared before the starts' read-back (the device works through
+    // them while the host waits)
+    EC_CHECK(s->headOf.ensure(Nn * 4));
+    EC_CHECK(s->tailOf.ensure(Nn * 4));
+    EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
+    EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
+    EC_HIP(hipMemsetAsync(&dsc->skew, 0, 4, st));  // k_emit: a position past the character bound
     unsigned long long async_M64 = 0;
     auto starts_pass = [&]() -> int {
     EC_HIP(hipMemsetAsync(s->cidxOf.p, 0xFF, Nn * 4, st));
@@ -2873,13 +2880,23 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         nc += xs[0];
     }
     s->stats.n_contigs = nc;
-    if (nsort)
+    EC_CHECK(s->cwalk.ensure((size_t)std::max(nc, 1u) * sizeof(Walk)));
+    EC_CHECK(s->coff.ensure((size_t)(nc + 1) * 8));
+    EC_CHECK(s->ewalk.ensure((size_t)std::max(nc, 1u) * sizeof(EWalk)));
+    // few starts: order, walks, offsets and emission records in one workgroup (k_starts_small)
+    const bool small = !nx && nc && nc <= SMALL_STARTS && !kn().no_small_starts;
+    if (small)
+        k_starts_small<<<1, SMALL_STARTS_NT, 0, st>>>(
+            s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(), nc, s->upal.as<uint8_t>(),
+            s->PK.as<unsigned int>(), s->RK.as<unsigned int>(), s->PL.as<unsigned int>(), k,
+            s->svals2.as<unsigned int>(), s->cidxOf.as<unsigned int>(), s->coff.as<unsigned long long>(),
+            s->cwalk.as<Walk>(), s->ewalk.as<EWalk>());
+    if (nsort && !small)
         EC_CHECK(sort_pairs(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(),
                             s->svals.as<unsigned int>(), s->svals2.as<unsigned int>(), nsort));
     const unsigned int *sorted_nodes = s->svals2.as<unsigned int>();
+    if (!small) {
     EC_CHECK(s->clen.ensure((size_t)(nc + 1) * 8));
-    EC_CHECK(s->cwalk.ensure((size_t)std::max(nc, 1u) * sizeof(Walk)));
-    EC_CHECK(s->coff.ensure((size_t)(nc + 1) * 8));
     EC_HIP(hipMemsetAsync(s->clen.p, 0, (size_t)(nc + 1) * 8, st));
     if (nc) {
         k_contig_len<<<grid_for(nc, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(),
@@ -2889,6 +2906,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                    nx ? s->x_cid.as<unsigned int>() : nullptr);
     }
     EC_CHECK(scan_u64(s, s->clen.as<unsigned long long>(), s->coff.as<unsigned long long>(), nc + 1));
+    }
     // the total travels with the other results (no round trip here): the character buffer is
     // sized for the bound 2U + nc (k - 1) (a walk covers at most its path; a self-twin path's
     // nodes are up to twice its canonical k-mers)
@@ -2927,13 +2945,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->chars.ensure(std::max<size_t>(chars_bound, 1)));
     EC_CHECK(s->cfirst.ensure((size_t)std::max(nc, 1u) * 4));
     EC_CHECK(s->clast.ensure((size_t)std::max(nc, 1u) * 4));
-    EC_CHECK(s->headOf.ensure(Nn * 4));
-    EC_CHECK(s->tailOf.ensure(Nn * 4));
-    EC_HIP(hipMemsetAsync(s->headOf.p, 0xFF, Nn * 4, st));
-    EC_HIP(hipMemsetAsync(s->tailOf.p, 0xFF, Nn * 4, st));
-    EC_HIP(hipMemsetAsync(&dsc->skew, 0, 4, st));  // k_emit: a position past the character bound
-    EC_CHECK(s->ewalk.ensure((size_t)std::max(nc, 1u) * sizeof(EWalk)));
-    if (nc)
+    if (nc && !small)
         k_ewalk<<<grid_for(nc, B), B, 0, st>>>(s->cwalk.as<Walk>(), s->coff.as<unsigned long long>(), nc,
                                               s->ewalk.as<EWalk>());
     if (U)
@@ -2994,7 +3006,20 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (!nc) s->h_coff[0] = 0;
     if (nc && !ocopy) EC_CHECK(d2h(s, s->h_coff.data(), s->coff.p, (size_t)nc * 8, st));
     unsigned long long nlinks64 = 0;
-    if (nc) {
+    if (nc && small) {
+        // (n2 <= 8192: counts, offsets and the compacted links in one launch; the links' bound
+        // 8 n2 travels with the total, so no second round trip follows)
+        EC_CHECK(s->lc8.ensure(n2));
+        EC_CHECK(s->dcounts.ensure((size_t)n2 * 8 * 4));
+        EC_CHECK(s->skeys2.ensure(8));
+        k_links_small<<<1, SMALL_LINK_NT, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(), n2,
+                                                   s->lc8.as<uint8_t>(), s->dcounts.as<uint32_t>(),
+                                                   s->skeys2.as<unsigned long long>());
+        EC_CHECK(d2h(s, s->h_lc8.data(), s->lc8.p, n2, st));
+        EC_CHECK(s->h_links32.resize((size_t)n2 * 8));
+        EC_CHECK(d2h(s, s->h_links32.data(), s->dcounts.p, (size_t)n2 * 8 * 4, st));
+        EC_CHECK(d2h(s, &nlinks64, s->skeys2.p, 8, st));
+    } else if (nc) {
         EC_CHECK(s->skeys.ensure(((size_t)n2 + 1) * 8));   // per-side counts as u64 (starts sorted)
         EC_CHECK(s->skeys2.ensure(((size_t)n2 + 1) * 8));  // their exclusive scan = link offsets
         // (the counts as bytes in a buffer of their own: the scan's temporary storage is s->tmp)
@@ -3028,17 +3053,19 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     }
     if (pre && nchars > pre) EC_HIP(hipEventSynchronize(s->oev[1]));  // (before h_chars may move)
     EC_CHECK(s->h_chars.resize(nchars));
+    bool again = nchars > pre;  // (a second round trip: characters or links still to copy)
     if (nchars > pre) EC_CHECK(d2h(s, s->h_chars.data(), s->chars.p, nchars, st));
     const uint64_t nlinks = nlinks64;
-    EC_CHECK(s->h_links32.resize(nlinks));
-    if (nlinks) {
+    EC_CHECK(s->h_links32.resize(nlinks));  // (small: the copied bound's first nlinks stay)
+    if (nlinks && !small) {
+        again = true;
         EC_CHECK(s->dcounts.ensure(nlinks * 4));
         k_links_compact<uint32_t><<<grid_for(n2, B), B, 0, st>>>(s->lk.as<long long>(), s->lcnt.as<unsigned int>(),
                                                                 s->skeys2.as<unsigned long long>(), n2,
                                                                 s->dcounts.as<uint32_t>());
         EC_CHECK(d2h(s, s->h_links32.data(), s->dcounts.p, nlinks * 4, st));
     }
-    EC_CHECK(host_sync(s, st));
+    if (again) EC_CHECK(host_sync(s, st));
     if (ocopy || pre) EC_HIP(hipStreamSynchronize(s->ostream));  // (offsets, characters, link counts)
     s->last_nchars = nchars;
     s->stats.n_links = nlinks;

@@ -42,6 +42,7 @@ void refresh_knobs() {
         k.merge_decode = flag("EULERHIP_MERGE_DECODE");
         k.skf_merge = num("EULERHIP_SKF_MERGE", 1);
         k.wide_runs = num("EULERHIP_WIDE_RUNS", 1);
+        k.no_small_starts = flag("EULERHIP_NO_SMALL_STARTS");
         k.wide_general = flag("EULERHIP_WIDE_GENERAL");
         k.wide_max_bbits = num("EULERHIP_WIDE_MAX_BBITS", -1);
         k.wide_l3 = num("EULERHIP_WIDE_L3", 0);

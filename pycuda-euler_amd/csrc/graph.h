@@ -774,6 +774,85 @@ __global__ void __launch_bounds__(256) k_ewalk(const Walk *cwalk, const unsigned
     }
 }
 
+// Few contigs (the headline: one): the order, walk geometry, offsets and emission records of
+// all starts in one workgroup -- the radix sort, length, scan and k_ewalk launches it replaces
+// were each a few microseconds of work behind ~10-30 us of host launch time.  Starts sorted by
+// first event (bitonic in LDS; first events are distinct, so it equals the stable radix sort),
+// contig i = k - 1 + its walk's node count characters at coff[i], coff[nc] = their total.
+constexpr unsigned int SMALL_STARTS = 4096;
+constexpr unsigned int SMALL_STARTS_NT = 1024;
+__global__ void __launch_bounds__(SMALL_STARTS_NT) k_starts_small(
+    const unsigned long long *skeys, const unsigned int *svals, unsigned int nc, const uint8_t *upal,
+    const unsigned int *PK, const unsigned int *RK, const unsigned int *PL, int k, unsigned int *sorted,
+    unsigned int *cidxOf, unsigned long long *coff, Walk *cwalk, EWalk *ew) {
+    __shared__ unsigned long long s_k[SMALL_STARTS];
+    __shared__ unsigned int s_v[SMALL_STARTS];
+    __shared__ unsigned long long s_sum[SMALL_STARTS_NT];
+    const unsigned int tid = threadIdx.x;
+    unsigned int P = 1;
+    while (P < nc) P <<= 1;
+    for (unsigned int i = tid; i < P; i += SMALL_STARTS_NT) {
+        s_k[i] = i < nc ? skeys[i] : ~0ull;
+        s_v[i] = i < nc ? svals[i] : 0u;
+    }
+    __syncthreads();
+    for (unsigned int size = 2; size <= P; size <<= 1)
+        for (unsigned int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (unsigned int i = tid; i < P / 2; i += SMALL_STARTS_NT) {
+                const unsigned int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned long long a = s_k[lo], b = s_k[hi];
+                if ((a > b) == up) {
+                    s_k[lo] = b;
+                    s_k[hi] = a;
+                    const unsigned int t = s_v[lo];
+                    s_v[lo] = s_v[hi];
+                    s_v[hi] = t;
+                }
+            }
+            __syncthreads();
+        }
+    // four consecutive contigs a thread: walks, lengths, then one block scan of the sums
+    unsigned long long len[4], run = 0;
+    Walk w[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const unsigned int i = 4 * tid + u;
+        len[u] = 0;
+        if (i < nc) {
+            const unsigned int s = s_v[i];
+            sorted[i] = s;
+            cidxOf[PK[s] & ~CYC] = i;
+            w[u] = walk_of(upal, PK, RK, PL, s);
+            len[u] = (unsigned long long)(k - 1) + w[u].len;
+        }
+        run += len[u];
+    }
+    s_sum[tid] = run;
+    __syncthreads();
+    for (unsigned int o = 1; o < SMALL_STARTS_NT; o <<= 1) {
+        const unsigned long long add = tid >= o ? s_sum[tid - o] : 0ull;
+        __syncthreads();
+        s_sum[tid] += add;
+        __syncthreads();
+    }
+    unsigned long long c = s_sum[tid] - run;  // exclusive
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const unsigned int i = 4 * tid + u;
+        if (i < nc) {
+            coff[i] = c;
+            cwalk[i] = w[u];
+            EWalk e;
+            e.w = w[u];
+            e.coff = c;
+            ew[i] = e;
+        }
+        c += len[u];
+    }
+    if (tid == SMALL_STARTS_NT - 1) coff[nc] = s_sum[tid];
+}
+
 // emit: every node finds its contig through its path key, computes its walk position and
 // writes its chars (contig_to_string:44-45: first node k chars, later nodes their last base).
 template <typename Ops>
@@ -881,6 +960,41 @@ __global__ void __launch_bounds__(256) k_links_compact(const long long *lk, cons
         const unsigned int c = lcnt[t];
         for (unsigned int j = 0; j < c; j++) out[loff[t] + j] = (T)lk[t * 8 + j];
     }
+}
+
+// Few contigs (k_starts_small's bound, n2 = 2 nc <= 8192 sides): the per-side link counts as
+// bytes, their offsets and the compacted links in one workgroup, the total to *nlinks -- the
+// count, scan and compaction launches with the host round trip between them in one launch
+constexpr unsigned int SMALL_LINK_NT = 1024;
+__global__ void __launch_bounds__(SMALL_LINK_NT) k_links_small(const long long *lk, const unsigned int *lcnt,
+                                                              unsigned int n2, uint8_t *c8, uint32_t *out,
+                                                              unsigned long long *nlinks) {
+    __shared__ unsigned int s_sum[SMALL_LINK_NT];
+    const unsigned int tid = threadIdx.x;
+    unsigned int c[8], run = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const unsigned int i = 8 * tid + u;
+        c[u] = i < n2 ? lcnt[i] : 0u;
+        if (i < n2) c8[i] = (uint8_t)c[u];
+        run += c[u];
+    }
+    s_sum[tid] = run;
+    __syncthreads();
+    for (unsigned int o = 1; o < SMALL_LINK_NT; o <<= 1) {
+        const unsigned int add = tid >= o ? s_sum[tid - o] : 0u;
+        __syncthreads();
+        s_sum[tid] += add;
+        __syncthreads();
+    }
+    unsigned int o = s_sum[tid] - run;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const unsigned long long side = 8ull * tid + u;
+        for (unsigned int j = 0; j < c[u]; j++) out[o + j] = (uint32_t)lk[side * 8 + j];
+        o += c[u];
+    }
+    if (tid == SMALL_LINK_NT - 1) *nlinks = s_sum[tid];
 }
 
 // ordered dict of build(): every valid oriented node with its first event (sort key)
