@@ -614,9 +614,12 @@ __device__ inline bool is_start(const uint8_t *upal, const unsigned long long *d
     if ((x & 1) && upal[x >> 1]) return false;
     if (excl && excl[x >> 1]) return false;  // (extended.h: a component with one-way links)
     f = first_event(dfc, dft, x);
+    // a <= f (x lies on its path), so f == min(a, b) iff f == a && a <= b: the twin path's
+    // gather only for the one node a path holds at its minimum
     const unsigned long long a = path_min(PK, PM, x);
+    if (f != a) return false;
     const unsigned long long b = path_min(PK, PM, twin_node(upal, x));
-    return f == (a < b ? a : b);
+    return a <= b;
 }
 
 // Starts are compacted in two passes, RULER_CHUNK nodes per block: counts, one scan, then
