@@ -2413,6 +2413,8 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
     while ((1ull << (rounds - 1)) < (unsigned long long)nr) rounds++;
     rounds = std::min(rounds + 1, 63);
     RJump *bufs[2] = {s->st0.as<RJump>(), s->st1.as<RJump>()};
+    // (the rounds only raise their flags: clear what an unconverged queued ranking left)
+    EC_HIP(hipMemsetAsync(dsc->active, 0, sizeof(dsc->active), st));
     for (int r = 0; r < rounds; r++)
         k_rjump<<<grid_for(nr, B), B, 0, st>>>(bufs[r & 1], bufs[(r + 1) & 1], nr, N, r ? &dsc->active[r - 1] : nullptr,
                                               &dsc->active[r], &dsc->final_sel, (unsigned)((r + 1) & 1));

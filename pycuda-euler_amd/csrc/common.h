@@ -57,7 +57,7 @@ struct Knobs {
     int wide_mb = -1;        // EULERHIP_WIDE_MB=0: 128-bit keys bucketed by mix128, not by minimizer
     int sruler_mask = 0;     // EULERHIP_SRULER_MASK: first ruler pass of the super list takes 1 / (mask + 1)
     int join_mb = -1;        // EULERHIP_JOIN_MB=0: junctions of minimizer-bucketed keys bucketed by mix128
-    bool no_small_starts = false; // EULERHIP_NO_SMALL_STARTS: few starts through the radix sort + scan launches (A/B)
+    bool no_small_starts = false; // EULERHIP_NO_SMALL_STARTS: short lists on the general launches (k_starts_small, k_links_small off)
 };
 void refresh_knobs();
 const Knobs &kn();
