@@ -127,6 +127,10 @@ int ec_session_create(ec_session **out, int device);
 #define EC_OWN_STREAM ((void *)-1)
 int ec_session_set_stream(ec_session *s, void *hip_stream);
 int ec_session_destroy(ec_session *s);
+/* Device memory held by the session buffers of this process (bytes) and its high-water mark;
+ * reset != 0 restarts the mark at the current holding after reading it.  EULERHIP_MEMLOG=1
+ * logs every buffer of >= 1 GB to stderr as it is allocated. */
+int ec_mem_stats(uint64_t *held, uint64_t *peak, int reset);
 
 /* Reads already resident in device memory: d_reads = concatenated ASCII, d_offsets[nreads+1]
  * = byte offsets (uint64).  limit: keep k-mers whose dict count > limit (build(limit=1)). */
@@ -318,6 +322,9 @@ uint64_t ec_reads_span(const ec_reads *r, uint64_t first, uint64_t count);
 /* copy reads [first, first+count): their bases and count+1 offsets rebased to 0 */
 int ec_reads_copy(const ec_reads *r, uint64_t first, uint64_t count, uint8_t *bases, uint64_t *offsets);
 void ec_reads_free(ec_reads *r);
+/* ec_reads_free keeps one page-locked code buffer for the next EC_READS_PACKED load; this
+ * releases it (teardown). */
+void ec_reads_release_pool(void);
 /* format | EC_READS_PACKED: ec_reads_load writes the bases straight as 2-bit codes (4 a byte, the
  * layout of ec_assemble_packed_host) into page-locked memory plus the bytes other than A/C/G/T as
  * (position, byte) exceptions -- no ASCII copy, no separate ec_pack_reads pass; read_len = the

@@ -44,12 +44,26 @@
 #include "rank_tile.h"
 #include "junction.h"
 
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 
 namespace ec {
 
 // ---------------------------------------------------------------------------------------
 // host side
+// device bytes the process's session buffers hold, and their high-water mark (ec_mem_stats:
+// the per-rank HBM of the sharded and streaming paths is reported from these)
+std::atomic<unsigned long long> g_hbm_held{0}, g_hbm_peak{0};
+inline void hbm_account(long long d) {
+    const unsigned long long now = g_hbm_held.fetch_add((unsigned long long)d) + (unsigned long long)d;
+    unsigned long long pk = g_hbm_peak.load();
+    while (now > pk && !g_hbm_peak.compare_exchange_weak(pk, now)) {
+    }
+}
+bool memlog_on();
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -60,20 +74,26 @@ struct DevBuf {
         // hipMalloc pair -- on every call that is a little larger than the last
         size_t want = std::max<size_t>(bytes, 256);
         if (cap) want += want / 8;
-        if (p) hipFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
             set_error("hipMalloc(%zu) failed", want);
             return EC_ERR_NOMEM;
         }
         cap = want;
+        hbm_account((long long)want);
+        if (want >= (1ull << 30) && memlog_on())  // EULERHIP_MEMLOG=1: large buffers and their call sites
+            fprintf(stderr, "[eulerhip mem] +%.2f GB (held %.2f GB) at %p\n", want / 1e9, g_hbm_held.load() / 1e9,
+                    __builtin_return_address(0));
         return EC_OK;
     }
     template <typename T>
     T *as() const { return reinterpret_cast<T *>(p); }
     void release() {
-        if (p) hipFree(p);
+        if (p) {
+            hipFree(p);
+            hbm_account(-(long long)cap);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -3703,6 +3723,13 @@ int ec_session_set_stream(ec_session *s, void *hip_stream) {
     return EC_OK;
 }
 
+int ec_mem_stats(uint64_t *held, uint64_t *peak, int reset) {
+    if (held) *held = g_hbm_held.load();
+    if (peak) *peak = g_hbm_peak.load();
+    if (reset) g_hbm_peak.store(g_hbm_held.load());
+    return EC_OK;
+}
+
 int ec_session_destroy(ec_session *s) {
     if (!s) return EC_OK;
     hipSetDevice(s->device);
@@ -4502,13 +4529,21 @@ int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const ui
     unsigned int *flag = s->jcnt.as<unsigned int>(), *nout = flag + 1;
     EC_CHECK(s->jout.ensure(std::max<uint64_t>(n, 1) * sizeof(LinkRec)));
     LinkRec *outbox = s->jout.as<LinkRec>();
-    // join buckets: ~n / 2 junction groups, <= ~900 a 2048-slot table (<= 2^14 buckets), 4096
-    // slots past that
-    int bt = 0;
-    while (bt < 14 && (double)n / 2.0 / (double)(1ull << bt) > 900.0) bt++;
-    for (int attempt = 0;; attempt++) {
-        const bool big = (double)n / 2.0 / (double)(1ull << bt) > 1500.0 || attempt > 0;
+    // join buckets: ~n / 2 junction groups, <= ~900 a 2048-slot table; at most 2^14 buckets (the
+    // counting sort's LDS histogram), each split into 2^sb sub-buckets past that.  A table that
+    // overflows (skewed junction hashes) retries with 4096 slots, then finer buckets, then more
+    // sub-buckets (EULERHIP_JUNCTION_BT / _SB / _CLAIM force the split / a smaller claim cap)
+    const int btmax = kn().junction_bt >= 0 ? std::min(kn().junction_bt, 14) : 14;
+    const double groups = (double)n / 2.0;
+    int bt = 0, sb = 0;
+    while (bt < btmax && groups / (double)(1ull << bt) > 900.0) bt++;
+    while (sb < 8 && groups / (double)(1ull << (bt + sb)) > 900.0) sb++;
+    if (kn().junction_sb > sb) sb = std::min(kn().junction_sb, 8);
+    bool big = groups / (double)(1ull << (bt + sb)) > 1500.0;
+    for (;;) {
         const unsigned int nb = 1u << bt;
+        const unsigned int claim = kn().junction_claim > 0 ? (unsigned int)kn().junction_claim
+                                                           : (big ? 4096u : 2048u) - 1u;
         EC_CHECK(s->joid.ensure(std::max<uint64_t>(n, 1) * 4));
         EC_HIP(hipMemsetAsync(flag, 0, 8, st));
         if (n) k_junction_bucket<R><<<grid_for(n, B), B, 0, st>>>(d_recs, n, bt, s->joid.as<unsigned int>());
@@ -4518,11 +4553,12 @@ int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const ui
             if (big)
                 k_junction_join<4096, 512, R><<<nb, 512, 0, st>>>(d_recs, s->midx2.as<unsigned int>(), bstart, n0, n1,
                                                                   s->succ.as<unsigned int>(), outbox, nout,
-                                                                  (unsigned int)n, flag);
+                                                                  (unsigned int)n, flag, bt, sb, claim);
             else
                 k_junction_join<2048, 512, R><<<nb, 512, 0, st>>>(d_recs, s->midx2.as<unsigned int>(), bstart, n0, n1,
                                                                   s->succ.as<unsigned int>(), outbox, nout,
-                                                                  (unsigned int)n, flag);
+                                                                  (unsigned int)n, flag, bt, sb, claim);
+            EC_HIP(hipGetLastError());
         }
         // outbox -> destination-major link records, sized by n on the host (the count stays on
         // the device: one read-back for the flags and the destinations' counts)
@@ -4543,12 +4579,16 @@ int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const ui
             set_error("junction join: link outbox overflow");
             return EC_ERR_STATE;
         }
-        if (hf[0] & 1u) {  // a table past its slots (skewed junction hashes): finer buckets, bigger tables
-            if (attempt >= 2 || bt >= 14) {
-                set_error("junction join: a bucket of %llu records overflows its table", (unsigned long long)n);
+        if (hf[0] & 1u) {  // a table past its slots: bigger tables, finer buckets, more sub-buckets
+            // (succ: a failed attempt's local links are the same links the retry writes)
+            if (!big) big = true;
+            else if (bt < btmax) bt++;
+            else if (sb < 8) sb++;
+            else {
+                set_error("junction join: a bucket of %llu records overflows its table at 2^%d x 2^%d buckets",
+                          (unsigned long long)n, bt, sb);
                 return EC_ERR_CAPACITY;
             }
-            bt++;
             s->stats.table_retries++;
             continue;
         }

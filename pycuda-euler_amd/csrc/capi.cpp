@@ -48,6 +48,9 @@ void refresh_knobs() {
         k.wide_l3 = num("EULERHIP_WIDE_L3", 0);
         k.join_links = num("EULERHIP_JOIN_LINKS", -1);
         k.join_cap = num("EULERHIP_JOIN_CAP", 0);
+        k.junction_bt = num("EULERHIP_JUNCTION_BT", -1);
+        k.junction_sb = num("EULERHIP_JUNCTION_SB", 0);
+        k.junction_claim = num("EULERHIP_JUNCTION_CLAIM", 0);
         if (const char *e = getenv("EULERHIP_WIDE_L3_CAP")) k.wide_l3_cap = atoll(e);
         k.host_chunks = num("EULERHIP_HOST_CHUNKS", 0);
         k.sk2_stats = flag("EULERHIP_SK2_STATS");
@@ -63,6 +66,10 @@ void refresh_knobs() {
         k.sruler_mask = num("EULERHIP_SRULER_MASK", 0);
     }
     g_knobs = k;
+}
+bool memlog_on() {
+    static const bool on = getenv("EULERHIP_MEMLOG") != nullptr;
+    return on;
 }
 }  // namespace ec
 

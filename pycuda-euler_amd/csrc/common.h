@@ -44,6 +44,9 @@ struct Knobs {
     int wide_l3 = 0;            // EULERHIP_WIDE_L3: third partition level of 2^n sub-buckets at any size
     long long wide_l3_cap = 0;  // EULERHIP_WIDE_L3_CAP: its sub-bucket capacity (forces its overflow)
     int join_links = -1;        // EULERHIP_JOIN_LINKS: links by the half-edge join 1 = always, 0 = never
+    int junction_bt = -1;       // EULERHIP_JUNCTION_BT: most join bucket bits of the junction join (<= 14)
+    int junction_sb = 0;        // EULERHIP_JUNCTION_SB: at least this many sub-bucket bits
+    int junction_claim = 0;     // EULERHIP_JUNCTION_CLAIM: slots a join table may claim (forces overflows)
     int join_cap = 0;           // EULERHIP_JOIN_CAP: its level regions' capacity (forces the fallback)
     int host_chunks = 0;        // EULERHIP_HOST_CHUNKS: host-input chunks (0 = ~32 MiB each)
     bool sk2_stats = false;     // EULERHIP_SK2_STATS: k_skbucket dedup statistics on stderr

@@ -48,6 +48,7 @@ struct ec_reads {
     size_t codes_cap = 0;
     std::vector<uint64_t> exc_pos;
     std::vector<uint8_t> exc_byte;
+    int staged_dev = -1;    // device of the last ec_stage_packed_reads: its async H2D copy may still read codes
     ~ec_reads();
 };
 
@@ -196,8 +197,20 @@ int host_threads(int threads) {
 }  // namespace
 
 ec_reads::~ec_reads() {
-    if (codes && pinned) pinned_give(codes, codes_cap);
-    else free(codes);
+    if (codes && pinned) {
+        // a staged batch's copy (ec_stage_packed_host returns before it ends) must not read a
+        // buffer the next load is already refilling: the copies of that device drain first
+        if (staged_dev >= 0) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(staged_dev);
+            (void)hipDeviceSynchronize();
+            (void)hipSetDevice(cur);
+        }
+        pinned_give(codes, codes_cap);
+    } else {
+        free(codes);
+    }
 }
 
 extern "C" {
@@ -533,9 +546,12 @@ int ec_stage_packed_reads(ec_session *s, const ec_reads *r) {
         return EC_ERR_ARG;
     }
     const uint64_t R = r->offsets.size() - 1;
-    return ec_stage_packed_host(s, r->codes, r->nbases, r->read_len ? nullptr : r->offsets.data(), R, r->read_len,
-                                r->exc_pos.empty() ? nullptr : r->exc_pos.data(),
-                                r->exc_byte.empty() ? nullptr : r->exc_byte.data(), r->exc_pos.size());
+    const int rc = ec_stage_packed_host(s, r->codes, r->nbases, r->read_len ? nullptr : r->offsets.data(), R,
+                                        r->read_len, r->exc_pos.empty() ? nullptr : r->exc_pos.data(),
+                                        r->exc_byte.empty() ? nullptr : r->exc_byte.data(), r->exc_pos.size());
+    int dev = 0;  // (ec_stage_packed_host made the session's device current)
+    if (hipGetDevice(&dev) == hipSuccess) const_cast<ec_reads *>(r)->staged_dev = dev;
+    return rc;
 }
 
 // the fused assembly straight from a packed read set (its page-locked codes go over PCIe)
@@ -580,6 +596,13 @@ int ec_reads_copy(const ec_reads *r, uint64_t first, uint64_t count, uint8_t *ba
 }
 
 void ec_reads_free(ec_reads *r) { delete r; }
+
+void ec_reads_release_pool(void) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_pool_p) (void)hipHostFree(g_pool_p);
+    g_pool_p = nullptr;
+    g_pool_cap = 0;
+}
 
 // ASCII -> 2 bits per base + exceptions (ec_assemble_packed_host's layout).  Threads own
 // base ranges aligned to 4 (whole code bytes); exceptions are counted per range, then written

@@ -135,16 +135,30 @@ static_assert(sizeof(LinkRec) == 8, "link record layout");
 // junction in an LDS table (as k_half_join: two CASes on the key's 63-bit halves, one id per
 // side whose MANY bit marks a second distinct id; ids carry the palindrome flag above bit 32).
 // Links of nodes in [n0, n1) go to succ, others to the link outbox (wave-aggregated append).
+//
+// More junctions than 2^14 buckets of tables hold (a rank past ~4.7 * 10^7 junctions): every
+// bucket is split again by the next sbits hash bits into 2^sbits sub-buckets, which the
+// workgroup joins one after the other in its table (its records read once per sub-bucket; the
+// bucket sort stays at <= 2^14 bins, the LDS histogram's limit).  claim: slots a table may
+// claim (SLOTS - 1; smaller only to test the overflow retries).
 template <int SLOTS, int NT, typename R>
 __global__ void __launch_bounds__(NT) k_junction_join(const R *recs, const unsigned int *perm,
                                                       const unsigned long long *bstart, unsigned int n0,
                                                       unsigned int n1, unsigned int *succ, LinkRec *outbox,
-                                                      unsigned int *nout, unsigned int outcap, unsigned int *overflow) {
+                                                      unsigned int *nout, unsigned int outcap, unsigned int *overflow,
+                                                      int bt, int sbits, unsigned int claim) {
     constexpr unsigned long long EMPTY = ~0ull, MANY = 1ull << 62;
+    // 4 SLOTS x 8 B of tables: 64 KB at 2048 slots, 128 KB at 4096 -- gfx950's 160 KB of LDS
+    // per workgroup (earlier CDNA parts allow 64 KB: the 4096-slot table needs MI355X)
+    static_assert(4 * SLOTS * 8 + 64 <= 160 * 1024, "junction tables exceed gfx950's LDS per workgroup");
     __shared__ unsigned long long w1[SLOTS], w2[SLOTS];
     __shared__ unsigned long long ids[2][SLOTS];
     __shared__ unsigned int s_over[2];
+    __shared__ unsigned int s_cnt, s_base;
     const unsigned int b = blockIdx.x;
+    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
+    const unsigned int nsub = 1u << sbits;
+    for (unsigned int sub = 0; sub < nsub; sub++) {
     for (int i = threadIdx.x; i < SLOTS; i += NT) {
         w1[i] = 0;
         w2[i] = 0;
@@ -156,12 +170,12 @@ __global__ void __launch_bounds__(NT) k_junction_join(const R *recs, const unsig
         s_over[1] = 0;
     }
     __syncthreads();
-    const uint64_t r0 = bstart[b], r1 = bstart[b + 1];
     for (uint64_t base = r0; base < r1; base += NT) {
         const uint64_t i = base + threadIdx.x;
-        const bool valid = i < r1;
+        bool valid = i < r1;
         R r{};
         if (valid) r = recs[perm[i]];
+        if (sbits && valid) valid = (unsigned int)((jhash(r) << bt) >> (64 - sbits)) == sub;
         const K128 o = jkey(r);
         const unsigned long long a1 = wide_w1(o), a2 = wide_w2(o);
         unsigned int slot = (unsigned int)(((uint64_t)(uint32_t)jhash(r) * SLOTS) >> 32);
@@ -176,7 +190,7 @@ __global__ void __launch_bounds__(NT) k_junction_join(const R *recs, const unsig
         while (__any(miss)) {
             if (miss) {
                 if (a == 0) {
-                    if (atomicAdd(&s_over[1], 1u) >= SLOTS - 1) {
+                    if (atomicAdd(&s_over[1], 1u) >= claim) {
                         s_over[0] = 1;
                         a = a1;
                         bw = a2;
@@ -209,8 +223,8 @@ __global__ void __launch_bounds__(NT) k_junction_join(const R *recs, const unsig
         }
     }
     __syncthreads();
-    if (s_over[0]) {
-        if (threadIdx.x == 0) atomicAdd(overflow, 1u);
+    if (s_over[0]) {  // (uniform: the host retries with finer buckets)
+        if (threadIdx.x == 0) atomicOr(overflow, 1u);
         return;
     }
     // links: local ones written at once; the other ranks' into the outbox at one global
@@ -235,7 +249,6 @@ __global__ void __launch_bounds__(NT) k_junction_join(const R *recs, const unsig
         if (!rf[2 * q + 1]) succ[ty] = tx;
         nr += rf[2 * q] + rf[2 * q + 1];
     }
-    __shared__ unsigned int s_cnt, s_base;
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     const unsigned int my = nr ? atomicAdd(&s_cnt, nr) : 0u;
@@ -249,6 +262,8 @@ __global__ void __launch_bounds__(NT) k_junction_join(const R *recs, const unsig
         if (p < outcap) outbox[p] = LinkRec{rt[j], rv[j]};
         else atomicOr(overflow, 2u);
         p++;
+    }
+    __syncthreads();  // (the next sub-bucket clears the tables)
     }
 }
 

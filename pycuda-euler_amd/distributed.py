@@ -506,7 +506,9 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     segment of the gathered solid set only ("each GPU builds its local graph partition").
     finish "partitioned" (the "auto" choice where the ids have minimizer locality): every rank
     ranks / emits its own segment and ONLY RANK 0 returns the result (None on the others);
-    "replicated": the successor parts are all-gathered and every rank returns the result."""
+    "replicated": the successor parts are all-gathered and every rank returns the result.  An
+    engine without graph_place runs the replicated finish for "partitioned" too (with a
+    RuntimeWarning), and then every rank returns the result."""
     import time
 
     if partitioned is None:
@@ -538,6 +540,13 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     src_base, src_lfb = [m[0] for m in metas], [m[1] for m in metas]
     tick("alltoall")
     junction = partitioned and finish == "partitioned" and hasattr(engine, "graph_place")
+    if partitioned and finish == "partitioned" and not junction:
+        # (an engine without the junction steps cannot keep only its segment: the replicated
+        # finish below gives the same result, and every rank returns it)
+        import warnings
+
+        warnings.warn("sharded_assemble: the engine cannot place segments (no graph_place); "
+                      "finish='partitioned' runs the replicated finish", RuntimeWarning, stacklevel=2)
     if junction:  # each rank keeps its own segment: the links come out of the junction join
         ur = engine.merge_owned_from(received, src_bytes, src_base, src_lfb, k, limit, flags, export=False)
         tick("merge")

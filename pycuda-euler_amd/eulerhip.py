@@ -98,6 +98,7 @@ _SIGS = {
     "ec_session_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int]),
     "ec_session_set_stream": (ctypes.c_int, [_P, _P]),
     "ec_session_destroy": (ctypes.c_int, [_P]),
+    "ec_mem_stats": (ctypes.c_int, [ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.c_int]),
     "ec_assemble_device": (ctypes.c_int, [_P, _P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_assemble_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_assemble_packed_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_uint32, _P, _P, _U64, ctypes.c_int,
@@ -155,6 +156,14 @@ def check(rc):
             raise AlphabetError(rc, msg)
         raise EulerHipError(rc, msg)
     return rc
+
+
+def mem_stats(reset=False):
+    """(held, peak): device bytes this process's session buffers hold and their high-water mark
+    (ec_mem_stats); reset restarts the mark at the current holding"""
+    h, p = _U64(0), _U64(0)
+    check(lib().ec_mem_stats(ctypes.byref(h), ctypes.byref(p), int(bool(reset))))
+    return int(h.value), int(p.value)
 
 
 def stage_names():

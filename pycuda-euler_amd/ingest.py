@@ -21,6 +21,7 @@ eulerhip.register("ec_reads_bases", _U64, [_P])
 eulerhip.register("ec_reads_span", _U64, [_P, _U64, _U64])
 eulerhip.register("ec_reads_copy", ctypes.c_int, [_P, _U64, _U64, _P, _P])
 eulerhip.register("ec_reads_free", None, [_P])
+eulerhip.register("ec_reads_release_pool", None, [])
 eulerhip.register("ec_reads_packed_info", ctypes.c_int, [_P, _P, _P, _P])
 eulerhip.register("ec_reads_packed_copy", ctypes.c_int, [_P, _P, _P, _P])
 eulerhip.register("ec_assemble_packed_reads", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_uint])
@@ -118,6 +119,11 @@ class ReadSet:
 
     def __del__(self):
         self.close()
+
+
+def release_pool():
+    """free the page-locked code buffer ec_reads_free keeps for the next packed load (teardown)"""
+    eulerhip.lib().ec_reads_release_pool()
 
 
 def load_reads(path, fmt=None, threads=0, fasta_mode="records", first=0, count=None):

@@ -357,3 +357,27 @@ def test_exchange_record_formats(engines, compact, k):
         assert P == ref["n_positions"]
         assert res.contig_bytes == ref["contig_chars"] and res.links == oracle.unpack_links(ref), finish
         assert res.stats.n_dict == ref["n_dict"]
+
+
+@pytest.mark.parametrize("knobs", [{"EULERHIP_JUNCTION_BT": "2", "EULERHIP_JUNCTION_SB": "3"},
+                                   {"EULERHIP_JUNCTION_BT": "1", "EULERHIP_JUNCTION_CLAIM": "64"},
+                                   {"EULERHIP_JUNCTION_CLAIM": "24"}])
+@pytest.mark.parametrize("k", [31, 51])
+def test_junction_join_split_and_retries(engines, monkeypatch, knobs, k):
+    """the junction join past 2^14 buckets' worth of junctions (a rank of > ~4.7 * 10^7 keys):
+    every bucket split into sub-buckets joined one after the other in one table, forced here on a
+    small set by capping the bucket bits; and a table that overflows (claim cap forced small)
+    retried with 4096-slot tables, finer buckets, then more sub-buckets -- the same contigs, links
+    and dict size as the oracle (a rank used to fail with EC_ERR_CAPACITY at 2^14 buckets)"""
+    import distributed
+
+    for n, v in knobs.items():
+        monkeypatch.setenv(n, v)
+    buf, off = make_reads(40_000, 12_000, 150 if k > 32 else 100, 9300 + k, err=0.002)
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    world = 2
+    res, P = distributed.local_sharded_assemble(engines[:world], buf, off, k, 1, finish="partitioned")
+    assert P == ref["n_positions"]
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert res.links == oracle.unpack_links(ref)

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20261019)
     ap.add_argument("--finish", default="partitioned", choices=["partitioned", "replicated"],
                     help="partitioned: every rank ranks / emits its own segment (distributed.partitioned_finish)")
+    ap.add_argument("--read-base", type=int, default=0,
+                    help="global id of the first read (one rank of a larger job: config 5's rank 3 of 8 = 37500000)")
     ap.add_argument("--weak", action="store_true",
                     help="bench.py's default N > 1 mode: every rank its own --reads reads (synth part = rank)")
     a = ap.parse_args()
@@ -47,8 +49,13 @@ def main():
         for r in range(world):
             lo, hi = distributed.shard_range(a.reads, r, world)
             shards.append((torch.from_numpy(np.ascontiguousarray(buf[int(off[lo]):int(off[hi])])).cuda(),
-                           torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).cuda(), hi - lo, lo))
+                           torch.from_numpy((off[lo:hi + 1] - off[lo]).astype(np.int64)).cuda(), hi - lo,
+                           a.read_base + lo))
+        del buf, off
     torch.cuda.synchronize()
+    import eulerhip
+    eulerhip.mem_stats(reset=True)
+    torch.cuda.reset_peak_memory_stats()
     for rep in range(a.reps):
         t = {}
 
@@ -191,6 +198,11 @@ def main():
         print("rep %d  ranks %d  per-rank max ms: %s  sum %.2f  exchanged bytes/rank ~%.0f MB, gathered %.0f MB%s" % (
             rep, world, mx_ph, sum(mx_ph.values()),
             sum(c for c in sends[0][1]) * rbs[0] / 1e6, xb / 1e6, extra))
+        held, peak = eulerhip.mem_stats()
+        print("rep %d  HBM: session buffers of all %d simulated ranks held %.1f GB, peak %.1f GB; torch tensors "
+              "(reads, exchange buffers) peak %.1f GB; device total %.1f GB" % (
+                  rep, world, held / 1e9, peak / 1e9, torch.cuda.max_memory_allocated() / 1e9,
+                  torch.cuda.mem_get_info()[1] / 1e9), flush=True)
     print("contigs", len(res.contig_offsets) - 1, "chars", len(res.contig_bytes))
 
 
