@@ -131,6 +131,14 @@ int ec_session_destroy(ec_session *s);
  * reset != 0 restarts the mark at the current holding after reading it.  EULERHIP_MEMLOG=1
  * logs every buffer of >= 1 GB to stderr as it is allocated. */
 int ec_mem_stats(uint64_t *held, uint64_t *peak, int reset);
+/* Release the session's device buffers of at least min_bytes (0: all but its scalars) and every
+ * device state they held (dense k-mer arrays, a loaded or placed graph): the next call starts
+ * from its inputs; results already copied to host memory stay fetchable.  The sharded path
+ * calls it after a large shard's export, so the owner merge and graph phase get the count's
+ * memory (distributed.py). */
+int ec_session_trim(ec_session *s, uint64_t min_bytes);
+/* Device bytes the session's buffers hold. */
+uint64_t ec_session_bytes(ec_session *s);
 
 /* Reads already resident in device memory: d_reads = concatenated ASCII, d_offsets[nreads+1]
  * = byte offsets (uint64).  limit: keep k-mers whose dict count > limit (build(limit=1)). */

@@ -45,6 +45,7 @@
 #include "junction.h"
 
 #include <atomic>
+#include <dlfcn.h>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -67,7 +68,7 @@ bool memlog_on();
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
-    int ensure(size_t bytes) {
+    __attribute__((noinline)) int ensure(size_t bytes) {
         if (bytes <= cap) return EC_OK;
         // a buffer that grows gets 1/8 of headroom: sizes that vary a little from call to call
         // (chain counts, received records) would otherwise reallocate -- ~1 ms a hipFree /
@@ -82,9 +83,14 @@ struct DevBuf {
         }
         cap = want;
         hbm_account((long long)want);
-        if (want >= (1ull << 30) && memlog_on())  // EULERHIP_MEMLOG=1: large buffers and their call sites
-            fprintf(stderr, "[eulerhip mem] +%.2f GB (held %.2f GB) at %p\n", want / 1e9, g_hbm_held.load() / 1e9,
-                    __builtin_return_address(0));
+        if (want >= (1ull << 30) && memlog_on()) {  // EULERHIP_MEMLOG=1: large buffers and their call sites
+            // (lib+offset: llvm-symbolizer --obj=libeulerhip.so of the same build names the caller)
+            Dl_info di{};
+            void *ra = __builtin_return_address(0);
+            const unsigned long off = dladdr(ra, &di) && di.dli_fbase ? (unsigned long)((char *)ra - (char *)di.dli_fbase) : 0ul;
+            fprintf(stderr, "[eulerhip mem] +%.2f GB (held %.2f GB) at lib+0x%lx\n", want / 1e9, g_hbm_held.load() / 1e9,
+                    off);
+        }
         return EC_OK;
     }
     template <typename T>
@@ -676,7 +682,7 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
 #define EC_SKPART_WV(NPF, W, VAL)                                                                             \
     k_skpart_w<NPF, W, VAL><<<lgb - lga, PT_THREADS, 0, st>>>(                                                   \
         d_reads, d_off, nreads, mc, M, gsize, (uint32_t)G, cap, smask, recs, s->cnt.as<unsigned int>(),          \
-        s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow, &dsc->lens[2], &dsc->npos, lga)
+        s->hll.as<uint8_t>(), &dsc->nrec, &dsc->overflow, &dsc->lens[2], &dsc->npos, lga, elim)
 #define EC_SKPART_W(NPF, W)            \
     if (validate)                      \
         EC_SKPART_WV(NPF, W, true);    \
@@ -692,6 +698,8 @@ int phase_count_sk2(ec_session *s, const uint8_t *d_reads, const uint64_t *d_off
     const bool chunked = s->pipe.active && s->pipe.done < s->pipe.nchunks;
     if (!chunked) EC_CHECK(pipe_all(s));
     unsigned lga = 0, lgb = (unsigned)G;
+    // entries a partition wave buffers (EULERHIP_SK2_ELIM: fewer, to test the overflow path)
+    const uint32_t elim = kn().sk2_elim >= 128 ? (uint32_t)std::min(kn().sk2_elim, SK2_ECAP_W) : (uint32_t)SK2_ECAP_W;
     for (int pc = chunked ? 0 : s->pipe.nchunks; ; pc++) {
       if (chunked) {
         if (pc >= s->pipe.nchunks) break;
@@ -1874,8 +1882,10 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     kmark(s, 0, 1);
     unsigned long long *ftot = s->ftot.as<unsigned long long>();
     EC_HIP(hipMemsetAsync(ftot, 0, (FINE_W + HR) * 8, st));
+    EC_HIP(hipMemsetAsync(&dsc->nrec, 0, sizeof(unsigned long long), st));
     k_fine_totals<FINE_W_BITS><<<dim3(FINE_W / 256, TOT_SLICES), 256, 0, st>>>(
-        s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), ngroups, ftot, reinterpret_cast<unsigned int *>(ftot + FINE_W));
+        s->hist.as<unsigned int>(), s->hll.as<uint8_t>(), ngroups, ftot, reinterpret_cast<unsigned int *>(ftot + FINE_W),
+        &dsc->nrec);
     k_hll_final<<<1, 1024, 0, st>>>(reinterpret_cast<unsigned int *>(ftot + FINE_W), HLL_REG_BITS, &dsc->est);
     mark(s, 2 * EC_STAGE_PRESCAN + 1);
     EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
@@ -1929,14 +1939,28 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_CHECK(s->offs.ensure(Ck * ngroups * 8));
     EC_CHECK(s->tot.ensure((Bk + 1) * 8));
     EC_CHECK(s->bstart.ensure((Bk + 1) * 8));
-    // (runs: P windows bound the run records; their count comes back with the bucket pass's
-    // scalars.  Both buffers take P window records: the runs are expanded into the other one)
+    // record buffers: window records, P of them; runs: the histogram's total (hsc.nrec, exact),
+    // and where the bucket pass rolls the runs out of 2-bit codes (third level) the codes go
+    // into the refined runs' buffer -- ceil((windows + k - 1) / 16) dwords a run (k_run_ccount).
+    // (Both buffers took P 24-B records before: 2 x 30 GB at config 5's rank shape for ~1.3 GB
+    // of runs and ~2 GB of codes.)  The two-level case expands the runs into P window records.
     const size_t rbytes = runs ? sizeof(RunWM) : sizeof(RecW);
-    EC_CHECK(s->recs.ensure(std::max<uint64_t>(P, 1) * sizeof(RecW)));
     const bool second = bbits > cbits;
-    if (second || runs) EC_CHECK(s->recs2.ensure(std::max<uint64_t>(P, 1) * sizeof(RecW)));
+    const bool direct = runs && sbits && kn().wide_runs != 2;
+    const uint64_t NR = runs ? hsc.nrec : P;
+    uint64_t b_recs = std::max<uint64_t>(P, 1) * sizeof(RecW), b_recs2 = b_recs;
+    if (direct) {
+        const uint64_t cbytes = 4 * ((P + NR * (uint64_t)(k - 1)) / 16 + 2 * NR + 64);
+        b_recs = b_recs2 = std::max<uint64_t>(std::max<uint64_t>(NR, 1) * sizeof(RunWM), cbytes);
+    } else if (runs) {  // the runs' input buffer rin (recs2 after a refine, else recs) takes the windows
+        b_recs = std::max<uint64_t>(P, 1) * sizeof(RecW);
+        b_recs2 = std::max<uint64_t>(NR, 1) * sizeof(RunWM);
+        if (second) std::swap(b_recs, b_recs2);
+    }
+    EC_CHECK(s->recs.ensure(b_recs));
+    if (second || runs) EC_CHECK(s->recs2.ensure(b_recs2));
     s->stats.record_bytes = (uint32_t)rbytes;
-    s->stats.n_records = P;
+    s->stats.n_records = NR;
     k_coarse<FINE_W_BITS><<<grid_for(Ck * ngroups, B, 8192), B, 0, st>>>(s->hist.as<unsigned int>(), ngroups, cbits,
                                                                         s->cnt.as<unsigned long long>());
     EC_CHECK(scan_u64(s, s->cnt.as<unsigned long long>(), s->offs.as<unsigned long long>(), Ck * ngroups));
@@ -3678,6 +3702,24 @@ int stage_packed(ec_session *s, Pipe &pp, DevBuf &codes_b, DevBuf &exc_b, DevBuf
 
 }  // namespace
 
+// every device buffer of a session (destroy, trim)
+template <typename Fn>
+static void for_each_buf(ec_session *s, Fn fn) {
+    DevBuf *all[] = {&s->h_reads, &s->h_offsets, &s->hll, &s->scal, &s->table, &s->dkey, &s->dcnt, &s->dfc, &s->dft,
+                     &s->upal, &s->outdeg, &s->cand, &s->succ, &s->pred, &s->st0, &s->st1, &s->startOf, &s->skeys,
+                     &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
+                     &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
+                     &s->rid, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
+                     &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->bnp, &s->rbc,
+                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->ewalk, &s->lc8, &s->x_par, &s->x_irr,
+                     &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
+                     &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
+                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
+                     &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec,
+                     &s->skm_rec, &s->skm_ev, &s->skm_end, &s->wcodes_tab};
+    for (auto *b : all) fn(*b);
+}
+
 extern "C" {
 
 int ec_session_create(ec_session **out, int device) {
@@ -3723,6 +3765,34 @@ int ec_session_set_stream(ec_session *s, void *hip_stream) {
     return EC_OK;
 }
 
+uint64_t ec_session_bytes(ec_session *s) {
+    uint64_t n = 0;
+    if (s) for_each_buf(s, [&](DevBuf &b) { n += b.cap; });
+    return n;
+}
+
+int ec_session_trim(ec_session *s, uint64_t min_bytes) {
+    if (!s) return EC_ERR_ARG;
+    EC_HIP(hipSetDevice(s->device));
+    if (s->stream) EC_HIP(hipStreamSynchronize(s->stream));
+    if (s->ostream) EC_HIP(hipStreamSynchronize(s->ostream));
+    if (s->cstream) EC_HIP(hipStreamSynchronize(s->cstream));
+    for_each_buf(s, [&](DevBuf &b) {
+        if (b.cap >= min_bytes && &b != &s->scal) b.release();
+    });
+    // no device state survives: the next call starts from its inputs (results already copied to
+    // host memory stay fetchable)
+    s->n_dense = 0;
+    s->own_valid = false;
+    s->bmark_ok = false;
+    s->seg_marks = 0;
+    s->skspec.valid = false;
+    s->graph_loaded = false;
+    s->placed = false;
+    s->pipe.active = false;
+    return EC_OK;
+}
+
 int ec_mem_stats(uint64_t *held, uint64_t *peak, int reset) {
     if (held) *held = g_hbm_held.load();
     if (peak) *peak = g_hbm_peak.load();
@@ -3738,19 +3808,7 @@ int ec_session_destroy(ec_session *s) {
     if (s->stream) hipStreamSynchronize(s->stream);
     if (s->ostream) hipStreamSynchronize(s->ostream);
     if (s->cstream) hipStreamSynchronize(s->cstream);
-    DevBuf *all[] = {&s->h_reads, &s->h_offsets, &s->hll, &s->scal, &s->table, &s->dkey, &s->dcnt, &s->dfc, &s->dft,
-                     &s->upal, &s->outdeg, &s->cand, &s->succ, &s->pred, &s->st0, &s->st1, &s->startOf, &s->skeys,
-                     &s->svals, &s->skeys2, &s->svals2, &s->cidxOf, &s->clen, &s->coff, &s->chars, &s->cfirst,
-                     &s->clast, &s->headOf, &s->tailOf, &s->lk, &s->lcnt, &s->tmp, &s->dchars, &s->dcounts,
-                     &s->rid, &s->rlist, &s->nextR, &s->PK, &s->RK, &s->PL, &s->PM,
-                     &s->ocnt, &s->hist, &s->ftot, &s->cnt, &s->offs, &s->bstart, &s->tot, &s->recs, &s->recs2, &s->sub, &s->bnp, &s->rbc,
-                     &s->mbid, &s->mbid2, &s->midx, &s->midx2, &s->gcur, &s->cwalk, &s->ewalk, &s->lc8, &s->x_par, &s->x_irr,
-                     &s->x_in, &s->x_succ, &s->x_done, &s->x_lk, &s->x_lv, &s->x_lk2, &s->x_lv2, &s->x_len,
-                     &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
-                     &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
-                     &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec,
-                     &s->skm_rec, &s->skm_ev, &s->skm_end, &s->wcodes_tab};
-    for (auto *b : all) b->release();
+    for_each_buf(s, [](DevBuf &b) { b.release(); });
     s->h_chars.release();
     s->hmeta.release();
     s->bounce.release();

@@ -328,7 +328,8 @@ __global__ void __launch_bounds__(256) k_coarse(const unsigned int *hist, uint64
 constexpr int TOT_SLICES = 32;
 template <int FB = FINE_BITS>
 __global__ void __launch_bounds__(256) k_fine_totals(const unsigned int *hist, const uint8_t *hll, uint64_t ngroups,
-                                                     unsigned long long *ftot, unsigned int *hreg) {
+                                                     unsigned long long *ftot, unsigned int *hreg,
+                                                     unsigned long long *total = nullptr) {
     constexpr int FINE = 1 << FB;
     const unsigned int f = blockIdx.x * blockDim.x + threadIdx.x;  // < FINE
     const unsigned int sl = blockIdx.y;
@@ -340,6 +341,11 @@ __global__ void __launch_bounds__(256) k_fine_totals(const unsigned int *hist, c
     }
     if (sum) atomicAdd(&ftot[f], sum);
     if (f < (1u << HLL_REG_BITS) && mx) atomicMax(&hreg[f], mx);
+    if (total) {  // (the records of all bins: one atomic per wave)
+        unsigned long long w = sum;
+        for (int o = 32; o > 0; o >>= 1) w += __shfl_down(w, o);
+        if ((threadIdx.x & 63) == 0 && w) atomicAdd(total, w);
+    }
 }
 
 // records per final bucket (bbits granularity); tot[B] = 0 so its exclusive scan ends at P

@@ -34,7 +34,14 @@
 namespace ec {
 
 constexpr int SK2_NMAX = 16;     // windows per record (n - 1 in 4 bits)
-constexpr int SK2_ECAP_W = 1600; // entries a partition wave buffers (LDS: 3 workgroups per CU)
+// entries a partition wave buffers: 1024 (40 KB of LDS a workgroup at NPF = 7: four workgroups,
+// four waves a SIMD, per CU).  A round adds ~2 W / (W + 1) entries a lane (~114 a wave at
+// k = 31), at most 64 W: the buffer is flushed past SK2_FLUSH_AT, which leaves room for 10 entries
+// a lane in the next round; a round that outgrows even that (never on sequence data: every lane's
+// minimizer changing at almost every window) stops storing and sets *overflow (the call is
+// redone on window records)
+constexpr int SK2_ECAP_W = 1024;
+constexpr int SK2_FLUSH_AT = SK2_ECAP_W - 64 - 640;
 #ifndef SK2_PD_DEF
 #define SK2_PD_DEF 4
 #endif
@@ -153,6 +160,7 @@ __device__ inline void skpart_flush(uint32_t cntw, const uint32_t *ent, uint16_t
 
 // Region of (c, g): records [(g * C + c) * cap, + cap) of recs, spill records at C * G * cap
 // (SK2_ECAP_W of them: a flush stores at most that many; *overflow set, the call is redone); cnt[c * G + g] = records stored.
+// elim (<= SK2_ECAP_W): the entries a wave may buffer (smaller only to test the overflow path).
 // Entry (u32): lane | first window << 6 | (n - 1) << 14 | top SK2_BBITS of min_remix << 18.
 // k_skpart_w: the partition for one compile-time window width W = k - m + 1 (the headline's k = 31: W = 17):
 // a round is one block of W m-mers, their hashes and the previous block's suffix minima held
@@ -171,11 +179,11 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
                                                          uint32_t smask, uint4 *recs, unsigned int *cnt, uint8_t *hll,
                                                          unsigned long long *nrec, unsigned int *overflow,
                                                          unsigned int *vfail, unsigned long long *npos,
-                                                         uint32_t g_lo) {
+                                                         uint32_t g_lo, uint32_t elim) {
     constexpr int C = 1 << SK2_CBITS;
     constexpr int NREG = 1 << HLL_REG_BITS;
     constexpr int SW = NPF * 64 + 4;
-    static_assert(SK2_ECAP_W >= 64 * (W + 2), "a round's entries fit the buffer");
+    static_assert(SK2_FLUSH_AT >= 64, "the entry buffer holds a flush's worth");
     __shared__ uint32_t s_stage[PT_WAVES][SW];
     __shared__ uint32_t s_ent[PT_WAVES][SK2_ECAP_W];
     __shared__ uint16_t s_srt[PT_WAVES][SK2_ECAP_W];
@@ -226,11 +234,15 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
                 if (lo >= nx_lo && lo + 16 <= nx_hi) {
                     diff |= d[0] | d[1] | d[2] | d[3];
                 } else if (lo < nx_hi && lo + 16 > nx_lo) {  // a chunk at the tile's ends: its read bytes only
+                    // bytes [from, to) of the chunk are the tile's: a 16-bit byte mask, each dword's
+                    // 4 bits widened to byte masks by one multiply
+                    const uint32_t from = (uint32_t)min(max((int)nx_lo - (int)lo, 0), 16);
+                    const uint32_t to = (uint32_t)min(max((int)nx_hi - (int)lo, 0), 16);
+                    const uint32_t m16 = (0xFFFFu >> (16 - to)) & ~((1u << from) - 1u);
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        const int b = (int)(lo + 4 * u);
-                        const int from = min(max((int)nx_lo - b, 0), 4), to = min(max((int)nx_hi - b, 0), 4);
-                        const uint32_t keep = to > from ? (0xFFFFFFFFu >> (32 - 8 * (to - from))) << (8 * from) : 0u;
+                        const uint32_t m4 = (m16 >> (4 * u)) & 15u;
+                        const uint32_t keep = ((m4 * 0x00204081u) & 0x01010101u) * 0xFFu;
                         diff |= d[u] & keep;
                     }
                 }
@@ -276,7 +288,6 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
             for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
         }
         const uint32_t nrounds = __any(has) ? (M + W - 1) / W : 0u;
-        if (nrounds == 0 && more) EC_PT_ISSUE(t + PT_WAVES);
         // the open run of a lane: windows [rs, w) of minimizer runv.  runv starts as window 0's
         // value, so window 0 never closes a run; a lane without a read never closes one (has).
         // The run start is kept as its entry term rsx = -16320 rs (below): the close test
@@ -323,7 +334,7 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
                 if (close) {
                     const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = entry(end);
+                    ent[min(cntw, elim - 64) + rk] = entry(end);  // (a uniform clamp: in bounds; past it, *overflow)
                     rsx = rw0 + (uint32_t)(j * -16320);
                 }
                 cntw += (uint32_t)__popcll(bal);
@@ -344,24 +355,32 @@ __global__ void __launch_bounds__(PT_THREADS) k_skpart_w(const uint8_t *__restri
             for (int j = 0; j < W; j++) S[j] = H[j];
 #pragma unroll
             for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
-            const bool last = round + 1 == nrounds;
-            if (last) {  // the reads' final runs: windows [rs, M)
-                const uint64_t bal = hasm;
-                if (has) {
-                    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    ent[cntw + rk] = entry(M);
-                }
-                cntw += (uint32_t)__popcll(bal);
-                if (more) EC_PT_ISSUE(t + PT_WAVES);
+            if (cntw > elim - 64) {  // entries were stored over others: the call is redone
+                if (lane == 0) atomicOr(overflow, 1u);
+                cntw = elim - 64;
             }
-            // flush: the buffer could not take another round, or the stage is about to change
-            if (last || cntw > (uint32_t)(SK2_ECAP_W - 64 * (W + 1))) {
+            // flush: the buffer may not take another round
+            if (round + 1 < nrounds && cntw > elim - 64 - 640) {
                 skpart_flush<C>(cntw, ent, s_srt[wid], s_wcnt[wid], s_cur, s_base[wid], s_rel[wid], st, lane, gcap,
                                 cap, spill, M, rtile, recs, overflow, s_hll, s_hq[wid], smask ? 0xFFu : 0u, k,
                                 kmask);
                 cntw = 0;
             }
+        }
+        // the next tile's loads go in flight here, past the rounds, on every path (the last tile
+        // reloads itself): the prefetch registers are then dead while the windows run -- issued
+        // inside the last round, they stayed live through every round (28 VGPRs at NPF = 7)
+        EC_PT_ISSUE(more ? t + PT_WAVES : t);
+        if (nrounds) {  // the reads' final runs (windows [rs, M)), then the stage's last flush
+            const uint64_t bal = hasm;
+            if (has) {
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                ent[cntw + rk] = entry(M);  // (cntw <= elim - 64 here)
+            }
+            cntw += (uint32_t)__popcll(bal);
+            skpart_flush<C>(cntw, ent, s_srt[wid], s_wcnt[wid], s_cur, s_base[wid], s_rel[wid], st, lane, gcap,
+                            cap, spill, M, rtile, recs, overflow, s_hll, s_hq[wid], smask ? 0xFFu : 0u, k, kmask);
         }
     }
     __shared__ unsigned int s_nwin[PT_WAVES];

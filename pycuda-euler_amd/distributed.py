@@ -129,6 +129,10 @@ def shard_range(nreads, rank, world):
     return lo, lo + q + (1 if rank < r else 0)
 
 
+# a shard count past this fraction of the device's memory is released after its export
+TRIM_FRACTION = 0.2
+
+
 # ---- engines -------------------------------------------------------------------------------
 class HipEngine:
     """The product engine: libeulerhip.so on this rank's GPU, buffers are torch uint8 tensors."""
@@ -160,6 +164,16 @@ class HipEngine:
 
     def rec_bytes(self):
         return int(self.L.ec_record_bytes(self.k))
+
+    def trim_if_large(self, frac=TRIM_FRACTION):
+        """after the export: a shard count holding more than frac of the device's memory releases
+        its buffers (ec_session_trim), so the owner merge and the graph phase get them -- config 5's
+        per-rank count holds ~10^11 B; the headline's ~10^10 B stays (re-allocating it costs ~ms)"""
+        total = self.torch.cuda.mem_get_info(self.device)[1]
+        if self.sess.device_bytes() > frac * total:
+            self.sess.trim(64 << 20)
+            return True
+        return False
 
     def owner_counts(self, nowners):
         """records per owner under the current rule (no export; the owner ids are kept for it)"""
@@ -532,6 +546,8 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     # compact records where the events fit (the receivers add this shard's read base)
     recs, counts, lfb = engine.export_by_owner(comm.world, compact=True)
     rb = compact_bytes(k) if lfb >= 0 else rec_bytes(k)
+    if hasattr(engine, "trim_if_large"):
+        engine.trim_if_large()
     tick("export")
     # the job's k-mer positions, this shard's read base and record format ride along with the
     # exchange's byte counts
@@ -679,6 +695,8 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
     for eng, c in zip(engines, comp):
         eng.set_owner_rule(rule)
         sends.append(eng.export_by_owner(world, compact=True) if c else eng.export_by_owner(world) + (-1,))
+        if hasattr(eng, "trim_if_large"):
+            eng.trim_if_large()
     local_sharded_assemble_shards.last_rule = rule
     finish = finish_mode(finish, k, rule)
     local_sharded_assemble_shards.last_counts = [c for _, c, _ in sends]

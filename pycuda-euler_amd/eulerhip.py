@@ -99,6 +99,8 @@ _SIGS = {
     "ec_session_set_stream": (ctypes.c_int, [_P, _P]),
     "ec_session_destroy": (ctypes.c_int, [_P]),
     "ec_mem_stats": (ctypes.c_int, [ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.c_int]),
+    "ec_session_trim": (ctypes.c_int, [_P, _U64]),
+    "ec_session_bytes": (_U64, [_P]),
     "ec_assemble_device": (ctypes.c_int, [_P, _P, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_assemble_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "ec_assemble_packed_host": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.c_uint32, _P, _P, _U64, ctypes.c_int,
@@ -291,6 +293,15 @@ class Session:
             self.close()
         except Exception:
             pass
+
+    def trim(self, min_bytes=0):
+        """release the device buffers of >= min_bytes and the device state they hold
+        (ec_session_trim); host-side results stay fetchable"""
+        check(lib().ec_session_trim(self._h, int(min_bytes)))
+
+    def device_bytes(self):
+        """device bytes the session's buffers hold (ec_session_bytes)"""
+        return int(lib().ec_session_bytes(self._h))
 
     def set_stream(self, stream):
         """stream: a hipStream_t handle (0 = the null stream, torch's default) or None for the

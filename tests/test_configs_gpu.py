@@ -133,6 +133,45 @@ def test_config5_rank_shape_solid_runs():
     assert got == want
 
 
+def test_config5_rank_sharded_junction_flow():
+    """One rank of BASELINE configs[4] through the whole sharded step of the multi-GPU design
+    (rank 3 of 8: its 12.5 M x 150 bp reads of the 200 Mbp genome at global read ids 37.5 M..,
+    k = 51): shard count, compact export, owner merge, placement at global ids, the junction join,
+    the partitioned finish -- distributed.local_sharded_assemble_shards at world 1, so this rank
+    owns every key (its merge and graph hold the whole genome's 2 * 10^8 keys, 8x the 8-rank
+    share: an upper bound of a real rank's memory).  Checks the size-independent properties of
+    test_config5_rank_shape_solid_runs and reports the peak HBM of the session buffers and of
+    torch's (reads, exchange records) -- src/cli_spark_gpu.py:37"""
+    import torch
+
+    import distributed
+
+    G, n, L, k, seed = 200_000_000, 12_500_000, 150, 51, 20261015 + 5
+    buf, off = make_reads(G, n, L, seed)
+    eng = distributed.HipEngine(0)
+    try:
+        torch.cuda.reset_peak_memory_stats()
+        eulerhip.mem_stats(reset=True)
+        res, P = distributed.local_sharded_assemble_shards([eng], [(buf, off, 37_500_000)], k, 1, finish="partitioned")
+        held, peak = eulerhip.mem_stats()
+        print("config-5 rank, sharded step: session buffers peak %.1f GB, torch peak %.1f GB, device %.1f GB"
+              % (peak / 1e9, torch.cuda.max_memory_allocated() / 1e9, torch.cuda.mem_get_info()[1] / 1e9))
+    finally:
+        eng.sess.close()
+    del buf, off
+    st = res.stats
+    assert P == n * (L - k + 1)
+    n_solid, a, b = _solid_runs(G, read_starts(G, n, L, seed), L, k)
+    assert st.n_dict == 2 * n_solid
+    assert st.n_contigs == len(a)
+    assert st.n_links == 0
+    genome = make_genome(G, seed)
+    ch, co = res.contig_bytes, res.contig_offsets
+    got = sorted(_canon(ch[int(co[i]):int(co[i + 1])]) for i in range(len(co) - 1))
+    want = sorted(_canon(genome[int(x):int(y) - 1 + k]) for x, y in zip(a, b))
+    assert got == want
+
+
 def test_genome20m_k51_third_level_vs_oracle(gpu_session, monkeypatch):
     """config 5's read shape at a tenth of its genome (20 Mbp, 10 M x 150 bp, k = 51: 10^9
     positions, 2 * 10^7 solid 51-mers) through the wide path's third partition level (forced:

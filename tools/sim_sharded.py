@@ -74,6 +74,7 @@ def main():
             tick("count", t0)
             t0 = t_start()
             sends.append(eng.export_by_owner(world, compact=True))
+            eng.trim_if_large()
             tick("export", t0)
         rb = distributed.rec_bytes(a.k)
         rbs = [distributed.compact_bytes(a.k) if b >= 0 else rb for _, _, b in sends]
