@@ -49,6 +49,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
+#include <thread>
 
 namespace ec {
 
@@ -172,6 +173,11 @@ struct ec_session {
     int k = 0;
     ec_stats stats{};
     HostBuf h_chars;
+    // the one-GPU results' characters in transfer form: 2-bit codes, 4 a byte (A C G T = 0..3;
+    // every character of a standard-alphabet contig is one of them), nchars_host of them --
+    // ec_copy_contigs widens them (ecoli10m_err: 38 MB of characters over PCIe took ~0.7 ms)
+    bool chars_packed = false;
+    uint64_t nchars_host = 0;
     // small device -> host reads (scalars, counts) go through this page-locked bounce buffer and
     // are delivered by host_sync: a pageable destination cost ~11 us more per round trip
     // (tools/micro/sync_lat.hip on MI355X: 27.2 vs 16.3 us), and a step has ~6 of them
@@ -2534,6 +2540,25 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     return EC_OK;
 }
 
+// contig characters -> 2-bit codes (A C G T = 0..3, pack4's mapping), 16 characters a thread,
+// up to *total (the contigs' offsets' last entry) of them; the bytes past it are padding
+__global__ void __launch_bounds__(256) k_pack_chars(const uint4 *chars, const unsigned long long *total, uint64_t cap16,
+                                                    uint32_t *codes) {
+    const uint64_t n16 = min<uint64_t>((*total + 15) / 16, cap16);
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n16; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 v = chars[t];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t out = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t x = ((w[u] >> 1) ^ (w[u] >> 2)) & 0x03030303u;  // A C G T -> 0 1 2 3 per byte
+            const uint32_t y = x | (x >> 6);
+            out |= ((y | (y >> 12)) & 0xFFu) << (8 * u);
+        }
+        codes[t] = out;
+    }
+}
+
 // the rounds a ranking used (the last round that still moved a pointer + 1), for the next
 // call's speculation; 0 when the last round still moved one (not converged)
 constexpr unsigned int OCOPY_MIN = 1u << 16;  // contigs past which results copy on the output stream
@@ -2988,7 +3013,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
 
     // ---- emit -----------------------------------------------------------------------------
     mark(s, 2 * EC_STAGE_EMIT);
-    EC_CHECK(s->chars.ensure(std::max<size_t>(chars_bound, 1)));
+    EC_CHECK(s->chars.ensure(std::max<size_t>(chars_bound, 1) + 16));  // (+16: k_pack_chars reads 16 at a time)
     EC_CHECK(s->cfirst.ensure((size_t)std::max(nc, 1u) * 4));
     EC_CHECK(s->clast.ensure((size_t)std::max(nc, 1u) * 4));
     if (nc && !small)
@@ -3021,13 +3046,24 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     // done, sized by the previous call's total (a stream of equal batches, the bench's steps): it
     // overlaps GFA and the link compaction instead of following a read-back of the total; a
     // larger total is copied again in full after the read-back
+    // standard alphabet: the characters travel as 2-bit codes (a quarter of the PCIe bytes)
+    const bool pack = !XT && kn().no_char_pack == 0;
+    const void *csrc = s->chars.p;
+    if (pack) {
+        const uint64_t cap16 = (std::max<uint64_t>(chars_bound, 1) + 15) / 16;
+        EC_CHECK(s->dchars.ensure(cap16 * 4));
+        k_pack_chars<<<std::min(grid_for(cap16, B), 8192u), B, 0, st>>>(
+            s->chars.as<uint4>(), s->coff.as<unsigned long long>() + nc, cap16, s->dchars.as<uint32_t>());
+        csrc = s->dchars.p;
+    }
+    auto hbytes = [&](uint64_t n) { return pack ? (n + 3) / 4 : n; };  // host bytes of n characters
     uint64_t pre = 0;
     if (s->last_nchars && s->last_nchars <= chars_bound && kn().no_spec == 0) {
         pre = s->last_nchars;
-        EC_CHECK(s->h_chars.resize(pre));
+        EC_CHECK(s->h_chars.resize(hbytes(pre)));
         EC_HIP(hipEventRecord(s->oev[0], st));
         EC_HIP(hipStreamWaitEvent(s->ostream, s->oev[0], 0));
-        EC_HIP(hipMemcpyAsync(s->h_chars.data(), s->chars.p, pre, hipMemcpyDeviceToHost, s->ostream));
+        EC_HIP(hipMemcpyAsync(s->h_chars.data(), csrc, hbytes(pre), hipMemcpyDeviceToHost, s->ostream));
         EC_HIP(hipEventRecord(s->oev[1], s->ostream));
     }
     s->last_nchars = 0;
@@ -3098,9 +3134,11 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         return EC_ERR_STATE;
     }
     if (pre && nchars > pre) EC_HIP(hipEventSynchronize(s->oev[1]));  // (before h_chars may move)
-    EC_CHECK(s->h_chars.resize(nchars));
+    EC_CHECK(s->h_chars.resize(hbytes(nchars)));
+    s->chars_packed = pack;
+    s->nchars_host = nchars;
     bool again = nchars > pre;  // (a second round trip: characters or links still to copy)
-    if (nchars > pre) EC_CHECK(d2h(s, s->h_chars.data(), s->chars.p, nchars, st));
+    if (nchars > pre) EC_CHECK(d2h(s, s->h_chars.data(), csrc, hbytes(nchars), st));
     const uint64_t nlinks = nlinks64;
     EC_CHECK(s->h_links32.resize(nlinks));  // (small: the copied bound's first nlinks stay)
     if (nlinks && !small) {
@@ -3402,6 +3440,8 @@ int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint6
         EC_CHECK(d2h(s, s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, st));
     }
     EC_CHECK(s->h_chars.resize(nchars));
+    s->chars_packed = false;
+    s->nchars_host = nchars;
     if (nchars) EC_CHECK(d2h(s, s->h_chars.data(), d_chars, nchars, st));
     EC_CHECK(host_sync(s, st));
     const uint64_t nlinks = s->h_loff[n2];
@@ -3702,6 +3742,35 @@ int stage_packed(ec_session *s, Pipe &pp, DevBuf &codes_b, DevBuf &exc_b, DevBuf
 
 }  // namespace
 
+// 2-bit codes (4 a byte, first character in the low bits) -> n ASCII characters; threads past
+// ~4 MB of characters (ecoli10m_err: 38 MB)
+static void unpack_codes(const uint8_t *codes, uint64_t n, char *out) {
+    static const struct Lut {
+        uint32_t v[256];
+        Lut() {
+            const char acgt[4] = {'A', 'C', 'G', 'T'};
+            for (int b = 0; b < 256; b++) {
+                uint32_t w = 0;
+                for (int j = 0; j < 4; j++) w |= (uint32_t)(uint8_t)acgt[(b >> (2 * j)) & 3] << (8 * j);
+                v[b] = w;
+            }
+        }
+    } lut;
+    auto run = [&](uint64_t b0, uint64_t b1) {  // whole bytes [b0, b1) -> characters 4 b0 ..
+        for (uint64_t i = b0; i < b1; i++) memcpy(out + 4 * i, &lut.v[codes[i]], 4);
+    };
+    const uint64_t full = n / 4;
+    const unsigned nt = full >= (1ull << 20) ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    if (nt > 1) {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; t++) th.emplace_back(run, full * t / nt, full * (t + 1) / nt);
+        for (auto &x : th) x.join();
+    } else {
+        run(0, full);
+    }
+    for (uint64_t c = 4 * full; c < n; c++) out[c] = "ACGT"[(codes[full] >> (2 * (c & 3))) & 3];
+}
+
 // every device buffer of a session (destroy, trim)
 template <typename Fn>
 static void for_each_buf(ec_session *s, Fn fn) {
@@ -3982,7 +4051,10 @@ int ec_copy_contigs(ec_session *s, char *chars, uint64_t *offsets) {
         set_error("no successful assembly in this session");
         return EC_ERR_STATE;
     }
-    if (chars && !s->h_chars.empty()) memcpy(chars, s->h_chars.data(), s->h_chars.size);
+    if (chars && s->nchars_host) {
+        if (s->chars_packed) unpack_codes(reinterpret_cast<const uint8_t *>(s->h_chars.data()), s->nchars_host, chars);
+        else memcpy(chars, s->h_chars.data(), s->nchars_host);
+    }
     if (offsets) memcpy(offsets, s->h_coff.data(), s->h_coff.size() * 8);
     return EC_OK;
 }

@@ -130,7 +130,7 @@ def shard_range(nreads, rank, world):
 
 
 # a shard count past this fraction of the device's memory is released after its export
-TRIM_FRACTION = 0.2
+TRIM_FRACTION = 0.1
 
 
 # ---- engines -------------------------------------------------------------------------------
@@ -554,6 +554,7 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     received, P, src_bytes, metas = comm.alltoallv(recs, [c * rb for c in counts], tag=st.n_positions,
                                                    meta=[read_base, lfb])
     src_base, src_lfb = [m[0] for m in metas], [m[1] for m in metas]
+    del recs  # (the send buffer: its memory goes to the merge)
     tick("alltoall")
     junction = partitioned and finish == "partitioned" and hasattr(engine, "graph_place")
     if partitioned and finish == "partitioned" and not junction:
@@ -565,6 +566,7 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
                       "finish='partitioned' runs the replicated finish", RuntimeWarning, stacklevel=2)
     if junction:  # each rank keeps its own segment: the links come out of the junction join
         ur = engine.merge_owned_from(received, src_bytes, src_base, src_lfb, k, limit, flags, export=False)
+        del received
         tick("merge")
         lo, hi, _, npal = junction_links(engine, comm, k, ur, tick=tick)
         res = partitioned_finish(engine, comm, k, lo, hi, None, fetch=fetch, tick=tick, npal=npal)
@@ -710,13 +712,14 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
             recs, counts, _ = sends[src]
             o = sum(counts[:dst]) * rbs[src]
             got.append(recs[o:o + counts[dst] * rbs[src]].to(eng.device))
-        return eng.merge_owned_from(torch.cat(got), [g.numel() for g in got], bases,
+        return eng.merge_owned_from(torch.cat(got) if world > 1 else got[0], [g.numel() for g in got], bases,
                                     [b for _, _, b in sends], k, limit, flags, export=export)
 
     if partitioned is None:
         partitioned = not (flags & eulerhip.EC_FLAG_GENERAL)
     if partitioned and finish == "partitioned":  # the junction-partitioned graph (junction_links)
         urs = [merge(dst, eng, False) for dst, eng in enumerate(engines)]
+        sends.clear()  # (each exchange buffer is dropped once consumed: config 5's rank holds ~10^11 B)
         seg_lo = [sum(urs[:r]) for r in range(world + 1)]
         U = seg_lo[-1]
         placed = [eng.graph_place(seg_lo[r], U, world) for r, eng in enumerate(engines)]
@@ -725,10 +728,13 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
         links = []
         for dst, eng in enumerate(engines):
             got = [rec[sum(c[:dst]) * jb:sum(c[:dst + 1]) * jb].to(eng.device) for rec, c, _ in placed]
-            links.append(eng.graph_join(torch.cat(got), seg_lo))
+            links.append(eng.graph_join(torch.cat(got) if len(got) > 1 else got[0], seg_lo))
+            del got
+        placed.clear()
         for dst, eng in enumerate(engines):
             got = [rec[sum(c[:dst]) * LINK_BYTES:sum(c[:dst + 1]) * LINK_BYTES].to(eng.device) for rec, c in links]
             eng.graph_links_apply(torch.cat(got))
+        links.clear()
         segs = [(seg_lo[r], seg_lo[r + 1], None) for r in range(world)]
         return local_partitioned_finish(engines, segs, k, npal), P
     solids = [merge(dst, eng, True) for dst, eng in enumerate(engines)]
@@ -761,10 +767,12 @@ def local_partitioned_finish(engines, segs, k, npal):
 
     dev = engines[0].device
     sups = [eng.graph_chains_part(lo, hi, part)[0] for eng, (lo, hi, part) in zip(engines, segs)]
-    supers = torch.cat([x.to(dev) for x in sups])
+    supers = torch.cat([x.to(dev) for x in sups]) if len(sups) > 1 else sups[0]
+    del sups
     M = supers.numel() // SUPER_BYTES
     for eng in engines:
         eng.graph_rank_supers(supers.to(eng.device), M)
+    del supers
     sts = [eng.graph_starts_part(M > 0, lo, hi)[0] for eng, (lo, hi, _) in zip(engines, segs)]
     starts = torch.cat([x.to(dev) for x in sts])
     nc = starts.numel() // START_BYTES

@@ -100,7 +100,7 @@ def _canon(s):
     return s if s <= t else t
 
 
-def test_config5_rank_shape_solid_runs():
+def test_config5_rank_shape_solid_runs(gpu_session):
     """BASELINE configs[4] at its per-rank shape (8 ranks: 12.5 M x 150 bp of the 200 Mbp genome,
     k = 51, 128-bit keys, third partition level, 1.9 * 10^9 positions): n_solid equals the
     solid positions computed from the read starts, and the contigs, each in canonical
@@ -110,6 +110,8 @@ def test_config5_rank_shape_solid_runs():
 
     G, n, L, k, seed = 200_000_000, 12_500_000, 150, 51, 20261015 + 5
     buf, off = make_reads(G, n, L, seed)
+    gpu_session.trim()
+    torch.cuda.empty_cache()
     s = eulerhip.Session(0)
     try:
         free0, total = torch.cuda.mem_get_info()
@@ -133,7 +135,7 @@ def test_config5_rank_shape_solid_runs():
     assert got == want
 
 
-def test_config5_rank_sharded_junction_flow():
+def test_config5_rank_sharded_junction_flow(gpu_session):
     """One rank of BASELINE configs[4] through the whole sharded step of the multi-GPU design
     (rank 3 of 8: its 12.5 M x 150 bp reads of the 200 Mbp genome at global read ids 37.5 M..,
     k = 51): shard count, compact export, owner merge, placement at global ids, the junction join,
@@ -148,6 +150,8 @@ def test_config5_rank_sharded_junction_flow():
 
     G, n, L, k, seed = 200_000_000, 12_500_000, 150, 51, 20261015 + 5
     buf, off = make_reads(G, n, L, seed)
+    gpu_session.trim()  # (the suite's shared session and torch's cache give their memory back first)
+    torch.cuda.empty_cache()
     eng = distributed.HipEngine(0)
     try:
         torch.cuda.reset_peak_memory_stats()
