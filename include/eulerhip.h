@@ -469,6 +469,16 @@ int ec_graph_starts_part(ec_session *s, int have_supers, void *d_starts, uint64_
 int ec_graph_layout(ec_session *s, const void *d_starts, uint64_t n, uint64_t *n_chars);
 int ec_graph_emit_part(ec_session *s, char *d_chars, void *d_ends);
 int ec_graph_collect(ec_session *s, const char *d_chars, const void *d_ends, uint64_t n_pal);
+/* The same emission and collection without job-sized buffers (round 6; distributed.py uses these
+ * with engines that have them): ec_graph_emit_runs emits this rank's characters and contig ends
+ * and sizes its transfer record -- the runs of consecutive character positions it wrote, their
+ * characters, the ends it holds -- into *nbytes; ec_graph_copy_runs writes the record into d_out
+ * (nbytes, 8-byte aligned; stream-ordered).  The records of all ranks are gathered (concatenated
+ * in rank order, src_bytes[r] each) to the collecting rank, whose ec_graph_collect_runs scatters
+ * them into the job's characters and ends and finishes as ec_graph_collect. */
+int ec_graph_emit_runs(ec_session *s, uint64_t *nbytes);
+int ec_graph_copy_runs(ec_session *s, void *d_out);
+int ec_graph_collect_runs(ec_session *s, const void *d_in, int nsrc, const uint64_t *src_bytes, uint64_t n_pal);
 int ec_end_record_bytes(int k);
 int ec_super_record_bytes(void);
 int ec_start_record_bytes(void);

@@ -311,6 +311,11 @@ struct ec_session {
     uint64_t seg_n0 = 0, seg_n1 = 0;
     unsigned int seg_nc = 0;     // contigs of the job (ec_graph_layout)
     uint64_t seg_nchars = 0;
+    // the partitioned finish's transfer record (ec_graph_emit_runs / ec_graph_copy_runs):
+    // chunk counts and scans, this rank's end records, the record's sizes
+    DevBuf run_cnt, run_ends, run_dends;
+    uint64_t run_nr = 0, run_nch = 0, run_nends = 0;
+    bool runs_ready = false;
 };
 
 namespace {
@@ -3363,7 +3368,7 @@ int part_layout(ec_session *s, const StartRec *d_all, uint64_t nc, uint64_t *n_c
 }
 
 template <typename Ops>
-int part_emit(ec_session *s, char *d_chars, void *d_ends) {
+int part_emit(ec_session *s, char *d_chars, void *d_ends, bool check = true) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
@@ -3389,10 +3394,11 @@ int part_emit(ec_session *s, char *d_chars, void *d_ends) {
             s->tailOf.as<unsigned int>(), &dsc->skew, n0);
     // contig ends as k-mer codes (the collecting rank holds no global set): 2 nc codes, each
     // written by the rank that emitted the node, zeros elsewhere
-    if (nc)
+    if (nc && d_ends)
         k_ends_codes<Ops><<<grid_for(nc, B), B, 0, st>>>(s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), nc,
                                                          s->dkey.as<typename Ops::K>(), s->k,
                                                          reinterpret_cast<typename Ops::K *>(d_ends));
+    if (!check) return EC_OK;  // (the caller reads dsc->skew with its own scalars)
     unsigned int bad = 0;
     EC_CHECK(d2h(s, &bad, &dsc->skew, 4, st));
     EC_CHECK(host_sync(s, st));
@@ -3404,7 +3410,7 @@ int part_emit(ec_session *s, char *d_chars, void *d_ends) {
 }
 
 template <typename Ops>
-int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint64_t n_pal) {
+int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint64_t n_pal, bool packable = false) {
     using K = typename Ops::K;
     using T = typename EndSlotOf<K>::T;
     hipStream_t st = s->stream;
@@ -3439,10 +3445,23 @@ int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint6
         EC_CHECK(scan_u64(s, s->skeys.as<unsigned long long>(), s->skeys2.as<unsigned long long>(), (size_t)n2 + 1));
         EC_CHECK(d2h(s, s->h_loff.data(), s->skeys2.p, ((size_t)n2 + 1) * 8, st));
     }
-    EC_CHECK(s->h_chars.resize(nchars));
-    s->chars_packed = false;
+    // (d_chars of the session, 16 B padded: the characters travel as 2-bit codes, as phase_graph's)
+    const bool pack = packable && !std::is_same<Ops, OpsX>::value && kn().no_char_pack == 0;
+    s->chars_packed = pack;
     s->nchars_host = nchars;
-    if (nchars) EC_CHECK(d2h(s, s->h_chars.data(), d_chars, nchars, st));
+    if (pack) {
+        const uint64_t cap16 = (nchars + 15) / 16;
+        EC_CHECK(s->dchars.ensure(std::max<uint64_t>(cap16, 1) * 4));
+        if (cap16)
+            k_pack_chars<<<std::min(grid_for(cap16, B), 8192u), B, 0, st>>>(
+                reinterpret_cast<const uint4 *>(d_chars), s->coff.as<unsigned long long>() + nc, cap16,
+                s->dchars.as<uint32_t>());
+        EC_CHECK(s->h_chars.resize((nchars + 3) / 4));
+        if (nchars) EC_CHECK(d2h(s, s->h_chars.data(), s->dchars.p, (nchars + 3) / 4, st));
+    } else {
+        EC_CHECK(s->h_chars.resize(nchars));
+        if (nchars) EC_CHECK(d2h(s, s->h_chars.data(), d_chars, nchars, st));
+    }
     EC_CHECK(host_sync(s, st));
     const uint64_t nlinks = s->h_loff[n2];
     EC_CHECK(s->h_links.resize(nlinks));
@@ -3462,6 +3481,129 @@ int part_collect(ec_session *s, const char *d_chars, const void *d_ends_v, uint6
     s->have = true;
     s->stats_ok = true;
     return EC_OK;
+}
+
+// ---- the partitioned finish's transfer to the collecting rank (junction.h, round 6) -----------
+// this rank's emission into a zeroed job-sized buffer of its own (never sent), its runs counted
+// per chunk and scanned, its contig ends as records; one read-back for the sizes
+template <typename Ops>
+int part_emit_runs(ec_session *s, uint64_t *nbytes) {
+    using K = typename Ops::K;
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    Scalars *dsc = s->scal.as<Scalars>();
+    const uint64_t nchars = s->seg_nchars;
+    const unsigned int nc = s->seg_nc;
+    s->runs_ready = false;
+    EC_CHECK(s->chars.ensure(nchars + 32));
+    EC_HIP(hipMemsetAsync(s->chars.p, 0, nchars + 32, st));
+    EC_CHECK(part_emit<Ops>(s, s->chars.as<char>(), nullptr, false));
+    const uint64_t nch = (nchars + RUN_CH - 1) / RUN_CH;
+    EC_CHECK(s->run_cnt.ensure(4 * (nch + 1) * 8));
+    unsigned long long *rc = s->run_cnt.as<unsigned long long>(), *cc = rc + nch + 1, *rb = cc + nch + 1,
+                       *cb = rb + nch + 1;
+    EC_HIP(hipMemsetAsync(rc, 0, 2 * (nch + 1) * 8, st));
+    if (nch) k_runs_count<<<(unsigned)nch, RUN_NT, 0, st>>>(s->chars.as<uint8_t>(), nchars, rc, cc);
+    EC_CHECK(scan_u64(s, rc, rb, nch + 1));
+    EC_CHECK(scan_u64(s, cc, cb, nch + 1));
+    EC_CHECK(s->run_ends.ensure(std::max<size_t>(2ull * nc, 1) * sizeof(EndRec<K>)));
+    EC_CHECK(s->jcnt.ensure(16));
+    unsigned int *nout = s->jcnt.as<unsigned int>();
+    EC_HIP(hipMemsetAsync(nout, 0, 4, st));
+    if (nc)
+        k_ends_recs<Ops><<<grid_for(nc, B), B, 0, st>>>(s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), nc,
+                                                        s->dkey.as<K>(), s->k, s->run_ends.as<EndRec<K>>(), nout);
+    unsigned long long tot[2] = {0, 0};
+    unsigned int ne = 0, bad = 0;
+    EC_CHECK(d2h(s, &tot[0], rb + nch, 8, st));
+    EC_CHECK(d2h(s, &tot[1], cb + nch, 8, st));
+    EC_CHECK(d2h(s, &ne, nout, 4, st));
+    EC_CHECK(d2h(s, &bad, &dsc->skew, 4, st));
+    EC_CHECK(host_sync(s, st));
+    if (bad) {
+        set_error("contig characters past their bound %llu (inconsistent ranking)", (unsigned long long)nchars);
+        return EC_ERR_STATE;
+    }
+    s->run_nr = tot[0];
+    s->run_nch = tot[1];
+    s->run_nends = ne;
+    s->runs_ready = true;
+    *nbytes = run_rec_bytes(tot[0], tot[1], ne, (int)sizeof(K));
+    return EC_OK;
+}
+
+// the transfer record into d_out (ec_graph_emit_runs' size), stream-ordered (no sync)
+template <typename Ops>
+int part_copy_runs(ec_session *s, void *d_out) {
+    using K = typename Ops::K;
+    hipStream_t st = s->stream;
+    const uint64_t nchars = s->seg_nchars, nch = (nchars + RUN_CH - 1) / RUN_CH, nr = s->run_nr;
+    unsigned long long *rc = s->run_cnt.as<unsigned long long>(), *rb = rc + 2 * (nch + 1), *cb = rb + nch + 1;
+    unsigned long long *hdr = static_cast<unsigned long long *>(d_out);
+    unsigned long long *rstart = hdr + 4, *rcoff = rstart + nr;
+    uint8_t *rchars = reinterpret_cast<uint8_t *>(rcoff + nr);
+    uint8_t *ends = rchars + ((s->run_nch + 7) & ~7ull);
+    k_put_u64x4<<<1, 64, 0, st>>>(hdr, nr, s->run_nch, s->run_nends, 0ull);
+    if (nch) k_runs_write<<<(unsigned)nch, RUN_NT, 0, st>>>(s->chars.as<uint8_t>(), nchars, rb, cb, rstart, rcoff, rchars);
+    if (s->run_nends)
+        EC_HIP(hipMemcpyAsync(ends, s->run_ends.p, s->run_nends * sizeof(EndRec<K>), hipMemcpyDeviceToDevice, st));
+    return EC_OK;
+}
+
+// the collecting rank: every rank's transfer record (concatenated, src_bytes each) into the
+// job's characters and end table, then part_collect
+template <typename Ops>
+int part_collect_runs(ec_session *s, const uint8_t *d_in, int nsrc, const uint64_t *src_bytes, uint64_t n_pal) {
+    using K = typename Ops::K;
+    hipStream_t st = s->stream;
+    const unsigned B = 256;
+    const uint64_t nchars = s->seg_nchars;
+    const unsigned int nc = s->seg_nc;
+    std::vector<unsigned long long> hdr(4 * (size_t)nsrc);
+    uint64_t o = 0;
+    for (int r = 0; r < nsrc; r++) {
+        if (src_bytes[r] < 32 || (o & 7)) {
+            set_error("ec_graph_collect_runs: source %d's record is %llu bytes at offset %llu", r,
+                      (unsigned long long)src_bytes[r], (unsigned long long)o);
+            return EC_ERR_ARG;
+        }
+        EC_CHECK(d2h(s, &hdr[4 * r], d_in + o, 32, st));
+        o += src_bytes[r];
+    }
+    EC_CHECK(host_sync(s, st));
+    EC_CHECK(s->chars.ensure(nchars + 32));
+    EC_CHECK(s->run_dends.ensure(std::max<size_t>(2ull * nc, 1) * sizeof(K)));
+    EC_HIP(hipMemsetAsync(s->run_dends.p, 0, std::max<size_t>(2ull * nc, 1) * sizeof(K), st));
+    EC_CHECK(s->jcnt.ensure(16));
+    unsigned int *bad = s->jcnt.as<unsigned int>();
+    EC_HIP(hipMemsetAsync(bad, 0, 4, st));
+    o = 0;
+    for (int r = 0; r < nsrc; r++) {
+        const uint64_t nr = hdr[4 * r], nch = hdr[4 * r + 1], ne = hdr[4 * r + 2];
+        if (run_rec_bytes(nr, nch, ne, (int)sizeof(K)) != src_bytes[r]) {
+            set_error("ec_graph_collect_runs: source %d's record holds %llu bytes, its header %llu", r,
+                      (unsigned long long)src_bytes[r], (unsigned long long)run_rec_bytes(nr, nch, ne, (int)sizeof(K)));
+            return EC_ERR_ARG;
+        }
+        const unsigned long long *rstart = reinterpret_cast<const unsigned long long *>(d_in + o) + 4;
+        const unsigned long long *rcoff = rstart + nr;
+        const uint8_t *rchars = reinterpret_cast<const uint8_t *>(rcoff + nr);
+        const EndRec<K> *ends = reinterpret_cast<const EndRec<K> *>(rchars + ((nch + 7) & ~7ull));
+        if (nr)
+            k_runs_scatter<<<std::min(grid_for(nr, B), 8192u), B, 0, st>>>(rstart, rcoff, nr, nch, rchars,
+                                                                         s->chars.as<uint8_t>(), nchars, bad);
+        if (ne)
+            k_ends_scatter<K><<<grid_for(ne, B), B, 0, st>>>(ends, ne, 2 * nc, s->run_dends.as<K>(), bad);
+        o += src_bytes[r];
+    }
+    unsigned int hb = 0;
+    EC_CHECK(d2h(s, &hb, bad, 4, st));
+    EC_CHECK(host_sync(s, st));
+    if (hb) {
+        set_error("ec_graph_collect_runs: a run or an end outside the layout");
+        return EC_ERR_ARG;
+    }
+    return part_collect<Ops>(s, s->chars.as<char>(), s->run_dends.p, n_pal, true);
 }
 
 // ---- extended alphabet (extended.h) -----------------------------------------------------------
@@ -3785,7 +3927,8 @@ static void for_each_buf(ec_session *s, Fn fn) {
                      &s->x_m, &s->x_cid, &s->x_head, &s->x_tail, &s->rt_tcnt, &s->rt_tbase, &s->rt_srec,
                      &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
                      &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec,
-                     &s->skm_rec, &s->skm_ev, &s->skm_end, &s->wcodes_tab};
+                     &s->skm_rec, &s->skm_ev, &s->skm_end, &s->wcodes_tab,
+                     &s->run_cnt, &s->run_ends, &s->run_dends};
     for (auto *b : all) fn(*b);
 }
 
@@ -4548,6 +4691,34 @@ int ec_graph_collect(ec_session *s, const char *d_chars, const void *d_ends, uin
     }
     EC_HIP(hipSetDevice(s->device));
     return s->k > 32 ? part_collect<OpsW>(s, d_chars, d_ends, n_pal) : part_collect<Ops64>(s, d_chars, d_ends, n_pal);
+}
+
+int ec_graph_emit_runs(ec_session *s, uint64_t *nbytes) {
+    if (!s || !s->graph_loaded || !nbytes) {
+        set_error("ec_graph_emit_runs: no layout");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return s->k > 32 ? part_emit_runs<OpsW>(s, nbytes) : part_emit_runs<Ops64>(s, nbytes);
+}
+
+int ec_graph_copy_runs(ec_session *s, void *d_out) {
+    if (!s || !s->runs_ready || !d_out) {
+        set_error("ec_graph_copy_runs: no emitted runs (ec_graph_emit_runs)");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return s->k > 32 ? part_copy_runs<OpsW>(s, d_out) : part_copy_runs<Ops64>(s, d_out);
+}
+
+int ec_graph_collect_runs(ec_session *s, const void *d_in, int nsrc, const uint64_t *src_bytes, uint64_t n_pal) {
+    if (!s || !s->graph_loaded || nsrc < 1 || !src_bytes || !d_in || n_pal > s->n_dense) {
+        set_error("ec_graph_collect_runs: no layout or bad arguments");
+        return EC_ERR_ARG;
+    }
+    EC_HIP(hipSetDevice(s->device));
+    return s->k > 32 ? part_collect_runs<OpsW>(s, static_cast<const uint8_t *>(d_in), nsrc, src_bytes, n_pal)
+                     : part_collect_runs<Ops64>(s, static_cast<const uint8_t *>(d_in), nsrc, src_bytes, n_pal);
 }
 
 int ec_end_record_bytes(int k) { return k > 32 ? 16 : 8; }

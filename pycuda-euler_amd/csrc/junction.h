@@ -409,4 +409,140 @@ __global__ void __launch_bounds__(256) k_ends_codes(const unsigned int *cfirst, 
     }
 }
 
+// ---- the partitioned finish's transfer to the collecting rank (round 6) ---------------------
+// Up to round 5 every rank emitted into a zeroed job-sized character buffer and a job-sized end
+// table, and one reduce-sum brought both to rank 0 (config 5: ~2 * 10^8 B a rank).  Now a rank
+// sends only what it wrote: runs of consecutive character positions (cut at RUN_CH-position
+// chunks) and the contig ends it holds, one transfer record a rank, gathered to rank 0:
+//   u64 header[4] = {runs, characters, ends, 0}
+//   u64 start[runs]   job position of each run's first character
+//   u64 coff[runs]    offset of its first character in chars (its length: the next one's - it)
+//   u8  chars[characters], padded to 8
+//   EndRec ends[ends] (idx = contig for its first k-mer, nc + contig for its last)
+constexpr unsigned int RUN_CH = 4096;  // positions a compaction workgroup scans (16 a thread)
+constexpr unsigned int RUN_NT = RUN_CH / 16;
+template <typename K>
+struct EndRec {
+    unsigned int idx, pad;
+    K code;
+};
+__host__ __device__ inline uint64_t run_rec_bytes(uint64_t runs, uint64_t chars, uint64_t ends, int kbytes) {
+    return 32 + 16 * runs + ((chars + 7) & ~7ull) + ends * (8 + (uint64_t)kbytes);
+}
+
+// written (non-zero) bytes of a thread's 16 positions and the run starts among them (a run starts
+// at a written byte whose predecessor is not written, or at the chunk's first position)
+__device__ inline void run_masks(const uint8_t *chars, uint64_t n, uint64_t p, uint32_t *s_nz, uint32_t &nz,
+                                 uint32_t &st) {
+    nz = 0;
+    if (p < n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(chars + p);  // (the buffer has 16 B of padding)
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t m = (((w[u] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w[u]) & 0x80808080u;  // byte != 0
+            nz |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * u);
+        }
+        if (n - p < 16) nz &= (1u << (n - p)) - 1u;
+    }
+    s_nz[threadIdx.x] = nz;
+    __syncthreads();
+    const uint32_t prev = threadIdx.x ? (s_nz[threadIdx.x - 1] >> 15) & 1u : 0u;
+    st = nz & ~((nz << 1) | prev) & 0xFFFFu;
+}
+// runs and characters of chunk blockIdx.x -> rc[chunk], cc[chunk]
+__global__ void __launch_bounds__(RUN_NT) k_runs_count(const uint8_t *chars, uint64_t n, unsigned long long *rc,
+                                                       unsigned long long *cc) {
+    __shared__ uint32_t s_nz[RUN_NT];
+    __shared__ unsigned int s_r[RUN_NT / 64], s_c[RUN_NT / 64];
+    uint32_t nz, st;
+    run_masks(chars, n, (uint64_t)blockIdx.x * RUN_CH + 16ull * threadIdx.x, s_nz, nz, st);
+    unsigned int r = (unsigned int)__popc(st), c = (unsigned int)__popc(nz);
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o), c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0) s_r[threadIdx.x >> 6] = r, s_c[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long R = 0, C = 0;
+        for (unsigned int q = 0; q < RUN_NT / 64; q++) R += s_r[q], C += s_c[q];
+        rc[blockIdx.x] = R;
+        cc[blockIdx.x] = C;
+    }
+}
+// the chunk's runs and characters at the scanned bases (rb, cb: exclusive scans of rc, cc)
+__global__ void __launch_bounds__(RUN_NT) k_runs_write(const uint8_t *chars, uint64_t n, const unsigned long long *rb,
+                                                       const unsigned long long *cb, unsigned long long *rstart,
+                                                       unsigned long long *rcoff, uint8_t *rchars) {
+    __shared__ uint32_t s_nz[RUN_NT];
+    __shared__ unsigned int s_r[RUN_NT], s_c[RUN_NT];
+    const uint64_t p = (uint64_t)blockIdx.x * RUN_CH + 16ull * threadIdx.x;
+    uint32_t nz, st;
+    run_masks(chars, n, p, s_nz, nz, st);
+    const unsigned int r = (unsigned int)__popc(st), c = (unsigned int)__popc(nz);
+    s_r[threadIdx.x] = r;
+    s_c[threadIdx.x] = c;
+    __syncthreads();
+    for (unsigned int o = 1; o < RUN_NT; o <<= 1) {  // inclusive block scans
+        const unsigned int ar = threadIdx.x >= o ? s_r[threadIdx.x - o] : 0u;
+        const unsigned int ac = threadIdx.x >= o ? s_c[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_r[threadIdx.x] += ar;
+        s_c[threadIdx.x] += ac;
+        __syncthreads();
+    }
+    unsigned long long ri = rb[blockIdx.x] + s_r[threadIdx.x] - r, ci = cb[blockIdx.x] + s_c[threadIdx.x] - c;
+    for (int i = 0; i < 16; i++) {
+        if (!((nz >> i) & 1u)) continue;
+        if ((st >> i) & 1u) {
+            rstart[ri] = p + i;
+            rcoff[ri] = ci;
+            ri++;
+        }
+        rchars[ci++] = chars[p + i];
+    }
+}
+// the contig ends this rank emitted (cfirst / clast set) as EndRecs, appended
+template <typename Ops>
+__global__ void __launch_bounds__(256) k_ends_recs(const unsigned int *cfirst, const unsigned int *clast, unsigned int nc,
+                                                   const typename Ops::K *dkey, int k,
+                                                   EndRec<typename Ops::K> *out, unsigned int *nout) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nc; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (cfirst[i] != NONE32) {
+            EndRec<typename Ops::K> e;
+            e.idx = (unsigned int)i, e.pad = 0, e.code = node_code<Ops>(dkey, cfirst[i], k);
+            out[atomicAdd(nout, 1u)] = e;
+        }
+        if (clast[i] != NONE32) {
+            EndRec<typename Ops::K> e;
+            e.idx = nc + (unsigned int)i, e.pad = 0, e.code = node_code<Ops>(dkey, clast[i], k);
+            out[atomicAdd(nout, 1u)] = e;
+        }
+    }
+}
+__global__ void k_put_u64x4(unsigned long long *d, unsigned long long a, unsigned long long b, unsigned long long c,
+                            unsigned long long e) {
+    if (threadIdx.x == 0) d[0] = a, d[1] = b, d[2] = c, d[3] = e;
+}
+// collecting rank: a source's runs into the job's characters, its ends into the end table
+__global__ void __launch_bounds__(256) k_runs_scatter(const unsigned long long *rstart, const unsigned long long *rcoff,
+                                                      uint64_t nr, uint64_t nch, const uint8_t *rchars, uint8_t *chars,
+                                                      uint64_t nchars, unsigned int *bad) {
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nr; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t c0 = rcoff[r], c1 = r + 1 < nr ? rcoff[r + 1] : nch, p = rstart[r];
+        if (c1 < c0 || c1 > nch || p + (c1 - c0) > nchars) {
+            atomicOr(bad, 1u);
+            continue;
+        }
+        for (uint64_t c = c0; c < c1; c++) chars[p + (c - c0)] = rchars[c];
+    }
+}
+template <typename K>
+__global__ void __launch_bounds__(256) k_ends_scatter(const EndRec<K> *in, uint64_t n, unsigned int nc2, K *ends,
+                                                      unsigned int *bad) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const EndRec<K> e = in[i];
+        if (e.idx < nc2) ends[e.idx] = e.code;
+        else atomicOr(bad, 1u);
+    }
+}
+
 }  // namespace ec

@@ -11,12 +11,17 @@ result (the reference's per-partition contigs were never merged):
      key) and exchanged with ONE all-to-all-v (torch.distributed, backend "nccl" = RCCL);
   3. each owner merges what it received (sum of counts, min of first events) and applies the
      solid filter count > limit (build:37-39) -- the reduceByKey of ref_spark.py:84;
-  4. the solid sets are all-gathered; every rank computes the successor links of its own
-     segment of them, ranks the chains of its segment in LDS tiles, and only the chains (~1/9
-     of the nodes) and then the contig starts are all-gathered: each rank emits its own nodes'
-     characters and rank 0 collects them (one reduce) with the GFA links -- the complete,
-     reference-identical result (finish="replicated": the successor parts all-gathered and
-     every rank ranks / emits the whole set).
+  4. each rank places its merged segment at its global ids and emits the (k-1)-mer junction
+     records of its keys to the junctions' owners (an all-to-all-v; with minimizer owners
+     nearly all stay local); the owners join them into successor links (the links of other
+     ranks' nodes travel back in a second, small all-to-all-v) -- no rank holds the job's solid
+     set (junction.h);
+  5. every rank ranks the chains of its segment in LDS tiles; only the chains (~1/9 of the
+     nodes) and then the contig starts are all-gathered; each rank emits its own nodes'
+     characters and contig ends and sends rank 0 just those (runs of the positions it wrote:
+     ec_graph_emit_runs), and rank 0 collects them with the GFA links -- the complete,
+     reference-identical result.  finish="replicated" (hash owners): the solid sets and the
+     successor parts are all-gathered and every rank ranks / emits the whole set.
 
 The compute steps go through an *engine* (HipEngine = libeulerhip.so on the rank's GPU) and
 the collectives through a *comm* (TorchComm = torch.distributed).  Tests drive the same
@@ -96,6 +101,9 @@ eulerhip.register("ec_graph_starts_part", ctypes.c_int, [_P, ctypes.c_int, _P, c
 eulerhip.register("ec_graph_layout", ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)])
 eulerhip.register("ec_graph_emit_part", ctypes.c_int, [_P, _P, _P])
 eulerhip.register("ec_graph_collect", ctypes.c_int, [_P, _P, _P, _U64])
+eulerhip.register("ec_graph_emit_runs", ctypes.c_int, [_P, ctypes.POINTER(_U64)])
+eulerhip.register("ec_graph_copy_runs", ctypes.c_int, [_P, _P])
+eulerhip.register("ec_graph_collect_runs", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(_U64), _U64])
 eulerhip.register("ec_end_record_bytes", ctypes.c_int, [ctypes.c_int])
 # junction-partitioned graph (round 5, csrc/junction.h): no rank holds the job's solid set
 eulerhip.register("ec_graph_place", ctypes.c_int, [_P, _U64, _U64, ctypes.c_int, _P, ctypes.POINTER(_U64),
@@ -333,6 +341,22 @@ class HipEngine:
                                                ctypes.c_void_p(ends.data_ptr()), int(npal)))
         return self.sess.fetch(k) if fetch else None
 
+    def graph_emit_runs(self):
+        """this rank's emission as one transfer record (uint8 tensor): the runs of character
+        positions it wrote, their characters and its contig ends (ec_graph_emit_runs / copy_runs)"""
+        n = _U64(0)
+        eulerhip.check(self.L.ec_graph_emit_runs(self._h(), ctypes.byref(n)))
+        out = self.empty(n.value)
+        eulerhip.check(self.L.ec_graph_copy_runs(self._h(), ctypes.c_void_p(out.data_ptr())))
+        return out[: n.value]
+
+    def graph_collect_runs(self, recs, src_bytes, k, npal, fetch=True):
+        """the collecting rank: every rank's transfer record (rank order) -> the job's results"""
+        ns = len(src_bytes)
+        eulerhip.check(self.L.ec_graph_collect_runs(self._h(), ctypes.c_void_p(recs.data_ptr()), ns,
+                                                    (_U64 * ns)(*[int(x) for x in src_bytes]), int(npal)))
+        return self.sess.fetch(k) if fetch else None
+
     def zeros(self, nbytes):
         return self.torch.zeros(max(int(nbytes), 1), dtype=self.torch.uint8, device=self.device)
 
@@ -351,6 +375,15 @@ class TorchComm:
         self.torch, self.dist, self.group = torch, dist, group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        # gloo moves host tensors only: device tensors are staged through host memory (a
+        # multi-process test of HipEngines sharing one GPU; RCCL takes device tensors as they are)
+        self.stage = dist.get_backend(group) == "gloo"
+
+    def _h(self, t):
+        return t.cpu() if self.stage and t.is_cuda else t
+
+    def _d(self, t, dev):
+        return t.to(dev) if self.stage and dev.type == "cuda" else t
 
     def alltoallv(self, send, counts_bytes, tag=0, meta=None):
         """send: uint8 tensor laid out destination-major with counts_bytes[d] bytes for rank d.
@@ -360,24 +393,22 @@ class TorchComm:
         and meta list (rank order)."""
         torch, dist = self.torch, self.dist
         dev = send.device
+        cdev = "cpu" if self.stage else dev
         m = [int(x) for x in (meta or [])]
-        sc = torch.tensor([[int(c), int(tag)] + m for c in counts_bytes], dtype=torch.int64, device=dev)
+        sc = torch.tensor([[int(c), int(tag)] + m for c in counts_bytes], dtype=torch.int64, device=cdev)
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=self.group)
         rcv = rc.tolist()
         rcl = [int(x[0]) for x in rcv]
         total_tag = sum(int(x[1]) for x in rcv)
-        if meta is not None:
-            recv = torch.empty(max(sum(rcl), 1), dtype=torch.uint8, device=dev)
-            if sum(rcl) or sum(counts_bytes):
-                dist.all_to_all_single(recv[: sum(rcl)], send[: sum(counts_bytes)], output_split_sizes=rcl,
-                                       input_split_sizes=list(counts_bytes), group=self.group)
-            return recv[: sum(rcl)], total_tag, rcl, [[int(v) for v in x[2:]] for x in rcv]
-        recv = torch.empty(max(sum(rcl), 1), dtype=torch.uint8, device=dev)
+        recv = torch.empty(max(sum(rcl), 1), dtype=torch.uint8, device=cdev)
         if sum(rcl) or sum(counts_bytes):
-            dist.all_to_all_single(recv[: sum(rcl)], send[: sum(counts_bytes)], output_split_sizes=rcl,
+            dist.all_to_all_single(recv[: sum(rcl)], self._h(send[: sum(counts_bytes)]), output_split_sizes=rcl,
                                    input_split_sizes=list(counts_bytes), group=self.group)
-        return recv[: sum(rcl)], total_tag
+        recv = self._d(recv[: sum(rcl)], dev)
+        if meta is not None:
+            return recv, total_tag, rcl, [[int(v) for v in x[2:]] for x in rcv]
+        return recv, total_tag
 
     def allgatherv(self, t, fill=0, with_sizes=False, sizes=None):
         """Concatenation of every rank's `t` in rank order, each part padded with `fill` bytes
@@ -388,19 +419,21 @@ class TorchComm:
         torch, dist = self.torch, self.dist
         if self.world == 1:
             return (t, [t.numel()]) if with_sizes else t
+        cdev = "cpu" if self.stage else t.device
         if sizes is not None:
             szl = [int(x) for x in sizes]
             assert szl[self.rank] == t.numel(), "allgatherv: this rank's size differs from sizes[rank]"
         else:
-            n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
-            sz = torch.empty(self.world, dtype=torch.int64, device=t.device)
+            n = torch.tensor([t.numel()], dtype=torch.int64, device=cdev)
+            sz = torch.empty(self.world, dtype=torch.int64, device=cdev)
             dist.all_gather_into_tensor(sz, n, group=self.group)
             szl = [int(x) for x in sz.tolist()]
         mx = max(max(szl), 1)
-        pad = torch.full((mx,), fill, dtype=torch.uint8, device=t.device)
-        pad[: t.numel()] = t
-        out = torch.empty(self.world * mx, dtype=torch.uint8, device=t.device)
+        pad = torch.full((mx,), fill, dtype=torch.uint8, device=cdev)
+        pad[: t.numel()] = self._h(t)
+        out = torch.empty(self.world * mx, dtype=torch.uint8, device=cdev)
         dist.all_gather_into_tensor(out, pad, group=self.group)
+        out = self._d(out, t.device)
         return (out, szl) if with_sizes else out
 
     def allgather_int(self, v):
@@ -417,7 +450,10 @@ class TorchComm:
         """element-wise sum of every rank's uint8 tensor `t` into rank dst's (in place); the
         partitioned finish's characters / contig ends, each byte set by exactly one rank"""
         if self.world > 1:
-            self.dist.reduce(t, dst=dst, op=self.dist.ReduceOp.SUM, group=self.group)
+            h = self._h(t)
+            self.dist.reduce(h, dst=dst, op=self.dist.ReduceOp.SUM, group=self.group)
+            if h is not t:
+                t.copy_(h)
         return t
 
     def allreduce_vec(self, vals):
@@ -472,9 +508,11 @@ def junction_links(engine, comm, k, ur, tick=None):
 def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None, npal=None):
     """The graph finish with every rank ranking / emitting its own segment (ec_graph_chains_part ..
     ec_graph_collect): all-gathers of the chains' super records (~1/9 of the nodes on the
-    super-k-mer path) and of the contig starts, one reduce of the contig characters and end
-    codes to rank 0.  part None: a placed segment (junction_links), npal its job palindromes.
-    Returns rank 0's result (None elsewhere)."""
+    super-k-mer path) and of the contig starts, then each rank's transfer record -- the runs of
+    character positions it wrote and the contig ends it holds -- gathered to rank 0 (round 5
+    reduced job-sized character and end buffers there; engines without graph_emit_runs still
+    do).  part None: a placed segment (junction_links), npal its job palindromes.  Returns rank
+    0's result (None elsewhere)."""
     tick = tick or (lambda name: None)
     sup, _ = engine.graph_chains_part(lo, hi, part)
     tick("chains")
@@ -487,6 +525,16 @@ def partitioned_finish(engine, comm, k, lo, hi, part, fetch=True, tick=None, npa
     nc = starts.numel() // START_BYTES
     nchars = engine.graph_layout(starts, nc)
     tick("starts")
+    if hasattr(engine, "graph_emit_runs"):
+        # each rank's own characters (runs of positions it wrote) and contig ends, gathered to
+        # rank 0 (an all-to-all-v with every other destination empty): no job-sized buffer
+        rec = engine.graph_emit_runs()
+        recv, _, rcl, _ = comm.alltoallv(rec, [rec.numel() if d == 0 else 0 for d in range(comm.world)], meta=[])
+        tick("emit")
+        res = engine.graph_collect_runs(recv, rcl, k, npal, fetch=fetch) if comm.rank == 0 else None
+        tick("collect")
+        return res
+    # (engines without the transfer records: job-sized buffers reduced to rank 0)
     chars = engine.zeros(nchars)
     ends = engine.zeros(max(2 * nc * end_bytes(k), 8))
     engine.graph_emit_part(chars, ends)
@@ -776,6 +824,15 @@ def local_partitioned_finish(engines, segs, k, npal):
     sts = [eng.graph_starts_part(M > 0, lo, hi)[0] for eng, (lo, hi, _) in zip(engines, segs)]
     starts = torch.cat([x.to(dev) for x in sts])
     nc = starts.numel() // START_BYTES
+    if hasattr(engines[0], "graph_emit_runs"):  # as partitioned_finish: transfer records gathered
+        recs = []
+        for eng in engines:
+            eng.graph_layout(starts.to(eng.device), nc)
+            recs.append(eng.graph_emit_runs().to(dev))
+        sizes = [r.numel() for r in recs]
+        allr = torch.cat(recs) if len(recs) > 1 else recs[0]
+        del recs
+        return engines[0].graph_collect_runs(allr, sizes, k, npal)
     chars, ends = None, None
     for eng in engines:
         nchars = eng.graph_layout(starts.to(eng.device), nc)

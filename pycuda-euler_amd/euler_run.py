@@ -9,10 +9,13 @@ partitions (src/cli_spark_gpu.py:37), whose per-partition contigs were never mer
 
 Every rank parses the file with the native reader (csrc/ingest.cpp) and moves only its
 contiguous read shard to its GPU; the counts are exchanged by owner with one RCCL
-all-to-all-v, owners merge and filter, the solid set is all-gathered and the graph phase runs
-on every rank (distributed.py).  Rank 0 writes the outputs.  With one process the fused
-single-GPU path runs instead.  Contigs equal referenceAssembler.all_contigs(build(reads, k,
-limit), k) with reads parsed as --fasta-mode says.
+all-to-all-v, owners merge and filter, and the graph is built, ranked and emitted in owner
+segments (distributed.sharded_assemble: junction join, partitioned finish).  Rank 0 writes
+the outputs.  With one process the fused single-GPU path runs instead (--sharded: the sharded
+path at any world size).  --backend gloo with --device N puts every rank on GPU N, the
+collectives staged through host memory (tests: several ranks of the real engine on one GPU).
+Contigs equal referenceAssembler.all_contigs(build(reads, k, limit), k) with reads parsed as
+--fasta-mode says.
 """
 import argparse
 import os
@@ -36,6 +39,10 @@ def main(argv=None):
     ap.add_argument("--fasta-mode", choices=["records", "lines"], default="records",
                     help="records: SeqIO-style multi-line records; lines: one read per line (src/eulercuda.py)")
     ap.add_argument("--threads", type=int, default=0, help="ingest threads (0: up to 16)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend (nccl = RCCL over xGMI; gloo stages through host memory)")
+    ap.add_argument("--device", type=int, default=-1, help="GPU of every rank (default: LOCAL_RANK)")
+    ap.add_argument("--sharded", action="store_true", help="the sharded path even with one process")
     a = ap.parse_args(argv)
 
     import torch
@@ -46,7 +53,7 @@ def main(argv=None):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if a.device < 0 else a.device
     torch.cuda.set_device(local)
     t0 = time.time()
     rs = ingest.ReadSet(a.input, None, a.threads, a.fasta_mode)
@@ -59,7 +66,8 @@ def main(argv=None):
     d_off = torch.from_numpy(off.astype(np.int64)).cuda()
     torch.cuda.synchronize()
     t1 = time.time()
-    if world == 1:
+    sharded = world > 1 or a.sharded
+    if not sharded:
         sess = eulerhip.Session(local, stream=torch.cuda.current_stream().cuda_stream)
         sess.run_device(d_buf.data_ptr(), d_off.data_ptr(), hi - lo, a.k, a.limit, 0)
         res = sess.fetch(a.k)
@@ -67,7 +75,10 @@ def main(argv=None):
     else:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
         eng = distributed.HipEngine(local, stream=torch.cuda.current_stream().cuda_stream)
         res, P = distributed.sharded_assemble(eng, distributed.TorchComm(), d_buf, d_off, hi - lo, lo, a.k, a.limit)
     torch.cuda.synchronize()
@@ -82,7 +93,7 @@ def main(argv=None):
               file=sys.stderr)
         if not a.output and not a.gfa:
             sys.stdout.write("".join(">contig%d\n%s\n" % (i, c) for i, c in enumerate(res.contigs)))
-    if world > 1:
+    if sharded:
         import torch.distributed as dist
 
         dist.barrier()

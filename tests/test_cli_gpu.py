@@ -62,3 +62,32 @@ def test_torchrun_rccl_one_rank(readfile, tmp_path):
           "127.0.0.1", "--master-port", port, RUN, "-i", path, "-k", "25", "-o", "c.fa"], tmp_path)
     fa, _ = _expected(reads, 25, 1)
     assert (tmp_path / "c.fa").read_text() == fa
+
+
+def test_torchrun_rccl_one_rank_sharded(readfile, tmp_path):
+    """the sharded step itself over a real RCCL group (world 1): TorchComm's all-to-all-v,
+    all-gathers and the run gather to rank 0 on device tensors, HipEngine's calls in between"""
+    path, reads = readfile
+    port = str(29300 + os.getpid() % 300)
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+          "127.0.0.1", "--master-port", port, RUN, "-i", path, "-k", "31", "--sharded", "-o", "c.fa", "--gfa",
+          "g.gfa"], tmp_path)
+    fa, gfa = _expected(reads, 31, 1)
+    assert (tmp_path / "c.fa").read_text() == fa
+    assert (tmp_path / "g.gfa").read_text() == gfa
+
+
+@pytest.mark.parametrize("world,k", [(2, 31), (3, 25), (2, 51)])
+def test_torchrun_gloo_ranks_share_one_gpu(readfile, tmp_path, world, k):
+    """N > 1 processes of the product engine (HipEngine on one MI355X) driven by TorchComm over
+    gloo, device tensors staged through host memory: the multi-GPU orchestration with real
+    collectives between real engines (the 8-GPU RCCL run is the driver's), bit-exact against the
+    oracle (contigs, GFA)"""
+    path, reads = readfile
+    port = str(29000 + os.getpid() % 300 + 7 * world + k)
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+          "--master-addr", "127.0.0.1", "--master-port", port, RUN, "-i", path, "-k", str(k), "--backend", "gloo",
+          "--device", "0", "-o", "c.fa", "--gfa", "g.gfa"], tmp_path)
+    fa, gfa = _expected(reads, k, 1)
+    assert (tmp_path / "c.fa").read_text() == fa
+    assert (tmp_path / "g.gfa").read_text() == gfa
