@@ -314,6 +314,8 @@ struct ec_session {
     // the partitioned finish's transfer record (ec_graph_emit_runs / ec_graph_copy_runs):
     // chunk counts and scans, this rank's end records, the record's sizes
     DevBuf run_cnt, run_ends, run_dends;
+    DevBuf rt_lb;                 // k_tile_chains' look-back status words (rank_tile.h TileLB)
+    unsigned long long lb_epoch = 0;
     uint64_t run_nr = 0, run_nch = 0, run_nends = 0;
     bool runs_ready = false;
 };
@@ -2414,13 +2416,14 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
 // weighted ruling set; per chain its path key / rank (rt_pks / rt_rks), paths' and cycles'
 // length / min first event at their key nodes (PL / PM)
 int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr, int &rounds,
-                bool pre_init = false) {
+                bool pre_init = false, const unsigned int *sidx = nullptr) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc{};
     SuperRec *srec = s->rt_srec.as<SuperRec>();
-    unsigned int *SIDX = s->rt_sidx.as<unsigned int>();
+    // (sidx: head node -> super index; the look-back compaction's LH serves, being that at heads)
+    const unsigned int *SIDX = sidx ? sidx : s->rt_sidx.as<unsigned int>();
     const size_t cap = std::max<size_t>(M, 1);
     EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec)));
     EC_CHECK(s->rt_hasp.ensure(cap));
@@ -2492,7 +2495,7 @@ int rank_supers(ec_session *s, unsigned int M, unsigned int N, unsigned int &nr,
 // chains without a sampled one) are caught by the caller's next scalar read (nvisited < M),
 // which redoes the ranking with rank_supers.  Needs k_tile_compact's initialisation (pre_init).
 int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *dM, int &rounds,
-                      unsigned int mcap = 0) {
+                      unsigned int mcap = 0, const unsigned int *sidx = nullptr) {
     // mcap: a bound of the chain count known on the host (the partitioned finish's gathered
     // list) -- grids and Wyllie rounds sized by it instead of the node count N, which stays the
     // cycle bound of the jumps (j.s < N)
@@ -2513,7 +2516,8 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
     const unsigned int *dnr = &dsc->nr;
     const unsigned int gs = std::min(grid_for(G, B), 4096u);  // grid-stride grids over <= G items
-    k_super_link<<<gs, B, 0, st>>>(srec, 0, s->rt_sidx.as<unsigned int>(), snrec, s->rt_hasp.as<uint8_t>(), dM);
+    k_super_link<<<gs, B, 0, st>>>(srec, 0, sidx ? sidx : s->rt_sidx.as<unsigned int>(), snrec,
+                                   s->rt_hasp.as<uint8_t>(), dM);
     const unsigned int smask = kn().sruler_mask > 0 ? (unsigned int)kn().sruler_mask : 15u;
     const unsigned int nblk = (G + RULER_CHUNK - 1) / RULER_CHUNK;
     k_srulers_count<<<nblk, B, 0, st>>>(s->rt_hasp.as<uint8_t>(), 0, smask, 1, s->rid.as<uint2>(),
@@ -2762,29 +2766,46 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         static_assert(sizeof(SuperRec) == sizeof(RJump), "tile scratch in the ruler state buffer");
         unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
         EC_CHECK(s->rt_hasp.ensure(Nn));  // (sized here: k_tile_compact initialises it for rank_supers)
-        k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
-                                                s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(), LH,
-                                                LR, tcnt, scratch, s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
-                                                s->PL.as<unsigned int>(), s->PM.as<unsigned long long>(), 0u, tbp);
-        EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
         // (2) the super list: compacted in tile order, linked, ranked by the weighted ruling set
         // (round 4 measured the same sequence as one cooperative launch: rank stage 0.63 -> 3.3
         // ms, its grid barriers far slower than the launches they replace; removed in round 5)
         unsigned int M = 0;
         rank_async = kn().rank_sync != 1;
-        async_M = tbase + ntiles;
         async_LH = LH;
         async_LR = LR;
         if (rank_async) {  // no read-back: the checks ride on the scalar read after the starts
-            k_tile_compact<<<ntiles, 256, 0, st>>>(scratch, tcnt, tbase, s->rt_srec.as<SuperRec>(),
-                                                   s->rt_sidx.as<unsigned int>(), s->rt_hasp.as<uint8_t>(),
-                                                   s->rid.as<uint2>(), &dsc->nr, &dsc->nvisited, &dsc->chains,
-                                                   tbp);
-            EC_CHECK(rank_supers_async(s, N, async_M, rounds));
-            k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, s->rt_sidx.as<unsigned int>(), s->rt_pks.as<unsigned int>(),
+            // the chains compacted by look-back in k_tile_chains itself (round 6: no scan, no
+            // k_tile_compact, LH = super index); the status words are cleared once per allocation
+            void *old = s->rt_lb.p;
+            EC_CHECK(s->rt_lb.ensure(((size_t)ntiles + 1) * 8));
+            if (s->rt_lb.p != old) {
+                EC_HIP(hipMemsetAsync(s->rt_lb.p, 0, s->rt_lb.cap, st));
+                s->lb_epoch = 0;
+            }
+            s->lb_epoch = (s->lb_epoch + 1) & ((1ull << 30) - 1);
+            if (s->lb_epoch == 0) {  // (wrapped: words of 2^30 calls ago could match)
+                EC_HIP(hipMemsetAsync(s->rt_lb.p, 0, s->rt_lb.cap, st));
+                s->lb_epoch = 1;
+            }
+            TileLB lb{s->rt_lb.as<unsigned long long>(), s->lb_epoch, s->rt_srec.as<SuperRec>(),
+                      s->rt_hasp.as<uint8_t>(), s->rid.as<uint2>(), &dsc->chains, &dsc->nr, &dsc->nvisited};
+            async_M = &dsc->chains;
+            k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
+                                                    s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                    LH, LR, tcnt, scratch, s->PK.as<unsigned int>(),
+                                                    s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
+                                                    s->PM.as<unsigned long long>(), 0u, tbp, lb);
+            EC_CHECK(rank_supers_async(s, N, async_M, rounds, 0, LH));
+            k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, nullptr, s->rt_pks.as<unsigned int>(),
                                                   s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
                                                   s->RK.as<unsigned int>());
         } else {
+            k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
+                                                    s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
+                                                    LH, LR, tcnt, scratch, s->PK.as<unsigned int>(),
+                                                    s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
+                                                    s->PM.as<unsigned long long>(), 0u, tbp);
+            EC_CHECK(scan_u64(s, tcnt, tbase, (size_t)ntiles + 1));
             // the chain count read back while k_tile_compact (sized by the tiles, not by M) runs:
             // the host's wake-up and next launches overlap the compaction
             unsigned long long M64 = 0;
@@ -2912,10 +2933,11 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                 fprintf(stderr, "rank: one ruler pass covered %llu of %u chains, ranking again\n",
                         (unsigned long long)hsc.nvisited, Ma);
             rank_async = false;
-            EC_CHECK(rank_supers(s, Ma, N, nr, rounds));
-            k_expand<<<grid_for(N, B), B, 0, st>>>(async_LH, async_LR, N, s->rt_sidx.as<unsigned int>(),
-                                                  s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>(),
-                                                  s->PK.as<unsigned int>(), s->RK.as<unsigned int>());
+            // (the look-back compaction's LH: super index per node, at heads the head -> index map)
+            EC_CHECK(rank_supers(s, Ma, N, nr, rounds, false, async_LH));
+            k_expand<<<grid_for(N, B), B, 0, st>>>(async_LH, async_LR, N, nullptr, s->rt_pks.as<unsigned int>(),
+                                                  s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
+                                                  s->RK.as<unsigned int>());
             s->stats.n_rulers = nr;
             EC_CHECK(starts_pass());
         }
@@ -3928,7 +3950,7 @@ static void for_each_buf(ec_session *s, Fn fn) {
                      &s->rt_snrec, &s->rt_sidx, &s->rt_pks, &s->rt_rks, &s->rt_hasp, &s->rt_lr, &s->wbv, &s->bmark, &s->rt_tb,
                      &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec,
                      &s->skm_rec, &s->skm_ev, &s->skm_end, &s->wcodes_tab,
-                     &s->run_cnt, &s->run_ends, &s->run_dends};
+                     &s->run_cnt, &s->run_ends, &s->run_dends, &s->rt_lb};
     for (auto *b : all) fn(*b);
 }
 

@@ -43,18 +43,76 @@ struct alignas(16) SNodeRec {
     unsigned long long fev;  // min first event over the chain
 };
 
+// The one-GPU ranking (round 6) compacts the chains in the same launch: each tile's chain count
+// is published in a status word and its global base found by a decoupled look-back over the
+// preceding tiles (a wave reads 64 of them at once; workgroups are dispatched in index order, so
+// every tile it waits on is running or done).  The chains go straight to the super list, and
+// LH holds the chain's super index instead of its head node -- no scan, no k_tile_compact, no
+// head -> index map (SIDX).  Status word: epoch (30 bits: this call) | flag (2: 1 = the tile's
+// own count, 2 = its inclusive prefix) | value (32).
+struct TileLB {
+    unsigned long long *status;  // ntiles words (cleared when allocated; the epoch tells calls apart)
+    unsigned long long epoch;
+    SuperRec *srec;              // the super list
+    uint8_t *hasp;               // rank_supers_async's state, set up per chain
+    uint2 *rid;
+    unsigned long long *nchains; // the last tile writes M
+    unsigned int *nr;            // ... and zeroes the ruler count and visit total
+    unsigned long long *nvisited;
+};
+__device__ inline unsigned long long lb_word(unsigned long long epoch, unsigned int flag, unsigned int v) {
+    return (epoch << 34) | ((unsigned long long)flag << 32) | v;
+}
+// wave 0 of the tile's workgroup: the exclusive prefix of the chain counts before tile t
+__device__ inline unsigned long long tile_lookback(const TileLB &lb, unsigned int t, unsigned int cnt,
+                                                   unsigned int lane) {
+    unsigned long long *st = lb.status;
+    if (lane == 0)
+        __hip_atomic_store(&st[t], lb_word(lb.epoch, t == 0 ? 2u : 1u, cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long excl = 0;
+    long long j0 = (long long)t - 1;
+    while (j0 >= 0) {
+        const long long j = j0 - (long long)lane;
+        unsigned long long w = 0;
+        unsigned int flag = 2;  // (lanes past tile 0: as if inclusive zero)
+        if (j >= 0) {
+            do {
+                w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                flag = (w >> 34) == lb.epoch ? (unsigned int)(w >> 32) & 3u : 0u;
+            } while (flag == 0);
+        } else {
+            w = 0;
+        }
+        const unsigned int v = j >= 0 ? (unsigned int)w : 0u;
+        const unsigned long long incl = __ballot(flag == 2);  // (never empty once j0 < 64)
+        const unsigned int stop = incl ? (unsigned int)__ffsll((long long)incl) - 1u : 64u;  // nearest inclusive
+        unsigned long long part = lane <= stop ? (unsigned long long)v : 0ull;
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        excl += part;
+        if (incl) break;
+        j0 -= 64;
+    }
+    if (lane == 0)
+        __hip_atomic_store(&st[t], lb_word(lb.epoch, 2u, (unsigned int)(excl + cnt)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 // nodes [n0, N): the tiles of a segment (the multi-GPU finish ranks its own segment's chains;
-// a successor outside the segment is external like one outside the tile)
+// a successor outside the segment is external like one outside the tile).  lb.status set: the
+// chains compacted in this launch (above; LH = super index), else tile-local records in scratch
+// for k_tile_compact (LH = head node).
 __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, const unsigned int *succ, unsigned int N,
                                                        const unsigned long long *dfc, const unsigned long long *dft,
                                                        unsigned int *LH, unsigned int *LR, unsigned long long *tcnt,
                                                        SuperRec *scratch, unsigned int *PK, unsigned int *RK,
                                                        unsigned int *PL, unsigned long long *PM, unsigned int n0 = 0,
-                                                       const unsigned int *tb = nullptr) {
+                                                       const unsigned int *tb = nullptr, TileLB lb = TileLB{}) {
     __shared__ uint16_t s_ls[RT_TN], s_lp[RT_TN], s_p[RT_TN], s_mn[RT_TN];
     __shared__ unsigned int s_d[RT_TN], s_cl[RT_TN];
     __shared__ unsigned long long s_cm[RT_TN];
-    __shared__ unsigned int s_wsum[RT_NT / 64];
+    __shared__ unsigned int s_wsum[RT_PER][RT_NT / 64];
+    __shared__ unsigned long long s_gbase;
     // tiles of RT_TN nodes from n0, or tb's tiles (k_tile_plan: cut at bucket starts, <= RT_TN)
     const unsigned int tile = blockIdx.x, tid = threadIdx.x;
     const unsigned int base = tb ? tb[tile] : n0 + tile * RT_TN;
@@ -174,6 +232,60 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         atomicMax(&s_cl[h], d[q] + 1);
         if (fev[q] < s_cm[h]) atomicMin(&s_cm[h], fev[q]);
     }
+    // the heads in node order (q-major: node i = tid + q * NT): a wave's count per q
+    const unsigned int lane = tid & 63, wid = tid >> 6;
+    unsigned long long hm[RT_PER];
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        hm[q] = __ballot(valid[q] && !cyc[q] && d[q] == 0);
+        if (lane == 0) s_wsum[q][wid] = (unsigned int)__popcll(hm[q]);
+    }
+    __syncthreads();
+    unsigned int off = 0;
+    for (int q = 0; q < RT_PER; q++)
+        for (unsigned int w = 0; w < RT_NT / 64; w++) off += s_wsum[q][w];
+    const bool direct = lb.status != nullptr;
+    if (direct && wid == 0) {
+        const unsigned long long g = tile_lookback(lb, tile, off, lane);
+        if (lane == 0) {
+            s_gbase = g;
+            if (tile + 1 == gridDim.x) {
+                *lb.nchains = g + off;
+                *lb.nr = 0;
+                *lb.nvisited = 0;
+            }
+        }
+    }
+    if (tile == 0 && tid == 0) tcnt[gridDim.x] = 0;  // (k_tile_compact's scan: its last element)
+    __syncthreads();
+    const unsigned long long gb = direct ? s_gbase : 0ull;
+    SuperRec *out = direct ? lb.srec + gb : scratch + soff;
+    unsigned int before = 0;  // heads of the earlier q
+#pragma unroll
+    for (int q = 0; q < RT_PER; q++) {
+        const unsigned int i = tid + q * RT_NT;
+        unsigned int o = before;
+        for (unsigned int w = 0; w < wid; w++) o += s_wsum[q][w];
+        for (unsigned int w = 0; w < RT_NT / 64; w++) before += s_wsum[q][w];
+        if ((hm[q] >> lane) & 1ull) {
+            const unsigned int j = o + (unsigned int)__popcll(hm[q] & ((1ull << lane) - 1));
+            // the chain's tail: the node at distance len - 1 from the head has no in-tile successor;
+            // its successor is filled in below by the tail's thread
+            SuperRec r;
+            r.head = base + i;
+            r.succ = NONE32;
+            r.w = s_cl[i];
+            r.pad = 0;
+            r.fmin = s_cm[i];
+            r.pad2 = 0;
+            out[j] = r;
+            if (direct) {
+                lb.hasp[gb + j] = 0;
+                lb.rid[gb + j] = make_uint2(NONE32, NONE32);
+            }
+            s_ls[i] = (uint16_t)j;  // (reused: head -> its index among the tile's heads)
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < RT_PER; q++) {
@@ -192,48 +304,12 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
                 PM[h] = s_cm[p[q]];
             }
         } else {
-            LH[x] = h;
+            const unsigned int j = s_ls[p[q]];
+            LH[x] = direct ? (unsigned int)(gb + j) : h;
+            // a chain's tail writes its external successor into the chain's record
+            if (d[q] + 1 == s_cl[p[q]] && ext[q] != NONE32) out[j].succ = ext[q];
         }
         LR[x] = d[q];
-    }
-    // compaction of the heads in node order (q-major: node i = tid + q * NT)
-    const unsigned int lane = tid & 63, wid = tid >> 6;
-    unsigned int off = 0;
-#pragma unroll
-    for (int q = 0; q < RT_PER; q++) {
-        const unsigned int i = tid + q * RT_NT;
-        const bool hd = valid[q] && !cyc[q] && d[q] == 0;
-        const unsigned long long m = __ballot(hd);
-        if (lane == 0) s_wsum[wid] = (unsigned int)__popcll(m);
-        __syncthreads();
-        unsigned int o = off;
-        for (unsigned int w = 0; w < wid; w++) o += s_wsum[w];
-        unsigned int tot = 0;
-        for (unsigned int w = 0; w < RT_NT / 64; w++) tot += s_wsum[w];
-        if (hd) {
-            const unsigned int j = o + (unsigned int)__popcll(m & ((1ull << lane) - 1));
-            // the chain's tail: the node at distance len - 1 from the head has no in-tile successor;
-            // its successor is filled in below by the tail's thread
-            SuperRec r;
-            r.head = base + i;
-            r.succ = NONE32;
-            r.w = s_cl[i];
-            r.pad = 0;
-            r.fmin = s_cm[i];
-            r.pad2 = 0;
-            scratch[soff + j] = r;
-            s_ls[i] = (uint16_t)j;  // (reused: head -> its index among the tile's heads)
-        }
-        off += tot;
-        __syncthreads();
-    }
-    // a chain's tail writes its external successor into the chain's record
-#pragma unroll
-    for (int q = 0; q < RT_PER; q++) {
-        if (!valid[q] || cyc[q]) continue;
-        const unsigned int i = tid + q * RT_NT;
-        if (d[q] + 1 == s_cl[p[q]] && ext[q] != NONE32) scratch[soff + s_ls[p[q]]].succ = ext[q];
-        (void)i;
     }
     if (tid == 0) tcnt[tile] = off;
 }
@@ -495,7 +571,8 @@ __global__ void __launch_bounds__(256) k_cycle_len_s(const unsigned int *nextR, 
     }
 }
 
-// every node: its chain's path key and rank + its offset in the chain
+// every node: its chain's path key and rank + its offset in the chain (SIDX null: LH holds the
+// chain's super index itself)
 __global__ void __launch_bounds__(256) k_expand(const unsigned int *LH, const unsigned int *LR, unsigned int N,
                                                 const unsigned int *SIDX, const unsigned int *PKs,
                                                 const unsigned int *RKs, unsigned int *PK, unsigned int *RK,
@@ -503,7 +580,7 @@ __global__ void __launch_bounds__(256) k_expand(const unsigned int *LH, const un
     for (uint64_t t = n0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int h = LH[t];
         if (h == NONE32 || (h & RT_FIN)) continue;  // palindrome twin / in-tile cycle (done)
-        const unsigned int si = SIDX[h];
+        const unsigned int si = SIDX ? SIDX[h] : h;
         PK[t] = PKs[si];
         RK[t] = RKs[si] + LR[t];
     }
