@@ -2776,9 +2776,10 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         if (rank_async) {  // no read-back: the checks ride on the scalar read after the starts
             // the chains compacted by look-back in k_tile_chains itself (round 6: no scan, no
             // k_tile_compact, LH = super index); the status words are cleared once per allocation
-            void *old = s->rt_lb.p;
+            // (a reallocation is told by the capacity: the new block may come back at the old address)
+            const size_t oldcap = s->rt_lb.cap;
             EC_CHECK(s->rt_lb.ensure(((size_t)ntiles + 1) * 8));
-            if (s->rt_lb.p != old) {
+            if (s->rt_lb.cap != oldcap) {
                 EC_HIP(hipMemsetAsync(s->rt_lb.p, 0, s->rt_lb.cap, st));
                 s->lb_epoch = 0;
             }

@@ -705,6 +705,70 @@ class ShardedAssembler:
         return self.count_stats
 
 
+def streaming_assemble(engine, buf, off, k, limit=1, chunk_reads=4_000_000, fold=4, read_base=0, flags=0,
+                       stats=None):
+    """Out-of-core count on one GPU for read sets whose one-shot count does not fit its memory
+    (BASELINE config 5 on fewer than 8 GPUs, larger genomes; the reference's chunk loop,
+    src/eulercuda.py:99-119, never finished).  The reads (host arrays: buf, uint64 offsets) go
+    through the shard count chunk_reads at a time -- each chunk's distinct k-mers exported with
+    their counts and first events (compact records, events relative to the chunk), the count's
+    buffers released -- and every `fold` chunks the pending records are merged into one running
+    set (counts summed, first events min'd, no filter: limit -1).  The last merge applies the
+    solid filter; the graph (junction join), ranking and emission then run on the merged set as
+    the one rank of the partitioned flow.  Events are global read ids from read_base, so the
+    dict order, contigs and links equal the one-shot assembly's (tests: bit-exact vs the oracle
+    at forced small chunks).  stats (a dict): chunks, folds, device-buffer peak, positions.
+    Returns (result, k-mer positions)."""
+    import torch
+
+    dev = engine.device
+    nreads = len(off) - 1
+    chunk_reads = max(1, int(chunk_reads))
+    k = int(k)
+    P = 0
+    running = None  # (records, lf_bits, read base) of the merged chunks so far
+    pending = []
+    nfold = 0
+    nchunks = 0
+
+    def merge(srcs, lim, export):
+        recs = torch.cat([r for r, _, _ in srcs]) if len(srcs) > 1 else srcs[0][0]
+        return engine.merge_owned_from(recs, [r.numel() for r, _, _ in srcs], [b for _, _, b in srcs],
+                                       [f for _, f, _ in srcs], k, lim, flags, export=export)
+
+    engine.set_owner_rule(OWNER_MINIMIZER)
+    for c0 in range(0, max(nreads, 1), chunk_reads):
+        c1 = min(nreads, c0 + chunk_reads)
+        b0, b1 = int(off[c0]), int(off[c1])
+        d_reads = torch.from_numpy(np.ascontiguousarray(buf[b0:b1]) if b1 > b0 else np.zeros(1, np.uint8)).to(dev)
+        d_off = torch.from_numpy((np.asarray(off[c0:c1 + 1]) - off[c0]).astype(np.int64)).to(dev)
+        st = engine.count_shard(d_reads, d_off, c1 - c0, read_base + c0, k, flags)
+        P += st.n_positions
+        recs, _, lfb = engine.export_by_owner(1, compact=True)
+        del d_reads, d_off
+        engine.sess.trim(64 << 20)  # (the count's buffers: the next chunk or the merge reuses the memory)
+        pending.append((recs, lfb, read_base + c0 if lfb >= 0 else 0))
+        nchunks += 1
+        if len(pending) >= fold and c1 < nreads:  # fold the pending chunks into the running set
+            merged = merge(([running] if running else []) + pending, -1, True)
+            running = (merged, -1, 0)  # (full records, global events)
+            pending = []
+            nfold += 1
+            engine.sess.trim(64 << 20)
+    ur = merge(([running] if running else []) + pending, limit, False)
+    running = None
+    pending = []
+    jrecs, _, npal = engine.graph_place(0, ur, 1)
+    links, _ = engine.graph_join(jrecs, [0, ur])
+    del jrecs
+    engine.graph_links_apply(links)
+    del links
+    res = local_partitioned_finish([engine], [(0, ur, None)], k, npal)
+    if stats is not None:
+        stats.update(chunks=nchunks, folds=nfold, positions=P, solid=ur)
+    return res, P
+
+
 def local_sharded_assemble(engines, buf, off, k, limit=1, flags=0, partitioned=None, finish="auto", compact=True):
     """Simulate the distributed algorithm with len(engines) ranks on the local device(s):
     same engine calls, the collectives done by concatenation.  Returns rank 0's result."""

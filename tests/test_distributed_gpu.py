@@ -381,3 +381,33 @@ def test_junction_join_split_and_retries(engines, monkeypatch, knobs, k):
     assert res.stats.n_dict == ref["n_dict"]
     assert res.contig_bytes == ref["contig_chars"]
     assert res.links == oracle.unpack_links(ref)
+
+
+@pytest.mark.parametrize("k,L,g,n,chunk,fold,err,base", [(51, 150, 2_000_000, 1_000_000, 150_000, 3, 0.0, 0),
+                                                         (31, 100, 300_000, 200_000, 37_000, 2, 0.003, 5_000_000),
+                                                         (25, 100, 50_000, 30_000, 7_000, 10, 0.01, 0),
+                                                         (45, 120, 60_000, 20_000, 20_000, 4, 0.002, 0)])
+def test_streaming_count_vs_oracle(k, L, g, n, chunk, fold, err, base):
+    """out-of-core count (distributed.streaming_assemble): the reads counted chunk by chunk (the
+    count's buffers released after each chunk's export), the chunks' records folded into a
+    running merged set, the final merge filtered, then the junction graph and partitioned
+    finish of one rank -- forced small chunks, bit-exact against the oracle (contigs, offsets,
+    GFA links, dict size); BASELINE config 5's read shape at 10^8 positions among them"""
+    import distributed
+
+    buf, off = make_reads(g, n, L, 9500 + k, err=err)
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    eng = distributed.HipEngine(0)
+    try:
+        stats = {}
+        res, P = distributed.streaming_assemble(eng, buf, off, k, 1, chunk_reads=chunk, fold=fold, read_base=base,
+                                                stats=stats)
+    finally:
+        eng.sess.close()
+    assert stats["chunks"] == (n + chunk - 1) // chunk
+    assert stats["folds"] == (stats["chunks"] - 1) // fold
+    assert P == ref["n_positions"]
+    assert res.stats.n_dict == ref["n_dict"]
+    assert res.contig_bytes == ref["contig_chars"]
+    assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
+    assert res.links == oracle.unpack_links(ref)
