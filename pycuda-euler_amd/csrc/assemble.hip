@@ -2734,6 +2734,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     bool rank_async = false;     // rank_supers_async: its checks wait for the next scalar read
     const unsigned long long *async_M = nullptr;  // (the chain count on the device)
     unsigned int *async_LH = nullptr, *async_LR = nullptr;
+    bool chain_paths = false;  // PK / RK of the tile ranking read through the chains (PathOf)
     s->stats.rank_rounds = 0;
     if (U && tile_rank) {
         // (1) chains of in-tile links ranked in LDS, in-tile cycles finished (rank_tile.h)
@@ -2797,9 +2798,8 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                                                     s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
                                                     s->PM.as<unsigned long long>(), 0u, tbp, lb);
             EC_CHECK(rank_supers_async(s, N, async_M, rounds, 0, LH));
-            k_expand<<<grid_for(N, B), B, 0, st>>>(LH, LR, N, nullptr, s->rt_pks.as<unsigned int>(),
-                                                  s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
-                                                  s->RK.as<unsigned int>());
+            // (3) no k_expand: every reader takes a node's key and rank from its chain (PathOf)
+            chain_paths = true;
         } else {
             k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), N,
                                                     s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
@@ -2879,6 +2879,9 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     mark(s, 2 * EC_STAGE_RANK + 1);
 
     // ---- starts + order -------------------------------------------------------------------
+    const PathOf P = chain_paths ? PathOf{s->PK.as<unsigned int>(), s->RK.as<unsigned int>(), async_LH, async_LR,
+                                          s->rt_pks.as<unsigned int>(), s->rt_rks.as<unsigned int>()}
+                                 : path_of(s->PK.as<unsigned int>(), s->RK.as<unsigned int>());
     mark(s, 2 * EC_STAGE_STARTS);
     EC_CHECK(s->cidxOf.ensure(Nn * 4));
     EC_CHECK(s->skeys.ensure(Nn * 8));
@@ -2903,12 +2906,12 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         EC_CHECK(s->cand.ensure(std::max<size_t>(Nn * 4, (Nn / 64 + 8) * 8)));
         unsigned long long *smask = s->cand.as<unsigned long long>();
         k_starts_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
-                                           s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                           s->dft.as<unsigned long long>(), P,
                                            s->PM.as<unsigned long long>(), N, bc, smask,
                                            nx ? s->x_in.as<uint8_t>() : nullptr);
         EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
         k_starts_write<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
-                                           s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                           s->dft.as<unsigned long long>(), P,
                                            s->PM.as<unsigned long long>(), N, bs, smask,
                                            s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(), 0u,
                                            &dsc->nstarts);
@@ -2935,10 +2938,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
                         (unsigned long long)hsc.nvisited, Ma);
             rank_async = false;
             // (the look-back compaction's LH: super index per node, at heads the head -> index map)
-            EC_CHECK(rank_supers(s, Ma, N, nr, rounds, false, async_LH));
-            k_expand<<<grid_for(N, B), B, 0, st>>>(async_LH, async_LR, N, nullptr, s->rt_pks.as<unsigned int>(),
-                                                  s->rt_rks.as<unsigned int>(), s->PK.as<unsigned int>(),
-                                                  s->RK.as<unsigned int>());
+            EC_CHECK(rank_supers(s, Ma, N, nr, rounds, false, async_LH));  // (PathOf reads the new PKs / RKs)
             s->stats.n_rulers = nr;
             EC_CHECK(starts_pass());
         }
@@ -2987,7 +2987,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     if (small)
         k_starts_small<<<1, SMALL_STARTS_NT, 0, st>>>(
             s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(), nc, s->upal.as<uint8_t>(),
-            s->PK.as<unsigned int>(), s->RK.as<unsigned int>(), s->PL.as<unsigned int>(), k,
+            P, s->PL.as<unsigned int>(), k,
             s->svals2.as<unsigned int>(), s->cidxOf.as<unsigned int>(), s->coff.as<unsigned long long>(),
             s->cwalk.as<Walk>(), s->ewalk.as<EWalk>());
     if (nsort && !small)
@@ -2998,8 +2998,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->clen.ensure((size_t)(nc + 1) * 8));
     EC_HIP(hipMemsetAsync(s->clen.p, 0, (size_t)(nc + 1) * 8, st));
     if (nc) {
-        k_contig_len<<<grid_for(nc, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(),
-                                                   s->RK.as<unsigned int>(), s->PL.as<unsigned int>(), sorted_nodes, nc,
+        k_contig_len<<<grid_for(nc, B), B, 0, st>>>(s->upal.as<uint8_t>(), P, s->PL.as<unsigned int>(), sorted_nodes, nc,
                                                    k, s->cidxOf.as<unsigned int>(), s->clen.as<unsigned long long>(),
                                                    s->cwalk.as<Walk>(), nx ? s->x_len.as<unsigned int>() : nullptr,
                                                    nx ? s->x_cid.as<unsigned int>() : nullptr);
@@ -3048,7 +3047,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
         k_ewalk<<<grid_for(nc, B), B, 0, st>>>(s->cwalk.as<Walk>(), s->coff.as<unsigned long long>(), nc,
                                               s->ewalk.as<EWalk>());
     if (U)
-        k_emit<Ops><<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
+        k_emit<Ops><<<grid_for(N, B), B, 0, st>>>(s->upal.as<uint8_t>(), P,
                                             s->PL.as<unsigned int>(), s->dkey.as<typename Ops::K>(),
                                             s->cidxOf.as<unsigned int>(), s->ewalk.as<EWalk>(),
                                             N, k, s->chars.as<char>(), std::max<uint64_t>(chars_bound, 1),
@@ -3336,12 +3335,12 @@ int part_starts(ec_session *s, bool have_supers, StartRec *d_starts, uint64_t *n
     EC_CHECK(s->svals.ensure(Nn * 4));
     unsigned int *bc = s->rbc.as<unsigned int>(), *bs = bc + nblk;
     k_starts_count<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
-                                       s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                       s->dft.as<unsigned long long>(), path_of(s->PK.as<unsigned int>(), s->RK.as<unsigned int>()),
                                        s->PM.as<unsigned long long>(), n1, bc, s->cand.as<unsigned long long>(), nullptr,
                                        n0);
     EC_CHECK(scan_incl_u32(s, bc, bs, nblk));
     k_starts_write<<<nblk, B, 0, st>>>(s->upal.as<uint8_t>(), s->dfc.as<unsigned long long>(),
-                                       s->dft.as<unsigned long long>(), s->PK.as<unsigned int>(),
+                                       s->dft.as<unsigned long long>(), path_of(s->PK.as<unsigned int>(), s->RK.as<unsigned int>()),
                                        s->PM.as<unsigned long long>(), n1, bs, s->cand.as<unsigned long long>(),
                                        s->skeys.as<unsigned long long>(), s->svals.as<unsigned int>(), n0);
     unsigned int cnt = 0;
@@ -3350,7 +3349,7 @@ int part_starts(ec_session *s, bool have_supers, StartRec *d_starts, uint64_t *n
     if (cnt)
         k_start_recs<<<grid_for(cnt, B), B, 0, st>>>(s->svals.as<unsigned int>(), cnt, s->upal.as<uint8_t>(),
                                                      s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),
-                                                     s->PK.as<unsigned int>(), s->RK.as<unsigned int>(),
+                                                     path_of(s->PK.as<unsigned int>(), s->RK.as<unsigned int>()),
                                                      s->PL.as<unsigned int>(), s->k, d_starts);
     EC_CHECK(host_sync(s, st));
     *n_starts = cnt;
@@ -3410,8 +3409,8 @@ int part_emit(ec_session *s, char *d_chars, void *d_ends, bool check = true) {
                                               s->ewalk.as<EWalk>());
     if (n1 > n0 && nc)
         k_emit<Ops><<<grid_for(n1 - n0, B), B, 0, st>>>(
-            s->upal.as<uint8_t>(), s->PK.as<unsigned int>(), s->RK.as<unsigned int>(), s->PL.as<unsigned int>(),
-            s->dkey.as<typename Ops::K>(), s->cidxOf.as<unsigned int>(), s->ewalk.as<EWalk>(),
+            s->upal.as<uint8_t>(), path_of(s->PK.as<unsigned int>(), s->RK.as<unsigned int>()),
+            s->PL.as<unsigned int>(), s->dkey.as<typename Ops::K>(), s->cidxOf.as<unsigned int>(), s->ewalk.as<EWalk>(),
             n1, s->k, d_chars, std::max<uint64_t>(s->seg_nchars, 1),
             s->cfirst.as<unsigned int>(), s->clast.as<unsigned int>(), s->headOf.as<unsigned int>(),
             s->tailOf.as<unsigned int>(), &dsc->skew, n0);

@@ -602,14 +602,43 @@ __global__ void __launch_bounds__(256) k_cycle_len(const unsigned int *nextR, co
     }
 }
 
-__device__ inline unsigned long long path_min(const unsigned int *PK, const unsigned long long *PM, unsigned int x) {
-    return PM[PK[x] & ~CYC];
+// A node's path key and rank: per node (PK / RK), or -- the one-GPU tile ranking, round 6 --
+// from its chain: LH[x] = the chain's super index (bit 31 set: an in-tile cycle or no node, whose
+// PK / RK k_tile_chains wrote per node), LR[x] = the node's offset in the chain, PKs / RKs per
+// chain.  No pass writes PK / RK for every node then (k_expand: 0.3 GB a step at the headline).
+struct PathOf {
+    const unsigned int *PK, *RK;
+    const unsigned int *LH, *LR, *PKs, *RKs;
+    __device__ inline unsigned int pk(unsigned int x) const {
+        if (LH) {
+            const unsigned int h = LH[x];
+            if (!(h & 0x80000000u)) return PKs[h];
+        }
+        return PK[x];
+    }
+    __device__ inline void get(unsigned int x, unsigned int &pk, unsigned int &rk) const {
+        if (LH) {
+            const unsigned int h = LH[x];
+            if (!(h & 0x80000000u)) {
+                pk = PKs[h];
+                rk = RKs[h] + LR[x];
+                return;
+            }
+        }
+        pk = PK[x];
+        rk = RK[x];
+    }
+};
+inline PathOf path_of(const unsigned int *PK, const unsigned int *RK) { return PathOf{PK, RK, nullptr, nullptr, nullptr, nullptr}; }
+
+__device__ inline unsigned long long path_min(const PathOf &P, const unsigned long long *PM, unsigned int x) {
+    return PM[P.pk(x) & ~CYC];
 }
 
 // start of each component (all_contigs:82-84): the oriented k-mer with the smallest first
 // event over the path and its twin path (= the first dict entry not yet `done`).
 __device__ inline bool is_start(const uint8_t *upal, const unsigned long long *dfc, const unsigned long long *dft,
-                                const unsigned int *PK, const unsigned long long *PM, unsigned int x,
+                                const PathOf &PK, const unsigned long long *PM, unsigned int x,
                                 unsigned long long &f, const uint8_t *excl = nullptr) {
     if ((x & 1) && upal[x >> 1]) return false;
     if (excl && excl[x >> 1]) return false;  // (extended.h: a component with one-way links)
@@ -626,7 +655,7 @@ __device__ inline bool is_start(const uint8_t *upal, const unsigned long long *d
 // ballot ranks inside the chunk (deterministic order; an append counter serialises at
 // ~88 atomics / us -- 4.6 ms for the 1.1 M contigs of reads with 0.5 % errors).
 __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const unsigned long long *dfc,
-                                                      const unsigned long long *dft, const unsigned int *PK,
+                                                      const unsigned long long *dft, const PathOf PK,
                                                       const unsigned long long *PM, unsigned int N, unsigned int *bc,
                                                       unsigned long long *smask, const uint8_t *excl = nullptr,
                                                       unsigned int n0 = 0) {
@@ -653,7 +682,7 @@ __global__ void __launch_bounds__(256) k_starts_count(const uint8_t *upal, const
 
 // bs = inclusive scan of the chunk counts
 __global__ void __launch_bounds__(256) k_starts_write(const uint8_t *upal, const unsigned long long *dfc,
-                                                      const unsigned long long *dft, const unsigned int *PK,
+                                                      const unsigned long long *dft, const PathOf PK,
                                                       const unsigned long long *PM, unsigned int N,
                                                       const unsigned int *bs, const unsigned long long *smask,
                                                       unsigned long long *skeys, unsigned int *svals,
@@ -694,12 +723,12 @@ struct Walk {
     unsigned int kind, n, j, m, lo, len;
 };
 
-__device__ inline Walk walk_of(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
-                               const unsigned int *PL, unsigned int s) {
+__device__ inline Walk walk_of(const uint8_t *upal, const PathOf &P, const unsigned int *PL, unsigned int s) {
     Walk w;
-    const unsigned int pk = PK[s], rk = RK[s];
+    unsigned int pk, rk, pk2, rk2;
+    P.get(s, pk, rk);
     const unsigned int ts = twin_node(upal, s);
-    const unsigned int pk2 = PK[ts], rk2 = RK[ts];
+    P.get(ts, pk2, rk2);
     const bool self = pk2 == pk;
     const unsigned int plen = PL[pk & ~CYC];
     w.j = rk;
@@ -740,7 +769,7 @@ __device__ inline Walk walk_of(const uint8_t *upal, const unsigned int *PK, cons
     return w;
 }
 
-__global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+__global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const PathOf P,
                                                     const unsigned int *PL, const unsigned int *sorted_nodes,
                                                     unsigned int nc, int k, unsigned int *cidxOf,
                                                     unsigned long long *clen, Walk *cwalk,
@@ -753,8 +782,8 @@ __global__ void __launch_bounds__(256) k_contig_len(const uint8_t *upal, const u
             xcid[j] = (unsigned int)i;
             continue;
         }
-        cidxOf[PK[s] & ~CYC] = (unsigned int)i;
-        const Walk w = walk_of(upal, PK, RK, PL, s);
+        cidxOf[P.pk(s) & ~CYC] = (unsigned int)i;
+        const Walk w = walk_of(upal, P, PL, s);
         clen[i] = (unsigned long long)(k - 1) + w.len;
         cwalk[i] = w;  // k_emit reads the contig's geometry once instead of re-deriving it per node
     }
@@ -786,7 +815,7 @@ constexpr unsigned int SMALL_STARTS = 4096;
 constexpr unsigned int SMALL_STARTS_NT = 1024;
 __global__ void __launch_bounds__(SMALL_STARTS_NT) k_starts_small(
     const unsigned long long *skeys, const unsigned int *svals, unsigned int nc, const uint8_t *upal,
-    const unsigned int *PK, const unsigned int *RK, const unsigned int *PL, int k, unsigned int *sorted,
+    const PathOf PO, const unsigned int *PL, int k, unsigned int *sorted,
     unsigned int *cidxOf, unsigned long long *coff, Walk *cwalk, EWalk *ew) {
     __shared__ unsigned long long s_k[SMALL_STARTS];
     __shared__ unsigned int s_v[SMALL_STARTS];
@@ -825,8 +854,8 @@ __global__ void __launch_bounds__(SMALL_STARTS_NT) k_starts_small(
         if (i < nc) {
             const unsigned int s = s_v[i];
             sorted[i] = s;
-            cidxOf[PK[s] & ~CYC] = i;
-            w[u] = walk_of(upal, PK, RK, PL, s);
+            cidxOf[PO.pk(s) & ~CYC] = i;
+            w[u] = walk_of(upal, PO, PL, s);
             len[u] = (unsigned long long)(k - 1) + w[u].len;
         }
         run += len[u];
@@ -859,7 +888,7 @@ __global__ void __launch_bounds__(SMALL_STARTS_NT) k_starts_small(
 // emit: every node finds its contig through its path key, computes its walk position and
 // writes its chars (contig_to_string:44-45: first node k chars, later nodes their last base).
 template <typename Ops>
-__global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigned int *PK, const unsigned int *RK,
+__global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const PathOf P,
                                               const unsigned int *PL, const typename Ops::K *dkey,
                                               const unsigned int *cidxOf, const EWalk *ew,
                                               unsigned int N, int k, char *chars,
@@ -869,7 +898,8 @@ __global__ void __launch_bounds__(256) k_emit(const uint8_t *upal, const unsigne
     for (uint64_t t = n0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < N; t += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = (unsigned int)t;
         if ((x & 1) && upal[x >> 1]) continue;
-        const unsigned int pk = PK[x], rk = RK[x];
+        unsigned int pk, rk;
+        P.get(x, pk, rk);
         const unsigned int ci = cidxOf[pk & ~CYC];
         if (ci == NONE32) continue;  // the twin path of a disjoint pair carries the contig
         const EWalk e = ew[ci];

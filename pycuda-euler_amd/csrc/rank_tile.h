@@ -600,15 +600,15 @@ static_assert(sizeof(StartRec) == 48, "start record layout");
 
 __global__ void __launch_bounds__(256) k_start_recs(const unsigned int *nodes, unsigned int n, const uint8_t *upal,
                                                     const unsigned long long *dfc, const unsigned long long *dft,
-                                                    const unsigned int *PK, const unsigned int *RK,
-                                                    const unsigned int *PL, int k, StartRec *out) {
+                                                    const PathOf P, const unsigned int *PL, int k,
+                                                    StartRec *out) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned int x = nodes[i];
         StartRec r;
         r.ev = first_event(dfc, dft, x);
         r.node = x;
-        r.pk = PK[x] & ~CYC;
-        r.w = walk_of(upal, PK, RK, PL, x);
+        r.pk = P.pk(x) & ~CYC;
+        r.w = walk_of(upal, P, PL, x);
         r.clen = (unsigned int)(k - 1) + r.w.len;
         r.pad = 0;
         out[i] = r;
