@@ -2097,14 +2097,19 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         SRC, BEG, END, limit, s->dkey.as<K128>(), s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(),    \
         s->dft.as<unsigned long long>(), s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid,            \
         &dsc->ndistinct, &dsc->overflow, bm)
-#define EC_BUCKET_WR(SL)                                                                                         \
-    k_bucket_wr<SL><<<(unsigned)Bt, WR_NT, 0, st>>>(                                                                \
+#define EC_BUCKET_WR(SL, ...)                                                                                    \
+    k_bucket_wr<SL, ##__VA_ARGS__><<<(unsigned)Bt, wr_nt, 0, st>>>(                                                 \
         rdirect, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1, limit, s->dkey.as<K128>(),      \
         s->dcnt.as<unsigned int>(), s->dfc.as<unsigned long long>(), s->dft.as<unsigned long long>(),                \
         s->no_index ? nullptr : s->sub.as<SubSlotW>(), &dsc->nsolid, &dsc->ndistinct, &dsc->overflow, bm,            \
         RunReads{d_reads, d_off, k, mbM, read_base}, wcodes, s->wcodes_tab.as<unsigned long long>())
-    if (rdirect)
+    // (round 6: two 79-KB workgroups a CU unless EULERHIP_WR_ONE=1 keeps round 5's one 104-KB one)
+    const bool wr_one = kn().wr_one != 0;
+    const unsigned int wr_nt = wr_one ? WR_NT : 512u;
+    if (rdirect && wr_one)
         EC_BUCKET_WR(1664);
+    else if (rdirect)
+        EC_BUCKET_WR(1664, 512, 1024, LSlotW40);
     else if (sbits && runs)
         EC_BUCKET_W(1664, RecWM, rwin, s->bb2.as<unsigned long long>(), s->bb2.as<unsigned long long>() + 1);
     else if (runs)

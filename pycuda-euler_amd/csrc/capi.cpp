@@ -51,6 +51,7 @@ void refresh_knobs() {
         k.junction_bt = num("EULERHIP_JUNCTION_BT", -1);
         k.sk2_elim = num("EULERHIP_SK2_ELIM", 0);
         k.no_char_pack = num("EULERHIP_NO_CHAR_PACK", 0);
+        k.wr_one = num("EULERHIP_WR_ONE", 0);
         k.junction_sb = num("EULERHIP_JUNCTION_SB", 0);
         k.junction_claim = num("EULERHIP_JUNCTION_CLAIM", 0);
         if (const char *e = getenv("EULERHIP_WIDE_L3_CAP")) k.wide_l3_cap = atoll(e);

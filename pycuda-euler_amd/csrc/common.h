@@ -47,7 +47,8 @@ struct Knobs {
     int junction_bt = -1;       // EULERHIP_JUNCTION_BT: most join bucket bits of the junction join (<= 14)
     int junction_sb = 0;        // EULERHIP_JUNCTION_SB: at least this many sub-bucket bits
     int junction_claim = 0;     // EULERHIP_JUNCTION_CLAIM: slots a join table may claim (forces overflows)
-    int no_char_pack = 0;       // EULERHIP_NO_CHAR_PACK: contig characters to host as ASCII
+    int no_char_pack = 0;
+    int wr_one = 0;             // EULERHIP_WR_ONE: k_bucket_wr as one 1024-thread workgroup per CU (round 5)       // EULERHIP_NO_CHAR_PACK: contig characters to host as ASCII
     int sk2_elim = 0;           // EULERHIP_SK2_ELIM: entries a k_skpart_w wave may buffer (>= 128)
     int join_cap = 0;           // EULERHIP_JOIN_CAP: its level regions' capacity (forces the fallback)
     int host_chunks = 0;        // EULERHIP_HOST_CHUNKS: host-input chunks (0 = ~32 MiB each)

@@ -751,8 +751,17 @@ __host__ __device__ inline unsigned int wide_slot0(uint64_t h, unsigned int slot
     return (unsigned int)(((uint64_t)(uint32_t)h * slots) >> 32);
 }
 
-template <int SLOTS>
-__device__ inline void lds_insert_w(LSlotW *tab, unsigned int *s_over, const K128 &c, unsigned int slot0,
+// k_bucket_wr's slot (round 6): LSlotW without its padding, 40 B -- 1664 slots in 65 KB, so with
+// 512 threads and a 1024-dword code stage two workgroups share a CU's 160 KB (one at 104 KB)
+struct LSlotW40 {
+    unsigned long long w1, w2;
+    unsigned int count, pad;
+    unsigned long long fC, fT;
+};
+static_assert(sizeof(LSlotW40) == 40, "compact wide LDS slot layout");
+
+template <int SLOTS, typename Slot = LSlotW>
+__device__ inline void lds_insert_w(Slot *tab, unsigned int *s_over, const K128 &c, unsigned int slot0,
                                     unsigned int add, unsigned long long eC, unsigned long long eT) {
     const unsigned long long w1 = wide_w1(c), w2 = wide_w2(c);
     unsigned int slot = slot0;
@@ -787,9 +796,11 @@ __device__ inline void lds_insert_w(LSlotW *tab, unsigned int *s_over, const K12
             miss = !(a == w1 && bw == w2);
         }
     }
-    LSlotW &sl = tab[slot];
+    Slot &sl = tab[slot];
     atomicAdd(&sl.count, add);
-    const ulonglong2 ev = *reinterpret_cast<const ulonglong2 *>(&sl.fC);
+    ulonglong2 ev;
+    if constexpr (sizeof(Slot) % 16 == 0) ev = *reinterpret_cast<const ulonglong2 *>(&sl.fC);  // (16-B aligned)
+    else ev = make_ulonglong2(sl.fC, sl.fT);
     if (eC < ev.x) atomicMin(&sl.fC, eC);
     if (eT < ev.y) atomicMin(&sl.fT, eT);
 }
@@ -899,20 +910,22 @@ __global__ void __launch_bounds__(512) k_run_codes(const RunWM *runs, const unsi
     if (tid == 0 && b + 1 == gridDim.x) ctab[(uint64_t)gridDim.x * F] = s_off;
 }
 
-template <int SLOTS, int NT>
-__device__ inline void bucket_w_finish(const LSlotW *tab, unsigned int b, long long limit, K128 *dkey, unsigned int *dcnt,
+template <int SLOTS, int NT, typename Slot = LSlotW>
+__device__ inline void bucket_w_finish(const Slot *tab, unsigned int b, long long limit, K128 *dkey, unsigned int *dcnt,
                                        unsigned long long *dfc, unsigned long long *dft, SubSlotW *sub,
                                        unsigned int *nsolid, unsigned long long *ndistinct, unsigned int *bmark,
                                        unsigned int *s_wave, unsigned int *s_pres, unsigned int &s_base);
 
-template <int SLOTS>
+// (WR_NT / WR_CODES / LSlotW: one 104-KB workgroup per CU, round 5; NT = 512, CODES = 1024,
+// LSlotW40: two 79-KB workgroups per CU, round 6)
+template <int SLOTS, int WR_NT = ::ec::WR_NT, int WR_CODES = ::ec::WR_CODES, typename Slot = LSlotW>
 __global__ void __launch_bounds__(WR_NT) k_bucket_wr(const RunWM *runs, const unsigned long long *bstart,
                                                     const unsigned long long *bend, long long limit, K128 *dkey,
                                                     unsigned int *dcnt, unsigned long long *dfc, unsigned long long *dft,
                                                     SubSlotW *sub, unsigned int *nsolid, unsigned long long *ndistinct,
                                                     unsigned int *overflow, unsigned int *bmark, RunReads rr,
                                                     const uint32_t *gcodes, const unsigned long long *ctab) {
-    __shared__ LSlotW tab[SLOTS];
+    __shared__ Slot tab[SLOTS];
     __shared__ unsigned int s_over[2];
     __shared__ unsigned int s_wave[WR_NT / 64], s_pres[WR_NT / 64], s_wave2[WR_NT / 64];
     __shared__ unsigned int s_base, s_nb;
@@ -992,7 +1005,8 @@ __global__ void __launch_bounds__(WR_NT) k_bucket_wr(const RunWM *runs, const un
             const K128 c = f ? fwd : rc;
             const uint32_t lC = f || pal ? w : m2 - w, lT = f && !pal ? m2 - w : w;
             const unsigned long long rd = (unsigned long long)(rr.read_base + mt.x) << 32;
-            lds_insert_w<SLOTS>(tab, s_over, c, wide_slot0(mix128(c), SLOTS), lC == lT ? 2u : 1u, rd | lC, rd | lT);
+            lds_insert_w<SLOTS, Slot>(tab, s_over, c, wide_slot0(mix128(c), SLOTS), lC == lT ? 2u : 1u, rd | lC,
+                                      rd | lT);
         }
         rb += nb;
         if (nb == 0) {  // (one run past WR_CODES: never for k <= 52 and reads <= 160 bp -- reported)
@@ -1006,8 +1020,8 @@ __global__ void __launch_bounds__(WR_NT) k_bucket_wr(const RunWM *runs, const un
         if (tid == 0) atomicAdd(overflow, 1u);
         return;
     }
-    bucket_w_finish<SLOTS, WR_NT>(tab, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, bmark, s_wave, s_pres,
-                                  s_base);
+    bucket_w_finish<SLOTS, WR_NT, Slot>(tab, b, limit, dkey, dcnt, dfc, dft, sub, nsolid, ndistinct, bmark, s_wave,
+                                        s_pres, s_base);
 }
 
 // ---- third partition level (more keys than 2^FINE_W_BITS tables hold) ---------------------
@@ -1036,8 +1050,8 @@ __global__ void __launch_bounds__(256) k_level3_ends(const unsigned long long *g
 
 // solid filter + compaction of a filled table (as lds_table_finish): the solid keys to the
 // dense arrays at a block-reserved base, the slots to the bucket's sub-table region
-template <int SLOTS, int NT>
-__device__ inline void bucket_w_finish(const LSlotW *tab, unsigned int b, long long limit, K128 *dkey, unsigned int *dcnt,
+template <int SLOTS, int NT, typename Slot>
+__device__ inline void bucket_w_finish(const Slot *tab, unsigned int b, long long limit, K128 *dkey, unsigned int *dcnt,
                                        unsigned long long *dfc, unsigned long long *dft, SubSlotW *sub,
                                        unsigned int *nsolid, unsigned long long *ndistinct, unsigned int *bmark,
                                        unsigned int *s_wave, unsigned int *s_pres, unsigned int &s_base) {
@@ -1051,7 +1065,7 @@ __device__ inline void bucket_w_finish(const LSlotW *tab, unsigned int b, long l
             solid[q] = false;
             continue;
         }
-        const LSlotW &sl = tab[idx];
+        const Slot &sl = tab[idx];
         present += sl.w1 != 0;
         solid[q] = sl.w1 != 0 && (long long)sl.count > limit;
         mine += solid[q];
@@ -1084,7 +1098,7 @@ __device__ inline void bucket_w_finish(const LSlotW *tab, unsigned int b, long l
     for (int q = 0; q < PER; q++) {
         const int idx = threadIdx.x * PER + q;
         if (idx >= SLOTS) break;
-        const LSlotW &sl = tab[idx];
+        const Slot &sl = tab[idx];
         SubSlotW o;
         o.w1 = sl.w1;
         o.w2 = sl.w2;
