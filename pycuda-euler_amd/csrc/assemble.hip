@@ -1790,15 +1790,18 @@ int phase_load_det_w(ec_session *s, const AggW *d_agg, uint64_t n, unsigned int 
 }
 
 // ---- 32 < k <= 63: 128-bit keys (wide.h), general-table counting ---------------------------
-int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, SolidIndexW &sidx) {
+int finish_wide(ec_session *s, uint64_t cap, long long limit, unsigned int &U, SolidIndexW &sidx,
+                uint64_t ubound = 0) {
     hipStream_t st = s->stream;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc;
     mark(s, 2 * EC_STAGE_COMPACT);
-    EC_CHECK(s->dkey.ensure(cap * sizeof(K128)));
-    EC_CHECK(s->dcnt.ensure(cap * 4));
-    EC_CHECK(s->dfc.ensure(cap * 8));
-    EC_CHECK(s->dft.ensure(cap * 8));
+    // (ubound: at most that many keys -- a merge's records; the table's capacity otherwise)
+    const uint64_t ucap = ubound ? std::min<uint64_t>(cap, ubound) : cap;
+    EC_CHECK(s->dkey.ensure(std::max<uint64_t>(ucap, 1) * sizeof(K128)));
+    EC_CHECK(s->dcnt.ensure(std::max<uint64_t>(ucap, 1) * 4));
+    EC_CHECK(s->dfc.ensure(std::max<uint64_t>(ucap, 1) * 8));
+    EC_CHECK(s->dft.ensure(std::max<uint64_t>(ucap, 1) * 8));
     EC_HIP(hipMemsetAsync(&dsc->nsolid, 0, 4, st));
     EC_HIP(hipMemsetAsync(&dsc->ndistinct, 0, 8, st));
     EC_CHECK(compact_table(s, s->table.as<SlotW>(), cap, limit, s->dkey.as<K128>()));
@@ -2280,8 +2283,23 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     Scalars hsc;
+    // the table for the distinct keys (HyperLogLog of the records' keys, +-2.3 %), not for the
+    // records: a rank's merge sees each key once per source (a table past 0.45 load retries x4)
+    double keys = (double)n;
+    if (n >= (1u << 20)) {
+        constexpr int HB = HLL_REG_BITS;
+        EC_CHECK(s->ftot.ensure((1 << HB) * 4));
+        unsigned int *hreg = s->ftot.as<unsigned int>();
+        EC_HIP(hipMemsetAsync(hreg, 0, (1 << HB) * 4, st));
+        k_hll_aggw<<<256, B, 0, st>>>(d_agg, n, HB, hreg);
+        k_hll_final<<<1, 1024, 0, st>>>(hreg, HB, &dsc->est);
+        double est = 0;
+        EC_CHECK(d2h(s, &est, &dsc->est, sizeof(double), st));
+        EC_CHECK(host_sync(s, st));
+        keys = std::min((double)n, est * 1.1 + 1024.0);
+    }
     uint64_t cap = 1024;
-    while (cap < (uint64_t)(2.2 * (double)n) + 1024) cap <<= 1;
+    while (cap < (uint64_t)(2.2 * keys) + 1024) cap <<= 1;
     for (int attempt = 0;; attempt++) {
         EC_CHECK(s->table.ensure(cap * sizeof(SlotW)));
         mark(s, 2 * EC_STAGE_COUNT);
@@ -2299,7 +2317,7 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
         cap <<= 2;
         s->stats.table_retries++;
     }
-    EC_CHECK(finish_wide(s, cap, limit, U, sidx));
+    EC_CHECK(finish_wide(s, cap, limit, U, sidx, std::max<uint64_t>(n, 1)));
     // an owner merge (no lookup index wanted) on minimizer owners: ids in minimizer order
     if (s->no_index && s->owner_rule == 0 && merge_wmb(s->k) && !(s->flags & EC_FLAG_GENERAL)) {
         EC_CHECK(order_by_minimizer_w(s, U));
