@@ -180,6 +180,7 @@ class HipEngine:
         total = self.torch.cuda.mem_get_info(self.device)[1]
         if self.sess.device_bytes() > frac * total:
             self.sess.trim(64 << 20)
+            self.torch.cuda.empty_cache()  # (and torch's cached blocks: the next allocations are the session's)
             return True
         return False
 
@@ -580,6 +581,8 @@ def sharded_assemble(engine, comm, d_reads, d_off, nreads, read_base, k, limit=1
     def tick(name):
         marks.append((name, time.perf_counter()))
 
+    if hasattr(engine, "trim_if_large"):  # (a large previous step's graph buffers: the count needs the memory)
+        engine.trim_if_large()
     st = engine.count_shard(d_reads, d_off, nreads, read_base, k, flags)
     tick("count")
     if on_count:
@@ -797,6 +800,8 @@ def local_sharded_assemble_shards(engines, parts, k, limit=1, flags=0, partition
     P = 0
     sends = []
     for eng, (d_reads, d_off, n, lo) in zip(engines, shards):
+        if hasattr(eng, "trim_if_large"):
+            eng.trim_if_large()
         st = eng.count_shard(d_reads, d_off, n, lo, k, flags)
         eng.count_variant = int(st.count_variant)
         P += st.n_positions

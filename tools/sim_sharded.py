@@ -69,6 +69,7 @@ def main():
 
         sends = []
         for eng, (d_reads, d_off, n, lo) in zip(engines, shards):
+            eng.trim_if_large()  # (as sharded_assemble: a large previous step's buffers released first)
             t0 = t_start()
             eng.count_shard(d_reads, d_off, n, lo, a.k, 0)
             tick("count", t0)
