@@ -477,6 +477,14 @@ int ec_graph_collect(ec_session *s, const char *d_chars, const void *d_ends, uin
  * in rank order, src_bytes[r] each) to the collecting rank, whose ec_graph_collect_runs scatters
  * them into the job's characters and ends and finishes as ec_graph_collect. */
 int ec_graph_emit_runs(ec_session *s, uint64_t *nbytes);
+/* Exact-size outputs (round 6): ec_graph_place, ec_graph_chains_part and ec_graph_starts_part
+ * called with a NULL output (d_jrecs / d_super / d_starts) count their records only (the counts
+ * returned as above) and hold them; the matching copy, before any other step of the session,
+ * writes them into a buffer of exactly that many records -- instead of the upper bounds (4 Ur
+ * junction records, 2 (hi - lo) super / start records: ~50 GB at config 5's per-rank size). */
+int ec_graph_place_copy(ec_session *s, void *d_jrecs);
+int ec_graph_chains_copy(ec_session *s, void *d_super);
+int ec_graph_starts_copy(ec_session *s, void *d_starts);
 int ec_graph_copy_runs(ec_session *s, void *d_out);
 int ec_graph_collect_runs(ec_session *s, const void *d_in, int nsrc, const uint64_t *src_bytes, uint64_t n_pal);
 int ec_end_record_bytes(int k);

@@ -66,6 +66,7 @@ void refresh_knobs() {
         k.skf_keys = num("EULERHIP_SKF_KEYS", 0);
         k.wide_mb = num("EULERHIP_WIDE_MB", -1);
         k.join_mb = num("EULERHIP_JOIN_MB", -1);
+        k.join_local = num("EULERHIP_JOIN_LOCAL", -1);
         k.sruler_mask = num("EULERHIP_SRULER_MASK", 0);
     }
     g_knobs = k;

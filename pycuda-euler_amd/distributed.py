@@ -105,6 +105,10 @@ eulerhip.register("ec_graph_emit_runs", ctypes.c_int, [_P, ctypes.POINTER(_U64)]
 eulerhip.register("ec_graph_copy_runs", ctypes.c_int, [_P, _P])
 eulerhip.register("ec_graph_collect_runs", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(_U64), _U64])
 eulerhip.register("ec_end_record_bytes", ctypes.c_int, [ctypes.c_int])
+# exact-size outputs: the steps called with a NULL output count, the copies write (round 6)
+eulerhip.register("ec_graph_place_copy", ctypes.c_int, [_P, _P])
+eulerhip.register("ec_graph_chains_copy", ctypes.c_int, [_P, _P])
+eulerhip.register("ec_graph_starts_copy", ctypes.c_int, [_P, _P])
 # junction-partitioned graph (round 5, csrc/junction.h): no rank holds the job's solid set
 eulerhip.register("ec_graph_place", ctypes.c_int, [_P, _U64, _U64, ctypes.c_int, _P, ctypes.POINTER(_U64),
                                                    ctypes.POINTER(_U64)])
@@ -139,6 +143,7 @@ def shard_range(nreads, rank, world):
 
 # a shard count past this fraction of the device's memory is released after its export
 TRIM_FRACTION = 0.1
+TRIM_FREE_FRACTION = 0.15
 
 
 # ---- engines -------------------------------------------------------------------------------
@@ -163,22 +168,39 @@ class HipEngine:
     def empty(self, nbytes):
         return self.torch.empty(max(int(nbytes), 1), dtype=self.torch.uint8, device=self.device)
 
+    def _retry_nomem(self, call):
+        """a call that ran out of device memory runs once more after the session's and torch's
+        cached buffers are released (the count and the merge start from scratch: re-runnable)"""
+        try:
+            eulerhip.check(call())
+        except eulerhip.EulerHipError as e:
+            if e.code != eulerhip.EC_ERR_NOMEM:
+                raise
+            self.sess.trim(0)
+            self.torch.cuda.empty_cache()
+            eulerhip.check(call())
+
     def count_shard(self, d_reads, d_off, nreads, read_base, k, flags=0):
         self.k = int(k)
-        eulerhip.check(self.L.ec_count_shard(self._h(), ctypes.c_void_p(d_reads.data_ptr()),
-                                             ctypes.c_void_p(d_off.data_ptr()), int(nreads), int(read_base), int(k),
-                                             flags))
+        self._retry_nomem(lambda: self.L.ec_count_shard(self._h(), ctypes.c_void_p(d_reads.data_ptr()),
+                                                        ctypes.c_void_p(d_off.data_ptr()), int(nreads),
+                                                        int(read_base), int(k), flags))
         return self.sess.stats()
 
     def rec_bytes(self):
         return int(self.L.ec_record_bytes(self.k))
 
-    def trim_if_large(self, frac=TRIM_FRACTION):
-        """after the export: a shard count holding more than frac of the device's memory releases
-        its buffers (ec_session_trim), so the owner merge and the graph phase get them -- config 5's
-        per-rank count holds ~10^11 B; the headline's ~10^10 B stays (re-allocating it costs ~ms)"""
-        total = self.torch.cuda.mem_get_info(self.device)[1]
-        if self.sess.device_bytes() > frac * total:
+    def trim_if_large(self, frac=TRIM_FRACTION, free_frac=TRIM_FREE_FRACTION):
+        """before the count and after the export: a session holding more than frac of the device's
+        memory releases its buffers (ec_session_trim) when less than free_frac of the device is
+        free (torch's cached blocks counted free), so the next phase gets them.  A session that
+        fits is kept: its buffers are the next phase's / step's at their sizes already, and large
+        buffers freed and allocated again are slow -- config 5's per-rank step freeing ~165 GB
+        before its count measured 5.6 s of count against 67 ms without (r06_f)"""
+        torch = self.torch
+        free, total = torch.cuda.mem_get_info(self.device)
+        free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
+        if self.sess.device_bytes() > frac * total and free < free_frac * total:
             self.sess.trim(64 << 20)
             self.torch.cuda.empty_cache()  # (and torch's cached blocks: the next allocations are the session's)
             return True
@@ -213,11 +235,10 @@ class HipEngine:
         """ec_merge_owned_from on the records of every source (rank order); export as merge_owned"""
         self.k = int(k)
         ns = len(src_bytes)
-        eulerhip.check(self.L.ec_merge_owned_from(self._h(), ctypes.c_void_p(recs.data_ptr()), ns,
-                                                  (ctypes.c_uint64 * ns)(*[int(x) for x in src_bytes]),
-                                                  (ctypes.c_int64 * ns)(*[int(x) for x in src_base]),
-                                                  (ctypes.c_int32 * ns)(*[int(x) for x in src_lfb]), int(k), int(limit),
-                                                  flags))
+        self._retry_nomem(lambda: self.L.ec_merge_owned_from(
+            self._h(), ctypes.c_void_p(recs.data_ptr()), ns, (ctypes.c_uint64 * ns)(*[int(x) for x in src_bytes]),
+            (ctypes.c_int64 * ns)(*[int(x) for x in src_base]), (ctypes.c_int32 * ns)(*[int(x) for x in src_lfb]),
+            int(k), int(limit), flags))
         m = int(self.L.ec_dense_count(self._h()))
         if not export:
             return m
@@ -279,14 +300,15 @@ class HipEngine:
     def graph_place(self, lo, U, nowners):
         """this rank's merged segment at global ids [lo, lo + Ur); returns (junction records
         grouped by owner, records per owner, palindromic keys of the segment)"""
-        ur = int(self.L.ec_dense_count(self._h()))
         jb = junction_bytes(self.k)
-        out = self.empty(4 * ur * jb)
         counts = (_U64 * nowners)()
         npal = _U64(0)
-        eulerhip.check(self.L.ec_graph_place(self._h(), int(lo), int(U), int(nowners), ctypes.c_void_p(out.data_ptr()),
-                                             counts, ctypes.byref(npal)))
+        # counted first, then copied into a buffer of exactly that size (not the 4 Ur bound)
+        eulerhip.check(self.L.ec_graph_place(self._h(), int(lo), int(U), int(nowners), None, counts,
+                                             ctypes.byref(npal)))
         tot = sum(int(c) for c in counts)
+        out = self.empty(tot * jb)
+        eulerhip.check(self.L.ec_graph_place_copy(self._h(), ctypes.c_void_p(out.data_ptr())))
         return out[: tot * jb], [int(c) for c in counts], int(npal.value)
 
     def graph_join(self, recs, seg_lo):
@@ -309,21 +331,21 @@ class HipEngine:
     def graph_chains_part(self, lo, hi, succ_part=None):
         """this rank's chains as super records (uint8 tensor of n * SUPER_BYTES) and n
         (succ_part None: a placed segment, whose links the session holds)"""
-        out = self.empty(2 * (hi - lo) * SUPER_BYTES)
         n = ctypes.c_uint64(0)
         sp = ctypes.c_void_p(succ_part.data_ptr()) if succ_part is not None else None
-        eulerhip.check(self.L.ec_graph_chains_part(self._h(), int(lo), int(hi), sp,
-                                                   ctypes.c_void_p(out.data_ptr()), ctypes.byref(n)))
+        eulerhip.check(self.L.ec_graph_chains_part(self._h(), int(lo), int(hi), sp, None, ctypes.byref(n)))
+        out = self.empty(n.value * SUPER_BYTES)
+        eulerhip.check(self.L.ec_graph_chains_copy(self._h(), ctypes.c_void_p(out.data_ptr())))
         return out[: n.value * SUPER_BYTES], int(n.value)
 
     def graph_rank_supers(self, supers, n):
         eulerhip.check(self.L.ec_graph_rank_supers(self._h(), ctypes.c_void_p(supers.data_ptr()), int(n)))
 
     def graph_starts_part(self, have_supers, lo, hi):
-        out = self.empty(2 * (hi - lo) * START_BYTES)
         n = ctypes.c_uint64(0)
-        eulerhip.check(self.L.ec_graph_starts_part(self._h(), 1 if have_supers else 0, ctypes.c_void_p(out.data_ptr()),
-                                                   ctypes.byref(n)))
+        eulerhip.check(self.L.ec_graph_starts_part(self._h(), 1 if have_supers else 0, None, ctypes.byref(n)))
+        out = self.empty(n.value * START_BYTES)
+        eulerhip.check(self.L.ec_graph_starts_copy(self._h(), ctypes.c_void_p(out.data_ptr())))
         return out[: n.value * START_BYTES], int(n.value)
 
     def graph_layout(self, starts, n):

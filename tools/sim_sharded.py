@@ -86,7 +86,7 @@ def main():
                 recs, counts, _ = sends[src]
                 o = sum(counts[:dst]) * rbs[src]
                 parts.append(recs[o:o + counts[dst] * rbs[src]])
-            recvs.append((torch.cat(parts), [x.numel() for x in parts]))
+            recvs.append((parts[0] if world == 1 else torch.cat(parts), [x.numel() for x in parts]))
         bases = [sh[3] for sh in shards]
         lfbs = [b for _, _, b in sends]
         import ctypes
@@ -145,7 +145,7 @@ def main():
             for dst, eng in enumerate(engines):
                 got = [rec[sum(c[:dst]) * jb:sum(c[:dst + 1]) * jb] for rec, c, _ in placed]
                 jx = max(jx, sum(g.numel() for i, g in enumerate(got) if i != dst))
-                recv = torch.cat(got)
+                recv = got[0] if len(got) == 1 else torch.cat(got)
                 t0 = t_start()
                 links.append(eng.graph_join(recv, seg_lo))
                 tick("join", t0)
