@@ -14,7 +14,7 @@ import os
 import re
 import sys
 
-KERNELS = ("k_bucket_wr", "k_run_codes", "k_downsweep_wr", "k_wbv", "k_jl_scan", "k_jl_bounds", "k_jl_scatter",
+KERNELS = ("k_bucket_wr", "k_run_codes", "k_downsweep_wr", "k_wbv", "k_jl_scan", "k_jl_edges", "k_jl_scatter",
            "k_jl_join", "k_upsweep", "k_downsweep", "k_bucket", "k_count", "k_refine", "k_prescan", "k_partition", "k_refine2",
            "k_skpart", "k_skrefine", "k_skbucket", "k_neighbors", "k_walk", "k_half_join64", "k_half_join", "k_half_emit64", "k_half_emit", "k_pred_rc",
            "k_tile_chains", "k_tile_compact", "k_walk_s", "k_rjump", "k_expand", "k_super_link", "k_finalize_s",

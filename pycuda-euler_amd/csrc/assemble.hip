@@ -277,6 +277,9 @@ struct ec_session {
     // stream (event wait + unpack) -- the super-k-mer partition runs on each chunk's read groups
     // as they arrive, any other count path waits for all of them (pipe_all)
     hipStream_t cstream = nullptr;
+    // a second copy stream: chunks alternate between the two, so two DMA queues share a batch's
+    // copy (one SDMA copy measured at half its idle rate while the count kernels ran, r06_i)
+    hipStream_t cstream2 = nullptr;
     struct Pipe {
         bool active = false;
         bool packed = false;          // 2-bit codes (k_unpack2 + k_patch) or ASCII
@@ -2492,29 +2495,31 @@ int links_local(ec_session *s, int k, unsigned int U, const Index &sidx, bool &o
     Scalars *dsc = s->scal.as<Scalars>();
     const uint64_t N = 2ull * U;
     // foreign records: ~2 / (w + 1) of the 2U (7 % at k = 31, 3 % at k = 51); room for a third
-    const unsigned int fcap = U / 3 + 4096;
+    const unsigned int fcap = (U / 3 / JL_NCTR + 64) * JL_NCTR;
     EC_CHECK(s->jl_kof.ensure((size_t)U * 4));
     EC_CHECK(s->jl_rs.ensure((size_t)ntab * 4));
     EC_CHECK(s->jl_re.ensure((size_t)ntab * 4));
     EC_CHECK(s->jl_cnt.ensure(((size_t)ntab + 1) * 4));
     EC_CHECK(s->jl_off.ensure(((size_t)ntab + 1) * 4));
-    EC_CHECK(s->jl_flag.ensure(16));
+    EC_CHECK(s->jl_flag.ensure((size_t)(JL_NCTR + 1) * JL_CSTRIDE * 4));
     EC_CHECK(s->recs.ensure((size_t)fcap * sizeof(R)));
     EC_CHECK(s->recs2.ensure((size_t)fcap * sizeof(R)));
-    unsigned int *flags = s->jl_flag.as<unsigned int>();  // [0]: foreign records, [1]: the gate
+    // [1]: the gate; [JL_CSTRIDE (r + 1)]: foreign records of region r
+    unsigned int *flags = s->jl_flag.as<unsigned int>(), *fctr = flags + JL_CSTRIDE;
     unsigned int *cnt = s->jl_cnt.as<unsigned int>(), *off = s->jl_off.as<unsigned int>();
-    EC_HIP(hipMemsetAsync(flags, 0, 8, st));
+    EC_HIP(hipMemsetAsync(flags, 0, (size_t)(JL_NCTR + 1) * JL_CSTRIDE * 4, st));
     EC_HIP(hipMemsetAsync(s->jl_rs.p, 0xFF, (size_t)ntab * 4, st));
     EC_HIP(hipMemsetAsync(cnt, 0, ((size_t)ntab + 1) * 4, st));
     const K *dkey = s->dkey.as<K>();
     uint8_t *upal = s->upal.as<uint8_t>();
     k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(dkey, U, k, upal, &dsc->npal);
     k_jl_scan<K><<<grid_for(U, B, 8192), B, 0, st>>>(dkey, U, k, bits, upal, s->jl_kof.as<unsigned int>(), s->recs.as<R>(),
-                                                     &flags[0], fcap, cnt, &flags[1]);
-    k_jl_bounds<<<grid_for(U, B, 8192), B, 0, st>>>(s->jl_kof.as<unsigned int>(), U, s->jl_rs.as<unsigned int>(),
-                                                    s->jl_re.as<unsigned int>(), &flags[1]);
+                                                     fctr, fcap, cnt, s->jl_rs.as<unsigned int>(),
+                                                     s->jl_re.as<unsigned int>(), &flags[1]);
+    k_jl_edges<<<grid_for(U / 64 + 2, B, 4096), B, 0, st>>>(s->jl_kof.as<unsigned int>(), U, s->jl_rs.as<unsigned int>(),
+                                                           s->jl_re.as<unsigned int>(), &flags[1]);
     EC_CHECK(scan_excl_u32(s, cnt, off, (size_t)ntab + 1));
-    k_jl_scatter<R><<<grid_for(fcap, B, 4096), B, 0, st>>>(s->recs.as<R>(), &flags[0], fcap, off, cnt, s->recs2.as<R>());
+    k_jl_scatter<R><<<grid_for(fcap, B, 4096), B, 0, st>>>(s->recs.as<R>(), fctr, fcap, off, cnt, s->recs2.as<R>());
     EC_HIP(hipMemsetAsync(s->succ.p, 0xFF, N * 4, st));
     // (4096 slots: 96 KB of 128-bit slots, one workgroup a CU -- 512 threads to hide the probes)
 #define EC_JL_JOIN(SL, ODD)                                                                                        \
@@ -3955,6 +3960,7 @@ int pipe_plan(ec_session *s, Pipe &pp, uint64_t nbases, uint64_t bytes_per_base4
         for (size_t i = have; i < (size_t)nc; i++) EC_HIP(hipEventCreateWithFlags(&pp.ev[i], hipEventDisableTiming));
     }
     if (!s->cstream) EC_HIP(hipStreamCreateWithFlags(&s->cstream, hipStreamNonBlocking));
+    if (!s->cstream2) EC_HIP(hipStreamCreateWithFlags(&s->cstream2, hipStreamNonBlocking));
     // the copies overwrite buffers a previous call's kernels may still read: after = the event
     // of their last reader (a staged slot), else everything queued on the session stream
     if (!after) {
@@ -3962,14 +3968,18 @@ int pipe_plan(ec_session *s, Pipe &pp, uint64_t nbases, uint64_t bytes_per_base4
         after = pp.ev[0];
     }
     EC_HIP(hipStreamWaitEvent(s->cstream, after, 0));
+    EC_HIP(hipStreamWaitEvent(s->cstream2, after, 0));
     return EC_OK;
 }
+
+// the copy stream of chunk c (EULERHIP_COPY_STREAMS=1: cstream only)
+inline hipStream_t copy_stream(ec_session *s, int c) { return (c & 1) && kn().copy_streams != 1 ? s->cstream2 : s->cstream; }
 
 // copy the offsets entries reads [r0, r1] need (chunk by chunk: [ravail[c-1] + 1, ravail[c] + 1))
 int pipe_copy_offsets(ec_session *s, const Pipe &pp, int c, const uint64_t *offsets, uint64_t *d_off) {
     const uint64_t o0 = c ? pp.ravail[c - 1] + 1 : 0, o1 = pp.ravail[c] + 1;
     if (o1 > o0)
-        EC_HIP(hipMemcpyAsync(d_off + o0, offsets + o0, (o1 - o0) * 8, hipMemcpyHostToDevice, s->cstream));
+        EC_HIP(hipMemcpyAsync(d_off + o0, offsets + o0, (o1 - o0) * 8, hipMemcpyHostToDevice, copy_stream(s, c)));
     return EC_OK;
 }
 
@@ -4054,11 +4064,12 @@ int stage_packed(ec_session *s, Pipe &pp, DevBuf &codes_b, DevBuf &exc_b, DevBuf
         // code bytes of bases [blo, bhi) (blo a multiple of 64: whole 32-bit words)
         const uint64_t c0 = pp.blo[c] / 4, c1 = c + 1 == pp.nchunks ? ncodes : pp.bhi[c] / 4;
         if (c1 > c0)
-            EC_HIP(hipMemcpyAsync(codes_b.as<uint8_t>() + c0, codes + c0, c1 - c0, hipMemcpyHostToDevice, s->cstream));
+            EC_HIP(hipMemcpyAsync(codes_b.as<uint8_t>() + c0, codes + c0, c1 - c0, hipMemcpyHostToDevice,
+                                  copy_stream(s, c)));
         if (offsets) EC_CHECK(pipe_copy_offsets(s, pp, c, offsets, off_b.as<uint64_t>()));
         pp.elo[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.blo[c]) - exc_pos);
         pp.ehi[c] = (uint64_t)(std::lower_bound(exc_pos, exc_pos + n_exc, pp.bhi[c]) - exc_pos);
-        EC_HIP(hipEventRecord(pp.ev[c], s->cstream));
+        EC_HIP(hipEventRecord(pp.ev[c], copy_stream(s, c)));
     }
     return EC_OK;
 }
@@ -4171,6 +4182,7 @@ int ec_session_trim(ec_session *s, uint64_t min_bytes) {
     if (s->stream) EC_HIP(hipStreamSynchronize(s->stream));
     if (s->ostream) EC_HIP(hipStreamSynchronize(s->ostream));
     if (s->cstream) EC_HIP(hipStreamSynchronize(s->cstream));
+    if (s->cstream2) EC_HIP(hipStreamSynchronize(s->cstream2));
     for_each_buf(s, [&](DevBuf &b) {
         if (b.cap >= min_bytes && &b != &s->scal) b.release();
     });
@@ -4202,6 +4214,7 @@ int ec_session_destroy(ec_session *s) {
     if (s->stream) hipStreamSynchronize(s->stream);
     if (s->ostream) hipStreamSynchronize(s->ostream);
     if (s->cstream) hipStreamSynchronize(s->cstream);
+    if (s->cstream2) hipStreamSynchronize(s->cstream2);
     for_each_buf(s, [](DevBuf &b) { b.release(); });
     s->h_chars.release();
     s->hmeta.release();
@@ -4236,6 +4249,10 @@ int ec_session_destroy(ec_session *s) {
     if (s->cstream) {
         hipStreamSynchronize(s->cstream);
         hipStreamDestroy(s->cstream);
+    }
+    if (s->cstream2) {
+        hipStreamSynchronize(s->cstream2);
+        hipStreamDestroy(s->cstream2);
     }
     if (s->own_stream && s->stream) hipStreamDestroy(s->stream);
     delete s;
@@ -4272,9 +4289,9 @@ int ec_assemble_host(ec_session *s, const uint8_t *reads, uint64_t nbytes, const
     for (int c = 0; c < pp.nchunks; c++) {
         if (pp.bhi[c] > pp.blo[c])
             EC_HIP(hipMemcpyAsync(s->h_reads.as<uint8_t>() + pp.blo[c], reads + pp.blo[c], pp.bhi[c] - pp.blo[c],
-                                  hipMemcpyHostToDevice, s->cstream));
+                                  hipMemcpyHostToDevice, copy_stream(s, c)));
         EC_CHECK(pipe_copy_offsets(s, pp, c, offsets, s->h_offsets.as<uint64_t>()));
-        EC_HIP(hipEventRecord(pp.ev[c], s->cstream));
+        EC_HIP(hipEventRecord(pp.ev[c], copy_stream(s, c)));
     }
     return assemble_piped(s, s->h_offsets.as<uint64_t>(), nreads, k, limit, flags);
 }
@@ -5037,13 +5054,30 @@ int graph_place(ec_session *s, uint64_t lo, uint64_t U, int nowners, void *d_out
     return EC_OK;
 }
 
+// bin starts of n bin ids sorted ascending (bstart[b] = first index with id >= b, bstart[nb] = n)
+__global__ void __launch_bounds__(256) k_sorted_starts(const unsigned int *key, uint64_t n, unsigned int nb,
+                                                      unsigned long long *bstart) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int kk = key[i];
+        const long long prev = i ? (long long)key[i - 1] : -1ll;
+        for (long long b = prev + 1; b <= (long long)kk; b++) bstart[b] = i;
+        if (i + 1 == n)
+            for (long long b = (long long)kk + 1; b <= (long long)nb; b++) bstart[b] = n;
+    }
+}
+__global__ void __launch_bounds__(256) k_iota_u32(unsigned int *v, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        v[i] = (unsigned int)i;
+}
+
 template <typename R>
 int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const uint64_t *seg_lo, LinkRec *d_links,
                uint64_t *owner_counts) {
     hipStream_t st = s->stream;
     const unsigned B = 256;
     s->hold.kind = 0;
-    EC_CHECK(s->jseg.ensure(((size_t)nowners + 2) * 8 + (size_t)(1u << 14) * 8 + 64));
+    constexpr int BT_CS = 14, BT_MAX = 22;  // counting sort's LDS histogram limit; radix sort past it
+    EC_CHECK(s->jseg.ensure(((size_t)nowners + 2) * 8 + ((size_t)(1u << BT_MAX) + 1) * 8 + 64));
     unsigned long long *dseg = s->jseg.as<unsigned long long>();
     unsigned long long *bstart = dseg + nowners + 2;
     EC_HIP(hipMemcpyAsync(dseg, seg_lo, ((size_t)nowners + 1) * 8, hipMemcpyHostToDevice, st));
@@ -5051,11 +5085,13 @@ int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const ui
     unsigned int *flag = s->jcnt.as<unsigned int>(), *nout = flag + 1;
     EC_CHECK(s->jout.ensure(std::max<uint64_t>(n, 1) * sizeof(LinkRec)));
     LinkRec *outbox = s->jout.as<LinkRec>();
-    // join buckets: ~n / 2 junction groups, <= ~900 a 2048-slot table; at most 2^14 buckets (the
-    // counting sort's LDS histogram), each split into 2^sb sub-buckets past that.  A table that
+    // join buckets: ~n / 2 junction groups, <= ~900 a 2048-slot table; up to 2^14 buckets by the
+    // counting sort (its LDS histogram's limit), up to 2^22 by a radix sort of the bucket ids --
+    // sub-buckets (each re-reading its bucket's records) only past that or when forced: config 5's
+    // per-rank step joined 4e8 records in 2^14 buckets x 16 sub-buckets in 195 ms.  A table that
     // overflows (skewed junction hashes) retries with 4096 slots, then finer buckets, then more
     // sub-buckets (EULERHIP_JUNCTION_BT / _SB / _CLAIM force the split / a smaller claim cap)
-    const int btmax = kn().junction_bt >= 0 ? std::min(kn().junction_bt, 14) : 14;
+    const int btmax = kn().junction_bt >= 0 ? std::min(kn().junction_bt, BT_MAX) : BT_MAX;
     const double groups = (double)n / 2.0;
     int bt = 0, sb = 0;
     while (bt < btmax && groups / (double)(1ull << bt) > 900.0) bt++;
@@ -5069,7 +5105,23 @@ int graph_join(ec_session *s, const R *d_recs, uint64_t n, int nowners, const ui
         EC_CHECK(s->joid.ensure(std::max<uint64_t>(n, 1) * 4));
         EC_HIP(hipMemsetAsync(flag, 0, 8, st));
         if (n) k_junction_bucket<R><<<grid_for(n, B), B, 0, st>>>(d_recs, n, bt, s->joid.as<unsigned int>());
-        EC_CHECK(bin_sort(s, s->joid.as<unsigned int>(), n, nb, bstart));
+        if ((bt <= BT_CS && kn().junction_radix != 1) || !n) {
+            EC_CHECK(bin_sort(s, s->joid.as<unsigned int>(), n, nb, bstart));
+        } else {  // record order by bucket id: rocprim radix sort of (id, index) pairs over bt bits
+            EC_CHECK(s->mbid.ensure(n * 4));
+            EC_CHECK(s->mbid2.ensure(n * 4));
+            EC_CHECK(s->midx2.ensure(n * 4));
+            k_iota_u32<<<grid_for(n, B, 8192), B, 0, st>>>(s->mbid.as<unsigned int>(), n);
+            size_t bytes = 0;
+            EC_HIP(rocprim::radix_sort_pairs(nullptr, bytes, s->joid.as<unsigned int>(), s->mbid2.as<unsigned int>(),
+                                             s->mbid.as<unsigned int>(), s->midx2.as<unsigned int>(), (size_t)n, 0, bt,
+                                             st));
+            EC_CHECK(s->tmp.ensure(bytes));
+            EC_HIP(rocprim::radix_sort_pairs(s->tmp.p, bytes, s->joid.as<unsigned int>(), s->mbid2.as<unsigned int>(),
+                                             s->mbid.as<unsigned int>(), s->midx2.as<unsigned int>(), (size_t)n, 0, bt,
+                                             st));
+            k_sorted_starts<<<grid_for(n, B, 8192), B, 0, st>>>(s->mbid2.as<unsigned int>(), n, nb, bstart);
+        }
         const unsigned int n0 = (unsigned int)(2 * s->seg_lo), n1 = (unsigned int)(2 * (s->seg_lo + s->seg_Ur));
         if (n) {
             if (big)

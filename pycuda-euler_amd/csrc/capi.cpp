@@ -67,6 +67,8 @@ void refresh_knobs() {
         k.wide_mb = num("EULERHIP_WIDE_MB", -1);
         k.join_mb = num("EULERHIP_JOIN_MB", -1);
         k.join_local = num("EULERHIP_JOIN_LOCAL", -1);
+        k.junction_radix = num("EULERHIP_JUNCTION_RADIX", -1);
+        k.copy_streams = num("EULERHIP_COPY_STREAMS", -1);
         k.sruler_mask = num("EULERHIP_SRULER_MASK", 0);
     }
     g_knobs = k;

@@ -17,8 +17,8 @@
 //   k_jl_scan     per key: its table b and its junctions' tables (one minimizer loop) -> kof[u]
 //                 = b << 2 | which of its two junctions are local; its foreign records appended
 //                 (pad = T) with per-target counts
-//   k_jl_bounds   each table's id range from kof (a table met in two runs: ids not grouped by
-//                 table -- the gate opens)
+//                 and each table's id range from shuffles (k_jl_edges: the pairs across wave
+//                 edges; a table met in two runs -- ids not grouped by table -- opens the gate)
 //   (exclusive scan of the per-target counts) k_jl_scatter: foreign records grouped by target
 //   k_jl_join     per table b: an LDS table keyed by junction collects its keys' local records
 //                 and the foreign records sent to it, then writes the links as k_half_join
@@ -70,38 +70,44 @@ template <typename K> struct JLRec;
 template <> struct JLRec<unsigned long long> { using R = RecJ64; };
 template <> struct JLRec<K128> { using R = RecJ; };
 
+// Foreign records are appended through JL_NCTR counters, 128 B apart, each owning a region of
+// fcap / JL_NCTR records (a wave takes counter wave-id % JL_NCTR): one counter for every wave
+// serialised at the memory side -- 0.83 ms at the headline's 7e4 waves, 34 ms at config 5's 3e6.
+constexpr unsigned int JL_NCTR = 256, JL_CSTRIDE = 32;
+
 // pass 1: per key, its table and local-junction bits into kof; foreign records appended (one
-// reservation per wave) with their targets counted in fcnt
+// reservation per wave) with their targets counted in fcnt.  Run bounds inside a wave from
+// shuffles (rs / re; a table met twice opens the gate); the pairs across wave edges are left to
+// k_jl_edges.  (No private arrays: the candidate records stay in named registers -- a
+// runtime-indexed array put them in scratch, 0.83 ms at the headline.)
 template <typename K>
 __global__ void __launch_bounds__(256) k_jl_scan(const K *dkey, unsigned int U, int k, int bits, const uint8_t *upal,
                                                  unsigned int *kof, typename JLRec<K>::R *fout,
                                                  unsigned int *fcount, unsigned int fcap, unsigned int *fcnt,
-                                                 unsigned int *gate) {
+                                                 unsigned int *rs, unsigned int *re, unsigned int *gate) {
     using R = typename JLRec<K>::R;
     const int j = k - 1, lane = threadIdx.x & 63;
     const K mj = kmask_j(j, (K *)nullptr);
     for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < U; t0 += (uint64_t)gridDim.x * 256) {
         const uint64_t u = t0 + threadIdx.x;
-        R r[4] = {};
-        unsigned int tt[4] = {0, 0, 0, 0};
-        unsigned int nf = 0;
-        if (u < U) {
+        const bool valid = u < U;
+        R r1{}, r2{}, x1{}, x2{};
+        bool e1 = false, e2 = false;
+        unsigned int tb = 0xFFFFFFFFu, ts = 0, tp = 0;
+        if (valid) {
             const K c = dkey[u];
-            unsigned int tb, ts, tp;
             jl_tables(c, k, bits, tb, ts, tp);
-            R r1, r2, x1, x2;
-            bool e1, e2;
             half_recs(c, (unsigned int)u, j, mj, upal, r1, r2, e1, e2, x1, x2);
             kof[u] = tb << 2 | (ts == tb ? 1u : 0u) | (tp == tb ? 2u : 0u);
-            if (ts != tb) {
-                r[nf] = r1, tt[nf++] = ts;
-                if (e1) r[nf] = x1, tt[nf++] = ts;
-            }
-            if (tp != tb) {
-                r[nf] = r2, tt[nf++] = tp;
-                if (e2) r[nf] = x2, tt[nf++] = tp;
-            }
         }
+        // run bounds inside the wave
+        const unsigned int tprev = __shfl_up(tb, 1), tnext = __shfl_down(tb, 1);
+        if (valid && lane > 0 && tprev != tb) {
+            if (atomicExch(&rs[tb], (unsigned int)u) != NONE32) atomicOr(gate, 1u);
+        }
+        if (valid && lane < 63 && (tnext != tb || u + 1 == U)) re[tb] = (unsigned int)u + 1;
+        const bool c1 = valid && ts != tb, c2 = c1 && e1, c3 = valid && tp != tb, c4 = c3 && e2;
+        const unsigned int nf = (unsigned int)c1 + c2 + c3 + c4;
         // wave prefix of the foreign counts, one reservation per wave
         unsigned int incl = nf;
         for (int o = 1; o < 64; o <<= 1) {
@@ -109,41 +115,55 @@ __global__ void __launch_bounds__(256) k_jl_scan(const K *dkey, unsigned int U, 
             if (lane >= o) incl += v;
         }
         const unsigned int tot = __shfl(incl, 63);
+        const unsigned int ctr = (unsigned int)((t0 >> 6) + (threadIdx.x >> 6)) % JL_NCTR, rsz = fcap / JL_NCTR;
         unsigned int base = 0;
-        if (lane == 63 && tot) base = atomicAdd(fcount, tot);
+        if (lane == 63 && tot) base = atomicAdd(&fcount[ctr * JL_CSTRIDE], tot);
         base = __shfl(base, 63);
         unsigned int p = base + incl - nf;
-        for (unsigned int q = 0; q < nf; q++, p++) {
-            if (p < fcap) {
-                R x = r[q];
-                x.pad = tt[q];
-                fout[p] = x;
-                atomicAdd(&fcnt[tt[q]], 1u);
+        const unsigned int p0 = ctr * rsz;
+        auto put = [&](bool c, R x, unsigned int t) {
+            if (!c) return;
+            if (p < rsz) {
+                x.pad = t;
+                fout[p0 + p] = x;
+                atomicAdd(&fcnt[t], 1u);
             } else {
                 atomicOr(gate, 1u);
             }
-        }
+            p++;
+        };
+        put(c1, r1, ts);
+        put(c2, x1, ts);
+        put(c3, r2, tp);
+        put(c4, x2, tp);
     }
 }
 
-// each table's id range [rs[b], re[b]) (rs filled with NONE32 before); a table met twice: gate
-__global__ void __launch_bounds__(256) k_jl_bounds(const unsigned int *kof, unsigned int U, unsigned int *rs,
-                                                   unsigned int *re, unsigned int *gate) {
-    for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned int b = kof[u] >> 2;
-        if (u == 0 || (kof[u - 1] >> 2) != b) {
+// run bounds across the wave edges of k_jl_scan (key pairs 64 i - 1, 64 i) and at 0 / U - 1
+__global__ void __launch_bounds__(256) k_jl_edges(const unsigned int *kof, unsigned int U, unsigned int *rs,
+                                                  unsigned int *re, unsigned int *gate) {
+    const uint64_t ne = ((uint64_t)U + 63) / 64;  // edge i: keys 64 i - 1 | 64 i
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= ne; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t u = i * 64;  // first key of wave i
+        const unsigned int a = u >= 1 && u - 1 < U ? kof[u - 1] >> 2 : 0xFFFFFFFFu;
+        const unsigned int b = u < U ? kof[u] >> 2 : 0xFFFFFFFFu;
+        if (u < U && a != b) {
             if (atomicExch(&rs[b], (unsigned int)u) != NONE32) atomicOr(gate, 1u);
         }
-        if (u + 1 == U || (kof[u + 1] >> 2) != b) re[b] = (unsigned int)u + 1;
+        if (u >= 1 && u - 1 < U && a != b) re[a] = (unsigned int)u;
     }
 }
 
 // foreign records grouped by target: position foff[t] + (the count's remaining share) - 1
+// (region r of fin holds fcount[r * JL_CSTRIDE] records, capped at its size)
 template <typename R>
 __global__ void __launch_bounds__(256) k_jl_scatter(const R *fin, const unsigned int *fcount, unsigned int fcap,
                                                     const unsigned int *foff, unsigned int *fcnt, R *fout) {
-    const unsigned int n = min(*fcount, fcap);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned int rsz = fcap / JL_NCTR;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (uint64_t)rsz * JL_NCTR;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned int r = (unsigned int)(i / rsz);
+        if (i - (uint64_t)r * rsz >= min(fcount[r * JL_CSTRIDE], rsz)) continue;
         const R x = fin[i];
         const unsigned int pos = foff[x.pad] + atomicSub(&fcnt[x.pad], 1u) - 1u;
         fout[pos] = x;

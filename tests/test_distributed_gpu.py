@@ -361,14 +361,17 @@ def test_exchange_record_formats(engines, compact, k):
 
 @pytest.mark.parametrize("knobs", [{"EULERHIP_JUNCTION_BT": "2", "EULERHIP_JUNCTION_SB": "3"},
                                    {"EULERHIP_JUNCTION_BT": "1", "EULERHIP_JUNCTION_CLAIM": "64"},
-                                   {"EULERHIP_JUNCTION_CLAIM": "24"}])
+                                   {"EULERHIP_JUNCTION_CLAIM": "24"},
+                                   {"EULERHIP_JUNCTION_RADIX": "1"},
+                                   {"EULERHIP_JUNCTION_RADIX": "1", "EULERHIP_JUNCTION_CLAIM": "64"}])
 @pytest.mark.parametrize("k", [31, 51])
 def test_junction_join_split_and_retries(engines, monkeypatch, knobs, k):
     """the junction join past 2^14 buckets' worth of junctions (a rank of > ~4.7 * 10^7 keys):
     every bucket split into sub-buckets joined one after the other in one table, forced here on a
     small set by capping the bucket bits; and a table that overflows (claim cap forced small)
     retried with 4096-slot tables, finer buckets, then more sub-buckets -- the same contigs, links
-    and dict size as the oracle (a rank used to fail with EC_ERR_CAPACITY at 2^14 buckets)"""
+    and dict size as the oracle (a rank used to fail with EC_ERR_CAPACITY at 2^14 buckets); and the
+    buckets ordered by the radix sort (past 2^14 buckets, EULERHIP_JUNCTION_RADIX forces it)"""
     import distributed
 
     for n, v in knobs.items():
