@@ -277,8 +277,9 @@ struct ec_session {
     // stream (event wait + unpack) -- the super-k-mer partition runs on each chunk's read groups
     // as they arrive, any other count path waits for all of them (pipe_all)
     hipStream_t cstream = nullptr;
-    // a second copy stream: chunks alternate between the two, so two DMA queues share a batch's
-    // copy (one SDMA copy measured at half its idle rate while the count kernels ran, r06_i)
+    // a second copy stream (EULERHIP_COPY_STREAMS=2): chunks alternate between the two DMA queues.
+    // One SDMA copy runs at half its idle rate while the count kernels run (r06_i trace); two
+    // queues did not help (pipelined 5.22 / 5.22 ms on one, 5.23 / 5.95 on two: r06_m), so one
     hipStream_t cstream2 = nullptr;
     struct Pipe {
         bool active = false;
@@ -2358,6 +2359,21 @@ int phase_merge_w(ec_session *s, const AggW *d_agg, uint64_t n, long long limit,
     return EC_OK;
 }
 
+// palindrome flags of the canonical keys (k_upal).  Odd k over A/C/G/T has no palindromic
+// k-mer (the middle base would be its own complement): the flags are a fill, not a pass over the
+// keys (config 5: 0.64 ms of reading 3.2 GB of keys for nothing)
+template <typename Ops>
+inline int launch_upal(hipStream_t st, const typename Ops::K *dkey, unsigned int U, int k, uint8_t *upal,
+                       unsigned int *npal) {
+    if (!U) return EC_OK;
+    if ((k & 1) && (std::is_same<Ops, Ops64>::value || std::is_same<Ops, OpsW>::value)) {
+        EC_HIP(hipMemsetAsync(upal, 0, U, st));
+        return EC_OK;
+    }
+    k_upal<Ops><<<grid_for(U, 256), 256, 0, st>>>(dkey, U, k, upal, npal);
+    return EC_OK;
+}
+
 // Links by the (k-1)-mer half-edge join (join_w.h), 128-bit (OpsW) or 64-bit (Ops64) keys.
 // gate: a device flag set when a level region or a join table overflowed; the caller then
 // launches k_neighbors / k_succ gated on it (they return at once unless it is set).
@@ -2434,7 +2450,7 @@ int links_join(ec_session *s, int k, unsigned int U, bool &ok, const unsigned in
     unsigned long long *ibeg = s->bb2.as<unsigned long long>(), *iend = ibeg + nbmax;
     EC_HIP(hipMemsetAsync(flags, 0, 8, st));
     const typename Ops::K *dkey = s->dkey.as<typename Ops::K>();
-    k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(dkey, U, k, s->upal.as<uint8_t>(), &dsc->npal);
+    EC_CHECK(launch_upal<Ops>(st, dkey, U, k, s->upal.as<uint8_t>(), &dsc->npal));
     R *src = s->recs.as<R>(), *dst = s->recs2.as<R>();
     // level 0 fused with the emit (k_half_emit_l1), its regions in dst
     const uint64_t nb0 = 1ull << lv[0];
@@ -2512,7 +2528,7 @@ int links_local(ec_session *s, int k, unsigned int U, const Index &sidx, bool &o
     EC_HIP(hipMemsetAsync(cnt, 0, ((size_t)ntab + 1) * 4, st));
     const K *dkey = s->dkey.as<K>();
     uint8_t *upal = s->upal.as<uint8_t>();
-    k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(dkey, U, k, upal, &dsc->npal);
+    EC_CHECK(launch_upal<Ops>(st, dkey, U, k, upal, &dsc->npal));
     k_jl_scan<K><<<grid_for(U, B, 8192), B, 0, st>>>(dkey, U, k, bits, upal, s->jl_kof.as<unsigned int>(), s->recs.as<R>(),
                                                      fctr, fcap, cnt, s->jl_rs.as<unsigned int>(),
                                                      s->jl_re.as<unsigned int>(), &flags[1]);
@@ -2793,8 +2809,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
     EC_CHECK(s->succ.ensure(Nn * 4));
     EC_CHECK(s->pred.ensure(Nn * 4));
     if (U && ext_succ) {  // partitioned links (ec_graph_finish): successors computed by the ranks
-        k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<typename Ops::K>(), U, k, s->upal.as<uint8_t>(),
-                                                 &dsc->npal);
+        EC_CHECK(launch_upal<Ops>(st, s->dkey.as<typename Ops::K>(), U, k, s->upal.as<uint8_t>(), &dsc->npal));
         EC_HIP(hipMemcpyAsync(s->succ.p, ext_succ, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
     }
     // links by the half-edge join (join_w.h) instead of neighbour probes from ~2e6 keys on, for
@@ -3361,8 +3376,7 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
     EC_CHECK(s->rt_sidx.ensure(Nn * 4));
     if (!s->placed) {  // (a placed segment has its flags and links already: ec_graph_place / join)
         EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
-        if (U) k_upal<Ops><<<grid_for(U, B), B, 0, st>>>(s->dkey.as<typename Ops::K>(), U, s->k, s->upal.as<uint8_t>(),
-                                                         &dsc->npal);
+        EC_CHECK(launch_upal<Ops>(st, s->dkey.as<typename Ops::K>(), U, s->k, s->upal.as<uint8_t>(), &dsc->npal));
     }
     if (n1 > n0 && d_succ)
         EC_HIP(hipMemcpyAsync(s->succ.as<unsigned int>() + n0, d_succ, (size_t)(n1 - n0) * 4, hipMemcpyDeviceToDevice,
@@ -3973,7 +3987,7 @@ int pipe_plan(ec_session *s, Pipe &pp, uint64_t nbases, uint64_t bytes_per_base4
 }
 
 // the copy stream of chunk c (EULERHIP_COPY_STREAMS=1: cstream only)
-inline hipStream_t copy_stream(ec_session *s, int c) { return (c & 1) && kn().copy_streams != 1 ? s->cstream2 : s->cstream; }
+inline hipStream_t copy_stream(ec_session *s, int c) { return (c & 1) && kn().copy_streams == 2 ? s->cstream2 : s->cstream; }
 
 // copy the offsets entries reads [r0, r1] need (chunk by chunk: [ravail[c-1] + 1, ravail[c] + 1))
 int pipe_copy_offsets(ec_session *s, const Pipe &pp, int c, const uint64_t *offsets, uint64_t *d_off) {
@@ -5011,8 +5025,8 @@ int graph_place(ec_session *s, uint64_t lo, uint64_t U, int nowners, void *d_out
     }
     EC_HIP(hipMemsetAsync(&dsc->npal, 0, 4, st));
     if (Ur)
-        k_upal<Ops><<<grid_for(Ur, B), B, 0, st>>>(s->dkey.as<K>() + lo, (unsigned int)Ur, s->k,
-                                                   s->upal.as<uint8_t>() + lo, &dsc->npal);
+        EC_CHECK(launch_upal<Ops>(st, s->dkey.as<K>() + lo, (unsigned int)Ur, s->k, s->upal.as<uint8_t>() + lo,
+                                  &dsc->npal));
     // junction records routed to the junctions' owners (the keys' rule, shard.h OwnerFn)
     OwnerFn own = owner_fn(s->k);
     if (s->owner_rule == 1) own.sk = 0, own.wk = 0;

@@ -51,15 +51,23 @@ __device__ inline void jl_tables(unsigned long long c, int k, int bits, unsigned
     ts = sk_bucket_of(min_remix(ms), bits);
     tp = sk_bucket_of(min_remix(mp), bits);
 }
+// 128-bit keys: the m-mers rolled out of the key two bits a step (m-mer p = w - 1 - q after q
+// steps) and reverse-complemented in registers (bit reverse + pair swap) -- not two 128-bit
+// extractions at variable shifts per m-mer (config 5: the scan was VALU-bound, ~900 VALU a key)
 __device__ inline void jl_tables(const K128 &c, int k, int bits, unsigned int &tb, unsigned int &ts, unsigned int &tp) {
     const int w = k - SK_M + 1;
-    const K128 tc = twin128(c, k);
+    constexpr uint32_t MM = (1u << (2 * SK_M)) - 1;
+    unsigned long long lo = c.lo, hi = c.hi;
     uint32_t mp = 0xFFFFFFFFu, ms = 0xFFFFFFFFu;
-    for (int p = 0; p < w; p++) {
-        const uint32_t f = bits30_128(c, 2 * (k - SK_M - p)), r = bits30_128(tc, 2 * p);
+    for (int q = 0; q < w; q++) {  // m-mer p = w - 1 - q: the prefix junction lacks q = 0, the suffix q = w - 1
+        const uint32_t f = (uint32_t)lo & MM;
+        uint32_t r = __builtin_bitreverse32(f ^ MM);                       // complement, bits reversed
+        r = (((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1)) >> (32 - 2 * SK_M);  // base order reversed
         const uint32_t h = mmer_hash(f < r ? f : r);
-        if (p < w - 1) mp = h < mp ? h : mp;
-        if (p > 0) ms = h < ms ? h : ms;
+        if (q > 0) mp = h < mp ? h : mp;
+        if (q < w - 1) ms = h < ms ? h : ms;
+        lo = (lo >> 2) | (hi << 62);
+        hi >>= 2;
     }
     tb = bits ? min_remix_w(mp < ms ? mp : ms) >> (32 - bits) : 0u;
     ts = bits ? min_remix_w(ms) >> (32 - bits) : 0u;
