@@ -155,6 +155,7 @@ class HipEngine:
 
         self.torch = torch
         self.device = torch.device("cuda", device)
+        self._total = None  # device memory (trim_if_large)
         # default: torch's current stream, so the engine's kernels are ordered after the torch
         # ops that produce its inputs (slices, concatenations, RCCL outputs)
         if stream is None:
@@ -198,9 +199,14 @@ class HipEngine:
         buffers freed and allocated again are slow -- config 5's per-rank step freeing ~165 GB
         before its count measured 5.6 s of count against 67 ms without (r06_f)"""
         torch = self.torch
+        held = self.sess.device_bytes()
+        if self._total is None:
+            self._total = torch.cuda.get_device_properties(self.device).total_memory
+        if held <= frac * self._total:  # (the common case decided without a device query)
+            return False
         free, total = torch.cuda.mem_get_info(self.device)
         free += torch.cuda.memory_reserved(self.device) - torch.cuda.memory_allocated(self.device)
-        if self.sess.device_bytes() > frac * total and free < free_frac * total:
+        if free < free_frac * total:
             self.sess.trim(64 << 20)
             self.torch.cuda.empty_cache()  # (and torch's cached blocks: the next allocations are the session's)
             return True

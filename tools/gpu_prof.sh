@@ -12,7 +12,8 @@ if [ -z "$NOPMC" ]; then
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run -- python3 $B > /dev/null 2> $O/fetch.err || { echo FETCH FAILED; tail -5 $O/fetch.err; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run -- python3 $B > /dev/null 2> $O/write.err || { echo WRITE FAILED; tail -5 $O/write.err; exit 1; }
 echo PMC done
-python3 profiles/collect_traffic.py $O/fetch $O/write $CFG ${TAG} > $O/traffic.json 2> $O/traffic.err || true
+WL=$(python3 -c "import sys; sys.path.insert(0, '.'); import bench; print(bench.CONFIGS['$CFG']['name'])")
+python3 profiles/collect_traffic.py $O/fetch $O/write "$WL" ${TAG} > $O/traffic.json 2> $O/traffic.err || true
 fi
 python3 tools/rocpd_stats.py $O/kt/run_results.db $O/kernel_stats.csv || true
 # (the databases stay on the box: a call's gpurun_out is merged back only below 64 MiB)

@@ -175,23 +175,22 @@ def main():
                 tick("starts", t0)
             starts = torch.cat(sts)
             nc = starts.numel() // distributed.START_BYTES
-            chars = ends = None
-            for eng in engines:
+            runs = []
+            for eng in engines:  # (as partitioned_finish: each rank's own runs gathered to rank 0)
                 t0 = t_start()
-                nchars = eng.graph_layout(starts, nc)
+                eng.graph_layout(starts, nc)
                 tick("layout", t0)
                 t0 = t_start()
-                c, e = eng.zeros(nchars), eng.zeros(max(2 * nc * distributed.end_bytes(a.k), 8))
-                eng.graph_emit_part(c, e)
+                runs.append(eng.graph_emit_runs())
                 tick("emit", t0)
-                chars = c if chars is None else chars + c
-                ends = e.view(torch.int32) if ends is None else ends + e.view(torch.int32)
+            allruns = torch.cat(runs)
             t0 = t_start()
-            res = engines[0].graph_collect(chars, ends.view(torch.uint8), a.k, npal)
-            tick("collect", t0)
+            engines[0].graph_collect_runs(allruns, [r.numel() for r in runs], a.k, npal, fetch=False)
+            tick("collect", t0)  # (results left in the session's pinned buffers, as the bench step)
+            res = engines[0].sess.fetch(a.k)
             extra = (", junction records off-rank %.2f MB, link records %.2f MB, chains gathered %.1f MB (%d), "
-                     "starts %.2f MB, chars %.1f MB" % (jx / 1e6, lx / 1e6, supers.numel() / 1e6, M,
-                                                        starts.numel() / 1e6, chars.numel() / 1e6))
+                     "starts %.2f MB, runs gathered %.1f MB" % (jx / 1e6, lx / 1e6, supers.numel() / 1e6, M,
+                                                                starts.numel() / 1e6, allruns.numel() / 1e6))
             xb = 0
         print("export per rank:", [round(x, 2) for x in t["export"]], "count per rank:", [round(x, 2) for x in t["count"]])
         mx_ph = {k: round(max(v), 2) for k, v in t.items()}
