@@ -2498,8 +2498,10 @@ int links_local(ec_session *s, int k, unsigned int U, const Index &sidx, bool &o
     using K = typename Ops::K;
     using R = typename JLRec<K>::R;
     ok = false;
-    const int bits = jl_bits(sidx);
+    int bits = jl_bits(sidx);
     if (bits < 1 || bits > 22 || k < SK_M + 2) return EC_OK;
+    // (tests: tables finer or coarser than the count's -- ids not grouped by table, the gate opens)
+    if (kn().jl_bits_delta) bits = std::max(1, std::min(22, bits + kn().jl_bits_delta));
     const unsigned int ntab = 1u << bits;
     // a table's junction groups ~ its keys (plus the foreign records sent to it): tables of mean
     // <= ~700 keys in 2048 slots, <= ~1500 in 4096 (an overflowing one opens the gate)
@@ -2511,7 +2513,8 @@ int links_local(ec_session *s, int k, unsigned int U, const Index &sidx, bool &o
     Scalars *dsc = s->scal.as<Scalars>();
     const uint64_t N = 2ull * U;
     // foreign records: ~2 / (w + 1) of the 2U (7 % at k = 31, 3 % at k = 51); room for a third
-    const unsigned int fcap = (U / 3 / JL_NCTR + 64) * JL_NCTR;
+    const unsigned int fcap = kn().jl_fcap > 0 ? ((unsigned int)kn().jl_fcap / JL_NCTR + 1) * JL_NCTR
+                                               : (U / 3 / JL_NCTR + 64) * JL_NCTR;
     EC_CHECK(s->jl_kof.ensure((size_t)U * 4));
     EC_CHECK(s->jl_rs.ensure((size_t)ntab * 4));
     EC_CHECK(s->jl_re.ensure((size_t)ntab * 4));
