@@ -98,6 +98,18 @@ __device__ inline unsigned long long tile_lookback(const TileLB &lb, unsigned in
     return excl;
 }
 
+// block-wide OR over three rotating flag words in LDS the caller owns (their words free at the
+// time; __syncthreads_or keeps a 256-B LDS buffer of its own, which put k_tile_chains just past
+// the 40 KB of four workgroups a CU).  Round r sets f[r % 3]; thread 0 clears f[(r + 1) % 3]
+// before the barrier: its last readers (round r - 2) have passed barrier r - 1, its next writers
+// (round r + 1) start after barrier r
+__device__ inline bool block_or3(bool v, unsigned int *f, unsigned int r) {
+    if (threadIdx.x == 0) f[(r + 1) % 3] = 0;
+    if (__ballot(v) && (threadIdx.x & 63) == 0) atomicOr(&f[r % 3], 1u);
+    __syncthreads();
+    return f[r % 3] != 0;
+}
+
 // nodes [n0, N): the tiles of a segment (the multi-GPU finish ranks its own segment's chains;
 // a successor outside the segment is external like one outside the tile).  lb.status set: the
 // chains compacted in this launch (above; LH = super index), else tile-local records in scratch
@@ -108,11 +120,20 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
                                                        SuperRec *scratch, unsigned int *PK, unsigned int *RK,
                                                        unsigned int *PL, unsigned long long *PM, unsigned int n0 = 0,
                                                        const unsigned int *tb = nullptr, TileLB lb = TileLB{}) {
+    // 40 KB of LDS, four workgroups a CU (round 6: 48.4 KB held three): distances and chain
+    // lengths fit 16 bits in a 2048-node tile, the chain length is written by the chain's tail
+    // (no 32-bit atomic), and the head counts / global base reuse the distances' words once the
+    // pointer jumping is done
     __shared__ uint16_t s_ls[RT_TN], s_lp[RT_TN], s_p[RT_TN], s_mn[RT_TN];
-    __shared__ unsigned int s_d[RT_TN], s_cl[RT_TN];
+    __shared__ __attribute__((aligned(16))) uint16_t s_cl[RT_TN];
     __shared__ unsigned long long s_cm[RT_TN];
-    __shared__ unsigned int s_wsum[RT_PER][RT_NT / 64];
-    __shared__ unsigned long long s_gbase;
+    __shared__ __attribute__((aligned(16))) uint16_t s_d[RT_TN];
+    static_assert(RT_PER * (RT_NT / 64) * 4 + 16 <= RT_TN * 2, "head counts fit the distance words");
+    unsigned int (*s_wsum)[RT_NT / 64] = reinterpret_cast<unsigned int (*)[RT_NT / 64]>(s_d);
+    unsigned long long &s_gbase = *reinterpret_cast<unsigned long long *>(s_d + RT_TN - 8);
+    // block_or3's flags: chain-length words, written only after the pointer jumping
+    unsigned int *s_or = reinterpret_cast<unsigned int *>(s_cl);
+    unsigned int orr = 0;
     // tiles of RT_TN nodes from n0, or tb's tiles (k_tile_plan: cut at bucket starts, <= RT_TN)
     const unsigned int tile = blockIdx.x, tid = threadIdx.x;
     const unsigned int base = tb ? tb[tile] : n0 + tile * RT_TN;
@@ -134,7 +155,6 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         s_ls[i] = in ? (uint16_t)(s - base) : RT_NONE;
         ext[q] = in ? NONE32 : s;
         s_lp[i] = RT_NONE;
-        s_cl[i] = 0;
         s_cm[i] = NONE64;
     }
     __syncthreads();
@@ -148,6 +168,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
     // node passed (on a cycle, after the rounds: the cycle's smallest node)
     uint16_t p[RT_PER], mn[RT_PER];
     unsigned int d[RT_PER];
+    if (tid == 0) s_or[0] = 0;  // (block_or3 round 0's flag; round r clears r + 1's)
 #pragma unroll
     for (int q = 0; q < RT_PER; q++) {
         const unsigned int i = tid + q * RT_NT;
@@ -156,7 +177,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         d[q] = lp == RT_NONE ? 0u : 1u;
         mn[q] = p[q] < i ? p[q] : (uint16_t)i;
         s_p[i] = p[q];
-        s_d[i] = d[q];
+        s_d[i] = (uint16_t)d[q];
         s_mn[i] = mn[q];
     }
     __syncthreads();
@@ -178,10 +199,10 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         for (int q = 0; q < RT_PER; q++) {
             const unsigned int i = tid + q * RT_NT;
             s_p[i] = p[q];
-            s_d[i] = d[q];
+            s_d[i] = (uint16_t)d[q];
             s_mn[i] = mn[q];
         }
-        if (!__syncthreads_or(more)) break;
+        if (!block_or3(more, s_or, orr++)) break;
     }
     // nodes of in-tile cycles: their "head" still has a predecessor.  Rank them again from the
     // cycle's smallest node (the cycle cut in front of it)
@@ -192,7 +213,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
         cyc[q] = valid[q] && s_lp[p[q]] != RT_NONE;
         anyc |= cyc[q];
     }
-    if (__syncthreads_or(anyc)) {
+    if (block_or3(anyc, s_or, orr++)) {
 #pragma unroll
         for (int q = 0; q < RT_PER; q++) {
             const unsigned int i = tid + q * RT_NT;
@@ -202,7 +223,7 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
                 d[q] = key ? 0u : 1u;
             }
             s_p[i] = p[q];
-            s_d[i] = d[q];
+            s_d[i] = (uint16_t)d[q];
         }
         __syncthreads();
         for (int r = 0; r < RT_ROUNDS; r++) {
@@ -219,17 +240,21 @@ __global__ void __launch_bounds__(RT_NT) k_tile_chains(const uint8_t *upal, cons
                 const unsigned int i = tid + q * RT_NT;
                 if (!cyc[q]) continue;
                 s_p[i] = p[q];
-                s_d[i] = d[q];
+                s_d[i] = (uint16_t)d[q];
             }
             __syncthreads();
         }
     }
-    // per chain / cycle at its head: length, min first event; the successor of a chain's tail
+    // per chain / cycle at its head: length (written by the chain's tail, or by the cycle node
+    // in front of its key), min first event; the successor of a chain's tail.  (The barrier: the
+    // chain lengths overwrite block_or3's flags, which a slow wave may still be reading)
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < RT_PER; q++) {
         if (!valid[q]) continue;
+        const unsigned int i = tid + q * RT_NT;
         const uint16_t h = p[q];
-        atomicMax(&s_cl[h], d[q] + 1);
+        if (cyc[q] ? s_ls[i] == h : s_ls[i] == RT_NONE) s_cl[h] = (uint16_t)(d[q] + 1);
         if (fev[q] < s_cm[h]) atomicMin(&s_cm[h], fev[q]);
     }
     // the heads in node order (q-major: node i = tid + q * NT): a wave's count per q
