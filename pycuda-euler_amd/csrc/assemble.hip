@@ -1913,16 +1913,18 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     }
     // minimizer runs as the partition records (count_wide.h RunWM; EULERHIP_WIDE_RUNS=0: windows)
     const bool runs = mb && kn().wide_runs != 0;
+    // HyperLogLog sampled by minimizer past ~6.7e7 positions (as the super-k-mer count)
+    const uint32_t hsmask = mb && (uint64_t)nreads * mbM >= (1ull << 26) ? 255u : 0u;
     if (runs)
         k_upsweep_w<true, true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
                                                                          s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
                                                                          &dsc->npos, &dsc->maxlocal, &dsc->skew,
-                                                                         dsc->lens, wbv, mbM);
+                                                                         dsc->lens, wbv, mbM, hsmask);
     else if (mb)
         k_upsweep_w<true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
                                                                    s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
                                                                    &dsc->npos, &dsc->maxlocal, &dsc->skew, dsc->lens,
-                                                                   wbv, mbM);
+                                                                   wbv, mbM, hsmask);
     else
         k_upsweep_w<false><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
                                                                     s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
@@ -1940,7 +1942,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     EC_CHECK(d2h(s, &hsc, dsc, sizeof(Scalars), st));
     EC_CHECK(host_sync(s, st));
     const uint64_t P = hsc.npos;
-    const double est = hsc.est;
+    const double est = hsc.est * (hsmask + 1.0);
     // Up to 2^FINE_W_BITS buckets of <= 1100 estimated keys in 3328-slot tables (156 KB: one
     // workgroup per CU), sized exactly by the fine histogram.  Past that (~1.8e7 keys: config
     // 5's 200 Mbp genome has 2e8) a third level splits every fine bucket into 2^sbits
@@ -2526,12 +2528,12 @@ int links_local(ec_session *s, int k, unsigned int U, const Index &sidx, bool &o
     // [1]: the gate; [JL_CSTRIDE (r + 1)]: foreign records of region r
     unsigned int *flags = s->jl_flag.as<unsigned int>(), *fctr = flags + JL_CSTRIDE;
     unsigned int *cnt = s->jl_cnt.as<unsigned int>(), *off = s->jl_off.as<unsigned int>();
-    EC_HIP(hipMemsetAsync(flags, 0, (size_t)(JL_NCTR + 1) * JL_CSTRIDE * 4, st));
-    EC_HIP(hipMemsetAsync(s->jl_rs.p, 0xFF, (size_t)ntab * 4, st));
-    EC_HIP(hipMemsetAsync(cnt, 0, ((size_t)ntab + 1) * 4, st));
     const K *dkey = s->dkey.as<K>();
     uint8_t *upal = s->upal.as<uint8_t>();
-    EC_CHECK(launch_upal<Ops>(st, dkey, U, k, upal, &dsc->npal));
+    // (odd k: no palindromic k-mer, the flags a fill in the same launch; even k: k_upal)
+    k_jl_init<<<grid_for(N, B, 4096), B, 0, st>>>(flags, (JL_NCTR + 1) * JL_CSTRIDE, s->jl_rs.as<unsigned int>(), cnt,
+                                                 ntab, s->succ.as<unsigned int>(), N, (k & 1) ? upal : nullptr, U);
+    if (!(k & 1)) EC_CHECK(launch_upal<Ops>(st, dkey, U, k, upal, &dsc->npal));
     k_jl_scan<K><<<grid_for(U, B, 8192), B, 0, st>>>(dkey, U, k, bits, upal, s->jl_kof.as<unsigned int>(), s->recs.as<R>(),
                                                      fctr, fcap, cnt, s->jl_rs.as<unsigned int>(),
                                                      s->jl_re.as<unsigned int>(), &flags[1]);
@@ -2539,7 +2541,6 @@ int links_local(ec_session *s, int k, unsigned int U, const Index &sidx, bool &o
                                                            s->jl_re.as<unsigned int>(), &flags[1]);
     EC_CHECK(scan_excl_u32(s, cnt, off, (size_t)ntab + 1));
     k_jl_scatter<R><<<grid_for(fcap, B, 4096), B, 0, st>>>(s->recs.as<R>(), fctr, fcap, off, cnt, s->recs2.as<R>());
-    EC_HIP(hipMemsetAsync(s->succ.p, 0xFF, N * 4, st));
     // (4096 slots: 96 KB of 128-bit slots, one workgroup a CU -- 512 threads to hide the probes)
 #define EC_JL_JOIN(SL, ODD)                                                                                        \
     k_jl_join<K, SL, SL / 8, ODD><<<ntab, SL / 8, 0, st>>>(dkey, s->jl_kof.as<unsigned int>(), s->jl_rs.as<unsigned int>(), \

@@ -194,7 +194,12 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
                                                           int k, uint64_t gsize, unsigned int *hist,
                                                           uint8_t *hll_blocks, unsigned long long *npos,
                                                           unsigned int *maxlocal, unsigned int *skew,
-                                                          unsigned int *lens, const uint32_t *wbv, uint32_t mbM) {
+                                                          unsigned int *lens, const uint32_t *wbv, uint32_t mbM,
+                                                          uint32_t smask = 0) {
+    // smask (minimizer buckets): the HyperLogLog sees only the k-mers whose minimizer's low bits
+    // (pv bits 12.., uniform) & smask are zero -- the estimate x (smask + 1), as the super-k-mer
+    // count samples it; the canonical form and mix128 of the other windows are not computed
+    // (config 5: the upsweep was compute-bound on them, 8 ms)
     static_assert(MB || !RUNS, "runs need minimizer buckets");
     __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE_W + 16];
     __shared__ unsigned int h_cnt[FINE_W / 2];
@@ -237,11 +242,14 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
             if ((t & 3) == 0) c4 = rv.chunk(t >> 2);
             roll_w(fwd, rc, code2(c4 >> (8 * (t & 3))), mask, sh);
             if (t + 1 < (uint32_t)k) continue;
-            const K128 c = fwd < rc ? fwd : rc;
-            const uint32_t hh = (uint32_t)(mix128(c) >> 32);  // as k_upsweep
-            const uint32_t j = hh >> (32 - HLL_REG_BITS);
-            const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
-            const uint32_t pv = MB ? wbv[wbv_at(r, t + 1 - (uint32_t)k, mbM)] : hh;
+            const uint32_t pv0 = MB ? wbv[wbv_at(r, t + 1 - (uint32_t)k, mbM)] : 0u;
+            const bool samp = !MB || ((pv0 >> 12) & smask) == 0;
+            uint32_t hh = 0;
+            if (samp) {
+                const K128 c = fwd < rc ? fwd : rc;
+                hh = (uint32_t)(mix128(c) >> 32);  // as k_upsweep
+            }
+            const uint32_t pv = MB ? pv0 : hh;
             const uint32_t f = pv >> (32 - FINE_W_BITS);
             bool open = true;
             if (RUNS) {
@@ -251,7 +259,11 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
                 myrec += open;
             }
             if (open) atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
-            if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
+            if (samp) {
+                const uint32_t j = hh >> (32 - HLL_REG_BITS);
+                const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+                if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
+            }
         }
     }
     unsigned long long binsum = 0;  // bin-sum overflow check of k_upsweep

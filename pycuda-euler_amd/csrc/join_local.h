@@ -78,6 +78,21 @@ template <typename K> struct JLRec;
 template <> struct JLRec<unsigned long long> { using R = RecJ64; };
 template <> struct JLRec<K128> { using R = RecJ; };
 
+// the join's state in one launch (four fills were four launches with host gaps between them,
+// ~30 us of the headline step): flags and counters zeroed, table starts NONE, successors NONE,
+// palindrome flags zeroed when odd k has none (upal non-null)
+__global__ void __launch_bounds__(256) k_jl_init(unsigned int *flags, unsigned int nflags, unsigned int *rs,
+                                                 unsigned int *cnt, unsigned int ntab, unsigned int *succ,
+                                                 uint64_t nsucc, uint8_t *upal, uint64_t nupal) {
+    const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, st = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = t0; i < nflags; i += st) flags[i] = 0;
+    for (uint64_t i = t0; i < ntab; i += st) rs[i] = NONE32;
+    for (uint64_t i = t0; i <= ntab; i += st) cnt[i] = 0;
+    for (uint64_t i = t0; i < nsucc; i += st) succ[i] = NONE32;
+    if (upal)
+        for (uint64_t i = t0; i < nupal; i += st) upal[i] = 0;
+}
+
 // Foreign records are appended through JL_NCTR counters, 128 B apart, each owning a region of
 // fcap / JL_NCTR records (a wave takes counter wave-id % JL_NCTR): one counter for every wave
 // serialised at the memory side -- 0.83 ms at the headline's 7e4 waves, 34 ms at config 5's 3e6.
