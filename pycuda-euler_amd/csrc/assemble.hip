@@ -1915,7 +1915,12 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     const bool runs = mb && kn().wide_runs != 0;
     // HyperLogLog sampled by minimizer past ~6.7e7 positions (as the super-k-mer count)
     const uint32_t hsmask = mb && (uint64_t)nreads * mbM >= (1ull << 26) ? 255u : 0u;
-    if (runs)
+    if (runs && kn().upsweep_staged != 1)
+        k_upsweep_runs<<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
+                                                                s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
+                                                                &dsc->npos, &dsc->maxlocal, &dsc->skew, wbv, mbM,
+                                                                hsmask);
+    else if (runs)  // (EULERHIP_UPSWEEP_STAGED=1: the staged kernel, A/B)
         k_upsweep_w<true, true><<<(unsigned)ngroups, TILE_READS, 0, st>>>(d_reads, d_off, nreads, k, gsize,
                                                                          s->hist.as<unsigned int>(), s->hll.as<uint8_t>(),
                                                                          &dsc->npos, &dsc->maxlocal, &dsc->skew,

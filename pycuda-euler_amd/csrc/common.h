@@ -66,6 +66,7 @@ struct Knobs {
     int junction_radix = -1;
     int jl_fcap = -1;        // EULERHIP_JL_FCAP: the local join's foreign-record capacity (tests: overflow)
     int jl_bits_delta = 0;   // EULERHIP_JL_BITS_DELTA: join tables finer / coarser than the count's (tests)
+    int upsweep_staged = -1;  // EULERHIP_UPSWEEP_STAGED=1: runs counted by the staged upsweep (A/B)
     int copy_streams = -1;    // EULERHIP_COPY_STREAMS=2: host-input chunks alternate over two copy streams  // EULERHIP_JUNCTION_RADIX=1: junction buckets by the radix sort at any size     // EULERHIP_JOIN_LOCAL=0: links of minimizer-table ids by the global half-edge join
     int join_mb = -1;        // EULERHIP_JOIN_MB=0: junctions of minimizer-bucketed keys bucketed by mix128
     bool no_small_starts = false; // EULERHIP_NO_SMALL_STARTS: short lists on the general launches (k_starts_small, k_links_small off)

@@ -68,16 +68,22 @@ __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *
     const uint8_t *rd = st + ((uint64_t)(buf + s) - a0);
     const uint32_t M = L - K + 1, nh = L - SK_M + 1;
     constexpr uint32_t MM = (1u << (2 * SK_M)) - 1;
-    uint32_t mf = 0, mr = 0;
+    uint32_t mf = 0, mr = 0, nonacgt = 0;
     auto push = [&](uint32_t b) {
         mf = ((mf << 2) | b) & MM;
         mr = (mr >> 2) | ((3u - b) << (2 * SK_M - 2));
     };
-    for (uint32_t t = 0; t < SK_M - 1; t++) push(code2(rd[t]));
+    // (every byte of the read passes here once: a byte other than A/C/G/T flags the call as the
+    // length check does -- k_upsweep_runs no longer stages the reads to look)
+    auto base = [&](uint32_t c) {
+        nonacgt |= is_acgt(c) ^ 1u;
+        return code2(c);
+    };
+    for (uint32_t t = 0; t < SK_M - 1; t++) push(base(rd[t]));
     uint32_t S[W];
 #pragma unroll
     for (int j = 0; j < W; j++) {  // block 0: m-mers 0 .. W - 1 (all exist: L >= K)
-        push(code2(rd[SK_M - 1 + j]));
+        push(base(rd[SK_M - 1 + j]));
         S[j] = mmer_hash(mf < mr ? mf : mr);
     }
 #pragma unroll
@@ -93,7 +99,7 @@ __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *
             const uint32_t e = w0 + W + j;  // m-mer of the next block
             H[j] = 0xFFFFFFFFu;
             if (e < nh) {
-                push(code2(rd[e + SK_M - 1]));
+                push(base(rd[e + SK_M - 1]));
                 H[j] = mmer_hash(mf < mr ? mf : mr);
             }
             P = min(P, H[j]);
@@ -103,6 +109,7 @@ __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *
 #pragma unroll
         for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
     }
+    if (nonacgt) *bad = 1u;
 }
 
 constexpr int STAGE_W = 40896;  // LDS stage of the wide kernels (256 reads of <= 159 bases; upsweep in 80 KB)
@@ -285,6 +292,90 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_w(const uint8_t *buf, co
         if (mypos) atomicAdd(npos, mypos);
         if (mymax) atomicMax(maxlocal, mymax);
         if (mynonclean) atomicOr(&lens[2], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && s_diff != 0) atomicOr(skew, 1u);
+    for (int i = threadIdx.x; i < FINE_W; i += blockDim.x) hist[g * FINE_W + i] = (h_cnt[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+    for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x)
+        hll_blocks[g * (1 << HLL_REG_BITS) + i] = (uint8_t)h_reg[i];
+}
+
+// ---- upsweep of minimizer runs without the reads (round 6) ------------------------------------
+// RUNS only needs each window's minimizer (k_wbv wrote it) to find where runs open, so the reads
+// are not staged and no window's k-mer is rolled: a thread a read walks its windows' wbv words
+// (lane-contiguous loads) and counts run opens into the fine histogram; only the HyperLogLog's
+// windows (minimizer low bits & smask == 0, see k_upsweep_w) build their canonical k-mer from the
+// read bytes.  k_wbv checked every byte (A/C/G/T) and length.  The staged kernel held 80 KB of
+// LDS (the 40-KB stage + histogram + registers: two workgroups a CU) and rolled every base:
+// config 5's upsweep 7.8 ms.
+__global__ void __launch_bounds__(TILE_READS) k_upsweep_runs(const uint8_t *buf, const uint64_t *off,
+                                                             uint64_t nreads, int k, uint64_t gsize, unsigned int *hist,
+                                                             uint8_t *hll_blocks, unsigned long long *npos,
+                                                             unsigned int *maxlocal, unsigned int *skew,
+                                                             const uint32_t *wbv, uint32_t mbM, uint32_t smask) {
+    __shared__ unsigned int h_cnt[FINE_W / 2];
+    __shared__ unsigned int h_reg[1 << HLL_REG_BITS];
+    for (int i = threadIdx.x; i < FINE_W / 2; i += blockDim.x) h_cnt[i] = 0;
+    for (int i = threadIdx.x; i < (1 << HLL_REG_BITS); i += blockDim.x) h_reg[i] = 0;
+    __syncthreads();
+    const uint64_t g = blockIdx.x;
+    const uint64_t g0 = group_begin(g, gsize, nreads), g1 = group_begin(g + 1, gsize, nreads);
+    const K128 mask = kmask128(k);
+    const int sh = 2 * (k - 1);
+    unsigned long long mypos = 0, myrec = 0;
+    unsigned int mymax = 0;
+    for (uint64_t r = g0 + threadIdx.x; r < g1; r += TILE_READS) {
+        const uint64_t s = off[r];
+        const uint64_t len = off[r + 1] - s;
+        if (len < (uint64_t)k) continue;
+        const uint32_t m = (uint32_t)(len - k + 1);
+        mypos += m;
+        mymax = max(mymax, 2 * m - 1);
+        uint32_t runv = 0, runl = 0;
+        K128 fwd{0, 0}, rc{0, 0};
+        bool have = false;  // fwd / rc hold the previous window's k-mer
+        for (uint32_t w = 0; w < m; w++) {
+            const uint32_t pv = wbv[wbv_at(r, w, mbM)];
+            const bool open = w == 0 || pv != runv || runl == RUN_MAXW;
+            runl = open ? 1u : runl + 1;
+            runv = pv;
+            myrec += open;
+            if (open) {
+                const uint32_t f = pv >> (32 - FINE_W_BITS);
+                atomicAdd(&h_cnt[f >> 1], 1u << ((f & 1) * 16));  // overflow: checked after the group
+            }
+            if (((pv >> 12) & smask) == 0) {
+                if (!have)
+                    for (int t = 0; t < k; t++) roll_w(fwd, rc, code2(buf[s + w + t]), mask, sh);
+                else
+                    roll_w(fwd, rc, code2(buf[s + w + k - 1]), mask, sh);
+                have = true;
+                const K128 c = fwd < rc ? fwd : rc;
+                const uint32_t hh = (uint32_t)(mix128(c) >> 32);
+                const uint32_t j = hh >> (32 - HLL_REG_BITS);
+                const uint32_t rho = (uint32_t)__clz((int)((hh << HLL_REG_BITS) | (1u << (HLL_REG_BITS - 1)))) + 1;
+                if (rho > h_reg[j]) atomicMax(&h_reg[j], rho);
+            } else {
+                have = false;
+            }
+        }
+    }
+    unsigned long long binsum = 0;  // bin-sum overflow check of k_upsweep
+    __syncthreads();
+    for (int i = threadIdx.x; i < FINE_W / 2; i += blockDim.x) binsum += (h_cnt[i] & 0xFFFFu) + (h_cnt[i] >> 16);
+    for (int o = 32; o > 0; o >>= 1) {
+        mypos += __shfl_down(mypos, o);
+        myrec += __shfl_down(myrec, o);
+        binsum += __shfl_down(binsum, o);
+        mymax = max(mymax, (unsigned int)__shfl_down(mymax, o));
+    }
+    __shared__ unsigned long long s_diff;
+    if (threadIdx.x == 0) s_diff = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&s_diff, myrec - binsum);
+        if (mypos) atomicAdd(npos, mypos);
+        if (mymax) atomicMax(maxlocal, mymax);
     }
     __syncthreads();
     if (threadIdx.x == 0 && s_diff != 0) atomicOr(skew, 1u);
