@@ -314,6 +314,7 @@ struct ec_session {
     // rank_tile.h: tile counts / bases, super list, its walk records, index map, path keys / ranks
     // join_local.h: per-key table words, table id ranges, foreign counts / offsets, flags
     DevBuf jl_kof, jl_rs, jl_re, jl_cnt, jl_off, jl_flag;
+    DevBuf rpack;  // k_wbv's 2-bit copy of the reads (config 5's run codes gathered from it)
     DevBuf rt_tcnt, rt_tbase, rt_srec, rt_snrec, rt_sidx, rt_pks, rt_rks, rt_hasp, rt_lr;
     // Wyllie rounds the last converged super ranking needed + 1 (0: none yet, or it did not
     // converge): rank_supers_async queues that many instead of ceil(log2 N) + 2 -- a round after
@@ -1887,6 +1888,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
     // minimizer buckets (count_wide.h k_wbv): every window's minimizer, indexed by its base offset
     uint32_t *wbv = nullptr;
     uint32_t mbM = 0;
+    uint32_t *rpack = nullptr, rpack_d = 0;
     if (mb) {  // reads of one length L <= WMB_MAXL only (k_wbv checks the others)
         uint64_t o2[2] = {0, 0};
         EC_CHECK(d2h(s, o2, d_off, 16, st));
@@ -1901,9 +1903,16 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         EC_CHECK(s->wbv.ensure(((nreads + 255) / 256) * 256 * (uint64_t)mbM * 4));
         wbv = s->wbv.as<uint32_t>();
         const unsigned g = (unsigned)((nreads + 63) / 64);
+        // large inputs (the third level's run codes): k_wbv also writes the reads as 2-bit codes,
+        // from which k_run_codes copies each run's codes (EULERHIP_RUN_PACKED=0: from the ASCII)
+        if (kn().wide_runs != 0 && kn().run_packed != 0 && (uint64_t)nreads * mbM >= (1ull << 26)) {
+            rpack_d = (uint32_t)((L + 15) / 16);
+            EC_CHECK(s->rpack.ensure((uint64_t)nreads * rpack_d * 4));
+            rpack = s->rpack.as<uint32_t>();
+        }
         switch (k - SK_M + 1) {  // (WMB_MAX_K = 52: w <= 38)
 #define EC_WBV(W) \
-    case W: k_wbv<W><<<g, 64, 0, st>>>(d_reads, d_off, nreads, (uint32_t)L, wbv, &dsc->wbv_long); break;
+    case W: k_wbv<W><<<g, 64, 0, st>>>(d_reads, d_off, nreads, (uint32_t)L, wbv, &dsc->wbv_long, rpack, rpack_d); break;
             EC_WBV(19) EC_WBV(20) EC_WBV(21) EC_WBV(22) EC_WBV(23) EC_WBV(24) EC_WBV(25) EC_WBV(26) EC_WBV(27)
             EC_WBV(28) EC_WBV(29) EC_WBV(30) EC_WBV(31) EC_WBV(32) EC_WBV(33) EC_WBV(34) EC_WBV(35) EC_WBV(36)
             EC_WBV(37) EC_WBV(38)
@@ -2092,7 +2101,7 @@ int phase_count_wpart(ec_session *s, const uint8_t *d_reads, const uint64_t *d_o
         k_run_codes<<<(unsigned)Bk, 512, 0, st>>>(rdirect, s->bstart.as<unsigned long long>(),
                                                   s->gcur.as<unsigned long long>(), s->bb2.as<unsigned long long>(),
                                                   sbits, wcodes, s->wcodes_tab.as<unsigned long long>(),
-                                                  RunReads{d_reads, d_off, k, mbM, read_base});
+                                                  RunReads{d_reads, d_off, k, mbM, read_base, rpack, rpack_d});
         kmark(s, 4, 1);
     } else if (runs) {
         // each fine bucket's runs sorted by sub-bucket (k_split3_runs, run units), then expanded
@@ -4144,7 +4153,7 @@ static void for_each_buf(ec_session *s, Fn fn) {
                      &s->jrec, &s->joid, &s->jout, &s->jseg, &s->jcnt, &s->xrec,
                      &s->skm_rec, &s->skm_ev, &s->skm_end, &s->wcodes_tab,
                      &s->run_cnt, &s->run_ends, &s->run_dends, &s->rt_lb,
-                     &s->jl_kof, &s->jl_rs, &s->jl_re, &s->jl_cnt, &s->jl_off, &s->jl_flag};
+                     &s->jl_kof, &s->jl_rs, &s->jl_re, &s->jl_cnt, &s->jl_off, &s->jl_flag, &s->rpack};
     for (auto *b : all) fn(*b);
 }
 

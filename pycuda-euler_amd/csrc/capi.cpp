@@ -69,6 +69,7 @@ void refresh_knobs() {
         k.join_local = num("EULERHIP_JOIN_LOCAL", -1);
         k.junction_radix = num("EULERHIP_JUNCTION_RADIX", -1);
         k.copy_streams = num("EULERHIP_COPY_STREAMS", -1);
+        k.run_packed = num("EULERHIP_RUN_PACKED", -1);
         k.upsweep_staged = num("EULERHIP_UPSWEEP_STAGED", -1);
         k.jl_fcap = num("EULERHIP_JL_FCAP", -1);
         k.jl_bits_delta = num("EULERHIP_JL_BITS_DELTA", 0);

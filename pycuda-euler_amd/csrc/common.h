@@ -67,6 +67,7 @@ struct Knobs {
     int jl_fcap = -1;        // EULERHIP_JL_FCAP: the local join's foreign-record capacity (tests: overflow)
     int jl_bits_delta = 0;   // EULERHIP_JL_BITS_DELTA: join tables finer / coarser than the count's (tests)
     int upsweep_staged = -1;  // EULERHIP_UPSWEEP_STAGED=1: runs counted by the staged upsweep (A/B)
+    int run_packed = -1;      // EULERHIP_RUN_PACKED=0: config 5's run codes gathered from the ASCII reads
     int copy_streams = -1;    // EULERHIP_COPY_STREAMS=2: host-input chunks alternate over two copy streams  // EULERHIP_JUNCTION_RADIX=1: junction buckets by the radix sort at any size     // EULERHIP_JOIN_LOCAL=0: links of minimizer-table ids by the global half-edge join
     int join_mb = -1;        // EULERHIP_JOIN_MB=0: junctions of minimizer-bucketed keys bucketed by mix128
     bool no_small_starts = false; // EULERHIP_NO_SMALL_STARTS: short lists on the general launches (k_starts_small, k_links_small off)

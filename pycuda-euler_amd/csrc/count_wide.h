@@ -43,7 +43,7 @@ __host__ __device__ inline uint64_t wbv_at(uint64_t r, uint32_t w, uint32_t M) {
 }
 template <int W>
 __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *off, uint64_t nreads, uint32_t L,
-                                            uint32_t *wbv, unsigned int *bad) {
+                                            uint32_t *wbv, unsigned int *bad, uint32_t *pk = nullptr, uint32_t pkd = 0) {
     __shared__ __attribute__((aligned(16))) uint8_t st[64 * WMB_MAXL + 32];
     constexpr int K = W + SK_M - 1;
     const uint32_t lane = threadIdx.x;
@@ -69,6 +69,8 @@ __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *
     const uint32_t M = L - K + 1, nh = L - SK_M + 1;
     constexpr uint32_t MM = (1u << (2 * SK_M)) - 1;
     uint32_t mf = 0, mr = 0, nonacgt = 0;
+    uint32_t pacc = 0, pcnt = 0;  // (pk: the read's 2-bit codes, base t at bits 2 (t % 16) of dword t / 16)
+    uint32_t *pout = pk ? pk + r * (uint64_t)pkd : nullptr;
     auto push = [&](uint32_t b) {
         mf = ((mf << 2) | b) & MM;
         mr = (mr >> 2) | ((3u - b) << (2 * SK_M - 2));
@@ -77,7 +79,13 @@ __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *
     // length check does -- k_upsweep_runs no longer stages the reads to look)
     auto base = [&](uint32_t c) {
         nonacgt |= is_acgt(c) ^ 1u;
-        return code2(c);
+        const uint32_t b = code2(c);
+        if (pout) {
+            pacc |= b << (2 * (pcnt & 15));
+            if ((pcnt & 15) == 15) pout[pcnt >> 4] = pacc, pacc = 0;
+            pcnt++;
+        }
+        return b;
     };
     for (uint32_t t = 0; t < SK_M - 1; t++) push(base(rd[t]));
     uint32_t S[W];
@@ -109,6 +117,7 @@ __global__ void __launch_bounds__(64) k_wbv(const uint8_t *buf, const uint64_t *
 #pragma unroll
         for (int j = W - 2; j >= 0; j--) S[j] = min(S[j], S[j + 1]);
     }
+    if (pout && (pcnt & 15)) pout[pcnt >> 4] = pacc;
     if (nonacgt) *bad = 1u;
 }
 
@@ -334,8 +343,18 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_runs(const uint8_t *buf,
         uint32_t runv = 0, runl = 0;
         K128 fwd{0, 0}, rc{0, 0};
         bool have = false;  // fwd / rc hold the previous window's k-mer
-        for (uint32_t w = 0; w < m; w++) {
-            const uint32_t pv = wbv[wbv_at(r, w, mbM)];
+        const uint32_t *wp = wbv + wbv_at(r, 0, mbM);
+        for (uint32_t w0 = 0; w0 < m; w0 += 8) {
+          // eight windows' minimizers loaded before any is used (one load in flight a lane kept
+          // the kernel latency-bound: 6.9 ms at config 5)
+          uint32_t pvs[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) pvs[u] = w0 + u < m ? wp[(uint64_t)(w0 + u) * 256u] : 0u;
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const uint32_t w = w0 + u;
+            if (w >= m) break;
+            const uint32_t pv = pvs[u];
             const bool open = w == 0 || pv != runv || runl == RUN_MAXW;
             runl = open ? 1u : runl + 1;
             runv = pv;
@@ -358,6 +377,7 @@ __global__ void __launch_bounds__(TILE_READS) k_upsweep_runs(const uint8_t *buf,
             } else {
                 have = false;
             }
+          }
         }
     }
     unsigned long long binsum = 0;  // bin-sum overflow check of k_upsweep
@@ -672,6 +692,8 @@ struct RunReads {
     int k;
     uint32_t m;          // windows per read (minimizer buckets: one read length)
     uint64_t read_base;  // global id of read 0
+    const uint32_t *pk = nullptr;  // the reads as 2-bit codes (k_wbv, 16 a dword), pkd dwords a read
+    uint32_t pkd = 0;
 };
 // windows per fine bucket (the expansion's output bases after a scan)
 __global__ void __launch_bounds__(256) k_run_wsum(const RunWM *runs, const unsigned long long *bstart,
@@ -983,28 +1005,40 @@ __global__ void __launch_bounds__(512) k_run_codes(const RunWM *runs, const unsi
             for (unsigned int j = 0; j < F; j++)
                 if (b3[(uint64_t)b * F + j] == ri) ctab[(uint64_t)b * F + j] = od0;
             const unsigned int nwin = x.wn >> 16, nbases = nwin + (unsigned int)k - 1;
-            const uint64_t s0 = rr.off[x.read] + (x.wn & 0xFFFFu);
-            const uint32_t *wp = reinterpret_cast<const uint32_t *>(rr.buf + (s0 & ~3ull));
-            const unsigned int skip = (unsigned int)(s0 & 3), nw = (skip + nbases + 3) >> 2;
-            uint32_t acc = 0;
-            unsigned int i = 0;
-            unsigned long long od = od0;
-            for (unsigned int q = 0; q < nw; q += 8) {
-                uint32_t d[8];
+            if (rr.pk) {  // from k_wbv's 2-bit reads: a shifted copy of the read's code dwords
+                const uint32_t *pr = rr.pk + (uint64_t)x.read * rr.pkd;
+                const unsigned int st = x.wn & 0xFFFFu, q0 = st >> 4, sft = 2 * (st & 15), ncd = run_cdw(x, k);
+                for (unsigned int q = 0; q < ncd; q++) {
+                    const uint32_t lo = pr[q0 + q], hi = q0 + q + 1 < rr.pkd ? pr[q0 + q + 1] : 0u;
+                    uint32_t v = sft ? __builtin_amdgcn_alignbit(hi, lo, sft) : lo;
+                    const unsigned int rem = nbases - 16 * q;  // (the run's last dword: its bases only)
+                    if (rem < 16) v &= (1u << (2 * rem)) - 1u;
+                    codes[od0 + q] = v;
+                }
+            } else {
+                const uint64_t s0 = rr.off[x.read] + (x.wn & 0xFFFFu);
+                const uint32_t *wp = reinterpret_cast<const uint32_t *>(rr.buf + (s0 & ~3ull));
+                const unsigned int skip = (unsigned int)(s0 & 3), nw = (skip + nbases + 3) >> 2;
+                uint32_t acc = 0;
+                unsigned int i = 0;
+                unsigned long long od = od0;
+                for (unsigned int q = 0; q < nw; q += 8) {
+                    uint32_t d[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) d[u] = q + u < nw ? wp[q + u] : 0u;
+                    for (int u = 0; u < 8; u++) d[u] = q + u < nw ? wp[q + u] : 0u;
 #pragma unroll
-                for (int u = 0; u < 8; u++)
+                    for (int u = 0; u < 8; u++)
 #pragma unroll
-                    for (int bt = 0; bt < 4; bt++) {
-                        const unsigned int bp = (q + u) * 4 + bt;
-                        if (bp < skip || bp >= skip + nbases) continue;
-                        acc |= code2((d[u] >> (8 * bt)) & 0xFFu) << (2 * (i & 15));
-                        if ((i & 15) == 15) codes[od++] = acc, acc = 0;
-                        i++;
-                    }
+                        for (int bt = 0; bt < 4; bt++) {
+                            const unsigned int bp = (q + u) * 4 + bt;
+                            if (bp < skip || bp >= skip + nbases) continue;
+                            acc |= code2((d[u] >> (8 * bt)) & 0xFFu) << (2 * (i & 15));
+                            if ((i & 15) == 15) codes[od++] = acc, acc = 0;
+                            i++;
+                        }
+                }
+                if (i & 15) codes[od] = acc;
             }
-            if (i & 15) codes[od] = acc;
         }
         __syncthreads();
         if (tid == 0) s_off += tot;
