@@ -71,13 +71,16 @@ bool memlog_on();
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
-    __attribute__((noinline)) int ensure(size_t bytes) {
+    // (spare: allocate that fraction more already the first time -- a size that varies from call
+    // to call, like the gathered chain count)
+    __attribute__((noinline)) int ensure(size_t bytes, unsigned int spare_div = 0) {
         if (bytes <= cap) return EC_OK;
         // a buffer that grows gets 1/8 of headroom: sizes that vary a little from call to call
         // (chain counts, received records) would otherwise reallocate -- ~1 ms a hipFree /
         // hipMalloc pair -- on every call that is a little larger than the last
         size_t want = std::max<size_t>(bytes, 256);
         if (cap) want += want / 8;
+        else if (spare_div) want += want / spare_div;
         release();
         const auto t0 = std::chrono::steady_clock::now();
         if (hipMalloc(&p, want) != hipSuccess) {
@@ -2666,15 +2669,17 @@ int rank_supers_async(ec_session *s, unsigned int N, const unsigned long long *d
     const unsigned B = 256;
     Scalars *dsc = s->scal.as<Scalars>();
     SuperRec *srec = s->rt_srec.as<SuperRec>();
-    // (buffers sized by N, not by the chain count: a count a little above the last call's would
-    // reallocate them -- a hipFree / hipMalloc pair of ~1 ms in the partitioned finish)
-    const size_t cap = std::max<size_t>(std::max(N, G), 1);
-    EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec)));
-    EC_CHECK(s->rt_pks.ensure(cap * 4));
-    EC_CHECK(s->rt_rks.ensure(cap * 4));
-    EC_CHECK(s->rlist.ensure(cap * 4));
-    EC_CHECK(s->nextR.ensure(cap * 4));
-    EC_CHECK(s->rbc.ensure(((cap + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8));
+    // (buffers sized by N, not by the chain count, when the count is only on the device: a count a
+    // little above the last call's would reallocate them; with mcap, by it with part_rank's spare
+    // -- the gathered list of the partitioned finish is far below its node count)
+    const size_t cap = mcap ? (size_t)mcap + 4096 : std::max<size_t>(N, 1);
+    const unsigned int spare = mcap ? 16u : 0u;
+    EC_CHECK(s->rt_snrec.ensure(cap * sizeof(SNodeRec), spare));
+    EC_CHECK(s->rt_pks.ensure(cap * 4, spare));
+    EC_CHECK(s->rt_rks.ensure(cap * 4, spare));
+    EC_CHECK(s->rlist.ensure(cap * 4, spare));
+    EC_CHECK(s->nextR.ensure(cap * 4, spare));
+    EC_CHECK(s->rbc.ensure(((cap + RULER_CHUNK - 1) / RULER_CHUNK) * 8 + 8, spare));
     SNodeRec *snrec = s->rt_snrec.as<SNodeRec>();
     const unsigned int *dnr = &dsc->nr;
     const unsigned int gs = std::min(grid_for(G, B), 4096u);  // grid-stride grids over <= G items
@@ -3446,7 +3451,12 @@ int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
     const unsigned int N = 2 * (unsigned int)s->n_dense;
     s->stats.n_rulers = 0;
     if (!M) return EC_OK;
-    EC_CHECK(s->rt_srec.ensure(std::max<size_t>(M, N) * sizeof(SuperRec)));
+    // the super list's buffers sized by its chain count (1/16 spare on first allocation, so a
+    // step whose count is a little above the last one's reuses them), not by the node count:
+    // config 5's one-rank step ranks 21 M chains of 400 M nodes, where node-sized ruler state
+    // held ~38 GB (r06_h)
+    const size_t mc = (size_t)M + 4096;
+    EC_CHECK(s->rt_srec.ensure(mc * sizeof(SuperRec), 16));
     EC_HIP(hipMemcpyAsync(s->rt_srec.p, d_all, (size_t)M * sizeof(SuperRec), hipMemcpyDeviceToDevice, st));
     k_super_index<<<grid_for(M, 256), 256, 0, st>>>(s->rt_srec.as<SuperRec>(), (unsigned int)M,
                                                     s->rt_sidx.as<unsigned int>());
@@ -3455,11 +3465,10 @@ int part_rank(ec_session *s, const SuperRec *d_all, uint64_t M) {
     if (kn().rank_sync != 1) {
         // rank_supers_async (one read-back at the end instead of one per ruler pass plus the
         // launch backlog after it): M on the device, the ruler state initialised here
-        const size_t Nn = std::max<size_t>(N, 1);
-        EC_CHECK(s->rt_hasp.ensure(Nn));
-        EC_CHECK(s->rid.ensure(Nn * 8));
-        EC_CHECK(s->st0.ensure(Nn * sizeof(RJump)));
-        EC_CHECK(s->st1.ensure(Nn * sizeof(RJump)));
+        EC_CHECK(s->rt_hasp.ensure(mc, 16));
+        EC_CHECK(s->rid.ensure(mc * 8, 16));
+        EC_CHECK(s->st0.ensure(mc * sizeof(RJump), 16));
+        EC_CHECK(s->st1.ensure(mc * sizeof(RJump), 16));
         EC_CHECK(s->rt_tbase.ensure(8));
         // the chain count on the device, the ruler state initialised: one launch (six memsets
         // cost ~40 us of launch gaps)
