@@ -336,6 +336,7 @@ struct ec_session {
         unsigned int ntiles = 0;
         bool planned = false;
     } hold;
+    SuperRec *chain_scr = nullptr;  // part_chains' tile records (st1, or a placed segment's jrec)
     unsigned int seg_nc = 0;     // contigs of the job (ec_graph_layout)
     uint64_t seg_nchars = 0;
     // the partitioned finish's transfer record (ec_graph_emit_runs / ec_graph_copy_runs):
@@ -3371,7 +3372,7 @@ int phase_graph(ec_session *s, int k, unsigned int U, const Index &sidx, const u
 int part_chains_copy(ec_session *s, uint64_t M, unsigned int ntiles, bool planned, SuperRec *d_super) {
     hipStream_t st = s->stream;
     if (M)
-        k_tile_compact<<<ntiles, 256, 0, st>>>(reinterpret_cast<SuperRec *>(s->st1.p), s->rt_tcnt.as<unsigned long long>(),
+        k_tile_compact<<<ntiles, 256, 0, st>>>(s->chain_scr, s->rt_tcnt.as<unsigned long long>(),
                                                s->rt_tbase.as<unsigned long long>(), d_super,
                                                s->rt_sidx.as<unsigned int>(), nullptr, nullptr, nullptr, nullptr,
                                                nullptr, planned ? s->rt_tb.as<unsigned int>() : nullptr);
@@ -3418,11 +3419,18 @@ int part_chains(ec_session *s, uint64_t lo, uint64_t hi, const uint32_t *d_succ,
     }
     EC_CHECK(s->rt_tcnt.ensure(((size_t)ntiles + 1) * 8));
     EC_CHECK(s->rt_tbase.ensure(((size_t)ntiles + 1) * 8));
-    // (planned tiles keep their chain records at node offsets: 2 (hi - lo) records)
-    EC_CHECK(s->st1.ensure(std::max<size_t>(planned ? 2 * (size_t)(hi - lo) : (size_t)ntiles * RT_TN, 1) *
-                           sizeof(SuperRec)));
+    // (planned tiles keep their chain records at node offsets: 2 (hi - lo) records.)  A placed
+    // segment's junction slots (4 a key of >= 16 B: >= the 64 B a key of chain records) are free
+    // once ec_graph_place_copy gathered them, so the records go there instead of a buffer of
+    // their own (12.6 GB at one config-5 rank); the pending place records are dropped with them
+    const size_t scr_bytes =
+        std::max<size_t>(planned ? 2 * (size_t)(hi - lo) : (size_t)ntiles * RT_TN, 1) * sizeof(SuperRec);
+    DevBuf &scr = s->placed && s->jrec.cap >= scr_bytes ? s->jrec : s->st1;
+    if (&scr == &s->jrec && s->hold.kind == 1) s->hold.kind = 0;
+    EC_CHECK(scr.ensure(scr_bytes));
     unsigned long long *tcnt = s->rt_tcnt.as<unsigned long long>(), *tbase = s->rt_tbase.as<unsigned long long>();
-    SuperRec *scratch = reinterpret_cast<SuperRec *>(s->st1.p);
+    SuperRec *scratch = reinterpret_cast<SuperRec *>(scr.p);
+    s->chain_scr = scratch;
     if (!ntiles) EC_HIP(hipMemsetAsync(tcnt, 0, 8, st));  // (k_tile_chains zeroes tcnt[ntiles])
     if (ntiles)
         k_tile_chains<<<ntiles, RT_NT, 0, st>>>(s->upal.as<uint8_t>(), s->succ.as<unsigned int>(), n1,
