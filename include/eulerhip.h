@@ -481,7 +481,10 @@ int ec_graph_emit_runs(ec_session *s, uint64_t *nbytes);
  * called with a NULL output (d_jrecs / d_super / d_starts) count their records only (the counts
  * returned as above) and hold them; the matching copy, before any other step of the session,
  * writes them into a buffer of exactly that many records -- instead of the upper bounds (4 Ur
- * junction records, 2 (hi - lo) super / start records: ~50 GB at config 5's per-rank size). */
+ * junction records, 2 (hi - lo) super / start records: ~50 GB at config 5's per-rank size).
+ * ec_graph_chains_part on a placed segment keeps its tile records in the junction-record buffer
+ * ec_graph_place filled, so place records still held then are dropped (ec_graph_place_copy
+ * returns EC_ERR_STATE). */
 int ec_graph_place_copy(ec_session *s, void *d_jrecs);
 int ec_graph_chains_copy(ec_session *s, void *d_super);
 int ec_graph_starts_copy(ec_session *s, void *d_starts);
