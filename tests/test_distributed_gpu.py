@@ -416,3 +416,39 @@ def test_streaming_count_vs_oracle(k, L, g, n, chunk, fold, err, base):
     assert res.contig_bytes == ref["contig_chars"]
     assert np.array_equal(res.contig_offsets, ref["contig_offsets"])
     assert res.links == oracle.unpack_links(ref)
+
+
+def test_chains_drop_held_place_records():
+    """ec_graph_chains_part keeps its tile records in the junction-record buffer ec_graph_place
+    filled (round 6: no 64-B-a-key buffer of its own), so place records still held then are
+    refused by ec_graph_place_copy (EC_ERR_STATE) instead of copied overwritten; copied first,
+    they are taken as before"""
+    import ctypes
+
+    import distributed
+
+    buf, off = make_reads(20_000, 6_000, 100, 7105, err=0.002)
+    k = 31
+    ref = oracle.assemble_packed(buf, off, k, 1)
+    e = distributed.HipEngine(0)
+    try:
+        st = {}
+        res, _ = distributed.streaming_assemble(e, buf, off, k, 1, chunk_reads=2_500, fold=2, stats=st)
+        assert res.contig_bytes == ref["contig_chars"]
+        ur = int(st["solid"])
+        L, h = e.L, e._h()
+        counts = (ctypes.c_uint64 * 1)()
+        npal = ctypes.c_uint64(0)
+        out = e.empty(4 * ur * distributed.junction_bytes(k))
+        # in order: counted, then copied
+        eulerhip.check(L.ec_graph_place(h, 0, ur, 1, None, counts, ctypes.byref(npal)))
+        assert 0 < counts[0] <= 4 * ur
+        assert L.ec_graph_place_copy(h, ctypes.c_void_p(out.data_ptr())) == 0
+        # counted, then the chains step reuses the buffer: the held records are gone
+        eulerhip.check(L.ec_graph_place(h, 0, ur, 1, None, counts, ctypes.byref(npal)))
+        n = ctypes.c_uint64(0)
+        eulerhip.check(L.ec_graph_chains_part(h, 0, ur, None, None, ctypes.byref(n)))
+        assert n.value > 0
+        assert L.ec_graph_place_copy(h, ctypes.c_void_p(out.data_ptr())) == eulerhip.EC_ERR_STATE
+    finally:
+        e.sess.close()
